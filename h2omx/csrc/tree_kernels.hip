@@ -1,0 +1,891 @@
+// Histogram tree engine kernels (GBM / XGBoost-hist / DRF) for gfx950.
+//
+// Design (see docs/ARCHITECTURE.md "Tree engine"):
+//   * Features are pre-binned once into uint8 codes stored FEATURE-MAJOR
+//     ([F][npad]) so that a workgroup that owns a group of features streams
+//     exactly those columns, 16 rows per lane per 16-byte load.
+//   * Trees grow level-wise.  Every level streams all rows once; rows are
+//     routed by a per-row node id (nid).  Only the smaller child of every
+//     split is histogrammed ("built"); the sibling is parent - built
+//     (subtraction trick), so LDS atomics are spent on <= half the rows.
+//   * Per-workgroup private histograms live in LDS (ds_add_f32); each
+//     workgroup flushes its histogram with plain coalesced stores into a
+//     partial slab and a second kernel reduces the slabs in fp64.  No global
+//     float atomics on the hot path (they run at ~1.3 TB/s chip-wide and
+//     would dominate, see MI355X_MICROARCH.md "Global float atomics").
+//   * The level bookkeeping (which nodes split, which child gets built,
+//     node numbering) runs on the device, so a whole tree is a fixed
+//     sequence of launches with NO host synchronisation: the host only
+//     enqueues work, the GPU decides the tree.  Between the reduce and the
+//     split scan the caller may insert an all-reduce of the built
+//     histograms (RCCL over xGMI) - that is the only communication.
+//
+// Reference parity: the reference repository (isgasho/h2o-kubernetes)
+// deploys the H2O-3 Java image whose GBM/DRF/XGBoost implement these
+// algorithms (src/k8s/templates.rs:28-30 launches h2o.jar); this file is the
+// MI355X-native replacement of that compute path.
+#include "common.h"
+#include <math.h>
+
+namespace {
+
+struct SplitParams {
+  int mode;          // 0: H2O squared-error gain on (G, W); 1: XGBoost 2nd-order gain on (G, H)
+  int leaf_mode;     // 0: Newton step -G/(H+lambda); 1: mean -G/W (DRF)
+  int F;
+  int is_last_level;
+  double min_rows;            // min sum of weights per child (mode 0 and 1)
+  double min_child_weight;    // min hessian sum per child (mode 1)
+  double lambda_;             // L2 on leaf weights (mode 1 / leaf)
+  double alpha;               // L1 on leaf weights
+  double gamma;               // min loss reduction (mode 1)
+  double min_split_improvement;  // relative (mode 0)
+  double learn_rate;          // multiplies leaf values
+  double max_abs_leaf;        // |leaf| clip (0 = none)
+  uint32_t seed;
+  int tree_index;
+  int depth;
+  float col_rate;             // per-node column sampling rate (1 = all)
+  int mtries;                 // exact per-node feature count (0 = off)
+  int children_leaves;        // children of splits at this level are final leaves
+};
+
+struct NodeSplit {  // best split of one node at the current level (64 B)
+  double gain;
+  double G, H, W;      // node totals
+  double GL, HL, WL;   // left-child totals of the chosen split
+  int feat;            // -1 = no valid split
+  int bin;             // rows with bin <= this go left
+  int na_left;
+  int pad;
+};
+
+struct NodeLink {  // per node of a level: where its histogram comes from
+  int slot;       // >= 0: histogram built this level in that slot
+  int sib_slot;   // if slot < 0: sibling's slot (hist = parent - sibling)
+  int parent;     // local index of the parent in the previous level
+  int pad;
+};
+
+struct PartInfo {  // per node of a level: routing decision for partition
+  int feat;
+  int bin;
+  int na_left;
+  int child;  // local id of left child at next level, -1 = node is a leaf
+  int gid;    // global node id inside the tree
+  int leaf_children;  // 1: children are leaves, rows retire into them now
+  int child_gid;      // global id of the left child
+  int pad;
+};
+
+struct TreeNode {  // model representation (32 B)
+  int feat;      // -1 = leaf
+  int bin;
+  int left;      // global id of left child (right = left + 1)
+  int na_left;
+  float thr;     // raw-value threshold: x <= thr goes left (NaN -> na_left)
+  float value;   // leaf value (already scaled by the learning rate)
+  float gain;
+  float weight;  // sum of weights in the node
+};
+
+// ctl layout (int32 device array, one per level buffer):
+//   [0] n_nodes at this level, [1] n_slots built at this level,
+//   [2] base = global id of local node 0, [3] total nodes in tree so far
+constexpr int CTL_N = 0, CTL_SLOTS = 1, CTL_BASE = 2, CTL_TOTAL = 3;
+
+__device__ __forceinline__ double leaf_value(double G, double H, double W, const SplitParams& p) {
+  double v;
+  if (p.leaf_mode == 1) {
+    v = (W > 0.0) ? -G / W : 0.0;
+  } else {
+    double g = G;
+    if (p.alpha > 0.0) {
+      if (g > p.alpha) g -= p.alpha;
+      else if (g < -p.alpha) g += p.alpha;
+      else g = 0.0;
+    }
+    double den = H + p.lambda_;
+    v = (den > 1e-12) ? -g / den : 0.0;
+  }
+  v *= p.learn_rate;
+  if (p.max_abs_leaf > 0.0) v = fmin(fmax(v, -p.max_abs_leaf), p.max_abs_leaf);
+  return v;
+}
+
+__device__ __forceinline__ double l1_thresh(double g, double a) {
+  if (a <= 0.0) return g;
+  if (g > a) return g - a;
+  if (g < -a) return g + a;
+  return 0.0;
+}
+
+// Gain of splitting (G,H,W) into L and R = total - L.  Returns -inf if the
+// split violates a constraint.
+__device__ __forceinline__ double split_gain(double GL, double HL, double WL, double G, double H, double W,
+                                             const SplitParams& p) {
+  const double GR = G - GL, HR = H - HL, WR = W - WL;
+  if (WL < p.min_rows || WR < p.min_rows || WL <= 0.0 || WR <= 0.0) return -INFINITY;
+  if (p.mode == 0) {
+    return GL * GL / WL + GR * GR / WR - G * G / W;
+  }
+  if (HL < p.min_child_weight || HR < p.min_child_weight) return -INFINITY;
+  const double lam = p.lambda_;
+  const double tl = l1_thresh(GL, p.alpha), tr = l1_thresh(GR, p.alpha), tt = l1_thresh(G, p.alpha);
+  return 0.5 * (tl * tl / (HL + lam) + tr * tr / (HR + lam) - tt * tt / (H + lam)) - p.gamma;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// K1: feature binning.  X is feature-major fp32 [F][ld]; edges is [F][NBT]
+// (edges[f][j] for j < nvb[f]-1 are the sorted bin upper edges).  A value v
+// maps to lower_bound(edges, v); NaN maps to the NA bin NBT-1.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bin_features_kernel(const float* __restrict__ X, int64_t ld, int64_t n,
+                                                           const float* __restrict__ edges,
+                                                           const int* __restrict__ nvb, int nbt,
+                                                           uint8_t* __restrict__ codes, int64_t npad) {
+  __shared__ float e[256];
+  const int f = blockIdx.y;
+  const int m = nvb[f] - 1;  // number of edges
+  for (int j = threadIdx.x; j < 256; j += blockDim.x) e[j] = (j < m) ? edges[(int64_t)f * nbt + j] : INFINITY;
+  __syncthreads();
+  const float* x = X + (int64_t)f * ld;
+  uint8_t* c = codes + (int64_t)f * npad;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < npad; r += (int64_t)gridDim.x * blockDim.x) {
+    uint8_t code = 0;
+    if (r < n) {
+      const float v = x[r];
+      if (v != v) {
+        code = (uint8_t)(nbt - 1);
+      } else {
+        int lo = 0, hi = m;  // first index with e[idx] >= v
+        while (lo < hi) {
+          int mid = (lo + hi) >> 1;
+          if (e[mid] < v) lo = mid + 1; else hi = mid;
+        }
+        code = (uint8_t)lo;
+      }
+    }
+    c[r] = code;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K3: LDS-privatised histogram build.
+// Grid = n_groups * wgpg workgroups (wgpg % 8 == 0).  blockIdx -> (chunk,
+// group) keeps the n_groups workgroups of one row chunk on one XCD
+// (b % 8 equal) so their shared g/h/nid reads hit that XCD's L2 (speed only).
+// Each lane handles ROWS consecutive rows per iteration (one 16-B code load
+// per feature).  Slots [slot_lo, slot_lo + slot_cnt) are accumulated.
+// ---------------------------------------------------------------------------
+template <int NBT, int ROWS>
+__global__ __launch_bounds__(512) void hist_build_kernel(
+    const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ h,
+    const float* __restrict__ w, const int* __restrict__ nid, const NodeLink* __restrict__ link,
+    const int* __restrict__ ctl, int F, int fg, int n_groups, int wgpg, int slot_lo, int slot_cnt,
+    float* __restrict__ partials) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int n_slots = ctl[CTL_SLOTS];
+  if (slot_lo >= n_slots) return;  // uniform: nothing to build in this pass
+
+  const int b = blockIdx.x;
+  const int xcd = b & 7, i = b >> 3;
+  const int group = i % n_groups;
+  const int chunk = xcd + 8 * (i / n_groups);
+  const int f0 = group * fg;
+  const int nf = min(fg, F - f0);
+  const int hist_floats = slot_cnt * fg * 3 * NBT;
+
+  for (int j = threadIdx.x * 4; j < hist_floats; j += blockDim.x * 4)
+    *reinterpret_cast<float4*>(lds + j) = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+
+  const int64_t units = npad / ROWS;
+  const int64_t u0 = units * chunk / wgpg, u1 = units * (chunk + 1) / wgpg;
+
+  for (int64_t u = u0 + threadIdx.x; u < u1; u += blockDim.x) {
+    const int64_t r0 = u * ROWS;
+    int s[ROWS];
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < ROWS / 4; ++q) {
+      const int4 n4 = *reinterpret_cast<const int4*>(nid + r0 + 4 * q);
+      const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        int sl = -1;
+        if (nn[k] >= 0) {
+          sl = link[nn[k]].slot - slot_lo;
+          if (sl >= slot_cnt) sl = -1;
+        }
+        s[4 * q + k] = sl;
+        any |= (sl >= 0);
+      }
+    }
+    if (!any) continue;
+    float gg[ROWS], hh[ROWS], ww[ROWS];
+#pragma unroll
+    for (int q = 0; q < ROWS / 4; ++q) {
+      const float4 g4 = *reinterpret_cast<const float4*>(g + r0 + 4 * q);
+      const float4 h4 = *reinterpret_cast<const float4*>(h + r0 + 4 * q);
+      gg[4 * q] = g4.x; gg[4 * q + 1] = g4.y; gg[4 * q + 2] = g4.z; gg[4 * q + 3] = g4.w;
+      hh[4 * q] = h4.x; hh[4 * q + 1] = h4.y; hh[4 * q + 2] = h4.z; hh[4 * q + 3] = h4.w;
+      if (w) {
+        const float4 w4 = *reinterpret_cast<const float4*>(w + r0 + 4 * q);
+        ww[4 * q] = w4.x; ww[4 * q + 1] = w4.y; ww[4 * q + 2] = w4.z; ww[4 * q + 3] = w4.w;
+      } else {
+        ww[4 * q] = ww[4 * q + 1] = ww[4 * q + 2] = ww[4 * q + 3] = 1.0f;
+      }
+    }
+    for (int fi = 0; fi < nf; ++fi) {
+      const uint8_t* cp = codes + (int64_t)(f0 + fi) * npad + r0;
+      uint32_t cw[ROWS / 4];
+      if constexpr (ROWS == 16) {
+        const uint4 c4 = *reinterpret_cast<const uint4*>(cp);
+        cw[0] = c4.x; cw[1] = c4.y; cw[2] = c4.z; cw[3] = c4.w;
+      } else {
+        const uint2 c2 = *reinterpret_cast<const uint2*>(cp);
+        cw[0] = c2.x; cw[1] = c2.y;
+      }
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r) {
+        if (s[r] >= 0 && ww[r] != 0.0f) {
+          const int bin = (cw[r >> 2] >> (8 * (r & 3))) & 0xff;
+          float* base = lds + (s[r] * fg + fi) * 3 * NBT + bin;
+          atomicAdd(base, gg[r]);
+          atomicAdd(base + NBT, hh[r]);
+          atomicAdd(base + 2 * NBT, ww[r]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  float* out = partials + (int64_t)(group * wgpg + chunk) * hist_floats;
+  for (int j = threadIdx.x * 4; j < hist_floats; j += blockDim.x * 4)
+    *reinterpret_cast<float4*>(out + j) = *reinterpret_cast<const float4*>(lds + j);
+}
+
+// Sum the per-workgroup slabs of one pass into the fp64 built histograms
+// built[slot][F][3][NBT].
+__global__ __launch_bounds__(256) void hist_reduce_kernel(const float* __restrict__ partials, int n_groups,
+                                                          int wgpg, int fg, int F, int nbt, int slot_lo,
+                                                          int slot_cnt, const int* __restrict__ ctl,
+                                                          double* __restrict__ built) {
+  const int64_t total = (int64_t)slot_cnt * F * 3 * nbt;
+  const int n_slots = ctl[CTL_SLOTS];
+  const int64_t hist_floats = (int64_t)slot_cnt * fg * 3 * nbt;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int bin = idx % nbt;
+    const int k = (idx / nbt) % 3;
+    const int f = (idx / (3 * nbt)) % F;
+    const int s = idx / ((int64_t)3 * nbt * F);
+    if (slot_lo + s >= n_slots) continue;
+    const int group = f / fg, fi = f % fg;
+    const float* p = partials + (int64_t)group * wgpg * hist_floats + ((int64_t)(s * fg + fi) * 3 + k) * nbt + bin;
+    double acc = 0.0;
+    for (int c = 0; c < wgpg; ++c) acc += (double)p[(int64_t)c * hist_floats];
+    built[(((int64_t)(slot_lo + s) * F + f) * 3 + k) * nbt + bin] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K4 + K5: complete the level's histograms (built or parent - sibling),
+// keep them as parents for the next level, and scan for the best threshold
+// of one (node, feature) pair per 256-thread workgroup (thread t owns bin t;
+// grid = max_nodes x F so even a 16-node level fills the chip).  The per-node
+// arg-max over features happens in level_finalize.
+// ---------------------------------------------------------------------------
+struct FeatBest {  // 64 B
+  double gain;
+  double GL, HL, WL;
+  double G, H, W;  // node totals (as seen from this feature's histogram)
+  int code;        // (bin * 2 + na_left), INT_MAX = none
+  int pad;
+};
+
+template <int NBT>
+__global__ __launch_bounds__(256) void split_find_kernel(const double* __restrict__ built,
+                                                         const double* __restrict__ parent_full,
+                                                         double* __restrict__ full, const int* __restrict__ ctl,
+                                                         const NodeLink* __restrict__ link,
+                                                         const int* __restrict__ nvb,
+                                                         const uint8_t* __restrict__ tree_fmask, SplitParams p,
+                                                         FeatBest* __restrict__ out) {
+  const int node = blockIdx.x;
+  const int f = blockIdx.y;
+  if (node >= ctl[CTL_N]) return;
+  const int F = p.F;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
+  const NodeLink lk = link[node];
+  __shared__ double wtot[3][4];
+  __shared__ double na[3];
+  __shared__ double bestg[4];
+  __shared__ int bestc[4];
+
+  double gv = 0, hv = 0, wv = 0;
+  if (t < NBT) {
+    const int64_t off = ((int64_t)f * 3) * NBT + t;
+    const int64_t per = (int64_t)F * 3 * NBT;
+    if (lk.slot >= 0) {
+      const double* bp = built + lk.slot * per + off;
+      gv = bp[0]; hv = bp[NBT]; wv = bp[2 * NBT];
+    } else {
+      const double* pp = parent_full + lk.parent * per + off;
+      const double* sp = built + lk.sib_slot * per + off;
+      gv = pp[0] - sp[0]; hv = pp[NBT] - sp[NBT]; wv = pp[2 * NBT] - sp[2 * NBT];
+    }
+    if (full) {
+      double* fp = full + node * per + off;
+      fp[0] = gv; fp[NBT] = hv; fp[2 * NBT] = wv;
+    }
+  }
+  if (t == NBT - 1) { na[0] = gv; na[1] = hv; na[2] = wv; }
+  // inclusive scan over the value bins (exclude NA bin)
+  double sg = (t < NBT - 1) ? gv : 0.0, sh = (t < NBT - 1) ? hv : 0.0, sw = (t < NBT - 1) ? wv : 0.0;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double ag = __shfl_up(sg, off, kWave), ah = __shfl_up(sh, off, kWave), aw = __shfl_up(sw, off, kWave);
+    if (lane >= off) { sg += ag; sh += ah; sw += aw; }
+  }
+  if (lane == 63) { wtot[0][wid] = sg; wtot[1][wid] = sh; wtot[2][wid] = sw; }
+  __syncthreads();
+  for (int k = 0; k < wid; ++k) { sg += wtot[0][k]; sh += wtot[1][k]; sw += wtot[2][k]; }
+  const double ng = na[0], nh = na[1], nw = na[2];
+  const double tg = wtot[0][0] + wtot[0][1] + wtot[0][2] + wtot[0][3] + ng;
+  const double th = wtot[1][0] + wtot[1][1] + wtot[1][2] + wtot[1][3] + nh;
+  const double tw = wtot[2][0] + wtot[2][1] + wtot[2][2] + wtot[2][3] + nw;
+
+  bool allowed = (tree_fmask == nullptr) || tree_fmask[f];
+  if (allowed && (p.mtries > 0 || p.col_rate < 1.0f)) {
+    const uint32_t key = (uint32_t)p.tree_index * 131u + (uint32_t)p.depth;
+    const uint32_t hf = hash4(p.seed, key, (uint32_t)node, (uint32_t)f);
+    if (p.mtries > 0) {
+      int rank = 0;  // rank of this feature's hash among all features
+      for (int j = 0; j < F; ++j) {
+        const uint32_t hj = hash4(p.seed, key, (uint32_t)node, (uint32_t)j);
+        rank += (hj < hf) || (hj == hf && j < f);
+      }
+      allowed = rank < p.mtries;
+    } else {
+      allowed = u01(hf) < p.col_rate;
+    }
+  }
+  double best_gain = -INFINITY;
+  int best_code = 0x7fffffff;
+  double bGL = 0, bHL = 0, bWL = 0;
+  const int m = nvb[f];  // thresholds t in [0, m-1]
+  if (allowed && t < m && t < NBT - 1) {
+    const double gA = split_gain(sg, sh, sw, tg, th, tw, p);  // NA goes right
+    const double gB = (nw > 0.0) ? split_gain(sg + ng, sh + nh, sw + nw, tg, th, tw, p) : -INFINITY;  // NA left
+    if (gA > -INFINITY) { best_gain = gA; best_code = 2 * t; bGL = sg; bHL = sh; bWL = sw; }
+    if (gB > -INFINITY && (gB > best_gain || (gB == best_gain && 2 * t + 1 < best_code))) {
+      best_gain = gB; best_code = 2 * t + 1; bGL = sg + ng; bHL = sh + nh; bWL = sw + nw;
+    }
+  }
+  double bg = best_gain;
+  int bc = best_code;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double og = __shfl_xor(bg, off, kWave);
+    const int oc = __shfl_xor(bc, off, kWave);
+    if (og > bg || (og == bg && oc < bc)) { bg = og; bc = oc; }
+  }
+  if (lane == 0) { bestg[wid] = bg; bestc[wid] = bc; }
+  __syncthreads();
+  double g0 = bestg[0];
+  int c0 = bestc[0];
+  for (int k = 1; k < 4; ++k)
+    if (bestg[k] > g0 || (bestg[k] == g0 && bestc[k] < c0)) { g0 = bestg[k]; c0 = bestc[k]; }
+  FeatBest* o = out + (int64_t)node * F + f;
+  if (c0 == 0x7fffffff) {
+    if (t == 0) {
+      FeatBest r;
+      r.gain = -INFINITY; r.GL = r.HL = r.WL = 0.0;
+      r.G = tg; r.H = th; r.W = tw;
+      r.code = 0x7fffffff; r.pad = 0;
+      *o = r;
+    }
+  } else if (best_code == c0) {  // unique owner of the winning threshold
+    FeatBest r;
+    r.gain = g0; r.GL = bGL; r.HL = bHL; r.WL = bWL;
+    r.G = tg; r.H = th; r.W = tw;
+    r.code = c0; r.pad = 0;
+    *o = r;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Level finalisation (single workgroup): decide split/leaf per node, number
+// the children, pick the smaller child to build, write tree records and the
+// partition table.  ctl_next receives the next level's counts.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void level_finalize_kernel(const FeatBest* __restrict__ fbest,
+                                                              const int* __restrict__ ctl, int* __restrict__ ctl_next,
+                                                              SplitParams p, const float* __restrict__ edges,
+                                                              const int* __restrict__ nvb, int nbt,
+                                                              int max_next_nodes, PartInfo* __restrict__ part,
+                                                              NodeLink* __restrict__ next_link,
+                                                              TreeNode* __restrict__ tree, int tree_capacity) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  const int n = ctl[CTL_N];
+  const int base = ctl[CTL_BASE];
+  const int next_base = base + n;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < n; c0 += blockDim.x) {
+    const int i = c0 + t;
+    bool do_split = false;
+    NodeSplit s;
+    if (i < n) {
+      // arg-max over features: gain desc, then (feature, bin, na) asc
+      const FeatBest* fb = fbest + (int64_t)i * p.F;
+      int bf = -1;
+      double bg = -INFINITY;
+      int bc = 0x7fffffff;
+      for (int f = 0; f < p.F; ++f) {
+        const FeatBest& c = fb[f];
+        if (c.code == 0x7fffffff || !(c.gain > -INFINITY)) continue;
+        if (bf < 0 || c.gain > bg || (c.gain == bg && (f < bf || (f == bf && c.code < bc)))) {
+          bf = f; bg = c.gain; bc = c.code;
+        }
+      }
+      s.G = fb[0].G; s.H = fb[0].H; s.W = fb[0].W;
+      if (bf >= 0) {
+        const FeatBest& c = fb[bf];
+        s.gain = c.gain; s.GL = c.GL; s.HL = c.HL; s.WL = c.WL;
+        s.feat = bf; s.bin = bc >> 1; s.na_left = bc & 1;
+      } else {
+        s.gain = -INFINITY; s.GL = s.HL = s.WL = 0.0;
+        s.feat = -1; s.bin = 0; s.na_left = 0;
+      }
+      do_split = !p.is_last_level && s.feat >= 0 && isfinite(s.gain) && s.gain > 0.0;
+      if (do_split && p.mode == 0 && p.min_split_improvement > 0.0) {
+        // relative improvement over the node's explained sum of squares
+        const double base_term = (s.W > 0.0) ? s.G * s.G / s.W : 0.0;
+        do_split = s.gain > p.min_split_improvement * fmax(base_term, 1e-12);
+      }
+    }
+    // block exclusive scan of do_split
+    const unsigned long long bal = __ballot(do_split);
+    const int within = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wid] = __popcll(bal);
+    __syncthreads();
+    int before = carry;
+    for (int k = 0; k < wid; ++k) before += wsum[k];
+    const int k_idx = before + within;
+    if (do_split && 2 * (k_idx + 1) > max_next_nodes) do_split = false;  // capacity guard
+    if (i < n) {
+      const int gid = base + i;
+      const double v = leaf_value(s.G, s.H, s.W, p);
+      PartInfo pi;
+      pi.gid = gid;
+      pi.leaf_children = 0;
+      pi.child_gid = -1;
+      pi.pad = 0;
+      TreeNode tn;
+      tn.value = (float)v;
+      tn.weight = (float)s.W;
+      tn.gain = do_split ? (float)s.gain : 0.0f;
+      if (do_split) {
+        pi.feat = s.feat; pi.bin = s.bin; pi.na_left = s.na_left; pi.child = 2 * k_idx;
+        tn.feat = s.feat; tn.bin = s.bin; tn.na_left = s.na_left; tn.left = next_base + 2 * k_idx;
+        const int m = nvb[s.feat];
+        tn.thr = (s.bin < m - 1) ? edges[(int64_t)s.feat * nbt + s.bin] : INFINITY;
+        const bool build_left = s.WL <= (s.W - s.WL);
+        NodeLink L, R;
+        L.parent = R.parent = i;
+        L.pad = R.pad = 0;
+        L.slot = build_left ? k_idx : -1;
+        L.sib_slot = build_left ? -1 : k_idx;
+        R.slot = build_left ? -1 : k_idx;
+        R.sib_slot = build_left ? k_idx : -1;
+        if (next_link) {
+          next_link[2 * k_idx] = L;
+          next_link[2 * k_idx + 1] = R;
+        }
+        pi.child_gid = next_base + 2 * k_idx;
+        if (p.children_leaves) {
+          // children are final: their totals come from this split's left stats
+          pi.leaf_children = 1;
+          const double GR = s.G - s.GL, HR = s.H - s.HL, WR = s.W - s.WL;
+          TreeNode lc, rc;
+          lc.feat = rc.feat = -1;
+          lc.bin = rc.bin = 0;
+          lc.left = rc.left = -1;
+          lc.na_left = rc.na_left = 0;
+          lc.thr = rc.thr = 0.0f;
+          lc.gain = rc.gain = 0.0f;
+          lc.value = (float)leaf_value(s.GL, s.HL, s.WL, p);
+          rc.value = (float)leaf_value(GR, HR, WR, p);
+          lc.weight = (float)s.WL;
+          rc.weight = (float)WR;
+          if (next_base + 2 * k_idx + 1 < tree_capacity) {
+            tree[next_base + 2 * k_idx] = lc;
+            tree[next_base + 2 * k_idx + 1] = rc;
+          }
+        }
+      } else {
+        pi.feat = -1; pi.bin = 0; pi.na_left = 0; pi.child = -1;
+        tn.feat = -1; tn.bin = 0; tn.na_left = 0; tn.left = -1; tn.thr = 0.0f;
+      }
+      part[i] = pi;
+      if (gid < tree_capacity) tree[gid] = tn;
+    }
+    __syncthreads();
+    if (t == 0) {
+      int tot = 0;
+      for (int k = 0; k < (int)(blockDim.x >> 6); ++k) tot += wsum[k];
+      carry += tot;
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    int ks = carry;
+    if (2 * ks > max_next_nodes) ks = max_next_nodes / 2;
+    ctl_next[CTL_N] = 2 * ks;
+    ctl_next[CTL_SLOTS] = ks;
+    ctl_next[CTL_BASE] = next_base;
+    ctl_next[CTL_TOTAL] = next_base + 2 * ks;
+  }
+}
+
+// K6: route every row to its child (or retire it into its leaf: nid = ~gid).
+__global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restrict__ codes, int64_t npad,
+                                                        int* __restrict__ nid, const PartInfo* __restrict__ part,
+                                                        int nbt) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r0 = q * 4;
+  if (r0 >= npad) return;
+  int4 n4 = *reinterpret_cast<int4*>(nid + r0);
+  int nn[4] = {n4.x, n4.y, n4.z, n4.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int n = nn[k];
+    if (n < 0) continue;
+    const PartInfo pi = part[n];
+    if (pi.child < 0) {
+      nn[k] = ~pi.gid;
+    } else {
+      const int b = codes[(int64_t)pi.feat * npad + r0 + k];
+      const int right = (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
+      nn[k] = pi.leaf_children ? ~(pi.child_gid + right) : (pi.child + right);
+    }
+  }
+  *reinterpret_cast<int4*>(nid + r0) = make_int4(nn[0], nn[1], nn[2], nn[3]);
+}
+
+// ---------------------------------------------------------------------------
+// K2 + K7: apply the finished tree to the margins and compute the next
+// tree's gradients, bagging weights and reset the row->node ids, fused in
+// one pass over the rows.
+// dist: 0 gaussian, 1 bernoulli, 2 poisson, 3 gamma, 4 tweedie, 5 laplace,
+//       6 quantile, 7 huber, 8 drf (g = -y, h = 1)
+// ---------------------------------------------------------------------------
+struct GradParams {
+  int dist;
+  int apply_tree;      // add the leaf values of `tree` to F first
+  float sample_rate;   // row bagging (1 = off)
+  uint32_t seed;
+  int tree_index;      // index of the NEXT tree (bag seed)
+  float tweedie_power;
+  float quantile_alpha;
+  float huber_delta;
+};
+
+__device__ __forceinline__ void dist_grad(int dist, float f, float y, const GradParams& gp, float& g, float& h) {
+  switch (dist) {
+    case 0: g = f - y; h = 1.0f; break;
+    case 1: {
+      const float pr = 1.0f / (1.0f + __expf(-f));
+      g = pr - y;
+      h = fmaxf(pr * (1.0f - pr), 1e-16f);
+      break;
+    }
+    case 2: { const float mu = __expf(f); g = mu - y; h = fmaxf(mu, 1e-16f); break; }
+    case 3: { const float e = y * __expf(-f); g = 1.0f - e; h = fmaxf(e, 1e-16f); break; }
+    case 4: {
+      const float rho = gp.tweedie_power;
+      const float a = y * __expf((1.0f - rho) * f), b = __expf((2.0f - rho) * f);
+      g = -a + b;
+      h = fmaxf(-(1.0f - rho) * a + (2.0f - rho) * b, 1e-16f);
+      break;
+    }
+    case 5: g = (f > y) ? 1.0f : ((f < y) ? -1.0f : 0.0f); h = 1.0f; break;
+    case 6: g = (y > f) ? -gp.quantile_alpha : (1.0f - gp.quantile_alpha); h = 1.0f; break;
+    case 7: { const float r = f - y; g = fabsf(r) <= gp.huber_delta ? r : copysignf(gp.huber_delta, r); h = 1.0f; break; }
+    default: g = -y; h = 1.0f; break;  // DRF: fit the response directly
+  }
+}
+
+__global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F, const float* __restrict__ y,
+                                                           const float* __restrict__ wobs, int64_t n, int64_t npad,
+                                                           int* __restrict__ nid, const TreeNode* __restrict__ tree,
+                                                           GradParams gp, float* __restrict__ g, float* __restrict__ h,
+                                                           float* __restrict__ wout) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= npad) return;
+  if (r >= n) {
+    nid[r] = INT32_MIN;
+    g[r] = 0.f; h[r] = 0.f;
+    if (wout) wout[r] = 0.f;
+    return;
+  }
+  float f = F[r];
+  if (gp.apply_tree) {
+    const int leaf = ~nid[r];
+    f += tree[leaf].value;
+    F[r] = f;
+  }
+  float gv, hv;
+  dist_grad(gp.dist, f, y[r], gp, gv, hv);
+  float wv = wobs ? wobs[r] : 1.0f;
+  if (gp.sample_rate < 1.0f) {
+    const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)r, 0x5bd1e995u));
+    if (u >= gp.sample_rate) wv = 0.0f;
+  }
+  g[r] = gv * wv;
+  h[r] = hv * wv;
+  if (wout) wout[r] = wv;
+  nid[r] = 0;
+}
+
+// Apply a finished tree only (multi-class path): F[k][r] += value[leaf].
+__global__ __launch_bounds__(256) void apply_tree_kernel(float* __restrict__ F, int64_t n,
+                                                         const int* __restrict__ nid,
+                                                         const TreeNode* __restrict__ tree) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  F[r] += tree[~nid[r]].value;
+}
+
+// Multinomial softmax gradients for class k plus bagging / nid reset.
+__global__ __launch_bounds__(256) void softmax_grad_kernel(const float* __restrict__ F, int K, int64_t ldF,
+                                                           const int* __restrict__ yk, const float* __restrict__ wobs,
+                                                           int64_t n, int64_t npad, int cls, GradParams gp,
+                                                           int* __restrict__ nid, float* __restrict__ g,
+                                                           float* __restrict__ h, float* __restrict__ wout) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= npad) return;
+  if (r >= n) {
+    nid[r] = INT32_MIN; g[r] = 0.f; h[r] = 0.f;
+    if (wout) wout[r] = 0.f;
+    return;
+  }
+  float mx = -INFINITY;
+  for (int k = 0; k < K; ++k) mx = fmaxf(mx, F[k * ldF + r]);
+  float den = 0.f, fk = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float e = __expf(F[k * ldF + r] - mx);
+    den += e;
+    if (k == cls) fk = e;
+  }
+  const float pk = fk / den;
+  const float yv = (yk[r] == cls) ? 1.0f : 0.0f;
+  float wv = wobs ? wobs[r] : 1.0f;
+  if (gp.sample_rate < 1.0f) {
+    const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)r, 0x5bd1e995u));
+    if (u >= gp.sample_rate) wv = 0.0f;
+  }
+  g[r] = (pk - yv) * wv;
+  h[r] = fmaxf(pk * (1.0f - pk), 1e-16f) * wv;
+  if (wout) wout[r] = wv;
+  nid[r] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// K8: score raw (unbinned) feature-major data with a tree ensemble.
+// nodes: all trees concatenated; roots[t] = offset of tree t; out[cls][r] +=
+// sum of leaf values of the trees of class cls (tree t belongs to class t % K).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void predict_raw_kernel(const float* __restrict__ X, int64_t ld, int64_t n,
+                                                          const TreeNode* __restrict__ nodes,
+                                                          const int* __restrict__ roots, int ntrees, int K,
+                                                          float* __restrict__ out, int64_t ldo) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  for (int t = 0; t < ntrees; ++t) {
+    const TreeNode* tr = nodes + roots[t];
+    int id = 0;
+    for (int guard = 0; guard < 64; ++guard) {
+      const TreeNode nd = tr[id];
+      if (nd.feat < 0) break;
+      const float v = X[(int64_t)nd.feat * ld + r];
+      const bool left = (v != v) ? (nd.na_left != 0) : (v <= nd.thr);
+      id = left ? nd.left : nd.left + 1;
+    }
+    out[(int64_t)(t % K) * ldo + r] += tr[id].value;
+  }
+}
+
+// Same on binned codes (training frame), avoids re-binning.
+__global__ __launch_bounds__(256) void predict_binned_kernel(const uint8_t* __restrict__ codes, int64_t npad,
+                                                             int64_t n, const TreeNode* __restrict__ nodes,
+                                                             const int* __restrict__ roots, int ntrees, int K,
+                                                             int nbt, float* __restrict__ out, int64_t ldo) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  for (int t = 0; t < ntrees; ++t) {
+    const TreeNode* tr = nodes + roots[t];
+    int id = 0;
+    for (int guard = 0; guard < 64; ++guard) {
+      const TreeNode nd = tr[id];
+      if (nd.feat < 0) break;
+      const int b = codes[(int64_t)nd.feat * npad + r];
+      const bool left = (b == nbt - 1) ? (nd.na_left != 0) : (b <= nd.bin);
+      id = left ? nd.left : nd.left + 1;
+    }
+    out[(int64_t)(t % K) * ldo + r] += tr[id].value;
+  }
+}
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+static inline int grid_for(int64_t n, int block, int cap = 1 << 20) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+H2OMX_API int h2omx_tree_sizes(int* out) {
+  out[0] = sizeof(SplitParams);
+  out[1] = sizeof(FeatBest);
+  out[2] = sizeof(NodeLink);
+  out[3] = sizeof(PartInfo);
+  out[4] = sizeof(TreeNode);
+  out[5] = sizeof(GradParams);
+  return kOk;
+}
+
+H2OMX_API int h2omx_bin_features(const float* X, int64_t ld, int64_t n, int F, const float* edges, const int* nvb,
+                                 int nbt, uint8_t* codes, int64_t npad, hipStream_t stream) {
+  if (nbt > 256 || nbt < 2 || npad < n) return kBadArg;
+  dim3 grid(grid_for(npad, 256, 4096), F);
+  hipLaunchKernelGGL(bin_features_kernel, grid, dim3(256), 0, stream, X, ld, n, edges, nvb, nbt, codes, npad);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* g, const float* h, const float* w,
+                               const int* nid, const void* link, const int* ctl, int F, int nbt, int fg,
+                               int n_groups, int wgpg, int slot_lo, int slot_cnt, int rows_per_lane,
+                               float* partials, hipStream_t stream) {
+  if (wgpg % 8 != 0 || npad % 16 != 0) return kBadArg;
+  const size_t lds = (size_t)slot_cnt * fg * 3 * nbt * sizeof(float);
+  if (lds > 160 * 1024) return kBadArg;
+  const int grid = n_groups * wgpg;
+  const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
+#define H2OMX_HB(NB, R)                                                                                      \
+  hipLaunchKernelGGL((hist_build_kernel<NB, R>), dim3(grid), dim3(512), lds, stream, codes, npad, g, h, w, nid, \
+                     lk, ctl, F, fg, n_groups, wgpg, slot_lo, slot_cnt, partials)
+  if (rows_per_lane == 16) {
+    switch (nbt) {
+      case 32: H2OMX_HB(32, 16); break;
+      case 64: H2OMX_HB(64, 16); break;
+      case 128: H2OMX_HB(128, 16); break;
+      case 256: H2OMX_HB(256, 16); break;
+      default: return kBadArg;
+    }
+  } else if (rows_per_lane == 8) {
+    switch (nbt) {
+      case 32: H2OMX_HB(32, 8); break;
+      case 64: H2OMX_HB(64, 8); break;
+      case 128: H2OMX_HB(128, 8); break;
+      case 256: H2OMX_HB(256, 8); break;
+      default: return kBadArg;
+    }
+  } else {
+    return kBadArg;
+  }
+#undef H2OMX_HB
+  return launch_status();
+}
+
+H2OMX_API int h2omx_hist_reduce(const float* partials, int n_groups, int wgpg, int fg, int F, int nbt, int slot_lo,
+                                int slot_cnt, const int* ctl, double* built, hipStream_t stream) {
+  const int64_t total = (int64_t)slot_cnt * F * 3 * nbt;
+  hipLaunchKernelGGL(hist_reduce_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, stream, partials,
+                     n_groups, wgpg, fg, F, nbt, slot_lo, slot_cnt, ctl, built);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_split_find(const double* built, const double* parent_full, double* full, const int* ctl,
+                               const void* link, const int* nvb, const uint8_t* tree_fmask, const void* params,
+                               int max_nodes, int nbt, void* out, hipStream_t stream) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
+  FeatBest* o = reinterpret_cast<FeatBest*>(out);
+  const dim3 grid(max_nodes, p.F);
+  switch (nbt) {
+    case 32: hipLaunchKernelGGL(split_find_kernel<32>, grid, dim3(256), 0, stream, built, parent_full, full, ctl, lk, nvb, tree_fmask, p, o); break;
+    case 64: hipLaunchKernelGGL(split_find_kernel<64>, grid, dim3(256), 0, stream, built, parent_full, full, ctl, lk, nvb, tree_fmask, p, o); break;
+    case 128: hipLaunchKernelGGL(split_find_kernel<128>, grid, dim3(256), 0, stream, built, parent_full, full, ctl, lk, nvb, tree_fmask, p, o); break;
+    case 256: hipLaunchKernelGGL(split_find_kernel<256>, grid, dim3(256), 0, stream, built, parent_full, full, ctl, lk, nvb, tree_fmask, p, o); break;
+    default: return kBadArg;
+  }
+  return launch_status();
+}
+
+H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_next, const void* params,
+                                   const float* edges, const int* nvb, int nbt, int max_next_nodes, void* part,
+                                   void* next_link, void* tree, int tree_capacity, hipStream_t stream) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  hipLaunchKernelGGL(level_finalize_kernel, dim3(1), dim3(1024), 0, stream,
+                     reinterpret_cast<const FeatBest*>(fbest), ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes,
+                     reinterpret_cast<PartInfo*>(part), reinterpret_cast<NodeLink*>(next_link),
+                     reinterpret_cast<TreeNode*>(tree), tree_capacity);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_partition(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt,
+                              hipStream_t stream) {
+  if (npad % 4 != 0) return kBadArg;
+  hipLaunchKernelGGL(partition_kernel, dim3(grid_for(npad / 4, 256)), dim3(256), 0, stream, codes, npad, nid,
+                     reinterpret_cast<const PartInfo*>(part), nbt);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_boost_update(float* F, const float* y, const float* wobs, int64_t n, int64_t npad, int* nid,
+                                 const void* tree, const void* gparams, float* g, float* h, float* wout,
+                                 hipStream_t stream) {
+  const GradParams gp = *reinterpret_cast<const GradParams*>(gparams);
+  hipLaunchKernelGGL(boost_update_kernel, dim3(grid_for(npad, 256)), dim3(256), 0, stream, F, y, wobs, n, npad, nid,
+                     reinterpret_cast<const TreeNode*>(tree), gp, g, h, wout);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_apply_tree(float* F, int64_t n, const int* nid, const void* tree, hipStream_t stream) {
+  hipLaunchKernelGGL(apply_tree_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, F, n, nid,
+                     reinterpret_cast<const TreeNode*>(tree));
+  return launch_status();
+}
+
+H2OMX_API int h2omx_softmax_grad(const float* F, int K, int64_t ldF, const int* yk, const float* wobs, int64_t n,
+                                 int64_t npad, int cls, const void* gparams, int* nid, float* g, float* h,
+                                 float* wout, hipStream_t stream) {
+  const GradParams gp = *reinterpret_cast<const GradParams*>(gparams);
+  hipLaunchKernelGGL(softmax_grad_kernel, dim3(grid_for(npad, 256)), dim3(256), 0, stream, F, K, ldF, yk, wobs, n,
+                     npad, cls, gp, nid, g, h, wout);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_predict_raw(const float* X, int64_t ld, int64_t n, const void* nodes, const int* roots,
+                                int ntrees, int K, float* out, int64_t ldo, hipStream_t stream) {
+  hipLaunchKernelGGL(predict_raw_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, X, ld, n,
+                     reinterpret_cast<const TreeNode*>(nodes), roots, ntrees, K, out, ldo);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_predict_binned(const uint8_t* codes, int64_t npad, int64_t n, const void* nodes,
+                                   const int* roots, int ntrees, int K, int nbt, float* out, int64_t ldo,
+                                   hipStream_t stream) {
+  hipLaunchKernelGGL(predict_binned_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, codes, npad, n,
+                     reinterpret_cast<const TreeNode*>(nodes), roots, ntrees, K, nbt, out, ldo);
+  return launch_status();
+}

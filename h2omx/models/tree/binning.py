@@ -1,0 +1,122 @@
+"""K1: quantile sketch + feature binning into uint8 codes (feature-major).
+
+Cut points are per-feature weighted-free quantiles of a row sample.  With
+several ranks, every rank contributes a sample and the samples are
+all-gathered so all ranks derive bit-identical cut points (SURVEY.md §2.5 K1,
+collective C1).  Codes are stored ``[F][npad]`` with ``npad`` a multiple of 64
+so that histogram lanes can issue 16-byte loads of 16 consecutive rows.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ... import ops
+
+ROW_ALIGN = 64
+
+
+@dataclass
+class BinnedMatrix:
+    codes: torch.Tensor      # uint8 [F][npad]
+    edges: torch.Tensor      # float32 [F][nbt]  (edges[f][:nvb[f]-1] used)
+    nvb: torch.Tensor        # int32 [F] number of value bins per feature
+    n: int
+    npad: int
+    nbt: int                 # histogram width; bin nbt-1 is the NA bin
+    names: list
+
+    @property
+    def F(self) -> int:
+        return self.codes.shape[0]
+
+    @property
+    def device(self):
+        return self.codes.device
+
+    def edges_numpy(self):
+        e = self.edges.cpu().numpy()
+        nv = self.nvb.cpu().numpy()
+        return [e[f, : max(int(nv[f]) - 1, 0)].copy() for f in range(len(nv))]
+
+
+def hist_width(nbins: int) -> int:
+    """Smallest supported histogram width holding nbins value bins + NA."""
+    for w in (32, 64, 128, 256):
+        if nbins + 1 <= w:
+            return w
+    return 256
+
+
+def _edges_from_sorted(col: np.ndarray, max_value_bins: int) -> np.ndarray:
+    col = col[~np.isnan(col)]
+    if col.size == 0:
+        return np.zeros(0, np.float32)
+    uniq = np.unique(col)
+    if uniq.size <= max_value_bins:
+        return uniq[:-1].astype(np.float32)
+    qs = np.quantile(col, np.linspace(0.0, 1.0, max_value_bins + 1)[1:-1], method="lower")
+    e = np.unique(qs.astype(np.float32))
+    # the top edge must be below the max so the last bin is non-empty
+    e = e[e < uniq[-1]]
+    return e[: max_value_bins - 1]
+
+
+def compute_edges(X: torch.Tensor, nbins: int, sample_rows: int = 1 << 20, seed: int = 1234,
+                  comm=None) -> tuple[np.ndarray, np.ndarray, int]:
+    """Per-feature cut points from a row sample of feature-major ``X`` [F][n].
+
+    Returns (edges [F][nbt] float32, nvb [F] int32, nbt).
+    """
+    F, n = X.shape
+    nbt = hist_width(nbins)
+    max_value_bins = min(nbins, nbt - 1)
+    if n > sample_rows:
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        idx = torch.randint(0, n, (sample_rows,), generator=g).to(X.device)
+        S = X.index_select(1, idx)
+    else:
+        S = X
+    if comm is not None and comm.world_size > 1:
+        S = comm.all_gather_cat(S.contiguous(), dim=1)
+    if S.is_cuda:
+        S = torch.sort(S, dim=1).values
+    Sn = S.float().cpu().numpy()
+    edges = np.full((F, nbt), np.inf, np.float32)
+    nvb = np.zeros(F, np.int32)
+    for f in range(F):
+        e = _edges_from_sorted(Sn[f], max_value_bins)
+        edges[f, : e.size] = e
+        nvb[f] = e.size + 1
+    return edges, nvb, nbt
+
+
+def bin_matrix(X: torch.Tensor, edges: np.ndarray, nvb: np.ndarray, nbt: int, names=None) -> BinnedMatrix:
+    """Bin feature-major float32 ``X`` [F][n] (any stride on dim 1 == 1)."""
+    F, n = X.shape
+    npad = max(ROW_ALIGN, int(math.ceil(n / ROW_ALIGN) * ROW_ALIGN))
+    dev = X.device
+    names = list(names) if names is not None else [f"C{i + 1}" for i in range(F)]
+    e_t = torch.from_numpy(np.ascontiguousarray(edges, np.float32)).to(dev)
+    nv_t = torch.from_numpy(np.ascontiguousarray(nvb, np.int32)).to(dev)
+    if X.is_cuda:
+        Xc = X.float().contiguous()
+        codes = torch.empty((F, npad), dtype=torch.uint8, device=dev)
+        lib = ops.tree()
+        ops.check(lib.h2omx_bin_features(ops.P(Xc), Xc.stride(0), n, F, ops.P(e_t), ops.P(nv_t), nbt,
+                                         ops.P(codes), npad, ops.stream(dev)), "bin_features")
+    else:
+        Xn = X.float().numpy()
+        codes_np = np.zeros((F, npad), np.uint8)
+        for f in range(F):
+            m = int(nvb[f]) - 1
+            col = Xn[f]
+            c = np.searchsorted(edges[f, :m], col, side="left").astype(np.uint8)
+            c[np.isnan(col)] = nbt - 1
+            codes_np[f, :n] = c
+        codes = torch.from_numpy(codes_np)
+    return BinnedMatrix(codes=codes, edges=e_t, nvb=nv_t, n=n, npad=npad, nbt=nbt, names=names)
+

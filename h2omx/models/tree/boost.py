@@ -1,0 +1,307 @@
+"""Boosting / bagging driver shared by GBM, XGBoost and DRF.
+
+One call to :func:`train_ensemble` grows ``ntrees`` iterations (``K`` trees
+per iteration for multinomial / multi-class DRF).  On the GPU every
+iteration is a fixed sequence of enqueued kernels (no host sync): the fused
+``boost_update`` kernel applies the finished tree to the margins and
+produces the next gradients, bagging weights and node ids in one pass.
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ... import ops
+from .binning import BinnedMatrix
+from .engine import HipTreeBuilder, TreeParams, make_grad_params, tree_capacity, trees_from_bytes
+from .reference import RefTreeBuilder, bag_weights, dist_grad
+from .structs import TREE_NODE_DTYPE
+
+
+@dataclass
+class TreeEnsemble:
+    trees: np.ndarray            # [n_trees_total][capacity] TREE_NODE_DTYPE
+    K: int                       # trees per iteration (classes for multinomial)
+    dist: str
+    init_f: np.ndarray           # [K] initial margin
+    average: bool = False        # DRF: prediction = sum / ntrees
+    nbt: int = 256
+    feature_names: list = field(default_factory=list)
+    edges: list = field(default_factory=list)   # per-feature numpy cut points
+    timings: dict = field(default_factory=dict)
+
+    @property
+    def ntrees(self) -> int:
+        return self.trees.shape[0] // max(self.K, 1)
+
+    def compact(self):
+        """Per tree, the list of reachable node records (for export)."""
+        out = []
+        for t in range(self.trees.shape[0]):
+            tr = self.trees[t]
+            keep, stack = [], [0]
+            while stack:
+                i = stack.pop()
+                keep.append(i)
+                if tr[i]["feat"] >= 0:
+                    stack += [int(tr[i]["left"]) + 1, int(tr[i]["left"])]
+            out.append(sorted(keep))
+        return out
+
+    # -- scoring ---------------------------------------------------------------
+    def raw_margin(self, X: torch.Tensor, ntrees: int | None = None) -> torch.Tensor:
+        """Margins [K][n] for feature-major raw data X [F][n]."""
+        nt = self.ntrees if ntrees is None else ntrees
+        T = nt * self.K
+        n = X.shape[1]
+        if X.is_cuda:
+            dev = X.device
+            Xc = X.float().contiguous()
+            nodes = torch.from_numpy(self.trees[:T].reshape(-1).view(np.uint8).copy()).to(dev)
+            cap = self.trees.shape[1]
+            roots = torch.arange(T, dtype=torch.int32, device=dev) * cap
+            out = torch.empty((self.K, n), dtype=torch.float32, device=dev)
+            out.copy_(torch.from_numpy(np.repeat(self.init_f.astype(np.float32)[:, None], n, 1)).to(dev)
+                      if not self.average else torch.zeros_like(out))
+            if T:
+                lib = ops.tree()
+                ops.check(lib.h2omx_predict_raw(ops.P(Xc), Xc.stride(0), n, ops.P(nodes), ops.P(roots), T, self.K,
+                                                ops.P(out), out.stride(0), ops.stream(dev)), "predict_raw")
+            if self.average and nt > 0:
+                out /= nt
+            return out
+        Xn = X.float().numpy()
+        out = np.zeros((self.K, n), np.float64) if self.average else np.repeat(self.init_f[:, None], n, 1).astype(np.float64)
+        for t in range(T):
+            out[t % self.K] += predict_tree_numpy(self.trees[t], Xn)
+        if self.average and nt > 0:
+            out /= nt
+        return torch.from_numpy(out.astype(np.float32))
+
+
+def predict_tree_numpy(tree: np.ndarray, Xn: np.ndarray) -> np.ndarray:
+    n = Xn.shape[1]
+    idx = np.zeros(n, np.int64)
+    for _ in range(64):
+        feat = tree["feat"][idx]
+        inner = feat >= 0
+        if not inner.any():
+            break
+        r = np.nonzero(inner)[0]
+        v = Xn[feat[r], r]
+        nd = tree[idx[r]]
+        left = np.where(np.isnan(v), nd["na_left"] != 0, v <= nd["thr"])
+        idx[r] = np.where(left, nd["left"], nd["left"] + 1)
+    return tree["value"][idx].astype(np.float64)
+
+
+def init_margin(dist: str, y: np.ndarray, w: np.ndarray | None, K: int) -> np.ndarray:
+    ww = np.ones_like(y, dtype=np.float64) if w is None else w.astype(np.float64)
+    sw = ww.sum()
+    if dist == "bernoulli":
+        p = float(np.clip((ww * y).sum() / sw, 1e-6, 1 - 1e-6))
+        return np.array([np.log(p / (1 - p))])
+    if dist == "multinomial":
+        return np.zeros(K)
+    if dist in ("poisson", "gamma", "tweedie"):
+        return np.array([np.log(max((ww * y).sum() / sw, 1e-12))])
+    if dist in ("laplace", "quantile"):
+        return np.array([float(np.median(y))])
+    if dist == "drf":
+        return np.zeros(K)
+    return np.array([(ww * y).sum() / sw])
+
+
+def train_ensemble(bm: BinnedMatrix, y, w=None, *, dist: str = "bernoulli", ntrees: int = 50,
+                   tparams: TreeParams | None = None, sample_rate: float = 1.0, nclass: int = 1,
+                   seed: int = 0, comm=None, init_f: np.ndarray | None = None, callback=None,
+                   dist_kw: dict | None = None) -> TreeEnsemble:
+    """Grow an ensemble on binned data.
+
+    ``y``: float targets (class index for multinomial / multi-class DRF).
+    ``dist``: gaussian|bernoulli|multinomial|poisson|gamma|tweedie|laplace|quantile|huber|drf.
+    """
+    tparams = tparams or TreeParams()
+    dist_kw = dist_kw or {}
+    n = bm.n
+    multi = dist == "multinomial" or (dist == "drf" and nclass > 2)
+    K = nclass if multi else 1
+    y_np = y.detach().float().cpu().numpy() if torch.is_tensor(y) else np.asarray(y, np.float32)
+    w_np = None if w is None else (w.detach().float().cpu().numpy() if torch.is_tensor(w) else np.asarray(w, np.float32))
+    if init_f is None:
+        if comm is not None and comm.world_size > 1:
+            init_f = _global_init(dist, y_np, w_np, K, comm)
+        else:
+            init_f = init_margin(dist, y_np, w_np, K)
+    ens = TreeEnsemble(trees=np.zeros((0, tree_capacity(tparams.max_depth)), TREE_NODE_DTYPE), K=K, dist=dist,
+                       init_f=np.asarray(init_f, np.float64), average=(dist == "drf"), nbt=bm.nbt,
+                       feature_names=list(bm.names), edges=bm.edges_numpy())
+    if bm.codes.is_cuda:
+        _train_gpu(bm, y_np, w_np, ens, ntrees, tparams, sample_rate, seed, comm, callback, dist_kw)
+    else:
+        _train_cpu(bm, y_np, w_np, ens, ntrees, tparams, sample_rate, seed, comm, callback, dist_kw)
+    return ens
+
+
+def _global_init(dist, y, w, K, comm):
+    ww = np.ones_like(y, dtype=np.float64) if w is None else w.astype(np.float64)
+    s = comm.all_reduce_numpy(np.array([(ww * y).sum(), ww.sum()], np.float64))
+    m = s[0] / max(s[1], 1e-300)
+    if dist == "bernoulli":
+        p = float(np.clip(m, 1e-6, 1 - 1e-6))
+        return np.array([np.log(p / (1 - p))])
+    if dist in ("multinomial", "drf"):
+        return np.zeros(K)
+    if dist in ("poisson", "gamma", "tweedie"):
+        return np.array([np.log(max(m, 1e-12))])
+    return np.array([m])
+
+
+class _GpuState:
+    def __init__(self, bm, y_np, w_np, K, dist, init_f):
+        dev = bm.device
+        npad, n = bm.npad, bm.n
+        self.Fm = torch.zeros((K, npad), dtype=torch.float32, device=dev)
+        for k in range(K):
+            self.Fm[k, :n] = float(init_f[k])
+        yp = np.zeros(npad, np.float32)
+        yp[:n] = y_np
+        self.y = torch.from_numpy(yp).to(dev)
+        self.yk = self.y.to(torch.int32) if K > 1 else None
+        if dist == "drf" and K > 1:
+            self.ycls = torch.stack([(self.y == k).float() for k in range(K)])
+        self.w = None
+        if w_np is not None:
+            wp = np.zeros(npad, np.float32)
+            wp[:n] = w_np
+            self.w = torch.from_numpy(wp).to(dev)
+        self.g = torch.empty((K, npad), dtype=torch.float32, device=dev)
+        self.h = torch.empty((K, npad), dtype=torch.float32, device=dev)
+
+
+class GpuBooster:
+    """Step-wise GPU boosting loop (one ``step()`` = one iteration = K trees)."""
+
+    def __init__(self, bm, y_np, w_np, ens, tp, sample_rate, seed, comm, dist_kw, ntrees_hint=64):
+        self.lib = ops.tree()
+        self.bm, self.ens, self.tp = bm, ens, tp
+        self.sample_rate, self.seed = sample_rate, seed
+        self.dev = bm.device
+        self.K, self.dist = ens.K, ens.dist
+        self.st = _GpuState(bm, y_np, w_np, self.K, self.dist, ens.init_f)
+        self.builder = HipTreeBuilder(bm, tp, comm)
+        self.cap = self.builder.capacity
+        self.trees_dev = []
+        need_w = sample_rate < 1.0 or self.st.w is not None
+        self.wout = torch.empty((bm.npad,), dtype=torch.float32, device=self.dev) if need_w else None
+        self.kw = dict(tweedie_power=dist_kw.get("tweedie_power", 1.5),
+                       quantile_alpha=dist_kw.get("quantile_alpha", 0.5),
+                       huber_delta=dist_kw.get("huber_delta", 1.0))
+        self.t = 0
+        if self.K == 1:
+            self._update(apply=False, next_tree=0, k=0)
+
+    def _update(self, apply: bool, next_tree: int, k: int, dist=None):
+        P, st, b = ops.P, self.st, self.builder
+        gp = make_grad_params(dist or self.dist, apply, self.sample_rate, self.seed, next_tree, **self.kw)
+        y = st.ycls[k] if (self.dist == "drf" and self.K > 1) else st.y
+        ops.check(self.lib.h2omx_boost_update(P(st.Fm[k]), P(y), P(st.w), self.bm.n, self.bm.npad, P(b.nid),
+                                              P(b.tree_buf), ctypes.addressof(gp), P(st.g[k]), P(st.h[k]),
+                                              P(self.wout), ops.stream(self.dev)), "boost_update")
+
+    def step(self):
+        P, st, b, bm, t = ops.P, self.st, self.builder, self.bm, self.t
+        fmask = _tree_fmask(self.tp, bm.F, t, self.dev)
+        if self.K == 1:
+            b.build(st.g[0], st.h[0], self.wout, t, fmask)
+            self.trees_dev.append(b.tree_buf.clone())
+            self._update(apply=True, next_tree=t + 1, k=0)
+        else:
+            s = ops.stream(self.dev)
+            gp = make_grad_params("bernoulli", False, self.sample_rate, self.seed, t, **self.kw)
+            for k in range(self.K):
+                if self.dist == "drf":
+                    self._update(apply=False, next_tree=t, k=k)
+                else:
+                    ops.check(self.lib.h2omx_softmax_grad(P(st.Fm), self.K, st.Fm.stride(0), P(st.yk), P(st.w),
+                                                          bm.n, bm.npad, k, ctypes.addressof(gp), P(b.nid),
+                                                          P(st.g[k]), P(st.h[k]), P(self.wout), s), "softmax_grad")
+            for k in range(self.K):
+                b.nid[: bm.n].zero_()
+                b.build(st.g[k], st.h[k], self.wout, t * self.K + k, fmask)
+                self.trees_dev.append(b.tree_buf.clone())
+                ops.check(self.lib.h2omx_apply_tree(P(st.Fm[k]), bm.n, P(b.nid), P(b.tree_buf), s), "apply_tree")
+        self.t += 1
+
+    def finish(self) -> TreeEnsemble:
+        torch.cuda.synchronize(self.dev)
+        if self.trees_dev:
+            self.ens.trees = trees_from_bytes(torch.stack(self.trees_dev).cpu().numpy(), self.cap)
+        self.ens._state = self.st
+        return self.ens
+
+
+def _train_gpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw):
+    t0 = time.perf_counter()
+    gb = GpuBooster(bm, y_np, w_np, ens, tp, sample_rate, seed, comm, dist_kw)
+    for t in range(ntrees):
+        gb.step()
+        if callback is not None:
+            callback(t, gb.st)
+    gb.finish()
+    ens.timings["train_s"] = time.perf_counter() - t0
+
+
+def _tree_fmask(tp: TreeParams, F: int, t: int, dev):
+    if tp.col_sample_rate_per_tree >= 1.0:
+        return None
+    from .reference import hash4, u01
+
+    hs = hash4(tp.seed & 0xFFFFFFFF, 0xC0FFEE, t, np.arange(F))
+    m = (u01(hs) < tp.col_sample_rate_per_tree).astype(np.uint8)
+    if m.sum() == 0:
+        m[int(np.argmin(hs))] = 1
+    return torch.from_numpy(m).to(dev) if dev is not None else m
+
+
+def _train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw):
+    K, dist, n = ens.K, ens.dist, bm.n
+    builder = RefTreeBuilder(bm, tp, comm)
+    Fm = np.repeat(ens.init_f[:, None], n, 1).astype(np.float32)
+    wobs = np.ones(n, np.float32) if w_np is None else w_np.astype(np.float32)
+    trees = []
+    t0 = time.perf_counter()
+    for t in range(ntrees):
+        wb = wobs * bag_weights(n, sample_rate, seed, t)
+        if K == 1:
+            gr, hs = dist_grad(dist, Fm[0], y_np, **dist_kw)
+            grads = [(gr, hs)]
+        elif dist == "drf":
+            grads = [(-(y_np == k).astype(np.float64), np.ones(n)) for k in range(K)]
+        else:
+            z = Fm - Fm.max(axis=0, keepdims=True)
+            pr = np.exp(z)
+            pr /= pr.sum(axis=0, keepdims=True)
+            grads = [(pr[k] - (y_np == k), np.maximum(pr[k] * (1 - pr[k]), 1e-16)) for k in range(K)]
+        fmask = _tree_fmask(tp, bm.F, t, None)
+        for k in range(K):
+            gr, hs = grads[k]
+            pad = bm.npad - n
+            builder.nid[:] = -1
+            builder.nid[:n] = 0
+            g32 = np.concatenate([(gr * wb).astype(np.float32), np.zeros(pad, np.float32)])
+            h32 = np.concatenate([(hs * wb).astype(np.float32), np.zeros(pad, np.float32)])
+            w32 = np.concatenate([wb, np.zeros(pad, np.float32)])
+            tree = builder.build(g32, h32, w32, t * K + k, fmask)
+            leaf = ~builder.nid[:n]
+            Fm[k] += tree["value"][leaf]
+            trees.append(tree)
+        if callback is not None:
+            callback(t, Fm)
+    ens.timings["train_s"] = time.perf_counter() - t0
+    ens.trees = np.stack(trees) if trees else ens.trees
+    ens._cpu_margin = Fm

@@ -1,0 +1,213 @@
+"""Level-wise histogram tree builder (the GBM / XGBoost / DRF hot loop).
+
+``HipTreeBuilder`` drives the gfx950 kernels of ``csrc/tree_kernels.hip``.
+Per tree level it enqueues, on the current HIP stream and without any host
+synchronisation::
+
+    hist_build (LDS)  ->  hist_reduce (fp64)  ->  [all_reduce over RCCL]
+    -> split_find (node x feature)  ->  level_finalize  ->  partition
+
+The decision of which nodes split, how children are numbered and which child
+is histogrammed (the smaller one; its sibling comes from parent - child) is
+taken on the device, so the host never waits for the GPU inside a tree.
+
+``RefTreeBuilder`` (``reference.py``) implements the same algorithm with
+NumPy on the CPU; it is the test oracle and the CPU plumbing path.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ... import ops
+from .binning import BinnedMatrix
+from .structs import (FEAT_BEST_BYTES, NODE_LINK_BYTES, PART_INFO_BYTES, TREE_NODE_DTYPE, GradParams,
+                      SplitParams, check_layout)
+
+
+@dataclass
+class TreeParams:
+    max_depth: int = 5
+    min_rows: float = 10.0
+    min_child_weight: float = 0.0
+    reg_lambda: float = 0.0
+    reg_alpha: float = 0.0
+    gamma: float = 0.0
+    min_split_improvement: float = 1e-5
+    learn_rate: float = 0.1
+    mode: int = 0            # 0: H2O squared error on residuals, 1: XGBoost second order
+    leaf_mode: int = 0       # 0: Newton (-G/(H+lambda)), 1: mean (DRF)
+    col_sample_rate: float = 1.0
+    col_sample_rate_per_tree: float = 1.0
+    mtries: int = 0
+    max_abs_leaf: float = 0.0
+    seed: int = 0
+    extra: dict = field(default_factory=dict)
+
+
+def tree_capacity(max_depth: int) -> int:
+    return (1 << (max_depth + 1)) - 1
+
+
+class HipTreeBuilder:
+    """Builds one tree per call entirely with enqueued HIP kernels."""
+
+    LDS_BUDGET = 64 * 1024     # bytes of LDS histogram per 512-thread workgroup (2 WGs per CU)
+    TARGET_WGS = 512           # 2 workgroups x 256 CUs
+    ROWS_PER_LANE = 16
+    SYNC_NODE_CAP = 4096       # above this many potential nodes the host reads the real count
+
+    def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
+        if not bm.codes.is_cuda:
+            raise ValueError("HipTreeBuilder needs device-resident codes")
+        self.lib = ops.tree()
+        check_layout(self.lib)
+        self.bm = bm
+        self.p = params
+        self.comm = comm
+        self.dev = bm.codes.device
+        self.F = bm.F
+        self.nbt = bm.nbt
+        self.per_node = self.F * 3 * self.nbt  # doubles per node histogram
+        if params.max_depth < 1:
+            raise ValueError("max_depth must be >= 1")
+        self.capacity = tree_capacity(min(params.max_depth, 24))
+        d = self.dev
+        self.ctl = torch.zeros((2, 4), dtype=torch.int32, device=d)
+        self.ctl_init = torch.tensor([1, 1, 0, 1], dtype=torch.int32, device=d)
+        self.link_init = torch.tensor([0, -1, -1, 0], dtype=torch.int32, device=d)
+        self._bufs: dict[str, torch.Tensor] = {}
+        self.tree_buf = torch.zeros((self.capacity * TREE_NODE_DTYPE.itemsize,), dtype=torch.uint8, device=d)
+        self.nid = torch.full((bm.npad,), -1, dtype=torch.int32, device=d)
+        self._sp = SplitParams()
+        self.stats = {"host_syncs": 0}
+
+    # -- buffers -----------------------------------------------------------
+    def _buf(self, name: str, numel: int, dtype) -> torch.Tensor:
+        b = self._bufs.get(name)
+        if b is None or b.numel() < numel:
+            b = torch.empty((max(numel, 1),), dtype=dtype, device=self.dev)
+            self._bufs[name] = b
+        return b
+
+    # -- planning ------------------------------------------------------------
+    def plan_level(self, max_slots: int):
+        """Feature grouping / slot passes / grid for a level with max_slots built nodes."""
+        per_slot_feat = 3 * self.nbt * 4
+        F = self.F
+        if max_slots * per_slot_feat <= self.LDS_BUDGET:
+            slot_cnt = max_slots
+            fg_max = max(1, min(F, self.LDS_BUDGET // (max_slots * per_slot_feat)))
+            n_groups = math.ceil(F / fg_max)
+            fg = math.ceil(F / n_groups)
+            passes = 1
+        else:
+            fg, n_groups = 1, F
+            slot_cnt = max(1, self.LDS_BUDGET // per_slot_feat)
+            passes = math.ceil(max_slots / slot_cnt)
+        units = self.bm.npad // self.ROWS_PER_LANE
+        wgpg = max(8, (self.TARGET_WGS // n_groups) // 8 * 8)
+        # keep at least ~2 row units per lane per workgroup
+        max_wgpg = max(8, (units // (512 * 2)) // 8 * 8)
+        wgpg = min(wgpg, max_wgpg)
+        return dict(slot_cnt=slot_cnt, fg=fg, n_groups=n_groups, passes=passes, wgpg=wgpg)
+
+    # -- one tree ------------------------------------------------------------
+    def build(self, g: torch.Tensor, h: torch.Tensor, w: torch.Tensor | None, tree_index: int,
+              tree_fmask: torch.Tensor | None = None) -> torch.Tensor:
+        """Grow one tree from per-row (g, h, w); ``self.nid`` must be 0 for rows
+        of the tree and INT_MIN for padding.  Returns the device tree buffer
+        (``TREE_NODE_DTYPE`` records, heap of capacity nodes; unused = garbage)."""
+        lib, bm, p = self.lib, self.bm, self.p
+        st = ops.stream(self.dev)
+        P = ops.P
+        F, nbt = self.F, self.nbt
+        sp = self._sp
+        sp.mode, sp.leaf_mode, sp.F, sp.is_last_level = p.mode, p.leaf_mode, F, 0
+        sp.min_rows, sp.min_child_weight = p.min_rows, p.min_child_weight
+        sp.lambda_, sp.alpha, sp.gamma = p.reg_lambda, p.reg_alpha, p.gamma
+        sp.min_split_improvement, sp.learn_rate, sp.max_abs_leaf = p.min_split_improvement, p.learn_rate, p.max_abs_leaf
+        sp.seed, sp.tree_index = p.seed & 0xFFFFFFFF, tree_index
+        sp.col_rate, sp.mtries = p.col_sample_rate, p.mtries
+        spp = ctypes.addressof(sp)
+
+        self.ctl[0].copy_(self.ctl_init)
+        link = [self._buf("link0", 4 * 1, torch.int32), None]
+        link[0][:4].copy_(self.link_init)
+        full_prev = None
+        max_depth = p.max_depth
+        max_nodes = 1
+        for d in range(max_depth):
+            cur, nxt = d % 2, (d + 1) % 2
+            ctl_cur, ctl_nxt = self.ctl[cur], self.ctl[nxt]
+            if max_nodes > self.SYNC_NODE_CAP:
+                n_now, s_now = [int(v) for v in ctl_cur[:2].tolist()]
+                self.stats["host_syncs"] += 1
+                if n_now == 0:
+                    break
+                max_nodes, max_slots = n_now, s_now
+            else:
+                max_slots = 1 if d == 0 else max(1, max_nodes // 2)
+            last = d == max_depth - 1
+            plan = self.plan_level(max_slots)
+            built = self._buf("built", max_slots * self.per_node, torch.float64)
+            hist_floats = plan["slot_cnt"] * plan["fg"] * 3 * nbt
+            partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_floats, torch.float32)
+            for ps in range(plan["passes"]):
+                slot_lo = ps * plan["slot_cnt"]
+                ops.check(lib.h2omx_hist_build(P(bm.codes), bm.npad, P(g), P(h), P(w), P(self.nid), P(link[cur]),
+                                               P(ctl_cur), F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"],
+                                               slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, P(partials), st),
+                          "hist_build")
+                ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F, nbt,
+                                                slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st), "hist_reduce")
+            if self.comm is not None and self.comm.world_size > 1:
+                self.comm.all_reduce_(built[: max_slots * self.per_node])
+            full_cur = None if last else self._buf(f"full{cur}", max_nodes * self.per_node, torch.float64)
+            fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
+            sp.depth = d
+            sp.children_leaves = 1 if last else 0
+            ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
+                                           P(bm.nvb), P(tree_fmask), spp, max_nodes, nbt, P(fbest), st),
+                      "split_find")
+            next_nodes = 2 * max_nodes
+            part = self._buf("part", max_nodes * PART_INFO_BYTES // 4, torch.int32)
+            nl = None
+            if not last:
+                nl = self._buf(f"link{nxt}", next_nodes * NODE_LINK_BYTES // 4, torch.int32)
+                link[nxt] = nl
+            ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges), P(bm.nvb), nbt,
+                                               next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity, st),
+                      "level_finalize")
+            ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, st), "partition")
+            full_prev = full_cur
+            max_nodes = next_nodes
+        return self.tree_buf
+
+    def tree_size(self) -> torch.Tensor:
+        """Device scalar with the node count of the last tree (ctl TOTAL)."""
+        return self.ctl[self.p.max_depth % 2, 3]
+
+
+def trees_from_bytes(buf: np.ndarray, capacity: int) -> np.ndarray:
+    """View raw bytes as [ntrees][capacity] TREE_NODE_DTYPE records."""
+    arr = np.frombuffer(buf.tobytes(), dtype=TREE_NODE_DTYPE)
+    return arr.reshape(-1, capacity)
+
+
+def make_grad_params(dist: str, apply_tree: bool, sample_rate: float, seed: int, tree_index: int,
+                     tweedie_power: float = 1.5, quantile_alpha: float = 0.5, huber_delta: float = 1.0) -> GradParams:
+    from .structs import DIST_CODES
+
+    gp = GradParams()
+    gp.dist = DIST_CODES[dist]
+    gp.apply_tree = 1 if apply_tree else 0
+    gp.sample_rate = sample_rate
+    gp.seed = seed & 0xFFFFFFFF
+    gp.tree_index = tree_index
+    gp.tweedie_power, gp.quantile_alpha, gp.huber_delta = tweedie_power, quantile_alpha, huber_delta
+    return gp

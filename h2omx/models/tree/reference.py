@@ -1,0 +1,264 @@
+"""CPU (NumPy) implementation of the level-wise histogram tree algorithm.
+
+This mirrors ``csrc/tree_kernels.hip`` decision for decision (same gain
+formulas, constraints, tie-breaking, child numbering, hashing for sampling)
+and serves two purposes:
+
+* the **numerics oracle** for the HIP kernels in ``tests/`` (GPU results are
+  compared against it), and
+* the CPU plumbing path (e.g. the "1-replica H2O CR on kind (CPU)" config),
+  so the REST/operator stack is testable on machines without an MI355X.
+
+It is not a performance path.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .binning import BinnedMatrix
+from .engine import TreeParams, tree_capacity
+from .structs import DIST_CODES, TREE_NODE_DTYPE
+
+M32 = np.uint64(0xFFFFFFFF)
+
+
+def _mix32(x):
+    x = np.asarray(x, dtype=np.uint64) & M32
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & M32
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & M32
+    x ^= x >> np.uint64(16)
+    return x
+
+
+def hash4(a, b, c, d):
+    a, b, c, d = (np.asarray(v, dtype=np.uint64) & M32 for v in (a, b, c, d))
+    return _mix32(a ^ _mix32(b ^ _mix32(c ^ _mix32((d + np.uint64(0x9E3779B9)) & M32))))
+
+
+def u01(hv):
+    return (np.asarray(hv, dtype=np.uint64) >> np.uint64(8)).astype(np.float64) * (1.0 / 16777216.0)
+
+
+def _l1(g, a):
+    if a <= 0:
+        return g
+    return np.where(g > a, g - a, np.where(g < -a, g + a, 0.0))
+
+
+def split_gain(GL, HL, WL, G, H, W, p: TreeParams):
+    GR, HR, WR = G - GL, H - HL, W - WL
+    ok = (WL >= p.min_rows) & (WR >= p.min_rows) & (WL > 0) & (WR > 0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        if p.mode == 0:
+            gain = GL * GL / WL + GR * GR / WR - G * G / W
+        else:
+            ok &= (HL >= p.min_child_weight) & (HR >= p.min_child_weight)
+            lam = p.reg_lambda
+            tl, tr, tt = _l1(GL, p.reg_alpha), _l1(GR, p.reg_alpha), _l1(G, p.reg_alpha)
+            gain = 0.5 * (tl * tl / (HL + lam) + tr * tr / (HR + lam) - tt * tt / (H + lam)) - p.gamma
+    return np.where(ok, gain, -np.inf)
+
+
+def leaf_value(G, H, W, p: TreeParams):
+    if p.leaf_mode == 1:
+        v = -G / W if W > 0 else 0.0
+    else:
+        g = float(_l1(np.float64(G), p.reg_alpha))
+        den = H + p.reg_lambda
+        v = -g / den if den > 1e-12 else 0.0
+    v *= p.learn_rate
+    if p.max_abs_leaf > 0:
+        v = min(max(v, -p.max_abs_leaf), p.max_abs_leaf)
+    return v
+
+
+def feature_allowed(p: TreeParams, F: int, tree_index: int, depth: int, node: int, tree_fmask=None):
+    allowed = np.ones(F, bool) if tree_fmask is None else np.asarray(tree_fmask, bool).copy()
+    if p.mtries > 0 or p.col_sample_rate < 1.0:
+        key = (tree_index * 131 + depth) & 0xFFFFFFFF
+        hs = hash4(p.seed & 0xFFFFFFFF, key, node, np.arange(F))
+        if p.mtries > 0:
+            order = np.lexsort((np.arange(F), hs))
+            rank = np.empty(F, np.int64)
+            rank[order] = np.arange(F)
+            allowed &= rank < p.mtries
+        else:
+            allowed &= u01(hs) < np.float32(p.col_sample_rate)
+    return allowed
+
+
+class RefTreeBuilder:
+    def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
+        self.bm = bm
+        self.p = params
+        self.comm = comm
+        self.codes = bm.codes.numpy() if hasattr(bm.codes, "numpy") else np.asarray(bm.codes)
+        self.nvb = np.asarray(bm.nvb.cpu().numpy() if hasattr(bm.nvb, "cpu") else bm.nvb)
+        self.edges = np.asarray(bm.edges.cpu().numpy() if hasattr(bm.edges, "cpu") else bm.edges)
+        self.capacity = tree_capacity(min(params.max_depth, 24))
+        self.nid = np.full(bm.npad, -1, np.int64)
+        self.n_nodes_total = 0
+
+    def _hist(self, rows_node, g, h, w, n_nodes):
+        """Full histograms [n_nodes][F][3][nbt] (float64) of active rows."""
+        F, nbt = self.bm.F, self.bm.nbt
+        out = np.zeros((n_nodes, F, 3, nbt), np.float64)
+        act = np.nonzero(rows_node >= 0)[0]
+        if act.size:
+            nn = rows_node[act]
+            gw, hw, ww = g[act].astype(np.float64), h[act].astype(np.float64), w[act].astype(np.float64)
+            for f in range(F):
+                key = nn * nbt + self.codes[f, act]
+                out[:, f, 0, :] = np.bincount(key, gw, n_nodes * nbt).reshape(n_nodes, nbt)
+                out[:, f, 1, :] = np.bincount(key, hw, n_nodes * nbt).reshape(n_nodes, nbt)
+                out[:, f, 2, :] = np.bincount(key, ww, n_nodes * nbt).reshape(n_nodes, nbt)
+        if self.comm is not None and self.comm.world_size > 1:
+            out = self.comm.all_reduce_numpy(out)
+        return out
+
+    def build(self, g, h, w, tree_index: int, tree_fmask=None) -> np.ndarray:
+        p, bm = self.p, self.bm
+        F, nbt = bm.F, bm.nbt
+        g = np.asarray(g, np.float32)
+        h = np.asarray(h, np.float32)
+        w = np.ones_like(g) if w is None else np.asarray(w, np.float32)
+        tree = np.zeros(self.capacity, TREE_NODE_DTYPE)
+        nid = self.nid
+        # rows of weight zero still get routed but do not contribute
+        contrib = np.where((nid >= 0) & (w != 0), nid, -1)
+        n_nodes, base = 1, 0
+        for d in range(p.max_depth):
+            last = d == p.max_depth - 1
+            contrib = np.where((nid >= 0) & (w != 0), nid, -1)
+            H = self._hist(contrib, g, h, w, n_nodes)
+            next_base = base + n_nodes
+            k = 0
+            child_of = np.full(n_nodes, -1, np.int64)
+            feat_of = np.zeros(n_nodes, np.int64)
+            bin_of = np.zeros(n_nodes, np.int64)
+            naleft_of = np.zeros(n_nodes, np.int64)
+            leafkids = np.zeros(n_nodes, bool)
+            for i in range(n_nodes):
+                hist = H[i]
+                tot = hist[0].sum(axis=1)  # feature 0 totals [3]
+                Gt, Ht, Wt = tot
+                allowed = feature_allowed(p, F, tree_index, d, i, tree_fmask)
+                best = (-np.inf, None)
+                for f in range(F):
+                    if not allowed[f]:
+                        continue
+                    m = int(self.nvb[f])
+                    hv = hist[f]
+                    tg, th, tw = hv.sum(axis=1)
+                    cs = np.cumsum(hv[:, : nbt - 1], axis=1)[:, : min(m, nbt - 1)]
+                    na = hv[:, nbt - 1]
+                    gA = split_gain(cs[0], cs[1], cs[2], tg, th, tw, p)
+                    if na[2] > 0:
+                        gB = split_gain(cs[0] + na[0], cs[1] + na[1], cs[2] + na[2], tg, th, tw, p)
+                    else:
+                        gB = np.full_like(gA, -np.inf)
+                    # codes 2t (NA right) / 2t+1 (NA left); best = max gain, min code
+                    both = np.stack([gA, gB], axis=1).reshape(-1)
+                    if not np.any(both > -np.inf):
+                        continue
+                    c = int(np.argmax(both))  # first max = smallest code
+                    gval = both[c]
+                    if gval > best[0]:
+                        t, na_left = c // 2, c % 2
+                        GL, HL, WL = cs[0, t], cs[1, t], cs[2, t]
+                        if na_left:
+                            GL, HL, WL = GL + na[0], HL + na[1], WL + na[2]
+                        best = (gval, (f, t, na_left, GL, HL, WL))
+                do_split = (not False) and best[1] is not None and np.isfinite(best[0]) and best[0] > 0
+                if do_split and p.mode == 0 and p.min_split_improvement > 0:
+                    base_term = Gt * Gt / Wt if Wt > 0 else 0.0
+                    do_split = best[0] > p.min_split_improvement * max(base_term, 1e-12)
+                gid = base + i
+                rec = tree[gid] if gid < self.capacity else np.zeros((), TREE_NODE_DTYPE)
+                rec["value"] = leaf_value(Gt, Ht, Wt, p)
+                rec["weight"] = Wt
+                if do_split:
+                    f, t, na_left, GL, HL, WL = best[1]
+                    m = int(self.nvb[f])
+                    rec["feat"], rec["bin"], rec["na_left"] = f, t, na_left
+                    rec["left"] = next_base + 2 * k
+                    rec["gain"] = best[0]
+                    rec["thr"] = self.edges[f, t] if t < m - 1 else np.inf
+                    child_of[i], feat_of[i], bin_of[i], naleft_of[i] = 2 * k, f, t, na_left
+                    if last:
+                        leafkids[i] = True
+                        lc = tree[next_base + 2 * k]
+                        rc = tree[next_base + 2 * k + 1]
+                        lc["feat"] = rc["feat"] = -1
+                        lc["left"] = rc["left"] = -1
+                        lc["value"] = leaf_value(GL, HL, WL, p)
+                        rc["value"] = leaf_value(Gt - GL, Ht - HL, Wt - WL, p)
+                        lc["weight"], rc["weight"] = WL, Wt - WL
+                    k += 1
+                else:
+                    rec["feat"], rec["left"] = -1, -1
+            # partition
+            act = np.nonzero(nid >= 0)[0]
+            if act.size:
+                nn = nid[act]
+                ch = child_of[nn]
+                leaf = ch < 0
+                new = np.empty_like(nn)
+                new[leaf] = ~(base + nn[leaf])
+                sp = ~leaf
+                if np.any(sp):
+                    a_sp = act[sp]
+                    nsp = nn[sp]
+                    b = self.codes[feat_of[nsp], a_sp].astype(np.int64)
+                    right = np.where(b == nbt - 1, 1 - naleft_of[nsp], (b > bin_of[nsp]).astype(np.int64))
+                    lk = leafkids[nsp]
+                    new_sp = np.where(lk, ~(next_base + ch[sp] + right), ch[sp] + right)
+                    new[sp] = new_sp
+                nid[act] = new
+            base = next_base
+            n_nodes = 2 * k
+            self.n_nodes_total = base + n_nodes
+            if n_nodes == 0:
+                break
+        return tree
+
+
+# ---------------------------------------------------------------------------
+# gradients (mirror of boost_update_kernel / softmax_grad_kernel)
+# ---------------------------------------------------------------------------
+def bag_weights(n: int, sample_rate: float, seed: int, tree_index: int) -> np.ndarray:
+    if sample_rate >= 1.0:
+        return np.ones(n, np.float32)
+    u = u01(hash4(seed & 0xFFFFFFFF, tree_index, np.arange(n), 0x5BD1E995))
+    return (u < np.float32(sample_rate)).astype(np.float32)
+
+
+def dist_grad(dist: str, F, y, tweedie_power=1.5, quantile_alpha=0.5, huber_delta=1.0):
+    F = np.asarray(F, np.float64)
+    y = np.asarray(y, np.float64)
+    code = DIST_CODES[dist]
+    if code == 0:
+        return F - y, np.ones_like(F)
+    if code == 1:
+        pr = 1.0 / (1.0 + np.exp(-F))
+        return pr - y, np.maximum(pr * (1 - pr), 1e-16)
+    if code == 2:
+        mu = np.exp(F)
+        return mu - y, np.maximum(mu, 1e-16)
+    if code == 3:
+        e = y * np.exp(-F)
+        return 1 - e, np.maximum(e, 1e-16)
+    if code == 4:
+        rho = tweedie_power
+        a, b = y * np.exp((1 - rho) * F), np.exp((2 - rho) * F)
+        return -a + b, np.maximum(-(1 - rho) * a + (2 - rho) * b, 1e-16)
+    if code == 5:
+        return np.sign(F - y), np.ones_like(F)
+    if code == 6:
+        return np.where(y > F, -quantile_alpha, 1 - quantile_alpha), np.ones_like(F)
+    if code == 7:
+        r = F - y
+        return np.where(np.abs(r) <= huber_delta, r, np.sign(r) * huber_delta), np.ones_like(F)
+    return -y, np.ones_like(F)

@@ -1,0 +1,50 @@
+"""Binary layouts shared with ``csrc/tree_kernels.hip`` (checked at load time)."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+TREE_NODE_DTYPE = np.dtype([
+    ("feat", "<i4"), ("bin", "<i4"), ("left", "<i4"), ("na_left", "<i4"),
+    ("thr", "<f4"), ("value", "<f4"), ("gain", "<f4"), ("weight", "<f4"),
+])
+NODE_LINK_BYTES = 16
+PART_INFO_BYTES = 32
+FEAT_BEST_BYTES = 64
+
+
+class SplitParams(ctypes.Structure):
+    _fields_ = [
+        ("mode", ctypes.c_int), ("leaf_mode", ctypes.c_int), ("F", ctypes.c_int), ("is_last_level", ctypes.c_int),
+        ("min_rows", ctypes.c_double), ("min_child_weight", ctypes.c_double), ("lambda_", ctypes.c_double),
+        ("alpha", ctypes.c_double), ("gamma", ctypes.c_double), ("min_split_improvement", ctypes.c_double),
+        ("learn_rate", ctypes.c_double), ("max_abs_leaf", ctypes.c_double),
+        ("seed", ctypes.c_uint32), ("tree_index", ctypes.c_int), ("depth", ctypes.c_int),
+        ("col_rate", ctypes.c_float), ("mtries", ctypes.c_int), ("children_leaves", ctypes.c_int),
+    ]
+
+
+class GradParams(ctypes.Structure):
+    _fields_ = [
+        ("dist", ctypes.c_int), ("apply_tree", ctypes.c_int), ("sample_rate", ctypes.c_float),
+        ("seed", ctypes.c_uint32), ("tree_index", ctypes.c_int), ("tweedie_power", ctypes.c_float),
+        ("quantile_alpha", ctypes.c_float), ("huber_delta", ctypes.c_float),
+    ]
+
+
+# distribution codes of boost_update_kernel
+DIST_CODES = {
+    "gaussian": 0, "bernoulli": 1, "poisson": 2, "gamma": 3, "tweedie": 4,
+    "laplace": 5, "quantile": 6, "huber": 7, "drf": 8,
+}
+
+
+def check_layout(lib) -> None:
+    sizes = (ctypes.c_int * 8)()
+    lib.h2omx_tree_sizes(sizes)
+    want = [ctypes.sizeof(SplitParams), FEAT_BEST_BYTES, NODE_LINK_BYTES, PART_INFO_BYTES,
+            TREE_NODE_DTYPE.itemsize, ctypes.sizeof(GradParams)]
+    got = list(sizes)[:6]
+    if got != want:
+        raise RuntimeError(f"tree kernel ABI mismatch: kernel sizes {got} != python {want}")

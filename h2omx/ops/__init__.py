@@ -1,0 +1,85 @@
+"""Typed bindings of the native kernel libraries.
+
+Each binding is declared with a compact signature string so every ctypes
+argument has an explicit C type (``P`` pointer, ``I`` int32, ``L`` int64,
+``F`` float, ``D`` double, ``S`` hipStream_t).  ``ops.tree`` / ``ops.dense`` /
+``ops.metrics`` return the bound libraries; on a GPU tensor the HIP path is
+the only path (missing libraries raise :class:`NativeLibraryMissing`).
+"""
+from __future__ import annotations
+
+import ctypes
+
+from .. import _native
+
+_CT = {"P": ctypes.c_void_p, "I": ctypes.c_int, "L": ctypes.c_int64, "F": ctypes.c_float,
+       "D": ctypes.c_double, "S": ctypes.c_void_p, "U": ctypes.c_uint32}
+
+TREE_SIGS = {
+    "h2omx_tree_sizes": "P",
+    "h2omx_bin_features": "PLLIPPIPLS",
+    "h2omx_hist_build": "PLPPPPPPIIIIIIIIPS",
+    "h2omx_hist_reduce": "PIIIIIIIPPS",
+    "h2omx_split_find": "PPPPPPPPIIPS",
+    "h2omx_level_finalize": "PPPPPPIIPPPIS",
+    "h2omx_partition": "PLPPIS",
+    "h2omx_boost_update": "PPPLLPPPPPPS",
+    "h2omx_apply_tree": "PLPPS",
+    "h2omx_softmax_grad": "PILPPLLIPPPPPS",
+    "h2omx_predict_raw": "PLLPPIIPLS",
+    "h2omx_predict_binned": "PLLPPIIIPLS",
+}
+
+DENSE_SIGS = {
+    "h2omx_gram": "PLLIPPPIS",
+    "h2omx_glm_irls": "PLLIPPPPIDPPPPS",
+    "h2omx_kmeans_assign": "PLLIPIPPPS",
+    "h2omx_kmeans_update": "PLLIPPIPPS",
+    "h2omx_gemm_bias_act": "PPPPIIIIIS",
+    "h2omx_gemm_nt": "PPPIIIIS",
+    "h2omx_gemm_tn": "PPPIIIIS",
+    "h2omx_act_backward": "PPPIIS",
+    "h2omx_bias_grad": "PPIIS",
+    "h2omx_softmax_xent": "PPPPIIS",
+    "h2omx_adadelta": "PPPPLFFFS",
+    "h2omx_sgd_momentum": "PPPLFFFS",
+}
+
+METRICS_SIGS = {
+    "h2omx_auc_hist": "PPPLIFFPS",
+    "h2omx_reduce_binary_metrics": "PPPLPS",
+}
+
+_bound: dict[str, ctypes.CDLL] = {}
+
+
+def _bind(name: str, sigs: dict[str, str]) -> ctypes.CDLL:
+    lib = _bound.get(name)
+    if lib is not None:
+        return lib
+    lib = _native.require(name)
+    for fn, sig in sigs.items():
+        f = getattr(lib, fn, None)
+        if f is None:
+            continue
+        f.argtypes = [_CT[c] for c in sig]
+        f.restype = ctypes.c_int
+    _bound[name] = lib
+    return lib
+
+
+def tree() -> ctypes.CDLL:
+    return _bind("tree", TREE_SIGS)
+
+
+def dense() -> ctypes.CDLL:
+    return _bind("dense", DENSE_SIGS)
+
+
+def metrics() -> ctypes.CDLL:
+    return _bind("metrics", METRICS_SIGS)
+
+
+P = _native.ptr
+check = _native.check
+stream = _native.stream_of

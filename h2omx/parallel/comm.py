@@ -1,0 +1,140 @@
+"""Collective communication for the data plane.
+
+Replaces H2O-3's MRTask map/reduce fabric: every
+algorithm keeps its row shard resident on its GPU and combines per-shard
+statistics with one fused collective per tree level / IRLS iteration /
+optimizer step.  On MI355X the process group uses backend ``"nccl"`` which
+is RCCL over xGMI on ROCm; on CPU-only hosts (tests, the kind/CPU config) it
+uses ``gloo``.  Collectives are enqueued on the current stream, ordered
+after the producing kernel, with no host synchronisation.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, rank: int = 0, world_size: int = 1, device: torch.device | None = None,
+                 group=None):
+        self.rank = rank
+        self.world_size = world_size
+        self.device = device or torch.device("cpu")
+        self.group = group
+        self.stats = {"all_reduce_calls": 0, "all_reduce_bytes": 0, "all_reduce_s": 0.0}
+
+    # ------------------------------------------------------------------
+    @classmethod
+    def from_env(cls, device: str | None = None, timeout_s: float = 600.0) -> "Comm":
+        """Initialise from torchrun / StatefulSet env (RANK, WORLD_SIZE, MASTER_ADDR)."""
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", str(rank)))
+        if device is None:
+            device = "cuda" if torch.cuda.device_count() > 0 else "cpu"
+        if device == "cuda":
+            dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+            torch.cuda.set_device(dev)
+        else:
+            dev = torch.device("cpu")
+        if world > 1 and not dist.is_initialized():
+            import datetime
+
+            backend = "nccl" if dev.type == "cuda" else "gloo"
+            kw = {}
+            if dev.type == "cuda":
+                kw["device_id"] = dev
+            dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        return cls(rank, world, dev)
+
+    @property
+    def is_leader(self) -> bool:
+        return self.rank == 0
+
+    # ------------------------------------------------------------------
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.world_size == 1:
+            return t
+        self.stats["all_reduce_calls"] += 1
+        self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        dist.all_reduce(t, op=rop, group=self.group)
+        return t
+
+    def all_reduce_numpy(self, a: np.ndarray, op: str = "sum") -> np.ndarray:
+        if self.world_size == 1:
+            return a
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        if self.device.type == "cuda":
+            t = t.to(self.device)
+        self.all_reduce_(t, op)
+        return t.cpu().numpy()
+
+    def all_gather_cat(self, t: torch.Tensor, dim: int = 0) -> torch.Tensor:
+        if self.world_size == 1:
+            return t
+        # shapes may differ in `dim`: gather sizes first
+        n = torch.tensor([t.shape[dim]], dtype=torch.int64, device=t.device)
+        sizes = [torch.zeros_like(n) for _ in range(self.world_size)]
+        dist.all_gather(sizes, n, group=self.group)
+        sizes = [int(s.item()) for s in sizes]
+        mx = max(sizes)
+        pad_shape = list(t.shape)
+        pad_shape[dim] = mx
+        buf = torch.zeros(pad_shape, dtype=t.dtype, device=t.device)
+        buf.narrow(dim, 0, t.shape[dim]).copy_(t)
+        outs = [torch.empty_like(buf) for _ in range(self.world_size)]
+        dist.all_gather(outs, buf, group=self.group)
+        return torch.cat([o.narrow(dim, 0, s) for o, s in zip(outs, sizes)], dim=dim)
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.world_size > 1:
+            dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def broadcast_object(self, obj, src: int = 0):
+        if self.world_size == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, group=self.group)
+        return lst[0]
+
+    def barrier(self) -> None:
+        if self.world_size > 1:
+            if self.device.type == "cuda":
+                dist.barrier(group=self.group, device_ids=[self.device.index])
+            else:
+                dist.barrier(group=self.group)
+
+    def max_scalar(self, v: float) -> float:
+        if self.world_size == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self.device)
+        self.all_reduce_(t, "max")
+        return float(t.item())
+
+    def shutdown(self) -> None:
+        if self.world_size > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+class Timer:
+    def __init__(self):
+        self.t = {}
+
+    def __call__(self, name):
+        timer = self
+
+        class _Ctx:
+            def __enter__(self_):
+                self_.t0 = time.perf_counter()
+
+            def __exit__(self_, *a):
+                timer.t[name] = timer.t.get(name, 0.0) + time.perf_counter() - self_.t0
+
+        return _Ctx()
