@@ -120,19 +120,19 @@ __device__ __forceinline__ double l1_thresh(double g, double a) {
   return 0.0;
 }
 
-// Gain of splitting (G,H,W) into L and R = total - L.  Returns -inf if the
-// split violates a constraint.
-__device__ __forceinline__ double split_gain(double GL, double HL, double WL, double G, double H, double W,
-                                             const SplitParams& p) {
-  const double GR = G - GL, HR = H - HL, WR = W - WL;
-  if (WL < p.min_rows || WR < p.min_rows || WL <= 0.0 || WR <= 0.0) return -INFINITY;
+// Gain of splitting a node with totals (G, S) into L = (GL, SL) and R = total
+// - L.  S is the weight/count (mode 0, H2O squared error) or the hessian
+// (mode 1, XGBoost).  Returns -inf if the split violates a constraint.
+__device__ __forceinline__ double split_gain(double GL, double SL, double G, double S, const SplitParams& p) {
+  const double GR = G - GL, SR = S - SL;
   if (p.mode == 0) {
-    return GL * GL / WL + GR * GR / WR - G * G / W;
+    if (SL < p.min_rows || SR < p.min_rows || SL <= 0.0 || SR <= 0.0) return -INFINITY;
+    return GL * GL / SL + GR * GR / SR - G * G / S;
   }
-  if (HL < p.min_child_weight || HR < p.min_child_weight) return -INFINITY;
+  if (SL < p.min_child_weight || SR < p.min_child_weight || SL <= 0.0 || SR <= 0.0) return -INFINITY;
   const double lam = p.lambda_;
   const double tl = l1_thresh(GL, p.alpha), tr = l1_thresh(GR, p.alpha), tt = l1_thresh(G, p.alpha);
-  return 0.5 * (tl * tl / (HL + lam) + tr * tr / (HR + lam) - tt * tt / (H + lam)) - p.gamma;
+  return 0.5 * (tl * tl / (SL + lam) + tr * tr / (SR + lam) - tt * tt / (S + lam)) - p.gamma;
 }
 
 }  // namespace
@@ -173,20 +173,47 @@ __global__ __launch_bounds__(256) void bin_features_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------------------
-// K3: LDS-privatised histogram build.
-// Grid = n_groups * wgpg workgroups (wgpg % 8 == 0).  blockIdx -> (chunk,
-// group) keeps the n_groups workgroups of one row chunk on one XCD
-// (b % 8 equal) so their shared g/h/nid reads hit that XCD's L2 (speed only).
-// Each lane handles ROWS consecutive rows per iteration (one 16-B code load
-// per feature).  Slots [slot_lo, slot_lo + slot_cnt) are accumulated.
+// K3: LDS-privatised histogram build with packed fixed-point integer atomics.
+//
+// Measured on MI355X (bench_micro/lds_atomics.hip): ds_add_f32 retires only
+// ~0.33 lanes/CU/cycle whatever the address pattern, while ds_add_u64 on
+// random bins retires ~4.5 lanes/CU/cycle.  So every (row, feature) does ONE
+// 64-bit integer LDS atomic carrying both statistics:
+//     packed = (int32 G_q) << 32 | (uint32 S_q)
+// G_q / S_q are the row's gradient and second statistic (weight/count for
+// H2O squared-error mode, hessian for XGBoost mode) stochastically rounded to
+// fixed point with per-tree scales (QG / max|g|, QS / max s).  A workgroup
+// accumulates at most ROWS_CAP rows, which bounds |sum G_q| < 2^31 and
+// sum S_q < 2^32, so the low half never carries into the high half and the
+// packed 64-bit add is exact.  The reduction over workgroups is exact int64
+// arithmetic: histograms are bitwise deterministic regardless of atomic order.
+// Low-cardinality features (e.g. 3-valued b-tags) are replicated R = NBT /
+// (nvb+1) times inside their own NBT-wide LDS slice, lane l using copy l % R,
+// which removes the same-address serialisation (measured 4x slower) at no LDS
+// cost.  Grid = n_groups * wgpg (wgpg % 8 == 0); blockIdx -> (chunk, group)
+// keeps the groups of one row chunk on one XCD (L2 reuse of g/h/nid; speed
+// only, never correctness).
 // ---------------------------------------------------------------------------
+constexpr int ROWS_CAP = 32768;          // rows per workgroup chunk (host enforced)
+constexpr float QG = 32768.0f;           // |G_q| per row <= QG  -> |sum| <= 2^30
+constexpr float QS = 65536.0f;           // S_q per row <= QS    -> sum <= 2^31
+
+// qscale (double[8]): [0] QG/gmax [1] QS/smax [2] 1/[0] [3] 1/[1]
+//                     [4] leaf g scale [5] leaf h scale [6] leaf w scale
+// stat_max (uint32[4] float bits): max|g|, max h, max w (atomicMax targets)
+
+__device__ __forceinline__ uint32_t row_hash(int64_t r, uint32_t salt) {
+  return mix32((uint32_t)r * 0x9E3779B1u ^ mix32(salt + (uint32_t)(r >> 32)));
+}
+
 template <int NBT, int ROWS>
 __global__ __launch_bounds__(512) void hist_build_kernel(
-    const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ h,
-    const float* __restrict__ w, const int* __restrict__ nid, const NodeLink* __restrict__ link,
-    const int* __restrict__ ctl, int F, int fg, int n_groups, int wgpg, int slot_lo, int slot_cnt,
-    float* __restrict__ partials) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+    const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ s2,
+    const int* __restrict__ nid, const NodeLink* __restrict__ link, const int* __restrict__ ctl,
+    const int* __restrict__ nvb, const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups,
+    int wgpg, int slot_lo, int slot_cnt, unsigned long long* __restrict__ partials) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
+  __shared__ int width_s[256], rep_s[256];
   const int n_slots = ctl[CTL_SLOTS];
   if (slot_lo >= n_slots) return;  // uniform: nothing to build in this pass
 
@@ -196,10 +223,18 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
   const int chunk = xcd + 8 * (i / n_groups);
   const int f0 = group * fg;
   const int nf = min(fg, F - f0);
-  const int hist_floats = slot_cnt * fg * 3 * NBT;
+  const int hist_elems = slot_cnt * fg * NBT;
+  const int lane = threadIdx.x & 63;
 
-  for (int j = threadIdx.x * 4; j < hist_floats; j += blockDim.x * 4)
-    *reinterpret_cast<float4*>(lds + j) = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) lds64[j] = 0ull;
+  if (threadIdx.x < fg) {
+    const int fi = threadIdx.x;
+    const int w = (fi < nf) ? nvb[f0 + fi] + 1 : NBT;
+    width_s[fi] = w;
+    int r = NBT / w;
+    rep_s[fi] = r < 1 ? 1 : (r > 64 ? 64 : r);
+  }
+  const float sg = (float)qscale[0], ss = (float)qscale[1];
   __syncthreads();
 
   const int64_t units = npad / ROWS;
@@ -225,18 +260,21 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
       }
     }
     if (!any) continue;
-    float gg[ROWS], hh[ROWS], ww[ROWS];
+    unsigned long long pk[ROWS];
 #pragma unroll
     for (int q = 0; q < ROWS / 4; ++q) {
       const float4 g4 = *reinterpret_cast<const float4*>(g + r0 + 4 * q);
-      const float4 h4 = *reinterpret_cast<const float4*>(h + r0 + 4 * q);
-      gg[4 * q] = g4.x; gg[4 * q + 1] = g4.y; gg[4 * q + 2] = g4.z; gg[4 * q + 3] = g4.w;
-      hh[4 * q] = h4.x; hh[4 * q + 1] = h4.y; hh[4 * q + 2] = h4.z; hh[4 * q + 3] = h4.w;
-      if (w) {
-        const float4 w4 = *reinterpret_cast<const float4*>(w + r0 + 4 * q);
-        ww[4 * q] = w4.x; ww[4 * q + 1] = w4.y; ww[4 * q + 2] = w4.z; ww[4 * q + 3] = w4.w;
-      } else {
-        ww[4 * q] = ww[4 * q + 1] = ww[4 * q + 2] = ww[4 * q + 3] = 1.0f;
+      float4 s4 = make_float4(1.f, 1.f, 1.f, 1.f);
+      if (s2) s4 = *reinterpret_cast<const float4*>(s2 + r0 + 4 * q);
+      const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+      const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t hsh = row_hash(r0 + 4 * q + k, salt);
+        const float d1 = (hsh & 0xFFFF) * (1.0f / 65536.0f), d2 = (hsh >> 16) * (1.0f / 65536.0f);
+        const int gq = (int)floorf(fmaf(gv[k], sg, d1));
+        const uint32_t sq = (uint32_t)floorf(fmaf(sv[k], ss, d2));
+        pk[4 * q + k] = ((unsigned long long)(uint32_t)gq << 32) | (unsigned long long)sq;
       }
     }
     for (int fi = 0; fi < nf; ++fi) {
@@ -249,70 +287,92 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
         const uint2 c2 = *reinterpret_cast<const uint2*>(cp);
         cw[0] = c2.x; cw[1] = c2.y;
       }
+      const int width = width_s[fi], rep = rep_s[fi];
+      const int copy_off = (rep > 1) ? (lane % rep) * width : 0;
+      unsigned long long* hb = lds64 + fi * NBT + copy_off;
 #pragma unroll
       for (int r = 0; r < ROWS; ++r) {
-        if (s[r] >= 0 && ww[r] != 0.0f) {
-          const int bin = (cw[r >> 2] >> (8 * (r & 3))) & 0xff;
-          float* base = lds + (s[r] * fg + fi) * 3 * NBT + bin;
-          atomicAdd(base, gg[r]);
-          atomicAdd(base + NBT, hh[r]);
-          atomicAdd(base + 2 * NBT, ww[r]);
+        if (s[r] >= 0 && pk[r] != 0ull) {
+          int bin = (cw[r >> 2] >> (8 * (r & 3))) & 0xff;
+          if (bin == NBT - 1) bin = width - 1;  // NA goes to the last slot of this feature's slice
+          atomicAdd(hb + s[r] * fg * NBT + bin, pk[r]);
         }
       }
     }
   }
   __syncthreads();
-  float* out = partials + (int64_t)(group * wgpg + chunk) * hist_floats;
-  for (int j = threadIdx.x * 4; j < hist_floats; j += blockDim.x * 4)
-    *reinterpret_cast<float4*>(out + j) = *reinterpret_cast<const float4*>(lds + j);
+  // fold the lane copies and write this workgroup's slab (plain stores)
+  unsigned long long* out = partials + (int64_t)(group * wgpg + chunk) * hist_elems;
+  for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) {
+    const int bin = j % NBT;
+    const int fi = (j / NBT) % fg;
+    const int sl = j / (NBT * fg);
+    const int width = width_s[fi], rep = rep_s[fi];
+    const int src = (bin == NBT - 1) ? width - 1 : bin;
+    unsigned long long acc = 0ull;
+    if (src < width - 1 || bin == NBT - 1) {
+      const unsigned long long* hb = lds64 + (sl * fg + fi) * NBT;
+      for (int c = 0; c < rep; ++c) acc += hb[c * width + src];
+    }
+    out[j] = acc;
+  }
 }
 
-// Sum the per-workgroup slabs of one pass into the fp64 built histograms
-// built[slot][F][3][NBT].
-__global__ __launch_bounds__(256) void hist_reduce_kernel(const float* __restrict__ partials, int n_groups,
-                                                          int wgpg, int fg, int F, int nbt, int slot_lo,
+// Sum the per-workgroup slabs of one pass into exact int64 histograms
+// built[slot][F][2][NBT] (plane 0: G_q, plane 1: S_q).
+__global__ __launch_bounds__(256) void hist_reduce_kernel(const unsigned long long* __restrict__ partials,
+                                                          int n_groups, int wgpg, int fg, int F, int nbt, int slot_lo,
                                                           int slot_cnt, const int* __restrict__ ctl,
-                                                          double* __restrict__ built) {
-  const int64_t total = (int64_t)slot_cnt * F * 3 * nbt;
+                                                          long long* __restrict__ built) {
+  const int64_t total = (int64_t)slot_cnt * F * nbt;
   const int n_slots = ctl[CTL_SLOTS];
-  const int64_t hist_floats = (int64_t)slot_cnt * fg * 3 * nbt;
+  const int64_t hist_elems = (int64_t)slot_cnt * fg * nbt;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int bin = idx % nbt;
-    const int k = (idx / nbt) % 3;
-    const int f = (idx / (3 * nbt)) % F;
-    const int s = idx / ((int64_t)3 * nbt * F);
+    const int f = (idx / nbt) % F;
+    const int s = idx / ((int64_t)nbt * F);
     if (slot_lo + s >= n_slots) continue;
     const int group = f / fg, fi = f % fg;
-    const float* p = partials + (int64_t)group * wgpg * hist_floats + ((int64_t)(s * fg + fi) * 3 + k) * nbt + bin;
-    double acc = 0.0;
-    for (int c = 0; c < wgpg; ++c) acc += (double)p[(int64_t)c * hist_floats];
-    built[(((int64_t)(slot_lo + s) * F + f) * 3 + k) * nbt + bin] = acc;
+    const unsigned long long* p =
+        partials + (int64_t)group * wgpg * hist_elems + ((int64_t)s * fg + fi) * nbt + bin;
+    long long ag = 0, as = 0;
+    for (int c = 0; c < wgpg; ++c) {
+      const unsigned long long v = p[(int64_t)c * hist_elems];
+      ag += (long long)(int32_t)(uint32_t)(v >> 32);
+      as += (long long)(uint32_t)v;
+    }
+    long long* o = built + (((int64_t)(slot_lo + s) * F + f) * 2) * nbt + bin;
+    o[0] = ag;
+    o[nbt] = as;
   }
 }
 
 // ---------------------------------------------------------------------------
-// K4 + K5: complete the level's histograms (built or parent - sibling),
-// keep them as parents for the next level, and scan for the best threshold
-// of one (node, feature) pair per 256-thread workgroup (thread t owns bin t;
-// grid = max_nodes x F so even a 16-node level fills the chip).  The per-node
-// arg-max over features happens in level_finalize.
+// K4 + K5: complete the level's histograms (built or parent - sibling, exact
+// int64), keep them as parents for the next level, and scan for the best
+// threshold of one (node, feature) pair per 256-thread workgroup (thread t
+// owns bin t; grid = max_nodes x F so even a 16-node level fills the chip).
+// The per-node arg-max over features happens in level_finalize.
 // ---------------------------------------------------------------------------
 struct FeatBest {  // 64 B
   double gain;
-  double GL, HL, WL;
-  double G, H, W;  // node totals (as seen from this feature's histogram)
+  double GL, SL;   // left-child totals of the chosen threshold
+  double G, S;     // node totals (as seen from this feature's histogram)
+  double pad0;
   int code;        // (bin * 2 + na_left), INT_MAX = none
-  int pad;
+  int pad1;
+  double pad2;
 };
 
 template <int NBT>
-__global__ __launch_bounds__(256) void split_find_kernel(const double* __restrict__ built,
-                                                         const double* __restrict__ parent_full,
-                                                         double* __restrict__ full, const int* __restrict__ ctl,
+__global__ __launch_bounds__(256) void split_find_kernel(const long long* __restrict__ built,
+                                                         const long long* __restrict__ parent_full,
+                                                         long long* __restrict__ full, const int* __restrict__ ctl,
                                                          const NodeLink* __restrict__ link,
                                                          const int* __restrict__ nvb,
-                                                         const uint8_t* __restrict__ tree_fmask, SplitParams p,
+                                                         const uint8_t* __restrict__ tree_fmask,
+                                                         const double* __restrict__ qscale, SplitParams p,
                                                          FeatBest* __restrict__ out) {
   const int node = blockIdx.x;
   const int f = blockIdx.y;
@@ -321,50 +381,52 @@ __global__ __launch_bounds__(256) void split_find_kernel(const double* __restric
   const int t = threadIdx.x;
   const int lane = t & 63, wid = t >> 6;
   const NodeLink lk = link[node];
-  __shared__ double wtot[3][4];
-  __shared__ double na[3];
+  __shared__ double wtot[2][4];
+  __shared__ double na[2];
   __shared__ double bestg[4];
   __shared__ int bestc[4];
+  const double ig = qscale[2], is = qscale[3];
 
-  double gv = 0, hv = 0, wv = 0;
+  double gv = 0, sv = 0;
   if (t < NBT) {
-    const int64_t off = ((int64_t)f * 3) * NBT + t;
-    const int64_t per = (int64_t)F * 3 * NBT;
+    const int64_t off = ((int64_t)f * 2) * NBT + t;
+    const int64_t per = (int64_t)F * 2 * NBT;
+    long long gi, si;
     if (lk.slot >= 0) {
-      const double* bp = built + lk.slot * per + off;
-      gv = bp[0]; hv = bp[NBT]; wv = bp[2 * NBT];
+      const long long* bp = built + lk.slot * per + off;
+      gi = bp[0]; si = bp[NBT];
     } else {
-      const double* pp = parent_full + lk.parent * per + off;
-      const double* sp = built + lk.sib_slot * per + off;
-      gv = pp[0] - sp[0]; hv = pp[NBT] - sp[NBT]; wv = pp[2 * NBT] - sp[2 * NBT];
+      const long long* pp = parent_full + lk.parent * per + off;
+      const long long* sp = built + lk.sib_slot * per + off;
+      gi = pp[0] - sp[0]; si = pp[NBT] - sp[NBT];
     }
     if (full) {
-      double* fp = full + node * per + off;
-      fp[0] = gv; fp[NBT] = hv; fp[2 * NBT] = wv;
+      long long* fp = full + node * per + off;
+      fp[0] = gi; fp[NBT] = si;
     }
+    gv = (double)gi * ig;
+    sv = (double)si * is;
   }
-  if (t == NBT - 1) { na[0] = gv; na[1] = hv; na[2] = wv; }
-  // inclusive scan over the value bins (exclude NA bin)
-  double sg = (t < NBT - 1) ? gv : 0.0, sh = (t < NBT - 1) ? hv : 0.0, sw = (t < NBT - 1) ? wv : 0.0;
+  if (t == NBT - 1) { na[0] = gv; na[1] = sv; }
+  double sg = (t < NBT - 1) ? gv : 0.0, ssum = (t < NBT - 1) ? sv : 0.0;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const double ag = __shfl_up(sg, off, kWave), ah = __shfl_up(sh, off, kWave), aw = __shfl_up(sw, off, kWave);
-    if (lane >= off) { sg += ag; sh += ah; sw += aw; }
+    const double ag = __shfl_up(sg, off, kWave), as = __shfl_up(ssum, off, kWave);
+    if (lane >= off) { sg += ag; ssum += as; }
   }
-  if (lane == 63) { wtot[0][wid] = sg; wtot[1][wid] = sh; wtot[2][wid] = sw; }
+  if (lane == 63) { wtot[0][wid] = sg; wtot[1][wid] = ssum; }
   __syncthreads();
-  for (int k = 0; k < wid; ++k) { sg += wtot[0][k]; sh += wtot[1][k]; sw += wtot[2][k]; }
-  const double ng = na[0], nh = na[1], nw = na[2];
+  for (int k = 0; k < wid; ++k) { sg += wtot[0][k]; ssum += wtot[1][k]; }
+  const double ng = na[0], ns = na[1];
   const double tg = wtot[0][0] + wtot[0][1] + wtot[0][2] + wtot[0][3] + ng;
-  const double th = wtot[1][0] + wtot[1][1] + wtot[1][2] + wtot[1][3] + nh;
-  const double tw = wtot[2][0] + wtot[2][1] + wtot[2][2] + wtot[2][3] + nw;
+  const double ts = wtot[1][0] + wtot[1][1] + wtot[1][2] + wtot[1][3] + ns;
 
   bool allowed = (tree_fmask == nullptr) || tree_fmask[f];
   if (allowed && (p.mtries > 0 || p.col_rate < 1.0f)) {
     const uint32_t key = (uint32_t)p.tree_index * 131u + (uint32_t)p.depth;
     const uint32_t hf = hash4(p.seed, key, (uint32_t)node, (uint32_t)f);
     if (p.mtries > 0) {
-      int rank = 0;  // rank of this feature's hash among all features
+      int rank = 0;
       for (int j = 0; j < F; ++j) {
         const uint32_t hj = hash4(p.seed, key, (uint32_t)node, (uint32_t)j);
         rank += (hj < hf) || (hj == hf && j < f);
@@ -376,14 +438,14 @@ __global__ __launch_bounds__(256) void split_find_kernel(const double* __restric
   }
   double best_gain = -INFINITY;
   int best_code = 0x7fffffff;
-  double bGL = 0, bHL = 0, bWL = 0;
-  const int m = nvb[f];  // thresholds t in [0, m-1]
+  double bGL = 0, bSL = 0;
+  const int m = nvb[f];
   if (allowed && t < m && t < NBT - 1) {
-    const double gA = split_gain(sg, sh, sw, tg, th, tw, p);  // NA goes right
-    const double gB = (nw > 0.0) ? split_gain(sg + ng, sh + nh, sw + nw, tg, th, tw, p) : -INFINITY;  // NA left
-    if (gA > -INFINITY) { best_gain = gA; best_code = 2 * t; bGL = sg; bHL = sh; bWL = sw; }
+    const double gA = split_gain(sg, ssum, tg, ts, p);
+    const double gB = (ns > 0.0) ? split_gain(sg + ng, ssum + ns, tg, ts, p) : -INFINITY;
+    if (gA > -INFINITY) { best_gain = gA; best_code = 2 * t; bGL = sg; bSL = ssum; }
     if (gB > -INFINITY && (gB > best_gain || (gB == best_gain && 2 * t + 1 < best_code))) {
-      best_gain = gB; best_code = 2 * t + 1; bGL = sg + ng; bHL = sh + nh; bWL = sw + nw;
+      best_gain = gB; best_code = 2 * t + 1; bGL = sg + ng; bSL = ssum + ns;
     }
   }
   double bg = best_gain;
@@ -403,17 +465,17 @@ __global__ __launch_bounds__(256) void split_find_kernel(const double* __restric
   FeatBest* o = out + (int64_t)node * F + f;
   if (c0 == 0x7fffffff) {
     if (t == 0) {
-      FeatBest r;
-      r.gain = -INFINITY; r.GL = r.HL = r.WL = 0.0;
-      r.G = tg; r.H = th; r.W = tw;
-      r.code = 0x7fffffff; r.pad = 0;
+      FeatBest r{};
+      r.gain = -INFINITY;
+      r.G = tg; r.S = ts;
+      r.code = 0x7fffffff;
       *o = r;
     }
   } else if (best_code == c0) {  // unique owner of the winning threshold
-    FeatBest r;
-    r.gain = g0; r.GL = bGL; r.HL = bHL; r.WL = bWL;
-    r.G = tg; r.H = th; r.W = tw;
-    r.code = c0; r.pad = 0;
+    FeatBest r{};
+    r.gain = g0; r.GL = bGL; r.SL = bSL;
+    r.G = tg; r.S = ts;
+    r.code = c0;
     *o = r;
   }
 }
@@ -455,10 +517,12 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(const FeatBest* __
           bf = f; bg = c.gain; bc = c.code;
         }
       }
-      s.G = fb[0].G; s.H = fb[0].H; s.W = fb[0].W;
+      // S is W (mode 0) or H (mode 1); the exact leaf (G, H, W) come later
+      // from leaf_stats, these only steer the split decisions
+      s.G = fb[0].G; s.H = fb[0].S; s.W = fb[0].S;
       if (bf >= 0) {
         const FeatBest& c = fb[bf];
-        s.gain = c.gain; s.GL = c.GL; s.HL = c.HL; s.WL = c.WL;
+        s.gain = c.gain; s.GL = c.GL; s.HL = c.SL; s.WL = c.SL;
         s.feat = bf; s.bin = bc >> 1; s.na_left = bc & 1;
       } else {
         s.gain = -INFINITY; s.GL = s.HL = s.WL = 0.0;
@@ -623,36 +687,59 @@ __device__ __forceinline__ void dist_grad(int dist, float f, float y, const Grad
   }
 }
 
+// Block-level max of three non-negative statistics folded into one
+// atomicMax per statistic per workgroup (float bits compare as uint32).
+__device__ __forceinline__ void block_max3(float a, float b, float c, unsigned int* __restrict__ stat_max) {
+  __shared__ float red[3][16];
+  a = wave_max(a); b = wave_max(b); c = wave_max(c);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { red[0][wid] = a; red[1][wid] = b; red[2][wid] = c; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    float m0 = 0.f, m1 = 0.f, m2 = 0.f;
+    for (int k = 0; k < nw; ++k) { m0 = fmaxf(m0, red[0][k]); m1 = fmaxf(m1, red[1][k]); m2 = fmaxf(m2, red[2][k]); }
+    atomicMax(stat_max + 0, __float_as_uint(m0));
+    atomicMax(stat_max + 1, __float_as_uint(m1));
+    atomicMax(stat_max + 2, __float_as_uint(m2));
+  }
+}
+
 __global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F, const float* __restrict__ y,
                                                            const float* __restrict__ wobs, int64_t n, int64_t npad,
                                                            int* __restrict__ nid, const TreeNode* __restrict__ tree,
                                                            GradParams gp, float* __restrict__ g, float* __restrict__ h,
-                                                           float* __restrict__ wout) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= npad) return;
-  if (r >= n) {
-    nid[r] = INT32_MIN;
-    g[r] = 0.f; h[r] = 0.f;
-    if (wout) wout[r] = 0.f;
-    return;
+                                                           float* __restrict__ wout, unsigned int* __restrict__ stat_max) {
+  float mg = 0.f, mh = 0.f, mw = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < npad; r += (int64_t)gridDim.x * blockDim.x) {
+    if (r >= n) {
+      nid[r] = INT32_MIN;
+      g[r] = 0.f; h[r] = 0.f;
+      if (wout) wout[r] = 0.f;
+      continue;
+    }
+    float f = F[r];
+    if (gp.apply_tree) {
+      const int leaf = ~nid[r];
+      f += tree[leaf].value;
+      F[r] = f;
+    }
+    float gv, hv;
+    dist_grad(gp.dist, f, y[r], gp, gv, hv);
+    float wv = wobs ? wobs[r] : 1.0f;
+    if (gp.sample_rate < 1.0f) {
+      const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)r, 0x5bd1e995u));
+      if (u >= gp.sample_rate) wv = 0.0f;
+    }
+    gv *= wv;
+    hv *= wv;
+    g[r] = gv;
+    h[r] = hv;
+    if (wout) wout[r] = wv;
+    nid[r] = 0;
+    mg = fmaxf(mg, fabsf(gv)); mh = fmaxf(mh, hv); mw = fmaxf(mw, wv);
   }
-  float f = F[r];
-  if (gp.apply_tree) {
-    const int leaf = ~nid[r];
-    f += tree[leaf].value;
-    F[r] = f;
-  }
-  float gv, hv;
-  dist_grad(gp.dist, f, y[r], gp, gv, hv);
-  float wv = wobs ? wobs[r] : 1.0f;
-  if (gp.sample_rate < 1.0f) {
-    const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)r, 0x5bd1e995u));
-    if (u >= gp.sample_rate) wv = 0.0f;
-  }
-  g[r] = gv * wv;
-  h[r] = hv * wv;
-  if (wout) wout[r] = wv;
-  nid[r] = 0;
+  if (stat_max) block_max3(mg, mh, mw, stat_max);
 }
 
 // Apply a finished tree only (multi-class path): F[k][r] += value[leaf].
@@ -669,33 +756,107 @@ __global__ __launch_bounds__(256) void softmax_grad_kernel(const float* __restri
                                                            const int* __restrict__ yk, const float* __restrict__ wobs,
                                                            int64_t n, int64_t npad, int cls, GradParams gp,
                                                            int* __restrict__ nid, float* __restrict__ g,
-                                                           float* __restrict__ h, float* __restrict__ wout) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= npad) return;
-  if (r >= n) {
-    nid[r] = INT32_MIN; g[r] = 0.f; h[r] = 0.f;
-    if (wout) wout[r] = 0.f;
-    return;
+                                                           float* __restrict__ h, float* __restrict__ wout,
+                                                           unsigned int* __restrict__ stat_max) {
+  float mg = 0.f, mh = 0.f, mw = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < npad; r += (int64_t)gridDim.x * blockDim.x) {
+    if (r >= n) {
+      nid[r] = INT32_MIN; g[r] = 0.f; h[r] = 0.f;
+      if (wout) wout[r] = 0.f;
+      continue;
+    }
+    float mx = -INFINITY;
+    for (int k = 0; k < K; ++k) mx = fmaxf(mx, F[k * ldF + r]);
+    float den = 0.f, fk = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float e = __expf(F[k * ldF + r] - mx);
+      den += e;
+      if (k == cls) fk = e;
+    }
+    const float pk = fk / den;
+    const float yv = (yk[r] == cls) ? 1.0f : 0.0f;
+    float wv = wobs ? wobs[r] : 1.0f;
+    if (gp.sample_rate < 1.0f) {
+      const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)r, 0x5bd1e995u));
+      if (u >= gp.sample_rate) wv = 0.0f;
+    }
+    const float gv = (pk - yv) * wv, hv = fmaxf(pk * (1.0f - pk), 1e-16f) * wv;
+    g[r] = gv;
+    h[r] = hv;
+    if (wout) wout[r] = wv;
+    nid[r] = 0;
+    mg = fmaxf(mg, fabsf(gv)); mh = fmaxf(mh, hv); mw = fmaxf(mw, wv);
   }
-  float mx = -INFINITY;
-  for (int k = 0; k < K; ++k) mx = fmaxf(mx, F[k * ldF + r]);
-  float den = 0.f, fk = 0.f;
-  for (int k = 0; k < K; ++k) {
-    const float e = __expf(F[k * ldF + r] - mx);
-    den += e;
-    if (k == cls) fk = e;
+  if (stat_max) block_max3(mg, mh, mw, stat_max);
+}
+
+// Turn the (all-reduced) per-tree maxima into quantisation scales.
+__global__ void quant_scales_kernel(const unsigned int* __restrict__ stat_max, int mode, double* __restrict__ qs) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double gmax = fmax((double)__uint_as_float(stat_max[0]), 1e-30);
+  const double hmax = fmax((double)__uint_as_float(stat_max[1]), 1e-30);
+  const double wmax = fmax((double)__uint_as_float(stat_max[2]), 1e-30);
+  const double smax = (mode == 0) ? wmax : hmax;
+  // power-of-two scales keep the double conversions exact
+  const double sg = exp2(floor(log2((double)QG / gmax)));
+  const double ss = exp2(floor(log2((double)QS / smax)));
+  qs[0] = sg; qs[1] = ss; qs[2] = 1.0 / sg; qs[3] = 1.0 / ss;
+  qs[4] = exp2(floor(log2(2147483647.0 / gmax)));
+  qs[5] = exp2(floor(log2(2147483647.0 / hmax)));
+  qs[6] = exp2(floor(log2(2147483647.0 / wmax)));
+  qs[7] = 0.0;
+}
+
+// Exact per-leaf (G, H, W) sums after the last partition: every row carries
+// nid = ~leaf_gid.  int64 fixed point -> deterministic; LDS-privatised when
+// the tree capacity fits (depth <= 10), global atomics otherwise.
+__global__ __launch_bounds__(256) void leaf_stats_kernel(const int* __restrict__ nid, const float* __restrict__ g,
+                                                         const float* __restrict__ h, const float* __restrict__ w,
+                                                         int64_t n, const double* __restrict__ qs, int cap,
+                                                         unsigned long long* __restrict__ acc) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lacc[];
+  const bool use_lds = cap <= 2048;
+  if (use_lds) {
+    for (int j = threadIdx.x; j < 3 * cap; j += blockDim.x) lacc[j] = 0ull;
+    __syncthreads();
   }
-  const float pk = fk / den;
-  const float yv = (yk[r] == cls) ? 1.0f : 0.0f;
-  float wv = wobs ? wobs[r] : 1.0f;
-  if (gp.sample_rate < 1.0f) {
-    const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)r, 0x5bd1e995u));
-    if (u >= gp.sample_rate) wv = 0.0f;
+  const double lg = qs[4], lh = qs[5], lw = qs[6];
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const int leaf = ~nid[r];
+    if (leaf < 0 || leaf >= cap) continue;
+    const float wv = w ? w[r] : 1.0f;
+    if (wv == 0.0f) continue;
+    const long long gq = llrint((double)g[r] * lg), hq = llrint((double)h[r] * lh), wq = llrint((double)wv * lw);
+    unsigned long long* dst = use_lds ? lacc + 3 * leaf : acc + 3 * leaf;
+    atomicAdd(dst + 0, (unsigned long long)gq);
+    atomicAdd(dst + 1, (unsigned long long)hq);
+    atomicAdd(dst + 2, (unsigned long long)wq);
   }
-  g[r] = (pk - yv) * wv;
-  h[r] = fmaxf(pk * (1.0f - pk), 1e-16f) * wv;
-  if (wout) wout[r] = wv;
-  nid[r] = 0;
+  if (use_lds) {
+    __syncthreads();
+    for (int j = threadIdx.x; j < 3 * cap; j += blockDim.x)
+      if (lacc[j]) atomicAdd(acc + j, lacc[j]);
+  }
+}
+
+// Overwrite every leaf's value with the Newton / mean step from the exact
+// leaf sums (and record its weight).
+__global__ __launch_bounds__(256) void leaf_finalize_kernel(const unsigned long long* __restrict__ acc,
+                                                            const int* __restrict__ ctl_final,
+                                                            const double* __restrict__ qs, SplitParams p,
+                                                            TreeNode* __restrict__ tree, int cap) {
+  const int total = min(ctl_final[CTL_TOTAL], cap);
+  for (int gid = blockIdx.x * blockDim.x + threadIdx.x; gid < total; gid += gridDim.x * blockDim.x) {
+    TreeNode nd = tree[gid];
+    const double G = (double)(long long)acc[3 * gid] / qs[4];
+    const double H = (double)(long long)acc[3 * gid + 1] / qs[5];
+    const double W = (double)(long long)acc[3 * gid + 2] / qs[6];
+    if (nd.feat < 0) {
+      nd.value = (float)leaf_value(G, H, W, p);
+      nd.weight = (float)W;
+      tree[gid] = nd;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -772,18 +933,20 @@ H2OMX_API int h2omx_bin_features(const float* X, int64_t ld, int64_t n, int F, c
   return launch_status();
 }
 
-H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* g, const float* h, const float* w,
-                               const int* nid, const void* link, const int* ctl, int F, int nbt, int fg,
-                               int n_groups, int wgpg, int slot_lo, int slot_cnt, int rows_per_lane,
-                               float* partials, hipStream_t stream) {
-  if (wgpg % 8 != 0 || npad % 16 != 0) return kBadArg;
-  const size_t lds = (size_t)slot_cnt * fg * 3 * nbt * sizeof(float);
-  if (lds > 160 * 1024) return kBadArg;
+H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* g, const float* s2, const int* nid,
+                               const void* link, const int* ctl, const int* nvb, const double* qscale, int salt,
+                               int F, int nbt, int fg, int n_groups, int wgpg, int slot_lo, int slot_cnt,
+                               int rows_per_lane, unsigned long long* partials, hipStream_t stream) {
+  if (wgpg % 8 != 0 || npad % 16 != 0 || fg > 256) return kBadArg;
+  const int64_t units = npad / rows_per_lane;
+  if ((units + wgpg - 1) / wgpg * rows_per_lane > ROWS_CAP) return kBadArg;  // fixed-point headroom
+  const size_t lds = (size_t)slot_cnt * fg * nbt * sizeof(unsigned long long);
+  if (lds > 150 * 1024) return kBadArg;
   const int grid = n_groups * wgpg;
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
-#define H2OMX_HB(NB, R)                                                                                      \
-  hipLaunchKernelGGL((hist_build_kernel<NB, R>), dim3(grid), dim3(512), lds, stream, codes, npad, g, h, w, nid, \
-                     lk, ctl, F, fg, n_groups, wgpg, slot_lo, slot_cnt, partials)
+#define H2OMX_HB(NB, R)                                                                                           \
+  hipLaunchKernelGGL((hist_build_kernel<NB, R>), dim3(grid), dim3(512), lds, stream, codes, npad, g, s2, nid, lk, \
+                     ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt, partials)
   if (rows_per_lane == 16) {
     switch (nbt) {
       case 32: H2OMX_HB(32, 16); break;
@@ -807,28 +970,32 @@ H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* 
   return launch_status();
 }
 
-H2OMX_API int h2omx_hist_reduce(const float* partials, int n_groups, int wgpg, int fg, int F, int nbt, int slot_lo,
-                                int slot_cnt, const int* ctl, double* built, hipStream_t stream) {
-  const int64_t total = (int64_t)slot_cnt * F * 3 * nbt;
+H2OMX_API int h2omx_hist_reduce(const unsigned long long* partials, int n_groups, int wgpg, int fg, int F, int nbt,
+                                int slot_lo, int slot_cnt, const int* ctl, long long* built, hipStream_t stream) {
+  const int64_t total = (int64_t)slot_cnt * F * nbt;
   hipLaunchKernelGGL(hist_reduce_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, stream, partials,
                      n_groups, wgpg, fg, F, nbt, slot_lo, slot_cnt, ctl, built);
   return launch_status();
 }
 
-H2OMX_API int h2omx_split_find(const double* built, const double* parent_full, double* full, const int* ctl,
-                               const void* link, const int* nvb, const uint8_t* tree_fmask, const void* params,
-                               int max_nodes, int nbt, void* out, hipStream_t stream) {
+H2OMX_API int h2omx_split_find(const long long* built, const long long* parent_full, long long* full, const int* ctl,
+                               const void* link, const int* nvb, const uint8_t* tree_fmask, const double* qscale,
+                               const void* params, int max_nodes, int nbt, void* out, hipStream_t stream) {
   const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
   FeatBest* o = reinterpret_cast<FeatBest*>(out);
   const dim3 grid(max_nodes, p.F);
+#define H2OMX_SF(NB)                                                                                      \
+  hipLaunchKernelGGL(split_find_kernel<NB>, grid, dim3(256), 0, stream, built, parent_full, full, ctl, lk, \
+                     nvb, tree_fmask, qscale, p, o)
   switch (nbt) {
-    case 32: hipLaunchKernelGGL(split_find_kernel<32>, grid, dim3(256), 0, stream, built, parent_full, full, ctl, lk, nvb, tree_fmask, p, o); break;
-    case 64: hipLaunchKernelGGL(split_find_kernel<64>, grid, dim3(256), 0, stream, built, parent_full, full, ctl, lk, nvb, tree_fmask, p, o); break;
-    case 128: hipLaunchKernelGGL(split_find_kernel<128>, grid, dim3(256), 0, stream, built, parent_full, full, ctl, lk, nvb, tree_fmask, p, o); break;
-    case 256: hipLaunchKernelGGL(split_find_kernel<256>, grid, dim3(256), 0, stream, built, parent_full, full, ctl, lk, nvb, tree_fmask, p, o); break;
+    case 32: H2OMX_SF(32); break;
+    case 64: H2OMX_SF(64); break;
+    case 128: H2OMX_SF(128); break;
+    case 256: H2OMX_SF(256); break;
     default: return kBadArg;
   }
+#undef H2OMX_SF
   return launch_status();
 }
 
@@ -851,12 +1018,14 @@ H2OMX_API int h2omx_partition(const uint8_t* codes, int64_t npad, int* nid, cons
   return launch_status();
 }
 
+static inline int stream_grid(int64_t n) { return grid_for(n, 256, 2048); }
+
 H2OMX_API int h2omx_boost_update(float* F, const float* y, const float* wobs, int64_t n, int64_t npad, int* nid,
                                  const void* tree, const void* gparams, float* g, float* h, float* wout,
-                                 hipStream_t stream) {
+                                 unsigned int* stat_max, hipStream_t stream) {
   const GradParams gp = *reinterpret_cast<const GradParams*>(gparams);
-  hipLaunchKernelGGL(boost_update_kernel, dim3(grid_for(npad, 256)), dim3(256), 0, stream, F, y, wobs, n, npad, nid,
-                     reinterpret_cast<const TreeNode*>(tree), gp, g, h, wout);
+  hipLaunchKernelGGL(boost_update_kernel, dim3(stream_grid(npad)), dim3(256), 0, stream, F, y, wobs, n, npad, nid,
+                     reinterpret_cast<const TreeNode*>(tree), gp, g, h, wout, stat_max);
   return launch_status();
 }
 
@@ -868,10 +1037,31 @@ H2OMX_API int h2omx_apply_tree(float* F, int64_t n, const int* nid, const void* 
 
 H2OMX_API int h2omx_softmax_grad(const float* F, int K, int64_t ldF, const int* yk, const float* wobs, int64_t n,
                                  int64_t npad, int cls, const void* gparams, int* nid, float* g, float* h,
-                                 float* wout, hipStream_t stream) {
+                                 float* wout, unsigned int* stat_max, hipStream_t stream) {
   const GradParams gp = *reinterpret_cast<const GradParams*>(gparams);
-  hipLaunchKernelGGL(softmax_grad_kernel, dim3(grid_for(npad, 256)), dim3(256), 0, stream, F, K, ldF, yk, wobs, n,
-                     npad, cls, gp, nid, g, h, wout);
+  hipLaunchKernelGGL(softmax_grad_kernel, dim3(stream_grid(npad)), dim3(256), 0, stream, F, K, ldF, yk, wobs, n,
+                     npad, cls, gp, nid, g, h, wout, stat_max);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_quant_scales(const unsigned int* stat_max, int mode, double* qscale, hipStream_t stream) {
+  hipLaunchKernelGGL(quant_scales_kernel, dim3(1), dim3(64), 0, stream, stat_max, mode, qscale);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_leaf_stats(const int* nid, const float* g, const float* h, const float* w, int64_t n,
+                               const double* qscale, int cap, unsigned long long* acc, hipStream_t stream) {
+  const size_t lds = cap <= 2048 ? (size_t)cap * 3 * sizeof(unsigned long long) : 0;
+  hipLaunchKernelGGL(leaf_stats_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), lds, stream, nid, g, h, w, n, qscale,
+                     cap, acc);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_leaf_finalize(const unsigned long long* acc, const int* ctl_final, const double* qscale,
+                                  const void* params, void* tree, int cap, hipStream_t stream) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  hipLaunchKernelGGL(leaf_finalize_kernel, dim3(grid_for(cap, 256, 1024)), dim3(256), 0, stream, acc, ctl_final,
+                     qscale, p, reinterpret_cast<TreeNode*>(tree), cap);
   return launch_status();
 }
 

@@ -209,9 +209,10 @@ class GpuBooster:
         P, st, b = ops.P, self.st, self.builder
         gp = make_grad_params(dist or self.dist, apply, self.sample_rate, self.seed, next_tree, **self.kw)
         y = st.ycls[k] if (self.dist == "drf" and self.K > 1) else st.y
+        b.stat_max.zero_()
         ops.check(self.lib.h2omx_boost_update(P(st.Fm[k]), P(y), P(st.w), self.bm.n, self.bm.npad, P(b.nid),
                                               P(b.tree_buf), ctypes.addressof(gp), P(st.g[k]), P(st.h[k]),
-                                              P(self.wout), ops.stream(self.dev)), "boost_update")
+                                              P(self.wout), P(b.stat_max), ops.stream(self.dev)), "boost_update")
 
     def step(self):
         P, st, b, bm, t = ops.P, self.st, self.builder, self.bm, self.t
@@ -223,15 +224,22 @@ class GpuBooster:
         else:
             s = ops.stream(self.dev)
             gp = make_grad_params("bernoulli", False, self.sample_rate, self.seed, t, **self.kw)
+            # all classes' gradients from the margins at the start of the iteration;
+            # per-class maxima are kept for the per-class quantisation scales
+            maxes = []
             for k in range(self.K):
                 if self.dist == "drf":
                     self._update(apply=False, next_tree=t, k=k)
                 else:
+                    b.stat_max.zero_()
                     ops.check(self.lib.h2omx_softmax_grad(P(st.Fm), self.K, st.Fm.stride(0), P(st.yk), P(st.w),
                                                           bm.n, bm.npad, k, ctypes.addressof(gp), P(b.nid),
-                                                          P(st.g[k]), P(st.h[k]), P(self.wout), s), "softmax_grad")
+                                                          P(st.g[k]), P(st.h[k]), P(self.wout), P(b.stat_max), s),
+                                  "softmax_grad")
+                maxes.append(b.stat_max.clone())
             for k in range(self.K):
                 b.nid[: bm.n].zero_()
+                b.stat_max.copy_(maxes[k])
                 b.build(st.g[k], st.h[k], self.wout, t * self.K + k, fmask)
                 self.trees_dev.append(b.tree_buf.clone())
                 ops.check(self.lib.h2omx_apply_tree(P(st.Fm[k]), bm.n, P(b.nid), P(b.tree_buf), s), "apply_tree")

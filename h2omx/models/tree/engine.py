@@ -54,11 +54,18 @@ def tree_capacity(max_depth: int) -> int:
 
 
 class HipTreeBuilder:
-    """Builds one tree per call entirely with enqueued HIP kernels."""
+    """Builds one tree per call entirely with enqueued HIP kernels.
+
+    Per tree: quantisation scales from the gradient maxima (written by the
+    boost kernel into ``stat_max``) -> per level {hist_build, hist_reduce,
+    [RCCL all-reduce], split_find, level_finalize, partition} -> exact leaf
+    sums (leaf_stats, [all-reduce], leaf_finalize).
+    """
 
     LDS_BUDGET = 64 * 1024     # bytes of LDS histogram per 512-thread workgroup (2 WGs per CU)
     TARGET_WGS = 512           # 2 workgroups x 256 CUs
     ROWS_PER_LANE = 16
+    ROWS_CAP = 32768           # rows per workgroup chunk (fixed-point headroom, see kernel)
     SYNC_NODE_CAP = 4096       # above this many potential nodes the host reads the real count
 
     def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
@@ -72,7 +79,7 @@ class HipTreeBuilder:
         self.dev = bm.codes.device
         self.F = bm.F
         self.nbt = bm.nbt
-        self.per_node = self.F * 3 * self.nbt  # doubles per node histogram
+        self.per_node = self.F * 2 * self.nbt  # int64 per node histogram (G_q, S_q planes)
         if params.max_depth < 1:
             raise ValueError("max_depth must be >= 1")
         self.capacity = tree_capacity(min(params.max_depth, 24))
@@ -83,8 +90,12 @@ class HipTreeBuilder:
         self._bufs: dict[str, torch.Tensor] = {}
         self.tree_buf = torch.zeros((self.capacity * TREE_NODE_DTYPE.itemsize,), dtype=torch.uint8, device=d)
         self.nid = torch.full((bm.npad,), -1, dtype=torch.int32, device=d)
+        self.stat_max = torch.zeros((4,), dtype=torch.int32, device=d)   # float bits of max|g|, max h, max w
+        self.qscale = torch.zeros((8,), dtype=torch.float64, device=d)
+        self.leaf_acc = torch.zeros((self.capacity * 3,), dtype=torch.int64, device=d)
         self._sp = SplitParams()
         self.stats = {"host_syncs": 0}
+        self.plans = {}
 
     # -- buffers -----------------------------------------------------------
     def _buf(self, name: str, numel: int, dtype) -> torch.Tensor:
@@ -97,11 +108,14 @@ class HipTreeBuilder:
     # -- planning ------------------------------------------------------------
     def plan_level(self, max_slots: int):
         """Feature grouping / slot passes / grid for a level with max_slots built nodes."""
-        per_slot_feat = 3 * self.nbt * 4
+        key = max_slots
+        if key in self.plans:
+            return self.plans[key]
+        per_slot_feat = self.nbt * 8
         F = self.F
         if max_slots * per_slot_feat <= self.LDS_BUDGET:
             slot_cnt = max_slots
-            fg_max = max(1, min(F, self.LDS_BUDGET // (max_slots * per_slot_feat)))
+            fg_max = max(1, min(F, 256, self.LDS_BUDGET // (max_slots * per_slot_feat)))
             n_groups = math.ceil(F / fg_max)
             fg = math.ceil(F / n_groups)
             passes = 1
@@ -111,32 +125,47 @@ class HipTreeBuilder:
             passes = math.ceil(max_slots / slot_cnt)
         units = self.bm.npad // self.ROWS_PER_LANE
         wgpg = max(8, (self.TARGET_WGS // n_groups) // 8 * 8)
-        # keep at least ~2 row units per lane per workgroup
-        max_wgpg = max(8, (units // (512 * 2)) // 8 * 8)
+        max_wgpg = max(8, (units // (512 * 2)) // 8 * 8)   # keep >= ~2 row units per lane
         wgpg = min(wgpg, max_wgpg)
-        return dict(slot_cnt=slot_cnt, fg=fg, n_groups=n_groups, passes=passes, wgpg=wgpg)
+        min_wgpg = math.ceil(math.ceil(units / (self.ROWS_CAP // self.ROWS_PER_LANE)) / 8) * 8
+        wgpg = max(wgpg, min_wgpg)
+        plan = dict(slot_cnt=slot_cnt, fg=fg, n_groups=n_groups, passes=passes, wgpg=wgpg)
+        self.plans[key] = plan
+        return plan
 
-    # -- one tree ------------------------------------------------------------
-    def build(self, g: torch.Tensor, h: torch.Tensor, w: torch.Tensor | None, tree_index: int,
-              tree_fmask: torch.Tensor | None = None) -> torch.Tensor:
-        """Grow one tree from per-row (g, h, w); ``self.nid`` must be 0 for rows
-        of the tree and INT_MIN for padding.  Returns the device tree buffer
-        (``TREE_NODE_DTYPE`` records, heap of capacity nodes; unused = garbage)."""
-        lib, bm, p = self.lib, self.bm, self.p
-        st = ops.stream(self.dev)
-        P = ops.P
-        F, nbt = self.F, self.nbt
-        sp = self._sp
-        sp.mode, sp.leaf_mode, sp.F, sp.is_last_level = p.mode, p.leaf_mode, F, 0
+    def _params(self, tree_index: int):
+        p, sp = self.p, self._sp
+        sp.mode, sp.leaf_mode, sp.F, sp.is_last_level = p.mode, p.leaf_mode, self.F, 0
         sp.min_rows, sp.min_child_weight = p.min_rows, p.min_child_weight
         sp.lambda_, sp.alpha, sp.gamma = p.reg_lambda, p.reg_alpha, p.gamma
         sp.min_split_improvement, sp.learn_rate, sp.max_abs_leaf = p.min_split_improvement, p.learn_rate, p.max_abs_leaf
         sp.seed, sp.tree_index = p.seed & 0xFFFFFFFF, tree_index
         sp.col_rate, sp.mtries = p.col_sample_rate, p.mtries
-        spp = ctypes.addressof(sp)
+        return ctypes.addressof(sp)
+
+    # -- one tree ------------------------------------------------------------
+    def build(self, g: torch.Tensor, h: torch.Tensor, w: torch.Tensor | None, tree_index: int,
+              tree_fmask: torch.Tensor | None = None) -> torch.Tensor:
+        """Grow one tree from per-row (g, h, w).  Preconditions (established by
+        the boost / softmax kernels): ``self.nid`` is 0 for rows of the tree and
+        INT_MIN for padding; ``self.stat_max`` holds this tree's maxima.
+        Returns the device tree buffer (``TREE_NODE_DTYPE`` heap of capacity
+        nodes; unreachable records are garbage)."""
+        lib, bm, p = self.lib, self.bm, self.p
+        st = ops.stream(self.dev)
+        P = ops.P
+        F, nbt = self.F, self.nbt
+        spp = self._params(tree_index)
+        sp = self._sp
+        comm = self.comm if (self.comm is not None and self.comm.world_size > 1) else None
+
+        if comm is not None:
+            comm.all_reduce_(self.stat_max, "max")
+        ops.check(lib.h2omx_quant_scales(P(self.stat_max), p.mode, P(self.qscale), st), "quant_scales")
+        s2 = w if p.mode == 0 else h
 
         self.ctl[0].copy_(self.ctl_init)
-        link = [self._buf("link0", 4 * 1, torch.int32), None]
+        link = [self._buf("link0", 4, torch.int32), None]
         link[0][:4].copy_(self.link_init)
         full_prev = None
         max_depth = p.max_depth
@@ -154,26 +183,27 @@ class HipTreeBuilder:
                 max_slots = 1 if d == 0 else max(1, max_nodes // 2)
             last = d == max_depth - 1
             plan = self.plan_level(max_slots)
-            built = self._buf("built", max_slots * self.per_node, torch.float64)
-            hist_floats = plan["slot_cnt"] * plan["fg"] * 3 * nbt
-            partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_floats, torch.float32)
+            built = self._buf("built", max_slots * self.per_node, torch.int64)
+            hist_elems = plan["slot_cnt"] * plan["fg"] * nbt
+            partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_elems, torch.int64)
             for ps in range(plan["passes"]):
                 slot_lo = ps * plan["slot_cnt"]
-                ops.check(lib.h2omx_hist_build(P(bm.codes), bm.npad, P(g), P(h), P(w), P(self.nid), P(link[cur]),
-                                               P(ctl_cur), F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"],
-                                               slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, P(partials), st),
+                ops.check(lib.h2omx_hist_build(P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]),
+                                               P(ctl_cur), P(bm.nvb), P(self.qscale), tree_index & 0x7FFFFFFF,
+                                               F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo,
+                                               plan["slot_cnt"], self.ROWS_PER_LANE, P(partials), st),
                           "hist_build")
                 ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F, nbt,
                                                 slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st), "hist_reduce")
-            if self.comm is not None and self.comm.world_size > 1:
-                self.comm.all_reduce_(built[: max_slots * self.per_node])
-            full_cur = None if last else self._buf(f"full{cur}", max_nodes * self.per_node, torch.float64)
+            if comm is not None:
+                comm.all_reduce_(built[: max_slots * self.per_node])
+            full_cur = None if last else self._buf(f"full{cur}", max_nodes * self.per_node, torch.int64)
             fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
             sp.depth = d
             sp.children_leaves = 1 if last else 0
             ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
-                                           P(bm.nvb), P(tree_fmask), spp, max_nodes, nbt, P(fbest), st),
-                      "split_find")
+                                           P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
+                                           P(fbest), st), "split_find")
             next_nodes = 2 * max_nodes
             part = self._buf("part", max_nodes * PART_INFO_BYTES // 4, torch.int32)
             nl = None
@@ -186,6 +216,14 @@ class HipTreeBuilder:
             ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, st), "partition")
             full_prev = full_cur
             max_nodes = next_nodes
+        # exact leaf values
+        self.leaf_acc.zero_()
+        ops.check(lib.h2omx_leaf_stats(P(self.nid), P(g), P(h), P(w), bm.n, P(self.qscale), self.capacity,
+                                       P(self.leaf_acc), st), "leaf_stats")
+        if comm is not None:
+            comm.all_reduce_(self.leaf_acc)
+        ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(self.ctl[max_depth % 2]), P(self.qscale), spp,
+                                          P(self.tree_buf), self.capacity, st), "leaf_finalize")
         return self.tree_buf
 
     def tree_size(self) -> torch.Tensor:

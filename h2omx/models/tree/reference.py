@@ -48,13 +48,15 @@ def _l1(g, a):
 
 
 def split_gain(GL, HL, WL, G, H, W, p: TreeParams):
+    """mode 0 (H2O): squared-error gain on (G, W) with min_rows on W;
+    mode 1 (XGBoost): second-order gain on (G, H) with min_child_weight on H."""
     GR, HR, WR = G - GL, H - HL, W - WL
-    ok = (WL >= p.min_rows) & (WR >= p.min_rows) & (WL > 0) & (WR > 0)
     with np.errstate(divide="ignore", invalid="ignore"):
         if p.mode == 0:
+            ok = (WL >= p.min_rows) & (WR >= p.min_rows) & (WL > 0) & (WR > 0)
             gain = GL * GL / WL + GR * GR / WR - G * G / W
         else:
-            ok &= (HL >= p.min_child_weight) & (HR >= p.min_child_weight)
+            ok = (HL >= p.min_child_weight) & (HR >= p.min_child_weight) & (HL > 0) & (HR > 0)
             lam = p.reg_lambda
             tl, tr, tt = _l1(GL, p.reg_alpha), _l1(GR, p.reg_alpha), _l1(G, p.reg_alpha)
             gain = 0.5 * (tl * tl / (HL + lam) + tr * tr / (HR + lam) - tt * tt / (H + lam)) - p.gamma

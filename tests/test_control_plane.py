@@ -1,0 +1,305 @@
+"""h2ok CLI + operator tests against the in-process fake Kubernetes API.
+
+Ports every test of the reference (src/cli/mod.rs:282-329,
+src/k8s/mod.rs:201-240, tests/integration_tests.rs of isgasho/h2o-kubernetes)
+with the live K3s cluster replaced by tests/fake_k8s.py, plus coverage the
+reference lacked (rollback, descriptor de-duplication, namespaces, TLS, the
+operator).
+"""
+import json
+import os
+import re
+import subprocess
+import time
+
+import pytest
+
+from tests.fake_k8s import FakeK8s
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CONTROL = os.path.join(ROOT, "control")
+H2OK = os.path.join(CONTROL, "build", "h2ok")
+OPERATOR = os.path.join(CONTROL, "build", "h2omx-operator")
+GENERAL_HELP = r"H2O Kubernetes CLI \d+.\d+.\d+.*"
+
+
+@pytest.fixture(scope="session", autouse=True)
+def built():
+    subprocess.run(["make", "-C", CONTROL, "-j8"], check=True, capture_output=True)
+    assert os.path.exists(H2OK) and os.path.exists(OPERATOR)
+
+
+@pytest.fixture()
+def k8s(tmp_path):
+    srv = FakeK8s(token="s3cr3t").start()
+    cfg = srv.kubeconfig(str(tmp_path / "kubeconfig"), namespace="default")
+    srv.cfg = cfg
+    yield srv
+    srv.stop()
+
+
+def run(args, cwd, stdin=None, env=None, timeout=60):
+    e = dict(os.environ)
+    e.pop("KUBECONFIG", None)
+    e["HOME"] = str(cwd)
+    if env:
+        e.update(env)
+    return subprocess.run([H2OK] + args, cwd=cwd, input=stdin, capture_output=True, text=True, timeout=timeout,
+                          env=e)
+
+
+# ---- tests/integration_tests.rs -------------------------------------------
+def test_general_help(tmp_path):
+    r = run(["-h"], tmp_path)
+    assert r.returncode == 0
+    assert re.match(GENERAL_HELP, r.stdout)
+
+
+def test_general_help_no_flag(tmp_path):
+    r = run([], tmp_path)
+    assert r.returncode != 0
+    assert re.match(GENERAL_HELP, r.stderr)
+
+
+def test_deployment_help(tmp_path):
+    r = run(["deploy", "-h"], tmp_path)
+    assert r.returncode == 0
+    assert re.match(r"h2ok-deploy.*", r.stdout)
+    assert "--cluster_size <cluster_size>" in r.stdout and "[default: 50]" in r.stdout
+
+
+def test_undeploy_help(tmp_path):
+    r = run(["undeploy", "-h"], tmp_path)
+    assert r.returncode == 0
+    assert re.match(r"h2ok-undeploy.*\nUndeploys an existing H2O cluster from Kubernetes.*", r.stdout)
+
+
+def test_deploy_undeploy(k8s, tmp_path):
+    r = run(["deploy", "--cluster_size", "1", "--kubeconfig", k8s.cfg], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert re.match(r".*\.h2ok", r.stdout)
+    descriptor = os.path.join(tmp_path, r.stdout.strip())
+    r = run(["ingress", "-f", descriptor], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert len(k8s.list("ingresses")) == 1
+    r = run(["undeploy", "-f", descriptor], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert re.match(r"Removed deployment 'h2o-.*", r.stdout)
+    assert not os.path.exists(descriptor)
+    assert k8s.list("services") == [] and k8s.list("statefulsets") == [] and k8s.list("ingresses") == []
+
+
+def test_undeploy_piping(k8s, tmp_path):
+    r = run(["deploy", "--cluster_size", "1", "--kubeconfig", k8s.cfg], tmp_path)
+    assert r.returncode == 0, r.stderr
+    r2 = run(["undeploy"], tmp_path, stdin=r.stdout)
+    assert r2.returncode == 0, r2.stderr
+    assert re.match(r"Removed deployment 'h2o-.*", r2.stdout)
+    # trailing newline from `echo` is tolerated (Q8)
+    r = run(["deploy", "--cluster_size", "1", "--kubeconfig", k8s.cfg], tmp_path)
+    r2 = run(["undeploy"], tmp_path, stdin=r.stdout + "\n")
+    assert r2.returncode == 0, r2.stderr
+
+
+def test_undeploy_missing_deployment_descriptor(tmp_path):
+    r = run(["undeploy"], tmp_path, stdin="nonexistent_file")
+    assert r.returncode == 1
+    assert re.search(r"Unable to process user input: UserInputError \{ kind: UnreachableDeploymentDescriptor \}",
+                     r.stderr)
+    r = run(["undeploy"], tmp_path, stdin="")
+    assert r.returncode == 1
+    assert "MissingDeploymentDescriptor" in r.stderr
+
+
+# ---- src/cli/mod.rs unit tests -------------------------------------------------
+def test_kubeconfig_path_and_namespace(k8s, tmp_path):
+    r = run(["deploy", "--kubeconfig", k8s.cfg, "--cluster_size", "1", "--dry-run"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "namespace: default" in r.stdout  # kubeconfig default namespace
+    r = run(["deploy", "--namespace", "non-default", "--cluster_size", "1", "--dry-run", "--kubeconfig", k8s.cfg],
+            tmp_path)
+    assert r.returncode == 0
+    assert "namespace: non-default" in r.stdout
+    r = run(["deploy", "--kubeconfig", str(tmp_path / "missing.yaml"), "--cluster_size", "1"], tmp_path)
+    assert r.returncode == 1 and "Invalid file path" in r.stderr
+
+
+def test_validate_number_range(tmp_path):
+    base = ["deploy", "--cluster_size", "1", "--dry-run", "--cluster_name", "x1"]
+    assert run(base + ["--memory_percentage", "10"], tmp_path).returncode == 0
+    r = run(base + ["--memory_percentage", "101"], tmp_path)
+    assert r.returncode == 1 and "withing range <0,100>" in r.stderr
+    r = run(["deploy", "--cluster_size", "0"], tmp_path)
+    assert r.returncode == 1 and "greater than zero" in r.stderr
+    r = run(["deploy", "--cluster_size", "abc"], tmp_path)  # Q10: no panic
+    assert r.returncode == 1 and "not an integer" in r.stderr
+    r = run(["deploy", "--cluster_size", "1", "--memory", "1 GB"], tmp_path)
+    assert r.returncode == 1 and "Memory requirement" in r.stderr
+    r = run(["deploy"], tmp_path)
+    assert r.returncode == 1 and "--cluster_size <cluster_size>" in r.stderr
+
+
+# ---- src/k8s/mod.rs::test_deploy_h2o ---------------------------------------------
+def test_deploy_h2o_objects(k8s, tmp_path):
+    r = run(["deploy", "--kubeconfig", k8s.cfg, "--cluster_name", "h2o-k8s-test-cluster", "-p", "80", "-m",
+             "256Mi", "--cpus", "2", "-s", "2"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == "h2o-k8s-test-cluster.h2ok"
+    svcs, stss = k8s.list("services"), k8s.list("statefulsets")
+    assert len(svcs) == 1 and len(stss) == 1 and k8s.list("ingresses") == []
+    svc, sts = svcs[0], stss[0]
+    assert svc["metadata"]["name"] == "h2o-k8s-test-cluster-service"
+    assert svc["spec"]["clusterIP"] == "None" and svc["spec"]["publishNotReadyAddresses"] is True
+    assert svc["spec"]["ports"][0]["port"] == 80 and svc["spec"]["ports"][0]["targetPort"] == 54321
+    spec = sts["spec"]
+    assert sts["metadata"]["name"] == "h2o-k8s-test-cluster-stateful-set"
+    assert spec["serviceName"] == "h2o-k8s-test-cluster-service"
+    assert spec["replicas"] == 2 and spec["podManagementPolicy"] == "Parallel"
+    c = spec["template"]["spec"]["containers"][0]
+    assert c["resources"]["limits"] == {"cpu": "2", "memory": "256Mi", "amd.com/gpu": "1"}
+    assert c["resources"]["requests"] == c["resources"]["limits"]
+    env = {e["name"]: e.get("value") for e in c["env"]}
+    assert env["H2O_KUBERNETES_SERVICE_DNS"] == "h2o-k8s-test-cluster-service.default.svc.cluster.local"
+    assert env["H2O_NODE_LOOKUP_TIMEOUT"] == "180" and env["H2O_NODE_EXPECTED_COUNT"] == "2"
+    assert env["H2O_KUBERNETES_API_PORT"] == "8081" and env["H2OMX_MEMORY_PERCENTAGE"] == "80"
+    probe = c["readinessProbe"]
+    assert probe["httpGet"] == {"path": "/kubernetes/isLeaderNode", "port": 8081}
+    assert (probe["initialDelaySeconds"], probe["periodSeconds"], probe["failureThreshold"]) == (5, 5, 1)
+    desc = json.load(open(tmp_path / "h2o-k8s-test-cluster.h2ok"))
+    assert list(desc) == ["specification", "ingresses", "stateful_sets", "services"]
+    sp = desc["specification"]
+    assert (sp["name"], sp["namespace"], sp["memory_percentage"], sp["memory"], sp["num_cpu"], sp["num_h2o_nodes"]) == \
+        ("h2o-k8s-test-cluster", "default", 80, "256Mi", 2, 2)
+    assert sp["kubeconfig_path"] == k8s.cfg
+    # ingress with a load-balancer IP (watch loop), connection hints in the object
+    r = run(["ingress", "-f", str(tmp_path / "h2o-k8s-test-cluster.h2ok")], tmp_path)
+    assert r.returncode == 0
+    desc = json.load(open(tmp_path / "h2o-k8s-test-cluster.h2ok"))
+    assert len(desc["ingresses"]) == 1
+    ing = desc["ingresses"][0]
+    assert ing["status"]["loadBalancer"]["ingress"][0]["ip"] == "10.43.0.7"
+    assert ing["spec"]["rules"][0]["http"]["paths"][0]["backend"]["service"]["name"] == "h2o-k8s-test-cluster-service"
+    r = run(["status", "-f", str(tmp_path / "h2o-k8s-test-cluster.h2ok")], tmp_path)
+    assert r.returncode == 0 and "2/2 pods, leader h2o-k8s-test-cluster-stateful-set-0" in r.stdout
+    r = run(["undeploy", "-f", str(tmp_path / "h2o-k8s-test-cluster.h2ok")], tmp_path)
+    assert r.returncode == 0
+    assert k8s.list("services") == [] and k8s.list("statefulsets") == [] and k8s.list("ingresses") == []
+
+
+def test_rollback_on_statefulset_failure(k8s, tmp_path):
+    k8s.fail[("POST", "statefulsets")] = 500
+    r = run(["deploy", "--kubeconfig", k8s.cfg, "-c", "rb", "-s", "1"], tmp_path)
+    assert r.returncode == 101
+    assert "Rewinding existing deployment" in r.stderr
+    assert k8s.list("services") == []  # service rolled back
+    assert not os.path.exists(tmp_path / "rb.h2ok")
+
+
+def test_descriptor_dedup_and_namespace(k8s, tmp_path):
+    r1 = run(["deploy", "--kubeconfig", k8s.cfg, "-c", "dup", "-s", "1", "-n", "team-a"], tmp_path)
+    r2 = run(["deploy", "--kubeconfig", k8s.cfg, "-c", "dup", "-s", "1", "-n", "team-b"], tmp_path)
+    assert r1.returncode == 0 and r2.returncode == 0
+    assert r1.stdout == "dup.h2ok" and r2.stdout == "dup(1).h2ok"  # Q4: real file name
+    assert "Writing file" in r2.stderr  # Q5: diagnostics never pollute the pipe
+    assert k8s.get("services", "team-a", "dup-service") and k8s.get("services", "team-b", "dup-service")
+    assert run(["undeploy", "-f", str(tmp_path / "dup(1).h2ok")], tmp_path).returncode == 0
+    assert k8s.get("services", "team-b", "dup-service") is None
+    assert k8s.get("services", "team-a", "dup-service")
+
+
+def test_partial_undeploy_keeps_descriptor(k8s, tmp_path):
+    run(["deploy", "--kubeconfig", k8s.cfg, "-c", "part", "-s", "1"], tmp_path)
+    k8s.fail[("DELETE", "statefulsets")] = 500
+    r = run(["undeploy", "-f", str(tmp_path / "part.h2ok")], tmp_path)
+    assert r.returncode == 2
+    assert "Unable to undeploy 'part-stateful-set' - skipping." in r.stdout
+    assert os.path.exists(tmp_path / "part.h2ok")  # Q7
+    del k8s.fail[("DELETE", "statefulsets")]
+    assert run(["undeploy", "-f", str(tmp_path / "part.h2ok")], tmp_path).returncode == 0
+
+
+def test_kubeconfig_inference_and_bad_token(k8s, tmp_path):
+    env = {"KUBECONFIG": k8s.cfg}
+    r = run(["deploy", "-c", "infer", "-s", "1"], tmp_path, env=env)
+    assert r.returncode == 0, r.stderr
+    bad = k8s.kubeconfig(str(tmp_path / "bad"), token="wrong")
+    r = run(["deploy", "-c", "nope", "-s", "1", "-k", bad], tmp_path)
+    assert r.returncode == 101 and "401" in r.stderr
+    r = run(["deploy", "-c", "nocfg", "-s", "1"], tmp_path)
+    assert r.returncode == 101 and "No kubeconfig provided" in r.stderr
+
+
+def test_tls_cluster(tmp_path):
+    srv = FakeK8s(token="t", tls=True, tmpdir=str(tmp_path)).start()
+    try:
+        cfg = srv.kubeconfig(str(tmp_path / "kc"))
+        r = run(["deploy", "-k", cfg, "-c", "tls", "-s", "1"], tmp_path)
+        assert r.returncode == 0, r.stderr
+        assert srv.get("statefulsets", "default", "tls-stateful-set")
+        assert run(["undeploy", "-f", str(tmp_path / "tls.h2ok")], tmp_path).returncode == 0
+    finally:
+        srv.stop()
+
+
+# ---- operator ------------------------------------------------------------------
+def _cr(name, nodes=2, **spec):
+    s = {"nodes": nodes, "version": "latest", "resources": {"cpu": 4, "memory": "64Gi", "memoryPercentage": 60,
+                                                            "gpu": 1}}
+    s.update(spec)
+    return {"apiVersion": "h2o.ai/v1beta", "kind": "H2O", "metadata": {"name": name}, "spec": s}
+
+
+def test_operator_reconcile(k8s, tmp_path):
+    k8s.put("h2os", "default", _cr("h2o-op", nodes=3))
+    r = subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    sts = k8s.get("statefulsets", "default", "h2o-op-stateful-set")
+    svc = k8s.get("services", "default", "h2o-op-service")
+    assert sts and svc
+    assert sts["spec"]["replicas"] == 3
+    cr = k8s.get("h2os", "default", "h2o-op")
+    assert sts["metadata"]["ownerReferences"][0]["uid"] == cr["metadata"]["uid"]
+    limits = sts["spec"]["template"]["spec"]["containers"][0]["resources"]["limits"]
+    assert limits == {"cpu": "4", "memory": "64Gi", "amd.com/gpu": "1"}
+    # second pass: pods exist (fake controller) -> status Ready with the leader
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    st = k8s.get("h2os", "default", "h2o-op")["status"]
+    assert st["phase"] == "Ready" and st["readyNodes"] == 1 and st["leaderPod"] == "h2o-op-stateful-set-0"
+    # spec change -> the fixed-size cloud is replaced
+    cr = k8s.get("h2os", "default", "h2o-op")
+    cr["spec"]["nodes"] = 5
+    k8s.put("h2os", "default", cr, "MODIFIED")
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    assert k8s.get("statefulsets", "default", "h2o-op-stateful-set")["spec"]["replicas"] == 5
+
+
+def test_operator_watch_loop(k8s, tmp_path):
+    p = subprocess.Popen([OPERATOR, "--kubeconfig", k8s.cfg, "--resync", "2"], stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(0.5)
+        k8s.put("h2os", "default", _cr("h2o-w", nodes=1))
+        for _ in range(50):
+            if k8s.get("statefulsets", "default", "h2o-w-stateful-set"):
+                break
+            time.sleep(0.1)
+        assert k8s.get("statefulsets", "default", "h2o-w-stateful-set")
+        k8s.delete("h2os", "default", "h2o-w")
+        for _ in range(50):
+            if not k8s.get("statefulsets", "default", "h2o-w-stateful-set"):
+                break
+            time.sleep(0.1)
+        assert k8s.get("statefulsets", "default", "h2o-w-stateful-set") is None
+    finally:
+        p.terminate()
+        p.wait(timeout=10)
+
+
+def test_crd_manifest_matches_operator():
+    from h2omx.utils.yamlio import load_all
+
+    docs = load_all(os.path.join(ROOT, "deploy", "crd.yaml"))
+    crd = docs[0]
+    assert crd["spec"]["group"] == "h2o.ai" and crd["spec"]["names"]["plural"] == "h2os"
+    v = crd["spec"]["versions"][0]
+    assert v["name"] == "v1beta" and "status" in v["subresources"]
