@@ -26,7 +26,7 @@ KERNEL_LIBS = {
     "metrics": ["metrics_kernels.hip"],
 }
 HOST_LIBS = {
-    "host": ["host/parser.cpp", "host/mojo_io.cpp"],
+    "host": ["host/parser.cpp"],
 }
 
 

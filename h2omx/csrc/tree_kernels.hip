@@ -27,6 +27,8 @@
 #include "common.h"
 #include <math.h>
 
+#include <algorithm>
+
 namespace {
 
 struct SplitParams {
@@ -207,7 +209,7 @@ __device__ __forceinline__ uint32_t row_hash(int64_t r, uint32_t salt) {
 }
 
 template <int NBT, int ROWS>
-__global__ __launch_bounds__(512) void hist_build_kernel(
+__global__ __launch_bounds__(1024) void hist_build_kernel(
     const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ s2,
     const int* __restrict__ nid, const NodeLink* __restrict__ link, const int* __restrict__ ctl,
     const int* __restrict__ nvb, const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups,
@@ -320,31 +322,52 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
 
 // Sum the per-workgroup slabs of one pass into exact int64 histograms
 // built[slot][F][2][NBT] (plane 0: G_q, plane 1: S_q).
+// Each 256-thread block owns 32 consecutive output bins and splits the
+// workgroup-slab dimension over 8 lane groups (4 loads in flight per lane),
+// then folds the 8 partial sums through LDS: latency is hidden by parallel
+// slabs instead of a long dependent chain per output element.
 __global__ __launch_bounds__(256) void hist_reduce_kernel(const unsigned long long* __restrict__ partials,
                                                           int n_groups, int wgpg, int fg, int F, int nbt, int slot_lo,
                                                           int slot_cnt, const int* __restrict__ ctl,
                                                           long long* __restrict__ built) {
-  const int64_t total = (int64_t)slot_cnt * F * nbt;
+  __shared__ long long rg[8][33], rs[8][33];
   const int n_slots = ctl[CTL_SLOTS];
   const int64_t hist_elems = (int64_t)slot_cnt * fg * nbt;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int bin = idx % nbt;
-    const int f = (idx / nbt) % F;
-    const int s = idx / ((int64_t)nbt * F);
-    if (slot_lo + s >= n_slots) continue;
+  const int e = threadIdx.x & 31, c0 = threadIdx.x >> 5;
+  const int64_t idx = (int64_t)blockIdx.x * 32 + e;  // output element (s, f, bin)
+  const int bin = idx % nbt;
+  const int f = (idx / nbt) % F;
+  const int s = idx / ((int64_t)nbt * F);
+  const bool live = (s < slot_cnt) && (slot_lo + s < n_slots);
+  long long ag = 0, as = 0;
+  if (live) {
     const int group = f / fg, fi = f % fg;
     const unsigned long long* p =
         partials + (int64_t)group * wgpg * hist_elems + ((int64_t)s * fg + fi) * nbt + bin;
-    long long ag = 0, as = 0;
-    for (int c = 0; c < wgpg; ++c) {
+    int c = c0;
+    for (; c + 24 < wgpg; c += 32) {
+      const unsigned long long v0 = p[(int64_t)c * hist_elems], v1 = p[(int64_t)(c + 8) * hist_elems];
+      const unsigned long long v2 = p[(int64_t)(c + 16) * hist_elems], v3 = p[(int64_t)(c + 24) * hist_elems];
+      ag += (long long)(int32_t)(uint32_t)(v0 >> 32) + (long long)(int32_t)(uint32_t)(v1 >> 32) +
+            (long long)(int32_t)(uint32_t)(v2 >> 32) + (long long)(int32_t)(uint32_t)(v3 >> 32);
+      as += (long long)(uint32_t)v0 + (long long)(uint32_t)v1 + (long long)(uint32_t)v2 + (long long)(uint32_t)v3;
+    }
+    for (; c < wgpg; c += 8) {
       const unsigned long long v = p[(int64_t)c * hist_elems];
       ag += (long long)(int32_t)(uint32_t)(v >> 32);
       as += (long long)(uint32_t)v;
     }
+  }
+  rg[c0][e] = ag;
+  rs[c0][e] = as;
+  __syncthreads();
+  if (c0 == 0 && live) {
+    long long tg = 0, ts = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { tg += rg[k][e]; ts += rs[k][e]; }
     long long* o = built + (((int64_t)(slot_lo + s) * F + f) * 2) * nbt + bin;
-    o[0] = ag;
-    o[nbt] = as;
+    o[0] = tg;
+    o[nbt] = ts;
   }
 }
 
@@ -480,12 +503,56 @@ __global__ __launch_bounds__(256) void split_find_kernel(const long long* __rest
   }
 }
 
+// Per-node arg-max over the features' best thresholds (gain desc, then
+// feature / bin / NA-direction asc): one wave per node, lane = feature.
+__global__ __launch_bounds__(64) void node_best_kernel(const FeatBest* __restrict__ fbest,
+                                                       const int* __restrict__ ctl, int F,
+                                                       NodeSplit* __restrict__ out) {
+  const int node = blockIdx.x;
+  if (node >= ctl[CTL_N]) return;
+  const int lane = threadIdx.x;
+  const FeatBest* fb = fbest + (int64_t)node * F;
+  double bg = -INFINITY;
+  long long key = 0x7fffffffffffffffLL;  // (feature, code) order for ties
+  int bf = -1;
+  for (int f = lane; f < F; f += 64) {
+    const double gn = fb[f].gain;
+    const int code = fb[f].code;
+    if (code == 0x7fffffff || !(gn > -INFINITY)) continue;
+    const long long k = ((long long)f << 32) | (unsigned)code;
+    if (bf < 0 || gn > bg || (gn == bg && k < key)) { bg = gn; key = k; bf = f; }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double og = __shfl_xor(bg, off, kWave);
+    const long long ok = __shfl_xor(key, off, kWave);
+    if (og > bg || (og == bg && ok < key)) { bg = og; key = ok; }
+  }
+  if (lane == 0) {
+    NodeSplit s;
+    // S is W (mode 0) or H (mode 1); exact leaf (G, H, W) sums come from the
+    // partition kernels, these only steer the split decisions
+    s.G = fb[0].G; s.H = fb[0].S; s.W = fb[0].S;
+    s.pad = 0;
+    if (key != 0x7fffffffffffffffLL) {
+      const int f = (int)(key >> 32), code = (int)(key & 0xffffffff);
+      const FeatBest& c = fb[f];
+      s.gain = c.gain; s.GL = c.GL; s.HL = c.SL; s.WL = c.SL;
+      s.feat = f; s.bin = code >> 1; s.na_left = code & 1;
+    } else {
+      s.gain = -INFINITY; s.GL = s.HL = s.WL = 0.0;
+      s.feat = -1; s.bin = 0; s.na_left = 0;
+    }
+    out[node] = s;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Level finalisation (single workgroup): decide split/leaf per node, number
 // the children, pick the smaller child to build, write tree records and the
 // partition table.  ctl_next receives the next level's counts.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void level_finalize_kernel(const FeatBest* __restrict__ fbest,
+__global__ __launch_bounds__(1024) void level_finalize_kernel(const NodeSplit* __restrict__ nsplit,
                                                               const int* __restrict__ ctl, int* __restrict__ ctl_next,
                                                               SplitParams p, const float* __restrict__ edges,
                                                               const int* __restrict__ nvb, int nbt,
@@ -505,29 +572,7 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(const FeatBest* __
     bool do_split = false;
     NodeSplit s;
     if (i < n) {
-      // arg-max over features: gain desc, then (feature, bin, na) asc
-      const FeatBest* fb = fbest + (int64_t)i * p.F;
-      int bf = -1;
-      double bg = -INFINITY;
-      int bc = 0x7fffffff;
-      for (int f = 0; f < p.F; ++f) {
-        const FeatBest& c = fb[f];
-        if (c.code == 0x7fffffff || !(c.gain > -INFINITY)) continue;
-        if (bf < 0 || c.gain > bg || (c.gain == bg && (f < bf || (f == bf && c.code < bc)))) {
-          bf = f; bg = c.gain; bc = c.code;
-        }
-      }
-      // S is W (mode 0) or H (mode 1); the exact leaf (G, H, W) come later
-      // from leaf_stats, these only steer the split decisions
-      s.G = fb[0].G; s.H = fb[0].S; s.W = fb[0].S;
-      if (bf >= 0) {
-        const FeatBest& c = fb[bf];
-        s.gain = c.gain; s.GL = c.GL; s.HL = c.SL; s.WL = c.SL;
-        s.feat = bf; s.bin = bc >> 1; s.na_left = bc & 1;
-      } else {
-        s.gain = -INFINITY; s.GL = s.HL = s.WL = 0.0;
-        s.feat = -1; s.bin = 0; s.na_left = 0;
-      }
+      s = nsplit[i];
       do_split = !p.is_last_level && s.feat >= 0 && isfinite(s.gain) && s.gain > 0.0;
       if (do_split && p.mode == 0 && p.min_split_improvement > 0.0) {
         // relative improvement over the node's explained sum of squares
@@ -619,29 +664,94 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(const FeatBest* __
   }
 }
 
-// K6: route every row to its child (or retire it into its leaf: nid = ~gid).
+// K6: route every row to its child, or retire it into its leaf (nid = ~gid).
+// Rows retiring at this level add their (g, h, w) to the exact int64 leaf
+// sums (every row retires exactly once per tree, so after the last level the
+// sums are complete) - this replaces a separate pass over the rows.  Leaf
+// sums are privatised in LDS per workgroup when the tree capacity fits.
 __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restrict__ codes, int64_t npad,
                                                         int* __restrict__ nid, const PartInfo* __restrict__ part,
-                                                        int nbt) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t r0 = q * 4;
-  if (r0 >= npad) return;
-  int4 n4 = *reinterpret_cast<int4*>(nid + r0);
-  int nn[4] = {n4.x, n4.y, n4.z, n4.w};
+                                                        int nbt, const float* __restrict__ g,
+                                                        const float* __restrict__ h, const float* __restrict__ w,
+                                                        const double* __restrict__ qs, int cap,
+                                                        unsigned long long* __restrict__ leaf_acc,
+                                                        unsigned long long* __restrict__ leaf_slab) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lacc[];
+  const bool use_lds = leaf_acc != nullptr && cap <= 2048;
+  // lane-replicated copies (lane % R) remove same-address serialisation when
+  // the 64 lanes of a wave retire into a handful of leaves
+  const int R = use_lds ? max(1, min(16, 4096 / (3 * cap))) : 1;
+  if (use_lds) {
+    for (int j = threadIdx.x; j < 3 * cap * R; j += blockDim.x) lacc[j] = 0ull;
+    __syncthreads();
+  }
+  unsigned long long* lcopy = lacc + 3 * cap * ((threadIdx.x & 63) % R);
+  double lg = 0, lh = 0, lw = 0;
+  if (leaf_acc) { lg = qs[4]; lh = qs[5]; lw = qs[6]; }
+  const int64_t nq = npad / 4;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r0 = q * 4;
+    int4 n4 = *reinterpret_cast<int4*>(nid + r0);
+    int nn[4] = {n4.x, n4.y, n4.z, n4.w};
+    bool changed = false;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int n = nn[k];
-    if (n < 0) continue;
-    const PartInfo pi = part[n];
-    if (pi.child < 0) {
-      nn[k] = ~pi.gid;
-    } else {
-      const int b = codes[(int64_t)pi.feat * npad + r0 + k];
-      const int right = (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
-      nn[k] = pi.leaf_children ? ~(pi.child_gid + right) : (pi.child + right);
+    for (int k = 0; k < 4; ++k) {
+      const int n = nn[k];
+      if (n < 0) continue;
+      changed = true;
+      const PartInfo pi = part[n];
+      int leaf = -1;
+      if (pi.child < 0) {
+        leaf = pi.gid;
+      } else {
+        const int b = codes[(int64_t)pi.feat * npad + r0 + k];
+        const int right = (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
+        if (pi.leaf_children) leaf = pi.child_gid + right;
+        else nn[k] = pi.child + right;
+      }
+      if (leaf >= 0) {
+        nn[k] = ~leaf;
+        if (leaf_acc && leaf < cap) {
+          const float wv = w ? w[r0 + k] : 1.0f;
+          if (wv != 0.0f) {
+            unsigned long long* dst = use_lds ? lcopy + 3 * leaf : leaf_acc + 3 * leaf;
+            atomicAdd(dst + 0, (unsigned long long)llrint((double)g[r0 + k] * lg));
+            atomicAdd(dst + 1, (unsigned long long)llrint((double)h[r0 + k] * lh));
+            atomicAdd(dst + 2, (unsigned long long)llrint((double)wv * lw));
+          }
+        }
+      }
+    }
+    if (changed) *reinterpret_cast<int4*>(nid + r0) = make_int4(nn[0], nn[1], nn[2], nn[3]);
+  }
+  if (use_lds) {
+    // fold the lane copies; with a slab each workgroup stores its sums
+    // (leaf_reduce adds the slabs) instead of 1000s of workgroups atomically
+    // adding into the same few leaf addresses
+    __syncthreads();
+    for (int j = threadIdx.x; j < 3 * cap; j += blockDim.x) {
+      unsigned long long v = 0ull;
+      for (int c = 0; c < R; ++c) v += lacc[c * 3 * cap + j];
+      if (leaf_slab) leaf_slab[(int64_t)blockIdx.x * 3 * cap + j] = v;
+      else if (v) atomicAdd(leaf_acc + j, v);
     }
   }
-  *reinterpret_cast<int4*>(nid + r0) = make_int4(nn[0], nn[1], nn[2], nn[3]);
+}
+
+// leaf_acc[j] += sum over the partition slabs (one 256-thread block per j).
+__global__ __launch_bounds__(256) void leaf_reduce_kernel(const unsigned long long* __restrict__ slab, int n_slabs,
+                                                          int width, unsigned long long* __restrict__ leaf_acc) {
+  __shared__ unsigned long long red[256];
+  const int j = blockIdx.x;
+  unsigned long long v = 0ull;
+  for (int s = threadIdx.x; s < n_slabs; s += blockDim.x) v += slab[(int64_t)s * width + j];
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && red[0]) leaf_acc[j] += red[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -711,33 +821,42 @@ __global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F
                                                            GradParams gp, float* __restrict__ g, float* __restrict__ h,
                                                            float* __restrict__ wout, unsigned int* __restrict__ stat_max) {
   float mg = 0.f, mh = 0.f, mw = 0.f;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < npad; r += (int64_t)gridDim.x * blockDim.x) {
-    if (r >= n) {
-      nid[r] = INT32_MIN;
-      g[r] = 0.f; h[r] = 0.f;
-      if (wout) wout[r] = 0.f;
-      continue;
+  const int64_t nq = npad / 4;  // 4 rows per lane, 16-byte accesses
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r0 = 4 * q;
+    float4 f4 = *reinterpret_cast<const float4*>(F + r0);
+    const float4 y4 = *reinterpret_cast<const float4*>(y + r0);
+    float4 w4 = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (wobs) w4 = *reinterpret_cast<const float4*>(wobs + r0);
+    int4 n4 = make_int4(0, 0, 0, 0);
+    if (gp.apply_tree) n4 = *reinterpret_cast<const int4*>(nid + r0);
+    float fv[4] = {f4.x, f4.y, f4.z, f4.w}, yv[4] = {y4.x, y4.y, y4.z, y4.w}, wv[4] = {w4.x, w4.y, w4.z, w4.w};
+    const int nv[4] = {n4.x, n4.y, n4.z, n4.w};
+    float gv[4], hv[4];
+    int nn[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t r = r0 + k;
+      if (r >= n) {
+        nn[k] = INT32_MIN; gv[k] = 0.f; hv[k] = 0.f; wv[k] = 0.f;
+        continue;
+      }
+      if (gp.apply_tree) fv[k] += tree[~nv[k]].value;
+      dist_grad(gp.dist, fv[k], yv[k], gp, gv[k], hv[k]);
+      if (gp.sample_rate < 1.0f) {
+        const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)r, 0x5bd1e995u));
+        if (u >= gp.sample_rate) wv[k] = 0.0f;
+      }
+      gv[k] *= wv[k];
+      hv[k] *= wv[k];
+      nn[k] = 0;
+      mg = fmaxf(mg, fabsf(gv[k])); mh = fmaxf(mh, hv[k]); mw = fmaxf(mw, wv[k]);
     }
-    float f = F[r];
-    if (gp.apply_tree) {
-      const int leaf = ~nid[r];
-      f += tree[leaf].value;
-      F[r] = f;
-    }
-    float gv, hv;
-    dist_grad(gp.dist, f, y[r], gp, gv, hv);
-    float wv = wobs ? wobs[r] : 1.0f;
-    if (gp.sample_rate < 1.0f) {
-      const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)r, 0x5bd1e995u));
-      if (u >= gp.sample_rate) wv = 0.0f;
-    }
-    gv *= wv;
-    hv *= wv;
-    g[r] = gv;
-    h[r] = hv;
-    if (wout) wout[r] = wv;
-    nid[r] = 0;
-    mg = fmaxf(mg, fabsf(gv)); mh = fmaxf(mh, hv); mw = fmaxf(mw, wv);
+    if (gp.apply_tree) *reinterpret_cast<float4*>(F + r0) = make_float4(fv[0], fv[1], fv[2], fv[3]);
+    *reinterpret_cast<float4*>(g + r0) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+    *reinterpret_cast<float4*>(h + r0) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+    if (wout) *reinterpret_cast<float4*>(wout + r0) = make_float4(wv[0], wv[1], wv[2], wv[3]);
+    *reinterpret_cast<int4*>(nid + r0) = make_int4(nn[0], nn[1], nn[2], nn[3]);
   }
   if (stat_max) block_max3(mg, mh, mw, stat_max);
 }
@@ -791,15 +910,19 @@ __global__ __launch_bounds__(256) void softmax_grad_kernel(const float* __restri
 }
 
 // Turn the (all-reduced) per-tree maxima into quantisation scales.
-__global__ void quant_scales_kernel(const unsigned int* __restrict__ stat_max, int mode, double* __restrict__ qs) {
+// qg / qs_: per-row fixed-point ranges chosen by the host from the largest
+// workgroup chunk of the tree's level plans (<= QG / QS): smaller chunks give
+// proportionally finer quantisation.
+__global__ void quant_scales_kernel(const unsigned int* __restrict__ stat_max, int mode, double qg, double qsr,
+                                    double* __restrict__ qs) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const double gmax = fmax((double)__uint_as_float(stat_max[0]), 1e-30);
   const double hmax = fmax((double)__uint_as_float(stat_max[1]), 1e-30);
   const double wmax = fmax((double)__uint_as_float(stat_max[2]), 1e-30);
   const double smax = (mode == 0) ? wmax : hmax;
   // power-of-two scales keep the double conversions exact
-  const double sg = exp2(floor(log2((double)QG / gmax)));
-  const double ss = exp2(floor(log2((double)QS / smax)));
+  const double sg = exp2(floor(log2(fmin(qg, (double)QG) / gmax)));
+  const double ss = exp2(floor(log2(fmin(qsr, (double)QS) / smax)));
   qs[0] = sg; qs[1] = ss; qs[2] = 1.0 / sg; qs[3] = 1.0 / ss;
   qs[4] = exp2(floor(log2(2147483647.0 / gmax)));
   qs[5] = exp2(floor(log2(2147483647.0 / hmax)));
@@ -936,16 +1059,17 @@ H2OMX_API int h2omx_bin_features(const float* X, int64_t ld, int64_t n, int F, c
 H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* g, const float* s2, const int* nid,
                                const void* link, const int* ctl, const int* nvb, const double* qscale, int salt,
                                int F, int nbt, int fg, int n_groups, int wgpg, int slot_lo, int slot_cnt,
-                               int rows_per_lane, unsigned long long* partials, hipStream_t stream) {
-  if (wgpg % 8 != 0 || npad % 16 != 0 || fg > 256) return kBadArg;
+                               int rows_per_lane, int threads, unsigned long long* partials, hipStream_t stream) {
+  if (wgpg % 8 != 0 || npad % 16 != 0 || fg > 256 || threads % 64 != 0 || threads > 1024 || threads < fg)
+    return kBadArg;
   const int64_t units = npad / rows_per_lane;
   if ((units + wgpg - 1) / wgpg * rows_per_lane > ROWS_CAP) return kBadArg;  // fixed-point headroom
   const size_t lds = (size_t)slot_cnt * fg * nbt * sizeof(unsigned long long);
-  if (lds > 150 * 1024) return kBadArg;
+  if (lds > 156 * 1024) return kBadArg;
   const int grid = n_groups * wgpg;
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
 #define H2OMX_HB(NB, R)                                                                                           \
-  hipLaunchKernelGGL((hist_build_kernel<NB, R>), dim3(grid), dim3(512), lds, stream, codes, npad, g, s2, nid, lk, \
+  hipLaunchKernelGGL((hist_build_kernel<NB, R>), dim3(grid), dim3(threads), lds, stream, codes, npad, g, s2, nid, lk, \
                      ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt, partials)
   if (rows_per_lane == 16) {
     switch (nbt) {
@@ -972,8 +1096,8 @@ H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* 
 
 H2OMX_API int h2omx_hist_reduce(const unsigned long long* partials, int n_groups, int wgpg, int fg, int F, int nbt,
                                 int slot_lo, int slot_cnt, const int* ctl, long long* built, hipStream_t stream) {
-  const int64_t total = (int64_t)slot_cnt * F * nbt;
-  hipLaunchKernelGGL(hist_reduce_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, stream, partials,
+  const int64_t total = (int64_t)slot_cnt * F * nbt;  // nbt is a multiple of 32
+  hipLaunchKernelGGL(hist_reduce_kernel, dim3((unsigned)(total / 32)), dim3(256), 0, stream, partials,
                      n_groups, wgpg, fg, F, nbt, slot_lo, slot_cnt, ctl, built);
   return launch_status();
 }
@@ -1001,20 +1125,31 @@ H2OMX_API int h2omx_split_find(const long long* built, const long long* parent_f
 
 H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_next, const void* params,
                                    const float* edges, const int* nvb, int nbt, int max_next_nodes, void* part,
-                                   void* next_link, void* tree, int tree_capacity, hipStream_t stream) {
+                                   void* next_link, void* tree, int tree_capacity, void* nsplit,
+                                   int max_nodes, hipStream_t stream) {
   const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  NodeSplit* ns = reinterpret_cast<NodeSplit*>(nsplit);
+  hipLaunchKernelGGL(node_best_kernel, dim3(max_nodes), dim3(64), 0, stream, reinterpret_cast<const FeatBest*>(fbest),
+                     ctl, p.F, ns);
   hipLaunchKernelGGL(level_finalize_kernel, dim3(1), dim3(1024), 0, stream,
-                     reinterpret_cast<const FeatBest*>(fbest), ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes,
+                     ns, ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes,
                      reinterpret_cast<PartInfo*>(part), reinterpret_cast<NodeLink*>(next_link),
                      reinterpret_cast<TreeNode*>(tree), tree_capacity);
   return launch_status();
 }
 
-H2OMX_API int h2omx_partition(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt,
-                              hipStream_t stream) {
+constexpr int PARTITION_BLOCKS = 1024;
+
+H2OMX_API int h2omx_partition(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt, const float* g,
+                              const float* h, const float* w, const double* qscale, int cap,
+                              unsigned long long* leaf_acc, unsigned long long* leaf_slab, hipStream_t stream) {
   if (npad % 4 != 0) return kBadArg;
-  hipLaunchKernelGGL(partition_kernel, dim3(grid_for(npad / 4, 256)), dim3(256), 0, stream, codes, npad, nid,
-                     reinterpret_cast<const PartInfo*>(part), nbt);
+  const int R = (leaf_acc && cap <= 2048) ? std::max(1, std::min(16, 4096 / (3 * cap))) : 1;
+  const size_t lds = (leaf_acc && cap <= 2048) ? (size_t)cap * 3 * R * sizeof(unsigned long long) : 0;
+  // fixed grid so the slab layout is known: [PARTITION_BLOCKS][3 * cap]
+  hipLaunchKernelGGL(partition_kernel, dim3(PARTITION_BLOCKS), dim3(256), lds, stream, codes, npad, nid,
+                     reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc,
+                     (leaf_acc && cap <= 2048) ? leaf_slab : nullptr);
   return launch_status();
 }
 
@@ -1044,8 +1179,12 @@ H2OMX_API int h2omx_softmax_grad(const float* F, int K, int64_t ldF, const int* 
   return launch_status();
 }
 
-H2OMX_API int h2omx_quant_scales(const unsigned int* stat_max, int mode, double* qscale, hipStream_t stream) {
-  hipLaunchKernelGGL(quant_scales_kernel, dim3(1), dim3(64), 0, stream, stat_max, mode, qscale);
+H2OMX_API int h2omx_quant_scales(const unsigned int* stat_max, int mode, int max_rows_per_wg, double* qscale,
+                                 hipStream_t stream) {
+  if (max_rows_per_wg < 1 || max_rows_per_wg > ROWS_CAP) return kBadArg;
+  const double qg = exp2(floor(log2(1073741824.0 / max_rows_per_wg)));   // |sum| <= 2^30
+  const double qsr = exp2(floor(log2(2147483648.0 / max_rows_per_wg)));  // sum <= 2^31
+  hipLaunchKernelGGL(quant_scales_kernel, dim3(1), dim3(64), 0, stream, stat_max, mode, qg, qsr, qscale);
   return launch_status();
 }
 
@@ -1054,6 +1193,15 @@ H2OMX_API int h2omx_leaf_stats(const int* nid, const float* g, const float* h, c
   const size_t lds = cap <= 2048 ? (size_t)cap * 3 * sizeof(unsigned long long) : 0;
   hipLaunchKernelGGL(leaf_stats_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), lds, stream, nid, g, h, w, n, qscale,
                      cap, acc);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_partition_blocks() { return PARTITION_BLOCKS; }
+
+H2OMX_API int h2omx_leaf_reduce(const unsigned long long* slab, int n_slabs, int cap, unsigned long long* leaf_acc,
+                                hipStream_t stream) {
+  if (n_slabs <= 0) return kOk;
+  hipLaunchKernelGGL(leaf_reduce_kernel, dim3(3 * cap), dim3(256), 0, stream, slab, n_slabs, 3 * cap, leaf_acc);
   return launch_status();
 }
 

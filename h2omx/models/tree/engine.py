@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -62,9 +63,12 @@ class HipTreeBuilder:
     sums (leaf_stats, [all-reduce], leaf_finalize).
     """
 
-    LDS_BUDGET = 64 * 1024     # bytes of LDS histogram per 512-thread workgroup (2 WGs per CU)
-    TARGET_WGS = 512           # 2 workgroups x 256 CUs
-    ROWS_PER_LANE = 16
+    # LDS histogram bytes per workgroup / threads per workgroup / target grid;
+    # tunable (H2OMX_HIST_LDS_KB, H2OMX_HIST_THREADS, H2OMX_HIST_WGS) for sweeps
+    LDS_BUDGET = int(os.environ.get("H2OMX_HIST_LDS_KB", "64")) * 1024
+    THREADS = int(os.environ.get("H2OMX_HIST_THREADS", "512"))
+    TARGET_WGS = int(os.environ.get("H2OMX_HIST_WGS", "512"))
+    ROWS_PER_LANE = int(os.environ.get("H2OMX_HIST_ROWS", "16"))
     ROWS_CAP = 32768           # rows per workgroup chunk (fixed-point headroom, see kernel)
     SYNC_NODE_CAP = 4096       # above this many potential nodes the host reads the real count
 
@@ -93,9 +97,17 @@ class HipTreeBuilder:
         self.stat_max = torch.zeros((4,), dtype=torch.int32, device=d)   # float bits of max|g|, max h, max w
         self.qscale = torch.zeros((8,), dtype=torch.float64, device=d)
         self.leaf_acc = torch.zeros((self.capacity * 3,), dtype=torch.int64, device=d)
+        self.part_blocks = int(self.lib.h2omx_partition_blocks())
+        self.leaf_slab = (torch.zeros((params.max_depth * self.part_blocks * 3 * self.capacity,), dtype=torch.int64,
+                                      device=d) if self.capacity <= 2048 else None)
         self._sp = SplitParams()
         self.stats = {"host_syncs": 0}
         self.plans = {}
+        # largest workgroup row chunk over every plan this tree can use: sets the
+        # fixed-point resolution (finer for smaller chunks), identical across levels
+        units = bm.npad // self.ROWS_PER_LANE
+        cands = [self.plan_level(1 << k) for k in range(0, 13)] + [self.plan_level(1 << 20)]
+        self.max_rows_per_wg = max(self.ROWS_PER_LANE * math.ceil(units / c["wgpg"]) for c in cands)
 
     # -- buffers -----------------------------------------------------------
     def _buf(self, name: str, numel: int, dtype) -> torch.Tensor:
@@ -106,31 +118,43 @@ class HipTreeBuilder:
         return b
 
     # -- planning ------------------------------------------------------------
-    def plan_level(self, max_slots: int):
-        """Feature grouping / slot passes / grid for a level with max_slots built nodes."""
-        key = max_slots
-        if key in self.plans:
-            return self.plans[key]
+    DEEP_LDS_BUDGET = int(os.environ.get("H2OMX_HIST_DEEP_LDS_KB", "128")) * 1024
+
+    def _plan(self, max_slots: int, budget: int, threads: int):
         per_slot_feat = self.nbt * 8
         F = self.F
-        if max_slots * per_slot_feat <= self.LDS_BUDGET:
+        if max_slots * per_slot_feat <= budget:
             slot_cnt = max_slots
-            fg_max = max(1, min(F, 256, self.LDS_BUDGET // (max_slots * per_slot_feat)))
+            fg_max = max(1, min(F, 256, budget // (max_slots * per_slot_feat)))
             n_groups = math.ceil(F / fg_max)
             fg = math.ceil(F / n_groups)
             passes = 1
         else:
             fg, n_groups = 1, F
-            slot_cnt = max(1, self.LDS_BUDGET // per_slot_feat)
+            slot_cnt = max(1, budget // per_slot_feat)
             passes = math.ceil(max_slots / slot_cnt)
         units = self.bm.npad // self.ROWS_PER_LANE
-        wgpg = max(8, (self.TARGET_WGS // n_groups) // 8 * 8)
-        max_wgpg = max(8, (units // (512 * 2)) // 8 * 8)   # keep >= ~2 row units per lane
+        target = self.TARGET_WGS * 512 // threads
+        wgpg = max(8, (target // n_groups) // 8 * 8)
+        max_wgpg = max(8, (units // (threads * 2)) // 8 * 8)   # keep >= ~2 row units per lane
         wgpg = min(wgpg, max_wgpg)
         min_wgpg = math.ceil(math.ceil(units / (self.ROWS_CAP // self.ROWS_PER_LANE)) / 8) * 8
         wgpg = max(wgpg, min_wgpg)
-        plan = dict(slot_cnt=slot_cnt, fg=fg, n_groups=n_groups, passes=passes, wgpg=wgpg)
-        self.plans[key] = plan
+        return dict(slot_cnt=slot_cnt, fg=fg, n_groups=n_groups, passes=passes, wgpg=wgpg, threads=threads)
+
+    def plan_level(self, max_slots: int):
+        """Feature grouping / slot passes / grid for a level with max_slots built nodes.
+        Shallow levels use 64 KB / 512-thread workgroups (2 per CU); levels
+        that would need >= 4 feature groups switch to 128 KB / 1024 threads
+        (1 per CU) so each row chunk is re-read by fewer groups."""
+        if max_slots in self.plans:
+            return self.plans[max_slots]
+        plan = self._plan(max_slots, self.LDS_BUDGET, self.THREADS)
+        if self.DEEP_LDS_BUDGET > self.LDS_BUDGET and plan["n_groups"] >= 4:
+            deep = self._plan(max_slots, self.DEEP_LDS_BUDGET, 1024)
+            if deep["n_groups"] < plan["n_groups"] or deep["passes"] < plan["passes"]:
+                plan = deep
+        self.plans[max_slots] = plan
         return plan
 
     def _params(self, tree_index: int):
@@ -161,15 +185,18 @@ class HipTreeBuilder:
 
         if comm is not None:
             comm.all_reduce_(self.stat_max, "max")
-        ops.check(lib.h2omx_quant_scales(P(self.stat_max), p.mode, P(self.qscale), st), "quant_scales")
+        ops.check(lib.h2omx_quant_scales(P(self.stat_max), p.mode, self.max_rows_per_wg, P(self.qscale), st),
+                  "quant_scales")
         s2 = w if p.mode == 0 else h
 
+        self.leaf_acc.zero_()
         self.ctl[0].copy_(self.ctl_init)
         link = [self._buf("link0", 4, torch.int32), None]
         link[0][:4].copy_(self.link_init)
         full_prev = None
         max_depth = p.max_depth
         max_nodes = 1
+        n_part = 0
         for d in range(max_depth):
             cur, nxt = d % 2, (d + 1) % 2
             ctl_cur, ctl_nxt = self.ctl[cur], self.ctl[nxt]
@@ -191,7 +218,7 @@ class HipTreeBuilder:
                 ops.check(lib.h2omx_hist_build(P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]),
                                                P(ctl_cur), P(bm.nvb), P(self.qscale), tree_index & 0x7FFFFFFF,
                                                F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo,
-                                               plan["slot_cnt"], self.ROWS_PER_LANE, P(partials), st),
+                                               plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"], P(partials), st),
                           "hist_build")
                 ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F, nbt,
                                                 slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st), "hist_reduce")
@@ -210,16 +237,24 @@ class HipTreeBuilder:
             if not last:
                 nl = self._buf(f"link{nxt}", next_nodes * NODE_LINK_BYTES // 4, torch.int32)
                 link[nxt] = nl
+            nsplit = self._buf("nsplit", max_nodes * 9, torch.float64)  # NodeSplit = 72 B
             ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges), P(bm.nvb), nbt,
-                                               next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity, st),
+                                               next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
+                                               P(nsplit), max_nodes, st),
                       "level_finalize")
-            ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, st), "partition")
+            slab = None
+            if self.leaf_slab is not None:
+                slab = self.leaf_slab[n_part * self.part_blocks * 3 * self.capacity:]
+            ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, P(g), P(h), P(w),
+                                          P(self.qscale), self.capacity, P(self.leaf_acc), P(slab), st),
+                      "partition")
+            n_part += 1
             full_prev = full_cur
             max_nodes = next_nodes
-        # exact leaf values
-        self.leaf_acc.zero_()
-        ops.check(lib.h2omx_leaf_stats(P(self.nid), P(g), P(h), P(w), bm.n, P(self.qscale), self.capacity,
-                                       P(self.leaf_acc), st), "leaf_stats")
+        # exact leaf values (sums accumulated by the partition kernels)
+        if self.leaf_slab is not None:
+            ops.check(lib.h2omx_leaf_reduce(P(self.leaf_slab), n_part * self.part_blocks, self.capacity,
+                                            P(self.leaf_acc), st), "leaf_reduce")
         if comm is not None:
             comm.all_reduce_(self.leaf_acc)
         ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(self.ctl[max_depth % 2]), P(self.qscale), spp,

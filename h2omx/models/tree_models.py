@@ -1,0 +1,249 @@
+"""GBM, XGBoost and DRF estimators on the shared histogram tree engine.
+
+Parameter names and defaults follow H2O-3's GBM / XGBoost / DRF model
+builders (the algorithms the reference's h2o.jar image serves; SURVEY.md
+§2.7).  Differences that come from the MI355X design are documented in
+docs/ALGORITHMS.md: features are binned once into <= 255 global quantile
+bins (``nbins``; H2O re-bins adaptively per node), categorical levels are
+binned as ordinal codes, and trees grow level-wise entirely on the GPU.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..frame.frame import ENUM, Frame
+from .base import Model, ModelBuilder, ModelCategory
+from .tree import TreeParams, bin_matrix, compute_edges, train_ensemble
+
+
+class TreeModel(Model):
+    algo = "tree"
+
+    def __init__(self, builder, model_id, ens, dist):
+        super().__init__(builder, model_id)
+        self.ens = ens
+        self.dist = dist
+
+    def _link(self, margin: torch.Tensor) -> torch.Tensor:
+        cat = self.category
+        if self.dist == "drf":
+            if cat == ModelCategory.BINOMIAL:
+                p1 = margin[0].clamp(0, 1)
+                return torch.stack([1 - p1, p1])
+            if cat == ModelCategory.MULTINOMIAL:
+                m = margin.clamp_min(0)
+                s = m.sum(0, keepdim=True)
+                return torch.where(s > 0, m / s.clamp_min(1e-30), torch.full_like(m, 1.0 / m.shape[0]))
+            return margin
+        if cat == ModelCategory.BINOMIAL:
+            p1 = torch.sigmoid(margin[0])
+            return torch.stack([1 - p1, p1])
+        if cat == ModelCategory.MULTINOMIAL:
+            return torch.softmax(margin, dim=0)
+        if self.dist in ("poisson", "gamma", "tweedie"):
+            return torch.exp(margin)
+        return margin
+
+    def predict_raw(self, frame: Frame) -> torch.Tensor:
+        X = frame.feature_matrix(self.x)
+        dev = X.device
+        m = self.ens.raw_margin(X)
+        if self.params.get("offset_column"):
+            m = m + frame.vec(self.params["offset_column"]).as_float()[None, :].to(m.device)
+        return self._link(m.to(dev))
+
+    def varimp(self):
+        gains = np.zeros(len(self.x))
+        for t in range(self.ens.trees.shape[0]):
+            tr = self.ens.trees[t]
+            for i in _reachable(tr):
+                if tr[i]["feat"] >= 0:
+                    gains[tr[i]["feat"]] += max(float(tr[i]["gain"]), 0.0)
+        if gains.max() <= 0:
+            return [(c, 0.0, 0.0, 0.0) for c in self.x]
+        order = np.argsort(-gains, kind="stable")
+        mx, tot = gains.max(), gains.sum()
+        return [(self.x[i], float(gains[i]), float(gains[i] / mx), float(gains[i] / tot)) for i in order]
+
+    def summary(self):
+        depths, leaves = [], []
+        for t in range(self.ens.trees.shape[0]):
+            nodes = _reachable(self.ens.trees[t])
+            lv = [i for i in nodes if self.ens.trees[t][i]["feat"] < 0]
+            leaves.append(len(lv))
+            depths.append(int(math.floor(math.log2(max(nodes) + 1))) if nodes else 0)
+        return {"model_id": self.model_id, "algo": self.algo, "number_of_trees": int(self.ens.trees.shape[0]),
+                "number_of_internal_trees": int(self.ens.trees.shape[0]),
+                "min_depth": int(min(depths) if depths else 0), "max_depth": int(max(depths) if depths else 0),
+                "mean_depth": float(np.mean(depths)) if depths else 0.0,
+                "min_leaves": int(min(leaves) if leaves else 0), "max_leaves": int(max(leaves) if leaves else 0),
+                "mean_leaves": float(np.mean(leaves)) if leaves else 0.0}
+
+
+def _reachable(tr):
+    out, stack = [], [0]
+    while stack:
+        i = stack.pop()
+        out.append(i)
+        if tr[i]["feat"] >= 0:
+            stack += [int(tr[i]["left"]), int(tr[i]["left"]) + 1]
+    return out
+
+
+class _TreeBuilder(ModelBuilder):
+    model_cls = TreeModel
+    mode = 0
+    default_nbins = 255
+
+    def _dist(self) -> str:
+        d = str(self.params.get("distribution", "AUTO")).lower()
+        if d in ("auto", ""):
+            return {ModelCategory.BINOMIAL: "bernoulli", ModelCategory.MULTINOMIAL: "multinomial"}.get(
+                self.category, "gaussian")
+        return d
+
+    def _tree_params(self, nfeat: int) -> TreeParams:
+        raise NotImplementedError
+
+    def _fit(self, train: Frame, valid: Frame | None, model_id: str) -> Model:
+        X = train.feature_matrix(self.x)
+        dist = self._dist()
+        yv = train.vec(self.y)
+        if self.category == ModelCategory.REGRESSION:
+            y = yv.as_float()
+        else:
+            y = yv.data.float()
+        w = train.vec(self.params["weights_column"]).as_float() if self.params.get("weights_column") else None
+        ok = (y >= 0) if self.category != ModelCategory.REGRESSION else ~torch.isnan(y)
+        if not bool(ok.all()):
+            X, y = X[:, ok], y[ok]
+            w = None if w is None else w[ok]
+        nbins = int(self.params.get("nbins") or self.params.get("max_bins") or self.default_nbins)
+        edges, nvb, nbt = compute_edges(X, min(nbins, 255), seed=self._seed(), comm=self.comm)
+        bm = bin_matrix(X, edges, nvb, nbt, names=self.x)
+        tp = self._tree_params(len(self.x))
+        nclass = len(self.response_domain) if self.response_domain else 1
+        ens_dist = self._engine_dist(dist)
+        init_f = None
+        if self.params.get("offset_column"):
+            raise NotImplementedError("offset_column is not supported by the tree engine yet")
+        ens = train_ensemble(bm, y, w, dist=ens_dist, ntrees=int(self.params["ntrees"]), tparams=tp,
+                             sample_rate=float(self.params.get("sample_rate", 1.0)), nclass=nclass,
+                             seed=self._seed(), comm=self.comm, init_f=init_f,
+                             dist_kw={"tweedie_power": float(self.params.get("tweedie_power", 1.5)),
+                                      "quantile_alpha": float(self.params.get("quantile_alpha", 0.5)),
+                                      "huber_delta": float(self.params.get("huber_alpha", 0.9))})
+        model = self.model_cls(self, model_id, ens, ens_dist)
+        model.timings = dict(ens.timings)
+        return model
+
+    def _engine_dist(self, dist: str) -> str:
+        return dist
+
+
+# ---------------------------------------------------------------------------
+class GBMModel(TreeModel):
+    algo = "gbm"
+    algo_full_name = "Gradient Boosting Machine"
+
+
+class H2OGradientBoostingEstimator(_TreeBuilder):
+    """H2O GBM: squared-error splits on pseudo-residuals, Newton leaf steps."""
+    algo = "gbm"
+    model_cls = GBMModel
+    DEFAULTS = dict(ntrees=50, max_depth=5, min_rows=10.0, nbins=255, nbins_top_level=1024, nbins_cats=1024,
+                    learn_rate=0.1, learn_rate_annealing=1.0, sample_rate=1.0, col_sample_rate=1.0,
+                    col_sample_rate_per_tree=1.0, min_split_improvement=1e-5, histogram_type="QuantilesGlobal",
+                    max_abs_leafnode_pred=0.0, tweedie_power=1.5, quantile_alpha=0.5, huber_alpha=0.9,
+                    stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0,
+                    offset_column=None, balance_classes=False, categorical_encoding="AUTO")
+
+    def _tree_params(self, nfeat):
+        p = self.params
+        return TreeParams(max_depth=int(p["max_depth"]), min_rows=float(p["min_rows"]), learn_rate=float(p["learn_rate"]),
+                          min_split_improvement=float(p["min_split_improvement"]), mode=0, leaf_mode=0,
+                          col_sample_rate=float(p["col_sample_rate"]),
+                          col_sample_rate_per_tree=float(p["col_sample_rate_per_tree"]),
+                          max_abs_leaf=float(p["max_abs_leafnode_pred"] or 0.0), seed=self._seed())
+
+
+# ---------------------------------------------------------------------------
+class XGBoostModel(TreeModel):
+    algo = "xgboost"
+    algo_full_name = "XGBoost"
+
+
+class H2OXGBoostEstimator(_TreeBuilder):
+    """XGBoost 'hist' semantics: second-order gain with L1/L2 leaf penalties,
+    min_child_weight on hessian mass, eta-scaled leaves."""
+    algo = "xgboost"
+    model_cls = XGBoostModel
+    mode = 1
+    default_nbins = 255
+    DEFAULTS = dict(ntrees=50, max_depth=6, min_rows=1.0, min_child_weight=None, learn_rate=0.3, eta=None,
+                    sample_rate=1.0, subsample=None, col_sample_rate=1.0, colsample_bylevel=None,
+                    col_sample_rate_per_tree=1.0, colsample_bytree=None, colsample_bynode=1.0, reg_lambda=1.0,
+                    reg_alpha=0.0, gamma=0.0, min_split_improvement=None, max_bins=256, tree_method="hist",
+                    booster="gbtree", grow_policy="depthwise", max_abs_leafnode_pred=0.0, tweedie_power=1.5,
+                    stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0,
+                    offset_column=None, backend="gpu", nbins=None, categorical_encoding="AUTO")
+
+    def _tree_params(self, nfeat):
+        p = self.params
+        mcw = p["min_child_weight"] if p["min_child_weight"] is not None else p["min_rows"]
+        eta = p["eta"] if p["eta"] is not None else p["learn_rate"]
+        gamma = p["min_split_improvement"] if p["min_split_improvement"] is not None else p["gamma"]
+        if p.get("subsample") is not None:
+            p["sample_rate"] = p["subsample"]
+        csr = p["colsample_bylevel"] if p["colsample_bylevel"] is not None else p["col_sample_rate"]
+        csr = float(csr) * float(p.get("colsample_bynode") or 1.0)
+        cst = p["colsample_bytree"] if p["colsample_bytree"] is not None else p["col_sample_rate_per_tree"]
+        return TreeParams(max_depth=int(p["max_depth"]), min_rows=0.0, min_child_weight=float(mcw),
+                          reg_lambda=float(p["reg_lambda"]), reg_alpha=float(p["reg_alpha"]), gamma=float(gamma),
+                          min_split_improvement=0.0, learn_rate=float(eta), mode=1, leaf_mode=0,
+                          col_sample_rate=csr, col_sample_rate_per_tree=float(cst),
+                          max_abs_leaf=float(p["max_abs_leafnode_pred"] or 0.0), seed=self._seed())
+
+
+# ---------------------------------------------------------------------------
+class DRFModel(TreeModel):
+    algo = "drf"
+    algo_full_name = "Distributed Random Forest"
+
+
+class H2ORandomForestEstimator(_TreeBuilder):
+    """Random forest: bagged (sample_rate) trees with per-node feature
+    sampling (mtries), leaves = mean response (class-indicator means for
+    classification), predictions averaged over trees."""
+    algo = "drf"
+    model_cls = DRFModel
+    default_nbins = 20
+    DEFAULTS = dict(ntrees=50, max_depth=20, min_rows=1.0, nbins=20, nbins_top_level=1024, nbins_cats=1024,
+                    mtries=-1, sample_rate=0.632, col_sample_rate_per_tree=1.0, min_split_improvement=1e-5,
+                    binomial_double_trees=False, histogram_type="QuantilesGlobal", stopping_rounds=0,
+                    stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0, balance_classes=False,
+                    categorical_encoding="AUTO", offset_column=None)
+
+    def _engine_dist(self, dist):
+        return "drf"
+
+    def _tree_params(self, nfeat):
+        p = self.params
+        mt = int(p["mtries"])
+        if mt == -1:
+            mt = max(1, int(math.sqrt(nfeat))) if self.category != ModelCategory.REGRESSION else max(1, nfeat // 3)
+        elif mt == -2 or mt >= nfeat:
+            mt = 0
+        return TreeParams(max_depth=int(p["max_depth"]), min_rows=float(p["min_rows"]), learn_rate=1.0,
+                          min_split_improvement=float(p["min_split_improvement"]), mode=0, leaf_mode=1, mtries=mt,
+                          col_sample_rate_per_tree=float(p["col_sample_rate_per_tree"]), seed=self._seed())
+
+    def _fit(self, train, valid, model_id):
+        if self.category == ModelCategory.BINOMIAL:
+            # one regression tree per iteration on the class-1 indicator (H2O
+            # DRF binomial without binomial_double_trees)
+            return super()._fit(train, valid, model_id)
+        return super()._fit(train, valid, model_id)

@@ -18,15 +18,17 @@ _CT = {"P": ctypes.c_void_p, "I": ctypes.c_int, "L": ctypes.c_int64, "F": ctypes
 TREE_SIGS = {
     "h2omx_tree_sizes": "P",
     "h2omx_bin_features": "PLLIPPIPLS",
-    "h2omx_hist_build": "PLPPPPPPPIIIIIIIIIPS",
+    "h2omx_hist_build": "PLPPPPPPPIIIIIIIIIIPS",
     "h2omx_hist_reduce": "PIIIIIIIPPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
-    "h2omx_level_finalize": "PPPPPPIIPPPIS",
-    "h2omx_partition": "PLPPIS",
+    "h2omx_level_finalize": "PPPPPPIIPPPIPIS",
+    "h2omx_partition": "PLPPIPPPPIPPS",
+    "h2omx_partition_blocks": "",
+    "h2omx_leaf_reduce": "PIIPS",
     "h2omx_boost_update": "PPPLLPPPPPPPS",
     "h2omx_apply_tree": "PLPPS",
     "h2omx_softmax_grad": "PILPPLLIPPPPPPS",
-    "h2omx_quant_scales": "PIPS",
+    "h2omx_quant_scales": "PIIPS",
     "h2omx_leaf_stats": "PPPPLPIPS",
     "h2omx_leaf_finalize": "PPPPPIS",
     "h2omx_predict_raw": "PLLPPIIPLS",
