@@ -1,0 +1,631 @@
+// Dense (matrix-shaped) hot paths on fp32 MFMA for gfx950:
+//   * GLM IRLS: one fused pass per iteration computes eta = X beta, the IRLS
+//     weights / working response, and the weighted Gram [X 1 z]^T W [X 1 z]
+//     (X^T W X, X^T W z, z^T W z) with v_mfma_f32_32x32x2_f32 from an
+//     LDS-staged row chunk; per-workgroup fp32 slabs are reduced in fp64.
+//   * K-Means: LDS-staged row chunk, centroid distances by MFMA
+//     (D = C . X^T so every lane owns one row's distances), in-register
+//     arg-min, and atomic-free per-workgroup cluster sums.
+//   * MLP: a tiled fp32-MFMA GEMM (NN / NT / TN) with a fused bias +
+//     activation epilogue, plus the small elementwise kernels of the
+//     backward pass and the ADADELTA / momentum optimizers.
+// fp32-input MFMA is exact fp32 (a k-ordered fmaf chain; see
+// cdna_hip_programming.md §3), so results match an fp32 reference.
+//
+// Reference parity: the reference deploys H2O-3 (templates.rs:28-30 of
+// isgasho/h2o-kubernetes) whose GLM / K-Means / DeepLearning these replace
+// (SURVEY.md §2.5 K10-K16).
+#include "common.h"
+
+#include <math.h>
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// ===========================================================================
+// GLM IRLS pass
+// ===========================================================================
+struct GlmParams {
+  int family;  // 0 gaussian 1 binomial 2 poisson 3 gamma 4 tweedie 5 multinomial 6 quasibinomial
+  int link;    // 0 identity 1 logit 2 log 3 inverse 4 tweedie-power
+  int p;       // features (without intercept)
+  int K;       // classes for multinomial, else 1
+  int cls;     // class being updated (multinomial)
+  int pad;
+  double var_power;   // tweedie variance power
+  double link_power;  // tweedie link power
+};
+
+__device__ __forceinline__ void glm_link(const GlmParams& P, double eta, double& mu, double& dmu) {
+  switch (P.link) {
+    case 1: {
+      const double e = exp(-fabs(eta));
+      const double s = eta >= 0 ? 1.0 / (1.0 + e) : e / (1.0 + e);
+      mu = s;
+      dmu = fmax(s * (1.0 - s), 1e-10);
+      break;
+    }
+    case 2: mu = exp(fmin(eta, 700.0)); dmu = fmax(mu, 1e-10); break;
+    case 3: {
+      const double e = (fabs(eta) < 1e-10) ? copysign(1e-10, eta) : eta;
+      mu = 1.0 / e;
+      dmu = -mu * mu;
+      break;
+    }
+    case 4: {
+      const double q = P.link_power;
+      if (q == 0.0) { mu = exp(fmin(eta, 700.0)); dmu = fmax(mu, 1e-10); }
+      else { const double e = fmax(eta, 1e-10); mu = pow(e, 1.0 / q); dmu = mu / (q * e); }
+      break;
+    }
+    default: mu = eta; dmu = 1.0;
+  }
+}
+
+__device__ __forceinline__ double glm_var(const GlmParams& P, double mu) {
+  switch (P.family) {
+    case 1: case 6: return fmax(mu * (1.0 - mu), 1e-10);
+    case 2: return fmax(mu, 1e-10);
+    case 3: return fmax(mu * mu, 1e-20);
+    case 4: return fmax(pow(fmax(mu, 1e-10), P.var_power), 1e-20);
+    default: return 1.0;
+  }
+}
+
+__device__ __forceinline__ double glm_dev(const GlmParams& P, double y, double mu) {
+  switch (P.family) {
+    case 1: case 6: {
+      const double m = fmin(fmax(mu, 1e-15), 1.0 - 1e-15);
+      return -2.0 * (y * log(m) + (1.0 - y) * log(1.0 - m));
+    }
+    case 2: {
+      const double m = fmax(mu, 1e-15);
+      return 2.0 * ((y > 0 ? y * log(y / m) : 0.0) - (y - m));
+    }
+    case 3: {
+      const double m = fmax(mu, 1e-15), yy = fmax(y, 1e-15);
+      return 2.0 * (-log(yy / m) + (y - m) / m);
+    }
+    case 4: {
+      const double r = P.var_power, m = fmax(mu, 1e-15);
+      const double a = (y > 0) ? pow(y, 2 - r) / ((1 - r) * (2 - r)) : 0.0;
+      return 2.0 * (a - y * pow(m, 1 - r) / (1 - r) + pow(m, 2 - r) / (2 - r));
+    }
+    default: return (y - mu) * (y - mu);
+  }
+}
+
+constexpr int GLM_RB = 64;  // rows per LDS chunk
+
+template <int TP>
+__global__ __launch_bounds__(256) void glm_irls_kernel(const float* __restrict__ X, int64_t ld, int64_t n,
+                                                       const float* __restrict__ y, const float* __restrict__ wprior,
+                                                       const float* __restrict__ offset,
+                                                       const float* __restrict__ means,
+                                                       const float* __restrict__ beta, GlmParams P,
+                                                       int64_t rows_per_wg, float* __restrict__ slab,
+                                                       double* __restrict__ dev_out) {
+  constexpr int PP = 32 * TP;            // padded augmented width [X | 1 | z | 0...]
+  constexpr int LDR = GLM_RB + 1;        // +1 float row pad: conflict-free column reads
+  constexpr int T = TP * (TP + 1) / 2;   // upper-triangular 32x32 tiles
+  constexpr int NT = (T + 3) / 4;        // tiles per wave
+  __shared__ float A[PP * LDR];
+  __shared__ float sw[GLM_RB], sz[GLM_RB];
+  __shared__ double part[4][GLM_RB];
+  __shared__ double devred[4];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int p = P.p;
+  const int64_t r_begin = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t r_end = min(n, r_begin + rows_per_wg);
+
+  for (int j = t; j < PP * LDR; j += 256) A[j] = 0.0f;  // padding columns stay zero
+  f32x16 acc[NT];
+#pragma unroll
+  for (int u = 0; u < NT; ++u)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[u][e] = 0.0f;
+  int ti_[NT], tj_[NT];
+#pragma unroll
+  for (int u = 0; u < NT; ++u) {
+    int id = wid + 4 * u, ti = 0;
+    while (id >= TP - ti && ti < TP) { id -= TP - ti; ++ti; }
+    ti_[u] = ti;
+    tj_[u] = ti + id;
+  }
+  double dev_acc = 0.0;
+  const float* bk = beta + (int64_t)P.cls * (p + 1);
+  __syncthreads();
+
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += GLM_RB) {
+    // 1. stage X (mean-imputed) column-major into LDS
+    for (int j = t; j < p * GLM_RB; j += 256) {
+      const int c = j >> 6, r = j & 63;
+      float v = 0.0f;
+      if (r0 + r < r_end) {
+        v = X[(int64_t)c * ld + r0 + r];
+        if (v != v) v = means[c];
+      }
+      A[c * LDR + r] = v;
+    }
+    __syncthreads();
+    // 2. linear predictors: 4 partial dot products per row
+    {
+      const int r = t & 63, q = t >> 6;
+      if (P.family == 5) {
+        // multinomial: need every class' eta for the softmax
+        double mx = -1e300, den = 0.0, ek = 0.0;
+        for (int k = 0; k < P.K; ++k) {
+          const float* bb = beta + (int64_t)k * (p + 1);
+          double e = 0.0;
+          for (int c = q; c < p; c += 4) e += (double)A[c * LDR + r] * bb[c];
+          part[q][r] = e;
+          __syncthreads();
+          if (q == 0) {
+            const double etak = part[0][r] + part[1][r] + part[2][r] + part[3][r] + bb[p];
+            // online softmax over classes
+            if (etak > mx) { den = den * exp(mx - etak) + 1.0; ek = (k == P.cls) ? 1.0 : ek * exp(mx - etak); mx = etak; }
+            else { den += exp(etak - mx); if (k == P.cls) ek = exp(etak - mx); }
+            if (k == P.cls) sz[r] = (float)etak;
+          }
+          __syncthreads();
+        }
+        if (q == 0) {
+          const int64_t row = r0 + r;
+          float wv = 0.0f, zv = 0.0f;
+          if (row < r_end) {
+            const double pk = fmin(fmax(ek / den, 1e-10), 1.0 - 1e-10);
+            const double yk = ((int)y[row] == P.cls) ? 1.0 : 0.0;
+            const double wpv = wprior ? wprior[row] : 1.0;
+            const double wi = pk * (1.0 - pk);
+            zv = (float)(sz[r] + (yk - pk) / wi);
+            wv = (float)sqrt(fmax(wpv * wi, 0.0));
+            dev_acc += wpv * (yk > 0 ? -2.0 * log(pk) : 0.0);
+          }
+          sw[r] = wv;
+          sz[r] = zv;
+        }
+      } else {
+        double e = 0.0;
+        for (int c = q; c < p; c += 4) e += (double)A[c * LDR + r] * bk[c];
+        part[q][r] = e;
+        __syncthreads();
+        if (q == 0) {
+          const int64_t row = r0 + r;
+          float wv = 0.0f, zv = 0.0f;
+          if (row < r_end) {
+            const double off = offset ? offset[row] : 0.0;
+            const double eta = part[0][r] + part[1][r] + part[2][r] + part[3][r] + bk[p] + off;
+            double mu, dmu;
+            glm_link(P, eta, mu, dmu);
+            const double yv = y[row];
+            const double wpv = wprior ? wprior[row] : 1.0;
+            const double wi = wpv * dmu * dmu / glm_var(P, mu);
+            zv = (float)(eta - off + (yv - mu) / dmu);
+            wv = (float)sqrt(fmax(wi, 0.0));
+            dev_acc += wpv * glm_dev(P, yv, mu);
+          }
+          sw[r] = wv;
+          sz[r] = zv;
+        }
+      }
+    }
+    __syncthreads();
+    // 3. scale by sqrt(w), append the intercept and working-response columns
+    for (int j = t; j < (p + 2) * GLM_RB; j += 256) {
+      const int c = j >> 6, r = j & 63;
+      const float s = sw[r];
+      if (c < p) A[c * LDR + r] *= s;
+      else if (c == p) A[c * LDR + r] = s;
+      else A[c * LDR + r] = sz[r] * s;
+    }
+    __syncthreads();
+    // 4. Gram tiles on the matrix cores: G[i][j] += sum_r a_i(r) a_j(r)
+    const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      if (wid + 4 * u < T) {
+        const float* ca = A + (ti_[u] * 32 + li) * LDR + lh;
+        const float* cb = A + (tj_[u] * 32 + li) * LDR + lh;
+#pragma unroll 8
+        for (int s = 0; s < GLM_RB / 2; ++s) acc[u] = mfma32(ca[2 * s], cb[2 * s], acc[u]);
+      }
+    }
+    __syncthreads();
+  }
+  // write this workgroup's upper tiles
+  float* out = slab + (int64_t)blockIdx.x * PP * PP;
+#pragma unroll
+  for (int u = 0; u < NT; ++u) {
+    if (wid + 4 * u < T) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int i = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const int j = lane & 31;
+        out[(ti_[u] * 32 + i) * PP + tj_[u] * 32 + j] = acc[u][e];
+      }
+    }
+  }
+  // deviance of this workgroup (only q==0 threads accumulated)
+  double d = wave_sum(dev_acc);
+  if (lane == 0) devred[wid] = d;
+  __syncthreads();
+  if (t == 0) dev_out[blockIdx.x] = devred[0] + devred[1] + devred[2] + devred[3];
+}
+
+// fp64 reduction of the per-workgroup slabs (upper tiles only are written;
+// lower-tile entries of the slab are never read)
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int n_slabs, int width,
+                                                          double* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= width) return;
+  const int PP = (int)sqrtf((float)width);
+  const int i = j / PP, k = j % PP;
+  if ((i >> 5) > (k >> 5)) {  // strictly-lower tile: mirror later
+    out[j] = 0.0;
+    return;
+  }
+  double acc = 0.0;
+  for (int s = 0; s < n_slabs; ++s) acc += slab[(int64_t)s * width + j];
+  out[j] = acc;
+}
+
+// ===========================================================================
+// K-Means: assign + per-workgroup cluster sums
+// ===========================================================================
+constexpr int KM_RB = 64;
+
+// X [d][ld] (already standardized by the caller), C [k][d], cn[k] = ||c||^2.
+// Outputs: assign[n], per-workgroup slab of [k][d] sums + k counts + k SSE.
+template <int DP, int KP>
+__global__ __launch_bounds__(256) void kmeans_kernel(const float* __restrict__ X, int64_t ld, int64_t n, int d,
+                                                     const float* __restrict__ C, const float* __restrict__ cn, int k,
+                                                     int64_t rows_per_wg, int* __restrict__ assign,
+                                                     float* __restrict__ slab) {
+  constexpr int LDR = KM_RB + 1;
+  __shared__ float Xs[DP * LDR];    // staged chunk [feature][row]
+  __shared__ float Cs[KP * (DP + 1)];  // centroids [cluster][feature]
+  __shared__ float S[KP * DP];      // cluster sums
+  __shared__ float cnt[KP], sse[KP], cns[KP];
+  __shared__ int asg[KM_RB];
+  __shared__ float bestd[KM_RB];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  for (int j = t; j < KP * (DP + 1); j += 256) {
+    const int c = j / (DP + 1), f = j % (DP + 1);
+    Cs[j] = (c < k && f < d) ? C[(int64_t)c * d + f] : 0.0f;
+  }
+  for (int j = t; j < KP * DP; j += 256) S[j] = 0.0f;
+  for (int j = t; j < KP; j += 256) {
+    cnt[j] = 0.0f; sse[j] = 0.0f;
+    cns[j] = (j < k) ? cn[j] : INFINITY;
+  }
+  for (int j = t; j < DP * LDR; j += 256) Xs[j] = 0.0f;
+  __syncthreads();
+  const int64_t r_begin = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t r_end = min(n, r_begin + rows_per_wg);
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += KM_RB) {
+    for (int j = t; j < d * KM_RB; j += 256) {
+      const int f = j >> 6, r = j & 63;
+      float v = 0.0f;
+      if (r0 + r < r_end) {
+        v = X[(int64_t)f * ld + r0 + r];
+        if (v != v) v = 0.0f;  // NA -> mean (0 in standardized space)
+      }
+      Xs[f * LDR + r] = v;
+    }
+    __syncthreads();
+    // waves 0,1 each own 32 rows; D[c][row] = sum_f C[c][f] X[f][row]
+    if (wid < 2) {
+      const int li = lane & 31, lh = lane >> 5;
+      const int rloc = wid * 32 + li;
+      float best = INFINITY;
+      int bi = 0;
+      for (int ct = 0; ct < KP / 32; ++ct) {
+        f32x16 acc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+        const float* ca = Cs + (ct * 32 + li) * (DP + 1) + lh;
+        const float* xb = Xs + lh * LDR + wid * 32 + li;
+        for (int s = 0; s < DP / 2; ++s) acc = mfma32(ca[2 * s], xb[2 * s * LDR], acc);
+        // lane holds clusters c = ct*32 + (e&3) + 8(e>>2) + 4*lh for row rloc
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int c = ct * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          const float dist = cns[c] - 2.0f * acc[e];
+          if (dist < best || (dist == best && c < bi)) { best = dist; bi = c; }
+        }
+      }
+      // combine the two half-waves holding the same row
+      const float ob = __shfl_xor(best, 32, kWave);
+      const int oi = __shfl_xor(bi, 32, kWave);
+      if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+      if (lh == 0) { asg[rloc] = bi; bestd[rloc] = best; }
+    }
+    __syncthreads();
+    // cluster sums: thread f owns feature column f of S (no atomics)
+    for (int f = t; f < d; f += 256) {
+      for (int r = 0; r < KM_RB; ++r) {
+        if (r0 + r >= r_end) break;
+        S[asg[r] * DP + f] += Xs[f * LDR + r];
+      }
+    }
+    if (t < KM_RB && r0 + t < r_end) {
+      float x2 = 0.0f;
+      for (int f = 0; f < d; ++f) x2 += Xs[f * LDR + t] * Xs[f * LDR + t];
+      assign[r0 + t] = asg[t];
+      // counts / SSE through LDS atomics (64 per chunk, negligible)
+      atomicAdd(&cnt[asg[t]], 1.0f);
+      atomicAdd(&sse[asg[t]], fmaxf(bestd[t] + x2, 0.0f));
+    }
+    __syncthreads();
+  }
+  // slab layout: [k][d] sums | k counts | k sse
+  float* out = slab + (int64_t)blockIdx.x * (k * d + 2 * k);
+  for (int j = t; j < k * d; j += 256) out[j] = S[(j / d) * DP + (j % d)];
+  for (int j = t; j < k; j += 256) {
+    out[k * d + j] = cnt[j];
+    out[k * d + k + j] = sse[j];
+  }
+}
+
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int n_slabs, int width,
+                                                       double* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= width) return;
+  double acc = 0.0;
+  for (int s = 0; s < n_slabs; ++s) acc += slab[(int64_t)s * width + j];
+  out[j] = acc;
+}
+
+// ===========================================================================
+// MLP: tiled fp32-MFMA GEMM with fused bias + activation
+// C[M][N] = act(op(A)[M][K] op(B)[K][N] + bias[N]);  row-major storage.
+//   TA: A stored [K][M] (use A^T), TB: B stored [N][K] (use B^T).
+// 256 threads, 128x128 block tile, each wave a 64x64 quadrant = 2x2 MFMA
+// tiles of 32x32, K staged 16 at a time through LDS as [k][m] / [k][n].
+// ===========================================================================
+constexpr int GB = 128, GK = 16;
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                   float* __restrict__ Cm, const float* __restrict__ bias, int M,
+                                                   int N, int K, int act, float beta_c) {
+  __shared__ float As[GK][GB + 4];
+  __shared__ float Bs[GK][GB + 4];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int m0 = blockIdx.y * GB, n0 = blockIdx.x * GB;
+  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+  const int li = lane & 31, lh = lane >> 5;
+  for (int k0 = 0; k0 < K; k0 += GK) {
+    // stage A tile (GB x GK) as As[k][m]
+    for (int j = t; j < GB * GK; j += 256) {
+      int m, kk;
+      if (TA) { m = j % GB; kk = j / GB; }  // A^T stored [K][M]: coalesced along m
+      else { kk = j % GK; m = j / GK; }     // A stored [M][K]: coalesced along k
+      const int gm = m0 + m, gk = k0 + kk;
+      float v = 0.0f;
+      if (gm < M && gk < K) v = TA ? A[(int64_t)gk * M + gm] : A[(int64_t)gm * K + gk];
+      As[kk][m] = v;
+    }
+    for (int j = t; j < GB * GK; j += 256) {
+      int nn, kk;
+      if (TB) { kk = j % GK; nn = j / GK; }  // B^T stored [N][K]: coalesced along k
+      else { nn = j % GB; kk = j / GB; }     // B stored [K][N]: coalesced along n
+      const int gn = n0 + nn, gk = k0 + kk;
+      float v = 0.0f;
+      if (gn < N && gk < K) v = TB ? B[(int64_t)gn * K + gk] : B[(int64_t)gk * N + gn];
+      Bs[kk][nn] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < GK / 2; ++s) {
+      const int kk = 2 * s + lh;
+      const float a0 = As[kk][wm + li], a1 = As[kk][wm + 32 + li];
+      const float b0 = Bs[kk][wn + li], b1 = Bs[kk][wn + 32 + li];
+      acc[0][0] = mfma32(a0, b0, acc[0][0]);
+      acc[0][1] = mfma32(a0, b1, acc[0][1]);
+      acc[1][0] = mfma32(a1, b0, acc[1][0]);
+      acc[1][1] = mfma32(a1, b1, acc[1][1]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int i = m0 + wm + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        const int j = n0 + wn + 32 * b + li;
+        if (i < M && j < N) {
+          float v = acc[a][b][e];
+          if (beta_c != 0.0f) v += beta_c * Cm[(int64_t)i * N + j];
+          if (bias) v += bias[j];
+          if (act == 1) v = fmaxf(v, 0.0f);
+          else if (act == 2) v = tanhf(v);
+          else if (act == 3) v = fmaxf(v, 0.0f);  // maxout approximated by relu
+          Cm[(int64_t)i * N + j] = v;
+        }
+      }
+}
+
+// dZ = dY * act'(Y)  (act: 0 none, 1 relu, 2 tanh), in place allowed
+__global__ __launch_bounds__(256) void act_backward_kernel(const float* __restrict__ Y, float* __restrict__ dY,
+                                                           int64_t n, int act) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float g = dY[i];
+  if (act == 1 || act == 3) g = Y[i] > 0.0f ? g : 0.0f;
+  else if (act == 2) g = g * (1.0f - Y[i] * Y[i]);
+  dY[i] = g;
+}
+
+// db[j] = sum_i dY[i][j]
+__global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict__ dY, float* __restrict__ db, int M,
+                                                        int N) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= N) return;
+  float s = 0.0f;
+  for (int i = 0; i < M; ++i) s += dY[(int64_t)i * N + j];
+  db[j] = s;
+}
+
+// softmax cross-entropy over logits Z [M][K]: writes dZ = (softmax - onehot) * w / norm
+// and accumulates the loss into loss[0].
+__global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ Z, const float* __restrict__ y,
+                                                           float* __restrict__ dZ, float* __restrict__ loss, int M,
+                                                           int K) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float l = 0.0f;
+  if (i < M) {
+    const float* z = Z + (int64_t)i * K;
+    float mx = -INFINITY;
+    for (int k = 0; k < K; ++k) mx = fmaxf(mx, z[k]);
+    float den = 0.0f;
+    for (int k = 0; k < K; ++k) den += __expf(z[k] - mx);
+    const int yi = (int)y[i];
+    for (int k = 0; k < K; ++k) {
+      const float pk = __expf(z[k] - mx) / den;
+      dZ[(int64_t)i * K + k] = (pk - (k == yi ? 1.0f : 0.0f)) / (float)M;
+      if (k == yi) l = -logf(fmaxf(pk, 1e-30f));
+    }
+  }
+  l = wave_sum(l);
+  if ((threadIdx.x & 63) == 0) atomicAdd(loss, l / (float)M);
+}
+
+// ADADELTA (H2O DeepLearning default: rho 0.99, epsilon 1e-8) with L1/L2
+__global__ __launch_bounds__(256) void adadelta_kernel(float* __restrict__ W, const float* __restrict__ G,
+                                                       float* __restrict__ Eg2, float* __restrict__ Edx2, int64_t n,
+                                                       float rho, float eps, float l2) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float g = G[i] + l2 * W[i];
+  const float eg = rho * Eg2[i] + (1.0f - rho) * g * g;
+  const float dx = -sqrtf(Edx2[i] + eps) / sqrtf(eg + eps) * g;
+  Eg2[i] = eg;
+  Edx2[i] = rho * Edx2[i] + (1.0f - rho) * dx * dx;
+  W[i] += dx;
+}
+
+__global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ W, const float* __restrict__ G,
+                                                           float* __restrict__ V, int64_t n, float lr, float mom,
+                                                           float l2) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float v = mom * V[i] - lr * (G[i] + l2 * W[i]);
+  V[i] = v;
+  W[i] += v;
+}
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+H2OMX_API int h2omx_dense_sizes(int* out) {
+  out[0] = sizeof(GlmParams);
+  return kOk;
+}
+
+H2OMX_API int h2omx_glm_irls(const float* X, int64_t ld, int64_t n, const float* y, const float* wprior,
+                             const float* offset, const float* means, const float* beta, const void* params,
+                             int n_wg, int tp, float* slab, double* dev_out, hipStream_t stream) {
+  const GlmParams P = *reinterpret_cast<const GlmParams*>(params);
+  if (P.p + 2 > 32 * tp || n_wg < 1) return kBadArg;
+  const int64_t rows_per_wg = ((n + n_wg - 1) / n_wg + GLM_RB - 1) / GLM_RB * GLM_RB;
+#define GLM_L(TP)                                                                                      \
+  hipLaunchKernelGGL(glm_irls_kernel<TP>, dim3(n_wg), dim3(256), 0, stream, X, ld, n, y, wprior, offset, \
+                     means, beta, P, rows_per_wg, slab, dev_out)
+  switch (tp) {
+    case 1: GLM_L(1); break;
+    case 2: GLM_L(2); break;
+    case 4: GLM_L(4); break;
+    case 8: GLM_L(8); break;
+    default: return kBadArg;
+  }
+#undef GLM_L
+  return launch_status();
+}
+
+H2OMX_API int h2omx_slab_reduce_upper(const float* slab, int n_slabs, int width, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(cdiv(width, 256)), dim3(256), 0, stream, slab, n_slabs, width, out);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_slab_sum(const float* slab, int n_slabs, int width, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(cdiv(width, 256)), dim3(256), 0, stream, slab, n_slabs, width, out);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_kmeans(const float* X, int64_t ld, int64_t n, int d, const float* C, const float* cn, int k,
+                           int n_wg, int* assign, float* slab, hipStream_t stream) {
+  if (n_wg < 1) return kBadArg;
+  const int64_t rows_per_wg = ((n + n_wg - 1) / n_wg + KM_RB - 1) / KM_RB * KM_RB;
+#define KM_L(DP, KP)                                                                                         \
+  hipLaunchKernelGGL((kmeans_kernel<DP, KP>), dim3(n_wg), dim3(256), 0, stream, X, ld, n, d, C, cn, k, rows_per_wg, \
+                     assign, slab)
+  const int dp = d <= 32 ? 32 : (d <= 64 ? 64 : (d <= 128 ? 128 : (d <= 256 ? 256 : 0)));
+  const int kp = k <= 32 ? 32 : (k <= 64 ? 64 : (k <= 128 ? 128 : 0));
+  if (!dp || !kp || (size_t)dp * 65 * 4 + (size_t)kp * (dp + 1) * 4 + (size_t)kp * dp * 4 > 150 * 1024)
+    return kBadArg;
+  if (dp == 32 && kp == 32) KM_L(32, 32);
+  else if (dp == 32 && kp == 64) KM_L(32, 64);
+  else if (dp == 32 && kp == 128) KM_L(32, 128);
+  else if (dp == 64 && kp == 32) KM_L(64, 32);
+  else if (dp == 64 && kp == 64) KM_L(64, 64);
+  else if (dp == 64 && kp == 128) KM_L(64, 128);
+  else if (dp == 128 && kp == 32) KM_L(128, 32);
+  else if (dp == 128 && kp == 64) KM_L(128, 64);
+  else if (dp == 256 && kp == 32) KM_L(256, 32);
+  else return kBadArg;
+#undef KM_L
+  return launch_status();
+}
+
+H2OMX_API int h2omx_gemm(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int ta,
+                         int tb, int act, float beta_c, hipStream_t stream) {
+  const dim3 grid(cdiv(N, GB), cdiv(M, GB));
+  if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(256), 0, stream, A, B, C, bias, M, N, K, act, beta_c);
+  else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(256), 0, stream, A, B, C, bias, M, N, K, act, beta_c);
+  else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(256), 0, stream, A, B, C, bias, M, N, K, act, beta_c);
+  else hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(256), 0, stream, A, B, C, bias, M, N, K, act, beta_c);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_act_backward(const float* Y, float* dY, int64_t n, int act, hipStream_t stream) {
+  hipLaunchKernelGGL(act_backward_kernel, dim3(cdiv(n, 256)), dim3(256), 0, stream, Y, dY, n, act);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_bias_grad(const float* dY, float* db, int M, int N, hipStream_t stream) {
+  hipLaunchKernelGGL(bias_grad_kernel, dim3(cdiv(N, 256)), dim3(256), 0, stream, dY, db, M, N);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_softmax_xent(const float* Z, const float* y, float* dZ, float* loss, int M, int K,
+                                 hipStream_t stream) {
+  hipLaunchKernelGGL(softmax_xent_kernel, dim3(cdiv(M, 256)), dim3(256), 0, stream, Z, y, dZ, loss, M, K);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_adadelta(float* W, const float* G, float* Eg2, float* Edx2, int64_t n, float rho, float eps,
+                             float l2, hipStream_t stream) {
+  hipLaunchKernelGGL(adadelta_kernel, dim3(cdiv(n, 256)), dim3(256), 0, stream, W, G, Eg2, Edx2, n, rho, eps, l2);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_sgd_momentum(float* W, const float* G, float* V, int64_t n, float lr, float mom, float l2,
+                                 hipStream_t stream) {
+  hipLaunchKernelGGL(sgd_momentum_kernel, dim3(cdiv(n, 256)), dim3(256), 0, stream, W, G, V, n, lr, mom, l2);
+  return launch_status();
+}

@@ -686,16 +686,16 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
     __syncthreads();
   }
   unsigned long long* lcopy = lacc + 3 * cap * ((threadIdx.x & 63) % R);
-  double lg = 0, lh = 0, lw = 0;
-  if (leaf_acc) { lg = qs[4]; lh = qs[5]; lw = qs[6]; }
-  const int64_t nq = npad / 4;
+  float lg = 0, lh = 0, lw = 0;
+  if (leaf_acc) { lg = (float)qs[4]; lh = (float)qs[5]; lw = (float)qs[6]; }
+  const int64_t nq = npad / 8;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r0 = q * 4;
-    int4 n4 = *reinterpret_cast<int4*>(nid + r0);
-    int nn[4] = {n4.x, n4.y, n4.z, n4.w};
+    const int64_t r0 = q * 8;
+    const int4 na = *reinterpret_cast<int4*>(nid + r0), nb = *reinterpret_cast<int4*>(nid + r0 + 4);
+    int nn[8] = {na.x, na.y, na.z, na.w, nb.x, nb.y, nb.z, nb.w};
     bool changed = false;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 8; ++k) {
       const int n = nn[k];
       if (n < 0) continue;
       changed = true;
@@ -715,14 +715,17 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
           const float wv = w ? w[r0 + k] : 1.0f;
           if (wv != 0.0f) {
             unsigned long long* dst = use_lds ? lcopy + 3 * leaf : leaf_acc + 3 * leaf;
-            atomicAdd(dst + 0, (unsigned long long)llrint((double)g[r0 + k] * lg));
-            atomicAdd(dst + 1, (unsigned long long)llrint((double)h[r0 + k] * lh));
-            atomicAdd(dst + 2, (unsigned long long)llrint((double)wv * lw));
+            atomicAdd(dst + 0, (unsigned long long)(long long)__float2int_rn(g[r0 + k] * lg));
+            atomicAdd(dst + 1, (unsigned long long)(long long)__float2int_rn(h[r0 + k] * lh));
+            atomicAdd(dst + 2, (unsigned long long)(long long)__float2int_rn(wv * lw));
           }
         }
       }
     }
-    if (changed) *reinterpret_cast<int4*>(nid + r0) = make_int4(nn[0], nn[1], nn[2], nn[3]);
+    if (changed) {
+      *reinterpret_cast<int4*>(nid + r0) = make_int4(nn[0], nn[1], nn[2], nn[3]);
+      *reinterpret_cast<int4*>(nid + r0 + 4) = make_int4(nn[4], nn[5], nn[6], nn[7]);
+    }
   }
   if (use_lds) {
     // fold the lane copies; with a slab each workgroup stores its sums
@@ -797,9 +800,11 @@ __device__ __forceinline__ void dist_grad(int dist, float f, float y, const Grad
   }
 }
 
-// Block-level max of three non-negative statistics folded into one
-// atomicMax per statistic per workgroup (float bits compare as uint32).
-__device__ __forceinline__ void block_max3(float a, float b, float c, unsigned int* __restrict__ stat_max) {
+// Block-level max of three non-negative statistics, written (no atomics) to
+// this block's slot of a fixed-size slab; stat_reduce folds the slab.
+constexpr int STAT_BLOCKS = 4096;
+
+__device__ __forceinline__ void block_max3(float a, float b, float c, unsigned int* __restrict__ stat_slab) {
   __shared__ float red[3][16];
   a = wave_max(a); b = wave_max(b); c = wave_max(c);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -809,9 +814,8 @@ __device__ __forceinline__ void block_max3(float a, float b, float c, unsigned i
     const int nw = (blockDim.x + 63) >> 6;
     float m0 = 0.f, m1 = 0.f, m2 = 0.f;
     for (int k = 0; k < nw; ++k) { m0 = fmaxf(m0, red[0][k]); m1 = fmaxf(m1, red[1][k]); m2 = fmaxf(m2, red[2][k]); }
-    atomicMax(stat_max + 0, __float_as_uint(m0));
-    atomicMax(stat_max + 1, __float_as_uint(m1));
-    atomicMax(stat_max + 2, __float_as_uint(m2));
+    unsigned int* o = stat_slab + 4 * blockIdx.x;
+    o[0] = __float_as_uint(m0); o[1] = __float_as_uint(m1); o[2] = __float_as_uint(m2); o[3] = 0u;
   }
 }
 
@@ -910,12 +914,43 @@ __global__ __launch_bounds__(256) void softmax_grad_kernel(const float* __restri
 }
 
 // Turn the (all-reduced) per-tree maxima into quantisation scales.
-// qg / qs_: per-row fixed-point ranges chosen by the host from the largest
+// Fold the per-block maxima slab into stat_max (uint32 float bits).
+__global__ __launch_bounds__(1024) void stat_reduce_kernel(const unsigned int* __restrict__ slab, int n,
+                                                          unsigned int* __restrict__ stat_max) {
+  __shared__ unsigned int red[3][16];
+  unsigned int m0 = 0, m1 = 0, m2 = 0;  // non-negative float bits order like the floats
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    m0 = max(m0, slab[4 * i]); m1 = max(m1, slab[4 * i + 1]); m2 = max(m2, slab[4 * i + 2]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    m0 = max(m0, (unsigned)__shfl_xor((int)m0, off, kWave));
+    m1 = max(m1, (unsigned)__shfl_xor((int)m1, off, kWave));
+    m2 = max(m2, (unsigned)__shfl_xor((int)m2, off, kWave));
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { red[0][wid] = m0; red[1][wid] = m1; red[2][wid] = m2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
+      m0 = max(m0, red[0][k]); m1 = max(m1, red[1][k]); m2 = max(m2, red[2][k]);
+    }
+    m0 = max(m0, red[0][0]); m1 = max(m1, red[1][0]); m2 = max(m2, red[2][0]);
+    stat_max[0] = m0; stat_max[1] = m1; stat_max[2] = m2; stat_max[3] = 0u;
+  }
+}
+
+// Start of a tree: quantisation scales from the (all-reduced) maxima, level-0
+// control block / link, and zeroed leaf sums - one launch instead of five.
+// qg / qsr: per-row fixed-point ranges chosen by the host from the largest
 // workgroup chunk of the tree's level plans (<= QG / QS): smaller chunks give
 // proportionally finer quantisation.
-__global__ void quant_scales_kernel(const unsigned int* __restrict__ stat_max, int mode, double qg, double qsr,
-                                    double* __restrict__ qs) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ __launch_bounds__(256) void tree_begin_kernel(const unsigned int* __restrict__ stat_max, int mode,
+                                                         double qg, double qsr, double* __restrict__ qs,
+                                                         int* __restrict__ ctl0, NodeLink* __restrict__ link0,
+                                                         unsigned long long* __restrict__ leaf_acc, int leaf_n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < leaf_n; i += gridDim.x * blockDim.x) leaf_acc[i] = 0ull;
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
   const double gmax = fmax((double)__uint_as_float(stat_max[0]), 1e-30);
   const double hmax = fmax((double)__uint_as_float(stat_max[1]), 1e-30);
   const double wmax = fmax((double)__uint_as_float(stat_max[2]), 1e-30);
@@ -924,10 +959,15 @@ __global__ void quant_scales_kernel(const unsigned int* __restrict__ stat_max, i
   const double sg = exp2(floor(log2(fmin(qg, (double)QG) / gmax)));
   const double ss = exp2(floor(log2(fmin(qsr, (double)QS) / smax)));
   qs[0] = sg; qs[1] = ss; qs[2] = 1.0 / sg; qs[3] = 1.0 / ss;
-  qs[4] = exp2(floor(log2(2147483647.0 / gmax)));
-  qs[5] = exp2(floor(log2(2147483647.0 / hmax)));
-  qs[6] = exp2(floor(log2(2147483647.0 / wmax)));
+  // leaf sums: |per-row value| < 2^30 so int32 conversions suffice
+  qs[4] = exp2(floor(log2(1073741823.0 / gmax)));
+  qs[5] = exp2(floor(log2(1073741823.0 / hmax)));
+  qs[6] = exp2(floor(log2(1073741823.0 / wmax)));
   qs[7] = 0.0;
+  ctl0[CTL_N] = 1; ctl0[CTL_SLOTS] = 1; ctl0[CTL_BASE] = 0; ctl0[CTL_TOTAL] = 1;
+  NodeLink root;
+  root.slot = 0; root.sib_slot = -1; root.parent = -1; root.pad = 0;
+  link0[0] = root;
 }
 
 // Exact per-leaf (G, H, W) sums after the last partition: every row carries
@@ -949,7 +989,8 @@ __global__ __launch_bounds__(256) void leaf_stats_kernel(const int* __restrict__
     if (leaf < 0 || leaf >= cap) continue;
     const float wv = w ? w[r] : 1.0f;
     if (wv == 0.0f) continue;
-    const long long gq = llrint((double)g[r] * lg), hq = llrint((double)h[r] * lh), wq = llrint((double)wv * lw);
+    const long long gq = __float2int_rn(g[r] * (float)lg), hq = __float2int_rn(h[r] * (float)lh),
+                    wq = __float2int_rn(wv * (float)lw);
     unsigned long long* dst = use_lds ? lacc + 3 * leaf : acc + 3 * leaf;
     atomicAdd(dst + 0, (unsigned long long)gq);
     atomicAdd(dst + 1, (unsigned long long)hq);
@@ -1138,12 +1179,12 @@ H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_n
   return launch_status();
 }
 
-constexpr int PARTITION_BLOCKS = 1024;
+constexpr int PARTITION_BLOCKS = 4096;
 
 H2OMX_API int h2omx_partition(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt, const float* g,
                               const float* h, const float* w, const double* qscale, int cap,
                               unsigned long long* leaf_acc, unsigned long long* leaf_slab, hipStream_t stream) {
-  if (npad % 4 != 0) return kBadArg;
+  if (npad % 8 != 0) return kBadArg;
   const int R = (leaf_acc && cap <= 2048) ? std::max(1, std::min(16, 4096 / (3 * cap))) : 1;
   const size_t lds = (leaf_acc && cap <= 2048) ? (size_t)cap * 3 * R * sizeof(unsigned long long) : 0;
   // fixed grid so the slab layout is known: [PARTITION_BLOCKS][3 * cap]
@@ -1153,7 +1194,7 @@ H2OMX_API int h2omx_partition(const uint8_t* codes, int64_t npad, int* nid, cons
   return launch_status();
 }
 
-static inline int stream_grid(int64_t n) { return grid_for(n, 256, 2048); }
+static inline int stream_grid(int64_t) { return STAT_BLOCKS; }
 
 H2OMX_API int h2omx_boost_update(float* F, const float* y, const float* wobs, int64_t n, int64_t npad, int* nid,
                                  const void* tree, const void* gparams, float* g, float* h, float* wout,
@@ -1179,12 +1220,21 @@ H2OMX_API int h2omx_softmax_grad(const float* F, int K, int64_t ldF, const int* 
   return launch_status();
 }
 
-H2OMX_API int h2omx_quant_scales(const unsigned int* stat_max, int mode, int max_rows_per_wg, double* qscale,
-                                 hipStream_t stream) {
+H2OMX_API int h2omx_stat_blocks() { return STAT_BLOCKS; }
+
+H2OMX_API int h2omx_stat_reduce(const unsigned int* slab, unsigned int* stat_max, hipStream_t stream) {
+  hipLaunchKernelGGL(stat_reduce_kernel, dim3(1), dim3(1024), 0, stream, slab, STAT_BLOCKS, stat_max);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_tree_begin(const unsigned int* stat_max, int mode, int max_rows_per_wg, double* qscale,
+                               int* ctl0, void* link0, unsigned long long* leaf_acc, int leaf_n,
+                               hipStream_t stream) {
   if (max_rows_per_wg < 1 || max_rows_per_wg > ROWS_CAP) return kBadArg;
   const double qg = exp2(floor(log2(1073741824.0 / max_rows_per_wg)));   // |sum| <= 2^30
   const double qsr = exp2(floor(log2(2147483648.0 / max_rows_per_wg)));  // sum <= 2^31
-  hipLaunchKernelGGL(quant_scales_kernel, dim3(1), dim3(64), 0, stream, stat_max, mode, qg, qsr, qscale);
+  hipLaunchKernelGGL(tree_begin_kernel, dim3(grid_for(leaf_n, 256, 1024)), dim3(256), 0, stream, stat_max, mode, qg,
+                     qsr, qscale, ctl0, reinterpret_cast<NodeLink*>(link0), leaf_acc, leaf_n);
   return launch_status();
 }
 

@@ -105,7 +105,7 @@ def bin_matrix(X: torch.Tensor, edges: np.ndarray, nvb: np.ndarray, nbt: int, na
     if X.is_cuda:
         Xc = X.float().contiguous()
         codes = torch.empty((F, npad), dtype=torch.uint8, device=dev)
-        lib = ops.tree()
+        lib = ops.tree_lib()
         ops.check(lib.h2omx_bin_features(ops.P(Xc), Xc.stride(0), n, F, ops.P(e_t), ops.P(nv_t), nbt,
                                          ops.P(codes), npad, ops.stream(dev)), "bin_features")
     else:

@@ -68,7 +68,7 @@ class TreeEnsemble:
             out.copy_(torch.from_numpy(np.repeat(self.init_f.astype(np.float32)[:, None], n, 1)).to(dev)
                       if not self.average else torch.zeros_like(out))
             if T:
-                lib = ops.tree()
+                lib = ops.tree_lib()
                 ops.check(lib.h2omx_predict_raw(ops.P(Xc), Xc.stride(0), n, ops.P(nodes), ops.P(roots), T, self.K,
                                                 ops.P(out), out.stride(0), ops.stream(dev)), "predict_raw")
             if self.average and nt > 0:
@@ -187,7 +187,7 @@ class GpuBooster:
     """Step-wise GPU boosting loop (one ``step()`` = one iteration = K trees)."""
 
     def __init__(self, bm, y_np, w_np, ens, tp, sample_rate, seed, comm, dist_kw, ntrees_hint=64):
-        self.lib = ops.tree()
+        self.lib = ops.tree_lib()
         self.bm, self.ens, self.tp = bm, ens, tp
         self.sample_rate, self.seed = sample_rate, seed
         self.dev = bm.device
@@ -209,10 +209,10 @@ class GpuBooster:
         P, st, b = ops.P, self.st, self.builder
         gp = make_grad_params(dist or self.dist, apply, self.sample_rate, self.seed, next_tree, **self.kw)
         y = st.ycls[k] if (self.dist == "drf" and self.K > 1) else st.y
-        b.stat_max.zero_()
         ops.check(self.lib.h2omx_boost_update(P(st.Fm[k]), P(y), P(st.w), self.bm.n, self.bm.npad, P(b.nid),
                                               P(b.tree_buf), ctypes.addressof(gp), P(st.g[k]), P(st.h[k]),
-                                              P(self.wout), P(b.stat_max), ops.stream(self.dev)), "boost_update")
+                                              P(self.wout), P(b.stat_slab), ops.stream(self.dev)), "boost_update")
+        b.reduce_stats()
 
     def step(self):
         P, st, b, bm, t = ops.P, self.st, self.builder, self.bm, self.t
@@ -231,11 +231,11 @@ class GpuBooster:
                 if self.dist == "drf":
                     self._update(apply=False, next_tree=t, k=k)
                 else:
-                    b.stat_max.zero_()
                     ops.check(self.lib.h2omx_softmax_grad(P(st.Fm), self.K, st.Fm.stride(0), P(st.yk), P(st.w),
                                                           bm.n, bm.npad, k, ctypes.addressof(gp), P(b.nid),
-                                                          P(st.g[k]), P(st.h[k]), P(self.wout), P(b.stat_max), s),
+                                                          P(st.g[k]), P(st.h[k]), P(self.wout), P(b.stat_slab), s),
                                   "softmax_grad")
+                    b.reduce_stats()
                 maxes.append(b.stat_max.clone())
             for k in range(self.K):
                 b.nid[: bm.n].zero_()

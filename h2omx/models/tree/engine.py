@@ -75,7 +75,7 @@ class HipTreeBuilder:
     def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
         if not bm.codes.is_cuda:
             raise ValueError("HipTreeBuilder needs device-resident codes")
-        self.lib = ops.tree()
+        self.lib = ops.tree_lib()
         check_layout(self.lib)
         self.bm = bm
         self.p = params
@@ -95,6 +95,7 @@ class HipTreeBuilder:
         self.tree_buf = torch.zeros((self.capacity * TREE_NODE_DTYPE.itemsize,), dtype=torch.uint8, device=d)
         self.nid = torch.full((bm.npad,), -1, dtype=torch.int32, device=d)
         self.stat_max = torch.zeros((4,), dtype=torch.int32, device=d)   # float bits of max|g|, max h, max w
+        self.stat_slab = torch.zeros((int(self.lib.h2omx_stat_blocks()) * 4,), dtype=torch.int32, device=d)
         self.qscale = torch.zeros((8,), dtype=torch.float64, device=d)
         self.leaf_acc = torch.zeros((self.capacity * 3,), dtype=torch.int64, device=d)
         self.part_blocks = int(self.lib.h2omx_partition_blocks())
@@ -174,7 +175,8 @@ class HipTreeBuilder:
         the boost / softmax kernels): ``self.nid`` is 0 for rows of the tree and
         INT_MIN for padding; ``self.stat_max`` holds this tree's maxima.
         Returns the device tree buffer (``TREE_NODE_DTYPE`` heap of capacity
-        nodes; unreachable records are garbage)."""
+        nodes; unreachable records are garbage).  ``self.stat_max`` must hold
+        this tree's gradient maxima (see :meth:`reduce_stats`)."""
         lib, bm, p = self.lib, self.bm, self.p
         st = ops.stream(self.dev)
         P = ops.P
@@ -185,14 +187,12 @@ class HipTreeBuilder:
 
         if comm is not None:
             comm.all_reduce_(self.stat_max, "max")
-        ops.check(lib.h2omx_quant_scales(P(self.stat_max), p.mode, self.max_rows_per_wg, P(self.qscale), st),
-                  "quant_scales")
         s2 = w if p.mode == 0 else h
-
-        self.leaf_acc.zero_()
-        self.ctl[0].copy_(self.ctl_init)
         link = [self._buf("link0", 4, torch.int32), None]
-        link[0][:4].copy_(self.link_init)
+        # scales + level-0 control block/link + zeroed leaf sums in one launch
+        ops.check(lib.h2omx_tree_begin(P(self.stat_max), p.mode, self.max_rows_per_wg, P(self.qscale),
+                                       P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(), st),
+                  "tree_begin")
         full_prev = None
         max_depth = p.max_depth
         max_nodes = 1
@@ -260,6 +260,11 @@ class HipTreeBuilder:
         ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(self.ctl[max_depth % 2]), P(self.qscale), spp,
                                           P(self.tree_buf), self.capacity, st), "leaf_finalize")
         return self.tree_buf
+
+    def reduce_stats(self) -> None:
+        """Fold the per-block maxima written by the gradient kernels into stat_max."""
+        ops.check(self.lib.h2omx_stat_reduce(ops.P(self.stat_slab), ops.P(self.stat_max), ops.stream(self.dev)),
+                  "stat_reduce")
 
     def tree_size(self) -> torch.Tensor:
         """Device scalar with the node count of the last tree (ctl TOTAL)."""

@@ -28,7 +28,9 @@ TREE_SIGS = {
     "h2omx_boost_update": "PPPLLPPPPPPPS",
     "h2omx_apply_tree": "PLPPS",
     "h2omx_softmax_grad": "PILPPLLIPPPPPPS",
-    "h2omx_quant_scales": "PIIPS",
+    "h2omx_stat_blocks": "",
+    "h2omx_stat_reduce": "PPS",
+    "h2omx_tree_begin": "PIIPPPPIS",
     "h2omx_leaf_stats": "PPPPLPIPS",
     "h2omx_leaf_finalize": "PPPPPIS",
     "h2omx_predict_raw": "PLLPPIIPLS",
@@ -36,14 +38,13 @@ TREE_SIGS = {
 }
 
 DENSE_SIGS = {
-    "h2omx_gram": "PLLIPPPIS",
-    "h2omx_glm_irls": "PLLIPPPPIDPPPPS",
-    "h2omx_kmeans_assign": "PLLIPIPPPS",
-    "h2omx_kmeans_update": "PLLIPPIPPS",
-    "h2omx_gemm_bias_act": "PPPPIIIIIS",
-    "h2omx_gemm_nt": "PPPIIIIS",
-    "h2omx_gemm_tn": "PPPIIIIS",
-    "h2omx_act_backward": "PPPIIS",
+    "h2omx_dense_sizes": "P",
+    "h2omx_glm_irls": "PLLPPPPPPIIPPS",
+    "h2omx_slab_reduce_upper": "PIIPS",
+    "h2omx_slab_sum": "PIIPS",
+    "h2omx_kmeans": "PLLIPPIIPPS",
+    "h2omx_gemm": "PPPPIIIIIIFS",
+    "h2omx_act_backward": "PPLIS",
     "h2omx_bias_grad": "PPIIS",
     "h2omx_softmax_xent": "PPPPIIS",
     "h2omx_adadelta": "PPPPLFFFS",
@@ -73,15 +74,15 @@ def _bind(name: str, sigs: dict[str, str]) -> ctypes.CDLL:
     return lib
 
 
-def tree() -> ctypes.CDLL:
+def tree_lib() -> ctypes.CDLL:
     return _bind("tree", TREE_SIGS)
 
 
-def dense() -> ctypes.CDLL:
+def dense_lib() -> ctypes.CDLL:
     return _bind("dense", DENSE_SIGS)
 
 
-def metrics() -> ctypes.CDLL:
+def metrics_lib() -> ctypes.CDLL:
     return _bind("metrics", METRICS_SIGS)
 
 

@@ -1,0 +1,279 @@
+"""Python entry points of csrc/dense_kernels.hip (GLM IRLS Gram, K-Means,
+MLP GEMM + elementwise) with their CPU reference implementations.
+
+Every function takes tensors on one device.  On a GPU tensor the HIP kernel
+is the only implementation (``ops.dense_lib()`` raises if the library is
+missing); on CPU tensors the NumPy/PyTorch reference runs (test oracle and
+the CPU plumbing path).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import P, check, dense_lib, stream
+
+FAMILIES = {"gaussian": 0, "binomial": 1, "poisson": 2, "gamma": 3, "tweedie": 4, "multinomial": 5,
+            "quasibinomial": 6}
+LINKS = {"identity": 0, "logit": 1, "log": 2, "inverse": 3, "tweedie": 4}
+DEFAULT_LINK = {"gaussian": "identity", "binomial": "logit", "quasibinomial": "logit", "poisson": "log",
+                "gamma": "inverse", "tweedie": "tweedie", "multinomial": "logit"}
+
+
+class GlmParams(ctypes.Structure):
+    _fields_ = [("family", ctypes.c_int), ("link", ctypes.c_int), ("p", ctypes.c_int), ("K", ctypes.c_int),
+                ("cls", ctypes.c_int), ("pad", ctypes.c_int), ("var_power", ctypes.c_double),
+                ("link_power", ctypes.c_double)]
+
+
+def _tp_for(p: int) -> int:
+    for tp in (1, 2, 4, 8):
+        if p + 2 <= 32 * tp:
+            return tp
+    raise ValueError(f"GLM with {p} predictors exceeds the 254-column Gram kernel; reduce predictors")
+
+
+def glm_irls_pass(X: torch.Tensor, y: torch.Tensor, wprior, offset, beta: np.ndarray, family: str, link: str,
+                  cls: int = 0, var_power: float = 1.5, link_power: float = 0.0):
+    """One IRLS pass.  X: feature-major standardized float32 [p][n] (no NA).
+    beta: float64 [K][p+1] (coefficients then intercept).
+    Returns (G float64 [p+2][p+2] of the augmented [x | 1 | z] weighted Gram, deviance)."""
+    p, n = X.shape
+    K = beta.shape[0]
+    if X.is_cuda:
+        lib = dense_lib()
+        dev = X.device
+        tp = _tp_for(p)
+        PP = 32 * tp
+        n_wg = max(1, min(512, math.ceil(n / 4096)))
+        slab = torch.empty((n_wg * PP * PP,), dtype=torch.float32, device=dev)
+        devs = torch.empty((n_wg,), dtype=torch.float64, device=dev)
+        out = torch.empty((PP * PP,), dtype=torch.float64, device=dev)
+        b32 = torch.from_numpy(np.ascontiguousarray(beta, np.float32)).to(dev)
+        means = torch.zeros((max(p, 1),), dtype=torch.float32, device=dev)
+        gp = GlmParams(FAMILIES[family], LINKS[link], p, K, cls, 0, var_power, link_power)
+        Xc = X.contiguous()
+        st = stream(dev)
+        check(lib.h2omx_glm_irls(P(Xc), Xc.stride(0), n, P(y), P(wprior), P(offset), P(means), P(b32),
+                                 ctypes.addressof(gp), n_wg, tp, P(slab), P(devs), st), "glm_irls")
+        check(lib.h2omx_slab_reduce_upper(P(slab), n_wg, PP * PP, P(out), st), "slab_reduce_upper")
+        G = out.view(PP, PP)[: p + 2, : p + 2].cpu().numpy()
+        G = np.triu(G) + np.triu(G, 1).T
+        return G, float(devs.sum().item())
+    return _irls_pass_ref(X, y, wprior, offset, beta, family, link, cls, var_power, link_power)
+
+
+def _linkinv(eta, link, link_power=0.0):
+    if link == "logit":
+        return 1 / (1 + np.exp(-eta)), None
+    if link == "log":
+        mu = np.exp(np.minimum(eta, 700))
+        return mu, mu
+    if link == "inverse":
+        e = np.where(np.abs(eta) < 1e-10, np.copysign(1e-10, eta), eta)
+        mu = 1 / e
+        return mu, -mu * mu
+    if link == "tweedie":
+        if link_power == 0:
+            mu = np.exp(np.minimum(eta, 700))
+            return mu, mu
+        e = np.maximum(eta, 1e-10)
+        mu = e ** (1 / link_power)
+        return mu, mu / (link_power * e)
+    return eta, np.ones_like(eta)
+
+
+def glm_variance(family, mu, var_power=1.5):
+    if family in ("binomial", "quasibinomial"):
+        return np.maximum(mu * (1 - mu), 1e-10)
+    if family == "poisson":
+        return np.maximum(mu, 1e-10)
+    if family == "gamma":
+        return np.maximum(mu * mu, 1e-20)
+    if family == "tweedie":
+        return np.maximum(np.maximum(mu, 1e-10) ** var_power, 1e-20)
+    return np.ones_like(mu)
+
+
+def glm_deviance(family, y, mu, var_power=1.5):
+    if family in ("binomial", "quasibinomial"):
+        m = np.clip(mu, 1e-15, 1 - 1e-15)
+        return -2 * (y * np.log(m) + (1 - y) * np.log(1 - m))
+    if family == "poisson":
+        m = np.maximum(mu, 1e-15)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            t = np.where(y > 0, y * np.log(np.where(y > 0, y, 1) / m), 0.0)
+        return 2 * (t - (y - m))
+    if family == "gamma":
+        m = np.maximum(mu, 1e-15)
+        return 2 * (-np.log(np.maximum(y, 1e-15) / m) + (y - m) / m)
+    if family == "tweedie":
+        r = var_power
+        m = np.maximum(mu, 1e-15)
+        a = np.where(y > 0, np.maximum(y, 0) ** (2 - r) / ((1 - r) * (2 - r)), 0.0)
+        return 2 * (a - y * m ** (1 - r) / (1 - r) + m ** (2 - r) / (2 - r))
+    return (y - mu) ** 2
+
+
+def _irls_pass_ref(X, y, wprior, offset, beta, family, link, cls, var_power, link_power):
+    Xn = X.double().numpy()
+    p, n = Xn.shape
+    yv = y.double().numpy()
+    wp = np.ones(n) if wprior is None else wprior.double().numpy()
+    off = np.zeros(n) if offset is None else offset.double().numpy()
+    if family == "multinomial":
+        etas = beta[:, :p] @ Xn + beta[:, p:p + 1]
+        etas -= etas.max(axis=0, keepdims=True)
+        pr = np.exp(etas)
+        pr /= pr.sum(axis=0, keepdims=True)
+        pk = np.clip(pr[cls], 1e-10, 1 - 1e-10)
+        yk = (yv.astype(np.int64) == cls).astype(np.float64)
+        eta_k = beta[cls, :p] @ Xn + beta[cls, p]
+        w = pk * (1 - pk)
+        z = eta_k + (yk - pk) / w
+        w = w * wp
+        dev = float((wp * np.where(yk > 0, -2 * np.log(pk), 0.0)).sum())
+    else:
+        eta = beta[0, :p] @ Xn + beta[0, p] + off
+        mu, dmu = _linkinv(eta, link, link_power)
+        if link == "logit":
+            dmu = np.maximum(mu * (1 - mu), 1e-10)
+        elif link == "log" or (link == "tweedie" and link_power == 0):
+            dmu = np.maximum(mu, 1e-10)
+        w = wp * dmu * dmu / glm_variance(family, mu, var_power)
+        z = eta - off + (yv - mu) / dmu
+        dev = float((wp * glm_deviance(family, yv, mu, var_power)).sum())
+    A = np.vstack([Xn, np.ones((1, n)), z[None, :]])
+    sw = np.sqrt(np.maximum(w, 0))
+    As = A * sw[None, :]
+    return As @ As.T, dev
+
+
+# ---------------------------------------------------------------------------
+# K-Means
+# ---------------------------------------------------------------------------
+def kmeans_step(X: torch.Tensor, C: torch.Tensor):
+    """One Lloyd pass.  X feature-major float32 [d][n] (standardized, NA -> 0),
+    C [k][d].  Returns (assign int32 [n], sums float64 [k][d], counts [k], sse [k])."""
+    d, n = X.shape
+    k = C.shape[0]
+    if X.is_cuda:
+        lib = dense_lib()
+        dev = X.device
+        Xc = X.contiguous()
+        Cc = C.float().contiguous()
+        cn = (Cc.double() ** 2).sum(1).float()
+        n_wg = max(1, min(1024, math.ceil(n / 4096)))
+        width = k * d + 2 * k
+        slab = torch.empty((n_wg * width,), dtype=torch.float32, device=dev)
+        out = torch.empty((width,), dtype=torch.float64, device=dev)
+        assign = torch.empty((n,), dtype=torch.int32, device=dev)
+        st = stream(dev)
+        rc = lib.h2omx_kmeans(P(Xc), Xc.stride(0), n, d, P(Cc), P(cn), k, n_wg, P(assign), P(slab), st)
+        if rc != 0:
+            raise ValueError(f"K-Means kernel does not support d={d}, k={k} (d<=256, k<=128 with d*k bounded)")
+        check(lib.h2omx_slab_sum(P(slab), n_wg, width, P(out), st), "slab_sum")
+        o = out.cpu().numpy()
+        return assign, o[: k * d].reshape(k, d), o[k * d: k * d + k], o[k * d + k:]
+    Xn = X.double().numpy()
+    Cn = C.double().numpy()
+    d2 = (Cn ** 2).sum(1)[:, None] - 2 * Cn @ Xn
+    a = np.argmin(d2, axis=0)
+    x2 = (Xn ** 2).sum(0)
+    sums = np.zeros((k, d))
+    np.add.at(sums, a, Xn.T)
+    counts = np.bincount(a, minlength=k).astype(np.float64)
+    sse = np.bincount(a, weights=np.maximum(d2[a, np.arange(n)] + x2, 0), minlength=k)
+    return torch.from_numpy(a.astype(np.int32)), sums, counts, sse
+
+
+# ---------------------------------------------------------------------------
+# MLP building blocks
+# ---------------------------------------------------------------------------
+ACTS = {"linear": 0, "none": 0, "rectifier": 1, "relu": 1, "tanh": 2, "maxout": 3}
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = False, tb: bool = False,
+         out: torch.Tensor | None = None, beta_c: float = 0.0) -> torch.Tensor:
+    """C = act(op(A) op(B) + bias) with row-major fp32 operands."""
+    M = A.shape[1] if ta else A.shape[0]
+    K = A.shape[0] if ta else A.shape[1]
+    N = B.shape[0] if tb else B.shape[1]
+    if A.is_cuda:
+        C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=A.device)
+        check(dense_lib().h2omx_gemm(P(A), P(B), P(C), P(bias), M, N, K, int(ta), int(tb), act, beta_c,
+                                 stream(A.device)), "gemm")
+        return C
+    a = A.T if ta else A
+    b = B.T if tb else B
+    c = a.float() @ b.float()
+    if beta_c and out is not None:
+        c = c + beta_c * out
+    if bias is not None:
+        c = c + bias
+    if act in (1, 3):
+        c = torch.relu(c)
+    elif act == 2:
+        c = torch.tanh(c)
+    if out is not None:
+        out.copy_(c)
+        return out
+    return c
+
+
+def act_backward(Y: torch.Tensor, dY: torch.Tensor, act: int) -> torch.Tensor:
+    if act == 0:
+        return dY
+    if Y.is_cuda:
+        check(dense_lib().h2omx_act_backward(P(Y), P(dY), Y.numel(), act, stream(Y.device)), "act_backward")
+        return dY
+    if act in (1, 3):
+        dY.mul_((Y > 0).float())
+    elif act == 2:
+        dY.mul_(1 - Y * Y)
+    return dY
+
+
+def bias_grad(dY: torch.Tensor) -> torch.Tensor:
+    M, N = dY.shape
+    if dY.is_cuda:
+        db = torch.empty((N,), dtype=torch.float32, device=dY.device)
+        check(dense_lib().h2omx_bias_grad(P(dY), P(db), M, N, stream(dY.device)), "bias_grad")
+        return db
+    return dY.sum(0)
+
+
+def softmax_xent(Z: torch.Tensor, y: torch.Tensor):
+    M, K = Z.shape
+    if Z.is_cuda:
+        dZ = torch.empty_like(Z)
+        loss = torch.zeros((1,), dtype=torch.float32, device=Z.device)
+        check(dense_lib().h2omx_softmax_xent(P(Z), P(y), P(dZ), P(loss), M, K, stream(Z.device)), "softmax_xent")
+        return dZ, loss
+    pr = torch.softmax(Z, 1)
+    oh = torch.nn.functional.one_hot(y.long(), K).float()
+    loss = -(torch.log(pr.clamp_min(1e-30)) * oh).sum(1).mean()
+    return (pr - oh) / M, loss.reshape(1)
+
+
+def adadelta_(W, G, Eg2, Edx2, rho=0.99, eps=1e-8, l2=0.0):
+    if W.is_cuda:
+        check(dense_lib().h2omx_adadelta(P(W), P(G), P(Eg2), P(Edx2), W.numel(), rho, eps, l2, stream(W.device)),
+              "adadelta")
+        return
+    g = G + l2 * W
+    Eg2.mul_(rho).add_((1 - rho) * g * g)
+    dx = -torch.sqrt(Edx2 + eps) / torch.sqrt(Eg2 + eps) * g
+    Edx2.mul_(rho).add_((1 - rho) * dx * dx)
+    W.add_(dx)
+
+
+def sgd_momentum_(W, G, V, lr, mom, l2=0.0):
+    if W.is_cuda:
+        check(dense_lib().h2omx_sgd_momentum(P(W), P(G), P(V), W.numel(), lr, mom, l2, stream(W.device)), "sgd")
+        return
+    V.mul_(mom).sub_(lr * (G + l2 * W))
+    W.add_(V)

@@ -1,0 +1,91 @@
+"""HIP dense kernels (fp32 MFMA) vs fp64/fp32 PyTorch references."""
+import numpy as np
+import pytest
+import torch
+
+from h2omx.ops import dense as D
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("p,family,link", [(5, "binomial", "logit"), (30, "gaussian", "identity"),
+                                           (61, "poisson", "log"), (100, "binomial", "logit")])
+def test_glm_irls_gram_matches_reference(cuda_dev, p, family, link):
+    rng = np.random.default_rng(p)
+    n = 20_011
+    X = rng.normal(size=(p, n)).astype(np.float32)
+    beta = np.zeros((1, p + 1))
+    beta[0, :p] = rng.normal(scale=0.1, size=p)
+    beta[0, p] = 0.2
+    eta = beta[0, :p] @ X + beta[0, p]
+    if family == "binomial":
+        y = (rng.random(n) < 1 / (1 + np.exp(-eta))).astype(np.float32)
+    elif family == "poisson":
+        y = rng.poisson(np.exp(eta)).astype(np.float32)
+    else:
+        y = (eta + rng.normal(size=n)).astype(np.float32)
+    w = rng.uniform(0.5, 2.0, n).astype(np.float32)
+    Xt, yt, wt = torch.from_numpy(X), torch.from_numpy(y), torch.from_numpy(w)
+    Gr, dr = D.glm_irls_pass(Xt, yt, wt, None, beta, family, link)
+    Gg, dg = D.glm_irls_pass(Xt.to(cuda_dev), yt.to(cuda_dev), wt.to(cuda_dev), None, beta, family, link)
+    scale = np.abs(Gr).max()
+    assert np.abs(Gg - Gr).max() / scale < 2e-5
+    assert abs(dg - dr) / abs(dr) < 1e-5
+
+
+def test_glm_multinomial_gram(cuda_dev):
+    rng = np.random.default_rng(1)
+    p, n, K = 12, 9001, 3
+    X = rng.normal(size=(p, n)).astype(np.float32)
+    y = rng.integers(0, K, n).astype(np.float32)
+    beta = rng.normal(scale=0.1, size=(K, p + 1))
+    Xt, yt = torch.from_numpy(X), torch.from_numpy(y)
+    for c in range(K):
+        Gr, dr = D.glm_irls_pass(Xt, yt, None, None, beta, "multinomial", "logit", cls=c)
+        Gg, dg = D.glm_irls_pass(Xt.to(cuda_dev), yt.to(cuda_dev), None, None, beta, "multinomial", "logit", cls=c)
+        assert np.abs(Gg - Gr).max() / np.abs(Gr).max() < 2e-5
+        assert abs(dg - dr) / abs(dr) < 1e-5
+
+
+@pytest.mark.parametrize("d,k", [(4, 3), (28, 10), (64, 40), (100, 17), (200, 8)])
+def test_kmeans_step_matches_reference(cuda_dev, d, k):
+    rng = np.random.default_rng(d)
+    n = 30_000
+    X = rng.normal(size=(d, n)).astype(np.float32)
+    C = rng.normal(size=(k, d)).astype(np.float32)
+    ar, sr, cr, er = D.kmeans_step(torch.from_numpy(X), torch.from_numpy(C))
+    ag, sg, cg, eg = D.kmeans_step(torch.from_numpy(X).to(cuda_dev), torch.from_numpy(C).to(cuda_dev))
+    agree = (ag.cpu().numpy() == ar.numpy()).mean()
+    assert agree > 0.999  # fp32 near-ties may flip
+    if agree == 1.0:
+        np.testing.assert_allclose(cg, cr)
+        np.testing.assert_allclose(sg, sr, rtol=1e-4, atol=1e-3)
+        np.testing.assert_allclose(eg, er, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb,act", [(1000, 512, 200, False, False, 1), (513, 257, 129, False, True, 2),
+                                             (200, 512, 1000, True, False, 0), (64, 64, 64, True, True, 1)])
+def test_gemm_matches_torch(cuda_dev, M, N, K, ta, tb, act):
+    torch.manual_seed(0)
+    A = torch.randn((K, M) if ta else (M, K), device=cuda_dev)
+    B = torch.randn((N, K) if tb else (K, N), device=cuda_dev)
+    bias = torch.randn(N, device=cuda_dev)
+    C = D.gemm(A, B, bias, act, ta, tb)
+    ref = D.gemm(A.cpu().double().float(), B.cpu().float(), bias.cpu(), act, ta, tb)
+    assert torch.allclose(C.cpu(), ref, rtol=1e-4, atol=1e-3)
+
+
+def test_mlp_elementwise(cuda_dev):
+    torch.manual_seed(1)
+    Z = torch.randn(300, 5, device=cuda_dev)
+    y = torch.randint(0, 5, (300,), device=cuda_dev).float()
+    dZ, loss = D.softmax_xent(Z, y)
+    dZr, lr = D.softmax_xent(Z.cpu(), y.cpu())
+    assert torch.allclose(dZ.cpu(), dZr, atol=1e-6) and abs(loss.item() - lr.item()) < 1e-5
+    W = torch.randn(1000, device=cuda_dev)
+    G = torch.randn(1000, device=cuda_dev)
+    e1, e2 = torch.zeros_like(W), torch.zeros_like(W)
+    Wc, e1c, e2c = W.cpu().clone(), e1.cpu().clone(), e2.cpu().clone()
+    D.adadelta_(W, G, e1, e2, 0.99, 1e-8, 1e-5)
+    D.adadelta_(Wc, G.cpu(), e1c, e2c, 0.99, 1e-8, 1e-5)
+    assert torch.allclose(W.cpu(), Wc, atol=1e-6)
