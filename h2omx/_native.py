@@ -49,6 +49,12 @@ def require(name: str) -> ctypes.CDLL:
         if lib is not None:
             return lib
         path = lib_path(name)
+        if not os.path.exists(path) and name in HOST_LIBS:
+            # host C++ (no GPU code): cheap to build on first use
+            from .build import build_host_lib
+
+            os.makedirs(_LIB_DIR, exist_ok=True)
+            build_host_lib(name)
         if not os.path.exists(path):
             raise NativeLibraryMissing(
                 f"{path} is missing: build the native kernels with `python -m h2omx.build` "

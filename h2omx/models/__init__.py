@@ -1,4 +1,16 @@
 """Model builders (H2O estimator API)."""
 from .base import Model, ModelBuilder, ModelCategory  # noqa: F401
+from .deeplearning import H2ODeepLearningEstimator  # noqa: F401
+from .glm import H2OGeneralizedLinearEstimator  # noqa: F401
+from .kmeans import H2OKMeansEstimator  # noqa: F401
 from .tree_models import (H2OGradientBoostingEstimator, H2ORandomForestEstimator,  # noqa: F401
                           H2OXGBoostEstimator)
+
+ESTIMATORS = {
+    "gbm": H2OGradientBoostingEstimator,
+    "xgboost": H2OXGBoostEstimator,
+    "drf": H2ORandomForestEstimator,
+    "glm": H2OGeneralizedLinearEstimator,
+    "kmeans": H2OKMeansEstimator,
+    "deeplearning": H2ODeepLearningEstimator,
+}

@@ -1,0 +1,421 @@
+"""Deep Learning (H2O DeepLearning equivalent): a feed-forward MLP trained
+with mini-batch back-propagation on the hand-written fp32 MFMA GEMM
+(csrc/dense_kernels.hip gemm_kernel, bias + activation fused into the
+epilogue), fused softmax-cross-entropy, activation-backward, bias-gradient
+and ADADELTA / momentum-SGD update kernels.
+
+Multi-GPU training is synchronous data parallel: every rank runs the same
+mini-batch schedule on its shard and the per-layer gradient buckets are
+all-reduced asynchronously as back-propagation walks down the layers (RCCL,
+one bucket per layer so the last layers' reduction overlaps the earlier
+layers' backward GEMMs).  H2O itself averages Hogwild replicas once per
+``train_samples_per_iteration``; synchronous gradient
+averaging is the MI355X-friendly equivalent and keeps replicas bit-identical.
+
+Parameters follow H2O names.  ``mini_batch_size`` = 1 (H2O's per-row
+Hogwild default) maps to a GPU mini-batch of 256 rows (fewer on small frames
+so an epoch still has >= 64 updates); any larger value is used as given.
+The non-adaptive learning rate is per row, as in H2O.  Supported: activations Rectifier / Tanh / Maxout /
+ExpRectifier (+ WithDropout variants), input / hidden dropout, L1 / L2,
+ADADELTA (``adaptive_rate``) or SGD with rate annealing and momentum ramp,
+classification (softmax), regression (quadratic / absolute / huber loss,
+standardized response) and autoencoders with ``anomaly()``.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..frame.frame import ENUM, Frame, Vec
+from ..ops import dense as D
+from .base import Model, ModelBuilder, ModelCategory
+from .glm import DesignInfo
+
+_ACT = {"rectifier": 1, "tanh": 2, "maxout": 3, "exprectifier": 4}
+
+
+def _act_code(name: str) -> tuple[int, bool]:
+    n = name.lower()
+    drop = n.endswith("withdropout")
+    if drop:
+        n = n[: -len("withdropout")]
+    if n not in _ACT:
+        raise ValueError(f"unsupported activation {name}")
+    return _ACT[n], drop
+
+
+class _Net:
+    """Flat parameter / gradient buffers with per-layer views."""
+
+    def __init__(self, sizes, act, dev, gen, scale=1.0, dist="UniformAdaptive"):
+        self.sizes = sizes
+        self.act = act
+        self.layers = []
+        shapes = []
+        for i in range(len(sizes) - 1):
+            fan_in, out = sizes[i], sizes[i + 1]
+            width = out * (2 if (act == 3 and i < len(sizes) - 2) else 1)
+            shapes.append((width, fan_in))
+        total = sum(w * f + w for w, f in shapes)
+        self.flat = torch.empty((total,), dtype=torch.float32, device=dev)
+        self.grad = torch.zeros_like(self.flat)
+        off = 0
+        init = torch.empty((total,), dtype=torch.float32)
+        for (w, f) in shapes:
+            nW = w * f
+            if dist.lower() == "uniform":
+                bound = scale
+                init[off:off + nW].uniform_(-bound, bound, generator=gen)
+            elif dist.lower() == "normal":
+                init[off:off + nW].normal_(0.0, scale, generator=gen)
+            else:  # UniformAdaptive (Glorot)
+                bound = math.sqrt(6.0 / (f + w))
+                init[off:off + nW].uniform_(-bound, bound, generator=gen)
+            init[off + nW: off + nW + w] = 0.0
+            self.layers.append((off, w, f))
+            off += nW + w
+        self.flat.copy_(init.to(dev))
+
+    def W(self, i, buf=None):
+        off, w, f = self.layers[i]
+        b = self.flat if buf is None else buf
+        return b[off: off + w * f].view(w, f)
+
+    def b(self, i, buf=None):
+        off, w, f = self.layers[i]
+        b = self.flat if buf is None else buf
+        return b[off + w * f: off + w * f + w]
+
+    def span(self, i):
+        off, w, f = self.layers[i]
+        return off, off + w * f + w
+
+
+def _forward(net: _Net, X, act, train, drop_in, drop_hid, gen_dev, out_act=0):
+    """Returns activations list [X, H1, ..., Z] and the maxout arg masks / dropout masks."""
+    Hs = [X]
+    aux = []
+    H = X
+    if train and drop_in > 0:
+        m = (torch.rand(H.shape, device=H.device, generator=gen_dev) >= drop_in).float() / (1 - drop_in)
+        H = H * m
+        Hs[0] = H
+    L = len(net.layers)
+    for i in range(L):
+        last = i == L - 1
+        W, b = net.W(i), net.b(i)
+        if last:
+            Z = D.gemm(H, W, bias=b, act=out_act, tb=True)
+            Hs.append(Z)
+            aux.append(None)
+            break
+        if act == 3:
+            Z2 = D.gemm(H, W, bias=b, act=0, tb=True)           # [M][2*out]
+            Zv = Z2.view(Z2.shape[0], -1, 2)
+            Hn, arg = Zv.max(-1)
+            aux.append(arg)
+        elif act == 4:
+            Z = D.gemm(H, W, bias=b, act=0, tb=True)
+            Hn = torch.nn.functional.elu(Z)
+            aux.append(None)
+        else:
+            Hn = D.gemm(H, W, bias=b, act=act, tb=True)
+            aux.append(None)
+        if train and drop_hid[i] > 0:
+            m = (torch.rand(Hn.shape, device=Hn.device, generator=gen_dev) >= drop_hid[i]).float() / (1 - drop_hid[i])
+            Hn = Hn * m
+            aux[-1] = (aux[-1], m)
+        else:
+            aux[-1] = (aux[-1], None)
+        Hs.append(Hn)
+        H = Hn
+    return Hs, aux
+
+
+class DeepLearningModel(Model):
+    algo = "deeplearning"
+    algo_full_name = "Deep Learning"
+
+    def __init__(self, builder, model_id, design, net, act, y_mean, y_sd, autoencoder):
+        super().__init__(builder, model_id)
+        self.design = design
+        self.net = net
+        self.act = act
+        self.y_mean, self.y_sd = y_mean, y_sd
+        self.autoencoder = autoencoder
+
+    def _rows(self, frame):
+        return self.design.transform(self.design.raw_matrix(frame)).T.contiguous()
+
+    def _score(self, X, batch=65536):
+        outs = []
+        for s in range(0, X.shape[0], batch):
+            Hs, _ = _forward(self.net, X[s:s + batch], self.act, False, 0.0, [0.0] * 16, None)
+            outs.append(Hs[-1])
+        return torch.cat(outs) if outs else torch.zeros((0, self.net.sizes[-1]), device=X.device)
+
+    def predict_raw(self, frame: Frame) -> torch.Tensor:
+        X = self._rows(frame)
+        Z = self._score(X)
+        if self.autoencoder:
+            return Z.T.contiguous()
+        if self.category in (ModelCategory.BINOMIAL, ModelCategory.MULTINOMIAL):
+            return torch.softmax(Z, 1).T.contiguous()
+        return (Z[:, 0] * self.y_sd + self.y_mean)[None, :]
+
+    def anomaly(self, frame: Frame, per_feature: bool = False) -> Frame:
+        """Reconstruction MSE per row (H2O ``anomaly``) for autoencoders."""
+        if not self.autoencoder:
+            raise ValueError("anomaly() requires an autoencoder model")
+        X = self._rows(frame)
+        R = self._score(X)
+        err = (R - X) ** 2
+        if per_feature:
+            return Frame([Vec(f"reconstr_{n}.SE", err[:, j], "real") for j, n in enumerate(self.design.names)])
+        return Frame([Vec("Reconstruction.MSE", err.mean(1), "real")])
+
+    def predict(self, frame: Frame) -> Frame:
+        if self.autoencoder:
+            R = self.predict_raw(frame)
+            return Frame([Vec(f"reconstr_{n}", R[j], "real") for j, n in enumerate(self.design.names)])
+        return super().predict(frame)
+
+    def model_performance(self, frame: Frame | None = None):
+        if self.autoencoder:
+            if frame is None:
+                return self.training_metrics
+            X = self._rows(frame)
+            return {"MSE": float(((self._score(X) - X) ** 2).mean())}
+        return super().model_performance(frame)
+
+    def varimp(self):
+        # Gedeon method (H2O's DL variable importance): input weights propagated
+        W = [self.net.W(i).detach().abs().double().cpu() for i in range(len(self.net.layers))]
+        if self.act == 3:
+            W = [w.view(-1, 2, w.shape[1]).max(1).values if i < len(W) - 1 else w for i, w in enumerate(W)]
+        imp = None
+        for w in W[::-1]:
+            r = w / w.sum(1, keepdim=True).clamp_min(1e-30)
+            imp = r if imp is None else imp @ r
+        v = imp.sum(0).numpy()
+        names = self.design.names
+        mx = v.max() if v.size and v.max() > 0 else 1.0
+        order = np.argsort(-v)
+        tot = v.sum() if v.sum() > 0 else 1.0
+        return [(names[j], float(v[j]), float(v[j] / mx), float(v[j] / tot)) for j in order]
+
+    def summary(self):
+        rows = [{"layer": 1, "units": self.net.sizes[0], "type": "Input"}]
+        for i in range(1, len(self.net.sizes)):
+            last = i == len(self.net.sizes) - 1
+            rows.append({"layer": i + 1, "units": self.net.sizes[i],
+                         "type": ("Softmax" if self.category in (ModelCategory.BINOMIAL, ModelCategory.MULTINOMIAL)
+                                  else "Linear") if last else self.params["activation"]})
+        return {"model_id": self.model_id, "layers": rows, "parameters": int(self.net.flat.numel())}
+
+
+class H2ODeepLearningEstimator(ModelBuilder):
+    algo = "deeplearning"
+    DEFAULTS = dict(hidden=[200, 200], epochs=10.0, activation="Rectifier", loss="Automatic",
+                    input_dropout_ratio=0.0, hidden_dropout_ratios=None, l1=0.0, l2=0.0,
+                    adaptive_rate=True, rho=0.99, epsilon=1e-8, rate=0.005, rate_annealing=1e-6, rate_decay=1.0,
+                    momentum_start=0.0, momentum_ramp=1e6, momentum_stable=0.0, nesterov_accelerated_gradient=True,
+                    mini_batch_size=1, standardize=True, autoencoder=False,
+                    initial_weight_distribution="UniformAdaptive", initial_weight_scale=1.0, max_w2=float("inf"),
+                    train_samples_per_iteration=-2, score_training_samples=10000, score_each_iteration=False,
+                    stopping_rounds=5, stopping_metric="AUTO", stopping_tolerance=0.0, huber_alpha=0.9,
+                    shuffle_training_data=True, reproducible=False, categorical_encoding="AUTO",
+                    use_all_factor_levels=True, offset_column=None, balance_classes=False)
+
+    def train(self, x=None, y=None, training_frame=None, validation_frame=None, comm=None, **kw):
+        if self.params.get("autoencoder"):
+            y = None
+        return super().train(x=x, y=y, training_frame=training_frame, validation_frame=validation_frame,
+                             comm=comm, **kw)
+
+    def _fit(self, train: Frame, valid, model_id):
+        p_ = self.params
+        comm = self.comm
+        world = comm.world_size if comm is not None else 1
+        dev = train.device
+        act, act_drop = _act_code(p_["activation"])
+        auto = bool(p_["autoencoder"])
+        design = DesignInfo(self.x, self.feature_types, self.feature_domains,
+                            use_all_levels=bool(p_["use_all_factor_levels"]))
+        Xraw = design.raw_matrix(train)
+        design.fit_standardization(Xraw, bool(p_["standardize"]), comm)
+        X = design.transform(Xraw).T.contiguous()       # row-major [n][d]
+        del Xraw
+        n, d = X.shape
+        cls = self.category in (ModelCategory.BINOMIAL, ModelCategory.MULTINOMIAL)
+        y_mean, y_sd = 0.0, 1.0
+        if auto:
+            K = d
+            Y = None
+        elif cls:
+            K = len(self.response_domain)
+            Y = train.vec(self.y).data.to(torch.int32)
+            ok = Y >= 0
+            if not bool(ok.all()):
+                X, Y = X[ok], Y[ok]
+        else:
+            K = 1
+            Y = train.vec(self.y).as_float()
+            ok = ~torch.isnan(Y)
+            if not bool(ok.all()):
+                X, Y = X[ok], Y[ok]
+            st = torch.stack([Y.double().sum(), (Y.double() ** 2).sum(), torch.tensor(float(Y.numel()), device=dev,
+                                                                                     dtype=torch.float64)])
+            if comm is not None and world > 1:
+                comm.all_reduce_(st)
+            cnt = max(float(st[2]), 1.0)
+            y_mean = float(st[0]) / cnt
+            y_sd = math.sqrt(max(float(st[1]) / cnt - y_mean ** 2, 0.0)) or 1.0
+            Y = ((Y - y_mean) / y_sd).float()
+        n = X.shape[0]
+        hidden = list(p_["hidden"])
+        sizes = [d] + hidden + [K]
+        seed = self._seed()
+        gen = torch.Generator().manual_seed(seed)
+        net = _Net(sizes, act, dev, gen, float(p_["initial_weight_scale"]), str(p_["initial_weight_distribution"]))
+        if comm is not None and world > 1:
+            comm.broadcast(net.flat, 0)
+        gen_dev = torch.Generator(device=dev).manual_seed(seed + 1000003 * (comm.rank if comm else 0))
+        drop_in = float(p_["input_dropout_ratio"] or 0.0)
+        hd = p_["hidden_dropout_ratios"]
+        if hd is None:
+            hd = [0.5 if act_drop else 0.0] * len(hidden)
+        hd = list(hd) + [0.0] * 16
+        mb = int(p_["mini_batch_size"])
+        # per-row Hogwild (H2O default) -> GPU mini-batches; small frames keep
+        # >= 64 updates per epoch
+        M = (256 if n >= 256 * 64 else max(16, n // 64)) if mb <= 1 else mb
+        # every rank runs the same number of steps (synchronous allreduce)
+        n_min = n
+        if comm is not None and world > 1:
+            n_min = int(-comm.max_scalar(-float(n)))
+        epochs = float(p_["epochs"])
+        steps_per_epoch = max(1, n_min // M)
+        total_steps = max(1, int(round(epochs * steps_per_epoch)))
+        adaptive = bool(p_["adaptive_rate"])
+        Eg2 = torch.zeros_like(net.flat)
+        Edx2 = torch.zeros_like(net.flat)
+        V = torch.zeros_like(net.flat)
+        l1, l2 = float(p_["l1"]), float(p_["l2"])
+        loss_kind = str(p_["loss"]).lower()
+        model = DeepLearningModel(self, model_id, design, net, act, y_mean, y_sd, auto)
+        history = []
+        perm = None
+        best, since_best = float("inf"), 0
+        samples = 0
+        score_every = max(1, steps_per_epoch)
+        for step in range(total_steps):
+            e_pos = step % steps_per_epoch
+            if e_pos == 0:
+                perm = (torch.randperm(n, generator=gen).to(dev) if p_["shuffle_training_data"]
+                        else torch.arange(n, device=dev))
+            idx = perm[e_pos * M:(e_pos + 1) * M]
+            xb = X.index_select(0, idx)
+            Hs, aux = _forward(net, xb, act, True, drop_in, hd, gen_dev)
+            Z = Hs[-1]
+            if auto:
+                dZ = (Z - xb) * (2.0 / Z.numel())
+            elif cls:
+                dZ, _ = D.softmax_xent(Z, Y.index_select(0, idx))
+            else:
+                r = Z[:, 0] - Y.index_select(0, idx)
+                if loss_kind == "absolute":
+                    g = torch.sign(r)
+                elif loss_kind == "huber":
+                    delta = float(p_["huber_alpha"])
+                    g = torch.clamp(r, -delta, delta)
+                else:
+                    g = r
+                dZ = (g / r.numel())[:, None].contiguous()
+            self._backward(net, Hs, aux, dZ, act, comm, world)
+            samples += M * world
+            if adaptive:
+                D.adadelta_(net.flat, net.grad, Eg2, Edx2, float(p_["rho"]), float(p_["epsilon"]), l2)
+            else:
+                # H2O's rate is per row: a mean-gradient step over M rows takes M of them
+                lr = M * float(p_["rate"]) / (1.0 + float(p_["rate_annealing"]) * samples)
+                ramp = min(1.0, samples / max(float(p_["momentum_ramp"]), 1.0))
+                mom = float(p_["momentum_start"]) + (float(p_["momentum_stable"]) - float(p_["momentum_start"])) * ramp
+                D.sgd_momentum_(net.flat, net.grad, V, lr, mom, l2)
+            if l1 > 0:
+                net.flat.sub_(l1 * torch.sign(net.flat) * (1.0 if adaptive else float(p_["rate"])))
+            if math.isfinite(float(p_["max_w2"])):
+                self._clip_w2(net, float(p_["max_w2"]))
+            if (step + 1) % score_every == 0 or step == total_steps - 1:
+                ent = self._score_entry(model, X, Y, cls, auto, (step + 1) / steps_per_epoch, samples, comm)
+                history.append(ent)
+                metric = ent["training_loss"]
+                sr = int(p_["stopping_rounds"] or 0)
+                if sr > 0:
+                    if metric < best * (1 - float(p_["stopping_tolerance"])):
+                        best, since_best = metric, 0
+                    else:
+                        since_best += 1
+                        if since_best >= sr:
+                            break
+        model.scoring_history = history
+        if auto:
+            model.training_metrics = {"MSE": history[-1]["training_loss"] if history else float("nan")}
+        return model
+
+    def _backward(self, net, Hs, aux, dZ, act, comm, world):
+        L = len(net.layers)
+        handles = []
+        for i in range(L - 1, -1, -1):
+            Hin = Hs[i]
+            W = net.W(i)
+            D.gemm(dZ, Hin, ta=True, out=net.W(i, net.grad))          # dW = dZ^T H
+            net.b(i, net.grad).copy_(D.bias_grad(dZ))
+            if comm is not None and world > 1:
+                a, b = net.span(i)
+                handles.append(comm.all_reduce_async(net.grad[a:b]))
+            if i == 0:
+                break
+            dH = D.gemm(dZ, W)                                            # [M][in]
+            arg, mask = aux[i - 1]
+            if mask is not None:
+                dH = dH * mask
+            if act == 3:
+                g2 = torch.zeros((dH.shape[0], dH.shape[1], 2), device=dH.device)
+                g2.scatter_(2, arg[..., None], dH[..., None])
+                dZ = g2.view(dH.shape[0], -1)
+            elif act == 4:
+                Hn = Hs[i]
+                dZ = dH * torch.where(Hn > 0, torch.ones_like(Hn), Hn + 1.0)
+            else:
+                dZ = D.act_backward(Hs[i] if mask is None else Hs[i] / mask.clamp_min(1e-30) * (mask > 0), dH, act)
+        for h in handles:
+            h.wait()
+        if comm is not None and world > 1:
+            net.grad.div_(world)
+
+    @staticmethod
+    def _clip_w2(net, max_w2):
+        for i in range(len(net.layers)):
+            W = net.W(i)
+            s = (W * W).sum(1, keepdim=True)
+            W.mul_(torch.where(s > max_w2, torch.sqrt(max_w2 / s), torch.ones_like(s)))
+
+    def _score_entry(self, model, X, Y, cls, auto, epoch, samples, comm):
+        ns = int(self.params["score_training_samples"] or 0)
+        xs = X if ns <= 0 or ns >= X.shape[0] else X[:ns]
+        Z = model._score(xs)
+        if auto:
+            loss = float(((Z - xs) ** 2).mean())
+        elif cls:
+            ys = Y[: xs.shape[0]].long()
+            loss = float(torch.nn.functional.cross_entropy(Z, ys))
+        else:
+            ys = Y[: xs.shape[0]]
+            loss = float(((Z[:, 0] - ys) ** 2).mean()) * model.y_sd ** 2
+        if comm is not None and comm.world_size > 1:
+            loss = float(comm.all_reduce_numpy(np.array([loss]))[0]) / comm.world_size
+        return {"epochs": epoch, "samples": samples, "training_loss": loss,
+                ("training_logloss" if cls else "training_mse"): loss}

@@ -16,6 +16,8 @@ import torch
 
 from . import P, check, dense_lib, stream
 
+KBADARG = 1  # common.h kBadArg
+
 FAMILIES = {"gaussian": 0, "binomial": 1, "poisson": 2, "gamma": 3, "tweedie": 4, "multinomial": 5,
             "quasibinomial": 6}
 LINKS = {"identity": 0, "logit": 1, "log": 2, "inverse": 3, "tweedie": 4}
@@ -173,8 +175,9 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor):
         assign = torch.empty((n,), dtype=torch.int32, device=dev)
         st = stream(dev)
         rc = lib.h2omx_kmeans(P(Xc), Xc.stride(0), n, d, P(Cc), P(cn), k, n_wg, P(assign), P(slab), st)
-        if rc != 0:
-            raise ValueError(f"K-Means kernel does not support d={d}, k={k} (d<=256, k<=128 with d*k bounded)")
+        if rc == KBADARG:
+            return _kmeans_large(Xc, Cc)
+        check(rc, "kmeans")
         check(lib.h2omx_slab_sum(P(slab), n_wg, width, P(out), st), "slab_sum")
         o = out.cpu().numpy()
         return assign, o[: k * d].reshape(k, d), o[k * d: k * d + k], o[k * d + k:]
@@ -188,6 +191,29 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor):
     counts = np.bincount(a, minlength=k).astype(np.float64)
     sse = np.bincount(a, weights=np.maximum(d2[a, np.arange(n)] + x2, 0), minlength=k)
     return torch.from_numpy(a.astype(np.int32)), sums, counts, sse
+
+
+def _kmeans_large(X: torch.Tensor, C: torch.Tensor):
+    """Shapes beyond the fused kernel's LDS tiles (d > 256 or large k): the
+    distance GEMM goes to hipBLASLt through torch, in row chunks."""
+    d, n = X.shape
+    k = C.shape[0]
+    cn = (C.double() ** 2).sum(1)
+    assign = torch.empty((n,), dtype=torch.int32, device=X.device)
+    sums = torch.zeros((k, d), dtype=torch.float64, device=X.device)
+    counts = torch.zeros((k,), dtype=torch.float64, device=X.device)
+    sse = torch.zeros((k,), dtype=torch.float64, device=X.device)
+    step = max(1, (1 << 26) // max(k, 1))
+    for s in range(0, n, step):
+        xb = X[:, s:s + step]
+        d2 = cn[:, None] - 2 * (C @ xb).double()
+        m, a = d2.min(0)
+        assign[s:s + step] = a.to(torch.int32)
+        x2 = (xb.double() ** 2).sum(0)
+        counts += torch.bincount(a, minlength=k).double()
+        sse += torch.bincount(a, weights=(m + x2).clamp_min(0), minlength=k)
+        sums.index_add_(0, a, xb.T.double())
+    return assign, sums.cpu().numpy(), counts.cpu().numpy(), sse.cpu().numpy()
 
 
 # ---------------------------------------------------------------------------

@@ -66,6 +66,19 @@ class Comm:
         dist.all_reduce(t, op=rop, group=self.group)
         return t
 
+    def all_reduce_async(self, t: torch.Tensor, op: str = "sum"):
+        """Non-blocking all-reduce; returns a handle with ``wait()`` (gradient
+        buckets overlapped with the rest of back-propagation)."""
+        if self.world_size == 1:
+            return _Done()
+        self.stats["all_reduce_calls"] += 1
+        self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        return dist.all_reduce(t, op=rop, group=self.group, async_op=True)
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        return self.broadcast_(t, src)
+
     def all_reduce_numpy(self, a: np.ndarray, op: str = "sum") -> np.ndarray:
         if self.world_size == 1:
             return a
@@ -121,6 +134,11 @@ class Comm:
     def shutdown(self) -> None:
         if self.world_size > 1 and dist.is_initialized():
             dist.destroy_process_group()
+
+
+class _Done:
+    def wait(self):
+        return True
 
 
 class Timer:
