@@ -1,0 +1,231 @@
+"""AutoML (H2O AutoML equivalent): trains a fixed sequence of algorithm
+presets, then random-grid GBM models, under a model-count / runtime budget,
+cross-validates every model with shared folds, and finishes with two
+Stacked Ensembles (all models, best of family).  Models are ranked on a
+leaderboard by the H2O default metric for the problem type.
+
+Every model is data-parallel over all ranks of the cluster (the row shards
+stay where they are and each model's collectives run over RCCL), so AutoML
+on 8 MI355X trains each model 8-way parallel in sequence.
+"""
+from __future__ import annotations
+
+import time
+import uuid
+
+import numpy as np
+
+from .frame.frame import DKV, Frame
+from .models import (H2ODeepLearningEstimator, H2OGeneralizedLinearEstimator, H2OGradientBoostingEstimator,
+                     H2ORandomForestEstimator, H2OXGBoostEstimator)
+from .models.base import ModelCategory
+from .models.ensemble import H2OStackedEnsembleEstimator
+
+ALGOS = ("GLM", "DRF", "GBM", "XGBoost", "DeepLearning", "StackedEnsemble")
+
+# (algo, id suffix, estimator class, params) in H2O's default training order
+PRESETS = [
+    ("XGBoost", "1", H2OXGBoostEstimator, dict(max_depth=10, min_child_weight=5, sample_rate=0.6,
+                                                col_sample_rate=0.8, col_sample_rate_per_tree=0.8)),
+    ("GLM", "1", H2OGeneralizedLinearEstimator, dict(lambda_search=True)),
+    ("DRF", "1", H2ORandomForestEstimator, dict()),
+    ("GBM", "1", H2OGradientBoostingEstimator, dict(max_depth=6, min_rows=1, sample_rate=0.8, col_sample_rate=0.8,
+                                                     col_sample_rate_per_tree=0.8)),
+    ("GBM", "2", H2OGradientBoostingEstimator, dict(max_depth=7, min_rows=10, sample_rate=0.8,
+                                                     col_sample_rate=0.8, col_sample_rate_per_tree=0.8)),
+    ("GBM", "3", H2OGradientBoostingEstimator, dict(max_depth=8, min_rows=10, sample_rate=0.8,
+                                                     col_sample_rate=0.8, col_sample_rate_per_tree=0.8)),
+    ("GBM", "4", H2OGradientBoostingEstimator, dict(max_depth=10, min_rows=10, sample_rate=0.8,
+                                                     col_sample_rate=0.8, col_sample_rate_per_tree=0.8)),
+    ("GBM", "5", H2OGradientBoostingEstimator, dict(max_depth=15, min_rows=100, sample_rate=0.8,
+                                                     col_sample_rate=0.8, col_sample_rate_per_tree=0.8)),
+    ("XGBoost", "2", H2OXGBoostEstimator, dict(max_depth=20, min_child_weight=10, sample_rate=0.6,
+                                                col_sample_rate=0.8, col_sample_rate_per_tree=0.8)),
+    ("XGBoost", "3", H2OXGBoostEstimator, dict(max_depth=5, min_child_weight=3, sample_rate=0.8,
+                                                col_sample_rate=0.8, col_sample_rate_per_tree=0.8)),
+    ("DRF", "XRT", H2ORandomForestEstimator, dict(sample_rate=0.632, col_sample_rate_per_tree=0.8, nbins=10)),
+    ("DeepLearning", "1", H2ODeepLearningEstimator, dict(hidden=[10, 10, 10], epochs=10)),
+]
+
+GRID = dict(max_depth=[3, 4, 5, 6, 7, 8, 9, 10, 12, 15], min_rows=[1, 5, 10, 15, 30, 100],
+            sample_rate=[0.5, 0.6, 0.7, 0.8, 0.9, 1.0], col_sample_rate=[0.4, 0.7, 1.0],
+            col_sample_rate_per_tree=[0.4, 0.7, 1.0], learn_rate=[0.05, 0.1])
+
+
+def _metric_spec(category, sort_metric):
+    sm = (sort_metric or "AUTO").lower()
+    if sm == "auto":
+        sm = {ModelCategory.BINOMIAL: "auc", ModelCategory.MULTINOMIAL: "mean_per_class_error"}.get(category,
+                                                                                                  "mean_residual_deviance")
+    key = {"auc": "AUC", "aucpr": "AUCPR", "logloss": "logloss", "rmse": "RMSE", "mse": "MSE", "mae": "mae",
+           "mean_per_class_error": "mean_per_class_error", "mean_residual_deviance": "mean_residual_deviance",
+           "rmsle": "rmsle"}[sm]
+    return sm, key, sm in ("auc", "aucpr")
+
+
+class H2OAutoML:
+    def __init__(self, max_models=None, max_runtime_secs=None, max_runtime_secs_per_model=0.0, nfolds=-1, seed=-1,
+                 project_name=None, include_algos=None, exclude_algos=None, sort_metric="AUTO",
+                 keep_cross_validation_predictions=True, stopping_rounds=3, stopping_tolerance=None,
+                 stopping_metric="AUTO", balance_classes=False, verbosity="warn", **_ignored):
+        self.max_models = max_models
+        self.max_runtime_secs = max_runtime_secs
+        self.nfolds = 5 if nfolds in (-1, None) else int(nfolds)
+        self.seed = seed
+        self.project_name = project_name or f"AutoML_{uuid.uuid4().hex[:8]}"
+        inc = [a.lower() for a in include_algos] if include_algos else [a.lower() for a in ALGOS]
+        exc = {a.lower() for a in (exclude_algos or [])}
+        self.algos = [a for a in inc if a not in exc]
+        self.sort_metric = sort_metric
+        self.events: list[dict] = []
+        self.models: list = []
+        self.leaderboard: list[dict] = []
+        self.leader = None
+
+    def _log(self, stage, msg):
+        self.events.append({"t": time.strftime("%H:%M:%S"), "stage": stage, "msg": msg})
+
+    def train(self, x=None, y=None, training_frame: Frame | None = None, leaderboard_frame: Frame | None = None,
+              validation_frame: Frame | None = None, comm=None):
+        t0 = time.time()
+        budget = self.max_runtime_secs
+        if not budget and not self.max_models:
+            budget = 3600.0
+        seed = self.seed if self.seed is not None and self.seed >= 0 else 42
+        rng = np.random.default_rng(seed)
+        cv = dict(nfolds=self.nfolds, fold_assignment="Modulo", keep_cross_validation_predictions=True,
+                  seed=seed) if self.nfolds > 1 else dict(seed=seed)
+        category = None
+
+        def out_of_budget():
+            if self.max_models and len(self.models) >= self.max_models:
+                return True
+            return bool(budget) and time.time() - t0 > budget
+
+        def fit(name, cls, params):
+            nonlocal category
+            mid = f"{name}_AutoML_{self.project_name}"
+            try:
+                est = cls(model_id=mid, **params, **cv)
+                m = est.train(x=x, y=y, training_frame=training_frame, validation_frame=validation_frame, comm=comm)
+            except Exception as e:  # noqa: BLE001
+                self._log("ModelTraining", f"{name} failed: {type(e).__name__}: {e}")
+                return None
+            category = m.category
+            self.models.append(m)
+            self._log("ModelTraining", f"{mid} trained")
+            return m
+
+        self._log("Workflow", f"AutoML build started: {self.project_name}")
+        for algo, suffix, cls, params in PRESETS:
+            if algo.lower() not in self.algos:
+                continue
+            if out_of_budget():
+                break
+            fit(f"{algo}_{suffix}", cls, dict(params))
+        g = 1
+        while "gbm" in self.algos and not out_of_budget() and (self.max_models or budget):
+            params = {k: v[int(rng.integers(len(v)))] for k, v in GRID.items()}
+            fit(f"GBM_grid_1_model_{g}", H2OGradientBoostingEstimator, params)
+            g += 1
+            if g > 200:
+                break
+        base = [m for m in self.models if m.cross_validation_holdout is not None]
+        if "stackedensemble" in self.algos and self.nfolds > 1 and len(base) >= 2 and category != ModelCategory.CLUSTERING:
+            for name, members in (("StackedEnsemble_AllModels", base),
+                                  ("StackedEnsemble_BestOfFamily", self._best_of_family(base, category))):
+                if len(members) < 2:
+                    continue
+                try:
+                    se = H2OStackedEnsembleEstimator(model_id=f"{name}_AutoML_{self.project_name}",
+                                                     base_models=[m.model_id for m in members], seed=seed)
+                    m = se.train(x=x, y=y, training_frame=training_frame, comm=comm)
+                    m.cross_validation_metrics = None
+                    self.models.append(m)
+                    self._log("ModelTraining", f"{m.model_id} trained")
+                except Exception as e:  # noqa: BLE001
+                    self._log("ModelTraining", f"{name} failed: {type(e).__name__}: {e}")
+        self._rank(category, leaderboard_frame, comm)
+        self._log("Workflow", f"AutoML build done: {len(self.models)} models in {time.time() - t0:.1f}s")
+        return self
+
+    def _score(self, m, key, lb_frame, comm):
+        if lb_frame is not None:
+            mm = m._metrics(lb_frame, m.predict_raw(lb_frame), comm)
+        else:
+            mm = m.cross_validation_metrics or m.training_metrics
+        return mm
+
+    def _best_of_family(self, models, category):
+        _, key, higher = _metric_spec(category, self.sort_metric)
+        best = {}
+        for m in models:
+            mm = m.cross_validation_metrics or m.training_metrics or {}
+            v = mm.get(key)
+            if v is None:
+                continue
+            fam = m.algo
+            if fam not in best or (v > best[fam][0] if higher else v < best[fam][0]):
+                best[fam] = (v, m)
+        return [m for _, m in best.values()]
+
+    def _rank(self, category, lb_frame, comm):
+        if category is None:
+            return
+        sm, key, higher = _metric_spec(category, self.sort_metric)
+        rows = []
+        for m in self.models:
+            mm = self._score(m, key, lb_frame, comm) or {}
+            r = {"model_id": m.model_id, "algo": m.algo}
+            if category == ModelCategory.BINOMIAL:
+                cols = [("auc", "AUC"), ("logloss", "logloss"), ("aucpr", "AUCPR"),
+                        ("mean_per_class_error", "mean_per_class_error"), ("rmse", "RMSE"), ("mse", "MSE")]
+            elif category == ModelCategory.MULTINOMIAL:
+                cols = [("mean_per_class_error", "mean_per_class_error"), ("logloss", "logloss"), ("rmse", "RMSE"),
+                        ("mse", "MSE")]
+            else:
+                cols = [("mean_residual_deviance", "mean_residual_deviance"), ("rmse", "RMSE"), ("mse", "MSE"),
+                        ("mae", "mae"), ("rmsle", "rmsle")]
+            for c, k in cols:
+                v = mm.get(k)
+                r[c] = float(v) if v is not None else float("nan")
+            r["_sort"] = float(mm.get(key, float("nan")) or float("nan"))
+            rows.append(r)
+        rows.sort(key=lambda r: (np.isnan(r["_sort"]), -r["_sort"] if higher else r["_sort"]))
+        for r in rows:
+            r.pop("_sort")
+        self.leaderboard = rows
+        self.sort_metric_used = sm
+        self.leader = DKV.get(rows[0]["model_id"]) if rows else None
+
+    def leaderboard_frame(self) -> Frame:
+        import pandas as pd
+
+        return Frame.from_pandas(pd.DataFrame(self.leaderboard))
+
+
+def run_automl(spec: dict, comm=None) -> dict:
+    """REST entry (/99/AutoMLBuilder JSON spec) executed on every rank."""
+    bc = spec.get("build_control", {}) or {}
+    isp = spec.get("input_spec", {}) or {}
+    bm = spec.get("build_models", {}) or {}
+    sc = bc.get("stopping_criteria", {}) or {}
+    aml = H2OAutoML(max_models=sc.get("max_models"), max_runtime_secs=sc.get("max_runtime_secs"),
+                    seed=sc.get("seed", -1), nfolds=bc.get("nfolds", -1), project_name=bc.get("project_name"),
+                    include_algos=bm.get("include_algos"), exclude_algos=bm.get("exclude_algos"),
+                    sort_metric=isp.get("sort_metric", "AUTO"))
+    tf = DKV.get(_key(isp.get("training_frame")))
+    lf = DKV.get(_key(isp.get("leaderboard_frame"))) if isp.get("leaderboard_frame") else None
+    y = isp.get("response_column")
+    y = _key(y)
+    ignored = set(isp.get("ignored_columns") or [])
+    x = [c for c in tf.names if c != y and c not in ignored]
+    aml.train(x=x, y=y, training_frame=tf, leaderboard_frame=lf, comm=comm)
+    return {"project_name": aml.project_name, "leaderboard": aml.leaderboard, "events": aml.events,
+            "sort_metric": getattr(aml, "sort_metric_used", None)}
+
+
+def _key(v):
+    if isinstance(v, dict):
+        return v.get("name") or v.get("column_name")
+    return v

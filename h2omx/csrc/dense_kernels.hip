@@ -452,7 +452,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float* __restrict__ A, 
           if (bias) v += bias[j];
           if (act == 1) v = fmaxf(v, 0.0f);
           else if (act == 2) v = tanhf(v);
-          else if (act == 3) v = fmaxf(v, 0.0f);  // maxout approximated by relu
           Cm[(int64_t)i * N + j] = v;
         }
       }
@@ -464,7 +463,7 @@ __global__ __launch_bounds__(256) void act_backward_kernel(const float* __restri
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float g = dY[i];
-  if (act == 1 || act == 3) g = Y[i] > 0.0f ? g : 0.0f;
+  if (act == 1) g = Y[i] > 0.0f ? g : 0.0f;
   else if (act == 2) g = g * (1.0f - Y[i] * Y[i]);
   dY[i] = g;
 }
@@ -481,7 +480,7 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict_
 
 // softmax cross-entropy over logits Z [M][K]: writes dZ = (softmax - onehot) * w / norm
 // and accumulates the loss into loss[0].
-__global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ Z, const float* __restrict__ y,
+__global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ Z, const int* __restrict__ y,
                                                            float* __restrict__ dZ, float* __restrict__ loss, int M,
                                                            int K) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -492,7 +491,7 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
     for (int k = 0; k < K; ++k) mx = fmaxf(mx, z[k]);
     float den = 0.0f;
     for (int k = 0; k < K; ++k) den += __expf(z[k] - mx);
-    const int yi = (int)y[i];
+    const int yi = y[i];
     for (int k = 0; k < K; ++k) {
       const float pk = __expf(z[k] - mx) / den;
       dZ[(int64_t)i * K + k] = (pk - (k == yi ? 1.0f : 0.0f)) / (float)M;
@@ -612,7 +611,7 @@ H2OMX_API int h2omx_bias_grad(const float* dY, float* db, int M, int N, hipStrea
   return launch_status();
 }
 
-H2OMX_API int h2omx_softmax_xent(const float* Z, const float* y, float* dZ, float* loss, int M, int K,
+H2OMX_API int h2omx_softmax_xent(const float* Z, const int* y, float* dZ, float* loss, int M, int K,
                                  hipStream_t stream) {
   hipLaunchKernelGGL(softmax_xent_kernel, dim3(cdiv(M, 256)), dim3(256), 0, stream, Z, y, dZ, loss, M, K);
   return launch_status();

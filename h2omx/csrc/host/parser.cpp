@@ -276,10 +276,12 @@ std::string read_range(const char* path, int64_t start, int64_t end, std::string
   // past `end`
   std::string data;
   if (start > 0) {
-    in.seekg(start - 1);
+    // the line containing byte start-1 belongs to the previous shard
+    int64_t p = start - 1;
+    in.seekg(p);
     char c;
-    while (in.get(c) && c != '\n') ++start;
-    ++start;
+    while (in.get(c) && c != '\n') ++p;
+    start = p + 1;
   }
   if (start >= size) return "";
   int64_t stop = end;

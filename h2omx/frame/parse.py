@@ -127,6 +127,41 @@ def import_file(path: str, sep: str | None = None, header: bool | None = None, c
     return fr
 
 
+def sample_setup(path: str, sep: str | None = None, header: bool | None = None, nbytes: int = 1 << 22) -> dict:
+    """ParseSetup guessed from the first ``nbytes`` of the file (cheap on big files)."""
+    size = os.path.getsize(path)
+    if size <= nbytes:
+        return parse_setup(path, sep, header)
+    with open(path, "rb") as f:
+        head = f.read(nbytes)
+    head = head[: head.rfind(b"\n") + 1] or head
+    h = _lib().h2omx_csv_parse_text(head, len(head), (sep or "\0").encode()[:1],
+                                    -1 if header is None else int(bool(header)), 8)
+    return _Parsed(h).setup()
+
+
+def import_shard(path: str, rank: int, world: int, setup: dict, device="cpu", key=None) -> Frame:
+    """Parse rank's byte range of ``path`` with the column names / types / separator
+    agreed on by the leader (``setup`` from :func:`sample_setup`)."""
+    types = ["enum" if t == "Enum" else ("string" if t == "String" else "numeric") for t in setup["column_types"]]
+    sep = chr(setup["separator"]) if setup.get("separator") else None
+    header = setup.get("check_header") == 1
+    try:
+        fr = import_file(path, sep=sep, header=header if rank == 0 else False, col_types=types, device=device,
+                         key=key, shard=(rank, world) if world > 1 else None, col_names=setup["column_names"])
+    except IOError as e:
+        if "empty" not in str(e):
+            raise
+        vecs = []
+        for name, t in zip(setup["column_names"], types):
+            if t == "enum":
+                vecs.append(Vec(name, torch.zeros(0, dtype=torch.int32, device=device), ENUM, []))
+            else:
+                vecs.append(Vec(name, torch.zeros(0, dtype=torch.float32, device=device), REAL))
+        fr = Frame(vecs, key=key)
+    return fr
+
+
 def parse_text(text: str, sep: str | None = None, header: bool | None = None, device="cpu", key=None) -> Frame:
     raw = text.encode()
     h = _lib().h2omx_csv_parse_text(raw, len(raw), (sep or "\0").encode()[:1],

@@ -1,6 +1,7 @@
 """Model builders (H2O estimator API)."""
 from .base import Model, ModelBuilder, ModelCategory  # noqa: F401
 from .deeplearning import H2ODeepLearningEstimator  # noqa: F401
+from .ensemble import H2OStackedEnsembleEstimator  # noqa: F401
 from .glm import H2OGeneralizedLinearEstimator  # noqa: F401
 from .kmeans import H2OKMeansEstimator  # noqa: F401
 from .tree_models import (H2OGradientBoostingEstimator, H2ORandomForestEstimator,  # noqa: F401
@@ -13,4 +14,5 @@ ESTIMATORS = {
     "glm": H2OGeneralizedLinearEstimator,
     "kmeans": H2OKMeansEstimator,
     "deeplearning": H2ODeepLearningEstimator,
+    "stackedensemble": H2OStackedEnsembleEstimator,
 }

@@ -219,7 +219,7 @@ def _kmeans_large(X: torch.Tensor, C: torch.Tensor):
 # ---------------------------------------------------------------------------
 # MLP building blocks
 # ---------------------------------------------------------------------------
-ACTS = {"linear": 0, "none": 0, "rectifier": 1, "relu": 1, "tanh": 2, "maxout": 3}
+ACTS = {"linear": 0, "none": 0, "rectifier": 1, "relu": 1, "tanh": 2}  # maxout: models/deeplearning.py
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = False, tb: bool = False,
@@ -240,7 +240,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
         c = c + beta_c * out
     if bias is not None:
         c = c + bias
-    if act in (1, 3):
+    if act == 1:
         c = torch.relu(c)
     elif act == 2:
         c = torch.tanh(c)
@@ -256,7 +256,7 @@ def act_backward(Y: torch.Tensor, dY: torch.Tensor, act: int) -> torch.Tensor:
     if Y.is_cuda:
         check(dense_lib().h2omx_act_backward(P(Y), P(dY), Y.numel(), act, stream(Y.device)), "act_backward")
         return dY
-    if act in (1, 3):
+    if act == 1:
         dY.mul_((Y > 0).float())
     elif act == 2:
         dY.mul_(1 - Y * Y)
@@ -273,8 +273,10 @@ def bias_grad(dY: torch.Tensor) -> torch.Tensor:
 
 
 def softmax_xent(Z: torch.Tensor, y: torch.Tensor):
+    """Z [M][K] logits, y int32 class ids -> (dZ = (softmax - onehot) / M, mean loss)."""
     M, K = Z.shape
     if Z.is_cuda:
+        y = y.to(torch.int32).contiguous()
         dZ = torch.empty_like(Z)
         loss = torch.zeros((1,), dtype=torch.float32, device=Z.device)
         check(dense_lib().h2omx_softmax_xent(P(Z), P(y), P(dZ), P(loss), M, K, stream(Z.device)), "softmax_xent")

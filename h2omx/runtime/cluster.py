@@ -1,0 +1,265 @@
+"""Cluster formation and the distributed command bus of a node.
+
+The reference deploys N pods of one StatefulSet and hands each pod the
+environment contract below (reference ``src/k8s/templates.rs:48-56``); the
+H2O image then forms a cloud from DNS lookups of the headless service.  Here
+the same contract forms a ``torch.distributed`` process group (RCCL over
+xGMI on MI355X, gloo on CPU):
+
+* ``H2O_KUBERNETES_SERVICE_DNS``  headless service name (peer discovery)
+* ``H2O_NODE_EXPECTED_COUNT``     world size
+* ``H2O_NODE_LOOKUP_TIMEOUT``     seconds to wait for all peers (default 180)
+* ``H2O_KUBERNETES_API_PORT``     port of the leader probe (default 8081)
+* rank = StatefulSet ordinal = numeric suffix of ``POD_NAME``/``HOSTNAME``
+* rendezvous master = ``<statefulset>-0.<service dns>`` (pod 0's stable DNS
+  name, valid because the StatefulSet's ``serviceName`` is the real service;
+  reference quirk Q2 fixed in control/src/deployment.cpp)
+
+Outside Kubernetes, torchrun-style ``RANK``/``WORLD_SIZE``/``MASTER_ADDR``
+work too, and a bare process is a one-node cluster.
+
+Command bus: the leader (rank 0) serves the REST API.  Every operation that
+touches sharded data (parse, train, predict, metrics, delete, ...) must run
+on all ranks in the same order, because each rank's kernels take part in
+the same collectives.  The leader publishes each command as JSON in a
+``TCPStore`` (``cmd/<seq>``); workers poll for the next sequence number, run
+it on their own shard with the shared communicator and acknowledge
+(``ack/<seq>/<rank>``) with a status, so a failing rank turns into a failed
+job on the leader instead of a hang.  The store is only a control channel;
+all bulk data moves through RCCL.
+"""
+from __future__ import annotations
+
+import datetime
+import json
+import os
+import re
+import socket
+import threading
+import time
+import traceback
+from dataclasses import dataclass, field
+
+import torch
+
+
+@dataclass
+class ClusterConfig:
+    rank: int = 0
+    world_size: int = 1
+    master_addr: str = "127.0.0.1"
+    master_port: int = 29500
+    service_dns: str | None = None
+    lookup_timeout_s: float = 180.0
+    api_port: int = 8081
+    rest_port: int = 54321
+    pod_name: str = field(default_factory=socket.gethostname)
+    cloud_name: str = "h2omx"
+
+    @property
+    def bus_port(self) -> int:
+        return self.master_port + 1
+
+
+_ORDINAL = re.compile(r"^(.*)-(\d+)$")
+
+
+def config_from_env(env=None) -> ClusterConfig:
+    env = dict(os.environ if env is None else env)
+    cfg = ClusterConfig()
+    cfg.api_port = int(env.get("H2O_KUBERNETES_API_PORT", "8081"))
+    cfg.rest_port = int(env.get("H2OMX_REST_PORT", "54321"))
+    cfg.lookup_timeout_s = float(env.get("H2O_NODE_LOOKUP_TIMEOUT", "180"))
+    cfg.master_port = int(env.get("MASTER_PORT", "29500"))
+    cfg.pod_name = env.get("POD_NAME") or env.get("HOSTNAME") or socket.gethostname()
+    svc = env.get("H2O_KUBERNETES_SERVICE_DNS")
+    if svc:
+        cfg.service_dns = svc
+        cfg.world_size = int(env.get("H2O_NODE_EXPECTED_COUNT", "1"))
+        m = _ORDINAL.match(cfg.pod_name)
+        if not m:
+            raise ValueError(f"pod name {cfg.pod_name!r} has no StatefulSet ordinal suffix")
+        cfg.rank = int(m.group(2))
+        cfg.master_addr = env.get("MASTER_ADDR") or f"{m.group(1)}-0.{svc}"
+        cfg.cloud_name = svc.split(".")[0]
+    else:
+        cfg.world_size = int(env.get("WORLD_SIZE", "1"))
+        cfg.rank = int(env.get("RANK", "0"))
+        cfg.master_addr = env.get("MASTER_ADDR", "127.0.0.1")
+        cfg.cloud_name = env.get("H2OMX_CLOUD_NAME", "h2omx")
+    if not 0 <= cfg.rank < cfg.world_size:
+        raise ValueError(f"rank {cfg.rank} outside world of {cfg.world_size}")
+    return cfg
+
+
+def wait_for_peers(cfg: ClusterConfig, resolver=socket.getaddrinfo, sleep=time.sleep, clock=time.monotonic) -> list[str]:
+    """Block until the headless service resolves to ``world_size`` addresses
+    (all pods published, ``publishNotReadyAddresses: true``) or time out."""
+    if not cfg.service_dns or cfg.world_size == 1:
+        return []
+    deadline = clock() + cfg.lookup_timeout_s
+    last: list[str] = []
+    while True:
+        try:
+            infos = resolver(cfg.service_dns, None, socket.AF_INET, socket.SOCK_STREAM)
+            last = sorted({i[4][0] for i in infos})
+        except OSError:
+            last = []
+        if len(last) >= cfg.world_size:
+            return last
+        if clock() > deadline:
+            raise TimeoutError(f"cluster formation timed out after {cfg.lookup_timeout_s:.0f}s: "
+                               f"{len(last)}/{cfg.world_size} nodes visible via {cfg.service_dns}")
+        sleep(1.0)
+
+
+# ----------------------------------------------------------------------------
+# command bus
+# ----------------------------------------------------------------------------
+class CommandFailed(RuntimeError):
+    pass
+
+
+class Cluster:
+    """One node's view of the cloud: communicator + command bus + op table."""
+
+    POLL_S = 0.5
+
+    def __init__(self, cfg: ClusterConfig, comm, store=None):
+        self.cfg = cfg
+        self.comm = comm
+        self.store = store
+        self.seq = 0
+        self.lock = threading.RLock()
+        self.ops: dict = {}
+        self.started = time.time()
+        self.formed = True
+        self.stop = threading.Event()
+
+    @property
+    def rank(self):
+        return self.cfg.rank
+
+    @property
+    def world_size(self):
+        return self.cfg.world_size
+
+    @property
+    def is_leader(self):
+        return self.cfg.rank == 0
+
+    def register(self, name, fn):
+        self.ops[name] = fn
+
+    # -- leader side ---------------------------------------------------------
+    def run(self, op: str, timeout_s: float = 86400.0, **kwargs):
+        """Run ``op`` on every rank (leader call); returns the leader's result."""
+        if not self.is_leader:
+            raise RuntimeError("only the leader issues cluster commands")
+        with self.lock:
+            if self.world_size == 1 or self.store is None:
+                return self._execute(op, kwargs)
+            self.seq += 1
+            seq = self.seq
+            self.store.set(f"cmd/{seq}", json.dumps({"op": op, "kwargs": kwargs}))
+            try:
+                res = self._execute(op, kwargs)
+                err = None
+            except Exception as e:  # noqa: BLE001
+                res, err = None, e
+            failures = self._collect_acks(seq, timeout_s)
+            if err is not None:
+                raise err
+            if failures:
+                raise CommandFailed("; ".join(failures))
+            return res
+
+    def _collect_acks(self, seq, timeout_s):
+        failures = []
+        for r in range(1, self.world_size):
+            key = f"ack/{seq}/{r}"
+            deadline = time.time() + timeout_s
+            while True:
+                try:
+                    self.store.wait([key], datetime.timedelta(seconds=self.POLL_S * 4))
+                    break
+                except Exception:  # noqa: BLE001 - store wait timeout
+                    if time.time() > deadline:
+                        failures.append(f"rank {r}: no acknowledgement")
+                        break
+            else:
+                continue
+            ack = json.loads(self.store.get(key).decode())
+            if ack.get("status") != "ok":
+                failures.append(f"rank {r}: {ack.get('error')}")
+        return failures
+
+    def shutdown_workers(self):
+        if self.is_leader and self.world_size > 1 and self.store is not None:
+            with self.lock:
+                self.seq += 1
+                self.store.set(f"cmd/{self.seq}", json.dumps({"op": "__shutdown__", "kwargs": {}}))
+
+    # -- worker side ---------------------------------------------------------
+    def worker_loop(self):
+        """Follow the leader's commands until shutdown."""
+        seq = 0
+        while not self.stop.is_set():
+            seq += 1
+            key = f"cmd/{seq}"
+            while True:
+                try:
+                    self.store.wait([key], datetime.timedelta(seconds=self.POLL_S * 4))
+                    break
+                except Exception:  # noqa: BLE001 - idle: keep polling
+                    if self.stop.is_set():
+                        return
+            cmd = json.loads(self.store.get(key).decode())
+            if cmd["op"] == "__shutdown__":
+                return
+            try:
+                self._execute(cmd["op"], cmd["kwargs"])
+                ack = {"status": "ok"}
+            except Exception as e:  # noqa: BLE001
+                ack = {"status": "error", "error": f"{type(e).__name__}: {e}",
+                       "trace": traceback.format_exc()[-2000:]}
+            self.store.set(f"ack/{seq}/{self.rank}", json.dumps(ack))
+
+    def _execute(self, op, kwargs):
+        fn = self.ops.get(op)
+        if fn is None:
+            raise KeyError(f"unknown cluster op {op!r}")
+        return fn(self, **kwargs)
+
+
+def form_cluster(cfg: ClusterConfig | None = None, device: str | None = None, timeout_s: float = 1800.0) -> Cluster:
+    """Discover peers, initialise the process group and the command bus."""
+    import torch.distributed as dist
+
+    from ..parallel.comm import Comm
+
+    cfg = cfg or config_from_env()
+    wait_for_peers(cfg)
+    if device is None:
+        device = "cuda" if torch.cuda.device_count() > 0 else "cpu"
+    if device == "cuda":
+        dev = torch.device("cuda", 0 if torch.cuda.device_count() == 1 else cfg.rank % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    store = None
+    if cfg.world_size > 1:
+        if not dist.is_initialized():
+            kw = {"device_id": dev} if dev.type == "cuda" else {}
+            dist.init_process_group(backend="nccl" if dev.type == "cuda" else "gloo",
+                                    init_method=f"tcp://{cfg.master_addr}:{cfg.master_port}",
+                                    rank=cfg.rank, world_size=cfg.world_size,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        store = dist.TCPStore(cfg.master_addr, cfg.bus_port, cfg.world_size, cfg.rank == 0,
+                              timeout=datetime.timedelta(seconds=timeout_s))
+    comm = Comm(cfg.rank, cfg.world_size, dev)
+    cl = Cluster(cfg, comm, store)
+    from . import ops
+
+    ops.register_all(cl)
+    return cl

@@ -78,7 +78,7 @@ def test_gemm_matches_torch(cuda_dev, M, N, K, ta, tb, act):
 def test_mlp_elementwise(cuda_dev):
     torch.manual_seed(1)
     Z = torch.randn(300, 5, device=cuda_dev)
-    y = torch.randint(0, 5, (300,), device=cuda_dev).float()
+    y = torch.randint(0, 5, (300,), device=cuda_dev, dtype=torch.int32)
     dZ, loss = D.softmax_xent(Z, y)
     dZr, lr = D.softmax_xent(Z.cpu(), y.cpu())
     assert torch.allclose(dZ.cpu(), dZr, atol=1e-6) and abs(loss.item() - lr.item()) < 1e-5

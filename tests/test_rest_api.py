@@ -1,0 +1,162 @@
+"""REST API tests: a one-node cluster serves the H2O routes over HTTP and
+h2omx.client drives the h2o-py workflow against it (connect, import /
+upload, parse, frames, model builders, jobs, predictions, metrics, MOJO,
+Rapids, AutoML, DKV removal, error shapes)."""
+import io
+import socket
+import zipfile
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from h2omx.api.server import H2OApi, serve
+from h2omx.client import H2OConnection, H2OResponseError
+from h2omx.frame.frame import DKV
+from h2omx.runtime.cluster import ClusterConfig, form_cluster
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def conn(tmp_path_factory):
+    cl = form_cluster(ClusterConfig(), device="cpu")
+    api = H2OApi(cl)
+    port = _free_port()
+    srv = serve(api, "127.0.0.1", port)
+    c = H2OConnection(f"http://127.0.0.1:{port}")
+    yield c
+    srv.shutdown()
+    DKV.clear()
+
+
+@pytest.fixture(scope="module")
+def csv_path(tmp_path_factory):
+    rng = np.random.default_rng(0)
+    n = 3000
+    df = pd.DataFrame({"a": rng.normal(size=n), "b": rng.normal(size=n), "c": rng.choice(["x", "y", "z"], n)})
+    logit = df.a - df.b + (df.c == "x") * 1.0
+    df["label"] = np.where(rng.random(n) < 1 / (1 + np.exp(-logit)), "yes", "no")
+    p = tmp_path_factory.mktemp("data") / "train.csv"
+    df.to_csv(p, index=False)
+    return str(p)
+
+
+def test_cloud_and_session(conn):
+    cloud = conn.connect()
+    assert cloud["cloud_size"] == 1 and cloud["cloud_healthy"] and cloud["consensus"]
+    assert cloud["version"].count(".") == 3
+    assert conn.session_key.startswith("_sid_")
+    about = conn.request("GET /3/About")
+    assert any(e["name"] == "Build project version" for e in about["entries"])
+
+
+def test_import_parse_frame(conn, csv_path):
+    key = conn.import_file(csv_path, destination_frame="train.hex")
+    assert key == "train.hex"
+    fr = conn.frame(key, rows=5)
+    assert fr["rows"] == 3000
+    labels = [c["label"] for c in fr["columns"]]
+    assert labels == ["a", "b", "c", "label"]
+    c = fr["columns"][2]
+    assert c["type"] == "enum" and c["domain"] == ["x", "y", "z"]
+    assert len(fr["columns"][0]["data"]) == 5
+    assert abs(fr["columns"][0]["mean"]) < 0.1
+    lst = conn.request("GET /3/Frames")
+    assert any(f["frame_id"]["name"] == "train.hex" for f in lst["frames"])
+
+
+def test_upload_file(conn, csv_path):
+    key = conn.upload_file(csv_path, destination_frame="uploaded.hex")
+    assert conn.frame(key)["rows"] == 3000
+
+
+@pytest.mark.parametrize("algo,params", [("gbm", {"ntrees": 10, "max_depth": 3, "seed": 1}),
+                                         ("glm", {"family": "binomial", "lambda": 0}),
+                                         ("drf", {"ntrees": 5, "seed": 1}),
+                                         ("deeplearning", {"hidden": [16], "epochs": 10, "seed": 1}),
+                                         ("xgboost", {"ntrees": 5, "max_depth": 3})])
+def test_build_predict_metrics(conn, algo, params):
+    m = conn.train(algo, "train.hex", y="label", **params)
+    tm = m["output"]["training_metrics"]
+    assert m["algo"] == algo
+    assert tm["__meta"]["schema_type"] == "ModelMetricsBinomial"
+    assert tm["AUC"] > 0.7
+    assert tm["cm"]["table"]["columns"][1]["name"] == "no"
+    pred = conn.predict(m["model_id"]["name"], "train.hex")
+    pf = conn.frame(pred, rows=3)
+    assert [c["label"] for c in pf["columns"]] == ["predict", "no", "yes"]
+    mm = conn.model_performance(m["model_id"]["name"], "train.hex")
+    assert abs(mm["AUC"] - tm["AUC"]) < 1e-9
+    vi = m["output"]["variable_importances"]
+    if vi is not None:
+        assert vi["columns"][0]["name"] == "variable"
+
+
+def test_unknown_param_is_warning_and_ignored_columns(conn):
+    m = conn.train("gbm", "train.hex", y="label", x=["a", "b"], ntrees=3, histogram_type="UniformAdaptive",
+                   build_tree_one_node="true")
+    names = m["output"]["names"]
+    assert names == ["a", "b", "label"]
+
+
+def test_kmeans_rest_and_mojo_roundtrip(conn):
+    from h2omx.frame.frame import DKV as dkv
+    from h2omx.mojo import GenericModel
+
+    m = conn.train("kmeans", "train.hex", x=["a", "b", "c"], k=3, seed=2)
+    assert m["output"]["model_category"] == "Clustering"
+    data = conn.download_mojo(m["model_id"]["name"])
+    z = zipfile.ZipFile(io.BytesIO(data))
+    assert "model.ini" in z.namelist()
+    g = GenericModel(data)
+    fr = dkv.get("train.hex")
+    orig = dkv.get(m["model_id"]["name"])
+    assert (g.predict_raw(fr) == orig.predict_raw(fr)).all()
+
+
+def test_rapids_split_and_slice(conn):
+    r = conn.rapids('(tmp= rnd_1 (h2o.runif train.hex 42))')
+    assert r["num_rows"] == 3000
+    r = conn.rapids('(tmp= part_a (rows train.hex (< rnd_1 0.75)))')
+    r2 = conn.rapids('(tmp= part_b (rows train.hex (>= rnd_1 0.75)))')
+    assert r["num_rows"] + r2["num_rows"] == 3000 and 2000 < r["num_rows"] < 2500
+    r = conn.rapids('(cols_py train.hex ["a" "c"])')
+    assert r["num_cols"] == 2
+    s = conn.rapids("(mean (cols_py train.hex 0) true)")
+    assert abs(s["scalar"]) < 0.1
+    r = conn.rapids('(tmp= t2 (:= train.hex (as.factor (cols_py train.hex "a")) 0 []))')
+    assert r["num_cols"] == 4
+    conn.rapids("(rm rnd_1)")
+
+
+def test_automl_rest(conn):
+    res = conn.automl("train.hex", "label", max_models=3, nfolds=3, project_name="aml_test",
+                      build_models={"include_algos": ["GLM", "GBM", "DRF", "StackedEnsemble"]})
+    lb = res["leaderboard_table"]
+    ids = lb["data"][0]
+    assert len(ids) >= 3
+    assert any(i.startswith("StackedEnsemble") for i in ids)
+    aucs = lb["data"][[c["name"] for c in lb["columns"]].index("auc")]
+    assert aucs == sorted(aucs, reverse=True)
+
+
+def test_errors_and_delete(conn):
+    with pytest.raises(H2OResponseError) as e:
+        conn.request("GET /3/Frames/nope.hex")
+    assert e.value.status == 404 and e.value.payload["__meta"]["schema_type"] == "H2OError"
+    with pytest.raises(H2OResponseError) as e:
+        conn.request("POST /3/ModelBuilders/gbm", {"training_frame": "missing.hex", "response_column": "y"})
+    assert e.value.status == 404
+    txt = conn.request("GET /metrics", raw=True).decode()
+    assert "h2omx_models_built_total" in txt
+    conn.request("DELETE /3/Frames/uploaded.hex")
+    assert not any(f["frame_id"]["name"] == "uploaded.hex" for f in conn.request("GET /3/Frames")["frames"])
+    conn.remove_all()
+    assert conn.request("GET /3/Frames")["frames"] == []
