@@ -945,12 +945,8 @@ __global__ __launch_bounds__(1024) void stat_reduce_kernel(const unsigned int* _
 // qg / qsr: per-row fixed-point ranges chosen by the host from the largest
 // workgroup chunk of the tree's level plans (<= QG / QS): smaller chunks give
 // proportionally finer quantisation.
-__global__ __launch_bounds__(256) void tree_begin_kernel(const unsigned int* __restrict__ stat_max, int mode,
-                                                         double qg, double qsr, double* __restrict__ qs,
-                                                         int* __restrict__ ctl0, NodeLink* __restrict__ link0,
-                                                         unsigned long long* __restrict__ leaf_acc, int leaf_n) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < leaf_n; i += gridDim.x * blockDim.x) leaf_acc[i] = 0ull;
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+__device__ void tree_begin_scales(const unsigned int* __restrict__ stat_max, int mode, double qg, double qsr,
+                                  double* __restrict__ qs, int* __restrict__ ctl0, NodeLink* __restrict__ link0) {
   const double gmax = fmax((double)__uint_as_float(stat_max[0]), 1e-30);
   const double hmax = fmax((double)__uint_as_float(stat_max[1]), 1e-30);
   const double wmax = fmax((double)__uint_as_float(stat_max[2]), 1e-30);
@@ -968,6 +964,15 @@ __global__ __launch_bounds__(256) void tree_begin_kernel(const unsigned int* __r
   NodeLink root;
   root.slot = 0; root.sib_slot = -1; root.parent = -1; root.pad = 0;
   link0[0] = root;
+}
+
+__global__ __launch_bounds__(256) void tree_begin_kernel(const unsigned int* __restrict__ stat_max, int mode,
+                                                         double qg, double qsr, double* __restrict__ qs,
+                                                         int* __restrict__ ctl0, NodeLink* __restrict__ link0,
+                                                         unsigned long long* __restrict__ leaf_acc, int leaf_n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < leaf_n; i += gridDim.x * blockDim.x) leaf_acc[i] = 0ull;
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0);
 }
 
 // Exact per-leaf (G, H, W) sums after the last partition: every row carries
@@ -1275,5 +1280,493 @@ H2OMX_API int h2omx_predict_binned(const uint8_t* codes, int64_t npad, int64_t n
                                    hipStream_t stream) {
   hipLaunchKernelGGL(predict_binned_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, codes, npad, n,
                      reinterpret_cast<const TreeNode*>(nodes), roots, ntrees, K, nbt, out, ldo);
+  return launch_status();
+}
+
+// ===========================================================================
+// Row-partitioned level pipeline ("segmented" engine).
+//
+// The scan engine above re-reads every row's node id, gradient and codes
+// once per feature group at every level; at depth >= 3 that is ~1 GB of HBM
+// traffic per level.  Here the rows of every node live in one contiguous
+// segment of a row-index permutation (idx), kept stably partitioned level
+// by level (XGBoost-hist / LightGBM style), so a level touches only the rows
+// of the nodes it actually builds:
+//
+//   tree_begin_seg  scales, root segment [0, n), chunk prefixes, zero built
+//   hist_build_seg  one workgroup per (row chunk of a built node, feature
+//                   group): gathers row-major codes (28 B/row) + g/s by idx,
+//                   packed fixed-point u64 LDS atomics, per-chunk slab
+//   hist_reduce_seg slabs of each slot -> exact int64 histograms (integer
+//                   atomics split over chunk subsets: deterministic)
+//   (split_find / level_finalize unchanged)
+//   part_count      left-row count per partition chunk
+//   level_close     one block: in-node chunk offsets, children segments,
+//                   next level's chunk prefixes, zero next built histograms
+//   part_scatter    stable in-chunk ranks (wave ballots) -> idx_out, node
+//                   ids, and exact leaf sums of retiring rows (block
+//                   reduction + 3 integer atomics per chunk: no LDS atomics)
+//
+// Chunk tables are implicit: per node an exclusive prefix of its chunk
+// count (hc_first / pc_first, length n+1); a workgroup finds its node by
+// binary search.  Chunk sizes: hist C_h rows (<= ROWS_CAP, fixed-point
+// headroom), partition C_p = 4096 rows.
+// ===========================================================================
+constexpr int PC_ROWS = 4096;
+
+// largest i in [0, n) with first[i] <= c < first[i + 1]
+__device__ __forceinline__ int chunk_node(const int* __restrict__ first, int n, int c) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (first[mid] <= c) lo = mid;
+    else hi = mid - 1;
+  }
+  // skip empty nodes sharing the same prefix value
+  while (lo + 1 < n && first[lo + 1] <= c) ++lo;
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void tree_begin_seg_kernel(
+    const unsigned int* __restrict__ stat_max, int mode, double qg, double qsr, double* __restrict__ qs,
+    int* __restrict__ ctl0, NodeLink* __restrict__ link0, unsigned long long* __restrict__ leaf_acc, int leaf_n,
+    long long* __restrict__ built, int built_n, int n_rows, int hc_rows, int* __restrict__ seg_start,
+    int* __restrict__ seg_cnt, int* __restrict__ hc_first, int* __restrict__ pc_first, int* __restrict__ slot_node) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < leaf_n; i += gridDim.x * blockDim.x) leaf_acc[i] = 0ull;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < built_n; i += gridDim.x * blockDim.x) built[i] = 0ll;
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0);
+  seg_start[0] = 0;
+  seg_cnt[0] = n_rows;
+  hc_first[0] = 0;
+  hc_first[1] = (n_rows + hc_rows - 1) / hc_rows;
+  pc_first[0] = 0;
+  pc_first[1] = (n_rows + PC_ROWS - 1) / PC_ROWS;
+  slot_node[0] = 0;
+}
+
+template <int NBT>
+__global__ __launch_bounds__(512) void hist_build_seg_kernel(
+    const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
+    const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
+    const int* __restrict__ hc_first, const int* __restrict__ ctl, const int* __restrict__ nvb,
+    const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups, int hc_rows,
+    unsigned long long* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
+  __shared__ int width_s[256], rep_s[256];
+  __shared__ int range_s[2];
+  const int n = ctl[CTL_N];
+  const int total = hc_first[n];
+  const int b = blockIdx.x;
+  const int xcd = b & 7, i = b >> 3;
+  const int grp = i % n_groups;
+  const int c = xcd + 8 * (i / n_groups);
+  if (c >= total) return;
+  const int f0 = grp * fg;
+  const int nf = min(fg, F - f0);
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) {
+    const int node = chunk_node(hc_first, n, c);
+    const int k = c - hc_first[node];
+    const int lo = seg_start[node] + k * hc_rows;
+    range_s[0] = lo;
+    range_s[1] = min(lo + hc_rows, seg_start[node] + seg_cnt[node]);
+  }
+  for (int j = threadIdx.x; j < fg * NBT; j += blockDim.x) lds64[j] = 0ull;
+  if (threadIdx.x < fg) {
+    const int fi = threadIdx.x;
+    const int w = (fi < nf) ? nvb[f0 + fi] + 1 : NBT;
+    width_s[fi] = w;
+    const int r = NBT / w;
+    rep_s[fi] = r < 1 ? 1 : (r > 64 ? 64 : r);
+  }
+  const float sg = (float)qscale[0], ss = (float)qscale[1];
+  __syncthreads();
+  const int lo = range_s[0], hi = range_s[1];
+  const int nw = (nf + 3) >> 2;
+  for (int j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+    const int r = idx ? idx[j] : j;
+    const uint32_t hsh = row_hash(r, salt);
+    const float d1 = (hsh & 0xFFFF) * (1.0f / 65536.0f), d2 = (hsh >> 16) * (1.0f / 65536.0f);
+    const float sv = s2 ? s2[r] : 1.0f;
+    const int gq = (int)floorf(fmaf(g[r], sg, d1));
+    const uint32_t sq = (uint32_t)floorf(fmaf(sv, ss, d2));
+    const unsigned long long pk = ((unsigned long long)(uint32_t)gq << 32) | (unsigned long long)sq;
+    if (pk == 0ull) continue;
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(codes_rm + (int64_t)r * fp + f0);
+    for (int wq = 0; wq < nw; ++wq) {
+      const uint32_t cw = row[wq];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int fi = 4 * wq + k;
+        if (fi < nf) {
+          const int width = width_s[fi];
+          int bin = (cw >> (8 * k)) & 0xff;
+          if (bin == NBT - 1) bin = width - 1;  // NA -> last slot of the feature slice
+          const int copy_off = (rep_s[fi] > 1) ? (lane % rep_s[fi]) * width : 0;
+          atomicAdd(lds64 + fi * NBT + copy_off + bin, pk);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  unsigned long long* out = slab + ((int64_t)c * n_groups + grp) * fg * NBT;
+  for (int j = threadIdx.x; j < fg * NBT; j += blockDim.x) {
+    const int bin = j % NBT, fi = j / NBT;
+    const int width = width_s[fi], rep = rep_s[fi];
+    const int src = (bin == NBT - 1) ? width - 1 : bin;
+    unsigned long long acc = 0ull;
+    if (src < width - 1 || bin == NBT - 1) {
+      const unsigned long long* hb = lds64 + fi * NBT;
+      for (int cc = 0; cc < rep; ++cc) acc += hb[cc * width + src];
+    }
+    out[j] = acc;
+  }
+}
+
+// built[s][F][2][NBT] += sum over the slot's chunks (subset blockIdx.z of K)
+__global__ __launch_bounds__(256) void hist_reduce_seg_kernel(const unsigned long long* __restrict__ slab,
+                                                              const int* __restrict__ hc_first,
+                                                              const int* __restrict__ slot_node,
+                                                              const int* __restrict__ ctl, int F, int nbt, int fg,
+                                                              int n_groups, long long* __restrict__ built) {
+  const int s = blockIdx.y;
+  if (s >= ctl[CTL_SLOTS]) return;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= F * nbt) return;
+  const int f = e / nbt, bin = e % nbt;
+  const int grp = f / fg, fi = f % fg;
+  const int node = slot_node[s];
+  const int c0 = hc_first[node], c1 = hc_first[node + 1];
+  const int K = gridDim.z;
+  long long ag = 0, as = 0;
+  const int64_t stride = (int64_t)n_groups * fg * nbt;
+  const unsigned long long* p = slab + (int64_t)grp * fg * nbt + (int64_t)fi * nbt + bin;
+  for (int c = c0 + (int)blockIdx.z; c < c1; c += K) {
+    const unsigned long long v = p[(int64_t)c * stride];
+    ag += (long long)(int32_t)(uint32_t)(v >> 32);
+    as += (long long)(uint32_t)v;
+  }
+  long long* o = built + (((int64_t)s * F + f) * 2) * nbt + bin;
+  if (ag) atomicAdd(reinterpret_cast<unsigned long long*>(o), (unsigned long long)ag);
+  if (as) atomicAdd(reinterpret_cast<unsigned long long*>(o + nbt), (unsigned long long)as);
+}
+
+__device__ __forceinline__ int split_dir(const uint8_t* __restrict__ codes, int64_t npad, const PartInfo& pi,
+                                         int nbt, int r) {
+  const int b = codes[(int64_t)pi.feat * npad + r];
+  return (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
+}
+
+// number of rows of chunk c going left (nodes that split into inner nodes)
+__global__ __launch_bounds__(256) void part_count_kernel(const uint8_t* __restrict__ codes, int64_t npad,
+                                                         const int* __restrict__ idx, const int* __restrict__ seg_start,
+                                                         const int* __restrict__ seg_cnt,
+                                                         const int* __restrict__ pc_first, const int* __restrict__ ctl,
+                                                         const PartInfo* __restrict__ part, int nbt,
+                                                         int* __restrict__ pc_left) {
+  __shared__ int red[4];
+  const int n = ctl[CTL_N];
+  const int c = blockIdx.x;
+  if (c >= pc_first[n]) return;
+  const int node = chunk_node(pc_first, n, c);
+  const PartInfo pi = part[node];
+  int cnt = 0;
+  if (pi.child >= 0 && !pi.leaf_children) {
+    const int lo = seg_start[node] + (c - pc_first[node]) * PC_ROWS;
+    const int hi = min(lo + PC_ROWS, seg_start[node] + seg_cnt[node]);
+    for (int j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+      const int r = idx ? idx[j] : j;
+      cnt += 1 - split_dir(codes, npad, pi, nbt, r);
+    }
+  }
+  cnt = (int)wave_sum((float)cnt);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) pc_left[c] = red[0] + red[1] + red[2] + red[3];
+}
+
+// Single block: offsets of every chunk's left rows inside its node, node
+// left totals, children segments, the next level's chunk prefixes and slot
+// map, and zeroed next-level histograms.
+__global__ __launch_bounds__(1024) void level_close_kernel(
+    const int* __restrict__ ctl, const int* __restrict__ ctl_next, const PartInfo* __restrict__ part,
+    const NodeLink* __restrict__ link_next, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
+    const int* __restrict__ pc_first, int* __restrict__ pc_left /* in: counts, out: in-node offsets */,
+    int* __restrict__ node_nl, int* __restrict__ nseg_start, int* __restrict__ nseg_cnt,
+    int* __restrict__ nhc_first, int* __restrict__ npc_first, int* __restrict__ nslot_node, int hc_rows,
+    long long* __restrict__ nbuilt, int per_slot) {
+  __shared__ int wsum[16];
+  __shared__ int carry_s[2];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int n = ctl[CTL_N];
+  const int total = pc_first[n];
+  // (a) global exclusive scan of left counts
+  if (t == 0) carry_s[0] = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < total; c0 += blockDim.x) {
+    const int c = c0 + t;
+    const int v = c < total ? pc_left[c] : 0;
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    int before = carry_s[0];
+    for (int k = 0; k < wid; ++k) before += wsum[k];
+    if (c < total) pc_left[c] = before + x - v;
+    __syncthreads();
+    if (t == 0) {
+      int tot = 0;
+      for (int k = 0; k < (int)(blockDim.x >> 6); ++k) tot += wsum[k];
+      carry_s[0] += tot;
+    }
+    __syncthreads();
+  }
+  const int grand = carry_s[0];
+  // (b) node left totals (node_nl) and node bases (kept in nseg_cnt temporarily is unsafe: use node_nl[n + i])
+  for (int i = t; i < n; i += blockDim.x) {
+    const int a = pc_first[i], z = pc_first[i + 1];
+    const int base = a < total ? pc_left[a] : grand;
+    const int end = z < total ? pc_left[z] : grand;
+    node_nl[i] = end - base;
+    node_nl[n + i] = base;
+  }
+  __syncthreads();
+  for (int c = t; c < total; c += blockDim.x) pc_left[c] -= node_nl[n + chunk_node(pc_first, n, c)];
+  // (c) children segments
+  for (int i = t; i < n; i += blockDim.x) {
+    const PartInfo pi = part[i];
+    if (pi.child >= 0 && !pi.leaf_children) {
+      const int nl = node_nl[i];
+      nseg_start[pi.child] = seg_start[i];
+      nseg_cnt[pi.child] = nl;
+      nseg_start[pi.child + 1] = seg_start[i] + nl;
+      nseg_cnt[pi.child + 1] = seg_cnt[i] - nl;
+    }
+  }
+  __syncthreads();
+  // (d) next level chunk prefixes + slot map
+  const int nn = ctl_next[CTL_N];
+  if (t == 0) { carry_s[0] = 0; carry_s[1] = 0; }
+  __syncthreads();
+  for (int j0 = 0; j0 < nn; j0 += blockDim.x) {
+    const int j = j0 + t;
+    int hcv = 0, pcv = 0;
+    if (j < nn) {
+      const int cnt = nseg_cnt[j];
+      const NodeLink L = link_next[j];
+      hcv = (L.slot >= 0) ? (cnt + hc_rows - 1) / hc_rows : 0;
+      pcv = (cnt + PC_ROWS - 1) / PC_ROWS;
+      if (L.slot >= 0) nslot_node[L.slot] = j;
+    }
+    // pack both counts in one 32-bit scan (each < 2^16 per block pass is not
+    // guaranteed) -> two scans
+    int xh = hcv, xp = pcv;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int yh = __shfl_up(xh, o, 64), yp = __shfl_up(xp, o, 64);
+      if (lane >= o) { xh += yh; xp += yp; }
+    }
+    __shared__ int wh[16], wp[16];
+    if (lane == 63) { wh[wid] = xh; wp[wid] = xp; }
+    __syncthreads();
+    int bh = carry_s[0], bp = carry_s[1];
+    for (int k = 0; k < wid; ++k) { bh += wh[k]; bp += wp[k]; }
+    if (j < nn) { nhc_first[j] = bh + xh - hcv; npc_first[j] = bp + xp - pcv; }
+    __syncthreads();
+    if (t == 0) {
+      int th = 0, tp = 0;
+      for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { th += wh[k]; tp += wp[k]; }
+      carry_s[0] += th; carry_s[1] += tp;
+    }
+    __syncthreads();
+  }
+  if (t == 0) { nhc_first[nn] = carry_s[0]; npc_first[nn] = carry_s[1]; }
+  // (e) zero the next level's built histograms
+  if (nbuilt) {
+    const int64_t m = (int64_t)ctl_next[CTL_SLOTS] * per_slot;
+    for (int64_t k = t; k < m; k += blockDim.x) nbuilt[k] = 0ll;
+  }
+}
+
+__device__ __forceinline__ long long block_sum_ll(long long v, long long* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  long long s = 0;
+  if (threadIdx.x == 0)
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) s += red[k];
+  return s;  // valid in thread 0
+}
+
+// Stable partition of each chunk into idx_out + node ids + leaf sums.
+__global__ __launch_bounds__(256) void part_scatter_kernel(
+    const uint8_t* __restrict__ codes, int64_t npad, const int* __restrict__ idx, int* __restrict__ idx_out,
+    int* __restrict__ nid, int write_nid, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
+    const int* __restrict__ pc_first, const int* __restrict__ pc_off, const int* __restrict__ node_nl,
+    const int* __restrict__ ctl, const PartInfo* __restrict__ part, int nbt, const float* __restrict__ g,
+    const float* __restrict__ h, const float* __restrict__ w, const double* __restrict__ qs, int cap,
+    unsigned long long* __restrict__ leaf_acc) {
+  __shared__ int wl[4];
+  __shared__ long long red[4];
+  const int n = ctl[CTL_N];
+  const int c = blockIdx.x;
+  if (c >= pc_first[n]) return;
+  const int node = chunk_node(pc_first, n, c);
+  const PartInfo pi = part[node];
+  const int start = seg_start[node];
+  const int lo = start + (c - pc_first[node]) * PC_ROWS;
+  const int hi = min(lo + PC_ROWS, start + seg_cnt[node]);
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const bool inner = pi.child >= 0 && !pi.leaf_children;
+  const bool retire = !inner;  // leaf here (no split) or children are leaves
+  long long sg[2] = {0, 0}, sh[2] = {0, 0}, sw[2] = {0, 0};
+  const float lg = leaf_acc ? (float)qs[4] : 0.f, lh = leaf_acc ? (float)qs[5] : 0.f,
+              lw = leaf_acc ? (float)qs[6] : 0.f;
+  int base_l = inner ? pc_off[c] : 0;
+  int base_r = inner ? (lo - start) - base_l : 0;
+  const int nl = inner ? node_nl[node] : 0;
+  for (int j0 = lo; j0 < hi; j0 += blockDim.x) {
+    const int j = j0 + t;
+    const bool valid = j < hi;
+    int r = 0, dir = 0;
+    if (valid) {
+      r = idx ? idx[j] : j;
+      if (pi.child >= 0) dir = split_dir(codes, npad, pi, nbt, r);
+    }
+    if (inner) {
+      const bool goes_left = valid && dir == 0;
+      const unsigned long long bl = __ballot(goes_left);
+      const unsigned long long bv = __ballot(valid);
+      if (lane == 0) wl[wid] = __popcll(bl) | (__popcll(bv) << 16);
+      __syncthreads();
+      int before_l = 0, before_v = 0, tot_l = 0, tot_v = 0;
+      for (int k = 0; k < 4; ++k) {
+        const int a = wl[k] & 0xFFFF, v = wl[k] >> 16;
+        if (k < wid) { before_l += a; before_v += v; }
+        tot_l += a; tot_v += v;
+      }
+      const unsigned long long lt = (1ull << lane) - 1ull;
+      const int my_l = before_l + __popcll(bl & lt);
+      const int my_v = before_v + __popcll(bv & lt);
+      if (valid) {
+        const int pos = goes_left ? base_l + my_l : nl + base_r + (my_v - my_l);
+        idx_out[start + pos] = r;
+        if (write_nid) nid[r] = pi.child + dir;
+      }
+      base_l += tot_l;
+      base_r += tot_v - tot_l;
+      __syncthreads();
+    } else if (valid) {
+      const int leaf = (pi.child >= 0) ? pi.child_gid + dir : pi.gid;
+      nid[r] = ~leaf;
+      if (leaf_acc && leaf < cap) {
+        const float wv = w ? w[r] : 1.0f;
+        if (wv != 0.0f) {
+          sg[dir] += __float2int_rn(g[r] * lg);
+          sh[dir] += __float2int_rn(h[r] * lh);
+          sw[dir] += __float2int_rn(wv * lw);
+        }
+      }
+    }
+  }
+  if (retire && leaf_acc) {
+    const int nleaf = (pi.child >= 0) ? 2 : 1;
+    for (int d = 0; d < nleaf; ++d) {
+      const int leaf = (pi.child >= 0) ? pi.child_gid + d : pi.gid;
+      const long long a = block_sum_ll(sg[d], red);
+      const long long b = block_sum_ll(sh[d], red);
+      const long long e = block_sum_ll(sw[d], red);
+      if (t == 0 && leaf < cap) {
+        if (a) atomicAdd(leaf_acc + 3 * leaf, (unsigned long long)a);
+        if (b) atomicAdd(leaf_acc + 3 * leaf + 1, (unsigned long long)b);
+        if (e) atomicAdd(leaf_acc + 3 * leaf + 2, (unsigned long long)e);
+      }
+    }
+  }
+}
+
+// --- C ABI of the segmented pipeline -----------------------------------------
+H2OMX_API int h2omx_pc_rows() { return PC_ROWS; }
+
+H2OMX_API int h2omx_tree_begin_seg(const unsigned int* stat_max, int mode, int max_rows_per_wg, double* qscale,
+                                   int* ctl0, void* link0, unsigned long long* leaf_acc, int leaf_n,
+                                   long long* built, int built_n, int n_rows, int hc_rows, int* seg_start,
+                                   int* seg_cnt, int* hc_first, int* pc_first, int* slot_node, hipStream_t stream) {
+  if (max_rows_per_wg < 1 || max_rows_per_wg > ROWS_CAP || hc_rows > max_rows_per_wg) return kBadArg;
+  const double qg = exp2(floor(log2(1073741824.0 / max_rows_per_wg)));
+  const double qsr = exp2(floor(log2(2147483648.0 / max_rows_per_wg)));
+  const int m = leaf_n > built_n ? leaf_n : built_n;
+  hipLaunchKernelGGL(tree_begin_seg_kernel, dim3(grid_for(m, 256, 1024)), dim3(256), 0, stream, stat_max, mode, qg,
+                     qsr, qscale, ctl0, reinterpret_cast<NodeLink*>(link0), leaf_acc, leaf_n, built, built_n, n_rows,
+                     hc_rows, seg_start, seg_cnt, hc_first, pc_first, slot_node);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_hist_build_seg(const uint8_t* codes_rm, int fp, const int* idx, const float* g, const float* s2,
+                                   const int* seg_start, const int* seg_cnt, const int* hc_first, const int* ctl,
+                                   const int* nvb, const double* qscale, int salt, int F, int nbt, int fg,
+                                   int n_groups, int hc_rows, int max_chunks, int threads,
+                                   unsigned long long* slab, hipStream_t stream) {
+  if (fg > 256 || threads > 512 || threads % 64 || threads < fg || fp % 4 || (n_groups > 1 && fg % 4) ||
+      hc_rows > ROWS_CAP)
+    return kBadArg;
+  const size_t lds = (size_t)fg * nbt * sizeof(unsigned long long);
+  if (lds > 156 * 1024) return kBadArg;
+  const int grid = ((max_chunks + 7) / 8) * 8 * n_groups;
+#define H2OMX_HBS(NB)                                                                                        \
+  hipLaunchKernelGGL(hist_build_seg_kernel<NB>, dim3(grid), dim3(threads), lds, stream, codes_rm, fp, idx, g, s2, \
+                     seg_start, seg_cnt, hc_first, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, hc_rows, slab)
+  switch (nbt) {
+    case 32: H2OMX_HBS(32); break;
+    case 64: H2OMX_HBS(64); break;
+    case 128: H2OMX_HBS(128); break;
+    case 256: H2OMX_HBS(256); break;
+    default: return kBadArg;
+  }
+#undef H2OMX_HBS
+  return launch_status();
+}
+
+H2OMX_API int h2omx_hist_reduce_seg(const unsigned long long* slab, const int* hc_first, const int* slot_node,
+                                    const int* ctl, int F, int nbt, int fg, int n_groups, int max_slots, int ksplit,
+                                    long long* built, hipStream_t stream) {
+  if (ksplit < 1 || max_slots < 1) return kBadArg;
+  dim3 grid((F * nbt + 255) / 256, max_slots, ksplit);
+  hipLaunchKernelGGL(hist_reduce_seg_kernel, grid, dim3(256), 0, stream, slab, hc_first, slot_node, ctl, F, nbt, fg,
+                     n_groups, built);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_part_count(const uint8_t* codes, int64_t npad, const int* idx, const int* seg_start,
+                               const int* seg_cnt, const int* pc_first, const int* ctl, const void* part, int nbt,
+                               int max_chunks, int* pc_left, hipStream_t stream) {
+  hipLaunchKernelGGL(part_count_kernel, dim3(max_chunks), dim3(256), 0, stream, codes, npad, idx, seg_start, seg_cnt,
+                     pc_first, ctl, reinterpret_cast<const PartInfo*>(part), nbt, pc_left);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_level_close(const int* ctl, const int* ctl_next, const void* part, const void* link_next,
+                                const int* seg_start, const int* seg_cnt, const int* pc_first, int* pc_left,
+                                int* node_nl, int* nseg_start, int* nseg_cnt, int* nhc_first, int* npc_first,
+                                int* nslot_node, int hc_rows, long long* nbuilt, int per_slot, hipStream_t stream) {
+  hipLaunchKernelGGL(level_close_kernel, dim3(1), dim3(1024), 0, stream, ctl, ctl_next,
+                     reinterpret_cast<const PartInfo*>(part), reinterpret_cast<const NodeLink*>(link_next), seg_start,
+                     seg_cnt, pc_first, pc_left, node_nl, nseg_start, nseg_cnt, nhc_first, npc_first, nslot_node,
+                     hc_rows, nbuilt, per_slot);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_part_scatter(const uint8_t* codes, int64_t npad, const int* idx, int* idx_out, int* nid,
+                                 int write_nid, const int* seg_start, const int* seg_cnt, const int* pc_first,
+                                 const int* pc_off, const int* node_nl, const int* ctl, const void* part, int nbt,
+                                 const float* g, const float* h, const float* w, const double* qscale, int cap,
+                                 unsigned long long* leaf_acc, int max_chunks, hipStream_t stream) {
+  hipLaunchKernelGGL(part_scatter_kernel, dim3(max_chunks), dim3(256), 0, stream, codes, npad, idx, idx_out, nid,
+                     write_nid, seg_start, seg_cnt, pc_first, pc_off, node_nl, ctl,
+                     reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc);
   return launch_status();
 }

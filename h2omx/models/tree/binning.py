@@ -37,6 +37,23 @@ class BinnedMatrix:
     def device(self):
         return self.codes.device
 
+    _codes_rm: torch.Tensor | None = None
+
+    @property
+    def fp(self) -> int:
+        """Row stride of the row-major codes (F rounded up to 4 bytes)."""
+        return (self.F + 3) // 4 * 4
+
+    @property
+    def codes_rm(self) -> torch.Tensor:
+        """Row-major copy uint8 [n][fp] (lazily built once): the segmented
+        histogram kernel gathers whole rows (28 B for HIGGS) by row index."""
+        if self._codes_rm is None:
+            rm = torch.zeros((self.n, self.fp), dtype=torch.uint8, device=self.codes.device)
+            rm[:, : self.F] = self.codes[:, : self.n].t()
+            self._codes_rm = rm
+        return self._codes_rm
+
     def edges_numpy(self):
         e = self.edges.cpu().numpy()
         nv = self.nvb.cpu().numpy()

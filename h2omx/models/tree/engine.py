@@ -71,6 +71,9 @@ class HipTreeBuilder:
     ROWS_PER_LANE = int(os.environ.get("H2OMX_HIST_ROWS", "16"))
     ROWS_CAP = 32768           # rows per workgroup chunk (fixed-point headroom, see kernel)
     SYNC_NODE_CAP = 4096       # above this many potential nodes the host reads the real count
+    SEG_TARGET_CHUNKS = 1024   # level-0 histogram chunks (2 resident 57 KB workgroups per CU)
+    SEG_LDS_BUDGET = 64 * 1024
+    SEG_MAX_SLOTS = int(os.environ.get("H2OMX_SEG_MAX_SLOTS", "256"))  # deeper: scan histogram kernel
 
     def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
         if not bm.codes.is_cuda:
@@ -109,6 +112,24 @@ class HipTreeBuilder:
         units = bm.npad // self.ROWS_PER_LANE
         cands = [self.plan_level(1 << k) for k in range(0, 13)] + [self.plan_level(1 << 20)]
         self.max_rows_per_wg = max(self.ROWS_PER_LANE * math.ceil(units / c["wgpg"]) for c in cands)
+        # segmented (row-partitioned) engine: default; H2OMX_TREE_ENGINE=scan selects
+        # the scan engine for A/B runs
+        self.segmented = os.environ.get("H2OMX_TREE_ENGINE", "seg") != "scan"
+        if self.segmented:
+            self.pc_rows = int(self.lib.h2omx_pc_rows())
+            hc = int(os.environ.get("H2OMX_SEG_CHUNK", "0")) or -(-bm.n // self.SEG_TARGET_CHUNKS)
+            self.hc_rows = min(self.ROWS_CAP, max(2048, -(-hc // 256) * 256))
+            self.max_rows_per_wg = max(self.max_rows_per_wg, self.hc_rows)
+            budget = self.SEG_LDS_BUDGET
+            fg = max(1, min(self.F, budget // (self.nbt * 8)))
+            groups = math.ceil(self.F / fg)
+            if groups > 1:
+                fg = max(4, (math.ceil(self.F / groups) + 3) // 4 * 4)
+                groups = math.ceil(self.F / fg)
+            self.seg_fg, self.seg_groups = fg, groups
+            self.seg_threads = 512
+            self.codes_rm = bm.codes_rm
+            self.idx = [torch.empty((max(bm.n, 1),), dtype=torch.int32, device=d) for _ in range(2)]
 
     # -- buffers -----------------------------------------------------------
     def _buf(self, name: str, numel: int, dtype) -> torch.Tensor:
@@ -177,6 +198,8 @@ class HipTreeBuilder:
         Returns the device tree buffer (``TREE_NODE_DTYPE`` heap of capacity
         nodes; unreachable records are garbage).  ``self.stat_max`` must hold
         this tree's gradient maxima (see :meth:`reduce_stats`)."""
+        if self.segmented:
+            return self._build_seg(g, h, w, tree_index, tree_fmask)
         lib, bm, p = self.lib, self.bm, self.p
         st = ops.stream(self.dev)
         P = ops.P
@@ -255,6 +278,139 @@ class HipTreeBuilder:
         if self.leaf_slab is not None:
             ops.check(lib.h2omx_leaf_reduce(P(self.leaf_slab), n_part * self.part_blocks, self.capacity,
                                             P(self.leaf_acc), st), "leaf_reduce")
+        if comm is not None:
+            comm.all_reduce_(self.leaf_acc)
+        ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(self.ctl[max_depth % 2]), P(self.qscale), spp,
+                                          P(self.tree_buf), self.capacity, st), "leaf_finalize")
+        return self.tree_buf
+
+    def _build_seg(self, g, h, w, tree_index, tree_fmask):
+        """Row-partitioned level pipeline (csrc/tree_kernels.hip, "segmented"
+        section): each level reads only the rows of the nodes it builds."""
+        lib, bm, p = self.lib, self.bm, self.p
+        st = ops.stream(self.dev)
+        P = ops.P
+        F, nbt, n = self.F, self.nbt, bm.n
+        spp = self._params(tree_index)
+        sp = self._sp
+        comm = self.comm if (self.comm is not None and self.comm.world_size > 1) else None
+        if comm is not None:
+            comm.all_reduce_(self.stat_max, "max")
+        s2 = w if p.mode == 0 else h
+        B = self._buf
+        i32 = torch.int32
+        link = [B("link0", 4, i32), None]
+        seg = [[B(f"seg_start{k}", 2, i32), B(f"seg_cnt{k}", 2, i32), B(f"hc_first{k}", 3, i32),
+                B(f"pc_first{k}", 3, i32), B(f"slot_node{k}", 2, i32)] for k in (0, 1)]
+        built = B("built", self.per_node, torch.int64)
+        ops.check(lib.h2omx_tree_begin_seg(P(self.stat_max), p.mode, self.max_rows_per_wg, P(self.qscale),
+                                           P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(),
+                                           P(built), self.per_node, n, self.hc_rows, P(seg[0][0]), P(seg[0][1]),
+                                           P(seg[0][2]), P(seg[0][3]), P(seg[0][4]), st), "tree_begin_seg")
+        full_prev = None
+        max_depth = p.max_depth
+        max_nodes = 1
+        idx_in = None
+        built_zeroed = True          # tree_begin_seg zeroed level 0's histogram
+        hc_cap = -(-n // self.hc_rows)
+        pc_cap = -(-n // self.pc_rows)
+        for d in range(max_depth):
+            cur, nxt = d % 2, (d + 1) % 2
+            ctl_cur, ctl_nxt = self.ctl[cur], self.ctl[nxt]
+            if max_nodes > self.SYNC_NODE_CAP:
+                n_now, s_now = [int(v) for v in ctl_cur[:2].tolist()]
+                self.stats["host_syncs"] += 1
+                if n_now == 0:
+                    break
+                max_nodes, max_slots = n_now, s_now
+            else:
+                max_slots = 1 if d == 0 else max(1, max_nodes // 2)
+            last = d == max_depth - 1
+            seg_start, seg_cnt, hc_first, pc_first, slot_node = seg[cur]
+            seg_hist = max_slots <= self.SEG_MAX_SLOTS
+            built = B("built", max_slots * self.per_node, torch.int64)
+            if seg_hist and not built_zeroed:
+                built[: max_slots * self.per_node].zero_()
+            built_zeroed = False
+            if seg_hist:
+                max_hc = hc_cap + max_slots
+                slab = B("seg_slab", max_hc * self.seg_groups * self.seg_fg * nbt, torch.int64)
+                ops.check(lib.h2omx_hist_build_seg(P(self.codes_rm), bm.fp, P(idx_in), P(g), P(s2), P(seg_start),
+                                                   P(seg_cnt), P(hc_first), P(ctl_cur), P(bm.nvb), P(self.qscale),
+                                                   tree_index & 0x7FFFFFFF, F, nbt, self.seg_fg, self.seg_groups,
+                                                   self.hc_rows, max_hc, self.seg_threads, P(slab), st),
+                          "hist_build_seg")
+                ksplit = max(1, min(32, 4096 // max(1, max_slots * ((F * nbt + 255) // 256))))
+                ksplit = max(ksplit, 4)
+                ops.check(lib.h2omx_hist_reduce_seg(P(slab), P(hc_first), P(slot_node), P(ctl_cur), F, nbt,
+                                                    self.seg_fg, self.seg_groups, max_slots, ksplit, P(built), st),
+                          "hist_reduce_seg")
+            else:
+                plan = self.plan_level(max_slots)
+                hist_elems = plan["slot_cnt"] * plan["fg"] * nbt
+                partials = B("partials", plan["n_groups"] * plan["wgpg"] * hist_elems, torch.int64)
+                for ps in range(plan["passes"]):
+                    slot_lo = ps * plan["slot_cnt"]
+                    ops.check(lib.h2omx_hist_build(P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]),
+                                                   P(ctl_cur), P(bm.nvb), P(self.qscale), tree_index & 0x7FFFFFFF,
+                                                   F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo,
+                                                   plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],
+                                                   P(partials), st), "hist_build")
+                    ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F, nbt,
+                                                    slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st),
+                              "hist_reduce")
+            if comm is not None:
+                comm.all_reduce_(built[: max_slots * self.per_node])
+            full_cur = None if last else B(f"full{cur}", max_nodes * self.per_node, torch.int64)
+            fbest = B("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
+            sp.depth = d
+            sp.children_leaves = 1 if last else 0
+            ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
+                                           P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
+                                           P(fbest), st), "split_find")
+            next_nodes = 2 * max_nodes
+            part = B("part", max_nodes * PART_INFO_BYTES // 4, i32)
+            nl = None
+            if not last:
+                nl = B(f"link{nxt}", next_nodes * NODE_LINK_BYTES // 4, i32)
+                link[nxt] = nl
+            nsplit = B("nsplit", max_nodes * 9, torch.float64)
+            ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges), P(bm.nvb), nbt,
+                                               next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
+                                               P(nsplit), max_nodes, st), "level_finalize")
+            max_pc = pc_cap + max_nodes
+            pc_left = B("pc_left", max_pc, i32)
+            node_nl = B("node_nl", 2 * max_nodes, i32)
+            idx_out = None
+            write_nid = 0
+            if not last:
+                nstart, ncnt, nhc, npc, nslot = seg[nxt]
+                nstart = seg[nxt][0] = B(f"seg_start{nxt}", next_nodes, i32)
+                ncnt = seg[nxt][1] = B(f"seg_cnt{nxt}", next_nodes, i32)
+                nhc = seg[nxt][2] = B(f"hc_first{nxt}", next_nodes + 1, i32)
+                npc = seg[nxt][3] = B(f"pc_first{nxt}", next_nodes + 1, i32)
+                nslot = seg[nxt][4] = B(f"slot_node{nxt}", max(1, max_nodes), i32)
+                next_seg_hist = max_nodes <= self.SEG_MAX_SLOTS and next_nodes <= self.SYNC_NODE_CAP
+                write_nid = 0 if next_seg_hist else 1
+                nbuilt = None
+                if next_seg_hist:
+                    nbuilt = B("built", max_nodes * self.per_node, torch.int64)
+                    built_zeroed = True
+                ops.check(lib.h2omx_part_count(P(bm.codes), bm.npad, P(idx_in), P(seg_start), P(seg_cnt),
+                                               P(pc_first), P(ctl_cur), P(part), nbt, max_pc, P(pc_left), st),
+                          "part_count")
+                ops.check(lib.h2omx_level_close(P(ctl_cur), P(ctl_nxt), P(part), P(nl), P(seg_start), P(seg_cnt),
+                                                P(pc_first), P(pc_left), P(node_nl), P(nstart), P(ncnt), P(nhc),
+                                                P(npc), P(nslot), self.hc_rows, P(nbuilt), self.per_node, st),
+                          "level_close")
+                idx_out = self.idx[d % 2]
+            ops.check(lib.h2omx_part_scatter(P(bm.codes), bm.npad, P(idx_in), P(idx_out), P(self.nid), write_nid,
+                                             P(seg_start), P(seg_cnt), P(pc_first), P(pc_left), P(node_nl),
+                                             P(ctl_cur), P(part), nbt, P(g), P(h), P(w), P(self.qscale),
+                                             self.capacity, P(self.leaf_acc), max_pc, st), "part_scatter")
+            idx_in = idx_out
+            full_prev = full_cur
+            max_nodes = next_nodes
         if comm is not None:
             comm.all_reduce_(self.leaf_acc)
         ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(self.ctl[max_depth % 2]), P(self.qscale), spp,

@@ -35,6 +35,13 @@ TREE_SIGS = {
     "h2omx_leaf_finalize": "PPPPPIS",
     "h2omx_predict_raw": "PLLPPIIPLS",
     "h2omx_predict_binned": "PLLPPIIIPLS",
+    "h2omx_pc_rows": "",
+    "h2omx_tree_begin_seg": "PIIPPPPIPIIIPPPPPS",
+    "h2omx_hist_build_seg": "PIPPPPPPPPPIIIIIIIIPS",
+    "h2omx_hist_reduce_seg": "PPPPIIIIIIPS",
+    "h2omx_part_count": "PLPPPPPPIIPS",
+    "h2omx_level_close": "PPPPPPPPPPPPPPIPIS",
+    "h2omx_part_scatter": "PLPPPIPPPPPPPIPPPPIPIS",
 }
 
 DENSE_SIGS = {

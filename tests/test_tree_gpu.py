@@ -123,3 +123,33 @@ def test_deep_tree_multipass(cuda_dev):
     from sklearn.metrics import roc_auc_score
     assert abs(roc_auc_score(y, mc) - roc_auc_score(y, mg)) < 5e-3
     assert (np.abs(mc - mg) < 1e-3).mean() > 0.7
+
+
+@pytest.mark.parametrize("dist,depth,sample_rate,nbins", [("bernoulli", 5, 1.0, 255), ("bernoulli", 8, 0.7, 63),
+                                                          ("gaussian", 6, 1.0, 20), ("multinomial", 4, 1.0, 255),
+                                                          ("drf", 12, 0.632, 20)])
+def test_segmented_engine_matches_scan_engine(cuda_dev, monkeypatch, dist, depth, sample_rate, nbins):
+    """The row-partitioned engine builds bit-identical trees to the scan engine:
+    both quantise every row with the same dither and sum integers."""
+    import h2omx.models.tree.engine as E
+
+    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi", "drf": "bin"}[dist]
+    X, y = _data(n=40000, F=9, seed=3, task=task)
+    _, bg = _both(X, y, nbins)
+    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2,
+                    leaf_mode=1 if dist == "drf" else 0, mtries=3 if dist == "drf" else 0)
+    yt = torch.from_numpy(y).cuda()
+    nclass = 3 if dist == "multinomial" else (2 if dist == "drf" else 1)
+    out = {}
+    for eng in ("scan", "seg"):
+        monkeypatch.setenv("H2OMX_TREE_ENGINE", eng)
+        if eng == "seg":
+            monkeypatch.setattr(E.HipTreeBuilder, "SEG_MAX_SLOTS", 8)   # also exercise the mixed path
+        out[eng] = train_ensemble(bg, yt, dist=dist, ntrees=4, tparams=tp, sample_rate=sample_rate, nclass=nclass,
+                                  seed=11)
+    a, b = out["scan"], out["seg"]
+    for t in range(a.trees.shape[0]):
+        for i in a.compact()[t]:
+            assert a.trees[t][i]["feat"] == b.trees[t][i]["feat"], (t, i)
+            assert a.trees[t][i]["bin"] == b.trees[t][i]["bin"], (t, i)
+            np.testing.assert_allclose(a.trees[t][i]["value"], b.trees[t][i]["value"], rtol=1e-6, atol=1e-7)
