@@ -320,6 +320,155 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
   }
 }
 
+// Same histogram, for levels where only part of the rows belong to the
+// nodes being built (smaller children: <= 50 % of the rows, fewer per slot
+// pass).  hist_build_kernel issues one wave-level LDS atomic per (16-row
+// slot, feature) whenever ANY lane holds a live row, so a half-empty wave
+// costs as much LDS issue time as a full one (the kernel is LDS-issue bound:
+// SQ_WAIT_INST_LDS ~ SQ_BUSY_CYCLES, profiles/pmc1_summary.txt).  Here each
+// wave streams its rows 64 at a time, keeps the live ones in a register
+// queue (ballot + k-th-set-bit lane selection + ds_bpermute pulls) and
+// issues the fg feature atomics only for full batches of 64 live rows.
+// Quantisation and dither are identical to hist_build_kernel, so the
+// integer histograms are bit-identical.
+__device__ __forceinline__ int kth_set_bit(unsigned long long m, int k) {
+  int pos = 0;
+  int c = __popc((uint32_t)m);
+  if (k >= c) { k -= c; m >>= 32; pos += 32; }
+  c = __popc((uint32_t)m & 0xFFFFu);
+  if (k >= c) { k -= c; m >>= 16; pos += 16; }
+  c = __popc((uint32_t)m & 0xFFu);
+  if (k >= c) { k -= c; m >>= 8; pos += 8; }
+  c = __popc((uint32_t)m & 0xFu);
+  if (k >= c) { k -= c; m >>= 4; pos += 4; }
+  c = __popc((uint32_t)m & 0x3u);
+  if (k >= c) { k -= c; m >>= 2; pos += 2; }
+  c = (int)(m & 1ull);
+  if (k >= c) pos += 1;
+  return pos;
+}
+
+template <int NBT>
+__global__ __launch_bounds__(1024) void hist_build_compact_kernel(
+    const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ s2,
+    const int* __restrict__ nid, const NodeLink* __restrict__ link, const int* __restrict__ ctl,
+    const int* __restrict__ nvb, const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups,
+    int wgpg, int slot_lo, int slot_cnt, int rows_per_unit, unsigned long long* __restrict__ partials) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
+  __shared__ int width_s[256], rep_s[256];
+  const int n_slots = ctl[CTL_SLOTS];
+  if (slot_lo >= n_slots) return;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, i = b >> 3;
+  const int group = i % n_groups;
+  const int chunk = xcd + 8 * (i / n_groups);
+  const int f0 = group * fg;
+  const int nf = min(fg, F - f0);
+  const int hist_elems = slot_cnt * fg * NBT;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) lds64[j] = 0ull;
+  if (threadIdx.x < fg) {
+    const int fi = threadIdx.x;
+    const int w = (fi < nf) ? nvb[f0 + fi] + 1 : NBT;
+    width_s[fi] = w;
+    int r = NBT / w;
+    rep_s[fi] = r < 1 ? 1 : (r > 64 ? 64 : r);
+  }
+  const float sg = (float)qscale[0], ss = (float)qscale[1];
+  __syncthreads();
+  // this workgroup's rows (same chunking as hist_build_kernel), split over waves
+  const int64_t units = npad / rows_per_unit;
+  const int64_t u0 = units * chunk / wgpg, u1 = units * (chunk + 1) / wgpg;
+  const int64_t row0 = u0 * rows_per_unit, row1 = u1 * rows_per_unit;
+  const int64_t per = ((row1 - row0 + nwaves - 1) / nwaves + 63) / 64 * 64;
+  const int64_t wr0 = row0 + wid * per, wr1 = min(row1, wr0 + per);
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int p_row = 0, p_slot = 0;
+  unsigned long long p_pk = 0ull;
+  int pend = 0;
+  auto flush = [&](int nact) {
+    const bool on = lane < nact;
+    const int64_t ro = p_row;
+    unsigned long long* hb = lds64 + p_slot * fg * NBT;
+    for (int fi = 0; fi < nf; ++fi) {
+      if (on) {
+        int bin = codes[(int64_t)(f0 + fi) * npad + ro];
+        const int width = width_s[fi], rep = rep_s[fi];
+        if (bin == NBT - 1) bin = width - 1;
+        const int copy_off = (rep > 1) ? (lane % rep) * width : 0;
+        atomicAdd(hb + fi * NBT + copy_off + bin, p_pk);
+      }
+    }
+  };
+  for (int64_t base = wr0; base < wr1; base += 64) {
+    const int64_t r = base + lane;
+    int sl = -1;
+    unsigned long long pk = 0ull;
+    if (r < wr1) {
+      const int nd = nid[r];
+      if (nd >= 0) {
+        sl = link[nd].slot - slot_lo;
+        if (sl >= slot_cnt) sl = -1;
+      }
+      if (sl >= 0) {
+        const uint32_t hsh = row_hash(r, salt);
+        const float d1 = (hsh & 0xFFFF) * (1.0f / 65536.0f), d2 = (hsh >> 16) * (1.0f / 65536.0f);
+        const float sv = s2 ? s2[r] : 1.0f;
+        const int gq = (int)floorf(fmaf(g[r], sg, d1));
+        const uint32_t sq = (uint32_t)floorf(fmaf(sv, ss, d2));
+        pk = ((unsigned long long)(uint32_t)gq << 32) | (unsigned long long)sq;
+        if (pk == 0ull) sl = -1;
+      }
+    }
+    const unsigned long long m = __ballot(sl >= 0);
+    const int cnt = __popcll(m);
+    if (cnt == 0) continue;
+    const int my_row = (int)r;
+    const int total = pend + cnt;
+    // lanes [pend, min(total, 64)) receive new entries k = lane - pend
+    {
+      const int k = lane - pend;
+      const bool take = lane >= pend && k < cnt;
+      const int src = take ? kth_set_bit(m, k) : lane;
+      const int nr = __shfl(my_row, src, 64);
+      const int ns = __shfl(sl, src, 64);
+      const unsigned long long npk = __shfl(pk, src, 64);
+      if (take) { p_row = nr; p_slot = ns; p_pk = npk; }
+    }
+    if (total >= 64) {
+      flush(64);
+      const int rem = total - 64;
+      const int k = (64 - pend) + lane;
+      const bool take = lane < rem;
+      const int src = take ? kth_set_bit(m, k) : lane;
+      const int nr = __shfl(my_row, src, 64);
+      const int ns = __shfl(sl, src, 64);
+      const unsigned long long npk = __shfl(pk, src, 64);
+      if (take) { p_row = nr; p_slot = ns; p_pk = npk; }
+      pend = rem;
+    } else {
+      pend = total;
+    }
+    (void)lt;
+  }
+  if (pend > 0) flush(pend);
+  __syncthreads();
+  unsigned long long* out = partials + (int64_t)(group * wgpg + chunk) * hist_elems;
+  for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) {
+    const int bin = j % NBT;
+    const int fi = (j / NBT) % fg;
+    const int sl2 = j / (NBT * fg);
+    const int width = width_s[fi], rep = rep_s[fi];
+    const int src = (bin == NBT - 1) ? width - 1 : bin;
+    unsigned long long acc = 0ull;
+    if (src < width - 1 || bin == NBT - 1) {
+      const unsigned long long* hb = lds64 + (sl2 * fg + fi) * NBT;
+      for (int c = 0; c < rep; ++c) acc += hb[c * width + src];
+    }
+    out[j] = acc;
+  }
+}
+
 // Sum the per-workgroup slabs of one pass into exact int64 histograms
 // built[slot][F][2][NBT] (plane 0: G_q, plane 1: S_q).
 // Each 256-thread block owns 32 consecutive output bins and splits the
@@ -1137,6 +1286,34 @@ H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* 
     return kBadArg;
   }
 #undef H2OMX_HB
+  return launch_status();
+}
+
+H2OMX_API int h2omx_hist_build_compact(const uint8_t* codes, int64_t npad, const float* g, const float* s2,
+                                       const int* nid, const void* link, const int* ctl, const int* nvb,
+                                       const double* qscale, int salt, int F, int nbt, int fg, int n_groups, int wgpg,
+                                       int slot_lo, int slot_cnt, int rows_per_lane, int threads,
+                                       unsigned long long* partials, hipStream_t stream) {
+  if (wgpg % 8 != 0 || npad % 16 != 0 || fg > 256 || threads % 64 != 0 || threads > 1024 || threads < fg)
+    return kBadArg;
+  const int64_t units = npad / rows_per_lane;
+  if ((units + wgpg - 1) / wgpg * rows_per_lane > ROWS_CAP) return kBadArg;
+  const size_t lds = (size_t)slot_cnt * fg * nbt * sizeof(unsigned long long);
+  if (lds > 156 * 1024) return kBadArg;
+  const int grid = n_groups * wgpg;
+  const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
+#define H2OMX_HBC(NB)                                                                                         \
+  hipLaunchKernelGGL((hist_build_compact_kernel<NB>), dim3(grid), dim3(threads), lds, stream, codes, npad, g, s2, \
+                     nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt,          \
+                     rows_per_lane, partials)
+  switch (nbt) {
+    case 32: H2OMX_HBC(32); break;
+    case 64: H2OMX_HBC(64); break;
+    case 128: H2OMX_HBC(128); break;
+    case 256: H2OMX_HBC(256); break;
+    default: return kBadArg;
+  }
+#undef H2OMX_HBC
   return launch_status();
 }
 

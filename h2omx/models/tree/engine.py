@@ -71,6 +71,7 @@ class HipTreeBuilder:
     ROWS_PER_LANE = int(os.environ.get("H2OMX_HIST_ROWS", "16"))
     ROWS_CAP = 32768           # rows per workgroup chunk (fixed-point headroom, see kernel)
     SYNC_NODE_CAP = 4096       # above this many potential nodes the host reads the real count
+    COMPACT = os.environ.get("H2OMX_HIST_COMPACT", "1") == "1"
     SEG_TARGET_CHUNKS = 1024   # level-0 histogram chunks (2 resident 57 KB workgroups per CU)
     SEG_LDS_BUDGET = 64 * 1024
     SEG_MAX_SLOTS = int(os.environ.get("H2OMX_SEG_MAX_SLOTS", "256"))  # deeper: scan histogram kernel
@@ -112,9 +113,12 @@ class HipTreeBuilder:
         units = bm.npad // self.ROWS_PER_LANE
         cands = [self.plan_level(1 << k) for k in range(0, 13)] + [self.plan_level(1 << 20)]
         self.max_rows_per_wg = max(self.ROWS_PER_LANE * math.ceil(units / c["wgpg"]) for c in cands)
-        # segmented (row-partitioned) engine: default; H2OMX_TREE_ENGINE=scan selects
-        # the scan engine for A/B runs
-        self.segmented = os.environ.get("H2OMX_TREE_ENGINE", "seg") != "scan"
+        # segmented (row-partitioned) engine, opt-in with H2OMX_TREE_ENGINE=seg: it
+        # builds bit-identical trees but measured slower on HIGGS-shape data
+        # (depth 5: 1.90 vs 1.52 ms/tree, profiles/seg_vs_scan_s1.txt) because its
+        # by-index gathers of codes / g / h and scattered node-id writes touch a
+        # cache line per row once nodes get sparse; kept for A/B work.
+        self.segmented = os.environ.get("H2OMX_TREE_ENGINE", "scan") == "seg"
         if self.segmented:
             self.pc_rows = int(self.lib.h2omx_pc_rows())
             hc = int(os.environ.get("H2OMX_SEG_CHUNK", "0")) or -(-bm.n // self.SEG_TARGET_CHUNKS)
@@ -236,12 +240,15 @@ class HipTreeBuilder:
             built = self._buf("built", max_slots * self.per_node, torch.int64)
             hist_elems = plan["slot_cnt"] * plan["fg"] * nbt
             partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_elems, torch.int64)
+            # level 0 streams every row; deeper levels touch only the built
+            # (smaller) children -> wave-compacted kernel keeps atomics dense
+            hb = lib.h2omx_hist_build_compact if (d > 0 and self.COMPACT) else lib.h2omx_hist_build
             for ps in range(plan["passes"]):
                 slot_lo = ps * plan["slot_cnt"]
-                ops.check(lib.h2omx_hist_build(P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]),
-                                               P(ctl_cur), P(bm.nvb), P(self.qscale), tree_index & 0x7FFFFFFF,
-                                               F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo,
-                                               plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"], P(partials), st),
+                ops.check(hb(P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]),
+                             P(ctl_cur), P(bm.nvb), P(self.qscale), tree_index & 0x7FFFFFFF,
+                             F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo,
+                             plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"], P(partials), st),
                           "hist_build")
                 ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F, nbt,
                                                 slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st), "hist_reduce")

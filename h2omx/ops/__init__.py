@@ -20,6 +20,7 @@ TREE_SIGS = {
     "h2omx_bin_features": "PLLIPPIPLS",
     "h2omx_hist_build": "PLPPPPPPPIIIIIIIIIIPS",
     "h2omx_hist_reduce": "PIIIIIIIPPS",
+    "h2omx_hist_build_compact": "PLPPPPPPPIIIIIIIIIIPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
     "h2omx_level_finalize": "PPPPPPIIPPPIPIS",
     "h2omx_partition": "PLPPIPPPPIPPS",

@@ -153,3 +153,25 @@ def test_segmented_engine_matches_scan_engine(cuda_dev, monkeypatch, dist, depth
             assert a.trees[t][i]["feat"] == b.trees[t][i]["feat"], (t, i)
             assert a.trees[t][i]["bin"] == b.trees[t][i]["bin"], (t, i)
             np.testing.assert_allclose(a.trees[t][i]["value"], b.trees[t][i]["value"], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("dist,depth,sample_rate", [("bernoulli", 6, 1.0), ("gaussian", 9, 0.7),
+                                                    ("multinomial", 4, 1.0)])
+def test_compact_hist_matches_plain(cuda_dev, monkeypatch, dist, depth, sample_rate):
+    """The wave-compacted histogram kernel produces bit-identical trees."""
+    import h2omx.models.tree.engine as E
+
+    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi"}[dist]
+    X, y = _data(n=50000, F=9, seed=5, task=task)
+    _, bg = _both(X, y, 255)
+    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2)
+    yt = torch.from_numpy(y).cuda()
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(E.HipTreeBuilder, "COMPACT", flag)
+        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
+                                   nclass=3 if dist == "multinomial" else 1, seed=7)
+    a, b = out[False], out[True]
+    assert np.array_equal(a.trees["feat"], b.trees["feat"])
+    assert np.array_equal(a.trees["bin"], b.trees["bin"])
+    np.testing.assert_array_equal(a.trees["value"], b.trees["value"])
