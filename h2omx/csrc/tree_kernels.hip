@@ -348,6 +348,9 @@ __device__ __forceinline__ int kth_set_bit(unsigned long long m, int k) {
   return pos;
 }
 
+constexpr int HC_UNROLL = 4;   // 64-row steps whose loads are issued together
+constexpr int HC_FB = 16;      // features whose codes are gathered before their atomics
+
 template <int NBT>
 __global__ __launch_bounds__(1024) void hist_build_compact_kernel(
     const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ s2,
@@ -376,80 +379,99 @@ __global__ __launch_bounds__(1024) void hist_build_compact_kernel(
   }
   const float sg = (float)qscale[0], ss = (float)qscale[1];
   __syncthreads();
-  // this workgroup's rows (same chunking as hist_build_kernel), split over waves
   const int64_t units = npad / rows_per_unit;
   const int64_t u0 = units * chunk / wgpg, u1 = units * (chunk + 1) / wgpg;
   const int64_t row0 = u0 * rows_per_unit, row1 = u1 * rows_per_unit;
-  const int64_t per = ((row1 - row0 + nwaves - 1) / nwaves + 63) / 64 * 64;
+  constexpr int STEP = 64 * HC_UNROLL;
+  const int64_t per = ((row1 - row0 + nwaves - 1) / nwaves + STEP - 1) / STEP * STEP;
   const int64_t wr0 = row0 + wid * per, wr1 = min(row1, wr0 + per);
-  const unsigned long long lt = (1ull << lane) - 1ull;
   int p_row = 0, p_slot = 0;
   unsigned long long p_pk = 0ull;
   int pend = 0;
+  const uint8_t* cbase = codes + (int64_t)f0 * npad;
   auto flush = [&](int nact) {
     const bool on = lane < nact;
-    const int64_t ro = p_row;
     unsigned long long* hb = lds64 + p_slot * fg * NBT;
-    for (int fi = 0; fi < nf; ++fi) {
-      if (on) {
-        int bin = codes[(int64_t)(f0 + fi) * npad + ro];
-        const int width = width_s[fi], rep = rep_s[fi];
-        if (bin == NBT - 1) bin = width - 1;
-        const int copy_off = (rep > 1) ? (lane % rep) * width : 0;
-        atomicAdd(hb + fi * NBT + copy_off + bin, p_pk);
+    for (int fb = 0; fb < nf; fb += HC_FB) {
+      int bins[HC_FB];
+#pragma unroll
+      for (int q = 0; q < HC_FB; ++q)
+        bins[q] = (on && fb + q < nf) ? (int)cbase[(int64_t)(fb + q) * npad + p_row] : 0;
+#pragma unroll
+      for (int q = 0; q < HC_FB; ++q) {
+        const int fi = fb + q;
+        if (on && fi < nf) {
+          const int width = width_s[fi], rep = rep_s[fi];
+          const int bin = (bins[q] == NBT - 1) ? width - 1 : bins[q];
+          const int copy_off = (rep > 1) ? (lane % rep) * width : 0;
+          atomicAdd(hb + fi * NBT + copy_off + bin, p_pk);
+        }
       }
     }
   };
-  for (int64_t base = wr0; base < wr1; base += 64) {
-    const int64_t r = base + lane;
-    int sl = -1;
-    unsigned long long pk = 0ull;
-    if (r < wr1) {
-      const int nd = nid[r];
-      if (nd >= 0) {
-        sl = link[nd].slot - slot_lo;
-        if (sl >= slot_cnt) sl = -1;
+  for (int64_t base = wr0; base < wr1; base += STEP) {
+    int sl[HC_UNROLL];
+    unsigned long long pk[HC_UNROLL];
+    int nd[HC_UNROLL];
+#pragma unroll
+    for (int u = 0; u < HC_UNROLL; ++u) {
+      const int64_t r = base + 64 * u + lane;
+      nd[u] = (r < wr1) ? nid[r] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < HC_UNROLL; ++u) {
+      int v = -1;
+      if (nd[u] >= 0) {
+        v = link[nd[u]].slot - slot_lo;
+        if (v >= slot_cnt) v = -1;
       }
-      if (sl >= 0) {
+      sl[u] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < HC_UNROLL; ++u) {
+      const int64_t r = base + 64 * u + lane;
+      pk[u] = 0ull;
+      if (sl[u] >= 0) {
         const uint32_t hsh = row_hash(r, salt);
         const float d1 = (hsh & 0xFFFF) * (1.0f / 65536.0f), d2 = (hsh >> 16) * (1.0f / 65536.0f);
         const float sv = s2 ? s2[r] : 1.0f;
         const int gq = (int)floorf(fmaf(g[r], sg, d1));
         const uint32_t sq = (uint32_t)floorf(fmaf(sv, ss, d2));
-        pk = ((unsigned long long)(uint32_t)gq << 32) | (unsigned long long)sq;
-        if (pk == 0ull) sl = -1;
+        pk[u] = ((unsigned long long)(uint32_t)gq << 32) | (unsigned long long)sq;
+        if (pk[u] == 0ull) sl[u] = -1;
       }
     }
-    const unsigned long long m = __ballot(sl >= 0);
-    const int cnt = __popcll(m);
-    if (cnt == 0) continue;
-    const int my_row = (int)r;
-    const int total = pend + cnt;
-    // lanes [pend, min(total, 64)) receive new entries k = lane - pend
-    {
-      const int k = lane - pend;
-      const bool take = lane >= pend && k < cnt;
-      const int src = take ? kth_set_bit(m, k) : lane;
-      const int nr = __shfl(my_row, src, 64);
-      const int ns = __shfl(sl, src, 64);
-      const unsigned long long npk = __shfl(pk, src, 64);
-      if (take) { p_row = nr; p_slot = ns; p_pk = npk; }
+#pragma unroll
+    for (int u = 0; u < HC_UNROLL; ++u) {
+      const unsigned long long m = __ballot(sl[u] >= 0);
+      const int cnt = __popcll(m);
+      if (cnt == 0) continue;
+      const int my_row = (int)(base + 64 * u + lane);
+      const int total = pend + cnt;
+      {
+        const int k = lane - pend;
+        const bool take = lane >= pend && k < cnt;
+        const int src = take ? kth_set_bit(m, k) : lane;
+        const int nr = __shfl(my_row, src, 64);
+        const int ns = __shfl(sl[u], src, 64);
+        const unsigned long long npk = __shfl(pk[u], src, 64);
+        if (take) { p_row = nr; p_slot = ns; p_pk = npk; }
+      }
+      if (total >= 64) {
+        flush(64);
+        const int rem = total - 64;
+        const int k = (64 - pend) + lane;
+        const bool take = lane < rem;
+        const int src = take ? kth_set_bit(m, k) : lane;
+        const int nr = __shfl(my_row, src, 64);
+        const int ns = __shfl(sl[u], src, 64);
+        const unsigned long long npk = __shfl(pk[u], src, 64);
+        if (take) { p_row = nr; p_slot = ns; p_pk = npk; }
+        pend = rem;
+      } else {
+        pend = total;
+      }
     }
-    if (total >= 64) {
-      flush(64);
-      const int rem = total - 64;
-      const int k = (64 - pend) + lane;
-      const bool take = lane < rem;
-      const int src = take ? kth_set_bit(m, k) : lane;
-      const int nr = __shfl(my_row, src, 64);
-      const int ns = __shfl(sl, src, 64);
-      const unsigned long long npk = __shfl(pk, src, 64);
-      if (take) { p_row = nr; p_slot = ns; p_pk = npk; }
-      pend = rem;
-    } else {
-      pend = total;
-    }
-    (void)lt;
   }
   if (pend > 0) flush(pend);
   __syncthreads();
@@ -863,10 +885,21 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
         if (leaf_acc && leaf < cap) {
           const float wv = w ? w[r0 + k] : 1.0f;
           if (wv != 0.0f) {
-            unsigned long long* dst = use_lds ? lcopy + 3 * leaf : leaf_acc + 3 * leaf;
-            atomicAdd(dst + 0, (unsigned long long)(long long)__float2int_rn(g[r0 + k] * lg));
-            atomicAdd(dst + 1, (unsigned long long)(long long)__float2int_rn(h[r0 + k] * lh));
-            atomicAdd(dst + 2, (unsigned long long)(long long)__float2int_rn(wv * lw));
+            const unsigned long long a = (unsigned long long)(long long)__float2int_rn(g[r0 + k] * lg);
+            const unsigned long long b = (unsigned long long)(long long)__float2int_rn(h[r0 + k] * lh);
+            const unsigned long long c = (unsigned long long)(long long)__float2int_rn(wv * lw);
+            // separate call sites: a pointer selected between LDS and global
+            // memory becomes a generic pointer and the atomics turn into slow
+            // FLAT atomics; here each branch keeps its address space (ds_add_u64)
+            if (use_lds) {
+              atomicAdd(lcopy + 3 * leaf + 0, a);
+              atomicAdd(lcopy + 3 * leaf + 1, b);
+              atomicAdd(lcopy + 3 * leaf + 2, c);
+            } else {
+              atomicAdd(leaf_acc + 3 * leaf + 0, a);
+              atomicAdd(leaf_acc + 3 * leaf + 1, b);
+              atomicAdd(leaf_acc + 3 * leaf + 2, c);
+            }
           }
         }
       }
@@ -1145,10 +1178,15 @@ __global__ __launch_bounds__(256) void leaf_stats_kernel(const int* __restrict__
     if (wv == 0.0f) continue;
     const long long gq = __float2int_rn(g[r] * (float)lg), hq = __float2int_rn(h[r] * (float)lh),
                     wq = __float2int_rn(wv * (float)lw);
-    unsigned long long* dst = use_lds ? lacc + 3 * leaf : acc + 3 * leaf;
-    atomicAdd(dst + 0, (unsigned long long)gq);
-    atomicAdd(dst + 1, (unsigned long long)hq);
-    atomicAdd(dst + 2, (unsigned long long)wq);
+    if (use_lds) {  // separate call sites keep ds_add_u64 (see partition_kernel)
+      atomicAdd(lacc + 3 * leaf + 0, (unsigned long long)gq);
+      atomicAdd(lacc + 3 * leaf + 1, (unsigned long long)hq);
+      atomicAdd(lacc + 3 * leaf + 2, (unsigned long long)wq);
+    } else {
+      atomicAdd(acc + 3 * leaf + 0, (unsigned long long)gq);
+      atomicAdd(acc + 3 * leaf + 1, (unsigned long long)hq);
+      atomicAdd(acc + 3 * leaf + 2, (unsigned long long)wq);
+    }
   }
   if (use_lds) {
     __syncthreads();
@@ -1365,12 +1403,13 @@ constexpr int PARTITION_BLOCKS = 4096;
 
 H2OMX_API int h2omx_partition(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt, const float* g,
                               const float* h, const float* w, const double* qscale, int cap,
-                              unsigned long long* leaf_acc, unsigned long long* leaf_slab, hipStream_t stream) {
-  if (npad % 8 != 0) return kBadArg;
+                              unsigned long long* leaf_acc, unsigned long long* leaf_slab, int blocks,
+                              hipStream_t stream) {
+  if (npad % 8 != 0 || blocks < 1 || blocks > PARTITION_BLOCKS) return kBadArg;
   const int R = (leaf_acc && cap <= 2048) ? std::max(1, std::min(16, 4096 / (3 * cap))) : 1;
   const size_t lds = (leaf_acc && cap <= 2048) ? (size_t)cap * 3 * R * sizeof(unsigned long long) : 0;
-  // fixed grid so the slab layout is known: [PARTITION_BLOCKS][3 * cap]
-  hipLaunchKernelGGL(partition_kernel, dim3(PARTITION_BLOCKS), dim3(256), lds, stream, codes, npad, nid,
+  // caller-chosen grid (<= PARTITION_BLOCKS) so the slab layout is known: [blocks][3 * cap]
+  hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(256), lds, stream, codes, npad, nid,
                      reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc,
                      (leaf_acc && cap <= 2048) ? leaf_slab : nullptr);
   return launch_status();

@@ -71,7 +71,10 @@ class HipTreeBuilder:
     ROWS_PER_LANE = int(os.environ.get("H2OMX_HIST_ROWS", "16"))
     ROWS_CAP = 32768           # rows per workgroup chunk (fixed-point headroom, see kernel)
     SYNC_NODE_CAP = 4096       # above this many potential nodes the host reads the real count
-    COMPACT = os.environ.get("H2OMX_HIST_COMPACT", "1") == "1"
+    # wave-compacted histogram kernel for levels > 0 (H2OMX_HIST_COMPACT=1): bit-identical
+    # but measured slower (byte gathers of column-major codes are TA-bound:
+    # depth-5 HIGGS 2.03 vs 1.52 ms/tree, profiles/compact_hist_p9.txt)
+    COMPACT = os.environ.get("H2OMX_HIST_COMPACT", "0") == "1"
     SEG_TARGET_CHUNKS = 1024   # level-0 histogram chunks (2 resident 57 KB workgroups per CU)
     SEG_LDS_BUDGET = 64 * 1024
     SEG_MAX_SLOTS = int(os.environ.get("H2OMX_SEG_MAX_SLOTS", "256"))  # deeper: scan histogram kernel
@@ -102,7 +105,8 @@ class HipTreeBuilder:
         self.stat_slab = torch.zeros((int(self.lib.h2omx_stat_blocks()) * 4,), dtype=torch.int32, device=d)
         self.qscale = torch.zeros((8,), dtype=torch.float64, device=d)
         self.leaf_acc = torch.zeros((self.capacity * 3,), dtype=torch.int64, device=d)
-        self.part_blocks = int(self.lib.h2omx_partition_blocks())
+        self.part_blocks = min(int(self.lib.h2omx_partition_blocks()),
+                               int(os.environ.get("H2OMX_PART_BLOCKS", "1024")))
         self.leaf_slab = (torch.zeros((params.max_depth * self.part_blocks * 3 * self.capacity,), dtype=torch.int64,
                                       device=d) if self.capacity <= 2048 else None)
         self._sp = SplitParams()
@@ -276,7 +280,8 @@ class HipTreeBuilder:
             if self.leaf_slab is not None:
                 slab = self.leaf_slab[n_part * self.part_blocks * 3 * self.capacity:]
             ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, P(g), P(h), P(w),
-                                          P(self.qscale), self.capacity, P(self.leaf_acc), P(slab), st),
+                                          P(self.qscale), self.capacity, P(self.leaf_acc), P(slab),
+                                          self.part_blocks, st),
                       "partition")
             n_part += 1
             full_prev = full_cur

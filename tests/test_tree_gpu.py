@@ -172,6 +172,8 @@ def test_compact_hist_matches_plain(cuda_dev, monkeypatch, dist, depth, sample_r
         out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
                                    nclass=3 if dist == "multinomial" else 1, seed=7)
     a, b = out[False], out[True]
-    assert np.array_equal(a.trees["feat"], b.trees["feat"])
-    assert np.array_equal(a.trees["bin"], b.trees["bin"])
-    np.testing.assert_array_equal(a.trees["value"], b.trees["value"])
+    for t in range(a.trees.shape[0]):
+        reach = a.compact()[t]
+        assert reach == b.compact()[t]
+        for f in ("feat", "bin", "value"):
+            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
