@@ -237,6 +237,7 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     rep_s[fi] = r < 1 ? 1 : (r > 64 ? 64 : r);
   }
   const float sg = (float)qscale[0], ss = (float)qscale[1];
+  const int64_t rb = (int64_t)qscale[7];  // global row offset of this rank (dither)
   __syncthreads();
 
   const int64_t units = npad / ROWS;
@@ -272,7 +273,7 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
       const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const uint32_t hsh = row_hash(r0 + 4 * q + k, salt);
+        const uint32_t hsh = row_hash(rb + r0 + 4 * q + k, salt);
         const float d1 = (hsh & 0xFFFF) * (1.0f / 65536.0f), d2 = (hsh >> 16) * (1.0f / 65536.0f);
         const int gq = (int)floorf(fmaf(gv[k], sg, d1));
         const uint32_t sq = (uint32_t)floorf(fmaf(sv[k], ss, d2));
@@ -378,6 +379,7 @@ __global__ __launch_bounds__(1024) void hist_build_compact_kernel(
     rep_s[fi] = r < 1 ? 1 : (r > 64 ? 64 : r);
   }
   const float sg = (float)qscale[0], ss = (float)qscale[1];
+  const int64_t rb = (int64_t)qscale[7];  // global row offset of this rank (dither)
   __syncthreads();
   const int64_t units = npad / rows_per_unit;
   const int64_t u0 = units * chunk / wgpg, u1 = units * (chunk + 1) / wgpg;
@@ -432,7 +434,7 @@ __global__ __launch_bounds__(1024) void hist_build_compact_kernel(
       const int64_t r = base + 64 * u + lane;
       pk[u] = 0ull;
       if (sl[u] >= 0) {
-        const uint32_t hsh = row_hash(r, salt);
+        const uint32_t hsh = row_hash(rb + r, salt);
         const float d1 = (hsh & 0xFFFF) * (1.0f / 65536.0f), d2 = (hsh >> 16) * (1.0f / 65536.0f);
         const float sv = s2 ? s2[r] : 1.0f;
         const int gq = (int)floorf(fmaf(g[r], sg, d1));
@@ -955,6 +957,7 @@ struct GradParams {
   float tweedie_power;
   float quantile_alpha;
   float huber_delta;
+  long long row_base;   // global index of this rank's first row (bagging hash)
 };
 
 __device__ __forceinline__ void dist_grad(int dist, float f, float y, const GradParams& gp, float& g, float& h) {
@@ -1030,7 +1033,7 @@ __global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F
       if (gp.apply_tree) fv[k] += tree[~nv[k]].value;
       dist_grad(gp.dist, fv[k], yv[k], gp, gv[k], hv[k]);
       if (gp.sample_rate < 1.0f) {
-        const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)r, 0x5bd1e995u));
+        const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)(r + gp.row_base), 0x5bd1e995u));
         if (u >= gp.sample_rate) wv[k] = 0.0f;
       }
       gv[k] *= wv[k];
@@ -1082,7 +1085,7 @@ __global__ __launch_bounds__(256) void softmax_grad_kernel(const float* __restri
     const float yv = (yk[r] == cls) ? 1.0f : 0.0f;
     float wv = wobs ? wobs[r] : 1.0f;
     if (gp.sample_rate < 1.0f) {
-      const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)r, 0x5bd1e995u));
+      const float u = u01(hash4(gp.seed, (uint32_t)gp.tree_index, (uint32_t)(r + gp.row_base), 0x5bd1e995u));
       if (u >= gp.sample_rate) wv = 0.0f;
     }
     const float gv = (pk - yv) * wv, hv = fmaxf(pk * (1.0f - pk), 1e-16f) * wv;
@@ -1128,7 +1131,8 @@ __global__ __launch_bounds__(1024) void stat_reduce_kernel(const unsigned int* _
 // workgroup chunk of the tree's level plans (<= QG / QS): smaller chunks give
 // proportionally finer quantisation.
 __device__ void tree_begin_scales(const unsigned int* __restrict__ stat_max, int mode, double qg, double qsr,
-                                  double* __restrict__ qs, int* __restrict__ ctl0, NodeLink* __restrict__ link0) {
+                                  double* __restrict__ qs, int* __restrict__ ctl0, NodeLink* __restrict__ link0,
+                                  long long row_base) {
   const double gmax = fmax((double)__uint_as_float(stat_max[0]), 1e-30);
   const double hmax = fmax((double)__uint_as_float(stat_max[1]), 1e-30);
   const double wmax = fmax((double)__uint_as_float(stat_max[2]), 1e-30);
@@ -1141,7 +1145,7 @@ __device__ void tree_begin_scales(const unsigned int* __restrict__ stat_max, int
   qs[4] = exp2(floor(log2(1073741823.0 / gmax)));
   qs[5] = exp2(floor(log2(1073741823.0 / hmax)));
   qs[6] = exp2(floor(log2(1073741823.0 / wmax)));
-  qs[7] = 0.0;
+  qs[7] = (double)row_base;  // exact below 2^53
   ctl0[CTL_N] = 1; ctl0[CTL_SLOTS] = 1; ctl0[CTL_BASE] = 0; ctl0[CTL_TOTAL] = 1;
   NodeLink root;
   root.slot = 0; root.sib_slot = -1; root.parent = -1; root.pad = 0;
@@ -1151,10 +1155,11 @@ __device__ void tree_begin_scales(const unsigned int* __restrict__ stat_max, int
 __global__ __launch_bounds__(256) void tree_begin_kernel(const unsigned int* __restrict__ stat_max, int mode,
                                                          double qg, double qsr, double* __restrict__ qs,
                                                          int* __restrict__ ctl0, NodeLink* __restrict__ link0,
-                                                         unsigned long long* __restrict__ leaf_acc, int leaf_n) {
+                                                         unsigned long long* __restrict__ leaf_acc, int leaf_n,
+                                                         long long row_base) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < leaf_n; i += gridDim.x * blockDim.x) leaf_acc[i] = 0ull;
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0);
+  tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0, row_base);
 }
 
 // Exact per-leaf (G, H, W) sums after the last partition: every row carries
@@ -1450,12 +1455,12 @@ H2OMX_API int h2omx_stat_reduce(const unsigned int* slab, unsigned int* stat_max
 
 H2OMX_API int h2omx_tree_begin(const unsigned int* stat_max, int mode, int max_rows_per_wg, double* qscale,
                                int* ctl0, void* link0, unsigned long long* leaf_acc, int leaf_n,
-                               hipStream_t stream) {
+                               long long row_base, hipStream_t stream) {
   if (max_rows_per_wg < 1 || max_rows_per_wg > ROWS_CAP) return kBadArg;
   const double qg = exp2(floor(log2(1073741824.0 / max_rows_per_wg)));   // |sum| <= 2^30
   const double qsr = exp2(floor(log2(2147483648.0 / max_rows_per_wg)));  // sum <= 2^31
   hipLaunchKernelGGL(tree_begin_kernel, dim3(grid_for(leaf_n, 256, 1024)), dim3(256), 0, stream, stat_max, mode, qg,
-                     qsr, qscale, ctl0, reinterpret_cast<NodeLink*>(link0), leaf_acc, leaf_n);
+                     qsr, qscale, ctl0, reinterpret_cast<NodeLink*>(link0), leaf_acc, leaf_n, row_base);
   return launch_status();
 }
 
@@ -1547,11 +1552,12 @@ __global__ __launch_bounds__(256) void tree_begin_seg_kernel(
     const unsigned int* __restrict__ stat_max, int mode, double qg, double qsr, double* __restrict__ qs,
     int* __restrict__ ctl0, NodeLink* __restrict__ link0, unsigned long long* __restrict__ leaf_acc, int leaf_n,
     long long* __restrict__ built, int built_n, int n_rows, int hc_rows, int* __restrict__ seg_start,
-    int* __restrict__ seg_cnt, int* __restrict__ hc_first, int* __restrict__ pc_first, int* __restrict__ slot_node) {
+    int* __restrict__ seg_cnt, int* __restrict__ hc_first, int* __restrict__ pc_first, int* __restrict__ slot_node,
+    long long row_base) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < leaf_n; i += gridDim.x * blockDim.x) leaf_acc[i] = 0ull;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < built_n; i += gridDim.x * blockDim.x) built[i] = 0ll;
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0);
+  tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0, row_base);
   seg_start[0] = 0;
   seg_cnt[0] = n_rows;
   hc_first[0] = 0;
@@ -1597,6 +1603,7 @@ __global__ __launch_bounds__(512) void hist_build_seg_kernel(
     rep_s[fi] = r < 1 ? 1 : (r > 64 ? 64 : r);
   }
   const float sg = (float)qscale[0], ss = (float)qscale[1];
+  const int64_t rb = (int64_t)qscale[7];  // global row offset of this rank (dither)
   __syncthreads();
   const int lo = range_s[0], hi = range_s[1];
   const int nw = (nf + 3) >> 2;
@@ -1911,14 +1918,15 @@ H2OMX_API int h2omx_pc_rows() { return PC_ROWS; }
 H2OMX_API int h2omx_tree_begin_seg(const unsigned int* stat_max, int mode, int max_rows_per_wg, double* qscale,
                                    int* ctl0, void* link0, unsigned long long* leaf_acc, int leaf_n,
                                    long long* built, int built_n, int n_rows, int hc_rows, int* seg_start,
-                                   int* seg_cnt, int* hc_first, int* pc_first, int* slot_node, hipStream_t stream) {
+                                   int* seg_cnt, int* hc_first, int* pc_first, int* slot_node, long long row_base,
+                                   hipStream_t stream) {
   if (max_rows_per_wg < 1 || max_rows_per_wg > ROWS_CAP || hc_rows > max_rows_per_wg) return kBadArg;
   const double qg = exp2(floor(log2(1073741824.0 / max_rows_per_wg)));
   const double qsr = exp2(floor(log2(2147483648.0 / max_rows_per_wg)));
   const int m = leaf_n > built_n ? leaf_n : built_n;
   hipLaunchKernelGGL(tree_begin_seg_kernel, dim3(grid_for(m, 256, 1024)), dim3(256), 0, stream, stat_max, mode, qg,
                      qsr, qscale, ctl0, reinterpret_cast<NodeLink*>(link0), leaf_acc, leaf_n, built, built_n, n_rows,
-                     hc_rows, seg_start, seg_cnt, hc_first, pc_first, slot_node);
+                     hc_rows, seg_start, seg_cnt, hc_first, pc_first, slot_node, row_base);
   return launch_status();
 }
 

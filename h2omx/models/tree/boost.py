@@ -207,7 +207,8 @@ class GpuBooster:
 
     def _update(self, apply: bool, next_tree: int, k: int, dist=None):
         P, st, b = ops.P, self.st, self.builder
-        gp = make_grad_params(dist or self.dist, apply, self.sample_rate, self.seed, next_tree, **self.kw)
+        gp = make_grad_params(dist or self.dist, apply, self.sample_rate, self.seed, next_tree,
+                              row_base=self.builder.row_base, **self.kw)
         y = st.ycls[k] if (self.dist == "drf" and self.K > 1) else st.y
         ops.check(self.lib.h2omx_boost_update(P(st.Fm[k]), P(y), P(st.w), self.bm.n, self.bm.npad, P(b.nid),
                                               P(b.tree_buf), ctypes.addressof(gp), P(st.g[k]), P(st.h[k]),
@@ -223,7 +224,8 @@ class GpuBooster:
             self._update(apply=True, next_tree=t + 1, k=0)
         else:
             s = ops.stream(self.dev)
-            gp = make_grad_params("bernoulli", False, self.sample_rate, self.seed, t, **self.kw)
+            gp = make_grad_params("bernoulli", False, self.sample_rate, self.seed, t,
+                                  row_base=self.builder.row_base, **self.kw)
             # all classes' gradients from the margins at the start of the iteration;
             # per-class maxima are kept for the per-class quantisation scales
             maxes = []
@@ -279,12 +281,15 @@ def _tree_fmask(tp: TreeParams, F: int, t: int, dev):
 def _train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw):
     K, dist, n = ens.K, ens.dist, bm.n
     builder = RefTreeBuilder(bm, tp, comm)
+    from .engine import global_row_base
+
+    row_base = global_row_base(n, comm)
     Fm = np.repeat(ens.init_f[:, None], n, 1).astype(np.float32)
     wobs = np.ones(n, np.float32) if w_np is None else w_np.astype(np.float32)
     trees = []
     t0 = time.perf_counter()
     for t in range(ntrees):
-        wb = wobs * bag_weights(n, sample_rate, seed, t)
+        wb = wobs * bag_weights(n, sample_rate, seed, t, row_base)
         if K == 1:
             gr, hs = dist_grad(dist, Fm[0], y_np, **dist_kw)
             grads = [(gr, hs)]

@@ -111,6 +111,10 @@ class HipTreeBuilder:
                                       device=d) if self.capacity <= 2048 else None)
         self._sp = SplitParams()
         self.stats = {"host_syncs": 0}
+        # global index of this rank's first row: the stochastic-rounding dither and
+        # bagging hash use global row ids, so a multi-GPU model is bit-identical to
+        # the single-GPU model on the concatenated rows
+        self.row_base = global_row_base(bm.n, comm)
         self.plans = {}
         # largest workgroup row chunk over every plan this tree can use: sets the
         # fixed-point resolution (finer for smaller chunks), identical across levels
@@ -222,8 +226,8 @@ class HipTreeBuilder:
         link = [self._buf("link0", 4, torch.int32), None]
         # scales + level-0 control block/link + zeroed leaf sums in one launch
         ops.check(lib.h2omx_tree_begin(P(self.stat_max), p.mode, self.max_rows_per_wg, P(self.qscale),
-                                       P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(), st),
-                  "tree_begin")
+                                       P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(),
+                                       self.row_base, st), "tree_begin")
         full_prev = None
         max_depth = p.max_depth
         max_nodes = 1
@@ -318,7 +322,8 @@ class HipTreeBuilder:
         ops.check(lib.h2omx_tree_begin_seg(P(self.stat_max), p.mode, self.max_rows_per_wg, P(self.qscale),
                                            P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(),
                                            P(built), self.per_node, n, self.hc_rows, P(seg[0][0]), P(seg[0][1]),
-                                           P(seg[0][2]), P(seg[0][3]), P(seg[0][4]), st), "tree_begin_seg")
+                                           P(seg[0][2]), P(seg[0][3]), P(seg[0][4]), self.row_base, st),
+                  "tree_begin_seg")
         full_prev = None
         max_depth = p.max_depth
         max_nodes = 1
@@ -439,6 +444,13 @@ class HipTreeBuilder:
         return self.ctl[self.p.max_depth % 2, 3]
 
 
+def global_row_base(n: int, comm) -> int:
+    if comm is None or comm.world_size <= 1:
+        return 0
+    counts = comm.all_gather_cat(torch.tensor([n], dtype=torch.int64, device=comm.device)).cpu().tolist()
+    return int(sum(counts[: comm.rank]))
+
+
 def trees_from_bytes(buf: np.ndarray, capacity: int) -> np.ndarray:
     """View raw bytes as [ntrees][capacity] TREE_NODE_DTYPE records."""
     arr = np.frombuffer(buf.tobytes(), dtype=TREE_NODE_DTYPE)
@@ -446,7 +458,8 @@ def trees_from_bytes(buf: np.ndarray, capacity: int) -> np.ndarray:
 
 
 def make_grad_params(dist: str, apply_tree: bool, sample_rate: float, seed: int, tree_index: int,
-                     tweedie_power: float = 1.5, quantile_alpha: float = 0.5, huber_delta: float = 1.0) -> GradParams:
+                     tweedie_power: float = 1.5, quantile_alpha: float = 0.5, huber_delta: float = 1.0,
+                     row_base: int = 0) -> GradParams:
     from .structs import DIST_CODES
 
     gp = GradParams()
@@ -456,4 +469,5 @@ def make_grad_params(dist: str, apply_tree: bool, sample_rate: float, seed: int,
     gp.seed = seed & 0xFFFFFFFF
     gp.tree_index = tree_index
     gp.tweedie_power, gp.quantile_alpha, gp.huber_delta = tweedie_power, quantile_alpha, huber_delta
+    gp.row_base = row_base
     return gp

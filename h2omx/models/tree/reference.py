@@ -230,10 +230,11 @@ class RefTreeBuilder:
 # ---------------------------------------------------------------------------
 # gradients (mirror of boost_update_kernel / softmax_grad_kernel)
 # ---------------------------------------------------------------------------
-def bag_weights(n: int, sample_rate: float, seed: int, tree_index: int) -> np.ndarray:
+def bag_weights(n: int, sample_rate: float, seed: int, tree_index: int, row_base: int = 0) -> np.ndarray:
     if sample_rate >= 1.0:
         return np.ones(n, np.float32)
-    u = u01(hash4(seed & 0xFFFFFFFF, tree_index, np.arange(n), 0x5BD1E995))
+    rows = (np.arange(n, dtype=np.int64) + row_base).astype(np.uint32)
+    u = u01(hash4(seed & 0xFFFFFFFF, tree_index, rows, 0x5BD1E995))
     return (u < np.float32(sample_rate)).astype(np.float32)
 
 

@@ -29,7 +29,7 @@ class GradParams(ctypes.Structure):
     _fields_ = [
         ("dist", ctypes.c_int), ("apply_tree", ctypes.c_int), ("sample_rate", ctypes.c_float),
         ("seed", ctypes.c_uint32), ("tree_index", ctypes.c_int), ("tweedie_power", ctypes.c_float),
-        ("quantile_alpha", ctypes.c_float), ("huber_delta", ctypes.c_float),
+        ("quantile_alpha", ctypes.c_float), ("huber_delta", ctypes.c_float), ("row_base", ctypes.c_int64),
     ]
 
 

@@ -44,9 +44,11 @@ class Comm:
         if world > 1 and not dist.is_initialized():
             import datetime
 
-            backend = "nccl" if dev.type == "cuda" else "gloo"
+            # H2OMX_DIST_BACKEND=gloo: several ranks sharing one GPU (tests of the
+            # multi-rank GPU path on a one-GPU box); production uses RCCL
+            backend = os.environ.get("H2OMX_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
             kw = {}
-            if dev.type == "cuda":
+            if dev.type == "cuda" and backend == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
@@ -119,7 +121,7 @@ class Comm:
 
     def barrier(self) -> None:
         if self.world_size > 1:
-            if self.device.type == "cuda":
+            if self.device.type == "cuda" and dist.get_backend(self.group) == "nccl":
                 dist.barrier(group=self.group, device_ids=[self.device.index])
             else:
                 dist.barrier(group=self.group)
