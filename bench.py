@@ -1,18 +1,28 @@
 #!/usr/bin/env python3
-"""Headline benchmark (BASELINE.json): GBM binomial training throughput on
-HIGGS-shape 11M x 28 synthetic data, one rank per MI355X.
+"""Benchmarks (BASELINE.json / BASELINE.md), one rank per MI355X.
 
-    python bench.py --gpus N --steps K --warmup W
-    torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
+    python bench.py --gpus N --steps K --warmup W                 # headline
+    torchrun --nproc-per-node N bench.py --gpus N ...             # driver, N > 1
+    python bench.py --model xgboost-airlines | dl-mlp ...         # other BASELINE configs
 
-One *step* is one full boosting iteration: gradients + a depth-5 tree grown
-level by level on the GPU (LDS histograms, fp64 reduce, RCCL all-reduce of
-the level histograms when N > 1, split scan, partition) + margin update.
-``value`` = total training rows x K / max-over-ranks wall time of the K timed
-steps = aggregate row-trees per second.  Scaling is *weak* by default: every
-rank holds its own 11M-row HIGGS-shape shard (global rows = N x 11M); use
-``--scaling strong`` to split 11M rows over the ranks instead.  Training AUC
-of the final model (all ranks) is reported next to the throughput.
+Headline (default, ``--model gbm-higgs``): GBM binomial training throughput
+on HIGGS-shape 11M x 28 synthetic data.  One *step* is one full boosting
+iteration: gradients + a depth-5 tree grown level by level on the GPU (LDS
+histograms, exact integer reduce, RCCL all-reduce of the level histograms
+when N > 1, split scan, partition, leaf values) + margin update.
+``value`` = total training rows x K / max-over-ranks wall time of the K
+timed steps = aggregate row-trees per second.  Scaling is *weak* by
+default: every rank holds its own 11M-row shard (global rows = N x 11M);
+``--scaling strong`` splits 11M rows over the ranks instead.  Training AUC
+of the final model (all ranks) is reported; ``--oracle-rows R`` adds a
+scikit-learn HistGradientBoosting fit on R rows for AUC parity.
+
+``xgboost-airlines``: XGBoost-hist (second-order gain, depth 6, eta 0.3) on
+Airlines-shape 31-column data, 150M rows over 8 GPUs = 18.75M rows per GPU
+(weak).  ``dl-mlp``: H2O DeepLearning MLP 4x512 (Rectifier, ADADELTA,
+softmax) on 200 features, 50M rows over 8 GPUs = 6.25M rows per GPU; one
+step = one synchronous mini-batch (``--batch`` rows per GPU) forward +
+backward + gradient all-reduce + update; value = samples/s.
 """
 from __future__ import annotations
 
@@ -25,83 +35,81 @@ import time
 METRIC = "GBM train rows/sec on HIGGS-shape 11M×28 at 1/2/4/8 MI355X; AUC parity"
 
 
-def main(argv=None) -> int:
-    ap = argparse.ArgumentParser(description=__doc__)
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=11_000_000)
-    ap.add_argument("--cols", type=int, default=28)
-    ap.add_argument("--max-depth", type=int, default=5)
-    ap.add_argument("--nbins", type=int, default=255)
-    ap.add_argument("--learn-rate", type=float, default=0.1)
-    ap.add_argument("--min-rows", type=float, default=10.0)
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
-    ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--no-auc", action="store_true")
-    ap.add_argument("--oracle-rows", type=int, default=0,
-                    help="also fit sklearn HistGradientBoosting on this many rows for AUC parity")
-    args = ap.parse_args(argv)
-
-    import torch
-
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from h2omx.frame.synthetic import higgs_like
-    from h2omx.metrics.core import auc_from_scores
-    from h2omx.models.tree import TreeParams, bin_matrix, compute_edges
-    from h2omx.models.tree.boost import GpuBooster, TreeEnsemble, init_margin
-    from h2omx.parallel.comm import Comm
-
-    comm = Comm.from_env("cuda")
-    dev = comm.device
-    world, rank = comm.world_size, comm.rank
-    if args.scaling == "weak":
-        n_local = args.rows
-    else:
-        n_local = args.rows // world + (1 if rank < args.rows % world else 0)
-
-    t_setup = time.perf_counter()
-    X, y = higgs_like(n_local, seed=args.seed + 1000 * rank, device=dev)
-    if args.cols != 28:
-        X = X[: args.cols].contiguous() if args.cols < 28 else torch.cat(
-            [X, torch.randn((args.cols - 28, n_local), device=dev)])
-    edges, nvb, nbt = compute_edges(X, args.nbins, comm=comm)
-    bm = bin_matrix(X, edges, nvb, nbt)
-    tp = TreeParams(max_depth=args.max_depth, min_rows=args.min_rows, learn_rate=args.learn_rate, mode=0,
-                    leaf_mode=0, min_split_improvement=1e-5, seed=args.seed)
-    y_np = y.cpu().numpy()
-    sums = comm.all_reduce_numpy(__import__("numpy").array([y_np.sum(), float(len(y_np))]))
-    p0 = min(max(sums[0] / sums[1], 1e-6), 1 - 1e-6)
-    import numpy as np
-
-    ens = TreeEnsemble(trees=np.zeros((0, 1)), K=1, dist="bernoulli",
-                       init_f=np.array([np.log(p0 / (1 - p0))]), nbt=nbt, feature_names=bm.names)
-    gb = GpuBooster(bm, y_np, None, ens, tp, 1.0, args.seed, comm, {})
-    torch.cuda.synchronize(dev)
-    comm.barrier()
-    setup_s = time.perf_counter() - t_setup
-
+def _timed(step, args, comm, torch, dev):
     for _ in range(args.warmup):
-        gb.step()
+        step()
     torch.cuda.synchronize(dev)
     comm.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        gb.step()
+        step()
     torch.cuda.synchronize(dev)
     comm.barrier()
     torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    elapsed = comm.max_scalar(elapsed)
+    return comm.max_scalar(time.perf_counter() - t0)
 
+
+def _trees(args, comm, torch, np, model):
+    from h2omx.frame.synthetic import airlines_like, higgs_like
+    from h2omx.metrics.core import auc_from_scores
+    from h2omx.models.tree import TreeParams, bin_matrix, compute_edges
+    from h2omx.models.tree.boost import GpuBooster, TreeEnsemble
+
+    dev = comm.device
+    world, rank = comm.world_size, comm.rank
+    rows = args.rows or (11_000_000 if model == "gbm-higgs" else 150_000_000 // 8)
+    n_local = rows if args.scaling == "weak" else rows // world + (1 if rank < rows % world else 0)
+    t_setup = time.perf_counter()
+    if model == "gbm-higgs":
+        X, y = higgs_like(n_local, seed=args.seed + 1000 * rank, device=dev)
+        if args.cols != 28:
+            X = X[: args.cols].contiguous() if args.cols < 28 else torch.cat(
+                [X, torch.randn((args.cols - 28, n_local), device=dev)])
+        depth = args.max_depth or 5
+        tp = TreeParams(max_depth=depth, min_rows=args.min_rows, learn_rate=args.learn_rate or 0.1, mode=0,
+                        leaf_mode=0, min_split_improvement=1e-5, seed=args.seed)
+    else:
+        X, y = airlines_like(n_local, seed=args.seed + 1000 * rank, device=dev)
+        depth = args.max_depth or 6
+        tp = TreeParams(max_depth=depth, min_rows=0.0, min_child_weight=1.0, reg_lambda=1.0, gamma=0.0,
+                        learn_rate=args.learn_rate or 0.3, mode=1, leaf_mode=0, min_split_improvement=0.0,
+                        seed=args.seed)
+    edges, nvb, nbt = compute_edges(X, args.nbins, comm=comm)
+    bm = bin_matrix(X, edges, nvb, nbt)
+    y_np = y.cpu().numpy()
+    sums = comm.all_reduce_numpy(np.array([y_np.sum(), float(len(y_np))]))
+    p0 = min(max(sums[0] / sums[1], 1e-6), 1 - 1e-6)
+    init = np.log(p0 / (1 - p0)) if model == "gbm-higgs" else 0.0   # XGBoost base_score 0.5
+    ens = TreeEnsemble(trees=np.zeros((0, 1)), K=1, dist="bernoulli", init_f=np.array([init]), nbt=nbt,
+                       feature_names=bm.names)
+    gb = GpuBooster(bm, y_np, None, ens, tp, 1.0, args.seed, comm, {})
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    setup_s = time.perf_counter() - t_setup
+    elapsed = _timed(gb.step, args, comm, torch, dev)
     total_rows = int(comm.all_reduce_numpy(np.array([float(n_local)]))[0])
-    value = total_rows * args.steps / elapsed
     auc = None
     if not args.no_auc:
-        margin = gb.st.Fm[0, : bm.n]
-        auc = auc_from_scores(margin, y, comm=comm)
-    oracle = None
+        auc = auc_from_scores(gb.st.Fm[0, : bm.n], y, comm=comm)
+    out = {
+        "metric": METRIC if model == "gbm-higgs" else
+        "XGBoost-hist train rows/sec on Airlines-shape 150M×31 (18.75M rows per MI355X); AUC",
+        "value": total_rows * args.steps / elapsed,
+        "unit": "rows/s (row-trees per second, all GPUs)",
+        "ms_per_step": 1000.0 * elapsed / args.steps,
+        "higher_is_better": True,
+        "dtype": "fp32 gradients/hessians; histograms in fixed-point int32 (stochastic rounding) summed "
+                 "exactly in int64; fp64 split gains; exact int64 leaf sums; uint8 bins",
+        "data": f"synthetic {'HIGGS' if model == 'gbm-higgs' else 'Airlines'}-shape generated on device; "
+                "random-init, seed per rank",
+        "config": {"model": "GBM bernoulli" if model == "gbm-higgs" else "XGBoost hist binary:logistic",
+                   "global_batch": total_rows, "seq_len": None, "rows_per_gpu": n_local,
+                   "cols": int(bm.F), "max_depth": depth, "nbins": args.nbins, "learn_rate": tp.learn_rate,
+                   "min_rows": tp.min_rows, "parallelism": f"dp{world}"},
+        "train_auc": auc,
+        "setup_s": setup_s,
+    }
     if args.oracle_rows and rank == 0:
         from sklearn.ensemble import HistGradientBoostingClassifier
         from sklearn.metrics import roc_auc_score
@@ -109,37 +117,113 @@ def main(argv=None) -> int:
         m = min(args.oracle_rows, n_local)
         Xs = X[:, :m].T.cpu().numpy()
         ys = y[:m].cpu().numpy()
-        ntr = args.warmup + args.steps
-        clf = HistGradientBoostingClassifier(max_iter=ntr, max_depth=args.max_depth, learning_rate=args.learn_rate,
-                                             min_samples_leaf=int(args.min_rows), max_bins=min(args.nbins, 255),
-                                             early_stopping=False, l2_regularization=0.0).fit(Xs, ys)
-        oracle = {"rows": m, "sklearn_train_auc": float(roc_auc_score(ys, clf.decision_function(Xs))),
-                  "h2omx_train_auc_same_rows": float(roc_auc_score(ys, gb.st.Fm[0, :m].cpu().numpy()))}
+        clf = HistGradientBoostingClassifier(max_iter=args.warmup + args.steps, max_depth=depth,
+                                             learning_rate=tp.learn_rate, min_samples_leaf=max(1, int(args.min_rows)),
+                                             max_bins=min(args.nbins, 255), early_stopping=False,
+                                             l2_regularization=0.0).fit(Xs, ys)
+        out["oracle"] = {"rows": m, "sklearn_hgb_train_auc": float(roc_auc_score(ys, clf.decision_function(Xs))),
+                         "h2omx_train_auc_same_rows": float(roc_auc_score(ys, gb.st.Fm[0, :m].cpu().numpy()))}
+    return out
 
-    if rank == 0:
-        out = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "rows/s (row-trees per second, all GPUs)",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": 1000.0 * elapsed / args.steps,
-            "higher_is_better": True,
-            "scaling": args.scaling,
-            "vs_baseline": None,
-            "dtype": "fp32 (gradients/hessians), fp64 histogram reduce, uint8 bins",
-            "data": "synthetic HIGGS-shape (28 cols) generated on device; random seed per rank",
-            "config": {"model": "GBM bernoulli", "global_batch": total_rows, "seq_len": None,
-                       "rows_per_gpu": n_local, "cols": args.cols, "max_depth": args.max_depth,
-                       "nbins": args.nbins, "learn_rate": args.learn_rate, "min_rows": args.min_rows,
-                       "parallelism": f"dp{world}"},
-            "train_auc": auc,
-            "setup_s": setup_s,
-        }
-        if oracle:
-            out["oracle"] = oracle
-        print(json.dumps(out), flush=True)
+
+def _mlp(args, comm, torch, np):
+    from h2omx.frame.synthetic import wide_gaussian
+    from h2omx.models.deeplearning import H2ODeepLearningEstimator, _forward, _Net
+    from h2omx.ops import dense as D
+
+    dev = comm.device
+    world, rank = comm.world_size, comm.rank
+    rows = args.rows or 50_000_000 // 8
+    n_local = rows if args.scaling == "weak" else rows // world
+    t_setup = time.perf_counter()
+    X, y = wide_gaussian(n_local, 200, seed=args.seed + 1000 * rank, device=dev)
+    X = X.T.contiguous()                    # row-major [n][200]
+    X = (X - X.mean(0)) / X.std(0).clamp_min(1e-6)
+    yi = y.to(torch.int32)
+    gen = torch.Generator().manual_seed(args.seed)
+    net = _Net([200, 512, 512, 512, 512, 2], 1, dev, gen)
+    comm.broadcast_(net.flat, 0)
+    Eg2, Edx2 = torch.zeros_like(net.flat), torch.zeros_like(net.flat)
+    B = args.batch
+    nb = max(1, n_local // B)
+    state = {"i": 0}
+    bw = H2ODeepLearningEstimator._backward
+
+    def step():
+        i = state["i"] % nb
+        state["i"] += 1
+        xb = X[i * B:(i + 1) * B]
+        Hs, aux = _forward(net, xb, 1, True, 0.0, [0.0] * 8, None)
+        dZ, _ = D.softmax_xent(Hs[-1], yi[i * B:(i + 1) * B])
+        bw(None, net, Hs, aux, dZ, 1, comm if world > 1 else None, world)
+        D.adadelta_(net.flat, net.grad, Eg2, Edx2, 0.99, 1e-8, 0.0)
+
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    setup_s = time.perf_counter() - t_setup
+    elapsed = _timed(step, args, comm, torch, dev)
+    with torch.no_grad():
+        xs, ys_ = X[:200_000], y[:200_000]
+        from h2omx.metrics.core import auc_from_scores
+
+        Z = _forward(net, xs, 1, False, 0.0, [0.0] * 8, None)[0][-1]
+        auc = auc_from_scores(torch.softmax(Z, 1)[:, 1], ys_, comm=comm)
+    flops_row = 6 * sum(a * b for a, b in zip([200, 512, 512, 512, 512], [512, 512, 512, 512, 2]))
+    return {
+        "metric": "H2O DeepLearning MLP 4×512 on 50M×200 synthetic (6.25M rows per MI355X): train samples/sec",
+        "value": world * B * args.steps / elapsed,
+        "unit": "samples/s (all GPUs)",
+        "ms_per_step": 1000.0 * elapsed / args.steps,
+        "higher_is_better": True,
+        "dtype": "fp32 (MFMA fp32 GEMMs, fp32 ADADELTA)",
+        "data": "synthetic wide-Gaussian 200 features generated on device; random-init weights",
+        "config": {"model": "MLP 200-512x4-2 Rectifier, ADADELTA(0.99,1e-8), softmax", "global_batch": world * B,
+                   "seq_len": None, "rows_per_gpu": n_local, "batch_per_gpu": B,
+                   "parallelism": f"dp{world} (gradient all-reduce per step)"},
+        "train_auc_200k": auc,
+        "achieved_tflops_per_gpu": flops_row * B * args.steps / elapsed / 1e12,
+        "setup_s": setup_s,
+    }
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", choices=["gbm-higgs", "xgboost-airlines", "dl-mlp"], default="gbm-higgs")
+    ap.add_argument("--rows", type=int, default=0, help="rows per GPU (weak) / total (strong); 0 = config default")
+    ap.add_argument("--cols", type=int, default=28)
+    ap.add_argument("--max-depth", type=int, default=0)
+    ap.add_argument("--nbins", type=int, default=255)
+    ap.add_argument("--learn-rate", type=float, default=0.0)
+    ap.add_argument("--min-rows", type=float, default=10.0)
+    ap.add_argument("--batch", type=int, default=8192, help="dl-mlp rows per GPU per step")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--no-auc", action="store_true")
+    ap.add_argument("--oracle-rows", type=int, default=0,
+                    help="also fit sklearn HistGradientBoosting on this many rows for AUC parity")
+    args = ap.parse_args(argv)
+
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from h2omx.parallel.comm import Comm
+
+    comm = Comm.from_env("cuda")
+    if args.model == "dl-mlp":
+        out = _mlp(args, comm, torch, np)
+    else:
+        out = _trees(args, comm, torch, np, args.model)
+    if comm.rank == 0:
+        res = {"metric": out.pop("metric"), "value": out.pop("value"), "unit": out.pop("unit"),
+               "n_gpus": comm.world_size, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": out.pop("ms_per_step"), "higher_is_better": out.pop("higher_is_better"),
+               "scaling": args.scaling, "vs_baseline": None}
+        res.update(out)
+        print(json.dumps(res), flush=True)
     comm.shutdown()
     return 0
 

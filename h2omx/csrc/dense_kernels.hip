@@ -405,7 +405,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float* __restrict__ A, 
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
   const int li = lane & 31, lh = lane >> 5;
-  for (int k0 = 0; k0 < K; k0 += GK) {
+  // split-K: blockIdx.z owns K range [kb, ke) (multiple of GK); partial tiles
+  // go to the workspace Cm + z*M*N and gemm_splitk_reduce applies the epilogue
+  const int S = gridDim.z;
+  const int kchunk = ((K + S - 1) / S + GK - 1) / GK * GK;
+  const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+  if (S > 1) Cm += (int64_t)blockIdx.z * M * N;
+  for (int k0 = kb; k0 < ke; k0 += GK) {
     // stage A tile (GB x GK) as As[k][m]
     for (int j = t; j < GB * GK; j += 256) {
       int m, kk;
@@ -413,7 +419,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float* __restrict__ A, 
       else { kk = j % GK; m = j / GK; }     // A stored [M][K]: coalesced along k
       const int gm = m0 + m, gk = k0 + kk;
       float v = 0.0f;
-      if (gm < M && gk < K) v = TA ? A[(int64_t)gk * M + gm] : A[(int64_t)gm * K + gk];
+      if (gm < M && gk < ke) v = TA ? A[(int64_t)gk * M + gm] : A[(int64_t)gm * K + gk];
       As[kk][m] = v;
     }
     for (int j = t; j < GB * GK; j += 256) {
@@ -422,7 +428,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float* __restrict__ A, 
       else { nn = j % GB; kk = j / GB; }     // B stored [K][N]: coalesced along n
       const int gn = n0 + nn, gk = k0 + kk;
       float v = 0.0f;
-      if (gn < N && gk < K) v = TB ? B[(int64_t)gn * K + gk] : B[(int64_t)gk * N + gn];
+      if (gn < N && gk < ke) v = TB ? B[(int64_t)gn * K + gk] : B[(int64_t)gk * N + gn];
       Bs[kk][nn] = v;
     }
     __syncthreads();
@@ -448,6 +454,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float* __restrict__ A, 
         const int j = n0 + wn + 32 * b + li;
         if (i < M && j < N) {
           float v = acc[a][b][e];
+          if (S > 1) {
+            Cm[(int64_t)i * N + j] = v;
+            continue;
+          }
           if (beta_c != 0.0f) v += beta_c * Cm[(int64_t)i * N + j];
           if (bias) v += bias[j];
           if (act == 1) v = fmaxf(v, 0.0f);
@@ -455,6 +465,42 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float* __restrict__ A, 
           Cm[(int64_t)i * N + j] = v;
         }
       }
+}
+
+// C = act(sum_z W[z] + beta_c * C + bias): split-K epilogue (fixed order: deterministic)
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __restrict__ W, int S, int M, int N,
+                                                                 float* __restrict__ C, const float* __restrict__ bias,
+                                                                 int act, float beta_c) {
+  const int64_t MN = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < MN; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.0f;
+    for (int z = 0; z < S; ++z) v += W[z * MN + i];
+    if (beta_c != 0.0f) v += beta_c * C[i];
+    if (bias) v += bias[i % N];
+    if (act == 1) v = fmaxf(v, 0.0f);
+    else if (act == 2) v = tanhf(v);
+    C[i] = v;
+  }
+}
+
+// column sums over a row slice: ws[blockIdx.y][j] (then summed by gemm_splitk_reduce with M = 1)
+__global__ __launch_bounds__(256) void bias_grad_split_kernel(const float* __restrict__ dY, float* __restrict__ ws,
+                                                              int M, int N) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= N) return;
+  const int S = gridDim.y;
+  const int rows = (M + S - 1) / S;
+  const int r0 = blockIdx.y * rows, r1 = min(M, r0 + rows);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int i = r0;
+  for (; i + 3 < r1; i += 4) {
+    s0 += dY[(int64_t)i * N + j];
+    s1 += dY[(int64_t)(i + 1) * N + j];
+    s2 += dY[(int64_t)(i + 2) * N + j];
+    s3 += dY[(int64_t)(i + 3) * N + j];
+  }
+  for (; i < r1; ++i) s0 += dY[(int64_t)i * N + j];
+  ws[(int64_t)blockIdx.y * N + j] = (s0 + s1) + (s2 + s3);
 }
 
 // dZ = dY * act'(Y)  (act: 0 none, 1 relu, 2 tanh), in place allowed
@@ -592,12 +638,17 @@ H2OMX_API int h2omx_kmeans(const float* X, int64_t ld, int64_t n, int d, const f
 }
 
 H2OMX_API int h2omx_gemm(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int ta,
-                         int tb, int act, float beta_c, hipStream_t stream) {
-  const dim3 grid(cdiv(N, GB), cdiv(M, GB));
-  if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(256), 0, stream, A, B, C, bias, M, N, K, act, beta_c);
-  else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(256), 0, stream, A, B, C, bias, M, N, K, act, beta_c);
-  else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(256), 0, stream, A, B, C, bias, M, N, K, act, beta_c);
-  else hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(256), 0, stream, A, B, C, bias, M, N, K, act, beta_c);
+                         int tb, int act, float beta_c, int splitk, float* ws, hipStream_t stream) {
+  if (splitk < 1 || (splitk > 1 && !ws)) return kBadArg;
+  const dim3 grid(cdiv(N, GB), cdiv(M, GB), splitk);
+  float* out = splitk > 1 ? ws : C;
+  if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(256), 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+  else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(256), 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+  else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(256), 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+  else hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(256), 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+  if (splitk > 1)
+    hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(cdiv((int64_t)M * N, 256) < 4096 ? cdiv((int64_t)M * N, 256) : 4096),
+                       dim3(256), 0, stream, ws, splitk, M, N, C, bias, act, beta_c);
   return launch_status();
 }
 
@@ -606,8 +657,11 @@ H2OMX_API int h2omx_act_backward(const float* Y, float* dY, int64_t n, int act, 
   return launch_status();
 }
 
-H2OMX_API int h2omx_bias_grad(const float* dY, float* db, int M, int N, hipStream_t stream) {
-  hipLaunchKernelGGL(bias_grad_kernel, dim3(cdiv(N, 256)), dim3(256), 0, stream, dY, db, M, N);
+H2OMX_API int h2omx_bias_grad(const float* dY, float* db, int M, int N, float* ws, int splits, hipStream_t stream) {
+  if (splits < 1 || !ws) return kBadArg;
+  hipLaunchKernelGGL(bias_grad_split_kernel, dim3(cdiv(N, 256), splits), dim3(256), 0, stream, dY, ws, M, N);
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(cdiv(N, 256)), dim3(256), 0, stream, ws, splits, 1, N, db,
+                     nullptr, 0, 0.0f);
   return launch_status();
 }
 

@@ -51,9 +51,9 @@ DENSE_SIGS = {
     "h2omx_slab_reduce_upper": "PIIPS",
     "h2omx_slab_sum": "PIIPS",
     "h2omx_kmeans": "PLLIPPIIPPS",
-    "h2omx_gemm": "PPPPIIIIIIFS",
+    "h2omx_gemm": "PPPPIIIIIIFIPS",
     "h2omx_act_backward": "PPLIS",
-    "h2omx_bias_grad": "PPIIS",
+    "h2omx_bias_grad": "PPIIPIS",
     "h2omx_softmax_xent": "PPPPIIS",
     "h2omx_adadelta": "PPPPLFFFS",
     "h2omx_sgd_momentum": "PPPLFFFS",

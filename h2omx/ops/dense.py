@@ -222,6 +222,19 @@ def _kmeans_large(X: torch.Tensor, C: torch.Tensor):
 ACTS = {"linear": 0, "none": 0, "rectifier": 1, "relu": 1, "tanh": 2}  # maxout: models/deeplearning.py
 
 
+_WS: dict = {}
+
+
+def _workspace(dev, numel: int, slot: int = 0) -> torch.Tensor:
+    """Per-device scratch for split-K partials (stream-ordered reuse)."""
+    key = (str(dev), slot)
+    w = _WS.get(key)
+    if w is None or w.numel() < numel:
+        w = torch.empty((numel,), dtype=torch.float32, device=dev)
+        _WS[key] = w
+    return w
+
+
 def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = False, tb: bool = False,
          out: torch.Tensor | None = None, beta_c: float = 0.0) -> torch.Tensor:
     """C = act(op(A) op(B) + bias) with row-major fp32 operands."""
@@ -230,7 +243,14 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
     N = B.shape[0] if tb else B.shape[1]
     if A.is_cuda:
         C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=A.device)
-        check(dense_lib().h2omx_gemm(P(A), P(B), P(C), P(bias), M, N, K, int(ta), int(tb), act, beta_c,
+        # split-K when the output has too few 128x128 tiles to fill 256 CUs
+        # (weight gradients: [out][in] outputs with K = batch rows)
+        tiles = -(-M // 128) * -(-N // 128)
+        S = 1
+        if tiles < 128 and K >= 1024:
+            S = max(1, min(64, 256 // tiles, K // 256))
+        ws = _workspace(A.device, S * M * N) if S > 1 else None
+        check(dense_lib().h2omx_gemm(P(A), P(B), P(C), P(bias), M, N, K, int(ta), int(tb), act, beta_c, S, P(ws),
                                  stream(A.device)), "gemm")
         return C
     a = A.T if ta else A
@@ -267,7 +287,9 @@ def bias_grad(dY: torch.Tensor) -> torch.Tensor:
     M, N = dY.shape
     if dY.is_cuda:
         db = torch.empty((N,), dtype=torch.float32, device=dY.device)
-        check(dense_lib().h2omx_bias_grad(P(dY), P(db), M, N, stream(dY.device)), "bias_grad")
+        splits = max(1, min(128, M // 64))
+        ws = _workspace(dY.device, splits * N, slot=1)
+        check(dense_lib().h2omx_bias_grad(P(dY), P(db), M, N, P(ws), splits, stream(dY.device)), "bias_grad")
         return db
     return dY.sum(0)
 

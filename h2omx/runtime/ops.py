@@ -134,14 +134,19 @@ def blob_setup(cl, key, sep=None, header=None) -> dict:
     return parse_setup(key, sep, header)
 
 
-def op_synthetic(cl, kind, rows, cols, dest, seed=42, **kw):
+def op_synthetic(cl, kind, rows, dest, cols=None, seed=42):
+    """Device-generated synthetic frames (HIGGS / Airlines / wide Gaussian
+    shapes from BASELINE.md); each rank generates its share of ``rows``."""
     from ..frame import synthetic
 
-    gen = getattr(synthetic, kind)
     per = rows // cl.world_size + (1 if cl.rank < rows % cl.world_size else 0)
-    fr = gen(per, cols, seed=seed + 1000003 * cl.rank, device=_dev(cl), **kw) if cols else \
-        gen(per, seed=seed + 1000003 * cl.rank, device=_dev(cl), **kw)
-    fr = unify_domains(fr, cl.comm)
+    s = seed + 1000003 * cl.rank
+    if kind == "wide_gaussian":
+        X, y = synthetic.wide_gaussian(per, int(cols or 100), seed=s, device=_dev(cl))
+    else:
+        X, y = getattr(synthetic, kind)(per, seed=s, device=_dev(cl))
+    fr = Frame.from_tensor(X.contiguous(), y=y, y_name="response", y_categorical=True)
+    fr.vecs[-1].domain = ["0", "1"]
     fr.key = dest
     DKV.put(dest, fr)
     return {"key": dest, "rows": global_nrows(fr, cl.comm), "cols": fr.ncols}

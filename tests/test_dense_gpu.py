@@ -89,3 +89,23 @@ def test_mlp_elementwise(cuda_dev):
     D.adadelta_(W, G, e1, e2, 0.99, 1e-8, 1e-5)
     D.adadelta_(Wc, G.cpu(), e1c, e2c, 0.99, 1e-8, 1e-5)
     assert torch.allclose(W.cpu(), Wc, atol=1e-6)
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb", [(512, 200, 8192, True, False), (512, 512, 8192, True, False),
+                                         (2, 512, 8192, True, False), (130, 70, 5000, False, True)])
+def test_gemm_splitk_matches_torch(cuda_dev, M, N, K, ta, tb):
+    """Weight-gradient shaped GEMMs (small output, long K) take the split-K path."""
+    torch.manual_seed(2)
+    A = torch.randn((K, M) if ta else (M, K), device=cuda_dev)
+    B = torch.randn((N, K) if tb else (K, N), device=cuda_dev)
+    C = D.gemm(A, B, None, 0, ta, tb)
+    ref = (A.T if ta else A).double() @ (B.T if tb else B).double()
+    assert torch.allclose(C.double(), ref, rtol=1e-4, atol=2e-2)
+    C2 = D.gemm(A, B, None, 0, ta, tb)
+    assert torch.equal(C, C2)   # deterministic
+
+
+def test_bias_grad_split(cuda_dev):
+    dY = torch.randn(8192, 300, device=cuda_dev)
+    db = D.bias_grad(dY)
+    assert torch.allclose(db.double(), dY.double().sum(0), atol=1e-3)
