@@ -114,6 +114,7 @@ class Model:
                                           "percentage": p} for v, r, s, p in self.varimp()],
                 "scoring_history": self.scoring_history,
                 "run_time": self.run_time_ms,
+                "h2omx_timings": {k: _jsonable(v) for k, v in (self.timings or {}).items()},
                 "model_summary": self.summary(),
                 "cross_validation_models": [{"name": m.model_id} for m in self.cv_models],
             },

@@ -227,7 +227,7 @@ class H2ODeepLearningEstimator(ModelBuilder):
                     train_samples_per_iteration=-2, score_training_samples=10000, score_each_iteration=False,
                     stopping_rounds=5, stopping_metric="AUTO", stopping_tolerance=0.0, huber_alpha=0.9,
                     shuffle_training_data=True, reproducible=False, categorical_encoding="AUTO",
-                    use_all_factor_levels=True, offset_column=None, balance_classes=False)
+                    use_all_factor_levels=True, offset_column=None, balance_classes=False, checkpoint=None)
 
     def train(self, x=None, y=None, training_frame=None, validation_frame=None, comm=None, **kw):
         if self.params.get("autoencoder"):
@@ -280,6 +280,17 @@ class H2ODeepLearningEstimator(ModelBuilder):
         seed = self._seed()
         gen = torch.Generator().manual_seed(seed)
         net = _Net(sizes, act, dev, gen, float(p_["initial_weight_scale"]), str(p_["initial_weight_distribution"]))
+        epochs_done = 0.0
+        ck = p_.get("checkpoint")
+        if ck:
+            # H2O checkpoint: continue training a previous model; `epochs` counts the total
+            from ..frame.frame import DKV
+
+            prev = DKV.get(ck) if isinstance(ck, str) else ck
+            if not isinstance(prev, DeepLearningModel) or prev.net.sizes != sizes or prev.act != act:
+                raise ValueError(f"checkpoint {ck!r} is not a DeepLearning model with the same architecture")
+            net.flat.copy_(prev.net.flat.to(dev))
+            epochs_done = float(getattr(prev, "epochs_trained", 0.0))
         if comm is not None and world > 1:
             comm.broadcast(net.flat, 0)
         gen_dev = torch.Generator(device=dev).manual_seed(seed + 1000003 * (comm.rank if comm else 0))
@@ -296,9 +307,9 @@ class H2ODeepLearningEstimator(ModelBuilder):
         n_min = n
         if comm is not None and world > 1:
             n_min = int(-comm.max_scalar(-float(n)))
-        epochs = float(p_["epochs"])
+        epochs = max(0.0, float(p_["epochs"]) - epochs_done)
         steps_per_epoch = max(1, n_min // M)
-        total_steps = max(1, int(round(epochs * steps_per_epoch)))
+        total_steps = max(1, int(round(epochs * steps_per_epoch))) if epochs > 0 else 0
         adaptive = bool(p_["adaptive_rate"])
         Eg2 = torch.zeros_like(net.flat)
         Edx2 = torch.zeros_like(net.flat)
@@ -308,7 +319,13 @@ class H2ODeepLearningEstimator(ModelBuilder):
         model = DeepLearningModel(self, model_id, design, net, act, y_mean, y_sd, auto)
         history = []
         perm = None
-        best, since_best = float("inf"), 0
+        from ..runtime.jobs import current_job
+        from .scoring import ScoreKeeper
+
+        keeper = ScoreKeeper(p_["stopping_metric"] if not auto else "mse",
+                             self.category if not auto else "Regression", int(p_["stopping_rounds"] or 0),
+                             float(p_["stopping_tolerance"]))
+        job = current_job()
         samples = 0
         score_every = max(1, steps_per_epoch)
         for step in range(total_steps):
@@ -348,19 +365,22 @@ class H2ODeepLearningEstimator(ModelBuilder):
                 net.flat.sub_(l1 * torch.sign(net.flat) * (1.0 if adaptive else float(p_["rate"])))
             if math.isfinite(float(p_["max_w2"])):
                 self._clip_w2(net, float(p_["max_w2"]))
+            if job is not None:
+                job.progress = (step + 1) / total_steps
             if (step + 1) % score_every == 0 or step == total_steps - 1:
-                ent = self._score_entry(model, X, Y, cls, auto, (step + 1) / steps_per_epoch, samples, comm)
+                ent = self._score_entry(model, X, Y, cls, auto, epochs_done + (step + 1) / steps_per_epoch,
+                                        samples, comm)
                 history.append(ent)
-                metric = ent["training_loss"]
-                sr = int(p_["stopping_rounds"] or 0)
-                if sr > 0:
-                    if metric < best * (1 - float(p_["stopping_tolerance"])):
-                        best, since_best = metric, 0
-                    else:
-                        since_best += 1
-                        if since_best >= sr:
-                            break
+                mk = {"logloss": ent["training_loss"], "MSE": ent["training_loss"],
+                      "mean_residual_deviance": ent["training_loss"]}
+                stop = keeper.record(ent, mk)
+                cancel = 1.0 if (job is not None and job.cancel_requested) else 0.0
+                if comm is not None and world > 1:
+                    cancel = float(comm.all_reduce_numpy(np.array([cancel]), "max")[0])
+                if stop or cancel > 0:
+                    break
         model.scoring_history = history
+        model.epochs_trained = epochs_done + (step + 1) / steps_per_epoch if total_steps else epochs_done
         if auto:
             model.training_metrics = {"MSE": history[-1]["training_loss"] if history else float("nan")}
         return model

@@ -119,11 +119,13 @@ def init_margin(dist: str, y: np.ndarray, w: np.ndarray | None, K: int) -> np.nd
 def train_ensemble(bm: BinnedMatrix, y, w=None, *, dist: str = "bernoulli", ntrees: int = 50,
                    tparams: TreeParams | None = None, sample_rate: float = 1.0, nclass: int = 1,
                    seed: int = 0, comm=None, init_f: np.ndarray | None = None, callback=None,
-                   dist_kw: dict | None = None) -> TreeEnsemble:
+                   dist_kw: dict | None = None, base_margin=None) -> TreeEnsemble:
     """Grow an ensemble on binned data.
 
     ``y``: float targets (class index for multinomial / multi-class DRF).
     ``dist``: gaussian|bernoulli|multinomial|poisson|gamma|tweedie|laplace|quantile|huber|drf.
+    ``base_margin``: [K][n] starting margins (checkpoint continuation) instead of ``init_f``.
+    ``callback(t, view)``: called after every iteration; returning True stops training.
     """
     tparams = tparams or TreeParams()
     dist_kw = dist_kw or {}
@@ -140,6 +142,7 @@ def train_ensemble(bm: BinnedMatrix, y, w=None, *, dist: str = "bernoulli", ntre
     ens = TreeEnsemble(trees=np.zeros((0, tree_capacity(tparams.max_depth)), TREE_NODE_DTYPE), K=K, dist=dist,
                        init_f=np.asarray(init_f, np.float64), average=(dist == "drf"), nbt=bm.nbt,
                        feature_names=list(bm.names), edges=bm.edges_numpy())
+    ens._base_margin = base_margin
     if bm.codes.is_cuda:
         _train_gpu(bm, y_np, w_np, ens, ntrees, tparams, sample_rate, seed, comm, callback, dist_kw)
     else:
@@ -162,12 +165,15 @@ def _global_init(dist, y, w, K, comm):
 
 
 class _GpuState:
-    def __init__(self, bm, y_np, w_np, K, dist, init_f):
+    def __init__(self, bm, y_np, w_np, K, dist, init_f, base_margin=None):
         dev = bm.device
         npad, n = bm.npad, bm.n
         self.Fm = torch.zeros((K, npad), dtype=torch.float32, device=dev)
-        for k in range(K):
-            self.Fm[k, :n] = float(init_f[k])
+        if base_margin is not None:
+            self.Fm[:, :n] = base_margin.to(dev).float()
+        else:
+            for k in range(K):
+                self.Fm[k, :n] = float(init_f[k])
         yp = np.zeros(npad, np.float32)
         yp[:n] = y_np
         self.y = torch.from_numpy(yp).to(dev)
@@ -192,7 +198,7 @@ class GpuBooster:
         self.sample_rate, self.seed = sample_rate, seed
         self.dev = bm.device
         self.K, self.dist = ens.K, ens.dist
-        self.st = _GpuState(bm, y_np, w_np, self.K, self.dist, ens.init_f)
+        self.st = _GpuState(bm, y_np, w_np, self.K, self.dist, ens.init_f, getattr(ens, "_base_margin", None))
         self.builder = HipTreeBuilder(bm, tp, comm)
         self.cap = self.builder.capacity
         self.trees_dev = []
@@ -210,10 +216,12 @@ class GpuBooster:
         gp = make_grad_params(dist or self.dist, apply, self.sample_rate, self.seed, next_tree,
                               row_base=self.builder.row_base, **self.kw)
         y = st.ycls[k] if (self.dist == "drf" and self.K > 1) else st.y
-        ops.check(self.lib.h2omx_boost_update(P(st.Fm[k]), P(y), P(st.w), self.bm.n, self.bm.npad, P(b.nid),
-                                              P(b.tree_buf), ctypes.addressof(gp), P(st.g[k]), P(st.h[k]),
-                                              P(self.wout), P(b.stat_slab), ops.stream(self.dev)), "boost_update")
-        b.reduce_stats()
+        with b.timer.phase("grad"):
+            ops.check(self.lib.h2omx_boost_update(P(st.Fm[k]), P(y), P(st.w), self.bm.n, self.bm.npad, P(b.nid),
+                                                  P(b.tree_buf), ctypes.addressof(gp), P(st.g[k]), P(st.h[k]),
+                                                  P(self.wout), P(b.stat_slab), ops.stream(self.dev)),
+                      "boost_update")
+            b.reduce_stats()
 
     def step(self):
         P, st, b, bm, t = ops.P, self.st, self.builder, self.bm, self.t
@@ -249,6 +257,8 @@ class GpuBooster:
 
     def finish(self) -> TreeEnsemble:
         torch.cuda.synchronize(self.dev)
+        if self.builder.timer.enabled:
+            self.ens.timings.update({f"gpu_ms_{k}": v for k, v in self.builder.timer.totals().items()})
         if self.trees_dev:
             self.ens.trees = trees_from_bytes(torch.stack(self.trees_dev).cpu().numpy(), self.cap)
         self.ens._state = self.st
@@ -260,10 +270,43 @@ def _train_gpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callbac
     gb = GpuBooster(bm, y_np, w_np, ens, tp, sample_rate, seed, comm, dist_kw)
     for t in range(ntrees):
         gb.step()
-        if callback is not None:
-            callback(t, gb.st)
+        if callback is not None and callback(t, _GpuView(gb)) is True:
+            break
     gb.finish()
     ens.timings["train_s"] = time.perf_counter() - t0
+
+
+class _GpuView:
+    """What a training callback sees (scoring / early stopping / cancel)."""
+
+    def __init__(self, gb):
+        self.gb = gb
+        self.init_f = gb.ens.init_f
+
+    @property
+    def margin(self) -> torch.Tensor:
+        return self.gb.st.Fm[:, : self.gb.bm.n]
+
+    def trees(self, lo: int, hi: int) -> np.ndarray:
+        """Tree records of iterations [lo, hi) (K trees each)."""
+        K = self.gb.K
+        bufs = self.gb.trees_dev[lo * K: hi * K]
+        if not bufs:
+            return np.zeros((0, self.gb.cap), TREE_NODE_DTYPE)
+        return trees_from_bytes(torch.stack(bufs).cpu().numpy(), self.gb.cap)
+
+
+class _CpuView:
+    def __init__(self, Fm, trees, K, init_f):
+        self.Fm, self._trees, self.K, self.init_f = Fm, trees, K, init_f
+
+    @property
+    def margin(self) -> torch.Tensor:
+        return torch.from_numpy(self.Fm)
+
+    def trees(self, lo: int, hi: int) -> np.ndarray:
+        sel = self._trees[lo * self.K: hi * self.K]
+        return np.stack(sel) if sel else np.zeros((0, 1), TREE_NODE_DTYPE)
 
 
 def _tree_fmask(tp: TreeParams, F: int, t: int, dev):
@@ -284,7 +327,9 @@ def _train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callbac
     from .engine import global_row_base
 
     row_base = global_row_base(n, comm)
-    Fm = np.repeat(ens.init_f[:, None], n, 1).astype(np.float32)
+    bmg = getattr(ens, "_base_margin", None)
+    Fm = (bmg.cpu().numpy().astype(np.float32).copy() if bmg is not None
+          else np.repeat(ens.init_f[:, None], n, 1).astype(np.float32))
     wobs = np.ones(n, np.float32) if w_np is None else w_np.astype(np.float32)
     trees = []
     t0 = time.perf_counter()
@@ -313,8 +358,8 @@ def _train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callbac
             leaf = ~builder.nid[:n]
             Fm[k] += tree["value"][leaf]
             trees.append(tree)
-        if callback is not None:
-            callback(t, Fm)
+        if callback is not None and callback(t, _CpuView(Fm, trees, K, ens.init_f)) is True:
+            break
     ens.timings["train_s"] = time.perf_counter() - t0
     ens.trees = np.stack(trees) if trees else ens.trees
     ens._cpu_margin = Fm

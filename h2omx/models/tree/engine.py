@@ -26,6 +26,7 @@ import torch
 
 from ... import ops
 from .binning import BinnedMatrix
+from ...utils.trace import PhaseTimer
 from .structs import (FEAT_BEST_BYTES, NODE_LINK_BYTES, PART_INFO_BYTES, TREE_NODE_DTYPE, GradParams,
                       SplitParams, check_layout)
 
@@ -111,6 +112,7 @@ class HipTreeBuilder:
                                       device=d) if self.capacity <= 2048 else None)
         self._sp = SplitParams()
         self.stats = {"host_syncs": 0}
+        self.timer = PhaseTimer(device=d)
         # global index of this rank's first row: the stochastic-rounding dither and
         # bagging hash use global row ids, so a multi-GPU model is bit-identical to
         # the single-GPU model on the concatenated rows
@@ -225,9 +227,11 @@ class HipTreeBuilder:
         s2 = w if p.mode == 0 else h
         link = [self._buf("link0", 4, torch.int32), None]
         # scales + level-0 control block/link + zeroed leaf sums in one launch
-        ops.check(lib.h2omx_tree_begin(P(self.stat_max), p.mode, self.max_rows_per_wg, P(self.qscale),
-                                       P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(),
-                                       self.row_base, st), "tree_begin")
+        T = self.timer.phase
+        with T("tree_begin"):
+            ops.check(lib.h2omx_tree_begin(P(self.stat_max), p.mode, self.max_rows_per_wg, P(self.qscale),
+                                           P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(),
+                                           self.row_base, st), "tree_begin")
         full_prev = None
         max_depth = p.max_depth
         max_nodes = 1
@@ -253,22 +257,26 @@ class HipTreeBuilder:
             hb = lib.h2omx_hist_build_compact if (d > 0 and self.COMPACT) else lib.h2omx_hist_build
             for ps in range(plan["passes"]):
                 slot_lo = ps * plan["slot_cnt"]
-                ops.check(hb(P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]),
-                             P(ctl_cur), P(bm.nvb), P(self.qscale), tree_index & 0x7FFFFFFF,
-                             F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo,
-                             plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"], P(partials), st),
-                          "hist_build")
-                ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F, nbt,
-                                                slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st), "hist_reduce")
+                with T("hist"):
+                    ops.check(hb(P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]),
+                                 P(ctl_cur), P(bm.nvb), P(self.qscale), tree_index & 0x7FFFFFFF,
+                                 F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo,
+                                 plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"], P(partials), st),
+                              "hist_build")
+                    ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F,
+                                                    nbt, slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st),
+                              "hist_reduce")
             if comm is not None:
-                comm.all_reduce_(built[: max_slots * self.per_node])
+                with T("allreduce"):
+                    comm.all_reduce_(built[: max_slots * self.per_node])
             full_cur = None if last else self._buf(f"full{cur}", max_nodes * self.per_node, torch.int64)
             fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
             sp.depth = d
             sp.children_leaves = 1 if last else 0
-            ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
-                                           P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
-                                           P(fbest), st), "split_find")
+            with T("split"):
+                ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
+                                               P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
+                                               P(fbest), st), "split_find")
             next_nodes = 2 * max_nodes
             part = self._buf("part", max_nodes * PART_INFO_BYTES // 4, torch.int32)
             nl = None
@@ -276,28 +284,31 @@ class HipTreeBuilder:
                 nl = self._buf(f"link{nxt}", next_nodes * NODE_LINK_BYTES // 4, torch.int32)
                 link[nxt] = nl
             nsplit = self._buf("nsplit", max_nodes * 9, torch.float64)  # NodeSplit = 72 B
-            ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges), P(bm.nvb), nbt,
-                                               next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
-                                               P(nsplit), max_nodes, st),
-                      "level_finalize")
+            with T("split"):
+                ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges), P(bm.nvb),
+                                                   nbt, next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
+                                                   P(nsplit), max_nodes, st), "level_finalize")
             slab = None
             if self.leaf_slab is not None:
                 slab = self.leaf_slab[n_part * self.part_blocks * 3 * self.capacity:]
-            ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, P(g), P(h), P(w),
-                                          P(self.qscale), self.capacity, P(self.leaf_acc), P(slab),
-                                          self.part_blocks, st),
-                      "partition")
+            with T("partition"):
+                ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, P(g), P(h), P(w),
+                                              P(self.qscale), self.capacity, P(self.leaf_acc), P(slab),
+                                              self.part_blocks, st), "partition")
             n_part += 1
             full_prev = full_cur
             max_nodes = next_nodes
         # exact leaf values (sums accumulated by the partition kernels)
         if self.leaf_slab is not None:
-            ops.check(lib.h2omx_leaf_reduce(P(self.leaf_slab), n_part * self.part_blocks, self.capacity,
-                                            P(self.leaf_acc), st), "leaf_reduce")
+            with T("leaf"):
+                ops.check(lib.h2omx_leaf_reduce(P(self.leaf_slab), n_part * self.part_blocks, self.capacity,
+                                                P(self.leaf_acc), st), "leaf_reduce")
         if comm is not None:
-            comm.all_reduce_(self.leaf_acc)
-        ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(self.ctl[max_depth % 2]), P(self.qscale), spp,
-                                          P(self.tree_buf), self.capacity, st), "leaf_finalize")
+            with T("allreduce"):
+                comm.all_reduce_(self.leaf_acc)
+        with T("leaf"):
+            ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(self.ctl[max_depth % 2]), P(self.qscale), spp,
+                                              P(self.tree_buf), self.capacity, st), "leaf_finalize")
         return self.tree_buf
 
     def _build_seg(self, g, h, w, tree_index, tree_fmask):

@@ -14,7 +14,7 @@ import math
 import numpy as np
 import torch
 
-from ..frame.frame import ENUM, Frame
+from ..frame.frame import ENUM, Frame, Vec
 from .base import Model, ModelBuilder, ModelCategory
 from .tree import TreeParams, bin_matrix, compute_edges, train_ensemble
 
@@ -130,21 +130,136 @@ class _TreeBuilder(ModelBuilder):
         init_f = None
         if self.params.get("offset_column"):
             raise NotImplementedError("offset_column is not supported by the tree engine yet")
-        ens = train_ensemble(bm, y, w, dist=ens_dist, ntrees=int(self.params["ntrees"]), tparams=tp,
+        ntrees = int(self.params["ntrees"])
+        ckpt = self._checkpoint_ensemble()
+        if ckpt is not None:
+            # H2O checkpoint: continue a previous model up to `ntrees` total trees
+            init_f = None
+            ntrees = max(0, ntrees - ckpt.ntrees)
+        scorer = _TreeScoring(self, train, valid, X, y, w, ens_dist, nclass, ckpt)
+        ens = train_ensemble(bm, y, w, dist=ens_dist, ntrees=ntrees, tparams=tp,
                              sample_rate=float(self.params.get("sample_rate", 1.0)), nclass=nclass,
                              seed=self._seed(), comm=self.comm, init_f=init_f,
+                             callback=scorer if scorer.active else None,
+                             base_margin=None if ckpt is None else ckpt.raw_margin(X),
                              dist_kw={"tweedie_power": float(self.params.get("tweedie_power", 1.5)),
                                       "quantile_alpha": float(self.params.get("quantile_alpha", 0.5)),
                                       "huber_delta": float(self.params.get("huber_alpha", 0.9))})
+        if ckpt is not None:
+            ens.trees = np.concatenate([ckpt.trees, ens.trees]) if len(ens.trees) else ckpt.trees
+            ens.init_f = ckpt.init_f
         model = self.model_cls(self, model_id, ens, ens_dist)
         model.timings = dict(ens.timings)
+        model.scoring_history = scorer.history
         return model
+
+    def _checkpoint_ensemble(self):
+        ck = self.params.get("checkpoint")
+        if not ck:
+            return None
+        from ..frame.frame import DKV
+
+        m = DKV.get(ck) if isinstance(ck, str) else ck
+        if m is None or not hasattr(m, "ens"):
+            raise ValueError(f"checkpoint model {ck!r} not found or not a tree model")
+        if list(m.x) != list(self.x):
+            raise ValueError("checkpoint model was trained on different predictors")
+        if m.ens.trees.shape[1] != (1 << (int(self.params["max_depth"]) + 1)) - 1 and m.ens.trees.size:
+            raise ValueError("checkpoint continuation requires the same max_depth")
+        return m.ens
 
     def _engine_dist(self, dist: str) -> str:
         return dist
 
 
 # ---------------------------------------------------------------------------
+class _TreeScoring:
+    """Training callback: scoring history every ``score_tree_interval`` trees
+    (training metrics from the device margins, validation metrics from the
+    new trees scored on the validation frame), early stopping, job cancel."""
+
+    def __init__(self, builder, train, valid, X, y, w, dist, nclass, ckpt):
+        from .scoring import ScoreKeeper
+
+        p = builder.params
+        self.b, self.dist, self.valid = builder, dist, valid
+        self.category = builder.category
+        self.k = int(p.get("stopping_rounds") or 0)
+        iv = int(p.get("score_tree_interval") or 0)
+        self.interval = iv if iv > 0 else (5 if (self.k > 0 or valid is not None) else 0)
+        self.keeper = ScoreKeeper(p.get("stopping_metric", "AUTO"), self.category, self.k,
+                                  float(p.get("stopping_tolerance", 1e-3)))
+        self.w = w
+        yv = train.vec(builder.y)
+        if self.category in ("Binomial", "Multinomial"):
+            self.yv = Vec(builder.y, y.to(torch.int32), ENUM, list(yv.domain))
+        else:
+            self.yv = Vec(builder.y, y.float(), "real")
+        self.n_ckpt = ckpt.ntrees if ckpt is not None else 0
+        self.vmargin = None
+        self.done = 0
+        if valid is not None and self.interval:
+            Xv = valid.feature_matrix(builder.x)
+            self.Xv = Xv
+            K = ckpt.K if ckpt is not None else (nclass if dist == "multinomial" or (dist == "drf" and nclass > 2) else 1)
+            self.vmargin = ckpt.raw_margin(Xv).to(Xv.device) if ckpt is not None else None
+            self.K = K
+        from ..runtime.jobs import current_job
+
+        self.job = current_job()
+        comm = builder.comm
+        self.multi = comm is not None and comm.world_size > 1
+        # cancellation is decided collectively so every rank stops on the same tree
+        self.cancel_every = 10 if self.multi else 1
+        self.active = bool(self.interval) or self.job is not None or self.multi
+
+    @property
+    def history(self):
+        return self.keeper.history
+
+    def __call__(self, t, view):
+        from ..metrics import binomial_metrics, multinomial_metrics, regression_metrics  # noqa: F401
+        from .base import compute_metrics
+        from .scoring import margins_to_scores
+
+        if self.job is not None:
+            self.job.progress = (t + 1) / max(1, int(self.b.params["ntrees"]))
+        if (t + 1) % self.cancel_every == 0:
+            flag = 1.0 if (self.job is not None and self.job.cancel_requested) else 0.0
+            if self.multi:
+                flag = float(self.b.comm.all_reduce_numpy(np.array([flag]), "max")[0])
+            if flag > 0:
+                return True
+        if not self.interval or (t + 1) % self.interval:
+            return False
+        ntot = self.n_ckpt + t + 1
+        comm = self.b.comm
+        cat = self.category
+        P = margins_to_scores(view.margin.to(self.yv.data.device).float(), self.dist, cat, ntot)
+        tm = compute_metrics(cat, P, self.yv, self.w, comm, self.dist)
+        entry = {"number_of_trees": ntot}
+        entry.update({f"training_{k.lower()}": v for k, v in tm.items() if isinstance(v, float)})
+        metrics = tm
+        if self.vmargin is not None or (self.valid is not None and hasattr(self, "Xv")):
+            from .tree.boost import TreeEnsemble
+
+            new = view.trees(self.done, t + 1)
+            part = TreeEnsemble(new, self.K, self.dist, np.zeros(self.K), average=False)
+            m = part.raw_margin(self.Xv).to(self.Xv.device) if len(new) else 0.0
+            if self.vmargin is None:
+                init = 0.0 if self.dist == "drf" else torch.from_numpy(
+                    np.asarray(view.init_f, np.float32)).to(self.Xv.device)[:, None]
+                self.vmargin = init + m
+            else:
+                self.vmargin = self.vmargin + m
+            self.done = t + 1
+            Pv = margins_to_scores(self.vmargin, self.dist, cat, ntot)
+            vm = compute_metrics(cat, Pv, self.valid.vec(self.b.y), None, comm, self.dist)
+            entry.update({f"validation_{k.lower()}": v for k, v in vm.items() if isinstance(v, float)})
+            metrics = vm
+        return self.keeper.record(entry, metrics)
+
+
 class GBMModel(TreeModel):
     algo = "gbm"
     algo_full_name = "Gradient Boosting Machine"
@@ -159,7 +274,7 @@ class H2OGradientBoostingEstimator(_TreeBuilder):
                     col_sample_rate_per_tree=1.0, min_split_improvement=1e-5, histogram_type="QuantilesGlobal",
                     max_abs_leafnode_pred=0.0, tweedie_power=1.5, quantile_alpha=0.5, huber_alpha=0.9,
                     stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0,
-                    offset_column=None, balance_classes=False, categorical_encoding="AUTO")
+                    offset_column=None, balance_classes=False, categorical_encoding="AUTO", checkpoint=None)
 
     def _tree_params(self, nfeat):
         p = self.params
@@ -189,7 +304,7 @@ class H2OXGBoostEstimator(_TreeBuilder):
                     reg_alpha=0.0, gamma=0.0, min_split_improvement=None, max_bins=256, tree_method="hist",
                     booster="gbtree", grow_policy="depthwise", max_abs_leafnode_pred=0.0, tweedie_power=1.5,
                     stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0,
-                    offset_column=None, backend="gpu", nbins=None, categorical_encoding="AUTO")
+                    offset_column=None, backend="gpu", nbins=None, categorical_encoding="AUTO", checkpoint=None)
 
     def _tree_params(self, nfeat):
         p = self.params
@@ -225,7 +340,7 @@ class H2ORandomForestEstimator(_TreeBuilder):
                     mtries=-1, sample_rate=0.632, col_sample_rate_per_tree=1.0, min_split_improvement=1e-5,
                     binomial_double_trees=False, histogram_type="QuantilesGlobal", stopping_rounds=0,
                     stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0, balance_classes=False,
-                    categorical_encoding="AUTO", offset_column=None)
+                    categorical_encoding="AUTO", offset_column=None, checkpoint=None)
 
     def _engine_dist(self, dist):
         return "drf"

@@ -12,6 +12,14 @@ import time
 import traceback
 import uuid
 
+_local = threading.local()
+
+
+def current_job():
+    """The Job the calling thread is executing (None outside jobs): model
+    builders report progress and honour cancellation through it."""
+    return getattr(_local, "job", None)
+
 
 class Job:
     def __init__(self, description: str, dest: str, dest_type: str):
@@ -68,6 +76,7 @@ class JobRegistry:
 
         def run():
             job.status = "RUNNING"
+            _local.job = job
             try:
                 job.result = fn(job, *args, **kw)
                 if job.cancel_requested:
@@ -80,6 +89,7 @@ class JobRegistry:
                 job.exception = f"{type(e).__name__}: {e}"
                 job.stacktrace = traceback.format_exc()
             finally:
+                _local.job = None
                 job.end_time = int(time.time() * 1000)
 
         if sync:

@@ -143,3 +143,34 @@ def test_parse_csv_native(tmp_path):
     assert fr.shape == (3, 3)
     assert list(pdf["b"].astype(str)) == ["x", "y", "x"]
     assert np.isnan(pdf["c"].iloc[1])
+
+
+def test_tree_early_stopping_checkpoint_and_scoring_history():
+    df = _binary_frame(n=4000, seed=1)
+    fr = Frame.from_pandas(df)
+    tr, va = fr.split_frame((0.7,), seed=3)
+    m = H2OGradientBoostingEstimator(ntrees=200, max_depth=6, learn_rate=0.3, stopping_rounds=3,
+                                     stopping_tolerance=1e-3, seed=1).train(y="y", training_frame=tr,
+                                                                            validation_frame=va)
+    assert m.ens.ntrees < 200                       # overfitting stopped early
+    assert "validation_logloss" in m.scoring_history[-1]
+    a = H2OGradientBoostingEstimator(ntrees=10, max_depth=3, seed=1).train(y="y", training_frame=tr)
+    b = H2OGradientBoostingEstimator(ntrees=25, max_depth=3, seed=1, checkpoint=a.model_id).train(
+        y="y", training_frame=tr)
+    c = H2OGradientBoostingEstimator(ntrees=25, max_depth=3, seed=1).train(y="y", training_frame=tr)
+    assert b.ens.ntrees == 25
+    assert abs(b.training_metrics["AUC"] - c.training_metrics["AUC"]) < 1e-9   # continuation == one run
+    d = H2ORandomForestEstimator(ntrees=20, seed=1, score_tree_interval=10).train(y="y", training_frame=tr,
+                                                                                  validation_frame=va)
+    assert [e["number_of_trees"] for e in d.scoring_history] == [10, 20]
+
+
+def test_deeplearning_checkpoint_continues():
+    df = _binary_frame(n=2000, seed=2)
+    fr = Frame.from_pandas(df)
+    a = H2ODeepLearningEstimator(hidden=[16], epochs=2, seed=1).train(y="y", training_frame=fr)
+    b = H2ODeepLearningEstimator(hidden=[16], epochs=6, seed=1, checkpoint=a.model_id).train(y="y", training_frame=fr)
+    assert abs(b.epochs_trained - 6) < 0.2
+    assert b.scoring_history[0]["epochs"] > 2
+    with pytest.raises(ValueError):
+        H2ODeepLearningEstimator(hidden=[8], epochs=3, checkpoint=a.model_id).train(y="y", training_frame=fr)
