@@ -386,74 +386,152 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
 // 256 threads, 128x128 block tile, each wave a 64x64 quadrant = 2x2 MFMA
 // tiles of 32x32, K staged 16 at a time through LDS as [k][m] / [k][n].
 // ===========================================================================
-constexpr int GB = 128, GK = 16;
+constexpr int GB = 128, GK = 32, GPAD = 4;
 
+// One K-step of a 128 x 32 operand tile: global -> registers (float4 along
+// the contiguous dimension when the leading dimension allows it).
+// "MK" layout: element (m, k) at P[m * ld + k] (contiguous along k);
+// "KM" layout: element (m, k) at P[k * ld + m] (contiguous along m).
+constexpr int GTHREADS = 512;   // 8 waves per 128 x 128 tile
+constexpr int GLD = GB * GK / 4 / GTHREADS;  // float4 per thread per operand tile
+
+struct TileRegs {
+  float v[4 * GLD];
+};
+
+template <bool KM>
+__device__ __forceinline__ void load_tile(const float* __restrict__ P, int ld, int rows, int k_lim, int r0, int k0,
+                                          bool vec, TileRegs& t) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < GLD; ++q) {
+    const int f = tid + GTHREADS * q;  // float4 index in the 128 x 32 tile
+    int r, k;
+    if (KM) { k = f >> 5; r = (f & 31) * 4; }   // 32 float4 per k-row of 128
+    else { r = f >> 3; k = (f & 7) * 4; }       // 8 float4 per m-row of 32
+    const int gr = r0 + r, gk = k0 + k;
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f;
+    if (KM) {
+      if (gk < k_lim) {
+        const float* src = P + (int64_t)gk * ld + gr;
+        if (vec && gr + 3 < rows) {
+          const float4 v4 = *reinterpret_cast<const float4*>(src);
+          x0 = v4.x; x1 = v4.y; x2 = v4.z; x3 = v4.w;
+        } else {
+          if (gr < rows) x0 = src[0];
+          if (gr + 1 < rows) x1 = src[1];
+          if (gr + 2 < rows) x2 = src[2];
+          if (gr + 3 < rows) x3 = src[3];
+        }
+      }
+    } else {
+      if (gr < rows) {
+        const float* src = P + (int64_t)gr * ld + gk;
+        if (vec && gk + 3 < k_lim) {
+          const float4 v4 = *reinterpret_cast<const float4*>(src);
+          x0 = v4.x; x1 = v4.y; x2 = v4.z; x3 = v4.w;
+        } else {
+          if (gk < k_lim) x0 = src[0];
+          if (gk + 1 < k_lim) x1 = src[1];
+          if (gk + 2 < k_lim) x2 = src[2];
+          if (gk + 3 < k_lim) x3 = src[3];
+        }
+      }
+    }
+    t.v[4 * q] = x0; t.v[4 * q + 1] = x1; t.v[4 * q + 2] = x2; t.v[4 * q + 3] = x3;
+  }
+}
+
+// registers -> LDS tile S[k][r] (r contiguous: MFMA operand reads are conflict free)
+template <bool KM>
+__device__ __forceinline__ void store_tile(float (*S)[GB + GPAD], const TileRegs& t) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < GLD; ++q) {
+    const int f = tid + GTHREADS * q;
+    if (KM) {
+      const int k = f >> 5, r = (f & 31) * 4;
+      *reinterpret_cast<float4*>(&S[k][r]) = make_float4(t.v[4 * q], t.v[4 * q + 1], t.v[4 * q + 2], t.v[4 * q + 3]);
+    } else {
+      const int r = f >> 3, k = (f & 7) * 4;
+      S[k][r] = t.v[4 * q];
+      S[k + 1][r] = t.v[4 * q + 1];
+      S[k + 2][r] = t.v[4 * q + 2];
+      S[k + 3][r] = t.v[4 * q + 3];
+    }
+  }
+}
+
+// MLP GEMM on the fp32 matrix cores:
+//   C[M][N] = act(op(A)[M][K] op(B)[K][N] + bias[N] (+ beta_c C)), row-major.
+//   TA: A stored [K][M]; TB: B stored [N][K].
+// 512 threads, 128 x 128 block tile, 8 waves of 32 x 64 (2 MFMA 32x32x2
+// accumulators each; 8 waves per CU even when the grid has only one tile
+// per CU).  K advances 32 per step through double-
+// buffered LDS; the next step's global loads are issued into registers
+// before the current step's 64 MFMAs per wave, so HBM latency hides behind
+// matrix-core work.  blockIdx.z splits K (split-K partials, see
+// gemm_splitk_reduce_kernel).
 template <bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_kernel(const float* __restrict__ A, const float* __restrict__ B,
-                                                   float* __restrict__ Cm, const float* __restrict__ bias, int M,
-                                                   int N, int K, int act, float beta_c) {
-  __shared__ float As[GK][GB + 4];
-  __shared__ float Bs[GK][GB + 4];
+__global__ __launch_bounds__(512, 1) void gemm_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                      float* __restrict__ Cm, const float* __restrict__ bias, int M,
+                                                      int N, int K, int act, float beta_c) {
+  __shared__ __attribute__((aligned(16))) float As[2][GK][GB + GPAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][GK][GB + GPAD];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int m0 = blockIdx.y * GB, n0 = blockIdx.x * GB;
-  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
-  const int li = lane & 31, lh = lane >> 5;
-  // split-K: blockIdx.z owns K range [kb, ke) (multiple of GK); partial tiles
-  // go to the workspace Cm + z*M*N and gemm_splitk_reduce applies the epilogue
+  const int wm = (wid >> 1) * 32, wn = (wid & 1) * 64;
   const int S = gridDim.z;
   const int kchunk = ((K + S - 1) / S + GK - 1) / GK * GK;
   const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
   if (S > 1) Cm += (int64_t)blockIdx.z * M * N;
-  for (int k0 = kb; k0 < ke; k0 += GK) {
-    // stage A tile (GB x GK) as As[k][m]
-    for (int j = t; j < GB * GK; j += 256) {
-      int m, kk;
-      if (TA) { m = j % GB; kk = j / GB; }  // A^T stored [K][M]: coalesced along m
-      else { kk = j % GK; m = j / GK; }     // A stored [M][K]: coalesced along k
-      const int gm = m0 + m, gk = k0 + kk;
-      float v = 0.0f;
-      if (gm < M && gk < ke) v = TA ? A[(int64_t)gk * M + gm] : A[(int64_t)gm * K + gk];
-      As[kk][m] = v;
-    }
-    for (int j = t; j < GB * GK; j += 256) {
-      int nn, kk;
-      if (TB) { kk = j % GK; nn = j / GK; }  // B^T stored [N][K]: coalesced along k
-      else { nn = j % GB; kk = j / GB; }     // B stored [K][N]: coalesced along n
-      const int gn = n0 + nn, gk = k0 + kk;
-      float v = 0.0f;
-      if (gn < N && gk < ke) v = TB ? B[(int64_t)gn * K + gk] : B[(int64_t)gk * N + gn];
-      Bs[kk][nn] = v;
-    }
-    __syncthreads();
+  // A as (m, k): TA -> KM layout (ld = M), else MK (ld = K); B as (n, k): TB -> MK (ld = K), else KM (ld = N)
+  const bool va = (TA ? (M % 4 == 0) : (K % 4 == 0)) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  const bool vb = (TB ? (K % 4 == 0) : (N % 4 == 0)) && ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
+  f32x16 acc[2];
 #pragma unroll
-    for (int s = 0; s < GK / 2; ++s) {
-      const int kk = 2 * s + lh;
-      const float a0 = As[kk][wm + li], a1 = As[kk][wm + 32 + li];
-      const float b0 = Bs[kk][wn + li], b1 = Bs[kk][wn + 32 + li];
-      acc[0][0] = mfma32(a0, b0, acc[0][0]);
-      acc[0][1] = mfma32(a0, b1, acc[0][1]);
-      acc[1][0] = mfma32(a1, b0, acc[1][0]);
-      acc[1][1] = mfma32(a1, b1, acc[1][1]);
+  for (int y = 0; y < 2; ++y)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[y][e] = 0.0f;
+  const int li = lane & 31, lh = lane >> 5;
+  TileRegs ra, rb;
+  int buf = 0;
+  if (kb < ke) {
+    load_tile<TA>(A, TA ? M : K, M, ke, m0, kb, va, ra);
+    load_tile<!TB>(B, TB ? K : N, N, ke, n0, kb, vb, rb);
+    store_tile<TA>(As[0], ra);
+    store_tile<!TB>(Bs[0], rb);
+  }
+  __syncthreads();
+  for (int k0 = kb; k0 < ke; k0 += GK) {
+    const bool more = k0 + GK < ke;
+    if (more) {
+      load_tile<TA>(A, TA ? M : K, M, ke, m0, k0 + GK, va, ra);
+      load_tile<!TB>(B, TB ? K : N, N, ke, n0, k0 + GK, vb, rb);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < GK / 2; ++s2) {
+      const int kk = 2 * s2 + lh;
+      const float a0 = As[buf][kk][wm + li];
+      const float b0 = Bs[buf][kk][wn + li], b1 = Bs[buf][kk][wn + 32 + li];
+      acc[0] = mfma32(a0, b0, acc[0]);
+      acc[1] = mfma32(a0, b1, acc[1]);
+    }
+    if (more) {
+      store_tile<TA>(As[buf ^ 1], ra);
+      store_tile<!TB>(Bs[buf ^ 1], rb);
     }
     __syncthreads();
+    buf ^= 1;
   }
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
+  for (int y = 0; y < 2; ++y)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int i = m0 + wm + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * lh;
-        const int j = n0 + wn + 32 * b + li;
+        const int i = m0 + wm + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        const int j = n0 + wn + 32 * y + li;
         if (i < M && j < N) {
-          float v = acc[a][b][e];
+          float v = acc[y][e];
           if (S > 1) {
             Cm[(int64_t)i * N + j] = v;
             continue;
@@ -642,10 +720,11 @@ H2OMX_API int h2omx_gemm(const float* A, const float* B, float* C, const float* 
   if (splitk < 1 || (splitk > 1 && !ws)) return kBadArg;
   const dim3 grid(cdiv(N, GB), cdiv(M, GB), splitk);
   float* out = splitk > 1 ? ws : C;
-  if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(256), 0, stream, A, B, out, bias, M, N, K, act, beta_c);
-  else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(256), 0, stream, A, B, out, bias, M, N, K, act, beta_c);
-  else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(256), 0, stream, A, B, out, bias, M, N, K, act, beta_c);
-  else hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(256), 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+  const dim3 blk(GTHREADS);
+  if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+  else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+  else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+  else hipLaunchKernelGGL((gemm_kernel<true, true>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
   if (splitk > 1)
     hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(cdiv((int64_t)M * N, 256) < 4096 ? cdiv((int64_t)M * N, 256) : 4096),
                        dim3(256), 0, stream, ws, splitk, M, N, C, bias, act, beta_c);

@@ -94,3 +94,17 @@ def test_tree_estimators_gpu(cuda_dev, cls):
     assert abs(m.training_metrics["AUC"] - mc.training_metrics["AUC"]) < 0.01
     assert m.training_metrics["AUC"] > 0.75
     assert "tree" in " ".join(_native.loaded_libraries())
+
+
+def test_gbm_gpu_early_stopping_and_checkpoint(cuda_dev):
+    df = _binary_df(n=30000, seed=4)
+    fr = Frame.from_pandas(df, device=cuda_dev)
+    tr, va = fr.split_frame((0.7,), seed=3)
+    m = H2OGradientBoostingEstimator(ntrees=300, max_depth=8, learn_rate=0.5, stopping_rounds=3, seed=1,
+                                     score_tree_interval=5).train(y="y", training_frame=tr, validation_frame=va)
+    assert m.ens.ntrees < 300 and "validation_auc" in m.scoring_history[-1]
+    a = H2OGradientBoostingEstimator(ntrees=6, max_depth=4, seed=1).train(y="y", training_frame=tr)
+    b = H2OGradientBoostingEstimator(ntrees=15, max_depth=4, seed=1, checkpoint=a.model_id).train(
+        y="y", training_frame=tr)
+    c = H2OGradientBoostingEstimator(ntrees=15, max_depth=4, seed=1).train(y="y", training_frame=tr)
+    assert abs(b.training_metrics["AUC"] - c.training_metrics["AUC"]) < 1e-6
