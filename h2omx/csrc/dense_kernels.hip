@@ -561,24 +561,28 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __
   }
 }
 
-// column sums over a row slice: ws[blockIdx.y][j] (then summed by gemm_splitk_reduce with M = 1)
+// column sums of dY [M][N] (bias gradients), stage 1: block (64 columns x
+// 4 row phases) sums one row slice, folds the phases in LDS -> ws[slice][col]
 __global__ __launch_bounds__(256) void bias_grad_split_kernel(const float* __restrict__ dY, float* __restrict__ ws,
                                                               int M, int N) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= N) return;
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + c;
   const int S = gridDim.y;
   const int rows = (M + S - 1) / S;
   const int r0 = blockIdx.y * rows, r1 = min(M, r0 + rows);
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int i = r0;
-  for (; i + 3 < r1; i += 4) {
-    s0 += dY[(int64_t)i * N + j];
-    s1 += dY[(int64_t)(i + 1) * N + j];
-    s2 += dY[(int64_t)(i + 2) * N + j];
-    s3 += dY[(int64_t)(i + 3) * N + j];
+  float s0 = 0.f, s1 = 0.f;
+  if (j < N) {
+    int i = r0 + ph;
+    for (; i + 4 < r1; i += 8) {
+      s0 += dY[(int64_t)i * N + j];
+      s1 += dY[(int64_t)(i + 4) * N + j];
+    }
+    for (; i < r1; i += 4) s0 += dY[(int64_t)i * N + j];
   }
-  for (; i < r1; ++i) s0 += dY[(int64_t)i * N + j];
-  ws[(int64_t)blockIdx.y * N + j] = (s0 + s1) + (s2 + s3);
+  red[ph][c] = s0 + s1;
+  __syncthreads();
+  if (ph == 0 && j < N) ws[(int64_t)blockIdx.y * N + j] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
 }
 
 // dZ = dY * act'(Y)  (act: 0 none, 1 relu, 2 tanh), in place allowed
@@ -738,7 +742,7 @@ H2OMX_API int h2omx_act_backward(const float* Y, float* dY, int64_t n, int act, 
 
 H2OMX_API int h2omx_bias_grad(const float* dY, float* db, int M, int N, float* ws, int splits, hipStream_t stream) {
   if (splits < 1 || !ws) return kBadArg;
-  hipLaunchKernelGGL(bias_grad_split_kernel, dim3(cdiv(N, 256), splits), dim3(256), 0, stream, dY, ws, M, N);
+  hipLaunchKernelGGL(bias_grad_split_kernel, dim3(cdiv(N, 64), splits), dim3(256), 0, stream, dY, ws, M, N);
   hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(cdiv(N, 256)), dim3(256), 0, stream, ws, splits, 1, N, db,
                      nullptr, 0, 0.0f);
   return launch_status();

@@ -392,7 +392,7 @@ class H2ODeepLearningEstimator(ModelBuilder):
             Hin = Hs[i]
             W = net.W(i)
             D.gemm(dZ, Hin, ta=True, out=net.W(i, net.grad))          # dW = dZ^T H
-            net.b(i, net.grad).copy_(D.bias_grad(dZ))
+            D.bias_grad(dZ, out=net.b(i, net.grad))
             if comm is not None and world > 1:
                 a, b = net.span(i)
                 handles.append(comm.all_reduce_async(net.grad[a:b]))

@@ -283,15 +283,21 @@ def act_backward(Y: torch.Tensor, dY: torch.Tensor, act: int) -> torch.Tensor:
     return dY
 
 
-def bias_grad(dY: torch.Tensor) -> torch.Tensor:
+def bias_grad(dY: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     M, N = dY.shape
     if dY.is_cuda:
-        db = torch.empty((N,), dtype=torch.float32, device=dY.device)
-        splits = max(1, min(128, M // 64))
+        db = out if out is not None else torch.empty((N,), dtype=torch.float32, device=dY.device)
+        # enough (64-column x row-slice) blocks to fill the GPU, few enough that
+        # the second stage sums a short column
+        splits = max(1, min(32, M // 256, 1024 // max(1, -(-N // 64))))
         ws = _workspace(dY.device, splits * N, slot=1)
         check(dense_lib().h2omx_bias_grad(P(dY), P(db), M, N, P(ws), splits, stream(dY.device)), "bias_grad")
         return db
-    return dY.sum(0)
+    r = dY.sum(0)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
 
 
 def softmax_xent(Z: torch.Tensor, y: torch.Tensor):

@@ -6,6 +6,7 @@ import glob
 import sys
 
 d = sys.argv[1]
+marker = sys.argv[2] if len(sys.argv) > 2 else "boost_update"   # kernel that starts a step
 stats = glob.glob(d + "/**/*kernel_stats.csv", recursive=True)
 trace = glob.glob(d + "/**/*kernel_trace.csv", recursive=True)
 if stats:
@@ -16,7 +17,7 @@ if stats:
               f"tot={float(x['TotalDurationNs'])/1e6:8.2f}ms {float(x['Percentage']):5.1f}%")
 if trace:
     t = sorted(csv.DictReader(open(trace[0])), key=lambda x: int(x["Start_Timestamp"]))
-    bu = [i for i, x in enumerate(t) if "boost_update" in x["Kernel_Name"]]
+    bu = [i for i, x in enumerate(t) if marker in x["Kernel_Name"]]
     if len(bu) >= 3:
         a, b = bu[-2], bu[-1]
         t0 = int(t[a]["Start_Timestamp"])
