@@ -108,8 +108,6 @@ class HipTreeBuilder:
         self.leaf_acc = torch.zeros((self.capacity * 3,), dtype=torch.int64, device=d)
         self.part_blocks = min(int(self.lib.h2omx_partition_blocks()),
                                int(os.environ.get("H2OMX_PART_BLOCKS", "1024")))
-        self.leaf_slab = (torch.zeros((params.max_depth * self.part_blocks * 3 * self.capacity,), dtype=torch.int64,
-                                      device=d) if self.capacity <= 2048 else None)
         self._sp = SplitParams()
         self.stats = {"host_syncs": 0}
         self.timer = PhaseTimer(device=d)
@@ -235,7 +233,6 @@ class HipTreeBuilder:
         full_prev = None
         max_depth = p.max_depth
         max_nodes = 1
-        n_part = 0
         for d in range(max_depth):
             cur, nxt = d % 2, (d + 1) % 2
             ctl_cur, ctl_nxt = self.ctl[cur], self.ctl[nxt]
@@ -288,21 +285,16 @@ class HipTreeBuilder:
                 ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges), P(bm.nvb),
                                                    nbt, next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
                                                    P(nsplit), max_nodes, st), "level_finalize")
-            slab = None
-            if self.leaf_slab is not None:
-                slab = self.leaf_slab[n_part * self.part_blocks * 3 * self.capacity:]
+            # leaves that can retire at this level: gids [base, base + n + n_next)
+            win = min(3 * max_nodes, self.capacity)
             with T("partition"):
                 ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, P(g), P(h), P(w),
-                                              P(self.qscale), self.capacity, P(self.leaf_acc), P(slab),
-                                              self.part_blocks, st), "partition")
-            n_part += 1
+                                              P(self.qscale), self.capacity, P(self.leaf_acc), P(ctl_cur),
+                                              P(ctl_nxt), win, self.part_blocks, 1 if last else 0, st),
+                          "partition")
             full_prev = full_cur
             max_nodes = next_nodes
         # exact leaf values (sums accumulated by the partition kernels)
-        if self.leaf_slab is not None:
-            with T("leaf"):
-                ops.check(lib.h2omx_leaf_reduce(P(self.leaf_slab), n_part * self.part_blocks, self.capacity,
-                                                P(self.leaf_acc), st), "leaf_reduce")
         if comm is not None:
             with T("allreduce"):
                 comm.all_reduce_(self.leaf_acc)

@@ -23,7 +23,7 @@ TREE_SIGS = {
     "h2omx_hist_build_compact": "PLPPPPPPPIIIIIIIIIIPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
     "h2omx_level_finalize": "PPPPPPIIPPPIPIS",
-    "h2omx_partition": "PLPPIPPPPIPPIS",
+    "h2omx_partition": "PLPPIPPPPIPPPIIIS",
     "h2omx_partition_blocks": "",
     "h2omx_leaf_reduce": "PIIPS",
     "h2omx_boost_update": "PPPLLPPPPPPPS",
