@@ -561,6 +561,14 @@ struct FeatBest {  // 64 B
   double pad2;
 };
 
+// K5: best threshold of every (node, feature).  One wave per (node, feature)
+// (4 features per 256-thread block, grid = nodes x ceil(F / 4)), each lane
+// owning NBT / 64 consecutive bins: the histogram row (built slot, or
+// parent - built sibling) is loaded as exact int64, scanned with wave
+// shuffles only (no LDS, no block barriers - deep trees run 10^5 nodes per
+// level, so per-block latency dominates), converted to fp64 exactly and
+// scored for both NA directions.  mtries / column sampling ranks the
+// feature's hash among all features with one ballot per 64 features.
 template <int NBT>
 __global__ __launch_bounds__(256) void split_find_kernel(const long long* __restrict__ built,
                                                          const long long* __restrict__ parent_full,
@@ -570,52 +578,55 @@ __global__ __launch_bounds__(256) void split_find_kernel(const long long* __rest
                                                          const uint8_t* __restrict__ tree_fmask,
                                                          const double* __restrict__ qscale, SplitParams p,
                                                          FeatBest* __restrict__ out) {
+  constexpr int B = NBT <= 64 ? 1 : NBT / 64;  // bins per lane
   const int node = blockIdx.x;
-  const int f = blockIdx.y;
   if (node >= ctl[CTL_N]) return;
   const int F = p.F;
-  const int t = threadIdx.x;
-  const int lane = t & 63, wid = t >> 6;
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (f >= F) return;  // whole wave
   const NodeLink lk = link[node];
-  __shared__ double wtot[2][4];
-  __shared__ double na[2];
-  __shared__ double bestg[4];
-  __shared__ int bestc[4];
   const double ig = qscale[2], is = qscale[3];
-
-  double gv = 0, sv = 0;
-  if (t < NBT) {
-    const int64_t off = ((int64_t)f * 2) * NBT + t;
-    const int64_t per = (int64_t)F * 2 * NBT;
-    long long gi, si;
-    if (lk.slot >= 0) {
-      const long long* bp = built + lk.slot * per + off;
-      gi = bp[0]; si = bp[NBT];
-    } else {
-      const long long* pp = parent_full + lk.parent * per + off;
-      const long long* sp = built + lk.sib_slot * per + off;
-      gi = pp[0] - sp[0]; si = pp[NBT] - sp[NBT];
-    }
-    if (full) {
-      long long* fp = full + node * per + off;
-      fp[0] = gi; fp[NBT] = si;
-    }
-    gv = (double)gi * ig;
-    sv = (double)si * is;
-  }
-  if (t == NBT - 1) { na[0] = gv; na[1] = sv; }
-  double sg = (t < NBT - 1) ? gv : 0.0, ssum = (t < NBT - 1) ? sv : 0.0;
+  const int64_t per = (int64_t)F * 2 * NBT;
+  const int64_t off = ((int64_t)f * 2) * NBT;
+  long long gi[B], si[B];
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const double ag = __shfl_up(sg, off, kWave), as = __shfl_up(ssum, off, kWave);
-    if (lane >= off) { sg += ag; ssum += as; }
+  for (int k = 0; k < B; ++k) {
+    const int bin = lane * B + k;
+    gi[k] = 0; si[k] = 0;
+    if (bin < NBT) {
+      if (lk.slot >= 0) {
+        const long long* bp = built + lk.slot * per + off + bin;
+        gi[k] = bp[0]; si[k] = bp[NBT];
+      } else {
+        const long long* pp = parent_full + lk.parent * per + off + bin;
+        const long long* sp = built + lk.sib_slot * per + off + bin;
+        gi[k] = pp[0] - sp[0]; si[k] = pp[NBT] - sp[NBT];
+      }
+      if (full) {
+        long long* fp = full + node * per + off + bin;
+        fp[0] = gi[k]; fp[NBT] = si[k];
+      }
+    }
   }
-  if (lane == 63) { wtot[0][wid] = sg; wtot[1][wid] = ssum; }
-  __syncthreads();
-  for (int k = 0; k < wid; ++k) { sg += wtot[0][k]; ssum += wtot[1][k]; }
-  const double ng = na[0], ns = na[1];
-  const double tg = wtot[0][0] + wtot[0][1] + wtot[0][2] + wtot[0][3] + ng;
-  const double ts = wtot[1][0] + wtot[1][1] + wtot[1][2] + wtot[1][3] + ns;
+  // NA bin (NBT - 1) excluded from the running sums
+  constexpr int NA_LANE = (NBT - 1) / B, NA_K = (NBT - 1) % B;
+  const long long ng_i = __shfl(gi[NA_K], NA_LANE, kWave), ns_i = __shfl(si[NA_K], NA_LANE, kWave);
+  if (lane == NA_LANE) { gi[NA_K] = 0; si[NA_K] = 0; }
+  long long lg = 0, ls = 0;  // inclusive local prefix
+  long long pg[B], ps[B];
+#pragma unroll
+  for (int k = 0; k < B; ++k) { lg += gi[k]; ls += si[k]; pg[k] = lg; ps[k] = ls; }
+  long long xg = lg, xs = ls;  // wave inclusive scan of lane totals
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long ag = __shfl_up(xg, o, kWave), as = __shfl_up(xs, o, kWave);
+    if (lane >= o) { xg += ag; xs += as; }
+  }
+  const long long tg_i = __shfl(xg, 63, kWave) + ng_i, ts_i = __shfl(xs, 63, kWave) + ns_i;
+  const long long eg = xg - lg, es = xs - ls;  // exclusive lane offset
+  const double ng = (double)ng_i * ig, ns = (double)ns_i * is;
+  const double tg = (double)tg_i * ig, ts = (double)ts_i * is;
 
   bool allowed = (tree_fmask == nullptr) || tree_fmask[f];
   if (allowed && (p.mtries > 0 || p.col_rate < 1.0f)) {
@@ -623,9 +634,14 @@ __global__ __launch_bounds__(256) void split_find_kernel(const long long* __rest
     const uint32_t hf = hash4(p.seed, key, (uint32_t)node, (uint32_t)f);
     if (p.mtries > 0) {
       int rank = 0;
-      for (int j = 0; j < F; ++j) {
-        const uint32_t hj = hash4(p.seed, key, (uint32_t)node, (uint32_t)j);
-        rank += (hj < hf) || (hj == hf && j < f);
+      for (int j0 = 0; j0 < F; j0 += 64) {
+        const int j = j0 + lane;
+        bool below = false;
+        if (j < F) {
+          const uint32_t hj = hash4(p.seed, key, (uint32_t)node, (uint32_t)j);
+          below = (hj < hf) || (hj == hf && j < f);
+        }
+        rank += __popcll(__ballot(below));
       }
       allowed = rank < p.mtries;
     } else {
@@ -636,42 +652,45 @@ __global__ __launch_bounds__(256) void split_find_kernel(const long long* __rest
   int best_code = 0x7fffffff;
   double bGL = 0, bSL = 0;
   const int m = nvb[f];
-  if (allowed && t < m && t < NBT - 1) {
-    const double gA = split_gain(sg, ssum, tg, ts, p);
-    const double gB = (ns > 0.0) ? split_gain(sg + ng, ssum + ns, tg, ts, p) : -INFINITY;
-    if (gA > -INFINITY) { best_gain = gA; best_code = 2 * t; bGL = sg; bSL = ssum; }
-    if (gB > -INFINITY && (gB > best_gain || (gB == best_gain && 2 * t + 1 < best_code))) {
-      best_gain = gB; best_code = 2 * t + 1; bGL = sg + ng; bSL = ssum + ns;
+  if (allowed) {
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+      const int t = lane * B + k;
+      if (t < m && t < NBT - 1) {
+        const double sg = (double)(eg + pg[k]) * ig, ssum = (double)(es + ps[k]) * is;
+        const double gA = split_gain(sg, ssum, tg, ts, p);
+        const double gB = (ns > 0.0) ? split_gain(sg + ng, ssum + ns, tg, ts, p) : -INFINITY;
+        if (gA > -INFINITY && (gA > best_gain || (gA == best_gain && 2 * t < best_code))) {
+          best_gain = gA; best_code = 2 * t; bGL = sg; bSL = ssum;
+        }
+        if (gB > -INFINITY && (gB > best_gain || (gB == best_gain && 2 * t + 1 < best_code))) {
+          best_gain = gB; best_code = 2 * t + 1; bGL = sg + ng; bSL = ssum + ns;
+        }
+      }
     }
   }
   double bg = best_gain;
   int bc = best_code;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double og = __shfl_xor(bg, off, kWave);
-    const int oc = __shfl_xor(bc, off, kWave);
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(bg, o, kWave);
+    const int oc = __shfl_xor(bc, o, kWave);
     if (og > bg || (og == bg && oc < bc)) { bg = og; bc = oc; }
   }
-  if (lane == 0) { bestg[wid] = bg; bestc[wid] = bc; }
-  __syncthreads();
-  double g0 = bestg[0];
-  int c0 = bestc[0];
-  for (int k = 1; k < 4; ++k)
-    if (bestg[k] > g0 || (bestg[k] == g0 && bestc[k] < c0)) { g0 = bestg[k]; c0 = bestc[k]; }
   FeatBest* o = out + (int64_t)node * F + f;
-  if (c0 == 0x7fffffff) {
-    if (t == 0) {
+  if (bc == 0x7fffffff) {
+    if (lane == 0) {
       FeatBest r{};
       r.gain = -INFINITY;
       r.G = tg; r.S = ts;
       r.code = 0x7fffffff;
       *o = r;
     }
-  } else if (best_code == c0) {  // unique owner of the winning threshold
+  } else if (best_code == bc) {  // unique owner of the winning threshold
     FeatBest r{};
-    r.gain = g0; r.GL = bGL; r.SL = bSL;
+    r.gain = bg; r.GL = bGL; r.SL = bSL;
     r.G = tg; r.S = ts;
-    r.code = c0;
+    r.code = bc;
     *o = r;
   }
 }
@@ -1396,7 +1415,7 @@ H2OMX_API int h2omx_split_find(const long long* built, const long long* parent_f
   const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
   FeatBest* o = reinterpret_cast<FeatBest*>(out);
-  const dim3 grid(max_nodes, p.F);
+  const dim3 grid(max_nodes, (p.F + 3) / 4);
 #define H2OMX_SF(NB)                                                                                      \
   hipLaunchKernelGGL(split_find_kernel<NB>, grid, dim3(256), 0, stream, built, parent_full, full, ctl, lk, \
                      nvb, tree_fmask, qscale, p, o)

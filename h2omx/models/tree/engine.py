@@ -78,7 +78,8 @@ class HipTreeBuilder:
     COMPACT = os.environ.get("H2OMX_HIST_COMPACT", "0") == "1"
     SEG_TARGET_CHUNKS = 1024   # level-0 histogram chunks (2 resident 57 KB workgroups per CU)
     SEG_LDS_BUDGET = 64 * 1024
-    SEG_MAX_SLOTS = int(os.environ.get("H2OMX_SEG_MAX_SLOTS", "256"))  # deeper: scan histogram kernel
+    SCAN_SLOTS = int(os.environ.get("H2OMX_SCAN_SLOTS", "16"))  # seg engine: scan hist up to this many slots
+    DEEP_DEPTH = 10
 
     def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
         if not bm.codes.is_cuda:
@@ -121,12 +122,17 @@ class HipTreeBuilder:
         units = bm.npad // self.ROWS_PER_LANE
         cands = [self.plan_level(1 << k) for k in range(0, 13)] + [self.plan_level(1 << 20)]
         self.max_rows_per_wg = max(self.ROWS_PER_LANE * math.ceil(units / c["wgpg"]) for c in cands)
-        # segmented (row-partitioned) engine, opt-in with H2OMX_TREE_ENGINE=seg: it
-        # builds bit-identical trees but measured slower on HIGGS-shape data
-        # (depth 5: 1.90 vs 1.52 ms/tree, profiles/seg_vs_scan_s1.txt) because its
-        # by-index gathers of codes / g / h and scattered node-id writes touch a
-        # cache line per row once nodes get sparse; kept for A/B work.
-        self.segmented = os.environ.get("H2OMX_TREE_ENGINE", "scan") == "seg"
+        # Engine choice (both build bit-identical trees):
+        # * scan: every level streams all rows; best for shallow trees (HIGGS depth 5:
+        #   1.52 vs 1.90 ms/tree for the segmented engine, profiles/seg_vs_scan_s1.txt)
+        #   but each level costs at least one full pass per slot pass, so deep trees
+        #   with thousands of nodes per level need hundreds of passes.
+        # * seg (row-partitioned): a level only touches the rows of the nodes it
+        #   builds; shallow levels still use the scan histogram kernel (<= SCAN_SLOTS
+        #   built nodes), deep levels the per-node-chunk kernel.  Default for trees
+        #   deeper than DEEP_DEPTH (DRF's default max_depth 20).
+        eng = os.environ.get("H2OMX_TREE_ENGINE", "auto")
+        self.segmented = eng == "seg" or (eng == "auto" and params.max_depth > self.DEEP_DEPTH)
         if self.segmented:
             self.pc_rows = int(self.lib.h2omx_pc_rows())
             hc = int(os.environ.get("H2OMX_SEG_CHUNK", "0")) or -(-bm.n // self.SEG_TARGET_CHUNKS)
@@ -347,7 +353,7 @@ class HipTreeBuilder:
                 max_slots = 1 if d == 0 else max(1, max_nodes // 2)
             last = d == max_depth - 1
             seg_start, seg_cnt, hc_first, pc_first, slot_node = seg[cur]
-            seg_hist = max_slots <= self.SEG_MAX_SLOTS
+            seg_hist = max_slots > self.SCAN_SLOTS or max_nodes > self.SYNC_NODE_CAP
             built = B("built", max_slots * self.per_node, torch.int64)
             if seg_hist and not built_zeroed:
                 built[: max_slots * self.per_node].zero_()
@@ -410,7 +416,7 @@ class HipTreeBuilder:
                 nhc = seg[nxt][2] = B(f"hc_first{nxt}", next_nodes + 1, i32)
                 npc = seg[nxt][3] = B(f"pc_first{nxt}", next_nodes + 1, i32)
                 nslot = seg[nxt][4] = B(f"slot_node{nxt}", max(1, max_nodes), i32)
-                next_seg_hist = max_nodes <= self.SEG_MAX_SLOTS and next_nodes <= self.SYNC_NODE_CAP
+                next_seg_hist = max_nodes > self.SCAN_SLOTS or next_nodes > self.SYNC_NODE_CAP
                 write_nid = 0 if next_seg_hist else 1
                 nbuilt = None
                 if next_seg_hist:

@@ -141,18 +141,19 @@ def test_segmented_engine_matches_scan_engine(cuda_dev, monkeypatch, dist, depth
     yt = torch.from_numpy(y).cuda()
     nclass = 3 if dist == "multinomial" else (2 if dist == "drf" else 1)
     out = {}
-    for eng in ("scan", "seg"):
-        monkeypatch.setenv("H2OMX_TREE_ENGINE", eng)
-        if eng == "seg":
-            monkeypatch.setattr(E.HipTreeBuilder, "SEG_MAX_SLOTS", 8)   # also exercise the mixed path
+    for eng, scan_slots in (("scan", 16), ("seg", 0), ("seg2", 2)):
+        monkeypatch.setenv("H2OMX_TREE_ENGINE", eng[:4] if eng != "scan" else "scan")
+        # seg: chunked histograms at every level; seg2: scan histograms while <= 2 built nodes
+        monkeypatch.setattr(E.HipTreeBuilder, "SCAN_SLOTS", scan_slots)
         out[eng] = train_ensemble(bg, yt, dist=dist, ntrees=4, tparams=tp, sample_rate=sample_rate, nclass=nclass,
                                   seed=11)
-    a, b = out["scan"], out["seg"]
-    for t in range(a.trees.shape[0]):
-        for i in a.compact()[t]:
-            assert a.trees[t][i]["feat"] == b.trees[t][i]["feat"], (t, i)
-            assert a.trees[t][i]["bin"] == b.trees[t][i]["bin"], (t, i)
-            np.testing.assert_allclose(a.trees[t][i]["value"], b.trees[t][i]["value"], rtol=1e-6, atol=1e-7)
+    a = out["scan"]
+    for b in (out["seg"], out["seg2"]):
+        for t in range(a.trees.shape[0]):
+            for i in a.compact()[t]:
+                assert a.trees[t][i]["feat"] == b.trees[t][i]["feat"], (t, i)
+                assert a.trees[t][i]["bin"] == b.trees[t][i]["bin"], (t, i)
+                np.testing.assert_allclose(a.trees[t][i]["value"], b.trees[t][i]["value"], rtol=1e-6, atol=1e-7)
 
 
 @pytest.mark.parametrize("dist,depth,sample_rate", [("bernoulli", 6, 1.0), ("gaussian", 9, 0.7),
