@@ -30,8 +30,21 @@ def score_histograms(score: torch.Tensor, y: torch.Tensor, w: torch.Tensor | Non
     lohi = _reduce(comm, lohi.clone(), "min")
     lo, hi = float(lohi[0]), float(-lohi[1])
     span = max(hi - lo, 1e-300)
-    idx = ((s - lo) / span * (nbins - 1)).round().clamp_(0, nbins - 1).long()
     yy = y.detach().double()
+    if s.is_cuda:
+        # HIP kernel (csrc/metrics_kernels.hip): fixed-point integer atomics ->
+        # deterministic histograms, then one all-reduce
+        from .. import ops
+
+        lib = ops.metrics_lib()
+        Hq = torch.zeros((2, nbins), dtype=torch.int64, device=s.device)
+        sc, yc = s.contiguous(), yy.contiguous()
+        wc = None if w is None else w.detach().double().contiguous()
+        ops.check(lib.h2omx_auc_hist(ops.P(sc), ops.P(yc), ops.P(wc), sc.numel(), nbins, lo, hi, ops.P(Hq),
+                                     ops.stream(s.device)), "auc_hist")
+        Hq = _reduce(comm, Hq)
+        return Hq.cpu().numpy().astype(np.float64) / 16777216.0, lo, hi
+    idx = ((s - lo) / span * (nbins - 1)).round().clamp_(0, nbins - 1).long()
     ww = torch.ones_like(yy) if w is None else w.detach().double()
     pos = torch.bincount(idx, weights=ww * yy, minlength=nbins)
     neg = torch.bincount(idx, weights=ww * (1 - yy), minlength=nbins)

@@ -60,8 +60,7 @@ DENSE_SIGS = {
 }
 
 METRICS_SIGS = {
-    "h2omx_auc_hist": "PPPLIFFPS",
-    "h2omx_reduce_binary_metrics": "PPPLPS",
+    "h2omx_auc_hist": "PPPLIDDPS",
 }
 
 _bound: dict[str, ctypes.CDLL] = {}

@@ -109,3 +109,20 @@ def test_bias_grad_split(cuda_dev):
     dY = torch.randn(8192, 300, device=cuda_dev)
     db = D.bias_grad(dY)
     assert torch.allclose(db.double(), dY.double().sum(0), atol=1e-3)
+
+
+def test_auc_hist_kernel_matches_cpu(cuda_dev):
+    from h2omx.metrics.core import score_histograms
+    from sklearn.metrics import roc_auc_score
+    from h2omx.metrics import auc_from_scores
+
+    torch.manual_seed(3)
+    s = torch.rand(200000, dtype=torch.float64)
+    y = (torch.rand(200000) < s).double()
+    w = torch.rand(200000, dtype=torch.float64)
+    Hc, lo, hi = score_histograms(s, y, w)
+    Hg, lo2, hi2 = score_histograms(s.to(cuda_dev), y.to(cuda_dev), w.to(cuda_dev))
+    assert lo == lo2 and hi == hi2
+    np.testing.assert_allclose(Hg, Hc, rtol=1e-6, atol=1e-6)
+    a = auc_from_scores(s.to(cuda_dev), y.to(cuda_dev))
+    assert abs(a - roc_auc_score(y.numpy(), s.numpy())) < 1e-4
