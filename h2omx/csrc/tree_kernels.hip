@@ -1867,6 +1867,131 @@ __global__ __launch_bounds__(1024) void level_close_kernel(
   }
 }
 
+// --- multi-block level close (levels with thousands of nodes) --------------
+// A single-block level_close scans ~10^5 chunks / nodes with block barriers
+// per 1024 entries (2.6 ms per deep DRF level); here the same work is a
+// device-wide 3-phase exclusive scan plus node-parallel kernels.
+constexpr int SCAN_TILE = 1024;
+
+// aux[0] = partition chunks of this level, aux[1] = next-level nodes
+__global__ void close_prep_kernel(const int* __restrict__ ctl, const int* __restrict__ ctl_next,
+                                  const int* __restrict__ pc_first, int* __restrict__ aux) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    aux[0] = pc_first[ctl[CTL_N]];
+    aux[1] = ctl_next[CTL_N];
+  }
+}
+
+__device__ __forceinline__ int block_excl_scan_1024(int v, int* wsum, int& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  int before = 0;
+  total = 0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+    if (k < wid) before += wsum[k];
+    total += wsum[k];
+  }
+  return before + x - v;
+}
+
+// phase 1: per-tile exclusive scan of in[0 .. aux[k]) -> out, tile totals -> tiles
+__global__ __launch_bounds__(SCAN_TILE) void scan_tiles_kernel(const int* __restrict__ in, int* __restrict__ out,
+                                                               int* __restrict__ tiles, const int* __restrict__ aux,
+                                                               int k) {
+  __shared__ int wsum[16];
+  const int count = aux[k];
+  const int i = blockIdx.x * SCAN_TILE + threadIdx.x;
+  if (blockIdx.x * SCAN_TILE >= count) return;  // uniform per block
+  const int v = i < count ? in[i] : 0;
+  int total;
+  const int e = block_excl_scan_1024(v, wsum, total);
+  if (i < count) out[i] = e;
+  if (threadIdx.x == 0) tiles[blockIdx.x] = total;
+}
+
+// phase 2 (one block): exclusive scan of the tile totals; grand total -> out[count] and total_out
+__global__ __launch_bounds__(SCAN_TILE) void scan_tile_sums_kernel(int* __restrict__ tiles, int* __restrict__ out,
+                                                                   const int* __restrict__ aux, int k,
+                                                                   int* __restrict__ total_out) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  const int count = aux[k];
+  const int nt = (count + SCAN_TILE - 1) / SCAN_TILE;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int t0 = 0; t0 < nt; t0 += SCAN_TILE) {
+    const int t = t0 + threadIdx.x;
+    const int v = t < nt ? tiles[t] : 0;
+    int total;
+    const int e = block_excl_scan_1024(v, wsum, total);
+    if (t < nt) tiles[t] = carry + e;
+    __syncthreads();
+    if (threadIdx.x == 0) carry += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (out) out[count] = carry;
+    if (total_out) *total_out = carry;
+  }
+}
+
+// phase 3: add tile offsets
+__global__ __launch_bounds__(SCAN_TILE) void scan_add_kernel(int* __restrict__ out, const int* __restrict__ tiles,
+                                                             const int* __restrict__ aux, int k) {
+  const int count = aux[k];
+  const int i = blockIdx.x * SCAN_TILE + threadIdx.x;
+  if (i < count) out[i] += tiles[blockIdx.x];
+}
+
+// node-parallel part of level_close: left totals, in-node chunk offsets,
+// children segments, next-level chunk counts and slot map
+__global__ __launch_bounds__(256) void node_close_kernel(
+    const int* __restrict__ ctl, const PartInfo* __restrict__ part, const NodeLink* __restrict__ link_next,
+    const int* __restrict__ seg_start, const int* __restrict__ seg_cnt, const int* __restrict__ pc_first,
+    const int* __restrict__ pc_excl, const int* __restrict__ aux, int* __restrict__ pc_off,
+    int* __restrict__ node_nl, int* __restrict__ nseg_start, int* __restrict__ nseg_cnt, int* __restrict__ cnt_h,
+    int* __restrict__ cnt_p, int* __restrict__ nslot_node, int hc_rows) {
+  const int n = ctl[CTL_N];
+  const int total = aux[0], grand = aux[2];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int a = pc_first[i], z = pc_first[i + 1];
+    const int base = a < total ? pc_excl[a] : grand;
+    const int end = z < total ? pc_excl[z] : grand;
+    const int nl = end - base;
+    node_nl[i] = nl;
+    for (int c = a; c < z; ++c) pc_off[c] = pc_excl[c] - base;
+    const PartInfo pi = part[i];
+    if (pi.child >= 0 && !pi.leaf_children) {
+      const int cl = pi.child, cr = pi.child + 1;
+      const int cntl = nl, cntr = seg_cnt[i] - nl;
+      nseg_start[cl] = seg_start[i];
+      nseg_cnt[cl] = cntl;
+      nseg_start[cr] = seg_start[i] + nl;
+      nseg_cnt[cr] = cntr;
+      const NodeLink L = link_next[cl], R = link_next[cr];
+      cnt_h[cl] = L.slot >= 0 ? (cntl + hc_rows - 1) / hc_rows : 0;
+      cnt_h[cr] = R.slot >= 0 ? (cntr + hc_rows - 1) / hc_rows : 0;
+      cnt_p[cl] = (cntl + PC_ROWS - 1) / PC_ROWS;
+      cnt_p[cr] = (cntr + PC_ROWS - 1) / PC_ROWS;
+      if (L.slot >= 0) nslot_node[L.slot] = cl;
+      if (R.slot >= 0) nslot_node[R.slot] = cr;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void zero_slots_kernel(long long* __restrict__ built,
+                                                         const int* __restrict__ ctl_next, int per_slot) {
+  const int64_t m = (int64_t)ctl_next[CTL_SLOTS] * per_slot;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+    built[k] = 0ll;
+}
+
 __device__ __forceinline__ long long block_sum_ll(long long v, long long* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
   __syncthreads();
@@ -2034,6 +2159,40 @@ H2OMX_API int h2omx_level_close(const int* ctl, const int* ctl_next, const void*
                      reinterpret_cast<const PartInfo*>(part), reinterpret_cast<const NodeLink*>(link_next), seg_start,
                      seg_cnt, pc_first, pc_left, node_nl, nseg_start, nseg_cnt, nhc_first, npc_first, nslot_node,
                      hc_rows, nbuilt, per_slot);
+  return launch_status();
+}
+
+static int device_scan(const int* in, int* out, int* tiles, const int* aux, int k, int max_count, int* total_out,
+                       bool write_end, hipStream_t stream) {
+  const int nt = (max_count + SCAN_TILE - 1) / SCAN_TILE;
+  if (nt < 1) return kOk;
+  hipLaunchKernelGGL(scan_tiles_kernel, dim3(nt), dim3(SCAN_TILE), 0, stream, in, out, tiles, aux, k);
+  hipLaunchKernelGGL(scan_tile_sums_kernel, dim3(1), dim3(SCAN_TILE), 0, stream, tiles, write_end ? out : nullptr,
+                     aux, k, total_out);
+  hipLaunchKernelGGL(scan_add_kernel, dim3(nt), dim3(SCAN_TILE), 0, stream, out, tiles, aux, k);
+  return launch_status();
+}
+
+// Multi-block level close; scratch: pc_excl[max_pc], tiles[max(max_pc, next_nodes)/1024 + 1],
+// cnt_h / cnt_p[next_nodes], aux[4]
+H2OMX_API int h2omx_level_close_mb(const int* ctl, const int* ctl_next, const void* part, const void* link_next,
+                                   const int* seg_start, const int* seg_cnt, const int* pc_first, int* pc_left,
+                                   int* node_nl, int* nseg_start, int* nseg_cnt, int* nhc_first, int* npc_first,
+                                   int* nslot_node, int hc_rows, long long* nbuilt, int per_slot, int max_nodes,
+                                   int max_pc, int* pc_excl, int* tiles, int* cnt_h, int* cnt_p, int* aux,
+                                   hipStream_t stream) {
+  hipLaunchKernelGGL(close_prep_kernel, dim3(1), dim3(64), 0, stream, ctl, ctl_next, pc_first, aux);
+  int rc = device_scan(pc_left, pc_excl, tiles, aux, 0, max_pc, aux + 2, false, stream);
+  if (rc) return rc;
+  const int nb = std::max(1, std::min(4096, (max_nodes + 255) / 256));
+  hipLaunchKernelGGL(node_close_kernel, dim3(nb), dim3(256), 0, stream, ctl, reinterpret_cast<const PartInfo*>(part),
+                     reinterpret_cast<const NodeLink*>(link_next), seg_start, seg_cnt, pc_first, pc_excl, aux,
+                     pc_left, node_nl, nseg_start, nseg_cnt, cnt_h, cnt_p, nslot_node, hc_rows);
+  rc = device_scan(cnt_h, nhc_first, tiles, aux, 1, 2 * max_nodes, nullptr, true, stream);
+  if (rc) return rc;
+  rc = device_scan(cnt_p, npc_first, tiles, aux, 1, 2 * max_nodes, nullptr, true, stream);
+  if (rc) return rc;
+  if (nbuilt) hipLaunchKernelGGL(zero_slots_kernel, dim3(1024), dim3(256), 0, stream, nbuilt, ctl_next, per_slot);
   return launch_status();
 }
 

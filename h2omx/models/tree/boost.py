@@ -22,6 +22,21 @@ from .reference import RefTreeBuilder, bag_weights, dist_grad
 from .structs import TREE_NODE_DTYPE
 
 
+def concat_trees(*parts: np.ndarray) -> np.ndarray:
+    """Stack tree heaps of different widths (compact deep-tree snapshots):
+    narrower heaps are padded with unreachable zero nodes."""
+    parts = [p for p in parts if p.size]
+    if not parts:
+        return np.zeros((0, 1), TREE_NODE_DTYPE)
+    width = max(p.shape[1] for p in parts)
+    out = np.zeros((sum(p.shape[0] for p in parts), width), TREE_NODE_DTYPE)
+    r = 0
+    for p in parts:
+        out[r: r + p.shape[0], : p.shape[1]] = p
+        r += p.shape[0]
+    return out
+
+
 @dataclass
 class TreeEnsemble:
     trees: np.ndarray            # [n_trees_total][capacity] TREE_NODE_DTYPE
@@ -61,7 +76,13 @@ class TreeEnsemble:
         if X.is_cuda:
             dev = X.device
             Xc = X.float().contiguous()
-            nodes = torch.from_numpy(self.trees[:T].reshape(-1).view(np.uint8).copy()).to(dev)
+            key = (T, str(dev), self.trees.shape, id(self.trees))
+            cache = getattr(self, "_dev_nodes", None)
+            if cache is not None and cache[0] == key:
+                nodes = cache[1]
+            else:
+                nodes = torch.from_numpy(self.trees[:T].reshape(-1).view(np.uint8).copy()).to(dev)
+                self._dev_nodes = (key, nodes)
             cap = self.trees.shape[1]
             roots = torch.arange(T, dtype=torch.int32, device=dev) * cap
             out = torch.empty((self.K, n), dtype=torch.float32, device=dev)
@@ -228,7 +249,7 @@ class GpuBooster:
         fmask = _tree_fmask(self.tp, bm.F, t, self.dev)
         if self.K == 1:
             b.build(st.g[0], st.h[0], self.wout, t, fmask)
-            self.trees_dev.append(b.tree_buf.clone())
+            self.trees_dev.append(self._snapshot())
             self._update(apply=True, next_tree=t + 1, k=0)
         else:
             s = ops.stream(self.dev)
@@ -251,16 +272,35 @@ class GpuBooster:
                 b.nid[: bm.n].zero_()
                 b.stat_max.copy_(maxes[k])
                 b.build(st.g[k], st.h[k], self.wout, t * self.K + k, fmask)
-                self.trees_dev.append(b.tree_buf.clone())
+                self.trees_dev.append(self._snapshot())
                 ops.check(self.lib.h2omx_apply_tree(P(st.Fm[k]), bm.n, P(b.nid), P(b.tree_buf), s), "apply_tree")
         self.t += 1
+
+    COMPACT_CAP = 8191   # deeper trees: copy only the nodes actually created
+
+    def _snapshot(self) -> torch.Tensor:
+        """Copy of the finished tree.  Shallow trees copy the whole capacity-sized
+        heap without a host sync; deep trees (DRF depth 20: 2^21 slots, 64 MB)
+        read the node count and copy only the used prefix."""
+        b = self.builder
+        if self.cap <= self.COMPACT_CAP:
+            return b.tree_buf.clone()
+        total = max(1, int(b.tree_size()))
+        return b.tree_buf[: total * TREE_NODE_DTYPE.itemsize].clone()
 
     def finish(self) -> TreeEnsemble:
         torch.cuda.synchronize(self.dev)
         if self.builder.timer.enabled:
             self.ens.timings.update({f"gpu_ms_{k}": v for k, v in self.builder.timer.totals().items()})
         if self.trees_dev:
-            self.ens.trees = trees_from_bytes(torch.stack(self.trees_dev).cpu().numpy(), self.cap)
+            width = max(t.numel() for t in self.trees_dev)
+            if all(t.numel() == width for t in self.trees_dev):
+                raw = torch.stack(self.trees_dev)
+            else:   # compact snapshots: pad to the largest tree with unreachable zero nodes
+                raw = torch.zeros((len(self.trees_dev), width), dtype=torch.uint8, device=self.dev)
+                for i, t in enumerate(self.trees_dev):
+                    raw[i, : t.numel()] = t
+            self.ens.trees = trees_from_bytes(raw.cpu().numpy(), width // TREE_NODE_DTYPE.itemsize)
         self.ens._state = self.st
         return self.ens
 
@@ -293,7 +333,11 @@ class _GpuView:
         bufs = self.gb.trees_dev[lo * K: hi * K]
         if not bufs:
             return np.zeros((0, self.gb.cap), TREE_NODE_DTYPE)
-        return trees_from_bytes(torch.stack(bufs).cpu().numpy(), self.gb.cap)
+        width = max(t.numel() for t in bufs)
+        raw = torch.zeros((len(bufs), width), dtype=torch.uint8, device=bufs[0].device)
+        for i, t in enumerate(bufs):
+            raw[i, : t.numel()] = t
+        return trees_from_bytes(raw.cpu().numpy(), width // TREE_NODE_DTYPE.itemsize)
 
 
 class _CpuView:

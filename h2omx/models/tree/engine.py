@@ -80,6 +80,7 @@ class HipTreeBuilder:
     SEG_LDS_BUDGET = 64 * 1024
     SCAN_SLOTS = int(os.environ.get("H2OMX_SCAN_SLOTS", "16"))  # seg engine: scan hist up to this many slots
     DEEP_DEPTH = 10
+    CLOSE_SINGLE_BLOCK = int(os.environ.get("H2OMX_CLOSE_SINGLE_BLOCK", "2048"))
 
     def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
         if not bm.codes.is_cuda:
@@ -238,6 +239,7 @@ class HipTreeBuilder:
                                            self.row_base, st), "tree_begin")
         full_prev = None
         max_depth = p.max_depth
+        final_ctl = self.ctl[max_depth % 2]
         max_nodes = 1
         for d in range(max_depth):
             cur, nxt = d % 2, (d + 1) % 2
@@ -246,6 +248,7 @@ class HipTreeBuilder:
                 n_now, s_now = [int(v) for v in ctl_cur[:2].tolist()]
                 self.stats["host_syncs"] += 1
                 if n_now == 0:
+                    final_ctl = ctl_cur     # tree finished early: ctl_cur holds its final TOTAL
                     break
                 max_nodes, max_slots = n_now, s_now
             else:
@@ -305,8 +308,9 @@ class HipTreeBuilder:
             with T("allreduce"):
                 comm.all_reduce_(self.leaf_acc)
         with T("leaf"):
-            ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(self.ctl[max_depth % 2]), P(self.qscale), spp,
+            ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(final_ctl), P(self.qscale), spp,
                                               P(self.tree_buf), self.capacity, st), "leaf_finalize")
+        self._final_ctl = final_ctl
         return self.tree_buf
 
     def _build_seg(self, g, h, w, tree_index, tree_fmask):
@@ -335,6 +339,7 @@ class HipTreeBuilder:
                   "tree_begin_seg")
         full_prev = None
         max_depth = p.max_depth
+        final_ctl = self.ctl[max_depth % 2]
         max_nodes = 1
         idx_in = None
         built_zeroed = True          # tree_begin_seg zeroed level 0's histogram
@@ -347,6 +352,7 @@ class HipTreeBuilder:
                 n_now, s_now = [int(v) for v in ctl_cur[:2].tolist()]
                 self.stats["host_syncs"] += 1
                 if n_now == 0:
+                    final_ctl = ctl_cur     # tree finished early: ctl_cur holds its final TOTAL
                     break
                 max_nodes, max_slots = n_now, s_now
             else:
@@ -425,10 +431,22 @@ class HipTreeBuilder:
                 ops.check(lib.h2omx_part_count(P(bm.codes), bm.npad, P(idx_in), P(seg_start), P(seg_cnt),
                                                P(pc_first), P(ctl_cur), P(part), nbt, max_pc, P(pc_left), st),
                           "part_count")
-                ops.check(lib.h2omx_level_close(P(ctl_cur), P(ctl_nxt), P(part), P(nl), P(seg_start), P(seg_cnt),
-                                                P(pc_first), P(pc_left), P(node_nl), P(nstart), P(ncnt), P(nhc),
-                                                P(npc), P(nslot), self.hc_rows, P(nbuilt), self.per_node, st),
-                          "level_close")
+                if max_nodes <= self.CLOSE_SINGLE_BLOCK:
+                    ops.check(lib.h2omx_level_close(P(ctl_cur), P(ctl_nxt), P(part), P(nl), P(seg_start),
+                                                    P(seg_cnt), P(pc_first), P(pc_left), P(node_nl), P(nstart),
+                                                    P(ncnt), P(nhc), P(npc), P(nslot), self.hc_rows, P(nbuilt),
+                                                    self.per_node, st), "level_close")
+                else:
+                    pc_excl = B("pc_excl", max_pc, i32)
+                    tiles = B("scan_tiles", max(max_pc, next_nodes) // 1024 + 2, i32)
+                    cnt_h = B("cnt_h", next_nodes, i32)
+                    cnt_p = B("cnt_p", next_nodes, i32)
+                    aux = B("close_aux", 4, i32)
+                    ops.check(lib.h2omx_level_close_mb(P(ctl_cur), P(ctl_nxt), P(part), P(nl), P(seg_start),
+                                                       P(seg_cnt), P(pc_first), P(pc_left), P(node_nl), P(nstart),
+                                                       P(ncnt), P(nhc), P(npc), P(nslot), self.hc_rows, P(nbuilt),
+                                                       self.per_node, max_nodes, max_pc, P(pc_excl), P(tiles),
+                                                       P(cnt_h), P(cnt_p), P(aux), st), "level_close_mb")
                 idx_out = self.idx[d % 2]
             ops.check(lib.h2omx_part_scatter(P(bm.codes), bm.npad, P(idx_in), P(idx_out), P(self.nid), write_nid,
                                              P(seg_start), P(seg_cnt), P(pc_first), P(pc_left), P(node_nl),
@@ -439,8 +457,9 @@ class HipTreeBuilder:
             max_nodes = next_nodes
         if comm is not None:
             comm.all_reduce_(self.leaf_acc)
-        ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(self.ctl[max_depth % 2]), P(self.qscale), spp,
+        ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(final_ctl), P(self.qscale), spp,
                                           P(self.tree_buf), self.capacity, st), "leaf_finalize")
+        self._final_ctl = final_ctl
         return self.tree_buf
 
     def reduce_stats(self) -> None:
@@ -450,7 +469,7 @@ class HipTreeBuilder:
 
     def tree_size(self) -> torch.Tensor:
         """Device scalar with the node count of the last tree (ctl TOTAL)."""
-        return self.ctl[self.p.max_depth % 2, 3]
+        return self._final_ctl[3]
 
 
 def global_row_base(n: int, comm) -> int:

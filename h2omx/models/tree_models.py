@@ -17,6 +17,7 @@ import torch
 from ..frame.frame import ENUM, Frame, Vec
 from .base import Model, ModelBuilder, ModelCategory
 from .tree import TreeParams, bin_matrix, compute_edges, train_ensemble
+from .tree.boost import concat_trees
 
 
 class TreeModel(Model):
@@ -146,7 +147,7 @@ class _TreeBuilder(ModelBuilder):
                                       "quantile_alpha": float(self.params.get("quantile_alpha", 0.5)),
                                       "huber_delta": float(self.params.get("huber_alpha", 0.9))})
         if ckpt is not None:
-            ens.trees = np.concatenate([ckpt.trees, ens.trees]) if len(ens.trees) else ckpt.trees
+            ens.trees = concat_trees(ckpt.trees, ens.trees) if len(ens.trees) else ckpt.trees
             ens.init_f = ckpt.init_f
         model = self.model_cls(self, model_id, ens, ens_dist)
         model.timings = dict(ens.timings)
@@ -164,7 +165,7 @@ class _TreeBuilder(ModelBuilder):
             raise ValueError(f"checkpoint model {ck!r} not found or not a tree model")
         if list(m.x) != list(self.x):
             raise ValueError("checkpoint model was trained on different predictors")
-        if m.ens.trees.shape[1] != (1 << (int(self.params["max_depth"]) + 1)) - 1 and m.ens.trees.size:
+        if int(m.params.get("max_depth", -1)) != int(self.params["max_depth"]):
             raise ValueError("checkpoint continuation requires the same max_depth")
         return m.ens
 

@@ -42,6 +42,7 @@ TREE_SIGS = {
     "h2omx_hist_reduce_seg": "PPPPIIIIIIPS",
     "h2omx_part_count": "PLPPPPPPIIPS",
     "h2omx_level_close": "PPPPPPPPPPPPPPIPIS",
+    "h2omx_level_close_mb": "PPPPPPPPPPPPPPIPIIIPPPPPS",
     "h2omx_part_scatter": "PLPPPIPPPPPPPIPPPPIPIS",
 }
 

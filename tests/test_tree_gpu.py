@@ -141,14 +141,16 @@ def test_segmented_engine_matches_scan_engine(cuda_dev, monkeypatch, dist, depth
     yt = torch.from_numpy(y).cuda()
     nclass = 3 if dist == "multinomial" else (2 if dist == "drf" else 1)
     out = {}
-    for eng, scan_slots in (("scan", 16), ("seg", 0), ("seg2", 2)):
-        monkeypatch.setenv("H2OMX_TREE_ENGINE", eng[:4] if eng != "scan" else "scan")
-        # seg: chunked histograms at every level; seg2: scan histograms while <= 2 built nodes
+    for eng, scan_slots, close_sb in (("scan", 16, 2048), ("seg", 0, 2048), ("seg2", 2, 2048), ("seg3", 0, 0)):
+        monkeypatch.setenv("H2OMX_TREE_ENGINE", eng[:3] if eng != "scan" else "scan")
+        # seg: chunked histograms at every level; seg2: scan histograms while <= 2 built
+        # nodes; seg3: multi-block level close at every level
         monkeypatch.setattr(E.HipTreeBuilder, "SCAN_SLOTS", scan_slots)
+        monkeypatch.setattr(E.HipTreeBuilder, "CLOSE_SINGLE_BLOCK", close_sb)
         out[eng] = train_ensemble(bg, yt, dist=dist, ntrees=4, tparams=tp, sample_rate=sample_rate, nclass=nclass,
                                   seed=11)
     a = out["scan"]
-    for b in (out["seg"], out["seg2"]):
+    for b in (out["seg"], out["seg2"], out["seg3"]):
         for t in range(a.trees.shape[0]):
             for i in a.compact()[t]:
                 assert a.trees[t][i]["feat"] == b.trees[t][i]["feat"], (t, i)
