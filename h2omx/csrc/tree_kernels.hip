@@ -77,7 +77,7 @@ struct PartInfo {  // per node of a level: routing decision for partition
   int gid;    // global node id inside the tree
   int leaf_children;  // 1: children are leaves, rows retire into them now
   int child_gid;      // global id of the left child
-  int pad;
+  int pad;            // split nodes: build slots of the children, int16 left | int16 right << 16
 };
 
 struct TreeNode {  // model representation (32 B)
@@ -208,12 +208,20 @@ __device__ __forceinline__ uint32_t row_hash(int64_t r, uint32_t salt) {
   return mix32((uint32_t)r * 0x9E3779B1u ^ mix32(salt + (uint32_t)(r >> 32)));
 }
 
-template <int NBT, int ROWS>
+// PKM (per-row inputs):
+//   0  node id -> NodeLink slot, (g, s2) quantised here (segmented engine)
+//   1  as 0, and feature group 0 stores the packed quantised row pk[r]
+//      (level 0 of the scan engine: the quantisation is fixed for the tree)
+//   2  slot16[r] written by the previous partition + stored pk[r]: no link
+//      gathers and no dither hashing on deeper levels, where several
+//      feature groups / slot passes would otherwise redo that per-row work
+template <int NBT, int ROWS, int PKM>
 __global__ __launch_bounds__(1024) void hist_build_kernel(
     const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ s2,
     const int* __restrict__ nid, const NodeLink* __restrict__ link, const int* __restrict__ ctl,
     const int* __restrict__ nvb, const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups,
-    int wgpg, int slot_lo, int slot_cnt, unsigned long long* __restrict__ partials) {
+    int wgpg, int slot_lo, int slot_cnt, const short* __restrict__ slot16, unsigned long long* __restrict__ pk_buf,
+    unsigned long long* __restrict__ partials) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
   __shared__ int width_s[256], rep_s[256];
   const int n_slots = ctl[CTL_SLOTS];
@@ -247,23 +255,46 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     const int64_t r0 = u * ROWS;
     int s[ROWS];
     bool any = false;
+    if constexpr (PKM == 2) {
 #pragma unroll
-    for (int q = 0; q < ROWS / 4; ++q) {
-      const int4 n4 = *reinterpret_cast<const int4*>(nid + r0 + 4 * q);
-      const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
+      for (int q = 0; q < ROWS / 8; ++q) {
+        const int4 v4 = *reinterpret_cast<const int4*>(slot16 + r0 + 8 * q);
+        const int vw[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        int sl = -1;
-        if (nn[k] >= 0) {
-          sl = link[nn[k]].slot - slot_lo;
-          if (sl >= slot_cnt) sl = -1;
+        for (int k = 0; k < 8; ++k) {
+          int sl = (int)(short)(vw[k >> 1] >> (16 * (k & 1))) - slot_lo;
+          if (sl < 0 || sl >= slot_cnt) sl = -1;
+          s[8 * q + k] = sl;
+          any |= (sl >= 0);
         }
-        s[4 * q + k] = sl;
-        any |= (sl >= 0);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < ROWS / 4; ++q) {
+        const int4 n4 = *reinterpret_cast<const int4*>(nid + r0 + 4 * q);
+        const int nn[4] = {n4.x, n4.y, n4.z, n4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          int sl = -1;
+          if (nn[k] >= 0) {
+            sl = link[nn[k]].slot - slot_lo;
+            if (sl >= slot_cnt) sl = -1;
+          }
+          s[4 * q + k] = sl;
+          any |= (sl >= 0);
+        }
       }
     }
     if (!any) continue;
     unsigned long long pk[ROWS];
+    if constexpr (PKM == 2) {
+#pragma unroll
+      for (int q = 0; q < ROWS / 2; ++q) {
+        const ulonglong2 p2 = *reinterpret_cast<const ulonglong2*>(pk_buf + r0 + 2 * q);
+        pk[2 * q] = p2.x;
+        pk[2 * q + 1] = p2.y;
+      }
+    } else {
 #pragma unroll
     for (int q = 0; q < ROWS / 4; ++q) {
       const float4 g4 = *reinterpret_cast<const float4*>(g + r0 + 4 * q);
@@ -279,6 +310,12 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
         const uint32_t sq = (uint32_t)floorf(fmaf(sv[k], ss, d2));
         pk[4 * q + k] = ((unsigned long long)(uint32_t)gq << 32) | (unsigned long long)sq;
       }
+    }
+    if (PKM == 1 && group == 0) {
+#pragma unroll
+      for (int q = 0; q < ROWS / 2; ++q)
+        *reinterpret_cast<ulonglong2*>(pk_buf + r0 + 2 * q) = make_ulonglong2(pk[2 * q], pk[2 * q + 1]);
+    }
     }
     for (int fi = 0; fi < nf; ++fi) {
       const uint8_t* cp = codes + (int64_t)(f0 + fi) * npad + r0;
@@ -810,6 +847,7 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(const NodeSplit* _
           next_link[2 * k_idx] = L;
           next_link[2 * k_idx + 1] = R;
         }
+        pi.pad = (L.slot & 0xFFFF) | (R.slot << 16);  // children's build slots (partition -> slot16)
         pi.child_gid = next_base + 2 * k_idx;
         if (p.children_leaves) {
           // children are final: their totals come from this split's left stats
@@ -868,7 +906,7 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(const NodeSplit* _
 // measured 4.3M LDS bank-conflict cycles per last-level dispatch with the
 // previous [copy][slot] layout).  Each workgroup folds its copies and adds
 // the window with integer global atomics (order-independent: deterministic).
-template <bool PREF>
+template <bool PREF, int RPL>
 __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restrict__ codes, int64_t npad,
                                                         int* __restrict__ nid, const PartInfo* __restrict__ part,
                                                         int nbt, const float* __restrict__ g,
@@ -876,7 +914,8 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
                                                         const double* __restrict__ qs, int cap,
                                                         unsigned long long* __restrict__ leaf_acc,
                                                         const int* __restrict__ ctl_cur,
-                                                        const int* __restrict__ ctl_next, int win_max, int R) {
+                                                        const int* __restrict__ ctl_next, int win_max, int R,
+                                                        short* __restrict__ slot16) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lacc[];
   const bool use_lds = leaf_acc != nullptr && win_max > 0;
   const int base = ctl_cur[CTL_BASE];
@@ -888,31 +927,42 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
   const int copy = (threadIdx.x & 63) % R;
   float lg = 0, lh = 0, lw = 0;
   if (leaf_acc) { lg = (float)qs[4]; lh = (float)qs[5]; lw = (float)qs[6]; }
-  const int64_t nq = npad / 8;
+  // RPL rows per lane per step: every node-id load of a step is issued before
+  // the dependent split-record and code loads (the chain nid -> split -> code
+  // is latency bound; a grid that covers all rows in one step keeps the whole
+  // chain in flight once)
+  const int64_t nq = npad / RPL;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r0 = q * 8;
-    const int4 na = *reinterpret_cast<int4*>(nid + r0), nb = *reinterpret_cast<int4*>(nid + r0 + 4);
-    int nn[8] = {na.x, na.y, na.z, na.w, nb.x, nb.y, nb.z, nb.w};
+    const int64_t r0 = q * RPL;
+    int nn[RPL];
+#pragma unroll
+    for (int v = 0; v < RPL / 4; ++v) {
+      const int4 na = *reinterpret_cast<int4*>(nid + r0 + 4 * v);
+      nn[4 * v] = na.x; nn[4 * v + 1] = na.y; nn[4 * v + 2] = na.z; nn[4 * v + 3] = na.w;
+    }
     // last level (every row retires): issue the gradient loads together with
     // the node-id loads instead of after the node -> split -> code chain
-    float gv[8], hv[8], wv8[8];
+    float gv[RPL], hv[RPL], wv8[RPL];
     if (PREF) {
-      const float4 g0 = *reinterpret_cast<const float4*>(g + r0), g1 = *reinterpret_cast<const float4*>(g + r0 + 4);
-      const float4 h0 = *reinterpret_cast<const float4*>(h + r0), h1 = *reinterpret_cast<const float4*>(h + r0 + 4);
-      gv[0] = g0.x; gv[1] = g0.y; gv[2] = g0.z; gv[3] = g0.w; gv[4] = g1.x; gv[5] = g1.y; gv[6] = g1.z; gv[7] = g1.w;
-      hv[0] = h0.x; hv[1] = h0.y; hv[2] = h0.z; hv[3] = h0.w; hv[4] = h1.x; hv[5] = h1.y; hv[6] = h1.z; hv[7] = h1.w;
-      if (w) {
-        const float4 w0 = *reinterpret_cast<const float4*>(w + r0), w1 = *reinterpret_cast<const float4*>(w + r0 + 4);
-        wv8[0] = w0.x; wv8[1] = w0.y; wv8[2] = w0.z; wv8[3] = w0.w;
-        wv8[4] = w1.x; wv8[5] = w1.y; wv8[6] = w1.z; wv8[7] = w1.w;
-      } else {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) wv8[k] = 1.0f;
+      for (int v = 0; v < RPL / 4; ++v) {
+        const float4 g0 = *reinterpret_cast<const float4*>(g + r0 + 4 * v);
+        const float4 h0 = *reinterpret_cast<const float4*>(h + r0 + 4 * v);
+        gv[4 * v] = g0.x; gv[4 * v + 1] = g0.y; gv[4 * v + 2] = g0.z; gv[4 * v + 3] = g0.w;
+        hv[4 * v] = h0.x; hv[4 * v + 1] = h0.y; hv[4 * v + 2] = h0.z; hv[4 * v + 3] = h0.w;
+        if (w) {
+          const float4 w0 = *reinterpret_cast<const float4*>(w + r0 + 4 * v);
+          wv8[4 * v] = w0.x; wv8[4 * v + 1] = w0.y; wv8[4 * v + 2] = w0.z; wv8[4 * v + 3] = w0.w;
+        } else {
+          wv8[4 * v] = wv8[4 * v + 1] = wv8[4 * v + 2] = wv8[4 * v + 3] = 1.0f;
+        }
       }
     }
     bool changed = false;
+    int sv[RPL];  // next level's build slot per row (-1: retired, or histogram derived from the sibling)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < RPL; ++k) {
+      sv[k] = -1;
       const int n = nn[k];
       if (n < 0) continue;
       changed = true;
@@ -923,8 +973,12 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
       } else {
         const int b = codes[(int64_t)pi.feat * npad + r0 + k];
         const int right = (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
-        if (pi.leaf_children) leaf = pi.child_gid + right;
-        else nn[k] = pi.child + right;
+        if (pi.leaf_children) {
+          leaf = pi.child_gid + right;
+        } else {
+          nn[k] = pi.child + right;
+          sv[k] = right ? (pi.pad >> 16) : (int)(short)(pi.pad & 0xFFFF);
+        }
       }
       if (leaf >= 0) {
         nn[k] = ~leaf;
@@ -953,8 +1007,16 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
       }
     }
     if (changed) {
-      *reinterpret_cast<int4*>(nid + r0) = make_int4(nn[0], nn[1], nn[2], nn[3]);
-      *reinterpret_cast<int4*>(nid + r0 + 4) = make_int4(nn[4], nn[5], nn[6], nn[7]);
+#pragma unroll
+      for (int v = 0; v < RPL / 4; ++v)
+        *reinterpret_cast<int4*>(nid + r0 + 4 * v) = make_int4(nn[4 * v], nn[4 * v + 1], nn[4 * v + 2], nn[4 * v + 3]);
+    }
+    if (slot16) {  // every row, so rows outside the tree read -1 on the next level
+#pragma unroll
+      for (int v = 0; v < RPL / 8; ++v)
+        *reinterpret_cast<int4*>(slot16 + r0 + 8 * v) =
+            make_int4((sv[8 * v] & 0xFFFF) | (sv[8 * v + 1] << 16), (sv[8 * v + 2] & 0xFFFF) | (sv[8 * v + 3] << 16),
+                      (sv[8 * v + 4] & 0xFFFF) | (sv[8 * v + 5] << 16), (sv[8 * v + 6] & 0xFFFF) | (sv[8 * v + 7] << 16));
     }
   }
   if (use_lds) {
@@ -1338,18 +1400,27 @@ H2OMX_API int h2omx_bin_features(const float* X, int64_t ld, int64_t n, int F, c
 H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* g, const float* s2, const int* nid,
                                const void* link, const int* ctl, const int* nvb, const double* qscale, int salt,
                                int F, int nbt, int fg, int n_groups, int wgpg, int slot_lo, int slot_cnt,
-                               int rows_per_lane, int threads, unsigned long long* partials, hipStream_t stream) {
+                               int rows_per_lane, int threads, const short* slot16, unsigned long long* pk_buf,
+                               int pkm, unsigned long long* partials, hipStream_t stream) {
   if (wgpg % 8 != 0 || npad % 16 != 0 || fg > 256 || threads % 64 != 0 || threads > 1024 || threads < fg)
     return kBadArg;
+  if (pkm < 0 || pkm > 2 || (pkm > 0 && pk_buf == nullptr) || (pkm == 2 && slot16 == nullptr)) return kBadArg;
   const int64_t units = npad / rows_per_lane;
   if ((units + wgpg - 1) / wgpg * rows_per_lane > ROWS_CAP) return kBadArg;  // fixed-point headroom
   const size_t lds = (size_t)slot_cnt * fg * nbt * sizeof(unsigned long long);
   if (lds > 156 * 1024) return kBadArg;
   const int grid = n_groups * wgpg;
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
-#define H2OMX_HB(NB, R)                                                                                           \
-  hipLaunchKernelGGL((hist_build_kernel<NB, R>), dim3(grid), dim3(threads), lds, stream, codes, npad, g, s2, nid, lk, \
-                     ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt, partials)
+#define H2OMX_HBK(NB, R, M)                                                                                      \
+  hipLaunchKernelGGL((hist_build_kernel<NB, R, M>), dim3(grid), dim3(threads), lds, stream, codes, npad, g, s2, nid, \
+                     lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt, slot16, pk_buf, \
+                     partials)
+#define H2OMX_HB(NB, R)                     \
+  do {                                      \
+    if (pkm == 0) H2OMX_HBK(NB, R, 0);      \
+    else if (pkm == 1) H2OMX_HBK(NB, R, 1); \
+    else H2OMX_HBK(NB, R, 2);               \
+  } while (0)
   if (rows_per_lane == 16) {
     switch (nbt) {
       case 32: H2OMX_HB(32, 16); break;
@@ -1370,6 +1441,7 @@ H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* 
     return kBadArg;
   }
 #undef H2OMX_HB
+#undef H2OMX_HBK
   return launch_status();
 }
 
@@ -1445,26 +1517,28 @@ H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_n
   return launch_status();
 }
 
-constexpr int PARTITION_BLOCKS = 4096;
+constexpr int PARTITION_BLOCKS = 8192;
+constexpr int PART_RPL = 8;    // rows per lane per step (16: 1.52 vs 1.47 ms/tree on HIGGS)
 
 H2OMX_API int h2omx_partition(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt, const float* g,
                               const float* h, const float* w, const double* qscale, int cap,
                               unsigned long long* leaf_acc, const int* ctl_cur, const int* ctl_next, int win_max,
-                              int blocks, int prefetch, hipStream_t stream) {
-  if (npad % 8 != 0 || blocks < 1 || blocks > PARTITION_BLOCKS || win_max < 0) return kBadArg;
+                              int blocks, int prefetch, short* slot16, hipStream_t stream) {
+  if (slot16 && prefetch) return kBadArg;
+  if (npad % PART_RPL != 0 || blocks < 1 || blocks > PARTITION_BLOCKS || win_max < 0) return kBadArg;
   // lane-private copies: the largest power of two <= 64 that fits 48 KB
   int R = 64;
   while (R > 1 && (size_t)3 * win_max * R * sizeof(unsigned long long) > 48 * 1024) R >>= 1;
   if ((size_t)3 * win_max * R * sizeof(unsigned long long) > 48 * 1024) win_max = 0;
   const size_t lds = (leaf_acc && win_max > 0) ? (size_t)3 * win_max * R * sizeof(unsigned long long) : 0;
   if (prefetch && leaf_acc)
-    hipLaunchKernelGGL(partition_kernel<true>, dim3(blocks), dim3(256), lds, stream, codes, npad, nid,
+    hipLaunchKernelGGL((partition_kernel<true, PART_RPL>), dim3(blocks), dim3(256), lds, stream, codes, npad, nid,
                        reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
-                       ctl_next, win_max, R);
+                       ctl_next, win_max, R, slot16);
   else
-    hipLaunchKernelGGL(partition_kernel<false>, dim3(blocks), dim3(256), lds, stream, codes, npad, nid,
+    hipLaunchKernelGGL((partition_kernel<false, PART_RPL>), dim3(blocks), dim3(256), lds, stream, codes, npad, nid,
                        reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
-                       ctl_next, leaf_acc ? win_max : 0, R);
+                       ctl_next, leaf_acc ? win_max : 0, R, slot16);
   return launch_status();
 }
 

@@ -108,6 +108,12 @@ class HipTreeBuilder:
         self.stat_slab = torch.zeros((int(self.lib.h2omx_stat_blocks()) * 4,), dtype=torch.int32, device=d)
         self.qscale = torch.zeros((8,), dtype=torch.float64, device=d)
         self.leaf_acc = torch.zeros((self.capacity * 3,), dtype=torch.int64, device=d)
+        # per-row packed quantised (g, s) of the current tree and next-level build
+        # slot (scan engine): written at level 0 / by partition, read by deeper levels
+        self.pk = torch.empty((bm.npad,), dtype=torch.int64, device=d)
+        self.slot16 = torch.empty((bm.npad,), dtype=torch.int16, device=d)
+        # partition grid: 1024 x 256 lanes (sweep on HIGGS 11M: 512 1.56, 1024 1.47,
+        # 2048 1.49, 4096 1.55 ms/tree)
         self.part_blocks = min(int(self.lib.h2omx_partition_blocks()),
                                int(os.environ.get("H2OMX_PART_BLOCKS", "1024")))
         self._sp = SplitParams()
@@ -260,15 +266,23 @@ class HipTreeBuilder:
             partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_elems, torch.int64)
             # level 0 streams every row; deeper levels touch only the built
             # (smaller) children -> wave-compacted kernel keeps atomics dense
-            hb = lib.h2omx_hist_build_compact if (d > 0 and self.COMPACT) else lib.h2omx_hist_build
             for ps in range(plan["passes"]):
                 slot_lo = ps * plan["slot_cnt"]
                 with T("hist"):
-                    ops.check(hb(P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]),
-                                 P(ctl_cur), P(bm.nvb), P(self.qscale), tree_index & 0x7FFFFFFF,
-                                 F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo,
-                                 plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"], P(partials), st),
-                              "hist_build")
+                    if d > 0 and self.COMPACT:
+                        ops.check(lib.h2omx_hist_build_compact(
+                            P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]), P(ctl_cur), P(bm.nvb),
+                            P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, plan["fg"], plan["n_groups"],
+                            plan["wgpg"], slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],
+                            P(partials), st), "hist_build")
+                    else:
+                        # level 0 stores the packed quantised rows; deeper levels read them
+                        # with the build slots the previous partition wrote
+                        ops.check(lib.h2omx_hist_build(
+                            P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]), P(ctl_cur), P(bm.nvb),
+                            P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, plan["fg"], plan["n_groups"],
+                            plan["wgpg"], slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],
+                            P(self.slot16), P(self.pk), 1 if d == 0 else 2, P(partials), st), "hist_build")
                     ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F,
                                                     nbt, slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st),
                               "hist_reduce")
@@ -299,7 +313,8 @@ class HipTreeBuilder:
             with T("partition"):
                 ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, P(g), P(h), P(w),
                                               P(self.qscale), self.capacity, P(self.leaf_acc), P(ctl_cur),
-                                              P(ctl_nxt), win, self.part_blocks, 1 if last else 0, st),
+                                              P(ctl_nxt), win, self.part_blocks, 1 if last else 0,
+                                              P(None if last else self.slot16), st),
                           "partition")
             full_prev = full_cur
             max_nodes = next_nodes
@@ -387,7 +402,7 @@ class HipTreeBuilder:
                                                    P(ctl_cur), P(bm.nvb), P(self.qscale), tree_index & 0x7FFFFFFF,
                                                    F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo,
                                                    plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],
-                                                   P(partials), st), "hist_build")
+                                                   None, None, 0, P(partials), st), "hist_build")
                     ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F, nbt,
                                                     slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st),
                               "hist_reduce")

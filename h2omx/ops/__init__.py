@@ -18,12 +18,12 @@ _CT = {"P": ctypes.c_void_p, "I": ctypes.c_int, "L": ctypes.c_int64, "F": ctypes
 TREE_SIGS = {
     "h2omx_tree_sizes": "P",
     "h2omx_bin_features": "PLLIPPIPLS",
-    "h2omx_hist_build": "PLPPPPPPPIIIIIIIIIIPS",
+    "h2omx_hist_build": "PLPPPPPPPIIIIIIIIIIPPIPS",
     "h2omx_hist_reduce": "PIIIIIIIPPS",
     "h2omx_hist_build_compact": "PLPPPPPPPIIIIIIIIIIPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
     "h2omx_level_finalize": "PPPPPPIIPPPIPIS",
-    "h2omx_partition": "PLPPIPPPPIPPPIIIS",
+    "h2omx_partition": "PLPPIPPPPIPPPIIIPS",
     "h2omx_partition_blocks": "",
     "h2omx_leaf_reduce": "PIIPS",
     "h2omx_boost_update": "PPPLLPPPPPPPS",
