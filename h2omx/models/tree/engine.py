@@ -166,6 +166,7 @@ class HipTreeBuilder:
 
     # -- planning ------------------------------------------------------------
     DEEP_LDS_BUDGET = int(os.environ.get("H2OMX_HIST_DEEP_LDS_KB", "128")) * 1024
+    DEEP_MIN_GROUPS = int(os.environ.get("H2OMX_HIST_DEEP_MIN_GROUPS", "4"))
 
     def _plan(self, max_slots: int, budget: int, threads: int):
         per_slot_feat = self.nbt * 8
@@ -197,7 +198,7 @@ class HipTreeBuilder:
         if max_slots in self.plans:
             return self.plans[max_slots]
         plan = self._plan(max_slots, self.LDS_BUDGET, self.THREADS)
-        if self.DEEP_LDS_BUDGET > self.LDS_BUDGET and plan["n_groups"] >= 4:
+        if self.DEEP_LDS_BUDGET > self.LDS_BUDGET and plan["n_groups"] >= self.DEEP_MIN_GROUPS:
             deep = self._plan(max_slots, self.DEEP_LDS_BUDGET, 1024)
             if deep["n_groups"] < plan["n_groups"] or deep["passes"] < plan["passes"]:
                 plan = deep
