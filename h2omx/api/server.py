@@ -147,6 +147,7 @@ class H2OApi:
         self.counters = {"requests": 0, "models_built": 0, "rows_parsed": 0}
         self.timeline: list[dict] = []
         self.automl: dict[str, object] = {}
+        self.grid_results: dict[str, dict] = {}
         self.routes = []
         R = self._route
         R("GET", r"/3/Cloud", self.cloud)
@@ -191,6 +192,9 @@ class H2OApi:
         R("POST", r"/4/Predictions/models/(?P<mid>[^/]+)/frames/(?P<fid>[^/]+)", self.predict_async)
         R("POST", r"/3/ModelMetrics/models/(?P<mid>[^/]+)/frames/(?P<fid>[^/]+)", self.model_metrics)
         R("GET", r"/3/ModelMetrics/models/(?P<mid>[^/]+)/frames/(?P<fid>[^/]+)", self.model_metrics)
+        R("POST", r"/99/Grid/(?P<algo>[^/]+)", self.grid_build)
+        R("GET", r"/99/Grids", self.grids)
+        R("GET", r"/99/Grids/(?P<gid>[^/]+)", self.grid_get)
         R("POST", r"/99/AutoMLBuilder", self.automl_build)
         R("GET", r"/99/AutoML/(?P<aid>[^/]+)", self.automl_get)
         R("GET", r"/99/Leaderboards/(?P<aid>[^/]+)", self.leaderboard)
@@ -518,6 +522,72 @@ class H2OApi:
         return {"__meta": S.meta(f"{algo.upper()}V3", "ModelBuilder"), "algo": algo, "job": job.to_json(),
                 "messages": msgs, "error_count": 0, "parameters": {k: _jsonable(v) for k, v in args.items()}}
 
+    # -- grid search ------------------------------------------------------------
+    def grid_build(self, algo, params, **_):
+        """POST /99/Grid/{algo}: model parameters plus ``hyper_parameters`` (JSON
+        map of lists), ``search_criteria`` (JSON) and ``grid_id``."""
+        from ..models import ESTIMATORS
+
+        params = dict(params)
+        hp_raw = params.pop("hyper_parameters", None)
+        sc_raw = params.pop("search_criteria", None)
+        grid_id = params.pop("grid_id", None) or f"Grid_{algo.upper()}_{uuid.uuid4().hex[:8]}"
+        hp = _json_arg(hp_raw) or {}
+        sc = _json_arg(sc_raw) or {}
+        if not isinstance(hp, dict) or not hp:
+            raise ApiError(412, "hyper_parameters must be a non-empty map of parameter -> list of values")
+        args, tf, y, vf, msgs = self._builder_args(algo, params)
+        known = {**ESTIMATORS[algo].COMMON, **ESTIMATORS[algo].DEFAULTS}
+        hyper = {}
+        for k, vals in hp.items():
+            kk = _REST_ALIASES.get(k, k)
+            if kk not in known:
+                raise ApiError(412, f"hyper parameter {k} is not a parameter of {algo}")
+            vals = vals if isinstance(vals, list) else [vals]
+            hyper[kk] = [coerce(v, known[kk]) for v in vals]
+        fr = DKV.get(tf)
+        ign = set(args.pop("ignored_columns", []) or [])
+        skip = {y, args.get("weights_column"), args.get("fold_column"), args.get("offset_column")}
+        x = [c for c in fr.names if c not in ign and c not in skip]
+
+        def work(job):
+            res = self.cluster.run("grid", algo=algo, params=args, hyper_params=hyper, search_criteria=sc, x=x, y=y,
+                                   training_frame=tf, validation_frame=vf, grid_id=grid_id)
+            self.grid_results[grid_id] = res
+            self.counters["models_built"] += len(res.get("model_ids", []))
+            return res
+
+        job = self.jobs.submit(f"{algo} grid search", grid_id, "Key<Grid>", work)
+        return {"__meta": S.meta(f"{algo.upper()}GridSearchV99", "Grid", 99), "job": job.to_json(),
+                "messages": msgs, "hyper_parameters": _jsonable(hyper), "search_criteria": sc}
+
+    def grids(self, **_):
+        return {"__meta": S.meta("GridsV99", "Grids", 99),
+                "grids": [self._grid_json(g, r) for g, r in self.grid_results.items()]}
+
+    def grid_get(self, gid, params=None, **_):
+        gid = unquote(gid)
+        res = self.grid_results.get(gid)
+        if res is None:
+            raise KeyError(gid)
+        params = params or {}
+        sort_by = params.get("sort_by")
+        dec = params.get("decreasing")
+        if sort_by:
+            res = self.cluster.run("grid_sorted", grid_id=gid, sort_by=sort_by,
+                                   decreasing=None if dec in (None, "") else str(dec).lower() == "true")
+        return self._grid_json(gid, res)
+
+    @staticmethod
+    def _grid_json(gid, res):
+        rows = res.get("summary_table") or []
+        cols = list(rows[0].keys()) if rows else ["model_ids"]
+        table = S.two_dim_table("Hyper-Parameter Search Summary", cols,
+                                ["string" if c == "model_ids" else "double" for c in cols],
+                                [[r.get(c) for c in cols] for r in rows])
+        return {"__meta": S.meta("GridSchemaV99", "Grid", 99), **{k: v for k, v in res.items() if k != "summary_table"},
+                "summary_table": table}
+
     # -- jobs -----------------------------------------------------------------
     def jobs_list(self, **_):
         return {"__meta": S.meta("JobsV3", "Iced"), "jobs": [j.to_json() for j in self.jobs.all()]}
@@ -737,6 +807,21 @@ def _lb_table(res):
     cols = list(lb[0].keys())
     return S.two_dim_table("Leaderboard", cols, ["string" if c in ("model_id", "algo") else "double" for c in cols],
                            [[r[c] for c in cols] for r in lb])
+
+
+def _json_arg(v):
+    """A JSON-valued REST argument (h2o-py sends maps as JSON or Python-literal text)."""
+    if v is None or isinstance(v, (dict, list)):
+        return v
+    txt = v.decode() if isinstance(v, bytes) else str(v)
+    if not txt.strip():
+        return None
+    try:
+        return json.loads(txt)
+    except ValueError:
+        import ast
+
+        return ast.literal_eval(txt)
 
 
 def _jsonable(v):

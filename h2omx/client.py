@@ -127,6 +127,31 @@ class H2OConnection:
         mid = b["job"]["dest"]["name"]
         return self.request(f"GET /3/Models/{mid}")["models"][0]
 
+    def grid(self, algo: str, training_frame: str, hyper_params: dict, y: str | None = None,
+             search_criteria: dict | None = None, grid_id: str | None = None, **params) -> dict:
+        """Grid search (POST /99/Grid/{algo}); returns the grid (GET /99/Grids/{id})."""
+        import json as _json
+
+        data = {"training_frame": training_frame, "hyper_parameters": _json.dumps(hyper_params)}
+        if y is not None:
+            data["response_column"] = y
+        if search_criteria:
+            data["search_criteria"] = _json.dumps(search_criteria)
+        if grid_id:
+            data["grid_id"] = grid_id
+        data.update(params)
+        b = self.request(f"POST /99/Grid/{algo}", data)
+        self.wait_job(b["job"])
+        return self.get_grid(b["job"]["dest"]["name"])
+
+    def get_grid(self, grid_id: str, sort_by: str | None = None, decreasing: bool | None = None) -> dict:
+        q = {}
+        if sort_by:
+            q["sort_by"] = sort_by
+        if decreasing is not None:
+            q["decreasing"] = "true" if decreasing else "false"
+        return self.request(f"GET /99/Grids/{grid_id}", q or None)
+
     def predict(self, model_id: str, frame: str) -> str:
         r = self.request(f"POST /4/Predictions/models/{model_id}/frames/{frame}")
         j = self.wait_job(r["job"])

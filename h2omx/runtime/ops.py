@@ -259,6 +259,21 @@ def op_automl(cl, spec):
     return run_automl(spec, comm=cl.comm if cl.world_size > 1 else None)
 
 
+def op_grid(cl, algo, params, hyper_params, search_criteria=None, x=None, y=None, training_frame=None,
+            validation_frame=None, grid_id=None):
+    from ..grid import run_grid
+
+    return run_grid(algo, _resolve_params(dict(params)), hyper_params, search_criteria, x, y, training_frame,
+                    validation_frame, grid_id, comm=cl.comm if cl.world_size > 1 else None)
+
+
+def op_grid_sorted(cl, grid_id, sort_by=None, decreasing=None):
+    g = DKV.get(grid_id)
+    if g is None:
+        raise KeyError(grid_id)
+    return g.get_grid(sort_by, decreasing).to_json()
+
+
 def op_save_model(cl, model, path):
     from ..mojo import save_model
 

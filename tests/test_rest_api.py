@@ -147,6 +147,20 @@ def test_automl_rest(conn):
     assert aucs == sorted(aucs, reverse=True)
 
 
+def test_grid_rest(conn):
+    g = conn.grid("gbm", "train.hex", {"max_depth": [2, 3], "learn_rate": [0.1, 0.3]}, y="label", ntrees=5,
+                  grid_id="gbm_grid_rest", seed=1)
+    assert len(g["model_ids"]) == 4 and g["hyper_names"] == ["max_depth", "learn_rate"]
+    s = conn.get_grid("gbm_grid_rest", sort_by="auc", decreasing=True)
+    names = [c["name"] for c in s["summary_table"]["columns"]]
+    aucs = s["summary_table"]["data"][names.index("auc")]
+    assert aucs == sorted(aucs, reverse=True)
+    assert any(gr["grid_id"]["name"] == "gbm_grid_rest" for gr in conn.request("GET /99/Grids")["grids"])
+    r = conn.grid("glm", "train.hex", {"alpha": [0.0, 0.5, 1.0]}, y="label", grid_id="glm_grid_rest",
+                  search_criteria={"strategy": "RandomDiscrete", "max_models": 2, "seed": 3})
+    assert len(r["model_ids"]) == 2
+
+
 def test_errors_and_delete(conn):
     with pytest.raises(H2OResponseError) as e:
         conn.request("GET /3/Frames/nope.hex")
