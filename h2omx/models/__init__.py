@@ -4,6 +4,8 @@ from .deeplearning import H2ODeepLearningEstimator  # noqa: F401
 from .ensemble import H2OStackedEnsembleEstimator  # noqa: F401
 from .glm import H2OGeneralizedLinearEstimator  # noqa: F401
 from .kmeans import H2OKMeansEstimator  # noqa: F401
+from .naive_bayes import H2ONaiveBayesEstimator  # noqa: F401
+from .pca import H2OPrincipalComponentAnalysisEstimator  # noqa: F401
 from .tree_models import (H2OGradientBoostingEstimator, H2ORandomForestEstimator,  # noqa: F401
                           H2OXGBoostEstimator)
 
@@ -15,4 +17,6 @@ ESTIMATORS = {
     "kmeans": H2OKMeansEstimator,
     "deeplearning": H2ODeepLearningEstimator,
     "stackedensemble": H2OStackedEnsembleEstimator,
+    "pca": H2OPrincipalComponentAnalysisEstimator,
+    "naivebayes": H2ONaiveBayesEstimator,
 }

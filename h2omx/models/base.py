@@ -33,10 +33,55 @@ class ModelCategory:
     MULTINOMIAL = "Multinomial"
     REGRESSION = "Regression"
     CLUSTERING = "Clustering"
+    DIMREDUCTION = "DimReduction"
+    ANOMALY = "AnomalyDetection"
+
+
+# categories whose models have no response column and no supervised metrics
+UNSUPERVISED = (ModelCategory.CLUSTERING, ModelCategory.DIMREDUCTION, ModelCategory.ANOMALY)
 
 
 class Model:
+    """Trained model.  Subclasses implement ``predict_raw``; every such
+    implementation is wrapped so categorical columns of the scored frame are
+    first mapped onto the training domains by level name (H2O
+    ``Model.adaptTestForTrain``: unseen levels become NA)."""
+
     algo = "model"
+
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        fn = cls.__dict__.get("predict_raw")
+        if fn is not None and not getattr(fn, "_adapts_domains", False):
+            def predict_raw(self, frame, *a, _fn=fn, **k):
+                return _fn(self, self.adapt_frame(frame), *a, **k)
+
+            predict_raw._adapts_domains = True
+            predict_raw.__doc__ = fn.__doc__
+            cls.predict_raw = predict_raw
+
+    def adapt_frame(self, frame: Frame) -> Frame:
+        cols = [c for c in self.x if self.feature_types.get(c) == ENUM]
+        doms = {c: self.feature_domains.get(c) or [] for c in cols}
+        if self.y is not None and self.response_domain is not None:
+            cols.append(self.y)
+            doms[self.y] = list(self.response_domain)
+        repl = {}
+        for c in cols:
+            if c not in frame.names:
+                continue
+            v = frame.vec(c)
+            if v.vtype != ENUM or list(v.domain or []) == list(doms[c]):
+                continue
+            idx = {d: i for i, d in enumerate(doms[c])}
+            lut = torch.tensor([idx.get(d, -1) for d in (v.domain or [])] + [-1], dtype=torch.int32,
+                               device=v.data.device)
+            codes = v.data.long()
+            codes = torch.where(codes >= 0, codes, torch.full_like(codes, lut.numel() - 1))
+            repl[c] = Vec(c, lut[codes], ENUM, list(doms[c]))
+        if not repl:
+            return frame
+        return Frame([repl.get(u.name, u) for u in frame.vecs], key=frame.key)
 
     def __init__(self, builder: "ModelBuilder", model_id: str):
         self.model_id = model_id
@@ -86,6 +131,7 @@ class Model:
         return self._metrics(frame, self.predict_raw(frame))
 
     def _metrics(self, frame: Frame, P: torch.Tensor, comm=None) -> dict:
+        frame = self.adapt_frame(frame)
         y = frame.vec(self.y)
         w = frame.vec(self.params["weights_column"]).as_float() if self.params.get("weights_column") else None
         return compute_metrics(self.category, P, y, w, comm, self.params.get("distribution"))
@@ -208,9 +254,11 @@ class ModelBuilder:
         x = [c for c in x if c not in special]
         return list(x), y
 
+    UNSUPERVISED_CATEGORY = ModelCategory.CLUSTERING
+
     def _response_category(self, frame: Frame, y: str):
         if y is None:
-            return ModelCategory.CLUSTERING, None
+            return self.UNSUPERVISED_CATEGORY, None
         v = frame.vec(y)
         dist = self.params.get("distribution", "AUTO")
         fam = self.params.get("family", "AUTO")
@@ -248,14 +296,14 @@ class ModelBuilder:
             cv_models, holdout = self._cross_validate(training_frame, validation_frame, nfolds, model_id)
         model = self._fit(training_frame, validation_frame, model_id)
         model.comm = comm
-        if model.training_metrics is None and self.category != ModelCategory.CLUSTERING:
+        if model.training_metrics is None and self.category not in UNSUPERVISED:
             model.training_metrics = model._metrics(training_frame, model.predict_raw(training_frame), comm)
-        if validation_frame is not None and self.category != ModelCategory.CLUSTERING:
+        if validation_frame is not None and self.category not in UNSUPERVISED:
             model.validation_metrics = model._metrics(validation_frame, model.predict_raw(validation_frame), comm)
         if nfolds > 1:
             model.cv_models = cv_models if self.params.get("keep_cross_validation_models", True) else []
             model.cross_validation_holdout = holdout
-            if self.category != ModelCategory.CLUSTERING:
+            if self.category not in UNSUPERVISED:
                 model.cross_validation_metrics = model._metrics(training_frame, holdout, comm)
         model.run_time_ms = int((time.time() - t0) * 1000)
         DKV.put(model.model_id, model)

@@ -108,3 +108,21 @@ def test_gbm_gpu_early_stopping_and_checkpoint(cuda_dev):
         y="y", training_frame=tr)
     c = H2OGradientBoostingEstimator(ntrees=15, max_depth=4, seed=1).train(y="y", training_frame=tr)
     assert abs(b.training_metrics["AUC"] - c.training_metrics["AUC"]) < 1e-6
+
+
+def test_pca_and_naive_bayes_gpu(cuda_dev):
+    from h2omx.models import H2ONaiveBayesEstimator, H2OPrincipalComponentAnalysisEstimator
+
+    rng = np.random.default_rng(9)
+    X = (rng.normal(size=(40000, 3)) @ rng.normal(size=(3, 12))).astype(np.float32)
+    names = [f"x{i}" for i in range(12)]
+    g = H2OPrincipalComponentAnalysisEstimator(k=3, transform="STANDARDIZE").train(
+        training_frame=Frame.from_numpy(X, names=names, device=cuda_dev))
+    c = H2OPrincipalComponentAnalysisEstimator(k=3, transform="STANDARDIZE").train(
+        training_frame=Frame.from_numpy(X, names=names))
+    np.testing.assert_allclose(g.eigenvalues, c.eigenvalues, rtol=1e-3)
+    assert sum(g.importance["Proportion of Variance"]) > 0.999
+    df = _binary_df(n=20000)
+    nb_g = H2ONaiveBayesEstimator().train(y="y", training_frame=Frame.from_pandas(df, device=cuda_dev))
+    nb_c = H2ONaiveBayesEstimator().train(y="y", training_frame=Frame.from_pandas(df))
+    assert abs(nb_g.training_metrics["AUC"] - nb_c.training_metrics["AUC"]) < 1e-4

@@ -174,3 +174,24 @@ def test_deeplearning_checkpoint_continues():
     assert b.scoring_history[0]["epochs"] > 2
     with pytest.raises(ValueError):
         H2ODeepLearningEstimator(hidden=[8], epochs=3, checkpoint=a.model_id).train(y="y", training_frame=fr)
+
+
+def test_scoring_adapts_categorical_domains():
+    """A scored frame whose categorical levels differ from training (subset,
+    other order, unseen level) is mapped onto the training domains by name."""
+    from h2omx.models import H2OGradientBoostingEstimator
+
+    rng = np.random.default_rng(5)
+    n = 3000
+    c = rng.choice(["a", "b", "c"], n)
+    yv = np.where(rng.random(n) < np.where(c == "a", 0.9, np.where(c == "b", 0.5, 0.1)), "yes", "no")
+    df = pd.DataFrame({"c": pd.Categorical(c), "z": rng.normal(size=n), "y": pd.Categorical(yv)})
+    m = H2OGradientBoostingEstimator(ntrees=10, max_depth=2, seed=1).train(y="y", training_frame=Frame.from_pandas(df))
+    t = pd.DataFrame({"c": pd.Categorical(["c", "a", "zzz"], categories=["zzz", "c", "a"]), "z": [0.0, 0.0, 0.0],
+                      "y": pd.Categorical(["no", "yes", "no"], categories=["yes", "no"])})
+    P = m.predict_raw(Frame.from_pandas(t)).numpy()
+    ref = m.predict_raw(Frame.from_pandas(df.iloc[[list(c).index("c"), list(c).index("a")]].assign(z=0.0))).numpy()
+    np.testing.assert_allclose(P[:, :2], ref, rtol=1e-6)
+    assert P[1, 1] > 0.7 and P[1, 0] < 0.3
+    perf = m.model_performance(Frame.from_pandas(t))
+    assert perf["AUC"] == 1.0
