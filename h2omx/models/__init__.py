@@ -3,6 +3,7 @@ from .base import Model, ModelBuilder, ModelCategory  # noqa: F401
 from .deeplearning import H2ODeepLearningEstimator  # noqa: F401
 from .ensemble import H2OStackedEnsembleEstimator  # noqa: F401
 from .glm import H2OGeneralizedLinearEstimator  # noqa: F401
+from .isolation_forest import H2OIsolationForestEstimator  # noqa: F401
 from .kmeans import H2OKMeansEstimator  # noqa: F401
 from .naive_bayes import H2ONaiveBayesEstimator  # noqa: F401
 from .pca import H2OPrincipalComponentAnalysisEstimator  # noqa: F401
@@ -19,4 +20,5 @@ ESTIMATORS = {
     "stackedensemble": H2OStackedEnsembleEstimator,
     "pca": H2OPrincipalComponentAnalysisEstimator,
     "naivebayes": H2ONaiveBayesEstimator,
+    "isolationforest": H2OIsolationForestEstimator,
 }

@@ -123,6 +123,10 @@ class Model:
             return Frame(vecs)
         if self.category == ModelCategory.CLUSTERING:
             return Frame([Vec("predict", P[0].to(torch.int32), "int")])
+        if self.category == ModelCategory.ANOMALY:
+            return Frame([Vec("predict", P[0].float(), "real"), Vec("mean_length", P[1].float(), "real")])
+        if self.category == ModelCategory.DIMREDUCTION:
+            return Frame([Vec(f"PC{i + 1}", P[i].float(), "real") for i in range(P.shape[0])])
         return Frame([Vec("predict", P[0].float(), "real")])
 
     def model_performance(self, frame: Frame | None = None) -> dict:

@@ -86,8 +86,10 @@ class TreeEnsemble:
             cap = self.trees.shape[1]
             roots = torch.arange(T, dtype=torch.int32, device=dev) * cap
             out = torch.empty((self.K, n), dtype=torch.float32, device=dev)
-            out.copy_(torch.from_numpy(np.repeat(self.init_f.astype(np.float32)[:, None], n, 1)).to(dev)
-                      if not self.average else torch.zeros_like(out))
+            if self.average:
+                out.zero_()
+            else:
+                out.copy_(torch.from_numpy(self.init_f.astype(np.float32)).to(dev)[:, None].expand(self.K, n))
             if T:
                 lib = ops.tree_lib()
                 ops.check(lib.h2omx_predict_raw(ops.P(Xc), Xc.stride(0), n, ops.P(nodes), ops.P(roots), T, self.K,

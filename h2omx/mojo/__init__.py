@@ -185,6 +185,9 @@ def mojo_bytes(model: Model) -> bytes:
     elif algo == "stackedensemble":
         columns = list(model.x)
         info.update(_se_info(model, files))
+    elif algo == "isolationforest":
+        columns = list(model.x)
+        info.update(_if_info(model, files))
     elif algo == "generic":
         return model.raw_mojo
     else:
@@ -243,6 +246,17 @@ def _tree_info(model, files):
             "init_f_per_class": [float(x) for x in ens.init_f], "distribution": dist,
             "h2omx_engine_dist": model.dist, "h2omx_average": bool(ens.average),
             "offset_column": "null", "binomial_double_trees": False, "link_function": _tree_link(model)}
+
+
+def _if_info(model, files):
+    ens = model.ens
+    for t in range(ens.ntrees):
+        files[f"trees/t00_{t:03d}.bin"] = _encode_tree(ens.trees[t])
+    return {"n_trees": ens.ntrees, "n_trees_per_class": 1, "init_f": 0.0, "init_f_per_class": [0.0],
+            "h2omx_engine_dist": "isolation", "h2omx_average": True, "sample_size": int(model.sample_size),
+            "min_path_length": float(model.min_path_length), "max_path_length": float(model.max_path_length),
+            "output_anomaly_flag": model.threshold is not None,
+            "h2omx_threshold": float(model.threshold) if model.threshold is not None else "null"}
 
 
 def _tree_link(model):
@@ -399,7 +413,8 @@ class GenericModel(Model):
         self.x = cols[:-1] if self.y is not None else list(cols)
         cat = info.get("category", "Regression")
         self.category = {"Binomial": ModelCategory.BINOMIAL, "Multinomial": ModelCategory.MULTINOMIAL,
-                         "Clustering": ModelCategory.CLUSTERING}.get(cat, ModelCategory.REGRESSION)
+                         "Clustering": ModelCategory.CLUSTERING, "DimReduction": ModelCategory.DIMREDUCTION,
+                         "AnomalyDetection": ModelCategory.ANOMALY}.get(cat, ModelCategory.REGRESSION)
         self.response_domain = doms.get(len(cols) - 1) if self.y is not None else None
         self.feature_domains = {c: doms.get(j) for j, c in enumerate(self.x)}
         self.feature_types = {c: (ENUM if doms.get(j) else "real") for j, c in enumerate(self.x)}
@@ -410,7 +425,7 @@ class GenericModel(Model):
         self.run_time_ms = 0
         self.comm = None
         z = m["zip"]
-        if self.mojo_algo in ("gbm", "drf", "xgboost"):
+        if self.mojo_algo in ("gbm", "drf", "xgboost", "isolationforest"):
             self._load_trees(z, info)
         elif self.mojo_algo == "stackedensemble":
             self.base = [GenericModel(z.read(f"models/{info[f'base_model{i}']}.zip"))
@@ -456,6 +471,10 @@ class GenericModel(Model):
     def predict_raw(self, frame: Frame) -> torch.Tensor:
         a = self.mojo_algo
         X = self._matrix(frame)
+        if a == "isolationforest":
+            L = self.ens.raw_margin(X)[0].to(X.device)
+            lo, hi = float(self.info["min_path_length"]), float(self.info["max_path_length"])
+            return torch.stack([(hi - L) / max(hi - lo, 1e-12), L])
         if a in ("gbm", "drf", "xgboost"):
             m = self.ens.raw_margin(X).to(X.device)
             if a == "drf" or self.link == "identity":

@@ -126,3 +126,21 @@ def test_pca_and_naive_bayes_gpu(cuda_dev):
     nb_g = H2ONaiveBayesEstimator().train(y="y", training_frame=Frame.from_pandas(df, device=cuda_dev))
     nb_c = H2ONaiveBayesEstimator().train(y="y", training_frame=Frame.from_pandas(df))
     assert abs(nb_g.training_metrics["AUC"] - nb_c.training_metrics["AUC"]) < 1e-4
+
+
+def test_isolation_forest_gpu(cuda_dev):
+    from h2omx.models import H2OIsolationForestEstimator
+
+    rng = np.random.default_rng(4)
+    X = rng.normal(size=(200000, 6)).astype(np.float32)
+    X[:100] += 7
+    names = [f"x{i}" for i in range(6)]
+    fr = Frame.from_numpy(X, names=names, device=cuda_dev)
+    m = H2OIsolationForestEstimator(ntrees=50, seed=2).train(training_frame=fr)
+    S = m.predict_raw(fr)
+    assert S.is_cuda
+    s = S[0].cpu().numpy()
+    assert s[:100].mean() > 0.8 > s[100:].mean() + 0.4
+    c = H2OIsolationForestEstimator(ntrees=50, seed=2).train(training_frame=Frame.from_numpy(X, names=names))
+    assert abs(c.training_metrics["mean_score"] - m.training_metrics["mean_score"]) < 0.2
+    assert "tree" in " ".join(_native.loaded_libraries())

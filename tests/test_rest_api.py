@@ -161,6 +161,21 @@ def test_grid_rest(conn):
     assert len(r["model_ids"]) == 2
 
 
+@pytest.mark.parametrize("algo,params", [("isolationforest", {"ntrees": 10, "seed": 1}),
+                                         ("pca", {"k": 2, "transform": "STANDARDIZE"}),
+                                         ("naivebayes", {"laplace": 1.0})])
+def test_more_algorithms_rest(conn, algo, params):
+    y = "label" if algo == "naivebayes" else None
+    m = conn.train(algo, "train.hex", y=y, **params)
+    assert m["algo"] == algo
+    pred = conn.predict(m["model_id"]["name"], "train.hex")
+    fr = conn.frame(pred, rows=3)
+    cols = [c["label"] for c in fr["columns"]]
+    expect = {"isolationforest": ["predict", "mean_length"], "pca": ["PC1", "PC2"],
+              "naivebayes": ["predict", "no", "yes"]}[algo]
+    assert cols == expect
+
+
 def test_errors_and_delete(conn):
     with pytest.raises(H2OResponseError) as e:
         conn.request("GET /3/Frames/nope.hex")
