@@ -24,6 +24,7 @@ KERNEL_LIBS = {
     "tree": ["tree_kernels.hip"],
     "dense": ["dense_kernels.hip"],
     "metrics": ["metrics_kernels.hip"],
+    "explain": ["explain_kernels.hip"],
 }
 HOST_LIBS = {
     "host": ["host/parser.cpp"],

@@ -15,6 +15,9 @@ build models, score and download MOJOs:
   POST /99/Models.bin/{id}   POST /99/Models.upload.bin   GET /99/Models.fetch.bin/{id}
   POST /3/Predictions/models/{m}/frames/{f}   POST /4/Predictions/models/{m}/frames/{f}
   POST /3/ModelMetrics/models/{m}/frames/{f}
+  POST /3/Predictions/...?predict_contributions=true  (TreeSHAP)
+  POST /3/PartialDependence  GET /3/PartialDependence/{id}
+  POST /99/Grid/{algo}       GET /99/Grids[/{id}]
   POST /99/AutoMLBuilder     GET /99/AutoML/{id}    GET /99/Leaderboards/{id}
   POST /99/Rapids            DELETE /3/DKV[/{key}]  POST /3/Shutdown
   GET  /3/Logs/nodes/{n}/files/{name}   GET /3/Timeline   GET /metrics
@@ -148,6 +151,7 @@ class H2OApi:
         self.timeline: list[dict] = []
         self.automl: dict[str, object] = {}
         self.grid_results: dict[str, dict] = {}
+        self.pdp_results: dict[str, list] = {}
         self.routes = []
         R = self._route
         R("GET", r"/3/Cloud", self.cloud)
@@ -198,6 +202,8 @@ class H2OApi:
         R("POST", r"/99/AutoMLBuilder", self.automl_build)
         R("GET", r"/99/AutoML/(?P<aid>[^/]+)", self.automl_get)
         R("GET", r"/99/Leaderboards/(?P<aid>[^/]+)", self.leaderboard)
+        R("POST", r"/3/PartialDependence/?", self.partial_dependence)
+        R("GET", r"/3/PartialDependence/(?P<pid>[^/]+)", self.partial_dependence_get)
         R("POST", r"/99/Rapids", self.rapids)
         R("DELETE", r"/3/DKV", self.delete_all)
         R("DELETE", r"/3/DKV/(?P<key>[^/]+)", self.delete_key)
@@ -659,12 +665,16 @@ class H2OApi:
         if not isinstance(DKV.get(fid), Frame):
             raise KeyError(fid)
         dest = params.get("predictions_frame") or f"prediction_{uuid.uuid4().hex[:10]}"
-        self.cluster.run("predict", model=m.model_id, frame=fid, dest=dest)
+        kind = "contributions" if str(params.get("predict_contributions", "false")).lower() == "true" else "predict"
+        self.cluster.run("predict", model=m.model_id, frame=fid, dest=dest, kind=kind)
         return m, dest
 
     def predict(self, mid, fid, params, **_):
         m, dest = self._predict(mid, fid, params)
         mm = None
+        if str(params.get("predict_contributions", "false")).lower() == "true":
+            return {"__meta": S.meta("ModelMetricsListSchemaV3", "Iced"), "model_metrics": [],
+                    "predictions_frame": S.key_ref(dest, "Key<Frame>")}
         if m.y is not None and m.y in DKV.get(unquote(fid)).names:
             mm = S.metrics_json(self.cluster.run("model_metrics", model=m.model_id, frame=unquote(fid)), m.category,
                                 m.model_id, unquote(fid), m.response_domain)
@@ -686,6 +696,46 @@ class H2OApi:
         res = self.cluster.run("model_metrics", model=m.model_id, frame=fid)
         return {"__meta": S.meta("ModelMetricsListSchemaV3", "Iced"),
                 "model_metrics": [S.metrics_json(res, m.category, m.model_id, fid, m.response_domain)]}
+
+    # -- partial dependence -------------------------------------------------------
+    def partial_dependence(self, params, **_):
+        mid = params.get("model_id")
+        fid = params.get("frame_id")
+        m = self._get_model(mid)
+        if not isinstance(DKV.get(fid), Frame):
+            raise KeyError(fid)
+        cols = parse_list(params.get("cols")) or list(m.x)
+        nbins = int(params.get("nbins", 20))
+        targets = parse_list(params.get("targets")) or [None]
+        dest = params.get("destination_key") or f"PartialDependence_{uuid.uuid4().hex[:10]}"
+
+        def work(job):
+            res = self.cluster.run("partial_dependence", model=m.model_id, frame=fid, cols=cols, nbins=nbins,
+                                   targets=targets)
+            self.pdp_results[dest] = res
+            return res
+
+        job = self.jobs.submit("PartialDependence", dest, "Key<PartialDependence>", work)
+        return {"__meta": S.meta("PartialDependenceV3", "PartialDependence"), "job": job.to_json(),
+                "model_id": S.key_ref(m.model_id, "Key<Model>"), "frame_id": S.key_ref(fid, "Key<Frame>"),
+                "destination_key": S.key_ref(dest, "Key<PartialDependence>"), "cols": cols, "nbins": nbins}
+
+    def partial_dependence_get(self, pid, **_):
+        pid = unquote(pid)
+        res = self.pdp_results.get(pid)
+        if res is None:
+            raise KeyError(pid)
+        tables = []
+        for r in res:
+            col = r["column"]
+            names = [col, "mean_response", "stddev_response", "std_error_mean_response"]
+            tables.append(S.two_dim_table(f"PartialDependence: {col}" + (f" class {r['target']}" if r["target"]
+                                                                         else ""), names,
+                                          ["string" if isinstance(r["data"][0][col], str) else "double"]
+                                          + ["double"] * 3 if r["data"] else ["double"] * 4,
+                                          [[d[c] for c in names] for d in r["data"]]))
+        return {"__meta": S.meta("PartialDependenceV3", "PartialDependence"),
+                "destination_key": S.key_ref(pid, "Key<PartialDependence>"), "partial_dependence_data": tables}
 
     # -- AutoML ---------------------------------------------------------------
     def automl_build(self, params, body, **_):

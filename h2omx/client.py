@@ -157,6 +157,18 @@ class H2OConnection:
         j = self.wait_job(r["job"])
         return j["dest"]["name"]
 
+    def predict_contributions(self, model_id: str, frame: str) -> str:
+        r = self.request(f"POST /3/Predictions/models/{model_id}/frames/{frame}", {"predict_contributions": True})
+        return r["predictions_frame"]["name"]
+
+    def partial_dependence(self, model_id: str, frame: str, cols=None, nbins: int = 20) -> list:
+        data = {"model_id": model_id, "frame_id": frame, "nbins": nbins}
+        if cols:
+            data["cols"] = list(cols)
+        r = self.request("POST /3/PartialDependence/", data)
+        self.wait_job(r["job"])
+        return self.request(f"GET /3/PartialDependence/{r['destination_key']['name']}")["partial_dependence_data"]
+
     def model_performance(self, model_id: str, frame: str) -> dict:
         return self.request(f"POST /3/ModelMetrics/models/{model_id}/frames/{frame}")["model_metrics"][0]
 

@@ -143,6 +143,18 @@ class Model:
     def varimp(self) -> list[tuple]:
         return []
 
+    def predict_contributions(self, frame: Frame) -> Frame:
+        """SHAP contributions + BiasTerm (tree models; h2omx.explain)."""
+        from ..explain import predict_contributions
+
+        return predict_contributions(self, frame)
+
+    def partial_dependence(self, frame: Frame, cols=None, nbins: int = 20, target=None) -> list[dict]:
+        from ..explain import partial_dependence
+
+        return [partial_dependence(self, frame, c, nbins=nbins, target=target, comm=self.comm)
+                for c in (cols or self.x)]
+
     def summary(self) -> dict:
         return {"model_id": self.model_id, "algo": self.algo, "category": self.category}
 

@@ -64,6 +64,10 @@ METRICS_SIGS = {
     "h2omx_auc_hist": "PPPLIDDPS",
 }
 
+EXPLAIN_SIGS = {
+    "h2omx_tree_shap": "PLLIPIPPIPS",
+}
+
 _bound: dict[str, ctypes.CDLL] = {}
 
 
@@ -92,6 +96,10 @@ def dense_lib() -> ctypes.CDLL:
 
 def metrics_lib() -> ctypes.CDLL:
     return _bind("metrics", METRICS_SIGS)
+
+
+def explain_lib() -> ctypes.CDLL:
+    return _bind("explain", EXPLAIN_SIGS)
 
 
 P = _native.ptr

@@ -178,13 +178,27 @@ def op_train(cl, algo, params, x=None, y=None, training_frame=None, validation_f
     return m.model_id
 
 
-def op_predict(cl, model, frame, dest):
+def op_predict(cl, model, frame, dest, kind="predict"):
     m = _model(model)
     fr = _frame(frame)
-    pf = m.predict(fr)
+    if kind == "contributions":
+        from ..explain import predict_contributions
+
+        pf = predict_contributions(m, fr)
+    else:
+        pf = m.predict(fr)
     pf.key = dest
     DKV.put(dest, pf)
     return {"key": dest, "rows": global_nrows(pf, cl.comm)}
+
+
+def op_partial_dependence(cl, model, frame, cols, nbins=20, targets=(None,)):
+    from ..explain import partial_dependence
+
+    m = _model(model)
+    fr = _frame(frame)
+    comm = cl.comm if cl.world_size > 1 else None
+    return [partial_dependence(m, fr, c, nbins=nbins, target=t, comm=comm) for c in cols for t in targets]
 
 
 def op_model_metrics(cl, model, frame):

@@ -176,6 +176,19 @@ def test_more_algorithms_rest(conn, algo, params):
     assert cols == expect
 
 
+def test_contributions_and_partial_dependence_rest(conn):
+    m = conn.train("gbm", "train.hex", y="label", ntrees=5, max_depth=3, seed=1)
+    mid = m["model_id"]["name"]
+    key = conn.predict_contributions(mid, "train.hex")
+    fr = conn.frame(key, rows=5)
+    assert [c["label"] for c in fr["columns"]] == ["a", "b", "c", "BiasTerm"]
+    tabs = conn.partial_dependence(mid, "train.hex", cols=["a", "c"], nbins=5)
+    assert len(tabs) == 2
+    assert [c["name"] for c in tabs[0]["columns"]] == ["a", "mean_response", "stddev_response",
+                                                        "std_error_mean_response"]
+    assert len(tabs[0]["data"][0]) == 5 and tabs[1]["data"][0] == ["x", "y", "z"]
+
+
 def test_errors_and_delete(conn):
     with pytest.raises(H2OResponseError) as e:
         conn.request("GET /3/Frames/nope.hex")
