@@ -323,4 +323,140 @@ def _eval(node, ctx):
               "ceiling": torch.ceil, "round": torch.round, "sign": torch.sign, "cos": torch.cos, "sin": torch.sin,
               "tanh": torch.tanh}[op]
         return Frame([Vec(v.name, fn(v.as_float()), REAL) for v in fr.vecs], key=_new_key())
+    out = _munge(op, args, E, ctx)
+    if out is not _NOT_MUNGE:
+        return out
     raise ValueError(f"rapids: unsupported operation {op!r}")
+
+
+_NOT_MUNGE = object()
+
+
+def _bool(v, default=False):
+    if v is None:
+        return default
+    if isinstance(v, str):
+        return v.lower() in ("true", "1")
+    if isinstance(v, tuple) and v and v[0] == "list":
+        return [_bool(x) for x in v[1]]
+    return bool(v)
+
+
+def _num_list(v):
+    return [float(x) for x in _idx_list(v, 0)] if v is not None else []
+
+
+def _munge(op, args, E, ctx):
+    """h2o-py frame methods (frame/munging.py)."""
+    from ..frame import munging as M
+
+    comm = ctx.comm
+    if op == "ifelse":
+        test = _frame(E(args[0]))
+        return Frame(list(M.ifelse(test, E(args[1]), E(args[2])).vecs), key=_new_key())
+    if op == "na.omit":
+        return Frame(list(M.na_omit(_frame(E(args[0]))).vecs), key=_new_key())
+    if op == "cut":
+        fr = _frame(E(args[0]))
+        labels = [str(x) for x in _idx_list(args[2], 0)] if len(args) > 2 and isinstance(args[2], tuple) and \
+            args[2][1] else None
+        return Frame(list(M.cut(fr, _num_list(args[1]), labels, _bool(args[3] if len(args) > 3 else False),
+                                _bool(args[4] if len(args) > 4 else True),
+                                int(args[5]) if len(args) > 5 else 3).vecs), key=_new_key())
+    if op == "relevel":
+        return Frame(list(M.relevel(_frame(E(args[0])), str(args[1])).vecs), key=_new_key())
+    if op == "h2o.random_stratified_split":
+        fr = _frame(E(args[0]))
+        return Frame(list(M.stratified_split(fr, float(args[1]), int(args[2]) if len(args) > 2 else 42,
+                                             comm).vecs), key=_new_key())
+    if op == "scale":
+        fr = _frame(E(args[0]))
+        return Frame(list(M.scale(fr, _bool(args[1], True), _bool(args[2], True), comm).vecs), key=_new_key())
+    if op in ("cumsum", "cumprod", "cummin", "cummax"):
+        return Frame(list(M.cumulative(_frame(E(args[0])), op, comm).vecs), key=_new_key())
+    if op in ("kfold_column", "modulo_kfold_column", "stratified_kfold_column"):
+        fr = _frame(E(args[0]))
+        how = "modulo" if op == "modulo_kfold_column" else "random"
+        seed = int(args[2]) if len(args) > 2 else -1
+        return Frame(list(M.kfold_column(fr, int(args[1]), seed, comm, how).vecs), key=_new_key())
+    if op == "which":
+        return Frame(list(M.which(_frame(E(args[0])), comm).vecs), key=_new_key())
+    if op in ("any", "all", "naCnt", "any.na"):
+        fr = _frame(E(args[0]))
+        vals = []
+        for v in fr.vecs:
+            x = v.as_float()
+            if op == "naCnt":
+                vals.append(float(torch.isnan(x).sum()))
+            elif op == "any.na":
+                vals.append(float(torch.isnan(x).any()))
+            elif op == "any":
+                vals.append(float((torch.nan_to_num(x, nan=0.0) != 0).any()))
+            else:
+                vals.append(float(((x != 0) | torch.isnan(x)).all()) if x.numel() else 1.0)
+        a = np.array(vals, np.float64)
+        if comm is not None:
+            a = comm.all_reduce_numpy(a, "sum" if op in ("naCnt", "any", "any.na") else "min")
+        if op in ("any", "any.na"):
+            return float(a.max() > 0)
+        if op == "all":
+            return float(a.min() > 0)
+        return [float(x) for x in a] if len(a) > 1 else float(a[0])
+    if op == "quantile":
+        fr = _frame(E(args[0]))
+        return Frame(list(M.quantile(fr, _num_list(args[1]), comm).vecs), key=_new_key())
+    if op == "h2o.impute":
+        fr = _frame(E(args[0]))
+        col = int(args[1]) if len(args) > 1 else -1
+        method = str(args[2]) if len(args) > 2 else "mean"
+        values = _num_list(args[6]) if len(args) > 6 and isinstance(args[6], tuple) and args[6][1] else None
+        cols = range(fr.ncols) if col < 0 else [col]
+        fills = []
+        for c in cols:
+            if method.lower() == "mean" and fr.vecs[c].vtype == ENUM:
+                method_c = "mode"
+            else:
+                method_c = method
+            fr, f = M.impute(fr, c, method_c, comm, values)
+            fills += f
+        DKV.put(fr.key, fr)
+        return fills if len(fills) > 1 else fills[0]
+    if op == "GB":
+        fr = _frame(E(args[0]))
+        gcols = _cols(fr, args[1])
+        rest = args[2:]
+        aggs = []
+        for i in range(0, len(rest) - 2, 3):
+            ci = rest[i + 1]
+            ci = fr.names.index(ci) if isinstance(ci, str) and ci in fr.names else int(ci)
+            aggs.append((str(rest[i]), ci, str(rest[i + 2])))
+        return Frame(list(M.group_by(fr, gcols, aggs, comm).vecs), key=_new_key())
+    if op == "unique":
+        fr = _frame(E(args[0]))
+        return Frame(list(M.unique(fr, comm, _bool(args[1] if len(args) > 1 else False)).vecs), key=_new_key())
+    if op == "table":
+        frs = [E(a) for a in args if isinstance(E(a), Frame)]
+        fr = frs[0] if len(frs) == 1 else Frame(frs[0].vecs + frs[1].vecs)
+        return Frame(list(M.table(fr, comm).vecs), key=_new_key())
+    if op == "sort":
+        fr = _frame(E(args[0]))
+        cols = _cols(fr, args[1])
+        asc = _bool(args[2]) if len(args) > 2 else None
+        asc = asc if isinstance(asc, list) else None
+        return Frame(list(M.sort(fr, cols, asc, comm).vecs), key=_new_key())
+    if op == "merge":
+        left, right = _frame(E(args[0])), _frame(E(args[1]))
+        bx = [int(x) for x in _idx_list(args[4], 0)] if len(args) > 4 and isinstance(args[4], tuple) and \
+            args[4][1] else None
+        by = [int(x) for x in _idx_list(args[5], 0)] if len(args) > 5 and isinstance(args[5], tuple) and \
+            args[5][1] else None
+        return Frame(list(M.merge(left, right, _bool(args[2]), _bool(args[3]), bx, by, comm).vecs),
+                     key=_new_key())
+    if op == "setDomain":
+        fr = _frame(E(args[0]))
+        levels = [str(x) for x in _idx_list(args[2], 0)]
+        v = fr.vecs[0]
+        if v.vtype != ENUM or len(levels) != len(v.domain or []):
+            raise ValueError("setDomain: the new domain must have as many levels as the column")
+        return Frame([Vec(v.name, v.data, ENUM, levels)] + list(fr.vecs[1:]), key=_new_key())
+    return _NOT_MUNGE
