@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void bin_features_kernel(const float* __restri
 // keeps the groups of one row chunk on one XCD (L2 reuse of g/h/nid; speed
 // only, never correctness).
 // ---------------------------------------------------------------------------
-constexpr int ROWS_CAP = 32768;          // rows per workgroup chunk (host enforced)
+constexpr int ROWS_CAP = 2097152;        // max rows per workgroup chunk (host picks <= this; the scales adapt)
 constexpr float QG = 32768.0f;           // |G_q| per row <= QG  -> |sum| <= 2^30
 constexpr float QS = 65536.0f;           // S_q per row <= QS    -> sum <= 2^31
 

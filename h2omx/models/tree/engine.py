@@ -70,7 +70,9 @@ class HipTreeBuilder:
     THREADS = int(os.environ.get("H2OMX_HIST_THREADS", "512"))
     TARGET_WGS = int(os.environ.get("H2OMX_HIST_WGS", "512"))
     ROWS_PER_LANE = int(os.environ.get("H2OMX_HIST_ROWS", "16"))
-    ROWS_CAP = 32768           # rows per workgroup chunk (fixed-point headroom, see kernel)
+    # rows per workgroup chunk: bounds the fixed-point headroom, so the gradient
+    # resolution is 2^30 / (largest chunk) levels (see tree_begin)
+    ROWS_CAP = int(os.environ.get("H2OMX_ROWS_CAP", "262144"))
     SYNC_NODE_CAP = 4096       # above this many potential nodes the host reads the real count
     # wave-compacted histogram kernel for levels > 0 (H2OMX_HIST_COMPACT=1): bit-identical
     # but measured slower (byte gathers of column-major codes are TA-bound:
