@@ -5,11 +5,13 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-iter}
-python -m h2omx.build > gpurun_out/build.log 2>&1 || { echo BUILD FAILED; cat gpurun_out/build.log; exit 1; }
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu_$TAG.log 2>&1
+ls h2omx/lib/libh2omx_tree.so >/dev/null 2>&1 || { python -m h2omx.build > gpurun_out/build.log 2>&1 || { echo BUILD FAILED; cat gpurun_out/build.log; exit 1; }; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1
 rc=$?
-tail -15 gpurun_out/pytest_gpu_$TAG.log
+grep -E "passed|failed|PASSED|FAILED|Error" gpurun_out/pytest_gpu_$TAG.log | tail -8
 [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke_$TAG.log 2>&1 || { tail -20 gpurun_out/smoke_$TAG.log; exit 1; }
+tail -1 gpurun_out/smoke_$TAG.log
 timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
 OUT=gpurun_out/prof_$TAG
