@@ -215,6 +215,11 @@ __device__ __forceinline__ uint32_t row_hash(int64_t r, uint32_t salt) {
 //   2  slot16[r] written by the previous partition + stored pk[r]: no link
 //      gathers and no dither hashing on deeper levels, where several
 //      feature groups / slot passes would otherwise redo that per-row work
+//   3  as 1, pk stored as 32 bits (int16 G_q << 16 | uint16 S_q)
+//   4  as 2, reading those 32-bit rows: halves the per-row stream that every
+//      feature group of a deep level re-reads.  The host picks 3/4 only when
+//      the per-row magnitudes fit 16 bits (rows per workgroup >= 2^16 puts
+//      |G_q| <= 2^14 and S_q <= 2^15), so histograms stay bit-identical.
 template <int NBT, int ROWS, int PKM>
 __global__ __launch_bounds__(1024) void hist_build_kernel(
     const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ s2,
@@ -255,7 +260,7 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     const int64_t r0 = u * ROWS;
     int s[ROWS];
     bool any = false;
-    if constexpr (PKM == 2) {
+    if constexpr (PKM == 2 || PKM == 4) {
 #pragma unroll
       for (int q = 0; q < ROWS / 8; ++q) {
         const int4 v4 = *reinterpret_cast<const int4*>(slot16 + r0 + 8 * q);
@@ -294,6 +299,17 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
         pk[2 * q] = p2.x;
         pk[2 * q + 1] = p2.y;
       }
+    } else if constexpr (PKM == 4) {
+      const uint32_t* pk32 = reinterpret_cast<const uint32_t*>(pk_buf);
+#pragma unroll
+      for (int q = 0; q < ROWS / 4; ++q) {
+        const uint4 p4 = *reinterpret_cast<const uint4*>(pk32 + r0 + 4 * q);
+        const uint32_t pw[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          pk[4 * q + k] = ((unsigned long long)(uint32_t)(int)(short)(pw[k] >> 16) << 32) |
+                          (unsigned long long)(pw[k] & 0xFFFFu);
+      }
     } else {
 #pragma unroll
     for (int q = 0; q < ROWS / 4; ++q) {
@@ -315,6 +331,19 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
 #pragma unroll
       for (int q = 0; q < ROWS / 2; ++q)
         *reinterpret_cast<ulonglong2*>(pk_buf + r0 + 2 * q) = make_ulonglong2(pk[2 * q], pk[2 * q + 1]);
+    }
+    if (PKM == 3 && group == 0) {
+      uint32_t* pk32 = reinterpret_cast<uint32_t*>(pk_buf);
+#pragma unroll
+      for (int q = 0; q < ROWS / 4; ++q) {
+        uint32_t pw[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const unsigned long long v = pk[4 * q + k];
+          pw[k] = ((uint32_t)(v >> 32) << 16) | ((uint32_t)v & 0xFFFFu);
+        }
+        *reinterpret_cast<uint4*>(pk32 + r0 + 4 * q) = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+      }
     }
     }
     for (int fi = 0; fi < nf; ++fi) {
@@ -1404,7 +1433,8 @@ H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* 
                                int pkm, unsigned long long* partials, hipStream_t stream) {
   if (wgpg % 8 != 0 || npad % 16 != 0 || fg > 256 || threads % 64 != 0 || threads > 1024 || threads < fg)
     return kBadArg;
-  if (pkm < 0 || pkm > 2 || (pkm > 0 && pk_buf == nullptr) || (pkm == 2 && slot16 == nullptr)) return kBadArg;
+  if (pkm < 0 || pkm > 4 || (pkm > 0 && pk_buf == nullptr) || ((pkm == 2 || pkm == 4) && slot16 == nullptr))
+    return kBadArg;
   const int64_t units = npad / rows_per_lane;
   if ((units + wgpg - 1) / wgpg * rows_per_lane > ROWS_CAP) return kBadArg;  // fixed-point headroom
   const size_t lds = (size_t)slot_cnt * fg * nbt * sizeof(unsigned long long);
@@ -1419,7 +1449,9 @@ H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* 
   do {                                      \
     if (pkm == 0) H2OMX_HBK(NB, R, 0);      \
     else if (pkm == 1) H2OMX_HBK(NB, R, 1); \
-    else H2OMX_HBK(NB, R, 2);               \
+    else if (pkm == 2) H2OMX_HBK(NB, R, 2); \
+    else if (pkm == 3) H2OMX_HBK(NB, R, 3); \
+    else H2OMX_HBK(NB, R, 4);               \
   } while (0)
   if (rows_per_lane == 16) {
     switch (nbt) {

@@ -131,6 +131,10 @@ class HipTreeBuilder:
         units = bm.npad // self.ROWS_PER_LANE
         cands = [self.plan_level(1 << k) for k in range(0, 13)] + [self.plan_level(1 << 20)]
         self.max_rows_per_wg = max(self.ROWS_PER_LANE * math.ceil(units / c["wgpg"]) for c in cands)
+        # >= 2^16 rows per workgroup bounds the per-row fixed-point values to 16 bits
+        # (tree_begin: |G_q| <= 2^14, S_q <= 2^15): the packed rows are then stored in
+        # 32 bits (hist_build PKM 3/4), halving what every deep-level feature group re-reads
+        self.pk32 = self.max_rows_per_wg >= 65536 and os.environ.get("H2OMX_PK32", "1") == "1"
         # Engine choice (both build bit-identical trees):
         # * scan: every level streams all rows; best for shallow trees (HIGGS depth 5:
         #   1.52 vs 1.90 ms/tree for the segmented engine, profiles/seg_vs_scan_s1.txt)
@@ -285,7 +289,8 @@ class HipTreeBuilder:
                             P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]), P(ctl_cur), P(bm.nvb),
                             P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, plan["fg"], plan["n_groups"],
                             plan["wgpg"], slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],
-                            P(self.slot16), P(self.pk), 1 if d == 0 else 2, P(partials), st), "hist_build")
+                            P(self.slot16), P(self.pk), (1 if d == 0 else 2) + (2 if self.pk32 else 0), P(partials),
+                            st), "hist_build")
                     ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F,
                                                     nbt, slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st),
                               "hist_reduce")

@@ -180,3 +180,35 @@ def test_compact_hist_matches_plain(cuda_dev, monkeypatch, dist, depth, sample_r
         assert reach == b.compact()[t]
         for f in ("feat", "bin", "value"):
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
+
+
+@pytest.mark.parametrize("dist,depth,sample_rate", [("bernoulli", 5, 1.0), ("gaussian", 7, 0.7)])
+def test_pk32_rows_match_pk64(cuda_dev, monkeypatch, dist, depth, sample_rate):
+    """32-bit packed rows (large row chunks: per-row values fit 16 bits) build
+    bit-identical trees to the 64-bit rows."""
+    import h2omx.models.tree.engine as E
+
+    X, y = _data(n=600_000, F=9, seed=8, task="bin" if dist == "bernoulli" else "reg")
+    _, bg = _both(X, y, 255)
+    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2)
+    yt = torch.from_numpy(y).cuda()
+    monkeypatch.setattr(E.HipTreeBuilder, "TARGET_WGS", 8)   # few, large row chunks
+    made = []
+    init = E.HipTreeBuilder.__init__
+
+    def spy(self, *a, **k):
+        init(self, *a, **k)
+        made.append(self)
+
+    monkeypatch.setattr(E.HipTreeBuilder, "__init__", spy)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("H2OMX_PK32", flag)
+        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate, seed=5)
+    assert [m.pk32 for m in made] == [False, True]
+    a, b = out["0"], out["1"]
+    for t in range(a.trees.shape[0]):
+        reach = a.compact()[t]
+        assert reach == b.compact()[t]
+        for f in ("feat", "bin", "value"):
+            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
