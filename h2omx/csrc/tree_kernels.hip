@@ -220,22 +220,33 @@ __device__ __forceinline__ uint32_t row_hash(int64_t r, uint32_t salt) {
 //      feature group of a deep level re-reads.  The host picks 3/4 only when
 //      the per-row magnitudes fit 16 bits (rows per workgroup >= 2^16 puts
 //      |G_q| <= 2^14 and S_q <= 2^15), so histograms stay bit-identical.
-template <int NBT, int ROWS, int PKM>
+// ROUTE (deeper levels, PKM 2/4): the previous level's partition is fused in.
+// Instead of slot16, every row's previous-level node id (nid) is routed
+// through that level's PartInfo table (split feature code gathered per row)
+// to its node at this level and its build slot; feature group 0 of the
+// writer pass stores the new node ids into nid_out (double-buffered: every
+// group and slot pass reads the previous ids).  Rows of nodes that stopped
+// splitting retire as ~gid; their exact leaf sums are added by the tree's
+// final partition (all-rows mode).  Saves one streaming pass per level.
+template <int NBT, int ROWS, int PKM, bool ROUTE>
 __global__ __launch_bounds__(1024) void hist_build_kernel(
     const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ s2,
     const int* __restrict__ nid, const NodeLink* __restrict__ link, const int* __restrict__ ctl,
     const int* __restrict__ nvb, const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups,
     int wgpg, int slot_lo, int slot_cnt, const short* __restrict__ slot16, unsigned long long* __restrict__ pk_buf,
-    unsigned long long* __restrict__ partials) {
+    unsigned long long* __restrict__ partials, const PartInfo* __restrict__ part_prev,
+    const int* __restrict__ ctl_prev, int* __restrict__ nid_out, int writer) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
   __shared__ int width_s[256], rep_s[256];
   const int n_slots = ctl[CTL_SLOTS];
-  if (slot_lo >= n_slots) return;  // uniform: nothing to build in this pass
-
   const int b = blockIdx.x;
   const int xcd = b & 7, i = b >> 3;
   const int group = i % n_groups;
   const int chunk = xcd + 8 * (i / n_groups);
+  // uniform: nothing to build in this pass (a routing writer still moves the rows)
+  const bool route_w = ROUTE && writer && group == 0 && ctl_prev[CTL_N] > 0;
+  const bool build = slot_lo < n_slots;
+  if (!build && !route_w) return;
   const int f0 = group * fg;
   const int nf = min(fg, F - f0);
   const int hist_elems = slot_cnt * fg * NBT;
@@ -260,7 +271,64 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     const int64_t r0 = u * ROWS;
     int s[ROWS];
     bool any = false;
-    if constexpr (PKM == 2 || PKM == 4) {
+    if constexpr (ROUTE) {
+      int nn[ROWS], nx[ROWS];
+#pragma unroll
+      for (int q = 0; q < ROWS / 4; ++q) {
+        const int4 n4 = *reinterpret_cast<const int4*>(nid + r0 + 4 * q);
+        nn[4 * q] = n4.x; nn[4 * q + 1] = n4.y; nn[4 * q + 2] = n4.z; nn[4 * q + 3] = n4.w;
+      }
+#pragma unroll
+      for (int k = 0; k < ROWS; ++k) { nx[k] = nn[k]; s[k] = -1; }
+      // one wave-uniform pass per previous-level node: its split feature's codes
+      // for the lane's ROWS rows come in ONE coalesced load (no per-row byte
+      // gathers); the host fuses only levels whose previous level has few nodes
+      const int n_prev = ctl_prev[CTL_N];
+      for (int j = 0; j < n_prev; ++j) {
+        bool mine = false;
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) mine |= (nn[k] == j);
+        if (!mine) continue;
+        const PartInfo pj = part_prev[j];
+        if (pj.child < 0) {
+#pragma unroll
+          for (int k = 0; k < ROWS; ++k)
+            if (nn[k] == j) nx[k] = ~pj.gid;
+          continue;
+        }
+        uint32_t cw[ROWS / 4];
+        const uint8_t* cp = codes + (int64_t)pj.feat * npad + r0;
+        if constexpr (ROWS == 16) {
+          const uint4 c4 = *reinterpret_cast<const uint4*>(cp);
+          cw[0] = c4.x; cw[1] = c4.y; cw[2] = c4.z; cw[3] = c4.w;
+        } else {
+          const uint2 c2 = *reinterpret_cast<const uint2*>(cp);
+          cw[0] = c2.x; cw[1] = c2.y;
+        }
+        const int sl_l = (int)(short)(pj.pad & 0xFFFF), sl_r = pj.pad >> 16;
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) {
+          if (nn[k] == j) {
+            const int bc = (cw[k >> 2] >> (8 * (k & 3))) & 0xff;
+            const int right = (bc == NBT - 1) ? !pj.na_left : (bc > pj.bin);
+            nx[k] = pj.child + right;
+            s[k] = right ? sl_r : sl_l;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < ROWS; ++k) {
+        int sl = s[k] - slot_lo;
+        if (sl < 0 || sl >= slot_cnt || !build) sl = -1;
+        s[k] = sl;
+        any |= (sl >= 0);
+      }
+      if (route_w) {
+#pragma unroll
+        for (int q = 0; q < ROWS / 4; ++q)
+          *reinterpret_cast<int4*>(nid_out + r0 + 4 * q) = make_int4(nx[4 * q], nx[4 * q + 1], nx[4 * q + 2], nx[4 * q + 3]);
+      }
+    } else if constexpr (PKM == 2 || PKM == 4) {
 #pragma unroll
       for (int q = 0; q < ROWS / 8; ++q) {
         const int4 v4 = *reinterpret_cast<const int4*>(slot16 + r0 + 8 * q);
@@ -937,18 +1005,21 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(const NodeSplit* _
 // the window with integer global atomics (order-independent: deterministic).
 template <bool PREF, int RPL>
 __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restrict__ codes, int64_t npad,
-                                                        int* __restrict__ nid, const PartInfo* __restrict__ part,
+                                                        int* nid, const PartInfo* __restrict__ part,
                                                         int nbt, const float* __restrict__ g,
                                                         const float* __restrict__ h, const float* __restrict__ w,
                                                         const double* __restrict__ qs, int cap,
                                                         unsigned long long* __restrict__ leaf_acc,
                                                         const int* __restrict__ ctl_cur,
                                                         const int* __restrict__ ctl_next, int win_max, int R,
-                                                        short* __restrict__ slot16) {
+                                                        short* __restrict__ slot16, int* nid_out, int all_rows) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lacc[];
   const bool use_lds = leaf_acc != nullptr && win_max > 0;
-  const int base = ctl_cur[CTL_BASE];
-  const int win = use_lds ? min(win_max, ctl_cur[CTL_N] + ctl_next[CTL_N]) : 0;
+  // all_rows (final level of the fused-routing pipeline): rows that retired at
+  // earlier levels (nid = ~gid) add their sums here too; the LDS window is the
+  // whole tree [0, win_max)
+  const int base = all_rows ? 0 : ctl_cur[CTL_BASE];
+  const int win = use_lds ? (all_rows ? win_max : min(win_max, ctl_cur[CTL_N] + ctl_next[CTL_N])) : 0;
   if (use_lds) {
     for (int j = threadIdx.x; j < 3 * win * R; j += blockDim.x) lacc[j] = 0ull;
     __syncthreads();
@@ -993,11 +1064,18 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
     for (int k = 0; k < RPL; ++k) {
       sv[k] = -1;
       const int n = nn[k];
-      if (n < 0) continue;
-      changed = true;
-      const PartInfo pi = part[n];
       int leaf = -1;
-      if (pi.child < 0) {
+      PartInfo pi;
+      if (n < 0) {
+        if (!all_rows) continue;
+        leaf = ~n;  // retired earlier (padding: INT_MIN -> beyond cap, no sums)
+        pi.child = -2;
+      } else {
+        changed = true;
+        pi = part[n];
+      }
+      if (pi.child == -2) {
+      } else if (pi.child < 0) {
         leaf = pi.gid;
       } else {
         const int b = codes[(int64_t)pi.feat * npad + r0 + k];
@@ -1010,7 +1088,7 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
         }
       }
       if (leaf >= 0) {
-        nn[k] = ~leaf;
+        if (n >= 0) nn[k] = ~leaf;
         if (leaf_acc && leaf < cap) {
           const float wv = PREF ? wv8[k] : (w ? w[r0 + k] : 1.0f);
           if (wv != 0.0f) {
@@ -1035,10 +1113,11 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
         }
       }
     }
-    if (changed) {
+    if (changed || nid_out != nid) {
 #pragma unroll
       for (int v = 0; v < RPL / 4; ++v)
-        *reinterpret_cast<int4*>(nid + r0 + 4 * v) = make_int4(nn[4 * v], nn[4 * v + 1], nn[4 * v + 2], nn[4 * v + 3]);
+        *reinterpret_cast<int4*>(nid_out + r0 + 4 * v) =
+            make_int4(nn[4 * v], nn[4 * v + 1], nn[4 * v + 2], nn[4 * v + 3]);
     }
     if (slot16) {  // every row, so rows outside the tree read -1 on the next level
 #pragma unroll
@@ -1426,14 +1505,19 @@ H2OMX_API int h2omx_bin_features(const float* X, int64_t ld, int64_t n, int F, c
   return launch_status();
 }
 
-H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* g, const float* s2, const int* nid,
-                               const void* link, const int* ctl, const int* nvb, const double* qscale, int salt,
-                               int F, int nbt, int fg, int n_groups, int wgpg, int slot_lo, int slot_cnt,
-                               int rows_per_lane, int threads, const short* slot16, unsigned long long* pk_buf,
-                               int pkm, unsigned long long* partials, hipStream_t stream) {
+static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g, const float* s2, const int* nid,
+                             const void* link, const int* ctl, const int* nvb, const double* qscale, int salt,
+                             int F, int nbt, int fg, int n_groups, int wgpg, int slot_lo, int slot_cnt,
+                             int rows_per_lane, int threads, const short* slot16, unsigned long long* pk_buf,
+                             int pkm, unsigned long long* partials, const void* part_prev, const int* ctl_prev,
+                             int* nid_out, int writer, hipStream_t stream) {
+  const bool route = part_prev != nullptr;
+  if (route && (ctl_prev == nullptr || nid_out == nullptr || nid_out == nid || (pkm != 2 && pkm != 4)))
+    return kBadArg;
+  const PartInfo* pp = reinterpret_cast<const PartInfo*>(part_prev);
   if (wgpg % 8 != 0 || npad % 16 != 0 || fg > 256 || threads % 64 != 0 || threads > 1024 || threads < fg)
     return kBadArg;
-  if (pkm < 0 || pkm > 4 || (pkm > 0 && pk_buf == nullptr) || ((pkm == 2 || pkm == 4) && slot16 == nullptr))
+  if (pkm < 0 || pkm > 4 || (pkm > 0 && pk_buf == nullptr) || ((pkm == 2 || pkm == 4) && !route && slot16 == nullptr))
     return kBadArg;
   const int64_t units = npad / rows_per_lane;
   if ((units + wgpg - 1) / wgpg * rows_per_lane > ROWS_CAP) return kBadArg;  // fixed-point headroom
@@ -1441,17 +1525,19 @@ H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* 
   if (lds > 156 * 1024) return kBadArg;
   const int grid = n_groups * wgpg;
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
-#define H2OMX_HBK(NB, R, M)                                                                                      \
-  hipLaunchKernelGGL((hist_build_kernel<NB, R, M>), dim3(grid), dim3(threads), lds, stream, codes, npad, g, s2, nid, \
-                     lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt, slot16, pk_buf, \
-                     partials)
-#define H2OMX_HB(NB, R)                     \
-  do {                                      \
-    if (pkm == 0) H2OMX_HBK(NB, R, 0);      \
-    else if (pkm == 1) H2OMX_HBK(NB, R, 1); \
-    else if (pkm == 2) H2OMX_HBK(NB, R, 2); \
-    else if (pkm == 3) H2OMX_HBK(NB, R, 3); \
-    else H2OMX_HBK(NB, R, 4);               \
+#define H2OMX_HBK(NB, R, M, RT)                                                                              \
+  hipLaunchKernelGGL((hist_build_kernel<NB, R, M, RT>), dim3(grid), dim3(threads), lds, stream, codes, npad, g, \
+                     s2, nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt,     \
+                     slot16, pk_buf, partials, pp, ctl_prev, nid_out, writer)
+#define H2OMX_HB(NB, R)                                     \
+  do {                                                      \
+    if (pkm == 0) H2OMX_HBK(NB, R, 0, false);               \
+    else if (pkm == 1) H2OMX_HBK(NB, R, 1, false);          \
+    else if (pkm == 2 && route) H2OMX_HBK(NB, R, 2, true);  \
+    else if (pkm == 2) H2OMX_HBK(NB, R, 2, false);          \
+    else if (pkm == 3) H2OMX_HBK(NB, R, 3, false);          \
+    else if (route) H2OMX_HBK(NB, R, 4, true);              \
+    else H2OMX_HBK(NB, R, 4, false);                        \
   } while (0)
   if (rows_per_lane == 16) {
     switch (nbt) {
@@ -1475,6 +1561,30 @@ H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* 
 #undef H2OMX_HB
 #undef H2OMX_HBK
   return launch_status();
+}
+
+H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* g, const float* s2, const int* nid,
+                               const void* link, const int* ctl, const int* nvb, const double* qscale, int salt,
+                               int F, int nbt, int fg, int n_groups, int wgpg, int slot_lo, int slot_cnt,
+                               int rows_per_lane, int threads, const short* slot16, unsigned long long* pk_buf,
+                               int pkm, unsigned long long* partials, hipStream_t stream) {
+  return hist_build_launch(codes, npad, g, s2, nid, link, ctl, nvb, qscale, salt, F, nbt, fg, n_groups, wgpg, slot_lo,
+                           slot_cnt, rows_per_lane, threads, slot16, pk_buf, pkm, partials, nullptr, nullptr, nullptr,
+                           0, stream);
+}
+
+// Deeper level with the previous level's partition fused in (see ROUTE):
+// nid_prev -> nid_out (writer pass only), part_prev / ctl_prev = that level.
+H2OMX_API int h2omx_hist_build_route(const uint8_t* codes, int64_t npad, const int* nid_prev, const void* part_prev,
+                                     const int* ctl_prev, int* nid_out, int writer, const int* ctl, const int* nvb,
+                                     const double* qscale, int F, int nbt, int fg, int n_groups, int wgpg,
+                                     int slot_lo, int slot_cnt, int rows_per_lane, int threads,
+                                     unsigned long long* pk_buf, int pkm, unsigned long long* partials,
+                                     hipStream_t stream) {
+  if (part_prev == nullptr) return kBadArg;
+  return hist_build_launch(codes, npad, nullptr, nullptr, nid_prev, nullptr, ctl, nvb, qscale, 0, F, nbt, fg, n_groups,
+                           wgpg, slot_lo, slot_cnt, rows_per_lane, threads, nullptr, pk_buf, pkm, partials, part_prev,
+                           ctl_prev, nid_out, writer, stream);
 }
 
 H2OMX_API int h2omx_hist_build_compact(const uint8_t* codes, int64_t npad, const float* g, const float* s2,
@@ -1552,26 +1662,61 @@ H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_n
 constexpr int PARTITION_BLOCKS = 8192;
 constexpr int PART_RPL = 8;    // rows per lane per step (16: 1.52 vs 1.47 ms/tree on HIGGS)
 
-H2OMX_API int h2omx_partition(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt, const float* g,
-                              const float* h, const float* w, const double* qscale, int cap,
-                              unsigned long long* leaf_acc, const int* ctl_cur, const int* ctl_next, int win_max,
-                              int blocks, int prefetch, short* slot16, hipStream_t stream) {
+static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt, const float* g,
+                            const float* h, const float* w, const double* qscale, int cap,
+                            unsigned long long* leaf_acc, const int* ctl_cur, const int* ctl_next, int win_max,
+                            int blocks, int prefetch, short* slot16, int* nid_out, int all_rows, hipStream_t stream) {
   if (slot16 && prefetch) return kBadArg;
   if (npad % PART_RPL != 0 || blocks < 1 || blocks > PARTITION_BLOCKS || win_max < 0) return kBadArg;
-  // lane-private copies: the largest power of two <= 64 that fits 48 KB
+  if (all_rows && (leaf_acc == nullptr || win_max > cap)) return kBadArg;
+  // lane-private copies: the largest power of two <= 64 that fits 64 KB
+  constexpr size_t kWinLds = 64 * 1024;
   int R = 64;
-  while (R > 1 && (size_t)3 * win_max * R * sizeof(unsigned long long) > 48 * 1024) R >>= 1;
-  if ((size_t)3 * win_max * R * sizeof(unsigned long long) > 48 * 1024) win_max = 0;
+  while (R > 1 && (size_t)3 * win_max * R * sizeof(unsigned long long) > kWinLds) R >>= 1;
+  if ((size_t)3 * win_max * R * sizeof(unsigned long long) > kWinLds) {
+    if (all_rows) return kBadArg;  // the whole-tree window must fit
+    win_max = 0;
+  }
   const size_t lds = (leaf_acc && win_max > 0) ? (size_t)3 * win_max * R * sizeof(unsigned long long) : 0;
   if (prefetch && leaf_acc)
     hipLaunchKernelGGL((partition_kernel<true, PART_RPL>), dim3(blocks), dim3(256), lds, stream, codes, npad, nid,
                        reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
-                       ctl_next, win_max, R, slot16);
+                       ctl_next, win_max, R, slot16, nid_out, all_rows);
   else
     hipLaunchKernelGGL((partition_kernel<false, PART_RPL>), dim3(blocks), dim3(256), lds, stream, codes, npad, nid,
                        reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
-                       ctl_next, leaf_acc ? win_max : 0, R, slot16);
+                       ctl_next, leaf_acc ? win_max : 0, R, slot16, nid_out, all_rows);
   return launch_status();
+}
+
+H2OMX_API int h2omx_partition(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt, const float* g,
+                              const float* h, const float* w, const double* qscale, int cap,
+                              unsigned long long* leaf_acc, const int* ctl_cur, const int* ctl_next, int win_max,
+                              int blocks, int prefetch, short* slot16, hipStream_t stream) {
+  return partition_launch(codes, npad, nid, part, nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur, ctl_next, win_max,
+                          blocks, prefetch, slot16, nid, 0, stream);
+}
+
+// Intermediate level of the fused-routing pipeline that is not fused into the
+// next histogram (previous level too wide for per-node code loads): routes
+// nid_in -> nid_out and writes slot16; no leaf sums (the final level adds them).
+H2OMX_API int h2omx_partition_route(const uint8_t* codes, int64_t npad, const int* nid_in, int* nid_out,
+                                    const void* part, int nbt, const int* ctl_cur, const int* ctl_next, int blocks,
+                                    short* slot16, hipStream_t stream) {
+  if (slot16 == nullptr) return kBadArg;
+  return partition_launch(codes, npad, const_cast<int*>(nid_in), part, nbt, nullptr, nullptr, nullptr, nullptr, 0,
+                          nullptr, ctl_cur, ctl_next, 0, blocks, 0, slot16, nid_out, 0, stream);
+}
+
+// Final level of the fused-routing pipeline: nid_in (this level's node ids,
+// earlier leaves as ~gid) -> nid_out leaves, exact sums of EVERY row into the
+// whole-tree LDS window [0, cap).
+H2OMX_API int h2omx_partition_final(const uint8_t* codes, int64_t npad, const int* nid_in, int* nid_out,
+                                    const void* part, int nbt, const float* g, const float* h, const float* w,
+                                    const double* qscale, int cap, unsigned long long* leaf_acc, const int* ctl_cur,
+                                    const int* ctl_next, int blocks, hipStream_t stream) {
+  return partition_launch(codes, npad, const_cast<int*>(nid_in), part, nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
+                          ctl_next, cap, blocks, 1, nullptr, nid_out, 1, stream);
 }
 
 static inline int stream_grid(int64_t) { return STAT_BLOCKS; }

@@ -82,6 +82,8 @@ class HipTreeBuilder:
     SEG_LDS_BUDGET = 64 * 1024
     SCAN_SLOTS = int(os.environ.get("H2OMX_SCAN_SLOTS", "16"))  # seg engine: scan hist up to this many slots
     DEEP_DEPTH = 10
+    FUSE_MAX_DEPTH = 8
+    FUSE_MAX_PREV = int(os.environ.get("H2OMX_FUSE_MAX_PREV", "4"))
     CLOSE_SINGLE_BLOCK = int(os.environ.get("H2OMX_CLOSE_SINGLE_BLOCK", "2048"))
 
     def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
@@ -135,6 +137,13 @@ class HipTreeBuilder:
         # (tree_begin: |G_q| <= 2^14, S_q <= 2^15): the packed rows are then stored in
         # 32 bits (hist_build PKM 3/4), halving what every deep-level feature group re-reads
         self.pk32 = self.max_rows_per_wg >= 65536 and os.environ.get("H2OMX_PK32", "1") == "1"
+        # fused routing (scan engine, shallow trees): level d's partition runs inside
+        # level d+1's histogram kernel (node ids double-buffered), and the last level's
+        # partition adds the exact sums of every row, early leaves included, into a
+        # whole-tree LDS window (needs the tree capacity to fit it: depth <= 8)
+        self.fuse_route = (params.max_depth <= self.FUSE_MAX_DEPTH and not self.COMPACT
+                           and os.environ.get("H2OMX_FUSE_ROUTE", "1") == "1")
+        self.nid2 = torch.full((bm.npad,), -1, dtype=torch.int32, device=d) if self.fuse_route else None
         # Engine choice (both build bit-identical trees):
         # * scan: every level streams all rows; best for shallow trees (HIGGS depth 5:
         #   1.52 vs 1.90 ms/tree for the segmented engine, profiles/seg_vs_scan_s1.txt)
@@ -147,6 +156,7 @@ class HipTreeBuilder:
         eng = os.environ.get("H2OMX_TREE_ENGINE", "auto")
         self.segmented = eng == "seg" or (eng == "auto" and params.max_depth > self.DEEP_DEPTH)
         if self.segmented:
+            self.fuse_route, self.nid2 = False, None
             self.pc_rows = int(self.lib.h2omx_pc_rows())
             hc = int(os.environ.get("H2OMX_SEG_CHUNK", "0")) or -(-bm.n // self.SEG_TARGET_CHUNKS)
             self.hc_rows = min(self.ROWS_CAP, max(2048, -(-hc // 256) * 256))
@@ -211,6 +221,12 @@ class HipTreeBuilder:
         self.plans[max_slots] = plan
         return plan
 
+    def _fused_level(self, d: int) -> bool:
+        """Level d >= 1 routes its rows inside its histogram kernel when the
+        previous level has at most FUSE_MAX_PREV nodes (one coalesced code load
+        per previous node and row unit; wider levels keep a routing pass)."""
+        return (1 << (d - 1)) <= self.FUSE_MAX_PREV
+
     def _params(self, tree_index: int):
         p, sp = self.p, self._sp
         sp.mode, sp.leaf_mode, sp.F, sp.is_last_level = p.mode, p.leaf_mode, self.F, 0
@@ -254,6 +270,9 @@ class HipTreeBuilder:
         max_depth = p.max_depth
         final_ctl = self.ctl[max_depth % 2]
         max_nodes = 1
+        fuse = self.fuse_route
+        nid_buf = (self.nid, self.nid2)
+        part_prev = None
         for d in range(max_depth):
             cur, nxt = d % 2, (d + 1) % 2
             ctl_cur, ctl_nxt = self.ctl[cur], self.ctl[nxt]
@@ -276,7 +295,15 @@ class HipTreeBuilder:
             for ps in range(plan["passes"]):
                 slot_lo = ps * plan["slot_cnt"]
                 with T("hist"):
-                    if d > 0 and self.COMPACT:
+                    if d > 0 and fuse and self._fused_level(d):
+                        # partition of level d - 1 fused in: nid_buf[d - 1] -> nid_buf[d]
+                        ops.check(lib.h2omx_hist_build_route(
+                            P(bm.codes), bm.npad, P(nid_buf[(d - 1) % 2]), P(part_prev), P(ctl_nxt),
+                            P(nid_buf[d % 2]), 1 if ps == 0 else 0, P(ctl_cur), P(bm.nvb), P(self.qscale), F, nbt,
+                            plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo, plan["slot_cnt"],
+                            self.ROWS_PER_LANE, plan["threads"], P(self.pk), 4 if self.pk32 else 2, P(partials), st),
+                            "hist_build_route")
+                    elif d > 0 and self.COMPACT:
                         ops.check(lib.h2omx_hist_build_compact(
                             P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]), P(ctl_cur), P(bm.nvb),
                             P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, plan["fg"], plan["n_groups"],
@@ -286,7 +313,8 @@ class HipTreeBuilder:
                         # level 0 stores the packed quantised rows; deeper levels read them
                         # with the build slots the previous partition wrote
                         ops.check(lib.h2omx_hist_build(
-                            P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]), P(ctl_cur), P(bm.nvb),
+                            P(bm.codes), bm.npad, P(g), P(s2), P(nid_buf[d % 2] if fuse else self.nid),
+                            P(link[cur]), P(ctl_cur), P(bm.nvb),
                             P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, plan["fg"], plan["n_groups"],
                             plan["wgpg"], slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],
                             P(self.slot16), P(self.pk), (1 if d == 0 else 2) + (2 if self.pk32 else 0), P(partials),
@@ -319,11 +347,23 @@ class HipTreeBuilder:
             # leaves that can retire at this level: gids [base, base + n + n_next)
             win = min(3 * max_nodes, self.capacity)
             with T("partition"):
-                ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, P(g), P(h), P(w),
-                                              P(self.qscale), self.capacity, P(self.leaf_acc), P(ctl_cur),
-                                              P(ctl_nxt), win, self.part_blocks, 1 if last else 0,
-                                              P(None if last else self.slot16), st),
-                          "partition")
+                if fuse and last:
+                    ops.check(lib.h2omx_partition_final(P(bm.codes), bm.npad, P(nid_buf[d % 2]), P(self.nid),
+                                                        P(part), nbt, P(g), P(h), P(w), P(self.qscale),
+                                                        self.capacity, P(self.leaf_acc), P(ctl_cur), P(ctl_nxt),
+                                                        self.part_blocks, st), "partition_final")
+                elif fuse and not self._fused_level(d + 1):
+                    ops.check(lib.h2omx_partition_route(P(bm.codes), bm.npad, P(nid_buf[d % 2]),
+                                                        P(nid_buf[(d + 1) % 2]), P(part), nbt, P(ctl_cur),
+                                                        P(ctl_nxt), self.part_blocks, P(self.slot16), st),
+                              "partition_route")
+                elif not fuse:
+                    ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, P(g), P(h),
+                                                  P(w), P(self.qscale), self.capacity, P(self.leaf_acc),
+                                                  P(ctl_cur), P(ctl_nxt), win, self.part_blocks, 1 if last else 0,
+                                                  P(None if last else self.slot16), st),
+                              "partition")
+            part_prev = part
             full_prev = full_cur
             max_nodes = next_nodes
         # exact leaf values (sums accumulated by the partition kernels)

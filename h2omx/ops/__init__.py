@@ -21,10 +21,13 @@ TREE_SIGS = {
     "h2omx_hist_build": "PLPPPPPPPIIIIIIIIIIPPIPS",
     "h2omx_hist_reduce": "PIIIIIIIPPS",
     "h2omx_hist_build_compact": "PLPPPPPPPIIIIIIIIIIPS",
+    "h2omx_hist_build_route": "PLPPPPIPPPIIIIIIIIIPIPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
     "h2omx_level_finalize": "PPPPPPIIPPPIPIS",
     "h2omx_partition": "PLPPIPPPPIPPPIIIPS",
     "h2omx_partition_blocks": "",
+    "h2omx_partition_final": "PLPPPIPPPPIPPPIS",
+    "h2omx_partition_route": "PLPPPIPPIPS",
     "h2omx_leaf_reduce": "PIIPS",
     "h2omx_boost_update": "PPPLLPPPPPPPS",
     "h2omx_apply_tree": "PLPPS",

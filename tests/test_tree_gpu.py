@@ -212,3 +212,45 @@ def test_pk32_rows_match_pk64(cuda_dev, monkeypatch, dist, depth, sample_rate):
         assert reach == b.compact()[t]
         for f in ("feat", "bin", "value"):
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
+
+
+@pytest.mark.parametrize("dist,depth,sample_rate,min_rows,lds_kb", [
+    ("bernoulli", 5, 1.0, 3, 0), ("bernoulli", 6, 0.6, 400, 0), ("gaussian", 8, 0.8, 50, 0),
+    ("multinomial", 4, 1.0, 3, 0), ("bernoulli", 1, 1.0, 3, 0), ("gaussian", 6, 1.0, 3, 16)])
+def test_fused_routing_matches_partition(cuda_dev, monkeypatch, dist, depth, sample_rate, min_rows, lds_kb):
+    """Partition fused into the next level's histogram kernel (double-buffered
+    node ids, whole-tree leaf sums at the last level) builds bit-identical
+    trees and margins: early leaves (large min_rows), bagging, several slot
+    passes per level (small LDS budget) and depth 1 included."""
+    import h2omx.models.tree.engine as E
+
+    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi"}[dist]
+    X, y = _data(n=30000, F=9, seed=9, task=task)
+    _, bg = _both(X, y, 255)
+    tp = TreeParams(max_depth=depth, min_rows=min_rows, learn_rate=0.2)
+    yt = torch.from_numpy(y).cuda()
+    if lds_kb:
+        monkeypatch.setattr(E.HipTreeBuilder, "LDS_BUDGET", lds_kb * 1024)
+        monkeypatch.setattr(E.HipTreeBuilder, "DEEP_LDS_BUDGET", lds_kb * 1024)
+    out = {}
+    # unfused; fused while the previous level has <= 4 nodes (routing pass after);
+    # fused at every level
+    for key, flag, max_prev in (("off", "0", 4), ("mixed", "1", 4), ("all", "1", 1 << 20)):
+        monkeypatch.setenv("H2OMX_FUSE_ROUTE", flag)
+        monkeypatch.setattr(E.HipTreeBuilder, "FUSE_MAX_PREV", max_prev)
+        out[key] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
+                                  nclass=3 if dist == "multinomial" else 1, seed=4)
+    Xd = torch.from_numpy(X).cuda()
+
+    def margin(e):
+        m = e.raw_margin(Xd)
+        return m.cpu().numpy() if torch.is_tensor(m) else np.asarray(m)
+
+    a = out["off"]
+    for b in (out["mixed"], out["all"]):
+        for t in range(a.trees.shape[0]):
+            reach = a.compact()[t]
+            assert reach == b.compact()[t]
+            for f in ("feat", "bin", "value", "weight"):
+                np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
+        np.testing.assert_array_equal(margin(a), margin(b))
