@@ -695,32 +695,24 @@ struct FeatBest {  // 64 B
   double pad2;
 };
 
-// K5: best threshold of every (node, feature).  One wave per (node, feature)
-// (4 features per 256-thread block, grid = nodes x ceil(F / 4)), each lane
-// owning NBT / 64 consecutive bins: the histogram row (built slot, or
-// parent - built sibling) is loaded as exact int64, scanned with wave
-// shuffles only (no LDS, no block barriers - deep trees run 10^5 nodes per
-// level, so per-block latency dominates), converted to fp64 exactly and
-// scored for both NA directions.  mtries / column sampling ranks the
-// feature's hash among all features with one ballot per 64 features.
+// Best threshold of (node, f) computed by one wave; every lane returns the
+// same result (gain -inf / code INT_MAX = none).  Also stores the completed
+// histogram row into `full` (parent of the next level) when given.
+struct WaveBest {
+  double gain, GL, SL, G, S;
+  int code;
+};
+
 template <int NBT>
-__global__ __launch_bounds__(256) void split_find_kernel(const long long* __restrict__ built,
-                                                         const long long* __restrict__ parent_full,
-                                                         long long* __restrict__ full, const int* __restrict__ ctl,
-                                                         const NodeLink* __restrict__ link,
-                                                         const int* __restrict__ nvb,
-                                                         const uint8_t* __restrict__ tree_fmask,
-                                                         const double* __restrict__ qscale, SplitParams p,
-                                                         FeatBest* __restrict__ out) {
+__device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__ built,
+                                                   const long long* __restrict__ parent_full,
+                                                   long long* __restrict__ full, const NodeLink& lk, int node, int f,
+                                                   const int* __restrict__ nvb,
+                                                   const uint8_t* __restrict__ tree_fmask, double ig, double is,
+                                                   const SplitParams& p) {
   constexpr int B = NBT <= 64 ? 1 : NBT / 64;  // bins per lane
-  const int node = blockIdx.x;
-  if (node >= ctl[CTL_N]) return;
   const int F = p.F;
   const int lane = threadIdx.x & 63;
-  const int f = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (f >= F) return;  // whole wave
-  const NodeLink lk = link[node];
-  const double ig = qscale[2], is = qscale[3];
   const int64_t per = (int64_t)F * 2 * NBT;
   const int64_t off = ((int64_t)f * 2) * NBT;
   long long gi[B], si[B];
@@ -811,21 +803,51 @@ __global__ __launch_bounds__(256) void split_find_kernel(const long long* __rest
     const int oc = __shfl_xor(bc, o, kWave);
     if (og > bg || (og == bg && oc < bc)) { bg = og; bc = oc; }
   }
-  FeatBest* o = out + (int64_t)node * F + f;
-  if (bc == 0x7fffffff) {
-    if (lane == 0) {
-      FeatBest r{};
-      r.gain = -INFINITY;
-      r.G = tg; r.S = ts;
-      r.code = 0x7fffffff;
-      *o = r;
-    }
-  } else if (best_code == bc) {  // unique owner of the winning threshold
+  WaveBest r;
+  r.G = tg; r.S = ts;
+  r.gain = (bc == 0x7fffffff) ? -INFINITY : bg;
+  r.code = bc;
+  r.GL = r.SL = 0.0;
+  if (bc != 0x7fffffff) {
+    // unique owner of the winning threshold broadcasts its left totals
+    const unsigned long long own = __ballot(best_code == bc);
+    const int src = __ffsll((long long)own) - 1;
+    r.GL = __shfl(bGL, src, kWave);
+    r.SL = __shfl(bSL, src, kWave);
+  }
+  return r;
+}
+
+// K5: best threshold of every (node, feature).  One wave per (node, feature)
+// (4 features per 256-thread block, grid = nodes x ceil(F / 4)), each lane
+// owning NBT / 64 consecutive bins: the histogram row (built slot, or
+// parent - built sibling) is loaded as exact int64, scanned with wave
+// shuffles only (no LDS, no block barriers - deep trees run 10^5 nodes per
+// level, so per-block latency dominates), converted to fp64 exactly and
+// scored for both NA directions.  mtries / column sampling ranks the
+// feature's hash among all features with one ballot per 64 features.
+template <int NBT>
+__global__ __launch_bounds__(256) void split_find_kernel(const long long* __restrict__ built,
+                                                         const long long* __restrict__ parent_full,
+                                                         long long* __restrict__ full, const int* __restrict__ ctl,
+                                                         const NodeLink* __restrict__ link,
+                                                         const int* __restrict__ nvb,
+                                                         const uint8_t* __restrict__ tree_fmask,
+                                                         const double* __restrict__ qscale, SplitParams p,
+                                                         FeatBest* __restrict__ out) {
+  const int node = blockIdx.x;
+  if (node >= ctl[CTL_N]) return;
+  const int f = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (f >= p.F) return;  // whole wave
+  const NodeLink lk = link[node];
+  const WaveBest w = feat_best_wave<NBT>(built, parent_full, full, lk, node, f, nvb, tree_fmask, qscale[2],
+                                         qscale[3], p);
+  if ((threadIdx.x & 63) == 0) {
     FeatBest r{};
-    r.gain = bg; r.GL = bGL; r.SL = bSL;
-    r.G = tg; r.S = ts;
-    r.code = bc;
-    *o = r;
+    r.gain = w.gain; r.GL = w.GL; r.SL = w.SL;
+    r.G = w.G; r.S = w.S;
+    r.code = w.code;
+    out[(int64_t)node * p.F + f] = r;
   }
 }
 
@@ -878,13 +900,11 @@ __global__ __launch_bounds__(64) void node_best_kernel(const FeatBest* __restric
 // the children, pick the smaller child to build, write tree records and the
 // partition table.  ctl_next receives the next level's counts.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void level_finalize_kernel(const NodeSplit* __restrict__ nsplit,
-                                                              const int* __restrict__ ctl, int* __restrict__ ctl_next,
-                                                              SplitParams p, const float* __restrict__ edges,
-                                                              const int* __restrict__ nvb, int nbt,
-                                                              int max_next_nodes, PartInfo* __restrict__ part,
-                                                              NodeLink* __restrict__ next_link,
-                                                              TreeNode* __restrict__ tree, int tree_capacity) {
+__device__ void level_finalize_body(const NodeSplit* __restrict__ nsplit, const int* __restrict__ ctl,
+                                    int* __restrict__ ctl_next, const SplitParams& p, const float* __restrict__ edges,
+                                    const int* __restrict__ nvb, int nbt, int max_next_nodes,
+                                    PartInfo* __restrict__ part, NodeLink* __restrict__ next_link,
+                                    TreeNode* __restrict__ tree, int tree_capacity) {
   __shared__ int wsum[16];
   __shared__ int carry;
   const int n = ctl[CTL_N];
@@ -989,6 +1009,106 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(const NodeSplit* _
     ctl_next[CTL_BASE] = next_base;
     ctl_next[CTL_TOTAL] = next_base + 2 * ks;
   }
+}
+
+__global__ __launch_bounds__(1024) void level_finalize_kernel(const NodeSplit* __restrict__ nsplit,
+                                                              const int* __restrict__ ctl, int* __restrict__ ctl_next,
+                                                              SplitParams p, const float* __restrict__ edges,
+                                                              const int* __restrict__ nvb, int nbt,
+                                                              int max_next_nodes, PartInfo* __restrict__ part,
+                                                              NodeLink* __restrict__ next_link,
+                                                              TreeNode* __restrict__ tree, int tree_capacity) {
+  level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes, part, next_link, tree,
+                      tree_capacity);
+}
+
+// K5 fused with the per-node arg-max and the level finalisation: one
+// 1024-thread workgroup per node, wave w scans features w, w + 16, ... and
+// the workgroup reduces the 16 wave winners (gain desc, then (feature, code)
+// asc - the node_best order) into the node's NodeSplit.  The last node
+// workgroup to finish (agent-scope release / ticket / acquire hand-off) runs
+// level_finalize_body, so a level's split decision is ONE launch instead of
+// three (split_find, node_best, level_finalize).  The ticket is reset by that
+// last workgroup (buffer zeroed once at allocation).
+template <int NBT>
+__global__ __launch_bounds__(1024) void split_level_kernel(
+    const long long* __restrict__ built, const long long* __restrict__ parent_full, long long* __restrict__ full,
+    const int* __restrict__ ctl, const NodeLink* __restrict__ link, const int* __restrict__ nvb,
+    const uint8_t* __restrict__ tree_fmask, const double* __restrict__ qscale, SplitParams p,
+    NodeSplit* __restrict__ nsplit, unsigned int* __restrict__ ticket, int* __restrict__ ctl_next,
+    const float* __restrict__ edges, int max_next_nodes, PartInfo* __restrict__ part,
+    NodeLink* __restrict__ next_link, TreeNode* __restrict__ tree, int tree_capacity) {
+  __shared__ double s_gain[16], s_gl[16], s_sl[16], s_tot[2];
+  __shared__ long long s_key[16];
+  __shared__ int s_last;
+  const int n = ctl[CTL_N];
+  const int node = blockIdx.x;
+  if (n == 0) {  // tree already finished: still publish the (empty) next level
+    if (node == 0)
+      level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, NBT, max_next_nodes, part, next_link, tree,
+                          tree_capacity);
+    return;
+  }
+  if (node >= n) return;
+  const int F = p.F;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const NodeLink lk = link[node];
+  const double ig = qscale[2], is = qscale[3];
+  double bg = -INFINITY, bgl = 0.0, bsl = 0.0;
+  long long key = 0x7fffffffffffffffLL;
+  for (int f = wave; f < F; f += nw) {
+    const WaveBest w = feat_best_wave<NBT>(built, parent_full, full, lk, node, f, nvb, tree_fmask, ig, is, p);
+    if (f == 0 && lane == 0) { s_tot[0] = w.G; s_tot[1] = w.S; }
+    if (w.code != 0x7fffffff && w.gain > -INFINITY) {
+      const long long k = ((long long)f << 32) | (unsigned)w.code;
+      if (key == 0x7fffffffffffffffLL || w.gain > bg || (w.gain == bg && k < key)) {
+        bg = w.gain; key = k; bgl = w.GL; bsl = w.SL;
+      }
+    }
+  }
+  if (lane == 0) { s_gain[wave] = bg; s_key[wave] = key; s_gl[wave] = bgl; s_sl[wave] = bsl; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double g = -INFINITY, gl = 0.0, sl = 0.0;
+    long long k = 0x7fffffffffffffffLL;
+    for (int w = 0; w < nw; ++w) {
+      if (s_key[w] == 0x7fffffffffffffffLL) continue;
+      if (k == 0x7fffffffffffffffLL || s_gain[w] > g || (s_gain[w] == g && s_key[w] < k)) {
+        g = s_gain[w]; k = s_key[w]; gl = s_gl[w]; sl = s_sl[w];
+      }
+    }
+    NodeSplit ns;
+    ns.G = s_tot[0]; ns.H = s_tot[1]; ns.W = s_tot[1];
+    ns.pad = 0;
+    if (k != 0x7fffffffffffffffLL) {
+      const int code = (int)(k & 0xffffffff);
+      ns.gain = g; ns.GL = gl; ns.HL = sl; ns.WL = sl;
+      ns.feat = (int)(k >> 32); ns.bin = code >> 1; ns.na_left = code & 1;
+    } else {
+      ns.gain = -INFINITY; ns.GL = ns.HL = ns.WL = 0.0;
+      ns.feat = -1; ns.bin = 0; ns.na_left = 0;
+    }
+    nsplit[node] = ns;
+  }
+  // hand-off to the last arriving node workgroup (cdna_hip_programming.md split-K recipe)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t == (unsigned)(n - 1));
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (s_last)
+    level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, NBT, max_next_nodes, part, next_link, tree,
+                        tree_capacity);
 }
 
 // K6: route every row to its child, or retire it into its leaf (nid = ~gid).
@@ -1641,6 +1761,30 @@ H2OMX_API int h2omx_split_find(const long long* built, const long long* parent_f
     default: return kBadArg;
   }
 #undef H2OMX_SF
+  return launch_status();
+}
+
+H2OMX_API int h2omx_split_level(const long long* built, const long long* parent_full, long long* full, const int* ctl,
+                                const void* link, const int* nvb, const uint8_t* tree_fmask, const double* qscale,
+                                const void* params, int max_nodes, int nbt, void* nsplit, unsigned int* ticket,
+                                int* ctl_next, const float* edges, int max_next_nodes, void* part, void* next_link,
+                                void* tree, int tree_capacity, hipStream_t stream) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  if (max_nodes < 1 || ticket == nullptr) return kBadArg;
+#define H2OMX_SL(NB)                                                                                            \
+  hipLaunchKernelGGL(split_level_kernel<NB>, dim3(max_nodes), dim3(1024), 0, stream, built, parent_full, full, ctl, \
+                     reinterpret_cast<const NodeLink*>(link), nvb, tree_fmask, qscale, p,                        \
+                     reinterpret_cast<NodeSplit*>(nsplit), ticket, ctl_next, edges, max_next_nodes,              \
+                     reinterpret_cast<PartInfo*>(part), reinterpret_cast<NodeLink*>(next_link),                  \
+                     reinterpret_cast<TreeNode*>(tree), tree_capacity)
+  switch (nbt) {
+    case 32: H2OMX_SL(32); break;
+    case 64: H2OMX_SL(64); break;
+    case 128: H2OMX_SL(128); break;
+    case 256: H2OMX_SL(256); break;
+    default: return kBadArg;
+  }
+#undef H2OMX_SL
   return launch_status();
 }
 

@@ -144,6 +144,13 @@ class HipTreeBuilder:
         self.fuse_route = (params.max_depth <= self.FUSE_MAX_DEPTH and not self.COMPACT
                            and os.environ.get("H2OMX_FUSE_ROUTE", "1") == "1")
         self.nid2 = torch.full((bm.npad,), -1, dtype=torch.int32, device=d) if self.fuse_route else None
+        # one-launch split decision (split_level: 16 waves per node scan <= 4 features each,
+        # last-arriver hand-off into the level finalisation).  Bit-identical but measured
+        # slower on HIGGS depth 5 (1.108 vs 1.071 ms/tree: one workgroup per node halves
+        # the scan parallelism and the agent-scope hand-off costs about a launch), so
+        # opt-in (H2OMX_FUSE_SPLIT=1)
+        self.fuse_split = self.F <= 64 and os.environ.get("H2OMX_FUSE_SPLIT", "0") == "1"
+        self.ticket = torch.zeros((4,), dtype=torch.int32, device=d)
         # Engine choice (both build bit-identical trees):
         # * scan: every level streams all rows; best for shallow trees (HIGGS depth 5:
         #   1.52 vs 1.90 ms/tree for the segmented engine, profiles/seg_vs_scan_s1.txt)
@@ -326,13 +333,8 @@ class HipTreeBuilder:
                 with T("allreduce"):
                     comm.all_reduce_(built[: max_slots * self.per_node])
             full_cur = None if last else self._buf(f"full{cur}", max_nodes * self.per_node, torch.int64)
-            fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
             sp.depth = d
             sp.children_leaves = 1 if last else 0
-            with T("split"):
-                ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
-                                               P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
-                                               P(fbest), st), "split_find")
             next_nodes = 2 * max_nodes
             part = self._buf("part", max_nodes * PART_INFO_BYTES // 4, torch.int32)
             nl = None
@@ -341,9 +343,22 @@ class HipTreeBuilder:
                 link[nxt] = nl
             nsplit = self._buf("nsplit", max_nodes * 9, torch.float64)  # NodeSplit = 72 B
             with T("split"):
-                ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges), P(bm.nvb),
-                                                   nbt, next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
-                                                   P(nsplit), max_nodes, st), "level_finalize")
+                if self.fuse_split:
+                    # scan + per-node arg-max + level finalisation in one launch
+                    ops.check(lib.h2omx_split_level(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
+                                                    P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
+                                                    P(nsplit), P(self.ticket), P(ctl_nxt), P(bm.edges),
+                                                    next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
+                                                    st), "split_level")
+                else:
+                    fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
+                    ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
+                                                   P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
+                                                   P(fbest), st), "split_find")
+                    ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
+                                                       P(bm.nvb), nbt, next_nodes, P(part), P(nl),
+                                                       P(self.tree_buf), self.capacity, P(nsplit), max_nodes, st),
+                              "level_finalize")
             # leaves that can retire at this level: gids [base, base + n + n_next)
             win = min(3 * max_nodes, self.capacity)
             with T("partition"):

@@ -24,6 +24,7 @@ TREE_SIGS = {
     "h2omx_hist_build_route": "PLPPPPIPPPIIIIIIIIIPIPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
     "h2omx_level_finalize": "PPPPPPIIPPPIPIS",
+    "h2omx_split_level": "PPPPPPPPPIIPPPPIPPPIS",
     "h2omx_partition": "PLPPIPPPPIPPPIIIPS",
     "h2omx_partition_blocks": "",
     "h2omx_partition_final": "PLPPPIPPPPIPPPIS",
