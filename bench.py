@@ -148,10 +148,47 @@ def _mlp(args, comm, torch, np):
     nb = max(1, n_local // B)
     state = {"i": 0}
     bw = H2ODeepLearningEstimator._backward
+    bf16 = args.precision == "bf16"
+    graph = None
+    if bf16:
+        from h2omx.models.deeplearning import _Bf16Mlp
+
+        mlp = _Bf16Mlp(net, 1, B, dev)
+        yb = torch.zeros((B,), dtype=torch.int32, device=dev)
+
+        def body():
+            mlp.forward(mlp.Xb)
+            mlp.loss_grad(yb)
+            mlp.backward(None, mlp.Xbt, comm if world > 1 else None, world)
+            D.adadelta_(net.flat, net.grad, Eg2, Edx2, 0.99, 1e-8, 0.0)
+            mlp.refresh()
+
+        if args.graph and world == 1:
+            # the step after the batch staging is one HIP graph (fixed buffers); warm-up
+            # on a side stream first so every lazily allocated workspace exists
+            mlp.load_batch(X[:B])
+            yb.copy_(yi[:B])
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                body()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                body()
 
     def step():
         i = state["i"] % nb
         state["i"] += 1
+        if bf16:
+            # stage the batch: bf16 row-major + transposed (+ ones row) and its labels
+            mlp.load_batch(X[i * B:(i + 1) * B])
+            yb.copy_(yi[i * B:(i + 1) * B])
+            if graph is not None:
+                graph.replay()
+            else:
+                body()
+            return
         xb = X[i * B:(i + 1) * B]
         Hs, aux = _forward(net, xb, 1, True, 0.0, [0.0] * 8, None)
         dZ, _ = D.softmax_xent(Hs[-1], yi[i * B:(i + 1) * B])
@@ -175,7 +212,8 @@ def _mlp(args, comm, torch, np):
         "unit": "samples/s (all GPUs)",
         "ms_per_step": 1000.0 * elapsed / args.steps,
         "higher_is_better": True,
-        "dtype": "fp32 (MFMA fp32 GEMMs, fp32 ADADELTA)",
+        "dtype": ("bf16 (bf16 MFMA GEMMs with fp32 accumulation; fp32 master weights, gradients and ADADELTA)"
+                  if bf16 else "fp32 (MFMA fp32 GEMMs, fp32 ADADELTA)"),
         "data": "synthetic wide-Gaussian 200 features generated on device; random-init weights",
         "config": {"model": "MLP 200-512x4-2 Rectifier, ADADELTA(0.99,1e-8), softmax", "global_batch": world * B,
                    "seq_len": None, "rows_per_gpu": n_local, "batch_per_gpu": B,
@@ -199,6 +237,10 @@ def main(argv=None) -> int:
     ap.add_argument("--learn-rate", type=float, default=0.0)
     ap.add_argument("--min-rows", type=float, default=10.0)
     ap.add_argument("--batch", type=int, default=8192, help="dl-mlp rows per GPU per step")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="dl-mlp bf16, 1 GPU: replay each step as a HIP graph (measured no faster: GPU-bound)")
+    ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16",
+                    help="dl-mlp GEMM operand precision (fp32 accumulation and master weights either way)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-auc", action="store_true")

@@ -655,6 +655,329 @@ __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ W
 }
 
 // ===========================================================================
+// bf16 MLP path: bf16 operands on the matrix cores (v_mfma_f32_32x32x16_bf16,
+// 16x the fp32-MFMA rate), fp32 accumulation, fp32 master weights / optimizer.
+//
+// One GEMM form, "NT": C[m][n] = sum_k A[m*lda + k] * B[n*ldb + k], both
+// operands K-contiguous, so every MFMA fragment (8 consecutive k of one row)
+// is ONE 16-byte LDS read.  The MLP's three products map onto it by keeping
+// the transposed copies the backward pass needs (written by the producing
+// epilogue, never by a separate transpose):
+//   forward   H_l     = act(H_{l-1} . W_l^T + b)   A = H_{l-1}, B = W_l
+//   weights   dW_l    = dZ_l^T . H_{l-1}            A = dZ_l^T,  B = H_{l-1}^T
+//   inputs    dZ_{l-1}= (dZ_l . W_l) * act'(H)      A = dZ_l,    B = W_l^T
+// K (and lda / ldb) must be multiples of 8 (16-byte rows; callers zero-pad).
+// 128 x 128 block tile, 8 waves of 32 x 64 (2 accumulators), BK = 64 per
+// double-buffered LDS stage (rows padded to 144 B: the 16 lanes of a
+// ds_read_b128 group hit 16 distinct 16-byte bank slots).
+// ===========================================================================
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+#ifndef H2OMX_BF16_HK
+#define H2OMX_BF16_HK 64
+#endif
+constexpr int HB = 128, HK = H2OMX_BF16_HK, HPAD = 8, HROW = HK + HPAD;   // bf16 elements
+static int H2OMX_BF16_VARIANT = -1;  // tile-variant override for A/B runs (h2omx_gemm_bf16_variant)
+
+struct BfEpi {
+  const float* bias;        // [N] or null
+  const uint16_t* ymask;    // act' source Y (bf16 [M][ldy]) or null
+  float* cf;                // fp32 out [M][ldc] or null
+  uint16_t* cb;             // bf16 out [M][ldc] or null
+  uint16_t* cbt;            // bf16 transposed out [N][ldt] or null
+  float* c_last;            // column N-1 -> c_last[m] instead of cf (bias gradients via a ones row)
+  int ldy, ldc, ldt;
+  int act;                  // 0 none, 1 relu, 2 tanh (applied to the output)
+  int mask_act;             // act' of ymask multiplied in (1 relu, 2 tanh), 0 none
+  float beta_c;             // cf += beta_c * old cf
+};
+
+__device__ __forceinline__ uint16_t f2bf(float v) {
+  __bf16 b = (__bf16)v;
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+__device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
+
+// global -> registers: a ROWS x 64 bf16 tile in 16-byte chunks, 8 chunks per row
+template <int ROWS, int THREADS>
+struct BfTile {
+  static constexpr int NQ = ROWS * 8 / THREADS;
+  uint4 v[NQ];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ P, int ld, int rows, int K, int r0, int k0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int c = threadIdx.x + THREADS * q;
+      const int r = r0 + (c >> 3), kk = k0 + (c & 7) * 8;
+      v[q] = (r < rows && kk < K) ? *reinterpret_cast<const uint4*>(P + (int64_t)r * ld + kk) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* S) const {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int c = threadIdx.x + THREADS * q;
+      *reinterpret_cast<uint4*>(S + (c >> 3) * HROW + (c & 7) * 8) = v[q];
+    }
+  }
+};
+
+// Block tile BM x BN, wave tile WTM x WTN ((WTM / 32) x (WTN / 32) MFMA
+// accumulators of 32 x 32), (BM / WTM) x (BN / WTN) waves.  Instances:
+//   <128, 128, 64, 64>  4 waves, one 128 x 128 block per CU: 2 + 2 fragment
+//                       reads per 4 MFMAs (the wide products)
+//   <128,  64, 32, 64>  4 waves, two blocks per CU (narrow outputs)
+template <int BM, int BN, int WTM, int WTN>
+__global__ __launch_bounds__(64 * (BM / WTM) * (BN / WTN))
+void gemm_bf16_nt_kernel(const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb, int M,
+                         int N, int K, float* __restrict__ ws, BfEpi ep) {
+  constexpr int WR = BM / WTM, WC = BN / WTN, THREADS = 64 * WR * WC;
+  constexpr int AM = WTM / 32, AN = WTN / 32;
+  __shared__ __attribute__((aligned(16))) uint16_t As[2][BM * HROW];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][BN * HROW];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int wm = (wid / WC) * WTM, wn = (wid % WC) * WTN;
+  const int S = gridDim.z;
+  const int kchunk = ((K + S - 1) / S + HK - 1) / HK * HK;
+  const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+  f32x16 acc[AM][AN];
+#pragma unroll
+  for (int a = 0; a < AM; ++a)
+#pragma unroll
+    for (int b = 0; b < AN; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+  const int li = lane & 31, lh = lane >> 5;
+  // register prefetch PD stages deep: at step s the tiles of stage s + 1 (loaded
+  // PD steps earlier) go to LDS and their registers immediately start loading
+  // stage s + 1 + PD, so several global-load latencies overlap
+  constexpr int PD = 3;
+  BfTile<BM, THREADS> ra[PD];
+  BfTile<BN, THREADS> rb[PD];
+  const int nsteps = kb < ke ? (ke - kb + HK - 1) / HK : 0;
+#pragma unroll
+  for (int d = 0; d < PD; ++d) {
+    if (d < nsteps) {
+      ra[d].load(A, lda, M, ke, m0, kb + d * HK);
+      rb[d].load(B, ldb, N, ke, n0, kb + d * HK);
+    }
+  }
+  if (nsteps > 0) {
+    ra[0].store(As[0]);
+    rb[0].store(Bs[0]);
+    if (PD < nsteps) {
+      ra[0].load(A, lda, M, ke, m0, kb + PD * HK);
+      rb[0].load(B, ldb, N, ke, n0, kb + PD * HK);
+    }
+  }
+  __syncthreads();
+  for (int s0 = 0; s0 < nsteps; s0 += PD) {
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      const int st = s0 + u;
+      if (st < nsteps) {
+        const int buf = st & 1;
+        const uint16_t* as = As[buf] + (wm + li) * HROW + 8 * lh;
+        const uint16_t* bs = Bs[buf] + (wn + li) * HROW + 8 * lh;
+#pragma unroll
+        for (int s2 = 0; s2 < HK / 16; ++s2) {
+          bf16x8 af[AM], bfr[AN];
+#pragma unroll
+          for (int a = 0; a < AM; ++a) af[a] = *reinterpret_cast<const bf16x8*>(as + a * 32 * HROW + 16 * s2);
+#pragma unroll
+          for (int b = 0; b < AN; ++b) bfr[b] = *reinterpret_cast<const bf16x8*>(bs + b * 32 * HROW + 16 * s2);
+#pragma unroll
+          for (int a = 0; a < AM; ++a)
+#pragma unroll
+            for (int b = 0; b < AN; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+        }
+        if (st + 1 < nsteps) {
+          const int nr = (u + 1) % PD;  // static once the u loop is unrolled
+          ra[nr].store(As[buf ^ 1]);
+          rb[nr].store(Bs[buf ^ 1]);
+          if (st + 1 + PD < nsteps) {
+            ra[nr].load(A, lda, M, ke, m0, kb + (st + 1 + PD) * HK);
+            rb[nr].load(B, ldb, N, ke, n0, kb + (st + 1 + PD) * HK);
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  // epilogue: lane owns column j, registers e are rows (e&3) + 8(e>>2) + 4h
+#pragma unroll
+  for (int a = 0; a < AM; ++a) {
+#pragma unroll
+    for (int y = 0; y < AN; ++y) {
+      const int j = n0 + wn + 32 * y + li;
+      if (j >= N) continue;
+      const int mrow = m0 + wm + 32 * a;
+      if (S > 1) {
+        float* w = ws + (int64_t)blockIdx.z * M * N;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = mrow + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          if (i < M) w[(int64_t)i * N + j] = acc[a][y][e];
+        }
+        continue;
+      }
+      const float bj = ep.bias ? ep.bias[j] : 0.0f;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int i0 = mrow + 8 * g4 + 4 * lh;
+        float v4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = i0 + q;
+          float v = acc[a][y][4 * g4 + q] + bj;
+          if (i < M) {
+            if (ep.cf && ep.beta_c != 0.0f) v += ep.beta_c * ep.cf[(int64_t)i * ep.ldc + j];
+            if (ep.act == 1) v = fmaxf(v, 0.0f);
+            else if (ep.act == 2) v = tanhf(v);
+            if (ep.mask_act) {
+              const float yv = bf2f(ep.ymask[(int64_t)i * ep.ldy + j]);
+              v = (ep.mask_act == 1) ? (yv > 0.0f ? v : 0.0f) : v * (1.0f - yv * yv);
+            }
+            if (ep.c_last && j == N - 1) ep.c_last[i] = v;
+            else if (ep.cf) ep.cf[(int64_t)i * ep.ldc + j] = v;
+            if (ep.cb) ep.cb[(int64_t)i * ep.ldc + j] = f2bf(v);
+          }
+          v4[q] = v;
+        }
+        if (ep.cbt) {
+          uint16_t* d = ep.cbt + (int64_t)j * ep.ldt + i0;
+          if (i0 + 3 < M) {
+            const uint32_t lo = (uint32_t)f2bf(v4[0]) | ((uint32_t)f2bf(v4[1]) << 16);
+            const uint32_t hi = (uint32_t)f2bf(v4[2]) | ((uint32_t)f2bf(v4[3]) << 16);
+            *reinterpret_cast<uint2*>(d) = make_uint2(lo, hi);
+          } else {
+            for (int q = 0; q < 4 && i0 + q < M; ++q) d[q] = f2bf(v4[q]);
+          }
+        }
+      }
+    }
+  }
+}
+
+// split-K partials [S][M][N] -> cf[m][n] (ld ldc) for n < N - 1 (or all n
+// when c_last is null) and c_last[m] for n = N - 1; fixed summation order
+__global__ __launch_bounds__(256) void splitk_reduce_cols_kernel(const float* __restrict__ W, int S, int M, int N,
+                                                                 float* __restrict__ C, int ldc,
+                                                                 float* __restrict__ c_last) {
+  const int64_t MN = (int64_t)M * N;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < MN; e += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.0f;
+    for (int z = 0; z < S; ++z) v += W[z * MN + e];
+    const int i = (int)(e / N), j = (int)(e % N);
+    if (c_last && j == N - 1) c_last[i] = v;
+    else C[(int64_t)i * ldc + j] = v;
+  }
+}
+
+// fp32 [R][C] (ld ldx) -> bf16 [R][ldo] (columns >= C zero up to ldo) and/or
+// bf16 transposed [C][ldot] (rows >= C untouched, columns >= R untouched).
+// 64 x 64 tiles through LDS so both outputs are written row-contiguous.
+__global__ __launch_bounds__(256) void cvt_bf16_kernel(const float* __restrict__ X, int ldx, int R, int C,
+                                                       uint16_t* __restrict__ out, int ldo,
+                                                       uint16_t* __restrict__ outT, int ldot) {
+  __shared__ float tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int rr = ty; rr < 64; rr += 4) {
+    const int r = r0 + rr, c = c0 + tx;
+    const float v = (r < R && c < C) ? X[(int64_t)r * ldx + c] : 0.0f;
+    tile[rr][tx] = v;
+    if (out && r < R && c < ldo) out[(int64_t)r * ldo + c] = f2bf(v);
+  }
+  if (!outT) return;
+  __syncthreads();
+  for (int cc = ty; cc < 64; cc += 4) {
+    const int c = c0 + cc, r = r0 + tx;
+    if (c < C && r < R) outT[(int64_t)c * ldot + r] = f2bf(tile[tx][cc]);
+  }
+}
+
+// out[n] = sum_b X[n][b] for bf16 rows (bias gradients from dZ^T): one wave per row
+__global__ __launch_bounds__(256) void rowsum_bf16_kernel(const uint16_t* __restrict__ X, int ld, int R, int C,
+                                                          float* __restrict__ out) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const uint16_t* x = X + (int64_t)r * ld;
+  float s = 0.0f;
+  for (int c = lane * 8; c < C; c += 512) {
+    if (c + 8 <= C) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + c);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s += bf2f((uint16_t)(w[q] & 0xFFFF)) + bf2f((uint16_t)(w[q] >> 16));
+    } else {
+      for (int q = c; q < C; ++q) s += bf2f(x[q]);
+    }
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[r] = s;
+}
+
+struct CvtJob {
+  const float* X;
+  uint16_t* out;
+  uint16_t* outT;
+  int ldx, R, C, ldo, ldot, pad[3];
+};
+struct CvtJobs {
+  CvtJob j[8];
+};
+
+// several fp32 -> bf16 (+ transposed) conversions in one launch (blockIdx.z = job):
+// the MLP's per-layer weight refresh after every optimizer step
+__global__ __launch_bounds__(256) void cvt_bf16_multi_kernel(CvtJobs jobs) {
+  const CvtJob& jb = jobs.j[blockIdx.z];
+  const int cols = jb.out ? (jb.ldo > jb.C ? jb.ldo : jb.C) : jb.C;
+  if ((int)blockIdx.x * 64 >= cols || (int)blockIdx.y * 64 >= jb.R) return;
+  __shared__ float tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int rr = ty; rr < 64; rr += 4) {
+    const int r = r0 + rr, c = c0 + tx;
+    const float v = (r < jb.R && c < jb.C) ? jb.X[(int64_t)r * jb.ldx + c] : 0.0f;
+    tile[rr][tx] = v;
+    if (jb.out && r < jb.R && c < jb.ldo) jb.out[(int64_t)r * jb.ldo + c] = f2bf(v);
+  }
+  if (!jb.outT) return;
+  __syncthreads();
+  for (int cc = ty; cc < 64; cc += 4) {
+    const int c = c0 + cc, r = r0 + tx;
+    if (c < jb.C && r < jb.R) jb.outT[(int64_t)c * jb.ldot + r] = f2bf(tile[tx][cc]);
+  }
+}
+
+// softmax cross-entropy of fp32 logits Z [M][K] -> bf16 dZ [M][ldd] (k < K) and
+// bf16 dZ^T [K][ldt]; mean loss accumulated into loss[0]
+__global__ __launch_bounds__(256) void softmax_xent_bf16_kernel(const float* __restrict__ Z, const int* __restrict__ y,
+                                                                uint16_t* __restrict__ dZ, int ldd,
+                                                                uint16_t* __restrict__ dZt, int ldt,
+                                                                float* __restrict__ loss, int M, int K) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float l = 0.0f;
+  if (i < M) {
+    const float* z = Z + (int64_t)i * K;
+    float mx = -INFINITY;
+    for (int k = 0; k < K; ++k) mx = fmaxf(mx, z[k]);
+    float den = 0.0f;
+    for (int k = 0; k < K; ++k) den += __expf(z[k] - mx);
+    const int yi = y[i];
+    for (int k = 0; k < K; ++k) {
+      const float pk = __expf(z[k] - mx) / den;
+      const uint16_t g = f2bf((pk - (k == yi ? 1.0f : 0.0f)) / (float)M);
+      dZ[(int64_t)i * ldd + k] = g;
+      dZt[(int64_t)k * ldt + i] = g;
+      if (k == yi) l = -logf(fmaxf(pk, 1e-30f));
+    }
+  }
+  l = wave_sum(l);
+  if ((threadIdx.x & 63) == 0) atomicAdd(loss, l / (float)M);
+}
+
+// ===========================================================================
 // C ABI
 // ===========================================================================
 static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
@@ -764,4 +1087,83 @@ H2OMX_API int h2omx_sgd_momentum(float* W, const float* G, float* V, int64_t n, 
                                  hipStream_t stream) {
   hipLaunchKernelGGL(sgd_momentum_kernel, dim3(cdiv(n, 256)), dim3(256), 0, stream, W, G, V, n, lr, mom, l2);
   return launch_status();
+}
+
+H2OMX_API int h2omx_gemm_bf16(const uint16_t* A, int lda, const uint16_t* B, int ldb, int M, int N, int K,
+                              const float* bias, int act, const uint16_t* ymask, int ldy, int mask_act, float* cf,
+                              uint16_t* cb, int ldc, uint16_t* cbt, int ldt, float beta_c, int splitk, float* ws,
+                              float* c_last, hipStream_t stream) {
+  if (K % 8 || lda % 8 || ldb % 8 || M < 1 || N < 1 || K < 8 || splitk < 1) return kBadArg;
+  if ((reinterpret_cast<uintptr_t>(A) & 15) || (reinterpret_cast<uintptr_t>(B) & 15)) return kBadArg;
+  if (cbt && ((ldt & 3) || (reinterpret_cast<uintptr_t>(cbt) & 7))) return kBadArg;
+  if (mask_act && !ymask) return kBadArg;
+  if (splitk > 1 && (!ws || !cf || cb || cbt || mask_act)) return kBadArg;  // split-K: fp32 out only
+  if (c_last && (bias || act || beta_c != 0.0f || cb || cbt || mask_act)) return kBadArg;
+  BfEpi ep{bias, ymask, cf, cb, cbt, c_last, ldy, ldc, ldt, act, mask_act, beta_c};
+  // 128 x 128 blocks of eight 32 x 64 wave tiles (two waves per SIMD hide each
+  // other's LDS / global latency: measured fastest, scripts/gemm_bf16_micro.py);
+  // 128 x 64 blocks of four where the output has at most one 64-column block.
+  // Variant 0 (four 64 x 64 wave tiles) is kept for A/B runs.
+  const int variant = H2OMX_BF16_VARIANT >= 0 ? H2OMX_BF16_VARIANT : (N <= 64 ? 1 : 2);
+  if (variant == 1) {
+    const dim3 grid(cdiv(N, 64), cdiv(M, HB), splitk);
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 64, 32, 64>), grid, dim3(256), 0, stream, A, lda, B, ldb, M, N, K, ws,
+                       ep);
+  } else if (variant == 2) {
+    const dim3 grid(cdiv(N, HB), cdiv(M, HB), splitk);
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 32, 64>), grid, dim3(512), 0, stream, A, lda, B, ldb, M, N, K,
+                       ws, ep);
+  } else {
+    const dim3 grid(cdiv(N, HB), cdiv(M, HB), splitk);
+    hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 64, 64>), grid, dim3(256), 0, stream, A, lda, B, ldb, M, N, K,
+                       ws, ep);
+  }
+  if (splitk > 1) {
+    const int64_t mn = (int64_t)M * N;
+    const int g = cdiv(mn, 256) < 4096 ? cdiv(mn, 256) : 4096;
+    if (bias || act || beta_c != 0.0f) {
+      if (ldc != N || c_last) return kBadArg;
+      hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(g), dim3(256), 0, stream, ws, splitk, M, N, cf, bias, act,
+                         beta_c);
+    } else {
+      hipLaunchKernelGGL(splitk_reduce_cols_kernel, dim3(g), dim3(256), 0, stream, ws, splitk, M, N, cf, ldc, c_last);
+    }
+  }
+  return launch_status();
+}
+
+H2OMX_API int h2omx_cvt_bf16(const float* X, int ldx, int R, int C, uint16_t* out, int ldo, uint16_t* outT, int ldot,
+                             hipStream_t stream) {
+  if (R < 1 || C < 1) return kOk;
+  hipLaunchKernelGGL(cvt_bf16_kernel, dim3(cdiv(out ? (ldo > C ? ldo : C) : C, 64), cdiv(R, 64)), dim3(256), 0,
+                     stream, X, ldx, R, C, out, ldo, outT, ldot);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_rowsum_bf16(const uint16_t* X, int ld, int R, int C, float* out, hipStream_t stream) {
+  if (ld % 8 || (reinterpret_cast<uintptr_t>(X) & 15)) return kBadArg;
+  hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(cdiv(R, 4)), dim3(256), 0, stream, X, ld, R, C, out);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_cvt_bf16_multi(const void* jobs, int n_jobs, int max_rows, int max_cols, hipStream_t stream) {
+  if (n_jobs < 1 || n_jobs > 8) return kBadArg;
+  CvtJobs J{};
+  const CvtJob* src = reinterpret_cast<const CvtJob*>(jobs);
+  for (int k = 0; k < n_jobs; ++k) J.j[k] = src[k];
+  hipLaunchKernelGGL(cvt_bf16_multi_kernel, dim3(cdiv(max_cols, 64), cdiv(max_rows, 64), n_jobs), dim3(256), 0, stream,
+                     J);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_softmax_xent_bf16(const float* Z, const int* y, uint16_t* dZ, int ldd, uint16_t* dZt, int ldt,
+                                      float* loss, int M, int K, hipStream_t stream) {
+  hipLaunchKernelGGL(softmax_xent_bf16_kernel, dim3(cdiv(M, 256)), dim3(256), 0, stream, Z, y, dZ, ldd, dZt, ldt, loss,
+                     M, K);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_gemm_bf16_variant(int v) {
+  H2OMX_BF16_VARIANT = v;
+  return kOk;
 }

@@ -134,6 +134,108 @@ def _forward(net: _Net, X, act, train, drop_in, drop_hid, gen_dev, out_act=0):
     return Hs, aux
 
 
+def _pad8(x: int) -> int:
+    return (x + 7) // 8 * 8
+
+
+class _Bf16Mlp:
+    """bf16-operand training step of a Rectifier / Tanh MLP (no maxout, no
+    dropout) on the bf16 matrix cores (ops.dense.gemm_bf16_nt: fp32
+    accumulation, bias / activation / activation-derivative fused into the
+    epilogue, which also writes the transposed bf16 copies the weight
+    gradients read).  The fp32 master weights and the optimizer stay in fp32
+    (``net.flat``); ``refresh()`` re-derives the bf16 weights after an update.
+    All activation buffers are persistent and zero-padded to 8-element rows.
+    """
+
+    def __init__(self, net: _Net, act: int, batch: int, dev, out_act: int = 0):
+        if act not in (1, 2) or batch % 8:
+            raise ValueError("bf16 MLP path needs Rectifier/Tanh and a batch that is a multiple of 8")
+        self.net, self.act, self.B, self.out_act = net, act, batch, out_act
+        self.L = L = len(net.layers)
+        self.shapes = [(w, f) for (_, w, f) in net.layers]
+        self.kp = [_pad8(f) for (w, f) in self.shapes]
+        self.wp = [_pad8(w) for (w, f) in self.shapes]
+
+        def z(*shape):
+            return torch.zeros(shape, dtype=torch.bfloat16, device=dev)
+
+        self.Wb = [z(w, kp) for (w, f), kp in zip(self.shapes, self.kp)]
+        self.Wbt = [z(f, wp) for (w, f), wp in zip(self.shapes, self.wp)]
+        self.H = [None] + [z(batch, self.kp[i]) for i in range(1, L)]
+        # transposed layer inputs carry an extra row of ones: the weight-gradient
+        # GEMM then also produces the bias gradient (its last output column)
+        self.Ht = [None] + [self.with_ones_row(z(self.shapes[i][1] + 1, batch)) for i in range(1, L)]
+        self.logits = torch.zeros((batch, self.shapes[-1][0]), dtype=torch.float32, device=dev)
+        self.loss = torch.zeros((1,), dtype=torch.float32, device=dev)
+        self.dZ = [z(batch, self.wp[i]) for i in range(L)]
+        self.dZt = [z(self.shapes[i][0], batch) for i in range(L)]
+        self.Xb = z(batch, self.kp[0])
+        self.Xbt = self.with_ones_row(z(self.shapes[0][1] + 1, batch))
+        self.refresh()
+
+    @staticmethod
+    def with_ones_row(t: torch.Tensor) -> torch.Tensor:
+        t[-1].fill_(1.0)
+        return t
+
+    def refresh(self) -> None:
+        """fp32 master weights -> bf16 [w][kp] and transposed [f][wp] copies (one launch)."""
+        D.cvt_bf16_multi([(self.net.W(i), self.Wb[i], self.Wbt[i]) for i in range(self.L)])
+
+    def load_batch(self, xb: torch.Tensor):
+        """fp32 [B][d] mini-batch -> bf16 row-major + transposed (ones row kept) staging buffers."""
+        D.cvt_bf16(xb, out=self.Xb, out_t=self.Xbt)
+        return self.Xb, self.Xbt
+
+    def forward(self, xb: torch.Tensor) -> torch.Tensor:
+        """xb: bf16 [B][kp0] (row stride multiple of 8).  Returns fp32 logits [B][K]."""
+        H = xb
+        for i in range(self.L):
+            w, f = self.shapes[i]
+            if i == self.L - 1:
+                D.gemm_bf16_nt(H, self.Wb[i], self.B, w, self.kp[i], bias=self.net.b(i), act=self.out_act,
+                               out_f32=self.logits)
+            else:
+                D.gemm_bf16_nt(H, self.Wb[i], self.B, w, self.kp[i], bias=self.net.b(i), act=self.act,
+                               out_bf16=self.H[i + 1], out_bf16_t=self.Ht[i + 1])
+                H = self.H[i + 1]
+        return self.logits
+
+    def loss_grad(self, y: torch.Tensor) -> None:
+        """Softmax cross-entropy of the last forward's logits: bf16 dZ / dZ^T of the output layer."""
+        self.loss.zero_()
+        D.softmax_xent_bf16(self.logits, y, self.dZ[self.L - 1], self.dZt[self.L - 1], self.loss)
+
+    def backward(self, dZ: torch.Tensor | None, xbt: torch.Tensor, comm=None, world: int = 1) -> None:
+        """dZ: fp32 [B][K] loss gradient of the logits, or None after ``loss_grad``;
+        xbt: bf16 [d + 1][>=B] (the batch's inputs transposed, last row ones).
+        Writes net.grad (all-reduced when world > 1)."""
+        net, B = self.net, self.B
+        L = self.L
+        if dZ is not None:
+            D.cvt_bf16(dZ, out=self.dZ[L - 1], out_t=self.dZt[L - 1])
+        handles = []
+        for i in range(L - 1, -1, -1):
+            w, f = self.shapes[i]
+            Hin_t = xbt if i == 0 else self.Ht[i]
+            tiles = -(-w // 128) * -(-(f + 1) // 128)
+            S = max(1, min(64, 256 // tiles, B // 256))
+            D.gemm_bf16_nt(self.dZt[i], Hin_t, w, f + 1, B, out_f32=net.W(i, net.grad), splitk=S,
+                           c_last=net.b(i, net.grad))
+            if comm is not None and world > 1:
+                a, b = net.span(i)
+                handles.append(comm.all_reduce_async(net.grad[a:b]))
+            if i == 0:
+                break
+            D.gemm_bf16_nt(self.dZ[i], self.Wbt[i], B, f, self.wp[i], ymask=self.H[i], mask_act=self.act,
+                           out_bf16=self.dZ[i - 1], out_bf16_t=self.dZt[i - 1])
+        for h in handles:
+            h.wait()
+        if comm is not None and world > 1:
+            net.grad.div_(world)
+
+
 class DeepLearningModel(Model):
     algo = "deeplearning"
     algo_full_name = "Deep Learning"
@@ -227,7 +329,8 @@ class H2ODeepLearningEstimator(ModelBuilder):
                     train_samples_per_iteration=-2, score_training_samples=10000, score_each_iteration=False,
                     stopping_rounds=5, stopping_metric="AUTO", stopping_tolerance=0.0, huber_alpha=0.9,
                     shuffle_training_data=True, reproducible=False, categorical_encoding="AUTO",
-                    use_all_factor_levels=True, offset_column=None, balance_classes=False, checkpoint=None)
+                    use_all_factor_levels=True, offset_column=None, balance_classes=False, checkpoint=None,
+                    precision="fp32")
 
     def train(self, x=None, y=None, training_frame=None, validation_frame=None, comm=None, **kw):
         if self.params.get("autoencoder"):
@@ -328,6 +431,12 @@ class H2ODeepLearningEstimator(ModelBuilder):
         job = current_job()
         samples = 0
         score_every = max(1, steps_per_epoch)
+        # h2omx extension: precision="bf16" trains Rectifier / Tanh nets without dropout
+        # on the bf16 matrix cores (fp32 accumulation, fp32 master weights / optimizer)
+        mlp = None
+        if (str(p_.get("precision", "fp32")).lower() == "bf16" and X.is_cuda and act in (1, 2) and drop_in == 0
+                and not any(hd[: len(hidden)]) and M % 8 == 0):
+            mlp = _Bf16Mlp(net, act, M, dev)
         for step in range(total_steps):
             e_pos = step % steps_per_epoch
             if e_pos == 0:
@@ -335,8 +444,13 @@ class H2ODeepLearningEstimator(ModelBuilder):
                         else torch.arange(n, device=dev))
             idx = perm[e_pos * M:(e_pos + 1) * M]
             xb = X.index_select(0, idx)
-            Hs, aux = _forward(net, xb, act, True, drop_in, hd, gen_dev)
-            Z = Hs[-1]
+            if mlp is not None:
+                xbb, xbt = mlp.load_batch(xb)
+                Z = mlp.forward(xbb)
+                Hs = aux = None
+            else:
+                Hs, aux = _forward(net, xb, act, True, drop_in, hd, gen_dev)
+                Z = Hs[-1]
             if auto:
                 dZ = (Z - xb) * (2.0 / Z.numel())
             elif cls:
@@ -351,7 +465,10 @@ class H2ODeepLearningEstimator(ModelBuilder):
                 else:
                     g = r
                 dZ = (g / r.numel())[:, None].contiguous()
-            self._backward(net, Hs, aux, dZ, act, comm, world)
+            if mlp is not None:
+                mlp.backward(dZ, xbt, comm, world)
+            else:
+                self._backward(net, Hs, aux, dZ, act, comm, world)
             samples += M * world
             if adaptive:
                 D.adadelta_(net.flat, net.grad, Eg2, Edx2, float(p_["rho"]), float(p_["epsilon"]), l2)
@@ -365,6 +482,8 @@ class H2ODeepLearningEstimator(ModelBuilder):
                 net.flat.sub_(l1 * torch.sign(net.flat) * (1.0 if adaptive else float(p_["rate"])))
             if math.isfinite(float(p_["max_w2"])):
                 self._clip_w2(net, float(p_["max_w2"]))
+            if mlp is not None:
+                mlp.refresh()
             if job is not None:
                 job.progress = (step + 1) / total_steps
             if (step + 1) % score_every == 0 or step == total_steps - 1:

@@ -62,6 +62,12 @@ DENSE_SIGS = {
     "h2omx_softmax_xent": "PPPPIIS",
     "h2omx_adadelta": "PPPPLFFFS",
     "h2omx_sgd_momentum": "PPPLFFFS",
+    "h2omx_gemm_bf16": "PIPIIIIPIPIIPPIPIFIPPS",
+    "h2omx_cvt_bf16_multi": "PIIIS",
+    "h2omx_gemm_bf16_variant": "I",
+    "h2omx_softmax_xent_bf16": "PPPIPIPIIS",
+    "h2omx_cvt_bf16": "PIIIPIPIS",
+    "h2omx_rowsum_bf16": "PIIIPS",
 }
 
 METRICS_SIGS = {

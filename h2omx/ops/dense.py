@@ -333,3 +333,124 @@ def sgd_momentum_(W, G, V, lr, mom, l2=0.0):
         return
     V.mul_(mom).sub_(lr * (G + l2 * W))
     W.add_(V)
+
+
+# ---------------------------------------------------------------------------
+# bf16 MLP path (csrc/dense_kernels.hip gemm_bf16_nt_kernel): operands are
+# torch.bfloat16 row-major matrices whose row strides are multiples of 8
+# elements (16-byte rows, zero-padded K).  GPU only: on CPU tensors the same
+# contract is computed in fp32 from the bf16 values (test oracle).
+# ---------------------------------------------------------------------------
+def gemm_bf16_nt(A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int, *, bias=None, act: int = 0,
+                 ymask: torch.Tensor | None = None, mask_act: int = 0, out_f32: torch.Tensor | None = None,
+                 out_bf16: torch.Tensor | None = None, out_bf16_t: torch.Tensor | None = None,
+                 beta_c: float = 0.0, splitk: int = 1, c_last: torch.Tensor | None = None) -> None:
+    """C[m][n] = sum_{k<K} A[m][k] B[n][k] (fp32 accumulate), epilogue
+    act(C + bias), optionally times act'(ymask) (1 relu, 2 tanh), written to
+    out_f32 [M][>=N] and/or out_bf16 [M][>=N] and/or out_bf16_t [N][>=M].
+    With ``c_last`` (plain products only) column N-1 goes to c_last [M] and
+    out_f32 receives columns < N-1: a weight gradient and, through a ones row
+    appended to B, its bias gradient in one GEMM.
+    Views with unit inner stride; A/B/out row strides multiples of 8."""
+    for t in (A, B):
+        assert t.dtype == torch.bfloat16 and t.stride(-1) == 1
+    if A.is_cuda:
+        ldc = (out_f32 if out_f32 is not None else out_bf16).stride(0) if (out_f32 is not None or out_bf16 is not None) else N
+        if out_f32 is not None and out_bf16 is not None:
+            assert out_f32.stride(0) == out_bf16.stride(0)
+        ws = _workspace(A.device, splitk * M * N, slot=1) if splitk > 1 else None
+        check(dense_lib().h2omx_gemm_bf16(
+            P(A), A.stride(0), P(B), B.stride(0), M, N, K, P(bias), act, P(ymask),
+            ymask.stride(0) if ymask is not None else 0, mask_act, P(out_f32), P(out_bf16), ldc, P(out_bf16_t),
+            out_bf16_t.stride(0) if out_bf16_t is not None else 0, float(beta_c), splitk, P(ws), P(c_last),
+            stream(A.device)), "gemm_bf16")
+        return
+    c = A[:M, :K].float() @ B[:N, :K].float().T
+    if out_f32 is not None and beta_c:
+        c = c + beta_c * out_f32[:M, :N]
+    if bias is not None:
+        c = c + bias[:N]
+    if act == 1:
+        c = torch.relu(c)
+    elif act == 2:
+        c = torch.tanh(c)
+    if mask_act:
+        y = ymask[:M, :N].float()
+        c = torch.where(y > 0, c, torch.zeros_like(c)) if mask_act == 1 else c * (1 - y * y)
+    if c_last is not None:
+        c_last[:M] = c[:, N - 1]
+        c = c[:, : N - 1]
+    if out_f32 is not None:
+        out_f32[:M, : c.shape[1]] = c
+    if out_bf16 is not None:
+        out_bf16[:M, :N] = c.to(torch.bfloat16)
+    if out_bf16_t is not None:
+        out_bf16_t[:N, :M] = c.T.to(torch.bfloat16)
+
+
+def cvt_bf16(X: torch.Tensor, out: torch.Tensor | None = None, out_t: torch.Tensor | None = None) -> None:
+    """fp32 [R][C] -> bf16 out [R][>=C] (pad columns zeroed up to out's row
+    stride) and/or bf16 out_t [C][>=R]."""
+    R, C = X.shape
+    assert X.stride(-1) == 1
+    if X.is_cuda:
+        check(dense_lib().h2omx_cvt_bf16(P(X), X.stride(0), R, C, P(out), out.stride(0) if out is not None else 0,
+                                         P(out_t), out_t.stride(0) if out_t is not None else 0, stream(X.device)),
+              "cvt_bf16")
+        return
+    if out is not None:
+        out[:R, :C] = X.to(torch.bfloat16)
+        if out.shape[1] > C:
+            out[:R, C:] = 0
+    if out_t is not None:
+        out_t[:C, :R] = X.T.to(torch.bfloat16)
+
+
+def rowsum_bf16(X: torch.Tensor, R: int, C: int, out: torch.Tensor) -> None:
+    """out[r] = sum_{c<C} X[r][c] (fp32) for a bf16 matrix (bias gradients from dZ^T)."""
+    if X.is_cuda:
+        check(dense_lib().h2omx_rowsum_bf16(P(X), X.stride(0), R, C, P(out), stream(X.device)), "rowsum_bf16")
+        return
+    out[:R] = X[:R, :C].float().sum(1)
+
+
+class _CvtJob(ctypes.Structure):
+    _fields_ = [("X", ctypes.c_void_p), ("out", ctypes.c_void_p), ("outT", ctypes.c_void_p), ("ldx", ctypes.c_int),
+                ("R", ctypes.c_int), ("C", ctypes.c_int), ("ldo", ctypes.c_int), ("ldot", ctypes.c_int),
+                ("pad", ctypes.c_int * 3)]
+
+
+def cvt_bf16_multi(jobs) -> None:
+    """Several ``cvt_bf16(X, out, out_t)`` conversions (<= 8) in one launch."""
+    jobs = list(jobs)
+    if not jobs:
+        return
+    if not jobs[0][0].is_cuda:
+        for X, out, out_t in jobs:
+            cvt_bf16(X, out, out_t)
+        return
+    arr = (_CvtJob * len(jobs))()
+    mr = mc = 1
+    for k, (X, out, out_t) in enumerate(jobs):
+        R, C = X.shape
+        arr[k] = _CvtJob(X.data_ptr(), P(out) or 0, P(out_t) or 0, X.stride(0), R, C,
+                         out.stride(0) if out is not None else 0, out_t.stride(0) if out_t is not None else 0)
+        mr = max(mr, R)
+        mc = max(mc, C, out.stride(0) if out is not None else 0)
+    check(dense_lib().h2omx_cvt_bf16_multi(ctypes.addressof(arr), len(jobs), mr, mc, stream(jobs[0][0].device)),
+          "cvt_bf16_multi")
+
+
+def softmax_xent_bf16(Z: torch.Tensor, y: torch.Tensor, dZ: torch.Tensor, dZt: torch.Tensor,
+                      loss: torch.Tensor) -> None:
+    """Softmax cross-entropy of fp32 logits Z [M][K]: bf16 dZ [M][>=K] and dZ^T
+    [K][>=M] ((softmax - onehot) / M); mean loss added into loss[0]."""
+    M, K = Z.shape
+    if Z.is_cuda:
+        check(dense_lib().h2omx_softmax_xent_bf16(P(Z), P(y), P(dZ), dZ.stride(0), P(dZt), dZt.stride(0), P(loss), M,
+                                                  K, stream(Z.device)), "softmax_xent_bf16")
+        return
+    g, l = softmax_xent(Z, y)
+    dZ[:M, :K] = g.to(torch.bfloat16)
+    dZt[:K, :M] = g.T.to(torch.bfloat16)
+    loss += l

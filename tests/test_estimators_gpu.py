@@ -144,3 +144,17 @@ def test_isolation_forest_gpu(cuda_dev):
     c = H2OIsolationForestEstimator(ntrees=50, seed=2).train(training_frame=Frame.from_numpy(X, names=names))
     assert abs(c.training_metrics["mean_score"] - m.training_metrics["mean_score"]) < 0.2
     assert "tree" in " ".join(_native.loaded_libraries())
+
+
+def test_deeplearning_bf16_precision_gpu(cuda_dev):
+    """precision="bf16" (bf16 matrix-core GEMMs, fp32 master weights) reaches the
+    fp32 model's quality; regression and Tanh included."""
+    df = _binary_df(n=50000)
+    fr = Frame.from_pandas(df, device=cuda_dev)
+    kw = dict(hidden=[64, 64], epochs=3, seed=1)
+    a32 = H2ODeepLearningEstimator(**kw).train(y="y", training_frame=fr).training_metrics["AUC"]
+    m = H2ODeepLearningEstimator(precision="bf16", **kw).train(y="y", training_frame=fr)
+    assert m.training_metrics["AUC"] > a32 - 0.01 and m.training_metrics["AUC"] > 0.74
+    r = H2ODeepLearningEstimator(hidden=[32], epochs=3, seed=1, activation="Tanh", precision="bf16").train(
+        y="x0", training_frame=fr)
+    assert np.isfinite(r.training_metrics["MSE"]) and r.training_metrics["MSE"] < 1.0
