@@ -52,6 +52,12 @@ log = logging.getLogger("h2omx.api")
 LOG_BUFFER: list[str] = []
 
 
+
+# model categories each builder produces (GET /3/ModelBuilders "can_build")
+_CAN_BUILD = {"kmeans": ["Clustering"], "pca": ["DimReduction"], "svd": ["DimReduction"], "glrm": ["DimReduction"],
+              "aggregator": ["DimReduction"], "isolationforest": ["AnomalyDetection"],
+              "targetencoder": ["TargetEncoder"], "isotonicregression": ["Regression"], "adaboost": ["Binomial"]}
+
 class _BufferHandler(logging.Handler):
     def emit(self, record):
         LOG_BUFFER.append(self.format(record))
@@ -468,8 +474,9 @@ class H2OApi:
             params = [{"name": k, "default_value": _jsonable(v), "type": type(v).__name__, "label": k,
                        "level": "critical" if k in ("training_frame", "response_column") else "secondary"}
                       for k, v in {**cls.COMMON, **cls.DEFAULTS}.items()]
-            out[name] = {"algo": name, "algo_full_name": name, "can_build": ["Binomial", "Multinomial", "Regression"]
-                         if name != "kmeans" else ["Clustering"], "visibility": "Stable", "parameters": params}
+            can = _CAN_BUILD.get(name, ["Binomial", "Multinomial", "Regression"])
+            out[name] = {"algo": name, "algo_full_name": name, "can_build": can, "visibility": "Stable",
+                         "parameters": params}
         if algo and not out:
             raise ApiError(404, f"Unknown algo {algo}")
         return {"__meta": S.meta("ModelBuildersV3", "Iced"), "model_builders": out}

@@ -1,12 +1,18 @@
 """Model builders (H2O estimator API)."""
 from .base import Model, ModelBuilder, ModelCategory  # noqa: F401
+from .adaboost import H2OAdaBoostEstimator, H2ODecisionTreeEstimator  # noqa: F401
+from .aggregator import H2OAggregatorEstimator  # noqa: F401
 from .deeplearning import H2ODeepLearningEstimator  # noqa: F401
 from .ensemble import H2OStackedEnsembleEstimator  # noqa: F401
 from .glm import H2OGeneralizedLinearEstimator  # noqa: F401
+from .glrm import H2OGeneralizedLowRankEstimator  # noqa: F401
 from .isolation_forest import H2OIsolationForestEstimator  # noqa: F401
+from .isotonic import H2OIsotonicRegressionEstimator  # noqa: F401
 from .kmeans import H2OKMeansEstimator  # noqa: F401
 from .naive_bayes import H2ONaiveBayesEstimator  # noqa: F401
 from .pca import H2OPrincipalComponentAnalysisEstimator  # noqa: F401
+from .svd import H2OSingularValueDecompositionEstimator  # noqa: F401
+from .target_encoder import H2OTargetEncoderEstimator  # noqa: F401
 from .tree_models import (H2OGradientBoostingEstimator, H2ORandomForestEstimator,  # noqa: F401
                           H2OXGBoostEstimator)
 
@@ -21,4 +27,11 @@ ESTIMATORS = {
     "pca": H2OPrincipalComponentAnalysisEstimator,
     "naivebayes": H2ONaiveBayesEstimator,
     "isolationforest": H2OIsolationForestEstimator,
+    "targetencoder": H2OTargetEncoderEstimator,
+    "svd": H2OSingularValueDecompositionEstimator,
+    "glrm": H2OGeneralizedLowRankEstimator,
+    "isotonicregression": H2OIsotonicRegressionEstimator,
+    "aggregator": H2OAggregatorEstimator,
+    "adaboost": H2OAdaBoostEstimator,
+    "decision_tree": H2ODecisionTreeEstimator,
 }
