@@ -2,7 +2,9 @@
 from .base import Model, ModelBuilder, ModelCategory  # noqa: F401
 from .adaboost import H2OAdaBoostEstimator, H2ODecisionTreeEstimator  # noqa: F401
 from .aggregator import H2OAggregatorEstimator  # noqa: F401
+from .coxph import H2OCoxProportionalHazardsEstimator  # noqa: F401
 from .deeplearning import H2ODeepLearningEstimator  # noqa: F401
+from .extended_isolation_forest import H2OExtendedIsolationForestEstimator  # noqa: F401
 from .ensemble import H2OStackedEnsembleEstimator  # noqa: F401
 from .glm import H2OGeneralizedLinearEstimator  # noqa: F401
 from .glrm import H2OGeneralizedLowRankEstimator  # noqa: F401
@@ -11,6 +13,7 @@ from .isotonic import H2OIsotonicRegressionEstimator  # noqa: F401
 from .kmeans import H2OKMeansEstimator  # noqa: F401
 from .naive_bayes import H2ONaiveBayesEstimator  # noqa: F401
 from .pca import H2OPrincipalComponentAnalysisEstimator  # noqa: F401
+from .rulefit import H2ORuleFitEstimator  # noqa: F401
 from .svd import H2OSingularValueDecompositionEstimator  # noqa: F401
 from .target_encoder import H2OTargetEncoderEstimator  # noqa: F401
 from .tree_models import (H2OGradientBoostingEstimator, H2ORandomForestEstimator,  # noqa: F401
@@ -34,4 +37,7 @@ ESTIMATORS = {
     "aggregator": H2OAggregatorEstimator,
     "adaboost": H2OAdaBoostEstimator,
     "decision_tree": H2ODecisionTreeEstimator,
+    "extendedisolationforest": H2OExtendedIsolationForestEstimator,
+    "coxph": H2OCoxProportionalHazardsEstimator,
+    "rulefit": H2ORuleFitEstimator,
 }

@@ -74,3 +74,24 @@ def test_decision_tree_fits_xor():
     fr = Frame.from_pandas(df)
     m = H2ODecisionTreeEstimator(max_depth=4, seed=1).train(y="y", training_frame=fr)
     assert m.training_metrics["AUC"] > 0.95
+
+
+@pytest.mark.parametrize("ext", [0, 2])
+def test_extended_isolation_forest_ranks_outliers(ext):
+    from sklearn.metrics import roc_auc_score
+
+    from h2omx.models.extended_isolation_forest import H2OExtendedIsolationForestEstimator
+
+    rng = np.random.default_rng(4)
+    inl = rng.normal(size=(3000, 3))
+    out = rng.uniform(-6, 6, size=(60, 3))
+    out = out[np.linalg.norm(out, axis=1) > 4]
+    X = np.concatenate([inl, out])
+    lab = np.r_[np.zeros(len(inl)), np.ones(len(out))]
+    fr = Frame.from_pandas(pd.DataFrame(X, columns=list("abc")))
+    m = H2OExtendedIsolationForestEstimator(ntrees=50, sample_size=256, extension_level=ext, seed=3).train(
+        training_frame=fr)
+    pr = m.predict(fr).to_pandas()
+    assert roc_auc_score(lab, pr["anomaly_score"]) > 0.95
+    assert ((pr["anomaly_score"] > 0) & (pr["anomaly_score"] < 1)).all()
+    assert pr["mean_length"].max() <= 8 + 10
