@@ -56,7 +56,7 @@ LOG_BUFFER: list[str] = []
 # model categories each builder produces (GET /3/ModelBuilders "can_build")
 _CAN_BUILD = {"kmeans": ["Clustering"], "pca": ["DimReduction"], "svd": ["DimReduction"], "glrm": ["DimReduction"],
               "aggregator": ["DimReduction"], "isolationforest": ["AnomalyDetection"],
-              "extendedisolationforest": ["AnomalyDetection"], "coxph": ["CoxPH"], "rulefit": ["Binomial", "Regression"],
+              "extendedisolationforest": ["AnomalyDetection"], "coxph": ["CoxPH"], "rulefit": ["Binomial", "Regression"], "word2vec": ["WordEmbedding"],
               "targetencoder": ["TargetEncoder"], "isotonicregression": ["Regression"], "adaboost": ["Binomial"]}
 
 class _BufferHandler(logging.Handler):

@@ -16,6 +16,7 @@ from .pca import H2OPrincipalComponentAnalysisEstimator  # noqa: F401
 from .rulefit import H2ORuleFitEstimator  # noqa: F401
 from .svd import H2OSingularValueDecompositionEstimator  # noqa: F401
 from .target_encoder import H2OTargetEncoderEstimator  # noqa: F401
+from .word2vec import H2OWord2vecEstimator  # noqa: F401
 from .tree_models import (H2OGradientBoostingEstimator, H2ORandomForestEstimator,  # noqa: F401
                           H2OXGBoostEstimator)
 
@@ -40,4 +41,5 @@ ESTIMATORS = {
     "extendedisolationforest": H2OExtendedIsolationForestEstimator,
     "coxph": H2OCoxProportionalHazardsEstimator,
     "rulefit": H2ORuleFitEstimator,
+    "word2vec": H2OWord2vecEstimator,
 }
