@@ -7,11 +7,13 @@ from .deeplearning import H2ODeepLearningEstimator  # noqa: F401
 from .extended_isolation_forest import H2OExtendedIsolationForestEstimator  # noqa: F401
 from .ensemble import H2OStackedEnsembleEstimator  # noqa: F401
 from .glm import H2OGeneralizedLinearEstimator  # noqa: F401
+from .gam import H2OGeneralizedAdditiveEstimator  # noqa: F401
 from .glrm import H2OGeneralizedLowRankEstimator  # noqa: F401
 from .isolation_forest import H2OIsolationForestEstimator  # noqa: F401
 from .isotonic import H2OIsotonicRegressionEstimator  # noqa: F401
 from .kmeans import H2OKMeansEstimator  # noqa: F401
 from .naive_bayes import H2ONaiveBayesEstimator  # noqa: F401
+from .model_selection import H2OANOVAGLMEstimator, H2OModelSelectionEstimator  # noqa: F401
 from .pca import H2OPrincipalComponentAnalysisEstimator  # noqa: F401
 from .rulefit import H2ORuleFitEstimator  # noqa: F401
 from .svd import H2OSingularValueDecompositionEstimator  # noqa: F401
@@ -42,4 +44,7 @@ ESTIMATORS = {
     "coxph": H2OCoxProportionalHazardsEstimator,
     "rulefit": H2ORuleFitEstimator,
     "word2vec": H2OWord2vecEstimator,
+    "gam": H2OGeneralizedAdditiveEstimator,
+    "modelselection": H2OModelSelectionEstimator,
+    "anovaglm": H2OANOVAGLMEstimator,
 }

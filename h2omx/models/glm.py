@@ -97,10 +97,15 @@ def _soft(x, t):
 
 
 def solve_enet(G: np.ndarray, p: int, N: float, lam: float, alpha: float, beta0: np.ndarray, intercept: bool,
-               non_negative: bool = False, max_iter: int = 500, tol: float = 1e-9):
-    """Minimise (1/2N) sum w (z - x.b)^2 + lam (alpha |b|_1 + (1-alpha)/2 |b|^2) given the
-    augmented Gram G of [x | 1 | z].  Returns beta (p coefficients + intercept)."""
+               non_negative: bool = False, max_iter: int = 500, tol: float = 1e-9, penalty: np.ndarray | None = None):
+    """Minimise (1/2N) sum w (z - x.b)^2 + lam (alpha |b|_1 + (1-alpha)/2 |b|^2)
+    (+ 1/2 bᵀ P b for a quadratic ``penalty`` P on the p coefficients, GAM
+    smoothness) given the augmented Gram G of [x | 1 | z].  Returns beta (p
+    coefficients + intercept)."""
     XtX = G[: p + 1, : p + 1] / N
+    if penalty is not None:
+        XtX = XtX.copy()
+        XtX[:p, :p] += penalty
     Xtz = G[: p + 1, p + 1] / N
     l1 = lam * alpha
     l2 = lam * (1 - alpha)
@@ -255,6 +260,11 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
                 self.category, "gaussian")
         return fam
 
+    def _penalty_matrix(self, design):
+        """Quadratic coefficient penalty (raw scale, p×p) added to the IRLS normal
+        equations; None for plain GLM (overridden by GAM)."""
+        return None
+
     def _fit(self, train: Frame, valid, model_id):
         p_ = self.params
         family = self._family()
@@ -278,6 +288,10 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
         del Xraw
         p = X.shape[0]
         K = len(self.response_domain) if family == "multinomial" else 1
+        # optional quadratic penalty on the raw-scale coefficients (GAM), moved to the
+        # standardised scale: b_raw = b_std / sd  ->  P_std = D⁻¹ P D⁻¹
+        pen_raw = self._penalty_matrix(design)
+        pen_std = None if pen_raw is None else pen_raw / np.outer(design.sds, design.sds)
         alpha = p_["alpha"]
         alpha = (0.0 if p_["solver"] == "L_BFGS" else 0.5) if alpha is None else float(alpha[0] if isinstance(alpha, (list, tuple)) else alpha)
         lam_param = p_["lambda_"] if p_["lambda_"] is not None else p_["Lambda"]
@@ -338,7 +352,8 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
                 old = beta.copy()
                 for k in range(K):
                     G, dev = allreduce(*D.glm_irls_pass(X, y, w, off, beta, family, link, k, var_power, link_power))
-                    beta[k] = solve_enet(G, p, N, lam, alpha, beta[k], intercept, bool(p_["non_negative"]))
+                    beta[k] = solve_enet(G, p, N, lam, alpha, beta[k], intercept, bool(p_["non_negative"]),
+                                         penalty=pen_std)
                 history.append({"iteration": iters_total, "lambda": lam, "deviance": dev})
                 if np.abs(beta - old).max() < beps:
                     break
