@@ -1,0 +1,67 @@
+"""Worker for tests/test_algos_multirank.py: one rank of a gloo world holding
+a row shard; trains the newer estimators and writes their key outputs (JSON)."""
+import json
+import os
+import sys
+
+import numpy as np
+import pandas as pd
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from h2omx.frame import Frame  # noqa: E402
+from h2omx.frame.distributed import unify_domains  # noqa: E402
+from h2omx.models import (H2OANOVAGLMEstimator, H2OCoxProportionalHazardsEstimator,  # noqa: E402
+                          H2OGeneralizedAdditiveEstimator, H2OGeneralizedLowRankEstimator,
+                          H2OIsotonicRegressionEstimator, H2OModelSelectionEstimator,
+                          H2OSingularValueDecompositionEstimator, H2OTargetEncoderEstimator)
+from h2omx.parallel.comm import Comm  # noqa: E402
+
+
+def data(n=1200):
+    rng = np.random.default_rng(11)
+    X = rng.normal(size=(n, 4))
+    df = pd.DataFrame(X, columns=["a", "b", "c", "d"])
+    df["g"] = pd.Categorical(rng.choice(list("pqrs"), n))
+    df["y"] = np.sin(X[:, 0]) + X[:, 1] - 0.5 * X[:, 2] + rng.normal(scale=0.3, size=n)
+    df["t"] = np.ceil(rng.exponential(np.exp(-0.5 * X[:, 0])) * 10) / 10
+    df["ev"] = (rng.random(n) < 0.7).astype(float)
+    return df
+
+
+def main():
+    out_path = sys.argv[1]
+    comm = Comm.from_env(device="cpu")
+    c = comm if comm.world_size > 1 else None
+    df = data()
+    n = len(df)
+    lo, hi = n * comm.rank // comm.world_size, n * (comm.rank + 1) // comm.world_size
+    fr = unify_domains(Frame.from_pandas(df.iloc[lo:hi].reset_index(drop=True)), c)
+    res = {}
+    te = H2OTargetEncoderEstimator(noise=0.0, blending=True).train(x=["g"], y="y", training_frame=fr, comm=c)
+    res["te"] = te.transform(fr).to_pandas()["g_te"].tolist()
+    svd = H2OSingularValueDecompositionEstimator(nv=3).train(x=["a", "b", "c", "d"], training_frame=fr, comm=c)
+    res["svd_d"] = svd.d.tolist()
+    gl = H2OGeneralizedLowRankEstimator(k=2, init="SVD", max_iterations=30, min_step_size=0.0).train(
+        x=["a", "b", "c", "d"], training_frame=fr, comm=c)
+    res["glrm_obj"] = gl.objective
+    iso = H2OIsotonicRegressionEstimator().train(x=["a"], y="y", training_frame=fr, comm=c)
+    res["iso"] = [iso.thresholds_x.tolist(), iso.thresholds_y.tolist()]
+    cox = H2OCoxProportionalHazardsEstimator(stop_column="t").train(x=["a", "b"], y="ev", training_frame=fr, comm=c)
+    res["cox"] = cox.beta.tolist()
+    ms = H2OModelSelectionEstimator(mode="maxr", max_predictor_number=2).train(
+        x=["a", "b", "c", "d"], y="y", training_frame=fr, comm=c)
+    res["ms"] = [[r["predictors"], r["best_r2_value"]] for r in ms.result()]
+    gam = H2OGeneralizedAdditiveEstimator(family="gaussian", gam_columns=["a"], num_knots=[6], lambda_=0.0).train(
+        x=["a", "b", "c"], y="y", training_frame=fr, comm=c)
+    res["gam"] = gam.coef()
+    an = H2OANOVAGLMEstimator(family="gaussian", highest_interaction_term=1).train(
+        x=["a", "b", "d"], y="y", training_frame=fr, comm=c)
+    res["anova"] = [r["deviance_difference"] for r in an.result()]
+    with open(out_path, "w") as f:
+        json.dump(res, f)
+    comm.barrier()
+
+
+if __name__ == "__main__":
+    main()

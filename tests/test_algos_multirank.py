@@ -1,0 +1,56 @@
+"""The newer estimators give the same model on 2 gloo ranks (row shards) as on
+one rank: every statistic is combined with collectives."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(world, tmp_path):
+    port = _port()
+    procs, outs = [], []
+    for r in range(world):
+        out = tmp_path / f"alg{world}_{r}.json"
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_algos_worker.py"), str(out)], env=env))
+        outs.append(out)
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    return [json.load(open(o)) for o in outs]
+
+
+@pytest.fixture(scope="module")
+def results(tmp_path_factory):
+    t = tmp_path_factory.mktemp("algos")
+    return _run(1, t)[0], _run(2, t)
+
+
+def test_two_ranks_match_one_rank(results):
+    one, two = results
+    np.testing.assert_allclose(two[0]["te"] + two[1]["te"], one["te"], rtol=1e-6)
+    for r in two:
+        np.testing.assert_allclose(r["svd_d"], one["svd_d"], rtol=1e-5)
+        np.testing.assert_allclose(r["glrm_obj"], one["glrm_obj"], rtol=1e-4)
+        np.testing.assert_allclose(r["iso"][0], one["iso"][0])
+        np.testing.assert_allclose(r["iso"][1], one["iso"][1], rtol=1e-9)
+        np.testing.assert_allclose(r["cox"], one["cox"], rtol=1e-7)
+        assert [m[0] for m in r["ms"]] == [m[0] for m in one["ms"]]
+        np.testing.assert_allclose([m[1] for m in r["ms"]], [m[1] for m in one["ms"]], rtol=1e-6)
+        for k, v in one["gam"].items():
+            assert abs(r["gam"][k] - v) < 1e-3 * max(1.0, abs(v)), k
+        np.testing.assert_allclose(r["anova"], one["anova"], rtol=1e-4)
