@@ -261,7 +261,7 @@ class H2OGeneralizedLowRankEstimator(ModelBuilder):
             order = np.argsort(w)[::-1][:k]
             nrows = float(n) * world
             Y = (V[:, order] * np.sqrt(np.maximum(w[order], 0) / max(nrows, 1.0))).T
-            return torch.from_numpy(Y.astype(np.float32))
+            return torch.from_numpy(np.ascontiguousarray(Y, dtype=np.float32))
         if init == "random":
             return torch.randn((k, p), generator=g)
         if init in ("plusplus", "user"):

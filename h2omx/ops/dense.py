@@ -242,7 +242,14 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
     K = A.shape[0] if ta else A.shape[1]
     N = B.shape[0] if tb else B.shape[1]
     if A.is_cuda:
+        # the kernel indexes dense row-major operands: copy strided views (no-op otherwise)
+        A = A.float().contiguous()
+        B = B.float().contiguous()
+        if bias is not None:
+            bias = bias.float().contiguous()
         C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=A.device)
+        if not C.is_contiguous():
+            raise ValueError("gemm: out must be contiguous")
         # split-K when the output has too few 128x128 tiles to fill 256 CUs
         # (weight gradients: [out][in] outputs with K = batch rows)
         tiles = -(-M // 128) * -(-N // 128)
