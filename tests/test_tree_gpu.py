@@ -281,3 +281,20 @@ def test_fused_split_level_matches(cuda_dev, monkeypatch, dist, depth, sample_ra
         assert reach == b.compact()[t]
         for f in ("feat", "bin", "value", "weight", "gain"):
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
+
+
+@pytest.mark.parametrize("nbins", [20, 255])
+def test_device_edges_match_host_edges(cuda_dev, nbins):
+    """compute_edges on the device == the NumPy sketch on the same sample."""
+    rng = np.random.default_rng(5)
+    n = 300_000
+    X = np.stack([rng.normal(size=n), rng.integers(0, 7, n).astype(float), rng.exponential(size=n),
+                  np.round(rng.normal(size=n), 1), np.full(n, 3.0)]).astype(np.float32)
+    X[0, rng.random(n) < 0.2] = np.nan
+    X[2, :] = np.nan
+    Xt = torch.from_numpy(X)
+    eh, nh, bh = compute_edges(Xt, nbins, sample_rows=100_000, seed=3)
+    ed, nd, bd = compute_edges(Xt.to(cuda_dev), nbins, sample_rows=100_000, seed=3)
+    assert bh == bd
+    np.testing.assert_array_equal(nh, nd)
+    np.testing.assert_array_equal(eh, ed)
