@@ -715,45 +715,10 @@ __device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__
   const int lane = threadIdx.x & 63;
   const int64_t per = (int64_t)F * 2 * NBT;
   const int64_t off = ((int64_t)f * 2) * NBT;
-  long long gi[B], si[B];
-#pragma unroll
-  for (int k = 0; k < B; ++k) {
-    const int bin = lane * B + k;
-    gi[k] = 0; si[k] = 0;
-    if (bin < NBT) {
-      if (lk.slot >= 0) {
-        const long long* bp = built + lk.slot * per + off + bin;
-        gi[k] = bp[0]; si[k] = bp[NBT];
-      } else {
-        const long long* pp = parent_full + lk.parent * per + off + bin;
-        const long long* sp = built + lk.sib_slot * per + off + bin;
-        gi[k] = pp[0] - sp[0]; si[k] = pp[NBT] - sp[NBT];
-      }
-      if (full) {
-        long long* fp = full + node * per + off + bin;
-        fp[0] = gi[k]; fp[NBT] = si[k];
-      }
-    }
-  }
-  // NA bin (NBT - 1) excluded from the running sums
-  constexpr int NA_LANE = (NBT - 1) / B, NA_K = (NBT - 1) % B;
-  const long long ng_i = __shfl(gi[NA_K], NA_LANE, kWave), ns_i = __shfl(si[NA_K], NA_LANE, kWave);
-  if (lane == NA_LANE) { gi[NA_K] = 0; si[NA_K] = 0; }
-  long long lg = 0, ls = 0;  // inclusive local prefix
-  long long pg[B], ps[B];
-#pragma unroll
-  for (int k = 0; k < B; ++k) { lg += gi[k]; ls += si[k]; pg[k] = lg; ps[k] = ls; }
-  long long xg = lg, xs = ls;  // wave inclusive scan of lane totals
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const long long ag = __shfl_up(xg, o, kWave), as = __shfl_up(xs, o, kWave);
-    if (lane >= o) { xg += ag; xs += as; }
-  }
-  const long long tg_i = __shfl(xg, 63, kWave) + ng_i, ts_i = __shfl(xs, 63, kWave) + ns_i;
-  const long long eg = xg - lg, es = xs - ls;  // exclusive lane offset
-  const double ng = (double)ng_i * ig, ns = (double)ns_i * is;
-  const double tg = (double)tg_i * ig, ts = (double)ts_i * is;
-
+  // feature eligibility first (wave-uniform): a feature outside the node's
+  // mtries / column sample only needs its histogram row completed for the
+  // next level and the node totals - no prefix scan, no gains (DRF looks at
+  // sqrt(F) of F features, so this skips most of the per-node work)
   bool allowed = (tree_fmask == nullptr) || tree_fmask[f];
   if (allowed && (p.mtries > 0 || p.col_rate < 1.0f)) {
     const uint32_t key = (uint32_t)p.tree_index * 131u + (uint32_t)p.depth;
@@ -774,6 +739,59 @@ __device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__
       allowed = u01(hf) < p.col_rate;
     }
   }
+  long long gi[B], si[B];
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const int bin = lane * B + k;
+    gi[k] = 0; si[k] = 0;
+    if (bin < NBT) {
+      if (lk.slot >= 0) {
+        const long long* bp = built + lk.slot * per + off + bin;
+        gi[k] = bp[0]; si[k] = bp[NBT];
+      } else {
+        const long long* pp = parent_full + lk.parent * per + off + bin;
+        const long long* sp = built + lk.sib_slot * per + off + bin;
+        gi[k] = pp[0] - sp[0]; si[k] = pp[NBT] - sp[NBT];
+      }
+      if (full) {
+        long long* fp = full + node * per + off + bin;
+        fp[0] = gi[k]; fp[NBT] = si[k];
+      }
+    }
+  }
+  if (!allowed) {
+    long long tg_i = 0, ts_i = 0;
+#pragma unroll
+    for (int k = 0; k < B; ++k) { tg_i += gi[k]; ts_i += si[k]; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      tg_i += __shfl_xor(tg_i, o, kWave);
+      ts_i += __shfl_xor(ts_i, o, kWave);
+    }
+    WaveBest r;
+    r.G = (double)tg_i * ig; r.S = (double)ts_i * is;
+    r.gain = -INFINITY; r.code = 0x7fffffff; r.GL = r.SL = 0.0;
+    return r;
+  }
+  // NA bin (NBT - 1) excluded from the running sums
+  constexpr int NA_LANE = (NBT - 1) / B, NA_K = (NBT - 1) % B;
+  const long long ng_i = __shfl(gi[NA_K], NA_LANE, kWave), ns_i = __shfl(si[NA_K], NA_LANE, kWave);
+  if (lane == NA_LANE) { gi[NA_K] = 0; si[NA_K] = 0; }
+  long long lg = 0, ls = 0;  // inclusive local prefix
+  long long pg[B], ps[B];
+#pragma unroll
+  for (int k = 0; k < B; ++k) { lg += gi[k]; ls += si[k]; pg[k] = lg; ps[k] = ls; }
+  long long xg = lg, xs = ls;  // wave inclusive scan of lane totals
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long ag = __shfl_up(xg, o, kWave), as = __shfl_up(xs, o, kWave);
+    if (lane >= o) { xg += ag; xs += as; }
+  }
+  const long long tg_i = __shfl(xg, 63, kWave) + ng_i, ts_i = __shfl(xs, 63, kWave) + ns_i;
+  const long long eg = xg - lg, es = xs - ls;  // exclusive lane offset
+  const double ng = (double)ng_i * ig, ns = (double)ns_i * is;
+  const double tg = (double)tg_i * ig, ts = (double)ts_i * is;
+
   double best_gain = -INFINITY;
   int best_code = 0x7fffffff;
   double bGL = 0, bSL = 0;
