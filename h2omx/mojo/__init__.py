@@ -19,6 +19,13 @@ following H2O-3's genmodel layout:
   ``standardize``/``center_mean``/``center_mult``.
 * deeplearning: ``neural_network_sizes``, ``activation``, ``norm_sub``,
   ``norm_mul``, ``norm_resp_*`` and ``weight_layer<i>``/``bias_layer<i>``.
+* pca, glrm, isotonicregression, coxph, targetencoder, word2vec,
+  extendedisolationforest, gam: scalar settings in ``model.ini`` and every
+  array (eigenvectors, archetypes, thresholds, coefficients, per-level
+  target sums, word vectors, hyperplanes, spline knots / bases, design
+  means / scales) as little-endian fp64 ``h2omx/<name>.bin`` with its shape
+  in ``h2omx_shape_<name>`` (h2omx's own payload layout; the genmodel
+  readers for these algorithms use other entry names).
 
 Binary compatibility with H2O's h2o-genmodel.jar cannot be checked here (no
 JVM or jar in the environment): the layout follows the public format as
@@ -43,7 +50,12 @@ from ..frame.frame import ENUM, Frame
 from ..models.base import Model, ModelCategory
 
 MOJO_VERSIONS = {"gbm": "1.40", "drf": "1.40", "xgboost": "1.00", "glm": "1.00", "kmeans": "1.00",
-                 "deeplearning": "1.10", "stackedensemble": "1.01"}
+                 "deeplearning": "1.10", "stackedensemble": "1.01", "pca": "1.00", "glrm": "1.10",
+                 "isotonicregression": "1.00", "coxph": "1.00", "targetencoder": "1.00", "word2vec": "1.00",
+                 "extendedisolationforest": "1.00", "gam": "1.00"}
+# algorithms whose payload is the h2omx array layout below (design + named arrays)
+ARRAY_ALGOS = ("pca", "glrm", "isotonicregression", "coxph", "targetencoder", "word2vec",
+               "extendedisolationforest", "gam")
 NSD_NA_LEFT, NSD_NA_RIGHT = 2, 3
 
 
@@ -153,7 +165,8 @@ def _fmt(v):
 
 def _category_name(cat):
     return {ModelCategory.BINOMIAL: "Binomial", ModelCategory.MULTINOMIAL: "Multinomial",
-            ModelCategory.REGRESSION: "Regression", ModelCategory.CLUSTERING: "Clustering"}.get(cat, str(cat))
+            ModelCategory.REGRESSION: "Regression", ModelCategory.CLUSTERING: "Clustering",
+            ModelCategory.DIMREDUCTION: "DimReduction", ModelCategory.ANOMALY: "AnomalyDetection"}.get(cat, str(cat))
 
 
 def _design_columns(design):
@@ -188,15 +201,22 @@ def mojo_bytes(model: Model) -> bytes:
     elif algo == "isolationforest":
         columns = list(model.x)
         info.update(_if_info(model, files))
+    elif algo in ARRAY_ALGOS:
+        columns = list(model.x)
+        if algo == "gam":
+            basis = {f"{c}_cr_{i}" for c, sp in model.gam_spec.items() for i in range(sp["Z"].shape[1])}
+            columns = [c for c in model.x if c not in basis] + [c for c in model.gam_spec if c not in model.x]
+        info.update(_array_info(model, files))
     elif algo == "generic":
         return model.raw_mojo
     else:
         raise NotImplementedError(f"MOJO export for {algo}")
-    if model.y is not None and algo != "kmeans" and not getattr(model, "autoencoder", False):
+    if model.y is not None and algo not in ("kmeans", "coxph") and not getattr(model, "autoencoder", False):
         columns = columns + [model.y]
     domains = []
     for j, c in enumerate(columns):
-        dom = model.response_domain if c == model.y else model.feature_domains.get(c)
+        dom = model.response_domain if c == model.y else (model.feature_domains.get(c) or (
+            model.gam_frame_domains.get(c) if hasattr(model, "gam_frame_domains") else None))
         if dom:
             domains.append((j, dom))
     nclass = len(model.response_domain) if model.response_domain else 1
@@ -211,6 +231,9 @@ def mojo_bytes(model: Model) -> bytes:
         "prior_class_distrib": "null", "model_class_distrib": "null", "timestamp": time.strftime("%Y-%m-%dT%H:%M:%S"),
         "h2omx_model_id": model.model_id, "response_column": model.y or "",
     }
+    if algo == "coxph":
+        head["supervised"] = False
+        head["category"] = "CoxPH"
     lines = ["[info]"] + [f"{k} = {_fmt(v)}" for k, v in {**head, **info}.items()]
     lines += ["", "[columns]"] + columns + ["", "[domains]"]
     for i, (j, dom) in enumerate(domains):
@@ -333,6 +356,89 @@ def _se_info(model, files):
     return out
 
 
+# ---------------------------------------------------------------------------
+# array payload (PCA, GLRM, isotonic, CoxPH, TargetEncoder, Word2Vec, EIF, GAM)
+# ---------------------------------------------------------------------------
+def _put(files, info, name, arr):
+    a = np.ascontiguousarray(np.asarray(arr, dtype="<f8"))
+    files[f"h2omx/{name}.bin"] = a.tobytes()
+    info[f"h2omx_shape_{name}"] = list(a.shape) if a.ndim else [1]
+
+
+def _get(z, info, name):
+    shape = info[f"h2omx_shape_{name}"]
+    shape = shape if isinstance(shape, list) else [shape]
+    return np.frombuffer(z.read(f"h2omx/{name}.bin"), dtype="<f8").reshape(shape).copy()
+
+
+def _design_info(design, info, files, tag="design"):
+    info[f"h2omx_{tag}_use_all"] = bool(design.use_all_levels)
+    info[f"h2omx_{tag}_x"] = list(design.x)
+    _put(files, info, f"{tag}_means", design.means)
+    _put(files, info, f"{tag}_sds", design.sds if design.sds is not None else np.ones(len(design.names)))
+    _put(files, info, f"{tag}_center", getattr(design, "center", np.zeros(len(design.names))))
+
+
+def _array_info(model, files):
+    info: dict = {}
+    a = model.algo
+    if a in ("pca", "glrm", "coxph", "extendedisolationforest"):
+        _design_info(model.design, info, files)
+    if a == "pca":
+        _put(files, info, "center", model.center)
+        _put(files, info, "scale", model.scale)
+        _put(files, info, "eigenvectors", model.eigenvectors)
+        info["k"] = int(model.eigenvectors.shape[1])
+    elif a == "glrm":
+        _put(files, info, "center", model.center)
+        _put(files, info, "scale", model.scale)
+        _put(files, info, "archetypes", model.Y)
+        info.update(ncolX=int(model.Y.shape[0]), regularization_x=str(model.params["regularization_x"]),
+                    gamma_x=float(model.params["gamma_x"]), h2omx_recon_names=list(model.design.names))
+    elif a == "isotonicregression":
+        _put(files, info, "thresholds_x", model.thresholds_x)
+        _put(files, info, "thresholds_y", model.thresholds_y)
+        info["out_of_bounds"] = str(model.params["out_of_bounds"])
+    elif a == "coxph":
+        _put(files, info, "coef", model.beta)
+        _put(files, info, "x_mean_num", model.x_mean)
+    elif a == "targetencoder":
+        info["te_columns"] = list(model.columns)
+        info["blending"] = bool(model.params["blending"])
+        info["inflection_point"] = float(model.params["inflection_point"])
+        info["smoothing"] = float(model.params["smoothing"])
+        info["keep_original_categorical_columns"] = bool(model.params["keep_original_categorical_columns"])
+        info["h2omx_classes"] = list(model.classes) if model.classes is not None else "null"
+        _put(files, info, "prior", model.prior.numpy())
+        for i, c in enumerate(model.columns):
+            sums, cnts, _ = model.stats[c]
+            _put(files, info, f"te_sums_{i}", sums.numpy())
+            _put(files, info, f"te_counts_{i}", cnts.numpy())
+    elif a == "word2vec":
+        files["h2omx/vocabulary.txt"] = ("\n".join(model.words) + "\n").encode()
+        _put(files, info, "vectors", model.vectors.float().cpu().numpy())
+        info["vec_size"] = int(model.vectors.shape[1])
+        info["vocab_size"] = len(model.words)
+    elif a == "extendedisolationforest":
+        _put(files, info, "normals", model.normals)
+        _put(files, info, "offsets", model.offs)
+        _put(files, info, "leaf_sizes", model.sizes)
+        info.update(limit=int(model.limit), sample_size=int(model.sample_size), ntrees=int(model.normals.shape[0]),
+                    extension_level=int(model.params["extension_level"]))
+    elif a == "gam":
+        _design_info(model.design, info, files)
+        _put(files, info, "beta", model.beta_std)      # standardised scale (design.transform)
+        info.update(family=model.family, link=model.link, gam_columns=list(model.gam_spec),
+                    h2omx_glm_x=list(model.x),
+                    tweedie_link_power=float(model.params.get("tweedie_link_power", 0.0) or 0.0))
+        for i, (c, sp) in enumerate(model.gam_spec.items()):
+            _put(files, info, f"gam_knots_{i}", sp["knots"])
+            _put(files, info, f"gam_F_{i}", sp["F"])
+            _put(files, info, f"gam_Z_{i}", sp["Z"])
+            info[f"gam_mean_{i}"] = float(sp["mean"])
+    return info
+
+
 def export_mojo(model: Model, path: str) -> str:
     import os
 
@@ -431,6 +537,192 @@ class GenericModel(Model):
             self.base = [GenericModel(z.read(f"models/{info[f'base_model{i}']}.zip"))
                          for i in range(int(info["base_models_num"]))]
             self.meta = GenericModel(z.read(f"models/{info['metalearner']}.zip"))
+        elif self.mojo_algo in ARRAY_ALGOS:
+            self._load_arrays(z, info)
+        if self.mojo_algo == "coxph":
+            self.category = ModelCategory.REGRESSION
+
+    def _design(self, z, info, tag="design"):
+        from ..models.glm import DesignInfo
+
+        x = info[f"h2omx_{tag}_x"]
+        x = x if isinstance(x, list) else [x]
+        d = DesignInfo(x, self.feature_types, self.feature_domains, bool(info[f"h2omx_{tag}_use_all"]))
+        d.means = _get(z, info, f"{tag}_means")
+        d.sds = _get(z, info, f"{tag}_sds")
+        d.center = _get(z, info, f"{tag}_center")
+        return d
+
+    def _load_arrays(self, z, info):
+        a = self.mojo_algo
+        self.arr = {}
+        if a in ("pca", "glrm", "coxph", "extendedisolationforest"):
+            self.design = self._design(z, info)
+        names = {"pca": ("center", "scale", "eigenvectors"), "glrm": ("center", "scale", "archetypes"),
+                 "isotonicregression": ("thresholds_x", "thresholds_y"), "coxph": ("coef", "x_mean_num"),
+                 "extendedisolationforest": ("normals", "offsets", "leaf_sizes"), "gam": ("beta",)}.get(a, ())
+        for nm in names:
+            self.arr[nm] = _get(z, info, nm)
+        if a == "targetencoder":
+            cols = info["te_columns"]
+            self.te_columns = cols if isinstance(cols, list) else [cols]
+            self.arr["prior"] = _get(z, info, "prior")
+            for i in range(len(self.te_columns)):
+                self.arr[f"te_sums_{i}"] = _get(z, info, f"te_sums_{i}")
+                self.arr[f"te_counts_{i}"] = _get(z, info, f"te_counts_{i}")
+        if a == "word2vec":
+            self.words = z.read("h2omx/vocabulary.txt").decode().split("\n")[: int(info["vocab_size"])]
+            self.vectors = torch.from_numpy(_get(z, info, "vectors").astype(np.float32))
+        if a == "gam":
+            dx = info["h2omx_design_x"]
+            for n in (dx if isinstance(dx, list) else [dx]):
+                self.feature_types.setdefault(n, "real")
+                self.feature_domains.setdefault(n, None)
+            self.design = self._design(z, info)
+            gcols = info["gam_columns"]
+            gcols = gcols if isinstance(gcols, list) else [gcols]
+            self.gam_spec = {c: {"knots": _get(z, info, f"gam_knots_{i}"), "F": _get(z, info, f"gam_F_{i}"),
+                                 "Z": _get(z, info, f"gam_Z_{i}"), "mean": info[f"gam_mean_{i}"]}
+                             for i, c in enumerate(gcols)}
+            for c in gcols:       # raw gam columns are numeric
+                self.feature_types[c] = "real"
+
+    # -- h2omx array payload scoring -------------------------------------------
+    def _score_arrays(self, frame: Frame) -> torch.Tensor:
+        a = self.mojo_algo
+        info = self.info
+        frame = self.adapt_frame(frame)
+        dev = frame.device
+        if a in ("pca", "glrm"):
+            Xraw = self.design.raw_matrix(frame)
+            c = torch.from_numpy(self.arr["center"]).to(dev, torch.float32)[:, None]
+            s_ = torch.from_numpy(self.arr["scale"]).to(dev, torch.float32)[:, None]
+            if a == "pca":
+                m = torch.from_numpy(self.design.means).to(dev, torch.float32)[:, None]
+                X = (torch.where(torch.isnan(Xraw), m.expand_as(Xraw), Xraw) - c) / s_
+                V = torch.from_numpy(self.arr["eigenvectors"]).to(dev, torch.float32)
+                return V.T @ X
+            from ..models.glrm import _solve_x
+
+            A = (Xraw - c) / s_
+            mask = ~torch.isnan(A)
+            A = torch.where(mask, A, torch.zeros_like(A))
+            Y = torch.from_numpy(self.arr["archetypes"]).to(dev, torch.float32)
+            Xk = _solve_x(A.contiguous(), mask, Y, {"regularization_x": info["regularization_x"],
+                                                    "gamma_x": info["gamma_x"]})
+            return (Y.T @ Xk) * s_ + c
+        if a == "isotonicregression":
+            x = frame.vec(self.x[0]).as_float().double()
+            tx = torch.from_numpy(self.arr["thresholds_x"]).to(dev)
+            ty = torch.from_numpy(self.arr["thresholds_y"]).to(dev)
+            if tx.numel() == 1:
+                out = ty[0].expand_as(x).clone()
+            else:
+                i = torch.searchsorted(tx, x).clamp(1, tx.numel() - 1)
+                t = ((x - tx[i - 1]) / (tx[i] - tx[i - 1]).clamp_min(1e-300)).clamp(0, 1)
+                out = ty[i - 1] + t * (ty[i] - ty[i - 1])
+            if str(info["out_of_bounds"]).lower() == "clip":
+                out = torch.where(x < tx[0], ty[0], torch.where(x > tx[-1], ty[-1], out))
+            else:
+                out = torch.where((x < tx[0]) | (x > tx[-1]), torch.full_like(out, float("nan")), out)
+            return torch.where(torch.isnan(x), torch.full_like(out, float("nan")), out).float()[None, :]
+        if a == "coxph":
+            X = self.design.raw_matrix(frame).double()
+            mu = torch.from_numpy(self.arr["x_mean_num"]).to(dev)[:, None]
+            X = torch.where(torch.isnan(X), mu.expand_as(X), X)
+            b = torch.from_numpy(self.arr["coef"]).to(dev)
+            return ((X - mu) * b[:, None]).sum(0).float()[None, :]
+        if a == "extendedisolationforest":
+            from ..models.extended_isolation_forest import ExtendedIsolationForestModel
+            from ..models.isolation_forest import avg_path
+
+            m = ExtendedIsolationForestModel.__new__(ExtendedIsolationForestModel)
+            m.design, m.limit = self.design, int(info["limit"])
+            m.normals = self.arr["normals"].astype(np.float32)
+            m.offs = self.arr["offsets"].astype(np.float32)
+            m.sizes = self.arr["leaf_sizes"].astype(np.float32)
+            ml = m.mean_length(frame)
+            cst = float(avg_path(np.array([int(info["sample_size"])]))[0]) or 1.0
+            return torch.stack([torch.pow(2.0, -ml / cst), ml])
+        if a == "targetencoder":
+            return self._te(frame)
+        if a == "gam":
+            from ..models.gam import _augment
+
+            aug = _augment(frame, self.gam_spec)
+            Xs = self.design.transform(self.design.raw_matrix(aug)).double()
+            beta = torch.from_numpy(self.arr["beta"]).to(dev)
+            beta = beta.view(-1, Xs.shape[0] + 1)
+            eta = beta[:, :-1] @ Xs + beta[:, -1:]
+            from ..models.glm import _torch_linkinv
+
+            mu = _torch_linkinv(eta[0], info["link"], info.get("tweedie_link_power", 0.0))
+            if self.category == ModelCategory.BINOMIAL:
+                return torch.stack([1 - mu, mu]).float()
+            return mu[None, :].float()
+        raise NotImplementedError(a)
+
+    def predict(self, frame: Frame) -> Frame:
+        from ..frame.frame import Vec
+
+        a = self.mojo_algo
+        if a == "targetencoder":
+            P = self._te(self.adapt_frame(frame))
+            cls = self.info.get("h2omx_classes")
+            names = [f"{c}_te" if not isinstance(cls, list) else f"{c}_{k}_te"
+                     for c in self.te_columns for k in (cls if isinstance(cls, list) else [None])]
+            return Frame([Vec(n, P[i], "real") for i, n in enumerate(names)])
+        if a == "glrm":
+            R = self._score_arrays(frame)
+            rn = self.info["h2omx_recon_names"]
+            rn = rn if isinstance(rn, list) else [rn]
+            return Frame([Vec(f"reconstr_{n}", R[j].float(), "real") for j, n in enumerate(rn)])
+        if a == "extendedisolationforest":
+            P = self._score_arrays(frame)
+            return Frame([Vec("anomaly_score", P[0].float(), "real"), Vec("mean_length", P[1].float(), "real")])
+        if a == "coxph":
+            return Frame([Vec("lp", self._score_arrays(frame)[0], "real")])
+        if a == "word2vec":
+            raise ValueError("word2vec MOJO: use transform() / find_synonyms()")
+        return super().predict(frame)
+
+    def _te(self, frame: Frame) -> torch.Tensor:
+        info = self.info
+        dev = frame.device
+        prior = torch.from_numpy(self.arr["prior"]).to(dev)
+        outs = []
+        for i, c in enumerate(self.te_columns):
+            sums = torch.from_numpy(self.arr[f"te_sums_{i}"]).to(dev)
+            cnts = torch.from_numpy(self.arr[f"te_counts_{i}"]).to(dev)
+            L = cnts.numel() - 1
+            codes = frame.vec(c).data.long()
+            idx = torch.where((codes >= 0) & (codes < L), codes, torch.full_like(codes, L))
+            mean = torch.where(cnts[:, None] > 0, sums / cnts.clamp_min(1e-300)[:, None], prior[None, :])
+            if info["blending"]:
+                lam = 1.0 / (1.0 + torch.exp((info["inflection_point"] - cnts) / max(info["smoothing"], 1e-12)))
+                mean = lam[:, None] * mean + (1 - lam[:, None]) * prior[None, :]
+            enc = mean[idx]
+            enc = torch.where((idx == L)[:, None], prior[None, :].expand_as(enc), enc)
+            outs.append(enc.T.float())
+        return torch.cat(outs) if outs else torch.zeros((0, frame.nrows), device=dev)
+
+    def find_synonyms(self, word: str, count: int = 20) -> dict:
+        from ..models.word2vec import Word2VecModel
+
+        return Word2VecModel.find_synonyms(self._w2v(), word, count)
+
+    def transform(self, frame: Frame, aggregate_method: str = "NONE") -> Frame:
+        from ..models.word2vec import Word2VecModel
+
+        return Word2VecModel.transform(self._w2v(), frame, aggregate_method)
+
+    def _w2v(self):
+        from ..models.word2vec import Word2VecModel
+
+        w = Word2VecModel.__new__(Word2VecModel)
+        w.words, w.vectors = self.words, self.vectors
+        w.index = {t: i for i, t in enumerate(self.words)}
+        return w
 
     def _load_trees(self, z, info):
         from ..models.tree.boost import TreeEnsemble
@@ -470,6 +762,8 @@ class GenericModel(Model):
 
     def predict_raw(self, frame: Frame) -> torch.Tensor:
         a = self.mojo_algo
+        if a in ARRAY_ALGOS:
+            return self._score_arrays(frame)
         X = self._matrix(frame)
         if a == "isolationforest":
             L = self.ens.raw_margin(X)[0].to(X.device)

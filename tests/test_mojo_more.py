@@ -1,0 +1,77 @@
+"""MOJO round trips (export -> import as Generic -> identical scores) for the
+newer estimators (h2omx array payload)."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from h2omx.frame import Frame
+from h2omx.models import (H2OCoxProportionalHazardsEstimator, H2OExtendedIsolationForestEstimator,
+                          H2OGeneralizedAdditiveEstimator, H2OGeneralizedLowRankEstimator,
+                          H2OIsotonicRegressionEstimator, H2OPrincipalComponentAnalysisEstimator,
+                          H2OTargetEncoderEstimator, H2OWord2vecEstimator)
+from h2omx.mojo import import_mojo
+
+
+def _df(n=800, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, 4))
+    df = pd.DataFrame(X, columns=list("abcd"))
+    df["g"] = pd.Categorical(rng.choice(list("pqr"), n))
+    df["y"] = np.sin(X[:, 0]) + X[:, 1] + 0.1 * rng.normal(size=n)
+    df["yb"] = pd.Categorical(np.where(df.y > 0, "t", "f"))
+    df["t"] = np.ceil(rng.exponential(np.exp(-0.5 * X[:, 0])) * 10) / 10
+    df["ev"] = (rng.random(n) < 0.7).astype(float)
+    df.loc[::17, "c"] = np.nan
+    return df
+
+
+def _roundtrip(model, tmp_path):
+    path = model.download_mojo(str(tmp_path))
+    return import_mojo(path)
+
+
+def _same(a: Frame, b: Frame, rtol=1e-5, atol=1e-6):
+    pa, pb = a.to_pandas(), b.to_pandas()
+    assert list(pa.columns) == list(pb.columns)
+    np.testing.assert_allclose(pa.to_numpy(dtype=float), pb.to_numpy(dtype=float), rtol=rtol, atol=atol)
+
+
+@pytest.mark.parametrize("kind", ["pca", "glrm", "isotonic", "coxph", "te", "eif", "gam"])
+def test_mojo_roundtrip(kind, tmp_path):
+    df = _df()
+    fr = Frame.from_pandas(df)
+    if kind == "pca":
+        m = H2OPrincipalComponentAnalysisEstimator(k=2, transform="STANDARDIZE").train(x=list("abcdg"), training_frame=fr)
+    elif kind == "glrm":
+        m = H2OGeneralizedLowRankEstimator(k=2, init="SVD", max_iterations=20).train(x=list("abcd"), training_frame=fr)
+    elif kind == "isotonic":
+        m = H2OIsotonicRegressionEstimator(out_of_bounds="clip").train(x=["a"], y="y", training_frame=fr)
+    elif kind == "coxph":
+        m = H2OCoxProportionalHazardsEstimator(stop_column="t").train(x=["a", "b", "g"], y="ev", training_frame=fr)
+    elif kind == "te":
+        m = H2OTargetEncoderEstimator(noise=0.0, blending=True).train(x=["g"], y="yb", training_frame=fr)
+    elif kind == "eif":
+        m = H2OExtendedIsolationForestEstimator(ntrees=10, extension_level=1, seed=1).train(x=list("abc"),
+                                                                                         training_frame=fr)
+    else:
+        m = H2OGeneralizedAdditiveEstimator(family="gaussian", gam_columns=["a"], num_knots=[6], lambda_=0.0).train(
+            x=["a", "b"], y="y", training_frame=fr)
+    g = _roundtrip(m, tmp_path)
+    if kind == "te":
+        got = g.predict(fr)
+        exp = m.transform(fr)
+        np.testing.assert_allclose(got.to_pandas()["g_te"], exp.to_pandas()["g_te"], rtol=1e-6)
+        return
+    _same(m.predict(fr), g.predict(fr), rtol=1e-4, atol=1e-5)
+
+
+def test_word2vec_mojo(tmp_path):
+    rng = np.random.default_rng(0)
+    toks = []
+    for _ in range(500):
+        toks += list(rng.choice([f"w{i}" for i in range(10)], size=5)) + [None]
+    fr = Frame.from_pandas(pd.DataFrame({"w": toks}))
+    m = H2OWord2vecEstimator(vec_size=8, epochs=1, min_word_freq=1, seed=1).train(training_frame=fr)
+    g = _roundtrip(m, tmp_path)
+    assert g.find_synonyms("w1", 3) == m.find_synonyms("w1", 3)
+    _same(m.transform(fr, "AVERAGE"), g.transform(fr, "AVERAGE"))
