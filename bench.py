@@ -35,18 +35,23 @@ import time
 METRIC = "GBM train rows/sec on HIGGS-shape 11M×28 at 1/2/4/8 MI355X; AUC parity"
 
 
+def _sync(torch, dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def _timed(step, args, comm, torch, dev):
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    _sync(torch, dev)
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    _sync(torch, dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
+    _sync(torch, dev)
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    _sync(torch, dev)
     return comm.max_scalar(time.perf_counter() - t0)
 
 
@@ -54,7 +59,7 @@ def _trees(args, comm, torch, np, model):
     from h2omx.frame.synthetic import airlines_like, higgs_like
     from h2omx.metrics.core import auc_from_scores
     from h2omx.models.tree import TreeParams, bin_matrix, compute_edges
-    from h2omx.models.tree.boost import GpuBooster, TreeEnsemble
+    from h2omx.models.tree.boost import GpuBooster, TreeEnsemble, train_ensemble
 
     dev = comm.device
     world, rank = comm.world_size, comm.rank
@@ -83,15 +88,37 @@ def _trees(args, comm, torch, np, model):
     init = np.log(p0 / (1 - p0)) if model == "gbm-higgs" else 0.0   # XGBoost base_score 0.5
     ens = TreeEnsemble(trees=np.zeros((0, 1)), K=1, dist="bernoulli", init_f=np.array([init]), nbt=nbt,
                        feature_names=bm.names)
-    gb = GpuBooster(bm, y_np, None, ens, tp, 1.0, args.seed, comm, {})
-    torch.cuda.synchronize(dev)
-    comm.barrier()
-    setup_s = time.perf_counter() - t_setup
-    elapsed = _timed(gb.step, args, comm, torch, dev)
+    if dev.type == "cuda":
+        gb = GpuBooster(bm, y_np, None, ens, tp, 1.0, args.seed, comm, {})
+        _sync(torch, dev)
+        comm.barrier()
+        setup_s = time.perf_counter() - t_setup
+        elapsed = _timed(gb.step, args, comm, torch, dev)
+        margin = gb.st.Fm[0, : bm.n]
+    else:
+        # CPU rehearsal (reference tree builder): the boosting loop owns the
+        # iterations, so the timed window is opened / closed from its callback
+        setup_s = time.perf_counter() - t_setup
+        clock = {}
+
+        def cb(t, view):
+            if t == args.warmup - 1 or (args.warmup == 0 and t == -1):
+                comm.barrier()
+                clock["t0"] = time.perf_counter()
+            return None
+
+        if args.warmup == 0:
+            cb(-1, None)
+        ens = train_ensemble(bm, y, dist="bernoulli",
+                             ntrees=args.warmup + args.steps, tparams=tp, seed=args.seed, comm=comm,
+                             init_f=np.array([init]), callback=cb)
+        comm.barrier()
+        elapsed = comm.max_scalar(time.perf_counter() - clock["t0"])
+        margin = torch.from_numpy(ens._cpu_margin[0])
     total_rows = int(comm.all_reduce_numpy(np.array([float(n_local)]))[0])
     auc = None
     if not args.no_auc:
-        auc = auc_from_scores(gb.st.Fm[0, : bm.n], y, comm=comm)
+        auc = auc_from_scores(margin, y, comm=comm)
     out = {
         "metric": METRIC if model == "gbm-higgs" else
         "XGBoost-hist train rows/sec on Airlines-shape 150M×31 (18.75M rows per MI355X); AUC",
@@ -122,7 +149,7 @@ def _trees(args, comm, torch, np, model):
                                              max_bins=min(args.nbins, 255), early_stopping=False,
                                              l2_regularization=0.0).fit(Xs, ys)
         out["oracle"] = {"rows": m, "sklearn_hgb_train_auc": float(roc_auc_score(ys, clf.decision_function(Xs))),
-                         "h2omx_train_auc_same_rows": float(roc_auc_score(ys, gb.st.Fm[0, :m].cpu().numpy()))}
+                         "h2omx_train_auc_same_rows": float(roc_auc_score(ys, margin[:m].cpu().numpy()))}
     return out
 
 
@@ -163,7 +190,7 @@ def _mlp(args, comm, torch, np):
             D.adadelta_(net.flat, net.grad, Eg2, Edx2, 0.99, 1e-8, 0.0)
             mlp.refresh()
 
-        if args.graph and world == 1:
+        if args.graph and world == 1 and dev.type == "cuda":
             # the step after the batch staging is one HIP graph (fixed buffers); warm-up
             # on a side stream first so every lazily allocated workspace exists
             mlp.load_batch(X[:B])
@@ -195,7 +222,7 @@ def _mlp(args, comm, torch, np):
         bw(None, net, Hs, aux, dZ, 1, comm if world > 1 else None, world)
         D.adadelta_(net.flat, net.grad, Eg2, Edx2, 0.99, 1e-8, 0.0)
 
-    torch.cuda.synchronize(dev)
+    _sync(torch, dev)
     comm.barrier()
     setup_s = time.perf_counter() - t_setup
     elapsed = _timed(step, args, comm, torch, dev)
@@ -243,6 +270,8 @@ def main(argv=None) -> int:
                     help="dl-mlp GEMM operand precision (fp32 accumulation and master weights either way)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto",
+                    help="cpu: the torch reference paths (multi-rank rehearsal of this script over gloo)")
     ap.add_argument("--no-auc", action="store_true")
     ap.add_argument("--oracle-rows", type=int, default=0,
                     help="also fit sklearn HistGradientBoosting on this many rows for AUC parity")
@@ -254,7 +283,8 @@ def main(argv=None) -> int:
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from h2omx.parallel.comm import Comm
 
-    comm = Comm.from_env("cuda")
+    device = args.device if args.device != "auto" else ("cuda" if torch.cuda.device_count() > 0 else "cpu")
+    comm = Comm.from_env(device)
     if args.model == "dl-mlp":
         out = _mlp(args, comm, torch, np)
     else:
