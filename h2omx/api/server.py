@@ -57,7 +57,8 @@ LOG_BUFFER: list[str] = []
 _CAN_BUILD = {"kmeans": ["Clustering"], "pca": ["DimReduction"], "svd": ["DimReduction"], "glrm": ["DimReduction"],
               "aggregator": ["DimReduction"], "isolationforest": ["AnomalyDetection"],
               "extendedisolationforest": ["AnomalyDetection"], "coxph": ["CoxPH"], "rulefit": ["Binomial", "Regression"], "word2vec": ["WordEmbedding"],
-              "targetencoder": ["TargetEncoder"], "isotonicregression": ["Regression"], "adaboost": ["Binomial"]}
+              "targetencoder": ["TargetEncoder"], "isotonicregression": ["Regression"], "adaboost": ["Binomial"],
+              "upliftdrf": ["BinomialUplift"]}
 
 class _BufferHandler(logging.Handler):
     def emit(self, record):

@@ -18,6 +18,7 @@ from .pca import H2OPrincipalComponentAnalysisEstimator  # noqa: F401
 from .rulefit import H2ORuleFitEstimator  # noqa: F401
 from .svd import H2OSingularValueDecompositionEstimator  # noqa: F401
 from .target_encoder import H2OTargetEncoderEstimator  # noqa: F401
+from .uplift import H2OUpliftRandomForestEstimator  # noqa: F401
 from .word2vec import H2OWord2vecEstimator  # noqa: F401
 from .tree_models import (H2OGradientBoostingEstimator, H2ORandomForestEstimator,  # noqa: F401
                           H2OXGBoostEstimator)
@@ -47,4 +48,5 @@ ESTIMATORS = {
     "gam": H2OGeneralizedAdditiveEstimator,
     "modelselection": H2OModelSelectionEstimator,
     "anovaglm": H2OANOVAGLMEstimator,
+    "upliftdrf": H2OUpliftRandomForestEstimator,
 }

@@ -14,7 +14,8 @@ from h2omx.frame.distributed import unify_domains  # noqa: E402
 from h2omx.models import (H2OANOVAGLMEstimator, H2OCoxProportionalHazardsEstimator,  # noqa: E402
                           H2OGeneralizedAdditiveEstimator, H2OGeneralizedLowRankEstimator,
                           H2OIsotonicRegressionEstimator, H2OModelSelectionEstimator,
-                          H2OSingularValueDecompositionEstimator, H2OTargetEncoderEstimator)
+                          H2OSingularValueDecompositionEstimator, H2OTargetEncoderEstimator,
+                          H2OUpliftRandomForestEstimator)
 from h2omx.parallel.comm import Comm  # noqa: E402
 
 
@@ -26,6 +27,10 @@ def data(n=1200):
     df["y"] = np.sin(X[:, 0]) + X[:, 1] - 0.5 * X[:, 2] + rng.normal(scale=0.3, size=n)
     df["t"] = np.ceil(rng.exponential(np.exp(-0.5 * X[:, 0])) * 10) / 10
     df["ev"] = (rng.random(n) < 0.7).astype(float)
+    trt = rng.random(n) < 0.5
+    df["trt"] = pd.Categorical(np.where(trt, "treatment", "control"), categories=["control", "treatment"])
+    p = np.clip(0.3 + 0.1 * X[:, 1] + trt * np.where(X[:, 0] > 0, 0.3, -0.1), 0.02, 0.98)
+    df["yb"] = pd.Categorical(np.where(rng.random(n) < p, "1", "0"), categories=["0", "1"])
     return df
 
 
@@ -58,6 +63,10 @@ def main():
     an = H2OANOVAGLMEstimator(family="gaussian", highest_interaction_term=1).train(
         x=["a", "b", "d"], y="y", training_frame=fr, comm=c)
     res["anova"] = [r["deviance_difference"] for r in an.result()]
+    up = H2OUpliftRandomForestEstimator(ntrees=3, max_depth=4, sample_rate=1.0, treatment_column="trt", seed=3).train(
+        x=["a", "b", "c"], y="yb", training_frame=fr, comm=c)
+    res["uplift"] = up.predict(fr).to_pandas()["uplift_predict"].tolist()
+    res["auuc"] = up.training_metrics["auuc"]
     with open(out_path, "w") as f:
         json.dump(res, f)
     comm.barrier()

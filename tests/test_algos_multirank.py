@@ -54,3 +54,5 @@ def test_two_ranks_match_one_rank(results):
         for k, v in one["gam"].items():
             assert abs(r["gam"][k] - v) < 1e-3 * max(1.0, abs(v)), k
         np.testing.assert_allclose(r["anova"], one["anova"], rtol=1e-4)
+        np.testing.assert_allclose(r["auuc"], one["auuc"], rtol=1e-9)
+    np.testing.assert_allclose(two[0]["uplift"] + two[1]["uplift"], one["uplift"], rtol=1e-6)
