@@ -9,6 +9,7 @@ from .ensemble import H2OStackedEnsembleEstimator  # noqa: F401
 from .glm import H2OGeneralizedLinearEstimator  # noqa: F401
 from .gam import H2OGeneralizedAdditiveEstimator  # noqa: F401
 from .glrm import H2OGeneralizedLowRankEstimator  # noqa: F401
+from .infogram import H2OInfogram  # noqa: F401
 from .isolation_forest import H2OIsolationForestEstimator  # noqa: F401
 from .isotonic import H2OIsotonicRegressionEstimator  # noqa: F401
 from .kmeans import H2OKMeansEstimator  # noqa: F401
@@ -49,4 +50,5 @@ ESTIMATORS = {
     "modelselection": H2OModelSelectionEstimator,
     "anovaglm": H2OANOVAGLMEstimator,
     "upliftdrf": H2OUpliftRandomForestEstimator,
+    "infogram": H2OInfogram,
 }
