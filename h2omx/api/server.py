@@ -58,7 +58,8 @@ _CAN_BUILD = {"kmeans": ["Clustering"], "pca": ["DimReduction"], "svd": ["DimRed
               "aggregator": ["DimReduction"], "isolationforest": ["AnomalyDetection"],
               "extendedisolationforest": ["AnomalyDetection"], "coxph": ["CoxPH"], "rulefit": ["Binomial", "Regression"], "word2vec": ["WordEmbedding"],
               "targetencoder": ["TargetEncoder"], "isotonicregression": ["Regression"], "adaboost": ["Binomial"],
-              "upliftdrf": ["BinomialUplift"], "infogram": ["Binomial", "Multinomial", "Regression"]}
+              "upliftdrf": ["BinomialUplift"], "infogram": ["Binomial", "Multinomial", "Regression"],
+              "psvm": ["Binomial"]}
 
 class _BufferHandler(logging.Handler):
     def emit(self, record):

@@ -16,6 +16,7 @@ from .kmeans import H2OKMeansEstimator  # noqa: F401
 from .naive_bayes import H2ONaiveBayesEstimator  # noqa: F401
 from .model_selection import H2OANOVAGLMEstimator, H2OModelSelectionEstimator  # noqa: F401
 from .pca import H2OPrincipalComponentAnalysisEstimator  # noqa: F401
+from .psvm import H2OSupportVectorMachineEstimator  # noqa: F401
 from .rulefit import H2ORuleFitEstimator  # noqa: F401
 from .svd import H2OSingularValueDecompositionEstimator  # noqa: F401
 from .target_encoder import H2OTargetEncoderEstimator  # noqa: F401
@@ -51,4 +52,5 @@ ESTIMATORS = {
     "anovaglm": H2OANOVAGLMEstimator,
     "upliftdrf": H2OUpliftRandomForestEstimator,
     "infogram": H2OInfogram,
+    "psvm": H2OSupportVectorMachineEstimator,
 }

@@ -15,7 +15,7 @@ from h2omx.models import (H2OANOVAGLMEstimator, H2OCoxProportionalHazardsEstimat
                           H2OGeneralizedAdditiveEstimator, H2OGeneralizedLowRankEstimator,
                           H2OIsotonicRegressionEstimator, H2OModelSelectionEstimator,
                           H2OSingularValueDecompositionEstimator, H2OTargetEncoderEstimator,
-                          H2OUpliftRandomForestEstimator)
+                          H2OSupportVectorMachineEstimator, H2OUpliftRandomForestEstimator)
 from h2omx.parallel.comm import Comm  # noqa: E402
 
 
@@ -67,6 +67,8 @@ def main():
         x=["a", "b", "c"], y="yb", training_frame=fr, comm=c)
     res["uplift"] = up.predict(fr).to_pandas()["uplift_predict"].tolist()
     res["auuc"] = up.training_metrics["auuc"]
+    sv = H2OSupportVectorMachineEstimator(gamma=0.5).train(x=["a", "b"], y="yb", training_frame=fr, comm=c)
+    res["svm"] = sv.decision_function(fr).tolist()
     with open(out_path, "w") as f:
         json.dump(res, f)
     comm.barrier()

@@ -56,3 +56,4 @@ def test_two_ranks_match_one_rank(results):
         np.testing.assert_allclose(r["anova"], one["anova"], rtol=1e-4)
         np.testing.assert_allclose(r["auuc"], one["auuc"], rtol=1e-9)
     np.testing.assert_allclose(two[0]["uplift"] + two[1]["uplift"], one["uplift"], rtol=1e-6)
+    np.testing.assert_allclose(two[0]["svm"] + two[1]["svm"], one["svm"], rtol=1e-4, atol=1e-4)
