@@ -223,6 +223,17 @@ class H2OApi:
         R("GET", r"/3/NodePersistentStorage/.*", self.nps)
         R("GET", r"/metrics", self.prometheus)
         R("POST", r"/3/LogAndEcho", self.log_and_echo)
+        R("POST", r"/3/Frames/(?P<fid>[^/]+)/export", self.frame_export)
+        R("POST", r"/3/CreateFrame", self.create_frame)
+        R("POST", r"/3/Interaction", self.interaction)
+        R("POST", r"/3/MissingInserter", self.missing_inserter)
+        R("GET", r"/3/Word2VecSynonyms", self.w2v_synonyms)
+        R("GET", r"/3/Word2VecTransform", self.w2v_transform)
+        R("GET", r"/3/NetworkTest", self.network_test)
+        R("GET", r"/3/Typeahead/files", self.typeahead_files)
+        R("POST", r"/3/GarbageCollect", self.garbage_collect)
+        R("GET", r"/3/JStack", self.jstack)
+        R("GET", r"/3/ModelMetrics", self.model_metrics_all)
         if os.environ.get("H2OMX_ENABLE_FAULT_INJECTION") == "1":
             R("POST", r"/99/h2omx/fault", self.inject_fault)
 
@@ -520,6 +531,8 @@ class H2OApi:
         return {"__meta": S.meta("ModelParametersSchemaV3", "Iced"), "messages": msgs, "error_count": 0}
 
     def build_model(self, algo, params, **_):
+        if algo == "generic":
+            return self._build_generic(params)
         args, tf, y, vf, msgs = self._builder_args(algo, params)
         model_id = params.get("model_id") or f"{algo.upper()}_model_h2omx_{uuid.uuid4().hex[:10]}"
         fr = DKV.get(tf)
@@ -537,6 +550,24 @@ class H2OApi:
         job = self.jobs.submit(f"{algo} model build", model_id, "Key<Model>", work, sync=blocking)
         return {"__meta": S.meta(f"{algo.upper()}V3", "ModelBuilder"), "algo": algo, "job": job.to_json(),
                 "messages": msgs, "error_count": 0, "parameters": {k: _jsonable(v) for k, v in args.items()}}
+
+    def _build_generic(self, params):
+        """POST /3/ModelBuilders/generic: import a MOJO from ``path`` or an
+        uploaded / imported file key (``model_key``) on every rank."""
+        src = params.get("path") or params.get("model_key")
+        if not src:
+            raise ApiError(412, "generic: path or model_key is required")
+        src = src.get("name") if isinstance(src, dict) else str(src)
+        model_id = params.get("model_id") or f"Generic_model_h2omx_{uuid.uuid4().hex[:10]}"
+
+        def work(job):
+            mid = self.cluster.run("train", algo="generic", params={"path": src}, model_id=model_id)
+            self.counters["models_built"] += 1
+            return mid
+
+        job = self.jobs.submit("generic model import", model_id, "Key<Model>", work, sync=True)
+        return {"__meta": S.meta("GenericV3", "ModelBuilder"), "algo": "generic", "job": job.to_json(),
+                "messages": [], "error_count": 0, "parameters": {"path": src}}
 
     # -- grid search ------------------------------------------------------------
     def grid_build(self, algo, params, **_):
@@ -824,6 +855,133 @@ class H2OApi:
     def timeline_get(self, **_):
         return {"__meta": S.meta("TimelineV3", "Iced"), "self": "rank0", "now": int(time.time() * 1000),
                 "events": list(self.timeline[-200:])}
+
+    # -- frame tools / word2vec / diagnostics ----------------------------------
+    def frame_export(self, fid, params, **_):
+        fid = unquote(fid)
+        if not isinstance(DKV.get(fid), Frame):
+            raise KeyError(fid)
+        path = params.get("path")
+        if not path:
+            raise ApiError(400, "path is required")
+        force = str(params.get("force", "false")).lower() == "true"
+        job = self.jobs.submit("Export", fid, "Key<Frame>",
+                               lambda j: self.cluster.run("frame_export", key=fid, path=path, force=force), sync=True)
+        return {"__meta": S.meta("FramesV3", "Frames"), "job": job.to_json(), "path": path}
+
+    def create_frame(self, params, **_):
+        dest = params.get("dest") or f"frame_{uuid.uuid4().hex[:10]}"
+        spec = {}
+        casts = {"rows": int, "cols": int, "seed": int, "factors": int, "integer_range": int, "response_factors": int,
+                 "real_range": float, "categorical_fraction": float, "integer_fraction": float,
+                 "binary_fraction": float, "binary_ones_fraction": float, "time_fraction": float,
+                 "string_fraction": float, "missing_fraction": float, "value": float}
+        for k, cast in casts.items():
+            if params.get(k) not in (None, ""):
+                spec[k] = cast(params[k])
+        for k in ("randomize", "has_response", "positive_response"):
+            if params.get(k) not in (None, ""):
+                spec[k] = str(params[k]).lower() == "true"
+        if spec.get("seed", 0) < 0:
+            spec["seed"] = int(time.time() * 1000) & 0x7FFFFFFF
+        job = self.jobs.submit("CreateFrame", dest, "Key<Frame>",
+                               lambda j: self.cluster.run("create_frame", dest=dest, spec=spec), sync=True)
+        return {"__meta": S.meta("CreateFrameV3", "Iced"), "dest": S.key_ref(dest, "Key<Frame>"),
+                "key": S.key_ref(job.key, "Key<Job>"), "job": job.to_json(), **job.to_json()}
+
+    def interaction(self, params, **_):
+        src = params.get("source_frame")
+        if not isinstance(DKV.get(src), Frame):
+            raise KeyError(src)
+        dest = params.get("dest") or f"interaction_{uuid.uuid4().hex[:10]}"
+        factors = parse_list(params.get("factor_columns"))
+        factors = [int(f) if str(f).lstrip("-").isdigit() else f for f in factors]
+        kw = dict(pairwise=str(params.get("pairwise", "false")).lower() == "true",
+                  max_factors=int(params.get("max_factors", 100)), min_occurrence=int(params.get("min_occurrence", 1)))
+        job = self.jobs.submit("Interaction", dest, "Key<Frame>",
+                               lambda j: self.cluster.run("interaction", source=src, dest=dest, factors=factors, **kw),
+                               sync=True)
+        return {"__meta": S.meta("InteractionV3", "Iced"), "dest": S.key_ref(dest, "Key<Frame>"),
+                "key": S.key_ref(job.key, "Key<Job>"), "job": job.to_json(), **job.to_json()}
+
+    def missing_inserter(self, params, **_):
+        fid = params.get("dataset")
+        if not isinstance(DKV.get(fid), Frame):
+            raise KeyError(fid)
+        frac = float(params.get("fraction", 0.1))
+        seed = int(params.get("seed", -1) or -1)
+        job = self.jobs.submit("MissingInserter", fid, "Key<Frame>",
+                               lambda j: self.cluster.run("insert_missing", key=fid, fraction=frac, seed=seed),
+                               sync=True)
+        return {"__meta": S.meta("MissingInserterV3", "Iced"), "dataset": S.key_ref(fid, "Key<Frame>"),
+                "key": S.key_ref(job.key, "Key<Job>"), "job": job.to_json(), **job.to_json()}
+
+    def w2v_synonyms(self, params, **_):
+        m = self._get_model(params.get("model"))
+        syn = self.cluster.run("w2v_synonyms", model=m.model_id, word=params.get("word"),
+                               count=int(params.get("count", 20)))
+        return {"__meta": S.meta("Word2VecSynonymsV3", "Iced"), "model": S.key_ref(m.model_id, "Key<Model>"),
+                "word": params.get("word"), "count": int(params.get("count", 20)),
+                "synonyms": list(syn.keys()), "scores": list(syn.values())}
+
+    def w2v_transform(self, params, **_):
+        m = self._get_model(params.get("model"))
+        fid = params.get("words_frame")
+        if not isinstance(DKV.get(fid), Frame):
+            raise KeyError(fid)
+        dest = f"w2v_transform_{uuid.uuid4().hex[:10]}"
+        self.cluster.run("w2v_transform", model=m.model_id, frame=fid, dest=dest,
+                         aggregate_method=params.get("aggregate_method", "NONE"))
+        return {"__meta": S.meta("Word2VecTransformV3", "Iced"), "model": S.key_ref(m.model_id, "Key<Model>"),
+                "words_frame": S.key_ref(fid, "Key<Frame>"), "vectors_frame": S.key_ref(dest, "Key<Frame>")}
+
+    def network_test(self, **_):
+        res = self.cluster.run("network_test")
+        rows = [[r["bytes"], r["microseconds"], r["bus_bandwidth_GBps"]] for r in res["results"]]
+        table = S.two_dim_table(f"Collective test ({res['backend']}, {res['world_size']} ranks)",
+                                ["bytes", "microseconds", "bus_bandwidth_GBps"], ["long", "double", "double"], rows)
+        return {"__meta": S.meta("NetworkTestV3", "Iced"), "table": table, **res}
+
+    def typeahead_files(self, params, **_):
+        src = params.get("src") or ""
+        limit = int(params.get("limit", 1000) or 1000)
+        d, pre = (src, "") if os.path.isdir(src) else (os.path.dirname(src) or ".", os.path.basename(src))
+        try:
+            names = sorted(n for n in os.listdir(d) if n.startswith(pre))
+        except OSError:
+            names = []
+        return {"__meta": S.meta("TypeaheadV3", "Iced"), "src": src, "limit": limit,
+                "matches": [os.path.join(d, n) for n in names[:limit]]}
+
+    def garbage_collect(self, **_):
+        import gc
+
+        import torch
+
+        gc.collect()
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+        return {"__meta": S.meta("GarbageCollectV3", "Iced")}
+
+    def jstack(self, **_):
+        import sys
+        import traceback
+
+        traces = []
+        for tid, frame in sys._current_frames().items():
+            traces.append(f"thread {tid}\n" + "".join(traceback.format_stack(frame)))
+        return {"__meta": S.meta("JStackV3", "Iced"),
+                "traces": [{"node": "rank0", "time": int(time.time() * 1000), "thread_traces": traces}]}
+
+    def model_metrics_all(self, **_):
+        from ..models.base import Model
+
+        out = []
+        for k in DKV.keys(Model):
+            m = DKV.get(k)
+            if m.training_metrics:
+                out.append(S.metrics_json(m.training_metrics, m.category, m.model_id, None, m.response_domain))
+        return {"__meta": S.meta("ModelMetricsListSchemaV3", "Iced"), "model_metrics": out}
 
     def nps(self, **_):
         return {"__meta": S.meta("NodePersistentStorageV3", "Iced"), "entries": []}

@@ -6,6 +6,7 @@ from .coxph import H2OCoxProportionalHazardsEstimator  # noqa: F401
 from .deeplearning import H2ODeepLearningEstimator  # noqa: F401
 from .extended_isolation_forest import H2OExtendedIsolationForestEstimator  # noqa: F401
 from .ensemble import H2OStackedEnsembleEstimator  # noqa: F401
+from .generic import H2OGenericEstimator  # noqa: F401
 from .glm import H2OGeneralizedLinearEstimator  # noqa: F401
 from .gam import H2OGeneralizedAdditiveEstimator  # noqa: F401
 from .glrm import H2OGeneralizedLowRankEstimator  # noqa: F401
@@ -53,4 +54,5 @@ ESTIMATORS = {
     "upliftdrf": H2OUpliftRandomForestEstimator,
     "infogram": H2OInfogram,
     "psvm": H2OSupportVectorMachineEstimator,
+    "generic": H2OGenericEstimator,
 }

@@ -52,10 +52,10 @@ from ..models.base import Model, ModelCategory
 MOJO_VERSIONS = {"gbm": "1.40", "drf": "1.40", "xgboost": "1.00", "glm": "1.00", "kmeans": "1.00",
                  "deeplearning": "1.10", "stackedensemble": "1.01", "pca": "1.00", "glrm": "1.10",
                  "isotonicregression": "1.00", "coxph": "1.00", "targetencoder": "1.00", "word2vec": "1.00",
-                 "extendedisolationforest": "1.00", "gam": "1.00"}
+                 "extendedisolationforest": "1.00", "gam": "1.00", "upliftdrf": "1.40"}
 # algorithms whose payload is the h2omx array layout below (design + named arrays)
 ARRAY_ALGOS = ("pca", "glrm", "isotonicregression", "coxph", "targetencoder", "word2vec",
-               "extendedisolationforest", "gam")
+               "extendedisolationforest", "gam", "upliftdrf")
 NSD_NA_LEFT, NSD_NA_RIGHT = 2, 3
 
 
@@ -234,7 +234,9 @@ def mojo_bytes(model: Model) -> bytes:
     if algo == "coxph":
         head["supervised"] = False
         head["category"] = "CoxPH"
-    lines = ["[info]"] + [f"{k} = {_fmt(v)}" for k, v in {**head, **info}.items()]
+    if algo == "upliftdrf":
+        head["category"] = "BinomialUplift"
+    lines =["[info]"] + [f"{k} = {_fmt(v)}" for k, v in {**head, **info}.items()]
     lines += ["", "[columns]"] + columns + ["", "[domains]"]
     for i, (j, dom) in enumerate(domains):
         lines.append(f"{j}: {len(dom)} d{i:03d}.txt")
@@ -379,6 +381,17 @@ def _design_info(design, info, files, tag="design"):
     _put(files, info, f"{tag}_center", getattr(design, "center", np.zeros(len(design.names))))
 
 
+def _uplift_info(model, info, files):
+    for k in ("feat", "bin", "na_left", "left", "pt", "pc"):
+        _put(files, info, f"uplift_{k}", np.concatenate([np.asarray(t[k], np.float64) for t in model.trees]))
+    _put(files, info, "uplift_tree_sizes", [len(t["feat"]) for t in model.trees])
+    _put(files, info, "uplift_edges", np.asarray(model.edges, np.float64))
+    _put(files, info, "uplift_nvb", np.asarray(model.nvb, np.float64))
+    info.update(nbt=int(model.nbt), treatment_column=model.treatment_column, ntrees=len(model.trees),
+                uplift_metric=str(model.params.get("uplift_metric", "AUTO")),
+                auuc_type=str(model.params.get("auuc_type", "AUTO")))
+
+
 def _array_info(model, files):
     info: dict = {}
     a = model.algo
@@ -399,6 +412,8 @@ def _array_info(model, files):
         _put(files, info, "thresholds_x", model.thresholds_x)
         _put(files, info, "thresholds_y", model.thresholds_y)
         info["out_of_bounds"] = str(model.params["out_of_bounds"])
+    elif a == "upliftdrf":
+        _uplift_info(model, info, files)
     elif a == "coxph":
         _put(files, info, "coef", model.beta)
         _put(files, info, "x_mean_num", model.x_mean)
@@ -541,6 +556,8 @@ class GenericModel(Model):
             self._load_arrays(z, info)
         if self.mojo_algo == "coxph":
             self.category = ModelCategory.REGRESSION
+        if self.mojo_algo == "upliftdrf":
+            self.category = "BinomialUplift"
 
     def _design(self, z, info, tag="design"):
         from ..models.glm import DesignInfo
@@ -570,6 +587,18 @@ class GenericModel(Model):
             for i in range(len(self.te_columns)):
                 self.arr[f"te_sums_{i}"] = _get(z, info, f"te_sums_{i}")
                 self.arr[f"te_counts_{i}"] = _get(z, info, f"te_counts_{i}")
+        if a == "upliftdrf":
+            sizes = _get(z, info, "uplift_tree_sizes").astype(np.int64)
+            cols = {k: _get(z, info, f"uplift_{k}") for k in ("feat", "bin", "na_left", "left", "pt", "pc")}
+            self.uplift_trees, o = [], 0
+            for sz in sizes:
+                t = {k: v[o:o + sz] for k, v in cols.items()}
+                self.uplift_trees.append({"feat": t["feat"].astype(np.int32), "bin": t["bin"].astype(np.int32),
+                                          "na_left": t["na_left"].astype(np.int8),
+                                          "left": t["left"].astype(np.int32), "pt": t["pt"], "pc": t["pc"]})
+                o += int(sz)
+            self.arr["edges"] = _get(z, info, "uplift_edges").astype(np.float32)
+            self.arr["nvb"] = _get(z, info, "uplift_nvb").astype(np.int64)
         if a == "word2vec":
             self.words = z.read("h2omx/vocabulary.txt").decode().split("\n")[: int(info["vocab_size"])]
             self.vectors = torch.from_numpy(_get(z, info, "vectors").astype(np.float32))
@@ -646,6 +675,22 @@ class GenericModel(Model):
             return torch.stack([torch.pow(2.0, -ml / cst), ml])
         if a == "targetencoder":
             return self._te(frame)
+        if a == "upliftdrf":
+            from ..models.tree import bin_matrix
+            from ..models.uplift import predict_tree
+
+            nbt = int(info["nbt"])
+            bm = bin_matrix(frame.feature_matrix(self.x), self.arr["edges"], self.arr["nvb"], nbt)
+            n = frame.nrows
+            pt = torch.zeros(n, dtype=torch.float64, device=bm.device)
+            pc = torch.zeros_like(pt)
+            for tr in self.uplift_trees:
+                a_, b_ = predict_tree(tr, bm.codes, n, nbt)
+                pt += a_
+                pc += b_
+            k = max(len(self.uplift_trees), 1)
+            pt, pc = (pt / k).float(), (pc / k).float()
+            return torch.stack([pt - pc, pt, pc]).to(dev)
         if a == "gam":
             from ..models.gam import _augment
 
@@ -684,6 +729,10 @@ class GenericModel(Model):
             return Frame([Vec("lp", self._score_arrays(frame)[0], "real")])
         if a == "word2vec":
             raise ValueError("word2vec MOJO: use transform() / find_synonyms()")
+        if a == "upliftdrf":
+            P = self._score_arrays(frame)
+            return Frame([Vec("uplift_predict", P[0], "real"), Vec("p_y1_with_treatment", P[1], "real"),
+                          Vec("p_y1_without_treatment", P[2], "real")])
         return super().predict(frame)
 
     def _te(self, frame: Frame) -> torch.Tensor:

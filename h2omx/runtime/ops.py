@@ -171,6 +171,8 @@ def op_train(cl, algo, params, x=None, y=None, training_frame=None, validation_f
     p = _resolve_params(dict(params))
     p["model_id"] = model_id
     est = cls(**p)
+    if algo == "generic":                      # MOJO import: no training frame
+        return est.train(comm=cl.comm if cl.world_size > 1 else None).model_id
     tr = _frame(training_frame)
     va = _frame(validation_frame) if validation_frame else None
     comm = cl.comm if cl.world_size > 1 else None
@@ -302,6 +304,86 @@ def op_load_model(cl, path):
     m = load_model(path)
     DKV.put(m.model_id, m)
     return m.model_id
+
+
+def op_create_frame(cl, dest, spec):
+    from ..frame.tools import create_frame
+
+    fr = create_frame(comm=cl.comm if cl.world_size > 1 else None, device=_dev(cl), **spec)
+    fr.key = dest
+    DKV.put(dest, fr)
+    return {"key": dest, "rows": global_nrows(fr, cl.comm), "cols": fr.ncols}
+
+
+def op_interaction(cl, source, dest, factors, pairwise=False, max_factors=100, min_occurrence=1):
+    from ..frame.tools import interaction
+
+    fr = interaction(_frame(source), factors, pairwise, max_factors, min_occurrence,
+                     comm=cl.comm if cl.world_size > 1 else None)
+    fr.key = dest
+    DKV.put(dest, fr)
+    return {"key": dest, "rows": global_nrows(fr, cl.comm), "cols": fr.ncols}
+
+
+def op_insert_missing(cl, key, fraction=0.1, seed=-1):
+    from ..frame.tools import insert_missing_values
+
+    insert_missing_values(_frame(key), fraction, seed, comm=cl.comm if cl.world_size > 1 else None)
+    return {"key": key}
+
+
+def op_frame_export(cl, key, path, force=False):
+    """h2o.export_file: the leader writes the gathered frame as CSV."""
+    fr = gather_frame(_frame(key), cl.comm)
+    if cl.rank == 0:
+        if os.path.exists(path) and not force:
+            raise FileExistsError(f"{path} exists (use force=True)")
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        fr.to_pandas().to_csv(path, index=False)
+    return path
+
+
+def op_w2v_synonyms(cl, model, word, count=20):
+    return _model(model).find_synonyms(word, int(count))
+
+
+def op_w2v_transform(cl, model, frame, dest, aggregate_method="NONE"):
+    m = _model(model)
+    out = m.transform(_frame(frame), aggregate_method)
+    out.key = dest
+    DKV.put(dest, out)
+    return {"key": dest, "rows": global_nrows(out, cl.comm)}
+
+
+def op_network_test(cl, sizes=(1 << 10, 1 << 16, 1 << 20, 1 << 24), reps=5):
+    """Collective latency / bandwidth over the cluster's communicator (H2O
+    NetworkTest): all-reduce of fp32 buffers of each size, timed on the leader."""
+    import time
+
+    dev = _dev(cl)
+    out = []
+    for nbytes in sizes:
+        t = torch.ones(max(1, int(nbytes) // 4), dtype=torch.float32, device=dev)
+        cl.comm.all_reduce_(t)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        cl.comm.barrier()
+        t0 = time.perf_counter()
+        for _ in range(int(reps)):
+            cl.comm.all_reduce_(t)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        dt = cl.comm.max_scalar((time.perf_counter() - t0) / int(reps))
+        w = cl.world_size
+        bus = 2.0 * (w - 1) / w * t.numel() * 4 / dt if w > 1 and dt > 0 else 0.0
+        out.append({"bytes": int(t.numel() * 4), "microseconds": dt * 1e6, "bus_bandwidth_GBps": bus / 1e9})
+    return {"world_size": cl.world_size, "backend": _backend_name(cl), "results": out}
+
+
+def _backend_name(cl):
+    import torch.distributed as dist
+
+    return dist.get_backend() if cl.world_size > 1 and dist.is_initialized() else "local"
 
 
 def op_fault(cl, rank=-1, kind="raise"):

@@ -69,6 +69,10 @@ def main():
     res["auuc"] = up.training_metrics["auuc"]
     sv = H2OSupportVectorMachineEstimator(gamma=0.5).train(x=["a", "b"], y="yb", training_frame=fr, comm=c)
     res["svm"] = sv.decision_function(fr).tolist()
+    from h2omx.frame.tools import interaction
+
+    ia = interaction(fr, ["g", "trt"], max_factors=5, comm=c).vecs[0]
+    res["inter"] = [ia.domain[i] if i >= 0 else None for i in ia.data.tolist()]
     with open(out_path, "w") as f:
         json.dump(res, f)
     comm.barrier()

@@ -75,3 +75,23 @@ def test_word2vec_mojo(tmp_path):
     g = _roundtrip(m, tmp_path)
     assert g.find_synonyms("w1", 3) == m.find_synonyms("w1", 3)
     _same(m.transform(fr, "AVERAGE"), g.transform(fr, "AVERAGE"))
+
+
+def test_uplift_mojo(tmp_path):
+    from h2omx.models import H2OUpliftRandomForestEstimator
+
+    rng = np.random.default_rng(2)
+    n = 3000
+    X = rng.normal(size=(n, 3))
+    trt = rng.random(n) < 0.5
+    p = np.clip(0.3 + 0.1 * X[:, 1] + trt * np.where(X[:, 0] > 0, 0.3, -0.1), 0.02, 0.98)
+    df = pd.DataFrame(X, columns=list("abc"))
+    df.loc[::13, "b"] = np.nan
+    df["trt"] = pd.Categorical(np.where(trt, "treatment", "control"), categories=["control", "treatment"])
+    df["y"] = pd.Categorical(np.where(rng.random(n) < p, "1", "0"), categories=["0", "1"])
+    fr = Frame.from_pandas(df)
+    m = H2OUpliftRandomForestEstimator(ntrees=4, max_depth=4, treatment_column="trt", seed=1).train(
+        x=list("abc"), y="y", training_frame=fr)
+    g = _roundtrip(m, tmp_path)
+    assert g.category == "BinomialUplift"
+    _same(g.predict(fr), m.predict(fr))
