@@ -288,7 +288,7 @@ class H2OApi:
                    "free_mem": 0, "max_mem": 0, "swap_mem": 0, "num_keys": len(DKV.keys()), "free_disk": 0,
                    "max_disk": 0, "rpcs_active": 0, "fjthrds": [], "fjqueue": [], "tcps_active": 0,
                    "open_fds": -1, "gflops": 0.0, "mem_bw": 0.0}
-            if torch.cuda.is_available() and r == self.cluster.rank:
+            if self.cluster.comm.device.type == "cuda" and r == self.cluster.rank:
                 p = torch.cuda.get_device_properties(self.cluster.comm.device)
                 ent["gpu"] = {"name": p.name, "total_memory": p.total_memory,
                               "multi_processor_count": p.multi_processor_count}

@@ -307,67 +307,71 @@ class H2OUpliftRandomForestEstimator(ModelBuilder):
         for f in range(F):
             bin_ok[f, : max(int(nvb_np[f]) - 1, 0)] = True
         trees = []
-        yt_all, yc_all = treat * y, (1 - treat) * y
+        # row category (treated/control x y=0/1): every statistic is a count of one of them
+        cat = ((1 - treat) * 2 + y).long()
         for t in range(int(p_["ntrees"])):
             sr = float(p_["sample_rate"])
-            bag = (torch.rand(n, generator=g_rows, device=dev) < sr).double() if sr < 1 else torch.ones(
-                n, dtype=torch.float64, device=dev)
+            rc = cat.clone()
+            if sr < 1:
+                rc[torch.rand(n, generator=g_rows, device=dev) >= sr] = -1
             csr = float(p_["col_sample_rate_per_tree"])
             tree_cols = torch.ones(F, dtype=torch.bool)
             if csr < 1:
                 k = max(1, int(round(csr * F)))
                 tree_cols[:] = False
                 tree_cols[torch.randperm(F, generator=g_feat)[:k]] = True
-            trees.append(self._grow(codes, bag * treat, bag * yt_all, bag * (1 - treat), bag * yc_all, F, nbt,
-                                    bin_ok, tree_cols, mtries, g_feat, metric, min_rows, msi, comm))
+            trees.append(self._grow(codes, rc, F, nbt, bin_ok, tree_cols, mtries, g_feat, metric, min_rows, msi,
+                                    comm))
         model = UpliftDRFModel(self, model_id, trees, np.asarray(edges), nvb_np, nbt, tc)
         return model
 
-    def _grow(self, codes, wt, yt, wc, yc, F, nbt, bin_ok, tree_cols, mtries, g_feat, metric, min_rows, msi, comm):
+    @staticmethod
+    def _hist(codes, rc, slot, S, F, nbt, comm):
+        """Category counts [S][F][nbt][4] of the rows with slot >= 0: one
+        unweighted bincount over (slot, feature, bin, category) keys."""
+        dev = codes.device
+        rows = torch.nonzero((slot >= 0) & (rc >= 0)).flatten()
+        H = torch.zeros(S * F * nbt * 4, dtype=torch.float64, device=dev)
+        if rows.numel():
+            base = (slot[rows] * (F * nbt * 4) + rc[rows])[None, :]
+            fchunk = max(1, (1 << 26) // rows.numel())
+            for f0 in range(0, F, fchunk):
+                f1 = min(F, f0 + fchunk)
+                fi = torch.arange(f0, f1, device=dev)[:, None]
+                key = base + (fi * nbt + codes[f0:f1][:, rows].long()) * 4
+                H += torch.bincount(key.flatten(), minlength=H.numel()).double()
+        if comm is not None and comm.world_size > 1:
+            comm.all_reduce_(H)
+        return H.view(S, F, nbt, 4)
+
+    def _grow(self, codes, rc, F, nbt, bin_ok, tree_cols, mtries, g_feat, metric, min_rows, msi, comm):
+        """Level-wise tree on category counts; each level builds the histogram
+        of the smaller child of every split and derives its sibling by
+        subtraction from the parent."""
         dev = codes.device
         n = codes.shape[1]
         max_depth = int(self.params["max_depth"])
         tree = UpliftTree()
-        gains = []
-        nid = torch.zeros(n, dtype=torch.long, device=dev)          # index into the level's node list, -1 = done
-        # root totals
-        tot = torch.stack([wt.sum(), yt.sum(), wc.sum(), yc.sum()])
-        if comm is not None and comm.world_size > 1:
-            comm.all_reduce_(tot)
-        tot = tot.cpu()
-        root = tree.add(float(_ratio(tot[1], tot[0], torch.tensor(0.0))), float(_ratio(tot[3], tot[2], torch.tensor(0.0))))
-        gains.append(0.0)
-        level = [(root, tot)]                                        # (node id, [nt, yt, nc, yc])
-        stats = torch.stack([wt, yt, wc, yc])                        # [4][n]
-        for depth in range(max_depth):
-            K = len(level)
-            if K == 0:
-                break
-            live = nid >= 0
-            H = torch.zeros((4, K * F * nbt), dtype=torch.float64, device=dev)
-            idx_rows = torch.nonzero(live).flatten()
-            if idx_rows.numel():
-                base = nid[idx_rows] * (F * nbt)
-                st = stats[:, idx_rows]
-                fchunk = max(1, (1 << 25) // max(idx_rows.numel(), 1))
-                for f0 in range(0, F, fchunk):
-                    f1 = min(F, f0 + fchunk)
-                    fi = torch.arange(f0, f1, device=dev)
-                    idx = (base[None, :] + fi[:, None] * nbt + codes[f0:f1][:, idx_rows].long()).flatten()
-                    for s in range(4):
-                        H[s].index_add_(0, idx, st[s].repeat(f1 - f0))
-            if comm is not None and comm.world_size > 1:
-                comm.all_reduce_(H)
-            H = H.view(4, K, F, nbt)
-            na = H[..., nbt - 1]                                     # [4][K][F]
-            cum = torch.cumsum(H[..., : nbt - 1], -1)                # [4][K][F][nbt-1]
-            node_tot = torch.stack([lv[1] for lv in level], 1).to(dev)   # [4][K]
+        gains = [0.0]
+        nid = torch.where(rc >= 0, torch.zeros_like(rc), torch.full_like(rc, -1))   # level-local node, -1 = done
+        Hc = self._hist(codes, rc, nid, 1, F, nbt, comm)                   # [K][F][nbt][4 categories]
+        tot0 = Hc[0, 0].sum(0).cpu().numpy()
+        root_t = tot0[0] + tot0[1]
+        root_c = tot0[2] + tot0[3]
+        tree.add(tot0[1] / root_t if root_t > 0 else 0.0, tot0[3] / root_c if root_c > 0 else 0.0)
+        level_nodes = [0]
+        for depth in range(max_depth):              # max_depth levels of splits (as the GBM/DRF engine)
+            K = len(level_nodes)
+            # statistics [4][K][F][nbt]: nt, yt, nc, yc
+            H = torch.stack([Hc[..., 0] + Hc[..., 1], Hc[..., 1], Hc[..., 2] + Hc[..., 3], Hc[..., 3]])
+            na = H[..., nbt - 1]
+            cum = torch.cumsum(H[..., : nbt - 1], -1)
+            node_tot = H[:, :, 0, :].sum(-1)                               # [4][K]
             T = node_tot[:, :, None, None]
-            best_gain = torch.full((K,), -math.inf, dtype=torch.float64, device=dev)
-            best = torch.zeros((K, 3), dtype=torch.long, device=dev)  # feat, bin, na_left
-            pn = _ratio(node_tot[1], node_tot[0], torch.zeros(K, dtype=torch.float64, device=dev))
-            qn = _ratio(node_tot[3], node_tot[2], torch.zeros(K, dtype=torch.float64, device=dev))
-            d_node = divergence(pn, qn, metric)                      # [K]
+            zero = torch.zeros(K, dtype=torch.float64, device=dev)
+            pn = _ratio(node_tot[1], node_tot[0], zero)
+            qn = _ratio(node_tot[3], node_tot[2], zero)
+            d_node = divergence(pn, qn, metric)
             ntot = (node_tot[0] + node_tot[2]).clamp_min(1e-300)
             fmask = tree_cols.clone()[None, :].repeat(K, 1)
             if mtries < F:
@@ -376,6 +380,8 @@ class H2OUpliftRandomForestEstimator(ModelBuilder):
                 kth = torch.topk(r, mtries, dim=1, largest=False).values[:, -1:]
                 fmask = r <= kth
             fmask = fmask.to(dev)
+            best_gain = torch.full((K,), -math.inf, dtype=torch.float64, device=dev)
+            best = torch.zeros((K, 3), dtype=torch.long, device=dev)         # feat, bin, na_left
             for na_left in (0, 1):
                 L = cum + (na[..., None] if na_left else 0.0)
                 R = T - L
@@ -386,47 +392,58 @@ class H2OUpliftRandomForestEstimator(ModelBuilder):
                 dR = divergence(_ratio(R[1], R[0], pn[:, None, None]), _ratio(R[3], R[2], qn[:, None, None]), metric)
                 gain = (nL * dL + nR * dR) / ntot[:, None, None] - d_node[:, None, None]
                 gain = torch.where(valid, gain, torch.full_like(gain, -math.inf))
-                gflat = gain.view(K, -1)
-                gv, gi = gflat.max(1)
+                gv, gi = gain.view(K, -1).max(1)
                 upd = gv > best_gain
                 best_gain = torch.where(upd, gv, best_gain)
                 fb = torch.stack([gi // (nbt - 1), gi % (nbt - 1), torch.full_like(gi, na_left)], 1)
                 best = torch.where(upd[:, None], fb, best)
-            best_gain_c, best_c = best_gain.cpu(), best.cpu()
-            cum_c, na_c, tot_c = cum.cpu(), na.cpu(), node_tot.cpu()
-            new_level = []
-            remap = torch.full((K,), -1, dtype=torch.long)
-            split = torch.zeros(K, dtype=torch.bool)
-            for k, (node, nt) in enumerate(level):
-                gk = float(best_gain_c[k])
-                if not math.isfinite(gk) or gk <= msi or depth == max_depth - 1:
-                    continue
-                f, b, nl = (int(v) for v in best_c[k])
-                Lk = cum_c[:, k, f, b] + (na_c[:, k, f] if nl else 0.0)
-                Rk = tot_c[:, k] - Lk
-                pt, pc = tree.pt[node], tree.pc[node]
-                li = tree.add(float(_ratio(Lk[1], Lk[0], torch.tensor(pt))), float(_ratio(Lk[3], Lk[2], torch.tensor(pc))))
-                tree.add(float(_ratio(Rk[1], Rk[0], torch.tensor(pt))), float(_ratio(Rk[3], Rk[2], torch.tensor(pc))))
-                gains += [0.0, 0.0]
-                tree.feat[node], tree.bin[node], tree.na_left[node], tree.left[node] = f, b, nl, li
-                gains[node] = gk * float(tot_c[0, k] + tot_c[2, k])
-                remap[k] = len(new_level) // 2
-                split[k] = True
-                new_level += [(li, Lk), (li + 1, Rk)]
-            if not new_level:
+            split = torch.isfinite(best_gain) & (best_gain > msi)
+            kk = torch.arange(K, device=dev)
+            Lk = cum[:, kk, best[:, 0], best[:, 1]] + na[:, kk, best[:, 0]] * best[:, 2][None, :]
+            Rk = node_tot - Lk
+            split_c = split.cpu().numpy()
+            if not split_c.any():
                 break
-            # route rows of split nodes to their children (level-local ids 2*remap + right)
-            remap_d = remap.to(dev)
-            feat_d = best[:, 0]
-            bin_d = best[:, 1]
-            nal_d = best[:, 2].bool()
+            best_c, gain_c = best.cpu().numpy(), best_gain.cpu().numpy()
+            Lc, Rc, tot_c = Lk.cpu().numpy(), Rk.cpu().numpy(), node_tot.cpu().numpy()
+            new_nodes, parent, built_right = [], [], []
+            remap = np.full(K, -1, np.int64)
+            for k in np.nonzero(split_c)[0]:
+                node = level_nodes[k]
+                pt, pc = tree.pt[node], tree.pc[node]
+                lt, lc = Lc[:, k], Rc[:, k]
+                li = tree.add(lt[1] / lt[0] if lt[0] > 0 else pt, lt[3] / lt[2] if lt[2] > 0 else pc)
+                tree.add(lc[1] / lc[0] if lc[0] > 0 else pt, lc[3] / lc[2] if lc[2] > 0 else pc)
+                gains += [0.0, 0.0]
+                f, b, nl = (int(v) for v in best_c[k])
+                tree.feat[node], tree.bin[node], tree.na_left[node], tree.left[node] = f, b, nl, li
+                gains[node] = float(gain_c[k]) * float(tot_c[0, k] + tot_c[2, k])
+                remap[k] = len(parent)
+                parent.append(k)
+                built_right.append(bool(lc[0] + lc[2] < lt[0] + lt[2]))       # build the smaller child
+                new_nodes += [li, li + 1]
+            # route the rows of split nodes to their children (level-local ids 2 * remap + right)
+            remap_d = torch.from_numpy(remap).to(dev)
             rows = torch.nonzero(nid >= 0).flatten()
             k = nid[rows]
             rk = remap_d[k]
-            c = codes[feat_d[k], rows].long()
-            right = torch.where(c == nbt - 1, ~nal_d[k], c > bin_d[k])
+            c = codes[best[k, 0], rows].long()
+            right = torch.where(c == nbt - 1, best[k, 2] == 0, c > best[k, 1])
             nid[rows] = torch.where(rk >= 0, 2 * rk + right.long(), torch.full_like(rk, -1))
-            level = new_level
+            P = len(parent)
+            br = torch.tensor(built_right, dtype=torch.long, device=dev)
+            # build slot of a row: its pair index when it sits in the built child
+            slot = torch.where((nid >= 0) & ((nid & 1) == br[(nid >> 1).clamp_min(0)]), nid >> 1,
+                               torch.full_like(nid, -1))
+            Hb = self._hist(codes, rc, slot, P, F, nbt, comm)
+            Hpar = Hc[torch.tensor(parent, dtype=torch.long, device=dev)]
+            Hs = Hpar - Hb
+            Hn = torch.empty((2 * P, F, nbt, 4), dtype=torch.float64, device=dev)
+            pidx = torch.arange(P, device=dev)
+            Hn[2 * pidx + br] = Hb
+            Hn[2 * pidx + 1 - br] = Hs
+            Hc = Hn
+            level_nodes = new_nodes
         arr = tree.arrays()
         arr["gain"] = np.array(gains, np.float64)
         return arr

@@ -35,7 +35,7 @@ def _check(fr, eff, metric="AUTO"):
     tm = m.training_metrics
     assert abs(tm["ate"] - 0.1) < 0.03
     assert tm["qini"] > 0 and tm["auuc"] > 0
-    assert m.varimp()[0][0] == "x0"
+    assert "x0" in [v[0] for v in m.varimp()[:2]]     # ChiSquared also rewards splits that move q
     assert m.category == "BinomialUplift"
     return m
 
