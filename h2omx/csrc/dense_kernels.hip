@@ -30,6 +30,7 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 // ===========================================================================
 struct GlmParams {
   int family;  // 0 gaussian 1 binomial 2 poisson 3 gamma 4 tweedie 5 multinomial 6 quasibinomial
+               // (also fractionalbinomial) 7 negativebinomial
   int link;    // 0 identity 1 logit 2 log 3 inverse 4 tweedie-power
   int p;       // features (without intercept)
   int K;       // classes for multinomial, else 1
@@ -71,6 +72,7 @@ __device__ __forceinline__ double glm_var(const GlmParams& P, double mu) {
     case 2: return fmax(mu, 1e-10);
     case 3: return fmax(mu * mu, 1e-20);
     case 4: return fmax(pow(fmax(mu, 1e-10), P.var_power), 1e-20);
+    case 7: return fmax(mu + P.var_power * mu * mu, 1e-10);   // negative binomial, var_power = theta
     default: return 1.0;
   }
 }
@@ -93,6 +95,11 @@ __device__ __forceinline__ double glm_dev(const GlmParams& P, double y, double m
       const double r = P.var_power, m = fmax(mu, 1e-15);
       const double a = (y > 0) ? pow(y, 2 - r) / ((1 - r) * (2 - r)) : 0.0;
       return 2.0 * (a - y * pow(m, 1 - r) / (1 - r) + pow(m, 2 - r) / (2 - r));
+    }
+    case 7: {  // negative binomial (theta = var_power)
+      const double th = P.var_power, m = fmax(mu, 1e-15);
+      const double a = (y > 0) ? y * log(y / m) : 0.0;
+      return 2.0 * (a - (y + 1.0 / th) * log((1.0 + th * y) / (1.0 + th * m)));
     }
     default: return (y - mu) * (y - mu);
   }

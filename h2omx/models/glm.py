@@ -7,8 +7,10 @@ weighted Gram of [X | 1 | z] on the fp32 matrix cores, reduced in fp64 and
 sub-problem is solved on the host by Cholesky (ridge) or cyclic coordinate
 descent on the Gram (lasso / elastic net), like H2O's IRLSM solver.
 
-Families: gaussian, binomial, quasibinomial, poisson, gamma, tweedie,
-multinomial (per-class cyclic IRLS).  Standardization, one-hot categorical
+Families: gaussian, binomial, quasibinomial, fractionalbinomial, poisson,
+gamma, tweedie, negativebinomial (fixed ``theta``), multinomial (per-class
+cyclic IRLS) and ordinal (cumulative logit, L-BFGS; models/glm_extras.py).
+``interactions`` / ``interaction_pairs`` add H2O-style interaction columns.  Standardization, one-hot categorical
 expansion (first level dropped, H2O's use_all_factor_levels=False), mean
 imputation of NAs, lambda search, p-values (lambda = 0) and the H2O output
 fields (coefficients, standardized coefficients, deviances, AIC) are
@@ -178,9 +180,19 @@ class GLMModel(Model):
         return out
 
     def predict_raw(self, frame: Frame) -> torch.Tensor:
+        spec = getattr(self, "interaction_spec", None)
+        if spec:
+            from .glm_extras import apply_interactions
+
+            frame = apply_interactions(frame, spec)
         Xs = self.design.transform(self.design.raw_matrix(frame))
         b = torch.from_numpy(self.beta_std.astype(np.float64)).to(Xs.device)
         p = Xs.shape[0]
+        if self.family == "ordinal":
+            from .glm_extras import ordinal_probs
+
+            th = torch.tensor(self.stats["ordinal_thresholds"], dtype=torch.float64, device=Xs.device)
+            return ordinal_probs(Xs.double(), b[0, :p], th).float()
         eta = b[:, :p] @ Xs.double() + b[:, p:p + 1]
         if self.params.get("offset_column"):
             eta = eta + frame.vec(self.params["offset_column"]).as_float().double()[None, :]
@@ -246,12 +258,36 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
                     max_iterations=-1, beta_epsilon=1e-4, objective_epsilon=-1.0, gradient_epsilon=-1.0,
                     non_negative=False, compute_p_values=False, remove_collinear_columns=False,
                     missing_values_handling="MeanImputation", tweedie_variance_power=0.0, tweedie_link_power=1.0,
-                    use_all_factor_levels=False, offset_column=None, prior=-1.0, balance_classes=False)
+                    use_all_factor_levels=False, offset_column=None, prior=-1.0, balance_classes=False,
+                    theta=1e-10, interactions=None, interaction_pairs=None)
 
     def __init__(self, **params):
         if "lambda" in params:
             params["lambda_"] = params.pop("lambda")
         super().__init__(**params)
+
+    def train(self, x=None, y=None, training_frame=None, validation_frame=None, comm=None, **kw):
+        """``interactions`` / ``interaction_pairs``: the frames gain the
+        interaction columns (glm_extras) before the usual fit; the spec is kept
+        on the model so scoring frames are augmented identically."""
+        from .glm_extras import apply_interactions, build_interaction_spec, interaction_columns, interaction_pairs
+
+        self.params.update(kw)
+        pairs = interaction_pairs(self.params, x, training_frame) if training_frame is not None else []
+        if not pairs:
+            return super().train(x=x, y=y, training_frame=training_frame, validation_frame=validation_frame,
+                                 comm=comm)
+        spec = build_interaction_spec(training_frame, pairs, comm)
+        aug = apply_interactions(training_frame, spec)
+        vaug = apply_interactions(validation_frame, spec) if validation_frame is not None else None
+        special = {y, self.params.get("weights_column"), self.params.get("fold_column"),
+                   self.params.get("offset_column")}
+        ign = set(self.params.get("ignored_columns") or [])
+        base_x = list(x) if x is not None else [n for n in training_frame.names if n not in special and n not in ign]
+        model = super().train(x=base_x + interaction_columns(spec), y=y, training_frame=aug, validation_frame=vaug,
+                              comm=comm)
+        model.interaction_spec = spec
+        return model
 
     def _family(self):
         fam = str(self.params["family"]).lower()
@@ -259,6 +295,9 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
             return {ModelCategory.BINOMIAL: "binomial", ModelCategory.MULTINOMIAL: "multinomial"}.get(
                 self.category, "gaussian")
         return fam
+
+    def _fit_ordinal(self, X, y, w, N, design, lam_param, alpha, model_id):
+        return _fit_ordinal_impl(self, X, y, w, N, design, lam_param, alpha, model_id)
 
     def _penalty_matrix(self, design):
         """Quadratic coefficient penalty (raw scale, p×p) added to the IRLS normal
@@ -288,6 +327,8 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
         del Xraw
         p = X.shape[0]
         K = len(self.response_domain) if family == "multinomial" else 1
+        if family == "ordinal" and not self.response_domain:
+            raise ValueError("glm: family='ordinal' needs a categorical response")
         # optional quadratic penalty on the raw-scale coefficients (GAM), moved to the
         # standardised scale: b_raw = b_std / sd  ->  P_std = D⁻¹ P D⁻¹
         pen_raw = self._penalty_matrix(design)
@@ -295,7 +336,7 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
         alpha = p_["alpha"]
         alpha = (0.0 if p_["solver"] == "L_BFGS" else 0.5) if alpha is None else float(alpha[0] if isinstance(alpha, (list, tuple)) else alpha)
         lam_param = p_["lambda_"] if p_["lambda_"] is not None else p_["Lambda"]
-        var_power = float(p_["tweedie_variance_power"] or 1.5)
+        var_power = float(p_["theta"]) if family == "negativebinomial" else float(p_["tweedie_variance_power"] or 1.5)
         link_power = float(p_["tweedie_link_power"]) if family == "tweedie" else 0.0
         if family == "tweedie" and link_power != 0.0 and link == "tweedie":
             pass
@@ -318,10 +359,12 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
         N = float(ysum[1])
         ybar = float(ysum[0]) / max(N, 1e-300)
         beta = np.zeros((K, p + 1))
-        if family in ("binomial", "quasibinomial"):
+        if family == "ordinal":
+            return self._fit_ordinal(X, y, w, N, design, lam_param, alpha, model_id)
+        if family in ("binomial", "quasibinomial", "fractionalbinomial"):
             pb = min(max(ybar, 1e-10), 1 - 1e-10)
             beta[0, p] = math.log(pb / (1 - pb))
-        elif family in ("poisson", "gamma") or (family == "tweedie" and link_power == 0.0):
+        elif family in ("poisson", "gamma", "negativebinomial") or (family == "tweedie" and link_power == 0.0):
             beta[0, p] = math.log(max(ybar, 1e-10)) if link in ("log", "tweedie") else (1.0 / ybar if link == "inverse" else ybar)
         elif family == "multinomial":
             ycpu = y.long()
@@ -372,6 +415,29 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
         model = GLMModel(self, model_id, design, beta, family, link, stats)
         model.scoring_history = history
         return model
+
+
+def _fit_ordinal_impl(est, X, y, w, N, design, lam_param, alpha, model_id):
+    from .glm_extras import fit_ordinal
+
+    K = len(est.response_domain)
+    lam = 0.0 if lam_param is None else float(lam_param[0] if isinstance(lam_param, (list, tuple)) else lam_param)
+    b, th, nll, nit = fit_ordinal(X, y, w, K, lam, alpha, est.comm,
+                                  max_iter=int(est.params["max_iterations"]) if int(est.params["max_iterations"]) > 0
+                                  else 200)
+    p = X.shape[0]
+    beta = np.zeros((1, p + 1))
+    beta[0, :p] = b
+    wd = w.double() if w is not None else torch.ones(y.numel(), dtype=torch.float64, device=y.device)
+    cnt = torch.bincount(y.long(), weights=wd, minlength=K).double()
+    if est.comm is not None and est.comm.world_size > 1:
+        est.comm.all_reduce_(cnt)
+    pr = (cnt / cnt.sum()).clamp_min(1e-15)
+    null_dev = float(-2 * (cnt * torch.log(pr)).sum())
+    stats = {"lambda": lam, "iterations": nit, "null_deviance": null_dev, "residual_deviance": 2 * nll,
+             "lambda_max": 0.0, "nobs": N, "ordinal_thresholds": th.tolist(),
+             "aic": 2 * nll + 2 * (p + K - 1)}
+    return GLMModel(est, model_id, design, beta, "ordinal", "ologit", stats)
 
 
 def _p_values(G, p, family, dev, N, k_active, design, beta_std):

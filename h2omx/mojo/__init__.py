@@ -184,6 +184,8 @@ def mojo_bytes(model: Model) -> bytes:
         columns = list(model.x)
         info.update(_tree_info(model, files))
     elif algo == "glm":
+        if getattr(model, "interaction_spec", None) or model.family == "ordinal":
+            raise NotImplementedError("MOJO export of GLMs with interactions or the ordinal family")
         cats, nums = _design_columns(model.design)
         columns = cats + nums
         info.update(_glm_info(model, cats, nums))

@@ -19,10 +19,11 @@ from . import P, check, dense_lib, stream
 KBADARG = 1  # common.h kBadArg
 
 FAMILIES = {"gaussian": 0, "binomial": 1, "poisson": 2, "gamma": 3, "tweedie": 4, "multinomial": 5,
-            "quasibinomial": 6}
+            "quasibinomial": 6, "fractionalbinomial": 6, "negativebinomial": 7}
 LINKS = {"identity": 0, "logit": 1, "log": 2, "inverse": 3, "tweedie": 4}
 DEFAULT_LINK = {"gaussian": "identity", "binomial": "logit", "quasibinomial": "logit", "poisson": "log",
-                "gamma": "inverse", "tweedie": "tweedie", "multinomial": "logit"}
+                "gamma": "inverse", "tweedie": "tweedie", "multinomial": "logit", "fractionalbinomial": "logit",
+                "negativebinomial": "log", "ordinal": "ologit"}
 
 
 class GlmParams(ctypes.Structure):
@@ -89,8 +90,10 @@ def _linkinv(eta, link, link_power=0.0):
 
 
 def glm_variance(family, mu, var_power=1.5):
-    if family in ("binomial", "quasibinomial"):
+    if family in ("binomial", "quasibinomial", "fractionalbinomial"):
         return np.maximum(mu * (1 - mu), 1e-10)
+    if family == "negativebinomial":                       # var_power carries theta
+        return np.maximum(mu + var_power * mu * mu, 1e-10)
     if family == "poisson":
         return np.maximum(mu, 1e-10)
     if family == "gamma":
@@ -101,7 +104,12 @@ def glm_variance(family, mu, var_power=1.5):
 
 
 def glm_deviance(family, y, mu, var_power=1.5):
-    if family in ("binomial", "quasibinomial"):
+    if family == "negativebinomial":
+        th, m = var_power, np.maximum(mu, 1e-15)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            a = np.where(y > 0, y * np.log(np.where(y > 0, y, 1) / m), 0.0)
+        return 2 * (a - (y + 1 / th) * np.log((1 + th * y) / (1 + th * m)))
+    if family in ("binomial", "quasibinomial", "fractionalbinomial"):
         m = np.clip(mu, 1e-15, 1 - 1e-15)
         return -2 * (y * np.log(m) + (1 - y) * np.log(1 - m))
     if family == "poisson":
