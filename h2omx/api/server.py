@@ -147,6 +147,16 @@ def coerce(value, default):
 _REST_ALIASES = {"lambda": "lambda_", "alpha": "alpha"}
 
 
+def _predict_kind(params) -> str:
+    """/3/Predictions flags (H2O PredictionsHandler): contributions, leaf node
+    assignment, staged probabilities or feature frequencies instead of scores."""
+    for flag, kind in (("predict_contributions", "contributions"), ("leaf_node_assignment", "leaf_nodes"),
+                       ("predict_staged_proba", "staged_proba"), ("feature_frequencies", "feature_frequencies")):
+        if str(params.get(flag, "false")).lower() == "true":
+            return kind
+    return "predict"
+
+
 class H2OApi:
     """Route table + handlers; transport-independent (tests call ``handle``)."""
 
@@ -706,14 +716,15 @@ class H2OApi:
         if not isinstance(DKV.get(fid), Frame):
             raise KeyError(fid)
         dest = params.get("predictions_frame") or f"prediction_{uuid.uuid4().hex[:10]}"
-        kind = "contributions" if str(params.get("predict_contributions", "false")).lower() == "true" else "predict"
-        self.cluster.run("predict", model=m.model_id, frame=fid, dest=dest, kind=kind)
+        kind = _predict_kind(params)
+        self.cluster.run("predict", model=m.model_id, frame=fid, dest=dest, kind=kind,
+                         leaf_type=params.get("leaf_node_assignment_type") or "Path")
         return m, dest
 
     def predict(self, mid, fid, params, **_):
         m, dest = self._predict(mid, fid, params)
         mm = None
-        if str(params.get("predict_contributions", "false")).lower() == "true":
+        if _predict_kind(params) != "predict":
             return {"__meta": S.meta("ModelMetricsListSchemaV3", "Iced"), "model_metrics": [],
                     "predictions_frame": S.key_ref(dest, "Key<Frame>")}
         if m.y is not None and m.y in DKV.get(unquote(fid)).names:

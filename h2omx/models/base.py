@@ -149,6 +149,37 @@ class Model:
 
         return predict_contributions(self, frame)
 
+    # -- h2omx.explain_more (H2O model introspection APIs) ---------------------
+    def predict_leaf_node_assignment(self, frame: Frame, type: str = "Path") -> Frame:  # noqa: A002
+        from ..explain_more import predict_leaf_node_assignment
+
+        return predict_leaf_node_assignment(self, frame, type)
+
+    def staged_predict_proba(self, frame: Frame) -> Frame:
+        from ..explain_more import staged_predict_proba
+
+        return staged_predict_proba(self, frame)
+
+    def feature_frequencies(self, frame: Frame) -> Frame:
+        from ..explain_more import feature_frequencies
+
+        return feature_frequencies(self, frame)
+
+    def fairness_metrics(self, frame: Frame, protected_columns, reference=None, favorable_class=None) -> dict:
+        from ..explain_more import fairness_metrics
+
+        return fairness_metrics(self, frame, protected_columns, reference, favorable_class, self.comm)
+
+    def ice(self, frame: Frame, column: str, nbins: int = 20, target=None) -> dict:
+        from ..explain_more import ice
+
+        return ice(self, frame, column, nbins, target)
+
+    def explain(self, frame: Frame, **kw) -> dict:
+        from ..explain_more import explain
+
+        return explain([self], frame, **kw)
+
     def partial_dependence(self, frame: Frame, cols=None, nbins: int = 20, target=None) -> list[dict]:
         from ..explain import partial_dependence
 

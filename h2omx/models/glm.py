@@ -203,6 +203,12 @@ class GLMModel(Model):
             return torch.stack([1 - mu, mu]).float()
         return mu[None, :].float()
 
+    def predict_contributions(self, frame: Frame) -> Frame:
+        """Exact linear SHAP values in link space (explain_more.glm_contributions)."""
+        from ..explain_more import glm_contributions
+
+        return glm_contributions(self, frame)
+
     def varimp(self):
         b = np.abs(self.beta_std[:, :-1]).sum(0)
         if b.max() <= 0:

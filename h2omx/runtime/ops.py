@@ -180,13 +180,17 @@ def op_train(cl, algo, params, x=None, y=None, training_frame=None, validation_f
     return m.model_id
 
 
-def op_predict(cl, model, frame, dest, kind="predict"):
+def op_predict(cl, model, frame, dest, kind="predict", leaf_type="Path"):
     m = _model(model)
     fr = _frame(frame)
     if kind == "contributions":
-        from ..explain import predict_contributions
-
-        pf = predict_contributions(m, fr)
+        pf = m.predict_contributions(fr)
+    elif kind == "leaf_nodes":
+        pf = m.predict_leaf_node_assignment(fr, leaf_type)
+    elif kind == "staged_proba":
+        pf = m.staged_predict_proba(fr)
+    elif kind == "feature_frequencies":
+        pf = m.feature_frequencies(fr)
     else:
         pf = m.predict(fr)
     pf.key = dest
