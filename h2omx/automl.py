@@ -1,5 +1,8 @@
 """AutoML (H2O AutoML equivalent): trains a fixed sequence of algorithm
-presets, then random-grid GBM models, under a model-count / runtime budget,
+presets, then random-grid XGBoost / GBM / DeepLearning models (round-robin),
+under a model-count / runtime budget (``max_runtime_secs_per_model`` caps
+each model through its own ``max_runtime_secs``), optionally restricted by a
+``modeling_plan``; re-running a ``project_name`` extends its leaderboard;
 cross-validates every model with shared folds, and finishes with two
 Stacked Ensembles (all models, best of family).  Models are ranked on a
 leaderboard by the H2O default metric for the problem type.
@@ -50,6 +53,19 @@ PRESETS = [
 GRID = dict(max_depth=[3, 4, 5, 6, 7, 8, 9, 10, 12, 15], min_rows=[1, 5, 10, 15, 30, 100],
             sample_rate=[0.5, 0.6, 0.7, 0.8, 0.9, 1.0], col_sample_rate=[0.4, 0.7, 1.0],
             col_sample_rate_per_tree=[0.4, 0.7, 1.0], learn_rate=[0.05, 0.1])
+# random-grid spaces after the presets (H2O AutoML's XGBoost / GBM / DeepLearning grids)
+GRIDS = {
+    "gbm": (H2OGradientBoostingEstimator, GRID),
+    "xgboost": (H2OXGBoostEstimator, dict(max_depth=[3, 6, 9, 12, 15], min_child_weight=[1, 3, 5, 10, 15],
+                                          sample_rate=[0.6, 0.8, 1.0], col_sample_rate=[0.6, 0.8, 1.0],
+                                          col_sample_rate_per_tree=[0.7, 0.8, 0.9, 1.0],
+                                          reg_lambda=[0.001, 0.01, 0.1, 1.0, 10.0], reg_alpha=[0.001, 0.01, 0.1, 0.5, 1.0],
+                                          learn_rate=[0.05, 0.1, 0.3])),
+    "deeplearning": (H2ODeepLearningEstimator, dict(hidden=[[20], [50], [100], [20, 20], [50, 50], [100, 100]],
+                                                    epochs=[10], input_dropout_ratio=[0.0, 0.05, 0.1],
+                                                    rho=[0.9, 0.95, 0.99], epsilon=[1e-6, 1e-7, 1e-8])),
+}
+_PROJECTS: dict = {}
 
 
 def _metric_spec(category, sort_metric):
@@ -67,20 +83,34 @@ class H2OAutoML:
     def __init__(self, max_models=None, max_runtime_secs=None, max_runtime_secs_per_model=0.0, nfolds=-1, seed=-1,
                  project_name=None, include_algos=None, exclude_algos=None, sort_metric="AUTO",
                  keep_cross_validation_predictions=True, stopping_rounds=3, stopping_tolerance=None,
-                 stopping_metric="AUTO", balance_classes=False, verbosity="warn", **_ignored):
+                 stopping_metric="AUTO", balance_classes=False, verbosity="warn", modeling_plan=None,
+                 preprocessing=None, exploitation_ratio=-1.0, **_ignored):
         self.max_models = max_models
         self.max_runtime_secs = max_runtime_secs
+        self.max_runtime_secs_per_model = float(max_runtime_secs_per_model or 0.0)
         self.nfolds = 5 if nfolds in (-1, None) else int(nfolds)
         self.seed = seed
         self.project_name = project_name or f"AutoML_{uuid.uuid4().hex[:8]}"
         inc = [a.lower() for a in include_algos] if include_algos else [a.lower() for a in ALGOS]
         exc = {a.lower() for a in (exclude_algos or [])}
         self.algos = [a for a in inc if a not in exc]
+        self.plan = _parse_plan(modeling_plan) if modeling_plan else None
+        if self.plan is not None:
+            self.algos = [a for a in self.algos if a in self.plan or a == "stackedensemble"]
         self.sort_metric = sort_metric
+        self.stopping = dict(stopping_rounds=int(stopping_rounds or 0), stopping_metric=stopping_metric,
+                             stopping_tolerance=stopping_tolerance)
+        self.preprocessing = preprocessing
         self.events: list[dict] = []
         self.models: list = []
         self.leaderboard: list[dict] = []
         self.leader = None
+        self.training_info: dict = {}
+        prev = _PROJECTS.get(self.project_name)
+        if prev is not None:                      # H2O: same project_name -> extend its leaderboard
+            self.models = list(prev.models)
+            self.events = list(prev.events)
+        _PROJECTS[self.project_name] = self
 
     def _log(self, stage, msg):
         self.events.append({"t": time.strftime("%H:%M:%S"), "stage": stage, "msg": msg})
@@ -105,6 +135,14 @@ class H2OAutoML:
         def fit(name, cls, params):
             nonlocal category
             mid = f"{name}_AutoML_{self.project_name}"
+            if any(m.model_id == mid for m in self.models):
+                mid = f"{mid}_{len(self.models)}"
+            rt = self.max_runtime_secs_per_model
+            if budget:
+                left = max(budget - (time.time() - t0), 1.0)
+                rt = min(rt, left) if rt else left
+            if rt:
+                params = dict(params, max_runtime_secs=rt)
             try:
                 est = cls(model_id=mid, **params, **cv)
                 m = est.train(x=x, y=y, training_frame=training_frame, validation_frame=validation_frame, comm=comm)
@@ -117,19 +155,31 @@ class H2OAutoML:
             return m
 
         self._log("Workflow", f"AutoML build started: {self.project_name}")
+        if self.preprocessing:
+            self._log("Workflow", f"preprocessing {self.preprocessing} not applied (models see the raw columns)")
+        start_models = len(self.models)
+        if self.max_models:
+            self.max_models = int(self.max_models) + start_models
         for algo, suffix, cls, params in PRESETS:
-            if algo.lower() not in self.algos:
+            if algo.lower() not in self.algos or not self._planned(algo, "defaults"):
                 continue
             if out_of_budget():
                 break
             fit(f"{algo}_{suffix}", cls, dict(params))
-        g = 1
-        while "gbm" in self.algos and not out_of_budget() and (self.max_models or budget):
-            params = {k: v[int(rng.integers(len(v)))] for k, v in GRID.items()}
-            fit(f"GBM_grid_1_model_{g}", H2OGradientBoostingEstimator, params)
-            g += 1
-            if g > 200:
-                break
+        # random grids, round-robin over the families still allowed
+        fams = [f for f in ("xgboost", "gbm", "deeplearning") if f in self.algos and self._planned(f, "grids")]
+        counters = {f: 1 for f in fams}
+        name = {"xgboost": "XGBoost", "gbm": "GBM", "deeplearning": "DeepLearning"}
+        while fams and not out_of_budget() and (self.max_models or budget) and sum(counters.values()) < 300:
+            for f in list(fams):
+                if out_of_budget():
+                    break
+                cls, space = GRIDS[f]
+                params = {k: v[int(rng.integers(len(v)))] for k, v in space.items()}
+                if f != "deeplearning":
+                    params.update({k: v for k, v in self.stopping.items() if v is not None})
+                fit(f"{name[f]}_grid_1_model_{counters[f]}", cls, params)
+                counters[f] += 1
         base = [m for m in self.models if m.cross_validation_holdout is not None]
         if "stackedensemble" in self.algos and self.nfolds > 1 and len(base) >= 2 and category != ModelCategory.CLUSTERING:
             for name, members in (("StackedEnsemble_AllModels", base),
@@ -147,7 +197,62 @@ class H2OAutoML:
                     self._log("ModelTraining", f"{name} failed: {type(e).__name__}: {e}")
         self._rank(category, leaderboard_frame, comm)
         self._log("Workflow", f"AutoML build done: {len(self.models)} models in {time.time() - t0:.1f}s")
+        self.training_info = {"start_epoch": int(t0), "stop_epoch": int(time.time()),
+                              "duration_secs": round(time.time() - t0, 3), "models": len(self.models),
+                              "leader": self.leader.model_id if self.leader is not None else None}
+        self._x, self._frame = x, training_frame
         return self
+
+    def _planned(self, algo: str, kind: str) -> bool:
+        if self.plan is None:
+            return True
+        steps = self.plan.get(algo.lower())
+        return steps is not None and (kind in steps or "all" in steps)
+
+    def get_best_model(self, algorithm: str | None = None, criterion: str | None = None):
+        """Best model overall, or of one algorithm family, by ``criterion``
+        (a leaderboard column; default: the sort metric)."""
+        rows = self.leaderboard
+        if algorithm:
+            a = algorithm.lower()
+            a = {"basemodel": None}.get(a, a)
+            rows = [r for r in rows if (r["algo"] != "stackedensemble" if a is None else r["algo"] == a)]
+        if not rows:
+            return None
+        if criterion:
+            c = criterion.lower()
+            higher = c in ("auc", "aucpr")
+            rows = sorted(rows, key=lambda r: (np.isnan(r.get(c, np.nan)), -r.get(c, np.nan) if higher
+                                               else r.get(c, np.nan)))
+        return DKV.get(rows[0]["model_id"])
+
+    def get_leaderboard(self, extra_columns=None) -> list[dict]:
+        """Leaderboard rows; ``extra_columns="ALL"`` adds training_time_ms and
+        predict_time_per_row_ms (timed on up to 10k training rows)."""
+        import torch
+
+        rows = [dict(r) for r in self.leaderboard]
+        extra = extra_columns if isinstance(extra_columns, (list, tuple)) else \
+            (["training_time_ms", "predict_time_per_row_ms"] if str(extra_columns).upper() == "ALL" else [])
+        fr = getattr(self, "_frame", None)
+        for r in rows:
+            m = DKV.get(r["model_id"])
+            if "training_time_ms" in extra:
+                r["training_time_ms"] = int(getattr(m, "run_time_ms", 0))
+            if "predict_time_per_row_ms" in extra and fr is not None:
+                sub = fr.rows(torch.arange(min(fr.nrows, 10000), device=fr.device))
+                t = time.perf_counter()
+                m.predict_raw(sub)
+                if sub.device.type == "cuda":
+                    torch.cuda.synchronize(sub.device)
+                r["predict_time_per_row_ms"] = (time.perf_counter() - t) * 1000 / max(sub.nrows, 1)
+        return rows
+
+    @property
+    def event_log(self) -> Frame:
+        import pandas as pd
+
+        return Frame.from_pandas(pd.DataFrame(self.events or [{"t": "", "stage": "", "msg": ""}]))
 
     def _score(self, m, key, lb_frame, comm):
         if lb_frame is not None:
@@ -204,6 +309,26 @@ class H2OAutoML:
         return Frame.from_pandas(pd.DataFrame(self.leaderboard))
 
 
+def _parse_plan(plan) -> dict:
+    """modeling_plan: ["GBM", ("XGBoost", "grids"), {"name": "DRF", "alias": "defaults"}, ...]
+    -> {algo: {"defaults", "grids", ...}}."""
+    out: dict = {}
+    for item in plan:
+        if isinstance(item, str):
+            out[item.lower()] = {"all"}
+        elif isinstance(item, dict):
+            steps = item.get("steps") or [item.get("alias", "all")]
+            out[str(item["name"]).lower()] = {str(s.get("id", s) if isinstance(s, dict) else s).lower() for s in steps}
+        else:
+            out[str(item[0]).lower()] = {str(s).lower() for s in (item[1] if isinstance(item[1], (list, tuple))
+                                                                  else [item[1]])}
+    return out
+
+
+def get_automl(project_name: str):
+    return _PROJECTS.get(project_name)
+
+
 def run_automl(spec: dict, comm=None) -> dict:
     """REST entry (/99/AutoMLBuilder JSON spec) executed on every rank."""
     bc = spec.get("build_control", {}) or {}
@@ -211,9 +336,12 @@ def run_automl(spec: dict, comm=None) -> dict:
     bm = spec.get("build_models", {}) or {}
     sc = bc.get("stopping_criteria", {}) or {}
     aml = H2OAutoML(max_models=sc.get("max_models"), max_runtime_secs=sc.get("max_runtime_secs"),
+                    max_runtime_secs_per_model=sc.get("max_runtime_secs_per_model", 0.0),
                     seed=sc.get("seed", -1), nfolds=bc.get("nfolds", -1), project_name=bc.get("project_name"),
                     include_algos=bm.get("include_algos"), exclude_algos=bm.get("exclude_algos"),
-                    sort_metric=isp.get("sort_metric", "AUTO"))
+                    sort_metric=isp.get("sort_metric", "AUTO"), modeling_plan=bm.get("modeling_plan"),
+                    stopping_rounds=sc.get("stopping_rounds", 3), stopping_metric=sc.get("stopping_metric", "AUTO"),
+                    stopping_tolerance=sc.get("stopping_tolerance"), preprocessing=bm.get("preprocessing"))
     tf = DKV.get(_key(isp.get("training_frame")))
     lf = DKV.get(_key(isp.get("leaderboard_frame"))) if isp.get("leaderboard_frame") else None
     y = isp.get("response_column")

@@ -212,7 +212,13 @@ class _TreeScoring:
         self.multi = comm is not None and comm.world_size > 1
         # cancellation is decided collectively so every rank stops on the same tree
         self.cancel_every = 10 if self.multi else 1
-        self.active = bool(self.interval) or self.job is not None or self.multi
+        # H2O max_runtime_secs: stop adding trees once the budget is spent (decided
+        # collectively with the cancellation flag)
+        import time as _time
+
+        self.t_start = _time.time()
+        self.max_rt = float(builder.params.get("max_runtime_secs") or 0.0)
+        self.active = bool(self.interval) or self.job is not None or self.multi or self.max_rt > 0
 
     @property
     def history(self):
@@ -226,7 +232,11 @@ class _TreeScoring:
         if self.job is not None:
             self.job.progress = (t + 1) / max(1, int(self.b.params["ntrees"]))
         if (t + 1) % self.cancel_every == 0:
+            import time as _time
+
             flag = 1.0 if (self.job is not None and self.job.cancel_requested) else 0.0
+            if self.max_rt > 0 and _time.time() - self.t_start > self.max_rt:
+                flag = 1.0
             if self.multi:
                 flag = float(self.b.comm.all_reduce_numpy(np.array([flag]), "max")[0])
             if flag > 0:

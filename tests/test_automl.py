@@ -1,0 +1,62 @@
+"""AutoML: presets + round-robin grids under a model budget, leaderboard
+ordering and extra columns, get_best_model, modeling_plan, project
+continuation, per-model runtime caps (tree models stop adding trees)."""
+import time
+
+import numpy as np
+import pandas as pd
+
+from h2omx.automl import H2OAutoML, get_automl
+from h2omx.frame import Frame
+from h2omx.models import H2OGradientBoostingEstimator
+
+
+def _frame(n=800, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, 4))
+    df = pd.DataFrame(X, columns=list("abcd"))
+    df["y"] = pd.Categorical(np.where(X[:, 0] - X[:, 1] + 0.3 * rng.normal(size=n) > 0, "yes", "no"))
+    return Frame.from_pandas(df)
+
+
+def test_automl_budget_leaderboard_and_helpers():
+    fr = _frame()
+    aml = H2OAutoML(max_models=6, nfolds=3, seed=1, project_name="t_aml",
+                    exclude_algos=["DeepLearning"]).train(y="y", training_frame=fr)
+    lb = aml.leaderboard
+    base = [r for r in lb if r["algo"] != "stackedensemble"]
+    assert len(base) == 6
+    aucs = [r["auc"] for r in lb]
+    assert aucs == sorted(aucs, reverse=True)
+    assert aml.leader.model_id == lb[0]["model_id"]
+    ext = aml.get_leaderboard("ALL")
+    assert all(r["training_time_ms"] >= 0 and r["predict_time_per_row_ms"] > 0 for r in ext)
+    best_gbm = aml.get_best_model(algorithm="gbm")
+    assert best_gbm is not None and best_gbm.algo == "gbm"
+    worst = aml.get_best_model(criterion="logloss")
+    assert worst is not None
+    assert get_automl("t_aml") is aml
+    assert aml.event_log.nrows >= 6
+    assert aml.training_info["models"] == len(aml.models)
+    # same project_name: the leaderboard grows
+    aml2 = H2OAutoML(max_models=2, nfolds=3, seed=2, project_name="t_aml", include_algos=["GLM", "DRF"]).train(
+        y="y", training_frame=fr)
+    assert len(aml2.models) > len(aml.models)
+
+
+def test_modeling_plan_and_grids():
+    fr = _frame(500)
+    aml = H2OAutoML(max_models=4, nfolds=0, seed=3, modeling_plan=[("XGBoost", "grids"), ("GBM", "grids")]).train(
+        y="y", training_frame=fr)
+    ids = [m.model_id for m in aml.models]
+    assert all("_grid_1_model_" in i for i in ids)
+    assert {m.algo for m in aml.models} == {"xgboost", "gbm"}
+
+
+def test_max_runtime_secs_stops_trees():
+    fr = _frame(3000)
+    t = time.time()
+    m = H2OGradientBoostingEstimator(ntrees=100000, max_depth=3, max_runtime_secs=1.0, seed=1).train(
+        y="y", training_frame=fr)
+    assert time.time() - t < 30
+    assert 0 < m.ens.ntrees < 100000
