@@ -10,6 +10,7 @@ from .generic import H2OGenericEstimator  # noqa: F401
 from .glm import H2OGeneralizedLinearEstimator  # noqa: F401
 from .gam import H2OGeneralizedAdditiveEstimator  # noqa: F401
 from .glrm import H2OGeneralizedLowRankEstimator  # noqa: F401
+from .hglm import H2OHGLMEstimator  # noqa: F401
 from .infogram import H2OInfogram  # noqa: F401
 from .isolation_forest import H2OIsolationForestEstimator  # noqa: F401
 from .isotonic import H2OIsotonicRegressionEstimator  # noqa: F401
@@ -55,4 +56,5 @@ ESTIMATORS = {
     "infogram": H2OInfogram,
     "psvm": H2OSupportVectorMachineEstimator,
     "generic": H2OGenericEstimator,
+    "hglm": H2OHGLMEstimator,
 }

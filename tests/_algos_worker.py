@@ -15,7 +15,8 @@ from h2omx.models import (H2OANOVAGLMEstimator, H2OCoxProportionalHazardsEstimat
                           H2OGeneralizedAdditiveEstimator, H2OGeneralizedLowRankEstimator,
                           H2OIsotonicRegressionEstimator, H2OModelSelectionEstimator,
                           H2OSingularValueDecompositionEstimator, H2OTargetEncoderEstimator,
-                          H2OSupportVectorMachineEstimator, H2OUpliftRandomForestEstimator)
+                          H2OHGLMEstimator, H2OSupportVectorMachineEstimator,
+                          H2OUpliftRandomForestEstimator)
 from h2omx.parallel.comm import Comm  # noqa: E402
 
 
@@ -69,6 +70,9 @@ def main():
     res["auuc"] = up.training_metrics["auuc"]
     sv = H2OSupportVectorMachineEstimator(gamma=0.5).train(x=["a", "b"], y="yb", training_frame=fr, comm=c)
     res["svm"] = sv.decision_function(fr).tolist()
+    hg = H2OHGLMEstimator(group_column="g", random_columns=["b"]).train(x=["a", "b"], y="y", training_frame=fr,
+                                                                      comm=c)
+    res["hglm"] = list(hg.coef().values()) + [hg.sigma2] + hg.T.ravel().tolist()
     from h2omx.frame.tools import interaction
 
     ia = interaction(fr, ["g", "trt"], max_factors=5, comm=c).vecs[0]

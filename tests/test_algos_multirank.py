@@ -58,3 +58,5 @@ def test_two_ranks_match_one_rank(results):
     np.testing.assert_allclose(two[0]["uplift"] + two[1]["uplift"], one["uplift"], rtol=1e-6)
     np.testing.assert_allclose(two[0]["svm"] + two[1]["svm"], one["svm"], rtol=1e-4, atol=1e-4)
     assert two[0]["inter"] + two[1]["inter"] == one["inter"]
+    for r in two:
+        np.testing.assert_allclose(r["hglm"], one["hglm"], rtol=1e-7, atol=1e-9)
