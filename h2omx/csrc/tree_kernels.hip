@@ -28,6 +28,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -871,12 +872,8 @@ __global__ __launch_bounds__(256) void split_find_kernel(const long long* __rest
 
 // Per-node arg-max over the features' best thresholds (gain desc, then
 // feature / bin / NA-direction asc): one wave per node, lane = feature.
-__global__ __launch_bounds__(64) void node_best_kernel(const FeatBest* __restrict__ fbest,
-                                                       const int* __restrict__ ctl, int F,
-                                                       NodeSplit* __restrict__ out) {
-  const int node = blockIdx.x;
-  if (node >= ctl[CTL_N]) return;
-  const int lane = threadIdx.x;
+__device__ __forceinline__ void node_best_wave(const FeatBest* __restrict__ fbest, int F, int node, int lane,
+                                               NodeSplit* __restrict__ out) {
   const FeatBest* fb = fbest + (int64_t)node * F;
   double bg = -INFINITY;
   long long key = 0x7fffffffffffffffLL;  // (feature, code) order for ties
@@ -911,6 +908,14 @@ __global__ __launch_bounds__(64) void node_best_kernel(const FeatBest* __restric
     }
     out[node] = s;
   }
+}
+
+__global__ __launch_bounds__(64) void node_best_kernel(const FeatBest* __restrict__ fbest,
+                                                       const int* __restrict__ ctl, int F,
+                                                       NodeSplit* __restrict__ out) {
+  const int node = blockIdx.x;
+  if (node >= ctl[CTL_N]) return;
+  node_best_wave(fbest, F, node, threadIdx.x, out);
 }
 
 // ---------------------------------------------------------------------------
@@ -1036,6 +1041,24 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(const NodeSplit* _
                                                               int max_next_nodes, PartInfo* __restrict__ part,
                                                               NodeLink* __restrict__ next_link,
                                                               TreeNode* __restrict__ tree, int tree_capacity) {
+  level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes, part, next_link, tree,
+                      tree_capacity);
+}
+
+// Per-node arg-max and level finalisation in ONE single-workgroup launch (the
+// 16 waves take the nodes round-robin, then the workgroup finalises): saves a
+// dependent launch per level on the scan engine, whose levels hold few nodes.
+// The NodeSplit records go through global memory; the workgroup barrier
+// (workgroup-scope fence + s_barrier) orders them for the finalising threads.
+__global__ __launch_bounds__(1024) void node_best_finalize_kernel(
+    const FeatBest* __restrict__ fbest, const int* __restrict__ ctl, int* __restrict__ ctl_next, SplitParams p,
+    const float* __restrict__ edges, const int* __restrict__ nvb, int nbt, int max_next_nodes,
+    PartInfo* __restrict__ part, NodeLink* __restrict__ next_link, TreeNode* __restrict__ tree, int tree_capacity,
+    NodeSplit* __restrict__ nsplit) {
+  const int n = ctl[CTL_N];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int node = wid; node < n; node += nw) node_best_wave(fbest, p.F, node, lane, nsplit);
+  __syncthreads();
   level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes, part, next_link, tree,
                       tree_capacity);
 }
@@ -1812,6 +1835,17 @@ H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_n
                                    int max_nodes, hipStream_t stream) {
   const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
   NodeSplit* ns = reinterpret_cast<NodeSplit*>(nsplit);
+  static const int fuse_cap = [] {
+    const char* e = getenv("H2OMX_FUSE_NODE_BEST");     // max nodes for the one-launch path (0 = off)
+    return e ? atoi(e) : 64;
+  }();
+  if (max_nodes <= fuse_cap) {
+    hipLaunchKernelGGL(node_best_finalize_kernel, dim3(1), dim3(1024), 0, stream,
+                       reinterpret_cast<const FeatBest*>(fbest), ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes,
+                       reinterpret_cast<PartInfo*>(part), reinterpret_cast<NodeLink*>(next_link),
+                       reinterpret_cast<TreeNode*>(tree), tree_capacity, ns);
+    return launch_status();
+  }
   hipLaunchKernelGGL(node_best_kernel, dim3(max_nodes), dim3(64), 0, stream, reinterpret_cast<const FeatBest*>(fbest),
                      ctl, p.F, ns);
   hipLaunchKernelGGL(level_finalize_kernel, dim3(1), dim3(1024), 0, stream,
