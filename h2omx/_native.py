@@ -27,7 +27,7 @@ KERNEL_LIBS = {
     "explain": ["explain_kernels.hip"],
 }
 HOST_LIBS = {
-    "host": ["host/parser.cpp"],
+    "host": ["host/parser.cpp", "host/solvers.cpp"],
 }
 
 

@@ -98,6 +98,26 @@ def _soft(x, t):
     return np.sign(x) * max(abs(x) - t, 0.0)
 
 
+def _enet_cd(A, r, pen, l1, free_idx, non_negative, b, max_iter, tol) -> int:
+    """Covariance-update cyclic coordinate descent in C++ (csrc/host/solvers.cpp)."""
+    import ctypes
+
+    from .._native import require
+
+    lib = require("host")
+    fn = lib.h2omx_enet_cd
+    fn.restype = ctypes.c_int
+    dp = ctypes.POINTER(ctypes.c_double)
+    fn.argtypes = [dp, ctypes.c_int, dp, dp, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int, dp,
+                   ctypes.c_int, ctypes.c_double]
+    k = len(r)
+    it = fn(A.ctypes.data_as(dp), A.shape[1], r.ctypes.data_as(dp), pen.ctypes.data_as(dp), k, float(l1),
+            int(free_idx), int(bool(non_negative)), b.ctypes.data_as(dp), int(max_iter), float(tol))
+    if it < 0:
+        raise RuntimeError("h2omx_enet_cd: bad arguments")
+    return it
+
+
 def solve_enet(G: np.ndarray, p: int, N: float, lam: float, alpha: float, beta0: np.ndarray, intercept: bool,
                non_negative: bool = False, max_iter: int = 500, tol: float = 1e-9, penalty: np.ndarray | None = None):
     """Minimise (1/2N) sum w (z - x.b)^2 + lam (alpha |b|_1 + (1-alpha)/2 |b|^2)
@@ -126,24 +146,9 @@ def solve_enet(G: np.ndarray, p: int, N: float, lam: float, alpha: float, beta0:
         except np.linalg.LinAlgError:
             b = np.linalg.lstsq(A, Xtz, rcond=None)[0]
     else:
-        b = beta0[:k].copy() if beta0 is not None else np.zeros(k)
-        diag = np.diag(XtX) + pen
-        for _ in range(max_iter):
-            mx = 0.0
-            for j in range(k):
-                if diag[j] <= 0:
-                    continue
-                r = Xtz[j] - XtX[j] @ b + XtX[j, j] * b[j]
-                if j == p and intercept:
-                    nb = r / diag[j]
-                else:
-                    nb = _soft(r, l1) / diag[j]
-                    if non_negative:
-                        nb = max(nb, 0.0)
-                mx = max(mx, abs(nb - b[j]))
-                b[j] = nb
-            if mx < tol:
-                break
+        b = np.ascontiguousarray(beta0[:k] if beta0 is not None else np.zeros(k), np.float64).copy()
+        _enet_cd(np.ascontiguousarray(XtX, np.float64), np.ascontiguousarray(Xtz, np.float64),
+                 np.ascontiguousarray(pen, np.float64), l1, p if intercept else -1, non_negative, b, max_iter, tol)
     if not intercept:
         b = np.concatenate([b, [0.0]])
     return b
@@ -395,6 +400,7 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
         dev = null_dev
         history = []
         best = None
+        lam_devs = []
         for lam in lambdas:
             for it in range(max_iter):
                 iters_total += 1
@@ -408,6 +414,12 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
                     break
             if best is None or p_["lambda_search"]:
                 best = (lam, beta.copy(), dev)
+            if p_["lambda_search"]:
+                # H2O-style early exit: the path stops once the last few lambdas no
+                # longer reduce the deviance noticeably (relative to the null deviance)
+                lam_devs.append(dev)
+                if len(lam_devs) >= 4 and lam_devs[-4] - lam_devs[-1] < 1e-4 * max(null_dev, 1e-300):
+                    break
         lam, beta, _ = best
         # final deviance at the chosen beta
         G, dev = allreduce(*D.glm_irls_pass(X, y, w, off, beta, family, link, 0, var_power, link_power))

@@ -94,22 +94,13 @@ def _rule_matrix(ens, rules, X: torch.Tensor) -> torch.Tensor:
 
 
 def _cd_lasso(G: np.ndarray, b: np.ndarray, lam: float, beta0: np.ndarray, iters: int = 500, tol: float = 1e-8):
-    """argmin 1/2 βᵀGβ − bᵀβ + lam |β|_1 by cyclic coordinate descent (G = XᵀWX / N)."""
-    beta = beta0.copy()
-    diag = np.maximum(np.diag(G), 1e-12)
-    Gb = G @ beta
-    for _ in range(iters):
-        delta = 0.0
-        for j in range(beta.size):
-            r = b[j] - Gb[j] + diag[j] * beta[j]
-            nb = np.sign(r) * max(abs(r) - lam, 0.0) / diag[j]
-            d = nb - beta[j]
-            if d != 0.0:
-                Gb += G[:, j] * d
-                beta[j] = nb
-                delta = max(delta, abs(d))
-        if delta < tol:
-            break
+    """argmin 1/2 βᵀGβ − bᵀβ + lam |β|_1 by cyclic coordinate descent (G = XᵀWX / N),
+    in the native covariance-update solver (csrc/host/solvers.cpp)."""
+    from .glm import _enet_cd
+
+    beta = np.ascontiguousarray(beta0, np.float64).copy()
+    _enet_cd(np.ascontiguousarray(G, np.float64), np.ascontiguousarray(b, np.float64), np.zeros(beta.size), lam, -1,
+             False, beta, iters, tol)
     return beta
 
 
