@@ -740,6 +740,14 @@ __device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__
       allowed = u01(hf) < p.col_rate;
     }
   }
+  if (!allowed && full == nullptr && f != 0) {
+    // last level: no histogram row to keep and the node totals come from
+    // feature 0 (node_best reads fbest[node][0]) - nothing to load at all
+    WaveBest r;
+    r.G = r.S = 0.0;
+    r.gain = -INFINITY; r.code = 0x7fffffff; r.GL = r.SL = 0.0;
+    return r;
+  }
   long long gi[B], si[B];
 #pragma unroll
   for (int k = 0; k < B; ++k) {
