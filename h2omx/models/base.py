@@ -261,7 +261,15 @@ class ModelBuilder:
     DEFAULTS: dict = {}
     COMMON = dict(model_id=None, nfolds=0, fold_assignment="AUTO", fold_column=None, seed=-1,
                   keep_cross_validation_predictions=False, keep_cross_validation_models=True,
-                  weights_column=None, ignored_columns=None, max_runtime_secs=0.0, distribution="AUTO")
+                  weights_column=None, ignored_columns=None, max_runtime_secs=0.0, distribution="AUTO",
+                  # H2O ModelParameters shared by every builder; accepted so h2o-py
+                  # call sites port unchanged (per-algorithm DEFAULTS override these)
+                  keep_cross_validation_fold_assignment=False, score_each_iteration=False,
+                  stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3,
+                  categorical_encoding="AUTO", export_checkpoints_dir=None, custom_metric_func=None,
+                  gainslift_bins=-1, auc_type="AUTO", ignore_const_cols=True, balance_classes=False,
+                  class_sampling_factors=None, max_after_balance_size=5.0, max_confusion_matrix_size=20,
+                  verbose=False, response_column=None, training_frame=None, validation_frame=None)
 
     def __init__(self, **params):
         unknown = set(params) - set(self.DEFAULTS) - set(self.COMMON)
