@@ -244,6 +244,10 @@ class H2OApi:
         R("POST", r"/3/GarbageCollect", self.garbage_collect)
         R("GET", r"/3/JStack", self.jstack)
         R("GET", r"/3/ModelMetrics", self.model_metrics_all)
+        R("POST", r"/3/ModelMetrics/predictions_frame/(?P<pf>[^/]+)/actuals_frame/(?P<af>[^/]+)", self.make_metrics)
+        R("POST", r"/3/PermutationVarImp", self.permutation_varimp)
+        R("POST", r"/99/SegmentModelsBuilders/(?P<algo>[^/]+)", self.segment_models)
+        R("GET", r"/3/SegmentModels/(?P<sid>[^/]+)", self.segment_models_get)
         if os.environ.get("H2OMX_ENABLE_FAULT_INJECTION") == "1":
             R("POST", r"/99/h2omx/fault", self.inject_fault)
 
@@ -993,6 +997,57 @@ class H2OApi:
             if m.training_metrics:
                 out.append(S.metrics_json(m.training_metrics, m.category, m.model_id, None, m.response_domain))
         return {"__meta": S.meta("ModelMetricsListSchemaV3", "Iced"), "model_metrics": out}
+
+    def make_metrics(self, pf, af, params, **_):
+        pf, af = unquote(pf), unquote(af)
+        for k in (pf, af):
+            if not isinstance(DKV.get(k), Frame):
+                raise KeyError(k)
+        dom = parse_list(params.get("domain")) or None
+        mm = self.cluster.run("make_metrics", predictions=pf, actuals=af, domain=dom,
+                              distribution=params.get("distribution"), weights=params.get("weights_frame"))
+        cat = mm.pop("model_category")
+        return {"__meta": S.meta("ModelMetricsMakerSchemaV3", "Iced"), "predictions_frame": S.key_ref(pf, "Key<Frame>"),
+                "actuals_frame": S.key_ref(af, "Key<Frame>"),
+                "model_metrics": S.metrics_json(mm, cat, None, af, dom)}
+
+    def permutation_varimp(self, params, **_):
+        m = self._get_model(params.get("model_id"))
+        fid = params.get("frame_id")
+        if not isinstance(DKV.get(fid), Frame):
+            raise KeyError(fid)
+        rows = self.cluster.run("permutation_importance", model=m.model_id, frame=fid,
+                                metric=params.get("metric", "AUTO"), n_repeats=int(params.get("n_repeats", 1)),
+                                seed=int(params.get("seed", -1)), features=parse_list(params.get("features")) or None)
+        table = S.two_dim_table("Permutation Variable Importance",
+                                ["Variable", "Relative Importance", "Scaled Importance", "Percentage"],
+                                ["string", "double", "double", "double"],
+                                [[r["variable"], r["relative_importance"], r["scaled_importance"], r["percentage"]]
+                                 for r in rows])
+        return {"__meta": S.meta("PermutationVarImpV3", "Iced"), "permutation_varimp": table}
+
+    def segment_models(self, algo, params, **_):
+        params = dict(params)
+        segs = parse_list(params.pop("segment_columns", None))
+        sid = params.pop("segment_models_id", None) or f"segment_models_{uuid.uuid4().hex[:8]}"
+        args, tf, y, vf, msgs = self._builder_args(algo, params)
+        fr = DKV.get(tf)
+        ign = set(args.pop("ignored_columns", []) or [])
+        x = [c for c in fr.names if c not in ign and c != y and c not in segs]
+
+        def work(job):
+            return self.cluster.run("train_segments", algo=algo, params=args, segment_columns=segs, x=x, y=y,
+                                    training_frame=tf, validation_frame=vf, segment_models_id=sid)
+
+        job = self.jobs.submit(f"{algo} segment models", sid, "Key<SegmentModels>", work, sync=True)
+        return {"__meta": S.meta("SegmentModelsParametersV3", "Iced"), "job": job.to_json(),
+                "segment_models_id": S.key_ref(sid, "Key<SegmentModels>"), "messages": msgs}
+
+    def segment_models_get(self, sid, **_):
+        res = DKV.get(unquote(sid))
+        if not isinstance(res, dict):
+            raise KeyError(sid)
+        return {"__meta": S.meta("SegmentModelsV3", "Iced"), **res}
 
     def nps(self, **_):
         return {"__meta": S.meta("NodePersistentStorageV3", "Iced"), "entries": []}

@@ -170,6 +170,12 @@ class Model:
 
         return fairness_metrics(self, frame, protected_columns, reference, favorable_class, self.comm)
 
+    def permutation_importance(self, frame: Frame, metric="AUTO", n_repeats: int = 1, seed: int = -1,
+                               features=None) -> list[dict]:
+        from ..tools import permutation_importance
+
+        return permutation_importance(self, frame, metric, n_repeats, seed, features)
+
     def ice(self, frame: Frame, column: str, nbins: int = 20, target=None) -> dict:
         from ..explain_more import ice
 

@@ -390,6 +390,35 @@ def _backend_name(cl):
     return dist.get_backend() if cl.world_size > 1 and dist.is_initialized() else "local"
 
 
+def op_make_metrics(cl, predictions, actuals, domain=None, distribution=None, weights=None):
+    from ..tools import make_metrics
+
+    return make_metrics(_frame(predictions), _frame(actuals), domain, distribution,
+                        _frame(weights) if weights else None, comm=cl.comm if cl.world_size > 1 else None)
+
+
+def op_permutation_importance(cl, model, frame, metric="AUTO", n_repeats=1, seed=-1, features=None):
+    from ..tools import permutation_importance
+
+    m = _model(model)
+    old = m.comm
+    m.comm = cl.comm if cl.world_size > 1 else None
+    try:
+        return permutation_importance(m, _frame(frame), metric, n_repeats, seed, features)
+    finally:
+        m.comm = old
+
+
+def op_train_segments(cl, algo, params, segment_columns, x=None, y=None, training_frame=None,
+                      validation_frame=None, segment_models_id=None):
+    from ..models import ESTIMATORS
+    from ..tools import train_segments
+
+    return train_segments(ESTIMATORS[algo], _resolve_params(dict(params)), segment_columns, x, y,
+                          _frame(training_frame), _frame(validation_frame) if validation_frame else None,
+                          segment_models_id, comm=cl.comm if cl.world_size > 1 else None)
+
+
 def op_fault(cl, rank=-1, kind="raise"):
     """Test-only fault injection: rank ``rank`` fails the command."""
     if rank in (-1, cl.rank):

@@ -138,3 +138,30 @@ def test_rest_generic_import(conn, tmp_path):
     assert mj["algo"] == "generic"
     pr = conn.request("POST /3/Predictions/models/imported_gbm/frames/gen.hex")
     assert pr["model_metrics"][0]["AUC"] > 0.9
+
+
+def test_rest_metrics_permutation_segments(conn):
+    from h2omx.models import H2OGradientBoostingEstimator
+
+    rng = np.random.default_rng(4)
+    n = 900
+    df = pd.DataFrame(rng.normal(size=(n, 3)), columns=list("abc"))
+    df["seg"] = pd.Categorical(rng.choice(["u", "v"], n))
+    df["y"] = pd.Categorical(np.where(df.a > 0, "t", "f"))
+    fr = Frame.from_pandas(df, key="pm.hex")
+    DKV.put("pm.hex", fr)
+    m = H2OGradientBoostingEstimator(ntrees=5, seed=1, model_id="pm_gbm").train(x=list("abc"), y="y",
+                                                                                 training_frame=fr)
+    pv = conn.request("POST /3/PermutationVarImp", {"model_id": "pm_gbm", "frame_id": "pm.hex", "metric": "AUC"})
+    assert pv["permutation_varimp"]["data"][0][0] == "a"
+    pred = m.predict(fr)
+    DKV.put("pm_pred.hex", Frame([pred.vecs[-1]], key="pm_pred.hex"))
+    DKV.put("pm_act.hex", Frame([fr.vec("y")], key="pm_act.hex"))
+    mm = conn.request("POST /3/ModelMetrics/predictions_frame/pm_pred.hex/actuals_frame/pm_act.hex")
+    assert abs(mm["model_metrics"]["AUC"] - m.training_metrics["AUC"]) < 1e-9
+    r = conn.request("POST /99/SegmentModelsBuilders/gbm", {"training_frame": "pm.hex", "response_column": "y",
+                                                            "segment_columns": "[seg]", "ntrees": 3,
+                                                            "segment_models_id": "pm_segs"})
+    assert r["job"]["status"] == "DONE"
+    segs = conn.request("GET /3/SegmentModels/pm_segs")["segments"]
+    assert [s["seg"] for s in segs] == ["u", "v"] and all(s["status"] == "SUCCEEDED" for s in segs)
