@@ -183,9 +183,10 @@ def mojo_bytes(model: Model) -> bytes:
     if algo in ("gbm", "drf", "xgboost"):
         columns = list(model.x)
         info.update(_tree_info(model, files))
+    elif algo == "glm" and (getattr(model, "interaction_spec", None) or model.family == "ordinal"):
+        columns, ext = _glm_ext_info(model, files)       # h2omx array payload
+        info.update(ext)
     elif algo == "glm":
-        if getattr(model, "interaction_spec", None) or model.family == "ordinal":
-            raise NotImplementedError("MOJO export of GLMs with interactions or the ordinal family")
         cats, nums = _design_columns(model.design)
         columns = cats + nums
         info.update(_glm_info(model, cats, nums))
@@ -317,6 +318,32 @@ def _glm_info(model, cats, nums):
             "nums": len(nums), "mean_imputation": True, "num_means": num_means,
             "cat_modes": [0] * len(cats), "h2omx_means": [float(d.means[i]) for i in order], "beta": betas, "family": model.family, "link": model.link,
             "tweedie_link_power": float(model.params.get("tweedie_link_power", 0.0) or 0.0)}
+
+
+def _glm_ext_info(model, files):
+    """GLM with interaction columns and / or the ordinal family: the raw
+    source columns, the interaction spec, the design over the augmented
+    columns and the standardised coefficients (h2omx array payload)."""
+    from ..models.glm_extras import interaction_columns
+
+    spec = getattr(model, "interaction_spec", None) or []
+    gen = set(interaction_columns(spec))
+    base = [c for c in model.x if c not in gen]
+    for _, a, b, _ in spec:
+        for c in (a, b):
+            if c not in base:
+                base.append(c)
+    info = {"h2omx_glm_ext": True, "family": model.family, "link": model.link,
+            "tweedie_link_power": float(model.params.get("tweedie_link_power", 0.0) or 0.0)}
+    # structured settings travel as a JSON entry (model.ini values are flat)
+    files["h2omx/glm_ext.json"] = json.dumps({
+        "interactions": [list(t) for t in spec],
+        "aug_types": {c: [model.feature_types.get(c), model.feature_domains.get(c)] for c in model.x if c in gen},
+        "ordinal_thresholds": list(model.stats.get("ordinal_thresholds") or []),
+    }).encode()
+    _design_info(model.design, info, files)
+    _put(files, info, "beta", model.beta_std)
+    return base, info
 
 
 def _kmeans_info(model, cats, nums):
@@ -556,6 +583,8 @@ class GenericModel(Model):
             self.meta = GenericModel(z.read(f"models/{info['metalearner']}.zip"))
         elif self.mojo_algo in ARRAY_ALGOS:
             self._load_arrays(z, info)
+        elif info.get("h2omx_glm_ext"):
+            self._load_glm_ext(z, info)
         if self.mojo_algo == "coxph":
             self.category = ModelCategory.REGRESSION
         if self.mojo_algo == "upliftdrf":
@@ -571,6 +600,16 @@ class GenericModel(Model):
         d.sds = _get(z, info, f"{tag}_sds")
         d.center = _get(z, info, f"{tag}_center")
         return d
+
+    def _load_glm_ext(self, z, info):
+        ext = json.loads(z.read("h2omx/glm_ext.json").decode())
+        for c, (t, dom) in ext["aug_types"].items():
+            self.feature_types[c] = t
+            self.feature_domains[c] = dom
+        self.ia_spec = [tuple(t) for t in ext["interactions"]]
+        self.ordinal_thresholds = ext["ordinal_thresholds"]
+        self.design = self._design(z, info)
+        self.arr = {"beta": _get(z, info, "beta")}
 
     def _load_arrays(self, z, info):
         a = self.mojo_algo
@@ -677,6 +716,24 @@ class GenericModel(Model):
             return torch.stack([torch.pow(2.0, -ml / cst), ml])
         if a == "targetencoder":
             return self._te(frame)
+        if a == "glm":                              # interactions / ordinal (h2omx_glm_ext)
+            from ..models.glm import _torch_linkinv
+            from ..models.glm_extras import apply_interactions, ordinal_probs
+
+            fr = apply_interactions(frame, self.ia_spec)
+            Xs = self.design.transform(self.design.raw_matrix(fr)).double()
+            p = Xs.shape[0]
+            beta = torch.from_numpy(self.arr["beta"]).to(dev).view(-1, p + 1)
+            if info["family"] == "ordinal":
+                th = torch.tensor(self.ordinal_thresholds, dtype=torch.float64, device=dev)
+                return ordinal_probs(Xs, beta[0, :p], th).float()
+            eta = beta[:, :p] @ Xs + beta[:, p:p + 1]
+            if info["family"] == "multinomial":
+                return torch.softmax(eta, 0).float()
+            mu = _torch_linkinv(eta[0], info["link"], info.get("tweedie_link_power", 0.0))
+            if self.category == ModelCategory.BINOMIAL:
+                return torch.stack([1 - mu, mu]).float()
+            return mu[None, :].float()
         if a == "upliftdrf":
             from ..models.tree import bin_matrix
             from ..models.uplift import predict_tree
@@ -813,7 +870,7 @@ class GenericModel(Model):
 
     def predict_raw(self, frame: Frame) -> torch.Tensor:
         a = self.mojo_algo
-        if a in ARRAY_ALGOS:
+        if a in ARRAY_ALGOS or self.info.get("h2omx_glm_ext"):
             return self._score_arrays(frame)
         X = self._matrix(frame)
         if a == "isolationforest":

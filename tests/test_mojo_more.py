@@ -95,3 +95,25 @@ def test_uplift_mojo(tmp_path):
     g = _roundtrip(m, tmp_path)
     assert g.category == "BinomialUplift"
     _same(g.predict(fr), m.predict(fr))
+
+
+@pytest.mark.parametrize("kind", ["interactions", "ordinal"])
+def test_glm_ext_mojo(kind, tmp_path):
+    from h2omx.models import H2OGeneralizedLinearEstimator
+
+    rng = np.random.default_rng(5)
+    n = 1500
+    df = pd.DataFrame(rng.normal(size=(n, 2)), columns=["a", "b"])
+    df["g"] = pd.Categorical(rng.choice(["p", "q", "r"], n))
+    if kind == "interactions":
+        df["y"] = 1 + df.a * df.b + np.where(df.g == "q", 1.0, -1.0) * df.b + 0.1 * rng.normal(size=n)
+        m = H2OGeneralizedLinearEstimator(lambda_=0.0, interaction_pairs=[("a", "b"), ("g", "b")]).train(
+            x=["a", "b", "g"], y="y", training_frame=Frame.from_pandas(df))
+    else:
+        eta = df.a - 0.5 * df.b
+        df["y"] = pd.Categorical(np.digitize(eta + rng.logistic(size=n), [-1, 1]).astype(str))
+        m = H2OGeneralizedLinearEstimator(family="ordinal", lambda_=0.0).train(x=["a", "b", "g"], y="y",
+                                                                               training_frame=Frame.from_pandas(df))
+    fr = Frame.from_pandas(df)
+    g = _roundtrip(m, tmp_path)
+    np.testing.assert_allclose(g.predict_raw(fr).numpy(), m.predict_raw(fr).numpy(), rtol=1e-4, atol=1e-5)
