@@ -37,12 +37,13 @@ def data(n=1200):
 
 def main():
     out_path = sys.argv[1]
-    comm = Comm.from_env(device="cpu")
+    device = os.environ.get("H2OMX_WORKER_DEVICE", "cpu")    # "cuda": ranks share the GPU over gloo
+    comm = Comm.from_env(device=device)
     c = comm if comm.world_size > 1 else None
     df = data()
     n = len(df)
     lo, hi = n * comm.rank // comm.world_size, n * (comm.rank + 1) // comm.world_size
-    fr = unify_domains(Frame.from_pandas(df.iloc[lo:hi].reset_index(drop=True)), c)
+    fr = unify_domains(Frame.from_pandas(df.iloc[lo:hi].reset_index(drop=True), device=comm.device), c)
     res = {}
     te = H2OTargetEncoderEstimator(noise=0.0, blending=True).train(x=["g"], y="y", training_frame=fr, comm=c)
     res["te"] = te.transform(fr).to_pandas()["g_te"].tolist()
