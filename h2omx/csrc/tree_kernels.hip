@@ -263,6 +263,7 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
   }
   const float sg = (float)qscale[0], ss = (float)qscale[1];
   const int64_t rb = (int64_t)qscale[7];  // global row offset of this rank (dither)
+  const int64_t n_rows = (int64_t)qscale[8];  // this rank's live rows (implicit-root levels)
   __syncthreads();
 
   const int64_t units = npad / ROWS;
@@ -274,10 +275,17 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     bool any = false;
     if constexpr (ROUTE) {
       int nn[ROWS], nx[ROWS];
+      if (nid == nullptr) {
+        // implicit root (previous level = the root): every live row is in node 0,
+        // no node-id stream to read (boost_update no longer resets it)
 #pragma unroll
-      for (int q = 0; q < ROWS / 4; ++q) {
-        const int4 n4 = *reinterpret_cast<const int4*>(nid + r0 + 4 * q);
-        nn[4 * q] = n4.x; nn[4 * q + 1] = n4.y; nn[4 * q + 2] = n4.z; nn[4 * q + 3] = n4.w;
+        for (int k = 0; k < ROWS; ++k) nn[k] = (r0 + k < n_rows) ? 0 : INT32_MIN;
+      } else {
+#pragma unroll
+        for (int q = 0; q < ROWS / 4; ++q) {
+          const int4 n4 = *reinterpret_cast<const int4*>(nid + r0 + 4 * q);
+          nn[4 * q] = n4.x; nn[4 * q + 1] = n4.y; nn[4 * q + 2] = n4.z; nn[4 * q + 3] = n4.w;
+        }
       }
 #pragma unroll
       for (int k = 0; k < ROWS; ++k) { nx[k] = nn[k]; s[k] = -1; }
@@ -341,6 +349,15 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
           s[8 * q + k] = sl;
           any |= (sl >= 0);
         }
+      }
+    } else if (nid == nullptr) {
+      // implicit root (level 0 of the scan engine): live rows are node 0, slot 0
+#pragma unroll
+      for (int k = 0; k < ROWS; ++k) {
+        int sl = (r0 + k < n_rows) ? 0 - slot_lo : -1;
+        if (sl >= slot_cnt) sl = -1;
+        s[k] = sl;
+        any |= (sl >= 0);
       }
     } else {
 #pragma unroll
@@ -1338,6 +1355,8 @@ struct GradParams {
   float quantile_alpha;
   float huber_delta;
   long long row_base;   // global index of this rank's first row (bagging hash)
+  int skip_nid;         // 1: leave nid alone (the scan engine treats level 0 / 1 as an implicit root)
+  int pad;
 };
 
 __device__ __forceinline__ void dist_grad(int dist, float f, float y, const GradParams& gp, float& g, float& h) {
@@ -1425,7 +1444,7 @@ __global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F
     *reinterpret_cast<float4*>(g + r0) = make_float4(gv[0], gv[1], gv[2], gv[3]);
     *reinterpret_cast<float4*>(h + r0) = make_float4(hv[0], hv[1], hv[2], hv[3]);
     if (wout) *reinterpret_cast<float4*>(wout + r0) = make_float4(wv[0], wv[1], wv[2], wv[3]);
-    *reinterpret_cast<int4*>(nid + r0) = make_int4(nn[0], nn[1], nn[2], nn[3]);
+    if (!gp.skip_nid) *reinterpret_cast<int4*>(nid + r0) = make_int4(nn[0], nn[1], nn[2], nn[3]);
   }
   if (stat_max) block_max3(mg, mh, mw, stat_max);
 }

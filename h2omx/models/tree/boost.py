@@ -238,6 +238,7 @@ class GpuBooster:
         P, st, b = ops.P, self.st, self.builder
         gp = make_grad_params(dist or self.dist, apply, self.sample_rate, self.seed, next_tree,
                               row_base=self.builder.row_base, **self.kw)
+        gp.skip_nid = 1 if getattr(self.builder, "implicit_root", False) else 0
         y = st.ycls[k] if (self.dist == "drf" and self.K > 1) else st.y
         with b.timer.phase("grad"):
             ops.check(self.lib.h2omx_boost_update(P(st.Fm[k]), P(y), P(st.w), self.bm.n, self.bm.npad, P(b.nid),

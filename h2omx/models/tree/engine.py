@@ -110,7 +110,8 @@ class HipTreeBuilder:
         self.nid = torch.full((bm.npad,), -1, dtype=torch.int32, device=d)
         self.stat_max = torch.zeros((4,), dtype=torch.int32, device=d)   # float bits of max|g|, max h, max w
         self.stat_slab = torch.zeros((int(self.lib.h2omx_stat_blocks()) * 4,), dtype=torch.int32, device=d)
-        self.qscale = torch.zeros((8,), dtype=torch.float64, device=d)
+        self.qscale = torch.zeros((16,), dtype=torch.float64, device=d)
+        self.qscale[8] = float(bm.n)          # live rows of this rank (implicit-root levels)
         self.leaf_acc = torch.zeros((self.capacity * 3,), dtype=torch.int64, device=d)
         # per-row packed quantised (g, s) of the current tree and next-level build
         # slot (scan engine): written at level 0 / by partition, read by deeper levels
@@ -143,6 +144,12 @@ class HipTreeBuilder:
         # whole-tree LDS window (needs the tree capacity to fit it: depth <= 8)
         self.fuse_route = (params.max_depth <= self.FUSE_MAX_DEPTH and not self.COMPACT
                            and os.environ.get("H2OMX_FUSE_ROUTE", "1") == "1")
+        # scan engine with fused routing: levels 0 / 1 take "every live row is in the
+        # root" from the row count instead of a node-id stream, so boost_update no
+        # longer resets nid and levels 0 / 1 skip reading it (needs >= 2 levels: a
+        # depth-1 tree's final partition reads level 0's ids)
+        self.implicit_root = (self.fuse_route and not getattr(self, "segmented", False)
+                              and params.max_depth >= 2 and os.environ.get("H2OMX_IMPLICIT_ROOT", "1") != "0")
         self.nid2 = torch.full((bm.npad,), -1, dtype=torch.int32, device=d) if self.fuse_route else None
         # one-launch split decision (split_level: 16 waves per node scan <= 4 features each,
         # last-arriver hand-off into the level finalisation).  Bit-identical but measured
@@ -164,6 +171,7 @@ class HipTreeBuilder:
         self.segmented = eng == "seg" or (eng == "auto" and params.max_depth > self.DEEP_DEPTH)
         if self.segmented:
             self.fuse_route, self.nid2 = False, None
+            self.implicit_root = False
             self.pc_rows = int(self.lib.h2omx_pc_rows())
             hc = int(os.environ.get("H2OMX_SEG_CHUNK", "0")) or -(-bm.n // self.SEG_TARGET_CHUNKS)
             self.hc_rows = min(self.ROWS_CAP, max(2048, -(-hc // 256) * 256))
@@ -305,7 +313,8 @@ class HipTreeBuilder:
                     if d > 0 and fuse and self._fused_level(d):
                         # partition of level d - 1 fused in: nid_buf[d - 1] -> nid_buf[d]
                         ops.check(lib.h2omx_hist_build_route(
-                            P(bm.codes), bm.npad, P(nid_buf[(d - 1) % 2]), P(part_prev), P(ctl_nxt),
+                            P(bm.codes), bm.npad, P(None if (d == 1 and self.implicit_root) else nid_buf[(d - 1) % 2]),
+                            P(part_prev), P(ctl_nxt),
                             P(nid_buf[d % 2]), 1 if ps == 0 else 0, P(ctl_cur), P(bm.nvb), P(self.qscale), F, nbt,
                             plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo, plan["slot_cnt"],
                             self.ROWS_PER_LANE, plan["threads"], P(self.pk), 4 if self.pk32 else 2, P(partials), st),
@@ -320,7 +329,8 @@ class HipTreeBuilder:
                         # level 0 stores the packed quantised rows; deeper levels read them
                         # with the build slots the previous partition wrote
                         ops.check(lib.h2omx_hist_build(
-                            P(bm.codes), bm.npad, P(g), P(s2), P(nid_buf[d % 2] if fuse else self.nid),
+                            P(bm.codes), bm.npad, P(g), P(s2),
+                            P(None if (d == 0 and self.implicit_root) else (nid_buf[d % 2] if fuse else self.nid)),
                             P(link[cur]), P(ctl_cur), P(bm.nvb),
                             P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, plan["fg"], plan["n_groups"],
                             plan["wgpg"], slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],

@@ -30,6 +30,7 @@ class GradParams(ctypes.Structure):
         ("dist", ctypes.c_int), ("apply_tree", ctypes.c_int), ("sample_rate", ctypes.c_float),
         ("seed", ctypes.c_uint32), ("tree_index", ctypes.c_int), ("tweedie_power", ctypes.c_float),
         ("quantile_alpha", ctypes.c_float), ("huber_delta", ctypes.c_float), ("row_base", ctypes.c_int64),
+        ("skip_nid", ctypes.c_int), ("pad", ctypes.c_int),
     ]
 
 
