@@ -25,18 +25,6 @@ def _free_port():
 
 
 @pytest.fixture(scope="module")
-def conn(tmp_path_factory):
-    cl = form_cluster(ClusterConfig(), device="cpu")
-    api = H2OApi(cl)
-    port = _free_port()
-    srv = serve(api, "127.0.0.1", port)
-    c = H2OConnection(f"http://127.0.0.1:{port}")
-    yield c
-    srv.shutdown()
-    DKV.clear()
-
-
-@pytest.fixture(scope="module")
 def csv_path(tmp_path_factory):
     rng = np.random.default_rng(0)
     n = 3000
@@ -46,6 +34,21 @@ def csv_path(tmp_path_factory):
     p = tmp_path_factory.mktemp("data") / "train.csv"
     df.to_csv(p, index=False)
     return str(p)
+
+
+@pytest.fixture(scope="module")
+def conn(csv_path):
+    cl = form_cluster(ClusterConfig(), device="cpu")
+    api = H2OApi(cl)
+    port = _free_port()
+    srv = serve(api, "127.0.0.1", port)
+    c = H2OConnection(f"http://127.0.0.1:{port}")
+    # every test may run alone (-k, xdist): the shared training frame is
+    # imported here rather than by test_import_parse_frame
+    c.import_file(csv_path, destination_frame="train.hex")
+    yield c
+    srv.shutdown()
+    DKV.clear()
 
 
 def test_cloud_and_session(conn):
