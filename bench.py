@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Benchmarks (BASELINE.json / BASELINE.md), one rank per MI355X.
 
-    python bench.py --gpus N --steps K --warmup W                 # headline
+    python bench.py --gpus N --steps K --warmup W                 # headline (N > 1: one
+                                                                  #   child rank per GPU)
     torchrun --nproc-per-node N bench.py --gpus N ...             # driver, N > 1
     python bench.py --model xgboost-airlines | dl-mlp ...         # other BASELINE configs
 
@@ -276,6 +277,15 @@ def main(argv=None) -> int:
     ap.add_argument("--oracle-rows", type=int, default=0,
                     help="also fit sklearn HistGradientBoosting on this many rows for AUC parity")
     args = ap.parse_args(argv)
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # not under torchrun: start one rank per GPU here (fresh child processes;
+        # this parent never touches the GPU) and exit with the first failure
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from h2omx.runtime.launch import spawn_ranks
+
+        cmd = [sys.executable, os.path.abspath(__file__), *(sys.argv[1:] if argv is None else argv)]
+        return spawn_ranks(cmd, args.gpus)
 
     import numpy as np
     import torch

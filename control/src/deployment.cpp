@@ -154,8 +154,15 @@ Json h2o_stateful_set(const DeploymentSpecification& s) {
   tmd["labels"] = labels_for(s);
   tmpl["metadata"] = tmd;
   Json pod = Json::object();
-  // RCCL's xGMI P2P transport between pods needs a shared IPC namespace and
-  // /dev/shm large enough for its proxy buffers.
+  // Topologies (docs/ARCHITECTURE.md "Multi-GPU topology"):
+  //  * one pod per node with gpus_per_node GPUs and gpus_per_node ranks
+  //    (--cluster_size 1 --gpus_per_node 8): every rank shares the pod's IPC,
+  //    /dev/shm and device view, so RCCL uses its P2P transport over xGMI;
+  //  * one pod per GPU (--gpus_per_node 1): RCCL's P2P / SHM transports between
+  //    pods need the host IPC namespace and the HOST /dev/shm, which hostIPC
+  //    mounts into the container.  Nothing may be mounted over /dev/shm (a
+  //    per-pod emptyDir would hide the host's and push RCCL onto sockets); the
+  //    GPU device plugin must also expose peer devices for xGMI P2P.
   pod["hostIPC"] = true;
   pod["terminationGracePeriodSeconds"] = 10;
   Json c = Json::object();
@@ -208,28 +215,16 @@ Json h2o_stateful_set(const DeploymentSpecification& s) {
   env.push_back(env_var("H2OMX_MEMORY_PERCENTAGE", std::to_string(s.memory_percentage)));
   env.push_back(env_var("H2OMX_CLUSTER_NAME", s.name));
   env.push_back(env_var("HSA_ENABLE_IPC_MODE_LEGACY", "0"));
+  // ranks per pod: the node entry point forks one rank per GPU before any GPU call
+  env.push_back(env_var("H2OMX_GPUS_PER_NODE", std::to_string(s.gpus_per_node > 0 ? s.gpus_per_node : 1)));
   Json pod_name = Json::object();
   pod_name["name"] = "POD_NAME";
   pod_name["valueFrom"] = kv("fieldRef", kv("fieldPath", "metadata.name"));
   env.push_back(pod_name);
   c["env"] = env;
-  Json vm = Json::array();
-  Json shm = Json::object();
-  shm["name"] = "dshm";
-  shm["mountPath"] = "/dev/shm";
-  vm.push_back(shm);
-  c["volumeMounts"] = vm;
   Json containers = Json::array();
   containers.push_back(c);
   pod["containers"] = containers;
-  Json vols = Json::array();
-  Json v = Json::object();
-  v["name"] = "dshm";
-  Json ed = Json::object();
-  ed["medium"] = "Memory";
-  v["emptyDir"] = ed;
-  vols.push_back(v);
-  pod["volumes"] = vols;
   tmpl["spec"] = pod;
   spec["template"] = tmpl;
   sts["spec"] = spec;

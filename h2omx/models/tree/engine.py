@@ -137,7 +137,7 @@ class HipTreeBuilder:
         # >= 2^16 rows per workgroup bounds the per-row fixed-point values to 16 bits
         # (tree_begin: |G_q| <= 2^14, S_q <= 2^15): the packed rows are then stored in
         # 32 bits (hist_build PKM 3/4), halving what every deep-level feature group re-reads
-        self.pk32 = self.max_rows_per_wg >= 65536 and os.environ.get("H2OMX_PK32", "1") == "1"
+        # (self.pk32, set once the ranks agree on max_rows_per_wg below)
         # fused routing (scan engine, shallow trees): level d's partition runs inside
         # level d+1's histogram kernel (node ids double-buffered), and the last level's
         # partition adds the exact sums of every row, early leaves included, into a
@@ -186,6 +186,14 @@ class HipTreeBuilder:
             self.seg_threads = 512
             self.codes_rm = bm.codes_rm
             self.idx = [torch.empty((max(bm.n, 1),), dtype=torch.int32, device=d) for _ in range(2)]
+        # the fixed-point scales (tree_begin) derive from max_rows_per_wg: every rank
+        # must quantise with the SAME scale or the summed int64 histograms mix units,
+        # so agree on the largest chunk over all ranks (shards differ in row count)
+        if comm is not None and comm.world_size > 1:
+            t = torch.tensor([self.max_rows_per_wg], dtype=torch.int64, device=d)
+            comm.all_reduce_(t, "max")
+            self.max_rows_per_wg = int(t.item())
+        self.pk32 = self.max_rows_per_wg >= 65536 and os.environ.get("H2OMX_PK32", "1") == "1"
 
     # -- buffers -----------------------------------------------------------
     def _buf(self, name: str, numel: int, dtype) -> torch.Tensor:

@@ -55,6 +55,8 @@ class ClusterConfig:
     rest_port: int = 54321
     pod_name: str = field(default_factory=socket.gethostname)
     cloud_name: str = "h2omx"
+    local_rank: int = 0          # rank inside this pod / host (selects cuda:local_rank)
+    gpus_per_node: int = 1       # ranks per pod (H2OMX_GPUS_PER_NODE)
 
     @property
     def bus_port(self) -> int:
@@ -74,17 +76,25 @@ def config_from_env(env=None) -> ClusterConfig:
     cfg.pod_name = env.get("POD_NAME") or env.get("HOSTNAME") or socket.gethostname()
     svc = env.get("H2O_KUBERNETES_SERVICE_DNS")
     if svc:
+        # StatefulSet: H2O_NODE_EXPECTED_COUNT pods x H2OMX_GPUS_PER_NODE ranks each;
+        # rank = ordinal * gpus_per_node + local rank (the launcher's child index)
         cfg.service_dns = svc
-        cfg.world_size = int(env.get("H2O_NODE_EXPECTED_COUNT", "1"))
+        cfg.gpus_per_node = max(1, int(env.get("H2OMX_GPUS_PER_NODE", "1")))
+        cfg.local_rank = int(env.get("H2OMX_LOCAL_RANK", "0"))
+        if not 0 <= cfg.local_rank < cfg.gpus_per_node:
+            raise ValueError(f"local rank {cfg.local_rank} outside {cfg.gpus_per_node} ranks per pod")
+        cfg.world_size = int(env.get("H2O_NODE_EXPECTED_COUNT", "1")) * cfg.gpus_per_node
         m = _ORDINAL.match(cfg.pod_name)
         if not m:
             raise ValueError(f"pod name {cfg.pod_name!r} has no StatefulSet ordinal suffix")
-        cfg.rank = int(m.group(2))
+        cfg.rank = int(m.group(2)) * cfg.gpus_per_node + cfg.local_rank
         cfg.master_addr = env.get("MASTER_ADDR") or f"{m.group(1)}-0.{svc}"
         cfg.cloud_name = svc.split(".")[0]
     else:
         cfg.world_size = int(env.get("WORLD_SIZE", "1"))
         cfg.rank = int(env.get("RANK", "0"))
+        cfg.local_rank = int(env.get("LOCAL_RANK", str(cfg.rank)))
+        cfg.gpus_per_node = int(env.get("LOCAL_WORLD_SIZE", "1"))
         cfg.master_addr = env.get("MASTER_ADDR", "127.0.0.1")
         cfg.cloud_name = env.get("H2OMX_CLOUD_NAME", "h2omx")
     if not 0 <= cfg.rank < cfg.world_size:
@@ -95,7 +105,8 @@ def config_from_env(env=None) -> ClusterConfig:
 def wait_for_peers(cfg: ClusterConfig, resolver=socket.getaddrinfo, sleep=time.sleep, clock=time.monotonic) -> list[str]:
     """Block until the headless service resolves to ``world_size`` addresses
     (all pods published, ``publishNotReadyAddresses: true``) or time out."""
-    if not cfg.service_dns or cfg.world_size == 1:
+    pods = cfg.world_size // max(cfg.gpus_per_node, 1)
+    if not cfg.service_dns or pods <= 1:
         return []
     deadline = clock() + cfg.lookup_timeout_s
     last: list[str] = []
@@ -105,11 +116,11 @@ def wait_for_peers(cfg: ClusterConfig, resolver=socket.getaddrinfo, sleep=time.s
             last = sorted({i[4][0] for i in infos})
         except OSError:
             last = []
-        if len(last) >= cfg.world_size:
+        if len(last) >= pods:
             return last
         if clock() > deadline:
             raise TimeoutError(f"cluster formation timed out after {cfg.lookup_timeout_s:.0f}s: "
-                               f"{len(last)}/{cfg.world_size} nodes visible via {cfg.service_dns}")
+                               f"{len(last)}/{pods} nodes visible via {cfg.service_dns}")
         sleep(1.0)
 
 
@@ -243,7 +254,7 @@ def form_cluster(cfg: ClusterConfig | None = None, device: str | None = None, ti
     if device is None:
         device = "cuda" if torch.cuda.device_count() > 0 else "cpu"
     if device == "cuda":
-        dev = torch.device("cuda", 0 if torch.cuda.device_count() == 1 else cfg.rank % torch.cuda.device_count())
+        dev = torch.device("cuda", cfg.local_rank % torch.cuda.device_count())
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")

@@ -33,6 +33,18 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
 
+    # a pod with several GPUs runs one rank per GPU: the pod's main process only
+    # starts them (before any GPU call) and fails the pod as soon as one dies
+    gpn = int(os.environ.get("H2OMX_GPUS_PER_NODE", "1") or "1")
+    if gpn > 1 and "H2OMX_LOCAL_RANK" not in os.environ:
+        from .launch import spawn_ranks
+
+        cmd = [sys.executable, "-m", "h2omx.runtime.node", *(sys.argv[1:] if argv is None else argv)]
+        env = dict(os.environ)
+        log.info("starting %d local ranks (one per GPU)", gpn)
+        # rendezvous address / ranks come from the StatefulSet contract in each child
+        return spawn_ranks(cmd, gpn, env=env, master_addr=None)
+
     from ..api.server import H2OApi, serve
     from .cluster import config_from_env, form_cluster
     from .leader import serve_leader_probe
@@ -44,7 +56,8 @@ def main(argv=None) -> int:
         cfg.cloud_name = a.name
     log.info("node rank %d/%d, master %s:%d", cfg.rank, cfg.world_size, cfg.master_addr, cfg.master_port)
     cl = form_cluster(cfg, device=a.device)
-    probe = None if a.no_probe else serve_leader_probe(cl, a.host)
+    # one probe server per pod (the ranks of a pod share its network namespace)
+    probe = None if (a.no_probe or cfg.local_rank != 0) else serve_leader_probe(cl, a.host)
     stop = threading.Event()
 
     def _term(*_):

@@ -186,6 +186,21 @@ def test_deploy_h2o_objects(k8s, tmp_path):
     assert k8s.list("services") == [] and k8s.list("statefulsets") == [] and k8s.list("ingresses") == []
 
 
+def test_single_pod_eight_gpu_topology(tmp_path):
+    """--cluster_size 1 --gpus_per_node 8: one pod holding the node's eight
+    GPUs and eight ranks (the node entry point forks one per GPU); nothing is
+    mounted over /dev/shm, so the host's shared memory stays visible to RCCL."""
+    r = run(["deploy", "--cluster_size", "1", "--gpus_per_node", "8", "--dry-run", "-c", "single"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout
+    assert "replicas: 1" in out and 'amd.com/gpu: "8"' in out
+    assert "- name: H2OMX_GPUS_PER_NODE\n          value: \"8\"" in out
+    assert "hostIPC: true" in out
+    assert "/dev/shm" not in out and "emptyDir" not in out
+    r = run(["deploy", "--cluster_size", "8", "--dry-run", "-c", "per-gpu"], tmp_path)
+    assert "replicas: 8" in r.stdout and 'amd.com/gpu: "1"' in r.stdout and "/dev/shm" not in r.stdout
+
+
 def test_rollback_on_statefulset_failure(k8s, tmp_path):
     k8s.fail[("POST", "statefulsets")] = 500
     r = run(["deploy", "--kubeconfig", k8s.cfg, "-c", "rb", "-s", "1"], tmp_path)

@@ -25,18 +25,26 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("dist,depth,sr", [("bernoulli", 5, 1.0), ("gaussian", 6, 0.7)])
-def test_two_ranks_equal_one_rank(cuda_dev, tmp_path, dist, depth, sr):
+@pytest.mark.parametrize("dist,depth,sr,n,split", [
+    ("bernoulli", 5, 1.0, 30001, 0.5),
+    ("gaussian", 6, 0.7, 30001, 0.5),
+    # 200k + 400k rows: on their own the two shards would pick different
+    # fixed-point scales (2^15 vs 2^14 per max|g|); the ranks must agree on one
+    ("bernoulli", 4, 1.0, 600000, 1 / 3),
+])
+def test_two_ranks_equal_one_rank(cuda_dev, tmp_path, dist, depth, sr, n, split):
     worker = os.path.join(HERE, "_multirank_worker.py")
     one = tmp_path / "one.npy"
-    subprocess.run([sys.executable, worker, str(one), dist, str(depth), str(sr)], check=True, timeout=300)
+    extra = [str(n), str(split)]
+    subprocess.run([sys.executable, worker, str(one), dist, str(depth), str(sr), *extra], check=True, timeout=300)
     two = tmp_path / "two.npy"
     port = _port()
     procs = []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), H2OMX_DIST_BACKEND="gloo")
-        procs.append(subprocess.Popen([sys.executable, worker, str(two), dist, str(depth), str(sr)], env=env))
+        procs.append(subprocess.Popen([sys.executable, worker, str(two), dist, str(depth), str(sr), *extra],
+                                      env=env))
     for p in procs:
         assert p.wait(timeout=300) == 0
     a, b = np.load(one), np.load(two)
