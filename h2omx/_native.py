@@ -36,7 +36,8 @@ class NativeLibraryMissing(RuntimeError):
 
 
 def lib_path(name: str) -> str:
-    return os.path.join(_LIB_DIR, f"libh2omx_{name}.so")
+    # H2OMX_LIB_DIR: load kernel-tuning variants built elsewhere (sweeps)
+    return os.path.join(os.environ.get("H2OMX_LIB_DIR") or _LIB_DIR, f"libh2omx_{name}.so")
 
 
 def available(name: str) -> bool:

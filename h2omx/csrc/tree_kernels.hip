@@ -229,7 +229,26 @@ __device__ __forceinline__ uint32_t row_hash(int64_t r, uint32_t salt) {
 // group and slot pass reads the previous ids).  Rows of nodes that stopped
 // splitting retire as ~gid; their exact leaf sums are added by the tree's
 // final partition (all-rows mode).  Saves one streaming pass per level.
-template <int NBT, int ROWS, int PKM, bool ROUTE>
+// CMP (deeper levels, PKM 2/4, ROWS 16): LDS-staged wave compaction.  A
+// ds_add_u64 wave-instruction costs ~14 CU-cycles whatever its lane mask
+// (bench_micro/lds_mask.hip: 14.3 cycles with 12 % of lanes active, 17.3 with
+// all), so issuing one atomic per (row position, feature) wastes most of the
+// LDS pipe on levels where only the smaller children (<= 50 % of the rows)
+// are built.  Here each wave (1024 consecutive rows) ranks its live rows with
+// five bit-plane ballots, writes them as 16-bit entries (row offset | slot <<
+// 10) into a per-wave 2 KB LDS area and reads them back transposed (lane j:
+// entries j, j + 64, ...).  Per feature the 1 KB code tile is stored to that
+// area with one ds_write_b128 per lane (the same coalesced column load as the
+// plain path) and every atomic then carries 64 live rows: ceil(live / 64)
+// full-mask atomics instead of 16 mostly-empty ones.  Same adds, same
+// integer histograms (bit-identical).
+constexpr int CMP_STAGE_BYTES = 2048;   // per wave
+#ifndef H2OMX_HB_PF
+#define H2OMX_HB_PF 1
+#endif
+constexpr int HB_PF = H2OMX_HB_PF;     // feature code loads kept in flight per lane
+
+template <int NBT, int ROWS, int PKM, bool ROUTE, bool CMP>
 __global__ __launch_bounds__(1024) void hist_build_kernel(
     const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ s2,
     const int* __restrict__ nid, const NodeLink* __restrict__ link, const int* __restrict__ ctl,
@@ -268,8 +287,13 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
 
   const int64_t units = npad / ROWS;
   const int64_t u0 = units * chunk / wgpg, u1 = units * (chunk + 1) / wgpg;
-
-  for (int64_t u = u0 + threadIdx.x; u < u1; u += blockDim.x) {
+  // CMP: waves step through the chunk together (64 consecutive units per wave
+  // step) so the ballots below see converged waves; tail lanes re-read the
+  // chunk's last unit and contribute no rows
+  const int64_t ustart = CMP ? u0 + (threadIdx.x & ~63) : u0 + threadIdx.x;
+  for (int64_t uu = ustart; uu < u1; uu += blockDim.x) {
+    const bool inb = !CMP || uu + lane < u1;
+    const int64_t u = CMP ? (inb ? uu + lane : u1 - 1) : uu;
     const int64_t r0 = u * ROWS;
     int s[ROWS];
     bool any = false;
@@ -376,7 +400,11 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
         }
       }
     }
-    if (!any) continue;
+    if constexpr (CMP) {
+      if (__ballot(any && inb) == 0ull) continue;   // wave-uniform
+    } else {
+      if (!any) continue;
+    }
     unsigned long long pk[ROWS];
     if constexpr (PKM == 2) {
 #pragma unroll
@@ -432,9 +460,88 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
       }
     }
     }
-    for (int fi = 0; fi < nf; ++fi) {
+    if constexpr (CMP) {
+      static_assert(ROWS == 16 && (PKM == 2 || PKM == 4), "compaction: 16-row units reading stored rows");
+      uint32_t m = 0;
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r)
+        if (inb && s[r] >= 0 && pk[r] != 0ull) m |= 1u << r;
+      // exclusive rank of this lane's first live row in the wave, from the
+      // bit planes of the per-lane counts (0..16): five ballots, no LDS
+      const uint32_t cnt = __popc(m);
+      const unsigned long long lt = (1ull << lane) - 1ull;
+      int excl = 0, total = 0;
+#pragma unroll
+      for (int bit = 0; bit < 5; ++bit) {
+        const unsigned long long bm = __ballot((cnt >> bit) & 1u);
+        excl += __popcll(bm & lt) << bit;
+        total += __popcll(bm) << bit;
+      }
+      if (total == 0) continue;
+      uint16_t* st16 = reinterpret_cast<uint16_t*>(lds64 + hist_elems) + (threadIdx.x >> 6) * (CMP_STAGE_BYTES / 2);
+      int j = excl;
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r)
+        if ((m >> r) & 1u) st16[j++] = (uint16_t)((lane * ROWS + r) | (s[r] << 10));
+      const int niter = (total + 63) >> 6;
+      const int64_t tile0 = (uu)*ROWS;   // first row of this wave's tile
+      // entry i of this lane is live iff i * 64 + lane < total (every 16-bit
+      // pattern is a valid entry: offset 1023 in slot 63 is 0xFFFF)
+      uint32_t ent[ROWS];
+      unsigned long long pkc[ROWS];
+#pragma unroll
+      for (int i = 0; i < ROWS; ++i) {
+        ent[i] = 0u;
+        if (i * 64 + lane < total) ent[i] = st16[i * 64 + lane];
+      }
+#pragma unroll
+      for (int i = 0; i < ROWS; ++i) {
+        pkc[i] = 0ull;
+        if (i * 64 + lane < total) {
+          const int64_t row = tile0 + (ent[i] & 1023u);
+          if constexpr (PKM == 2) {
+            pkc[i] = pk_buf[row];
+          } else {
+            const uint32_t pw = reinterpret_cast<const uint32_t*>(pk_buf)[row];
+            pkc[i] = ((unsigned long long)(uint32_t)(int)(short)(pw >> 16) << 32) | (unsigned long long)(pw & 0xFFFFu);
+          }
+        }
+      }
+      // the entries are in registers before the code tiles overwrite the area
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      uint8_t* stc = reinterpret_cast<uint8_t*>(st16);
+      uint4 pf[HB_PF];
+#pragma unroll
+      for (int q = 0; q < HB_PF; ++q)
+        if (q < nf) pf[q] = *reinterpret_cast<const uint4*>(codes + (int64_t)(f0 + q) * npad + r0);
+      for (int fb = 0; fb < nf; fb += HB_PF) {
+#pragma unroll
+        for (int q = 0; q < HB_PF; ++q) {
+          const int fi = fb + q;
+          if (fi < nf) {
+            *reinterpret_cast<uint4*>(stc + lane * ROWS) = pf[q];
+            if (fi + HB_PF < nf) pf[q] = *reinterpret_cast<const uint4*>(codes + (int64_t)(f0 + fi + HB_PF) * npad + r0);
+            const int width = width_s[fi], rep = rep_s[fi];
+            const int copy_off = (rep > 1) ? (lane % rep) * width : 0;
+            unsigned long long* hb = lds64 + fi * NBT + copy_off;
+#pragma unroll
+            for (int i = 0; i < ROWS; ++i) {
+              if (i < niter && i * 64 + lane < total) {
+                int bin = stc[ent[i] & 1023u];
+                if (bin == NBT - 1) bin = width - 1;
+                atomicAdd(hb + (int)(ent[i] >> 10) * fg * NBT + bin, pkc[i]);
+              }
+            }
+          }
+        }
+      }
+      continue;
+    }
+    // codes of the next HB_PF features are in flight while this feature's
+    // atomics issue (one load per wave in flight starved HBM: ~3 TB/s)
+    uint32_t pf[HB_PF][ROWS / 4];
+    auto load_codes = [&](int fi, uint32_t* cw) {
       const uint8_t* cp = codes + (int64_t)(f0 + fi) * npad + r0;
-      uint32_t cw[ROWS / 4];
       if constexpr (ROWS == 16) {
         const uint4 c4 = *reinterpret_cast<const uint4*>(cp);
         cw[0] = c4.x; cw[1] = c4.y; cw[2] = c4.z; cw[3] = c4.w;
@@ -442,15 +549,30 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
         const uint2 c2 = *reinterpret_cast<const uint2*>(cp);
         cw[0] = c2.x; cw[1] = c2.y;
       }
-      const int width = width_s[fi], rep = rep_s[fi];
-      const int copy_off = (rep > 1) ? (lane % rep) * width : 0;
-      unsigned long long* hb = lds64 + fi * NBT + copy_off;
+    };
 #pragma unroll
-      for (int r = 0; r < ROWS; ++r) {
-        if (s[r] >= 0 && pk[r] != 0ull) {
-          int bin = (cw[r >> 2] >> (8 * (r & 3))) & 0xff;
-          if (bin == NBT - 1) bin = width - 1;  // NA goes to the last slot of this feature's slice
-          atomicAdd(hb + s[r] * fg * NBT + bin, pk[r]);
+    for (int q = 0; q < HB_PF; ++q)
+      if (q < nf) load_codes(q, pf[q]);
+    for (int fb = 0; fb < nf; fb += HB_PF) {
+#pragma unroll
+      for (int q = 0; q < HB_PF; ++q) {
+        const int fi = fb + q;
+        if (fi < nf) {
+          uint32_t cw[ROWS / 4];
+#pragma unroll
+          for (int k = 0; k < ROWS / 4; ++k) cw[k] = pf[q][k];
+          if (fi + HB_PF < nf) load_codes(fi + HB_PF, pf[q]);
+          const int width = width_s[fi], rep = rep_s[fi];
+          const int copy_off = (rep > 1) ? (lane % rep) * width : 0;
+          unsigned long long* hb = lds64 + fi * NBT + copy_off;
+#pragma unroll
+          for (int r = 0; r < ROWS; ++r) {
+            if (s[r] >= 0 && pk[r] != 0ull) {
+              int bin = (cw[r >> 2] >> (8 * (r & 3))) & 0xff;
+              if (bin == NBT - 1) bin = width - 1;  // NA goes to the last slot of this feature's slice
+              atomicAdd(hb + s[r] * fg * NBT + bin, pk[r]);
+            }
+          }
         }
       }
     }
@@ -1700,6 +1822,10 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
                              int pkm, unsigned long long* partials, const void* part_prev, const int* ctl_prev,
                              int* nid_out, int writer, hipStream_t stream) {
   const bool route = part_prev != nullptr;
+  // pkm bit 3: wave-compacted atomics (CMP; stored rows, 16-row units, <= 64 slots per pass)
+  const bool cmp = (pkm & 8) != 0;
+  pkm &= 7;
+  if (cmp && ((pkm != 2 && pkm != 4) || rows_per_lane != 16 || slot_cnt > 64)) return kBadArg;
   if (route && (ctl_prev == nullptr || nid_out == nullptr || nid_out == nid || (pkm != 2 && pkm != 4)))
     return kBadArg;
   const PartInfo* pp = reinterpret_cast<const PartInfo*>(part_prev);
@@ -1709,25 +1835,41 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
     return kBadArg;
   const int64_t units = npad / rows_per_lane;
   if ((units + wgpg - 1) / wgpg * rows_per_lane > ROWS_CAP) return kBadArg;  // fixed-point headroom
-  const size_t lds = (size_t)slot_cnt * fg * nbt * sizeof(unsigned long long);
+  const size_t lds = (size_t)slot_cnt * fg * nbt * sizeof(unsigned long long) +
+                     (cmp ? (size_t)(threads / 64) * CMP_STAGE_BYTES : 0);
   if (lds > 156 * 1024) return kBadArg;
   const int grid = n_groups * wgpg;
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
-#define H2OMX_HBK(NB, R, M, RT)                                                                              \
-  hipLaunchKernelGGL((hist_build_kernel<NB, R, M, RT>), dim3(grid), dim3(threads), lds, stream, codes, npad, g, \
-                     s2, nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt,     \
+#define H2OMX_HBK(NB, R, M, RT, C)                                                                           \
+  hipLaunchKernelGGL((hist_build_kernel<NB, R, M, RT, C>), dim3(grid), dim3(threads), lds, stream, codes, npad, \
+                     g, s2, nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt,  \
                      slot16, pk_buf, partials, pp, ctl_prev, nid_out, writer)
-#define H2OMX_HB(NB, R)                                     \
-  do {                                                      \
-    if (pkm == 0) H2OMX_HBK(NB, R, 0, false);               \
-    else if (pkm == 1) H2OMX_HBK(NB, R, 1, false);          \
-    else if (pkm == 2 && route) H2OMX_HBK(NB, R, 2, true);  \
-    else if (pkm == 2) H2OMX_HBK(NB, R, 2, false);          \
-    else if (pkm == 3) H2OMX_HBK(NB, R, 3, false);          \
-    else if (route) H2OMX_HBK(NB, R, 4, true);              \
-    else H2OMX_HBK(NB, R, 4, false);                        \
+#define H2OMX_HB(NB, R)                                            \
+  do {                                                             \
+    if (pkm == 0) H2OMX_HBK(NB, R, 0, false, false);               \
+    else if (pkm == 1) H2OMX_HBK(NB, R, 1, false, false);          \
+    else if (pkm == 2 && route) H2OMX_HBK(NB, R, 2, true, false);  \
+    else if (pkm == 2) H2OMX_HBK(NB, R, 2, false, false);          \
+    else if (pkm == 3) H2OMX_HBK(NB, R, 3, false, false);          \
+    else if (route) H2OMX_HBK(NB, R, 4, true, false);              \
+    else H2OMX_HBK(NB, R, 4, false, false);                        \
   } while (0)
-  if (rows_per_lane == 16) {
+#define H2OMX_HBCMP(NB)                                             \
+  do {                                                              \
+    if (pkm == 2 && route) H2OMX_HBK(NB, 16, 2, true, true);        \
+    else if (pkm == 2) H2OMX_HBK(NB, 16, 2, false, true);           \
+    else if (route) H2OMX_HBK(NB, 16, 4, true, true);               \
+    else H2OMX_HBK(NB, 16, 4, false, true);                         \
+  } while (0)
+  if (cmp) {
+    switch (nbt) {
+      case 32: H2OMX_HBCMP(32); break;
+      case 64: H2OMX_HBCMP(64); break;
+      case 128: H2OMX_HBCMP(128); break;
+      case 256: H2OMX_HBCMP(256); break;
+      default: return kBadArg;
+    }
+  } else if (rows_per_lane == 16) {
     switch (nbt) {
       case 32: H2OMX_HB(32, 16); break;
       case 64: H2OMX_HB(64, 16); break;
@@ -1747,6 +1889,7 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
     return kBadArg;
   }
 #undef H2OMX_HB
+#undef H2OMX_HBCMP
 #undef H2OMX_HBK
   return launch_status();
 }

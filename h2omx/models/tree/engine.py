@@ -132,7 +132,8 @@ class HipTreeBuilder:
         # largest workgroup row chunk over every plan this tree can use: sets the
         # fixed-point resolution (finer for smaller chunks), identical across levels
         units = bm.npad // self.ROWS_PER_LANE
-        cands = [self.plan_level(1 << k) for k in range(0, 13)] + [self.plan_level(1 << 20)]
+        # (compacted plans included either way: the scale must not depend on the CMP switch)
+        cands = [self.plan_level(1 << k, c) for k in range(0, 13) for c in (False, True)] + [self.plan_level(1 << 20)]
         self.max_rows_per_wg = max(self.ROWS_PER_LANE * math.ceil(units / c["wgpg"]) for c in cands)
         # >= 2^16 rows per workgroup bounds the per-row fixed-point values to 16 bits
         # (tree_begin: |G_q| <= 2^14, S_q <= 2^15): the packed rows are then stored in
@@ -206,6 +207,17 @@ class HipTreeBuilder:
     # -- planning ------------------------------------------------------------
     DEEP_LDS_BUDGET = int(os.environ.get("H2OMX_HIST_DEEP_LDS_KB", "128")) * 1024
     DEEP_MIN_GROUPS = int(os.environ.get("H2OMX_HIST_DEEP_MIN_GROUPS", "4"))
+    # levels >= 1 of the scan engine: wave-compacted LDS atomics (hist_build CMP: a
+    # partly-masked ds_add_u64 costs as much as a full one, bench_micro/lds_mask.hip).
+    # The kernel adds a 2 KB staging area per wave, so the histogram budgets shrink
+    # to keep 2 (512 threads) / 1 (1024 threads) workgroups per CU.  Bit-identical
+    # but measured slower on HIGGS depth 5 (built fraction 0.3-0.45 per level: 1.28
+    # vs 0.97 ms/tree; the staging round trips cost more than the ~40 % of atomics
+    # saved), so opt-in (H2OMX_HIST_CMP=1)
+    CMP = os.environ.get("H2OMX_HIST_CMP", "0") == "1"
+    CMP_LDS_BUDGET = 56 * 1024
+    CMP_DEEP_LDS_BUDGET = 112 * 1024
+    CMP_MAX_SLOTS = 64
 
     def _plan(self, max_slots: int, budget: int, threads: int):
         per_slot_feat = self.nbt * 8
@@ -229,19 +241,26 @@ class HipTreeBuilder:
         wgpg = max(wgpg, min_wgpg)
         return dict(slot_cnt=slot_cnt, fg=fg, n_groups=n_groups, passes=passes, wgpg=wgpg, threads=threads)
 
-    def plan_level(self, max_slots: int):
+    def plan_level(self, max_slots: int, cmp: bool = False):
         """Feature grouping / slot passes / grid for a level with max_slots built nodes.
         Shallow levels use 64 KB / 512-thread workgroups (2 per CU); levels
         that would need >= 4 feature groups switch to 128 KB / 1024 threads
-        (1 per CU) so each row chunk is re-read by fewer groups."""
-        if max_slots in self.plans:
-            return self.plans[max_slots]
-        plan = self._plan(max_slots, self.LDS_BUDGET, self.THREADS)
-        if self.DEEP_LDS_BUDGET > self.LDS_BUDGET and plan["n_groups"] >= self.DEEP_MIN_GROUPS:
-            deep = self._plan(max_slots, self.DEEP_LDS_BUDGET, 1024)
+        (1 per CU) so each row chunk is re-read by fewer groups.  ``cmp``
+        plans for the wave-compacted kernel (smaller histogram budgets, <= 64
+        slots per pass; plan["cmp"] is False when that does not fit)."""
+        key = (max_slots, cmp)
+        if key in self.plans:
+            return self.plans[key]
+        lo, hi = (self.CMP_LDS_BUDGET, self.CMP_DEEP_LDS_BUDGET) if cmp else (self.LDS_BUDGET, self.DEEP_LDS_BUDGET)
+        plan = self._plan(max_slots, lo, self.THREADS)
+        if hi > lo and plan["n_groups"] >= self.DEEP_MIN_GROUPS:
+            deep = self._plan(max_slots, hi, 1024)
             if deep["n_groups"] < plan["n_groups"] or deep["passes"] < plan["passes"]:
                 plan = deep
-        self.plans[max_slots] = plan
+        plan["cmp"] = cmp
+        if cmp and (plan["slot_cnt"] > self.CMP_MAX_SLOTS or self.ROWS_PER_LANE != 16):
+            plan = dict(self.plan_level(max_slots, False))
+        self.plans[key] = plan
         return plan
 
     def _fused_level(self, d: int) -> bool:
@@ -309,7 +328,8 @@ class HipTreeBuilder:
             else:
                 max_slots = 1 if d == 0 else max(1, max_nodes // 2)
             last = d == max_depth - 1
-            plan = self.plan_level(max_slots)
+            plan = self.plan_level(max_slots, cmp=d > 0 and self.CMP and not self.COMPACT)
+            cmp_flag = 8 if plan["cmp"] else 0
             built = self._buf("built", max_slots * self.per_node, torch.int64)
             hist_elems = plan["slot_cnt"] * plan["fg"] * nbt
             partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_elems, torch.int64)
@@ -325,7 +345,8 @@ class HipTreeBuilder:
                             P(part_prev), P(ctl_nxt),
                             P(nid_buf[d % 2]), 1 if ps == 0 else 0, P(ctl_cur), P(bm.nvb), P(self.qscale), F, nbt,
                             plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo, plan["slot_cnt"],
-                            self.ROWS_PER_LANE, plan["threads"], P(self.pk), 4 if self.pk32 else 2, P(partials), st),
+                            self.ROWS_PER_LANE, plan["threads"], P(self.pk), (4 if self.pk32 else 2) + cmp_flag,
+                            P(partials), st),
                             "hist_build_route")
                     elif d > 0 and self.COMPACT:
                         ops.check(lib.h2omx_hist_build_compact(
@@ -342,8 +363,9 @@ class HipTreeBuilder:
                             P(link[cur]), P(ctl_cur), P(bm.nvb),
                             P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, plan["fg"], plan["n_groups"],
                             plan["wgpg"], slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],
-                            P(self.slot16), P(self.pk), (1 if d == 0 else 2) + (2 if self.pk32 else 0), P(partials),
-                            st), "hist_build")
+                            P(self.slot16), P(self.pk),
+                            (1 if d == 0 else 2 + cmp_flag) + (2 if self.pk32 else 0), P(partials), st),
+                            "hist_build")
                     ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F,
                                                     nbt, slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st),
                               "hist_reduce")

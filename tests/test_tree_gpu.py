@@ -182,6 +182,37 @@ def test_compact_hist_matches_plain(cuda_dev, monkeypatch, dist, depth, sample_r
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
 
 
+@pytest.mark.parametrize("dist,depth,sample_rate,nbins,fuse", [
+    ("bernoulli", 5, 1.0, 255, True), ("bernoulli", 5, 1.0, 255, False), ("gaussian", 9, 0.7, 63, True),
+    ("multinomial", 4, 1.0, 255, True), ("drf", 12, 0.632, 20, False)])
+def test_wave_compacted_atomics_match_plain(cuda_dev, monkeypatch, dist, depth, sample_rate, nbins, fuse):
+    """hist_build's LDS-staged wave compaction (CMP, levels >= 1) builds
+    bit-identical trees to one atomic per row position; the depth-12 / 20-bin
+    case runs passes of 64 slots (16-bit entry 0xFFFF is a live row)."""
+    import h2omx.models.tree.engine as E
+
+    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi", "drf": "bin"}[dist]
+    X, y = _data(n=60000, F=9, seed=8, task=task)
+    _, bg = _both(X, y, nbins)
+    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2, leaf_mode=1 if dist == "drf" else 0,
+                    mtries=3 if dist == "drf" else 0)
+    yt = torch.from_numpy(y).cuda()
+    monkeypatch.setenv("H2OMX_TREE_ENGINE", "scan")
+    monkeypatch.setenv("H2OMX_FUSE_ROUTE", "1" if fuse else "0")
+    nclass = 3 if dist == "multinomial" else (2 if dist == "drf" else 1)
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(E.HipTreeBuilder, "CMP", flag)
+        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
+                                   nclass=nclass, seed=7)
+    a, b = out[False], out[True]
+    for t in range(a.trees.shape[0]):
+        reach = a.compact()[t]
+        assert reach == b.compact()[t]
+        for f in ("feat", "bin", "value"):
+            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
+
+
 @pytest.mark.parametrize("dist,depth,sample_rate", [("bernoulli", 5, 1.0), ("gaussian", 7, 0.7)])
 def test_pk32_rows_match_pk64(cuda_dev, monkeypatch, dist, depth, sample_rate):
     """32-bit packed rows (large row chunks: per-row values fit 16 bits) build
