@@ -258,6 +258,7 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     const int* __restrict__ ctl_prev, int* __restrict__ nid_out, int writer) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
   __shared__ int width_s[256], rep_s[256];
+  __shared__ float rcp_s[256];
   const int n_slots = ctl[CTL_SLOTS];
   const int b = blockIdx.x;
   const int xcd = b & 7, i = b >> 3;
@@ -278,7 +279,9 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     const int w = (fi < nf) ? nvb[f0 + fi] + 1 : NBT;
     width_s[fi] = w;
     int r = NBT / w;
-    rep_s[fi] = r < 1 ? 1 : (r > 64 ? 64 : r);
+    r = r < 1 ? 1 : (r > 64 ? 64 : r);
+    rep_s[fi] = r;
+    rcp_s[fi] = 1.0f / (float)r;   // lane % rep without an integer division (lane < 64: exact)
   }
   const float sg = (float)qscale[0], ss = (float)qscale[1];
   const int64_t rb = (int64_t)qscale[7];  // global row offset of this rank (dither)
@@ -523,12 +526,13 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
             if (fi + HB_PF < nf) pf[q] = *reinterpret_cast<const uint4*>(codes + (int64_t)(f0 + fi + HB_PF) * npad + r0);
             const int width = width_s[fi], rep = rep_s[fi];
             const int copy_off = (rep > 1) ? (lane % rep) * width : 0;
+            const int na_slot = (rep > 1) ? width - 1 : NBT - 1;   // see the fold below
             unsigned long long* hb = lds64 + fi * NBT + copy_off;
 #pragma unroll
             for (int i = 0; i < ROWS; ++i) {
               if (i < niter && i * 64 + lane < total) {
                 int bin = stc[ent[i] & 1023u];
-                if (bin == NBT - 1) bin = width - 1;
+                if (bin == NBT - 1) bin = na_slot;
                 atomicAdd(hb + (int)(ent[i] >> 10) * fg * NBT + bin, pkc[i]);
               }
             }
@@ -553,6 +557,10 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
 #pragma unroll
     for (int q = 0; q < HB_PF; ++q)
       if (q < nf) load_codes(q, pf[q]);
+    // per-row slot offset into the histogram (-1: nothing to add), once per unit
+    int so[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) so[r] = (s[r] >= 0 && pk[r] != 0ull) ? s[r] * fg * NBT : -1;
     for (int fb = 0; fb < nf; fb += HB_PF) {
 #pragma unroll
       for (int q = 0; q < HB_PF; ++q) {
@@ -562,15 +570,27 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
 #pragma unroll
           for (int k = 0; k < ROWS / 4; ++k) cw[k] = pf[q][k];
           if (fi + HB_PF < nf) load_codes(fi + HB_PF, pf[q]);
-          const int width = width_s[fi], rep = rep_s[fi];
-          const int copy_off = (rep > 1) ? (lane % rep) * width : 0;
-          unsigned long long* hb = lds64 + fi * NBT + copy_off;
+          const int rep = rep_s[fi];
+          if (rep > 1) {
+            // replicated low-cardinality slice: copy lane % rep, NA at the
+            // slice's last slot (wave-uniform branch: rep is per feature)
+            const int width = width_s[fi];
+            const int copy = lane - rep * (int)(((float)lane + 0.5f) * rcp_s[fi]);
+            unsigned long long* hb = lds64 + fi * NBT + copy * width;
 #pragma unroll
-          for (int r = 0; r < ROWS; ++r) {
-            if (s[r] >= 0 && pk[r] != 0ull) {
-              int bin = (cw[r >> 2] >> (8 * (r & 3))) & 0xff;
-              if (bin == NBT - 1) bin = width - 1;  // NA goes to the last slot of this feature's slice
-              atomicAdd(hb + s[r] * fg * NBT + bin, pk[r]);
+            for (int r = 0; r < ROWS; ++r) {
+              if (so[r] >= 0) {
+                int bin = (cw[r >> 2] >> (8 * (r & 3))) & 0xff;
+                if (bin == NBT - 1) bin = width - 1;
+                atomicAdd(hb + so[r] + bin, pk[r]);
+              }
+            }
+          } else {
+            // one NBT-wide slice: the NA code NBT - 1 is its own slot (no remap)
+            unsigned long long* hb = lds64 + fi * NBT;
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+              if (so[r] >= 0) atomicAdd(hb + so[r] + ((cw[r >> 2] >> (8 * (r & 3))) & 0xff), pk[r]);
             }
           }
         }
@@ -585,11 +605,14 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     const int fi = (j / NBT) % fg;
     const int sl = j / (NBT * fg);
     const int width = width_s[fi], rep = rep_s[fi];
-    const int src = (bin == NBT - 1) ? width - 1 : bin;
+    const unsigned long long* hb = lds64 + (sl * fg + fi) * NBT;
     unsigned long long acc = 0ull;
-    if (src < width - 1 || bin == NBT - 1) {
-      const unsigned long long* hb = lds64 + (sl * fg + fi) * NBT;
-      for (int c = 0; c < rep; ++c) acc += hb[c * width + src];
+    if (rep == 1) {
+      acc = hb[bin];   // one slice, NA kept in its own slot NBT - 1
+    } else {
+      const int src = (bin == NBT - 1) ? width - 1 : bin;
+      if (src < width - 1 || bin == NBT - 1)
+        for (int c = 0; c < rep; ++c) acc += hb[c * width + src];
     }
     out[j] = acc;
   }
@@ -1444,6 +1467,173 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
     }
   }
 }
+// Routing pass of the fused pipeline (levels whose partition is not fused
+// into the next histogram, and the final level).  Same decisions as
+// partition_kernel(all_rows), restructured for the memory system:
+//   * the level's PartInfo table is staged in LDS (no dependent global
+//     gather per row between the node id and the split code);
+//   * split codes come from ONE coalesced 16-byte column load per distinct
+//     split feature of the level and lane (wave-uniform loop; a feature no
+//     row of the wave needs is skipped), not from per-row byte gathers
+//     scattered over up to n_nodes columns;
+//   * 16 rows per lane: node ids / g / h / w / slot16 move as 16-byte vectors.
+// LEAF (final level): every row retires and adds its exact fixed-point
+// (g, h, w) to the whole-tree LDS window (lane-private copies [slot][copy]),
+// folded into leaf_acc with integer atomics (deterministic).
+constexpr int ROUTE_MAX_NODES = 256;
+constexpr int ROUTE_RPL = 16;
+#ifndef H2OMX_ROUTE_FB
+#define H2OMX_ROUTE_FB 8
+#endif
+constexpr int ROUTE_FB = H2OMX_ROUTE_FB;
+
+template <bool LEAF>
+__global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ codes, int64_t npad,
+                                                    const int* nid_in, int* nid_out,
+                                                    const PartInfo* __restrict__ part, int nbt,
+                                                    const float* __restrict__ g, const float* __restrict__ h,
+                                                    const float* __restrict__ w, const double* __restrict__ qs,
+                                                    int cap, unsigned long long* __restrict__ leaf_acc,
+                                                    const int* __restrict__ ctl_cur, int R,
+                                                    short* __restrict__ slot16) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lacc[];
+  __shared__ PartInfo pi_s[ROUTE_MAX_NODES];
+  __shared__ int first_s[ROUTE_MAX_NODES];
+  __shared__ int flist[ROUTE_MAX_NODES];
+  __shared__ int nfl_s;
+  const int n_nodes = ctl_cur[CTL_N];
+  for (int j = threadIdx.x; j < n_nodes; j += blockDim.x) pi_s[j] = part[j];
+  if (LEAF)
+    for (int j = threadIdx.x; j < 3 * cap * R; j += blockDim.x) lacc[j] = 0ull;
+  __syncthreads();
+  // distinct split features of the level, in node order
+  for (int j = threadIdx.x; j < n_nodes; j += blockDim.x) {
+    int first = pi_s[j].child >= 0;
+    for (int i = 0; i < j && first; ++i)
+      if (pi_s[i].child >= 0 && pi_s[i].feat == pi_s[j].feat) first = 0;
+    first_s[j] = first;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int c = 0;
+    for (int j = 0; j < n_nodes; ++j)
+      if (first_s[j]) flist[c++] = pi_s[j].feat;
+    nfl_s = c;
+  }
+  __syncthreads();
+  const int nfl = nfl_s;
+  const int lane = threadIdx.x & 63;
+  const int copy = lane % R;
+  float lg = 0.f, lh = 0.f, lw = 0.f;
+  if (LEAF) { lg = (float)qs[4]; lh = (float)qs[5]; lw = (float)qs[6]; }
+  const int64_t nq = npad / ROUTE_RPL;
+  // waves step together (the per-feature ballot needs converged waves)
+  const int64_t qstep = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t qb = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); qb < nq; qb += qstep) {
+    const int64_t q = qb + lane;
+    const bool inb = q < nq;
+    const int64_t r0 = (inb ? q : nq - 1) * ROUTE_RPL;
+    int nn[ROUTE_RPL];
+#pragma unroll
+    for (int v = 0; v < ROUTE_RPL / 4; ++v) {
+      const int4 a = *reinterpret_cast<const int4*>(nid_in + r0 + 4 * v);
+      nn[4 * v] = a.x; nn[4 * v + 1] = a.y; nn[4 * v + 2] = a.z; nn[4 * v + 3] = a.w;
+    }
+    float gv[ROUTE_RPL], hv[ROUTE_RPL], wv[ROUTE_RPL];
+    if (LEAF) {
+#pragma unroll
+      for (int v = 0; v < ROUTE_RPL / 4; ++v) {
+        const float4 g4 = *reinterpret_cast<const float4*>(g + r0 + 4 * v);
+        const float4 h4 = *reinterpret_cast<const float4*>(h + r0 + 4 * v);
+        float4 w4 = make_float4(1.f, 1.f, 1.f, 1.f);
+        if (w) w4 = *reinterpret_cast<const float4*>(w + r0 + 4 * v);
+        gv[4 * v] = g4.x; gv[4 * v + 1] = g4.y; gv[4 * v + 2] = g4.z; gv[4 * v + 3] = g4.w;
+        hv[4 * v] = h4.x; hv[4 * v + 1] = h4.y; hv[4 * v + 2] = h4.z; hv[4 * v + 3] = h4.w;
+        wv[4 * v] = w4.x; wv[4 * v + 1] = w4.y; wv[4 * v + 2] = w4.z; wv[4 * v + 3] = w4.w;
+      }
+    }
+    int fe[ROUTE_RPL];   // split feature of the row's node (-1: none)
+#pragma unroll
+    for (int k = 0; k < ROUTE_RPL; ++k) fe[k] = (nn[k] >= 0 && pi_s[nn[k]].child >= 0) ? pi_s[nn[k]].feat : -1;
+    uint32_t right = 0;
+    // ROUTE_FB column loads issued together per batch (a loop with one dependent
+    // load per feature exposed ~16 HBM latencies per lane step)
+    for (int t0 = 0; t0 < nfl; t0 += ROUTE_FB) {
+      uint4 c4[ROUTE_FB];
+#pragma unroll
+      for (int q = 0; q < ROUTE_FB; ++q)
+        if (t0 + q < nfl) c4[q] = *reinterpret_cast<const uint4*>(codes + (int64_t)flist[t0 + q] * npad + r0);
+#pragma unroll
+      for (int q = 0; q < ROUTE_FB; ++q) {
+        if (t0 + q < nfl) {
+          const int f = flist[t0 + q];
+          const uint32_t cw[4] = {c4[q].x, c4[q].y, c4[q].z, c4[q].w};
+#pragma unroll
+          for (int k = 0; k < ROUTE_RPL; ++k) {
+            if (fe[k] == f) {
+              const PartInfo& pi = pi_s[nn[k]];
+              const int bc = (cw[k >> 2] >> (8 * (k & 3))) & 0xff;
+              const int rt = (bc == nbt - 1) ? !pi.na_left : (bc > pi.bin);
+              right |= (uint32_t)rt << k;
+            }
+          }
+        }
+      }
+    }
+    int sv[ROUTE_RPL];
+#pragma unroll
+    for (int k = 0; k < ROUTE_RPL; ++k) {
+      sv[k] = -1;
+      const int n = nn[k];
+      int leaf = -1;
+      if (n < 0) {
+        leaf = ~n;   // retired at an earlier level (padding INT_MIN -> beyond cap)
+      } else {
+        const PartInfo& pi = pi_s[n];
+        const int rt = (right >> k) & 1;
+        if (pi.child < 0) {
+          leaf = pi.gid;
+        } else if (pi.leaf_children) {
+          leaf = pi.child_gid + rt;
+        } else {
+          nn[k] = pi.child + rt;
+          sv[k] = rt ? (pi.pad >> 16) : (int)(short)(pi.pad & 0xFFFF);
+        }
+        if (leaf >= 0) nn[k] = ~leaf;
+      }
+      if (LEAF && inb && leaf >= 0 && leaf < cap && wv[k] != 0.0f) {
+        const unsigned long long a = (unsigned long long)(long long)__float2int_rn(gv[k] * lg);
+        const unsigned long long b = (unsigned long long)(long long)__float2int_rn(hv[k] * lh);
+        const unsigned long long c = (unsigned long long)(long long)__float2int_rn(wv[k] * lw);
+        unsigned long long* d = lacc + (3 * leaf) * R + copy;
+        atomicAdd(d, a);
+        atomicAdd(d + R, b);
+        atomicAdd(d + 2 * R, c);
+      }
+    }
+    if (inb) {
+#pragma unroll
+      for (int v = 0; v < ROUTE_RPL / 4; ++v)
+        *reinterpret_cast<int4*>(nid_out + r0 + 4 * v) = make_int4(nn[4 * v], nn[4 * v + 1], nn[4 * v + 2], nn[4 * v + 3]);
+      if (!LEAF) {
+#pragma unroll
+        for (int v = 0; v < ROUTE_RPL / 8; ++v)
+          *reinterpret_cast<int4*>(slot16 + r0 + 8 * v) =
+              make_int4((sv[8 * v] & 0xFFFF) | (sv[8 * v + 1] << 16), (sv[8 * v + 2] & 0xFFFF) | (sv[8 * v + 3] << 16),
+                        (sv[8 * v + 4] & 0xFFFF) | (sv[8 * v + 5] << 16), (sv[8 * v + 6] & 0xFFFF) | (sv[8 * v + 7] << 16));
+      }
+    }
+  }
+  if (LEAF) {
+    __syncthreads();
+    for (int s = threadIdx.x; s < 3 * cap; s += blockDim.x) {
+      unsigned long long v = 0ull;
+      for (int c = 0; c < R; ++c) v += lacc[s * R + c];
+      if (v) atomicAdd(leaf_acc + s, v);
+    }
+  }
+}
+
 // leaf_acc[j] += sum over the partition slabs (one 256-thread block per j).
 __global__ __launch_bounds__(256) void leaf_reduce_kernel(const unsigned long long* __restrict__ slab, int n_slabs,
                                                           int width, unsigned long long* __restrict__ leaf_acc) {
@@ -2083,6 +2273,33 @@ H2OMX_API int h2omx_partition_final(const uint8_t* codes, int64_t npad, const in
                                     const int* ctl_next, int blocks, hipStream_t stream) {
   return partition_launch(codes, npad, const_cast<int*>(nid_in), part, nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
                           ctl_next, cap, blocks, 1, nullptr, nid_out, 1, stream);
+}
+
+// route_kernel entry (fused pipeline): final = 1 -> last level (leaf sums of
+// every row into leaf_acc, nid_out = ~leaf gid); final = 0 -> intermediate
+// level (nid_out, slot16).  max_nodes bounds the level's node count.
+H2OMX_API int h2omx_route_level(const uint8_t* codes, int64_t npad, const int* nid_in, int* nid_out, const void* part,
+                                int nbt, const float* g, const float* h, const float* w, const double* qscale,
+                                int cap, unsigned long long* leaf_acc, const int* ctl_cur, int max_nodes, int blocks,
+                                short* slot16, int final_level, hipStream_t stream) {
+  // nid_in == nid_out is allowed (each lane rewrites only the rows it read)
+  if (max_nodes > ROUTE_MAX_NODES || npad % ROUTE_RPL != 0 || blocks < 1) return kBadArg;
+  const PartInfo* pp = reinterpret_cast<const PartInfo*>(part);
+  if (final_level) {
+    if (leaf_acc == nullptr || g == nullptr || h == nullptr || qscale == nullptr) return kBadArg;
+    constexpr size_t kWinLds = 64 * 1024;
+    int R = 64;
+    while (R > 1 && (size_t)3 * cap * R * sizeof(unsigned long long) > kWinLds) R >>= 1;
+    if ((size_t)3 * cap * R * sizeof(unsigned long long) > kWinLds) return kBadArg;
+    hipLaunchKernelGGL(route_kernel<true>, dim3(blocks), dim3(256), (size_t)3 * cap * R * sizeof(unsigned long long),
+                       stream, codes, npad, nid_in, nid_out, pp, nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur, R,
+                       nullptr);
+  } else {
+    if (slot16 == nullptr) return kBadArg;
+    hipLaunchKernelGGL(route_kernel<false>, dim3(blocks), dim3(256), 0, stream, codes, npad, nid_in, nid_out, pp, nbt,
+                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, ctl_cur, 1, slot16);
+  }
+  return launch_status();
 }
 
 static inline int stream_grid(int64_t) { return STAT_BLOCKS; }

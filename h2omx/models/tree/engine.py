@@ -218,6 +218,9 @@ class HipTreeBuilder:
     CMP_LDS_BUDGET = 56 * 1024
     CMP_DEEP_LDS_BUDGET = 112 * 1024
     CMP_MAX_SLOTS = 64
+    # fused pipeline: routing passes via route_kernel (PartInfo in LDS, one coalesced
+    # column load per distinct split feature) instead of partition_kernel's gathers
+    ROUTE_KERNEL = os.environ.get("H2OMX_ROUTE_KERNEL", "0") == "1"
 
     def _plan(self, max_slots: int, budget: int, threads: int):
         per_slot_feat = self.nbt * 8
@@ -402,7 +405,16 @@ class HipTreeBuilder:
             # leaves that can retire at this level: gids [base, base + n + n_next)
             win = min(3 * max_nodes, self.capacity)
             with T("partition"):
-                if fuse and last:
+                route_k = self.ROUTE_KERNEL and max_nodes <= 256
+                if fuse and route_k and (last or not self._fused_level(d + 1)):
+                    ops.check(lib.h2omx_route_level(P(bm.codes), bm.npad, P(nid_buf[d % 2]),
+                                                    P(self.nid if last else nid_buf[(d + 1) % 2]), P(part), nbt,
+                                                    P(g if last else None), P(h if last else None),
+                                                    P(w if last else None), P(self.qscale if last else None),
+                                                    self.capacity, P(self.leaf_acc if last else None), P(ctl_cur),
+                                                    max_nodes, self.part_blocks, P(None if last else self.slot16),
+                                                    1 if last else 0, st), "route_level")
+                elif fuse and last:
                     ops.check(lib.h2omx_partition_final(P(bm.codes), bm.npad, P(nid_buf[d % 2]), P(self.nid),
                                                         P(part), nbt, P(g), P(h), P(w), P(self.qscale),
                                                         self.capacity, P(self.leaf_acc), P(ctl_cur), P(ctl_nxt),

@@ -29,6 +29,7 @@ TREE_SIGS = {
     "h2omx_partition_blocks": "",
     "h2omx_partition_final": "PLPPPIPPPPIPPPIS",
     "h2omx_partition_route": "PLPPPIPPIPS",
+    "h2omx_route_level": "PLPPPIPPPPIPPIIPIS",
     "h2omx_leaf_reduce": "PIIPS",
     "h2omx_boost_update": "PPPLLPPPPPPPS",
     "h2omx_apply_tree": "PLPPS",

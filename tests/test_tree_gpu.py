@@ -213,6 +213,36 @@ def test_wave_compacted_atomics_match_plain(cuda_dev, monkeypatch, dist, depth, 
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
 
 
+@pytest.mark.parametrize("dist,depth,sample_rate,nbins", [
+    ("bernoulli", 5, 1.0, 255), ("gaussian", 8, 0.7, 63), ("multinomial", 4, 1.0, 255), ("bernoulli", 2, 1.0, 20),
+    ("drf", 7, 0.632, 255)])
+def test_route_kernel_matches_partition_kernel(cuda_dev, monkeypatch, dist, depth, sample_rate, nbins):
+    """The fused pipeline's routing passes through route_kernel (LDS split
+    table, per-feature coalesced code loads) build bit-identical trees and
+    exact leaf sums to partition_kernel's per-row gathers."""
+    import h2omx.models.tree.engine as E
+
+    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi", "drf": "bin"}[dist]
+    X, y = _data(n=70000, F=11, seed=4, task=task)
+    _, bg = _both(X, y, nbins)
+    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2, leaf_mode=1 if dist == "drf" else 0,
+                    mtries=4 if dist == "drf" else 0)
+    yt = torch.from_numpy(y).cuda()
+    monkeypatch.setenv("H2OMX_TREE_ENGINE", "scan")
+    nclass = 3 if dist == "multinomial" else (2 if dist == "drf" else 1)
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(E.HipTreeBuilder, "ROUTE_KERNEL", flag)
+        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
+                                   nclass=nclass, seed=9)
+    a, b = out[False], out[True]
+    for t in range(a.trees.shape[0]):
+        reach = a.compact()[t]
+        assert reach == b.compact()[t]
+        for f in ("feat", "bin", "value", "weight"):
+            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
+
+
 @pytest.mark.parametrize("dist,depth,sample_rate", [("bernoulli", 5, 1.0), ("gaussian", 7, 0.7)])
 def test_pk32_rows_match_pk64(cuda_dev, monkeypatch, dist, depth, sample_rate):
     """32-bit packed rows (large row chunks: per-row values fit 16 bits) build
