@@ -163,6 +163,10 @@ class H2OApi:
     def __init__(self, cluster, shutdown_cb=None):
         self.cluster = cluster
         self.jobs = JobRegistry()
+        self.peer_lost: str | None = None
+        wd = getattr(cluster, "watchdog", None)
+        if wd is not None:
+            wd.on_lost(self._on_peer_lost)
         self.sessions: dict[str, float] = {}
         self.started_ms = int(time.time() * 1000)
         self.shutdown_cb = shutdown_cb
@@ -296,7 +300,8 @@ class H2OApi:
         infos = []
         for r in range(self.cluster.world_size):
             ent = {"__meta": S.meta("NodeV3", "Iced"), "h2o": f"rank{r}", "ip_port": f"rank{r}:54321",
-                   "healthy": True, "last_ping": int(time.time() * 1000), "pid": os.getpid() if r == 0 else -1,
+                   "healthy": self.peer_lost is None, "last_ping": int(time.time() * 1000),
+                   "pid": os.getpid() if r == 0 else -1,
                    "num_cpus": os.cpu_count() or 1, "cpus_allowed": os.cpu_count() or 1, "nthreads": 16,
                    "sys_load": 0.0, "my_cpu_pct": -1, "sys_cpu_pct": -1, "mem_value_size": 0, "pojo_mem": 0,
                    "free_mem": 0, "max_mem": 0, "swap_mem": 0, "num_keys": len(DKV.keys()), "free_disk": 0,
@@ -310,8 +315,16 @@ class H2OApi:
             infos.append(ent)
         return infos
 
+    def _on_peer_lost(self, reason: str) -> None:
+        self.peer_lost = reason
+        self.jobs.fail_running(reason)
+
     def cloud(self, **_):
-        return S.cloud_json(self.cluster, self.started_ms, self._node_infos())
+        out = S.cloud_json(self.cluster, self.started_ms, self._node_infos())
+        if self.peer_lost is not None:
+            out["cloud_healthy"] = False
+            out["bad_nodes"] = max(1, int(out.get("bad_nodes") or 0))
+        return out
 
     def about(self, **_):
         import torch

@@ -26,6 +26,15 @@ class Comm:
         self.device = device or torch.device("cpu")
         self.group = group
         self.stats = {"all_reduce_calls": 0, "all_reduce_bytes": 0, "all_reduce_s": 0.0}
+        # set by the peer watchdog (runtime/watchdog.py) once a rank is lost:
+        # collectives then fail fast instead of blocking on the missing peer
+        self.failed: str | None = None
+
+    def _check(self) -> None:
+        if self.failed is not None:
+            from ..runtime.watchdog import PeerLost
+
+            raise PeerLost(self.failed)
 
     # ------------------------------------------------------------------
     @classmethod
@@ -62,6 +71,7 @@ class Comm:
     def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if self.world_size == 1:
             return t
+        self._check()
         self.stats["all_reduce_calls"] += 1
         self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
@@ -73,6 +83,7 @@ class Comm:
         buckets overlapped with the rest of back-propagation)."""
         if self.world_size == 1:
             return _Done()
+        self._check()
         self.stats["all_reduce_calls"] += 1
         self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
@@ -93,6 +104,7 @@ class Comm:
     def all_gather_cat(self, t: torch.Tensor, dim: int = 0) -> torch.Tensor:
         if self.world_size == 1:
             return t
+        self._check()
         # shapes may differ in `dim`: gather sizes first
         n = torch.tensor([t.shape[dim]], dtype=torch.int64, device=t.device)
         sizes = [torch.zeros_like(n) for _ in range(self.world_size)]
@@ -109,6 +121,7 @@ class Comm:
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.world_size > 1:
+            self._check()
             dist.broadcast(t, src=src, group=self.group)
         return t
 
@@ -121,6 +134,7 @@ class Comm:
 
     def barrier(self) -> None:
         if self.world_size > 1:
+            self._check()
             if self.device.type == "cuda" and dist.get_backend(self.group) == "nccl":
                 dist.barrier(group=self.group, device_ids=[self.device.index])
             else:

@@ -144,6 +144,7 @@ class Cluster:
         self.lock = threading.RLock()
         self.ops: dict = {}
         self.started = time.time()
+        self.watchdog = None      # runtime/watchdog.PeerWatchdog on multi-node clouds
         self.formed = True
         self.stop = threading.Event()
 
@@ -206,6 +207,8 @@ class Cluster:
         return failures
 
     def shutdown_workers(self):
+        if self.watchdog is not None:
+            self.watchdog.stop()      # peers leaving on purpose are not lost
         if self.is_leader and self.world_size > 1 and self.store is not None:
             with self.lock:
                 self.seq += 1
@@ -227,6 +230,8 @@ class Cluster:
                         return
             cmd = json.loads(self.store.get(key).decode())
             if cmd["op"] == "__shutdown__":
+                if self.watchdog is not None:
+                    self.watchdog.stop()
                 return
             try:
                 self._execute(cmd["op"], cmd["kwargs"])
@@ -270,6 +275,11 @@ def form_cluster(cfg: ClusterConfig | None = None, device: str | None = None, ti
                               timeout=datetime.timedelta(seconds=timeout_s))
     comm = Comm(cfg.rank, cfg.world_size, dev)
     cl = Cluster(cfg, comm, store)
+    if cfg.world_size > 1 and os.environ.get("H2OMX_WATCHDOG", "1") != "0":
+        from .watchdog import PeerWatchdog
+
+        # bounded detection of a lost / hung peer (instead of the PG timeout)
+        cl.watchdog = PeerWatchdog(cfg.master_addr, cfg.bus_port, cfg.rank, cfg.world_size, comm).start()
     from . import ops
 
     ops.register_all(cl)

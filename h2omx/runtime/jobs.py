@@ -79,15 +79,18 @@ class JobRegistry:
             _local.job = job
             try:
                 job.result = fn(job, *args, **kw)
-                if job.cancel_requested:
+                if job.status == "FAILED":
+                    pass   # failed meanwhile by the peer watchdog (fail_running)
+                elif job.cancel_requested:
                     job.status = "CANCELLED"
                 else:
                     job.status = "DONE"
                     job.progress = 1.0
             except Exception as e:  # noqa: BLE001
-                job.status = "FAILED"
-                job.exception = f"{type(e).__name__}: {e}"
-                job.stacktrace = traceback.format_exc()
+                if job.status != "FAILED":
+                    job.status = "FAILED"
+                    job.exception = f"{type(e).__name__}: {e}"
+                    job.stacktrace = traceback.format_exc()
             finally:
                 _local.job = None
                 job.end_time = int(time.time() * 1000)
@@ -98,6 +101,18 @@ class JobRegistry:
             job.thread = threading.Thread(target=run, name=f"job-{job.key[-12:]}", daemon=True)
             job.thread.start()
         return job
+
+    def fail_running(self, reason: str) -> int:
+        """Fail every running job now (a peer rank was lost: their collectives
+        cannot complete).  Returns the number of jobs failed."""
+        n = 0
+        for j in list(self.jobs.values()):
+            if j.status in ("CREATED", "RUNNING"):
+                j.status = "FAILED"
+                j.exception = f"PeerLost: {reason}"
+                j.end_time = int(time.time() * 1000)
+                n += 1
+        return n
 
     def get(self, key: str) -> Job | None:
         return self.jobs.get(key)
