@@ -30,6 +30,7 @@ struct Options {
   std::string ns;  // "" = all namespaces
   bool once = false;
   int resync_s = 30;
+  int requeue_s = 2;
   std::string default_image = "h2omx/h2omx-node";
   std::string default_tag = "latest";
 };
@@ -101,14 +102,47 @@ void adopt(Json& obj, const Json& cr, const std::string& hash) {
   md["annotations"]["h2o.ai/spec-hash"] = hash;
 }
 
+// Desired-vs-actual comparison of the fields of the headless Service that
+// someone may edit by hand (ports, selector); clusterIP is immutable.
+bool service_drifted(const Json& cur, const Json& want) {
+  const Json* cs = cur.find("spec");
+  const Json* ws = want.find("spec");
+  if (!cs || !ws) return true;
+  auto ports = [](const Json* spec) {
+    Json out = Json::array();
+    if (const Json* ps = spec->find("ports"))
+      if (ps->is_array())
+        for (auto& p : ps->as_array()) {
+          Json q = Json::object();
+          q["port"] = p.get_int("port", 0);
+          q["targetPort"] = p.find("targetPort") ? p.at("targetPort") : Json(p.get_int("port", 0));
+          q["protocol"] = p.get_string("protocol", "TCP");
+          out.push_back(q);
+        }
+    return out;
+  };
+  const Json* csel = cs->find("selector");
+  const Json* wsel = ws->find("selector");
+  return ports(cs) != ports(ws) || !csel || !wsel || *csel != *wsel;
+}
+
+const std::string* annotation(const Json& obj, const std::string& key) {
+  const Json* ann = obj.path("metadata.annotations");
+  if (!ann || !ann->is_object() || !ann->has(key)) return nullptr;
+  const Json& v = ann->at(key);
+  return v.is_string() ? &v.as_string() : nullptr;
+}
+
 class Reconciler {
  public:
   Reconciler(KubeClient& c, Options o) : c_(c), o_(std::move(o)) {}
 
-  void reconcile(const Json& cr) {
+  // Returns true when the CR needs another pass soon (a replaced StatefulSet
+  // is still terminating): the main loop then re-lists within seconds.
+  bool reconcile(const Json& cr) {
     const std::string name = object_name(cr);
     const std::string ns = cr.get_string("metadata.namespace", "default");
-    if (cr.path("metadata.deletionTimestamp")) return;  // GC via ownerReferences
+    if (cr.path("metadata.deletionTimestamp")) return false;  // GC via ownerReferences
     DeploymentSpecification s = spec_from_cr(cr, o_);
     Json svc = h2o_service(s);
     Json sts = h2o_stateful_set(s);
@@ -116,37 +150,30 @@ class Reconciler {
     adopt(svc, cr, hash);
     adopt(sts, cr, hash);
     std::string phase, message;
+    bool requeue = false;
+    IngressState ing;
     try {
-      if (!c_.get_opt(kinds::Service, ns, s.name + "-service")) {
-        c_.create(kinds::Service, ns, svc);
-        log(ns, name, "created service " + s.name + "-service");
-      }
-      auto cur = c_.get_opt(kinds::StatefulSet, ns, s.name + "-stateful-set");
-      if (!cur) {
-        c_.create(kinds::StatefulSet, ns, sts);
-        log(ns, name, "created statefulset " + s.name + "-stateful-set");
-      } else if (cur->get_string("metadata.annotations.h2o.ai/spec-hash") != hash &&
-                 cur->path("metadata.annotations") &&
-                 cur->path("metadata.annotations")->find("h2o.ai/spec-hash") &&
-                 cur->path("metadata.annotations")->at("h2o.ai/spec-hash").as_string() != hash) {
-        // An H2O cloud has a fixed size and configuration: replace it.
-        c_.remove(kinds::StatefulSet, ns, s.name + "-stateful-set", "Foreground");
-        c_.create(kinds::StatefulSet, ns, sts);
-        log(ns, name, "spec changed: recreated statefulset");
-      }
+      reconcile_service(cr, ns, name, s, svc);
+      requeue = reconcile_statefulset(ns, name, s, sts, hash, phase, message);
+      ing = reconcile_ingress(cr, ns, name, s, hash);
+      if (ing.pending) requeue = true;
     } catch (const std::exception& e) {
       phase = "Failed";
       message = e.what();
       log(ns, name, std::string("reconcile failed: ") + e.what());
     }
-    update_status(cr, s, phase, message);
+    update_status(cr, s, phase, message, ing);
+    return requeue;
   }
 
   void cleanup(const Json& cr) {
     const std::string name = object_name(cr);
     const std::string ns = cr.get_string("metadata.namespace", "default");
+    const std::string api = cr.get_string("spec.ingress.apiVersion", "networking.k8s.io/v1");
+    const ResourceKind& ik = api == "networking.k8s.io/v1beta1" ? kinds::IngressV1beta1 : kinds::IngressV1;
     for (auto& [k, n] : std::vector<std::pair<const ResourceKind*, std::string>>{
-             {&kinds::StatefulSet, name + "-stateful-set"}, {&kinds::Service, name + "-service"}}) {
+             {&ik, name + "-ingress"}, {&kinds::StatefulSet, name + "-stateful-set"},
+             {&kinds::Service, name + "-service"}}) {
       try {
         c_.remove(*k, ns, n, "Background");
       } catch (const ApiError& e) {
@@ -159,7 +186,110 @@ class Reconciler {
   }
 
  private:
-  void update_status(const Json& cr, const DeploymentSpecification& s, std::string phase, const std::string& msg) {
+  struct IngressState {
+    bool enabled = false, pending = false;
+    std::string ip, path;
+  };
+
+  void reconcile_service(const Json& cr, const std::string& ns, const std::string& name,
+                         const DeploymentSpecification& s, const Json& svc) {
+    auto cur = c_.get_opt(kinds::Service, ns, s.name + "-service");
+    if (!cur) {
+      c_.create(kinds::Service, ns, svc);
+      log(ns, name, "created service " + s.name + "-service");
+    } else if (service_drifted(*cur, svc)) {
+      // merge patch replaces the lists wholesale: ports / selector back to the template
+      Json patch = Json::object();
+      patch["spec"]["ports"] = svc.at("spec").at("ports");
+      patch["spec"]["selector"] = svc.at("spec").at("selector");
+      c_.merge_patch(kinds::Service, ns, s.name + "-service", patch);
+      log(ns, name, "service drifted from the template: repaired ports / selector");
+    }
+    (void)cr;
+  }
+
+  // An H2O cloud has a fixed size and configuration, so a spec change replaces
+  // the StatefulSet: delete with Foreground propagation (pods go first), and
+  // create the new one only once the old object is really gone.  A real
+  // apiserver keeps a foreground-deleted object (deletionTimestamp set) until
+  // its pods are removed and answers 409 AlreadyExists to a create meanwhile.
+  bool reconcile_statefulset(const std::string& ns, const std::string& name, const DeploymentSpecification& s,
+                             const Json& sts, const std::string& hash, std::string& phase, std::string& message) {
+    const std::string sname = s.name + "-stateful-set";
+    auto cur = c_.get_opt(kinds::StatefulSet, ns, sname);
+    if (cur && cur->path("metadata.deletionTimestamp")) {
+      phase = "Replacing";
+      message = "waiting for the previous statefulset to terminate";
+      return true;
+    }
+    if (cur) {
+      const std::string* have = annotation(*cur, "h2o.ai/spec-hash");
+      if (have && *have == hash) return false;
+      c_.remove(kinds::StatefulSet, ns, sname, "Foreground");
+      log(ns, name, "spec changed: deleting statefulset (foreground)");
+      if (c_.get_opt(kinds::StatefulSet, ns, sname)) {
+        phase = "Replacing";
+        message = "waiting for the previous statefulset to terminate";
+        return true;
+      }
+    }
+    try {
+      c_.create(kinds::StatefulSet, ns, sts);
+    } catch (const ApiError& e) {
+      if (e.status != 409) throw;
+      phase = "Replacing";
+      message = "waiting for the previous statefulset to terminate";
+      return true;
+    }
+    log(ns, name, std::string(cur ? "recreated" : "created") + " statefulset " + sname);
+    return false;
+  }
+
+  // spec.ingress {enabled, apiVersion}: the operator owns <name>-ingress
+  // (h2ok's third verb, reference src/k8s/mod.rs:166-199) and reports the
+  // load-balancer address in status (reference any_ip / any_path).
+  IngressState reconcile_ingress(const Json& cr, const std::string& ns, const std::string& name,
+                                 DeploymentSpecification s, const std::string& hash) {
+    IngressState st;
+    const Json* spec_ing = cr.path("spec.ingress");
+    st.enabled = spec_ing && spec_ing->is_object() && spec_ing->find("enabled") &&
+                 spec_ing->at("enabled").is_bool() && spec_ing->at("enabled").as_bool();
+    s.ingress_api = cr.get_string("spec.ingress.apiVersion", "networking.k8s.io/v1");
+    const ResourceKind& ik = s.ingress_api == "networking.k8s.io/v1beta1" ? kinds::IngressV1beta1 : kinds::IngressV1;
+    const ResourceKind& other = &ik == &kinds::IngressV1 ? kinds::IngressV1beta1 : kinds::IngressV1;
+    const std::string iname = s.name + "-ingress";
+    auto drop = [&](const ResourceKind& k) {
+      try {
+        c_.remove(k, ns, iname, "Background");
+        log(ns, name, "deleted ingress " + iname + " (" + k.api + ")");
+      } catch (const ApiError& e) {
+        if (e.status != 404 && e.status != 405) throw;
+      }
+    };
+    if (!st.enabled) {
+      if (c_.get_opt(ik, ns, iname)) drop(ik);
+      return st;
+    }
+    Json ing = h2o_ingress(s);
+    adopt(ing, cr, hash);
+    auto cur = c_.get_opt(ik, ns, iname);
+    if (!cur) {
+      // apiVersion switched: the object under the other API group goes first
+      try {
+        if (c_.get_opt(other, ns, iname)) drop(other);
+      } catch (const ApiError&) {
+      }
+      cur = c_.create(ik, ns, ing);
+      log(ns, name, "created ingress " + iname);
+    }
+    if (auto ip = any_ip(*cur)) st.ip = *ip;
+    if (auto p = any_path(*cur)) st.path = *p;
+    st.pending = st.ip.empty();   // poll until the load balancer publishes an address
+    return st;
+  }
+
+  void update_status(const Json& cr, const DeploymentSpecification& s, std::string phase, const std::string& msg,
+                     const IngressState& ing) {
     const std::string ns = s.ns;
     int ready = 0, total = 0;
     std::string leader;
@@ -188,13 +318,24 @@ class Reconciler {
     st["serviceName"] = s.name + "-service";
     st["observedGeneration"] = cr.get_int("metadata.generation", 0);
     if (!msg.empty()) st["message"] = msg;
+    if (ing.enabled) {
+      st["ingressIP"] = ing.ip;
+      st["ingressPath"] = ing.path;
+      if (!ing.ip.empty()) st["connectURL"] = "http://" + ing.ip + ":80/" + s.name;
+    }
     const Json* old = cr.find("status");
     if (old && old->is_object()) {
       Json cmp = st.deep_copy();
       if (*old == cmp) return;
     }
     Json patch = Json::object();
-    patch["status"] = st;
+    Json pst = st.deep_copy();
+    // a merge patch only removes keys that are explicitly null: clear a stale
+    // message / ingress address from an earlier pass
+    if (old && old->is_object())
+      for (const char* k : {"message", "ingressIP", "ingressPath", "connectURL"})
+        if (old->has(k) && !st.has(k)) pst[k] = Json();
+    patch["status"] = pst;
     try {
       c_.merge_patch(kinds::H2O, ns, s.name, patch, "status");
     } catch (const ApiError& e) {
@@ -217,7 +358,7 @@ class Reconciler {
 };
 
 int usage() {
-  std::cerr << "usage: h2omx-operator [--kubeconfig PATH] [--namespace NS] [--once] [--resync SECONDS]\n"
+  std::cerr << "usage: h2omx-operator [--kubeconfig PATH] [--namespace NS] [--once] [--resync SECONDS] [--requeue SECONDS]\n"
                "                      [--image NAME] [--image-tag TAG]\n";
   return 1;
 }
@@ -233,6 +374,7 @@ int main(int argc, char** argv) {
     else if (a == "--namespace" || a == "-n") o.ns = next();
     else if (a == "--once") o.once = true;
     else if (a == "--resync") o.resync_s = std::max(1, std::atoi(next().c_str()));
+    else if (a == "--requeue") o.requeue_s = std::max(1, std::atoi(next().c_str()));
     else if (a == "--image") o.default_image = next();
     else if (a == "--image-tag") o.default_tag = next();
     else if (a == "-h" || a == "--help") return usage(), 0;
@@ -252,10 +394,11 @@ int main(int argc, char** argv) {
             << (o.ns.empty() ? std::string("all namespaces") : "namespace " + o.ns) << std::endl;
   while (!g_stop) {
     std::string rv;
+    bool requeue = false;
     try {
       Json lst = client->list(kinds::H2O, o.ns);
       rv = lst.get_string("metadata.resourceVersion");
-      for (auto& cr : lst.at("items").as_array()) rec.reconcile(cr);
+      for (auto& cr : lst.at("items").as_array()) requeue |= rec.reconcile(cr);
     } catch (const std::exception& e) {
       std::cerr << "[h2omx-operator] list failed: " << e.what() << std::endl;
       if (o.once) return 1;
@@ -264,9 +407,12 @@ int main(int argc, char** argv) {
     }
     if (o.once) break;
     try {
-      client->watch(kinds::H2O, o.ns, "", rv, o.resync_s, [&](const WatchEvent& ev) {
+      // a pending replacement / ingress address: re-list after a short watch
+      client->watch(kinds::H2O, o.ns, "", rv, requeue ? o.requeue_s : o.resync_s, [&](const WatchEvent& ev) {
         if (g_stop) return false;
-        if (ev.type == "ADDED" || ev.type == "MODIFIED") rec.reconcile(ev.object);
+        // a CR that needs another pass soon ends this watch: the loop re-lists
+        // and then watches with the short requeue timeout
+        if (ev.type == "ADDED" || ev.type == "MODIFIED") return !rec.reconcile(ev.object);
         else if (ev.type == "DELETED") rec.cleanup(ev.object);
         return true;
       });

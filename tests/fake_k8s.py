@@ -9,6 +9,13 @@ watch streams for services, statefulsets, pods, ingresses (v1, v1beta1) and
 the h2o.ai/v1beta `H2O` custom resource.  Optional TLS and bearer-token auth,
 fault injection, and a load balancer that assigns an ingress IP shortly after
 creation (so `h2ok ingress` exercises its watch loop).
+
+Deletion follows the real apiserver's propagation semantics: with
+``propagationPolicy: Foreground`` the object stays (``deletionTimestamp`` +
+``foregroundDeletion`` finalizer, MODIFIED event) until its dependents are
+gone, for ``foreground_delay`` seconds here; a create of the same name in
+that window answers 409 AlreadyExists.  Background / orphan deletes remove
+the object at once.
 """
 from __future__ import annotations
 
@@ -30,7 +37,7 @@ _PATH = re.compile(
 
 class FakeK8s:
     def __init__(self, token: str | None = None, tls: bool = False, tmpdir: str | None = None,
-                 ingress_ip_delay: float = 0.3):
+                 ingress_ip_delay: float = 0.3, foreground_delay: float = 0.5):
         self.objects: dict[tuple, dict] = {}
         self.rv = 100
         self.lock = threading.Condition()
@@ -39,6 +46,7 @@ class FakeK8s:
         self.fail: dict[tuple[str, str], int] = {}   # (METHOD, plural) -> status
         self.requests: list[tuple[str, str]] = []
         self.ingress_ip_delay = ingress_ip_delay
+        self.foreground_delay = foreground_delay
         self.tls = tls
         self.tmpdir = tmpdir
         self.ca_pem = None
@@ -220,13 +228,19 @@ class FakeK8s:
                     return self._send(200, {"kind": "List", "apiVersion": "v1", "items": items,
                                             "metadata": {"resourceVersion": str(fake.rv)}})
                 if method == "DELETE":
-                    o = fake.delete(plural, ns, name)
-                    if o is None:
+                    policy = (self._body() or {}).get("propagationPolicy") or ""
+                    cur = fake.get(plural, ns, name)
+                    if cur is None:
                         return self._status(404, "NotFound", f'"{name}" not found')
-                    if plural == "statefulsets":
-                        for p in fake.list("pods", ns):
-                            if p["metadata"].get("labels", {}).get("app") == o["metadata"].get("labels", {}).get("app"):
-                                fake.delete("pods", ns, p["metadata"]["name"])
+                    if cur["metadata"].get("deletionTimestamp"):
+                        return self._send(200, cur)       # already terminating
+                    if policy == "Foreground":
+                        cur["metadata"]["deletionTimestamp"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+                        cur["metadata"]["finalizers"] = ["foregroundDeletion"]
+                        obj = fake.put(plural, ns, cur, "MODIFIED")
+                        threading.Timer(fake.foreground_delay, fake._finish_delete, args=(plural, ns, name)).start()
+                        return self._send(200, obj)
+                    fake._finish_delete(plural, ns, name)
                     return self._send(200, {"kind": "Status", "status": "Success"})
                 if method in ("PUT", "PATCH"):
                     cur = fake.get(plural, ns, name)
@@ -289,6 +303,14 @@ class FakeK8s:
                 self._route("PATCH")
 
         return H
+
+    def _finish_delete(self, plural, ns, name):
+        o = self.delete(plural, ns, name)
+        if o is not None and plural == "statefulsets":
+            for p in self.list("pods", ns):
+                if p["metadata"].get("labels", {}).get("app") == o["metadata"].get("labels", {}).get("app"):
+                    self.delete("pods", ns, p["metadata"]["name"])
+        return o
 
     def _assign_ip(self, ns, name):
         o = self.get("ingresses", ns, name)

@@ -280,12 +280,99 @@ def test_operator_reconcile(k8s, tmp_path):
     subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
     st = k8s.get("h2os", "default", "h2o-op")["status"]
     assert st["phase"] == "Ready" and st["readyNodes"] == 1 and st["leaderPod"] == "h2o-op-stateful-set-0"
-    # spec change -> the fixed-size cloud is replaced
+    # spec change -> the fixed-size cloud is replaced.  The fake keeps a
+    # foreground-deleted StatefulSet terminating for a while (409 on create),
+    # like a real apiserver: the pass deletes it and reports Replacing ...
     cr = k8s.get("h2os", "default", "h2o-op")
     cr["spec"]["nodes"] = 5
     k8s.put("h2os", "default", cr, "MODIFIED")
     subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    old = k8s.get("statefulsets", "default", "h2o-op-stateful-set")
+    assert old["spec"]["replicas"] == 3 and old["metadata"]["deletionTimestamp"]
+    st = k8s.get("h2os", "default", "h2o-op")["status"]
+    assert st["phase"] == "Replacing" and "terminate" in st["message"]
+    # ... a pass while it is still terminating changes nothing (no 409 -> Failed)
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    assert k8s.get("h2os", "default", "h2o-op")["status"]["phase"] == "Replacing"
+    # ... and once it is gone the new one is created; the stale message is cleared
+    for _ in range(50):
+        if k8s.get("statefulsets", "default", "h2o-op-stateful-set") is None:
+            break
+        time.sleep(0.05)
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
     assert k8s.get("statefulsets", "default", "h2o-op-stateful-set")["spec"]["replicas"] == 5
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    st = k8s.get("h2os", "default", "h2o-op")["status"]
+    assert st["phase"] == "Ready" and "message" not in st
+
+
+def test_operator_watch_loop_replaces_statefulset(k8s, tmp_path):
+    """The long-running operator requeues a CR whose StatefulSet is still
+    terminating and converges without a spec event."""
+    k8s.foreground_delay = 1.5
+    p = subprocess.Popen([OPERATOR, "--kubeconfig", k8s.cfg, "--resync", "60", "--requeue", "1"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        k8s.put("h2os", "default", _cr("h2o-rq", nodes=2))
+        for _ in range(100):
+            if k8s.get("statefulsets", "default", "h2o-rq-stateful-set"):
+                break
+            time.sleep(0.05)
+        cr = k8s.get("h2os", "default", "h2o-rq")
+        cr["spec"]["nodes"] = 4
+        k8s.put("h2os", "default", cr, "MODIFIED")
+        for _ in range(200):
+            s = k8s.get("statefulsets", "default", "h2o-rq-stateful-set")
+            if s and s["spec"]["replicas"] == 4:
+                break
+            time.sleep(0.05)
+        assert k8s.get("statefulsets", "default", "h2o-rq-stateful-set")["spec"]["replicas"] == 4
+    finally:
+        p.terminate()
+        p.wait(timeout=10)
+
+
+def test_operator_repairs_service_drift(k8s, tmp_path):
+    k8s.put("h2os", "default", _cr("h2o-dr", nodes=1))
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    svc = k8s.get("services", "default", "h2o-dr-service")
+    want_ports, want_sel = svc["spec"]["ports"], svc["spec"]["selector"]
+    svc["spec"]["ports"] = [{"port": 8080, "targetPort": 1234, "protocol": "TCP"}]
+    svc["spec"]["selector"] = {"app": "someone-else"}
+    k8s.put("services", "default", svc, "MODIFIED")
+    r = subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], capture_output=True, text=True, timeout=60)
+    assert "drifted" in r.stdout
+    svc = k8s.get("services", "default", "h2o-dr-service")
+    assert svc["spec"]["ports"] == want_ports and svc["spec"]["selector"] == want_sel
+    # an unchanged service is left alone
+    n = len(k8s.requests)
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    assert not any(m == "PATCH" and "/services/" in path for m, path in k8s.requests[n:])
+
+
+@pytest.mark.parametrize("api", ["networking.k8s.io/v1", "networking.k8s.io/v1beta1"])
+def test_operator_ingress_from_cr(k8s, tmp_path, api):
+    """spec.ingress: the operator owns <name>-ingress (h2ok's ingress verb) and
+    publishes the load-balancer address in status; disabling removes it."""
+    plural = "ingresses"
+    k8s.put("h2os", "default", _cr("h2o-in", nodes=1, ingress={"enabled": True, "apiVersion": api}))
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    ing = k8s.get(plural, "default", "h2o-in-ingress")
+    assert ing and ing["apiVersion"] == api
+    cr = k8s.get("h2os", "default", "h2o-in")
+    assert ing["metadata"]["ownerReferences"][0]["uid"] == cr["metadata"]["uid"]
+    assert cr["status"]["ingressIP"] == ""            # load balancer not there yet
+    time.sleep(0.6)                                   # fake LB assigns 10.43.0.7
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    st = k8s.get("h2os", "default", "h2o-in")["status"]
+    assert st["ingressIP"] == "10.43.0.7" and st["connectURL"] == "http://10.43.0.7:80/h2o-in"
+    assert st["ingressPath"].startswith("/h2o-in")
+    cr = k8s.get("h2os", "default", "h2o-in")
+    cr["spec"]["ingress"]["enabled"] = False
+    k8s.put("h2os", "default", cr, "MODIFIED")
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    assert k8s.get(plural, "default", "h2o-in-ingress") is None
+    assert "ingressIP" not in k8s.get("h2os", "default", "h2o-in")["status"]
 
 
 def test_operator_watch_loop(k8s, tmp_path):
@@ -311,10 +398,14 @@ def test_operator_watch_loop(k8s, tmp_path):
 
 
 def test_crd_manifest_matches_operator():
-    from h2omx.utils.yamlio import load_all
+    from tests.yamlio import load_all
 
     docs = load_all(os.path.join(ROOT, "deploy", "crd.yaml"))
     crd = docs[0]
     assert crd["spec"]["group"] == "h2o.ai" and crd["spec"]["names"]["plural"] == "h2os"
     v = crd["spec"]["versions"][0]
     assert v["name"] == "v1beta" and "status" in v["subresources"]
+    props = v["schema"]["openAPIV3Schema"]["properties"]
+    assert set(props["spec"]["properties"]["ingress"]["properties"]) == {"enabled", "apiVersion"}
+    for k in ("ingressIP", "ingressPath", "connectURL", "message"):
+        assert k in props["status"]["properties"]
