@@ -1,8 +1,16 @@
 #include "k8s.hpp"
 
+#include <fcntl.h>
+#include <poll.h>
+#include <signal.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
+#include <chrono>
 #include <cstdlib>
+#include <cstring>
+#include <ctime>
 #include <fstream>
 #include <sstream>
 
@@ -111,11 +119,189 @@ KubeConfig load_kubeconfig(const std::string& path, const std::string& context) 
     kc.tls.client_key_pem = data_or_file(ub, "client-key", base);
     kc.username = ub.get_string("username");
     kc.password = ub.get_string("password");
-    if (ub.find("exec") || ub.find("auth-provider"))
-      if (kc.token.empty() && kc.tls.client_cert_pem.empty())
-        throw KubeConfigError("user '" + uname + "' uses an exec/auth-provider plugin, which h2ok does not run");
+    if (const Json* ex = ub.find("exec")) {
+      ExecPlugin pl;
+      pl.api_version = ex->get_string("apiVersion", pl.api_version);
+      pl.command = ex->get_string("command");
+      if (pl.command.empty()) throw KubeConfigError("user '" + uname + "': exec plugin has no command");
+      if (const Json* a = ex->find("args"))
+        if (a->is_array())
+          for (auto& v : a->as_array()) pl.args.push_back(v.is_string() ? v.as_string() : v.dump());
+      if (const Json* e = ex->find("env"))
+        if (e->is_array())
+          for (auto& v : e->as_array()) pl.env.emplace_back(v.get_string("name"), v.get_string("value"));
+      pl.install_hint = ex->get_string("installHint");
+      const Json* pci = ex->find("provideClusterInfo");
+      pl.provide_cluster_info = pci && pci->is_bool() && pci->as_bool();
+      pl.base_dir = base;
+      kc.exec = pl;
+    } else if (const Json* ap = ub.find("auth-provider")) {
+      AuthProvider a;
+      a.name = ap->get_string("name");
+      const Json* cfg = ap->find("config");
+      a.config = cfg ? cfg->deep_copy() : Json::object();
+      a.base_dir = base;
+      kc.auth_provider = a;
+    }
   }
   return kc;
+}
+
+namespace {
+
+// fork/exec argv with extra environment; stdout / stderr captured; killed
+// after timeout_s.  Returns the exit status (-1: could not run / timed out).
+int run_capture(const std::vector<std::string>& argv, const std::vector<std::pair<std::string, std::string>>& env,
+                std::string& out, std::string& err, double timeout_s) {
+  int po[2], pe[2];
+  if (pipe(po) != 0) return -1;
+  if (pipe(pe) != 0) {
+    close(po[0]);
+    close(po[1]);
+    return -1;
+  }
+  pid_t pid = fork();
+  if (pid < 0) return -1;
+  if (pid == 0) {
+    dup2(po[1], 1);
+    dup2(pe[1], 2);
+    close(po[0]);
+    close(pe[0]);
+    int devnull = open("/dev/null", O_RDONLY);
+    if (devnull >= 0) dup2(devnull, 0);
+    for (auto& [k, v] : env) setenv(k.c_str(), v.c_str(), 1);
+    std::vector<char*> av;
+    for (auto& a : argv) av.push_back(const_cast<char*>(a.c_str()));
+    av.push_back(nullptr);
+    execvp(av[0], av.data());
+    std::fprintf(stderr, "exec %s: %s\n", av[0], std::strerror(errno));
+    _exit(127);
+  }
+  close(po[1]);
+  close(pe[1]);
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds((long long)(timeout_s * 1000));
+  struct pollfd fds[2] = {{po[0], POLLIN, 0}, {pe[0], POLLIN, 0}};
+  int open_fds = 2;
+  bool timed_out = false;
+  char buf[4096];
+  while (open_fds > 0) {
+    auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now());
+    if (left.count() <= 0) {
+      timed_out = true;
+      break;
+    }
+    if (poll(fds, 2, (int)left.count()) <= 0) continue;
+    for (int i = 0; i < 2; ++i) {
+      if (fds[i].fd < 0 || !(fds[i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+      ssize_t n = read(fds[i].fd, buf, sizeof buf);
+      if (n > 0) {
+        (i == 0 ? out : err).append(buf, (size_t)n);
+      } else {
+        close(fds[i].fd);
+        fds[i].fd = -1;
+        --open_fds;
+      }
+    }
+  }
+  for (auto& f : fds)
+    if (f.fd >= 0) close(f.fd);
+  if (timed_out) kill(pid, SIGKILL);
+  int st = 0;
+  waitpid(pid, &st, 0);
+  if (timed_out) return -1;
+  return WIFEXITED(st) ? WEXITSTATUS(st) : -1;
+}
+
+long long parse_rfc3339(const std::string& t) {
+  if (t.size() < 19) return 0;
+  struct tm tm{};
+  if (!strptime(t.c_str(), "%Y-%m-%dT%H:%M:%S", &tm)) return 0;
+  return (long long)timegm(&tm);
+}
+
+std::string resolve_command(const std::string& base_dir, const std::string& cmd) {
+  // a path with a separator is relative to the kubeconfig; a bare name is a PATH lookup
+  if (cmd.find('/') != std::string::npos) return resolve(base_dir, cmd);
+  return cmd;
+}
+
+}  // namespace
+
+ExecCredential run_exec_plugin(const ExecPlugin& p, const KubeConfig& cluster) {
+  Json info = Json::object();
+  info["apiVersion"] = p.api_version;
+  info["kind"] = "ExecCredential";
+  Json spec = Json::object();
+  spec["interactive"] = false;
+  if (p.provide_cluster_info) {
+    Json c = Json::object();
+    c["server"] = cluster.server;
+    if (!cluster.tls.ca_pem.empty()) c["certificate-authority-data"] = base64_encode(cluster.tls.ca_pem);
+    if (cluster.tls.insecure) c["insecure-skip-tls-verify"] = true;
+    if (!cluster.tls.server_name.empty()) c["tls-server-name"] = cluster.tls.server_name;
+    spec["cluster"] = c;
+  }
+  info["spec"] = spec;
+  std::vector<std::string> argv{resolve_command(p.base_dir, p.command)};
+  argv.insert(argv.end(), p.args.begin(), p.args.end());
+  auto env = p.env;
+  env.emplace_back("KUBERNETES_EXEC_INFO", info.dump());
+  std::string out, err;
+  int rc = run_capture(argv, env, out, err, 60.0);
+  if (rc != 0) {
+    std::string msg = "exec plugin '" + p.command + "' failed (status " + std::to_string(rc) + ")";
+    if (!err.empty()) msg += ": " + err.substr(0, 2000);
+    if (rc == 127 && !p.install_hint.empty()) msg += "\n" + p.install_hint;
+    throw KubeConfigError(msg);
+  }
+  Json doc;
+  try {
+    doc = Json::parse(out);
+  } catch (const std::exception& e) {
+    throw KubeConfigError("exec plugin '" + p.command + "' printed no ExecCredential JSON: " + e.what());
+  }
+  if (doc.get_string("kind") != "ExecCredential")
+    throw KubeConfigError("exec plugin '" + p.command + "': expected kind ExecCredential");
+  const Json* st = doc.find("status");
+  if (!st) throw KubeConfigError("exec plugin '" + p.command + "': ExecCredential has no status");
+  ExecCredential c;
+  c.token = st->get_string("token");
+  c.client_cert_pem = st->get_string("clientCertificateData");
+  c.client_key_pem = st->get_string("clientKeyData");
+  c.expires_at = parse_rfc3339(st->get_string("expirationTimestamp"));
+  if (c.token.empty() && (c.client_cert_pem.empty() || c.client_key_pem.empty()))
+    throw KubeConfigError("exec plugin '" + p.command + "' returned neither a token nor a client certificate");
+  return c;
+}
+
+std::string auth_provider_token(const AuthProvider& a) {
+  if (a.name == "oidc") {
+    std::string t = a.config.get_string("id-token");
+    if (t.empty()) throw KubeConfigError("auth-provider oidc: no id-token in the kubeconfig (log in with kubelogin)");
+    return t;
+  }
+  if (a.name == "gcp") {
+    std::string t = a.config.get_string("access-token");
+    long long exp = parse_rfc3339(a.config.get_string("expiry"));
+    if (!t.empty() && (exp == 0 || exp > (long long)std::time(nullptr) + 10)) return t;
+    std::string cmd = a.config.get_string("cmd-path");
+    if (cmd.empty()) throw KubeConfigError("auth-provider gcp: access token expired and no cmd-path to refresh it");
+    std::vector<std::string> argv{resolve_command(a.base_dir, cmd)};
+    std::istringstream ss(a.config.get_string("cmd-args"));
+    for (std::string w; ss >> w;) argv.push_back(w);
+    std::string out, err;
+    if (run_capture(argv, {}, out, err, 60.0) != 0)
+      throw KubeConfigError("auth-provider gcp: '" + cmd + "' failed: " + err.substr(0, 2000));
+    Json doc = Json::parse(out);
+    // token-key is a JSONPath such as {.credential.access_token}
+    std::string key = a.config.get_string("token-key", "{.credential.access_token}");
+    if (!key.empty() && key.front() == '{') key = key.substr(1, key.size() - 2);
+    if (!key.empty() && key.front() == '.') key = key.substr(1);
+    t = doc.get_string(key);
+    if (t.empty()) throw KubeConfigError("auth-provider gcp: no token at " + key);
+    return t;
+  }
+  throw KubeConfigError("auth-provider '" + a.name + "' is not supported (use an exec plugin)");
 }
 
 KubeConfig in_cluster_config() {
@@ -154,6 +340,27 @@ KubeConfig infer_kubeconfig() {
 
 KubeClient::KubeClient(KubeConfig cfg) : cfg_(std::move(cfg)), url_(parse_url(cfg_.server)) {}
 
+// Credentials from an exec plugin / auth-provider: fetched on first use,
+// cached until their expiry, re-fetched once after a 401.
+void KubeClient::refresh_credentials(bool force) {
+  const long long now = (long long)std::time(nullptr);
+  if (cfg_.exec) {
+    if (!force && cred_loaded_ && (cred_expires_ == 0 || cred_expires_ > now + 10)) return;
+    ExecCredential c = run_exec_plugin(*cfg_.exec, cfg_);
+    cfg_.token = c.token;
+    if (!c.client_cert_pem.empty()) {
+      cfg_.tls.client_cert_pem = c.client_cert_pem;
+      cfg_.tls.client_key_pem = c.client_key_pem;
+    }
+    cred_expires_ = c.expires_at;
+    cred_loaded_ = true;
+  } else if (cfg_.auth_provider) {
+    if (!force && cred_loaded_) return;
+    cfg_.token = auth_provider_token(*cfg_.auth_provider);
+    cred_loaded_ = true;
+  }
+}
+
 void KubeClient::add_auth(HttpRequest& req) const {
   if (!cfg_.token.empty()) req.headers.emplace_back("Authorization", "Bearer " + cfg_.token);
   else if (!cfg_.username.empty())
@@ -169,8 +376,17 @@ HttpResponse KubeClient::call(const std::string& method, const std::string& targ
   req.timeout_s = timeout_s;
   if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH")
     req.headers.emplace_back("Content-Type", content_type);
-  add_auth(req);
-  return http_request(url_, req, cfg_.tls);
+  const bool plugin = cfg_.exec.has_value() || cfg_.auth_provider.has_value();
+  if (plugin) refresh_credentials(false);
+  HttpRequest first = req;
+  add_auth(first);
+  HttpResponse r = http_request(url_, first, cfg_.tls);
+  if (r.status == 401 && plugin) {
+    refresh_credentials(true);
+    add_auth(req);
+    r = http_request(url_, req, cfg_.tls);
+  }
+  return r;
 }
 
 Json KubeClient::checked(const HttpResponse& r) {
@@ -252,6 +468,7 @@ int KubeClient::watch(const ResourceKind& k, const std::string& ns, const std::s
   req.method = "GET";
   req.target = url_.path + collection_path(k, ns) + q;
   req.timeout_s = timeout_s > 0 ? timeout_s + 5.0 : 3600.0;
+  if (cfg_.exec || cfg_.auth_provider) refresh_credentials(false);
   add_auth(req);
   return http_stream_lines(url_, req, cfg_.tls, [&](const std::string& line) {
     Json ev;

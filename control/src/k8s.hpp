@@ -10,11 +10,32 @@
 #include <functional>
 #include <optional>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "http.hpp"
 #include "json.hpp"
 
 namespace h2ok {
+
+// users[].user.exec: a client.authentication.k8s.io credential plugin (EKS
+// `aws eks get-token`, GKE `gke-gcloud-auth-plugin`, AKS `kubelogin`, ...)
+struct ExecPlugin {
+  std::string api_version = "client.authentication.k8s.io/v1";
+  std::string command;
+  std::vector<std::string> args;
+  std::vector<std::pair<std::string, std::string>> env;
+  std::string install_hint;
+  bool provide_cluster_info = false;
+  std::string base_dir;  // kubeconfig directory: relative command paths resolve here
+};
+
+// users[].user.auth-provider (legacy): oidc id-token, gcp access-token / cmd-path
+struct AuthProvider {
+  std::string name;
+  Json config;
+  std::string base_dir;
+};
 
 struct KubeConfig {
   std::string server;          // https://host:port[/base]
@@ -24,7 +45,20 @@ struct KubeConfig {
   std::string ns = "default";  // context namespace (kubeconfig default)
   std::string source;          // kubeconfig path ("" = in-cluster)
   std::string context;
+  std::optional<ExecPlugin> exec;
+  std::optional<AuthProvider> auth_provider;
 };
+
+// ExecCredential.status returned by a plugin (PEM strings, RFC 3339 expiry)
+struct ExecCredential {
+  std::string token, client_cert_pem, client_key_pem;
+  long long expires_at = 0;  // unix seconds, 0 = does not expire
+};
+// Run an exec plugin (fork/exec, KUBERNETES_EXEC_INFO in its environment) and
+// parse its ExecCredential; throws KubeConfigError with the plugin's stderr.
+ExecCredential run_exec_plugin(const ExecPlugin& p, const KubeConfig& cluster);
+// Bearer token of a legacy auth-provider (runs gcp's cmd-path when needed).
+std::string auth_provider_token(const AuthProvider& a);
 
 class KubeConfigError : public std::runtime_error {
  public:
@@ -99,8 +133,12 @@ class KubeClient {
   Json checked(const HttpResponse& r);
   void add_auth(HttpRequest& req) const;
 
+  void refresh_credentials(bool force);
+
   KubeConfig cfg_;
   Url url_;
+  long long cred_expires_ = 0;   // exec plugin credential expiry (unix s)
+  bool cred_loaded_ = false;
 };
 
 // metadata.name of an object ("" if absent)

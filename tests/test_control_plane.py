@@ -10,6 +10,7 @@ import json
 import os
 import re
 import subprocess
+import sys
 import time
 
 import pytest
@@ -409,3 +410,125 @@ def test_crd_manifest_matches_operator():
     assert set(props["spec"]["properties"]["ingress"]["properties"]) == {"enabled", "apiVersion"}
     for k in ("ingressIP", "ingressPath", "connectURL", "message"):
         assert k in props["status"]["properties"]
+
+
+# ---- kubeconfig credential plugins (kube-rs Config::infer parity) ---------------
+_PLUGIN = r'''
+import json, os, sys
+state = sys.argv[1]
+n = int(open(state).read()) if os.path.exists(state) else 0
+open(state, "w").write(str(n + 1))
+info = json.loads(os.environ["KUBERNETES_EXEC_INFO"])
+open(state + ".info", "w").write(json.dumps(info))
+if os.environ.get("PLUGIN_FAIL"):
+    sys.stderr.write("token service unreachable\n")
+    sys.exit(3)
+tokens = os.environ["PLUGIN_TOKENS"].split(",")
+print(json.dumps({"apiVersion": info["apiVersion"], "kind": "ExecCredential",
+                  "status": {"token": tokens[min(n, len(tokens) - 1)],
+                             "expirationTimestamp": "2099-01-01T00:00:00Z"}}))
+'''
+
+
+def _exec_kubeconfig(k8s, tmp_path, tokens, fail=False):
+    plugin = tmp_path / "plugin.py"
+    plugin.write_text(_PLUGIN)
+    state = tmp_path / "calls"
+    env = [("PLUGIN_TOKENS", ",".join(tokens))] + ([("PLUGIN_FAIL", "1")] if fail else [])
+    lines = ["apiVersion: v1", "kind: Config", "clusters:", "- cluster:", f"    server: {k8s.url}", "  name: fake",
+             "contexts:", "- context:", "    cluster: fake", "    user: eks-user", "    namespace: default",
+             "  name: ctx", "current-context: ctx", "users:", "- name: eks-user", "  user:", "    exec:",
+             "      apiVersion: client.authentication.k8s.io/v1beta1", f"      command: {sys.executable}",
+             "      args:", f"      - {plugin}", f"      - {state}", "      env:"]
+    for k, v in env:
+        lines += [f"      - name: {k}", f"        value: \"{v}\""]
+    lines += ["      provideClusterInfo: true", "      installHint: install the fake plugin"]
+    cfg = tmp_path / "exec-kubeconfig"
+    cfg.write_text("\n".join(lines) + "\n")
+    return str(cfg), state
+
+
+def test_exec_plugin_credentials(k8s, tmp_path):
+    cfg, state = _exec_kubeconfig(k8s, tmp_path, ["s3cr3t"])
+    r = run(["deploy", "--cluster_size", "1", "--kubeconfig", cfg], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert len(k8s.list("statefulsets")) == 1
+    assert int(state.read_text()) == 1                # cached for the whole run (expiry 2099)
+    info = json.loads(open(str(state) + ".info").read())
+    assert info["kind"] == "ExecCredential" and info["apiVersion"] == "client.authentication.k8s.io/v1beta1"
+    assert info["spec"]["interactive"] is False and info["spec"]["cluster"]["server"] == k8s.url
+
+
+def test_exec_plugin_refreshes_after_401(k8s, tmp_path):
+    cfg, state = _exec_kubeconfig(k8s, tmp_path, ["stale-token", "s3cr3t"])
+    r = run(["deploy", "--cluster_size", "1", "--kubeconfig", cfg], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert int(state.read_text()) == 2
+
+
+def test_exec_plugin_failure_is_reported(k8s, tmp_path):
+    cfg, _ = _exec_kubeconfig(k8s, tmp_path, ["x"], fail=True)
+    r = run(["deploy", "--cluster_size", "1", "--kubeconfig", cfg], tmp_path)
+    assert r.returncode != 0
+    assert "token service unreachable" in r.stderr and "status 3" in r.stderr
+    assert k8s.list("statefulsets") == []
+
+
+def test_auth_provider_oidc_token(k8s, tmp_path):
+    lines = ["apiVersion: v1", "kind: Config", "clusters:", "- cluster:", f"    server: {k8s.url}", "  name: fake",
+             "contexts:", "- context:", "    cluster: fake", "    user: oidc", "  name: ctx", "current-context: ctx",
+             "users:", "- name: oidc", "  user:", "    auth-provider:", "      name: oidc", "      config:",
+             "        id-token: s3cr3t", "        idp-issuer-url: https://issuer"]
+    cfg = tmp_path / "oidc-kubeconfig"
+    cfg.write_text("\n".join(lines) + "\n")
+    r = run(["deploy", "--cluster_size", "1", "--kubeconfig", str(cfg)], tmp_path)
+    assert r.returncode == 0, r.stderr
+
+
+# ---- sanitizers (SURVEY.md §5.2): the control plane under ASan + UBSan -------------
+def test_control_plane_under_asan_ubsan(k8s, tmp_path):
+    """`make -C control asan` builds h2ok / h2omx-operator with
+    -fsanitize=address,undefined; the deploy -> ingress -> undeploy flow, an
+    exec-plugin login and an operator pass run clean (no sanitizer report,
+    leak checking on)."""
+    subprocess.run(["make", "-C", CONTROL, "asan", "-j8"], check=True, capture_output=True, timeout=900)
+    h2ok = os.path.join(CONTROL, "build-asan", "h2ok")
+    op = os.path.join(CONTROL, "build-asan", "h2omx-operator")
+    env = dict(os.environ, HOME=str(tmp_path), ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    env.pop("KUBECONFIG", None)
+
+    def go(args, **kw):
+        r = subprocess.run(args, cwd=tmp_path, capture_output=True, text=True, timeout=120, env=env, **kw)
+        for bad in ("AddressSanitizer", "LeakSanitizer", "runtime error:"):
+            assert bad not in r.stderr, r.stderr[-4000:]
+        return r
+
+    r = go([h2ok, "deploy", "--cluster_size", "2", "--kubeconfig", k8s.cfg])
+    assert r.returncode == 0, r.stderr
+    d = os.path.join(tmp_path, r.stdout.strip())
+    assert go([h2ok, "ingress", "-f", d]).returncode == 0
+    assert go([h2ok, "undeploy"], input=d).returncode == 0
+    assert go([h2ok, "deploy", "--cluster_size", "x"]).returncode == 1        # validator error path
+    cfg, _ = _exec_kubeconfig(k8s, tmp_path, ["s3cr3t"])
+    assert go([h2ok, "deploy", "--cluster_size", "1", "--kubeconfig", cfg]).returncode == 0
+    k8s.put("h2os", "default", _cr("h2o-asan", nodes=2, ingress={"enabled": True}))
+    assert go([op, "--kubeconfig", k8s.cfg, "--once"]).returncode == 0
+    assert k8s.get("statefulsets", "default", "h2o-asan-stateful-set")
+
+
+def test_ci_and_release_workflows():
+    """CI builds + tests the control plane (also under ASan/UBSan) and the CPU
+    suite with gfx950 kernels; tags produce packaged binaries (reference
+    .github/workflows/rust.yml, release.yml)."""
+    from tests.yamlio import load_all
+
+    ci = load_all(os.path.join(ROOT, ".github", "workflows", "ci.yml"))[0]
+    steps = " ".join(str(s.get("run", "")) for j in ci["jobs"].values() for s in j["steps"])
+    assert "make -C control asan" in steps and 'pytest tests -x -q -m "not gpu"' in steps
+    assert "-m gpu" in steps and "bench.py" in steps
+    rel = load_all(os.path.join(ROOT, ".github", "workflows", "release.yml"))[0]
+    trigger = rel.get("on", rel.get(True))          # YAML 1.1 reads the key `on` as true
+    assert trigger["push"]["tags"] == ["v*"]
+    rsteps = " ".join(str(s.get("run", "")) for j in rel["jobs"].values() for s in j["steps"])
+    assert "make -C control package" in rsteps and "gh release create" in rsteps
