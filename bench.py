@@ -189,7 +189,7 @@ def _fit_end_to_end(X, y, ntrees, tp, args, comm, torch, dev, total_rows):
 def _mlp(args, comm, torch, np):
     from h2omx.frame.synthetic import wide_gaussian
     from h2omx.models.deeplearning import H2ODeepLearningEstimator, _forward, _Net
-    from h2omx.ops import dense as D
+    from h2omx.backend import dense as D
 
     dev = comm.device
     world, rank = comm.world_size, comm.rank
@@ -299,8 +299,9 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=8192, help="dl-mlp rows per GPU per step")
     ap.add_argument("--graph", type=int, default=0,
                     help="dl-mlp bf16, 1 GPU: replay each step as a HIP graph (measured no faster: GPU-bound)")
-    ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16",
-                    help="dl-mlp GEMM operand precision (fp32 accumulation and master weights either way)")
+    ap.add_argument("--precision", choices=["bf16", "fp32"], default="fp32",
+                    help="dl-mlp GEMM operand precision: fp32 (default, H2O DeepLearning trains in fp32) or bf16 "
+                         "(h2omx extension; fp32 accumulation and master weights either way)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto",

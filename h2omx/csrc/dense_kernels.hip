@@ -105,6 +105,84 @@ __device__ __forceinline__ double glm_dev(const GlmParams& P, double y, double m
   }
 }
 
+// ---------------------------------------------------------------------------
+// GLM with more predictors than the fused Gram kernel's 254-column tile
+// (one-hot categoricals with hundreds of levels): per row chunk the linear
+// predictors come from the MFMA GEMM E = B [K][p] x Xc [p][m] (gemm_kernel),
+// glm_wz_kernel turns them into IRLS weights / working responses (same
+// per-row math as glm_irls_kernel), glm_aug_kernel writes the scaled augmented
+// design sqrt(w) [x | 1 | z] [(p+2)][m], and the Gram is the GEMM A x A^T
+// (fp32 per chunk, summed in fp64 by slab_sum_kernel).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void glm_wz_kernel(const float* __restrict__ E, int64_t m,
+                                                     const float* __restrict__ y, const float* __restrict__ wprior,
+                                                     const float* __restrict__ offset,
+                                                     const float* __restrict__ beta, GlmParams P,
+                                                     float* __restrict__ sw, float* __restrict__ z,
+                                                     double* __restrict__ dev_part) {
+  __shared__ double red[256];
+  const int p = P.p;
+  double dacc = 0.0;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < m; r += (int64_t)gridDim.x * 256) {
+    const double wpv = wprior ? wprior[r] : 1.0;
+    double wi, zv;
+    if (P.family == 5) {
+      double mx = -1e300;
+      for (int k = 0; k < P.K; ++k) mx = fmax(mx, (double)E[(int64_t)k * m + r] + beta[(int64_t)k * (p + 1) + p]);
+      double den = 0.0, ek = 0.0, etak = 0.0;
+      for (int k = 0; k < P.K; ++k) {
+        const double e = (double)E[(int64_t)k * m + r] + beta[(int64_t)k * (p + 1) + p];
+        const double x = exp(e - mx);
+        den += x;
+        if (k == P.cls) { ek = x; etak = e; }
+      }
+      const double pk = fmin(fmax(ek / den, 1e-10), 1.0 - 1e-10);
+      const double yk = ((int)y[r] == P.cls) ? 1.0 : 0.0;
+      const double w0 = pk * (1.0 - pk);
+      zv = etak + (yk - pk) / w0;
+      wi = wpv * w0;
+      dacc += wpv * (yk > 0 ? -2.0 * log(pk) : 0.0);
+    } else {
+      const double off = offset ? offset[r] : 0.0;
+      const double eta = (double)E[(int64_t)P.cls * m + r] + beta[(int64_t)P.cls * (p + 1) + p] + off;
+      double mu, dmu;
+      glm_link(P, eta, mu, dmu);
+      const double yv = y[r];
+      wi = wpv * dmu * dmu / glm_var(P, mu);
+      zv = eta - off + (yv - mu) / dmu;
+      dacc += wpv * glm_dev(P, yv, mu);
+    }
+    sw[r] = (float)sqrt(fmax(wi, 0.0));
+    z[r] = (float)zv;
+  }
+  red[threadIdx.x] = dacc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dev_part[blockIdx.x] = red[0];
+}
+
+// A [(p+2)][m] = sqrt(w) * [x (NaN -> column mean) | 1 | z]; Xc [p][m] is the
+// staged chunk (NaN kept), grid.y = augmented row
+__global__ __launch_bounds__(256) void glm_aug_kernel(const float* __restrict__ Xc, int p, int64_t m,
+                                                      const float* __restrict__ means,
+                                                      const float* __restrict__ sw, const float* __restrict__ z,
+                                                      float* __restrict__ A) {
+  const int c = blockIdx.y;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < m; r += (int64_t)gridDim.x * 256) {
+    float v;
+    if (c < p) {
+      v = Xc[(int64_t)c * m + r];
+      if (v != v) v = means[c];
+    } else {
+      v = (c == p) ? 1.0f : z[r];
+    }
+    A[(int64_t)c * m + r] = sw[r] * v;
+  }
+}
+
 constexpr int GLM_RB = 64;  // rows per LDS chunk
 
 template <int TP>
@@ -375,6 +453,61 @@ __global__ __launch_bounds__(256) void kmeans_kernel(const float* __restrict__ X
     out[k * d + j] = cnt[j];
     out[k * d + k + j] = sse[j];
   }
+}
+
+// ---------------------------------------------------------------------------
+// K-Means beyond the fused kernel's LDS tiles (d > 256 or k > 128): per row
+// chunk [row0, row0 + m) the distances come from the MFMA GEMM
+// G = C [k][d] x Xc [d][m] (gemm_kernel), then
+//   kmeans_stage_kernel   X chunk -> dense Xc [d][m] (NaN -> 0, standardized space)
+//   kmeans_argmin_kernel  best cluster per row from cn - 2 G, ||x||^2, per-block
+//                         count / SSE slab (LDS atomics, one slab per block)
+//   kmeans_onehot_kernel  OH [k][m] indicator of the assignment
+// and the cluster sums are the GEMM OH x Xc^T (per-chunk fp32 slabs, reduced in
+// fp64 by slab_sum_kernel): every FLOP on the matrix cores, no vendor library.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void kmeans_stage_kernel(const float* __restrict__ X, int64_t ldx, int d,
+                                                           int64_t row0, int64_t m, float* __restrict__ Xc) {
+  const int f = blockIdx.y;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < m; r += (int64_t)gridDim.x * 256) {
+    float v = X[(int64_t)f * ldx + row0 + r];
+    Xc[(int64_t)f * m + r] = (v != v) ? 0.0f : v;
+  }
+}
+
+__global__ __launch_bounds__(256) void kmeans_argmin_kernel(const float* __restrict__ G, int k, int64_t m,
+                                                            const float* __restrict__ cn,
+                                                            const float* __restrict__ Xc, int d,
+                                                            int* __restrict__ assign, float* __restrict__ stat) {
+  extern __shared__ float kst[];   // [k] counts | [k] sse
+  for (int c = threadIdx.x; c < 2 * k; c += 256) kst[c] = 0.0f;
+  __syncthreads();
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < m; r += (int64_t)gridDim.x * 256) {
+    float best = INFINITY;
+    int bi = 0;
+    for (int c = 0; c < k; ++c) {
+      const float dist = cn[c] - 2.0f * G[(int64_t)c * m + r];
+      if (dist < best) { best = dist; bi = c; }   // ascending c: ties keep the smaller id
+    }
+    float x2 = 0.0f;
+    for (int f = 0; f < d; ++f) {
+      const float v = Xc[(int64_t)f * m + r];
+      x2 = fmaf(v, v, x2);
+    }
+    assign[r] = bi;
+    atomicAdd(&kst[bi], 1.0f);
+    atomicAdd(&kst[k + bi], fmaxf(best + x2, 0.0f));
+  }
+  __syncthreads();
+  float* out = stat + (int64_t)blockIdx.x * 2 * k;
+  for (int c = threadIdx.x; c < 2 * k; c += 256) out[c] = kst[c];
+}
+
+__global__ __launch_bounds__(256) void kmeans_onehot_kernel(const int* __restrict__ assign, int k, int64_t m,
+                                                            float* __restrict__ OH) {
+  const int c = blockIdx.y;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < m; r += (int64_t)gridDim.x * 256)
+    OH[(int64_t)c * m + r] = (assign[r] == c) ? 1.0f : 0.0f;
 }
 
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int n_slabs, int width,
@@ -1021,6 +1154,48 @@ H2OMX_API int h2omx_slab_reduce_upper(const float* slab, int n_slabs, int width,
 
 H2OMX_API int h2omx_slab_sum(const float* slab, int n_slabs, int width, double* out, hipStream_t stream) {
   hipLaunchKernelGGL(slab_sum_kernel, dim3(cdiv(width, 256)), dim3(256), 0, stream, slab, n_slabs, width, out);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_glm_wz(const float* E, int64_t m, const float* y, const float* wprior, const float* offset,
+                           const float* beta, const void* params, float* sw, float* z, double* dev_part, int n_blk,
+                           hipStream_t stream) {
+  if (m < 1 || n_blk < 1) return kBadArg;
+  const GlmParams P = *reinterpret_cast<const GlmParams*>(params);
+  hipLaunchKernelGGL(glm_wz_kernel, dim3(n_blk), dim3(256), 0, stream, E, m, y, wprior, offset, beta, P, sw, z,
+                     dev_part);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_glm_aug(const float* Xc, int p, int64_t m, const float* means, const float* sw, const float* z,
+                            float* A, hipStream_t stream) {
+  if (p < 1 || m < 1) return kBadArg;
+  hipLaunchKernelGGL(glm_aug_kernel, dim3((unsigned)std::min<int64_t>(cdiv(m, 256), 1024), p + 2), dim3(256), 0,
+                     stream, Xc, p, m, means, sw, z, A);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_kmeans_stage(const float* X, int64_t ldx, int d, int64_t row0, int64_t m, float* Xc,
+                                 hipStream_t stream) {
+  if (d < 1 || m < 1) return kBadArg;
+  hipLaunchKernelGGL(kmeans_stage_kernel, dim3((unsigned)std::min<int64_t>(cdiv(m, 256), 1024), d), dim3(256), 0,
+                     stream, X, ldx, d, row0, m, Xc);
+  return launch_status();
+}
+
+// stat: [n_blk][2k] floats (counts | sse per block); k <= 8192 (LDS)
+H2OMX_API int h2omx_kmeans_argmin(const float* G, int k, int64_t m, const float* cn, const float* Xc, int d,
+                                  int* assign, float* stat, int n_blk, hipStream_t stream) {
+  if (k < 1 || k > 8192 || m < 1 || n_blk < 1) return kBadArg;
+  hipLaunchKernelGGL(kmeans_argmin_kernel, dim3(n_blk), dim3(256), (size_t)2 * k * sizeof(float), stream, G, k, m,
+                     cn, Xc, d, assign, stat);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_kmeans_onehot(const int* assign, int k, int64_t m, float* OH, hipStream_t stream) {
+  if (k < 1 || k > 65535 || m < 1) return kBadArg;
+  hipLaunchKernelGGL(kmeans_onehot_kernel, dim3((unsigned)std::min<int64_t>(cdiv(m, 256), 1024), k), dim3(256), 0,
+                     stream, assign, k, m, OH);
   return launch_status();
 }
 

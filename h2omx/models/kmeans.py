@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from ..frame.frame import ENUM, Frame
-from ..ops import dense as D
+from ..backend import dense as D
 from .base import Model, ModelBuilder, ModelCategory
 from .glm import DesignInfo
 

@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from ..frame.frame import DKV, ENUM, Frame, Vec
-from ..ops import dense as D
+from ..backend import dense as D
 from .base import Model, ModelBuilder, ModelCategory
 from .glm import DesignInfo, H2OGeneralizedLinearEstimator
 

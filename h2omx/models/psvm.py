@@ -33,7 +33,7 @@ import numpy as np
 import torch
 
 from ..frame.frame import Frame, Vec
-from ..ops import dense as D
+from ..backend import dense as D
 from .base import Model, ModelBuilder, ModelCategory
 
 

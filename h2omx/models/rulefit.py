@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from ..frame.frame import ENUM, Frame
-from ..ops import dense as D
+from ..backend import dense as D
 from .base import Model, ModelBuilder, ModelCategory
 
 

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from ..frame.frame import DKV, Frame, Vec
-from ..ops import dense as D
+from ..backend import dense as D
 from .base import Model, ModelBuilder, ModelCategory
 from .pca import TRANSFORMS
 from .glm import DesignInfo

@@ -18,7 +18,6 @@ import torch
 from ... import ops
 from .binning import BinnedMatrix
 from .engine import HipTreeBuilder, TreeParams, make_grad_params, tree_capacity, trees_from_bytes
-from .reference import RefTreeBuilder, bag_weights, dist_grad
 from .structs import TREE_NODE_DTYPE
 
 
@@ -97,29 +96,10 @@ class TreeEnsemble:
             if self.average and nt > 0:
                 out /= nt
             return out
-        Xn = X.float().numpy()
-        out = np.zeros((self.K, n), np.float64) if self.average else np.repeat(self.init_f[:, None], n, 1).astype(np.float64)
-        for t in range(T):
-            out[t % self.K] += predict_tree_numpy(self.trees[t], Xn)
-        if self.average and nt > 0:
-            out /= nt
-        return torch.from_numpy(out.astype(np.float32))
+        from ...reference.tree import raw_margin_cpu
 
+        return raw_margin_cpu(self, X, nt)
 
-def predict_tree_numpy(tree: np.ndarray, Xn: np.ndarray) -> np.ndarray:
-    n = Xn.shape[1]
-    idx = np.zeros(n, np.int64)
-    for _ in range(64):
-        feat = tree["feat"][idx]
-        inner = feat >= 0
-        if not inner.any():
-            break
-        r = np.nonzero(inner)[0]
-        v = Xn[feat[r], r]
-        nd = tree[idx[r]]
-        left = np.where(np.isnan(v), nd["na_left"] != 0, v <= nd["thr"])
-        idx[r] = np.where(left, nd["left"], nd["left"] + 1)
-    return tree["value"][idx].astype(np.float64)
 
 
 def init_margin(dist: str, y: np.ndarray, w: np.ndarray | None, K: int) -> np.ndarray:
@@ -169,7 +149,10 @@ def train_ensemble(bm: BinnedMatrix, y, w=None, *, dist: str = "bernoulli", ntre
     if bm.codes.is_cuda:
         _train_gpu(bm, y_np, w_np, ens, ntrees, tparams, sample_rate, seed, comm, callback, dist_kw)
     else:
-        _train_cpu(bm, y_np, w_np, ens, ntrees, tparams, sample_rate, seed, comm, callback, dist_kw)
+        # host-resident bins: the fp64 reference builder (test oracle, CPU-only clouds)
+        from ...reference.tree import train_cpu
+
+        train_cpu(bm, y_np, w_np, ens, ntrees, tparams, sample_rate, seed, comm, callback, dist_kw)
     return ens
 
 
@@ -343,23 +326,11 @@ class _GpuView:
         return trees_from_bytes(raw.cpu().numpy(), width // TREE_NODE_DTYPE.itemsize)
 
 
-class _CpuView:
-    def __init__(self, Fm, trees, K, init_f):
-        self.Fm, self._trees, self.K, self.init_f = Fm, trees, K, init_f
-
-    @property
-    def margin(self) -> torch.Tensor:
-        return torch.from_numpy(self.Fm)
-
-    def trees(self, lo: int, hi: int) -> np.ndarray:
-        sel = self._trees[lo * self.K: hi * self.K]
-        return np.stack(sel) if sel else np.zeros((0, 1), TREE_NODE_DTYPE)
-
 
 def _tree_fmask(tp: TreeParams, F: int, t: int, dev):
     if tp.col_sample_rate_per_tree >= 1.0:
         return None
-    from .reference import hash4, u01
+    from .hashing import hash4, u01
 
     hs = hash4(tp.seed & 0xFFFFFFFF, 0xC0FFEE, t, np.arange(F))
     m = (u01(hs) < tp.col_sample_rate_per_tree).astype(np.uint8)
@@ -368,45 +339,3 @@ def _tree_fmask(tp: TreeParams, F: int, t: int, dev):
     return torch.from_numpy(m).to(dev) if dev is not None else m
 
 
-def _train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw):
-    K, dist, n = ens.K, ens.dist, bm.n
-    builder = RefTreeBuilder(bm, tp, comm)
-    from .engine import global_row_base
-
-    row_base = global_row_base(n, comm)
-    bmg = getattr(ens, "_base_margin", None)
-    Fm = (bmg.cpu().numpy().astype(np.float32).copy() if bmg is not None
-          else np.repeat(ens.init_f[:, None], n, 1).astype(np.float32))
-    wobs = np.ones(n, np.float32) if w_np is None else w_np.astype(np.float32)
-    trees = []
-    t0 = time.perf_counter()
-    for t in range(ntrees):
-        wb = wobs * bag_weights(n, sample_rate, seed, t, row_base)
-        if K == 1:
-            gr, hs = dist_grad(dist, Fm[0], y_np, **dist_kw)
-            grads = [(gr, hs)]
-        elif dist == "drf":
-            grads = [(-(y_np == k).astype(np.float64), np.ones(n)) for k in range(K)]
-        else:
-            z = Fm - Fm.max(axis=0, keepdims=True)
-            pr = np.exp(z)
-            pr /= pr.sum(axis=0, keepdims=True)
-            grads = [(pr[k] - (y_np == k), np.maximum(pr[k] * (1 - pr[k]), 1e-16)) for k in range(K)]
-        fmask = _tree_fmask(tp, bm.F, t, None)
-        for k in range(K):
-            gr, hs = grads[k]
-            pad = bm.npad - n
-            builder.nid[:] = -1
-            builder.nid[:n] = 0
-            g32 = np.concatenate([(gr * wb).astype(np.float32), np.zeros(pad, np.float32)])
-            h32 = np.concatenate([(hs * wb).astype(np.float32), np.zeros(pad, np.float32)])
-            w32 = np.concatenate([wb, np.zeros(pad, np.float32)])
-            tree = builder.build(g32, h32, w32, t * K + k, fmask)
-            leaf = ~builder.nid[:n]
-            Fm[k] += tree["value"][leaf]
-            trees.append(tree)
-        if callback is not None and callback(t, _CpuView(Fm, trees, K, ens.init_f)) is True:
-            break
-    ens.timings["train_s"] = time.perf_counter() - t0
-    ens.trees = np.stack(trees) if trees else ens.trees
-    ens._cpu_margin = Fm

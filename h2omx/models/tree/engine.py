@@ -11,7 +11,7 @@ The decision of which nodes split, how children are numbered and which child
 is histogrammed (the smaller one; its sibling comes from parent - child) is
 taken on the device, so the host never waits for the GPU inside a tree.
 
-``RefTreeBuilder`` (``reference.py``) implements the same algorithm with
+``RefTreeBuilder`` (``h2omx/reference/tree.py``) implements the same algorithm with
 NumPy on the CPU; it is the test oracle and the CPU plumbing path.
 """
 from __future__ import annotations

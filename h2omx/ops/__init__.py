@@ -57,6 +57,11 @@ DENSE_SIGS = {
     "h2omx_slab_reduce_upper": "PIIPS",
     "h2omx_slab_sum": "PIIPS",
     "h2omx_kmeans": "PLLIPPIIPPS",
+    "h2omx_glm_wz": "PLPPPPPPPPIS",
+    "h2omx_glm_aug": "PILPPPPS",
+    "h2omx_kmeans_stage": "PLILLPS",
+    "h2omx_kmeans_argmin": "PILPPIPPIS",
+    "h2omx_kmeans_onehot": "PILPS",
     "h2omx_gemm": "PPPPIIIIIIFIPS",
     "h2omx_act_backward": "PPLIS",
     "h2omx_bias_grad": "PPIIPIS",

@@ -1,15 +1,17 @@
 """Python entry points of csrc/dense_kernels.hip (GLM IRLS Gram, K-Means,
-MLP GEMM + elementwise) with their CPU reference implementations.
+MLP GEMM + elementwise).
 
-Every function takes tensors on one device.  On a GPU tensor the HIP kernel
-is the only implementation (``ops.dense_lib()`` raises if the library is
-missing); on CPU tensors the NumPy/PyTorch reference runs (test oracle and
-the CPU plumbing path).
+Device tensors only: every function launches its HIP kernel on the current
+stream (``ops.dense_lib()`` raises if the library is missing) and rejects
+host tensors.  The CPU reference implementations (test oracle, CPU-only
+deployments) live in :mod:`h2omx.reference.dense`; :mod:`h2omx.backend`
+routes a call to one or the other by the device of its data.
 """
 from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -17,6 +19,9 @@ import torch
 from . import P, check, dense_lib, stream
 
 KBADARG = 1  # common.h kBadArg
+# workgroups of the fused GLM Gram / K-Means kernels (sweeps: H2OMX_GLM_WGS, H2OMX_KM_WGS)
+GLM_WGS = int(os.environ.get("H2OMX_GLM_WGS", "512"))
+KM_WGS = int(os.environ.get("H2OMX_KM_WGS", "1024"))
 
 FAMILIES = {"gaussian": 0, "binomial": 1, "poisson": 2, "gamma": 3, "tweedie": 4, "multinomial": 5,
             "quasibinomial": 6, "fractionalbinomial": 6, "negativebinomial": 7}
@@ -32,11 +37,64 @@ class GlmParams(ctypes.Structure):
                 ("link_power", ctypes.c_double)]
 
 
+def _dev(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"ops.dense.{what}: device tensors only (CPU runs go through h2omx.backend -> "
+                         "h2omx.reference.dense)")
+
+
 def _tp_for(p: int) -> int:
     for tp in (1, 2, 4, 8):
         if p + 2 <= 32 * tp:
             return tp
-    raise ValueError(f"GLM with {p} predictors exceeds the 254-column Gram kernel; reduce predictors")
+    raise ValueError(f"GLM with {p} predictors exceeds the 254-column fused Gram kernel")
+
+
+def _glm_irls_wide(X, y, wprior, offset, beta, family, link, cls, var_power, link_power):
+    """IRLS pass for p > 254 (e.g. one-hot categoricals with hundreds of levels):
+    chunked eta GEMM -> glm_wz_kernel -> glm_aug_kernel -> Gram GEMM A A^T on the
+    fp32 MFMA gemm_kernel, fp32 per chunk, fp64 across chunks (slab_sum)."""
+    lib = dense_lib()
+    p, n = X.shape
+    K = beta.shape[0]
+    dev = X.device
+    st = stream(dev)
+    PA = p + 2
+    m_chunk = int(max(4096, min(n, (1 << 27) // PA)))
+    nchunks = -(-n // m_chunk)
+    B = torch.from_numpy(np.ascontiguousarray(beta[:, :p], np.float32)).to(dev)
+    b_full = torch.from_numpy(np.ascontiguousarray(beta, np.float32)).to(dev)
+    means = torch.zeros((p,), dtype=torch.float32, device=dev)
+    gp = GlmParams(FAMILIES[family], LINKS[link], p, K, cls, 0, var_power, link_power)
+    Xc = torch.empty((p * m_chunk,), dtype=torch.float32, device=dev)
+    E = torch.empty((K * m_chunk,), dtype=torch.float32, device=dev)
+    sw = torch.empty((m_chunk,), dtype=torch.float32, device=dev)
+    z = torch.empty((m_chunk,), dtype=torch.float32, device=dev)
+    A = torch.empty((PA * m_chunk,), dtype=torch.float32, device=dev)
+    grams = torch.empty((nchunks, PA * PA), dtype=torch.float32, device=dev)
+    n_blk = 256
+    devs = torch.empty((nchunks * n_blk,), dtype=torch.float64, device=dev)
+    Xs = X.contiguous()
+    for ci in range(nchunks):
+        s0 = ci * m_chunk
+        m = min(m_chunk, n - s0)
+        xc = Xc[: p * m].view(p, m)
+        check(lib.h2omx_kmeans_stage(P(Xs), Xs.stride(0), p, s0, m, P(xc), st), "stage")
+        e = E[: K * m].view(K, m)
+        gemm(B, xc, out=e)
+        yy = y[s0: s0 + m]
+        wp = None if wprior is None else wprior[s0: s0 + m]
+        of = None if offset is None else offset[s0: s0 + m]
+        check(lib.h2omx_glm_wz(P(e), m, P(yy), P(wp), P(of), P(b_full), ctypes.addressof(gp), P(sw), P(z),
+                               P(devs[ci * n_blk:]), n_blk, st), "glm_wz")
+        a = A[: PA * m].view(PA, m)
+        check(lib.h2omx_glm_aug(P(xc), p, m, P(means), P(sw), P(z), P(a), st), "glm_aug")
+        gemm(a, a, tb=True, out=grams[ci].view(PA, PA))
+    out = torch.empty((PA * PA,), dtype=torch.float64, device=dev)
+    check(lib.h2omx_slab_sum(P(grams), nchunks, PA * PA, P(out), st), "slab_sum")
+    G = out.view(PA, PA).cpu().numpy()
+    G = 0.5 * (G + G.T)
+    return G, float(devs.sum().item())
 
 
 def glm_irls_pass(X: torch.Tensor, y: torch.Tensor, wprior, offset, beta: np.ndarray, family: str, link: str,
@@ -44,122 +102,30 @@ def glm_irls_pass(X: torch.Tensor, y: torch.Tensor, wprior, offset, beta: np.nda
     """One IRLS pass.  X: feature-major standardized float32 [p][n] (no NA).
     beta: float64 [K][p+1] (coefficients then intercept).
     Returns (G float64 [p+2][p+2] of the augmented [x | 1 | z] weighted Gram, deviance)."""
+    _dev(X, "glm_irls_pass")
     p, n = X.shape
     K = beta.shape[0]
-    if X.is_cuda:
-        lib = dense_lib()
-        dev = X.device
-        tp = _tp_for(p)
-        PP = 32 * tp
-        n_wg = max(1, min(512, math.ceil(n / 4096)))
-        slab = torch.empty((n_wg * PP * PP,), dtype=torch.float32, device=dev)
-        devs = torch.empty((n_wg,), dtype=torch.float64, device=dev)
-        out = torch.empty((PP * PP,), dtype=torch.float64, device=dev)
-        b32 = torch.from_numpy(np.ascontiguousarray(beta, np.float32)).to(dev)
-        means = torch.zeros((max(p, 1),), dtype=torch.float32, device=dev)
-        gp = GlmParams(FAMILIES[family], LINKS[link], p, K, cls, 0, var_power, link_power)
-        Xc = X.contiguous()
-        st = stream(dev)
-        check(lib.h2omx_glm_irls(P(Xc), Xc.stride(0), n, P(y), P(wprior), P(offset), P(means), P(b32),
-                                 ctypes.addressof(gp), n_wg, tp, P(slab), P(devs), st), "glm_irls")
-        check(lib.h2omx_slab_reduce_upper(P(slab), n_wg, PP * PP, P(out), st), "slab_reduce_upper")
-        G = out.view(PP, PP)[: p + 2, : p + 2].cpu().numpy()
-        G = np.triu(G) + np.triu(G, 1).T
-        return G, float(devs.sum().item())
-    return _irls_pass_ref(X, y, wprior, offset, beta, family, link, cls, var_power, link_power)
-
-
-def _linkinv(eta, link, link_power=0.0):
-    if link == "logit":
-        return 1 / (1 + np.exp(-eta)), None
-    if link == "log":
-        mu = np.exp(np.minimum(eta, 700))
-        return mu, mu
-    if link == "inverse":
-        e = np.where(np.abs(eta) < 1e-10, np.copysign(1e-10, eta), eta)
-        mu = 1 / e
-        return mu, -mu * mu
-    if link == "tweedie":
-        if link_power == 0:
-            mu = np.exp(np.minimum(eta, 700))
-            return mu, mu
-        e = np.maximum(eta, 1e-10)
-        mu = e ** (1 / link_power)
-        return mu, mu / (link_power * e)
-    return eta, np.ones_like(eta)
-
-
-def glm_variance(family, mu, var_power=1.5):
-    if family in ("binomial", "quasibinomial", "fractionalbinomial"):
-        return np.maximum(mu * (1 - mu), 1e-10)
-    if family == "negativebinomial":                       # var_power carries theta
-        return np.maximum(mu + var_power * mu * mu, 1e-10)
-    if family == "poisson":
-        return np.maximum(mu, 1e-10)
-    if family == "gamma":
-        return np.maximum(mu * mu, 1e-20)
-    if family == "tweedie":
-        return np.maximum(np.maximum(mu, 1e-10) ** var_power, 1e-20)
-    return np.ones_like(mu)
-
-
-def glm_deviance(family, y, mu, var_power=1.5):
-    if family == "negativebinomial":
-        th, m = var_power, np.maximum(mu, 1e-15)
-        with np.errstate(divide="ignore", invalid="ignore"):
-            a = np.where(y > 0, y * np.log(np.where(y > 0, y, 1) / m), 0.0)
-        return 2 * (a - (y + 1 / th) * np.log((1 + th * y) / (1 + th * m)))
-    if family in ("binomial", "quasibinomial", "fractionalbinomial"):
-        m = np.clip(mu, 1e-15, 1 - 1e-15)
-        return -2 * (y * np.log(m) + (1 - y) * np.log(1 - m))
-    if family == "poisson":
-        m = np.maximum(mu, 1e-15)
-        with np.errstate(divide="ignore", invalid="ignore"):
-            t = np.where(y > 0, y * np.log(np.where(y > 0, y, 1) / m), 0.0)
-        return 2 * (t - (y - m))
-    if family == "gamma":
-        m = np.maximum(mu, 1e-15)
-        return 2 * (-np.log(np.maximum(y, 1e-15) / m) + (y - m) / m)
-    if family == "tweedie":
-        r = var_power
-        m = np.maximum(mu, 1e-15)
-        a = np.where(y > 0, np.maximum(y, 0) ** (2 - r) / ((1 - r) * (2 - r)), 0.0)
-        return 2 * (a - y * m ** (1 - r) / (1 - r) + m ** (2 - r) / (2 - r))
-    return (y - mu) ** 2
-
-
-def _irls_pass_ref(X, y, wprior, offset, beta, family, link, cls, var_power, link_power):
-    Xn = X.double().numpy()
-    p, n = Xn.shape
-    yv = y.double().numpy()
-    wp = np.ones(n) if wprior is None else wprior.double().numpy()
-    off = np.zeros(n) if offset is None else offset.double().numpy()
-    if family == "multinomial":
-        etas = beta[:, :p] @ Xn + beta[:, p:p + 1]
-        etas -= etas.max(axis=0, keepdims=True)
-        pr = np.exp(etas)
-        pr /= pr.sum(axis=0, keepdims=True)
-        pk = np.clip(pr[cls], 1e-10, 1 - 1e-10)
-        yk = (yv.astype(np.int64) == cls).astype(np.float64)
-        eta_k = beta[cls, :p] @ Xn + beta[cls, p]
-        w = pk * (1 - pk)
-        z = eta_k + (yk - pk) / w
-        w = w * wp
-        dev = float((wp * np.where(yk > 0, -2 * np.log(pk), 0.0)).sum())
-    else:
-        eta = beta[0, :p] @ Xn + beta[0, p] + off
-        mu, dmu = _linkinv(eta, link, link_power)
-        if link == "logit":
-            dmu = np.maximum(mu * (1 - mu), 1e-10)
-        elif link == "log" or (link == "tweedie" and link_power == 0):
-            dmu = np.maximum(mu, 1e-10)
-        w = wp * dmu * dmu / glm_variance(family, mu, var_power)
-        z = eta - off + (yv - mu) / dmu
-        dev = float((wp * glm_deviance(family, yv, mu, var_power)).sum())
-    A = np.vstack([Xn, np.ones((1, n)), z[None, :]])
-    sw = np.sqrt(np.maximum(w, 0))
-    As = A * sw[None, :]
-    return As @ As.T, dev
+    if p + 2 > 256:
+        return _glm_irls_wide(X, y, wprior, offset, beta, family, link, cls, var_power, link_power)
+    lib = dense_lib()
+    dev = X.device
+    tp = _tp_for(p)
+    PP = 32 * tp
+    n_wg = max(1, min(GLM_WGS, math.ceil(n / 4096)))
+    slab = torch.empty((n_wg * PP * PP,), dtype=torch.float32, device=dev)
+    devs = torch.empty((n_wg,), dtype=torch.float64, device=dev)
+    out = torch.empty((PP * PP,), dtype=torch.float64, device=dev)
+    b32 = torch.from_numpy(np.ascontiguousarray(beta, np.float32)).to(dev)
+    means = torch.zeros((max(p, 1),), dtype=torch.float32, device=dev)
+    gp = GlmParams(FAMILIES[family], LINKS[link], p, K, cls, 0, var_power, link_power)
+    Xc = X.contiguous()
+    st = stream(dev)
+    check(lib.h2omx_glm_irls(P(Xc), Xc.stride(0), n, P(y), P(wprior), P(offset), P(means), P(b32),
+                             ctypes.addressof(gp), n_wg, tp, P(slab), P(devs), st), "glm_irls")
+    check(lib.h2omx_slab_reduce_upper(P(slab), n_wg, PP * PP, P(out), st), "slab_reduce_upper")
+    G = out.view(PP, PP)[: p + 2, : p + 2].cpu().numpy()
+    G = np.triu(G) + np.triu(G, 1).T
+    return G, float(devs.sum().item())
 
 
 # ---------------------------------------------------------------------------
@@ -168,60 +134,68 @@ def _irls_pass_ref(X, y, wprior, offset, beta, family, link, cls, var_power, lin
 def kmeans_step(X: torch.Tensor, C: torch.Tensor):
     """One Lloyd pass.  X feature-major float32 [d][n] (standardized, NA -> 0),
     C [k][d].  Returns (assign int32 [n], sums float64 [k][d], counts [k], sse [k])."""
+    _dev(X, "kmeans_step")
     d, n = X.shape
     k = C.shape[0]
-    if X.is_cuda:
-        lib = dense_lib()
-        dev = X.device
-        Xc = X.contiguous()
-        Cc = C.float().contiguous()
-        cn = (Cc.double() ** 2).sum(1).float()
-        n_wg = max(1, min(1024, math.ceil(n / 4096)))
-        width = k * d + 2 * k
-        slab = torch.empty((n_wg * width,), dtype=torch.float32, device=dev)
-        out = torch.empty((width,), dtype=torch.float64, device=dev)
-        assign = torch.empty((n,), dtype=torch.int32, device=dev)
-        st = stream(dev)
-        rc = lib.h2omx_kmeans(P(Xc), Xc.stride(0), n, d, P(Cc), P(cn), k, n_wg, P(assign), P(slab), st)
-        if rc == KBADARG:
-            return _kmeans_large(Xc, Cc)
-        check(rc, "kmeans")
-        check(lib.h2omx_slab_sum(P(slab), n_wg, width, P(out), st), "slab_sum")
-        o = out.cpu().numpy()
-        return assign, o[: k * d].reshape(k, d), o[k * d: k * d + k], o[k * d + k:]
-    Xn = X.double().numpy()
-    Cn = C.double().numpy()
-    d2 = (Cn ** 2).sum(1)[:, None] - 2 * Cn @ Xn
-    a = np.argmin(d2, axis=0)
-    x2 = (Xn ** 2).sum(0)
-    sums = np.zeros((k, d))
-    np.add.at(sums, a, Xn.T)
-    counts = np.bincount(a, minlength=k).astype(np.float64)
-    sse = np.bincount(a, weights=np.maximum(d2[a, np.arange(n)] + x2, 0), minlength=k)
-    return torch.from_numpy(a.astype(np.int32)), sums, counts, sse
+    lib = dense_lib()
+    dev = X.device
+    Xc = X.contiguous()
+    Cc = C.float().contiguous()
+    cn = (Cc.double() ** 2).sum(1).float()
+    n_wg = max(1, min(KM_WGS, math.ceil(n / 4096)))
+    width = k * d + 2 * k
+    slab = torch.empty((n_wg * width,), dtype=torch.float32, device=dev)
+    out = torch.empty((width,), dtype=torch.float64, device=dev)
+    assign = torch.empty((n,), dtype=torch.int32, device=dev)
+    st = stream(dev)
+    rc = lib.h2omx_kmeans(P(Xc), Xc.stride(0), n, d, P(Cc), P(cn), k, n_wg, P(assign), P(slab), st)
+    if rc == KBADARG:
+        return _kmeans_large(Xc, Cc)
+    check(rc, "kmeans")
+    check(lib.h2omx_slab_sum(P(slab), n_wg, width, P(out), st), "slab_sum")
+    o = out.cpu().numpy()
+    return assign, o[: k * d].reshape(k, d), o[k * d: k * d + k], o[k * d + k:]
 
 
 def _kmeans_large(X: torch.Tensor, C: torch.Tensor):
-    """Shapes beyond the fused kernel's LDS tiles (d > 256 or large k): the
-    distance GEMM goes to hipBLASLt through torch, in row chunks."""
+    """Shapes beyond the fused kernel's LDS tiles (d > 256 or k > 128), all on
+    our HIP kernels: per row chunk the distance GEMM C x Xc and the sums GEMM
+    OH x Xc^T on the fp32 MFMA gemm_kernel, argmin / one-hot / staging kernels
+    in between (csrc/dense_kernels.hip, "K-Means beyond the fused kernel")."""
+    lib = dense_lib()
     d, n = X.shape
     k = C.shape[0]
-    cn = (C.double() ** 2).sum(1)
-    assign = torch.empty((n,), dtype=torch.int32, device=X.device)
-    sums = torch.zeros((k, d), dtype=torch.float64, device=X.device)
-    counts = torch.zeros((k,), dtype=torch.float64, device=X.device)
-    sse = torch.zeros((k,), dtype=torch.float64, device=X.device)
-    step = max(1, (1 << 26) // max(k, 1))
-    for s in range(0, n, step):
-        xb = X[:, s:s + step]
-        d2 = cn[:, None] - 2 * (C @ xb).double()
-        m, a = d2.min(0)
-        assign[s:s + step] = a.to(torch.int32)
-        x2 = (xb.double() ** 2).sum(0)
-        counts += torch.bincount(a, minlength=k).double()
-        sse += torch.bincount(a, weights=(m + x2).clamp_min(0), minlength=k)
-        sums.index_add_(0, a, xb.T.double())
-    return assign, sums.cpu().numpy(), counts.cpu().numpy(), sse.cpu().numpy()
+    dev = X.device
+    st = stream(dev)
+    Cc = C.float().contiguous()
+    cn = (Cc.double() ** 2).sum(1).float().contiguous()
+    # chunk so G / OH ([k][m]) and Xc ([d][m]) stay within ~1.5 GB of the 288 GB HBM
+    m_chunk = int(max(4096, min(n, (1 << 27) // max(k, d))))
+    nchunks = -(-n // m_chunk)
+    assign = torch.empty((n,), dtype=torch.int32, device=dev)
+    n_blk = 256
+    stat = torch.empty((nchunks * n_blk * 2 * k,), dtype=torch.float32, device=dev)
+    sums = torch.empty((nchunks, k * d), dtype=torch.float32, device=dev)
+    Xc = torch.empty((d * m_chunk,), dtype=torch.float32, device=dev)
+    G = torch.empty((k * m_chunk,), dtype=torch.float32, device=dev)
+    for ci in range(nchunks):
+        s0 = ci * m_chunk
+        m = min(m_chunk, n - s0)
+        xc = Xc[: d * m].view(d, m)
+        g = G[: k * m].view(k, m)
+        check(lib.h2omx_kmeans_stage(P(X), X.stride(0), d, s0, m, P(xc), st), "kmeans_stage")
+        gemm(Cc, xc, out=g)
+        a = assign[s0: s0 + m]
+        check(lib.h2omx_kmeans_argmin(P(g), k, m, P(cn), P(xc), d, P(a), P(stat[ci * n_blk * 2 * k:]), n_blk, st),
+              "kmeans_argmin")
+        check(lib.h2omx_kmeans_onehot(P(a), k, m, P(g), st), "kmeans_onehot")    # G reused as OH
+        gemm(g, xc, tb=True, out=sums[ci].view(k, d))
+    o_stat = torch.empty((2 * k,), dtype=torch.float64, device=dev)
+    check(lib.h2omx_slab_sum(P(stat), nchunks * n_blk, 2 * k, P(o_stat), st), "slab_sum")
+    o_sums = torch.empty((k * d,), dtype=torch.float64, device=dev)
+    check(lib.h2omx_slab_sum(P(sums), nchunks, k * d, P(o_sums), st), "slab_sum")
+    o_stat = o_stat.cpu().numpy()
+    return assign, o_sums.cpu().numpy().reshape(k, d), o_stat[:k], o_stat[k:]
 
 
 # ---------------------------------------------------------------------------
@@ -249,112 +223,73 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
     M = A.shape[1] if ta else A.shape[0]
     K = A.shape[0] if ta else A.shape[1]
     N = B.shape[0] if tb else B.shape[1]
-    if A.is_cuda:
-        # the kernel indexes dense row-major operands: copy strided views (no-op otherwise)
-        A = A.float().contiguous()
-        B = B.float().contiguous()
-        if bias is not None:
-            bias = bias.float().contiguous()
-        C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=A.device)
-        if not C.is_contiguous():
-            raise ValueError("gemm: out must be contiguous")
-        # split-K when the output has too few 128x128 tiles to fill 256 CUs
-        # (weight gradients: [out][in] outputs with K = batch rows)
-        tiles = -(-M // 128) * -(-N // 128)
-        S = 1
-        if tiles < 128 and K >= 1024:
-            S = max(1, min(64, 256 // tiles, K // 256))
-        ws = _workspace(A.device, S * M * N) if S > 1 else None
-        check(dense_lib().h2omx_gemm(P(A), P(B), P(C), P(bias), M, N, K, int(ta), int(tb), act, beta_c, S, P(ws),
-                                 stream(A.device)), "gemm")
-        return C
-    a = A.T if ta else A
-    b = B.T if tb else B
-    c = a.float() @ b.float()
-    if beta_c and out is not None:
-        c = c + beta_c * out
+    _dev(A, "gemm")
+    # the kernel indexes dense row-major operands: copy strided views (no-op otherwise)
+    A = A.float().contiguous()
+    B = B.float().contiguous()
     if bias is not None:
-        c = c + bias
-    if act == 1:
-        c = torch.relu(c)
-    elif act == 2:
-        c = torch.tanh(c)
-    if out is not None:
-        out.copy_(c)
-        return out
-    return c
+        bias = bias.float().contiguous()
+    C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=A.device)
+    if not C.is_contiguous():
+        raise ValueError("gemm: out must be contiguous")
+    # split-K when the output has too few 128x128 tiles to fill 256 CUs
+    # (weight gradients: [out][in] outputs with K = batch rows)
+    tiles = -(-M // 128) * -(-N // 128)
+    S = 1
+    if tiles < 128 and K >= 1024:
+        S = max(1, min(64, 256 // tiles, K // 256))
+    ws = _workspace(A.device, S * M * N) if S > 1 else None
+    check(dense_lib().h2omx_gemm(P(A), P(B), P(C), P(bias), M, N, K, int(ta), int(tb), act, beta_c, S, P(ws),
+                             stream(A.device)), "gemm")
+    return C
 
 
 def act_backward(Y: torch.Tensor, dY: torch.Tensor, act: int) -> torch.Tensor:
     if act == 0:
         return dY
-    if Y.is_cuda:
-        check(dense_lib().h2omx_act_backward(P(Y), P(dY), Y.numel(), act, stream(Y.device)), "act_backward")
-        return dY
-    if act == 1:
-        dY.mul_((Y > 0).float())
-    elif act == 2:
-        dY.mul_(1 - Y * Y)
+    _dev(Y, "act_backward")
+    check(dense_lib().h2omx_act_backward(P(Y), P(dY), Y.numel(), act, stream(Y.device)), "act_backward")
     return dY
 
 
 def bias_grad(dY: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     M, N = dY.shape
-    if dY.is_cuda:
-        db = out if out is not None else torch.empty((N,), dtype=torch.float32, device=dY.device)
-        # enough (64-column x row-slice) blocks to fill the GPU, few enough that
-        # the second stage sums a short column
-        splits = max(1, min(32, M // 256, 1024 // max(1, -(-N // 64))))
-        ws = _workspace(dY.device, splits * N, slot=1)
-        check(dense_lib().h2omx_bias_grad(P(dY), P(db), M, N, P(ws), splits, stream(dY.device)), "bias_grad")
-        return db
-    r = dY.sum(0)
-    if out is not None:
-        out.copy_(r)
-        return out
-    return r
+    _dev(dY, "bias_grad")
+    db = out if out is not None else torch.empty((N,), dtype=torch.float32, device=dY.device)
+    # enough (64-column x row-slice) blocks to fill the GPU, few enough that
+    # the second stage sums a short column
+    splits = max(1, min(32, M // 256, 1024 // max(1, -(-N // 64))))
+    ws = _workspace(dY.device, splits * N, slot=1)
+    check(dense_lib().h2omx_bias_grad(P(dY), P(db), M, N, P(ws), splits, stream(dY.device)), "bias_grad")
+    return db
 
 
 def softmax_xent(Z: torch.Tensor, y: torch.Tensor):
     """Z [M][K] logits, y int32 class ids -> (dZ = (softmax - onehot) / M, mean loss)."""
     M, K = Z.shape
-    if Z.is_cuda:
-        y = y.to(torch.int32).contiguous()
-        dZ = torch.empty_like(Z)
-        loss = torch.zeros((1,), dtype=torch.float32, device=Z.device)
-        check(dense_lib().h2omx_softmax_xent(P(Z), P(y), P(dZ), P(loss), M, K, stream(Z.device)), "softmax_xent")
-        return dZ, loss
-    pr = torch.softmax(Z, 1)
-    oh = torch.nn.functional.one_hot(y.long(), K).float()
-    loss = -(torch.log(pr.clamp_min(1e-30)) * oh).sum(1).mean()
-    return (pr - oh) / M, loss.reshape(1)
+    _dev(Z, "softmax_xent")
+    y = y.to(torch.int32).contiguous()
+    dZ = torch.empty_like(Z)
+    loss = torch.zeros((1,), dtype=torch.float32, device=Z.device)
+    check(dense_lib().h2omx_softmax_xent(P(Z), P(y), P(dZ), P(loss), M, K, stream(Z.device)), "softmax_xent")
+    return dZ, loss
 
 
 def adadelta_(W, G, Eg2, Edx2, rho=0.99, eps=1e-8, l2=0.0):
-    if W.is_cuda:
-        check(dense_lib().h2omx_adadelta(P(W), P(G), P(Eg2), P(Edx2), W.numel(), rho, eps, l2, stream(W.device)),
-              "adadelta")
-        return
-    g = G + l2 * W
-    Eg2.mul_(rho).add_((1 - rho) * g * g)
-    dx = -torch.sqrt(Edx2 + eps) / torch.sqrt(Eg2 + eps) * g
-    Edx2.mul_(rho).add_((1 - rho) * dx * dx)
-    W.add_(dx)
+    _dev(W, "adadelta_")
+    check(dense_lib().h2omx_adadelta(P(W), P(G), P(Eg2), P(Edx2), W.numel(), rho, eps, l2, stream(W.device)),
+          "adadelta")
 
 
 def sgd_momentum_(W, G, V, lr, mom, l2=0.0):
-    if W.is_cuda:
-        check(dense_lib().h2omx_sgd_momentum(P(W), P(G), P(V), W.numel(), lr, mom, l2, stream(W.device)), "sgd")
-        return
-    V.mul_(mom).sub_(lr * (G + l2 * W))
-    W.add_(V)
+    _dev(W, "sgd_momentum_")
+    check(dense_lib().h2omx_sgd_momentum(P(W), P(G), P(V), W.numel(), lr, mom, l2, stream(W.device)), "sgd")
 
 
 # ---------------------------------------------------------------------------
 # bf16 MLP path (csrc/dense_kernels.hip gemm_bf16_nt_kernel): operands are
 # torch.bfloat16 row-major matrices whose row strides are multiples of 8
-# elements (16-byte rows, zero-padded K).  GPU only: on CPU tensors the same
-# contract is computed in fp32 from the bf16 values (test oracle).
+# elements (16-byte rows, zero-padded K).
 # ---------------------------------------------------------------------------
 def gemm_bf16_nt(A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int, *, bias=None, act: int = 0,
                  ymask: torch.Tensor | None = None, mask_act: int = 0, out_f32: torch.Tensor | None = None,
@@ -369,38 +304,16 @@ def gemm_bf16_nt(A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int, *, bi
     Views with unit inner stride; A/B/out row strides multiples of 8."""
     for t in (A, B):
         assert t.dtype == torch.bfloat16 and t.stride(-1) == 1
-    if A.is_cuda:
-        ldc = (out_f32 if out_f32 is not None else out_bf16).stride(0) if (out_f32 is not None or out_bf16 is not None) else N
-        if out_f32 is not None and out_bf16 is not None:
-            assert out_f32.stride(0) == out_bf16.stride(0)
-        ws = _workspace(A.device, splitk * M * N, slot=1) if splitk > 1 else None
-        check(dense_lib().h2omx_gemm_bf16(
-            P(A), A.stride(0), P(B), B.stride(0), M, N, K, P(bias), act, P(ymask),
-            ymask.stride(0) if ymask is not None else 0, mask_act, P(out_f32), P(out_bf16), ldc, P(out_bf16_t),
-            out_bf16_t.stride(0) if out_bf16_t is not None else 0, float(beta_c), splitk, P(ws), P(c_last),
-            stream(A.device)), "gemm_bf16")
-        return
-    c = A[:M, :K].float() @ B[:N, :K].float().T
-    if out_f32 is not None and beta_c:
-        c = c + beta_c * out_f32[:M, :N]
-    if bias is not None:
-        c = c + bias[:N]
-    if act == 1:
-        c = torch.relu(c)
-    elif act == 2:
-        c = torch.tanh(c)
-    if mask_act:
-        y = ymask[:M, :N].float()
-        c = torch.where(y > 0, c, torch.zeros_like(c)) if mask_act == 1 else c * (1 - y * y)
-    if c_last is not None:
-        c_last[:M] = c[:, N - 1]
-        c = c[:, : N - 1]
-    if out_f32 is not None:
-        out_f32[:M, : c.shape[1]] = c
-    if out_bf16 is not None:
-        out_bf16[:M, :N] = c.to(torch.bfloat16)
-    if out_bf16_t is not None:
-        out_bf16_t[:N, :M] = c.T.to(torch.bfloat16)
+    _dev(A, "gemm_bf16_nt")
+    ldc = (out_f32 if out_f32 is not None else out_bf16).stride(0) if (out_f32 is not None or out_bf16 is not None) else N
+    if out_f32 is not None and out_bf16 is not None:
+        assert out_f32.stride(0) == out_bf16.stride(0)
+    ws = _workspace(A.device, splitk * M * N, slot=1) if splitk > 1 else None
+    check(dense_lib().h2omx_gemm_bf16(
+        P(A), A.stride(0), P(B), B.stride(0), M, N, K, P(bias), act, P(ymask),
+        ymask.stride(0) if ymask is not None else 0, mask_act, P(out_f32), P(out_bf16), ldc, P(out_bf16_t),
+        out_bf16_t.stride(0) if out_bf16_t is not None else 0, float(beta_c), splitk, P(ws), P(c_last),
+        stream(A.device)), "gemm_bf16")
 
 
 def cvt_bf16(X: torch.Tensor, out: torch.Tensor | None = None, out_t: torch.Tensor | None = None) -> None:
@@ -408,25 +321,16 @@ def cvt_bf16(X: torch.Tensor, out: torch.Tensor | None = None, out_t: torch.Tens
     stride) and/or bf16 out_t [C][>=R]."""
     R, C = X.shape
     assert X.stride(-1) == 1
-    if X.is_cuda:
-        check(dense_lib().h2omx_cvt_bf16(P(X), X.stride(0), R, C, P(out), out.stride(0) if out is not None else 0,
-                                         P(out_t), out_t.stride(0) if out_t is not None else 0, stream(X.device)),
-              "cvt_bf16")
-        return
-    if out is not None:
-        out[:R, :C] = X.to(torch.bfloat16)
-        if out.shape[1] > C:
-            out[:R, C:] = 0
-    if out_t is not None:
-        out_t[:C, :R] = X.T.to(torch.bfloat16)
+    _dev(X, "cvt_bf16")
+    check(dense_lib().h2omx_cvt_bf16(P(X), X.stride(0), R, C, P(out), out.stride(0) if out is not None else 0,
+                                     P(out_t), out_t.stride(0) if out_t is not None else 0, stream(X.device)),
+          "cvt_bf16")
 
 
 def rowsum_bf16(X: torch.Tensor, R: int, C: int, out: torch.Tensor) -> None:
     """out[r] = sum_{c<C} X[r][c] (fp32) for a bf16 matrix (bias gradients from dZ^T)."""
-    if X.is_cuda:
-        check(dense_lib().h2omx_rowsum_bf16(P(X), X.stride(0), R, C, P(out), stream(X.device)), "rowsum_bf16")
-        return
-    out[:R] = X[:R, :C].float().sum(1)
+    _dev(X, "rowsum_bf16")
+    check(dense_lib().h2omx_rowsum_bf16(P(X), X.stride(0), R, C, P(out), stream(X.device)), "rowsum_bf16")
 
 
 class _CvtJob(ctypes.Structure):
@@ -440,10 +344,7 @@ def cvt_bf16_multi(jobs) -> None:
     jobs = list(jobs)
     if not jobs:
         return
-    if not jobs[0][0].is_cuda:
-        for X, out, out_t in jobs:
-            cvt_bf16(X, out, out_t)
-        return
+    _dev(jobs[0][0], "cvt_bf16_multi")
     arr = (_CvtJob * len(jobs))()
     mr = mc = 1
     for k, (X, out, out_t) in enumerate(jobs):
@@ -461,11 +362,6 @@ def softmax_xent_bf16(Z: torch.Tensor, y: torch.Tensor, dZ: torch.Tensor, dZt: t
     """Softmax cross-entropy of fp32 logits Z [M][K]: bf16 dZ [M][>=K] and dZ^T
     [K][>=M] ((softmax - onehot) / M); mean loss added into loss[0]."""
     M, K = Z.shape
-    if Z.is_cuda:
-        check(dense_lib().h2omx_softmax_xent_bf16(P(Z), P(y), P(dZ), dZ.stride(0), P(dZt), dZt.stride(0), P(loss), M,
-                                                  K, stream(Z.device)), "softmax_xent_bf16")
-        return
-    g, l = softmax_xent(Z, y)
-    dZ[:M, :K] = g.to(torch.bfloat16)
-    dZt[:K, :M] = g.T.to(torch.bfloat16)
-    loss += l
+    _dev(Z, "softmax_xent_bf16")
+    check(dense_lib().h2omx_softmax_xent_bf16(P(Z), P(y), P(dZ), dZ.stride(0), P(dZt), dZt.stride(0), P(loss), M,
+                                              K, stream(Z.device)), "softmax_xent_bf16")

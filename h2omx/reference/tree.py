@@ -13,32 +13,17 @@ It is not a performance path.
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
+import torch
 
-from .binning import BinnedMatrix
-from .engine import TreeParams, tree_capacity
-from .structs import DIST_CODES, TREE_NODE_DTYPE
-
-M32 = np.uint64(0xFFFFFFFF)
-
-
-def _mix32(x):
-    x = np.asarray(x, dtype=np.uint64) & M32
-    x ^= x >> np.uint64(16)
-    x = (x * np.uint64(0x7FEB352D)) & M32
-    x ^= x >> np.uint64(15)
-    x = (x * np.uint64(0x846CA68B)) & M32
-    x ^= x >> np.uint64(16)
-    return x
+from ..models.tree.binning import BinnedMatrix
+from ..models.tree.engine import TreeParams, tree_capacity
+from ..models.tree.hashing import M32, _mix32, hash4, u01  # noqa: F401
+from ..models.tree.structs import DIST_CODES, TREE_NODE_DTYPE
 
 
-def hash4(a, b, c, d):
-    a, b, c, d = (np.asarray(v, dtype=np.uint64) & M32 for v in (a, b, c, d))
-    return _mix32(a ^ _mix32(b ^ _mix32(c ^ _mix32((d + np.uint64(0x9E3779B9)) & M32))))
-
-
-def u01(hv):
-    return (np.asarray(hv, dtype=np.uint64) >> np.uint64(8)).astype(np.float64) * (1.0 / 16777216.0)
 
 
 def _l1(g, a):
@@ -265,3 +250,93 @@ def dist_grad(dist: str, F, y, tweedie_power=1.5, quantile_alpha=0.5, huber_delt
         r = F - y
         return np.where(np.abs(r) <= huber_delta, r, np.sign(r) * huber_delta), np.ones_like(F)
     return -y, np.ones_like(F)
+
+
+# ---- CPU boosting loop and scoring (moved out of models/tree/boost.py) ----
+def predict_tree_numpy(tree: np.ndarray, Xn: np.ndarray) -> np.ndarray:
+    n = Xn.shape[1]
+    idx = np.zeros(n, np.int64)
+    for _ in range(64):
+        feat = tree["feat"][idx]
+        inner = feat >= 0
+        if not inner.any():
+            break
+        r = np.nonzero(inner)[0]
+        v = Xn[feat[r], r]
+        nd = tree[idx[r]]
+        left = np.where(np.isnan(v), nd["na_left"] != 0, v <= nd["thr"])
+        idx[r] = np.where(left, nd["left"], nd["left"] + 1)
+    return tree["value"][idx].astype(np.float64)
+
+
+def raw_margin_cpu(ens, X, nt: int):
+    """TreeEnsemble.raw_margin for host tensors: margins [K][n] in fp64 NumPy."""
+    import torch
+
+    T = nt * ens.K
+    n = X.shape[1]
+    Xn = X.float().numpy()
+    out = np.zeros((ens.K, n), np.float64) if ens.average else np.repeat(ens.init_f[:, None], n, 1).astype(np.float64)
+    for t in range(T):
+        out[t % ens.K] += predict_tree_numpy(ens.trees[t], Xn)
+    if ens.average and nt > 0:
+        out /= nt
+    return torch.from_numpy(out.astype(np.float32))
+
+
+class _CpuView:
+    def __init__(self, Fm, trees, K, init_f):
+        self.Fm, self._trees, self.K, self.init_f = Fm, trees, K, init_f
+
+    @property
+    def margin(self) -> torch.Tensor:
+        return torch.from_numpy(self.Fm)
+
+    def trees(self, lo: int, hi: int) -> np.ndarray:
+        sel = self._trees[lo * self.K: hi * self.K]
+        return np.stack(sel) if sel else np.zeros((0, 1), TREE_NODE_DTYPE)
+
+
+def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw):
+    K, dist, n = ens.K, ens.dist, bm.n
+    builder = RefTreeBuilder(bm, tp, comm)
+    from ..models.tree.boost import _tree_fmask
+    from ..models.tree.engine import global_row_base
+
+    row_base = global_row_base(n, comm)
+    bmg = getattr(ens, "_base_margin", None)
+    Fm = (bmg.cpu().numpy().astype(np.float32).copy() if bmg is not None
+          else np.repeat(ens.init_f[:, None], n, 1).astype(np.float32))
+    wobs = np.ones(n, np.float32) if w_np is None else w_np.astype(np.float32)
+    trees = []
+    t0 = time.perf_counter()
+    for t in range(ntrees):
+        wb = wobs * bag_weights(n, sample_rate, seed, t, row_base)
+        if K == 1:
+            gr, hs = dist_grad(dist, Fm[0], y_np, **dist_kw)
+            grads = [(gr, hs)]
+        elif dist == "drf":
+            grads = [(-(y_np == k).astype(np.float64), np.ones(n)) for k in range(K)]
+        else:
+            z = Fm - Fm.max(axis=0, keepdims=True)
+            pr = np.exp(z)
+            pr /= pr.sum(axis=0, keepdims=True)
+            grads = [(pr[k] - (y_np == k), np.maximum(pr[k] * (1 - pr[k]), 1e-16)) for k in range(K)]
+        fmask = _tree_fmask(tp, bm.F, t, None)
+        for k in range(K):
+            gr, hs = grads[k]
+            pad = bm.npad - n
+            builder.nid[:] = -1
+            builder.nid[:n] = 0
+            g32 = np.concatenate([(gr * wb).astype(np.float32), np.zeros(pad, np.float32)])
+            h32 = np.concatenate([(hs * wb).astype(np.float32), np.zeros(pad, np.float32)])
+            w32 = np.concatenate([wb, np.zeros(pad, np.float32)])
+            tree = builder.build(g32, h32, w32, t * K + k, fmask)
+            leaf = ~builder.nid[:n]
+            Fm[k] += tree["value"][leaf]
+            trees.append(tree)
+        if callback is not None and callback(t, _CpuView(Fm, trees, K, ens.init_f)) is True:
+            break
+    ens.timings["train_s"] = time.perf_counter() - t0
+    ens.trees = np.stack(trees) if trees else ens.trees
+    ens._cpu_margin = Fm

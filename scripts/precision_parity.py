@@ -5,7 +5,7 @@ Same 1M-row HIGGS-shape data (generated on the CPU with a fixed seed, binned
 once with the same 255 quantile bins) is trained three ways, 50 trees,
 depth 5, learn_rate 0.1, min_rows 10:
 
-  * ``--part cpu``: ``RefTreeBuilder`` (h2omx/models/tree/reference.py: fp64
+  * ``--part cpu``: ``RefTreeBuilder`` (h2omx/reference/tree.py: fp64
     histograms, exact sums - the "exact" mode) and scikit-learn
     HistGradientBoosting (max_bins 255, no regularisation) -> margins + AUCs
   * ``--part gpu``: the HIP engine (int32 fixed-point rows with stochastic

@@ -3,13 +3,14 @@ import numpy as np
 import pytest
 import torch
 
-from h2omx.ops import dense as D
+from h2omx.backend import dense as D
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("p,family,link", [(5, "binomial", "logit"), (30, "gaussian", "identity"),
-                                           (61, "poisson", "log"), (100, "binomial", "logit")])
+                                           (61, "poisson", "log"), (100, "binomial", "logit"),
+                                           (300, "binomial", "logit"), (700, "gaussian", "identity")])
 def test_glm_irls_gram_matches_reference(cuda_dev, p, family, link):
     rng = np.random.default_rng(p)
     n = 20_011
@@ -33,9 +34,11 @@ def test_glm_irls_gram_matches_reference(cuda_dev, p, family, link):
     assert abs(dg - dr) / abs(dr) < 1e-5
 
 
-def test_glm_multinomial_gram(cuda_dev):
+@pytest.mark.parametrize("p", [12, 290])
+def test_glm_multinomial_gram(cuda_dev, p):
+    """p = 290 runs the wide path (eta GEMM + glm_wz / glm_aug + Gram GEMM)."""
     rng = np.random.default_rng(1)
-    p, n, K = 12, 9001, 3
+    n, K = 9001, 3
     X = rng.normal(size=(p, n)).astype(np.float32)
     y = rng.integers(0, K, n).astype(np.float32)
     beta = rng.normal(scale=0.1, size=(K, p + 1))

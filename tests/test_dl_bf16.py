@@ -6,7 +6,7 @@ import pytest
 import torch
 
 from h2omx.models.deeplearning import _Bf16Mlp, _Net
-from h2omx.ops import dense as D
+from h2omx.backend import dense as D
 
 
 def _net(sizes, act, dev, seed=0):
