@@ -7,9 +7,18 @@ cross-validates every model with shared folds, and finishes with two
 Stacked Ensembles (all models, best of family).  Models are ranked on a
 leaderboard by the H2O default metric for the problem type.
 
-Every model is data-parallel over all ranks of the cluster (the row shards
-stay where they are and each model's collectives run over RCCL), so AutoML
-on 8 MI355X trains each model 8-way parallel in sequence.
+Two schedulers (``parallelism``, an h2omx extension):
+
+* ``"data"`` (default): every model is data-parallel over all ranks (the row
+  shards stay where they are and each model's collectives run over RCCL), so
+  AutoML on 8 MI355X trains each model 8-way parallel in sequence.
+* ``"task"``: the training frame is replicated on every GPU (all-gather; 288
+  GB of HBM holds the AutoML shapes many times over) and the model plan is
+  dealt round-robin to the ranks, each training its models on its own GPU
+  with no collectives.  The models are then exchanged (MOJO bytes + metrics +
+  cross-validation holdout predictions) so every rank holds the full set; the
+  stacked ensembles and the leaderboard are computed identically everywhere.
+  Small and medium models stop paying per-level collective latency.
 """
 from __future__ import annotations
 
@@ -84,7 +93,10 @@ class H2OAutoML:
                  project_name=None, include_algos=None, exclude_algos=None, sort_metric="AUTO",
                  keep_cross_validation_predictions=True, stopping_rounds=3, stopping_tolerance=None,
                  stopping_metric="AUTO", balance_classes=False, verbosity="warn", modeling_plan=None,
-                 preprocessing=None, exploitation_ratio=-1.0, **_ignored):
+                 preprocessing=None, exploitation_ratio=-1.0, parallelism="data", **_ignored):
+        if parallelism not in ("data", "task"):
+            raise ValueError("parallelism must be 'data' or 'task'")
+        self.parallelism = parallelism
         self.max_models = max_models
         self.max_runtime_secs = max_runtime_secs
         self.max_runtime_secs_per_model = float(max_runtime_secs_per_model or 0.0)
@@ -160,26 +172,14 @@ class H2OAutoML:
         start_models = len(self.models)
         if self.max_models:
             self.max_models = int(self.max_models) + start_models
-        for algo, suffix, cls, params in PRESETS:
-            if algo.lower() not in self.algos or not self._planned(algo, "defaults"):
-                continue
-            if out_of_budget():
-                break
-            fit(f"{algo}_{suffix}", cls, dict(params))
-        # random grids, round-robin over the families still allowed
-        fams = [f for f in ("xgboost", "gbm", "deeplearning") if f in self.algos and self._planned(f, "grids")]
-        counters = {f: 1 for f in fams}
-        name = {"xgboost": "XGBoost", "gbm": "GBM", "deeplearning": "DeepLearning"}
-        while fams and not out_of_budget() and (self.max_models or budget) and sum(counters.values()) < 300:
-            for f in list(fams):
-                if out_of_budget():
-                    break
-                cls, space = GRIDS[f]
-                params = {k: v[int(rng.integers(len(v)))] for k, v in space.items()}
-                if f != "deeplearning":
-                    params.update({k: v for k, v in self.stopping.items() if v is not None})
-                fit(f"{name[f]}_grid_1_model_{counters[f]}", cls, params)
-                counters[f] += 1
+        if self.parallelism == "task" and comm is not None and comm.world_size > 1:
+            category = self._train_task_parallel(x, y, training_frame, validation_frame, comm, cv, rng, budget, t0,
+                                                 start_models)
+            training_frame = self._local_frame
+            comm_se = None
+        else:
+            category = self._train_sequential(fit, rng, out_of_budget)
+            comm_se = comm
         base = [m for m in self.models if m.cross_validation_holdout is not None]
         if "stackedensemble" in self.algos and self.nfolds > 1 and len(base) >= 2 and category != ModelCategory.CLUSTERING:
             for name, members in (("StackedEnsemble_AllModels", base),
@@ -189,7 +189,7 @@ class H2OAutoML:
                 try:
                     se = H2OStackedEnsembleEstimator(model_id=f"{name}_AutoML_{self.project_name}",
                                                      base_models=[m.model_id for m in members], seed=seed)
-                    m = se.train(x=x, y=y, training_frame=training_frame, comm=comm)
+                    m = se.train(x=x, y=y, training_frame=training_frame, comm=comm_se)
                     m.cross_validation_metrics = None
                     self.models.append(m)
                     self._log("ModelTraining", f"{m.model_id} trained")
@@ -199,9 +199,114 @@ class H2OAutoML:
         self._log("Workflow", f"AutoML build done: {len(self.models)} models in {time.time() - t0:.1f}s")
         self.training_info = {"start_epoch": int(t0), "stop_epoch": int(time.time()),
                               "duration_secs": round(time.time() - t0, 3), "models": len(self.models),
-                              "leader": self.leader.model_id if self.leader is not None else None}
+                              "leader": self.leader.model_id if self.leader is not None else None,
+                              "parallelism": self.parallelism}
         self._x, self._frame = x, training_frame
         return self
+
+    def _plan_models(self, rng) -> list:
+        """The ordered model plan: presets, then the round-robin random grids
+        (identical on every rank for a given seed)."""
+        out = [(f"{algo}_{suffix}", cls, dict(params)) for algo, suffix, cls, params in PRESETS
+               if algo.lower() in self.algos and self._planned(algo, "defaults")]
+        fams = [f for f in ("xgboost", "gbm", "deeplearning") if f in self.algos and self._planned(f, "grids")]
+        name = {"xgboost": "XGBoost", "gbm": "GBM", "deeplearning": "DeepLearning"}
+        cap = (self.max_models - len(self.models)) if self.max_models else 300
+        counters = {f: 1 for f in fams}
+        while fams and len(out) < cap and sum(counters.values()) < 300:
+            for f in fams:
+                cls, space = GRIDS[f]
+                params = {k: v[int(rng.integers(len(v)))] for k, v in space.items()}
+                if f != "deeplearning":
+                    params.update({k: v for k, v in self.stopping.items() if v is not None})
+                out.append((f"{name[f]}_grid_1_model_{counters[f]}", cls, params))
+                counters[f] += 1
+        return out[:cap] if self.max_models else out
+
+    def _train_sequential(self, fit, rng, out_of_budget):
+        category = None
+        for algo, suffix, cls, params in PRESETS:
+            if algo.lower() not in self.algos or not self._planned(algo, "defaults"):
+                continue
+            if out_of_budget():
+                break
+            m = fit(f"{algo}_{suffix}", cls, dict(params))
+            category = m.category if m is not None else category
+        # random grids, round-robin over the families still allowed
+        fams = [f for f in ("xgboost", "gbm", "deeplearning") if f in self.algos and self._planned(f, "grids")]
+        counters = {f: 1 for f in fams}
+        name = {"xgboost": "XGBoost", "gbm": "GBM", "deeplearning": "DeepLearning"}
+        while fams and not out_of_budget() and sum(counters.values()) < 300:
+            for f in list(fams):
+                if out_of_budget():
+                    break
+                cls, space = GRIDS[f]
+                params = {k: v[int(rng.integers(len(v)))] for k, v in space.items()}
+                if f != "deeplearning":
+                    params.update({k: v for k, v in self.stopping.items() if v is not None})
+                m = fit(f"{name[f]}_grid_1_model_{counters[f]}", cls, params)
+                category = m.category if m is not None else category
+                counters[f] += 1
+        return category
+
+    def _train_task_parallel(self, x, y, training_frame, validation_frame, comm, cv, rng, budget, t0, start_models):
+        """parallelism="task": replicate the frame, deal the plan round-robin to
+        the ranks, train locally (comm=None), exchange the trained models."""
+        from .frame.distributed import _gather_objects, gather_frame
+        from .mojo import GenericModel, mojo_bytes
+
+        local = gather_frame(training_frame, comm)
+        valid = gather_frame(validation_frame, comm) if validation_frame is not None else None
+        self._local_frame = local
+        plan = self._plan_models(rng)
+        mine = []
+        self._log("Workflow", f"task-parallel: {len(plan)} models over {comm.world_size} ranks "
+                              f"({local.nrows} rows replicated per rank)")
+        for i in range(comm.rank, len(plan), comm.world_size):
+            if budget and time.time() - t0 > budget:
+                break
+            name, cls, params = plan[i]
+            mid = f"{name}_AutoML_{self.project_name}"
+            rt = self.max_runtime_secs_per_model
+            if budget:
+                left = max(budget - (time.time() - t0), 1.0)
+                rt = min(rt, left) if rt else left
+            if rt:
+                params = dict(params, max_runtime_secs=rt)
+            try:
+                m = cls(model_id=mid, **params, **cv).train(x=x, y=y, training_frame=local, validation_frame=valid,
+                                                            comm=None)
+            except Exception as e:  # noqa: BLE001
+                self._log("ModelTraining", f"{name} failed on rank {comm.rank}: {type(e).__name__}: {e}")
+                continue
+            h = m.cross_validation_holdout
+            mine.append((i, {"model_id": m.model_id, "algo": m.algo, "mojo": mojo_bytes(m),
+                             "training_metrics": m.training_metrics, "validation_metrics": m.validation_metrics,
+                             "cross_validation_metrics": m.cross_validation_metrics,
+                             "holdout": None if h is None else h.detach().cpu().numpy(),
+                             "run_time_ms": getattr(m, "run_time_ms", 0), "rank": comm.rank}, m))
+        payloads = _gather_objects(comm, [(i, pl) for i, pl, _ in mine])
+        native = {i: m for i, _, m in mine}
+        category = None
+        for i, pl in sorted((e for lst in payloads for e in lst), key=lambda e: e[0]):
+            m = native.get(i)
+            if m is None:
+                # trained on another rank: scoring model from its MOJO + the training-side metrics
+                m = GenericModel(pl["mojo"], pl["model_id"])
+                m.algo = pl["algo"]
+                m.training_metrics = pl["training_metrics"]
+                m.validation_metrics = pl["validation_metrics"]
+                m.cross_validation_metrics = pl["cross_validation_metrics"]
+                m.run_time_ms = pl["run_time_ms"]
+                if pl["holdout"] is not None:
+                    import torch
+
+                    m.cross_validation_holdout = torch.from_numpy(pl["holdout"]).to(local.device)
+                DKV.put(m.model_id, m)
+            category = m.category
+            self.models.append(m)
+            self._log("ModelTraining", f"{pl['model_id']} trained on rank {pl['rank']}")
+        return category
 
     def _planned(self, algo: str, kind: str) -> bool:
         if self.plan is None:
@@ -341,7 +446,8 @@ def run_automl(spec: dict, comm=None) -> dict:
                     include_algos=bm.get("include_algos"), exclude_algos=bm.get("exclude_algos"),
                     sort_metric=isp.get("sort_metric", "AUTO"), modeling_plan=bm.get("modeling_plan"),
                     stopping_rounds=sc.get("stopping_rounds", 3), stopping_metric=sc.get("stopping_metric", "AUTO"),
-                    stopping_tolerance=sc.get("stopping_tolerance"), preprocessing=bm.get("preprocessing"))
+                    stopping_tolerance=sc.get("stopping_tolerance"), preprocessing=bm.get("preprocessing"),
+                    parallelism=bc.get("parallelism", "data"))
     tf = DKV.get(_key(isp.get("training_frame")))
     lf = DKV.get(_key(isp.get("leaderboard_frame"))) if isp.get("leaderboard_frame") else None
     y = isp.get("response_column")
