@@ -8,11 +8,15 @@
 //     routed by a per-row node id (nid).  Only the smaller child of every
 //     split is histogrammed ("built"); the sibling is parent - built
 //     (subtraction trick), so LDS atomics are spent on <= half the rows.
-//   * Per-workgroup private histograms live in LDS (ds_add_f32); each
-//     workgroup flushes its histogram with plain coalesced stores into a
-//     partial slab and a second kernel reduces the slabs in fp64.  No global
-//     float atomics on the hot path (they run at ~1.3 TB/s chip-wide and
-//     would dominate, see MI355X_MICROARCH.md "Global float atomics").
+//   * Per-workgroup private histograms live in LDS as packed fixed-point
+//     integers: one ds_add_u64 per (row, feature) carries (int32 G_q << 32 |
+//     uint32 S_q) (see K3 below).  Each workgroup flushes its histogram with
+//     plain coalesced stores into a partial slab and hist_reduce sums the
+//     slabs in exact int64; split scans decode to fp64.  No global atomics
+//     on the hot path (see MI355X_MICROARCH.md "Global float atomics").
+//   * Deep levels of the segmented engine (DRF / XGBoost depth 10-20) run
+//     in direct mode: rows live in per-node segments and seg_direct_kernel
+//     builds each node's eligible features and scans them in LDS.
 //   * The level bookkeeping (which nodes split, which child gets built,
 //     node numbering) runs on the device, so a whole tree is a fixed
 //     sequence of launches with NO host synchronisation: the host only
@@ -1093,6 +1097,90 @@ __global__ __launch_bounds__(64) void node_best_kernel(const FeatBest* __restric
 // the children, pick the smaller child to build, write tree records and the
 // partition table.  ctl_next receives the next level's counts.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ bool lf_decide(const NodeSplit& s, const SplitParams& p) {
+  bool do_split = !p.is_last_level && s.feat >= 0 && isfinite(s.gain) && s.gain > 0.0;
+  if (do_split && p.mode == 0 && p.min_split_improvement > 0.0) {
+    // relative improvement over the node's explained sum of squares
+    const double base_term = (s.W > 0.0) ? s.G * s.G / s.W : 0.0;
+    do_split = s.gain > p.min_split_improvement * fmax(base_term, 1e-12);
+  }
+  return do_split;
+}
+
+// node i of the level: tree record, partition entry and (split nodes) the
+// children's links; k_idx = rank of i among the level's splitting nodes
+__device__ __forceinline__ void lf_write_node(int i, const NodeSplit& s, bool do_split, int k_idx, int base,
+                                              int next_base, int max_next_nodes, const SplitParams& p,
+                                              const float* __restrict__ edges, const int* __restrict__ nvb, int nbt,
+                                              PartInfo* __restrict__ part, NodeLink* __restrict__ next_link,
+                                              TreeNode* __restrict__ tree, int tree_capacity) {
+  if (do_split && 2 * (k_idx + 1) > max_next_nodes) do_split = false;  // capacity guard
+  const int gid = base + i;
+  const double v = leaf_value(s.G, s.H, s.W, p);
+  PartInfo pi;
+  pi.gid = gid;
+  pi.leaf_children = 0;
+  pi.child_gid = -1;
+  pi.pad = 0;
+  TreeNode tn;
+  tn.value = (float)v;
+  tn.weight = (float)s.W;
+  tn.gain = do_split ? (float)s.gain : 0.0f;
+  if (do_split) {
+    pi.feat = s.feat; pi.bin = s.bin; pi.na_left = s.na_left; pi.child = 2 * k_idx;
+    tn.feat = s.feat; tn.bin = s.bin; tn.na_left = s.na_left; tn.left = next_base + 2 * k_idx;
+    const int m = nvb[s.feat];
+    tn.thr = (s.bin < m - 1) ? edges[(int64_t)s.feat * nbt + s.bin] : INFINITY;
+    const bool build_left = s.WL <= (s.W - s.WL);
+    NodeLink L, R;
+    L.parent = R.parent = i;
+    L.pad = R.pad = 0;
+    L.slot = build_left ? k_idx : -1;
+    L.sib_slot = build_left ? -1 : k_idx;
+    R.slot = build_left ? -1 : k_idx;
+    R.sib_slot = build_left ? k_idx : -1;
+    if (next_link) {
+      next_link[2 * k_idx] = L;
+      next_link[2 * k_idx + 1] = R;
+    }
+    pi.pad = (L.slot & 0xFFFF) | (R.slot << 16);  // children's build slots (partition -> slot16)
+    pi.child_gid = next_base + 2 * k_idx;
+    if (p.children_leaves) {
+      // children are final: their totals come from this split's left stats
+      pi.leaf_children = 1;
+      const double GR = s.G - s.GL, HR = s.H - s.HL, WR = s.W - s.WL;
+      TreeNode lc, rc;
+      lc.feat = rc.feat = -1;
+      lc.bin = rc.bin = 0;
+      lc.left = rc.left = -1;
+      lc.na_left = rc.na_left = 0;
+      lc.thr = rc.thr = 0.0f;
+      lc.gain = rc.gain = 0.0f;
+      lc.value = (float)leaf_value(s.GL, s.HL, s.WL, p);
+      rc.value = (float)leaf_value(GR, HR, WR, p);
+      lc.weight = (float)s.WL;
+      rc.weight = (float)WR;
+      if (next_base + 2 * k_idx + 1 < tree_capacity) {
+        tree[next_base + 2 * k_idx] = lc;
+        tree[next_base + 2 * k_idx + 1] = rc;
+      }
+    }
+  } else {
+    pi.feat = -1; pi.bin = 0; pi.na_left = 0; pi.child = -1;
+    tn.feat = -1; tn.bin = 0; tn.na_left = 0; tn.left = -1; tn.thr = 0.0f;
+  }
+  part[i] = pi;
+  if (gid < tree_capacity) tree[gid] = tn;
+}
+
+__device__ __forceinline__ void lf_write_ctl(int* __restrict__ ctl_next, int ks, int next_base, int max_next_nodes) {
+  if (2 * ks > max_next_nodes) ks = max_next_nodes / 2;
+  ctl_next[CTL_N] = 2 * ks;
+  ctl_next[CTL_SLOTS] = ks;
+  ctl_next[CTL_BASE] = next_base;
+  ctl_next[CTL_TOTAL] = next_base + 2 * ks;
+}
+
 __device__ void level_finalize_body(const NodeSplit* __restrict__ nsplit, const int* __restrict__ ctl,
                                     int* __restrict__ ctl_next, const SplitParams& p, const float* __restrict__ edges,
                                     const int* __restrict__ nvb, int nbt, int max_next_nodes,
@@ -1112,12 +1200,7 @@ __device__ void level_finalize_body(const NodeSplit* __restrict__ nsplit, const 
     NodeSplit s;
     if (i < n) {
       s = nsplit[i];
-      do_split = !p.is_last_level && s.feat >= 0 && isfinite(s.gain) && s.gain > 0.0;
-      if (do_split && p.mode == 0 && p.min_split_improvement > 0.0) {
-        // relative improvement over the node's explained sum of squares
-        const double base_term = (s.W > 0.0) ? s.G * s.G / s.W : 0.0;
-        do_split = s.gain > p.min_split_improvement * fmax(base_term, 1e-12);
-      }
+      do_split = lf_decide(s, p);
     }
     // block exclusive scan of do_split
     const unsigned long long bal = __ballot(do_split);
@@ -1126,66 +1209,9 @@ __device__ void level_finalize_body(const NodeSplit* __restrict__ nsplit, const 
     __syncthreads();
     int before = carry;
     for (int k = 0; k < wid; ++k) before += wsum[k];
-    const int k_idx = before + within;
-    if (do_split && 2 * (k_idx + 1) > max_next_nodes) do_split = false;  // capacity guard
-    if (i < n) {
-      const int gid = base + i;
-      const double v = leaf_value(s.G, s.H, s.W, p);
-      PartInfo pi;
-      pi.gid = gid;
-      pi.leaf_children = 0;
-      pi.child_gid = -1;
-      pi.pad = 0;
-      TreeNode tn;
-      tn.value = (float)v;
-      tn.weight = (float)s.W;
-      tn.gain = do_split ? (float)s.gain : 0.0f;
-      if (do_split) {
-        pi.feat = s.feat; pi.bin = s.bin; pi.na_left = s.na_left; pi.child = 2 * k_idx;
-        tn.feat = s.feat; tn.bin = s.bin; tn.na_left = s.na_left; tn.left = next_base + 2 * k_idx;
-        const int m = nvb[s.feat];
-        tn.thr = (s.bin < m - 1) ? edges[(int64_t)s.feat * nbt + s.bin] : INFINITY;
-        const bool build_left = s.WL <= (s.W - s.WL);
-        NodeLink L, R;
-        L.parent = R.parent = i;
-        L.pad = R.pad = 0;
-        L.slot = build_left ? k_idx : -1;
-        L.sib_slot = build_left ? -1 : k_idx;
-        R.slot = build_left ? -1 : k_idx;
-        R.sib_slot = build_left ? k_idx : -1;
-        if (next_link) {
-          next_link[2 * k_idx] = L;
-          next_link[2 * k_idx + 1] = R;
-        }
-        pi.pad = (L.slot & 0xFFFF) | (R.slot << 16);  // children's build slots (partition -> slot16)
-        pi.child_gid = next_base + 2 * k_idx;
-        if (p.children_leaves) {
-          // children are final: their totals come from this split's left stats
-          pi.leaf_children = 1;
-          const double GR = s.G - s.GL, HR = s.H - s.HL, WR = s.W - s.WL;
-          TreeNode lc, rc;
-          lc.feat = rc.feat = -1;
-          lc.bin = rc.bin = 0;
-          lc.left = rc.left = -1;
-          lc.na_left = rc.na_left = 0;
-          lc.thr = rc.thr = 0.0f;
-          lc.gain = rc.gain = 0.0f;
-          lc.value = (float)leaf_value(s.GL, s.HL, s.WL, p);
-          rc.value = (float)leaf_value(GR, HR, WR, p);
-          lc.weight = (float)s.WL;
-          rc.weight = (float)WR;
-          if (next_base + 2 * k_idx + 1 < tree_capacity) {
-            tree[next_base + 2 * k_idx] = lc;
-            tree[next_base + 2 * k_idx + 1] = rc;
-          }
-        }
-      } else {
-        pi.feat = -1; pi.bin = 0; pi.na_left = 0; pi.child = -1;
-        tn.feat = -1; tn.bin = 0; tn.na_left = 0; tn.left = -1; tn.thr = 0.0f;
-      }
-      part[i] = pi;
-      if (gid < tree_capacity) tree[gid] = tn;
-    }
+    if (i < n)
+      lf_write_node(i, s, do_split, before + within, base, next_base, max_next_nodes, p, edges, nvb, nbt, part,
+                    next_link, tree, tree_capacity);
     __syncthreads();
     if (t == 0) {
       int tot = 0;
@@ -1194,14 +1220,97 @@ __device__ void level_finalize_body(const NodeSplit* __restrict__ nsplit, const 
     }
     __syncthreads();
   }
-  if (t == 0) {
-    int ks = carry;
-    if (2 * ks > max_next_nodes) ks = max_next_nodes / 2;
-    ctl_next[CTL_N] = 2 * ks;
-    ctl_next[CTL_SLOTS] = ks;
-    ctl_next[CTL_BASE] = next_base;
-    ctl_next[CTL_TOTAL] = next_base + 2 * ks;
+  if (t == 0) lf_write_ctl(ctl_next, carry, next_base, max_next_nodes);
+}
+
+// Multi-block level finalisation (levels with tens of thousands of nodes,
+// where one workgroup walking the level took ~0.9 ms at depth 19): count the
+// splitting nodes per 1024-node tile, scan the tile counts in one small
+// workgroup, then every tile numbers its nodes from its prefix.  Same
+// decisions and numbering as level_finalize_body.
+constexpr int LF_TILE = 1024;
+__global__ __launch_bounds__(LF_TILE) void lf_count_kernel(const NodeSplit* __restrict__ nsplit,
+                                                           const int* __restrict__ ctl, SplitParams p,
+                                                           int* __restrict__ tiles) {
+  __shared__ int wsum[16];
+  const int n = ctl[CTL_N];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int i = blockIdx.x * LF_TILE + t;
+  if (blockIdx.x * LF_TILE >= n) {
+    if (t == 0) tiles[blockIdx.x] = 0;
+    return;
   }
+  const bool do_split = i < n && lf_decide(nsplit[i], p);
+  const unsigned long long bal = __ballot(do_split);
+  if (lane == 0) wsum[wid] = __popcll(bal);
+  __syncthreads();
+  if (t == 0) {
+    int tot = 0;
+    for (int k = 0; k < LF_TILE / 64; ++k) tot += wsum[k];
+    tiles[blockIdx.x] = tot;
+  }
+}
+
+__global__ __launch_bounds__(1024) void lf_scan_kernel(int* __restrict__ tiles, int ntiles, const int* __restrict__ ctl,
+                                                       int* __restrict__ ctl_next, int max_next_nodes) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < ntiles; c0 += 1024) {
+    const int i = c0 + t;
+    const int v = i < ntiles ? tiles[i] : 0;
+    int x = v;   // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, kWave);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    int before = carry;
+    for (int k = 0; k < wid; ++k) before += wsum[k];
+    if (i < ntiles) tiles[i] = before + x - v;   // exclusive
+    __syncthreads();
+    if (t == 0) {
+      int tot = 0;
+      for (int k = 0; k < 16; ++k) tot += wsum[k];
+      carry += tot;
+    }
+    __syncthreads();
+  }
+  if (t == 0) lf_write_ctl(ctl_next, carry, ctl[CTL_BASE] + ctl[CTL_N], max_next_nodes);
+}
+
+__global__ __launch_bounds__(LF_TILE) void lf_write_kernel(const NodeSplit* __restrict__ nsplit,
+                                                           const int* __restrict__ ctl, SplitParams p,
+                                                           const float* __restrict__ edges,
+                                                           const int* __restrict__ nvb, int nbt, int max_next_nodes,
+                                                           PartInfo* __restrict__ part,
+                                                           NodeLink* __restrict__ next_link,
+                                                           TreeNode* __restrict__ tree, int tree_capacity,
+                                                           const int* __restrict__ tiles) {
+  __shared__ int wsum[16];
+  const int n = ctl[CTL_N];
+  if (blockIdx.x * LF_TILE >= n) return;
+  const int base = ctl[CTL_BASE];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int i = blockIdx.x * LF_TILE + t;
+  NodeSplit s;
+  bool do_split = false;
+  if (i < n) {
+    s = nsplit[i];
+    do_split = lf_decide(s, p);
+  }
+  const unsigned long long bal = __ballot(do_split);
+  if (lane == 0) wsum[wid] = __popcll(bal);
+  __syncthreads();
+  int before = tiles[blockIdx.x];
+  for (int k = 0; k < wid; ++k) before += wsum[k];
+  if (i < n)
+    lf_write_node(i, s, do_split, before + __popcll(bal & ((1ull << lane) - 1ull)), base, base + n, max_next_nodes,
+                  p, edges, nvb, nbt, part, next_link, tree, tree_capacity);
 }
 
 __global__ __launch_bounds__(1024) void level_finalize_kernel(const NodeSplit* __restrict__ nsplit,
@@ -2189,10 +2298,33 @@ H2OMX_API int h2omx_split_level(const long long* built, const long long* parent_
   return launch_status();
 }
 
+// level finalisation from per-node splits: one workgroup for small levels,
+// count / scan / write tiles (lf_*_kernel) when the level can hold more than
+// LF_MB_NODES nodes and the caller passed a tile scratch (>= max_nodes / 1024 + 1 ints)
+constexpr int LF_MB_NODES = 8192;
+static void level_finalize_launch(const NodeSplit* ns, const int* ctl, int* ctl_next, const SplitParams& p,
+                                  const float* edges, const int* nvb, int nbt, int max_next_nodes, void* part,
+                                  void* next_link, void* tree, int tree_capacity, int max_nodes, int* tiles,
+                                  hipStream_t stream) {
+  PartInfo* pi = reinterpret_cast<PartInfo*>(part);
+  NodeLink* nl = reinterpret_cast<NodeLink*>(next_link);
+  TreeNode* tr = reinterpret_cast<TreeNode*>(tree);
+  if (tiles == nullptr || max_nodes <= LF_MB_NODES) {
+    hipLaunchKernelGGL(level_finalize_kernel, dim3(1), dim3(1024), 0, stream, ns, ctl, ctl_next, p, edges, nvb, nbt,
+                       max_next_nodes, pi, nl, tr, tree_capacity);
+    return;
+  }
+  const int nt = (max_nodes + LF_TILE - 1) / LF_TILE;
+  hipLaunchKernelGGL(lf_count_kernel, dim3(nt), dim3(LF_TILE), 0, stream, ns, ctl, p, tiles);
+  hipLaunchKernelGGL(lf_scan_kernel, dim3(1), dim3(1024), 0, stream, tiles, nt, ctl, ctl_next, max_next_nodes);
+  hipLaunchKernelGGL(lf_write_kernel, dim3(nt), dim3(LF_TILE), 0, stream, ns, ctl, p, edges, nvb, nbt, max_next_nodes,
+                     pi, nl, tr, tree_capacity, tiles);
+}
+
 H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_next, const void* params,
                                    const float* edges, const int* nvb, int nbt, int max_next_nodes, void* part,
                                    void* next_link, void* tree, int tree_capacity, void* nsplit,
-                                   int max_nodes, hipStream_t stream) {
+                                   int max_nodes, int* tiles, hipStream_t stream) {
   const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
   NodeSplit* ns = reinterpret_cast<NodeSplit*>(nsplit);
   static const int fuse_cap = [] {
@@ -2208,10 +2340,8 @@ H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_n
   }
   hipLaunchKernelGGL(node_best_kernel, dim3(max_nodes), dim3(64), 0, stream, reinterpret_cast<const FeatBest*>(fbest),
                      ctl, p.F, ns);
-  hipLaunchKernelGGL(level_finalize_kernel, dim3(1), dim3(1024), 0, stream,
-                     ns, ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes,
-                     reinterpret_cast<PartInfo*>(part), reinterpret_cast<NodeLink*>(next_link),
-                     reinterpret_cast<TreeNode*>(tree), tree_capacity);
+  level_finalize_launch(ns, ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes, part, next_link, tree, tree_capacity,
+                        max_nodes, tiles, stream);
   return launch_status();
 }
 
@@ -2455,7 +2585,7 @@ __global__ __launch_bounds__(512) void hist_build_seg_kernel(
     const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
     const int* __restrict__ hc_first, const int* __restrict__ ctl, const int* __restrict__ nvb,
     const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups, int hc_rows,
-    unsigned long long* __restrict__ slab) {
+    unsigned long long* __restrict__ slab, int gpos) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
   __shared__ int width_s[256], rep_s[256];
   __shared__ int range_s[2];
@@ -2491,10 +2621,11 @@ __global__ __launch_bounds__(512) void hist_build_seg_kernel(
   const int nw = (nf + 3) >> 2;
   for (int j = lo + threadIdx.x; j < hi; j += blockDim.x) {
     const int r = idx ? idx[j] : j;
-    const uint32_t hsh = row_hash(r, salt);
+    const uint32_t hsh = row_hash(rb + r, salt);   // global row id: multi-rank == one rank
     const float d1 = (hsh & 0xFFFF) * (1.0f / 65536.0f), d2 = (hsh >> 16) * (1.0f / 65536.0f);
-    const float sv = s2 ? s2[r] : 1.0f;
-    const int gq = (int)floorf(fmaf(g[r], sg, d1));
+    const int gi = gpos ? j : r;   // g / s2 stored in segment order (part_scatter) or by row
+    const float sv = s2 ? s2[gi] : 1.0f;
+    const int gq = (int)floorf(fmaf(g[gi], sg, d1));
     const uint32_t sq = (uint32_t)floorf(fmaf(sv, ss, d2));
     const unsigned long long pk = ((unsigned long long)(uint32_t)gq << 32) | (unsigned long long)sq;
     if (pk == 0ull) continue;
@@ -2819,6 +2950,663 @@ __global__ __launch_bounds__(256) void node_close_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Deep levels, direct mode (segmented engine): one workgroup per node builds
+// the histograms of the node's ELIGIBLE features only (mtries / column
+// sampling / per-tree mask, the same hash ranks as split_find) straight from
+// the node's rows and scans them in LDS - no parent histograms, no sibling
+// subtraction, no histogram ever written to global memory.  At depth 10-20
+// the subtraction machinery moved nodes x F x bins int64 rows per level
+// (split_find copying parents, hist_reduce, zero_slots: ~15 ms at level 18 of
+// DRF 10M x 100, profiles/drf_depth20_level_breakdown.txt) while the rows of
+// all nodes are only n x (eligible F) bytes.  Exact int64 sums of the same
+// quantised rows: bit-identical splits to the subtraction path.  Writes the
+// node's NodeSplit directly (level_finalize_ns follows).
+// ---------------------------------------------------------------------------
+constexpr int DIRECT_LDS_BYTES = 96 * 1024;   // histogram batch (G and S int64 planes)
+#ifndef H2OMX_DIRECT_WAVES
+#define H2OMX_DIRECT_WAVES 4
+#endif
+constexpr int DIRECT_WAVES = H2OMX_DIRECT_WAVES;   // waves per node workgroup (<= 4)
+// Nodes with fewer rows than this accumulate ONE packed 64-bit LDS atomic per
+// (row, feature) - (int32 G_q << 32) + uint32 S_q, as hist_build_kernel - instead
+// of a G and an S plane: per-row |G_q| <= 2^15 and S_q <= 2^16 keep |sum G_q| <
+// 2^31 and sum S_q < 2^32, so the halves never carry into each other.
+constexpr int DIRECT_PACK_ROWS = 65536;
+
+struct DirectBest {
+  double gain, GL, SL;
+  long long key;   // (feature << 32 | code), smallest wins ties; LLONG_MAX = none
+};
+
+// the split scan of one feature's LDS histogram by one wave (split_find's
+// feat_best_wave on exact int64 rows); PACKED: one packed u64 per bin
+template <int NBT, bool PACKED>
+__device__ __forceinline__ void direct_scan_feature(const long long* __restrict__ h, int f, int m, double ig,
+                                                    double is, const SplitParams& p, int lane, DirectBest& best) {
+  constexpr int B = NBT <= 64 ? 1 : NBT / 64;
+  constexpr int NA_LANE = (NBT - 1) / B, NA_K = (NBT - 1) % B;
+  long long gi[B], si[B];
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const int bin = lane * B + k;
+    gi[k] = 0; si[k] = 0;
+    if (bin < NBT) {
+      if constexpr (PACKED) {
+        const unsigned long long v = (unsigned long long)h[bin];
+        gi[k] = (long long)(int)(uint32_t)(v >> 32);
+        si[k] = (long long)(uint32_t)v;
+      } else {
+        gi[k] = h[bin];
+        si[k] = h[NBT + bin];
+      }
+    }
+  }
+  const long long ng_i = __shfl(gi[NA_K], NA_LANE, kWave), ns_i = __shfl(si[NA_K], NA_LANE, kWave);
+  if (lane == NA_LANE) { gi[NA_K] = 0; si[NA_K] = 0; }
+  long long lg = 0, ls = 0;
+  long long pg[B], ps[B];
+#pragma unroll
+  for (int k = 0; k < B; ++k) { lg += gi[k]; ls += si[k]; pg[k] = lg; ps[k] = ls; }
+  long long xg = lg, xs = ls;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long ag = __shfl_up(xg, o, kWave), as = __shfl_up(xs, o, kWave);
+    if (lane >= o) { xg += ag; xs += as; }
+  }
+  const long long tg_i = __shfl(xg, 63, kWave) + ng_i, ts_i = __shfl(xs, 63, kWave) + ns_i;
+  const long long eg = xg - lg, es = xs - ls;
+  const double ng = (double)ng_i * ig, ns = (double)ns_i * is;
+  const double tg = (double)tg_i * ig, ts = (double)ts_i * is;
+  double fbg = -INFINITY;
+  int fbc = 0x7fffffff;
+  double fGL = 0, fSL = 0;
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const int tt = lane * B + k;
+    if (tt < m && tt < NBT - 1) {
+      const double sgd = (double)(eg + pg[k]) * ig, ssum = (double)(es + ps[k]) * is;
+      const double gA = split_gain(sgd, ssum, tg, ts, p);
+      const double gB = (ns > 0.0) ? split_gain(sgd + ng, ssum + ns, tg, ts, p) : -INFINITY;
+      if (gA > -INFINITY && (gA > fbg || (gA == fbg && 2 * tt < fbc))) { fbg = gA; fbc = 2 * tt; fGL = sgd; fSL = ssum; }
+      if (gB > -INFINITY && (gB > fbg || (gB == fbg && 2 * tt + 1 < fbc))) {
+        fbg = gB; fbc = 2 * tt + 1; fGL = sgd + ng; fSL = ssum + ns;
+      }
+    }
+  }
+  double bg = fbg;
+  int bc = fbc;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(bg, o, kWave);
+    const int oc = __shfl_xor(bc, o, kWave);
+    if (og > bg || (og == bg && oc < bc)) { bg = og; bc = oc; }
+  }
+  if (bc != 0x7fffffff) {
+    const unsigned long long own = __ballot(fbc == bc);
+    const int src = __ffsll((long long)own) - 1;
+    const double GL = __shfl(fGL, src, kWave), SL = __shfl(fSL, src, kWave);
+    const long long key = ((long long)f << 32) | (unsigned)bc;
+    if (bg > best.gain || (bg == best.gain && key < best.key)) { best.gain = bg; best.key = key; best.GL = GL; best.SL = SL; }
+  }
+}
+
+__device__ __forceinline__ NodeSplit direct_node_split(const DirectBest& b, long long tgq, long long tsq, double ig,
+                                                       double is) {
+  NodeSplit sp;
+  sp.G = (double)tgq * ig; sp.H = (double)tsq * is; sp.W = sp.H;
+  sp.pad = 0;
+  if (b.key != 0x7fffffffffffffffLL) {
+    sp.gain = b.gain; sp.GL = b.GL; sp.HL = b.SL; sp.WL = b.SL;
+    sp.feat = (int)(b.key >> 32); const int code = (int)(b.key & 0xffffffff);
+    sp.bin = code >> 1; sp.na_left = code & 1;
+  } else {
+    sp.gain = -INFINITY; sp.GL = sp.HL = sp.WL = 0.0; sp.feat = -1; sp.bin = 0; sp.na_left = 0;
+  }
+  return sp;
+}
+
+// per-row quantised statistics, the same dither as every histogram path
+// (gi: index of the row's g / s2 - its segment position when part_scatter
+// keeps them in segment order, else the row id)
+__device__ __forceinline__ void direct_row_q(int r, int gi, int64_t rb, uint32_t salt, const float* __restrict__ g,
+                                             const float* __restrict__ s2, float sg, float ss, long long& gq,
+                                             long long& sq) {
+  const uint32_t hsh = row_hash(rb + r, salt);
+  const float d1 = (hsh & 0xFFFF) * (1.0f / 65536.0f), d2 = (hsh >> 16) * (1.0f / 65536.0f);
+  const float sv = s2 ? s2[gi] : 1.0f;
+  gq = (long long)(int)floorf(fmaf(g[gi], sg, d1));
+  sq = (long long)(uint32_t)floorf(fmaf(sv, ss, d2));
+}
+
+// one row's atomics for features flist[0, nb) of the batch: the code bytes of
+// DIRECT_FB features are loaded together (independent loads in flight) before
+// their atomics - a load -> atomic chain per feature left each node's rows
+// waiting on nb serial HBM round trips.  c0: codes of the first chunk,
+// already loaded by the caller (issued before the gradient loads resolve).
+// Eligible-feature codes kept for the partition (nodes of few eligible
+// features, e.g. DRF mtries): the direct pass already loads every row's codes
+// of the node's eligible features, so it also stores them in segment order
+// (codes[j * stride + q], q = index in the node's feature list) and the index
+// of the chosen feature per node (nodeq); part_count / part_scatter then read
+// one byte at the row's segment position instead of gathering a byte from
+// the 10M-row feature column at a random row.
+struct ECodes {
+  uint8_t* codes;   // nullptr = off; the host enables it only when the node's features fit one batch
+  int stride;       // 8 or 16 bytes per row
+  int* nodeq;
+};
+
+template <typename FL>
+__device__ __forceinline__ int direct_feat_pos(const FL* flist, int nfl, long long key) {
+  if (key == 0x7fffffffffffffffLL) return -1;
+  const int f = (int)(key >> 32);
+  for (int q = 0; q < nfl; ++q)
+    if ((int)flist[q] == f) return q;
+  return -1;
+}
+
+constexpr int DIRECT_FB = 8;
+template <int NBT>
+__device__ __forceinline__ void direct_chunk_atomics(int q0, int nb, bool packed, int per_f, long long* hist,
+                                                     unsigned long long pk, long long gq, long long sq,
+                                                     const uint32_t* c) {
+  if (packed) {
+#pragma unroll
+    for (int u = 0; u < DIRECT_FB; ++u)
+      if (q0 + u < nb) atomicAdd(reinterpret_cast<unsigned long long*>(hist + (q0 + u) * NBT + c[u]), pk);
+  } else {
+#pragma unroll
+    for (int u = 0; u < DIRECT_FB; ++u) {
+      if (q0 + u < nb) {
+        unsigned long long* hb = reinterpret_cast<unsigned long long*>(hist + (q0 + u) * per_f + c[u]);
+        atomicAdd(hb, (unsigned long long)gq);
+        atomicAdd(hb + NBT, (unsigned long long)sq);
+      }
+    }
+  }
+}
+
+// erow (ECodes, nb <= 16): the row's codes of the node's features stored as
+// ONE 8- or 16-byte vector (estride) at its segment position
+template <int NBT, typename FL>
+__device__ __forceinline__ void direct_row_atomics(const uint8_t* __restrict__ row, const FL* flist, int nb,
+                                                   bool packed, int per_f, long long* hist, long long gq, long long sq,
+                                                   const uint32_t* c0, uint8_t* erow, int estride) {
+  const bool live = gq != 0 || sq != 0;
+  if (!live && erow == nullptr) return;
+  const unsigned long long pk = ((unsigned long long)(uint32_t)(int)gq << 32) | (unsigned long long)sq;
+  uint32_t c1[DIRECT_FB];
+#pragma unroll
+  for (int u = 0; u < DIRECT_FB; ++u) c1[u] = (DIRECT_FB + u < nb) ? row[flist[DIRECT_FB + u]] : 0u;
+  if (erow) {
+    const uint32_t w0 = c0[0] | (c0[1] << 8) | (c0[2] << 16) | (c0[3] << 24);
+    const uint32_t w1 = c0[4] | (c0[5] << 8) | (c0[6] << 16) | (c0[7] << 24);
+    if (estride == 16) {
+      const uint32_t w2 = c1[0] | (c1[1] << 8) | (c1[2] << 16) | (c1[3] << 24);
+      const uint32_t w3 = c1[4] | (c1[5] << 8) | (c1[6] << 16) | (c1[7] << 24);
+      *reinterpret_cast<uint4*>(erow) = make_uint4(w0, w1, w2, w3);
+    } else {
+      *reinterpret_cast<uint2*>(erow) = make_uint2(w0, w1);
+    }
+  }
+  if (!live) return;
+  direct_chunk_atomics<NBT>(0, nb, packed, per_f, hist, pk, gq, sq, c0);
+  if (nb > DIRECT_FB) direct_chunk_atomics<NBT>(DIRECT_FB, nb, packed, per_f, hist, pk, gq, sq, c1);
+  uint32_t c[DIRECT_FB];
+  for (int q0 = 2 * DIRECT_FB; q0 < nb; q0 += DIRECT_FB) {
+#pragma unroll
+    for (int u = 0; u < DIRECT_FB; ++u) c[u] = (q0 + u < nb) ? row[flist[q0 + u]] : 0u;
+    direct_chunk_atomics<NBT>(q0, nb, packed, per_f, hist, pk, gq, sq, c);
+  }
+}
+
+template <int NBT>
+__global__ __launch_bounds__(256) void seg_direct_kernel(
+    const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
+    const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
+    const int* __restrict__ ctl, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
+    const double* __restrict__ qscale, uint32_t salt, SplitParams p, int batch, NodeSplit* __restrict__ out,
+    int gpos, ECodes ec) {
+  extern __shared__ __attribute__((aligned(16))) long long hist[];   // [batch][2][NBT] (packed: [batch][NBT])
+  __shared__ int flist[1024];
+  __shared__ uint32_t hsh_s[1024];
+  __shared__ int nfl_s;
+  __shared__ long long tot_s[2][4];
+  __shared__ double wb_gain[4], wb_GL[4], wb_SL[4];
+  __shared__ long long wb_key[4];
+  const int node = blockIdx.x;
+  if (node >= ctl[CTL_N]) return;
+  const int F = p.F;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int lo = seg_start[node], cnt = seg_cnt[node];
+  // eligible features of this node (wave 0), in ascending order; the mtries
+  // rank of feature f counts the features whose hash is smaller (ties: lower
+  // index), as split_find - with the F hashes computed once into LDS
+  if (wid == 0) {
+    const uint32_t key = (uint32_t)p.tree_index * 131u + (uint32_t)p.depth;
+    const bool sampled = p.mtries > 0 || p.col_rate < 1.0f;
+    if (sampled)
+      for (int f = lane; f < F; f += 64) hsh_s[f] = hash4(p.seed, key, (uint32_t)node, (uint32_t)f);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    int c = 0;
+    for (int f0 = 0; f0 < F; f0 += 64) {
+      const int f = f0 + lane;
+      bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]);
+      if (ok && sampled) {
+        const uint32_t hf = hsh_s[f];
+        if (p.mtries > 0) {
+          int rank = 0;
+          for (int j = 0; j < F; ++j) {
+            const uint32_t hj = hsh_s[j];
+            rank += (hj < hf) || (hj == hf && j < f);
+          }
+          ok = rank < p.mtries;
+        } else {
+          ok = u01(hf) < p.col_rate;
+        }
+      }
+      const unsigned long long bal = __ballot(ok);
+      const int pos = c + __popcll(bal & ((1ull << lane) - 1ull));
+      if (ok && pos < 1024) flist[pos] = f;
+      c += __popcll(bal);
+    }
+    if (lane == 0) nfl_s = c < 1024 ? c : 1024;
+  }
+  if (t < 8) tot_s[t >> 2][t & 3] = 0;
+  __syncthreads();
+  const int nfl = nfl_s;
+  const float sg = (float)qscale[0], ss = (float)qscale[1];
+  const double ig = qscale[2], is = qscale[3];
+  const int64_t rb = (int64_t)qscale[7];
+  const bool packed = cnt < DIRECT_PACK_ROWS;                 // block-uniform
+  const int per_f = packed ? NBT : 2 * NBT;                   // int64 entries per feature
+  const int bat = packed ? 2 * batch : batch;                 // same LDS bytes
+  DirectBest best;
+  best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  long long tg_row = 0, ts_row = 0;   // node totals (G_q, S_q), accumulated in the first batch
+  for (int b0 = 0; b0 < nfl; b0 += bat) {
+    const int nb = min(bat, nfl - b0);
+    for (int j = t; j < nb * per_f; j += blockDim.x) hist[j] = 0;
+    __syncthreads();
+    for (int j = lo + t; j < lo + cnt; j += blockDim.x) {
+      const int r = idx ? idx[j] : j;
+      const uint8_t* row = codes_rm + (int64_t)r * fp;
+      uint32_t c0[DIRECT_FB];
+#pragma unroll
+      for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
+      long long gq, sq;
+      direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
+      if (b0 == 0) { tg_row += gq; ts_row += sq; }
+      direct_row_atomics<NBT>(row, flist + b0, nb, packed, per_f, hist, gq, sq, c0,
+                              ec.codes ? ec.codes + (int64_t)j * ec.stride : nullptr, ec.stride);
+    }
+    __syncthreads();
+    if (b0 == 0) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        tg_row += __shfl_xor(tg_row, o, kWave);
+        ts_row += __shfl_xor(ts_row, o, kWave);
+      }
+      if (lane == 0) { tot_s[0][wid] = tg_row; tot_s[1][wid] = ts_row; }
+    }
+    // one wave per feature of the batch
+    for (int q = wid; q < nb; q += DIRECT_WAVES) {
+      const int f = flist[b0 + q];
+      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, f, nvb[f], ig, is, p, lane, best);
+      else direct_scan_feature<NBT, false>(hist + q * per_f, f, nvb[f], ig, is, p, lane, best);
+    }
+    __syncthreads();
+  }
+  if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
+  __syncthreads();
+  if (t == 0) {
+    DirectBest b;
+    b.gain = -INFINITY; b.GL = b.SL = 0.0; b.key = 0x7fffffffffffffffLL;
+    for (int w = 0; w < DIRECT_WAVES; ++w)
+      if (wb_key[w] != 0x7fffffffffffffffLL && (wb_gain[w] > b.gain || (wb_gain[w] == b.gain && wb_key[w] < b.key))) {
+        b.gain = wb_gain[w]; b.key = wb_key[w]; b.GL = wb_GL[w]; b.SL = wb_SL[w];
+      }
+    const long long tgq = tot_s[0][0] + tot_s[0][1] + tot_s[0][2] + tot_s[0][3];
+    const long long tsq = tot_s[1][0] + tot_s[1][1] + tot_s[1][2] + tot_s[1][3];
+    out[node] = direct_node_split(b, tgq, tsq, ig, is);
+    if (ec.nodeq) ec.nodeq[node] = direct_feat_pos(flist, nfl, b.key);
+  }
+}
+
+__device__ __forceinline__ int chunk_node_wave(const int* __restrict__ first, int n, int c, int lane) {
+  int lo = 0, hi = n - 1;   // answer: the largest i with first[i] <= c (first[0] = 0 <= c)
+  while (hi > lo) {
+    const int span = hi - lo + 1;
+    const int st = (span + 63) >> 6;
+    const int i = lo + lane * st;
+    const bool ok = i <= hi && first[i] <= c;
+    const unsigned long long b = __ballot(ok);
+    const int k = 63 - __clzll((long long)b);   // last probe at or below c (lane 0 always is)
+    lo = lo + k * st;
+    hi = min(hi, lo + st - 1);
+    if (st == 1) break;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Eligible features of a node (mtries / column sample / tree mask), ascending,
+// computed by ONE wave into flist; returns the count (wave-uniform).  F <=
+// 256: per-lane hashes in registers ranked with scalar lane reads; wider: the
+// hashes go through LDS (hsh_s, F entries).
+template <typename FL>
+__device__ __forceinline__ int direct_eligible(int node, const SplitParams& p, const uint8_t* __restrict__ tree_fmask,
+                                              FL* flist, uint32_t* hsh_s, int lane) {
+  const int F = p.F;
+  const uint32_t key = (uint32_t)p.tree_index * 131u + (uint32_t)p.depth;
+  const bool sampled = p.mtries > 0 || p.col_rate < 1.0f;
+  int nfl = 0;
+  if (F <= 256) {
+    uint32_t hv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int f = lane + 64 * k;
+      hv[k] = (sampled && f < F) ? hash4(p.seed, key, (uint32_t)node, (uint32_t)f) : 0xffffffffu;
+    }
+    int rank[4] = {0, 0, 0, 0};
+    if (p.mtries > 0) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        if (64 * kk >= F) break;
+        const int jn = min(64, F - 64 * kk);
+        for (int jj = 0; jj < jn; ++jj) {
+          const uint32_t hj = (uint32_t)__builtin_amdgcn_readlane((int)hv[kk], jj);
+          const int j = 64 * kk + jj;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) rank[k] += (hj < hv[k]) || (hj == hv[k] && j < lane + 64 * k);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int f = lane + 64 * k;
+      bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]);
+      if (ok && sampled) ok = p.mtries > 0 ? rank[k] < p.mtries : u01(hv[k]) < p.col_rate;
+      const unsigned long long bal = __ballot(ok);
+      if (ok) flist[nfl + __popcll(bal & ((1ull << lane) - 1ull))] = (FL)f;
+      nfl += __popcll(bal);
+    }
+    return nfl;
+  }
+  if (sampled)
+    for (int f = lane; f < F; f += 64) hsh_s[f] = hash4(p.seed, key, (uint32_t)node, (uint32_t)f);
+  wave_lds_sync();
+  for (int f0 = 0; f0 < F; f0 += 64) {
+    const int f = f0 + lane;
+    bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]);
+    if (ok && sampled) {
+      const uint32_t hf = hsh_s[f];
+      if (p.mtries > 0) {
+        int rank = 0;
+        for (int j = 0; j < F; ++j) {
+          const uint32_t hj = hsh_s[j];
+          rank += (hj < hf) || (hj == hf && j < f);
+        }
+        ok = rank < p.mtries;
+      } else {
+        ok = u01(hf) < p.col_rate;
+      }
+    }
+    const unsigned long long bal = __ballot(ok);
+    const int pos = nfl + __popcll(bal & ((1ull << lane) - 1ull));
+    if (ok && pos < 1024) flist[pos] = (FL)f;
+    nfl += __popcll(bal);
+  }
+  return nfl < 1024 ? nfl : 1024;
+}
+
+// Direct levels whose nodes still hold thousands of rows (the first direct
+// levels): one workgroup per PC_ROWS row chunk, not per node, so a large node
+// is spread over many workgroups instead of being the kernel's tail.  Each
+// chunk (<= 4096 rows: packed 64-bit atomics are always exact) builds the
+// node's eligible features in LDS; a single-chunk node scans them at once,
+// otherwise the chunk stores its packed histogram and totals in a slab and
+// the node's last chunk to arrive (agent-scope release / ticket / acquire)
+// sums the slabs exactly into G and S planes and scans.
+constexpr int DIRECT_CHUNK_LDS = 64 * 1024;   // two-plane histograms of every eligible feature
+__global__ __launch_bounds__(256) void direct_empty_kernel(const int* __restrict__ seg_cnt,
+                                                           const int* __restrict__ ctl, NodeSplit* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ctl[CTL_N] || seg_cnt[i] != 0) return;
+  DirectBest b;
+  b.gain = -INFINITY; b.GL = b.SL = 0.0; b.key = 0x7fffffffffffffffLL;
+  out[i] = direct_node_split(b, 0, 0, 0.0, 0.0);
+}
+
+template <int NBT>
+__global__ __launch_bounds__(256) void seg_direct_chunk_kernel(
+    const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
+    const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
+    const int* __restrict__ pc_first, const int* __restrict__ ctl, const int* __restrict__ nvb,
+    const uint8_t* __restrict__ tree_fmask, const double* __restrict__ qscale, uint32_t salt, SplitParams p,
+    int nfl_max, unsigned long long* __restrict__ slab, long long* __restrict__ tot_slab, int* __restrict__ ticket,
+    NodeSplit* __restrict__ out, int gpos, ECodes ec) {
+  extern __shared__ __attribute__((aligned(16))) long long hist[];   // packed [nfl][NBT]; reduce: [nfl][2][NBT]
+  __shared__ int flist[1024];
+  __shared__ uint32_t hsh_s[1024];
+  __shared__ int node_s, nfl_s, last_s;
+  __shared__ long long tot_s[2][4];
+  __shared__ double wb_gain[4], wb_GL[4], wb_SL[4];
+  __shared__ long long wb_key[4];
+  const int n = ctl[CTL_N];
+  const int c = blockIdx.x;
+  if (c >= pc_first[n]) return;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  if (wid == 0) {
+    const int node = chunk_node_wave(pc_first, n, c, lane);
+    const int nfl = direct_eligible(node, p, tree_fmask, flist, hsh_s, lane);
+    if (lane == 0) { node_s = node; nfl_s = min(nfl, nfl_max); }
+  }
+  __syncthreads();
+  const int node = node_s, nfl = nfl_s;
+  const int c0 = pc_first[node], nch = pc_first[node + 1] - c0;
+  const int start = seg_start[node];
+  const int lo = start + (c - c0) * PC_ROWS;
+  const int hi = min(lo + PC_ROWS, start + seg_cnt[node]);
+  const float sg = (float)qscale[0], ss = (float)qscale[1];
+  const double ig = qscale[2], is = qscale[3];
+  const int64_t rb = (int64_t)qscale[7];
+  for (int j = t; j < nfl * NBT; j += blockDim.x) hist[j] = 0;
+  __syncthreads();
+  long long tg_row = 0, ts_row = 0;
+  for (int j = lo + t; j < hi; j += blockDim.x) {
+    const int r = idx ? idx[j] : j;
+    const uint8_t* row = codes_rm + (int64_t)r * fp;
+    uint32_t cc[DIRECT_FB];
+#pragma unroll
+    for (int u = 0; u < DIRECT_FB; ++u) cc[u] = (u < nfl) ? row[flist[u]] : 0u;
+    long long gq, sq;
+    direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
+    tg_row += gq; ts_row += sq;
+    direct_row_atomics<NBT>(row, flist, nfl, true, NBT, hist, gq, sq, cc,
+                            ec.codes ? ec.codes + (int64_t)j * ec.stride : nullptr, ec.stride);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    tg_row += __shfl_xor(tg_row, o, kWave);
+    ts_row += __shfl_xor(ts_row, o, kWave);
+  }
+  if (lane == 0) { tot_s[0][wid] = tg_row; tot_s[1][wid] = ts_row; }
+  __syncthreads();
+  long long tgq = tot_s[0][0] + tot_s[0][1] + tot_s[0][2] + tot_s[0][3];
+  long long tsq = tot_s[1][0] + tot_s[1][1] + tot_s[1][2] + tot_s[1][3];
+  bool packed = true;
+  if (nch > 1) {
+    // publish this chunk, then the node's last chunk reduces every chunk
+    unsigned long long* my = slab + (int64_t)c * nfl_max * NBT;
+    for (int j = t; j < nfl * NBT; j += blockDim.x) my[j] = (unsigned long long)hist[j];
+    if (t == 0) { tot_slab[2 * c] = tgq; tot_slab[2 * c + 1] = tsq; }
+    __syncthreads();
+    if (t == 0) {
+      __atomic_thread_fence(__ATOMIC_RELEASE);
+      const int prev = __hip_atomic_fetch_add(ticket + node, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      last_s = prev == nch - 1;
+      if (last_s) ticket[node] = 0;   // ready for the next level
+    }
+    __syncthreads();
+    if (!last_s) return;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    packed = false;
+    for (int e = t; e < nfl * NBT; e += blockDim.x) {
+      long long G = 0, S = 0;
+      for (int k = 0; k < nch; ++k) {
+        const unsigned long long v = __hip_atomic_load(slab + (int64_t)(c0 + k) * nfl_max * NBT + e, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        G += (long long)(int)(uint32_t)(v >> 32);
+        S += (long long)(uint32_t)v;
+      }
+      const int q = e / NBT, b = e - q * NBT;
+      hist[q * 2 * NBT + b] = G;
+      hist[q * 2 * NBT + NBT + b] = S;
+    }
+    if (t == 0) {
+      long long a = 0, b = 0;
+      for (int k = 0; k < nch; ++k) {
+        a += __hip_atomic_load(tot_slab + 2 * (c0 + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        b += __hip_atomic_load(tot_slab + 2 * (c0 + k) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      tot_s[0][0] = a; tot_s[1][0] = b;
+    }
+    __syncthreads();
+    tgq = tot_s[0][0]; tsq = tot_s[1][0];
+  }
+  DirectBest best;
+  best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  for (int q = wid; q < nfl; q += 4) {
+    const int f = flist[q];
+    if (packed) direct_scan_feature<NBT, true>(hist + q * NBT, f, nvb[f], ig, is, p, lane, best);
+    else direct_scan_feature<NBT, false>(hist + q * 2 * NBT, f, nvb[f], ig, is, p, lane, best);
+  }
+  if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
+  __syncthreads();
+  if (t == 0) {
+    DirectBest b;
+    b.gain = -INFINITY; b.GL = b.SL = 0.0; b.key = 0x7fffffffffffffffLL;
+    for (int w = 0; w < 4; ++w)
+      if (wb_key[w] != 0x7fffffffffffffffLL && (wb_gain[w] > b.gain || (wb_gain[w] == b.gain && wb_key[w] < b.key))) {
+        b.gain = wb_gain[w]; b.key = wb_key[w]; b.GL = wb_GL[w]; b.SL = wb_SL[w];
+      }
+    out[node] = direct_node_split(b, tgq, tsq, ig, is);
+    if (ec.nodeq) ec.nodeq[node] = direct_feat_pos(flist, nfl, b.key);
+  }
+}
+
+// Deepest levels (nodes of a few hundred rows): one WAVE per node, four
+// nodes per 256-thread workgroup, every wave on its own LDS area - no
+// workgroup barriers, so a node's short latency chain (segment -> rows ->
+// codes -> atomics -> scan) overlaps with three others per workgroup and
+// many more per CU.  Eligible features from per-lane hashes in registers
+// (F <= 256) ranked with scalar lane reads (no LDS round trips).
+constexpr int DIRECT_WAVE_F = 256;
+constexpr int DIRECT_WAVE_LDS = 8 * 1024;   // max histogram bytes per wave
+
+template <int NBT>
+__global__ __launch_bounds__(256) void seg_direct_wave_kernel(
+    const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
+    const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
+    const int* __restrict__ ctl, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
+    const double* __restrict__ qscale, uint32_t salt, SplitParams p, int batch, NodeSplit* __restrict__ out,
+    int gpos, ECodes ec) {
+  extern __shared__ __attribute__((aligned(16))) long long hist_all[];   // [4][batch * 2 * NBT]
+  __shared__ short flist_all[4][DIRECT_WAVE_F];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int node = blockIdx.x * 4 + wid;
+  if (node >= ctl[CTL_N]) return;   // whole wave: no workgroup barrier below
+  long long* hist = hist_all + wid * batch * 2 * NBT;
+  short* flist = flist_all[wid];
+  const int F = p.F;
+  const int lo = seg_start[node], cnt = seg_cnt[node];
+  // eligible features, ascending
+  const uint32_t key = (uint32_t)p.tree_index * 131u + (uint32_t)p.depth;
+  const bool sampled = p.mtries > 0 || p.col_rate < 1.0f;
+  uint32_t hv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int f = lane + 64 * k;
+    hv[k] = (sampled && f < F) ? hash4(p.seed, key, (uint32_t)node, (uint32_t)f) : 0xffffffffu;
+  }
+  int rank[4] = {0, 0, 0, 0};
+  if (p.mtries > 0) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (64 * kk >= F) break;
+      const int jn = min(64, F - 64 * kk);
+      for (int jj = 0; jj < jn; ++jj) {
+        const uint32_t hj = (uint32_t)__builtin_amdgcn_readlane((int)hv[kk], jj);
+        const int j = 64 * kk + jj;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rank[k] += (hj < hv[k]) || (hj == hv[k] && j < lane + 64 * k);
+      }
+    }
+  }
+  int nfl = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int f = lane + 64 * k;
+    bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]);
+    if (ok && sampled) ok = p.mtries > 0 ? rank[k] < p.mtries : u01(hv[k]) < p.col_rate;
+    const unsigned long long bal = __ballot(ok);
+    if (ok) flist[nfl + __popcll(bal & ((1ull << lane) - 1ull))] = (short)f;
+    nfl += __popcll(bal);
+  }
+  const float sg = (float)qscale[0], ss = (float)qscale[1];
+  const double ig = qscale[2], is = qscale[3];
+  const int64_t rb = (int64_t)qscale[7];
+  const bool packed = cnt < DIRECT_PACK_ROWS;
+  const int per_f = packed ? NBT : 2 * NBT;
+  const int bat = packed ? 2 * batch : batch;
+  DirectBest best;
+  best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  long long tg_row = 0, ts_row = 0;
+  wave_lds_sync();
+  for (int b0 = 0; b0 < max(nfl, 1); b0 += bat) {
+    const int nb = min(bat, nfl - b0);
+    for (int j = lane; j < nb * per_f; j += 64) hist[j] = 0;
+    wave_lds_sync();
+    for (int j = lo + lane; j < lo + cnt; j += 64) {
+      const int r = idx ? idx[j] : j;
+      const uint8_t* row = codes_rm + (int64_t)r * fp;
+      uint32_t c0[DIRECT_FB];
+#pragma unroll
+      for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
+      long long gq, sq;
+      direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
+      if (b0 == 0) { tg_row += gq; ts_row += sq; }
+      if (nb <= 0) continue;
+      direct_row_atomics<NBT>(row, flist + b0, nb, packed, per_f, hist, gq, sq, c0,
+                              ec.codes ? ec.codes + (int64_t)j * ec.stride : nullptr, ec.stride);
+    }
+    wave_lds_sync();
+    for (int q = 0; q < nb; ++q) {
+      const int f = flist[b0 + q];
+      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, f, nvb[f], ig, is, p, lane, best);
+      else direct_scan_feature<NBT, false>(hist + q * per_f, f, nvb[f], ig, is, p, lane, best);
+    }
+    wave_lds_sync();
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    tg_row += __shfl_xor(tg_row, o, kWave);
+    ts_row += __shfl_xor(ts_row, o, kWave);
+  }
+  if (lane == 0) {
+    out[node] = direct_node_split(best, tg_row, ts_row, ig, is);
+    if (ec.nodeq) ec.nodeq[node] = direct_feat_pos(flist, nfl, best.key);
+  }
+}
+
 __global__ __launch_bounds__(256) void zero_slots_kernel(long long* __restrict__ built,
                                                          const int* __restrict__ ctl_next, int per_slot) {
   const int64_t m = (int64_t)ctl_next[CTL_SLOTS] * per_slot;
@@ -2844,7 +3632,8 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
     const int* __restrict__ pc_first, const int* __restrict__ pc_off, const int* __restrict__ node_nl,
     const int* __restrict__ ctl, const PartInfo* __restrict__ part, int nbt, const float* __restrict__ g,
     const float* __restrict__ h, const float* __restrict__ w, const double* __restrict__ qs, int cap,
-    unsigned long long* __restrict__ leaf_acc) {
+    unsigned long long* __restrict__ leaf_acc, const float* __restrict__ gin, const float* __restrict__ sin,
+    float* __restrict__ gout, float* __restrict__ sout) {
   __shared__ int wl[4];
   __shared__ long long red[4];
   const int n = ctl[CTL_N];
@@ -2891,6 +3680,10 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
         const int pos = goes_left ? base_l + my_l : nl + base_r + (my_v - my_l);
         idx_out[start + pos] = r;
         if (write_nid) nid[r] = pi.child + dir;
+        if (gout) {   // the (g, s2) the next level reads, moved with the row into segment order
+          gout[start + pos] = gin[j];
+          if (sout) sout[start + pos] = sin[j];
+        }
       }
       base_l += tot_l;
       base_r += tot_v - tot_l;
@@ -2924,6 +3717,145 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
   }
 }
 
+// Wave-granular partition for levels with thousands of nodes: one WAVE per
+// PC_ROWS chunk (four chunks per workgroup) and the chunk's node found by a
+// 64-ary search (three rounds of 64 parallel probes instead of ~18 dependent
+// binary-search loads), so a level of 10^5 single-chunk nodes launches 4x
+// fewer workgroups whose latency chains overlap.  part_count_wave also stores
+// each row's direction byte (dirb, indexed like idx) for every node with a
+// split, so part_scatter_wave moves rows without re-gathering split codes.
+// Same counts, offsets and row order as part_count / part_scatter.
+
+__global__ __launch_bounds__(256) void part_count_wave_kernel(const uint8_t* __restrict__ codes, int64_t npad,
+                                                              const int* __restrict__ idx,
+                                                              const int* __restrict__ seg_start,
+                                                              const int* __restrict__ seg_cnt,
+                                                              const int* __restrict__ pc_first,
+                                                              const int* __restrict__ ctl,
+                                                              const PartInfo* __restrict__ part, int nbt,
+                                                              int* __restrict__ pc_left, int8_t* __restrict__ dirb,
+                                                              const uint8_t* __restrict__ ecodes, int ecs,
+                                                              const int* __restrict__ nodeq) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int n = ctl[CTL_N];
+  if (c >= pc_first[n]) return;
+  const int node = chunk_node_wave(pc_first, n, c, lane);
+  const PartInfo pi = part[node];
+  int cnt = 0;
+  if (pi.child >= 0) {
+    const int lo = seg_start[node] + (c - pc_first[node]) * PC_ROWS;
+    const int hi = min(lo + PC_ROWS, seg_start[node] + seg_cnt[node]);
+    const int eq = ecodes ? nodeq[node] : 0;
+    for (int j = lo + lane; j < hi; j += 64) {
+      int d;
+      if (ecodes) {
+        const int b = ecodes[(int64_t)j * ecs + eq];
+        d = (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
+      } else {
+        d = split_dir(codes, npad, pi, nbt, idx ? idx[j] : j);
+      }
+      if (dirb) dirb[j] = (int8_t)d;
+      cnt += 1 - d;
+    }
+    if (pi.leaf_children) cnt = 0;   // only inner splits count (as part_count)
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, kWave);
+  if (lane == 0) pc_left[c] = cnt;
+}
+
+__global__ __launch_bounds__(256) void part_scatter_wave_kernel(
+    const uint8_t* __restrict__ codes, int64_t npad, const int* __restrict__ idx, int* __restrict__ idx_out,
+    int* __restrict__ nid, int write_nid, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
+    const int* __restrict__ pc_first, const int* __restrict__ pc_off, const int* __restrict__ node_nl,
+    const int* __restrict__ ctl, const PartInfo* __restrict__ part, int nbt, const float* __restrict__ g,
+    const float* __restrict__ h, const float* __restrict__ w, const double* __restrict__ qs, int cap,
+    unsigned long long* __restrict__ leaf_acc, const int8_t* __restrict__ dirb, const float* __restrict__ gin,
+    const float* __restrict__ sin, float* __restrict__ gout, float* __restrict__ sout,
+    const uint8_t* __restrict__ ecodes, int ecs, const int* __restrict__ nodeq) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int n = ctl[CTL_N];
+  if (c >= pc_first[n]) return;
+  const int node = chunk_node_wave(pc_first, n, c, lane);
+  const PartInfo pi = part[node];
+  const int start = seg_start[node];
+  const int lo = start + (c - pc_first[node]) * PC_ROWS;
+  const int hi = min(lo + PC_ROWS, start + seg_cnt[node]);
+  const bool inner = pi.child >= 0 && !pi.leaf_children;
+  long long sg[2] = {0, 0}, sh[2] = {0, 0}, sw[2] = {0, 0};
+  const float lg = leaf_acc ? (float)qs[4] : 0.f, lh = leaf_acc ? (float)qs[5] : 0.f,
+              lw = leaf_acc ? (float)qs[6] : 0.f;
+  int base_l = inner ? pc_off[c] : 0;
+  int base_r = inner ? (lo - start) - base_l : 0;
+  const int nl = inner ? node_nl[node] : 0;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int j0 = lo; j0 < hi; j0 += 64) {
+    const int j = j0 + lane;
+    const bool valid = j < hi;
+    int r = 0, dir = 0;
+    if (valid) {
+      r = idx ? idx[j] : j;
+      if (pi.child >= 0) {
+        if (dirb) {
+          dir = dirb[j];
+        } else if (ecodes) {
+          const int b = ecodes[(int64_t)j * ecs + nodeq[node]];
+          dir = (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
+        } else {
+          dir = split_dir(codes, npad, pi, nbt, r);
+        }
+      }
+    }
+    if (inner) {
+      const unsigned long long bl = __ballot(valid && dir == 0);
+      const unsigned long long bv = __ballot(valid);
+      if (valid) {
+        const int my_l = __popcll(bl & lt), my_v = __popcll(bv & lt);
+        const int pos = dir == 0 ? base_l + my_l : nl + base_r + (my_v - my_l);
+        idx_out[start + pos] = r;
+        if (write_nid) nid[r] = pi.child + dir;
+        if (gout) {
+          gout[start + pos] = gin[j];
+          if (sout) sout[start + pos] = sin[j];
+        }
+      }
+      base_l += __popcll(bl);
+      base_r += __popcll(bv) - __popcll(bl);
+    } else if (valid) {
+      const int leaf = (pi.child >= 0) ? pi.child_gid + dir : pi.gid;
+      nid[r] = ~leaf;
+      if (leaf_acc && leaf < cap) {
+        const float wv = w ? w[r] : 1.0f;
+        if (wv != 0.0f) {
+          sg[dir] += __float2int_rn(g[r] * lg);
+          sh[dir] += __float2int_rn(h[r] * lh);
+          sw[dir] += __float2int_rn(wv * lw);
+        }
+      }
+    }
+  }
+  if (!inner && leaf_acc) {
+    const int nleaf = (pi.child >= 0) ? 2 : 1;
+    for (int d = 0; d < nleaf; ++d) {
+      long long a = sg[d], b = sh[d], e = sw[d];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, kWave);
+        b += __shfl_xor(b, o, kWave);
+        e += __shfl_xor(e, o, kWave);
+      }
+      const int leaf = (pi.child >= 0) ? pi.child_gid + d : pi.gid;
+      if (lane == 0 && leaf < cap) {
+        if (a) atomicAdd(leaf_acc + 3 * leaf, (unsigned long long)a);
+        if (b) atomicAdd(leaf_acc + 3 * leaf + 1, (unsigned long long)b);
+        if (e) atomicAdd(leaf_acc + 3 * leaf + 2, (unsigned long long)e);
+      }
+    }
+  }
+}
+
 // --- C ABI of the segmented pipeline -----------------------------------------
 H2OMX_API int h2omx_pc_rows() { return PC_ROWS; }
 
@@ -2946,7 +3878,7 @@ H2OMX_API int h2omx_hist_build_seg(const uint8_t* codes_rm, int fp, const int* i
                                    const int* seg_start, const int* seg_cnt, const int* hc_first, const int* ctl,
                                    const int* nvb, const double* qscale, int salt, int F, int nbt, int fg,
                                    int n_groups, int hc_rows, int max_chunks, int threads,
-                                   unsigned long long* slab, hipStream_t stream) {
+                                   unsigned long long* slab, int gpos, hipStream_t stream) {
   if (fg > 256 || threads > 512 || threads % 64 || threads < fg || fp % 4 || (n_groups > 1 && fg % 4) ||
       hc_rows > ROWS_CAP)
     return kBadArg;
@@ -2955,7 +3887,8 @@ H2OMX_API int h2omx_hist_build_seg(const uint8_t* codes_rm, int fp, const int* i
   const int grid = ((max_chunks + 7) / 8) * 8 * n_groups;
 #define H2OMX_HBS(NB)                                                                                        \
   hipLaunchKernelGGL(hist_build_seg_kernel<NB>, dim3(grid), dim3(threads), lds, stream, codes_rm, fp, idx, g, s2, \
-                     seg_start, seg_cnt, hc_first, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, hc_rows, slab)
+                     seg_start, seg_cnt, hc_first, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, hc_rows, slab, \
+                     gpos)
   switch (nbt) {
     case 32: H2OMX_HBS(32); break;
     case 64: H2OMX_HBS(64); break;
@@ -2979,9 +3912,97 @@ H2OMX_API int h2omx_hist_reduce_seg(const unsigned long long* slab, const int* h
 
 H2OMX_API int h2omx_part_count(const uint8_t* codes, int64_t npad, const int* idx, const int* seg_start,
                                const int* seg_cnt, const int* pc_first, const int* ctl, const void* part, int nbt,
-                               int max_chunks, int* pc_left, hipStream_t stream) {
+                               int max_chunks, int* pc_left, int wave, int8_t* dirb, const uint8_t* ecodes,
+                               int ecs, const int* nodeq, hipStream_t stream) {
+  if (ecodes && !wave) return kBadArg;
+  if (wave) {
+    hipLaunchKernelGGL(part_count_wave_kernel, dim3((max_chunks + 3) / 4), dim3(256), 0, stream, codes, npad, idx,
+                       seg_start, seg_cnt, pc_first, ctl, reinterpret_cast<const PartInfo*>(part), nbt, pc_left, dirb,
+                       ecodes, ecs, nodeq);
+    return launch_status();
+  }
   hipLaunchKernelGGL(part_count_kernel, dim3(max_chunks), dim3(256), 0, stream, codes, npad, idx, seg_start, seg_cnt,
                      pc_first, ctl, reinterpret_cast<const PartInfo*>(part), nbt, pc_left);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, const float* g, const float* s2,
+                               const int* seg_start, const int* seg_cnt, const int* ctl, const int* nvb,
+                               const uint8_t* tree_fmask, const double* qscale, int salt, const void* params, int nbt,
+                               int max_nodes, int mode, const int* pc_first, int max_pc, unsigned long long* slab,
+                               long long* tot_slab, int* ticket, void* nsplit, int gpos, uint8_t* ecodes, int ecs,
+                               int* nodeq, hipStream_t stream) {
+  if (ecodes && ecs != 8 && ecs != 16) return kBadArg;
+  const ECodes ec{ecodes, ecs, nodeq};
+  // mode 0: one workgroup per node, 1: one wave per node (F <= 256),
+  // 2: one workgroup per PC_ROWS chunk (slab / tot_slab: max_pc x max_elig x
+  //    nbt and max_pc x 2 int64, ticket: max_nodes zeroed ints)
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  if (max_nodes < 1 || p.F > 1024 || p.F > fp || nbt < 2) return kBadArg;
+  NodeSplit* ns = reinterpret_cast<NodeSplit*>(nsplit);
+  // LDS sized to the features a node can have (mtries, else F): small
+  // allocations keep many node workgroups resident per CU
+  const int per_f_bytes = 2 * nbt * 8;
+  const int max_elig = p.mtries > 0 ? std::min(p.mtries, p.F) : p.F;
+  if (mode == 2) {
+    if (max_elig * per_f_bytes > DIRECT_CHUNK_LDS || !pc_first || !slab || !tot_slab || !ticket) return kBadArg;
+    hipLaunchKernelGGL(direct_empty_kernel, dim3((max_nodes + 255) / 256), dim3(256), 0, stream, seg_cnt, ctl, ns);
+    const size_t lds = (size_t)max_elig * per_f_bytes;
+#define H2OMX_SDC(NB)                                                                                            \
+  hipLaunchKernelGGL(seg_direct_chunk_kernel<NB>, dim3(max_pc), dim3(256), lds, stream, codes_rm, fp, idx, g, s2, \
+                     seg_start, seg_cnt, pc_first, ctl, nvb, tree_fmask, qscale, (uint32_t)salt, p, max_elig, slab, \
+                     tot_slab, ticket, ns, gpos, ec)
+    switch (nbt) {
+      case 32: H2OMX_SDC(32); break;
+      case 64: H2OMX_SDC(64); break;
+      case 128: H2OMX_SDC(128); break;
+      case 256: H2OMX_SDC(256); break;
+      default: return kBadArg;
+    }
+#undef H2OMX_SDC
+    return launch_status();
+  }
+  if (mode == 1 && p.F <= DIRECT_WAVE_F) {
+    const int batch = std::max(1, std::min(max_elig, DIRECT_WAVE_LDS / per_f_bytes));
+    const size_t lds = (size_t)4 * batch * per_f_bytes;
+#define H2OMX_SDW(NB)                                                                                              \
+  hipLaunchKernelGGL(seg_direct_wave_kernel<NB>, dim3((max_nodes + 3) / 4), dim3(256), lds, stream, codes_rm, fp, \
+                     idx, g, s2, seg_start, seg_cnt, ctl, nvb, tree_fmask, qscale, (uint32_t)salt, p, batch, ns, gpos, ec)
+    switch (nbt) {
+      case 32: H2OMX_SDW(32); break;
+      case 64: H2OMX_SDW(64); break;
+      case 128: H2OMX_SDW(128); break;
+      case 256: H2OMX_SDW(256); break;
+      default: return kBadArg;
+    }
+#undef H2OMX_SDW
+    return launch_status();
+  }
+  const int batch = std::max(1, std::min(max_elig, DIRECT_LDS_BYTES / per_f_bytes));
+  const size_t lds = (size_t)batch * per_f_bytes;
+#define H2OMX_SD(NB)                                                                                             \
+  hipLaunchKernelGGL(seg_direct_kernel<NB>, dim3(max_nodes), dim3(64 * DIRECT_WAVES), lds, stream, codes_rm, fp, \
+                     idx, g, s2,                                                                                 \
+                     seg_start, seg_cnt, ctl, nvb, tree_fmask, qscale, (uint32_t)salt, p, batch, ns, gpos, ec)
+  switch (nbt) {
+    case 32: H2OMX_SD(32); break;
+    case 64: H2OMX_SD(64); break;
+    case 128: H2OMX_SD(128); break;
+    case 256: H2OMX_SD(256); break;
+    default: return kBadArg;
+  }
+#undef H2OMX_SD
+  return launch_status();
+}
+
+// level_finalize from per-node splits already in nsplit (direct mode)
+H2OMX_API int h2omx_level_finalize_ns(const void* nsplit, const int* ctl, int* ctl_next, const void* params,
+                                      const float* edges, const int* nvb, int nbt, int max_next_nodes, void* part,
+                                      void* next_link, void* tree, int tree_capacity, int max_nodes, int* tiles,
+                                      hipStream_t stream) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  level_finalize_launch(reinterpret_cast<const NodeSplit*>(nsplit), ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes,
+                        part, next_link, tree, tree_capacity, max_nodes, tiles, stream);
   return launch_status();
 }
 
@@ -3034,9 +4055,20 @@ H2OMX_API int h2omx_part_scatter(const uint8_t* codes, int64_t npad, const int* 
                                  int write_nid, const int* seg_start, const int* seg_cnt, const int* pc_first,
                                  const int* pc_off, const int* node_nl, const int* ctl, const void* part, int nbt,
                                  const float* g, const float* h, const float* w, const double* qscale, int cap,
-                                 unsigned long long* leaf_acc, int max_chunks, hipStream_t stream) {
+                                 unsigned long long* leaf_acc, int max_chunks, int wave, const int8_t* dirb,
+                                 const float* gin, const float* sin, float* gout, float* sout,
+                                 const uint8_t* ecodes, int ecs, const int* nodeq, hipStream_t stream) {
+  if (ecodes && !wave) return kBadArg;
+  if (wave) {
+    hipLaunchKernelGGL(part_scatter_wave_kernel, dim3((max_chunks + 3) / 4), dim3(256), 0, stream, codes, npad, idx,
+                       idx_out, nid, write_nid, seg_start, seg_cnt, pc_first, pc_off, node_nl, ctl,
+                       reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, dirb, gin, sin,
+                       gout, sout, ecodes, ecs, nodeq);
+    return launch_status();
+  }
   hipLaunchKernelGGL(part_scatter_kernel, dim3(max_chunks), dim3(256), 0, stream, codes, npad, idx, idx_out, nid,
                      write_nid, seg_start, seg_cnt, pc_first, pc_off, node_nl, ctl,
-                     reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc);
+                     reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, gin, sin, gout,
+                     sout);
   return launch_status();
 }

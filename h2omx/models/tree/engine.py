@@ -85,6 +85,25 @@ class HipTreeBuilder:
     FUSE_MAX_DEPTH = 8
     FUSE_MAX_PREV = int(os.environ.get("H2OMX_FUSE_MAX_PREV", "4"))
     CLOSE_SINGLE_BLOCK = int(os.environ.get("H2OMX_CLOSE_SINGLE_BLOCK", "2048"))
+    # segmented engine, single rank: levels with >= this many potential nodes build each
+    # node's eligible-feature histograms directly and scan them in LDS (seg_direct_kernel:
+    # no parent histograms / subtraction); 0 = off.  Multi-rank runs keep the all-reduced
+    # subtraction path (direct histograms are rank-local)
+    DIRECT_MIN_NODES = int(os.environ.get("H2OMX_DIRECT_MIN_NODES", "1024"))
+    # direct levels whose average node holds fewer rows than this run one wave per node
+    # (seg_direct_wave_kernel, F <= 256) instead of one workgroup per node
+    DIRECT_WAVE_ROWS = int(os.environ.get("H2OMX_DIRECT_WAVE_ROWS", "256"))
+    # segmented partition: levels of at least this many potential nodes run one wave per row chunk
+    # (part_count_wave / part_scatter_wave: 64-ary chunk -> node search, stored row directions)
+    PART_WAVE_NODES = int(os.environ.get("H2OMX_PART_WAVE_NODES", "2048"))
+    # direct levels of large nodes: one workgroup per row chunk (False: one per node)
+    DIRECT_CHUNKED = True
+    # segmented engine: part_scatter moves each row's (g, s2) into segment order with it
+    PERMUTE_GS = True
+    # direct levels of <= 16 eligible features store them per row for the partition
+    ECODES = True
+    # levels of more than 8192 nodes finalise in count / scan / write tiles (False: one workgroup)
+    LF_MULTI_BLOCK = True
 
     def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
         if not bm.codes.is_cuda:
@@ -197,6 +216,19 @@ class HipTreeBuilder:
         self.pk32 = self.max_rows_per_wg >= 65536 and os.environ.get("H2OMX_PK32", "1") == "1"
 
     # -- buffers -----------------------------------------------------------
+    def _ticket_buf(self, numel: int) -> torch.Tensor:
+        """zeroed per-node arrival counters; kernels reset the entries they use"""
+        t = getattr(self, "_tickets", None)
+        if t is None or t.numel() < numel:
+            t = self._tickets = torch.zeros(max(numel, 1024), dtype=torch.int32, device=self.dev)
+        return t
+
+    def _lf_tiles(self, max_nodes: int) -> int:
+        """tile scratch of the multi-block level finalisation (0 = single workgroup)"""
+        if not self.LF_MULTI_BLOCK:
+            return 0
+        return self._buf("lf_tiles", max_nodes // 1024 + 2, torch.int32).data_ptr()
+
     def _buf(self, name: str, numel: int, dtype) -> torch.Tensor:
         b = self._bufs.get(name)
         if b is None or b.numel() < numel:
@@ -400,8 +432,9 @@ class HipTreeBuilder:
                                                    P(fbest), st), "split_find")
                     ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
                                                        P(bm.nvb), nbt, next_nodes, P(part), P(nl),
-                                                       P(self.tree_buf), self.capacity, P(nsplit), max_nodes, st),
-                              "level_finalize")
+                                                       P(self.tree_buf), self.capacity, P(nsplit), max_nodes,
+                                                       self._lf_tiles(max_nodes),
+                                                       st), "level_finalize")
             # leaves that can retire at this level: gids [base, base + n + n_next)
             win = min(3 * max_nodes, self.capacity)
             with T("partition"):
@@ -475,6 +508,76 @@ class HipTreeBuilder:
         built_zeroed = True          # tree_begin_seg zeroed level 0's histogram
         hc_cap = -(-n // self.hc_rows)
         pc_cap = -(-n // self.pc_rows)
+        # (g, s2) as the current level reads them: by row at level 0, afterwards in segment order
+        # (part_scatter moves them with the rows, so the histogram passes read them contiguously)
+        gs = {"g": g, "s": s2, "pos": 0}
+
+        def route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first, ctl_cur, ctl_nxt,
+                  idx_in, next_direct, ec=None):
+            """part_count -> level_close -> part_scatter: rows into their next-level segments.
+            ec: (codes, stride, nodeq) of the direct pass - split codes read in segment order."""
+            cur, nxt = d % 2, (d + 1) % 2
+            nbuilt = None
+            max_pc = pc_cap + max_nodes
+            pwave = int(max_nodes >= self.PART_WAVE_NODES or ec is not None)
+            ecodes, ecs, nodeq = ec if ec is not None else (None, 0, None)
+            # row directions stored by part_count for part_scatter (not on the last level: no count pass)
+            dirb = B("dirb", n + 64, torch.int8) if (pwave and not last) else None
+            pc_left = B("pc_left", max_pc, i32)
+            node_nl = B("node_nl", 2 * max_nodes, i32)
+            idx_out = None
+            write_nid = 0
+            if not last:
+                nstart, ncnt, nhc, npc, nslot = seg[nxt]
+                nstart = seg[nxt][0] = B(f"seg_start{nxt}", next_nodes, i32)
+                ncnt = seg[nxt][1] = B(f"seg_cnt{nxt}", next_nodes, i32)
+                nhc = seg[nxt][2] = B(f"hc_first{nxt}", next_nodes + 1, i32)
+                npc = seg[nxt][3] = B(f"pc_first{nxt}", next_nodes + 1, i32)
+                nslot = seg[nxt][4] = B(f"slot_node{nxt}", max(1, max_nodes), i32)
+                next_seg_hist = (not next_direct) and (max_nodes > self.SCAN_SLOTS or next_nodes > self.SYNC_NODE_CAP)
+                # live-row node ids feed the next level's scan histograms only
+                write_nid = 0 if (next_seg_hist or next_direct) else 1
+                nbuilt = None
+                if next_seg_hist:
+                    nbuilt = B("built", max_nodes * self.per_node, torch.int64)
+                ops.check(lib.h2omx_part_count(P(bm.codes), bm.npad, P(idx_in), P(seg_start), P(seg_cnt),
+                                               P(pc_first), P(ctl_cur), P(part), nbt, max_pc, P(pc_left), pwave,
+                                               P(dirb), P(ecodes), ecs, P(nodeq), st), "part_count")
+                if max_nodes <= self.CLOSE_SINGLE_BLOCK:
+                    ops.check(lib.h2omx_level_close(P(ctl_cur), P(ctl_nxt), P(part), P(nl), P(seg_start),
+                                                    P(seg_cnt), P(pc_first), P(pc_left), P(node_nl), P(nstart),
+                                                    P(ncnt), P(nhc), P(npc), P(nslot), self.hc_rows, P(nbuilt),
+                                                    self.per_node, st), "level_close")
+                else:
+                    pc_excl = B("pc_excl", max_pc, i32)
+                    tiles = B("scan_tiles", max(max_pc, next_nodes) // 1024 + 2, i32)
+                    cnt_h = B("cnt_h", next_nodes, i32)
+                    cnt_p = B("cnt_p", next_nodes, i32)
+                    aux = B("close_aux", 4, i32)
+                    ops.check(lib.h2omx_level_close_mb(P(ctl_cur), P(ctl_nxt), P(part), P(nl), P(seg_start),
+                                                       P(seg_cnt), P(pc_first), P(pc_left), P(node_nl), P(nstart),
+                                                       P(ncnt), P(nhc), P(npc), P(nslot), self.hc_rows, P(nbuilt),
+                                                       self.per_node, max_nodes, max_pc, P(pc_excl), P(tiles),
+                                                       P(cnt_h), P(cnt_p), P(aux), st), "level_close_mb")
+                idx_out = self.idx[d % 2]
+            gout = sout = None
+            if not last and self.PERMUTE_GS:
+                gout = B(f"gperm{d % 2}", n + 64, torch.float32)
+                sout = None if s2 is None else B(f"sperm{d % 2}", n + 64, torch.float32)
+            ops.check(lib.h2omx_part_scatter(P(bm.codes), bm.npad, P(idx_in), P(idx_out), P(self.nid), write_nid,
+                                             P(seg_start), P(seg_cnt), P(pc_first), P(pc_left), P(node_nl),
+                                             P(ctl_cur), P(part), nbt, P(g), P(h), P(w), P(self.qscale),
+                                             self.capacity, P(self.leaf_acc), max_pc, pwave, P(dirb), P(gs["g"]),
+                                             P(gs["s"]), P(gout), P(sout), P(ecodes), ecs, P(nodeq), st),
+                      "part_scatter")
+            if gout is not None:
+                gs.update(g=gout, s=sout, pos=1)
+            else:
+                gs.update(g=g, s=s2, pos=0)
+            return idx_out, nbuilt is not None
+
+        direct = False
+        direct_ok = comm is None and self.DIRECT_MIN_NODES > 0 and F <= 1024
         for d in range(max_depth):
             cur, nxt = d % 2, (d + 1) % 2
             ctl_cur, ctl_nxt = self.ctl[cur], self.ctl[nxt]
@@ -489,6 +592,54 @@ class HipTreeBuilder:
                 max_slots = 1 if d == 0 else max(1, max_nodes // 2)
             last = d == max_depth - 1
             seg_start, seg_cnt, hc_first, pc_first, slot_node = seg[cur]
+            direct = direct or (direct_ok and d > 0 and max_nodes >= self.DIRECT_MIN_NODES)
+            if direct:
+                # eligible-feature histograms of every node built and scanned in LDS
+                sp.depth = d
+                sp.children_leaves = 1 if last else 0
+                next_nodes = 2 * max_nodes
+                nsplit = B("nsplit", max_nodes * 9, torch.float64)
+                part = B("part", max_nodes * PART_INFO_BYTES // 4, i32)
+                nl = None
+                if not last:
+                    nl = B(f"link{nxt}", next_nodes * NODE_LINK_BYTES // 4, i32)
+                    link[nxt] = nl
+                # one wave per node for small nodes, one workgroup per row chunk while nodes
+                # are large (big nodes spread over many workgroups), else one workgroup per node
+                max_pc = pc_cap + max_nodes
+                n_elig = min(p.mtries, F) if p.mtries > 0 else F
+                slab = tot_slab = ticket = None
+                if n < self.DIRECT_WAVE_ROWS * max_nodes and F <= 256:
+                    dmode = 1
+                elif self.DIRECT_CHUNKED and n_elig * nbt * 16 <= 65536:
+                    dmode = 2
+                    slab = B("dslab", max_pc * n_elig * nbt, torch.int64)
+                    tot_slab = B("dtot", 2 * max_pc, torch.int64)
+                    ticket = self._ticket_buf(max_nodes)
+                else:
+                    dmode = 0
+                ec = None
+                # every eligible feature in one LDS batch (batch sizes of h2omx_seg_direct)
+                one_batch = {0: 98304, 1: 8192, 2: 1 << 30}[dmode] // (16 * nbt) >= n_elig
+                if self.ECODES and n_elig <= 16 and one_batch:
+                    ecs = 8 if n_elig <= 8 else 16
+                    ec = (B("ecodes", (n + 64) * ecs, torch.uint8), ecs, B("nodeq", max_nodes, i32))
+                ecodes, ecs, nodeq = ec if ec is not None else (None, 0, None)
+                ops.check(lib.h2omx_seg_direct(P(self.codes_rm), bm.fp, P(idx_in), P(gs["g"]), P(gs["s"]),
+                                               P(seg_start), P(seg_cnt), P(ctl_cur), P(bm.nvb), P(tree_fmask),
+                                               P(self.qscale), tree_index & 0x7FFFFFFF, spp, nbt, max_nodes, dmode,
+                                               P(pc_first), max_pc, P(slab), P(tot_slab), P(ticket), P(nsplit),
+                                               gs["pos"], P(ecodes), ecs, P(nodeq), st), "seg_direct")
+                ops.check(lib.h2omx_level_finalize_ns(P(nsplit), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
+                                                      P(bm.nvb), nbt, next_nodes, P(part), P(nl), P(self.tree_buf),
+                                                      self.capacity, max_nodes,
+                                                      self._lf_tiles(max_nodes), st),
+                          "level_finalize_ns")
+                idx_in, _ = route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first, ctl_cur,
+                                  ctl_nxt, idx_in, True, ec)
+                full_prev = None
+                max_nodes = next_nodes
+                continue
             seg_hist = max_slots > self.SCAN_SLOTS or max_nodes > self.SYNC_NODE_CAP
             built = B("built", max_slots * self.per_node, torch.int64)
             if seg_hist and not built_zeroed:
@@ -497,11 +648,11 @@ class HipTreeBuilder:
             if seg_hist:
                 max_hc = hc_cap + max_slots
                 slab = B("seg_slab", max_hc * self.seg_groups * self.seg_fg * nbt, torch.int64)
-                ops.check(lib.h2omx_hist_build_seg(P(self.codes_rm), bm.fp, P(idx_in), P(g), P(s2), P(seg_start),
-                                                   P(seg_cnt), P(hc_first), P(ctl_cur), P(bm.nvb), P(self.qscale),
-                                                   tree_index & 0x7FFFFFFF, F, nbt, self.seg_fg, self.seg_groups,
-                                                   self.hc_rows, max_hc, self.seg_threads, P(slab), st),
-                          "hist_build_seg")
+                ops.check(lib.h2omx_hist_build_seg(P(self.codes_rm), bm.fp, P(idx_in), P(gs["g"]), P(gs["s"]),
+                                                   P(seg_start), P(seg_cnt), P(hc_first), P(ctl_cur), P(bm.nvb),
+                                                   P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, self.seg_fg,
+                                                   self.seg_groups, self.hc_rows, max_hc, self.seg_threads, P(slab),
+                                                   gs["pos"], st), "hist_build_seg")
                 ksplit = max(1, min(32, 4096 // max(1, max_slots * ((F * nbt + 255) // 256))))
                 ksplit = max(ksplit, 4)
                 ops.check(lib.h2omx_hist_reduce_seg(P(slab), P(hc_first), P(slot_node), P(ctl_cur), F, nbt,
@@ -539,50 +690,10 @@ class HipTreeBuilder:
             nsplit = B("nsplit", max_nodes * 9, torch.float64)
             ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges), P(bm.nvb), nbt,
                                                next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
-                                               P(nsplit), max_nodes, st), "level_finalize")
-            max_pc = pc_cap + max_nodes
-            pc_left = B("pc_left", max_pc, i32)
-            node_nl = B("node_nl", 2 * max_nodes, i32)
-            idx_out = None
-            write_nid = 0
-            if not last:
-                nstart, ncnt, nhc, npc, nslot = seg[nxt]
-                nstart = seg[nxt][0] = B(f"seg_start{nxt}", next_nodes, i32)
-                ncnt = seg[nxt][1] = B(f"seg_cnt{nxt}", next_nodes, i32)
-                nhc = seg[nxt][2] = B(f"hc_first{nxt}", next_nodes + 1, i32)
-                npc = seg[nxt][3] = B(f"pc_first{nxt}", next_nodes + 1, i32)
-                nslot = seg[nxt][4] = B(f"slot_node{nxt}", max(1, max_nodes), i32)
-                next_seg_hist = max_nodes > self.SCAN_SLOTS or next_nodes > self.SYNC_NODE_CAP
-                write_nid = 0 if next_seg_hist else 1
-                nbuilt = None
-                if next_seg_hist:
-                    nbuilt = B("built", max_nodes * self.per_node, torch.int64)
-                    built_zeroed = True
-                ops.check(lib.h2omx_part_count(P(bm.codes), bm.npad, P(idx_in), P(seg_start), P(seg_cnt),
-                                               P(pc_first), P(ctl_cur), P(part), nbt, max_pc, P(pc_left), st),
-                          "part_count")
-                if max_nodes <= self.CLOSE_SINGLE_BLOCK:
-                    ops.check(lib.h2omx_level_close(P(ctl_cur), P(ctl_nxt), P(part), P(nl), P(seg_start),
-                                                    P(seg_cnt), P(pc_first), P(pc_left), P(node_nl), P(nstart),
-                                                    P(ncnt), P(nhc), P(npc), P(nslot), self.hc_rows, P(nbuilt),
-                                                    self.per_node, st), "level_close")
-                else:
-                    pc_excl = B("pc_excl", max_pc, i32)
-                    tiles = B("scan_tiles", max(max_pc, next_nodes) // 1024 + 2, i32)
-                    cnt_h = B("cnt_h", next_nodes, i32)
-                    cnt_p = B("cnt_p", next_nodes, i32)
-                    aux = B("close_aux", 4, i32)
-                    ops.check(lib.h2omx_level_close_mb(P(ctl_cur), P(ctl_nxt), P(part), P(nl), P(seg_start),
-                                                       P(seg_cnt), P(pc_first), P(pc_left), P(node_nl), P(nstart),
-                                                       P(ncnt), P(nhc), P(npc), P(nslot), self.hc_rows, P(nbuilt),
-                                                       self.per_node, max_nodes, max_pc, P(pc_excl), P(tiles),
-                                                       P(cnt_h), P(cnt_p), P(aux), st), "level_close_mb")
-                idx_out = self.idx[d % 2]
-            ops.check(lib.h2omx_part_scatter(P(bm.codes), bm.npad, P(idx_in), P(idx_out), P(self.nid), write_nid,
-                                             P(seg_start), P(seg_cnt), P(pc_first), P(pc_left), P(node_nl),
-                                             P(ctl_cur), P(part), nbt, P(g), P(h), P(w), P(self.qscale),
-                                             self.capacity, P(self.leaf_acc), max_pc, st), "part_scatter")
-            idx_in = idx_out
+                                               P(nsplit), max_nodes, self._lf_tiles(max_nodes), st),
+                      "level_finalize")
+            idx_in, built_zeroed = route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first,
+                                         ctl_cur, ctl_nxt, idx_in, False)
             full_prev = full_cur
             max_nodes = next_nodes
         if comm is not None:

@@ -23,7 +23,7 @@ TREE_SIGS = {
     "h2omx_hist_build_compact": "PLPPPPPPPIIIIIIIIIIPS",
     "h2omx_hist_build_route": "PLPPPPIPPPIIIIIIIIIPIPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
-    "h2omx_level_finalize": "PPPPPPIIPPPIPIS",
+    "h2omx_level_finalize": "PPPPPPIIPPPIPIPS",
     "h2omx_split_level": "PPPPPPPPPIIPPPPIPPPIS",
     "h2omx_partition": "PLPPIPPPPIPPPIIIPS",
     "h2omx_partition_blocks": "",
@@ -43,12 +43,14 @@ TREE_SIGS = {
     "h2omx_predict_binned": "PLLPPIIIPLS",
     "h2omx_pc_rows": "",
     "h2omx_tree_begin_seg": "PIIPPPPIPIIIPPPPPLS",
-    "h2omx_hist_build_seg": "PIPPPPPPPPPIIIIIIIIPS",
+    "h2omx_hist_build_seg": "PIPPPPPPPPPIIIIIIIIPIS",
     "h2omx_hist_reduce_seg": "PPPPIIIIIIPS",
-    "h2omx_part_count": "PLPPPPPPIIPS",
+    "h2omx_part_count": "PLPPPPPPIIPIPPIPS",
     "h2omx_level_close": "PPPPPPPPPPPPPPIPIS",
     "h2omx_level_close_mb": "PPPPPPPPPPPPPPIPIIIPPPPPS",
-    "h2omx_part_scatter": "PLPPPIPPPPPPPIPPPPIPIS",
+    "h2omx_part_scatter": "PLPPPIPPPPPPPIPPPPIPIIPPPPPPIPS",
+    "h2omx_seg_direct": "PIPPPPPPPPPIPIIIPIPPPPIPIPS",
+    "h2omx_level_finalize_ns": "PPPPPPIIPPPIIPS",
 }
 
 DENSE_SIGS = {

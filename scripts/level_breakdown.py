@@ -3,22 +3,23 @@ import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
-keys = ["split_find", "hist_build_seg", "hist_build_kernel", "hist_reduce", "level_finalize", "level_close",
-        "part_scatter", "zero_slots", "part_count", "node_best"]
+keys = ["split_find", "seg_direct", "hist_build_seg", "hist_build_kernel", "hist_reduce", "level_finalize", "level_close",
+        "part_scatter", "zero_slots", "part_count", "node_best", "lf_"]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 seq = [(r["Kernel_Name"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3, r["Grid_Size_X"]) for r in rows]
-idx = [i for i, (n, d, g) in enumerate(seq) if "split_find" in n]
+LEVEL = ("split_find", "seg_direct")   # one of these per level (direct mode replaces split_find)
+idx = [i for i, (n, d, g) in enumerate(seq) if any(k in n for k in LEVEL)]
 depth = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 start = idx[-depth]
 lvl, out = -1, {}
 for n, d, g in seq[start - 3:]:
     for k in keys:
         if k in n:
-            if k == "split_find":
+            if k in LEVEL:
                 lvl += 1
             e = out.setdefault(lvl, {})
             e[k] = e.get(k, 0.0) + d
-            if k == "split_find":
+            if k in LEVEL:
                 e["grid"] = g
 tot = 0.0
 for lv in sorted(out):

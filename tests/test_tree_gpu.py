@@ -243,6 +243,49 @@ def test_route_kernel_matches_partition_kernel(cuda_dev, monkeypatch, dist, dept
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
 
 
+@pytest.mark.parametrize("dist,depth,sample_rate,nbins,mtries,col_rate,mode", [
+    ("drf", 12, 0.632, 20, 3, 1.0, 0), ("bernoulli", 13, 0.8, 255, 0, 0.7, 1), ("gaussian", 14, 1.0, 63, 0, 1.0, 0),
+    ("multinomial", 11, 1.0, 255, 0, 1.0, 0), ("drf", 16, 1.0, 127, 4, 1.0, 0)])
+def test_direct_deep_levels_match_subtraction(cuda_dev, monkeypatch, dist, depth, sample_rate, nbins, mtries,
+                                              col_rate, mode):
+    """Deep levels in direct mode - one workgroup per node (seg_direct_kernel)
+    or one wave per node (seg_direct_wave_kernel), packed or two-plane LDS
+    histograms built and scanned in LDS - grow the same trees as the
+    parent-minus-sibling histogram path; so does the multi-block level
+    finalisation against the single-workgroup one."""
+    import h2omx.models.tree.engine as E
+
+    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi", "drf": "bin"}[dist]
+    X, y = _data(n=50000, F=13, seed=6, task=task)
+    _, bg = _both(X, y, nbins)
+    tp = TreeParams(max_depth=depth, min_rows=2, learn_rate=0.2, leaf_mode=1 if dist == "drf" else 0,
+                    mtries=mtries, col_sample_rate=col_rate, mode=mode, reg_lambda=1.0 if mode else 0.0,
+                    min_child_weight=1.0 if mode else 0.0)
+    yt = torch.from_numpy(y).cuda()
+    monkeypatch.setenv("H2OMX_TREE_ENGINE", "seg")
+    nclass = 3 if dist == "multinomial" else (2 if dist == "drf" else 1)
+    out = {}
+    # engine switches: direct from this many nodes, wave-per-node below this many rows per node,
+    # multi-block finalise, wave-chunk partition from this many nodes, chunked direct workgroups,
+    # (g, s2) moved into segment order, eligible-feature codes stored for the partition
+    keys = ("DIRECT_MIN_NODES", "DIRECT_WAVE_ROWS", "LF_MULTI_BLOCK", "PART_WAVE_NODES", "DIRECT_CHUNKED",
+            "PERMUTE_GS", "ECODES")
+    for cfg in ((0, 0, False, 1 << 30, True, False, False), (0, 0, True, 1, True, True, True),
+                (2, 0, True, 1 << 30, True, True, True), (64, 0, True, 1 << 30, False, False, True),
+                (64, 1 << 30, True, 1, True, True, False), (64, 1 << 30, False, 2048, True, False, True)):
+        for k, v in zip(keys, cfg):
+            monkeypatch.setattr(E.HipTreeBuilder, k, v)
+        out[cfg] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
+                                  nclass=nclass, seed=13)
+    a = out[(0, 0, False, 1 << 30, True, False, False)]
+    for cfg, b in out.items():
+        for t in range(a.trees.shape[0]):
+            reach = a.compact()[t]
+            assert reach == b.compact()[t], (cfg, t)
+            for f in ("feat", "bin", "value", "weight"):
+                np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"{cfg} tree {t} {f}")
+
+
 @pytest.mark.parametrize("dist,depth,sample_rate", [("bernoulli", 5, 1.0), ("gaussian", 7, 0.7)])
 def test_pk32_rows_match_pk64(cuda_dev, monkeypatch, dist, depth, sample_rate):
     """32-bit packed rows (large row chunks: per-row values fit 16 bits) build
