@@ -116,34 +116,35 @@ def compute_edges(X: torch.Tensor, nbins: int, sample_rows: int = 1 << 20, seed:
 
 def _edges_device(S: torch.Tensor, max_value_bins: int) -> list:
     """``_edges_from_sorted`` for every row of the ascending-sorted sample S
-    [F][m] (NaNs last) with the heavy work on the device: distinct-value
-    counts and ranks by adjacent comparison + cumsum, the 'lower' quantiles
-    as index gathers; only [F][<= 256] values reach the host."""
+    [F][m] (NaNs last) with the heavy work on the device: distinct values by
+    adjacent comparison, the 'lower' quantiles as index gathers; only the
+    distinct values of low-cardinality features and [F][<= 256] quantiles
+    reach the host (no [F][m] rank / cumsum temporaries)."""
     F, m = S.shape
     dev = S.device
     cnt = (~torch.isnan(S)).sum(1)                                      # non-NaN prefix length
-    pos = torch.arange(m, device=dev)[None, :]
-    valid = pos < cnt[:, None]
-    new = valid.clone()
+    new = torch.arange(m, device=dev)[None, :] < cnt[:, None]
     new[:, 1:] &= S[:, 1:] != S[:, :-1]
     nuniq = new.sum(1)
-    rank = torch.cumsum(new.long(), 1) - 1
-    U = torch.full((F, max_value_bins + 1), float("nan"), dtype=torch.float32, device=dev)
-    small = new & (rank <= max_value_bins)
-    U[torch.nonzero(small, as_tuple=True)[0], rank[small]] = S[small]
+    # distinct values of the features with <= max_value_bins of them (row-major
+    # nonzero order = ascending within each feature)
+    fi, pi = torch.nonzero(new & (nuniq <= max_value_bins)[:, None], as_tuple=True)
+    uval = S[fi, pi]
     cnt_h = cnt.cpu().numpy()
     # numpy 'lower' quantile: index floor((n - 1) q) in float64
     qv = np.linspace(0.0, 1.0, max_value_bins + 1)[1:-1]
     idx = np.floor((np.maximum(cnt_h, 1) - 1)[:, None].astype(np.float64) * qv[None, :]).astype(np.int64)
     Q = torch.gather(S, 1, torch.from_numpy(idx).to(dev))
     mx = torch.gather(S, 1, (cnt - 1).clamp_min(0)[:, None])[:, 0]
-    U, Q, nu, mx = U.cpu().numpy(), Q.cpu().numpy(), nuniq.cpu().numpy(), mx.cpu().numpy()
+    Q, nu, mx = Q.cpu().numpy(), nuniq.cpu().numpy(), mx.cpu().numpy()
+    fi, uval = fi.cpu().numpy(), uval.cpu().numpy()
+    starts = np.searchsorted(fi, np.arange(F + 1))
     out = []
     for f in range(F):
         if cnt_h[f] == 0:
             out.append(np.zeros(0, np.float32))
         elif nu[f] <= max_value_bins:
-            out.append(U[f, : nu[f] - 1].astype(np.float32))
+            out.append(uval[starts[f]: starts[f + 1]][: nu[f] - 1].astype(np.float32))
         else:
             e = np.unique(Q[f].astype(np.float32))
             e = e[e < mx[f]]

@@ -102,7 +102,24 @@ class TreeEnsemble:
 
 
 
-def init_margin(dist: str, y: np.ndarray, w: np.ndarray | None, K: int) -> np.ndarray:
+def init_margin(dist: str, y, w, K: int) -> np.ndarray:
+    """Initial margin (H2O's init_f).  ``y`` / ``w`` may be device tensors: the
+    weighted sums then run on the device and only scalars reach the host."""
+    if torch.is_tensor(y):
+        if dist in ("multinomial", "drf"):
+            return np.zeros(K)
+        if dist in ("laplace", "quantile"):
+            return init_margin(dist, y.detach().float().cpu().numpy(), None, K)
+        yd = y.detach().double()
+        sw = float(yd.numel()) if w is None else float(w.detach().double().sum())
+        swy = float(yd.sum()) if w is None else float((w.detach().double() * yd).sum())
+        m = swy / sw
+        if dist == "bernoulli":
+            p = float(np.clip(m, 1e-6, 1 - 1e-6))
+            return np.array([np.log(p / (1 - p))])
+        if dist in ("poisson", "gamma", "tweedie"):
+            return np.array([np.log(max(m, 1e-12))])
+        return np.array([m])
     ww = np.ones_like(y, dtype=np.float64) if w is None else w.astype(np.float64)
     sw = ww.sum()
     if dist == "bernoulli":
@@ -135,8 +152,17 @@ def train_ensemble(bm: BinnedMatrix, y, w=None, *, dist: str = "bernoulli", ntre
     n = bm.n
     multi = dist == "multinomial" or (dist == "drf" and nclass > 2)
     K = nclass if multi else 1
-    y_np = y.detach().float().cpu().numpy() if torch.is_tensor(y) else np.asarray(y, np.float32)
-    w_np = None if w is None else (w.detach().float().cpu().numpy() if torch.is_tensor(w) else np.asarray(w, np.float32))
+    if bm.codes.is_cuda:
+        # device-resident labels / weights stay on the device (no 11M-row host round trip)
+        def _dev(v):
+            return v.detach().float().to(bm.device) if torch.is_tensor(v) else \
+                torch.from_numpy(np.asarray(v, np.float32)).to(bm.device)
+        y_np = _dev(y)
+        w_np = None if w is None else _dev(w)
+    else:
+        y_np = y.detach().float().cpu().numpy() if torch.is_tensor(y) else np.asarray(y, np.float32)
+        w_np = None if w is None else (w.detach().float().cpu().numpy() if torch.is_tensor(w)
+                                       else np.asarray(w, np.float32))
     if init_f is None:
         if comm is not None and comm.world_size > 1:
             init_f = _global_init(dist, y_np, w_np, K, comm)
@@ -157,8 +183,14 @@ def train_ensemble(bm: BinnedMatrix, y, w=None, *, dist: str = "bernoulli", ntre
 
 
 def _global_init(dist, y, w, K, comm):
-    ww = np.ones_like(y, dtype=np.float64) if w is None else w.astype(np.float64)
-    s = comm.all_reduce_numpy(np.array([(ww * y).sum(), ww.sum()], np.float64))
+    if torch.is_tensor(y):
+        yd = y.double()
+        wd = None if w is None else w.double()
+        loc = [float(yd.sum() if wd is None else (wd * yd).sum()), float(yd.numel() if wd is None else wd.sum())]
+        s = comm.all_reduce_numpy(np.array(loc, np.float64))
+    else:
+        ww = np.ones_like(y, dtype=np.float64) if w is None else w.astype(np.float64)
+        s = comm.all_reduce_numpy(np.array([(ww * y).sum(), ww.sum()], np.float64))
     m = s[0] / max(s[1], 1e-300)
     if dist == "bernoulli":
         p = float(np.clip(m, 1e-6, 1 - 1e-6))
@@ -180,14 +212,21 @@ class _GpuState:
         else:
             for k in range(K):
                 self.Fm[k, :n] = float(init_f[k])
-        yp = np.zeros(npad, np.float32)
-        yp[:n] = y_np
-        self.y = torch.from_numpy(yp).to(dev)
+        if torch.is_tensor(y_np):
+            self.y = torch.zeros(npad, dtype=torch.float32, device=dev)
+            self.y[:n] = y_np.to(dev)
+        else:
+            yp = np.zeros(npad, np.float32)
+            yp[:n] = y_np
+            self.y = torch.from_numpy(yp).to(dev)
         self.yk = self.y.to(torch.int32) if K > 1 else None
         if dist == "drf" and K > 1:
             self.ycls = torch.stack([(self.y == k).float() for k in range(K)])
         self.w = None
-        if w_np is not None:
+        if w_np is not None and torch.is_tensor(w_np):
+            self.w = torch.zeros(npad, dtype=torch.float32, device=dev)
+            self.w[:n] = w_np.to(dev)
+        elif w_np is not None:
             wp = np.zeros(npad, np.float32)
             wp[:n] = w_np
             self.w = torch.from_numpy(wp).to(dev)
