@@ -526,7 +526,10 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
 // 256 threads, 128x128 block tile, each wave a 64x64 quadrant = 2x2 MFMA
 // tiles of 32x32, K staged 16 at a time through LDS as [k][m] / [k][n].
 // ===========================================================================
-constexpr int GB = 128, GK = 32, GPAD = 4;
+#ifndef H2OMX_GEMM_GK
+#define H2OMX_GEMM_GK 32
+#endif
+constexpr int GB = 128, GK = H2OMX_GEMM_GK, GPAD = 4;
 
 // One K-step of a 128 x 32 operand tile: global -> registers (float4 along
 // the contiguous dimension when the leading dimension allows it).
@@ -547,8 +550,8 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ P, int ld, i
   for (int q = 0; q < GLD; ++q) {
     const int f = tid + GTHREADS * q;  // float4 index in the 128 x 32 tile
     int r, k;
-    if (KM) { k = f >> 5; r = (f & 31) * 4; }   // 32 float4 per k-row of 128
-    else { r = f >> 3; k = (f & 7) * 4; }       // 8 float4 per m-row of 32
+    if (KM) { k = f >> 5; r = (f & 31) * 4; }                  // 32 float4 per k-row of 128
+    else { r = f / (GK / 4); k = (f % (GK / 4)) * 4; }         // GK / 4 float4 per m-row of GK
     const int gr = r0 + r, gk = k0 + k;
     float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f;
     if (KM) {
@@ -593,7 +596,7 @@ __device__ __forceinline__ void store_tile(float (*S)[GB + GPAD], const TileRegs
       const int k = f >> 5, r = (f & 31) * 4;
       *reinterpret_cast<float4*>(&S[k][r]) = make_float4(t.v[4 * q], t.v[4 * q + 1], t.v[4 * q + 2], t.v[4 * q + 3]);
     } else {
-      const int r = f >> 3, k = (f & 7) * 4;
+      const int r = f / (GK / 4), k = (f % (GK / 4)) * 4;
       S[k][r] = t.v[4 * q];
       S[k + 1][r] = t.v[4 * q + 1];
       S[k + 2][r] = t.v[4 * q + 2];
@@ -685,12 +688,168 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const float* __restrict__ 
       }
 }
 
+// Skinny outputs (N <= 8, e.g. the MLP's 2-class output layer): C[M][N] =
+// act(A[M][K] B[N][K]^T + bias).  A 128 x 128 MFMA tile would compute 64x
+// more zeros than results (45 us for 8192 x 2 x 512); here one wave per row
+// streams its A row with float4 loads (B rows stay in L1/L2) and reduces
+// the N dot products with wave shuffles.
+constexpr int SKINNY_N = 8;
+__global__ __launch_bounds__(256) void gemm_skinny_nt_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                             float* __restrict__ C, const float* __restrict__ bias,
+                                                             int M, int N, int K, int act) {
+  const int lane = threadIdx.x & 63;
+  const int waves = gridDim.x * (blockDim.x >> 6);
+  const bool vec = (K % 4 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
+  for (int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < M; i += waves) {
+    const float* a = A + (int64_t)i * K;
+    float acc[SKINNY_N];
+#pragma unroll
+    for (int n = 0; n < SKINNY_N; ++n) acc[n] = 0.0f;
+    if (vec) {
+      for (int k = 4 * lane; k < K; k += 256) {
+        const float4 x = *reinterpret_cast<const float4*>(a + k);
+#pragma unroll
+        for (int n = 0; n < SKINNY_N; ++n) {
+          if (n < N) {
+            const float4 w = *reinterpret_cast<const float4*>(B + (int64_t)n * K + k);
+            acc[n] += x.x * w.x + x.y * w.y + x.z * w.z + x.w * w.w;
+          }
+        }
+      }
+    } else {
+      for (int k = lane; k < K; k += 64) {
+        const float x = a[k];
+#pragma unroll
+        for (int n = 0; n < SKINNY_N; ++n)
+          if (n < N) acc[n] += x * B[(int64_t)n * K + k];
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < SKINNY_N; ++n) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc[n] += __shfl_xor(acc[n], o, 64);
+    }
+    if (lane < N) {
+      float v = 0.0f;
+#pragma unroll
+      for (int n = 0; n < SKINNY_N; ++n)
+        if (n == lane) v = acc[n];
+      if (bias) v += bias[lane];
+      if (act == 1) v = fmaxf(v, 0.0f);
+      else if (act == 2) v = tanhf(v);
+      C[(int64_t)i * N + lane] = v;
+    }
+  }
+}
+
+// Tiny inner dimension (K <= 8, e.g. dH = dZ W through the 2-class output
+// layer): C[M][N] = A[M][K] B[K][N] as a streaming outer-product sum, fused
+// with the activation derivative of the layer below (act_y: Y of that layer,
+// act: 1 relu, 2 tanh) so dZ comes out in one pass.
+__global__ __launch_bounds__(256) void gemm_thin_k_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                          float* __restrict__ C, int64_t M, int N, int K,
+                                                          const float* __restrict__ act_y, int act) {
+  const int64_t total = M * N;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / N;
+    const int j = (int)(e - i * N);
+    float v = 0.0f;
+    for (int k = 0; k < K; ++k) v += A[i * K + k] * B[(int64_t)k * N + j];
+    if (act_y) {
+      const float y = act_y[e];
+      if (act == 1) v = y > 0.0f ? v : 0.0f;
+      else if (act == 2) v *= 1.0f - y * y;
+    }
+    C[e] = v;
+  }
+}
+
+// dZ = dY * act'(Y) and the column partial sums of dZ (the bias gradient of
+// that layer) in ONE pass over dY: block = 256 columns (float4 per lane) x 4
+// row phases over one row slice -> ws[slice][col]; the slices are summed
+// later in a fixed order (deterministic), e.g. by the weight gradient's
+// split-K reduce (gemm_splitk_reduce_kernel second job).  N % 4 == 0.
+__device__ __forceinline__ float act_grad(float g, float y, int act) {
+  if (act == 1) return y > 0.0f ? g : 0.0f;
+  if (act == 2) return g * (1.0f - y * y);
+  return g;
+}
+
+__global__ __launch_bounds__(256) void act_backward_bias_kernel(const float* __restrict__ Y, float* __restrict__ dY,
+                                                                float* __restrict__ ws, int M, int N, int act) {
+  __shared__ float4 red[4][64];
+  const int c = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int j = (blockIdx.x * 64 + c) * 4;
+  const int S = gridDim.y;
+  const int rows = (M + S - 1) / S;
+  const int r0 = blockIdx.y * rows, r1 = min(M, r0 + rows);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (j < N) {
+    int i = r0 + ph;
+    for (; i + 4 < r1; i += 8) {   // two rows' loads in flight per lane
+      const int64_t e0 = (int64_t)i * N + j, e1 = e0 + 4 * (int64_t)N;
+      float4 g0 = *reinterpret_cast<const float4*>(dY + e0), g1 = *reinterpret_cast<const float4*>(dY + e1);
+      const float4 y0 = *reinterpret_cast<const float4*>(Y + e0), y1 = *reinterpret_cast<const float4*>(Y + e1);
+      g0 = make_float4(act_grad(g0.x, y0.x, act), act_grad(g0.y, y0.y, act), act_grad(g0.z, y0.z, act),
+                       act_grad(g0.w, y0.w, act));
+      g1 = make_float4(act_grad(g1.x, y1.x, act), act_grad(g1.y, y1.y, act), act_grad(g1.z, y1.z, act),
+                       act_grad(g1.w, y1.w, act));
+      *reinterpret_cast<float4*>(dY + e0) = g0;
+      *reinterpret_cast<float4*>(dY + e1) = g1;
+      s.x += g0.x + g1.x; s.y += g0.y + g1.y; s.z += g0.z + g1.z; s.w += g0.w + g1.w;
+    }
+    for (; i < r1; i += 4) {
+      const int64_t e0 = (int64_t)i * N + j;
+      float4 g0 = *reinterpret_cast<const float4*>(dY + e0);
+      const float4 y0 = *reinterpret_cast<const float4*>(Y + e0);
+      g0 = make_float4(act_grad(g0.x, y0.x, act), act_grad(g0.y, y0.y, act), act_grad(g0.z, y0.z, act),
+                       act_grad(g0.w, y0.w, act));
+      *reinterpret_cast<float4*>(dY + e0) = g0;
+      s.x += g0.x; s.y += g0.y; s.z += g0.z; s.w += g0.w;
+    }
+  }
+  red[ph][c] = s;
+  __syncthreads();
+  if (ph == 0 && j < N) {
+    const float4 a = red[0][c], b = red[1][c], d = red[2][c], e = red[3][c];
+    *reinterpret_cast<float4*>(ws + (int64_t)blockIdx.y * N + j) =
+        make_float4((a.x + b.x) + (d.x + e.x), (a.y + b.y) + (d.y + e.y), (a.z + b.z) + (d.z + e.z),
+                    (a.w + b.w) + (d.w + e.w));
+  }
+}
+
 // C = act(sum_z W[z] + beta_c * C + bias): split-K epilogue (fixed order: deterministic)
+// Optional second job (W2 != nullptr): blocks >= main_blocks sum the S2
+// slices of a [S2][N2] workspace into C2 (a bias gradient folded into the
+// weight gradient's reduce launch).
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __restrict__ W, int S, int M, int N,
                                                                  float* __restrict__ C, const float* __restrict__ bias,
-                                                                 int act, float beta_c) {
+                                                                 int act, float beta_c, int main_blocks = 0,
+                                                                 const float* __restrict__ W2 = nullptr, int S2 = 0,
+                                                                 int N2 = 0, float* __restrict__ C2 = nullptr) {
+  if (W2 != nullptr && (int)blockIdx.x >= main_blocks) {
+    // 64 columns per block, the 4 waves take every 4th slice (loads in flight), fixed-order fold
+    __shared__ float red2[4][64];
+    const int c = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const int j = (blockIdx.x - main_blocks) * 64 + c;
+    float a = 0.0f, b = 0.0f;
+    if (j < N2) {
+      int z = ph;
+      for (; z + 4 < S2; z += 8) {
+        a += W2[(int64_t)z * N2 + j];
+        b += W2[(int64_t)(z + 4) * N2 + j];
+      }
+      for (; z < S2; z += 4) a += W2[(int64_t)z * N2 + j];
+    }
+    red2[ph][c] = a + b;
+    __syncthreads();
+    if (ph == 0 && j < N2) C2[j] = (red2[0][c] + red2[1][c]) + (red2[2][c] + red2[3][c]);
+    return;
+  }
   const int64_t MN = (int64_t)M * N;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < MN; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t gstride = (int64_t)(W2 != nullptr ? main_blocks : gridDim.x) * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < MN; i += gstride) {
     float v = 0.0f;
     for (int z = 0; z < S; ++z) v += W[z * MN + i];
     if (beta_c != 0.0f) v += beta_c * C[i];
@@ -1237,6 +1396,43 @@ H2OMX_API int h2omx_gemm(const float* A, const float* B, float* C, const float* 
   if (splitk > 1)
     hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(cdiv((int64_t)M * N, 256) < 4096 ? cdiv((int64_t)M * N, 256) : 4096),
                        dim3(256), 0, stream, ws, splitk, M, N, C, bias, act, beta_c);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_gemm_skinny_nt(const float* A, const float* B, float* C, const float* bias, int M, int N, int K,
+                                   int act, hipStream_t stream) {
+  if (N < 1 || N > SKINNY_N) return kBadArg;
+  const int blocks = std::min(cdiv(M, 4), 4096);
+  hipLaunchKernelGGL(gemm_skinny_nt_kernel, dim3(blocks), dim3(256), 0, stream, A, B, C, bias, M, N, K, act);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_gemm_thin_k(const float* A, const float* B, float* C, int64_t M, int N, int K, const float* act_y,
+                                int act, hipStream_t stream) {
+  if (K < 1 || K > 8) return kBadArg;
+  const int64_t blocks = std::min<int64_t>(cdiv(M * N, 256), 8192);
+  hipLaunchKernelGGL(gemm_thin_k_kernel, dim3(blocks), dim3(256), 0, stream, A, B, C, M, N, K, act_y, act);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_act_backward_bias(const float* Y, float* dY, float* ws, int M, int N, int splits, int act,
+                                      hipStream_t stream) {
+  if (splits < 1 || !ws || N % 4 || (reinterpret_cast<uintptr_t>(Y) & 15) || (reinterpret_cast<uintptr_t>(dY) & 15) ||
+      (reinterpret_cast<uintptr_t>(ws) & 15))
+    return kBadArg;
+  hipLaunchKernelGGL(act_backward_bias_kernel, dim3(cdiv(N, 256), splits), dim3(256), 0, stream, Y, dY, ws, M, N, act);
+  return launch_status();
+}
+
+// weight-gradient GEMM (split-K) whose reduce launch also sums a bias-gradient workspace
+H2OMX_API int h2omx_gemm_wgrad_bias(const float* A, const float* B, float* C, int M, int N, int K, int splitk,
+                                    float* ws, const float* bws, int bsplits, int bn, float* db, hipStream_t stream) {
+  if (splitk < 2 || !ws || !bws || !db) return kBadArg;
+  const dim3 grid(cdiv(N, GB), cdiv(M, GB), splitk);
+  hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(GTHREADS), 0, stream, A, B, ws, nullptr, M, N, K, 0, 0.0f);
+  const int mb = cdiv((int64_t)M * N, 256) < 4096 ? (int)cdiv((int64_t)M * N, 256) : 4096;
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(mb + cdiv(bn, 64)), dim3(256), 0, stream, ws, splitk, M, N, C,
+                     nullptr, 0, 0.0f, mb, bws, bsplits, bn, db);
   return launch_status();
 }
 

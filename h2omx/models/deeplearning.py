@@ -507,11 +507,16 @@ class H2ODeepLearningEstimator(ModelBuilder):
     def _backward(self, net, Hs, aux, dZ, act, comm, world):
         L = len(net.layers)
         handles = []
+        bpart = None   # bias-gradient slices of dZ from the fused activation backward
         for i in range(L - 1, -1, -1):
             Hin = Hs[i]
             W = net.W(i)
-            D.gemm(dZ, Hin, ta=True, out=net.W(i, net.grad))          # dW = dZ^T H
-            D.bias_grad(dZ, out=net.b(i, net.grad))
+            if bpart is not None:
+                D.wgrad_bias(dZ, Hin, net.W(i, net.grad), net.b(i, net.grad), bpart)   # dW = dZ^T H, db
+            else:
+                D.gemm(dZ, Hin, ta=True, out=net.W(i, net.grad))          # dW = dZ^T H
+                D.bias_grad(dZ, out=net.b(i, net.grad))
+            bpart = None
             if comm is not None and world > 1:
                 a, b = net.span(i)
                 handles.append(comm.all_reduce_async(net.grad[a:b]))
@@ -528,8 +533,10 @@ class H2ODeepLearningEstimator(ModelBuilder):
             elif act == 4:
                 Hn = Hs[i]
                 dZ = dH * torch.where(Hn > 0, torch.ones_like(Hn), Hn + 1.0)
+            elif mask is None:
+                dZ, bpart = D.act_backward_bias(Hs[i], dH, act)
             else:
-                dZ = D.act_backward(Hs[i] if mask is None else Hs[i] / mask.clamp_min(1e-30) * (mask > 0), dH, act)
+                dZ = D.act_backward(Hs[i] / mask.clamp_min(1e-30) * (mask > 0), dH, act)
         for h in handles:
             h.wait()
         if comm is not None and world > 1:

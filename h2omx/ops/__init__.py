@@ -66,6 +66,10 @@ DENSE_SIGS = {
     "h2omx_kmeans_onehot": "PILPS",
     "h2omx_gemm": "PPPPIIIIIIFIPS",
     "h2omx_act_backward": "PPLIS",
+    "h2omx_gemm_skinny_nt": "PPPPIIIIS",
+    "h2omx_gemm_thin_k": "PPPLIIPIS",
+    "h2omx_act_backward_bias": "PPPIIIIS",
+    "h2omx_gemm_wgrad_bias": "PPPIIIIPPIIPS",
     "h2omx_bias_grad": "PPIIPIS",
     "h2omx_softmax_xent": "PPPPIIS",
     "h2omx_adadelta": "PPPPLFFFS",

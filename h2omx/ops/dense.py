@@ -232,16 +232,71 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
     C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=A.device)
     if not C.is_contiguous():
         raise ValueError("gemm: out must be contiguous")
-    # split-K when the output has too few 128x128 tiles to fill 256 CUs
-    # (weight gradients: [out][in] outputs with K = batch rows)
-    tiles = -(-M // 128) * -(-N // 128)
-    S = 1
-    if tiles < 128 and K >= 1024:
-        S = max(1, min(64, 256 // tiles, K // 256))
+    if beta_c == 0.0 and not ta:
+        if tb and N <= 8 and K >= 16:
+            # skinny output (classifier layer): one wave per row, no 128 x 128 tile of zeros
+            check(dense_lib().h2omx_gemm_skinny_nt(P(A), P(B), P(C), P(bias), M, N, K, act, stream(A.device)),
+                  "gemm_skinny_nt")
+            return C
+        if not tb and K <= 8 and bias is None and act == 0:
+            check(dense_lib().h2omx_gemm_thin_k(P(A), P(B), P(C), M, N, K, None, 0, stream(A.device)),
+                  "gemm_thin_k")
+            return C
+    S = _splitk(M, N, K)
     ws = _workspace(A.device, S * M * N) if S > 1 else None
     check(dense_lib().h2omx_gemm(P(A), P(B), P(C), P(bias), M, N, K, int(ta), int(tb), act, beta_c, S, P(ws),
                              stream(A.device)), "gemm")
     return C
+
+
+def _splitk(M: int, N: int, K: int) -> int:
+    """split-K when the output has too few 128x128 tiles to fill 256 CUs
+    (weight gradients: [out][in] outputs with K = batch rows)"""
+    tiles = -(-M // 128) * -(-N // 128)
+    if tiles < 128 and K >= 1024:
+        return max(1, min(64, 256 // tiles, K // 256))
+    return 1
+
+
+def _bias_splits(M: int, N: int) -> int:
+    # enough (64-column x row-slice) blocks to fill the GPU, few enough that
+    # the second stage sums a short column
+    return max(1, min(32, M // 256, 1024 // max(1, -(-N // 64))))
+
+
+def act_backward_bias(Y: torch.Tensor, dY: torch.Tensor, act: int):
+    """dZ = dY * act'(Y) in place, plus the per-slice column sums of dZ (the
+    layer's bias gradient before its final fixed-order reduce) in one pass.
+    Returns (dZ, (workspace, splits)) for :func:`wgrad_bias` / :func:`bias_reduce`."""
+    M, N = dY.shape
+    _dev(dY, "act_backward_bias")
+    if N % 4 or not (Y.is_contiguous() and dY.is_contiguous()):
+        act_backward(Y, dY, act)
+        return dY, (bias_grad(dY)[None, :], 1)
+    # 256-column blocks: enough row slices to put ~512 workgroups on the GPU
+    splits = max(1, min(128, M // 32, 512 // max(1, -(-N // 256))))
+    ws = _workspace(dY.device, splits * N, slot=1)
+    check(dense_lib().h2omx_act_backward_bias(P(Y), P(dY), P(ws), M, N, splits, act, stream(dY.device)),
+          "act_backward_bias")
+    return dY, (ws, splits)
+
+
+def wgrad_bias(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Tensor, bpart) -> None:
+    """dW = dZ^T H and db = the reduce of the slices in ``bpart`` (from
+    :func:`act_backward_bias`), the bias reduce riding on the split-K reduce launch."""
+    K, M = dZ.shape
+    N = H.shape[1]
+    S = _splitk(M, N, K)
+    bws, bsplits = bpart
+    if S < 2:
+        gemm(dZ, H, ta=True, out=dW)
+        tmp = torch.empty((M,), dtype=torch.float64, device=dZ.device)
+        check(dense_lib().h2omx_slab_sum(P(bws), bsplits, M, P(tmp), stream(dZ.device)), "slab_sum")
+        db.copy_(tmp)
+        return
+    ws = _workspace(dZ.device, S * M * N)
+    check(dense_lib().h2omx_gemm_wgrad_bias(P(dZ.contiguous()), P(H.contiguous()), P(dW), M, N, K, S, P(ws), P(bws),
+                                            bsplits, M, P(db), stream(dZ.device)), "gemm_wgrad_bias")
 
 
 def act_backward(Y: torch.Tensor, dY: torch.Tensor, act: int) -> torch.Tensor:
@@ -256,9 +311,7 @@ def bias_grad(dY: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor
     M, N = dY.shape
     _dev(dY, "bias_grad")
     db = out if out is not None else torch.empty((N,), dtype=torch.float32, device=dY.device)
-    # enough (64-column x row-slice) blocks to fill the GPU, few enough that
-    # the second stage sums a short column
-    splits = max(1, min(32, M // 256, 1024 // max(1, -(-N // 64))))
+    splits = _bias_splits(M, N)
     ws = _workspace(dY.device, splits * N, slot=1)
     check(dense_lib().h2omx_bias_grad(P(dY), P(db), M, N, P(ws), splits, stream(dY.device)), "bias_grad")
     return db

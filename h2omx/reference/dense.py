@@ -157,6 +157,17 @@ def act_backward(Y: torch.Tensor, dY: torch.Tensor, act: int) -> torch.Tensor:
     return dY
 
 
+def act_backward_bias(Y: torch.Tensor, dY: torch.Tensor, act: int):
+    """Reference of ops.dense.act_backward_bias: the 'slices' are the full column sums."""
+    act_backward(Y, dY, act)
+    return dY, (dY.sum(0)[None, :], 1)
+
+
+def wgrad_bias(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Tensor, bpart) -> None:
+    dW.copy_(dZ.T @ H)
+    db.copy_(bpart[0].sum(0))
+
+
 def bias_grad(dY: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     r = dY.sum(0)
     if out is not None:

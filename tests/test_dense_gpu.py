@@ -129,3 +129,52 @@ def test_auc_hist_kernel_matches_cpu(cuda_dev):
     np.testing.assert_allclose(Hg, Hc, rtol=1e-6, atol=1e-6)
     a = auc_from_scores(s.to(cuda_dev), y.to(cuda_dev))
     assert abs(a - roc_auc_score(y.numpy(), s.numpy())) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K,act", [(8192, 2, 512, 0), (1000, 3, 200, 1), (777, 8, 37, 2), (64, 1, 16, 0)])
+def test_gemm_skinny_output_matches_torch(cuda_dev, M, N, K, act):
+    """Classifier-layer shapes (N <= 8) take the one-wave-per-row kernel."""
+    torch.manual_seed(3)
+    A = torch.randn((M, K), device=cuda_dev)
+    B = torch.randn((N, K), device=cuda_dev)
+    bias = torch.randn(N, device=cuda_dev)
+    C = D.gemm(A, B, bias, act, False, True)
+    ref = D.gemm(A.cpu(), B.cpu(), bias.cpu(), act, False, True)
+    assert torch.allclose(C.cpu(), ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 512, 2), (333, 100, 5)])
+def test_gemm_thin_k_matches_torch(cuda_dev, M, N, K):
+    torch.manual_seed(4)
+    A = torch.randn((M, K), device=cuda_dev)
+    B = torch.randn((K, N), device=cuda_dev)
+    C = D.gemm(A, B)
+    assert torch.allclose(C.cpu(), A.cpu() @ B.cpu(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,out,inp,act", [(8192, 512, 512, 1), (8192, 512, 200, 2), (300, 64, 40, 0), (300, 30, 40, 1)])
+def test_act_backward_bias_and_wgrad(cuda_dev, M, out, inp, act):
+    """Fused activation backward + bias-gradient slices, and the weight-gradient
+    GEMM whose split-K reduce also folds the bias slices (fp64 reference)."""
+    torch.manual_seed(5)
+    Y = torch.randn((M, out), device=cuda_dev)
+    if act == 1:
+        Y = Y.clamp_min(0)
+    elif act == 2:
+        Y = torch.tanh(Y)
+    dY = torch.randn((M, out), device=cuda_dev)
+    H = torch.randn((M, inp), device=cuda_dev)
+    dYr = dY.double().cpu()
+    if act == 1:
+        dZr = dYr * (Y.cpu() > 0).double()
+    elif act == 2:
+        dZr = dYr * (1 - Y.cpu().double() ** 2)
+    else:
+        dZr = dYr
+    dZ, bpart = D.act_backward_bias(Y, dY.clone(), act)
+    assert torch.allclose(dZ.double().cpu(), dZr, atol=1e-6)
+    dW = torch.empty((out, inp), device=cuda_dev)
+    db = torch.empty((out,), device=cuda_dev)
+    D.wgrad_bias(dZ, H, dW, db, bpart)
+    assert torch.allclose(dW.double().cpu(), dZr.T @ H.double().cpu(), rtol=1e-4, atol=2e-2)
+    assert torch.allclose(db.double().cpu(), dZr.sum(0), atol=1e-3)
