@@ -688,6 +688,143 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const float* __restrict__ 
       }
 }
 
+// Same GEMM on 64 x 64 tiles: 256 threads, each wave one 32 x 32 MFMA
+// accumulator.  The MLP's GEMMs (8192 x 512 x 512, weight gradients split-K)
+// give only one 128 x 128 tile per CU - 8 waves whose load / barrier latency
+// nothing else covers; quarter-size tiles put 4 workgroups (16 waves) on every
+// CU.  Same K order per output element as gemm_kernel (k ascending in fmaf
+// steps): bit-identical results.
+constexpr int G64 = 64, G64T = 256;
+struct Tile64 {
+  float v[8];
+};
+template <bool KM>
+__device__ __forceinline__ void load_tile64(const float* __restrict__ P, int ld, int rows, int k_lim, int r0, int k0,
+                                            bool vec, Tile64& t) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int f = tid + G64T * q;   // float4 index in the 64 x 32 tile
+    int r, k;
+    if (KM) { k = f >> 4; r = (f & 15) * 4; }   // 16 float4 per k-row of 64
+    else { r = f >> 3; k = (f & 7) * 4; }       // 8 float4 per m-row of 32
+    const int gr = r0 + r, gk = k0 + k;
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f;
+    if (KM) {
+      if (gk < k_lim) {
+        const float* src = P + (int64_t)gk * ld + gr;
+        if (vec && gr + 3 < rows) {
+          const float4 v4 = *reinterpret_cast<const float4*>(src);
+          x0 = v4.x; x1 = v4.y; x2 = v4.z; x3 = v4.w;
+        } else {
+          if (gr < rows) x0 = src[0];
+          if (gr + 1 < rows) x1 = src[1];
+          if (gr + 2 < rows) x2 = src[2];
+          if (gr + 3 < rows) x3 = src[3];
+        }
+      }
+    } else {
+      if (gr < rows) {
+        const float* src = P + (int64_t)gr * ld + gk;
+        if (vec && gk + 3 < k_lim) {
+          const float4 v4 = *reinterpret_cast<const float4*>(src);
+          x0 = v4.x; x1 = v4.y; x2 = v4.z; x3 = v4.w;
+        } else {
+          if (gk < k_lim) x0 = src[0];
+          if (gk + 1 < k_lim) x1 = src[1];
+          if (gk + 2 < k_lim) x2 = src[2];
+          if (gk + 3 < k_lim) x3 = src[3];
+        }
+      }
+    }
+    t.v[4 * q] = x0; t.v[4 * q + 1] = x1; t.v[4 * q + 2] = x2; t.v[4 * q + 3] = x3;
+  }
+}
+
+template <bool KM>
+__device__ __forceinline__ void store_tile64(float (*S)[G64 + GPAD], const Tile64& t) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int f = tid + G64T * q;
+    if (KM) {
+      const int k = f >> 4, r = (f & 15) * 4;
+      *reinterpret_cast<float4*>(&S[k][r]) = make_float4(t.v[4 * q], t.v[4 * q + 1], t.v[4 * q + 2], t.v[4 * q + 3]);
+    } else {
+      const int r = f >> 3, k = (f & 7) * 4;
+      S[k][r] = t.v[4 * q];
+      S[k + 1][r] = t.v[4 * q + 1];
+      S[k + 2][r] = t.v[4 * q + 2];
+      S[k + 3][r] = t.v[4 * q + 3];
+    }
+  }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm64_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                     float* __restrict__ Cm, const float* __restrict__ bias, int M,
+                                                     int N, int K, int act, float beta_c) {
+  __shared__ __attribute__((aligned(16))) float As[2][32][G64 + GPAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][32][G64 + GPAD];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int m0 = blockIdx.y * G64, n0 = blockIdx.x * G64;
+  const int wm = (wid >> 1) * 32, wn = (wid & 1) * 32;
+  const int S = gridDim.z;
+  const int kchunk = ((K + S - 1) / S + 31) / 32 * 32;
+  const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+  if (S > 1) Cm += (int64_t)blockIdx.z * M * N;
+  const bool va = (TA ? (M % 4 == 0) : (K % 4 == 0)) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  const bool vb = (TB ? (K % 4 == 0) : (N % 4 == 0)) && ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+  const int li = lane & 31, lh = lane >> 5;
+  Tile64 ra, rb;
+  int buf = 0;
+  if (kb < ke) {
+    load_tile64<TA>(A, TA ? M : K, M, ke, m0, kb, va, ra);
+    load_tile64<!TB>(B, TB ? K : N, N, ke, n0, kb, vb, rb);
+    store_tile64<TA>(As[0], ra);
+    store_tile64<!TB>(Bs[0], rb);
+  }
+  __syncthreads();
+  for (int k0 = kb; k0 < ke; k0 += 32) {
+    const bool more = k0 + 32 < ke;
+    if (more) {
+      load_tile64<TA>(A, TA ? M : K, M, ke, m0, k0 + 32, va, ra);
+      load_tile64<!TB>(B, TB ? K : N, N, ke, n0, k0 + 32, vb, rb);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const int kk = 2 * s2 + lh;
+      acc = mfma32(As[buf][kk][wm + li], Bs[buf][kk][wn + li], acc);
+    }
+    if (more) {
+      store_tile64<TA>(As[buf ^ 1], ra);
+      store_tile64<!TB>(Bs[buf ^ 1], rb);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int i = m0 + wm + (e & 3) + 8 * (e >> 2) + 4 * lh;
+    const int j = n0 + wn + li;
+    if (i < M && j < N) {
+      float v = acc[e];
+      if (S > 1) {
+        Cm[(int64_t)i * N + j] = v;
+        continue;
+      }
+      if (beta_c != 0.0f) v += beta_c * Cm[(int64_t)i * N + j];
+      if (bias) v += bias[j];
+      if (act == 1) v = fmaxf(v, 0.0f);
+      else if (act == 2) v = tanhf(v);
+      Cm[(int64_t)i * N + j] = v;
+    }
+  }
+}
+
 // Skinny outputs (N <= 8, e.g. the MLP's 2-class output layer): C[M][N] =
 // act(A[M][K] B[N][K]^T + bias).  A 128 x 128 MFMA tile would compute 64x
 // more zeros than results (45 us for 8192 x 2 x 512); here one wave per row
@@ -1383,16 +1520,39 @@ H2OMX_API int h2omx_kmeans(const float* X, int64_t ld, int64_t n, int d, const f
   return launch_status();
 }
 
-H2OMX_API int h2omx_gemm(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int ta,
-                         int tb, int act, float beta_c, int splitk, float* ws, hipStream_t stream) {
-  if (splitk < 1 || (splitk > 1 && !ws)) return kBadArg;
+// tile edge of the fp32 GEMM: 0 = by shape (64 when 128-tiles leave CUs short of work), 64, 128
+static int g_gemm_tile = 0;
+H2OMX_API int h2omx_gemm_set_tile(int tile) {
+  if (tile != 0 && tile != 64 && tile != 128) return kBadArg;
+  g_gemm_tile = tile;
+  return kOk;
+}
+
+static void launch_gemm(const float* A, const float* B, float* out, const float* bias, int M, int N, int K, int ta,
+                        int tb, int act, float beta_c, int splitk, hipStream_t stream) {
+  const int64_t tiles128 = (int64_t)cdiv(N, GB) * cdiv(M, GB) * splitk;
+  const bool t64 = g_gemm_tile == 64 || (g_gemm_tile == 0 && tiles128 < 512);
+  if (t64) {
+    const dim3 grid(cdiv(N, G64), cdiv(M, G64), splitk), blk(G64T);
+    if (!ta && !tb) hipLaunchKernelGGL((gemm64_kernel<false, false>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+    else if (!ta && tb) hipLaunchKernelGGL((gemm64_kernel<false, true>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+    else if (ta && !tb) hipLaunchKernelGGL((gemm64_kernel<true, false>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+    else hipLaunchKernelGGL((gemm64_kernel<true, true>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+    return;
+  }
   const dim3 grid(cdiv(N, GB), cdiv(M, GB), splitk);
-  float* out = splitk > 1 ? ws : C;
   const dim3 blk(GTHREADS);
   if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
   else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
   else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
   else hipLaunchKernelGGL((gemm_kernel<true, true>), grid, blk, 0, stream, A, B, out, bias, M, N, K, act, beta_c);
+}
+
+H2OMX_API int h2omx_gemm(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int ta,
+                         int tb, int act, float beta_c, int splitk, float* ws, hipStream_t stream) {
+  if (splitk < 1 || (splitk > 1 && !ws)) return kBadArg;
+  float* out = splitk > 1 ? ws : C;
+  launch_gemm(A, B, out, bias, M, N, K, ta, tb, act, beta_c, splitk, stream);
   if (splitk > 1)
     hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(cdiv((int64_t)M * N, 256) < 4096 ? cdiv((int64_t)M * N, 256) : 4096),
                        dim3(256), 0, stream, ws, splitk, M, N, C, bias, act, beta_c);
@@ -1428,8 +1588,7 @@ H2OMX_API int h2omx_act_backward_bias(const float* Y, float* dY, float* ws, int 
 H2OMX_API int h2omx_gemm_wgrad_bias(const float* A, const float* B, float* C, int M, int N, int K, int splitk,
                                     float* ws, const float* bws, int bsplits, int bn, float* db, hipStream_t stream) {
   if (splitk < 2 || !ws || !bws || !db) return kBadArg;
-  const dim3 grid(cdiv(N, GB), cdiv(M, GB), splitk);
-  hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(GTHREADS), 0, stream, A, B, ws, nullptr, M, N, K, 0, 0.0f);
+  launch_gemm(A, B, ws, nullptr, M, N, K, 1, 0, 0, 0.0f, splitk, stream);
   const int mb = cdiv((int64_t)M * N, 256) < 4096 ? (int)cdiv((int64_t)M * N, 256) : 4096;
   hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(mb + cdiv(bn, 64)), dim3(256), 0, stream, ws, splitk, M, N, C,
                      nullptr, 0, 0.0f, mb, bws, bsplits, bn, db);

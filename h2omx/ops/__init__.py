@@ -67,6 +67,7 @@ DENSE_SIGS = {
     "h2omx_gemm": "PPPPIIIIIIFIPS",
     "h2omx_act_backward": "PPLIS",
     "h2omx_gemm_skinny_nt": "PPPPIIIIS",
+    "h2omx_gemm_set_tile": "I",
     "h2omx_gemm_thin_k": "PPPLIIPIS",
     "h2omx_act_backward_bias": "PPPIIIIS",
     "h2omx_gemm_wgrad_bias": "PPPIIIIPPIIPS",

@@ -249,6 +249,12 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
     return C
 
 
+def set_gemm_tile(tile: int) -> None:
+    """fp32 GEMM tile edge: 0 = by shape (64 x 64 when 128 x 128 tiles would
+    leave CUs short of work), 64 or 128 (tests / tuning)."""
+    check(dense_lib().h2omx_gemm_set_tile(int(tile)), "gemm_set_tile")
+
+
 def _splitk(M: int, N: int, K: int) -> int:
     """split-K when the output has too few 128x128 tiles to fill 256 CUs
     (weight gradients: [out][in] outputs with K = batch rows)"""

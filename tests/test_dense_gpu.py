@@ -178,3 +178,29 @@ def test_act_backward_bias_and_wgrad(cuda_dev, M, out, inp, act):
     D.wgrad_bias(dZ, H, dW, db, bpart)
     assert torch.allclose(dW.double().cpu(), dZr.T @ H.double().cpu(), rtol=1e-4, atol=2e-2)
     assert torch.allclose(db.double().cpu(), dZr.sum(0), atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb", [(8192, 512, 512, False, True), (8192, 512, 512, False, False),
+                                         (512, 512, 8192, True, False), (1000, 300, 77, False, False),
+                                         (130, 70, 5000, True, True)])
+def test_gemm_64_tiles_bit_identical_to_128(cuda_dev, M, N, K, ta, tb):
+    """The 64 x 64-tile kernel keeps each element's k-ordered fmaf chain (and
+    the split-K chunking) of the 128 x 128 one: bit-identical outputs."""
+    from h2omx.ops import dense as OD
+
+    torch.manual_seed(6)
+    A = torch.randn((K, M) if ta else (M, K), device=cuda_dev)
+    B = torch.randn((N, K) if tb else (K, N), device=cuda_dev)
+    bias = None if ta else torch.randn(N, device=cuda_dev)
+    out = {}
+    try:
+        for tile in (128, 64):
+            OD.set_gemm_tile(tile)
+            out[tile] = D.gemm(A, B, bias, 0 if ta else 1, ta, tb)
+    finally:
+        OD.set_gemm_tile(0)
+    assert torch.equal(out[64], out[128])
+    ref = (A.T if ta else A).double() @ (B.T if tb else B).double()
+    if bias is not None:
+        ref = (ref + bias.double()).clamp_min(0)
+    assert torch.allclose(out[64].double(), ref, rtol=1e-4, atol=2e-2)
