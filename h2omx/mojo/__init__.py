@@ -24,8 +24,14 @@ following H2O-3's genmodel layout:
   array (eigenvectors, archetypes, thresholds, coefficients, per-level
   target sums, word vectors, hyperplanes, spline knots / bases, design
   means / scales) as little-endian fp64 ``h2omx/<name>.bin`` with its shape
-  in ``h2omx_shape_<name>`` (h2omx's own payload layout; the genmodel
-  readers for these algorithms use other entry names).
+  in ``h2omx_shape_<name>`` (h2omx's own payload, exact round trip).  pca,
+  isotonicregression, coxph and word2vec ALSO carry the entries the genmodel
+  readers use (PCAMojoReader: ``k``/``eigenvector_size``/``catOffsets``/
+  ``permutation``/``normSub``/``normMul`` + big-endian ``eigenvectors_raw``;
+  IsotonicRegressionMojoReader: ``thresholds_x``/``thresholds_y``/
+  ``min_x``/``max_x``; CoxPHMojoReader: ``coef``/``x_mean_num``/...;
+  Word2VecMojoReader: text ``vocabulary`` + big-endian float ``vectors``), and
+  isotonic / word2vec MOJOs that hold only those entries import.
 
 Binary compatibility with H2O's h2o-genmodel.jar cannot be checked here (no
 JVM or jar in the environment): the layout follows the public format as
@@ -421,6 +427,28 @@ def _uplift_info(model, info, files):
                 auuc_type=str(model.params.get("auuc_type", "AUTO")))
 
 
+def _pca_genmodel(model, info, files):
+    """genmodel PCAMojoReader entries next to the h2omx arrays: DataInfo
+    counts / offsets, numeric normalisation (normSub subtracted, normMul
+    multiplied) and ``eigenvectors_raw`` ([eigenvector_size][k] big-endian
+    fp64, java.nio.ByteBuffer order)."""
+    d = model.design
+    cats, nums = _design_columns(d)
+    offs, o = [0], 0
+    for c in cats:
+        o += len(d.domains[c]) - (0 if d.use_all_levels else 1)
+        offs.append(o)
+    ev = np.asarray(model.eigenvectors, np.float64)
+    ncat_cols = offs[-1]
+    cen = np.asarray(model.center, np.float64)
+    sc = np.asarray(model.scale, np.float64)
+    info.update(use_all_factor_levels=bool(d.use_all_levels), pcaMethod="GramSVD", pca_impl="MTJ_EVD_SYMMMATRIX",
+                eigenvector_size=int(ev.shape[0]), ncats=len(cats), nnums=len(nums), catOffsets=offs,
+                permutation=[model.x.index(c) for c in cats + nums],
+                normSub=cen[ncat_cols:].tolist(), normMul=(1.0 / np.where(sc[ncat_cols:] == 0, 1.0, sc[ncat_cols:])).tolist())
+    files["eigenvectors_raw"] = np.ascontiguousarray(ev, dtype=">f8").tobytes()
+
+
 def _array_info(model, files):
     info: dict = {}
     a = model.algo
@@ -431,6 +459,7 @@ def _array_info(model, files):
         _put(files, info, "scale", model.scale)
         _put(files, info, "eigenvectors", model.eigenvectors)
         info["k"] = int(model.eigenvectors.shape[1])
+        _pca_genmodel(model, info, files)
     elif a == "glrm":
         _put(files, info, "center", model.center)
         _put(files, info, "scale", model.scale)
@@ -441,11 +470,20 @@ def _array_info(model, files):
         _put(files, info, "thresholds_x", model.thresholds_x)
         _put(files, info, "thresholds_y", model.thresholds_y)
         info["out_of_bounds"] = str(model.params["out_of_bounds"])
+        # genmodel IsotonicRegressionMojoReader entries
+        tx = np.asarray(model.thresholds_x, np.float64)
+        info.update(thresholds_x=tx.tolist(), thresholds_y=np.asarray(model.thresholds_y, np.float64).tolist(),
+                    min_x=float(tx.min()) if tx.size else 0.0, max_x=float(tx.max()) if tx.size else 0.0)
     elif a == "upliftdrf":
         _uplift_info(model, info, files)
     elif a == "coxph":
         _put(files, info, "coef", model.beta)
         _put(files, info, "x_mean_num", model.x_mean)
+        # genmodel CoxPHMojoReader key/values (numeric predictors)
+        info.update(coef=np.asarray(model.beta, np.float64).ravel().tolist(),
+                    x_mean_num=np.asarray(model.x_mean, np.float64).ravel().tolist(),
+                    x_mean_cat=[], cat_offsets=[0], cats=0, nums=int(np.asarray(model.x_mean).size),
+                    use_all_factor_levels=bool(model.design.use_all_levels))
     elif a == "targetencoder":
         info["te_columns"] = list(model.columns)
         info["blending"] = bool(model.params["blending"])
@@ -460,9 +498,14 @@ def _array_info(model, files):
             _put(files, info, f"te_counts_{i}", cnts.numpy())
     elif a == "word2vec":
         files["h2omx/vocabulary.txt"] = ("\n".join(model.words) + "\n").encode()
-        _put(files, info, "vectors", model.vectors.float().cpu().numpy())
+        vec = model.vectors.float().cpu().numpy()
+        _put(files, info, "vectors", vec)
         info["vec_size"] = int(model.vectors.shape[1])
         info["vocab_size"] = len(model.words)
+        # genmodel Word2VecMojoReader entries: text "vocabulary", blob "vectors"
+        # (java.nio.ByteBuffer order: big-endian float32, word-major)
+        files["vocabulary"] = ("\n".join(model.words) + "\n").encode()
+        files["vectors"] = np.ascontiguousarray(vec, dtype=">f4").tobytes()
     elif a == "extendedisolationforest":
         _put(files, info, "normals", model.normals)
         _put(files, info, "offsets", model.offs)
@@ -620,7 +663,13 @@ class GenericModel(Model):
                  "isotonicregression": ("thresholds_x", "thresholds_y"), "coxph": ("coef", "x_mean_num"),
                  "extendedisolationforest": ("normals", "offsets", "leaf_sizes"), "gam": ("beta",)}.get(a, ())
         for nm in names:
+            if f"h2omx_shape_{nm}" not in info and a == "isotonicregression":
+                continue   # H2O-written MOJO: genmodel key/values below
             self.arr[nm] = _get(z, info, nm)
+        if a == "isotonicregression" and "thresholds_x" not in self.arr:
+            tx, ty = info["thresholds_x"], info["thresholds_y"]
+            self.arr["thresholds_x"] = np.asarray(tx if isinstance(tx, list) else [tx], np.float64)
+            self.arr["thresholds_y"] = np.asarray(ty if isinstance(ty, list) else [ty], np.float64)
         if a == "targetencoder":
             cols = info["te_columns"]
             self.te_columns = cols if isinstance(cols, list) else [cols]
@@ -641,8 +690,14 @@ class GenericModel(Model):
             self.arr["edges"] = _get(z, info, "uplift_edges").astype(np.float32)
             self.arr["nvb"] = _get(z, info, "uplift_nvb").astype(np.int64)
         if a == "word2vec":
-            self.words = z.read("h2omx/vocabulary.txt").decode().split("\n")[: int(info["vocab_size"])]
-            self.vectors = torch.from_numpy(_get(z, info, "vectors").astype(np.float32))
+            if "h2omx_shape_vectors" in info:
+                self.words = z.read("h2omx/vocabulary.txt").decode().split("\n")[: int(info["vocab_size"])]
+                self.vectors = torch.from_numpy(_get(z, info, "vectors").astype(np.float32))
+            else:   # H2O-written MOJO: genmodel text "vocabulary" + big-endian blob "vectors"
+                nv, vs = int(info["vocab_size"]), int(info["vec_size"])
+                self.words = z.read("vocabulary").decode().split("\n")[:nv]
+                vec = np.frombuffer(z.read("vectors"), dtype=">f4", count=nv * vs).reshape(nv, vs)
+                self.vectors = torch.from_numpy(vec.astype(np.float32))
         if a == "gam":
             dx = info["h2omx_design_x"]
             for n in (dx if isinstance(dx, list) else [dx]):

@@ -117,3 +117,51 @@ def test_glm_ext_mojo(kind, tmp_path):
     fr = Frame.from_pandas(df)
     g = _roundtrip(m, tmp_path)
     np.testing.assert_allclose(g.predict_raw(fr).numpy(), m.predict_raw(fr).numpy(), rtol=1e-4, atol=1e-5)
+
+
+def _genmodel_only(path, out):
+    """Copy of a MOJO without h2omx's own payload (h2omx/* entries, h2omx_* keys):
+    what an H2O-written MOJO of the same model would hold."""
+    import zipfile
+
+    with zipfile.ZipFile(path) as zi, zipfile.ZipFile(out, "w") as zo:
+        for n in zi.namelist():
+            if n.startswith("h2omx/"):
+                continue
+            data = zi.read(n)
+            if n == "model.ini":
+                data = "\n".join(ln for ln in data.decode().split("\n") if not ln.startswith("h2omx_")).encode()
+            zo.writestr(n, data)
+    return out
+
+
+def test_genmodel_entries_import_without_h2omx_payload(tmp_path):
+    """isotonic regression and word2vec MOJOs carry genmodel's entries
+    (thresholds_x/_y key/values; text vocabulary + big-endian vectors blob) and
+    import from those alone; PCA's eigenvectors_raw / normalisation match."""
+    import zipfile
+
+    df = _df()
+    fr = Frame.from_pandas(df)
+    m = H2OIsotonicRegressionEstimator(out_of_bounds="clip").train(x=["a"], y="y", training_frame=fr)
+    g = import_mojo(_genmodel_only(m.download_mojo(str(tmp_path)), str(tmp_path / "iso_gm.zip")))
+    _same(m.predict(fr), g.predict(fr), rtol=1e-6, atol=1e-7)
+
+    rng = np.random.default_rng(0)
+    toks = []
+    for _ in range(300):
+        toks += list(rng.choice([f"w{i}" for i in range(10)], size=5)) + [None]
+    wf = Frame.from_pandas(pd.DataFrame({"w": toks}))
+    w2v = H2OWord2vecEstimator(vec_size=8, epochs=1, min_word_freq=1, seed=1).train(training_frame=wf)
+    g = import_mojo(_genmodel_only(w2v.download_mojo(str(tmp_path)), str(tmp_path / "w2v_gm.zip")))
+    _same(w2v.transform(wf, "AVERAGE"), g.transform(wf, "AVERAGE"))
+
+    pca = H2OPrincipalComponentAnalysisEstimator(k=2, transform="STANDARDIZE").train(x=list("abcd"), training_frame=fr)
+    with zipfile.ZipFile(pca.download_mojo(str(tmp_path))) as z:
+        ini = z.read("model.ini").decode()
+        raw = np.frombuffer(z.read("eigenvectors_raw"), dtype=">f8")
+    kv = dict(ln.split(" = ", 1) for ln in ini.split("\n") if " = " in ln)
+    assert int(kv["k"]) == 2 and int(kv["eigenvector_size"]) == pca.eigenvectors.shape[0]
+    np.testing.assert_array_equal(raw.reshape(pca.eigenvectors.shape), pca.eigenvectors)
+    norm_mul = np.array([float(v) for v in kv["normMul"].strip("[]").split(",")])
+    np.testing.assert_allclose(norm_mul, 1.0 / pca.scale, rtol=1e-12)
