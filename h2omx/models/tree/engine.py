@@ -90,6 +90,8 @@ class HipTreeBuilder:
     # no parent histograms / subtraction); 0 = off.  Multi-rank runs keep the all-reduced
     # subtraction path (direct histograms are rank-local)
     DIRECT_MIN_NODES = int(os.environ.get("H2OMX_DIRECT_MIN_NODES", "1024"))
+    # ... and only when a node has at most this many eligible features on average
+    DIRECT_MAX_ELIG = float(os.environ.get("H2OMX_DIRECT_MAX_ELIG", "32"))
     # direct levels whose average node holds fewer rows than this run one wave per node
     # (seg_direct_wave_kernel, F <= 256) instead of one workgroup per node
     DIRECT_WAVE_ROWS = int(os.environ.get("H2OMX_DIRECT_WAVE_ROWS", "256"))
@@ -577,7 +579,11 @@ class HipTreeBuilder:
             return idx_out, nbuilt is not None
 
         direct = False
-        direct_ok = comm is None and self.DIRECT_MIN_NODES > 0 and F <= 1024
+        # direct mode pays n x (eligible features) per level; the subtraction path
+        # n / 2 x F + nodes x F x bins: direct only for few eligible features (DRF mtries)
+        exp_elig = min(p.mtries, F) if p.mtries > 0 else F * min(1.0, p.col_sample_rate)
+        direct_ok = (comm is None and self.DIRECT_MIN_NODES > 0 and F <= 1024
+                     and exp_elig <= self.DIRECT_MAX_ELIG)
         for d in range(max_depth):
             cur, nxt = d % 2, (d + 1) % 2
             ctl_cur, ctl_nxt = self.ctl[cur], self.ctl[nxt]
