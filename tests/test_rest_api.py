@@ -192,7 +192,7 @@ def test_contributions_and_partial_dependence_rest(conn):
     assert len(tabs[0]["data"][0]) == 5 and tabs[1]["data"][0] == ["x", "y", "z"]
 
 
-def test_errors_and_delete(conn):
+def test_errors_and_delete(conn, csv_path):
     with pytest.raises(H2OResponseError) as e:
         conn.request("GET /3/Frames/nope.hex")
     assert e.value.status == 404 and e.value.payload["__meta"]["schema_type"] == "H2OError"
@@ -201,6 +201,7 @@ def test_errors_and_delete(conn):
     assert e.value.status == 404
     txt = conn.request("GET /metrics", raw=True).decode()
     assert "h2omx_models_built_total" in txt
+    conn.upload_file(csv_path, destination_frame="uploaded.hex")   # may run alone (-k, xdist)
     conn.request("DELETE /3/Frames/uploaded.hex")
     assert not any(f["frame_id"]["name"] == "uploaded.hex" for f in conn.request("GET /3/Frames")["frames"])
     conn.remove_all()
