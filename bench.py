@@ -96,6 +96,7 @@ def _trees(args, comm, torch, np, model):
         comm.barrier()
         setup_s = time.perf_counter() - t_setup
         elapsed = _timed(gb.step, args, comm, torch, dev)
+        gb.flush()   # fused mode: the last tree is applied inside the next step's level 0
         margin = gb.st.Fm[0, : bm.n]
     else:
         # CPU rehearsal (reference tree builder): the boosting loop owns the

@@ -246,6 +246,67 @@ __device__ __forceinline__ uint32_t row_hash(int64_t r, uint32_t salt) {
 // plain path) and every atomic then carries 64 live rows: ceil(live / 64)
 // full-mask atomics instead of 16 mostly-empty ones.  Same adds, same
 // integer histograms (bit-identical).
+struct GradParams {
+  int dist;
+  int apply_tree;      // add the leaf values of `tree` to F first
+  float sample_rate;   // row bagging (1 = off)
+  uint32_t seed;
+  int tree_index;      // index of the NEXT tree (bag seed)
+  float tweedie_power;
+  float quantile_alpha;
+  float huber_delta;
+  long long row_base;   // global index of this rank's first row (bagging hash)
+  int skip_nid;         // 1: leave nid alone (the scan engine treats level 0 / 1 as an implicit root)
+  int pad;
+};
+
+__device__ __forceinline__ void dist_grad(int dist, float f, float y, const GradParams& gp, float& g, float& h) {
+  switch (dist) {
+    case 0: g = f - y; h = 1.0f; break;
+    case 1: {
+      const float pr = 1.0f / (1.0f + __expf(-f));
+      g = pr - y;
+      h = fmaxf(pr * (1.0f - pr), 1e-16f);
+      break;
+    }
+    case 2: { const float mu = __expf(f); g = mu - y; h = fmaxf(mu, 1e-16f); break; }
+    case 3: { const float e = y * __expf(-f); g = 1.0f - e; h = fmaxf(e, 1e-16f); break; }
+    case 4: {
+      const float rho = gp.tweedie_power;
+      const float a = y * __expf((1.0f - rho) * f), b = __expf((2.0f - rho) * f);
+      g = -a + b;
+      h = fmaxf(-(1.0f - rho) * a + (2.0f - rho) * b, 1e-16f);
+      break;
+    }
+    case 5: g = (f > y) ? 1.0f : ((f < y) ? -1.0f : 0.0f); h = 1.0f; break;
+    case 6: g = (y > f) ? -gp.quantile_alpha : (1.0f - gp.quantile_alpha); h = 1.0f; break;
+    case 7: { const float r = f - y; g = fabsf(r) <= gp.huber_delta ? r : copysignf(gp.huber_delta, r); h = 1.0f; break; }
+    default: g = -y; h = 1.0f; break;  // DRF: fit the response directly
+  }
+}
+
+// PKM 5: level 0 with the gradient pass fused in (K2 + K7 + K3).  The tree
+// begins from the PREVIOUS tree's leaves: F += value[~nid] (apply), (g, h)
+// from (F, y) by dist_grad, quantised with scales fixed by the distribution's
+// gradient bounds (|g| <= 1, h <= 1/4 for bernoulli, ...: the host writes the
+// bounds into stat_max instead of reducing per-tree maxima), so the separate
+// boost_update pass and the max reduction disappear.  Group 0 stores F, g, h
+// (exact leaf sums of the final partition) and the 32-bit packed rows.
+constexpr int GF_LDS_NODES = 1024;
+struct GradFuse {
+  float* F;
+  const float* y;
+  const int* nid;          // previous tree's leaf per row (~gid), read when apply
+  const TreeNode* tree;    // previous tree
+  float* g;
+  float* h;
+  int apply;
+  int s_is_h;              // second statistic: h (mode 1) or w = 1 (mode 0)
+  int pk64;                // store 64-bit packed rows (PKM 1 layout) instead of 32-bit (PKM 3)
+  int cap;                 // tree capacity (nodes): <= GF_LDS_NODES values are staged in LDS
+  GradParams gp;
+};
+
 constexpr int CMP_STAGE_BYTES = 2048;   // per wave
 #ifndef H2OMX_HB_PF
 #define H2OMX_HB_PF 1
@@ -259,7 +320,7 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     const int* __restrict__ nvb, const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups,
     int wgpg, int slot_lo, int slot_cnt, const short* __restrict__ slot16, unsigned long long* __restrict__ pk_buf,
     unsigned long long* __restrict__ partials, const PartInfo* __restrict__ part_prev,
-    const int* __restrict__ ctl_prev, int* __restrict__ nid_out, int writer) {
+    const int* __restrict__ ctl_prev, int* __restrict__ nid_out, int writer, GradFuse gf) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
   __shared__ int width_s[256], rep_s[256];
   __shared__ float rcp_s[256];
@@ -286,6 +347,11 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     r = r < 1 ? 1 : (r > 64 ? 64 : r);
     rep_s[fi] = r;
     rcp_s[fi] = 1.0f / (float)r;   // lane % rep without an integer division (lane < 64: exact)
+  }
+  __shared__ float tval_s[PKM == 5 ? GF_LDS_NODES : 1];
+  if constexpr (PKM == 5) {   // previous tree's node values (leaf gathers from LDS)
+    if (gf.apply && gf.cap <= GF_LDS_NODES)
+      for (int j = threadIdx.x; j < gf.cap; j += blockDim.x) tval_s[j] = gf.tree[j].value;
   }
   const float sg = (float)qscale[0], ss = (float)qscale[1];
   const int64_t rb = (int64_t)qscale[7];  // global row offset of this rank (dither)
@@ -412,6 +478,26 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     } else {
       if (!any) continue;
     }
+    // codes of the next HB_PF features are in flight while this feature's
+    // atomics issue (one load per wave in flight starved HBM: ~3 TB/s); the
+    // first ones are issued before the per-row inputs below, so their latency
+    // overlaps the (g, s) loads / gradient chain instead of following it
+    uint32_t pf[HB_PF][ROWS / 4];
+    auto load_codes = [&](int fi, uint32_t* cw) {
+      const uint8_t* cp = codes + (int64_t)(f0 + fi) * npad + r0;
+      if constexpr (ROWS == 16) {
+        const uint4 c4 = *reinterpret_cast<const uint4*>(cp);
+        cw[0] = c4.x; cw[1] = c4.y; cw[2] = c4.z; cw[3] = c4.w;
+      } else {
+        const uint2 c2 = *reinterpret_cast<const uint2*>(cp);
+        cw[0] = c2.x; cw[1] = c2.y;
+      }
+    };
+    if constexpr (!CMP) {
+#pragma unroll
+      for (int q = 0; q < HB_PF; ++q)
+        if (q < nf) load_codes(q, pf[q]);
+    }
     unsigned long long pk[ROWS];
     if constexpr (PKM == 2) {
 #pragma unroll
@@ -430,6 +516,46 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
         for (int k = 0; k < 4; ++k)
           pk[4 * q + k] = ((unsigned long long)(uint32_t)(int)(short)(pw[k] >> 16) << 32) |
                           (unsigned long long)(pw[k] & 0xFFFFu);
+      }
+    } else if constexpr (PKM == 5) {
+#pragma unroll
+      for (int q = 0; q < ROWS / 4; ++q) {
+        const float4 f4 = *reinterpret_cast<const float4*>(gf.F + r0 + 4 * q);
+        const float4 y4 = *reinterpret_cast<const float4*>(gf.y + r0 + 4 * q);
+        int4 n4 = make_int4(-1, -1, -1, -1);
+        if (gf.apply) n4 = *reinterpret_cast<const int4*>(gf.nid + r0 + 4 * q);
+        float fv[4] = {f4.x, f4.y, f4.z, f4.w};
+        const float yv[4] = {y4.x, y4.y, y4.z, y4.w};
+        const int nv[4] = {n4.x, n4.y, n4.z, n4.w};
+        float gv[4], hv[4];
+        uint32_t pw[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t r = r0 + 4 * q + k;
+          gv[k] = 0.f; hv[k] = 0.f; pw[k] = 0u;
+          pk[4 * q + k] = 0ull;
+          if (r >= n_rows) continue;
+          if (gf.apply) fv[k] += (gf.cap <= GF_LDS_NODES) ? tval_s[~nv[k]] : gf.tree[~nv[k]].value;
+          dist_grad(gf.gp.dist, fv[k], yv[k], gf.gp, gv[k], hv[k]);
+          const uint32_t hsh = row_hash(rb + r, salt);
+          const float d1 = (hsh & 0xFFFF) * (1.0f / 65536.0f), d2 = (hsh >> 16) * (1.0f / 65536.0f);
+          const int gq = (int)floorf(fmaf(gv[k], sg, d1));
+          const uint32_t sq = (uint32_t)floorf(fmaf(gf.s_is_h ? hv[k] : 1.0f, ss, d2));
+          pk[4 * q + k] = ((unsigned long long)(uint32_t)gq << 32) | (unsigned long long)sq;
+          pw[k] = ((uint32_t)gq << 16) | (sq & 0xFFFFu);
+        }
+        if (group == 0) {
+          if (gf.apply) *reinterpret_cast<float4*>(gf.F + r0 + 4 * q) = make_float4(fv[0], fv[1], fv[2], fv[3]);
+          *reinterpret_cast<float4*>(gf.g + r0 + 4 * q) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+          *reinterpret_cast<float4*>(gf.h + r0 + 4 * q) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+          if (gf.pk64) {   // deeper levels read PKM 2 rows
+            *reinterpret_cast<ulonglong2*>(pk_buf + r0 + 4 * q) = make_ulonglong2(pk[4 * q], pk[4 * q + 1]);
+            *reinterpret_cast<ulonglong2*>(pk_buf + r0 + 4 * q + 2) = make_ulonglong2(pk[4 * q + 2], pk[4 * q + 3]);
+          } else {         // PKM 4 rows (16-bit fields: the host picked pk32)
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(pk_buf) + r0 + 4 * q) =
+                make_uint4(pw[0], pw[1], pw[2], pw[3]);
+          }
+        }
       }
     } else {
 #pragma unroll
@@ -545,22 +671,6 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
       }
       continue;
     }
-    // codes of the next HB_PF features are in flight while this feature's
-    // atomics issue (one load per wave in flight starved HBM: ~3 TB/s)
-    uint32_t pf[HB_PF][ROWS / 4];
-    auto load_codes = [&](int fi, uint32_t* cw) {
-      const uint8_t* cp = codes + (int64_t)(f0 + fi) * npad + r0;
-      if constexpr (ROWS == 16) {
-        const uint4 c4 = *reinterpret_cast<const uint4*>(cp);
-        cw[0] = c4.x; cw[1] = c4.y; cw[2] = c4.z; cw[3] = c4.w;
-      } else {
-        const uint2 c2 = *reinterpret_cast<const uint2*>(cp);
-        cw[0] = c2.x; cw[1] = c2.y;
-      }
-    };
-#pragma unroll
-    for (int q = 0; q < HB_PF; ++q)
-      if (q < nf) load_codes(q, pf[q]);
     // per-row slot offset into the histogram (-1: nothing to add), once per unit
     int so[ROWS];
 #pragma unroll
@@ -1766,44 +1876,8 @@ __global__ __launch_bounds__(256) void leaf_reduce_kernel(const unsigned long lo
 // dist: 0 gaussian, 1 bernoulli, 2 poisson, 3 gamma, 4 tweedie, 5 laplace,
 //       6 quantile, 7 huber, 8 drf (g = -y, h = 1)
 // ---------------------------------------------------------------------------
-struct GradParams {
-  int dist;
-  int apply_tree;      // add the leaf values of `tree` to F first
-  float sample_rate;   // row bagging (1 = off)
-  uint32_t seed;
-  int tree_index;      // index of the NEXT tree (bag seed)
-  float tweedie_power;
-  float quantile_alpha;
-  float huber_delta;
-  long long row_base;   // global index of this rank's first row (bagging hash)
-  int skip_nid;         // 1: leave nid alone (the scan engine treats level 0 / 1 as an implicit root)
-  int pad;
-};
 
-__device__ __forceinline__ void dist_grad(int dist, float f, float y, const GradParams& gp, float& g, float& h) {
-  switch (dist) {
-    case 0: g = f - y; h = 1.0f; break;
-    case 1: {
-      const float pr = 1.0f / (1.0f + __expf(-f));
-      g = pr - y;
-      h = fmaxf(pr * (1.0f - pr), 1e-16f);
-      break;
-    }
-    case 2: { const float mu = __expf(f); g = mu - y; h = fmaxf(mu, 1e-16f); break; }
-    case 3: { const float e = y * __expf(-f); g = 1.0f - e; h = fmaxf(e, 1e-16f); break; }
-    case 4: {
-      const float rho = gp.tweedie_power;
-      const float a = y * __expf((1.0f - rho) * f), b = __expf((2.0f - rho) * f);
-      g = -a + b;
-      h = fmaxf(-(1.0f - rho) * a + (2.0f - rho) * b, 1e-16f);
-      break;
-    }
-    case 5: g = (f > y) ? 1.0f : ((f < y) ? -1.0f : 0.0f); h = 1.0f; break;
-    case 6: g = (y > f) ? -gp.quantile_alpha : (1.0f - gp.quantile_alpha); h = 1.0f; break;
-    case 7: { const float r = f - y; g = fabsf(r) <= gp.huber_delta ? r : copysignf(gp.huber_delta, r); h = 1.0f; break; }
-    default: g = -y; h = 1.0f; break;  // DRF: fit the response directly
-  }
-}
+
 
 // Block-level max of three non-negative statistics, written (no atomics) to
 // this block's slot of a fixed-size slab; stat_reduce folds the slab.
@@ -2119,8 +2193,10 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
                              int F, int nbt, int fg, int n_groups, int wgpg, int slot_lo, int slot_cnt,
                              int rows_per_lane, int threads, const short* slot16, unsigned long long* pk_buf,
                              int pkm, unsigned long long* partials, const void* part_prev, const int* ctl_prev,
-                             int* nid_out, int writer, hipStream_t stream) {
+                             int* nid_out, int writer, hipStream_t stream, const GradFuse* gfp = nullptr) {
   const bool route = part_prev != nullptr;
+  GradFuse gfz{};
+  if (gfp) gfz = *gfp;
   // pkm bit 3: wave-compacted atomics (CMP; stored rows, 16-row units, <= 64 slots per pass)
   const bool cmp = (pkm & 8) != 0;
   pkm &= 7;
@@ -2130,7 +2206,12 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
   const PartInfo* pp = reinterpret_cast<const PartInfo*>(part_prev);
   if (wgpg % 8 != 0 || npad % 16 != 0 || fg > 256 || threads % 64 != 0 || threads > 1024 || threads < fg)
     return kBadArg;
-  if (pkm < 0 || pkm > 4 || (pkm > 0 && pk_buf == nullptr) || ((pkm == 2 || pkm == 4) && !route && slot16 == nullptr))
+  if (pkm < 0 || pkm > 5 || (pkm > 0 && pk_buf == nullptr) || ((pkm == 2 || pkm == 4) && !route && slot16 == nullptr))
+    return kBadArg;
+  // fused gradient level: implicit root (no node ids), 32-bit packed rows, no compaction / routing
+  if ((pkm == 5) != (gfp != nullptr) || (pkm == 5 && (nid != nullptr || route || cmp || gfz.F == nullptr ||
+                                                      gfz.y == nullptr || gfz.g == nullptr || gfz.h == nullptr ||
+                                                      (gfz.apply && (gfz.nid == nullptr || gfz.tree == nullptr)))))
     return kBadArg;
   const int64_t units = npad / rows_per_lane;
   if ((units + wgpg - 1) / wgpg * rows_per_lane > ROWS_CAP) return kBadArg;  // fixed-point headroom
@@ -2142,7 +2223,7 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
 #define H2OMX_HBK(NB, R, M, RT, C)                                                                           \
   hipLaunchKernelGGL((hist_build_kernel<NB, R, M, RT, C>), dim3(grid), dim3(threads), lds, stream, codes, npad, \
                      g, s2, nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt,  \
-                     slot16, pk_buf, partials, pp, ctl_prev, nid_out, writer)
+                     slot16, pk_buf, partials, pp, ctl_prev, nid_out, writer, gfz)
 #define H2OMX_HB(NB, R)                                            \
   do {                                                             \
     if (pkm == 0) H2OMX_HBK(NB, R, 0, false, false);               \
@@ -2150,6 +2231,7 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
     else if (pkm == 2 && route) H2OMX_HBK(NB, R, 2, true, false);  \
     else if (pkm == 2) H2OMX_HBK(NB, R, 2, false, false);          \
     else if (pkm == 3) H2OMX_HBK(NB, R, 3, false, false);          \
+    else if (pkm == 5) H2OMX_HBK(NB, R, 5, false, false);          \
     else if (route) H2OMX_HBK(NB, R, 4, true, false);              \
     else H2OMX_HBK(NB, R, 4, false, false);                        \
   } while (0)
@@ -2201,6 +2283,24 @@ H2OMX_API int h2omx_hist_build(const uint8_t* codes, int64_t npad, const float* 
   return hist_build_launch(codes, npad, g, s2, nid, link, ctl, nvb, qscale, salt, F, nbt, fg, n_groups, wgpg, slot_lo,
                            slot_cnt, rows_per_lane, threads, slot16, pk_buf, pkm, partials, nullptr, nullptr, nullptr,
                            0, stream);
+}
+
+// Level 0 with the gradient pass fused in (PKM 5, see GradFuse): F / y / the
+// previous tree's leaves -> F, g, h and the 32-bit packed rows.
+H2OMX_API int h2omx_hist_build_grad(const uint8_t* codes, int64_t npad, const int* ctl, const int* nvb,
+                                    const double* qscale, int salt, int F, int nbt, int fg, int n_groups, int wgpg,
+                                    int slot_cnt, int rows_per_lane, int threads, unsigned long long* pk_buf,
+                                    unsigned long long* partials, float* Fm, const float* y, const int* nid_leaf,
+                                    const void* tree, int cap, float* g, float* h, int apply, int s_is_h,
+                                    int pk64, const void* gparams, hipStream_t stream) {
+  if (gparams == nullptr) return kBadArg;
+  GradFuse gf{};
+  gf.F = Fm; gf.y = y; gf.nid = nid_leaf; gf.tree = reinterpret_cast<const TreeNode*>(tree);
+  gf.g = g; gf.h = h; gf.apply = apply; gf.s_is_h = s_is_h; gf.pk64 = pk64; gf.cap = cap;
+  gf.gp = *reinterpret_cast<const GradParams*>(gparams);
+  return hist_build_launch(codes, npad, nullptr, nullptr, nullptr, nullptr, ctl, nvb, qscale, salt, F, nbt, fg,
+                           n_groups, wgpg, 0, slot_cnt, rows_per_lane, threads, nullptr, pk_buf, 5, partials, nullptr,
+                           nullptr, nullptr, 0, stream, &gf);
 }
 
 // Deeper level with the previous level's partition fused in (see ROUTE):

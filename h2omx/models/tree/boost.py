@@ -17,7 +17,8 @@ import torch
 
 from ... import ops
 from .binning import BinnedMatrix
-from .engine import HipTreeBuilder, TreeParams, make_grad_params, tree_capacity, trees_from_bytes
+from .engine import (GRAD_BOUNDS, HipTreeBuilder, TreeParams, grad_bounds_tensor, make_grad_params, tree_capacity,
+                     trees_from_bytes)
 from .structs import TREE_NODE_DTYPE
 
 
@@ -253,8 +254,29 @@ class GpuBooster:
                        quantile_alpha=dist_kw.get("quantile_alpha", 0.5),
                        huber_delta=dist_kw.get("huber_delta", 1.0))
         self.t = 0
-        if self.K == 1:
+        # K == 1 with bounded gradients: each tree's level 0 applies the previous
+        # tree and computes the gradients itself (no boost_update pass); the
+        # margins then lag one tree until flush()
+        self.fused = (self.K == 1 and self.builder.can_fuse_grad(self.dist, self.st.w is not None, sample_rate))
+        self.pending = False
+        # bounded gradients (unweighted rows; bagging only zeroes rows) quantise with
+        # the bound scales on every path, fused or not
+        self._bounds = None
+        if self.K == 1 and self.st.w is None and self.dist in GRAD_BOUNDS:
+            self._bounds = grad_bounds_tensor(self.dist, self.dev)
+        if self.fused:
+            pass
+        elif self.K == 1:
             self._update(apply=False, next_tree=0, k=0)
+
+    def flush(self):
+        """Bring the margins up to date (fused mode applies each tree inside the
+        next tree's first level)."""
+        if self.pending:
+            b = self.builder
+            ops.check(self.lib.h2omx_apply_tree(ops.P(self.st.Fm[0]), self.bm.n, ops.P(b.nid), ops.P(b.tree_buf),
+                                                ops.stream(self.dev)), "apply_tree")
+            self.pending = False
 
     def _update(self, apply: bool, next_tree: int, k: int, dist=None):
         P, st, b = ops.P, self.st, self.builder
@@ -268,11 +290,19 @@ class GpuBooster:
                                                   P(self.wout), P(b.stat_slab), ops.stream(self.dev)),
                       "boost_update")
             b.reduce_stats()
+            if self._bounds is not None and k == 0 and self.K == 1:
+                b.stat_max.copy_(self._bounds)
 
     def step(self):
         P, st, b, bm, t = ops.P, self.st, self.builder, self.bm, self.t
         fmask = _tree_fmask(self.tp, bm.F, t, self.dev)
-        if self.K == 1:
+        if self.K == 1 and self.fused:
+            gp = make_grad_params(self.dist, False, 1.0, self.seed, t, row_base=b.row_base, **self.kw)
+            gf = dict(F=st.Fm[0], y=st.y, apply=self.pending, gp=gp, bounds=self._bounds)
+            b.build(st.g[0], st.h[0], None, t, fmask, grad_fuse=gf)
+            self.pending = True
+            self.trees_dev.append(self._snapshot())
+        elif self.K == 1:
             b.build(st.g[0], st.h[0], self.wout, t, fmask)
             self.trees_dev.append(self._snapshot())
             self._update(apply=True, next_tree=t + 1, k=0)
@@ -314,6 +344,7 @@ class GpuBooster:
         return b.tree_buf[: total * TREE_NODE_DTYPE.itemsize].clone()
 
     def finish(self) -> TreeEnsemble:
+        self.flush()
         torch.cuda.synchronize(self.dev)
         if self.builder.timer.enabled:
             self.ens.timings.update({f"gpu_ms_{k}": v for k, v in self.builder.timer.totals().items()})
@@ -350,6 +381,7 @@ class _GpuView:
 
     @property
     def margin(self) -> torch.Tensor:
+        self.gb.flush()
         return self.gb.st.Fm[:, : self.gb.bm.n]
 
     def trees(self, lo: int, hi: int) -> np.ndarray:

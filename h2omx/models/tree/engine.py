@@ -317,8 +317,18 @@ class HipTreeBuilder:
         return ctypes.addressof(sp)
 
     # -- one tree ------------------------------------------------------------
+    def can_fuse_grad(self, dist: str, weighted: bool, sample_rate: float) -> bool:
+        """Level 0 can run the gradient pass itself (hist_build PKM 5): scan
+        engine with the implicit root, one tree per iteration, no weights /
+        bagging, and a distribution whose gradients have fixed bounds
+        (GRAD_BOUNDS: every engine quantises those with the bound scales, so
+        fused and separate gradient passes build bit-identical trees)."""
+        return (not self.segmented and self.implicit_root and not weighted
+                and sample_rate >= 1.0 and dist in GRAD_BOUNDS
+                and os.environ.get("H2OMX_FUSE_GRAD", "0") == "1")
+
     def build(self, g: torch.Tensor, h: torch.Tensor, w: torch.Tensor | None, tree_index: int,
-              tree_fmask: torch.Tensor | None = None) -> torch.Tensor:
+              tree_fmask: torch.Tensor | None = None, grad_fuse: dict | None = None) -> torch.Tensor:
         """Grow one tree from per-row (g, h, w).  Preconditions (established by
         the boost / softmax kernels): ``self.nid`` is 0 for rows of the tree and
         INT_MIN for padding; ``self.stat_max`` holds this tree's maxima.
@@ -328,6 +338,9 @@ class HipTreeBuilder:
         if self.segmented:
             return self._build_seg(g, h, w, tree_index, tree_fmask)
         lib, bm, p = self.lib, self.bm, self.p
+        if grad_fuse is not None:
+            # fixed gradient bounds instead of this tree's maxima (see can_fuse_grad)
+            self.stat_max.copy_(grad_fuse["bounds"])
         st = ops.stream(self.dev)
         P = ops.P
         F, nbt = self.F, self.nbt
@@ -335,7 +348,7 @@ class HipTreeBuilder:
         sp = self._sp
         comm = self.comm if (self.comm is not None and self.comm.world_size > 1) else None
 
-        if comm is not None:
+        if comm is not None and grad_fuse is None:   # fused: the bounds are the same on every rank
             comm.all_reduce_(self.stat_max, "max")
         s2 = w if p.mode == 0 else h
         link = [self._buf("link0", 4, torch.int32), None]
@@ -385,6 +398,15 @@ class HipTreeBuilder:
                             self.ROWS_PER_LANE, plan["threads"], P(self.pk), (4 if self.pk32 else 2) + cmp_flag,
                             P(partials), st),
                             "hist_build_route")
+                    elif d == 0 and grad_fuse is not None:
+                        gf = grad_fuse
+                        ops.check(lib.h2omx_hist_build_grad(
+                            P(bm.codes), bm.npad, P(ctl_cur), P(bm.nvb), P(self.qscale), tree_index & 0x7FFFFFFF,
+                            F, nbt, plan["fg"], plan["n_groups"], plan["wgpg"], plan["slot_cnt"],
+                            self.ROWS_PER_LANE, plan["threads"], P(self.pk), P(partials), P(gf["F"]), P(gf["y"]),
+                            P(self.nid), P(self.tree_buf), self.capacity, P(g), P(h), 1 if gf["apply"] else 0,
+                            0 if p.mode == 0 else 1, 0 if self.pk32 else 1, ctypes.addressof(gf["gp"]), st),
+                            "hist_build_grad")
                     elif d > 0 and self.COMPACT:
                         ops.check(lib.h2omx_hist_build_compact(
                             P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]), P(ctl_cur), P(bm.nvb),
@@ -730,6 +752,17 @@ def trees_from_bytes(buf: np.ndarray, capacity: int) -> np.ndarray:
     """View raw bytes as [ntrees][capacity] TREE_NODE_DTYPE records."""
     arr = np.frombuffer(buf.tobytes(), dtype=TREE_NODE_DTYPE)
     return arr.reshape(-1, capacity)
+
+
+# fixed (max|g|, max h, max w) of unweighted rows per distribution: a tree whose
+# level 0 computes the gradients itself quantises with these (can_fuse_grad)
+GRAD_BOUNDS = {"bernoulli": (1.0, 0.25, 1.0), "laplace": (1.0, 1.0, 1.0), "quantile": (1.0, 1.0, 1.0)}
+
+
+def grad_bounds_tensor(dist: str, device) -> torch.Tensor:
+    """stat_max image (float bits as int32) of GRAD_BOUNDS[dist]"""
+    b = np.array(list(GRAD_BOUNDS[dist]) + [0.0], np.float32).view(np.int32)
+    return torch.from_numpy(b.copy()).to(device)
 
 
 def make_grad_params(dist: str, apply_tree: bool, sample_rate: float, seed: int, tree_index: int,

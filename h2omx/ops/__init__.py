@@ -22,6 +22,7 @@ TREE_SIGS = {
     "h2omx_hist_reduce": "PIIIIIIIPPS",
     "h2omx_hist_build_compact": "PLPPPPPPPIIIIIIIIIIPS",
     "h2omx_hist_build_route": "PLPPPPIPPPIIIIIIIIIPIPS",
+    "h2omx_hist_build_grad": "PLPPPIIIIIIIIIPPPPPPIPPIIIPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
     "h2omx_level_finalize": "PPPPPPIIPPPIPIPS",
     "h2omx_split_level": "PPPPPPPPPIIPPPPIPPPIS",
