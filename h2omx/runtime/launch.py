@@ -45,6 +45,32 @@ def free_port(host: str = "127.0.0.1") -> int:
     return p
 
 
+def free_ports(k: int = 2, host: str = "127.0.0.1") -> list[int]:
+    """``k`` distinct ports, all bound at once while choosing (so none repeats);
+    the first is a rendezvous port whose successor (the command bus,
+    ClusterConfig.bus_port) is free too."""
+    held, out = [], []
+    try:
+        while len(out) < k:
+            s = socket.socket()
+            s.bind((host, 0))
+            held.append(s)
+            p = s.getsockname()[1]
+            if not out:
+                t = socket.socket()
+                try:
+                    t.bind((host, p + 1))
+                except OSError:
+                    t.close()
+                    continue
+                held.append(t)
+            out.append(p)
+    finally:
+        for s in held:
+            s.close()
+    return out
+
+
 def rank_env(base: dict, local_rank: int, nproc: int, rank_base: int, world: int, master_addr: str | None,
              master_port: int | None) -> dict:
     """Child environment.  ``master_addr=None``: the global rank / world /
@@ -78,7 +104,7 @@ def spawn_ranks(cmd: list[str], nproc: int, *, rank_base: int = 0, world: int | 
     world = nproc if world is None else world
     port = None
     if master_addr is not None:
-        port = master_port or free_port(master_addr if master_addr != "0.0.0.0" else "127.0.0.1")
+        port = master_port or free_ports(1, master_addr if master_addr != "0.0.0.0" else "127.0.0.1")[0]
     base = dict(os.environ if env is None else env)
     procs = [subprocess.Popen(cmd, env=rank_env(base, i, nproc, rank_base, world, master_addr, port))
              for i in range(nproc)]

@@ -100,8 +100,9 @@ def two_node_cloud(tmp_path_factory):
     df["y"] = np.where(rng.random(n) < 1 / (1 + np.exp(-s)), "1", "0")
     csv = d / "train.csv"
     df.to_csv(csv, index=False)
-    rest = _free_port()
-    mport = _free_port()
+    from h2omx.runtime.launch import free_ports
+
+    mport, rest = free_ports(2)   # mport + 1 (the command bus) is free as well
     procs = []
     for rank in (0, 1):
         env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(mport),

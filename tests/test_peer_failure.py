@@ -106,7 +106,9 @@ def test_frozen_rank_fails_leader_job_within_bound(tmp_path):
     df["y"] = np.where(rng.random(n) < 1 / (1 + np.exp(-(df.x0 - df.x1))), "1", "0")
     csv = tmp_path / "train.csv"
     df.to_csv(csv, index=False)
-    rest, mport = _free_port(), _free_port()
+    from h2omx.runtime.launch import free_ports
+
+    mport, rest = free_ports(2)
     procs = []
     for rank in (0, 1):
         env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(mport),
