@@ -31,7 +31,13 @@ following H2O-3's genmodel layout:
   IsotonicRegressionMojoReader: ``thresholds_x``/``thresholds_y``/
   ``min_x``/``max_x``; CoxPHMojoReader: ``coef``/``x_mean_num``/...;
   Word2VecMojoReader: text ``vocabulary`` + big-endian float ``vectors``), and
-  isotonic / word2vec MOJOs that hold only those entries import.
+  isotonic / word2vec MOJOs that hold only those entries import.  glrm and
+  targetencoder also write their genmodel entries (GlrmMojoReader:
+  ``ncolA``/``ncolY``/``nrowY``/``cat_offsets``/``norm_sub``/``norm_mul`` +
+  text ``losses`` + big-endian ``archetypes``; TargetEncoderMojoReader:
+  ``with_blending``/``non_predictors`` + ``feature_engineering/
+  target_encoding/encoding_map.ini`` and its NA-presence / column maps), and
+  target-encoder MOJOs import from the encoding map alone.
 
 Binary compatibility with H2O's h2o-genmodel.jar cannot be checked here (no
 JVM or jar in the environment): the layout follows the public format as
@@ -449,6 +455,103 @@ def _pca_genmodel(model, info, files):
     files["eigenvectors_raw"] = np.ascontiguousarray(ev, dtype=">f8").tobytes()
 
 
+def _glrm_genmodel(model, info, files):
+    """genmodel GlrmMojoReader entries: A / Y / X dimensions, regulariser and
+    initialisation, DataInfo layout (categoricals first: ``num_categories``,
+    ``cat_offsets``, ``cols_permutation``), the numeric normalisation
+    (``norm_sub`` subtracted, ``norm_mul`` multiplied), one loss per original
+    column in the text entry ``losses`` and the archetypes as ``archetypes``
+    ([nrowY][ncolY] big-endian fp64, java.nio.ByteBuffer order)."""
+    d, p = model.design, model.params
+    cats, nums = _design_columns(d)
+    offs, o = [0], 0
+    for c in cats:
+        o += len(d.domains[c]) - (0 if d.use_all_levels else 1)
+        offs.append(o)
+    Y = np.asarray(model.Y, np.float64)
+    ncat_cols = offs[-1]
+    cen = np.asarray(model.center, np.float64)
+    sc = np.asarray(model.scale, np.float64)
+    info.update(ncolA=len(d.x), ncolY=int(Y.shape[1]), nrowY=int(Y.shape[0]), regularizationX=str(p["regularization_x"]),
+                gammaX=float(p["gamma_x"]), initialization=str(p["init"]), num_categories=len(cats),
+                num_numeric=len(nums), cat_offsets=offs, cols_permutation=[d.x.index(c) for c in cats + nums],
+                norm_sub=cen[ncat_cols:].tolist(),
+                norm_mul=(1.0 / np.where(sc[ncat_cols:] == 0, 1.0, sc[ncat_cols:])).tolist(),
+                transposed=False, reverse_transform=True, seed=int(p.get("seed") or -1),
+                max_iterations=int(p["max_iterations"]))
+    files["losses"] = ("\n".join([str(p["multi_loss"])] * len(cats) + [str(p["loss"])] * len(nums)) + "\n").encode()
+    files["archetypes"] = np.ascontiguousarray(Y, dtype=">f8").tobytes()
+
+
+TE_DIR = "feature_engineering/target_encoding/"
+
+
+def _te_genmodel(model, info, files):
+    """genmodel TargetEncoderMojoReader entries: ``with_blending`` /
+    ``non_predictors`` key/values, the per-column encoding map
+    (``[col]`` sections of ``level = numerator denominator [targetClass]``,
+    the NA level last), the NA-presence map and the input -> output column
+    mappings.  Multinomial rows carry the class index (1..K-1) as H2O's."""
+    p = model.params
+    info.update(with_blending=bool(p["blending"]),
+                non_predictors=";".join(c for c in (model.y, p.get("fold_column"), p.get("weights_column")) if c))
+    enc, na = [], []
+    for c in model.columns:
+        sums, cnts, _ = model.stats[c]
+        s, n = sums.double().numpy(), cnts.double().numpy()
+        enc.append(f"[{c}]")
+        for lv in range(n.size):
+            if n[lv] == 0 and lv == n.size - 1:
+                continue        # no NA level seen in training
+            if model.classes is None:
+                enc.append(f"{lv} = {_fmt(float(s[lv, 0]))} {_fmt(float(n[lv]))}")
+            else:
+                enc.extend(f"{lv} = {_fmt(float(s[lv, k]))} {_fmt(float(n[lv]))} {k + 1}" for k in range(s.shape[1]))
+        na.append(f"{c} = {1 if n[-1] > 0 else 0}")
+    files[TE_DIR + "encoding_map.ini"] = ("\n".join(enc) + "\n").encode()
+    files[TE_DIR + "te_column_name_to_missing_values_presence.ini"] = ("\n".join(na) + "\n").encode()
+    frm = "\n".join(f"[from]\n{c}\n[to]\n{c}" for c in model.columns)
+    files[TE_DIR + "input_encoding_columns_map.ini"] = (frm + "\n").encode()
+    outs = "\n".join(f"[from]\n{c}\n[to]\n" + "\n".join(n for n in _te_out_names(c, model.classes))
+                     for c in model.columns)
+    files[TE_DIR + "input_output_columns_map.ini"] = (outs + "\n").encode()
+
+
+def _te_out_names(col, classes):
+    return [f"{col}_te"] if classes is None else [f"{col}_{k}_te" for k in classes]
+
+
+def _te_from_genmodel(z, info, levels: dict):
+    """Per-column (sums [L+1][C], counts [L+1]) and the prior from the genmodel
+    encoding map alone (H2O's prior: total numerator / total denominator)."""
+    text = z.read(TE_DIR + "encoding_map.ini").decode()
+    cols, cur = {}, None
+    for line in text.splitlines():
+        line = line.strip()
+        if not line:
+            continue
+        if line.startswith("[") and line.endswith("]"):
+            cur = line[1:-1]
+            cols[cur] = []
+            continue
+        k, v = line.split("=", 1)
+        parts = v.split()
+        cols[cur].append((int(k), float(parts[0]), float(parts[1]), int(parts[2]) if len(parts) > 2 else 1))
+    C = max((t[3] for rows in cols.values() for t in rows), default=1)
+    out, tot_s, tot_n = {}, np.zeros(C), 0.0
+    for c, rows in cols.items():
+        L = len(levels.get(c) or []) or (max(t[0] for t in rows) if rows else 0)
+        s, n = np.zeros((L + 1, C)), np.zeros(L + 1)
+        for lv, num, den, tc in rows:
+            s[min(lv, L), tc - 1] = num
+            n[min(lv, L)] = den
+        out[c] = (s, n)
+        if not tot_n:
+            tot_s, tot_n = s.sum(0), n.sum()
+    prior = tot_s / tot_n if tot_n else np.zeros(C)
+    return out, prior
+
+
 def _array_info(model, files):
     info: dict = {}
     a = model.algo
@@ -466,6 +569,7 @@ def _array_info(model, files):
         _put(files, info, "archetypes", model.Y)
         info.update(ncolX=int(model.Y.shape[0]), regularization_x=str(model.params["regularization_x"]),
                     gamma_x=float(model.params["gamma_x"]), h2omx_recon_names=list(model.design.names))
+        _glrm_genmodel(model, info, files)
     elif a == "isotonicregression":
         _put(files, info, "thresholds_x", model.thresholds_x)
         _put(files, info, "thresholds_y", model.thresholds_y)
@@ -496,6 +600,7 @@ def _array_info(model, files):
             sums, cnts, _ = model.stats[c]
             _put(files, info, f"te_sums_{i}", sums.numpy())
             _put(files, info, f"te_counts_{i}", cnts.numpy())
+        _te_genmodel(model, info, files)
     elif a == "word2vec":
         files["h2omx/vocabulary.txt"] = ("\n".join(model.words) + "\n").encode()
         vec = model.vectors.float().cpu().numpy()
@@ -670,7 +775,19 @@ class GenericModel(Model):
             tx, ty = info["thresholds_x"], info["thresholds_y"]
             self.arr["thresholds_x"] = np.asarray(tx if isinstance(tx, list) else [tx], np.float64)
             self.arr["thresholds_y"] = np.asarray(ty if isinstance(ty, list) else [ty], np.float64)
-        if a == "targetencoder":
+        if a == "targetencoder" and "h2omx_shape_prior" not in info:
+            # H2O-written MOJO: the genmodel encoding map alone
+            stats, prior = _te_from_genmodel(z, info, self.feature_domains)
+            self.te_columns = list(stats)
+            self.arr["prior"] = prior
+            for i, c in enumerate(self.te_columns):
+                self.arr[f"te_sums_{i}"], self.arr[f"te_counts_{i}"] = stats[c]
+            info.setdefault("blending", bool(info.get("with_blending", False)))
+            info.setdefault("inflection_point", 10.0)
+            info.setdefault("smoothing", 20.0)
+            if prior.size > 1 and self.response_domain:
+                info.setdefault("h2omx_classes", list(self.response_domain)[1:])
+        elif a == "targetencoder":
             cols = info["te_columns"]
             self.te_columns = cols if isinstance(cols, list) else [cols]
             self.arr["prior"] = _get(z, info, "prior")

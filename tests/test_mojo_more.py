@@ -165,3 +165,49 @@ def test_genmodel_entries_import_without_h2omx_payload(tmp_path):
     np.testing.assert_array_equal(raw.reshape(pca.eigenvectors.shape), pca.eigenvectors)
     norm_mul = np.array([float(v) for v in kv["normMul"].strip("[]").split(",")])
     np.testing.assert_allclose(norm_mul, 1.0 / pca.scale, rtol=1e-12)
+
+
+@pytest.mark.parametrize("resp", ["yb", "y", "ym"])
+def test_target_encoder_genmodel_entries(resp, tmp_path):
+    """TargetEncoder MOJOs carry genmodel's encoding map (``[col]`` sections of
+    ``level = numerator denominator [class]``), NA-presence and column maps,
+    and import from those alone (binomial, regression, multinomial)."""
+    import zipfile
+
+    df = _df()
+    rng = np.random.default_rng(4)
+    df["ym"] = pd.Categorical(rng.choice(["u", "v", "w"], len(df)))
+    df.loc[::11, "g"] = np.nan
+    fr = Frame.from_pandas(df)
+    m = H2OTargetEncoderEstimator(noise=0.0, blending=True).train(x=["g"], y=resp, training_frame=fr)
+    path = m.download_mojo(str(tmp_path))
+    with zipfile.ZipFile(path) as z:
+        enc = z.read("feature_engineering/target_encoding/encoding_map.ini").decode().split("\n")
+        na = z.read("feature_engineering/target_encoding/te_column_name_to_missing_values_presence.ini").decode()
+    assert enc[0] == "[g]" and na.strip() == "g = 1"
+    sums, cnts, _ = m.stats["g"]
+    lv, rest = enc[1].split(" = ")
+    assert int(lv) == 0 and float(rest.split()[1]) == float(cnts[0])
+    g = import_mojo(_genmodel_only(path, str(tmp_path / "te_gm.zip")))
+    got, exp = g.predict(fr).to_pandas(), m.transform(fr).to_pandas()
+    te_cols = [c for c in got.columns if c.endswith("_te")]
+    assert te_cols and all(c in exp.columns for c in te_cols)
+    np.testing.assert_allclose(got[te_cols].to_numpy(float), exp[te_cols].to_numpy(float), rtol=1e-9, atol=1e-12)
+
+
+def test_glrm_genmodel_entries(tmp_path):
+    """GLRM MOJOs carry GlrmMojoReader's dimensions, DataInfo layout, losses
+    text and the big-endian archetypes blob."""
+    import zipfile
+
+    fr = Frame.from_pandas(_df())
+    m = H2OGeneralizedLowRankEstimator(k=2, init="SVD", max_iterations=20).train(x=list("abcdg"), training_frame=fr)
+    with zipfile.ZipFile(m.download_mojo(str(tmp_path))) as z:
+        ini = z.read("model.ini").decode()
+        Y = np.frombuffer(z.read("archetypes"), dtype=">f8")
+        losses = z.read("losses").decode().split()
+    kv = dict(ln.split(" = ", 1) for ln in ini.split("\n") if " = " in ln)
+    assert (int(kv["nrowY"]), int(kv["ncolY"])) == m.Y.shape and int(kv["ncolA"]) == 5
+    np.testing.assert_array_equal(Y.reshape(m.Y.shape), m.Y)
+    assert int(kv["num_categories"]) == 1 and kv["cat_offsets"] == f"[0, {m.Y.shape[1] - 4}]"
+    assert losses == ["Categorical"] + ["Quadratic"] * 4
