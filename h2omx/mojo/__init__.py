@@ -37,7 +37,9 @@ following H2O-3's genmodel layout:
   text ``losses`` + big-endian ``archetypes``; TargetEncoderMojoReader:
   ``with_blending``/``non_predictors`` + ``feature_engineering/
   target_encoding/encoding_map.ini`` and its NA-presence / column maps), and
-  target-encoder MOJOs import from the encoding map alone.
+  target-encoder MOJOs import from the encoding map alone; extended isolation
+  forests write genmodel's per-tree ``trees/tNN.bin`` (node number, ``'N'``
+  normal + intercept point or ``'L'`` row count) and import from those.
 
 Binary compatibility with H2O's h2o-genmodel.jar cannot be checked here (no
 JVM or jar in the environment): the layout follows the public format as
@@ -483,6 +485,55 @@ def _glrm_genmodel(model, info, files):
     files["archetypes"] = np.ascontiguousarray(Y, dtype=">f8").tobytes()
 
 
+EIF_NODE, EIF_LEAF = ord("N"), ord("L")
+
+
+def eif_encode_tree(normals: np.ndarray, offs: np.ndarray, sizes: np.ndarray) -> bytes:
+    """One extended-isolation tree in genmodel's CompressedIsolationTree byte
+    layout (little-endian): ``int32 p`` (branching-array length), then every
+    reachable heap node in index order as ``int32 nodeNumber | u8 type`` and
+    for ``'N'`` the normal ``n`` and an intercept point ``p`` (p doubles each;
+    a row goes left when ``(x - p) . n <= 0``), for ``'L'`` ``int32 numRows``.
+    h2omx stores the offset ``b`` (left when ``x . n <= b``); the point
+    ``p = b n / |n|^2`` lies on that hyperplane, so both rules agree."""
+    p = normals.shape[1]
+    out = [struct.pack("<i", p)]
+    stack, nodes = [0], []
+    while stack:
+        i = stack.pop()
+        nodes.append(i)
+        if sizes[i] < 0:
+            stack += [2 * i + 1, 2 * i + 2]
+    for i in sorted(nodes):
+        if sizes[i] >= 0:
+            out.append(struct.pack("<iBi", i, EIF_LEAF, int(sizes[i])))
+        else:
+            n = normals[i].astype(np.float64)
+            pt = n * (float(offs[i]) / max(float(n @ n), 1e-300))
+            out.append(struct.pack("<iB", i, EIF_NODE) + n.astype("<f8").tobytes() + pt.astype("<f8").tobytes())
+    return b"".join(out)
+
+
+def eif_decode_tree(data: bytes, cap: int):
+    """Inverse of :func:`eif_encode_tree` into heap arrays (normals [cap][p],
+    offsets [cap] with ``b = p . n``, leaf sizes [cap], -1 inner)."""
+    (p,) = struct.unpack_from("<i", data, 0)
+    normals, offs, sizes = np.zeros((cap, p), np.float32), np.zeros(cap, np.float32), np.full(cap, -1.0, np.float32)
+    o = 4
+    while o < len(data):
+        i, typ = struct.unpack_from("<iB", data, o)
+        o += 5
+        if typ == EIF_LEAF:
+            sizes[i] = struct.unpack_from("<i", data, o)[0]
+            o += 4
+        else:
+            n = np.frombuffer(data, "<f8", p, o)
+            pt = np.frombuffer(data, "<f8", p, o + 8 * p)
+            normals[i], offs[i] = n, float(pt @ n)
+            o += 16 * p
+    return normals, offs, sizes
+
+
 TE_DIR = "feature_engineering/target_encoding/"
 
 
@@ -617,6 +668,8 @@ def _array_info(model, files):
         _put(files, info, "leaf_sizes", model.sizes)
         info.update(limit=int(model.limit), sample_size=int(model.sample_size), ntrees=int(model.normals.shape[0]),
                     extension_level=int(model.params["extension_level"]))
+        for t in range(model.normals.shape[0]):
+            files[f"trees/t{t:02d}.bin"] = eif_encode_tree(model.normals[t], model.offs[t], model.sizes[t])
     elif a == "gam":
         _design_info(model.design, info, files)
         _put(files, info, "beta", model.beta_std)      # standardised scale (design.transform)
@@ -762,13 +815,26 @@ class GenericModel(Model):
     def _load_arrays(self, z, info):
         a = self.mojo_algo
         self.arr = {}
-        if a in ("pca", "glrm", "coxph", "extendedisolationforest"):
+        eif_gm = a == "extendedisolationforest" and "h2omx_shape_normals" not in info
+        if eif_gm:
+            # H2O-written MOJO: numeric predictors in [columns] order, trees/tNN.bin only
+            from ..models.glm import DesignInfo
+
+            self.design = DesignInfo(self.x, self.feature_types, self.feature_domains, False)
+            self.design.means = np.zeros(len(self.design.names))
+            ss = int(info["sample_size"])
+            info.setdefault("limit", int(np.ceil(np.log2(max(ss, 2)))))
+            cap = (1 << (int(info["limit"]) + 1)) - 1
+            trees = [eif_decode_tree(z.read(f"trees/t{t:02d}.bin"), cap) for t in range(int(info["ntrees"]))]
+            for j, nm in enumerate(("normals", "offsets", "leaf_sizes")):
+                self.arr[nm] = np.stack([t[j] for t in trees])
+        elif a in ("pca", "glrm", "coxph", "extendedisolationforest"):
             self.design = self._design(z, info)
         names = {"pca": ("center", "scale", "eigenvectors"), "glrm": ("center", "scale", "archetypes"),
                  "isotonicregression": ("thresholds_x", "thresholds_y"), "coxph": ("coef", "x_mean_num"),
                  "extendedisolationforest": ("normals", "offsets", "leaf_sizes"), "gam": ("beta",)}.get(a, ())
         for nm in names:
-            if f"h2omx_shape_{nm}" not in info and a == "isotonicregression":
+            if f"h2omx_shape_{nm}" not in info and (a == "isotonicregression" or eif_gm):
                 continue   # H2O-written MOJO: genmodel key/values below
             self.arr[nm] = _get(z, info, nm)
         if a == "isotonicregression" and "thresholds_x" not in self.arr:

@@ -211,3 +211,15 @@ def test_glrm_genmodel_entries(tmp_path):
     np.testing.assert_array_equal(Y.reshape(m.Y.shape), m.Y)
     assert int(kv["num_categories"]) == 1 and kv["cat_offsets"] == f"[0, {m.Y.shape[1] - 4}]"
     assert losses == ["Categorical"] + ["Quadratic"] * 4
+
+
+def test_eif_genmodel_trees(tmp_path):
+    """Extended isolation forest MOJOs carry one genmodel tree blob per tree
+    (trees/tNN.bin: node number, 'N' normal + intercept point / 'L' row count)
+    and score identically when imported from those blobs alone."""
+    df = _df()
+    fr = Frame.from_pandas(df[list("abd")])
+    m = H2OExtendedIsolationForestEstimator(ntrees=8, extension_level=2, seed=3).train(training_frame=fr)
+    g = import_mojo(_genmodel_only(m.download_mojo(str(tmp_path)), str(tmp_path / "eif_gm.zip")))
+    assert "h2omx_shape_normals" not in g.info
+    _same(m.predict(fr), g.predict(fr), rtol=1e-5, atol=1e-6)
