@@ -284,14 +284,17 @@ class GpuBooster:
                               row_base=self.builder.row_base, **self.kw)
         gp.skip_nid = 1 if getattr(self.builder, "implicit_root", False) else 0
         y = st.ycls[k] if (self.dist == "drf" and self.K > 1) else st.y
+        # bounded gradients: the next build() takes the bounds (stat=), so no
+        # per-block maxima, no maxima reduction and no bounds copy per tree
+        fixed = self._bounds is not None and k == 0 and self.K == 1
         with b.timer.phase("grad"):
             ops.check(self.lib.h2omx_boost_update(P(st.Fm[k]), P(y), P(st.w), self.bm.n, self.bm.npad, P(b.nid),
                                                   P(b.tree_buf), ctypes.addressof(gp), P(st.g[k]), P(st.h[k]),
-                                                  P(self.wout), P(b.stat_slab), ops.stream(self.dev)),
+                                                  P(self.wout), P(None if fixed else b.stat_slab),
+                                                  ops.stream(self.dev)),
                       "boost_update")
-            b.reduce_stats()
-            if self._bounds is not None and k == 0 and self.K == 1:
-                b.stat_max.copy_(self._bounds)
+            if not fixed:
+                b.reduce_stats()
 
     def step(self):
         P, st, b, bm, t = ops.P, self.st, self.builder, self.bm, self.t
@@ -303,8 +306,13 @@ class GpuBooster:
             self.pending = True
             self.trees_dev.append(self._snapshot())
         elif self.K == 1:
-            b.build(st.g[0], st.h[0], self.wout, t, fmask)
-            self.trees_dev.append(self._snapshot())
+            fresh = self.cap <= self.COMPACT_CAP
+            if fresh:
+                # grow the tree straight into its own buffer (no copy afterwards);
+                # the next boost_update applies it from there
+                b.tree_buf = torch.empty_like(b.tree_buf)
+            b.build(st.g[0], st.h[0], self.wout, t, fmask, stat=self._bounds)
+            self.trees_dev.append(b.tree_buf if fresh else self._snapshot())
             self._update(apply=True, next_tree=t + 1, k=0)
         else:
             s = ops.stream(self.dev)

@@ -328,19 +328,22 @@ class HipTreeBuilder:
                 and os.environ.get("H2OMX_FUSE_GRAD", "0") == "1")
 
     def build(self, g: torch.Tensor, h: torch.Tensor, w: torch.Tensor | None, tree_index: int,
-              tree_fmask: torch.Tensor | None = None, grad_fuse: dict | None = None) -> torch.Tensor:
+              tree_fmask: torch.Tensor | None = None, grad_fuse: dict | None = None,
+              stat: torch.Tensor | None = None) -> torch.Tensor:
         """Grow one tree from per-row (g, h, w).  Preconditions (established by
         the boost / softmax kernels): ``self.nid`` is 0 for rows of the tree and
         INT_MIN for padding; ``self.stat_max`` holds this tree's maxima.
         Returns the device tree buffer (``TREE_NODE_DTYPE`` heap of capacity
         nodes; unreachable records are garbage).  ``self.stat_max`` must hold
         this tree's gradient maxima (see :meth:`reduce_stats`)."""
-        if self.segmented:
-            return self._build_seg(g, h, w, tree_index, tree_fmask)
-        lib, bm, p = self.lib, self.bm, self.p
+        # ``stat``: fixed gradient bounds (stat_max image, identical on every rank)
+        # used instead of this tree's maxima: no maxima reduction, no all-reduce
         if grad_fuse is not None:
-            # fixed gradient bounds instead of this tree's maxima (see can_fuse_grad)
-            self.stat_max.copy_(grad_fuse["bounds"])
+            stat = grad_fuse["bounds"]      # see can_fuse_grad
+        smax = self.stat_max if stat is None else stat
+        if self.segmented:
+            return self._build_seg(g, h, w, tree_index, tree_fmask, smax, stat is not None)
+        lib, bm, p = self.lib, self.bm, self.p
         st = ops.stream(self.dev)
         P = ops.P
         F, nbt = self.F, self.nbt
@@ -348,14 +351,14 @@ class HipTreeBuilder:
         sp = self._sp
         comm = self.comm if (self.comm is not None and self.comm.world_size > 1) else None
 
-        if comm is not None and grad_fuse is None:   # fused: the bounds are the same on every rank
-            comm.all_reduce_(self.stat_max, "max")
+        if comm is not None and stat is None:   # fixed bounds are the same on every rank
+            comm.all_reduce_(smax, "max")
         s2 = w if p.mode == 0 else h
         link = [self._buf("link0", 4, torch.int32), None]
         # scales + level-0 control block/link + zeroed leaf sums in one launch
         T = self.timer.phase
         with T("tree_begin"):
-            ops.check(lib.h2omx_tree_begin(P(self.stat_max), p.mode, self.max_rows_per_wg, P(self.qscale),
+            ops.check(lib.h2omx_tree_begin(P(smax), p.mode, self.max_rows_per_wg, P(self.qscale),
                                            P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(),
                                            self.row_base, st), "tree_begin")
         full_prev = None
@@ -500,7 +503,7 @@ class HipTreeBuilder:
         self._final_ctl = final_ctl
         return self.tree_buf
 
-    def _build_seg(self, g, h, w, tree_index, tree_fmask):
+    def _build_seg(self, g, h, w, tree_index, tree_fmask, smax, fixed):
         """Row-partitioned level pipeline (csrc/tree_kernels.hip, "segmented"
         section): each level reads only the rows of the nodes it builds."""
         lib, bm, p = self.lib, self.bm, self.p
@@ -510,8 +513,8 @@ class HipTreeBuilder:
         spp = self._params(tree_index)
         sp = self._sp
         comm = self.comm if (self.comm is not None and self.comm.world_size > 1) else None
-        if comm is not None:
-            comm.all_reduce_(self.stat_max, "max")
+        if comm is not None and not fixed:
+            comm.all_reduce_(smax, "max")
         s2 = w if p.mode == 0 else h
         B = self._buf
         i32 = torch.int32
@@ -519,7 +522,7 @@ class HipTreeBuilder:
         seg = [[B(f"seg_start{k}", 2, i32), B(f"seg_cnt{k}", 2, i32), B(f"hc_first{k}", 3, i32),
                 B(f"pc_first{k}", 3, i32), B(f"slot_node{k}", 2, i32)] for k in (0, 1)]
         built = B("built", self.per_node, torch.int64)
-        ops.check(lib.h2omx_tree_begin_seg(P(self.stat_max), p.mode, self.max_rows_per_wg, P(self.qscale),
+        ops.check(lib.h2omx_tree_begin_seg(P(smax), p.mode, self.max_rows_per_wg, P(self.qscale),
                                            P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(),
                                            P(built), self.per_node, n, self.hc_rows, P(seg[0][0]), P(seg[0][1]),
                                            P(seg[0][2]), P(seg[0][3]), P(seg[0][4]), self.row_base, st),
