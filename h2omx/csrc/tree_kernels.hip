@@ -3873,7 +3873,10 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
     const float* __restrict__ h, const float* __restrict__ w, const double* __restrict__ qs, int cap,
     unsigned long long* __restrict__ leaf_acc, const int8_t* __restrict__ dirb, const float* __restrict__ gin,
     const float* __restrict__ sin, float* __restrict__ gout, float* __restrict__ sout,
-    const uint8_t* __restrict__ ecodes, int ecs, const int* __restrict__ nodeq) {
+    const uint8_t* __restrict__ ecodes, int ecs, const int* __restrict__ nodeq, int segf) {
+  // segf (last level): bit 0 - gin / sin hold g and s2 in segment order (read
+  // them at j instead of gathering g[r] / s2[r] by row: one random 4-byte
+  // gather per row left instead of three); bit 1 - s2 is h (else w)
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int n = ctl[CTL_N];
@@ -3927,10 +3930,13 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
       const int leaf = (pi.child >= 0) ? pi.child_gid + dir : pi.gid;
       nid[r] = ~leaf;
       if (leaf_acc && leaf < cap) {
-        const float wv = w ? w[r] : 1.0f;
+        const bool sg_seg = segf & 1, s_is_h = segf & 2;
+        const float wv = (sg_seg && !s_is_h) ? (sin ? sin[j] : 1.0f) : (w ? w[r] : 1.0f);
         if (wv != 0.0f) {
-          sg[dir] += __float2int_rn(g[r] * lg);
-          sh[dir] += __float2int_rn(h[r] * lh);
+          const float gk = sg_seg ? gin[j] : g[r];
+          const float hk = (sg_seg && s_is_h) ? sin[j] : h[r];
+          sg[dir] += __float2int_rn(gk * lg);
+          sh[dir] += __float2int_rn(hk * lh);
           sw[dir] += __float2int_rn(wv * lw);
         }
       }
@@ -4158,12 +4164,16 @@ H2OMX_API int h2omx_part_scatter(const uint8_t* codes, int64_t npad, const int* 
                                  unsigned long long* leaf_acc, int max_chunks, int wave, const int8_t* dirb,
                                  const float* gin, const float* sin, float* gout, float* sout,
                                  const uint8_t* ecodes, int ecs, const int* nodeq, hipStream_t stream) {
-  if (ecodes && !wave) return kBadArg;
+  // wave: bit 0 wave-granular kernel; bits 1-2 its segf flags (last level)
+  const int segf = wave >> 1;
+  wave &= 1;
+  if ((ecodes || segf) && !wave) return kBadArg;
+  if ((segf & 1) && (!gin || ((segf & 2) && !sin))) return kBadArg;
   if (wave) {
     hipLaunchKernelGGL(part_scatter_wave_kernel, dim3((max_chunks + 3) / 4), dim3(256), 0, stream, codes, npad, idx,
                        idx_out, nid, write_nid, seg_start, seg_cnt, pc_first, pc_off, node_nl, ctl,
                        reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, dirb, gin, sin,
-                       gout, sout, ecodes, ecs, nodeq);
+                       gout, sout, ecodes, ecs, nodeq, segf);
     return launch_status();
   }
   hipLaunchKernelGGL(part_scatter_kernel, dim3(max_chunks), dim3(256), 0, stream, codes, npad, idx, idx_out, nid,

@@ -102,6 +102,7 @@ class HipTreeBuilder:
     DIRECT_CHUNKED = True
     # segmented engine: part_scatter moves each row's (g, s2) into segment order with it
     PERMUTE_GS = True
+    SEG_LEAF_GS = os.environ.get("H2OMX_SEG_LEAF_GS", "1") == "1"
     # direct levels of <= 16 eligible features store them per row for the partition
     ECODES = True
     # levels of more than 8192 nodes finalise in count / scan / write tiles (False: one workgroup)
@@ -588,13 +589,18 @@ class HipTreeBuilder:
                                                        P(cnt_h), P(cnt_p), P(aux), st), "level_close_mb")
                 idx_out = self.idx[d % 2]
             gout = sout = None
+            # last level: leaf sums read (g, s2) in segment order where the previous
+            # scatter left them (SEG_LEAF_GS=0: gather every row's g / h / w by row id)
+            segf = 0
+            if last and pwave and gs["pos"] == 1 and self.SEG_LEAF_GS:
+                segf = 2 | (4 if p.mode != 0 else 0)
             if not last and self.PERMUTE_GS:
                 gout = B(f"gperm{d % 2}", n + 64, torch.float32)
                 sout = None if s2 is None else B(f"sperm{d % 2}", n + 64, torch.float32)
             ops.check(lib.h2omx_part_scatter(P(bm.codes), bm.npad, P(idx_in), P(idx_out), P(self.nid), write_nid,
                                              P(seg_start), P(seg_cnt), P(pc_first), P(pc_left), P(node_nl),
                                              P(ctl_cur), P(part), nbt, P(g), P(h), P(w), P(self.qscale),
-                                             self.capacity, P(self.leaf_acc), max_pc, pwave, P(dirb), P(gs["g"]),
+                                             self.capacity, P(self.leaf_acc), max_pc, pwave | segf, P(dirb), P(gs["g"]),
                                              P(gs["s"]), P(gout), P(sout), P(ecodes), ecs, P(nodeq), st),
                       "part_scatter")
             if gout is not None:
