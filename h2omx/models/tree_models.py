@@ -129,20 +129,32 @@ class _TreeBuilder(ModelBuilder):
         nclass = len(self.response_domain) if self.response_domain else 1
         ens_dist = self._engine_dist(dist)
         init_f = None
+        offset = None
         if self.params.get("offset_column"):
-            raise NotImplementedError("offset_column is not supported by the tree engine yet")
+            # H2O: margin = init_f + offset + trees; init_f fitted with the offset held fixed
+            if ens_dist in ("drf", "multinomial"):
+                raise ValueError(f"offset_column is not supported for {self.algo} / {ens_dist} (as in H2O)")
+            offset = train.vec(self.params["offset_column"]).as_float().to(X.device)
+            if not bool(ok.all()):
+                offset = offset[ok]
         ntrees = int(self.params["ntrees"])
         ckpt = self._checkpoint_ensemble()
+        base_margin = None if ckpt is None else ckpt.raw_margin(X)
         if ckpt is not None:
             # H2O checkpoint: continue a previous model up to `ntrees` total trees
             init_f = None
             ntrees = max(0, ntrees - ckpt.ntrees)
+        if offset is not None:
+            if base_margin is None:
+                init_f = np.array([_offset_init(ens_dist, y, w, offset, self.params, self.comm)], np.float64)
+                base_margin = torch.full((1, offset.numel()), float(init_f[0]), device=offset.device)
+            base_margin = base_margin.to(offset.device) + offset[None, :]
         scorer = _TreeScoring(self, train, valid, X, y, w, ens_dist, nclass, ckpt)
         ens = train_ensemble(bm, y, w, dist=ens_dist, ntrees=ntrees, tparams=tp,
                              sample_rate=float(self.params.get("sample_rate", 1.0)), nclass=nclass,
                              seed=self._seed(), comm=self.comm, init_f=init_f,
                              callback=scorer if scorer.active else None,
-                             base_margin=None if ckpt is None else ckpt.raw_margin(X),
+                             base_margin=base_margin,
                              dist_kw={"tweedie_power": float(self.params.get("tweedie_power", 1.5)),
                                       "quantile_alpha": float(self.params.get("quantile_alpha", 0.5)),
                                       "huber_delta": float(self.params.get("huber_alpha", 0.9))})
@@ -171,6 +183,46 @@ class _TreeBuilder(ModelBuilder):
 
     def _engine_dist(self, dist: str) -> str:
         return dist
+
+
+def _offset_init(dist: str, y, w, off, params, comm=None) -> float:
+    """Initial margin c minimising the loss of ``c + offset`` (H2O GBM with an
+    offset column): closed forms where they exist, Newton steps for bernoulli.
+    Sums are all-reduced over the ranks (laplace / quantile: the mean of the
+    per-rank medians / quantiles, an approximation on N ranks)."""
+    multi = comm is not None and comm.world_size > 1
+
+    def red(*v):
+        a = np.array(v, np.float64)
+        return comm.all_reduce_numpy(a) if multi else a
+
+    y = y.double().to(off.device)
+    o = off.double()
+    wt = torch.ones_like(y) if w is None else w.double().to(off.device)
+    if dist == "bernoulli":
+        c = 0.0
+        for _ in range(50):
+            p = torch.sigmoid(c + o)
+            g, h = red(float((wt * (y - p)).sum()), float((wt * p * (1 - p)).sum()))
+            if h <= 0:
+                break
+            c += g / h
+            if abs(g / h) < 1e-12:
+                break
+        return c
+    if dist in ("poisson", "tweedie"):
+        a, b = red(float((wt * y).sum()), float((wt * torch.exp(o)).sum()))
+        return float(np.log(a / b))
+    if dist == "gamma":
+        a, b = red(float((wt * y * torch.exp(-o)).sum()), float(wt.sum()))
+        return float(np.log(a / b))
+    r = y - o
+    if dist in ("laplace", "quantile"):
+        q = 0.5 if dist == "laplace" else float(params.get("quantile_alpha", 0.5))
+        v, = red(float(torch.quantile(r, q)))
+        return float(v / (comm.world_size if multi else 1))
+    a, b = red(float((wt * r).sum()), float(wt.sum()))
+    return float(a / b)      # gaussian / huber
 
 
 # ---------------------------------------------------------------------------
@@ -203,7 +255,9 @@ class _TreeScoring:
             Xv = valid.feature_matrix(builder.x)
             self.Xv = Xv
             K = ckpt.K if ckpt is not None else (nclass if dist == "multinomial" or (dist == "drf" and nclass > 2) else 1)
-            self.vmargin = ckpt.raw_margin(Xv).to(Xv.device) if ckpt is not None else None
+            ocol = p.get("offset_column")
+            self.voff = valid.vec(ocol).as_float().to(Xv.device)[None, :] if ocol else 0.0
+            self.vmargin = ckpt.raw_margin(Xv).to(Xv.device) + self.voff if ckpt is not None else None
             self.K = K
         from ..runtime.jobs import current_job
 
@@ -260,7 +314,7 @@ class _TreeScoring:
             if self.vmargin is None:
                 init = 0.0 if self.dist == "drf" else torch.from_numpy(
                     np.asarray(view.init_f, np.float32)).to(self.Xv.device)[:, None]
-                self.vmargin = init + m
+                self.vmargin = init + m + self.voff
             else:
                 self.vmargin = self.vmargin + m
             self.done = t + 1
