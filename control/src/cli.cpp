@@ -94,8 +94,6 @@ std::vector<SubSpec> build_app() {
   return subs;
 }
 
-std::string wrap_help(const std::string& s) { return s; }
-
 std::string opt_sig(const ArgSpec& a) {
   std::string sig = a.short_name.empty() ? "    " : "-" + a.short_name + ", ";
   sig += "--" + a.long_name;
@@ -131,7 +129,7 @@ std::string sub_help(const SubSpec& s) {
     os << "\nOPTIONS:\n";
     w = 0;
     for (auto& o : opts) w = std::max(w, o.first.size());
-    for (auto& o : opts) os << "    " << o.first << std::string(w - o.first.size() + 4, ' ') << wrap_help(o.second) << "\n";
+    for (auto& o : opts) os << "    " << o.first << std::string(w - o.first.size() + 4, ' ') << o.second << "\n";
   }
   return os.str();
 }
