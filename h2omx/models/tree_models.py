@@ -54,7 +54,9 @@ class TreeModel(Model):
         m = self.ens.raw_margin(X)
         if self.params.get("offset_column"):
             m = m + frame.vec(self.params["offset_column"]).as_float()[None, :].to(m.device)
-        return self._link(m.to(dev))
+        P = self._link(m.to(dev))
+        cd = getattr(self, "class_dist", None)
+        return P if cd is None else correct_probabilities(P, *cd)
 
     def varimp(self):
         gains = np.zeros(len(self.x))
@@ -122,6 +124,10 @@ class _TreeBuilder(ModelBuilder):
         if not bool(ok.all()):
             X, y = X[:, ok], y[ok]
             w = None if w is None else w[ok]
+        balance = None
+        if self.params.get("balance_classes") and self.category in (ModelCategory.BINOMIAL,
+                                                                     ModelCategory.MULTINOMIAL):
+            w, balance = _balance_weights(y, w, len(self.response_domain), self.params, self.comm)
         nbins = int(self.params.get("nbins") or self.params.get("max_bins") or self.default_nbins)
         edges, nvb, nbt = compute_edges(X, min(nbins, 255), seed=self._seed(), comm=self.comm)
         bm = bin_matrix(X, edges, nvb, nbt, names=self.x)
@@ -162,6 +168,7 @@ class _TreeBuilder(ModelBuilder):
             ens.trees = concat_trees(ckpt.trees, ens.trees) if len(ens.trees) else ckpt.trees
             ens.init_f = ckpt.init_f
         model = self.model_cls(self, model_id, ens, ens_dist)
+        model.class_dist = balance      # (prior, modelled) class fractions for correctProbabilities
         model.timings = dict(ens.timings)
         model.scoring_history = scorer.history
         return model
@@ -183,6 +190,40 @@ class _TreeBuilder(ModelBuilder):
 
     def _engine_dist(self, dist: str) -> str:
         return dist
+
+
+def correct_probabilities(P: torch.Tensor, prior, modelled) -> torch.Tensor:
+    """H2O ModelUtils.correctProbabilities: class probabilities [K][n] of a
+    model trained on a rebalanced class mix, mapped back to the original
+    class priors (p_k * prior_k / modelled_k, renormalised)."""
+    pr = torch.as_tensor(np.asarray(prior, np.float64), dtype=P.dtype, device=P.device)[:, None]
+    md = torch.as_tensor(np.asarray(modelled, np.float64), dtype=P.dtype, device=P.device)[:, None]
+    P = P * torch.where((pr > 0) & (md > 0), pr / md.clamp_min(1e-300), torch.ones_like(pr))
+    s = P.sum(0, keepdim=True)
+    return torch.where(s > 0, P / s.clamp_min(1e-300), P)
+
+
+def _balance_weights(y, w, K: int, params, comm=None):
+    """H2O ``balance_classes`` as row weights: class k's rows carry
+    t_k / n_k where t_k is the majority count (or n_k x
+    ``class_sampling_factors[k]``), all t_k scaled down so that sum t_k <=
+    ``max_after_balance_size`` x N.  Returns the weights and the (prior,
+    modelled) class fractions used to correct predicted probabilities."""
+    codes = y.long().clamp(0, K - 1)
+    n = torch.bincount(codes, weights=None if w is None else w.double().to(codes.device), minlength=K).double().cpu()
+    if comm is not None and comm.world_size > 1:
+        n = torch.from_numpy(comm.all_reduce_numpy(n.numpy()))
+    N = float(n.sum())
+    f = params.get("class_sampling_factors")
+    t = n * torch.tensor([float(v) for v in f], dtype=torch.float64) if f else torch.where(
+        n > 0, torch.full_like(n, float(n.max())), n)
+    cap = float(params.get("max_after_balance_size") or 5.0) * N
+    if float(t.sum()) > cap:
+        t = t * (cap / float(t.sum()))
+    ratio = torch.where(n > 0, t / n.clamp_min(1e-300), torch.zeros_like(n)).float().to(y.device)
+    rw = ratio[codes]
+    w = rw if w is None else w.float().to(y.device) * rw
+    return w, ((n / N).numpy(), (t / float(t.sum())).numpy())
 
 
 def _offset_init(dist: str, y, w, off, params, comm=None) -> float:
@@ -339,7 +380,8 @@ class H2OGradientBoostingEstimator(_TreeBuilder):
                     col_sample_rate_per_tree=1.0, min_split_improvement=1e-5, histogram_type="QuantilesGlobal",
                     max_abs_leafnode_pred=0.0, tweedie_power=1.5, quantile_alpha=0.5, huber_alpha=0.9,
                     stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0,
-                    offset_column=None, balance_classes=False, categorical_encoding="AUTO", checkpoint=None)
+                    offset_column=None, balance_classes=False, class_sampling_factors=None,
+                    max_after_balance_size=5.0, categorical_encoding="AUTO", checkpoint=None)
 
     def _tree_params(self, nfeat):
         p = self.params
@@ -405,6 +447,7 @@ class H2ORandomForestEstimator(_TreeBuilder):
                     mtries=-1, sample_rate=0.632, col_sample_rate_per_tree=1.0, min_split_improvement=1e-5,
                     binomial_double_trees=False, histogram_type="QuantilesGlobal", stopping_rounds=0,
                     stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0, balance_classes=False,
+                    class_sampling_factors=None, max_after_balance_size=5.0,
                     categorical_encoding="AUTO", offset_column=None, checkpoint=None)
 
     def _engine_dist(self, dist):

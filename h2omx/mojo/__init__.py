@@ -237,15 +237,18 @@ def mojo_bytes(model: Model) -> bytes:
         if dom:
             domains.append((j, dom))
     nclass = len(model.response_domain) if model.response_domain else 1
+    cd = getattr(model, "class_dist", None)     # balance_classes: (prior, modelled) class fractions
     head = {
         "h2o_version": "3.46.0.6", "mojo_version": MOJO_VERSIONS.get(algo, "1.00"),
         "license": "Apache License Version 2.0", "algo": algo, "algorithm": getattr(model, "algo_full_name", algo),
         "endianness": "LITTLE_ENDIAN", "category": _category_name(model.category),
         "uuid": str(uuid.uuid4().int & ((1 << 63) - 1)),
         "supervised": model.y is not None, "n_features": len(model.x), "n_classes": nclass,
-        "n_columns": len(columns), "n_domains": len(domains), "balance_classes": False,
+        "n_columns": len(columns), "n_domains": len(domains), "balance_classes": cd is not None,
         "default_threshold": float((model.training_metrics or {}).get("max_f1_threshold", 0.5) or 0.5),
-        "prior_class_distrib": "null", "model_class_distrib": "null", "timestamp": time.strftime("%Y-%m-%dT%H:%M:%S"),
+        "prior_class_distrib": "null" if cd is None else [float(v) for v in cd[0]],
+        "model_class_distrib": "null" if cd is None else [float(v) for v in cd[1]],
+        "timestamp": time.strftime("%Y-%m-%dT%H:%M:%S"),
         "h2omx_model_id": model.model_id, "response_column": model.y or "",
     }
     if algo == "coxph":
@@ -1116,23 +1119,13 @@ class GenericModel(Model):
             lo, hi = float(self.info["min_path_length"]), float(self.info["max_path_length"])
             return torch.stack([(hi - L) / max(hi - lo, 1e-12), L])
         if a in ("gbm", "drf", "xgboost"):
-            m = self.ens.raw_margin(X).to(X.device)
-            if a == "drf" or self.link == "identity":
-                if self.category == ModelCategory.BINOMIAL:
-                    p1 = m[0].clamp(0, 1)
-                    return torch.stack([1 - p1, p1])
-                if self.category == ModelCategory.MULTINOMIAL:
-                    mm = m.clamp_min(0)
-                    return mm / mm.sum(0, keepdim=True).clamp_min(1e-30)
-                return m
-            if self.link == "logit":
-                p1 = torch.sigmoid(m[0])
-                return torch.stack([1 - p1, p1])
-            if self.link == "multinomial":
-                return torch.softmax(m, 0)
-            if self.link == "log":
-                return torch.exp(m)
-            return m
+            P = self._tree_scores(self.ens.raw_margin(X).to(X.device))
+            if self.info.get("balance_classes") and isinstance(self.info.get("prior_class_distrib"), list):
+                # balance_classes models: genmodel's correctProbabilities
+                from ..models.tree_models import correct_probabilities
+
+                P = correct_probabilities(P, self.info["prior_class_distrib"], self.info["model_class_distrib"])
+            return P
         if a == "glm":
             return self._glm(X)
         if a == "kmeans":
@@ -1142,6 +1135,24 @@ class GenericModel(Model):
         if a == "stackedensemble":
             return self._se(frame)
         raise NotImplementedError(a)
+
+    def _tree_scores(self, m: torch.Tensor) -> torch.Tensor:
+        if self.mojo_algo == "drf" or self.link == "identity":
+            if self.category == ModelCategory.BINOMIAL:
+                p1 = m[0].clamp(0, 1)
+                return torch.stack([1 - p1, p1])
+            if self.category == ModelCategory.MULTINOMIAL:
+                mm = m.clamp_min(0)
+                return mm / mm.sum(0, keepdim=True).clamp_min(1e-30)
+            return m
+        if self.link == "logit":
+            p1 = torch.sigmoid(m[0])
+            return torch.stack([1 - p1, p1])
+        if self.link == "multinomial":
+            return torch.softmax(m, 0)
+        if self.link == "log":
+            return torch.exp(m)
+        return m
 
     def _expand(self, X, use_all, means=None, center=None, mult=None):
         """One-hot categoricals (the first ``cats`` columns) + numerics in MOJO
