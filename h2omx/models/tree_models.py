@@ -58,6 +58,15 @@ class TreeModel(Model):
         cd = getattr(self, "class_dist", None)
         return P if cd is None else correct_probabilities(P, *cd)
 
+    def predict(self, frame: Frame) -> Frame:
+        fr = super().predict(frame)
+        cal = getattr(self, "calibration", None)
+        if cal is None:
+            return fr
+        p1 = fr.vec(self.response_domain[1]).data.double()
+        c1 = _apply_calibration(cal, p1).float()
+        return Frame(list(fr.vecs) + [Vec("cal_p0", 1.0 - c1, "real"), Vec("cal_p1", c1, "real")])
+
     def varimp(self):
         gains = np.zeros(len(self.x))
         for t in range(self.ens.trees.shape[0]):
@@ -169,6 +178,10 @@ class _TreeBuilder(ModelBuilder):
             ens.init_f = ckpt.init_f
         model = self.model_cls(self, model_id, ens, ens_dist)
         model.class_dist = balance      # (prior, modelled) class fractions for correctProbabilities
+        model.calibration = None
+        if self.params.get("calibrate_model"):
+            model.calibration = _fit_calibration(model, self.params.get("calibration_frame"),
+                                                 str(self.params.get("calibration_method") or "AUTO"))
         model.timings = dict(ens.timings)
         model.scoring_history = scorer.history
         return model
@@ -190,6 +203,59 @@ class _TreeBuilder(ModelBuilder):
 
     def _engine_dist(self, dist: str) -> str:
         return dist
+
+
+def _fit_calibration(model, cal, method: str) -> dict:
+    """H2O ``calibrate_model``: map the binomial p1 on ``calibration_frame`` to
+    calibrated probabilities - Platt scaling (logistic regression of y on p1,
+    Newton in fp64; method AUTO / PlattScaling) or isotonic regression
+    (pool-adjacent-violators, clipped to the fitted range)."""
+    from ..frame.frame import DKV
+
+    if model.category != ModelCategory.BINOMIAL:
+        raise ValueError("calibrate_model: binomial models only (as in H2O)")
+    cal = DKV.get(cal) if isinstance(cal, str) else cal
+    if cal is None:
+        raise ValueError("calibrate_model requires calibration_frame")
+    p1 = model.predict_raw(cal)[-1].double()
+    y = model.adapt_frame(cal).vec(model.y).data.long().to(p1.device)
+    ok = y >= 0
+    p1, y = p1[ok], (y[ok] == 1).double()
+    m = method.lower()
+    if m in ("auto", "plattscaling", "platt_scaling"):
+        a = torch.zeros(2, dtype=torch.float64, device=p1.device)
+        Xd = torch.stack([torch.ones_like(p1), p1], 1)
+        for _ in range(100):
+            mu = torch.sigmoid(Xd @ a)
+            g = Xd.T @ (y - mu)
+            H = (Xd * (mu * (1 - mu))[:, None]).T @ Xd + 1e-10 * torch.eye(2, dtype=torch.float64, device=p1.device)
+            step = torch.linalg.solve(H, g)
+            a = a + step
+            if float(step.abs().max()) < 1e-12:
+                break
+        return {"method": "PlattScaling", "intercept": float(a[0]), "slope": float(a[1])}
+    if m in ("isotonicregression", "isotonic_regression"):
+        order = torch.argsort(p1)
+        xs, ys = p1[order].cpu().numpy(), y[order].cpu().numpy()
+        vals, wts, xs_hi = [], [], []
+        for xv, yv in zip(xs, ys):            # pool adjacent violators
+            vals.append(yv); wts.append(1.0); xs_hi.append(xv)
+            while len(vals) > 1 and vals[-2] > vals[-1]:
+                v = (vals[-2] * wts[-2] + vals[-1] * wts[-1]) / (wts[-2] + wts[-1])
+                w = wts[-2] + wts[-1]
+                vals[-2:], wts[-2:], xs_hi[-2:] = [v], [w], [xs_hi[-1]]
+        return {"method": "IsotonicRegression", "x": [float(v) for v in xs_hi], "y": [float(v) for v in vals],
+                "x_min": float(xs[0])}
+    raise ValueError(f"calibration_method {method!r}: AUTO, PlattScaling or IsotonicRegression")
+
+
+def _apply_calibration(cal: dict, p1: torch.Tensor) -> torch.Tensor:
+    if cal["method"] == "PlattScaling":
+        return torch.sigmoid(cal["intercept"] + cal["slope"] * p1)
+    xs = torch.tensor(cal["x"], dtype=torch.float64, device=p1.device)
+    ys = torch.tensor(cal["y"], dtype=torch.float64, device=p1.device)
+    i = torch.searchsorted(xs, p1.clamp(cal["x_min"], float(xs[-1]))).clamp_max(xs.numel() - 1)
+    return ys[i]
 
 
 def correct_probabilities(P: torch.Tensor, prior, modelled) -> torch.Tensor:
@@ -381,7 +447,8 @@ class H2OGradientBoostingEstimator(_TreeBuilder):
                     max_abs_leafnode_pred=0.0, tweedie_power=1.5, quantile_alpha=0.5, huber_alpha=0.9,
                     stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0,
                     offset_column=None, balance_classes=False, class_sampling_factors=None,
-                    max_after_balance_size=5.0, categorical_encoding="AUTO", checkpoint=None)
+                    max_after_balance_size=5.0, categorical_encoding="AUTO", checkpoint=None,
+                    calibrate_model=False, calibration_frame=None, calibration_method="AUTO")
 
     def _tree_params(self, nfeat):
         p = self.params
@@ -411,7 +478,8 @@ class H2OXGBoostEstimator(_TreeBuilder):
                     reg_alpha=0.0, gamma=0.0, min_split_improvement=None, max_bins=256, tree_method="hist",
                     booster="gbtree", grow_policy="depthwise", max_abs_leafnode_pred=0.0, tweedie_power=1.5,
                     stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0,
-                    offset_column=None, backend="gpu", nbins=None, categorical_encoding="AUTO", checkpoint=None)
+                    offset_column=None, backend="gpu", nbins=None, categorical_encoding="AUTO", checkpoint=None,
+                    calibrate_model=False, calibration_frame=None, calibration_method="AUTO")
 
     def _tree_params(self, nfeat):
         p = self.params
@@ -448,7 +516,8 @@ class H2ORandomForestEstimator(_TreeBuilder):
                     binomial_double_trees=False, histogram_type="QuantilesGlobal", stopping_rounds=0,
                     stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0, balance_classes=False,
                     class_sampling_factors=None, max_after_balance_size=5.0,
-                    categorical_encoding="AUTO", offset_column=None, checkpoint=None)
+                    categorical_encoding="AUTO", offset_column=None, checkpoint=None,
+                    calibrate_model=False, calibration_frame=None, calibration_method="AUTO")
 
     def _engine_dist(self, dist):
         return "drf"

@@ -197,6 +197,10 @@ def mojo_bytes(model: Model) -> bytes:
     if algo in ("gbm", "drf", "xgboost"):
         columns = list(model.x)
         info.update(_tree_info(model, files))
+        cal = getattr(model, "calibration", None)
+        if cal is not None and cal["method"] == "PlattScaling":
+            # genmodel calibrateClassProbabilities: p1' = logitInv(p1 * beta[0] + beta[1])
+            info.update(calib_method="platt", calib_glm_beta=[cal["slope"], cal["intercept"]])
     elif algo == "glm" and (getattr(model, "interaction_spec", None) or model.family == "ordinal"):
         columns, ext = _glm_ext_info(model, files)       # h2omx array payload
         info.update(ext)
@@ -1033,7 +1037,13 @@ class GenericModel(Model):
             P = self._score_arrays(frame)
             return Frame([Vec("uplift_predict", P[0], "real"), Vec("p_y1_with_treatment", P[1], "real"),
                           Vec("p_y1_without_treatment", P[2], "real")])
-        return super().predict(frame)
+        fr = super().predict(frame)
+        beta = self.info.get("calib_glm_beta")
+        if self.info.get("calib_method") == "platt" and isinstance(beta, list) and self.response_domain:
+            p1 = fr.vec(self.response_domain[1]).data.double()
+            c1 = torch.sigmoid(p1 * float(beta[0]) + float(beta[1])).float()
+            fr = Frame(list(fr.vecs) + [Vec("cal_p0", 1.0 - c1, "real"), Vec("cal_p1", c1, "real")])
+        return fr
 
     def _te(self, frame: Frame) -> torch.Tensor:
         info = self.info
