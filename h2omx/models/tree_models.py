@@ -121,6 +121,9 @@ class _TreeBuilder(ModelBuilder):
         raise NotImplementedError
 
     def _fit(self, train: Frame, valid: Frame | None, model_id: str) -> Model:
+        enc = str(self.params.get("categorical_encoding") or "AUTO").lower().replace("_", "")
+        if enc == "sortbyresponse":
+            train, valid = self._sort_levels_by_response(train, valid)
         X = train.feature_matrix(self.x)
         dist = self._dist()
         yv = train.vec(self.y)
@@ -185,6 +188,34 @@ class _TreeBuilder(ModelBuilder):
         model.timings = dict(ens.timings)
         model.scoring_history = scorer.history
         return model
+
+    def _sort_levels_by_response(self, train: Frame, valid: Frame | None):
+        """H2O ``categorical_encoding="SortByResponse"``: every categorical
+        predictor's levels are reordered by their mean response (lowest -> code
+        0; levels without training rows last), so ordinal bin splits separate
+        low- from high-response levels.  The reordered domain is the model's
+        (scoring frames and MOJOs map level names onto it)."""
+        yv = train.vec(self.y)
+        yval = yv.as_float().double() if self.category == ModelCategory.REGRESSION else yv.data.double()
+        ok = ~torch.isnan(yval) & (yval >= 0 if self.category != ModelCategory.REGRESSION else True)
+        for c in self.x:
+            if self.feature_types.get(c) != ENUM:
+                continue
+            dom = list(self.feature_domains.get(c) or [])
+            L = len(dom)
+            if L < 2:
+                continue
+            codes = train.vec(c).data.long().to(yval.device)
+            m = ok & (codes >= 0) & (codes < L)
+            sums = torch.bincount(codes[m], weights=yval[m], minlength=L).cpu().numpy()
+            cnt = torch.bincount(codes[m], minlength=L).cpu().numpy()
+            if self.comm is not None and self.comm.world_size > 1:
+                sums = self.comm.all_reduce_numpy(sums.astype(np.float64))
+                cnt = self.comm.all_reduce_numpy(cnt.astype(np.float64))
+            key = [(sums[i] / cnt[i] if cnt[i] > 0 else float("inf"), i) for i in range(L)]
+            self.feature_domains[c] = [dom[i] for _, i in sorted(key)]
+        adapt = Model.adapt_frame.__get__(self)
+        return adapt(train), (adapt(valid) if valid is not None else None)
 
     def _checkpoint_ensemble(self):
         ck = self.params.get("checkpoint")
