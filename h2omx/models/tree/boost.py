@@ -372,11 +372,15 @@ class GpuBooster:
 def _train_gpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw):
     t0 = time.perf_counter()
     gb = GpuBooster(bm, y_np, w_np, ens, tp, sample_rate, seed, comm, dist_kw)
+    lr0, ann = tp.learn_rate, tp.learn_rate_annealing
     for t in range(ntrees):
+        if ann != 1.0:
+            gb.builder.p.learn_rate = lr0 * ann ** t
         gb.step()
         if callback is not None and callback(t, _GpuView(gb)) is True:
             break
     gb.finish()
+    gb.builder.p.learn_rate = lr0
     ens.timings["train_s"] = time.perf_counter() - t0
 
 

@@ -41,6 +41,7 @@ class TreeParams:
     gamma: float = 0.0
     min_split_improvement: float = 1e-5
     learn_rate: float = 0.1
+    learn_rate_annealing: float = 1.0   # H2O GBM: iteration t uses learn_rate * annealing^t
     mode: int = 0            # 0: H2O squared error on residuals, 1: XGBoost second order
     leaf_mode: int = 0       # 0: Newton (-G/(H+lambda)), 1: mean (DRF)
     col_sample_rate: float = 1.0

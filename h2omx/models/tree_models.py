@@ -484,6 +484,7 @@ class H2OGradientBoostingEstimator(_TreeBuilder):
     def _tree_params(self, nfeat):
         p = self.params
         return TreeParams(max_depth=int(p["max_depth"]), min_rows=float(p["min_rows"]), learn_rate=float(p["learn_rate"]),
+                          learn_rate_annealing=float(p.get("learn_rate_annealing") or 1.0),
                           min_split_improvement=float(p["min_split_improvement"]), mode=0, leaf_mode=0,
                           col_sample_rate=float(p["col_sample_rate"]),
                           col_sample_rate_per_tree=float(p["col_sample_rate_per_tree"]),

@@ -310,7 +310,9 @@ def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback
     wobs = np.ones(n, np.float32) if w_np is None else w_np.astype(np.float32)
     trees = []
     t0 = time.perf_counter()
+    lr0, ann = tp.learn_rate, getattr(tp, "learn_rate_annealing", 1.0)
     for t in range(ntrees):
+        builder.p.learn_rate = lr0 * ann ** t
         wb = wobs * bag_weights(n, sample_rate, seed, t, row_base)
         if K == 1:
             gr, hs = dist_grad(dist, Fm[0], y_np, **dist_kw)
@@ -338,5 +340,6 @@ def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback
         if callback is not None and callback(t, _CpuView(Fm, trees, K, ens.init_f)) is True:
             break
     ens.timings["train_s"] = time.perf_counter() - t0
+    builder.p.learn_rate = lr0
     ens.trees = np.stack(trees) if trees else ens.trees
     ens._cpu_margin = Fm
