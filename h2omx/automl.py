@@ -107,6 +107,9 @@ class H2OAutoML:
         exc = {a.lower() for a in (exclude_algos or [])}
         self.algos = [a for a in inc if a not in exc]
         self.plan = _parse_plan(modeling_plan) if modeling_plan else None
+        # H2O exploitation phase: a share of the budget (time and models) refines the
+        # best explored GBM with learning-rate annealing (-1 / 0: off)
+        self.exploitation_ratio = float(exploitation_ratio or 0.0)
         if self.plan is not None:
             self.algos = [a for a in self.algos if a in self.plan or a == "stackedensemble"]
         self.sort_metric = sort_metric
@@ -139,10 +142,16 @@ class H2OAutoML:
                   seed=seed) if self.nfolds > 1 else dict(seed=seed)
         category = None
 
-        def out_of_budget():
-            if self.max_models and len(self.models) >= self.max_models:
+        explo = min(max(self.exploitation_ratio, 0.0), 1.0)
+        # model slots kept for the exploitation steps (one step: GBM_lr_annealing_selection)
+        explo_models = min(1, int(np.ceil(explo * int(self.max_models)))) if (explo and self.max_models) else 0
+
+        def out_of_budget(phase="explore"):
+            reserve = explo_models if phase == "explore" else 0
+            if self.max_models and len(self.models) >= self.max_models - reserve:
                 return True
-            return bool(budget) and time.time() - t0 > budget
+            share = (1.0 - explo) if phase == "explore" else 1.0
+            return bool(budget) and time.time() - t0 > budget * share
 
         def fit(name, cls, params):
             nonlocal category
@@ -179,6 +188,8 @@ class H2OAutoML:
             comm_se = None
         else:
             category = self._train_sequential(fit, rng, out_of_budget)
+            if explo > 0 and category is not None:
+                self._exploit(fit, category, lambda: out_of_budget("exploit"))
             comm_se = comm
         base = [m for m in self.models if m.cross_validation_holdout is not None]
         if "stackedensemble" in self.algos and self.nfolds > 1 and len(base) >= 2 and category != ModelCategory.CLUSTERING:
@@ -248,6 +259,25 @@ class H2OAutoML:
                 category = m.category if m is not None else category
                 counters[f] += 1
         return category
+
+    def _exploit(self, fit, category, out_of_budget):
+        """Exploitation step ``GBM_lr_annealing_selection`` (H2O AutoML): the
+        best explored GBM retrained with its hyper-parameters and learning rate,
+        decaying by 0.99 per tree (``learn_rate_annealing``) over twice the
+        trees, early stopping as configured; ranked like any other model."""
+        gbms = [m for m in self._best_of_family(list(self.models), category) if m.algo == "gbm"]
+        if not gbms or out_of_budget():
+            return
+        best = gbms[0]
+        keep = ("max_depth", "min_rows", "sample_rate", "col_sample_rate", "col_sample_rate_per_tree",
+                "min_split_improvement", "distribution", "nbins")
+        params = {k: best.params[k] for k in keep if k in best.params}
+        lr = float(best.params.get("learn_rate", 0.1))
+        params.update(learn_rate=lr, learn_rate_annealing=0.99, ntrees=int(best.params.get("ntrees", 50)) * 2,
+                      score_tree_interval=5)
+        params.update({k: v for k, v in self.stopping.items() if v is not None})
+        self._log("ModelTraining", f"exploitation: GBM_lr_annealing_selection from {best.model_id}")
+        fit("GBM_lr_annealing_selection", H2OGradientBoostingEstimator, params)
 
     def _train_task_parallel(self, x, y, training_frame, validation_frame, comm, cv, rng, budget, t0, start_models):
         """parallelism="task": replicate the frame, deal the plan round-robin to

@@ -60,3 +60,20 @@ def test_max_runtime_secs_stops_trees():
         y="y", training_frame=fr)
     assert time.time() - t < 30
     assert 0 < m.ens.ntrees < 100000
+
+
+def test_exploitation_phase_lr_annealing():
+    """exploitation_ratio > 0 reserves part of the model budget for the
+    exploitation step: the best explored GBM retrained with learning-rate
+    annealing (H2O's GBM_lr_annealing_selection)."""
+    fr = _frame(seed=4)
+    aml = H2OAutoML(max_models=8, nfolds=3, seed=1, project_name="t_aml_exploit", exploitation_ratio=0.2,
+                    include_algos=["GBM", "StackedEnsemble"]).train(y="y", training_frame=fr)
+    ids = [m.model_id for m in aml.models]
+    ex = [m for m in aml.models if m.model_id.startswith("GBM_lr_annealing_selection")]
+    assert len(ex) == 1 and ex[0].params["learn_rate_annealing"] == 0.99
+    base = [m for m in aml.models if m.algo == "gbm"]
+    assert len(base) == 8 and ids.index(ex[0].model_id) == len(base) - 1
+    off = H2OAutoML(max_models=3, nfolds=0, seed=1, project_name="t_aml_noexploit",
+                    include_algos=["GBM"]).train(y="y", training_frame=fr)
+    assert not any(m.model_id.startswith("GBM_lr_annealing") for m in off.models)
