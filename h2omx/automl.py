@@ -143,8 +143,10 @@ class H2OAutoML:
         category = None
 
         explo = min(max(self.exploitation_ratio, 0.0), 1.0)
-        # model slots kept for the exploitation steps (one step: GBM_lr_annealing_selection)
-        explo_models = min(1, int(np.ceil(explo * int(self.max_models)))) if (explo and self.max_models) else 0
+        # model slots kept for the exploitation steps (GBM_lr_annealing_selection,
+        # XGBoost_lr_search_selection)
+        n_steps = sum(a in self.algos for a in ("gbm", "xgboost"))
+        explo_models = min(n_steps, int(np.ceil(explo * int(self.max_models)))) if (explo and self.max_models) else 0
 
         def out_of_budget(phase="explore"):
             reserve = explo_models if phase == "explore" else 0
@@ -265,10 +267,23 @@ class H2OAutoML:
         best explored GBM retrained with its hyper-parameters and learning rate,
         decaying by 0.99 per tree (``learn_rate_annealing``) over twice the
         trees, early stopping as configured; ranked like any other model."""
-        gbms = [m for m in self._best_of_family(list(self.models), category) if m.algo == "gbm"]
-        if not gbms or out_of_budget():
+        best_of = {m.algo: m for m in self._best_of_family(list(self.models), category)}
+        xgb = best_of.get("xgboost")
+        if xgb is not None and not out_of_budget():
+            # XGBoost_lr_search_selection: the best XGBoost at half its learning rate
+            # over twice the trees (early stopping as configured)
+            keep = ("max_depth", "min_rows", "min_child_weight", "sample_rate", "subsample", "col_sample_rate",
+                    "colsample_bylevel", "col_sample_rate_per_tree", "colsample_bytree", "reg_lambda", "reg_alpha",
+                    "gamma", "distribution")
+            params = {k: xgb.params[k] for k in keep if xgb.params.get(k) is not None}
+            lr = float(xgb.params.get("eta") or xgb.params.get("learn_rate") or 0.3)
+            params.update(learn_rate=lr / 2, ntrees=int(xgb.params.get("ntrees", 50)) * 2, score_tree_interval=5)
+            params.update({k: v for k, v in self.stopping.items() if v is not None})
+            self._log("ModelTraining", f"exploitation: XGBoost_lr_search_selection from {xgb.model_id}")
+            fit("XGBoost_lr_search_selection", H2OXGBoostEstimator, params)
+        if "gbm" not in best_of or out_of_budget():
             return
-        best = gbms[0]
+        best = best_of["gbm"]
         keep = ("max_depth", "min_rows", "sample_rate", "col_sample_rate", "col_sample_rate_per_tree",
                 "min_split_improvement", "distribution", "nbins")
         params = {k: best.params[k] for k in keep if k in best.params}

@@ -77,3 +77,15 @@ def test_exploitation_phase_lr_annealing():
     off = H2OAutoML(max_models=3, nfolds=0, seed=1, project_name="t_aml_noexploit",
                     include_algos=["GBM"]).train(y="y", training_frame=fr)
     assert not any(m.model_id.startswith("GBM_lr_annealing") for m in off.models)
+
+
+def test_exploitation_xgboost_lr_search():
+    fr = _frame(seed=5)
+    aml = H2OAutoML(max_models=6, nfolds=3, seed=2, project_name="t_aml_exploit_xgb", exploitation_ratio=0.3,
+                    include_algos=["GBM", "XGBoost"]).train(y="y", training_frame=fr)
+    ids = [m.model_id for m in aml.models]
+    assert len(ids) == 6
+    assert any(i.startswith("XGBoost_lr_search_selection") for i in ids)
+    assert any(i.startswith("GBM_lr_annealing_selection") for i in ids)
+    xs = [m for m in aml.models if m.model_id.startswith("XGBoost_lr_search_selection")][0]
+    assert xs.algo == "xgboost" and "failed" not in " ".join(str(e) for e in aml.event_log.to_pandas().values.ravel())
