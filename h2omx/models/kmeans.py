@@ -76,7 +76,11 @@ class H2OKMeansEstimator(ModelBuilder):
         del Xraw
         d, n = X.shape
         g = torch.Generator().manual_seed(self._seed())
-        C = self._init(X, k, str(p_["init"]).lower(), g, design)
+        if p_.get("estimate_k") and p_.get("user_points") is None:
+            C = self._estimate_k(X, k, str(p_["init"]).lower(), g, design)
+            k = C.shape[0]
+        else:
+            C = self._init(X, k, str(p_["init"]).lower(), g, design)
         it = 0
         prev = None
         stats = {}
@@ -114,6 +118,46 @@ class H2OKMeansEstimator(ModelBuilder):
         model = KMeansModel(self, model_id, design, C, stats)
         model.training_metrics = stats
         return model
+
+    # estimate_k: stop adding centers once the proportional reduction in the
+    # within-cluster sum of squares falls below this (H2O's PRE rule; the exact
+    # H2O threshold is unpinned here)
+    PRE_MIN = 0.1
+
+    def _estimate_k(self, X, kmax, how, g, design):
+        """H2O ``estimate_k``: grow k from 1 up to ``k`` (the maximum), each step
+        seeding the new center at the point farthest from the current centers
+        and running Lloyd iterations; keep the last k whose step still reduced
+        the total within-cluster SS by at least PRE_MIN."""
+        comm = self.comm
+        C = self._init(X, 1, how, g, design)
+        prev_ss, best = None, C
+        for kk in range(1, kmax + 1):
+            if kk > 1:
+                far = self._farthest(X, C, 1)
+                if comm is not None and comm.world_size > 1:   # every rank adopts rank 0's point
+                    t = torch.from_numpy(far).to(X.device)
+                    comm.broadcast(t, 0)
+                    far = t.cpu().numpy()
+                C = np.concatenate([C, far])
+            for _ in range(int(self.params["max_iterations"])):
+                assign, sums, cnt, sse = D.kmeans_step(X, torch.from_numpy(C.astype(np.float32)).to(X.device))
+                if comm is not None and comm.world_size > 1:
+                    red = comm.all_reduce_numpy(np.concatenate([sums.ravel(), cnt, sse]))
+                    d = X.shape[0]
+                    sums, cnt, sse = red[: kk * d].reshape(kk, d), red[kk * d: kk * d + kk], red[kk * d + kk:]
+                nz = cnt > 0
+                newC = C.copy()
+                newC[nz] = sums[nz] / cnt[nz, None]
+                if np.allclose(newC, C, rtol=0, atol=1e-9):
+                    C = newC
+                    break
+                C = newC
+            ss = float(sse.sum())
+            if prev_ss is not None and (prev_ss <= 0 or (prev_ss - ss) / prev_ss < self.PRE_MIN):
+                break
+            best, prev_ss = C.copy(), ss
+        return best
 
     def _init(self, X, k, how, g, design):
         d, n = X.shape
