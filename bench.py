@@ -12,11 +12,16 @@ iteration: gradients + a depth-5 tree grown level by level on the GPU (LDS
 histograms, exact integer reduce, RCCL all-reduce of the level histograms
 when N > 1, split scan, partition, leaf values) + margin update.
 ``value`` = total training rows x K / max-over-ranks wall time of the K
-timed steps = aggregate row-trees per second.  Scaling is *weak* by
-default: every rank holds its own 11M-row shard (global rows = N x 11M);
-``--scaling strong`` splits 11M rows over the ranks instead.  Training AUC
-of the final model (all ranks) is reported; ``--oracle-rows R`` adds a
-scikit-learn HistGradientBoosting fit on R rows for AUC parity.
+timed steps = aggregate row-trees per second.  Scaling is *strong* by
+default for the headline: the metric is "HIGGS-shape 11M x 28 at 1/2/4/8
+MI355X", so the same 11M rows (same seed) are split over the N ranks and
+N ranks grow the 1-rank trees; ``--scaling weak`` gives every rank its own
+11M-row shard instead (global rows = N x 11M).  Each step is replayed as a
+HIP graph when eligible (``--tree-graph``); after the timed steps a few
+instrumented steps report the host-enqueue, per-phase and collective time
+per tree.  Training AUC of the final model (all ranks) is reported;
+``--oracle-rows R`` adds a scikit-learn HistGradientBoosting fit on R rows
+for AUC parity.
 
 ``xgboost-airlines``: XGBoost-hist (second-order gain, depth 6, eta 0.3) on
 Airlines-shape 31-column data, 150M rows over 8 GPUs = 18.75M rows per GPU
@@ -65,23 +70,40 @@ def _trees(args, comm, torch, np, model):
     dev = comm.device
     world, rank = comm.world_size, comm.rank
     rows = args.rows or (11_000_000 if model == "gbm-higgs" else 150_000_000 // 8)
-    n_local = rows if args.scaling == "weak" else rows // world + (1 if rank < rows % world else 0)
+    strong = args.scaling == "strong"
     t_setup = time.perf_counter()
+    gen = higgs_like if model == "gbm-higgs" else airlines_like
+    if strong:
+        # strong scaling: the SAME global data set at every N (every rank generates
+        # it with the global seed and keeps its contiguous row slice), so N ranks
+        # train on exactly the rows of the 1-rank run and grow the same trees
+        lo, hi = rows * rank // world, rows * (rank + 1) // world
+        X, y = gen(rows, seed=args.seed, device=dev)
+        X_full = X
+        X, y = X[:, lo:hi].contiguous(), y[lo:hi].contiguous()
+    else:
+        X, y = gen(rows, seed=args.seed + 1000 * rank, device=dev)
+        X_full = None
+    n_local = X.shape[1]
     if model == "gbm-higgs":
-        X, y = higgs_like(n_local, seed=args.seed + 1000 * rank, device=dev)
         if args.cols != 28:
             X = X[: args.cols].contiguous() if args.cols < 28 else torch.cat(
                 [X, torch.randn((args.cols - 28, n_local), device=dev)])
+            X_full = None
         depth = args.max_depth or 5
         tp = TreeParams(max_depth=depth, min_rows=args.min_rows, learn_rate=args.learn_rate or 0.1, mode=0,
                         leaf_mode=0, min_split_improvement=1e-5, seed=args.seed)
     else:
-        X, y = airlines_like(n_local, seed=args.seed + 1000 * rank, device=dev)
         depth = args.max_depth or 6
         tp = TreeParams(max_depth=depth, min_rows=0.0, min_child_weight=1.0, reg_lambda=1.0, gamma=0.0,
                         learn_rate=args.learn_rate or 0.3, mode=1, leaf_mode=0, min_split_improvement=0.0,
                         seed=args.seed)
-    edges, nvb, nbt = compute_edges(X, args.nbins, comm=comm)
+    if X_full is not None:
+        # strong scaling: cut points of the global data (= the 1-rank run's)
+        edges, nvb, nbt = compute_edges(X_full, args.nbins)
+        del X_full
+    else:
+        edges, nvb, nbt = compute_edges(X, args.nbins, comm=comm)
     bm = bin_matrix(X, edges, nvb, nbt)
     y_np = y.cpu().numpy()
     sums = comm.all_reduce_numpy(np.array([y_np.sum(), float(len(y_np))]))
@@ -95,9 +117,12 @@ def _trees(args, comm, torch, np, model):
         _sync(torch, dev)
         comm.barrier()
         setup_s = time.perf_counter() - t_setup
+        comm.collective_stats(reset=True)
         elapsed = _timed(gb.step, args, comm, torch, dev)
+        coll = comm.collective_stats()
         gb.flush()   # fused mode: the last tree is applied inside the next step's level 0
         margin = gb.st.Fm[0, : bm.n]
+        graph_used = gb.graph is not None
     else:
         # CPU rehearsal (reference tree builder): the boosting loop owns the
         # iterations, so the timed window is opened / closed from its callback
@@ -118,10 +143,18 @@ def _trees(args, comm, torch, np, model):
         comm.barrier()
         elapsed = comm.max_scalar(time.perf_counter() - clock["t0"])
         margin = torch.from_numpy(ens._cpu_margin[0])
+        coll, graph_used = comm.collective_stats(), False
     total_rows = int(comm.all_reduce_numpy(np.array([float(n_local)]))[0])
+    if args.dump_trees:
+        trees = gb.finish().trees if gb is not None else ens.trees
+        if rank == 0:
+            np.save(args.dump_trees, trees)
     auc = None
     if not args.no_auc:
         auc = auc_from_scores(margin, y, comm=comm)
+    per_tree = None
+    if gb is not None and args.instrument_steps > 0:
+        per_tree = _instrument(gb, args, comm, torch, dev)
     fit = None
     fit_trees = args.fit_trees if args.fit_trees >= 0 else (50 if dev.type == "cuda" else 0)
     if fit_trees > 0:
@@ -137,14 +170,21 @@ def _trees(args, comm, torch, np, model):
         "dtype": "fp32 gradients/hessians; histograms in fixed-point int32 (stochastic rounding) summed "
                  "exactly in int64; fp64 split gains; exact int64 leaf sums; uint8 bins",
         "data": f"synthetic {'HIGGS' if model == 'gbm-higgs' else 'Airlines'}-shape generated on device; "
-                "random-init, seed per rank",
+                + ("one global data set (global seed), contiguous row slice per rank" if strong
+                   else "own shard per rank (seed per rank)"),
         "config": {"model": "GBM bernoulli" if model == "gbm-higgs" else "XGBoost hist binary:logistic",
                    "global_batch": total_rows, "seq_len": None, "rows_per_gpu": n_local,
                    "cols": int(bm.F), "max_depth": depth, "nbins": args.nbins, "learn_rate": tp.learn_rate,
                    "min_rows": tp.min_rows, "parallelism": f"dp{world}"},
         "train_auc": auc,
         "setup_s": setup_s,
+        "graph_replay": graph_used,
+        "collectives_per_tree": {"calls": coll["all_reduce_calls"] / max(args.steps, 1),
+                                 "bytes": coll["all_reduce_bytes"] / max(args.steps, 1),
+                                 "host_us": 1e6 * coll["all_reduce_s"] / max(args.steps, 1)},
     }
+    if per_tree is not None:
+        out.update(per_tree)
     if fit is not None:
         out.update(fit)
     if args.oracle_rows and rank == 0:
@@ -160,6 +200,66 @@ def _trees(args, comm, torch, np, model):
                                              l2_regularization=0.0).fit(Xs, ys)
         out["oracle"] = {"rows": m, "sklearn_hgb_train_auc": float(roc_auc_score(ys, clf.decision_function(Xs))),
                          "h2omx_train_auc_same_rows": float(roc_auc_score(ys, margin[:m].cpu().numpy()))}
+    return out
+
+
+def _instrument(gb, args, comm, torch, dev):
+    """Per-tree cost structure, measured AFTER the timed steps on the same
+    booster (extra trees; the reported model / AUC are taken before this):
+
+    * ``host_enqueue_us_per_tree``: host time to enqueue one step with the GPU
+      idle (synchronised before and after), with graph replay when the timed
+      run used it and for the eager launch sequence;
+    * ``phase_us_per_tree``: device time per phase (HIP events, eager steps);
+      ``small_kernel_us_per_tree`` = hist_reduce + split + tree_begin + leaf,
+      the launch-latency-bound part that does not shrink with rows per GPU;
+    * ``allreduce_us_per_tree``: device time of the collectives (events around
+      each RCCL call on the compute stream: includes waiting for the slowest
+      rank) and their count / bytes."""
+    b = gb.builder
+    k = args.instrument_steps
+    out = {}
+
+    def enqueue_us(n):
+        ts = []
+        for _ in range(n):
+            _sync(torch, dev)
+            comm.barrier()
+            t0 = time.perf_counter()
+            gb.step()
+            ts.append(time.perf_counter() - t0)
+            _sync(torch, dev)
+        return 1e6 * float(np.median(ts))
+
+    import numpy as np
+
+    if gb.graph is not None:
+        out["host_enqueue_us_per_tree_graph"] = enqueue_us(k)
+    # eager launch sequence with per-phase device timers
+    gb.graph, gb.use_graph = None, False
+    b.tree_ctr = None
+    out["host_enqueue_us_per_tree_eager"] = enqueue_us(k)
+    b.timer.enabled = True
+    comm.enable_timing(True)
+    comm.collective_stats(reset=True)
+    b.timer.acc.clear()
+    for _ in range(k):
+        gb.step()
+    _sync(torch, dev)
+    ph = {name: 1000.0 * v / k for name, v in b.timer.totals().items()}
+    coll = comm.collective_stats()
+    comm.enable_timing(False)
+    b.timer.enabled = False
+    ph["grad"] = ph.get("grad", 0.0)
+    out["host_enqueue_us_per_tree"] = out.get("host_enqueue_us_per_tree_graph", out["host_enqueue_us_per_tree_eager"])
+    out["phase_us_per_tree"] = {n: round(v, 1) for n, v in ph.items()}
+    out["small_kernel_us_per_tree"] = round(sum(ph.get(n, 0.0) for n in ("hist_reduce", "split", "tree_begin",
+                                                                         "leaf")), 1)
+    out["allreduce_us_per_tree"] = round(ph.get("allreduce", 0.0), 1)
+    out["allreduce_calls_per_tree"] = coll["all_reduce_calls"] / k
+    out["allreduce_bytes_per_tree"] = coll["all_reduce_bytes"] / k
+    out["instrument_note"] = (f"{k} extra eager trees after the timed run with HIP-event phase timers "
+                              "(phase sums include event overhead); host enqueue = median over steps with the GPU idle")
     return out
 
 
@@ -303,7 +403,15 @@ def main(argv=None) -> int:
     ap.add_argument("--precision", choices=["bf16", "fp32"], default="fp32",
                     help="dl-mlp GEMM operand precision: fp32 (default, H2O DeepLearning trains in fp32) or bf16 "
                          "(h2omx extension; fp32 accumulation and master weights either way)")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="gbm-higgs default strong (11M rows in total, split over the ranks: the headline metric's "
+                         "config at every N); xgboost-airlines / dl-mlp default weak (their configs are per-GPU)")
+    ap.add_argument("--dump-trees", default="", help="tree models: rank 0 saves the trained trees (.npy)")
+    ap.add_argument("--instrument-steps", type=int, default=-1,
+                    help="tree models: extra steps measuring host enqueue / per-phase / collective time; "
+                         "-1 = 5 on GPU, 0 on CPU")
+    ap.add_argument("--tree-graph", choices=["auto", "0", "1"], default="auto",
+                    help="tree models: HIP-graph replay of each boosting step (H2OMX_TREE_GRAPH)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto",
                     help="cpu: the torch reference paths (multi-rank rehearsal of this script over gloo)")
@@ -314,6 +422,9 @@ def main(argv=None) -> int:
     ap.add_argument("--oracle-rows", type=int, default=0,
                     help="also fit sklearn HistGradientBoosting on this many rows for AUC parity")
     args = ap.parse_args(argv)
+    if args.scaling is None:
+        args.scaling = "strong" if args.model == "gbm-higgs" else "weak"
+    os.environ["H2OMX_TREE_GRAPH"] = args.tree_graph
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # not under torchrun: start one rank per GPU here (fresh child processes;
@@ -331,7 +442,14 @@ def main(argv=None) -> int:
     from h2omx.parallel.comm import Comm
 
     device = args.device if args.device != "auto" else ("cuda" if torch.cuda.device_count() > 0 else "cpu")
+    if args.instrument_steps < 0:
+        args.instrument_steps = 5 if device == "cuda" else 0
     comm = Comm.from_env(device)
+    topo = None
+    if comm.world_size > 1:
+        from h2omx.runtime.topology import check_cloud
+
+        topo = check_cloud(comm)
     if args.model == "dl-mlp":
         out = _mlp(args, comm, torch, np)
     else:
@@ -342,6 +460,8 @@ def main(argv=None) -> int:
                "ms_per_step": out.pop("ms_per_step"), "higher_is_better": out.pop("higher_is_better"),
                "scaling": args.scaling, "vs_baseline": None}
         res.update(out)
+        if topo is not None:
+            res["topology"] = {"p2p": {h: e["p2p"] for h, e in topo["hosts"].items()}, "problems": topo["problems"]}
         print(json.dumps(res), flush=True)
     comm.shutdown()
     return 0

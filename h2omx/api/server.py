@@ -1084,6 +1084,9 @@ class H2OApi:
             "# TYPE h2omx_cloud_size gauge", f"h2omx_cloud_size {self.cluster.world_size}",
             "# TYPE h2omx_allreduce_calls_total counter", f"h2omx_allreduce_calls_total {comm['all_reduce_calls']}",
             "# TYPE h2omx_allreduce_bytes_total counter", f"h2omx_allreduce_bytes_total {comm['all_reduce_bytes']}",
+            "# TYPE h2omx_allreduce_seconds_total counter", f"h2omx_allreduce_seconds_total {comm['all_reduce_s']}",
+            "# TYPE h2omx_allgather_calls_total counter", f"h2omx_allgather_calls_total {comm['all_gather_calls']}",
+            "# TYPE h2omx_broadcast_calls_total counter", f"h2omx_broadcast_calls_total {comm['broadcast_calls']}",
             "# TYPE h2omx_dkv_keys gauge", f"h2omx_dkv_keys {len(DKV.keys())}",
         ]
         try:

@@ -321,6 +321,7 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     int wgpg, int slot_lo, int slot_cnt, const short* __restrict__ slot16, unsigned long long* __restrict__ pk_buf,
     unsigned long long* __restrict__ partials, const PartInfo* __restrict__ part_prev,
     const int* __restrict__ ctl_prev, int* __restrict__ nid_out, int writer, GradFuse gf) {
+  salt = (uint32_t)qscale[9];  // per-tree dither salt, written by tree_begin (graph-replay safe)
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
   __shared__ int width_s[256], rep_s[256];
   __shared__ float rcp_s[256];
@@ -769,6 +770,7 @@ __global__ __launch_bounds__(1024) void hist_build_compact_kernel(
     const int* __restrict__ nid, const NodeLink* __restrict__ link, const int* __restrict__ ctl,
     const int* __restrict__ nvb, const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups,
     int wgpg, int slot_lo, int slot_cnt, int rows_per_unit, unsigned long long* __restrict__ partials) {
+  salt = (uint32_t)qscale[9];  // per-tree dither salt, written by tree_begin (graph-replay safe)
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
   __shared__ int width_s[256], rep_s[256];
   const int n_slots = ctl[CTL_SLOTS];
@@ -2026,7 +2028,12 @@ __global__ __launch_bounds__(1024) void stat_reduce_kernel(const unsigned int* _
 // proportionally finer quantisation.
 __device__ void tree_begin_scales(const unsigned int* __restrict__ stat_max, int mode, double qg, double qsr,
                                   double* __restrict__ qs, int* __restrict__ ctl0, NodeLink* __restrict__ link0,
-                                  long long row_base) {
+                                  long long row_base, int tree_index, int* __restrict__ tree_ctr) {
+  // dither salt of this tree: the host's tree index, or (captured / replayed
+  // trees) a device counter that advances once per tree
+  int ti = tree_index;
+  if (tree_ctr != nullptr) { ti = tree_ctr[0]; tree_ctr[0] = ti + 1; }
+  qs[9] = (double)(ti & 0x7FFFFFFF);
   const double gmax = fmax((double)__uint_as_float(stat_max[0]), 1e-30);
   const double hmax = fmax((double)__uint_as_float(stat_max[1]), 1e-30);
   const double wmax = fmax((double)__uint_as_float(stat_max[2]), 1e-30);
@@ -2050,10 +2057,10 @@ __global__ __launch_bounds__(256) void tree_begin_kernel(const unsigned int* __r
                                                          double qg, double qsr, double* __restrict__ qs,
                                                          int* __restrict__ ctl0, NodeLink* __restrict__ link0,
                                                          unsigned long long* __restrict__ leaf_acc, int leaf_n,
-                                                         long long row_base) {
+                                                         long long row_base, int tree_index, int* __restrict__ tree_ctr) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < leaf_n; i += gridDim.x * blockDim.x) leaf_acc[i] = 0ull;
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0, row_base);
+  tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0, row_base, tree_index, tree_ctr);
 }
 
 // Exact per-leaf (G, H, W) sums after the last partition: every row carries
@@ -2567,12 +2574,13 @@ H2OMX_API int h2omx_stat_reduce(const unsigned int* slab, unsigned int* stat_max
 
 H2OMX_API int h2omx_tree_begin(const unsigned int* stat_max, int mode, int max_rows_per_wg, double* qscale,
                                int* ctl0, void* link0, unsigned long long* leaf_acc, int leaf_n,
-                               long long row_base, hipStream_t stream) {
+                               long long row_base, int tree_index, int* tree_ctr, hipStream_t stream) {
   if (max_rows_per_wg < 1 || max_rows_per_wg > ROWS_CAP) return kBadArg;
   const double qg = exp2(floor(log2(1073741824.0 / max_rows_per_wg)));   // |sum| <= 2^30
   const double qsr = exp2(floor(log2(2147483648.0 / max_rows_per_wg)));  // sum <= 2^31
   hipLaunchKernelGGL(tree_begin_kernel, dim3(grid_for(leaf_n, 256, 1024)), dim3(256), 0, stream, stat_max, mode, qg,
-                     qsr, qscale, ctl0, reinterpret_cast<NodeLink*>(link0), leaf_acc, leaf_n, row_base);
+                     qsr, qscale, ctl0, reinterpret_cast<NodeLink*>(link0), leaf_acc, leaf_n, row_base, tree_index,
+                     tree_ctr);
   return launch_status();
 }
 
@@ -2665,11 +2673,11 @@ __global__ __launch_bounds__(256) void tree_begin_seg_kernel(
     int* __restrict__ ctl0, NodeLink* __restrict__ link0, unsigned long long* __restrict__ leaf_acc, int leaf_n,
     long long* __restrict__ built, int built_n, int n_rows, int hc_rows, int* __restrict__ seg_start,
     int* __restrict__ seg_cnt, int* __restrict__ hc_first, int* __restrict__ pc_first, int* __restrict__ slot_node,
-    long long row_base) {
+    long long row_base, int tree_index, int* __restrict__ tree_ctr) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < leaf_n; i += gridDim.x * blockDim.x) leaf_acc[i] = 0ull;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < built_n; i += gridDim.x * blockDim.x) built[i] = 0ll;
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0, row_base);
+  tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0, row_base, tree_index, tree_ctr);
   seg_start[0] = 0;
   seg_cnt[0] = n_rows;
   hc_first[0] = 0;
@@ -2686,6 +2694,7 @@ __global__ __launch_bounds__(512) void hist_build_seg_kernel(
     const int* __restrict__ hc_first, const int* __restrict__ ctl, const int* __restrict__ nvb,
     const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups, int hc_rows,
     unsigned long long* __restrict__ slab, int gpos) {
+  salt = (uint32_t)qscale[9];  // per-tree dither salt, written by tree_begin (graph-replay safe)
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
   __shared__ int width_s[256], rep_s[256];
   __shared__ int range_s[2];
@@ -3268,6 +3277,7 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
     const int* __restrict__ ctl, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
     const double* __restrict__ qscale, uint32_t salt, SplitParams p, int batch, NodeSplit* __restrict__ out,
     int gpos, ECodes ec) {
+  salt = (uint32_t)qscale[9];  // per-tree dither salt, written by tree_begin (graph-replay safe)
   extern __shared__ __attribute__((aligned(16))) long long hist[];   // [batch][2][NBT] (packed: [batch][NBT])
   __shared__ int flist[1024];
   __shared__ uint32_t hsh_s[1024];
@@ -3493,6 +3503,7 @@ __global__ __launch_bounds__(256) void seg_direct_chunk_kernel(
     const uint8_t* __restrict__ tree_fmask, const double* __restrict__ qscale, uint32_t salt, SplitParams p,
     int nfl_max, unsigned long long* __restrict__ slab, long long* __restrict__ tot_slab, int* __restrict__ ticket,
     NodeSplit* __restrict__ out, int gpos, ECodes ec) {
+  salt = (uint32_t)qscale[9];  // per-tree dither salt, written by tree_begin (graph-replay safe)
   extern __shared__ __attribute__((aligned(16))) long long hist[];   // packed [nfl][NBT]; reduce: [nfl][2][NBT]
   __shared__ int flist[1024];
   __shared__ uint32_t hsh_s[1024];
@@ -3619,6 +3630,7 @@ __global__ __launch_bounds__(256) void seg_direct_wave_kernel(
     const int* __restrict__ ctl, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
     const double* __restrict__ qscale, uint32_t salt, SplitParams p, int batch, NodeSplit* __restrict__ out,
     int gpos, ECodes ec) {
+  salt = (uint32_t)qscale[9];  // per-tree dither salt, written by tree_begin (graph-replay safe)
   extern __shared__ __attribute__((aligned(16))) long long hist_all[];   // [4][batch * 2 * NBT]
   __shared__ short flist_all[4][DIRECT_WAVE_F];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -3969,14 +3981,14 @@ H2OMX_API int h2omx_tree_begin_seg(const unsigned int* stat_max, int mode, int m
                                    int* ctl0, void* link0, unsigned long long* leaf_acc, int leaf_n,
                                    long long* built, int built_n, int n_rows, int hc_rows, int* seg_start,
                                    int* seg_cnt, int* hc_first, int* pc_first, int* slot_node, long long row_base,
-                                   hipStream_t stream) {
+                                   int tree_index, int* tree_ctr, hipStream_t stream) {
   if (max_rows_per_wg < 1 || max_rows_per_wg > ROWS_CAP || hc_rows > max_rows_per_wg) return kBadArg;
   const double qg = exp2(floor(log2(1073741824.0 / max_rows_per_wg)));
   const double qsr = exp2(floor(log2(2147483648.0 / max_rows_per_wg)));
   const int m = leaf_n > built_n ? leaf_n : built_n;
   hipLaunchKernelGGL(tree_begin_seg_kernel, dim3(grid_for(m, 256, 1024)), dim3(256), 0, stream, stat_max, mode, qg,
                      qsr, qscale, ctl0, reinterpret_cast<NodeLink*>(link0), leaf_acc, leaf_n, built, built_n, n_rows,
-                     hc_rows, seg_start, seg_cnt, hc_first, pc_first, slot_node, row_base);
+                     hc_rows, seg_start, seg_cnt, hc_first, pc_first, slot_node, row_base, tree_index, tree_ctr);
   return launch_status();
 }
 

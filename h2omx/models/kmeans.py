@@ -120,8 +120,9 @@ class H2OKMeansEstimator(ModelBuilder):
         return model
 
     # estimate_k: stop adding centers once the proportional reduction in the
-    # within-cluster sum of squares falls below this (H2O's PRE rule; the exact
-    # H2O threshold is unpinned here)
+    # within-cluster sum of squares falls below this (H2O's PRE rule; the
+    # threshold is unpinned: the reference holds no estimate_k output, see
+    # docs/PARITY.md)
     PRE_MIN = 0.1
 
     def _estimate_k(self, X, kmax, how, g, design):
@@ -134,11 +135,13 @@ class H2OKMeansEstimator(ModelBuilder):
         prev_ss, best = None, C
         for kk in range(1, kmax + 1):
             if kk > 1:
-                far = self._farthest(X, C, 1)
-                if comm is not None and comm.world_size > 1:   # every rank adopts rank 0's point
-                    t = torch.from_numpy(far).to(X.device)
-                    comm.broadcast(t, 0)
-                    far = t.cpu().numpy()
+                far, dist2 = self._farthest(X, C, 1, with_dist=True)
+                if comm is not None and comm.world_size > 1:
+                    # the GLOBAL farthest point: every rank offers its local candidate
+                    # and distance; the largest distance wins (lowest rank on a tie)
+                    cands = comm.all_gather_object((float(dist2[0]), comm.rank, far[0].tolist()))
+                    best_c = max(cands, key=lambda c: (c[0], -c[1]))
+                    far = np.asarray([best_c[2]], np.float64)
                 C = np.concatenate([C, far])
             for _ in range(int(self.params["max_iterations"])):
                 assign, sums, cnt, sse = D.kmeans_step(X, torch.from_numpy(C.astype(np.float32)).to(X.device))
@@ -182,11 +185,12 @@ class H2OKMeansEstimator(ModelBuilder):
             mind = torch.minimum(mind, ((X.double() - c[:, None]) ** 2).sum(0))
         return np.stack(C)
 
-    def _farthest(self, X, C, m):
+    def _farthest(self, X, C, m, with_dist: bool = False):
         Ct = torch.from_numpy(C).to(X.device)
         d2 = (X.double().pow(2).sum(0)[None, :] - 2 * Ct @ X.double() + Ct.pow(2).sum(1)[:, None]).min(0).values
-        idx = torch.topk(d2, m).indices
-        return X[:, idx].T.double().cpu().numpy()
+        top = torch.topk(d2, m)
+        pts = X[:, top.indices].T.double().cpu().numpy()
+        return (pts, top.values.cpu().numpy()) if with_dist else pts
 
     def train(self, x=None, y=None, training_frame=None, validation_frame=None, comm=None, **kw):
         return super().train(x=x, y=None, training_frame=training_frame, validation_frame=validation_frame,

@@ -9,6 +9,8 @@ produces the next gradients, bagging weights and node ids in one pass.
 from __future__ import annotations
 
 import ctypes
+import gc
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -137,15 +139,58 @@ def init_margin(dist: str, y, w, K: int) -> np.ndarray:
     return np.array([(ww * y).sum() / sw])
 
 
+def weighted_quantile(r, w, q: float, comm=None) -> float:
+    """Weighted 'lower' q-quantile of ``r`` over every rank: the smallest value
+    v of the data with sum(w[r <= v]) >= q * sum(w).  Bisection on the value
+    with one all-reduced weight sum per step (no gather of the rows, any row
+    count; torch.quantile is limited to 2^24 elements), then snapped to the
+    smallest data value >= the bracket."""
+    multi = comm is not None and comm.world_size > 1
+    r = r.detach().double() if torch.is_tensor(r) else torch.from_numpy(np.asarray(r, np.float64))
+    wt = torch.ones_like(r) if w is None else (w.detach().double() if torch.is_tensor(w)
+                                               else torch.from_numpy(np.asarray(w, np.float64))).to(r.device)
+    keep = wt > 0
+    r, wt = r[keep], wt[keep]
+
+    def red(v, op="sum"):
+        a = np.array(v, np.float64)
+        return comm.all_reduce_numpy(a, op) if multi else a
+
+    big = 1e300
+    lo = -float(red([-(float(r.min()) if r.numel() else -big)], "max")[0])
+    hi = float(red([float(r.max()) if r.numel() else -big], "max")[0])
+    W = float(red([float(wt.sum())])[0])
+    if W <= 0:
+        return 0.0
+    target = q * W
+    if float(red([float(wt[r <= lo].sum())])[0]) >= target:
+        return lo
+    for _ in range(200):            # invariant: cum(lo) < target <= cum(hi)
+        mid = 0.5 * (lo + hi)
+        if mid <= lo or mid >= hi:
+            break
+        if float(red([float(wt[r <= mid].sum())])[0]) >= target:
+            hi = mid
+        else:
+            lo = mid
+    # smallest data value in (lo, hi]
+    cand = r[(r > lo) & (r <= hi)]
+    v = -float(red([-(float(cand.min()) if cand.numel() else big)], "max")[0])
+    return v if v < big else hi
+
+
 def train_ensemble(bm: BinnedMatrix, y, w=None, *, dist: str = "bernoulli", ntrees: int = 50,
                    tparams: TreeParams | None = None, sample_rate: float = 1.0, nclass: int = 1,
                    seed: int = 0, comm=None, init_f: np.ndarray | None = None, callback=None,
-                   dist_kw: dict | None = None, base_margin=None) -> TreeEnsemble:
+                   dist_kw: dict | None = None, base_margin=None, tree_offset: int = 0) -> TreeEnsemble:
     """Grow an ensemble on binned data.
 
     ``y``: float targets (class index for multinomial / multi-class DRF).
     ``dist``: gaussian|bernoulli|multinomial|poisson|gamma|tweedie|laplace|quantile|huber|drf.
     ``base_margin``: [K][n] starting margins (checkpoint continuation) instead of ``init_f``.
+    ``tree_offset``: iterations already in the model being continued: iteration t
+    is global iteration tree_offset + t (learn-rate annealing, bagging / column
+    sampling hashes, dither), so a continued model equals one long run.
     ``callback(t, view)``: called after every iteration; returning True stops training.
     """
     tparams = tparams or TreeParams()
@@ -165,7 +210,11 @@ def train_ensemble(bm: BinnedMatrix, y, w=None, *, dist: str = "bernoulli", ntre
         w_np = None if w is None else (w.detach().float().cpu().numpy() if torch.is_tensor(w)
                                        else np.asarray(w, np.float32))
     if init_f is None:
-        if comm is not None and comm.world_size > 1:
+        if dist in ("laplace", "quantile"):
+            # H2O: weighted median / alpha-quantile of the response, over all ranks
+            q = 0.5 if dist == "laplace" else float(dist_kw.get("quantile_alpha", 0.5))
+            init_f = np.array([weighted_quantile(y_np, w_np, q, comm)])
+        elif comm is not None and comm.world_size > 1:
             init_f = _global_init(dist, y_np, w_np, K, comm)
         else:
             init_f = init_margin(dist, y_np, w_np, K)
@@ -174,12 +223,12 @@ def train_ensemble(bm: BinnedMatrix, y, w=None, *, dist: str = "bernoulli", ntre
                        feature_names=list(bm.names), edges=bm.edges_numpy())
     ens._base_margin = base_margin
     if bm.codes.is_cuda:
-        _train_gpu(bm, y_np, w_np, ens, ntrees, tparams, sample_rate, seed, comm, callback, dist_kw)
+        _train_gpu(bm, y_np, w_np, ens, ntrees, tparams, sample_rate, seed, comm, callback, dist_kw, tree_offset)
     else:
         # host-resident bins: the fp64 reference builder (test oracle, CPU-only clouds)
         from ...reference.tree import train_cpu
 
-        train_cpu(bm, y_np, w_np, ens, ntrees, tparams, sample_rate, seed, comm, callback, dist_kw)
+        train_cpu(bm, y_np, w_np, ens, ntrees, tparams, sample_rate, seed, comm, callback, dist_kw, tree_offset)
     return ens
 
 
@@ -238,7 +287,7 @@ class _GpuState:
 class GpuBooster:
     """Step-wise GPU boosting loop (one ``step()`` = one iteration = K trees)."""
 
-    def __init__(self, bm, y_np, w_np, ens, tp, sample_rate, seed, comm, dist_kw, ntrees_hint=64):
+    def __init__(self, bm, y_np, w_np, ens, tp, sample_rate, seed, comm, dist_kw, ntrees_hint=64, tree_offset=0):
         self.lib = ops.tree_lib()
         self.bm, self.ens, self.tp = bm, ens, tp
         self.sample_rate, self.seed = sample_rate, seed
@@ -253,11 +302,17 @@ class GpuBooster:
         self.kw = dict(tweedie_power=dist_kw.get("tweedie_power", 1.5),
                        quantile_alpha=dist_kw.get("quantile_alpha", 0.5),
                        huber_delta=dist_kw.get("huber_delta", 1.0))
-        self.t = 0
+        self.t = tree_offset       # global iteration index (checkpoint continuation)
+        self.t_start = tree_offset
         # K == 1 with bounded gradients: each tree's level 0 applies the previous
         # tree and computes the gradients itself (no boost_update pass); the
         # margins then lag one tree until flush()
         self.fused = (self.K == 1 and self.builder.can_fuse_grad(self.dist, self.st.w is not None, sample_rate))
+        # HIP-graph replay of the step (TreeGraph): H2OMX_TREE_GRAPH=0 off, 1 / auto on
+        # when graph_eligible(); captured at the second step (the first allocates buffers)
+        self.use_graph = os.environ.get("H2OMX_TREE_GRAPH", "auto") != "0" and self.graph_eligible()
+        self.graph = None
+        self.graph_error = None
         self.pending = False
         # bounded gradients (unweighted rows; bagging only zeroes rows) quantise with
         # the bound scales on every path, fused or not
@@ -267,7 +322,7 @@ class GpuBooster:
         if self.fused:
             pass
         elif self.K == 1:
-            self._update(apply=False, next_tree=0, k=0)
+            self._update(apply=False, next_tree=self.t, k=0)
 
     def flush(self):
         """Bring the margins up to date (fused mode applies each tree inside the
@@ -296,8 +351,36 @@ class GpuBooster:
             if not fixed:
                 b.reduce_stats()
 
+    def graph_eligible(self) -> bool:
+        """A step is a fixed launch sequence whose only per-tree host input is
+        the tree index (dither salt, read on the device from builder.tree_ctr):
+        one tree per iteration, no bagging / column sampling / learn-rate
+        annealing (those bake per-tree host values into the launches), the scan
+        engine (the segmented one reads node counts on the host) and no phase
+        timers (events are host objects)."""
+        tp, b = self.tp, self.builder
+        return (self.K == 1 and not self.fused and self.sample_rate >= 1.0 and tp.col_sample_rate >= 1.0
+                and tp.col_sample_rate_per_tree >= 1.0 and tp.mtries == 0 and tp.learn_rate_annealing == 1.0
+                and not b.segmented and not b.timer.enabled and self.cap <= self.COMPACT_CAP
+                and self.dev.type == "cuda")
+
+    def _body_k1(self, t: int, fresh: bool):
+        b = self.builder
+        if fresh:
+            # grow the tree straight into its own buffer (no copy afterwards);
+            # the next boost_update applies it from there
+            b.tree_buf = torch.empty_like(b.tree_buf)
+        b.build(self.st.g[0], self.st.h[0], self.wout, t, None, stat=self._bounds)
+
     def step(self):
         P, st, b, bm, t = ops.P, self.st, self.builder, self.bm, self.t
+        if self.graph is None and self.use_graph and t >= self.t_start + 1:
+            self._try_capture()
+        if self.graph is not None:
+            self.graph.replay(t)
+            self.trees_dev.append(b.tree_buf.clone())
+            self.t += 1
+            return
         fmask = _tree_fmask(self.tp, bm.F, t, self.dev)
         if self.K == 1 and self.fused:
             gp = make_grad_params(self.dist, False, 1.0, self.seed, t, row_base=b.row_base, **self.kw)
@@ -341,6 +424,21 @@ class GpuBooster:
 
     COMPACT_CAP = 8191   # deeper trees: copy only the nodes actually created
 
+    def _try_capture(self):
+        b = self.builder
+        try:
+            g = TreeGraph(self)
+            g.capture()
+        except Exception as e:   # capture unsupported here: keep stepping eagerly
+            b.tree_ctr = None
+            self.use_graph = False
+            self.graph_error = f"{type(e).__name__}: {e}"
+            import warnings
+
+            warnings.warn(f"h2omx: tree step graph capture failed, running eagerly ({self.graph_error})")
+            return
+        self.graph = g
+
     def _snapshot(self) -> torch.Tensor:
         """Copy of the finished tree.  Shallow trees copy the whole capacity-sized
         heap without a host sync; deep trees (DRF depth 20: 2^21 slots, 64 MB)
@@ -369,13 +467,13 @@ class GpuBooster:
         return self.ens
 
 
-def _train_gpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw):
+def _train_gpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw, tree_offset=0):
     t0 = time.perf_counter()
-    gb = GpuBooster(bm, y_np, w_np, ens, tp, sample_rate, seed, comm, dist_kw)
+    gb = GpuBooster(bm, y_np, w_np, ens, tp, sample_rate, seed, comm, dist_kw, tree_offset=tree_offset)
     lr0, ann = tp.learn_rate, tp.learn_rate_annealing
     for t in range(ntrees):
         if ann != 1.0:
-            gb.builder.p.learn_rate = lr0 * ann ** t
+            gb.builder.p.learn_rate = lr0 * ann ** (tree_offset + t)
         gb.step()
         if callback is not None and callback(t, _GpuView(gb)) is True:
             break
@@ -421,4 +519,103 @@ def _tree_fmask(tp: TreeParams, F: int, t: int, dev):
         m[int(np.argmin(hs))] = 1
     return torch.from_numpy(m).to(dev) if dev is not None else m
 
+
+class TreeGraph:
+    """HIP-graph replay of one boosting step (K == 1): tree_begin -> per level
+    {hist_build, hist_reduce, [all-reduce], split_find, level_finalize,
+    partition} -> leaf_finalize -> boost_update, i.e. ~30 launches that the
+    host otherwise enqueues one ctypes call at a time.
+
+    The only per-tree host input of the sequence is the tree index (dither
+    salt); replays take it from ``builder.tree_ctr``, which tree_begin reads
+    and advances on the device, so replayed trees are bit-identical to eager
+    ones.  Buffers are the builder's fixed ones (allocated by the first, eager
+    step) and the tree is grown in place in ``builder.tree_buf``; the caller
+    snapshots it after every replay.
+
+    Multi-rank: by default the step is captured in SEGMENTS split at the
+    collectives, which are issued eagerly between segment replays (works with
+    any backend, nothing of RCCL inside a graph).  ``H2OMX_GRAPH_COLLECTIVES=1``
+    captures the RCCL all-reduces inside one graph instead (RCCL supports
+    stream capture; not exercised on the one-GPU development box).
+    """
+
+    def __init__(self, booster):
+        self.gb = booster
+        self.comm = booster.builder.comm
+        self.graphs: list = []
+        self.colls: list = []
+        self.pool = None
+
+    def capture(self):
+        gb, b = self.gb, self.gb.builder
+        dev = gb.dev
+        b.tree_ctr = torch.zeros((1,), dtype=torch.int32, device=dev)
+        # the graph's own tree buffer: eager steps hand their tree_buf to trees_dev
+        # (fresh buffers), which replays must not overwrite
+        b.tree_buf = torch.zeros_like(b.tree_buf)
+        multi = self.comm is not None and self.comm.world_size > 1
+        segmented = multi and os.environ.get("H2OMX_GRAPH_COLLECTIVES", "0") != "1"
+        self.pool = torch.cuda.graph_pool_handle()
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.synchronize(dev)
+        # no garbage collection while capturing: a collected graph / event / pool
+        # of an earlier model would be destroyed inside the capture (illegal
+        # while a stream captures; torch.cuda.graph collects up front the same way)
+        gc.collect()
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.stream(side):
+                g = torch.cuda.CUDAGraph()
+                g.capture_begin(pool=self.pool)
+                self._open = g
+                if segmented:
+                    b.comm = _SegmentComm(self, self.comm)
+                try:
+                    gb._body_k1(gb.t, fresh=False)
+                    gb._update(apply=True, next_tree=gb.t + 1, k=0)
+                finally:
+                    b.comm = self.comm
+                    self._open.capture_end()
+                    self.graphs.append(self._open)
+                    self._open = None
+        finally:
+            if gc_was:
+                gc.enable()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+
+    def _cut(self, t, op):
+        """segment boundary at a collective: close the open graph, remember the
+        collective, open the next graph"""
+        self._open.capture_end()
+        self.graphs.append(self._open)
+        self.colls.append((t, op))
+        g = torch.cuda.CUDAGraph()
+        g.capture_begin(pool=self.pool)
+        self._open = g
+
+    def replay(self, t: int):
+        """Grow tree ``t`` (and update margins / gradients for tree t + 1)."""
+        self.gb.builder.tree_ctr.fill_(t & 0x7FFFFFFF)
+        for i, g in enumerate(self.graphs):
+            g.replay()
+            if i < len(self.colls):
+                buf, op = self.colls[i]
+                self.comm.all_reduce_(buf, op)
+
+
+class _SegmentComm:
+    """Stand-in for the builder's Comm while a segmented TreeGraph is captured:
+    every collective becomes a segment boundary instead of a captured call."""
+
+    def __init__(self, graph: TreeGraph, comm):
+        self._graph, self._comm = graph, comm
+        self.world_size, self.rank, self.device = comm.world_size, comm.rank, comm.device
+
+    def all_reduce_(self, t, op: str = "sum"):
+        self._graph._cut(t, op)
+        return t
 

@@ -182,6 +182,9 @@ class HipTreeBuilder:
         # opt-in (H2OMX_FUSE_SPLIT=1)
         self.fuse_split = self.F <= 64 and os.environ.get("H2OMX_FUSE_SPLIT", "0") == "1"
         self.ticket = torch.zeros((4,), dtype=torch.int32, device=d)
+        # graph replay (boost.TreeGraph): tree_begin takes the tree index (dither salt,
+        # qscale[9]) from this device counter instead of the host argument, and advances it
+        self.tree_ctr = None
         # Engine choice (both build bit-identical trees):
         # * scan: every level streams all rows; best for shallow trees (HIGGS depth 5:
         #   1.52 vs 1.90 ms/tree for the segmented engine, profiles/seg_vs_scan_s1.txt)
@@ -362,7 +365,7 @@ class HipTreeBuilder:
         with T("tree_begin"):
             ops.check(lib.h2omx_tree_begin(P(smax), p.mode, self.max_rows_per_wg, P(self.qscale),
                                            P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(),
-                                           self.row_base, st), "tree_begin")
+                                           self.row_base, tree_index & 0x7FFFFFFF, P(self.tree_ctr), st), "tree_begin")
         full_prev = None
         max_depth = p.max_depth
         final_ctl = self.ctl[max_depth % 2]
@@ -430,6 +433,7 @@ class HipTreeBuilder:
                             P(self.slot16), P(self.pk),
                             (1 if d == 0 else 2 + cmp_flag) + (2 if self.pk32 else 0), P(partials), st),
                             "hist_build")
+                with T("hist_reduce"):
                     ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F,
                                                     nbt, slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st),
                               "hist_reduce")
@@ -527,7 +531,8 @@ class HipTreeBuilder:
         ops.check(lib.h2omx_tree_begin_seg(P(smax), p.mode, self.max_rows_per_wg, P(self.qscale),
                                            P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(),
                                            P(built), self.per_node, n, self.hc_rows, P(seg[0][0]), P(seg[0][1]),
-                                           P(seg[0][2]), P(seg[0][3]), P(seg[0][4]), self.row_base, st),
+                                           P(seg[0][2]), P(seg[0][3]), P(seg[0][4]), self.row_base,
+                                           tree_index & 0x7FFFFFFF, P(self.tree_ctr), st),
                   "tree_begin_seg")
         full_prev = None
         max_depth = p.max_depth

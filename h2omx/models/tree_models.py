@@ -172,7 +172,7 @@ class _TreeBuilder(ModelBuilder):
                              sample_rate=float(self.params.get("sample_rate", 1.0)), nclass=nclass,
                              seed=self._seed(), comm=self.comm, init_f=init_f,
                              callback=scorer if scorer.active else None,
-                             base_margin=base_margin,
+                             base_margin=base_margin, tree_offset=0 if ckpt is None else ckpt.ntrees,
                              dist_kw={"tweedie_power": float(self.params.get("tweedie_power", 1.5)),
                                       "quantile_alpha": float(self.params.get("quantile_alpha", 0.5)),
                                       "huber_delta": float(self.params.get("huber_alpha", 0.9))})
@@ -252,22 +252,36 @@ def _fit_calibration(model, cal, method: str) -> dict:
     y = model.adapt_frame(cal).vec(model.y).data.long().to(p1.device)
     ok = y >= 0
     p1, y = p1[ok], (y[ok] == 1).double()
+    comm = getattr(model, "comm", None)
+    multi = comm is not None and comm.world_size > 1
     m = method.lower()
     if m in ("auto", "plattscaling", "platt_scaling"):
-        a = torch.zeros(2, dtype=torch.float64, device=p1.device)
+        # Newton on the row-sharded calibration frame: the 2-vector gradient and
+        # 2x2 Hessian are all-reduced every iteration, so all ranks take the
+        # same steps and end with the coefficients of the whole frame
+        a = np.zeros(2)
         Xd = torch.stack([torch.ones_like(p1), p1], 1)
         for _ in range(100):
-            mu = torch.sigmoid(Xd @ a)
+            mu = torch.sigmoid(Xd @ torch.from_numpy(a).to(p1.device))
             g = Xd.T @ (y - mu)
-            H = (Xd * (mu * (1 - mu))[:, None]).T @ Xd + 1e-10 * torch.eye(2, dtype=torch.float64, device=p1.device)
-            step = torch.linalg.solve(H, g)
+            H = (Xd * (mu * (1 - mu))[:, None]).T @ Xd
+            gh = torch.cat([g, H.reshape(-1)]).cpu().numpy()
+            if multi:
+                gh = comm.all_reduce_numpy(gh)
+            step = np.linalg.solve(gh[2:].reshape(2, 2) + 1e-10 * np.eye(2), gh[:2])
             a = a + step
-            if float(step.abs().max()) < 1e-12:
+            if float(np.abs(step).max()) < 1e-12:
                 break
         return {"method": "PlattScaling", "intercept": float(a[0]), "slope": float(a[1])}
     if m in ("isotonicregression", "isotonic_regression"):
-        order = torch.argsort(p1)
-        xs, ys = p1[order].cpu().numpy(), y[order].cpu().numpy()
+        if multi:
+            # PAV needs the globally sorted pairs: every rank gathers them and fits
+            # the same step function
+            p1, y = comm.all_gather_cat(p1.contiguous()), comm.all_gather_cat(y.contiguous())
+        # ties ordered by y too, so the fit does not depend on the row order / sharding
+        pn, yn = p1.cpu().numpy(), y.cpu().numpy()
+        order = np.lexsort((yn, pn))
+        xs, ys = pn[order], yn[order]
         vals, wts, xs_hi = [], [], []
         for xv, yv in zip(xs, ys):            # pool adjacent violators
             vals.append(yv); wts.append(1.0); xs_hi.append(xv)
@@ -326,8 +340,8 @@ def _balance_weights(y, w, K: int, params, comm=None):
 def _offset_init(dist: str, y, w, off, params, comm=None) -> float:
     """Initial margin c minimising the loss of ``c + offset`` (H2O GBM with an
     offset column): closed forms where they exist, Newton steps for bernoulli.
-    Sums are all-reduced over the ranks (laplace / quantile: the mean of the
-    per-rank medians / quantiles, an approximation on N ranks)."""
+    Sums are all-reduced over the ranks; laplace / quantile take the weighted
+    quantile of y - offset over all ranks (boost.weighted_quantile)."""
     multi = comm is not None and comm.world_size > 1
 
     def red(*v):
@@ -348,17 +362,23 @@ def _offset_init(dist: str, y, w, off, params, comm=None) -> float:
             if abs(g / h) < 1e-12:
                 break
         return c
-    if dist in ("poisson", "tweedie"):
+    if dist == "poisson":
         a, b = red(float((wt * y).sum()), float((wt * torch.exp(o)).sum()))
+        return float(np.log(a / b))
+    if dist == "tweedie":
+        # H2O Tweedie initF: log(sum w y e^{o (1-p)} / sum w e^{o (2-p)})
+        pw = float(params.get("tweedie_power", 1.5))
+        a, b = red(float((wt * y * torch.exp(o * (1 - pw))).sum()), float((wt * torch.exp(o * (2 - pw))).sum()))
         return float(np.log(a / b))
     if dist == "gamma":
         a, b = red(float((wt * y * torch.exp(-o)).sum()), float(wt.sum()))
         return float(np.log(a / b))
     r = y - o
     if dist in ("laplace", "quantile"):
+        from .tree.boost import weighted_quantile
+
         q = 0.5 if dist == "laplace" else float(params.get("quantile_alpha", 0.5))
-        v, = red(float(torch.quantile(r, q)))
-        return float(v / (comm.world_size if multi else 1))
+        return weighted_quantile(r, None if w is None else wt, q, comm)
     a, b = red(float((wt * r).sum()), float(wt.sum()))
     return float(a / b)      # gaussian / huber
 

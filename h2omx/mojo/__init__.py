@@ -201,6 +201,13 @@ def mojo_bytes(model: Model) -> bytes:
         if cal is not None and cal["method"] == "PlattScaling":
             # genmodel calibrateClassProbabilities: p1' = logitInv(p1 * beta[0] + beta[1])
             info.update(calib_method="platt", calib_glm_beta=[cal["slope"], cal["intercept"]])
+        elif cal is not None and cal["method"] == "IsotonicRegression":
+            # step function of the pooled-adjacent-violators fit: p1 clipped to
+            # [x_min, x_max], value of the first threshold >= p1 (h2omx entries;
+            # genmodel parity of the isotonic calibration block is unpinned)
+            info.update(calib_method="isotonic", calib_isotonic_x_min=cal["x_min"])
+            _put(files, info, "calib_isotonic_x", np.asarray(cal["x"], np.float64))
+            _put(files, info, "calib_isotonic_y", np.asarray(cal["y"], np.float64))
     elif algo == "glm" and (getattr(model, "interaction_spec", None) or model.family == "ordinal"):
         columns, ext = _glm_ext_info(model, files)       # h2omx array payload
         info.update(ext)
@@ -294,7 +301,8 @@ def _tree_info(model, files):
     return {"n_trees": nt, "n_trees_per_class": K, "init_f": float(ens.init_f[0]) if K == 1 else 0.0,
             "init_f_per_class": [float(x) for x in ens.init_f], "distribution": dist,
             "h2omx_engine_dist": model.dist, "h2omx_average": bool(ens.average),
-            "offset_column": "null", "binomial_double_trees": False, "link_function": _tree_link(model)}
+            "offset_column": model.params.get("offset_column") or "null", "binomial_double_trees": False,
+            "link_function": _tree_link(model)}
 
 
 def _if_info(model, files):
@@ -1043,6 +1051,16 @@ class GenericModel(Model):
             p1 = fr.vec(self.response_domain[1]).data.double()
             c1 = torch.sigmoid(p1 * float(beta[0]) + float(beta[1])).float()
             fr = Frame(list(fr.vecs) + [Vec("cal_p0", 1.0 - c1, "real"), Vec("cal_p1", c1, "real")])
+        elif self.info.get("calib_method") == "isotonic" and self.response_domain:
+            from ..models.tree_models import _apply_calibration
+
+            z = read_mojo(self.raw_mojo)["zip"]
+            p1 = fr.vec(self.response_domain[1]).data.double()
+            cal = {"method": "IsotonicRegression", "x": _get(z, self.info, "calib_isotonic_x").tolist(),
+                   "y": _get(z, self.info, "calib_isotonic_y").tolist(),
+                   "x_min": float(self.info["calib_isotonic_x_min"])}
+            c1 = _apply_calibration(cal, p1).float()
+            fr = Frame(list(fr.vecs) + [Vec("cal_p0", 1.0 - c1, "real"), Vec("cal_p1", c1, "real")])
         return fr
 
     def _te(self, frame: Frame) -> torch.Tensor:
@@ -1129,7 +1147,14 @@ class GenericModel(Model):
             lo, hi = float(self.info["min_path_length"]), float(self.info["max_path_length"])
             return torch.stack([(hi - L) / max(hi - lo, 1e-12), L])
         if a in ("gbm", "drf", "xgboost"):
-            P = self._tree_scores(self.ens.raw_margin(X).to(X.device))
+            m = self.ens.raw_margin(X).to(X.device)
+            oc = self.info.get("offset_column")
+            if oc not in (None, "null", ""):
+                # H2O GBM with an offset: margin = init_f + offset + trees, link applied after
+                if oc not in frame.names:
+                    raise ValueError(f"MOJO was trained with offset_column {oc!r}; the scoring frame lacks it")
+                m = m + frame.vec(oc).as_float().to(m.device)[None, :]
+            P = self._tree_scores(m)
             if self.info.get("balance_classes") and isinstance(self.info.get("prior_class_distrib"), list):
                 # balance_classes models: genmodel's correctProbabilities
                 from ..models.tree_models import correct_probabilities

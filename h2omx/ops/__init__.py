@@ -37,13 +37,13 @@ TREE_SIGS = {
     "h2omx_softmax_grad": "PILPPLLIPPPPPPS",
     "h2omx_stat_blocks": "",
     "h2omx_stat_reduce": "PPS",
-    "h2omx_tree_begin": "PIIPPPPILS",
+    "h2omx_tree_begin": "PIIPPPPILIPS",
     "h2omx_leaf_stats": "PPPPLPIPS",
     "h2omx_leaf_finalize": "PPPPPIS",
     "h2omx_predict_raw": "PLLPPIIPLS",
     "h2omx_predict_binned": "PLLPPIIIPLS",
     "h2omx_pc_rows": "",
-    "h2omx_tree_begin_seg": "PIIPPPPIPIIIPPPPPLS",
+    "h2omx_tree_begin_seg": "PIIPPPPIPIIIPPPPPLIPS",
     "h2omx_hist_build_seg": "PIPPPPPPPPPIIIIIIIIPIS",
     "h2omx_hist_reduce_seg": "PPPPIIIIIIPS",
     "h2omx_part_count": "PLPPPPPPIIPIPPIPS",

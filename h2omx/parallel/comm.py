@@ -25,7 +25,17 @@ class Comm:
         self.world_size = world_size
         self.device = device or torch.device("cpu")
         self.group = group
-        self.stats = {"all_reduce_calls": 0, "all_reduce_bytes": 0, "all_reduce_s": 0.0}
+        # every collective: calls / bytes / host seconds inside the call (for RCCL the
+        # enqueue cost; gloo blocks, so there it is the whole collective).  With
+        # timing enabled (enable_timing / H2OMX_COMM_TIMING=1) HIP events also
+        # bracket each collective on the current stream: device time including
+        # the wait for the slowest peer, resolved lazily by collective_stats()
+        self.stats = {"all_reduce_calls": 0, "all_reduce_bytes": 0, "all_reduce_s": 0.0,
+                      "all_gather_calls": 0, "all_gather_bytes": 0, "all_gather_s": 0.0,
+                      "broadcast_calls": 0, "broadcast_bytes": 0, "broadcast_s": 0.0}
+        self.timing = os.environ.get("H2OMX_COMM_TIMING") == "1"
+        self._events: list = []
+        self._device_ms: dict[str, float] = {}
         # set by the peer watchdog (runtime/watchdog.py) once a rank is lost:
         # collectives then fail fast instead of blocking on the missing peer
         self.failed: str | None = None
@@ -68,14 +78,53 @@ class Comm:
         return self.rank == 0
 
     # ------------------------------------------------------------------
+    def enable_timing(self, on: bool = True) -> None:
+        self.timing = on
+
+    def _begin(self, kind: str, nbytes: int):
+        self.stats[f"{kind}_calls"] += 1
+        self.stats[f"{kind}_bytes"] += nbytes
+        ev = None
+        if self.timing and self.device.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+        return kind, ev, time.perf_counter()
+
+    def _end(self, tok) -> None:
+        kind, ev, t0 = tok
+        self.stats[f"{kind}_s"] += time.perf_counter() - t0
+        if ev is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._events.append((kind, ev, e1))
+            if len(self._events) > 4096:
+                self._drain()
+
+    def _drain(self) -> None:
+        for kind, a, b in self._events:
+            b.synchronize()
+            self._device_ms[kind] = self._device_ms.get(kind, 0.0) + a.elapsed_time(b)
+        self._events.clear()
+
+    def collective_stats(self, reset: bool = False) -> dict:
+        """Counters of every collective so far (+ device ms per kind when timed)."""
+        self._drain()
+        out = dict(self.stats)
+        out.update({f"{k}_device_ms": v for k, v in self._device_ms.items()})
+        if reset:
+            for k in self.stats:
+                self.stats[k] = 0.0 if k.endswith("_s") else 0
+            self._device_ms.clear()
+        return out
+
     def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if self.world_size == 1:
             return t
         self._check()
-        self.stats["all_reduce_calls"] += 1
-        self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
+        tok = self._begin("all_reduce", t.numel() * t.element_size())
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
         dist.all_reduce(t, op=rop, group=self.group)
+        self._end(tok)
         return t
 
     def all_reduce_async(self, t: torch.Tensor, op: str = "sum"):
@@ -87,7 +136,10 @@ class Comm:
         self.stats["all_reduce_calls"] += 1
         self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
-        return dist.all_reduce(t, op=rop, group=self.group, async_op=True)
+        t0 = time.perf_counter()
+        work = dist.all_reduce(t, op=rop, group=self.group, async_op=True)
+        self.stats["all_reduce_s"] += time.perf_counter() - t0
+        return work
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         return self.broadcast_(t, src)
@@ -116,13 +168,17 @@ class Comm:
         buf = torch.zeros(pad_shape, dtype=t.dtype, device=t.device)
         buf.narrow(dim, 0, t.shape[dim]).copy_(t)
         outs = [torch.empty_like(buf) for _ in range(self.world_size)]
+        tok = self._begin("all_gather", buf.numel() * buf.element_size() * self.world_size)
         dist.all_gather(outs, buf, group=self.group)
+        self._end(tok)
         return torch.cat([o.narrow(dim, 0, s) for o, s in zip(outs, sizes)], dim=dim)
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.world_size > 1:
             self._check()
+            tok = self._begin("broadcast", t.numel() * t.element_size())
             dist.broadcast(t, src=src, group=self.group)
+            self._end(tok)
         return t
 
     def broadcast_object(self, obj, src: int = 0):
@@ -131,6 +187,17 @@ class Comm:
         lst = [obj]
         dist.broadcast_object_list(lst, src=src, group=self.group)
         return lst[0]
+
+    def all_gather_object(self, obj) -> list:
+        """Every rank's picklable ``obj``, in rank order (small control data)."""
+        if self.world_size == 1:
+            return [obj]
+        self._check()
+        out = [None] * self.world_size
+        tok = self._begin("all_gather", 0)
+        dist.all_gather_object(out, obj, group=self.group)
+        self._end(tok)
+        return out
 
     def barrier(self) -> None:
         if self.world_size > 1:

@@ -297,7 +297,7 @@ class _CpuView:
         return np.stack(sel) if sel else np.zeros((0, 1), TREE_NODE_DTYPE)
 
 
-def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw):
+def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw, tree_offset=0):
     K, dist, n = ens.K, ens.dist, bm.n
     builder = RefTreeBuilder(bm, tp, comm)
     from ..models.tree.boost import _tree_fmask
@@ -312,8 +312,9 @@ def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback
     t0 = time.perf_counter()
     lr0, ann = tp.learn_rate, getattr(tp, "learn_rate_annealing", 1.0)
     for t in range(ntrees):
-        builder.p.learn_rate = lr0 * ann ** t
-        wb = wobs * bag_weights(n, sample_rate, seed, t, row_base)
+        ti = tree_offset + t      # global iteration index (checkpoint continuation)
+        builder.p.learn_rate = lr0 * ann ** ti
+        wb = wobs * bag_weights(n, sample_rate, seed, ti, row_base)
         if K == 1:
             gr, hs = dist_grad(dist, Fm[0], y_np, **dist_kw)
             grads = [(gr, hs)]
@@ -324,7 +325,7 @@ def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback
             pr = np.exp(z)
             pr /= pr.sum(axis=0, keepdims=True)
             grads = [(pr[k] - (y_np == k), np.maximum(pr[k] * (1 - pr[k]), 1e-16)) for k in range(K)]
-        fmask = _tree_fmask(tp, bm.F, t, None)
+        fmask = _tree_fmask(tp, bm.F, ti, None)
         for k in range(K):
             gr, hs = grads[k]
             pad = bm.npad - n
@@ -333,7 +334,7 @@ def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback
             g32 = np.concatenate([(gr * wb).astype(np.float32), np.zeros(pad, np.float32)])
             h32 = np.concatenate([(hs * wb).astype(np.float32), np.zeros(pad, np.float32)])
             w32 = np.concatenate([wb, np.zeros(pad, np.float32)])
-            tree = builder.build(g32, h32, w32, t * K + k, fmask)
+            tree = builder.build(g32, h32, w32, ti * K + k, fmask)
             leaf = ~builder.nid[:n]
             Fm[k] += tree["value"][leaf]
             trees.append(tree)

@@ -145,6 +145,7 @@ class Cluster:
         self.ops: dict = {}
         self.started = time.time()
         self.watchdog = None      # runtime/watchdog.PeerWatchdog on multi-node clouds
+        self.topology = None      # runtime/topology.check_cloud report (world > 1)
         self.formed = True
         self.stop = threading.Event()
 
@@ -275,6 +276,12 @@ def form_cluster(cfg: ClusterConfig | None = None, device: str | None = None, ti
                               timeout=datetime.timedelta(seconds=timeout_s))
     comm = Comm(cfg.rank, cfg.world_size, dev)
     cl = Cluster(cfg, comm, store)
+    if cfg.world_size > 1:
+        from .topology import check_cloud
+
+        # which GPUs can reach each other over xGMI (fails formation when
+        # H2OMX_REQUIRE_P2P=1 and a host's ranks cannot see their peers)
+        cl.topology = check_cloud(comm)
     if cfg.world_size > 1 and os.environ.get("H2OMX_WATCHDOG", "1") != "0":
         from .watchdog import PeerWatchdog
 

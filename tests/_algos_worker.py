@@ -78,6 +78,25 @@ def main():
 
     ia = interaction(fr, ["g", "trt"], max_factors=5, comm=c).vecs[0]
     res["inter"] = [ia.domain[i] if i >= 0 else None for i in ia.data.tolist()]
+    # calibration on a row-sharded calibration frame: Platt's Newton steps and the
+    # isotonic PAV fit see the whole frame (all-reduce / all-gather), and the
+    # laplace / quantile initial margins are the weighted quantiles over all ranks
+    from h2omx.models import H2OGradientBoostingEstimator, H2OKMeansEstimator
+
+    for meth in ("PlattScaling", "IsotonicRegression"):
+        gb = H2OGradientBoostingEstimator(ntrees=3, max_depth=3, seed=1, calibrate_model=True, calibration_frame=fr,
+                                          calibration_method=meth).train(x=["a", "b", "c"], y="yb",
+                                                                         training_frame=fr, comm=c)
+        cal = gb.calibration
+        res[f"cal_{meth}"] = ([cal["intercept"], cal["slope"]] if meth == "PlattScaling"
+                              else [cal["x"], cal["y"], cal["x_min"]])
+    for dist in ("laplace", "quantile"):
+        gq = H2OGradientBoostingEstimator(ntrees=2, max_depth=2, seed=1, distribution=dist, quantile_alpha=0.3).train(
+            x=["a", "b"], y="y", training_frame=fr, comm=c)
+        res[f"init_{dist}"] = float(gq.ens.init_f[0])
+    km = H2OKMeansEstimator(k=6, estimate_k=True, standardize=True, seed=4, max_iterations=20).train(
+        x=["a", "b", "c"], training_frame=fr, comm=c)
+    res["km_k"] = int(km.centers.shape[0])
     with open(out_path, "w") as f:
         json.dump(res, f)
     comm.barrier()

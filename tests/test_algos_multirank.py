@@ -74,3 +74,13 @@ def _compare(one, two, f=1.0):
     assert two[0]["inter"] + two[1]["inter"] == one["inter"]
     for r in two:
         np.testing.assert_allclose(r["hglm"], one["hglm"], rtol=1e-7 * f, atol=1e-9 * f)
+        np.testing.assert_allclose(r["cal_PlattScaling"], one["cal_PlattScaling"], rtol=1e-5 * f)
+        xs, ys, xmin = r["cal_IsotonicRegression"]
+        assert len(xs) == len(one["cal_IsotonicRegression"][0])
+        np.testing.assert_allclose(xs, one["cal_IsotonicRegression"][0], rtol=1e-5 * f)
+        # p1 of the 1- and 2-rank models agree to rounding, which can move a row
+        # across a PAV block boundary: the fitted step values agree to ~1e-3
+        np.testing.assert_allclose(ys, one["cal_IsotonicRegression"][1], atol=5e-3)
+        for dist in ("laplace", "quantile"):
+            assert r[f"init_{dist}"] == one[f"init_{dist}"], dist
+        assert r["km_k"] == one["km_k"]

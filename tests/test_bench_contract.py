@@ -47,7 +47,8 @@ def _run(nproc, extra, env_extra=None, timeout=600):
 def test_bench_two_ranks_cpu(model, extra):
     out = _run(2, ["--device", "cpu", "--model", model] + extra)
     if model == "gbm-higgs":
-        assert out["config"]["global_batch"] == 12000
+        assert out["scaling"] == "strong"          # headline default: 11M rows in total at every N
+        assert out["config"]["global_batch"] == 6000 and out["config"]["rows_per_gpu"] == 3000
         assert 0.6 < out["train_auc"] <= 1.0
     else:
         assert out["config"]["global_batch"] == 512
@@ -57,6 +58,67 @@ def test_bench_two_ranks_cpu(model, extra):
 def test_bench_two_ranks_one_gpu():
     """Two ranks on the one GPU (gloo carries the collectives): the weak-scaling
     GBM path of the driver's N>1 run, HIP kernels included."""
-    out = _run(2, ["--model", "gbm-higgs", "--rows", "200000"], {"H2OMX_DIST_BACKEND": "gloo"}, timeout=300)
+    out = _run(2, ["--model", "gbm-higgs", "--rows", "200000", "--scaling", "weak"], {"H2OMX_DIST_BACKEND": "gloo"},
+               timeout=300)
     assert out["config"]["global_batch"] == 400000
     assert 0.6 < out["train_auc"] <= 1.0
+
+
+def _reachable(tr):
+    keep, stack = [], [0]
+    while stack:
+        i = stack.pop()
+        keep.append(i)
+        if tr[i]["feat"] >= 0:
+            stack += [int(tr[i]["left"]), int(tr[i]["left"]) + 1]
+    return sorted(keep)
+
+
+def _assert_same_trees(a, b, exact_values):
+    import numpy as np
+
+    assert a.shape[0] == b.shape[0]
+    for t in range(a.shape[0]):
+        keep = _reachable(a[t])
+        assert keep == _reachable(b[t]), f"tree {t} shape"
+        for f in ("feat", "bin", "na_left"):
+            np.testing.assert_array_equal(a[t][keep][f], b[t][keep][f], err_msg=f"tree {t} {f}")
+        if exact_values:
+            np.testing.assert_array_equal(a[t][keep]["value"], b[t][keep]["value"], err_msg=f"tree {t}")
+        else:
+            np.testing.assert_allclose(a[t][keep]["value"], b[t][keep]["value"], rtol=1e-5, atol=1e-7)
+
+
+def test_bench_strong_two_ranks_reproduce_one_rank_cpu(tmp_path):
+    """Strong scaling splits ONE data set over the ranks: the 2-rank run grows
+    the 1-rank trees (CPU reference builder: identical splits, fp64 leaf sums
+    equal to rounding since the all-reduce changes the summation order)."""
+    import numpy as np
+
+    extra = ["--device", "cpu", "--rows", "6000", "--scaling", "strong"]
+    one, two = tmp_path / "one.npy", tmp_path / "two.npy"
+    _run(1, extra + ["--dump-trees", str(one)])
+    _run(2, extra + ["--dump-trees", str(two)])
+    _assert_same_trees(np.load(one), np.load(two), exact_values=False)
+
+
+@pytest.mark.gpu
+def test_bench_strong_two_ranks_reproduce_one_rank_gpu(tmp_path):
+    """HIP engine, two ranks sharing the GPU over gloo, strong scaling: the
+    integer histograms and global-row-id dither make the 2-rank trees
+    bit-identical to the 1-rank trees, with graph replay on (segments split
+    at the collectives) as in the timed run."""
+    import numpy as np
+
+    extra = ["--rows", "300000", "--scaling", "strong", "--instrument-steps", "2", "--fit-trees", "0"]
+    one, two = tmp_path / "one.npy", tmp_path / "two.npy"
+    o1 = _run(1, extra + ["--dump-trees", str(one)], timeout=300)
+    o2 = _run(2, extra + ["--dump-trees", str(two)], {"H2OMX_DIST_BACKEND": "gloo"}, timeout=300)
+    assert o1["graph_replay"] and o2["graph_replay"]
+    _assert_same_trees(np.load(one), np.load(two), exact_values=True)
+    assert o1["train_auc"] == o2["train_auc"]
+    for o in (o1, o2):
+        for k in ("host_enqueue_us_per_tree", "small_kernel_us_per_tree", "allreduce_us_per_tree",
+                  "phase_us_per_tree"):
+            assert k in o, k
+    assert o2["allreduce_calls_per_tree"] >= 6     # one per level + leaf sums

@@ -47,3 +47,18 @@ def test_learn_rate_annealing_cpu():
 @pytest.mark.gpu
 def test_learn_rate_annealing_gpu(cuda_dev):
     _check(_frame(cuda_dev))
+
+
+def test_checkpoint_continues_annealing_and_hashes():
+    """A model continued from a checkpoint keeps counting iterations: tree t of
+    the continuation uses learn_rate x annealing^(t0 + t) and the same bagging
+    hashes as one long run, so 4 + 4 trees equal 8 trees."""
+    fr = _frame()
+    kw = dict(max_depth=3, seed=1, learn_rate=0.5, learn_rate_annealing=0.7, sample_rate=0.8)
+    full = H2OGradientBoostingEstimator(ntrees=8, **kw).train(x=["a", "b"], y="y", training_frame=fr)
+    half = H2OGradientBoostingEstimator(ntrees=4, model_id="half_ann", **kw).train(x=["a", "b"], y="y",
+                                                                                  training_frame=fr)
+    cont = H2OGradientBoostingEstimator(ntrees=8, checkpoint=half, **kw).train(x=["a", "b"], y="y",
+                                                                             training_frame=fr)
+    for t in range(8):
+        np.testing.assert_allclose(_values(cont, t), _values(full, t), rtol=1e-4, atol=1e-6, err_msg=f"tree {t}")

@@ -438,3 +438,38 @@ def test_fused_gradient_level_matches_boost_update(cuda_dev, monkeypatch, n, mod
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
     torch.testing.assert_close(ma[0], mb[0], rtol=0, atol=0)
     torch.testing.assert_close(fa, fb, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("dist,depth,min_rows,n", [("bernoulli", 5, 10, 400_000), ("gaussian", 7, 3, 150_000),
+                                                   ("bernoulli", 1, 3, 50_000)])
+def test_graph_replay_matches_eager(cuda_dev, monkeypatch, dist, depth, min_rows, n):
+    """Each boosting step replayed as one HIP graph (tree index / dither salt
+    taken from the device counter) builds bit-identical trees and margins to
+    the eager launch sequence."""
+    from h2omx.models.tree import boost as B
+
+    X, y = _data(n=n, F=11, seed=21, task="bin" if dist == "bernoulli" else "reg")
+    _, bg = _both(X, y, 255)
+    tp = TreeParams(max_depth=depth, min_rows=min_rows, learn_rate=0.2)
+    yt = torch.from_numpy(y).cuda()
+    made = []
+    init = B.GpuBooster.__init__
+
+    def spy(self, *a, **k):
+        init(self, *a, **k)
+        made.append(self)
+
+    monkeypatch.setattr(B.GpuBooster, "__init__", spy)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("H2OMX_TREE_GRAPH", flag)
+        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=6, tparams=tp, seed=5)
+    assert made[0].graph is None and made[1].graph is not None, made[1].graph_error
+    a, b = out["0"], out["1"]
+    assert a.trees.shape == b.trees.shape
+    for t in range(a.trees.shape[0]):
+        reach = a.compact()[t]
+        assert reach == b.compact()[t], t
+        for f in ("feat", "bin", "value", "weight"):
+            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"tree {t} {f}")
+    torch.testing.assert_close(a._state.Fm, b._state.Fm, rtol=0, atol=0)

@@ -81,3 +81,55 @@ def test_gaussian_and_bernoulli_offset_gpu(cuda_dev):
     yb = (df.yb == "1").to_numpy(float)
     np.testing.assert_allclose(np.mean(1 / (1 + np.exp(-(c + df.o.to_numpy())))), yb.mean(), rtol=1e-6)
     assert mb.training_metrics["AUC"] > 0.7
+
+
+@pytest.mark.parametrize("dist,y", [("gaussian", "y"), ("bernoulli", "yb"), ("poisson", "cnt")])
+def test_offset_model_mojo_round_trip(dist, y):
+    """The MOJO of an offset model records the offset column and its Generic
+    scorer adds it to the margin before the link: predictions match the native
+    model's."""
+    from h2omx.mojo import GenericModel, mojo_bytes
+
+    df = _frame(seed=3)
+    fr = Frame.from_pandas(df)
+    m = H2OGradientBoostingEstimator(ntrees=8, max_depth=3, seed=1, distribution=dist, offset_column="o").train(
+        x=["x1", "x2"], y=y, training_frame=fr)
+    g = GenericModel(mojo_bytes(m))
+    assert g.info["offset_column"] == "o"
+    a, b = m.predict(fr).to_pandas(), g.predict(fr).to_pandas()
+    for c in a.columns:
+        if c == "predict" and dist == "bernoulli":
+            assert (a[c].astype(str) == b[c].astype(str)).all()
+        else:
+            np.testing.assert_allclose(a[c].to_numpy(float), b[c].to_numpy(float), rtol=1e-5, atol=1e-6)
+    with pytest.raises(ValueError, match="offset_column"):
+        g.predict(Frame.from_pandas(df.drop(columns=["o"])))
+
+
+def test_tweedie_offset_init():
+    """H2O Tweedie initF with an offset: log(sum w y e^{o(1-p)} / sum w e^{o(2-p)})."""
+    df = _frame(seed=4)
+    fr = Frame.from_pandas(df)
+    p = 1.3
+    m = H2OGradientBoostingEstimator(ntrees=2, max_depth=2, seed=1, distribution="tweedie", tweedie_power=p,
+                                     offset_column="o").train(x=["x1", "x2"], y="cnt", training_frame=fr)
+    o, yv = df.o.to_numpy(), df.cnt.to_numpy()
+    want = np.log((yv * np.exp(o * (1 - p))).sum() / np.exp(o * (2 - p)).sum())
+    np.testing.assert_allclose(float(m.ens.init_f[0]), want, rtol=1e-6)
+
+
+def test_laplace_quantile_init_weighted_quantile():
+    """laplace / quantile initial margins are weighted (alpha-)quantiles of
+    y - offset at any row count (no torch.quantile 2^24 limit)."""
+    from h2omx.models.tree.boost import weighted_quantile
+
+    rng = np.random.default_rng(5)
+    r = torch.from_numpy(rng.normal(size=20001))
+    w = torch.from_numpy(rng.random(20001))
+    for q in (0.1, 0.5, 0.9):
+        v = weighted_quantile(r, w, q)
+        order = np.argsort(r.numpy())
+        cw = np.cumsum(w.numpy()[order])
+        want = r.numpy()[order][np.searchsorted(cw, q * cw[-1])]
+        assert v == want, (q, v, want)
+    assert weighted_quantile(r, None, 0.5) == float(np.sort(r.numpy())[10000])
