@@ -18,6 +18,11 @@
 #include <memory>
 #include <sstream>
 
+
+#ifndef MSG_NOSIGNAL
+#define MSG_NOSIGNAL 0   // macOS: SO_NOSIGPIPE is set on every socket instead
+#endif
+
 namespace h2ok {
 
 namespace {
@@ -147,6 +152,10 @@ class Conn {
       setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
       int one = 1;
       setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+#ifdef SO_NOSIGPIPE
+      // macOS has no MSG_NOSIGNAL: a closed peer must not SIGPIPE the CLI
+      setsockopt(fd, SOL_SOCKET, SO_NOSIGPIPE, &one, sizeof one);
+#endif
       if (::connect(fd, a->ai_addr, a->ai_addrlen) == 0) {
         fd_ = fd;
         return;

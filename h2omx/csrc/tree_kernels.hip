@@ -213,6 +213,13 @@ __device__ __forceinline__ uint32_t row_hash(int64_t r, uint32_t salt) {
   return mix32((uint32_t)r * 0x9E3779B1u ^ mix32(salt + (uint32_t)(r >> 32)));
 }
 
+// LDS written by some lanes of a wave, read by other lanes of the same wave
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // PKM (per-row inputs):
 //   0  node id -> NodeLink slot, (g, s2) quantised here (segmented engine)
 //   1  as 0, and feature group 0 stores the packed quantised row pk[r]
@@ -901,6 +908,225 @@ __global__ __launch_bounds__(1024) void hist_build_compact_kernel(
     if (src < width - 1 || bin == NBT - 1) {
       const unsigned long long* hb = lds64 + (sl2 * fg + fi) * NBT;
       for (int c = 0; c < rep; ++c) acc += hb[c * width + src];
+    }
+    out[j] = acc;
+  }
+}
+
+// Row-major compacted histogram build for levels >= 1 of the scan engine
+// (H2OMX_HIST_RM).  Levels >= 1 histogram only the smaller children (built
+// slots: ~30-50 % of the rows), but the column-major kernel issues one
+// ds_add_u64 wave-instruction per (16-row position, feature) whenever ANY
+// lane holds a built row, and a wave-instruction costs ~14-17 CU-cycles
+// whatever its lane mask (bench_micro/lds_mask.hip), so those levels cost
+// about as much LDS time as level 0.  Here every wave
+//   1. computes the build slot of its 1024 rows (64 lanes x 16 consecutive
+//      rows) exactly as hist_build_kernel does (slot16 from the previous
+//      partition, or the previous level's routing fused in: ROUTE),
+//   2. ranks the built rows with five bit-plane ballots and stages them as
+//      16-bit entries (row offset | slot << 10) in a per-wave 2 KB LDS area,
+//   3. hands lane j the entries j, j + 64, ... and gathers each entry's
+//      WHOLE row from the row-major code copy (codes_rm: [npad][32] bytes,
+//      two 16-byte loads, F <= 32) plus its stored packed (G_q, S_q),
+//   4. issues the F atomics of 64 built rows per wave-instruction.
+// So the atomic count follows the built rows, not the row positions, and no
+// per-feature code tile goes through LDS (the round-2 CMP variant staged one
+// per feature and lost on the extra LDS round trips).  The adds are the same
+// integers as hist_build_kernel's (same slots, same stored rows, same
+// low-cardinality replication), so histograms are bit-identical.  One
+// feature group only (fg = F <= 32); the next row's loads are issued before
+// the current row's atomics.
+constexpr int RM_PITCH = 32;     // bytes per row of codes_rm
+constexpr int RM_STAGE = 1024;   // u16 entries per wave
+
+template <int NBT, int PKM, bool ROUTE>
+__global__ __launch_bounds__(1024) void hist_build_rm_kernel(
+    const uint8_t* __restrict__ codes, const uint8_t* __restrict__ codes_rm, int64_t npad,
+    const int* __restrict__ nid, const int* __restrict__ ctl, const int* __restrict__ nvb,
+    const double* __restrict__ qscale, int F, int wgpg, int slot_lo, int slot_cnt,
+    const short* __restrict__ slot16, const unsigned long long* __restrict__ pk_buf,
+    unsigned long long* __restrict__ partials, const PartInfo* __restrict__ part_prev,
+    const int* __restrict__ ctl_prev, int* __restrict__ nid_out, int writer) {
+  constexpr int ROWS = 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
+  __shared__ int width_s[32], rep_s[32];
+  __shared__ float rcp_s[32];
+  const int n_slots = ctl[CTL_SLOTS];
+  const int chunk = blockIdx.x;   // one feature group: the grid is the row chunks
+  const bool route_w = ROUTE && writer && ctl_prev[CTL_N] > 0;
+  const bool build = slot_lo < n_slots;
+  if (!build && !route_w) return;
+  const int fg = F;
+  const int hist_elems = slot_cnt * fg * NBT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) lds64[j] = 0ull;
+  if (threadIdx.x < fg) {
+    const int w = nvb[threadIdx.x] + 1;
+    width_s[threadIdx.x] = w;
+    int r = NBT / w;
+    r = r < 1 ? 1 : (r > 64 ? 64 : r);
+    rep_s[threadIdx.x] = r;
+    rcp_s[threadIdx.x] = 1.0f / (float)r;
+  }
+  uint16_t* st16 = reinterpret_cast<uint16_t*>(lds64 + hist_elems) + wave * RM_STAGE;
+  const int64_t n_rows = (int64_t)qscale[8];
+  __syncthreads();
+
+  const int64_t units = npad / ROWS;
+  const int64_t u0 = units * chunk / wgpg, u1 = units * (chunk + 1) / wgpg;
+  for (int64_t uu = u0 + (int64_t)wave * 64; uu < u1; uu += (int64_t)nwaves * 64) {
+    const bool inb = uu + lane < u1;
+    const int64_t u = inb ? uu + lane : u1 - 1;
+    const int64_t r0 = u * ROWS;
+    int s[ROWS];
+    if constexpr (ROUTE) {
+      int nn[ROWS], nx[ROWS];
+      if (nid == nullptr) {
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) nn[k] = (r0 + k < n_rows) ? 0 : INT32_MIN;
+      } else {
+#pragma unroll
+        for (int q = 0; q < ROWS / 4; ++q) {
+          const int4 n4 = *reinterpret_cast<const int4*>(nid + r0 + 4 * q);
+          nn[4 * q] = n4.x; nn[4 * q + 1] = n4.y; nn[4 * q + 2] = n4.z; nn[4 * q + 3] = n4.w;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < ROWS; ++k) { nx[k] = nn[k]; s[k] = -1; }
+      const int n_prev = ctl_prev[CTL_N];
+      for (int j = 0; j < n_prev; ++j) {
+        bool mine = false;
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) mine |= (nn[k] == j);
+        if (!mine) continue;
+        const PartInfo pj = part_prev[j];
+        if (pj.child < 0) {
+#pragma unroll
+          for (int k = 0; k < ROWS; ++k)
+            if (nn[k] == j) nx[k] = ~pj.gid;
+          continue;
+        }
+        const uint4 c4 = *reinterpret_cast<const uint4*>(codes + (int64_t)pj.feat * npad + r0);
+        const uint32_t cw[4] = {c4.x, c4.y, c4.z, c4.w};
+        const int sl_l = (int)(short)(pj.pad & 0xFFFF), sl_r = pj.pad >> 16;
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) {
+          if (nn[k] == j) {
+            const int bc = (cw[k >> 2] >> (8 * (k & 3))) & 0xff;
+            const int right = (bc == NBT - 1) ? !pj.na_left : (bc > pj.bin);
+            nx[k] = pj.child + right;
+            s[k] = right ? sl_r : sl_l;
+          }
+        }
+      }
+      if (route_w && inb) {
+#pragma unroll
+        for (int q = 0; q < ROWS / 4; ++q)
+          *reinterpret_cast<int4*>(nid_out + r0 + 4 * q) = make_int4(nx[4 * q], nx[4 * q + 1], nx[4 * q + 2], nx[4 * q + 3]);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < ROWS / 8; ++q) {
+        const int4 v4 = *reinterpret_cast<const int4*>(slot16 + r0 + 8 * q);
+        const int vw[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[8 * q + k] = (int)(short)(vw[k >> 1] >> (16 * (k & 1)));
+      }
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < ROWS; ++k) {
+      const int sl = s[k] - slot_lo;
+      if (inb && build && sl >= 0 && sl < slot_cnt && s[k] >= 0) m |= 1u << k;
+      s[k] = sl;
+    }
+    // exclusive rank of this lane's first built row in the wave (five ballots)
+    const uint32_t cnt = __popc(m);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int excl = 0, total = 0;
+#pragma unroll
+    for (int bit = 0; bit < 5; ++bit) {
+      const unsigned long long bm = __ballot((cnt >> bit) & 1u);
+      excl += __popcll(bm & lt) << bit;
+      total += __popcll(bm) << bit;
+    }
+    if (total == 0) continue;   // wave-uniform
+    {
+      int j = excl;
+#pragma unroll
+      for (int k = 0; k < ROWS; ++k)
+        if ((m >> k) & 1u) st16[j++] = (uint16_t)((lane * ROWS + k) | (s[k] << 10));
+    }
+    wave_lds_sync();
+    const int64_t tile0 = uu * ROWS;
+    const int niter = (total + 63) >> 6;
+    // software pipeline: entry it + 1's row / packed value are in flight while
+    // entry it's atomics issue
+    uint4 ca = make_uint4(0, 0, 0, 0), cb = make_uint4(0, 0, 0, 0);
+    unsigned long long pka = 0ull;
+    int soa = -1;
+    auto fetch = [&](int it, uint4& c0, uint4& c1, unsigned long long& pk, int& so) {
+      const int e = it * 64 + lane;
+      so = -1;
+      if (e < total) {
+        const uint32_t ent = st16[e];
+        const int64_t row = tile0 + (ent & 1023u);
+        so = (int)(ent >> 10) * fg * NBT;
+        const uint4* rp = reinterpret_cast<const uint4*>(codes_rm + row * RM_PITCH);
+        c0 = rp[0];
+        c1 = rp[1];
+        if constexpr (PKM == 2) {
+          pk = pk_buf[row];
+        } else {
+          const uint32_t pw = reinterpret_cast<const uint32_t*>(pk_buf)[row];
+          pk = ((unsigned long long)(uint32_t)(int)(short)(pw >> 16) << 32) | (unsigned long long)(pw & 0xFFFFu);
+        }
+      }
+    };
+    fetch(0, ca, cb, pka, soa);
+    for (int it = 0; it < niter; ++it) {
+      uint4 na = make_uint4(0, 0, 0, 0), nb = make_uint4(0, 0, 0, 0);
+      unsigned long long pkn = 0ull;
+      int son = -1;
+      if (it + 1 < niter) fetch(it + 1, na, nb, pkn, son);
+      const uint32_t w[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
+#pragma unroll
+      for (int fi = 0; fi < 32; ++fi) {
+        if (fi < fg) {
+          int bin = (w[fi >> 2] >> (8 * (fi & 3))) & 0xff;
+          const int rep = rep_s[fi];
+          if (soa >= 0 && pka != 0ull) {
+            if (rep > 1) {
+              const int width = width_s[fi];
+              const int copy = lane - rep * (int)(((float)lane + 0.5f) * rcp_s[fi]);
+              if (bin == NBT - 1) bin = width - 1;
+              atomicAdd(lds64 + soa + fi * NBT + copy * width + bin, pka);
+            } else {
+              atomicAdd(lds64 + soa + fi * NBT + bin, pka);
+            }
+          }
+        }
+      }
+      ca = na; cb = nb; pka = pkn; soa = son;
+    }
+    // the next tile overwrites this wave's entries only after every lane read them
+    wave_lds_sync();
+  }
+  __syncthreads();
+  unsigned long long* out = partials + (int64_t)chunk * hist_elems;
+  for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) {
+    const int bin = j % NBT;
+    const int fi = (j / NBT) % fg;
+    const int sl = j / (NBT * fg);
+    const int width = width_s[fi], rep = rep_s[fi];
+    const unsigned long long* hb = lds64 + (sl * fg + fi) * NBT;
+    unsigned long long acc = 0ull;
+    if (rep == 1) {
+      acc = hb[bin];
+    } else {
+      const int src = (bin == NBT - 1) ? width - 1 : bin;
+      if (src < width - 1 || bin == NBT - 1)
+        for (int c = 0; c < rep; ++c) acc += hb[c * width + src];
     }
     out[j] = acc;
   }
@@ -2352,6 +2578,50 @@ H2OMX_API int h2omx_hist_build_compact(const uint8_t* codes, int64_t npad, const
   return launch_status();
 }
 
+// Row-major compacted histograms (hist_build_rm_kernel): levels >= 1, one
+// feature group (F <= 32), stored rows (pkm 2: 64-bit, 4: 32-bit); slot16
+// rows, or the previous level's routing fused in (part_prev != NULL).  The
+// partial slabs have the hist_build layout with n_groups = 1.
+H2OMX_API int h2omx_hist_build_rm(const uint8_t* codes, const uint8_t* codes_rm, int64_t npad, const int* nid,
+                                  const int* ctl, const int* nvb, const double* qscale, int F, int nbt, int wgpg,
+                                  int slot_lo, int slot_cnt, int threads, const short* slot16,
+                                  const unsigned long long* pk_buf, int pkm, unsigned long long* partials,
+                                  const void* part_prev, const int* ctl_prev, int* nid_out, int writer,
+                                  hipStream_t stream) {
+  const bool route = part_prev != nullptr;
+  if (F < 1 || F > RM_PITCH || npad % 16 != 0 || slot_cnt < 1 || slot_cnt > 63 || (pkm != 2 && pkm != 4) ||
+      pk_buf == nullptr || codes_rm == nullptr || threads % 64 != 0 || threads > 1024 || threads < 64 || wgpg < 1)
+    return kBadArg;
+  if (route && (ctl_prev == nullptr || nid_out == nullptr || nid_out == nid || codes == nullptr)) return kBadArg;
+  if (!route && slot16 == nullptr) return kBadArg;
+  const int64_t units = npad / 16;
+  if ((units + wgpg - 1) / wgpg * 16 > ROWS_CAP) return kBadArg;
+  const size_t lds = (size_t)slot_cnt * F * nbt * sizeof(unsigned long long) + (size_t)(threads / 64) * RM_STAGE * 2;
+  if (lds > 160 * 1024) return kBadArg;
+  const PartInfo* pp = reinterpret_cast<const PartInfo*>(part_prev);
+#define H2OMX_HRM(NB, M, RT)                                                                                   \
+  hipLaunchKernelGGL((hist_build_rm_kernel<NB, M, RT>), dim3(wgpg), dim3(threads), lds, stream, codes, codes_rm, \
+                     npad, nid, ctl, nvb, qscale, F, wgpg, slot_lo, slot_cnt, slot16, pk_buf, partials, pp,       \
+                     ctl_prev, nid_out, writer)
+#define H2OMX_HRM_NB(NB)                                   \
+  do {                                                     \
+    if (pkm == 2 && route) H2OMX_HRM(NB, 2, true);         \
+    else if (pkm == 2) H2OMX_HRM(NB, 2, false);            \
+    else if (route) H2OMX_HRM(NB, 4, true);                \
+    else H2OMX_HRM(NB, 4, false);                          \
+  } while (0)
+  switch (nbt) {
+    case 32: H2OMX_HRM_NB(32); break;
+    case 64: H2OMX_HRM_NB(64); break;
+    case 128: H2OMX_HRM_NB(128); break;
+    case 256: H2OMX_HRM_NB(256); break;
+    default: return kBadArg;
+  }
+#undef H2OMX_HRM_NB
+#undef H2OMX_HRM
+  return launch_status();
+}
+
 H2OMX_API int h2omx_hist_reduce(const unsigned long long* partials, int n_groups, int wgpg, int fg, int F, int nbt,
                                 int slot_lo, int slot_cnt, const int* ctl, long long* built, hipStream_t stream) {
   const int64_t total = (int64_t)slot_cnt * F * nbt;  // nbt is a multiple of 32
@@ -3401,11 +3671,6 @@ __device__ __forceinline__ int chunk_node_wave(const int* __restrict__ first, in
   return lo;
 }
 
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 
 // Eligible features of a node (mtries / column sample / tree mask), ascending,
 // computed by ONE wave into flist; returns the count (wave-uniform).  F <=

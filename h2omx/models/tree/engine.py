@@ -257,6 +257,38 @@ class HipTreeBuilder:
     CMP_LDS_BUDGET = 56 * 1024
     CMP_DEEP_LDS_BUDGET = 112 * 1024
     CMP_MAX_SLOTS = 64
+    # levels >= 1 of the scan engine (F <= 32): built rows compacted per wave and
+    # gathered from the row-major code copy (hist_build_rm_kernel); bit-identical
+    RM = os.environ.get("H2OMX_HIST_RM", "1") == "1"
+    RM_THREADS = int(os.environ.get("H2OMX_RM_THREADS", "1024"))
+    RM_ROWS_PER_WG = int(os.environ.get("H2OMX_RM_ROWS_PER_WG", "32768"))
+    RM_MAX_WGS = int(os.environ.get("H2OMX_RM_MAX_WGS", "256"))
+
+    def plan_rm(self, max_slots: int):
+        """Slots per pass / passes / grid of the compacted row-major kernel (one
+        feature group; 160 KB LDS = histograms + a 2 KB entry stage per wave)."""
+        key = ("rm", max_slots)
+        if key in self.plans:
+            return self.plans[key]
+        threads = self.RM_THREADS
+        per_slot = self.F * self.nbt * 8
+        budget = 160 * 1024 - (threads // 64) * 2048
+        slot_cnt = max(1, min(max_slots, 63, budget // per_slot))
+        passes = math.ceil(max_slots / slot_cnt)
+        npad = self.bm.npad
+        wgpg = min(self.RM_MAX_WGS, max(1, math.ceil(npad / self.RM_ROWS_PER_WG)))
+        # rows per workgroup <= the fixed-point headroom the scales were chosen for
+        units = npad // 16
+        while 16 * math.ceil(units / wgpg) > self.max_rows_per_wg:
+            wgpg += 1
+        plan = dict(slot_cnt=slot_cnt, passes=passes, wgpg=wgpg, threads=threads, fg=self.F, n_groups=1)
+        self.plans[key] = plan
+        return plan
+
+    def _rm_ok(self) -> bool:
+        return (self.RM and self.F <= 32 and not self.COMPACT and not self.CMP and per_slot_fits(self.F, self.nbt,
+                                                                                                self.RM_THREADS))
+
     # fused pipeline: routing passes via route_kernel (PartInfo in LDS, one coalesced
     # column load per distinct split feature) instead of partition_kernel's gathers
     ROUTE_KERNEL = os.environ.get("H2OMX_ROUTE_KERNEL", "0") == "1"
@@ -391,6 +423,29 @@ class HipTreeBuilder:
             built = self._buf("built", max_slots * self.per_node, torch.int64)
             hist_elems = plan["slot_cnt"] * plan["fg"] * nbt
             partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_elems, torch.int64)
+            if d > 0 and self._rm_ok():
+                # deeper levels: built rows only, whole rows gathered row-major
+                plan = self.plan_rm(max_slots)
+                hist_elems = plan["slot_cnt"] * self.F * nbt
+                partials = self._buf("partials", plan["wgpg"] * hist_elems, torch.int64)
+                routed = fuse and self._fused_level(d)
+                for ps in range(plan["passes"]):
+                    slot_lo = ps * plan["slot_cnt"]
+                    with T("hist"):
+                        ops.check(lib.h2omx_hist_build_rm(
+                            P(bm.codes), P(bm.codes_rm32), bm.npad,
+                            P((None if (d == 1 and self.implicit_root) else nid_buf[(d - 1) % 2]) if routed
+                              else None),
+                            P(ctl_cur), P(bm.nvb), P(self.qscale), F, nbt, plan["wgpg"], slot_lo,
+                            plan["slot_cnt"], plan["threads"], P(None if routed else self.slot16), P(self.pk),
+                            4 if self.pk32 else 2, P(partials), P(part_prev if routed else None),
+                            P(ctl_nxt if routed else None), P(nid_buf[d % 2] if routed else None),
+                            1 if ps == 0 else 0, st), "hist_build_rm")
+                    with T("hist_reduce"):
+                        ops.check(lib.h2omx_hist_reduce(P(partials), 1, plan["wgpg"], F, F, nbt, slot_lo,
+                                                        plan["slot_cnt"], P(ctl_cur), P(built), st),
+                                  "hist_reduce")
+                plan = dict(passes=0)
             # level 0 streams every row; deeper levels touch only the built
             # (smaller) children -> wave-compacted kernel keeps atomics dense
             for ps in range(plan["passes"]):
@@ -754,6 +809,11 @@ class HipTreeBuilder:
     def tree_size(self) -> torch.Tensor:
         """Device scalar with the node count of the last tree (ctl TOTAL)."""
         return self._final_ctl[3]
+
+
+def per_slot_fits(F: int, nbt: int, threads: int) -> bool:
+    """One slot of F x nbt packed histograms + the entry stages fit 160 KB LDS."""
+    return F * nbt * 8 + (threads // 64) * 2048 <= 160 * 1024
 
 
 def global_row_base(n: int, comm) -> int:

@@ -20,6 +20,7 @@ TREE_SIGS = {
     "h2omx_bin_features": "PLLIPPIPLS",
     "h2omx_hist_build": "PLPPPPPPPIIIIIIIIIIPPIPS",
     "h2omx_hist_reduce": "PIIIIIIIPPS",
+    "h2omx_hist_build_rm": "PPLPPPPIIIIIIPPIPPPPIS",
     "h2omx_hist_build_compact": "PLPPPPPPPIIIIIIIIIIPS",
     "h2omx_hist_build_route": "PLPPPPIPPPIIIIIIIIIPIPS",
     "h2omx_hist_build_grad": "PLPPPIIIIIIIIIPPPPPPIPPIIIPS",

@@ -49,6 +49,9 @@ class FakeK8s:
         self.foreground_delay = foreground_delay
         self.tls = tls
         self.tmpdir = tmpdir
+        # StatefulSet controller + kubelet stand-in (tests/fake_kubelet.py): runs the
+        # rendered pod containers as local processes; None = canned pods only
+        self.kubelet = None
         self.ca_pem = None
         self.httpd = ThreadingHTTPServer(("127.0.0.1", 0), self._handler())
         self.httpd.daemon_threads = True
@@ -321,6 +324,8 @@ class FakeK8s:
 
     def _spawn_pods(self, sts):
         """StatefulSet controller stand-in: pods <sts>-<ordinal>, pod 0 Ready (leader)."""
+        if self.kubelet is not None:
+            return self.kubelet.start(self, sts)
         ns = sts["metadata"]["namespace"]
         name = sts["metadata"]["name"]
         labels = sts["spec"]["template"]["metadata"].get("labels", {})

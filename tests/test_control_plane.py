@@ -532,3 +532,7 @@ def test_ci_and_release_workflows():
     assert trigger["push"]["tags"] == ["v*"]
     rsteps = " ".join(str(s.get("run", "")) for j in rel["jobs"].values() for s in j["steps"])
     assert "make -C control package" in rsteps and "gh release create" in rsteps
+    # BASELINE config #1 on a kind cluster; h2ok also ships for macOS
+    assert "scripts/e2e/iris_glm_rest.py" in steps and "kind load docker-image" in steps
+    assert any("macos" in str(j.get("runs-on", "")) or "macos" in str(j.get("strategy", ""))
+               for j in rel["jobs"].values())

@@ -473,3 +473,31 @@ def test_graph_replay_matches_eager(cuda_dev, monkeypatch, dist, depth, min_rows
         for f in ("feat", "bin", "value", "weight"):
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"tree {t} {f}")
     torch.testing.assert_close(a._state.Fm, b._state.Fm, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("dist,depth,sample_rate,nbins,n,F", [
+    ("bernoulli", 5, 1.0, 255, 300_000, 11), ("bernoulli", 8, 0.7, 63, 200_000, 9),
+    ("gaussian", 6, 1.0, 31, 150_000, 28), ("multinomial", 4, 1.0, 255, 100_000, 7),
+    ("bernoulli", 2, 1.0, 127, 50_000, 32)])
+def test_row_major_compacted_hist_matches_plain(cuda_dev, monkeypatch, dist, depth, sample_rate, nbins, n, F):
+    """Levels >= 1 built from compacted built rows gathered row-major
+    (hist_build_rm_kernel: routed and slot16 levels, several slot passes,
+    low-cardinality replication, bagged-out rows) give bit-identical trees."""
+    import h2omx.models.tree.engine as E
+
+    X, y = _data(n=n, F=F, seed=13, task={"bernoulli": "bin", "gaussian": "reg"}.get(dist, "multi"))
+    _, bg = _both(X, y, nbins)
+    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2)
+    yt = torch.from_numpy(y).cuda()
+    monkeypatch.setenv("H2OMX_TREE_GRAPH", "0")
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(E.HipTreeBuilder, "RM", flag)
+        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate, seed=5,
+                                   nclass=4 if dist == "multinomial" else 1)
+    a, b = out[False], out[True]
+    for t in range(a.trees.shape[0]):
+        reach = a.compact()[t]
+        assert reach == b.compact()[t], t
+        for f in ("feat", "bin", "value", "weight"):
+            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"tree {t} {f}")
