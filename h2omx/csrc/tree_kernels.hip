@@ -939,8 +939,9 @@ __global__ __launch_bounds__(1024) void hist_build_compact_kernel(
 constexpr int RM_PITCH = 32;     // bytes per row of codes_rm
 constexpr int RM_STAGE = 1024;   // u16 entries per wave
 
+// (routing keeps 48 more row registers live: 512-thread workgroups, 8 waves of up to 256 VGPRs)
 template <int NBT, int PKM, bool ROUTE>
-__global__ __launch_bounds__(1024) void hist_build_rm_kernel(
+__global__ __launch_bounds__(ROUTE ? 512 : 1024) void hist_build_rm_kernel(
     const uint8_t* __restrict__ codes, const uint8_t* __restrict__ codes_rm, int64_t npad,
     const int* __restrict__ nid, const int* __restrict__ ctl, const int* __restrict__ nvb,
     const double* __restrict__ qscale, int F, int wgpg, int slot_lo, int slot_cnt,
@@ -971,10 +972,33 @@ __global__ __launch_bounds__(1024) void hist_build_rm_kernel(
   uint16_t* st16 = reinterpret_cast<uint16_t*>(lds64 + hist_elems) + wave * RM_STAGE;
   const int64_t n_rows = (int64_t)qscale[8];
   __syncthreads();
+  // features whose histogram slice is replicated (rep > 1): one uniform bit mask
+  uint32_t rep_mask = 0;
+  for (int fi = 0; fi < fg; ++fi) rep_mask |= (rep_s[fi] > 1 ? 1u : 0u) << fi;
+  rep_mask = __builtin_amdgcn_readfirstlane(rep_mask);
 
   const int64_t units = npad / ROWS;
   const int64_t u0 = units * chunk / wgpg, u1 = units * (chunk + 1) / wgpg;
-  for (int64_t uu = u0 + (int64_t)wave * 64; uu < u1; uu += (int64_t)nwaves * 64) {
+  const int64_t ustep = (int64_t)nwaves * 64;
+  // Pipeline (per wave, tiles of 64 lanes x 16 rows):
+  //   * a tile's per-row inputs (slot16) are loaded one tile ahead;
+  //   * stage(): slots -> ballot ranks -> 16-bit entries through the wave's LDS
+  //     area -> this lane's entries into registers (packed pairs);
+  //   * the gathers run two entries ahead, and the NEXT tile is staged (and its
+  //     first two gathers issued) before the current tile's last two entries'
+  //     atomics, so no tile boundary exposes a memory latency.
+  int4 in_a = make_int4(0, 0, 0, 0), in_b = make_int4(0, 0, 0, 0);
+  auto load_inputs = [&](int64_t uu) {
+    if constexpr (!ROUTE) {   // (routing loads its node ids in place: register pressure)
+      const int64_t u = (uu + lane < u1) ? uu + lane : u1 - 1;
+      const int4* sp = reinterpret_cast<const int4*>(slot16 + u * ROWS);
+      in_a = sp[0];
+      in_b = sp[1];
+    }
+  };
+  // stage tile uu: returns its built-row count (wave-uniform), entries in ep[8]
+  // (lane's entries i = 0..15 as 16-bit halves: ep[i / 2] >> 16 * (i % 2)), 0xFFFF = none
+  auto stage = [&](int64_t uu, uint32_t* ep) -> int {
     const bool inb = uu + lane < u1;
     const int64_t u = inb ? uu + lane : u1 - 1;
     const int64_t r0 = u * ROWS;
@@ -1025,14 +1049,11 @@ __global__ __launch_bounds__(1024) void hist_build_rm_kernel(
           *reinterpret_cast<int4*>(nid_out + r0 + 4 * q) = make_int4(nx[4 * q], nx[4 * q + 1], nx[4 * q + 2], nx[4 * q + 3]);
       }
     } else {
+      const int vw[8] = {in_a.x, in_a.y, in_a.z, in_a.w, in_b.x, in_b.y, in_b.z, in_b.w};
 #pragma unroll
-      for (int q = 0; q < ROWS / 8; ++q) {
-        const int4 v4 = *reinterpret_cast<const int4*>(slot16 + r0 + 8 * q);
-        const int vw[4] = {v4.x, v4.y, v4.z, v4.w};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s[8 * q + k] = (int)(short)(vw[k >> 1] >> (16 * (k & 1)));
-      }
+      for (int k = 0; k < ROWS; ++k) s[k] = (int)(short)(vw[k >> 1] >> (16 * (k & 1)));
     }
+    if (uu + ustep < u1) load_inputs(uu + ustep);   // the following tile's inputs in flight
     uint32_t m = 0;
 #pragma unroll
     for (int k = 0; k < ROWS; ++k) {
@@ -1050,7 +1071,9 @@ __global__ __launch_bounds__(1024) void hist_build_rm_kernel(
       excl += __popcll(bm & lt) << bit;
       total += __popcll(bm) << bit;
     }
-    if (total == 0) continue;   // wave-uniform
+#pragma unroll
+    for (int i = 0; i < ROWS / 2; ++i) ep[i] = 0xFFFFFFFFu;
+    if (total == 0) return 0;   // wave-uniform
     {
       int j = excl;
 #pragma unroll
@@ -1058,59 +1081,103 @@ __global__ __launch_bounds__(1024) void hist_build_rm_kernel(
         if ((m >> k) & 1u) st16[j++] = (uint16_t)((lane * ROWS + k) | (s[k] << 10));
     }
     wave_lds_sync();
-    const int64_t tile0 = uu * ROWS;
-    const int niter = (total + 63) >> 6;
-    // software pipeline: entry it + 1's row / packed value are in flight while
-    // entry it's atomics issue
-    uint4 ca = make_uint4(0, 0, 0, 0), cb = make_uint4(0, 0, 0, 0);
-    unsigned long long pka = 0ull;
-    int soa = -1;
-    auto fetch = [&](int it, uint4& c0, uint4& c1, unsigned long long& pk, int& so) {
-      const int e = it * 64 + lane;
-      so = -1;
-      if (e < total) {
-        const uint32_t ent = st16[e];
-        const int64_t row = tile0 + (ent & 1023u);
-        so = (int)(ent >> 10) * fg * NBT;
-        const uint4* rp = reinterpret_cast<const uint4*>(codes_rm + row * RM_PITCH);
-        c0 = rp[0];
-        c1 = rp[1];
-        if constexpr (PKM == 2) {
-          pk = pk_buf[row];
-        } else {
-          const uint32_t pw = reinterpret_cast<const uint32_t*>(pk_buf)[row];
-          pk = ((unsigned long long)(uint32_t)(int)(short)(pw >> 16) << 32) | (unsigned long long)(pw & 0xFFFFu);
-        }
+#pragma unroll
+    for (int i = 0; i < ROWS; ++i) {
+      const uint32_t v = (i * 64 + lane < total) ? (uint32_t)st16[i * 64 + lane] : 0xFFFFu;
+      ep[i >> 1] = (i & 1) ? ((ep[i >> 1] & 0xFFFFu) | (v << 16)) : ((ep[i >> 1] & 0xFFFF0000u) | v);
+    }
+    wave_lds_sync();   // entries in registers: the area is free for the next tile
+    return total;
+  };
+  struct Ent { uint4 c0, c1; unsigned long long pk; int so; };
+  auto fetch = [&](uint32_t en, int64_t tile0, Ent& E) {
+    E.so = -1;
+    if (en != 0xFFFFu) {
+      const int64_t row = tile0 + (en & 1023u);
+      E.so = (int)(en >> 10) * fg * NBT;
+      const uint4* rp = reinterpret_cast<const uint4*>(codes_rm + row * RM_PITCH);
+      E.c0 = rp[0];
+      E.c1 = rp[1];
+      if constexpr (PKM == 2) {
+        E.pk = pk_buf[row];
+      } else {
+        const uint32_t pw = reinterpret_cast<const uint32_t*>(pk_buf)[row];
+        E.pk = ((unsigned long long)(uint32_t)(int)(short)(pw >> 16) << 32) | (unsigned long long)(pw & 0xFFFFu);
       }
-    };
-    fetch(0, ca, cb, pka, soa);
+    }
+  };
+  // shift a packed entry window by one entry
+  auto shift = [&](uint32_t* ep) {
+#pragma unroll
+    for (int k = 0; k < ROWS / 2 - 1; ++k) ep[k] = (ep[k] >> 16) | (ep[k + 1] << 16);
+    ep[ROWS / 2 - 1] = (ep[ROWS / 2 - 1] >> 16) | 0xFFFF0000u;
+  };
+
+  int64_t uu = u0 + (int64_t)wave * 64;
+  if (uu < u1) load_inputs(uu);
+  uint32_t ec[ROWS / 2], en_[ROWS / 2];
+  int nC = 0;
+  Ent e0, e1, e2, f0, f1;
+  e0.so = e1.so = e2.so = f0.so = f1.so = -1;
+  if (uu < u1) {
+    nC = stage(uu, ec);
+    fetch(ec[0] & 0xFFFFu, uu * ROWS, e0);
+    fetch(ec[0] >> 16, uu * ROWS, e1);
+  }
+  while (uu < u1) {
+    const int64_t uuN = uu + ustep;
+    const int niter = (nC + 63) >> 6;
+    int nN = 0;
+    bool staged = false;
+#pragma unroll 1
     for (int it = 0; it < niter; ++it) {
-      uint4 na = make_uint4(0, 0, 0, 0), nb = make_uint4(0, 0, 0, 0);
-      unsigned long long pkn = 0ull;
-      int son = -1;
-      if (it + 1 < niter) fetch(it + 1, na, nb, pkn, son);
-      const uint32_t w[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
+      // entry it + 2 of this tile (window position 2 after the shifts)
+      fetch(ec[1] & 0xFFFFu, uu * ROWS, e2);
+      if (it == (niter >= 2 ? niter - 2 : 0) && uuN < u1) {
+        // stage the next tile now: its first gathers overlap this tile's last atomics
+        nN = stage(uuN, en_);
+        fetch(en_[0] & 0xFFFFu, uuN * ROWS, f0);
+        fetch(en_[0] >> 16, uuN * ROWS, f1);
+        staged = true;
+      }
+      const uint32_t w[8] = {e0.c0.x, e0.c0.y, e0.c0.z, e0.c0.w, e0.c1.x, e0.c1.y, e0.c1.z, e0.c1.w};
+      // opaque per iteration: keeps the compiler from hoisting 32 per-feature lane
+      // masks out of the loop (they spill and come back as v_readlane pairs)
+      uint32_t rmask = rep_mask;
+      asm volatile("" : "+s"(rmask));
+      if (e0.so >= 0 && e0.pk != 0ull)
 #pragma unroll
       for (int fi = 0; fi < 32; ++fi) {
         if (fi < fg) {
           int bin = (w[fi >> 2] >> (8 * (fi & 3))) & 0xff;
-          const int rep = rep_s[fi];
-          if (soa >= 0 && pka != 0ull) {
-            if (rep > 1) {
-              const int width = width_s[fi];
-              const int copy = lane - rep * (int)(((float)lane + 0.5f) * rcp_s[fi]);
-              if (bin == NBT - 1) bin = width - 1;
-              atomicAdd(lds64 + soa + fi * NBT + copy * width + bin, pka);
-            } else {
-              atomicAdd(lds64 + soa + fi * NBT + bin, pka);
-            }
+          if ((rmask >> fi) & 1u) {
+            // replicated low-cardinality slice (rare): per-feature values read in
+            // place (relaxed atomic loads are not hoisted into registers)
+            const int rep = __hip_atomic_load(&rep_s[fi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int width = __hip_atomic_load(&width_s[fi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int copy = lane % rep;
+            if (bin == NBT - 1) bin = width - 1;
+            atomicAdd(lds64 + e0.so + fi * NBT + copy * width + bin, e0.pk);
+          } else {
+            atomicAdd(lds64 + e0.so + fi * NBT + bin, e0.pk);
           }
         }
       }
-      ca = na; cb = nb; pka = pkn; soa = son;
+      shift(ec);
+      e0 = e1;
+      e1 = e2;
     }
-    // the next tile overwrites this wave's entries only after every lane read them
-    wave_lds_sync();
+    if (!staged && uuN < u1) {   // empty tile: stage the next one here
+      nN = stage(uuN, en_);
+      fetch(en_[0] & 0xFFFFu, uuN * ROWS, f0);
+      fetch(en_[0] >> 16, uuN * ROWS, f1);
+    }
+    uu = uuN;
+    nC = nN;
+#pragma unroll
+    for (int k = 0; k < ROWS / 2; ++k) ec[k] = en_[k];
+    e0 = f0;
+    e1 = f1;
   }
   __syncthreads();
   unsigned long long* out = partials + (int64_t)chunk * hist_elems;
@@ -2592,7 +2659,8 @@ H2OMX_API int h2omx_hist_build_rm(const uint8_t* codes, const uint8_t* codes_rm,
   if (F < 1 || F > RM_PITCH || npad % 16 != 0 || slot_cnt < 1 || slot_cnt > 63 || (pkm != 2 && pkm != 4) ||
       pk_buf == nullptr || codes_rm == nullptr || threads % 64 != 0 || threads > 1024 || threads < 64 || wgpg < 1)
     return kBadArg;
-  if (route && (ctl_prev == nullptr || nid_out == nullptr || nid_out == nid || codes == nullptr)) return kBadArg;
+  if (route && (ctl_prev == nullptr || nid_out == nullptr || nid_out == nid || codes == nullptr || threads > 512))
+    return kBadArg;
   if (!route && slot16 == nullptr) return kBadArg;
   const int64_t units = npad / 16;
   if ((units + wgpg - 1) / wgpg * 16 > ROWS_CAP) return kBadArg;

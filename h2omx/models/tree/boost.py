@@ -561,9 +561,10 @@ class TreeGraph:
         side.wait_stream(torch.cuda.current_stream(dev))
         torch.cuda.synchronize(dev)
         # no garbage collection while capturing: a collected graph / event / pool
-        # of an earlier model would be destroyed inside the capture (illegal
-        # while a stream captures; torch.cuda.graph collects up front the same way)
-        gc.collect()
+        # of an earlier model would be destroyed inside the capture (illegal while
+        # a stream captures).  (No gc.collect() up front: in a large process it
+        # costs tens of ms per fit; reference-counted frees of tensors from the
+        # regular pool are safe during capture.)
         gc_was = gc.isenabled()
         gc.disable()
         try:

@@ -150,14 +150,19 @@ class HipTreeBuilder:
         # global index of this rank's first row: the stochastic-rounding dither and
         # bagging hash use global row ids, so a multi-GPU model is bit-identical to
         # the single-GPU model on the concatenated rows
-        self.row_base = global_row_base(bm.n, comm)
+        self.row_base, n_global = global_rows(bm.n, comm)
         self.plans = {}
         # largest workgroup row chunk over every plan this tree can use: sets the
-        # fixed-point resolution (finer for smaller chunks), identical across levels
-        units = bm.npad // self.ROWS_PER_LANE
+        # fixed-point resolution (finer for smaller chunks), identical across levels.
+        # Evaluated on the GLOBAL row count (every rank, and a 1-rank run on the
+        # same rows, derives the same scale: strong-scaled runs are bit-identical to
+        # one GPU); the local plans are then held to chunks <= this (see _plan).
+        self.max_rows_per_wg = None
+        g_units = max(1, -(-n_global // 64) * 64) // self.ROWS_PER_LANE
         # (compacted plans included either way: the scale must not depend on the CMP switch)
-        cands = [self.plan_level(1 << k, c) for k in range(0, 13) for c in (False, True)] + [self.plan_level(1 << 20)]
-        self.max_rows_per_wg = max(self.ROWS_PER_LANE * math.ceil(units / c["wgpg"]) for c in cands)
+        cands = [self._choose(1 << k, c, g_units) for k in range(0, 13) for c in (False, True)] + \
+                [self._choose(1 << 20, False, g_units)]
+        self.max_rows_per_wg = max(self.ROWS_PER_LANE * math.ceil(g_units / c["wgpg"]) for c in cands)
         # >= 2^16 rows per workgroup bounds the per-row fixed-point values to 16 bits
         # (tree_begin: |G_q| <= 2^14, S_q <= 2^15): the packed rows are then stored in
         # 32 bits (hist_build PKM 3/4), halving what every deep-level feature group re-reads
@@ -202,7 +207,10 @@ class HipTreeBuilder:
             self.pc_rows = int(self.lib.h2omx_pc_rows())
             hc = int(os.environ.get("H2OMX_SEG_CHUNK", "0")) or -(-bm.n // self.SEG_TARGET_CHUNKS)
             self.hc_rows = min(self.ROWS_CAP, max(2048, -(-hc // 256) * 256))
-            self.max_rows_per_wg = max(self.max_rows_per_wg, self.hc_rows)
+            # the scale covers the chunk size a 1-rank run on all rows would use
+            hc_g = int(os.environ.get("H2OMX_SEG_CHUNK", "0")) or -(-n_global // self.SEG_TARGET_CHUNKS)
+            self.max_rows_per_wg = max(self.max_rows_per_wg, self.hc_rows,
+                                       min(self.ROWS_CAP, max(2048, -(-hc_g // 256) * 256)))
             budget = self.SEG_LDS_BUDGET
             fg = max(1, min(self.F, budget // (self.nbt * 8)))
             groups = math.ceil(self.F / fg)
@@ -214,12 +222,8 @@ class HipTreeBuilder:
             self.codes_rm = bm.codes_rm
             self.idx = [torch.empty((max(bm.n, 1),), dtype=torch.int32, device=d) for _ in range(2)]
         # the fixed-point scales (tree_begin) derive from max_rows_per_wg: every rank
-        # must quantise with the SAME scale or the summed int64 histograms mix units,
-        # so agree on the largest chunk over all ranks (shards differ in row count)
-        if comm is not None and comm.world_size > 1:
-            t = torch.tensor([self.max_rows_per_wg], dtype=torch.int64, device=d)
-            comm.all_reduce_(t, "max")
-            self.max_rows_per_wg = int(t.item())
+        # quantises with the SAME scale (derived from the global row count above), so
+        # the summed int64 histograms are in one unit
         self.pk32 = self.max_rows_per_wg >= 65536 and os.environ.get("H2OMX_PK32", "1") == "1"
 
     # -- buffers -----------------------------------------------------------
@@ -258,19 +262,25 @@ class HipTreeBuilder:
     CMP_DEEP_LDS_BUDGET = 112 * 1024
     CMP_MAX_SLOTS = 64
     # levels >= 1 of the scan engine (F <= 32): built rows compacted per wave and
-    # gathered from the row-major code copy (hist_build_rm_kernel); bit-identical
-    RM = os.environ.get("H2OMX_HIST_RM", "1") == "1"
+    # gathered from the row-major code copy (hist_build_rm_kernel).  Bit-identical
+    # but measured slower on HIGGS 11M depth 5 (1.25 vs 0.945 ms/tree: routed
+    # levels 135-149 vs 110-127 us although they issue ~2.2x fewer LDS atomics,
+    # profiles/r3/hist_rm_ab.txt), so opt-in (H2OMX_HIST_RM=1)
+    RM = os.environ.get("H2OMX_HIST_RM", "0") == "1"
     RM_THREADS = int(os.environ.get("H2OMX_RM_THREADS", "1024"))
     RM_ROWS_PER_WG = int(os.environ.get("H2OMX_RM_ROWS_PER_WG", "32768"))
     RM_MAX_WGS = int(os.environ.get("H2OMX_RM_MAX_WGS", "256"))
+    # levels needing more slot passes re-gather the rows once per pass: column path
+    RM_MAX_PASSES = int(os.environ.get("H2OMX_RM_MAX_PASSES", "8"))
 
-    def plan_rm(self, max_slots: int):
+    def plan_rm(self, max_slots: int, routed: bool = False):
         """Slots per pass / passes / grid of the compacted row-major kernel (one
-        feature group; 160 KB LDS = histograms + a 2 KB entry stage per wave)."""
-        key = ("rm", max_slots)
+        feature group; 160 KB LDS = histograms + a 2 KB entry stage per wave).
+        Routed levels run 512-thread workgroups (register pressure)."""
+        key = ("rm", max_slots, routed)
         if key in self.plans:
             return self.plans[key]
-        threads = self.RM_THREADS
+        threads = min(self.RM_THREADS, 512) if routed else self.RM_THREADS
         per_slot = self.F * self.nbt * 8
         budget = 160 * 1024 - (threads // 64) * 2048
         slot_cnt = max(1, min(max_slots, 63, budget // per_slot))
@@ -293,7 +303,7 @@ class HipTreeBuilder:
     # column load per distinct split feature) instead of partition_kernel's gathers
     ROUTE_KERNEL = os.environ.get("H2OMX_ROUTE_KERNEL", "0") == "1"
 
-    def _plan(self, max_slots: int, budget: int, threads: int):
+    def _plan(self, max_slots: int, budget: int, threads: int, units: int | None = None):
         per_slot_feat = self.nbt * 8
         F = self.F
         if max_slots * per_slot_feat <= budget:
@@ -306,12 +316,14 @@ class HipTreeBuilder:
             fg, n_groups = 1, F
             slot_cnt = max(1, budget // per_slot_feat)
             passes = math.ceil(max_slots / slot_cnt)
-        units = self.bm.npad // self.ROWS_PER_LANE
+        if units is None:
+            units = self.bm.npad // self.ROWS_PER_LANE
         target = self.TARGET_WGS * 512 // threads
         wgpg = max(8, (target // n_groups) // 8 * 8)
         max_wgpg = max(8, (units // (threads * 2)) // 8 * 8)   # keep >= ~2 row units per lane
         wgpg = min(wgpg, max_wgpg)
-        min_wgpg = math.ceil(math.ceil(units / (self.ROWS_CAP // self.ROWS_PER_LANE)) / 8) * 8
+        cap = self.ROWS_CAP if self.max_rows_per_wg is None else min(self.ROWS_CAP, self.max_rows_per_wg)
+        min_wgpg = math.ceil(math.ceil(units / (cap // self.ROWS_PER_LANE)) / 8) * 8
         wgpg = max(wgpg, min_wgpg)
         return dict(slot_cnt=slot_cnt, fg=fg, n_groups=n_groups, passes=passes, wgpg=wgpg, threads=threads)
 
@@ -325,16 +337,21 @@ class HipTreeBuilder:
         key = (max_slots, cmp)
         if key in self.plans:
             return self.plans[key]
+        plan = self._choose(max_slots, cmp)
+        self.plans[key] = plan
+        return plan
+
+    def _choose(self, max_slots: int, cmp: bool, units: int | None = None):
+        """plan_level's choice for ``units`` row units (default: this rank's)."""
         lo, hi = (self.CMP_LDS_BUDGET, self.CMP_DEEP_LDS_BUDGET) if cmp else (self.LDS_BUDGET, self.DEEP_LDS_BUDGET)
-        plan = self._plan(max_slots, lo, self.THREADS)
+        plan = self._plan(max_slots, lo, self.THREADS, units)
         if hi > lo and plan["n_groups"] >= self.DEEP_MIN_GROUPS:
-            deep = self._plan(max_slots, hi, 1024)
+            deep = self._plan(max_slots, hi, 1024, units)
             if deep["n_groups"] < plan["n_groups"] or deep["passes"] < plan["passes"]:
                 plan = deep
         plan["cmp"] = cmp
         if cmp and (plan["slot_cnt"] > self.CMP_MAX_SLOTS or self.ROWS_PER_LANE != 16):
-            plan = dict(self.plan_level(max_slots, False))
-        self.plans[key] = plan
+            plan = dict(self._choose(max_slots, False, units))
         return plan
 
     def _fused_level(self, d: int) -> bool:
@@ -423,12 +440,12 @@ class HipTreeBuilder:
             built = self._buf("built", max_slots * self.per_node, torch.int64)
             hist_elems = plan["slot_cnt"] * plan["fg"] * nbt
             partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_elems, torch.int64)
-            if d > 0 and self._rm_ok():
+            routed = fuse and d > 0 and self._fused_level(d)
+            if d > 0 and self._rm_ok() and self.plan_rm(max_slots, routed)["passes"] <= self.RM_MAX_PASSES:
                 # deeper levels: built rows only, whole rows gathered row-major
-                plan = self.plan_rm(max_slots)
+                plan = self.plan_rm(max_slots, routed)
                 hist_elems = plan["slot_cnt"] * self.F * nbt
                 partials = self._buf("partials", plan["wgpg"] * hist_elems, torch.int64)
-                routed = fuse and self._fused_level(d)
                 for ps in range(plan["passes"]):
                     slot_lo = ps * plan["slot_cnt"]
                     with T("hist"):
@@ -816,11 +833,16 @@ def per_slot_fits(F: int, nbt: int, threads: int) -> bool:
     return F * nbt * 8 + (threads // 64) * 2048 <= 160 * 1024
 
 
-def global_row_base(n: int, comm) -> int:
+def global_rows(n: int, comm) -> tuple[int, int]:
+    """(global index of this rank's first row, global row count)."""
     if comm is None or comm.world_size <= 1:
-        return 0
+        return 0, n
     counts = comm.all_gather_cat(torch.tensor([n], dtype=torch.int64, device=comm.device)).cpu().tolist()
-    return int(sum(counts[: comm.rank]))
+    return int(sum(counts[: comm.rank])), int(sum(counts))
+
+
+def global_row_base(n: int, comm) -> int:
+    return global_rows(n, comm)[0]
 
 
 def trees_from_bytes(buf: np.ndarray, capacity: int) -> np.ndarray:

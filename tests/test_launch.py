@@ -118,7 +118,7 @@ def test_bench_spawns_its_own_ranks_cpu():
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
-    assert out["config"]["global_batch"] == 8000
+    assert out["config"]["global_batch"] == 4000 and out["scaling"] == "strong"   # 4000 rows over 2 ranks
 
 
 @pytest.mark.gpu
