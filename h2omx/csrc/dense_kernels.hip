@@ -340,6 +340,233 @@ __global__ __launch_bounds__(256) void glm_irls_kernel(const float* __restrict__
   if (t == 0) dev_out[blockIdx.x] = devred[0] + devred[1] + devred[2] + devred[3];
 }
 
+// ---------------------------------------------------------------------------
+// GLM IRLS pass, wave-private row chunks (glm_irls_wave_kernel): the default
+// for p + 2 <= 128 and every family but multinomial.
+//
+// glm_irls_kernel above runs each 64-row chunk as a workgroup-wide chain
+// (stage -> barrier -> dot products -> barrier -> link math on ONE wave ->
+// barrier -> scale -> barrier -> MFMA), ~7 ms per pass at 10M x 100 with the
+// waves parked on barriers ~75 % of the time (profiles/r2/dense_pmc).  Here
+// every wave is an independent unit over its own row range:
+//   * the augmented design [x | 1 | z] of a 64-row chunk lives in REGISTERS:
+//     lane l = (h = l / 16, c = l % 16) holds column blk * 16 + c of rows
+//     h * 16 .. h * 16 + 15 for every 16-column block blk (64 contiguous bytes
+//     per lane and block), which is exactly the operand layout of
+//     v_mfma_f32_16x16x4f32 (A: i = l % 16, k = l / 16; step s = row h*16+s);
+//   * the next chunk's columns / y / weights / offsets are loaded while the
+//     current chunk is computed (register double buffer, one wait per chunk);
+//   * linear predictors: per lane 16 partial dot products (its columns) in
+//     fp64, reduce-scattered over the 16 lanes of the row group (15 shuffles)
+//     so that every lane owns ONE row: the link / weight / deviance math runs
+//     on all 64 lanes;
+//   * sqrt(w) and z come back to the column lanes with 16 + 16 shuffles; the
+//     scaled chunk feeds 16 MFMA steps per upper 16x16 Gram tile (16-column
+//     granularity: 28 tiles at p = 100 instead of 10 32x32 tiles padded to 128);
+//   * no LDS, no barriers.  Each unit accumulates at most a few thousand rows
+//     in fp32 before the fp64 slab reduction (slab_reduce16_kernel).
+// ---------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int GW_S = 8;            // rows per lane group and chunk = MFMA k-steps of 4 rows
+constexpr int GW_RB = 4 * GW_S;    // rows per chunk
+
+template <int NB, bool VEC>
+__global__ __launch_bounds__(256) void glm_irls_wave_kernel(const float* __restrict__ X, int64_t ld, int64_t n,
+                                                            const float* __restrict__ y,
+                                                            const float* __restrict__ wprior,
+                                                            const float* __restrict__ offset,
+                                                            const float* __restrict__ means,
+                                                            const float* __restrict__ beta, GlmParams P,
+                                                            int64_t rows_per_unit, int n_units,
+                                                            float* __restrict__ slab, double* __restrict__ dev_out) {
+  constexpr int PW = NB * 16;                 // padded augmented width
+  constexpr int T = NB * (NB + 1) / 2;        // upper 16x16 tiles
+  // coefficients / imputation means in LDS: read per chunk through the LDS
+  // counter, so they never wait behind the next chunk's in-flight global loads
+  __shared__ double bsh[PW];
+  __shared__ float msh[PW];
+  const int p = P.p;
+  for (int c = threadIdx.x; c < PW; c += blockDim.x) {
+    bsh[c] = (c < p) ? (double)beta[c] : 0.0;
+    msh[c] = (c < p) ? means[c] : 0.0f;
+  }
+  __syncthreads();   // the only barrier: before any wave can leave
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (unit >= n_units) return;
+  const int h = lane >> 4, cl = lane & 15;
+  const int64_t r_begin = (int64_t)unit * rows_per_unit;
+  const int64_t r_end = min(n, r_begin + rows_per_unit);
+
+  f32x4 acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const double b0 = (double)beta[p];
+  double dev_acc = 0.0;
+
+  float xc[NB][GW_S], xn[NB][GW_S];
+  float yc = 0.f, wc = 1.f, oc = 0.f, yn = 0.f, wn = 1.f, on = 0.f;
+  auto load = [&](int64_t r0, float (&xb)[NB][GW_S], float& yv, float& wv, float& ov) {
+    const int64_t rr = r0 + h * GW_S;         // first row of this lane's group
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int c = b * 16 + cl;
+      if (c < p) {
+        const float* src = X + (int64_t)c * ld + rr;
+        if (VEC && rr + GW_S <= r_end) {
+#pragma unroll
+          for (int q = 0; q < GW_S / 4; ++q) {
+            const float4 v = *reinterpret_cast<const float4*>(src + 4 * q);
+            xb[b][4 * q] = v.x; xb[b][4 * q + 1] = v.y; xb[b][4 * q + 2] = v.z; xb[b][4 * q + 3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < GW_S; ++s) xb[b][s] = (rr + s < r_end) ? src[s] : 0.0f;
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < GW_S; ++s) xb[b][s] = 0.0f;
+      }
+    }
+    const int64_t row = r0 + h * GW_S + (cl & (GW_S - 1));   // the row this lane owns in the link step
+    if (row < r_end) {
+      yv = y[row];
+      wv = wprior ? wprior[row] : 1.0f;
+      ov = offset ? offset[row] : 0.0f;
+    } else {
+      yv = 0.f; wv = 0.f; ov = 0.f;
+    }
+  };
+  auto compute = [&](int64_t r0, float (&xb)[NB][GW_S], float yv, float wv, float ov) {
+    // 1. mean-impute NaNs, partial linear predictors of the lane's rows
+    double part[GW_S];
+#pragma unroll
+    for (int s = 0; s < GW_S; ++s) part[s] = 0.0;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int c = b * 16 + cl;
+      const double bc = bsh[c];
+      const float mc = msh[c];
+#pragma unroll
+      for (int s = 0; s < GW_S; ++s) {
+        float v = xb[b][s];
+        if (v != v) v = mc;
+        xb[b][s] = v;
+        part[s] = fma((double)v, bc, part[s]);
+      }
+    }
+    // 2. sum over the 16 column lanes of the group: a butterfly over lane bit 3,
+    //    then a reduce-scatter over bits 2..0 -> lane c owns row c % 8
+#pragma unroll
+    for (int s = 0; s < GW_S; ++s) part[s] += __shfl_xor(part[s], 8, kWave);
+#pragma unroll
+    for (int off = GW_S / 2; off >= 1; off >>= 1) {
+      const bool hi = (cl & off) != 0;
+#pragma unroll
+      for (int j = 0; j < off; ++j) {
+        const double send = hi ? part[j] : part[j + off];
+        const double recv = __shfl_xor(send, off, kWave);
+        part[j] = (hi ? part[j + off] : part[j]) + recv;
+      }
+    }
+    // 3. link / IRLS weight / working response / deviance of this lane's row
+    const int64_t row = r0 + h * GW_S + (cl & (GW_S - 1));
+    float sw = 0.f, zz = 0.f;
+    if (row < r_end) {
+      const double eta = part[0] + b0 + (double)ov;
+      double mu, dmu;
+      glm_link(P, eta, mu, dmu);
+      const double wi = (double)wv * dmu * dmu / glm_var(P, mu);
+      zz = (float)(eta - (double)ov + ((double)yv - mu) / dmu);
+      sw = (float)sqrt(fmax(wi, 0.0));
+      if (cl < GW_S) dev_acc += (double)wv * glm_dev(P, (double)yv, mu);   // lanes c and c + 8 share a row
+    }
+    // 4. scale the columns by sqrt(w) of their rows; intercept and z columns
+    const int base = lane & 48;
+#pragma unroll
+    for (int s = 0; s < GW_S; ++s) {
+      const float sws = __shfl(sw, base + s, kWave);
+      const float zs = __shfl(zz, base + s, kWave);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int c = b * 16 + cl;
+        const float v = xb[b][s] * sws;
+        xb[b][s] = (c == p) ? sws : ((c == p + 1) ? zs * sws : v);
+      }
+    }
+    // 5. upper Gram tiles on the matrix cores (A: i = lane % 16, k = lane / 16)
+    int t = 0;
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int bj = bi; bj < NB; ++bj, ++t)
+#pragma unroll
+        for (int s = 0; s < GW_S; ++s)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[bi][s], xb[bj][s], acc[t], 0, 0, 0);
+  };
+
+  int64_t r0 = r_begin;
+  if (r0 < r_end) load(r0, xc, yc, wc, oc);
+  for (; r0 < r_end; r0 += GW_RB) {
+    // the next chunk's loads are in flight while this one computes; one copy of
+    // compute() (a two-chunk unroll doubles the inlined link math and spills)
+    if (r0 + GW_RB < r_end) load(r0 + GW_RB, xn, yn, wn, on);
+    compute(r0, xc, yc, wc, oc);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int s = 0; s < GW_S; ++s) xc[b][s] = xn[b][s];
+    yc = yn; wc = wn; oc = on;
+  }
+  // this unit's upper tiles -> slab [unit][PW][PW] (16x16 tile layout: lane
+  // holds D[4 * (l / 16) + v][l % 16]); strictly-lower tiles are never read
+  float* out = slab + (int64_t)unit * PW * PW;
+  int t = 0;
+#pragma unroll
+  for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+    for (int bj = bi; bj < NB; ++bj, ++t)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) out[(bi * 16 + 4 * h + v) * PW + bj * 16 + cl] = acc[t][v];
+  const double d = wave_sum(dev_acc);
+  if (lane == 0) dev_out[unit] = d;
+}
+
+// fp64 sum of the per-unit slabs of glm_irls_wave_kernel (upper 16x16 tiles;
+// strictly-lower tile entries come out 0 and are mirrored on the host).
+// Pass 1 (grid.y = SLAB_SPLIT): each thread sums every SLAB_SPLIT-th slab of
+// one element into part[y][j] (enough independent loads in flight to stream
+// the slabs at HBM rate); pass 2 folds the SLAB_SPLIT partials in fixed order.
+constexpr int SLAB_SPLIT = 32;
+__global__ __launch_bounds__(256) void slab_reduce16_kernel(const float* __restrict__ slab, int n_slabs, int pw,
+                                                            double* __restrict__ part) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t w = (int64_t)pw * pw;
+  if (j >= w) return;
+  const int i = j / pw, k = j % pw;
+  double a0 = 0.0, a1 = 0.0;
+  if ((i >> 4) <= (k >> 4)) {
+    int s = blockIdx.y;
+    for (; s + SLAB_SPLIT < n_slabs; s += 2 * SLAB_SPLIT) {
+      a0 += slab[(int64_t)s * w + j];
+      a1 += slab[(int64_t)(s + SLAB_SPLIT) * w + j];
+    }
+    if (s < n_slabs) a0 += slab[(int64_t)s * w + j];
+  }
+  part[(int64_t)blockIdx.y * w + j] = a0 + a1;
+}
+
+__global__ __launch_bounds__(256) void slab_fold_kernel(const double* __restrict__ part, int64_t w,
+                                                        double* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= w) return;
+  double a = 0.0;
+#pragma unroll
+  for (int y = 0; y < SLAB_SPLIT; ++y) a += part[(int64_t)y * w + j];
+  out[j] = a;
+}
+
 // fp64 reduction of the per-workgroup slabs (upper tiles only are written;
 // lower-tile entries of the slab are never read)
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int n_slabs, int width,
@@ -1440,6 +1667,51 @@ H2OMX_API int h2omx_glm_irls(const float* X, int64_t ld, int64_t n, const float*
     default: return kBadArg;
   }
 #undef GLM_L
+  return launch_status();
+}
+
+// Wave-unit GLM IRLS pass (glm_irls_wave_kernel): p + 2 <= 128, not
+// multinomial.  n_units waves of rows_per_unit rows (multiple of 64); slab
+// [n_units][pw][pw] fp32 with pw = 16 * ceil((p + 2) / 16); dev_out [n_units].
+H2OMX_API int h2omx_glm_irls_wave(const float* X, int64_t ld, int64_t n, const float* y, const float* wprior,
+                                  const float* offset, const float* means, const float* beta, const void* params,
+                                  int n_units, int64_t rows_per_unit, float* slab, double* dev_out,
+                                  hipStream_t stream) {
+  const GlmParams P = *reinterpret_cast<const GlmParams*>(params);
+  if (P.family == 5 || P.p + 2 > 128 || n_units < 1 || rows_per_unit % GW_RB != 0 ||
+      (int64_t)n_units * rows_per_unit < n)
+    return kBadArg;
+  const int nb = (P.p + 2 + 15) / 16;
+  // 16-byte column loads need 16-byte aligned column starts
+  const bool vec = (ld % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0);
+  const int blocks = cdiv(n_units, 4);
+#define GWL(NB, V)                                                                                            \
+  hipLaunchKernelGGL((glm_irls_wave_kernel<NB, V>), dim3(blocks), dim3(256), 0, stream, X, ld, n, y, wprior,   \
+                     offset, means, beta, P, rows_per_unit, n_units, slab, dev_out)
+#define GWL_NB(NB) do { if (vec) GWL(NB, true); else GWL(NB, false); } while (0)
+  switch (nb) {
+    case 1: GWL_NB(1); break;
+    case 2: GWL_NB(2); break;
+    case 3: GWL_NB(3); break;
+    case 4: GWL_NB(4); break;
+    case 5: GWL_NB(5); break;
+    case 6: GWL_NB(6); break;
+    case 7: GWL_NB(7); break;
+    case 8: GWL_NB(8); break;
+    default: return kBadArg;
+  }
+#undef GWL_NB
+#undef GWL
+  return launch_status();
+}
+
+// out: fp64 [(SLAB_SPLIT + 1) * pw * pw] scratch; the sum lands in out[0 : pw * pw]
+H2OMX_API int h2omx_slab_reduce16(const float* slab, int n_slabs, int pw, double* out, hipStream_t stream) {
+  const int64_t w = (int64_t)pw * pw;
+  double* part = out + w;
+  hipLaunchKernelGGL(slab_reduce16_kernel, dim3(cdiv(w, 256), SLAB_SPLIT), dim3(256), 0, stream, slab, n_slabs, pw,
+                     part);
+  hipLaunchKernelGGL(slab_fold_kernel, dim3(cdiv(w, 256)), dim3(256), 0, stream, part, w, out);
   return launch_status();
 }
 

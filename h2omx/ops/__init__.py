@@ -59,6 +59,8 @@ DENSE_SIGS = {
     "h2omx_dense_sizes": "P",
     "h2omx_glm_irls": "PLLPPPPPPIIPPS",
     "h2omx_slab_reduce_upper": "PIIPS",
+    "h2omx_glm_irls_wave": "PLLPPPPPPILPPS",
+    "h2omx_slab_reduce16": "PIIPS",
     "h2omx_slab_sum": "PIIPS",
     "h2omx_kmeans": "PLLIPPIIPPS",
     "h2omx_glm_wz": "PLPPPPPPPPIS",

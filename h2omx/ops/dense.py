@@ -21,6 +21,12 @@ from . import P, check, dense_lib, stream
 KBADARG = 1  # common.h kBadArg
 # workgroups of the fused GLM Gram / K-Means kernels (sweeps: H2OMX_GLM_WGS, H2OMX_KM_WGS)
 GLM_WGS = int(os.environ.get("H2OMX_GLM_WGS", "512"))
+# wave-unit IRLS kernel (p + 2 <= 128, not multinomial): H2OMX_GLM_WAVE=0 -> workgroup kernel;
+# units = independent waves, each over a contiguous row range (fp32 within a unit, fp64 across)
+GLM_WAVE = os.environ.get("H2OMX_GLM_WAVE", "1") != "0"
+GLM_UNITS = int(os.environ.get("H2OMX_GLM_UNITS", "2048"))
+GLM_UNIT_MIN_ROWS = 512
+SLAB_SPLIT = 32          # dense_kernels.hip slab_reduce16_kernel
 KM_WGS = int(os.environ.get("H2OMX_KM_WGS", "1024"))
 
 FAMILIES = {"gaussian": 0, "binomial": 1, "poisson": 2, "gamma": 3, "tweedie": 4, "multinomial": 5,
@@ -109,6 +115,8 @@ def glm_irls_pass(X: torch.Tensor, y: torch.Tensor, wprior, offset, beta: np.nda
         return _glm_irls_wide(X, y, wprior, offset, beta, family, link, cls, var_power, link_power)
     lib = dense_lib()
     dev = X.device
+    if GLM_WAVE and family != "multinomial" and p + 2 <= 128:
+        return _glm_irls_wave(X, y, wprior, offset, beta, family, link, cls, var_power, link_power)
     tp = _tp_for(p)
     PP = 32 * tp
     n_wg = max(1, min(GLM_WGS, math.ceil(n / 4096)))
@@ -124,6 +132,34 @@ def glm_irls_pass(X: torch.Tensor, y: torch.Tensor, wprior, offset, beta: np.nda
                              ctypes.addressof(gp), n_wg, tp, P(slab), P(devs), st), "glm_irls")
     check(lib.h2omx_slab_reduce_upper(P(slab), n_wg, PP * PP, P(out), st), "slab_reduce_upper")
     G = out.view(PP, PP)[: p + 2, : p + 2].cpu().numpy()
+    G = np.triu(G) + np.triu(G, 1).T
+    return G, float(devs.sum().item())
+
+
+def _glm_irls_wave(X, y, wprior, offset, beta, family, link, cls, var_power, link_power):
+    """glm_irls_wave_kernel: independent wave units over contiguous row ranges
+    (register-resident 32-row chunks, 16x16x4 fp32 MFMA Gram tiles), then the
+    fp64 sum of the per-unit upper tiles."""
+    lib = dense_lib()
+    p, n = X.shape
+    K = beta.shape[0]
+    dev = X.device
+    pw = 16 * math.ceil((p + 2) / 16)
+    units = max(1, min(GLM_UNITS, math.ceil(n / GLM_UNIT_MIN_ROWS)))
+    rows = max(32, -(-math.ceil(n / units) // 32) * 32)
+    units = max(1, math.ceil(n / rows))
+    slab = torch.empty((units * pw * pw,), dtype=torch.float32, device=dev)
+    devs = torch.empty((units,), dtype=torch.float64, device=dev)
+    out = torch.empty(((SLAB_SPLIT + 1) * pw * pw,), dtype=torch.float64, device=dev)   # sum + partials
+    b32 = torch.from_numpy(np.ascontiguousarray(beta, np.float32)).to(dev)
+    means = torch.zeros((max(p, 1),), dtype=torch.float32, device=dev)
+    gp = GlmParams(FAMILIES[family], LINKS[link], p, K, cls, 0, var_power, link_power)
+    Xc = X if X.stride(1) == 1 else X.contiguous()
+    st = stream(dev)
+    check(lib.h2omx_glm_irls_wave(P(Xc), Xc.stride(0), n, P(y), P(wprior), P(offset), P(means), P(b32),
+                                  ctypes.addressof(gp), units, rows, P(slab), P(devs), st), "glm_irls_wave")
+    check(lib.h2omx_slab_reduce16(P(slab), units, pw, P(out), st), "slab_reduce16")
+    G = out[: pw * pw].view(pw, pw)[: p + 2, : p + 2].cpu().numpy()
     G = np.triu(G) + np.triu(G, 1).T
     return G, float(devs.sum().item())
 
