@@ -1052,6 +1052,246 @@ __global__ __launch_bounds__(256) void gemm64_kernel(const float* __restrict__ A
   }
 }
 
+// ---------------------------------------------------------------------------
+// fp32 GEMM with 64 x 64 wave tiles (the MLP's 8192 x 512 x 512 layers).
+// gemm64_kernel gives each wave one 32 x 32 accumulator: two LDS reads per
+// 32x32x2 MFMA and a barrier every 16 MFMAs, ~50 % of the fp32 MFMA peak.
+// Here 4 waves (2 x 2) share a BM x BN block tile and each wave owns a
+// (BM/2) x (BN/2) tile of (BM/64) x (BN/64) 32x32 accumulators: per k pair a
+// lane reads BM/64 + BN/64 operands for (BM/64)(BN/64) MFMAs, and a K-step of
+// 32 is 16 x that many MFMAs between barriers (64 per wave at 128 x 128), long
+// enough to hide the register-staged global loads of the next K-step.
+// LDS images are [k][row]: row-major (MK) operands are transposed by scalar
+// ds_write_b32 into rows of 129 floats (bank (k + r) % 32: the 32 lanes of a
+// half-wave write 32 distinct banks), column-major (KM) ones by ds_write_b128
+// into rows of 132 floats.
+// EPI 0: C = act(acc + bias + beta_c C), or the raw split-K partial (gridDim.z > 1).
+// EPI 1 (back-propagation through an activation): C = acc * act'(Y) with Y the
+//   layer's output [M][N], plus the column sums of C over this block's BM rows
+//   -> bws[blockIdx.y][N] (the bias-gradient partials gemm_wgrad_bias folds).
+// ---------------------------------------------------------------------------
+constexpr int GW_T = 256;
+// dY * act'(Y) given the activation's output Y (Rectifier / Tanh)
+__device__ __forceinline__ float act_grad(float g, float y, int act) {
+  if (act == 1) return y > 0.0f ? g : 0.0f;
+  if (act == 2) return g * (1.0f - y * y);
+  return g;
+}
+
+template <bool KM> struct GwPad { static constexpr int v = KM ? 4 : 1; };
+
+template <int R, bool KM, bool FULL>
+__device__ __forceinline__ void gw_load(const float* __restrict__ P, int ld, int rows, int k_lim, int r0, int k0,
+                                        bool vec, float (&t)[R / 8]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < R / 32; ++q) {
+    const int f = tid + GW_T * q;   // float4 index in the R x 32 tile
+    int r, k;
+    if (KM) { k = f / (R / 4); r = (f % (R / 4)) * 4; }
+    else { r = f >> 3; k = (f & 7) * 4; }
+    const int gr = r0 + r, gk = k0 + k;
+    if (FULL) {
+      // whole tiles, 16-byte aligned rows: no bounds checks, one dwordx4 per float4
+      const float4 v4 = *reinterpret_cast<const float4*>(KM ? P + (int64_t)gk * ld + gr : P + (int64_t)gr * ld + gk);
+      t[4 * q] = v4.x; t[4 * q + 1] = v4.y; t[4 * q + 2] = v4.z; t[4 * q + 3] = v4.w;
+      continue;
+    }
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f;
+    if (KM) {
+      if (gk < k_lim) {
+        const float* src = P + (int64_t)gk * ld + gr;
+        if (vec && gr + 3 < rows) {
+          const float4 v4 = *reinterpret_cast<const float4*>(src);
+          x0 = v4.x; x1 = v4.y; x2 = v4.z; x3 = v4.w;
+        } else {
+          if (gr < rows) x0 = src[0];
+          if (gr + 1 < rows) x1 = src[1];
+          if (gr + 2 < rows) x2 = src[2];
+          if (gr + 3 < rows) x3 = src[3];
+        }
+      }
+    } else {
+      if (gr < rows) {
+        const float* src = P + (int64_t)gr * ld + gk;
+        if (vec && gk + 3 < k_lim) {
+          const float4 v4 = *reinterpret_cast<const float4*>(src);
+          x0 = v4.x; x1 = v4.y; x2 = v4.z; x3 = v4.w;
+        } else {
+          if (gk < k_lim) x0 = src[0];
+          if (gk + 1 < k_lim) x1 = src[1];
+          if (gk + 2 < k_lim) x2 = src[2];
+          if (gk + 3 < k_lim) x3 = src[3];
+        }
+      }
+    }
+    t[4 * q] = x0; t[4 * q + 1] = x1; t[4 * q + 2] = x2; t[4 * q + 3] = x3;
+  }
+}
+
+template <int R, bool KM>
+__device__ __forceinline__ void gw_store(float* __restrict__ S, const float (&t)[R / 8]) {
+  constexpr int LD = R + GwPad<KM>::v;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < R / 32; ++q) {
+    const int f = tid + GW_T * q;
+    if (KM) {
+      const int k = f / (R / 4), r = (f % (R / 4)) * 4;
+      *reinterpret_cast<float4*>(S + k * LD + r) = make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
+    } else {
+      const int r = f >> 3, k = (f & 7) * 4;
+      S[k * LD + r] = t[4 * q];
+      S[(k + 1) * LD + r] = t[4 * q + 1];
+      S[(k + 2) * LD + r] = t[4 * q + 2];
+      S[(k + 3) * LD + r] = t[4 * q + 3];
+    }
+  }
+}
+
+// FULL: M % BM == N % BN == K % 32 == 0 (per split), 16-byte aligned operands:
+// unchecked dwordx4 loads, the XCD-aware tile order (consecutive tiles of one
+// XCD share A row blocks in its L2) and the next K-step's LDS image written
+// between the two halves of the current step's MFMAs.
+template <bool TA, bool TB, int BM, int BN, int EPI, bool FULL>
+__global__ __launch_bounds__(GW_T) void gemm_w64_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                       float* __restrict__ Cm, const float* __restrict__ bias,
+                                                       const float* __restrict__ Y, float* __restrict__ bws, int M,
+                                                       int N, int K, int act, float beta_c) {
+  constexpr int FM = BM / 64, FN = BN / 64;
+  constexpr int LDA = BM + GwPad<TA>::v, LDB = BN + GwPad<!TB>::v;
+  __shared__ __attribute__((aligned(16))) float As[2][32 * LDA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][32 * LDB];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  int tile_x = blockIdx.x, tile_y = blockIdx.y;
+  if (FULL) {
+    // dispatch puts linear block b on XCD b % 8: renumber so that XCD x owns the
+    // contiguous tile range [x * nb / 8, (x + 1) * nb / 8) (row-major over tiles)
+    const int gx = gridDim.x, nb = gx * gridDim.y;
+    if ((nb & 7) == 0) {
+      const int b = blockIdx.y * gx + blockIdx.x;
+      const int r = (b & 7) * (nb >> 3) + (b >> 3);
+      tile_x = r % gx;
+      tile_y = r / gx;
+    }
+  }
+  const int m0 = tile_y * BM, n0 = tile_x * BN;
+  const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
+  const int S = gridDim.z;
+  const int kchunk = ((K + S - 1) / S + 31) / 32 * 32;
+  const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+  if (S > 1) Cm += (int64_t)blockIdx.z * M * N;
+  const bool va = (TA ? (M % 4 == 0) : (K % 4 == 0)) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  const bool vb = (TB ? (K % 4 == 0) : (N % 4 == 0)) && ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int x = 0; x < FM; ++x)
+#pragma unroll
+    for (int y = 0; y < FN; ++y)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.0f;
+  const int li = lane & 31, lh = lane >> 5;
+  float ra[BM / 8], rb[BN / 8];
+  int buf = 0;
+  if (kb < ke) {
+    gw_load<BM, TA, FULL>(A, TA ? M : K, M, ke, m0, kb, va, ra);
+    gw_load<BN, !TB, FULL>(B, TB ? K : N, N, ke, n0, kb, vb, rb);
+    gw_store<BM, TA>(As[0], ra);
+    gw_store<BN, !TB>(Bs[0], rb);
+  }
+  __syncthreads();
+  auto mfma_steps = [&](const float* as, const float* bs, int s_lo, int s_hi) {
+#pragma unroll
+    for (int s2 = s_lo; s2 < s_hi; ++s2) {
+      const int kk = 2 * s2 + lh;
+      float a[FM], b[FN];
+#pragma unroll
+      for (int x = 0; x < FM; ++x) a[x] = as[kk * LDA + wm + 32 * x + li];
+#pragma unroll
+      for (int y = 0; y < FN; ++y) b[y] = bs[kk * LDB + wn + 32 * y + li];
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y) acc[x][y] = mfma32(a[x], b[y], acc[x][y]);
+    }
+  };
+  for (int k0 = kb; k0 < ke; k0 += 32) {
+    const bool more = k0 + 32 < ke;
+    if (more) {
+      gw_load<BM, TA, FULL>(A, TA ? M : K, M, ke, m0, k0 + 32, va, ra);
+      gw_load<BN, !TB, FULL>(B, TB ? K : N, N, ke, n0, k0 + 32, vb, rb);
+    }
+    if (FULL) {
+      // the other buffer was last read before the previous barrier: write the next
+      // step's image while the second half of this step's MFMAs runs
+      mfma_steps(As[buf], Bs[buf], 0, 8);
+      if (more) {
+        gw_store<BM, TA>(As[buf ^ 1], ra);
+        gw_store<BN, !TB>(Bs[buf ^ 1], rb);
+      }
+      mfma_steps(As[buf], Bs[buf], 8, 16);
+    } else {
+      mfma_steps(As[buf], Bs[buf], 0, 16);
+      if (more) {
+        gw_store<BM, TA>(As[buf ^ 1], ra);
+        gw_store<BN, !TB>(Bs[buf ^ 1], rb);
+      }
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  if (EPI == 1) {
+    // C = acc * act'(Y); per-column partial sums of C over the block's rows
+    float* red = As[0];   // [2 row-waves][BN] (the K loop ended on a barrier)
+#pragma unroll
+    for (int y = 0; y < FN; ++y) {
+      const int j = n0 + wn + 32 * y + li;
+      float cs = 0.0f;
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = m0 + wm + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          if (i < M && j < N) {
+            const int64_t o = (int64_t)i * N + j;
+            const float v = act_grad(acc[x][y][e], Y[o], act);
+            Cm[o] = v;
+            cs += v;
+          }
+        }
+      cs += __shfl_xor(cs, 32);
+      if (lh == 0) red[(wid >> 1) * BN + wn + 32 * y + li] = cs;
+    }
+    __syncthreads();
+    for (int c = t; c < BN; c += GW_T) {
+      const int j = n0 + c;
+      if (j < N) bws[(int64_t)tile_y * N + j] = red[c] + red[BN + c];
+    }
+    return;
+  }
+#pragma unroll
+  for (int x = 0; x < FM; ++x)
+#pragma unroll
+    for (int y = 0; y < FN; ++y)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int i = m0 + wm + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        const int j = n0 + wn + 32 * y + li;
+        if (i < M && j < N) {
+          float v = acc[x][y][e];
+          if (S > 1) {
+            Cm[(int64_t)i * N + j] = v;
+            continue;
+          }
+          if (beta_c != 0.0f) v += beta_c * Cm[(int64_t)i * N + j];
+          if (bias) v += bias[j];
+          if (act == 1) v = fmaxf(v, 0.0f);
+          else if (act == 2) v = tanhf(v);
+          Cm[(int64_t)i * N + j] = v;
+        }
+      }
+}
+
 // Skinny outputs (N <= 8, e.g. the MLP's 2-class output layer): C[M][N] =
 // act(A[M][K] B[N][K]^T + bias).  A 128 x 128 MFMA tile would compute 64x
 // more zeros than results (45 us for 8192 x 2 x 512); here one wave per row
@@ -1134,12 +1374,6 @@ __global__ __launch_bounds__(256) void gemm_thin_k_kernel(const float* __restric
 // row phases over one row slice -> ws[slice][col]; the slices are summed
 // later in a fixed order (deterministic), e.g. by the weight gradient's
 // split-K reduce (gemm_splitk_reduce_kernel second job).  N % 4 == 0.
-__device__ __forceinline__ float act_grad(float g, float y, int act) {
-  if (act == 1) return y > 0.0f ? g : 0.0f;
-  if (act == 2) return g * (1.0f - y * y);
-  return g;
-}
-
 __global__ __launch_bounds__(256) void act_backward_bias_kernel(const float* __restrict__ Y, float* __restrict__ dY,
                                                                 float* __restrict__ ws, int M, int N, int act) {
   __shared__ float4 red[4][64];
@@ -1794,14 +2028,46 @@ H2OMX_API int h2omx_kmeans(const float* X, int64_t ld, int64_t n, int d, const f
 
 // tile edge of the fp32 GEMM: 0 = by shape (64 when 128-tiles leave CUs short of work), 64, 128
 static int g_gemm_tile = 0;
+// (1: 64 x 64 wave tiles on 128 x 128 blocks, 2: ... on 128 x 64 blocks)
 H2OMX_API int h2omx_gemm_set_tile(int tile) {
-  if (tile != 0 && tile != 64 && tile != 128) return kBadArg;
+  if (tile != 0 && tile != 64 && tile != 128 && tile != 1 && tile != 2) return kBadArg;
   g_gemm_tile = tile;
   return kOk;
 }
 
+static int g_gemm_full = 1;   // FULL fast path of gemm_w64_kernel when the shape allows (A/B switch)
+H2OMX_API int h2omx_gemm_set_full(int on) {
+  g_gemm_full = on ? 1 : 0;
+  return kOk;
+}
+
+template <int BM, int BN, int EPI>
+static void launch_w64(const float* A, const float* B, float* out, const float* bias, const float* Y, float* bws,
+                       int M, int N, int K, int ta, int tb, int act, float beta_c, int splitk, hipStream_t stream) {
+  const dim3 grid(cdiv(N, BN), cdiv(M, BM), splitk), blk(GW_T);
+  const int kchunk = ((K + splitk - 1) / splitk + 31) / 32 * 32;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0;
+  const bool full = g_gemm_full && aligned && M % BM == 0 && N % BN == 0 && K % 32 == 0 && kchunk * splitk == K;
+#define GW_L(TA_, TB_, F_)                                                                                     \
+  hipLaunchKernelGGL((gemm_w64_kernel<TA_, TB_, BM, BN, EPI, F_>), grid, blk, 0, stream, A, B, out, bias, Y, bws, M, \
+                     N, K, act, beta_c)
+#define GW_T2(F_)                        \
+  if (!ta && !tb) GW_L(false, false, F_); \
+  else if (!ta && tb) GW_L(false, true, F_); \
+  else if (ta && !tb) GW_L(true, false, F_); \
+  else GW_L(true, true, F_)
+  if (full) { GW_T2(true); } else { GW_T2(false); }
+#undef GW_T2
+#undef GW_L
+}
+
 static void launch_gemm(const float* A, const float* B, float* out, const float* bias, int M, int N, int K, int ta,
                         int tb, int act, float beta_c, int splitk, hipStream_t stream) {
+  if (g_gemm_tile == 1 || g_gemm_tile == 2) {
+    if (g_gemm_tile == 1) launch_w64<128, 128, 0>(A, B, out, bias, nullptr, nullptr, M, N, K, ta, tb, act, beta_c, splitk, stream);
+    else launch_w64<128, 64, 0>(A, B, out, bias, nullptr, nullptr, M, N, K, ta, tb, act, beta_c, splitk, stream);
+    return;
+  }
   const int64_t tiles128 = (int64_t)cdiv(N, GB) * cdiv(M, GB) * splitk;
   const bool t64 = g_gemm_tile == 64 || (g_gemm_tile == 0 && tiles128 < 512);
   if (t64) {
@@ -1828,6 +2094,19 @@ H2OMX_API int h2omx_gemm(const float* A, const float* B, float* C, const float* 
   if (splitk > 1)
     hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(cdiv((int64_t)M * N, 256) < 4096 ? cdiv((int64_t)M * N, 256) : 4096),
                        dim3(256), 0, stream, ws, splitk, M, N, C, bias, act, beta_c);
+  return launch_status();
+}
+
+// back-propagation through an activation: C[M][N] = (A[M][K] B[K][N]) * act'(Y),
+// Y = the activation's output [M][N]; bws[cdiv(M, bm)][N] receives the column sums
+// of C per bm-row block (bias-gradient partials).  Returns the block count via
+// *splits.  tile: 1 = 128 x 128 blocks, 2 = 128 x 64.
+H2OMX_API int h2omx_gemm_dact(const float* A, const float* B, float* C, const float* Y, float* bws, int M, int N,
+                              int K, int act, int tile, int* splits, hipStream_t stream) {
+  if (!A || !B || !C || !Y || !bws || M < 1 || N < 1 || K < 1 || (tile != 1 && tile != 2)) return kBadArg;
+  if (tile == 1) launch_w64<128, 128, 1>(A, B, C, nullptr, Y, bws, M, N, K, 0, 0, act, 0.0f, 1, stream);
+  else launch_w64<128, 64, 1>(A, B, C, nullptr, Y, bws, M, N, K, 0, 0, act, 0.0f, 1, stream);
+  if (splits) *splits = cdiv(M, 128);
   return launch_status();
 }
 

@@ -55,6 +55,11 @@ struct SplitParams {
   float col_rate;             // per-node column sampling rate (1 = all)
   int mtries;                 // exact per-node feature count (0 = off)
   int children_leaves;        // children of splits at this level are final leaves
+  int pad2;
+  // monotone constraints (nullptr = none): mono[F] in {-1, 0, +1}; gbound
+  // [capacity][2] = [lo, hi] interval of every node's value, set by its parent
+  const signed char* mono;
+  double* gbound;
 };
 
 struct NodeSplit {  // best split of one node at the current level (64 B)
@@ -140,6 +145,22 @@ __device__ __forceinline__ double split_gain(double GL, double SL, double G, dou
   const double lam = p.lambda_;
   const double tl = l1_thresh(GL, p.alpha), tr = l1_thresh(GR, p.alpha), tt = l1_thresh(G, p.alpha);
   return 0.5 * (tl * tl / (SL + lam) + tr * tr / (SR + lam) - tt * tt / (S + lam)) - p.gamma;
+}
+
+// Monotone constraint of the candidate split's feature (H2O / XGBoost
+// monotone_constraints): +1 needs value(left) <= value(right), -1 the
+// reverse; child values from the split's (G, S) totals (S = W or H by mode).
+// The node-value interval [lo, hi] (SplitParams::gbound) then keeps every
+// descendant on its side of the split's midpoint (see lf_write_node).
+__device__ __forceinline__ bool mono_ok(int mf, double GL, double SL, double G, double S, const SplitParams& p) {
+  if (mf == 0) return true;
+  const double wl = leaf_value(GL, SL, SL, p), wr = leaf_value(G - GL, S - SL, S - SL, p);
+  return mf > 0 ? wl <= wr : wl >= wr;
+}
+
+__device__ __forceinline__ double clamp_bound(double v, const SplitParams& p, int gid, int cap) {
+  if (p.gbound == nullptr || gid <= 0 || gid >= cap) return v;
+  return fmin(fmax(v, p.gbound[2 * gid]), p.gbound[2 * gid + 1]);
 }
 
 }  // namespace
@@ -1376,14 +1397,16 @@ __device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__
   int best_code = 0x7fffffff;
   double bGL = 0, bSL = 0;
   const int m = nvb[f];
+  const int mf = p.mono ? (int)p.mono[f] : 0;
   if (allowed) {
 #pragma unroll
     for (int k = 0; k < B; ++k) {
       const int t = lane * B + k;
       if (t < m && t < NBT - 1) {
         const double sg = (double)(eg + pg[k]) * ig, ssum = (double)(es + ps[k]) * is;
-        const double gA = split_gain(sg, ssum, tg, ts, p);
-        const double gB = (ns > 0.0) ? split_gain(sg + ng, ssum + ns, tg, ts, p) : -INFINITY;
+        const double gA = mono_ok(mf, sg, ssum, tg, ts, p) ? split_gain(sg, ssum, tg, ts, p) : -INFINITY;
+        const double gB = (ns > 0.0 && mono_ok(mf, sg + ng, ssum + ns, tg, ts, p))
+                              ? split_gain(sg + ng, ssum + ns, tg, ts, p) : -INFINITY;
         if (gA > -INFINITY && (gA > best_gain || (gA == best_gain && 2 * t < best_code))) {
           best_gain = gA; best_code = 2 * t; bGL = sg; bSL = ssum;
         }
@@ -1521,7 +1544,7 @@ __device__ __forceinline__ void lf_write_node(int i, const NodeSplit& s, bool do
                                               TreeNode* __restrict__ tree, int tree_capacity) {
   if (do_split && 2 * (k_idx + 1) > max_next_nodes) do_split = false;  // capacity guard
   const int gid = base + i;
-  const double v = leaf_value(s.G, s.H, s.W, p);
+  const double v = clamp_bound(leaf_value(s.G, s.H, s.W, p), p, gid, tree_capacity);
   PartInfo pi;
   pi.gid = gid;
   pi.leaf_children = 0;
@@ -1550,6 +1573,23 @@ __device__ __forceinline__ void lf_write_node(int i, const NodeSplit& s, bool do
     }
     pi.pad = (L.slot & 0xFFFF) | (R.slot << 16);  // children's build slots (partition -> slot16)
     pi.child_gid = next_base + 2 * k_idx;
+    const int cg = next_base + 2 * k_idx;
+    if (p.gbound != nullptr && cg + 1 < tree_capacity) {
+      // monotone constraints: children inherit this node's interval; a split on a
+      // constrained feature cuts it at the midpoint of the (clipped) child values
+      double lo = -INFINITY, hi = INFINITY;
+      if (gid > 0 && gid < tree_capacity) { lo = p.gbound[2 * gid]; hi = p.gbound[2 * gid + 1]; }
+      double llo = lo, lhi = hi, rlo = lo, rhi = hi;
+      const int mf = (int)p.mono[s.feat];
+      if (mf != 0) {
+        const double wl = fmin(fmax(leaf_value(s.GL, s.HL, s.WL, p), lo), hi);
+        const double wr = fmin(fmax(leaf_value(s.G - s.GL, s.H - s.HL, s.W - s.WL, p), lo), hi);
+        const double mid = 0.5 * (wl + wr);
+        if (mf > 0) { lhi = mid; rlo = mid; } else { llo = mid; rhi = mid; }
+      }
+      p.gbound[2 * cg] = llo; p.gbound[2 * cg + 1] = lhi;
+      p.gbound[2 * cg + 2] = rlo; p.gbound[2 * cg + 3] = rhi;
+    }
     if (p.children_leaves) {
       // children are final: their totals come from this split's left stats
       pi.leaf_children = 1;
@@ -1561,8 +1601,8 @@ __device__ __forceinline__ void lf_write_node(int i, const NodeSplit& s, bool do
       lc.na_left = rc.na_left = 0;
       lc.thr = rc.thr = 0.0f;
       lc.gain = rc.gain = 0.0f;
-      lc.value = (float)leaf_value(s.GL, s.HL, s.WL, p);
-      rc.value = (float)leaf_value(GR, HR, WR, p);
+      lc.value = (float)clamp_bound(leaf_value(s.GL, s.HL, s.WL, p), p, cg, tree_capacity);
+      rc.value = (float)clamp_bound(leaf_value(GR, HR, WR, p), p, cg + 1, tree_capacity);
       lc.weight = (float)s.WL;
       rc.weight = (float)WR;
       if (next_base + 2 * k_idx + 1 < tree_capacity) {
@@ -2248,6 +2288,29 @@ __global__ __launch_bounds__(256) void apply_tree_kernel(float* __restrict__ F, 
   F[r] += tree[~nid[r]].value;
 }
 
+// DRF out-of-bag accumulation: after tree t (class k) is built, every row
+// that tree t's bag left out (same hash as boost_update's bagging) adds the
+// value of the leaf it fell into (nid = ~leaf gid) to oob_sum and, for the
+// first class, counts the tree in oob_cnt.  H2O DRF reports its training
+// metrics on these out-of-bag predictions.
+__global__ __launch_bounds__(256) void oob_accumulate_kernel(float* __restrict__ oob_sum,
+                                                             float* __restrict__ oob_cnt, int64_t n,
+                                                             const int* __restrict__ nid,
+                                                             const TreeNode* __restrict__ tree,
+                                                             const float* __restrict__ wobs, uint32_t seed,
+                                                             uint32_t tree_index, float sample_rate,
+                                                             int64_t row_base, int count) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const float u = u01(hash4(seed, tree_index, (uint32_t)(r + row_base), 0x5bd1e995u));
+    if (u < sample_rate) continue;                       // in the bag of this tree
+    if (wobs && wobs[r] == 0.0f) continue;
+    const int leaf = ~nid[r];
+    if (leaf < 0) continue;
+    oob_sum[r] += tree[leaf].value;
+    if (count) oob_cnt[r] += 1.0f;
+  }
+}
+
 // Multinomial softmax gradients for class k plus bagging / nid reset.
 __global__ __launch_bounds__(256) void softmax_grad_kernel(const float* __restrict__ F, int K, int64_t ldF,
                                                            const int* __restrict__ yk, const float* __restrict__ wobs,
@@ -2407,7 +2470,7 @@ __global__ __launch_bounds__(256) void leaf_finalize_kernel(const unsigned long 
     const double H = (double)(long long)acc[3 * gid + 1] / qs[5];
     const double W = (double)(long long)acc[3 * gid + 2] / qs[6];
     if (nd.feat < 0) {
-      nd.value = (float)leaf_value(G, H, W, p);
+      nd.value = (float)clamp_bound(leaf_value(G, H, W, p), p, gid, cap);
       nd.weight = (float)W;
       tree[gid] = nd;
     }
@@ -2891,6 +2954,15 @@ H2OMX_API int h2omx_boost_update(float* F, const float* y, const float* wobs, in
 H2OMX_API int h2omx_apply_tree(float* F, int64_t n, const int* nid, const void* tree, hipStream_t stream) {
   hipLaunchKernelGGL(apply_tree_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, F, n, nid,
                      reinterpret_cast<const TreeNode*>(tree));
+  return launch_status();
+}
+
+H2OMX_API int h2omx_oob_accumulate(float* oob_sum, float* oob_cnt, int64_t n, const int* nid, const void* tree,
+                                   const float* wobs, uint32_t seed, int tree_index, float sample_rate,
+                                   int64_t row_base, int count, hipStream_t stream) {
+  hipLaunchKernelGGL(oob_accumulate_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, stream, oob_sum, oob_cnt, n,
+                     nid, reinterpret_cast<const TreeNode*>(tree), wobs, seed, (uint32_t)tree_index, sample_rate,
+                     row_base, count);
   return launch_status();
 }
 
@@ -3468,13 +3540,15 @@ __device__ __forceinline__ void direct_scan_feature(const long long* __restrict_
   double fbg = -INFINITY;
   int fbc = 0x7fffffff;
   double fGL = 0, fSL = 0;
+  const int mf = p.mono ? (int)p.mono[f] : 0;
 #pragma unroll
   for (int k = 0; k < B; ++k) {
     const int tt = lane * B + k;
     if (tt < m && tt < NBT - 1) {
       const double sgd = (double)(eg + pg[k]) * ig, ssum = (double)(es + ps[k]) * is;
-      const double gA = split_gain(sgd, ssum, tg, ts, p);
-      const double gB = (ns > 0.0) ? split_gain(sgd + ng, ssum + ns, tg, ts, p) : -INFINITY;
+      const double gA = mono_ok(mf, sgd, ssum, tg, ts, p) ? split_gain(sgd, ssum, tg, ts, p) : -INFINITY;
+      const double gB = (ns > 0.0 && mono_ok(mf, sgd + ng, ssum + ns, tg, ts, p))
+                            ? split_gain(sgd + ng, ssum + ns, tg, ts, p) : -INFINITY;
       if (gA > -INFINITY && (gA > fbg || (gA == fbg && 2 * tt < fbc))) { fbg = gA; fbc = 2 * tt; fGL = sgd; fSL = ssum; }
       if (gB > -INFINITY && (gB > fbg || (gB == fbg && 2 * tt + 1 < fbc))) {
         fbg = gB; fbc = 2 * tt + 1; fGL = sgd + ng; fSL = ssum + ns;

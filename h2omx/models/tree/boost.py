@@ -313,6 +313,13 @@ class GpuBooster:
         self.use_graph = os.environ.get("H2OMX_TREE_GRAPH", "auto") != "0" and self.graph_eligible()
         self.graph = None
         self.graph_error = None
+        # DRF out-of-bag predictions (H2O reports DRF training metrics on them):
+        # per row the sum of the leaf values of the trees whose bag left it out
+        self.oob = None
+        if self.dist == "drf" and sample_rate < 1.0:
+            self.oob = (torch.zeros((self.K, bm.npad), dtype=torch.float32, device=self.dev),
+                        torch.zeros((bm.npad,), dtype=torch.float32, device=self.dev))
+            self.use_graph = False
         self.pending = False
         # bounded gradients (unweighted rows; bagging only zeroes rows) quantise with
         # the bound scales on every path, fused or not
@@ -396,6 +403,7 @@ class GpuBooster:
                 b.tree_buf = torch.empty_like(b.tree_buf)
             b.build(st.g[0], st.h[0], self.wout, t, fmask, stat=self._bounds)
             self.trees_dev.append(b.tree_buf if fresh else self._snapshot())
+            self._oob(t, 0)
             self._update(apply=True, next_tree=t + 1, k=0)
         else:
             s = ops.stream(self.dev)
@@ -419,10 +427,22 @@ class GpuBooster:
                 b.stat_max.copy_(maxes[k])
                 b.build(st.g[k], st.h[k], self.wout, t * self.K + k, fmask)
                 self.trees_dev.append(self._snapshot())
+                self._oob(t, k)
                 ops.check(self.lib.h2omx_apply_tree(P(st.Fm[k]), bm.n, P(b.nid), P(b.tree_buf), s), "apply_tree")
         self.t += 1
 
     COMPACT_CAP = 8191   # deeper trees: copy only the nodes actually created
+
+    def _oob(self, t: int, k: int):
+        """Add tree (t, k) to the out-of-bag sums of the rows its bag left out
+        (bag hash of iteration t, as boost_update / softmax_grad draw it)."""
+        if self.oob is None:
+            return
+        b = self.builder
+        ops.check(self.lib.h2omx_oob_accumulate(ops.P(self.oob[0][k]), ops.P(self.oob[1]), self.bm.n, ops.P(b.nid),
+                                                ops.P(b.tree_buf), ops.P(self.st.w), self.seed & 0xFFFFFFFF, t,
+                                                self.sample_rate, b.row_base, 1 if k == 0 else 0,
+                                                ops.stream(self.dev)), "oob_accumulate")
 
     def _try_capture(self):
         b = self.builder
@@ -464,6 +484,8 @@ class GpuBooster:
                     raw[i, : t.numel()] = t
             self.ens.trees = trees_from_bytes(raw.cpu().numpy(), width // TREE_NODE_DTYPE.itemsize)
         self.ens._state = self.st
+        if self.oob is not None:
+            self.ens._oob = (self.oob[0][:, : self.bm.n], self.oob[1][: self.bm.n])
         return self.ens
 
 

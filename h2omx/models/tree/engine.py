@@ -49,6 +49,8 @@ class TreeParams:
     mtries: int = 0
     max_abs_leaf: float = 0.0
     seed: int = 0
+    # per-feature monotone constraint (-1 / 0 / +1), None = unconstrained
+    monotone: tuple | None = None
     extra: dict = field(default_factory=dict)
 
 
@@ -145,6 +147,14 @@ class HipTreeBuilder:
         self.part_blocks = min(int(self.lib.h2omx_partition_blocks()),
                                int(os.environ.get("H2OMX_PART_BLOCKS", "1024")))
         self._sp = SplitParams()
+        # monotone constraints: per-feature sign + every node's value interval
+        # (written by the parent's level finalisation, read by its children)
+        self.mono = self.gbound = None
+        if params.monotone is not None and any(int(m) != 0 for m in params.monotone):
+            if len(params.monotone) != self.F:
+                raise ValueError(f"monotone has {len(params.monotone)} entries for {self.F} features")
+            self.mono = torch.tensor([int(np.sign(m)) for m in params.monotone], dtype=torch.int8, device=d)
+            self.gbound = torch.zeros((2 * self.capacity,), dtype=torch.float64, device=d)
         self.stats = {"host_syncs": 0}
         self.timer = PhaseTimer(device=d)
         # global index of this rank's first row: the stochastic-rounding dither and
@@ -368,6 +378,8 @@ class HipTreeBuilder:
         sp.min_split_improvement, sp.learn_rate, sp.max_abs_leaf = p.min_split_improvement, p.learn_rate, p.max_abs_leaf
         sp.seed, sp.tree_index = p.seed & 0xFFFFFFFF, tree_index
         sp.col_rate, sp.mtries = p.col_sample_rate, p.mtries
+        sp.mono = self.mono.data_ptr() if self.mono is not None else None
+        sp.gbound = self.gbound.data_ptr() if self.gbound is not None else None
         return ctypes.addressof(sp)
 
     # -- one tree ------------------------------------------------------------

@@ -22,6 +22,7 @@ class SplitParams(ctypes.Structure):
         ("learn_rate", ctypes.c_double), ("max_abs_leaf", ctypes.c_double),
         ("seed", ctypes.c_uint32), ("tree_index", ctypes.c_int), ("depth", ctypes.c_int),
         ("col_rate", ctypes.c_float), ("mtries", ctypes.c_int), ("children_leaves", ctypes.c_int),
+        ("pad2", ctypes.c_int), ("mono", ctypes.c_void_p), ("gbound", ctypes.c_void_p),
     ]
 
 

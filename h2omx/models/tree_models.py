@@ -120,6 +120,34 @@ class _TreeBuilder(ModelBuilder):
     def _tree_params(self, nfeat: int) -> TreeParams:
         raise NotImplementedError
 
+    def _monotone(self):
+        """H2O ``monotone_constraints`` ({column: +1 / -1}, or the REST form
+        [{"key": column, "value": sign}]) as one sign per predictor; None if
+        unconstrained.  Numeric predictors only; not for multinomial models
+        (hex/tree/gbm/GBMModel.java monotone checks)."""
+        mc = self.params.get("monotone_constraints")
+        if not mc:
+            return None
+        if isinstance(mc, dict):
+            items = list(mc.items())
+        else:
+            items = [(e["key"], e["value"]) if isinstance(e, dict) else tuple(e) for e in mc]
+        signs = [0] * len(self.x)
+        for col, v in items:
+            if col not in self.x:
+                raise ValueError(f"monotone_constraints: column {col!r} is not a predictor")
+            if self.feature_types.get(col) == ENUM:
+                raise ValueError(f"monotone_constraints: column {col!r} is categorical (numeric columns only)")
+            v = int(float(v))
+            if v not in (-1, 0, 1):
+                raise ValueError(f"monotone_constraints: {col!r} must be -1, 0 or 1, got {v}")
+            signs[self.x.index(col)] = v
+        if not any(signs):
+            return None
+        if self.category == ModelCategory.MULTINOMIAL:
+            raise ValueError("monotone_constraints are not supported for multinomial models")
+        return tuple(signs)
+
     def _fit(self, train: Frame, valid: Frame | None, model_id: str) -> Model:
         enc = str(self.params.get("categorical_encoding") or "AUTO").lower().replace("_", "")
         if enc == "sortbyresponse":
@@ -187,6 +215,9 @@ class _TreeBuilder(ModelBuilder):
                                                  str(self.params.get("calibration_method") or "AUTO"))
         model.timings = dict(ens.timings)
         model.scoring_history = scorer.history
+        oob = getattr(ens, "_oob", None)
+        if oob is not None and ckpt is None and not self.params.get("offset_column"):
+            model.training_metrics = _oob_metrics(model, train, y, w, oob, ens_dist)
         return model
 
     def _sort_levels_by_response(self, train: Frame, valid: Frame | None):
@@ -234,6 +265,31 @@ class _TreeBuilder(ModelBuilder):
 
     def _engine_dist(self, dist: str) -> str:
         return dist
+
+
+def _oob_metrics(model, train, y, w, oob, dist) -> dict:
+    """H2O DRF training metrics: every row scored by the trees whose bag left
+    it out only (average of their leaf values); rows no tree left out are not
+    scored.  ``oob_rows`` = the scored count (all ranks)."""
+    from .base import compute_metrics
+    from .scoring import margins_to_scores
+
+    s, cnt = oob
+    dev = y.device
+    s, cnt = s.to(dev), cnt.to(dev)
+    ok = cnt > 0
+    P = margins_to_scores(s[:, ok] / cnt[ok][None, :], dist, model.category, 1)
+    yv = train.vec(model.y)
+    yy = Vec(model.y, (y.to(torch.int32) if model.category in ("Binomial", "Multinomial") else y.float())[ok],
+             ENUM if model.category in ("Binomial", "Multinomial") else "real",
+             list(yv.domain) if yv.domain else None)
+    m = compute_metrics(model.category, P, yy, None if w is None else w.to(dev)[ok], model.comm, dist)
+    n_ok = float(ok.sum())
+    if model.comm is not None and model.comm.world_size > 1:
+        n_ok = float(model.comm.all_reduce_numpy(np.array([n_ok]))[0])
+    m["oob_rows"] = int(n_ok)
+    m["description"] = "Metrics reported on Out-Of-Bag training samples"
+    return m
 
 
 def _fit_calibration(model, cal, method: str) -> dict:
@@ -499,7 +555,8 @@ class H2OGradientBoostingEstimator(_TreeBuilder):
                     stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0,
                     offset_column=None, balance_classes=False, class_sampling_factors=None,
                     max_after_balance_size=5.0, categorical_encoding="AUTO", checkpoint=None,
-                    calibrate_model=False, calibration_frame=None, calibration_method="AUTO")
+                    calibrate_model=False, calibration_frame=None, calibration_method="AUTO",
+                    monotone_constraints=None)
 
     def _tree_params(self, nfeat):
         p = self.params
@@ -508,7 +565,8 @@ class H2OGradientBoostingEstimator(_TreeBuilder):
                           min_split_improvement=float(p["min_split_improvement"]), mode=0, leaf_mode=0,
                           col_sample_rate=float(p["col_sample_rate"]),
                           col_sample_rate_per_tree=float(p["col_sample_rate_per_tree"]),
-                          max_abs_leaf=float(p["max_abs_leafnode_pred"] or 0.0), seed=self._seed())
+                          max_abs_leaf=float(p["max_abs_leafnode_pred"] or 0.0), seed=self._seed(),
+                          monotone=self._monotone())
 
 
 # ---------------------------------------------------------------------------
@@ -531,7 +589,8 @@ class H2OXGBoostEstimator(_TreeBuilder):
                     booster="gbtree", grow_policy="depthwise", max_abs_leafnode_pred=0.0, tweedie_power=1.5,
                     stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0,
                     offset_column=None, backend="gpu", nbins=None, categorical_encoding="AUTO", checkpoint=None,
-                    calibrate_model=False, calibration_frame=None, calibration_method="AUTO")
+                    calibrate_model=False, calibration_frame=None, calibration_method="AUTO",
+                    monotone_constraints=None)
 
     def _tree_params(self, nfeat):
         p = self.params
@@ -547,7 +606,8 @@ class H2OXGBoostEstimator(_TreeBuilder):
                           reg_lambda=float(p["reg_lambda"]), reg_alpha=float(p["reg_alpha"]), gamma=float(gamma),
                           min_split_improvement=0.0, learn_rate=float(eta), mode=1, leaf_mode=0,
                           col_sample_rate=csr, col_sample_rate_per_tree=float(cst),
-                          max_abs_leaf=float(p["max_abs_leafnode_pred"] or 0.0), seed=self._seed())
+                          max_abs_leaf=float(p["max_abs_leafnode_pred"] or 0.0), seed=self._seed(),
+                          monotone=self._monotone())
 
 
 # ---------------------------------------------------------------------------

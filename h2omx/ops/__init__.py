@@ -36,6 +36,7 @@ TREE_SIGS = {
     "h2omx_boost_update": "PPPLLPPPPPPPS",
     "h2omx_apply_tree": "PLPPS",
     "h2omx_softmax_grad": "PILPPLLIPPPPPPS",
+    "h2omx_oob_accumulate": "PPLPPPUIFLIS",
     "h2omx_stat_blocks": "",
     "h2omx_stat_reduce": "PPS",
     "h2omx_tree_begin": "PIIPPPPILIPS",
@@ -72,8 +73,10 @@ DENSE_SIGS = {
     "h2omx_act_backward": "PPLIS",
     "h2omx_gemm_skinny_nt": "PPPPIIIIS",
     "h2omx_gemm_set_tile": "I",
+    "h2omx_gemm_set_full": "I",
     "h2omx_gemm_thin_k": "PPPLIIPIS",
     "h2omx_act_backward_bias": "PPPIIIIS",
+    "h2omx_gemm_dact": "PPPPPIIIIIPS",
     "h2omx_gemm_wgrad_bias": "PPPIIIIPPIIPS",
     "h2omx_bias_grad": "PPIIPIS",
     "h2omx_softmax_xent": "PPPPIIS",

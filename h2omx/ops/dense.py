@@ -287,8 +287,38 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
 
 def set_gemm_tile(tile: int) -> None:
     """fp32 GEMM tile edge: 0 = by shape (64 x 64 when 128 x 128 tiles would
-    leave CUs short of work), 64 or 128 (tests / tuning)."""
+    leave CUs short of work), 64 or 128 (tests / tuning); 1 / 2 = 64 x 64 wave
+    tiles on 128 x 128 / 128 x 64 blocks (gemm_w64_kernel)."""
     check(dense_lib().h2omx_gemm_set_tile(int(tile)), "gemm_set_tile")
+
+
+def set_gemm_full(on: int) -> None:
+    """gemm_w64_kernel's whole-tile fast path (unchecked loads, XCD-aware tile
+    order, mid-step LDS writes) when the shape allows it; 0 = always the checked
+    kernel (A/B measurements)."""
+    check(dense_lib().h2omx_gemm_set_full(int(on)), "gemm_set_full")
+
+
+def gemm_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int, out: torch.Tensor | None = None,
+              tile: int = 1):
+    """Back-propagation through a Rectifier / Tanh layer in one GEMM:
+    dZ_prev = (dZ[M][K] W[K][N]) * act'(Y[M][N]) (Y = that layer's output), plus
+    the column sums of dZ_prev per 128-row block (its bias gradient before the
+    fixed-order fold).  Returns (dZ_prev, (workspace, splits)) like
+    :func:`act_backward_bias`."""
+    M, K = dZ.shape
+    N = W.shape[1]
+    _dev(dZ, "gemm_dact")
+    if W.shape[0] != K or tuple(Y.shape) != (M, N) or not (dZ.is_contiguous() and W.is_contiguous()
+                                                            and Y.is_contiguous()):
+        raise ValueError("gemm_dact: needs contiguous dZ [M][K], W [K][N], Y [M][N]")
+    C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=dZ.device)
+    splits = -(-M // 128)
+    ws = _workspace(dZ.device, splits * N, slot=1)
+    sp = ctypes.c_int(0)
+    check(dense_lib().h2omx_gemm_dact(P(dZ), P(W), P(C), P(Y), P(ws), M, N, K, int(act), int(tile),
+                                      ctypes.addressof(sp), stream(dZ.device)), "gemm_dact")
+    return C, (ws, splits)
 
 
 def _splitk(M: int, N: int, K: int) -> int:

@@ -116,6 +116,36 @@ class RefTreeBuilder:
         # rows of weight zero still get routed but do not contribute
         contrib = np.where((nid >= 0) & (w != 0), nid, -1)
         n_nodes, base = 1, 0
+        # monotone constraints (mirror of mono_ok / SplitParams::gbound): sign per
+        # feature, [lo, hi] value interval per node id set by the parent's split
+        mono = None
+        if p.monotone is not None and any(int(m) != 0 for m in p.monotone):
+            mono = np.sign(np.asarray(p.monotone, np.int64))
+            bounds = {}
+
+        def clip(v, gid):
+            if mono is None or gid == 0 or gid not in bounds:
+                return v
+            lo, hi = bounds[gid]
+            return min(max(v, lo), hi)
+
+        def lv_vec(Gv, Sv):
+            # leaf_value(G, S, S) over arrays (leaf_mode 0, S = W or H by mode)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                if p.leaf_mode == 1:
+                    v = np.where(Sv > 0, -Gv / Sv, 0.0)
+                else:
+                    den = Sv + p.reg_lambda
+                    v = np.where(den > 1e-12, -_l1(Gv, p.reg_alpha) / den, 0.0)
+            v = v * p.learn_rate
+            if p.max_abs_leaf > 0:
+                v = np.clip(v, -p.max_abs_leaf, p.max_abs_leaf)
+            return v
+
+        def mono_mask(mf, GLv, SLv, Gs, Ss):
+            wl, wr = lv_vec(GLv, SLv), lv_vec(Gs - GLv, Ss - SLv)
+            return wl <= wr if mf > 0 else wl >= wr
+
         for d in range(p.max_depth):
             last = d == p.max_depth - 1
             contrib = np.where((nid >= 0) & (w != 0), nid, -1)
@@ -146,6 +176,11 @@ class RefTreeBuilder:
                         gB = split_gain(cs[0] + na[0], cs[1] + na[1], cs[2] + na[2], tg, th, tw, p)
                     else:
                         gB = np.full_like(gA, -np.inf)
+                    if mono is not None and mono[f] != 0:
+                        si, ts = (2, tw) if p.mode == 0 else (1, th)
+                        gA = np.where(mono_mask(mono[f], cs[0], cs[si], tg, ts), gA, -np.inf)
+                        if na[2] > 0:
+                            gB = np.where(mono_mask(mono[f], cs[0] + na[0], cs[si] + na[si], tg, ts), gB, -np.inf)
                     # codes 2t (NA right) / 2t+1 (NA left); best = max gain, min code
                     both = np.stack([gA, gB], axis=1).reshape(-1)
                     if not np.any(both > -np.inf):
@@ -164,10 +199,24 @@ class RefTreeBuilder:
                     do_split = best[0] > p.min_split_improvement * max(base_term, 1e-12)
                 gid = base + i
                 rec = tree[gid] if gid < self.capacity else np.zeros((), TREE_NODE_DTYPE)
-                rec["value"] = leaf_value(Gt, Ht, Wt, p)
+                rec["value"] = clip(leaf_value(Gt, Ht, Wt, p), gid)
                 rec["weight"] = Wt
                 if do_split:
                     f, t, na_left, GL, HL, WL = best[1]
+                    if mono is not None:
+                        cg = next_base + 2 * k
+                        lo, hi = bounds.get(gid, (-np.inf, np.inf)) if gid else (-np.inf, np.inf)
+                        llo, lhi, rlo, rhi = lo, hi, lo, hi
+                        if mono[f] != 0:
+                            SL, St = (WL, Wt) if p.mode == 0 else (HL, Ht)
+                            wl = min(max(leaf_value(GL, SL, SL, p), lo), hi)
+                            wr = min(max(leaf_value(Gt - GL, St - SL, St - SL, p), lo), hi)
+                            mid = 0.5 * (wl + wr)
+                            if mono[f] > 0:
+                                lhi = rlo = mid
+                            else:
+                                llo = rhi = mid
+                        bounds[cg], bounds[cg + 1] = (llo, lhi), (rlo, rhi)
                     m = int(self.nvb[f])
                     rec["feat"], rec["bin"], rec["na_left"] = f, t, na_left
                     rec["left"] = next_base + 2 * k
@@ -180,8 +229,8 @@ class RefTreeBuilder:
                         rc = tree[next_base + 2 * k + 1]
                         lc["feat"] = rc["feat"] = -1
                         lc["left"] = rc["left"] = -1
-                        lc["value"] = leaf_value(GL, HL, WL, p)
-                        rc["value"] = leaf_value(Gt - GL, Ht - HL, Wt - WL, p)
+                        lc["value"] = clip(leaf_value(GL, HL, WL, p), next_base + 2 * k)
+                        rc["value"] = clip(leaf_value(Gt - GL, Ht - HL, Wt - WL, p), next_base + 2 * k + 1)
                         lc["weight"], rc["weight"] = WL, Wt - WL
                     k += 1
                 else:
@@ -309,6 +358,8 @@ def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback
           else np.repeat(ens.init_f[:, None], n, 1).astype(np.float32))
     wobs = np.ones(n, np.float32) if w_np is None else w_np.astype(np.float32)
     trees = []
+    # DRF out-of-bag sums (GPU: oob_accumulate_kernel)
+    oob = (np.zeros((K, n), np.float64), np.zeros(n, np.float64)) if (dist == "drf" and sample_rate < 1.0) else None
     t0 = time.perf_counter()
     lr0, ann = tp.learn_rate, getattr(tp, "learn_rate_annealing", 1.0)
     for t in range(ntrees):
@@ -338,9 +389,18 @@ def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback
             leaf = ~builder.nid[:n]
             Fm[k] += tree["value"][leaf]
             trees.append(tree)
+            if oob is not None:
+                out_of_bag = (wb == 0) & (wobs != 0)
+                oob[0][k][out_of_bag] += tree["value"][leaf[out_of_bag]].astype(np.float32)
+                if k == 0:
+                    oob[1][out_of_bag] += 1.0
         if callback is not None and callback(t, _CpuView(Fm, trees, K, ens.init_f)) is True:
             break
     ens.timings["train_s"] = time.perf_counter() - t0
     builder.p.learn_rate = lr0
     ens.trees = np.stack(trees) if trees else ens.trees
     ens._cpu_margin = Fm
+    if oob is not None:
+        import torch
+
+        ens._oob = (torch.from_numpy(oob[0].astype(np.float32)), torch.from_numpy(oob[1].astype(np.float32)))

@@ -194,12 +194,13 @@ def test_gemm_64_tiles_bit_identical_to_128(cuda_dev, M, N, K, ta, tb):
     bias = None if ta else torch.randn(N, device=cuda_dev)
     out = {}
     try:
-        for tile in (128, 64):
+        for tile in (128, 64, 1, 2):     # 1 / 2: 64 x 64 wave tiles on 128 x 128 / 128 x 64 blocks
             OD.set_gemm_tile(tile)
             out[tile] = D.gemm(A, B, bias, 0 if ta else 1, ta, tb)
     finally:
         OD.set_gemm_tile(0)
     assert torch.equal(out[64], out[128])
+    assert torch.equal(out[1], out[128]) and torch.equal(out[2], out[128])
     ref = (A.T if ta else A).double() @ (B.T if tb else B).double()
     if bias is not None:
         ref = (ref + bias.double()).clamp_min(0)
@@ -279,3 +280,32 @@ def test_glm_gram_ill_conditioned_collinear_design(cuda_dev):
     fitted_ref = A @ coef
     fitted = m.predict(fr).to_pandas()["predict"].to_numpy(np.float64)
     assert np.abs(fitted - fitted_ref).max() < 1e-4 * np.abs(fitted_ref).max()
+
+
+@pytest.mark.parametrize("M,K,N,act,tile", [(8192, 512, 512, 1, 1), (8192, 512, 512, 2, 2), (1000, 77, 300, 1, 1),
+                                            (333, 130, 70, 2, 2)])
+def test_gemm_dact_matches_reference(cuda_dev, M, K, N, act, tile):
+    """dZ_prev = (dZ W) * act'(Y) in the GEMM epilogue + per-128-row bias partials,
+    folded by the weight-gradient reduce (fp64 reference)."""
+    from h2omx.ops import dense as OD
+
+    torch.manual_seed(7)
+    dZ = torch.randn((M, K), device=cuda_dev)
+    W = torch.randn((K, N), device=cuda_dev)
+    Y = torch.randn((M, N), device=cuda_dev)
+    Y = Y.clamp_min(0) if act == 1 else torch.tanh(Y)
+    out, bpart = OD.gemm_dact(dZ, W, Y, act, tile=tile)
+    dH = dZ.double() @ W.double()
+    ref = dH * ((Y > 0).double() if act == 1 else (1 - Y.double() ** 2))
+    assert torch.allclose(out.double(), ref, rtol=1e-4, atol=2e-3)
+    ws, splits = bpart
+    assert splits == -(-M // 128)
+    assert torch.allclose(ws[: splits * N].view(splits, N).double().sum(0), ref.sum(0), atol=2e-2)
+    # the unfused pair gives the same dZ_prev bits (same k-ordered fmaf chain)
+    OD.set_gemm_tile(tile)
+    try:
+        dH32 = D.gemm(dZ, W)
+    finally:
+        OD.set_gemm_tile(0)
+    dZ2, _ = D.act_backward_bias(Y, dH32, act)
+    assert torch.equal(out, dZ2)
