@@ -338,7 +338,22 @@ def _mlp(args, comm, torch, np):
             with torch.cuda.graph(graph):
                 body()
 
+    trainer = None
+    if args.estimator_defaults:
+        from h2omx.models.deeplearning import _DLTrainer
+
+        p = dict(H2ODeepLearningEstimator.DEFAULTS)
+        p.update(hidden=[512] * 4, activation="Rectifier", precision=args.precision)
+        B = 256 if n_local >= 256 * 64 else max(16, n_local // 64)   # the estimator's mini_batch_size=1 mapping
+        n_min = int(-comm.max_scalar(-float(n_local))) if world > 1 else n_local
+        trainer = _DLTrainer(p, net, X, yi, 1, True, False, 0.0, [0.0] * 8, B, max(1, n_min // B),
+                             comm if world > 1 else None, torch.Generator().manual_seed(args.seed),
+                             None, 4, backward=bw)
+
     def step():
+        if trainer is not None:
+            trainer.step()
+            return
         i = state["i"] % nb
         state["i"] += 1
         if bf16:
@@ -353,13 +368,15 @@ def _mlp(args, comm, torch, np):
         xb = X[i * B:(i + 1) * B]
         Hs, aux = _forward(net, xb, 1, True, 0.0, [0.0] * 8, None)
         dZ, _ = D.softmax_xent(Hs[-1], yi[i * B:(i + 1) * B])
-        bw(None, net, Hs, aux, dZ, 1, comm if world > 1 else None, world)
+        bw(net, Hs, aux, dZ, 1, comm if world > 1 else None, world)
         D.adadelta_(net.flat, net.grad, Eg2, Edx2, 0.99, 1e-8, 0.0)
 
     _sync(torch, dev)
     comm.barrier()
     setup_s = time.perf_counter() - t_setup
     elapsed = _timed(step, args, comm, torch, dev)
+    if trainer is not None:
+        trainer.sync()
     with torch.no_grad():
         xs, ys_ = X[:200_000], y[:200_000]
         from h2omx.metrics.core import auc_from_scores
@@ -378,8 +395,13 @@ def _mlp(args, comm, torch, np):
         "data": "synthetic wide-Gaussian 200 features generated on device; random-init weights",
         "config": {"model": "MLP 200-512x4-2 Rectifier, ADADELTA(0.99,1e-8), softmax", "global_batch": world * B,
                    "seq_len": None, "rows_per_gpu": n_local, "batch_per_gpu": B,
-                   "parallelism": f"dp{world} (gradient all-reduce per step)"},
+                   "parallelism": f"dp{world} (" + ("model averaging per iteration" if trainer is not None
+                                                     else "gradient all-reduce per step") + ")"},
         "train_auc_200k": auc,
+        **({"estimator_defaults": {"mini_batch_rows_per_gpu": B, "replica_sync": "model averaging"
+                                   if world > 1 else "none (1 GPU)",
+                                   "train_samples_per_iteration": trainer.samples_per_iteration(),
+                                   "steps_per_iteration": trainer.spi}} if trainer is not None else {}),
         "achieved_tflops_per_gpu": flops_row * B * args.steps / elapsed / 1e12,
         "setup_s": setup_s,
     }
@@ -403,6 +425,10 @@ def main(argv=None) -> int:
     ap.add_argument("--precision", choices=["bf16", "fp32"], default="fp32",
                     help="dl-mlp GEMM operand precision: fp32 (default, H2O DeepLearning trains in fp32) or bf16 "
                          "(h2omx extension; fp32 accumulation and master weights either way)")
+    ap.add_argument("--estimator-defaults", action="store_true",
+                    help="dl-mlp: one step = one mini-batch of H2ODeepLearningEstimator's shipped defaults "
+                         "(mini_batch_size=1 -> 256 rows per GPU, train_samples_per_iteration=-2 model averaging, "
+                         "ADADELTA) through the estimator's own trainer")
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="gbm-higgs default strong (11M rows in total, split over the ranks: the headline metric's "
                          "config at every N); xgboost-airlines / dl-mlp default weak (their configs are per-GPU)")

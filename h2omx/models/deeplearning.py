@@ -236,6 +236,183 @@ class _Bf16Mlp:
             net.grad.div_(world)
 
 
+class _DLTrainer:
+    """One rank's mini-batch training loop (H2O DeepLearningTask's role).
+
+    Replica synchronisation when the job spans several GPUs:
+
+    * **model averaging** (default; H2O semantics): each
+      rank trains its own replica on its shard for one *iteration* of
+      ``train_samples_per_iteration`` samples, then one all-reduce averages the
+      weights and the ADADELTA accumulators (H2O averages its
+      DeepLearningModelInfo the same way).  ``train_samples_per_iteration``:
+      > 0 global samples per iteration, 0 one epoch, -1 every rank's whole shard,
+      -2 (default) auto-tuned so that the averaging all-reduce costs
+      ``target_ratio_comm_to_comp`` of the compute, timed on the first
+      iteration and agreed across ranks.  Over xGMI this turns one 3.6 MB
+      all-reduce per 256-row mini-batch into one per iteration.
+    * ``sync_gradients=True``: a gradient all-reduce per mini-batch, bucketed
+      per layer and overlapped with back-propagation (replicas bit-identical).
+    """
+
+    PROBE_STEPS = 32
+
+    def __init__(self, p_, net, X, Y, act, cls, auto, drop_in, hd, M, steps_per_epoch, comm, gen, gen_dev,
+                 n_hidden, backward):
+        self.p, self.net, self.X, self.Y = p_, net, X, Y
+        self.act, self.cls, self.auto = act, cls, auto
+        self.drop_in, self.hd, self.M = drop_in, hd, M
+        self.steps_per_epoch = steps_per_epoch
+        self.comm = comm
+        self.world = comm.world_size if comm is not None else 1
+        self.gen, self.gen_dev = gen, gen_dev
+        self.backward = backward
+        self.adaptive = bool(p_["adaptive_rate"])
+        P = net.flat.numel()
+        dev = net.flat.device
+        self.sync_grad = self.world > 1 and bool(p_.get("sync_gradients"))
+        self.avg = self.world > 1 and not self.sync_grad
+        if self.avg:
+            # weights (+ ADADELTA accumulators) in one buffer: one all-reduce per iteration
+            state = torch.zeros(((3 if self.adaptive else 1) * P,), dtype=torch.float32, device=dev)
+            state[:P].copy_(net.flat)
+            net.flat = state[:P]
+            self.state = state
+            self.Eg2 = state[P:2 * P] if self.adaptive else torch.zeros_like(net.flat)
+            self.Edx2 = state[2 * P:] if self.adaptive else torch.zeros_like(net.flat)
+        else:
+            self.Eg2 = torch.zeros_like(net.flat)
+            self.Edx2 = torch.zeros_like(net.flat)
+        self.V = torch.zeros_like(net.flat)
+        self.l1, self.l2 = float(p_["l1"]), float(p_["l2"])
+        self.loss_kind = str(p_["loss"]).lower()
+        self.samples = 0
+        self.n_steps = 0
+        self.since_sync = 0
+        self.perm = None
+        self.spi = None      # steps per iteration (model averaging)
+        self._t0 = None
+        if self.avg:
+            t = int(p_.get("train_samples_per_iteration", -2))
+            if t == 0 or t == -1:
+                self.spi = steps_per_epoch
+            elif t > 0:
+                self.spi = max(1, round(t / (self.world * M)))
+        # h2omx extension: precision="bf16" trains Rectifier / Tanh nets without dropout
+        # on the bf16 matrix cores (fp32 accumulation, fp32 master weights / optimizer)
+        self.mlp = None
+        if (str(p_.get("precision", "fp32")).lower() == "bf16" and X.is_cuda and act in (1, 2) and drop_in == 0
+                and not any(hd[:n_hidden]) and M % 8 == 0):
+            self.mlp = _Bf16Mlp(net, act, M, dev)
+
+    def samples_per_iteration(self) -> int:
+        """global samples between replica synchronisations (0: single GPU)"""
+        if self.world == 1:
+            return 0
+        if self.sync_grad:
+            return self.world * self.M
+        return self.world * self.M * (self.spi or self.steps_per_epoch)
+
+    def step(self) -> None:
+        p_, net, M = self.p, self.net, self.M
+        e_pos = self.n_steps % self.steps_per_epoch
+        n = self.X.shape[0]
+        if e_pos == 0:
+            self.perm = (torch.randperm(n, generator=self.gen).to(self.X.device) if p_["shuffle_training_data"]
+                         else torch.arange(n, device=self.X.device))
+        idx = self.perm[e_pos * M:(e_pos + 1) * M]
+        xb = self.X.index_select(0, idx)
+        mlp = self.mlp
+        if mlp is not None:
+            xbb, xbt = mlp.load_batch(xb)
+            Z = mlp.forward(xbb)
+            Hs = aux = None
+        else:
+            Hs, aux = _forward(net, xb, self.act, True, self.drop_in, self.hd, self.gen_dev)
+            Z = Hs[-1]
+        if self.auto:
+            dZ = (Z - xb) * (2.0 / Z.numel())
+        elif self.cls:
+            dZ, _ = D.softmax_xent(Z, self.Y.index_select(0, idx))
+        else:
+            r = Z[:, 0] - self.Y.index_select(0, idx)
+            if self.loss_kind == "absolute":
+                g = torch.sign(r)
+            elif self.loss_kind == "huber":
+                delta = float(p_["huber_alpha"])
+                g = torch.clamp(r, -delta, delta)
+            else:
+                g = r
+            dZ = (g / r.numel())[:, None].contiguous()
+        comm = self.comm if self.sync_grad else None
+        if mlp is not None:
+            mlp.backward(dZ, xbt, comm, self.world)
+        else:
+            self.backward(net, Hs, aux, dZ, self.act, comm, self.world)
+        self.samples += M * self.world
+        if self.adaptive:
+            D.adadelta_(net.flat, net.grad, self.Eg2, self.Edx2, float(p_["rho"]), float(p_["epsilon"]), self.l2)
+        else:
+            # H2O's rate is per row: a mean-gradient step over M rows takes M of them
+            lr = M * float(p_["rate"]) / (1.0 + float(p_["rate_annealing"]) * self.samples)
+            ramp = min(1.0, self.samples / max(float(p_["momentum_ramp"]), 1.0))
+            mom = float(p_["momentum_start"]) + (float(p_["momentum_stable"]) - float(p_["momentum_start"])) * ramp
+            D.sgd_momentum_(net.flat, net.grad, self.V, lr, mom, self.l2)
+        if self.l1 > 0:
+            net.flat.sub_(self.l1 * torch.sign(net.flat) * (1.0 if self.adaptive else float(p_["rate"])))
+        if math.isfinite(float(p_["max_w2"])):
+            H2ODeepLearningEstimator._clip_w2(net, float(p_["max_w2"]))
+        if mlp is not None:
+            mlp.refresh()
+        self.n_steps += 1
+        self.since_sync += 1
+        if not self.avg:
+            return
+        if self.spi is None:
+            self._autotune()
+        elif self.since_sync >= self.spi:
+            self.sync()
+
+    def _autotune(self) -> None:
+        """train_samples_per_iteration = -2: after PROBE_STEPS local steps, time one
+        averaging all-reduce against the per-step compute and set the iteration
+        length so that the all-reduce is ``target_ratio_comm_to_comp`` of it."""
+        import time
+
+        dev = self.X.device
+        if self.since_sync == 1:
+            _sync_dev(dev)
+            self._t0 = time.perf_counter()
+            return
+        if self.since_sync < min(self.PROBE_STEPS, self.steps_per_epoch) + 1:
+            return
+        _sync_dev(dev)
+        t_step = (time.perf_counter() - self._t0) / (self.since_sync - 1)
+        t1 = time.perf_counter()
+        self.sync()
+        _sync_dev(dev)
+        t_ar = time.perf_counter() - t1
+        ratio = float(self.p.get("target_ratio_comm_to_comp") or 0.05)
+        spi = max(1, math.ceil(t_ar / max(ratio * t_step, 1e-9)))
+        spi = float(min(spi, self.steps_per_epoch))
+        self.spi = int(self.comm.max_scalar(spi))       # every rank the same schedule
+
+    def sync(self) -> None:
+        """model averaging: mean of the replicas' weights (+ ADADELTA state)"""
+        if not self.avg or self.since_sync == 0:
+            return
+        self.comm.all_reduce_(self.state)
+        self.state.div_(self.world)
+        if self.mlp is not None:
+            self.mlp.refresh()
+        self.since_sync = 0
+
+
+def _sync_dev(dev) -> None:
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 class DeepLearningModel(Model):
     algo = "deeplearning"
     algo_full_name = "Deep Learning"
@@ -330,7 +507,7 @@ class H2ODeepLearningEstimator(ModelBuilder):
                     stopping_rounds=5, stopping_metric="AUTO", stopping_tolerance=0.0, huber_alpha=0.9,
                     shuffle_training_data=True, reproducible=False, categorical_encoding="AUTO",
                     use_all_factor_levels=True, offset_column=None, balance_classes=False, checkpoint=None,
-                    precision="fp32")
+                    target_ratio_comm_to_comp=0.05, sync_gradients=False, precision="fp32")
 
     def train(self, x=None, y=None, training_frame=None, validation_frame=None, comm=None, **kw):
         if self.params.get("autoencoder"):
@@ -413,15 +590,8 @@ class H2ODeepLearningEstimator(ModelBuilder):
         epochs = max(0.0, float(p_["epochs"]) - epochs_done)
         steps_per_epoch = max(1, n_min // M)
         total_steps = max(1, int(round(epochs * steps_per_epoch))) if epochs > 0 else 0
-        adaptive = bool(p_["adaptive_rate"])
-        Eg2 = torch.zeros_like(net.flat)
-        Edx2 = torch.zeros_like(net.flat)
-        V = torch.zeros_like(net.flat)
-        l1, l2 = float(p_["l1"]), float(p_["l2"])
-        loss_kind = str(p_["loss"]).lower()
         model = DeepLearningModel(self, model_id, design, net, act, y_mean, y_sd, auto)
         history = []
-        perm = None
         from ..runtime.jobs import current_job
         from .scoring import ScoreKeeper
 
@@ -429,66 +599,18 @@ class H2ODeepLearningEstimator(ModelBuilder):
                              self.category if not auto else "Regression", int(p_["stopping_rounds"] or 0),
                              float(p_["stopping_tolerance"]))
         job = current_job()
-        samples = 0
         score_every = max(1, steps_per_epoch)
-        # h2omx extension: precision="bf16" trains Rectifier / Tanh nets without dropout
-        # on the bf16 matrix cores (fp32 accumulation, fp32 master weights / optimizer)
-        mlp = None
-        if (str(p_.get("precision", "fp32")).lower() == "bf16" and X.is_cuda and act in (1, 2) and drop_in == 0
-                and not any(hd[: len(hidden)]) and M % 8 == 0):
-            mlp = _Bf16Mlp(net, act, M, dev)
+        tr = _DLTrainer(p_, net, X, Y, act, cls, auto, drop_in, hd, M, steps_per_epoch, comm, gen, gen_dev,
+                        len(hidden), backward=self._backward)
+        step = -1
         for step in range(total_steps):
-            e_pos = step % steps_per_epoch
-            if e_pos == 0:
-                perm = (torch.randperm(n, generator=gen).to(dev) if p_["shuffle_training_data"]
-                        else torch.arange(n, device=dev))
-            idx = perm[e_pos * M:(e_pos + 1) * M]
-            xb = X.index_select(0, idx)
-            if mlp is not None:
-                xbb, xbt = mlp.load_batch(xb)
-                Z = mlp.forward(xbb)
-                Hs = aux = None
-            else:
-                Hs, aux = _forward(net, xb, act, True, drop_in, hd, gen_dev)
-                Z = Hs[-1]
-            if auto:
-                dZ = (Z - xb) * (2.0 / Z.numel())
-            elif cls:
-                dZ, _ = D.softmax_xent(Z, Y.index_select(0, idx))
-            else:
-                r = Z[:, 0] - Y.index_select(0, idx)
-                if loss_kind == "absolute":
-                    g = torch.sign(r)
-                elif loss_kind == "huber":
-                    delta = float(p_["huber_alpha"])
-                    g = torch.clamp(r, -delta, delta)
-                else:
-                    g = r
-                dZ = (g / r.numel())[:, None].contiguous()
-            if mlp is not None:
-                mlp.backward(dZ, xbt, comm, world)
-            else:
-                self._backward(net, Hs, aux, dZ, act, comm, world)
-            samples += M * world
-            if adaptive:
-                D.adadelta_(net.flat, net.grad, Eg2, Edx2, float(p_["rho"]), float(p_["epsilon"]), l2)
-            else:
-                # H2O's rate is per row: a mean-gradient step over M rows takes M of them
-                lr = M * float(p_["rate"]) / (1.0 + float(p_["rate_annealing"]) * samples)
-                ramp = min(1.0, samples / max(float(p_["momentum_ramp"]), 1.0))
-                mom = float(p_["momentum_start"]) + (float(p_["momentum_stable"]) - float(p_["momentum_start"])) * ramp
-                D.sgd_momentum_(net.flat, net.grad, V, lr, mom, l2)
-            if l1 > 0:
-                net.flat.sub_(l1 * torch.sign(net.flat) * (1.0 if adaptive else float(p_["rate"])))
-            if math.isfinite(float(p_["max_w2"])):
-                self._clip_w2(net, float(p_["max_w2"]))
-            if mlp is not None:
-                mlp.refresh()
+            tr.step()
             if job is not None:
                 job.progress = (step + 1) / total_steps
             if (step + 1) % score_every == 0 or step == total_steps - 1:
+                tr.sync()     # replicas agree before they are scored
                 ent = self._score_entry(model, X, Y, cls, auto, epochs_done + (step + 1) / steps_per_epoch,
-                                        samples, comm)
+                                        tr.samples, comm)
                 history.append(ent)
                 mk = {"logloss": ent["training_loss"], "MSE": ent["training_loss"],
                       "mean_residual_deviance": ent["training_loss"]}
@@ -498,13 +620,16 @@ class H2ODeepLearningEstimator(ModelBuilder):
                     cancel = float(comm.all_reduce_numpy(np.array([cancel]), "max")[0])
                 if stop or cancel > 0:
                     break
+        tr.sync()
+        model.train_samples_per_iteration = tr.samples_per_iteration()
         model.scoring_history = history
         model.epochs_trained = epochs_done + (step + 1) / steps_per_epoch if total_steps else epochs_done
         if auto:
             model.training_metrics = {"MSE": history[-1]["training_loss"] if history else float("nan")}
         return model
 
-    def _backward(self, net, Hs, aux, dZ, act, comm, world):
+    @staticmethod
+    def _backward(net, Hs, aux, dZ, act, comm, world):
         L = len(net.layers)
         handles = []
         bpart = None   # bias-gradient slices of dZ from the fused activation backward

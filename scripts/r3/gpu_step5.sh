@@ -17,4 +17,6 @@ for cfg in "1 0" "1 1" "2 1"; do
     python3 scripts/pmc_summary.py $OUT > $OUT/summary.txt || exit 1
   done
 done
+timeout -k 10 200 python bench.py --model dl-mlp --steps 30 --warmup 5 > $O/bench_dl_fp32.json 2> $O/bench_dl_fp32.err || exit $?
+timeout -k 10 200 python bench.py --model dl-mlp --estimator-defaults --steps 300 --warmup 30 > $O/bench_dl_estdef.json 2> $O/bench_dl_estdef.err || exit $?
 echo done
