@@ -367,7 +367,7 @@ def _mlp(args, comm, torch, np):
             return
         xb = X[i * B:(i + 1) * B]
         Hs, aux = _forward(net, xb, 1, True, 0.0, [0.0] * 8, None)
-        dZ, _ = D.softmax_xent(Hs[-1], yi[i * B:(i + 1) * B])
+        dZ, _ = D.softmax_xent(Hs[-1], yi[i * B:(i + 1) * B], with_loss=False)
         bw(net, Hs, aux, dZ, 1, comm if world > 1 else None, world)
         D.adadelta_(net.flat, net.grad, Eg2, Edx2, 0.99, 1e-8, 0.0)
 

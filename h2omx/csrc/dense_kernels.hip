@@ -1071,6 +1071,9 @@ __global__ __launch_bounds__(256) void gemm64_kernel(const float* __restrict__ A
 //   -> bws[blockIdx.y][N] (the bias-gradient partials gemm_wgrad_bias folds).
 // ---------------------------------------------------------------------------
 constexpr int GW_T = 256;
+#ifndef GW_SPLIT
+#define GW_SPLIT 4   // k pairs (of 16 per K-step) before the FULL pipeline's LDS write / next loads
+#endif
 // dY * act'(Y) given the activation's output Y (Rectifier / Tanh)
 __device__ __forceinline__ float act_grad(float g, float y, int act) {
   if (act == 1) return y > 0.0f ? g : 0.0f;
@@ -1092,8 +1095,11 @@ __device__ __forceinline__ void gw_load(const float* __restrict__ P, int ld, int
     else { r = f >> 3; k = (f & 7) * 4; }
     const int gr = r0 + r, gk = k0 + k;
     if (FULL) {
-      // whole tiles, 16-byte aligned rows: no bounds checks, one dwordx4 per float4
-      const float4 v4 = *reinterpret_cast<const float4*>(KM ? P + (int64_t)gk * ld + gr : P + (int64_t)gr * ld + gk);
+      // 16-byte aligned rows, K and the KM operands' row counts % 4 == 0: one dwordx4
+      // per float4, masked by one compare per edge (partial K-step / partial tile)
+      float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gk < k_lim && gr < rows)
+        v4 = *reinterpret_cast<const float4*>(KM ? P + (int64_t)gk * ld + gr : P + (int64_t)gr * ld + gk);
       t[4 * q] = v4.x; t[4 * q + 1] = v4.y; t[4 * q + 2] = v4.z; t[4 * q + 3] = v4.w;
       continue;
     }
@@ -1149,8 +1155,8 @@ __device__ __forceinline__ void gw_store(float* __restrict__ S, const float (&t)
   }
 }
 
-// FULL: M % BM == N % BN == K % 32 == 0 (per split), 16-byte aligned operands:
-// unchecked dwordx4 loads, the XCD-aware tile order (consecutive tiles of one
+// FULL: M, N, K % 4 == 0, 16-byte aligned operands: dwordx4 loads masked by one
+// compare per edge, the XCD-aware tile order (consecutive tiles of one
 // XCD share A row blocks in its L2) and the next K-step's LDS image written
 // between the two halves of the current step's MFMAs.
 template <bool TA, bool TB, int BM, int BN, int EPI, bool FULL>
@@ -1198,39 +1204,67 @@ __global__ __launch_bounds__(GW_T) void gemm_w64_kernel(const float* __restrict_
     gw_load<BN, !TB, FULL>(B, TB ? K : N, N, ke, n0, kb, vb, rb);
     gw_store<BM, TA>(As[0], ra);
     gw_store<BN, !TB>(Bs[0], rb);
+    if (FULL && kb + 32 < ke) {
+      // FULL pipeline: the registers always hold the NEXT K-step's tile
+      gw_load<BM, TA, FULL>(A, TA ? M : K, M, ke, m0, kb + 32, va, ra);
+      gw_load<BN, !TB, FULL>(B, TB ? K : N, N, ke, n0, kb + 32, vb, rb);
+    }
   }
   __syncthreads();
+  // operands of k pair s2 + 1 are read from LDS before the MFMAs of pair s2
+  // issue (register double buffer): the LDS latency hides behind the matrix
+  // pipe instead of stalling every pair at an lgkmcnt(0)
   auto mfma_steps = [&](const float* as, const float* bs, int s_lo, int s_hi) {
+    float a[2][FM], b[2][FN];
+#pragma unroll
+    for (int x = 0; x < FM; ++x) a[0][x] = as[(2 * s_lo + lh) * LDA + wm + 32 * x + li];
+#pragma unroll
+    for (int y = 0; y < FN; ++y) b[0][y] = bs[(2 * s_lo + lh) * LDB + wn + 32 * y + li];
 #pragma unroll
     for (int s2 = s_lo; s2 < s_hi; ++s2) {
-      const int kk = 2 * s2 + lh;
-      float a[FM], b[FN];
+      const int c = (s2 - s_lo) & 1;
+      if (s2 + 1 < s_hi) {
+        const int kn = 2 * (s2 + 1) + lh;
 #pragma unroll
-      for (int x = 0; x < FM; ++x) a[x] = as[kk * LDA + wm + 32 * x + li];
+        for (int x = 0; x < FM; ++x) a[c ^ 1][x] = as[kn * LDA + wm + 32 * x + li];
 #pragma unroll
-      for (int y = 0; y < FN; ++y) b[y] = bs[kk * LDB + wn + 32 * y + li];
+        for (int y = 0; y < FN; ++y) b[c ^ 1][y] = bs[kn * LDB + wn + 32 * y + li];
+      }
+      // keep the scheduler from sinking the prefetch below the MFMAs
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int x = 0; x < FM; ++x)
 #pragma unroll
-        for (int y = 0; y < FN; ++y) acc[x][y] = mfma32(a[x], b[y], acc[x][y]);
+        for (int y = 0; y < FN; ++y) acc[x][y] = mfma32(a[c][x], b[c][y], acc[x][y]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
   for (int k0 = kb; k0 < ke; k0 += 32) {
     const bool more = k0 + 32 < ke;
-    if (more) {
-      gw_load<BM, TA, FULL>(A, TA ? M : K, M, ke, m0, k0 + 32, va, ra);
-      gw_load<BN, !TB, FULL>(B, TB ? K : N, N, ke, n0, k0 + 32, vb, rb);
-    }
     if (FULL) {
-      // the other buffer was last read before the previous barrier: write the next
-      // step's image while the second half of this step's MFMAs runs
-      mfma_steps(As[buf], Bs[buf], 0, 8);
+      // registers hold step k+1 (loaded one whole K-step ago): after the first
+      // GW_SPLIT k pairs, write them to the other LDS buffer (last read before the
+      // previous barrier) and issue step k+2's loads into the same registers, so
+      // every global load has a full K-step of MFMAs to arrive.  (Spreading the
+      // stores / loads one float4 per k pair between the MFMA groups measured
+      // slower: 51.5 vs 50.0 us at 8192 x 512 x 512, 57 vs 50 us for the weight
+      // gradient.)
+      mfma_steps(As[buf], Bs[buf], 0, GW_SPLIT);
       if (more) {
         gw_store<BM, TA>(As[buf ^ 1], ra);
         gw_store<BN, !TB>(Bs[buf ^ 1], rb);
+        if (k0 + 64 < ke) {
+          gw_load<BM, TA, FULL>(A, TA ? M : K, M, ke, m0, k0 + 64, va, ra);
+          gw_load<BN, !TB, FULL>(B, TB ? K : N, N, ke, n0, k0 + 64, vb, rb);
+        }
       }
-      mfma_steps(As[buf], Bs[buf], 8, 16);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_steps(As[buf], Bs[buf], GW_SPLIT, 16);
     } else {
+      if (more) {
+        gw_load<BM, TA, FULL>(A, TA ? M : K, M, ke, m0, k0 + 32, va, ra);
+        gw_load<BN, !TB, FULL>(B, TB ? K : N, N, ke, n0, k0 + 32, vb, rb);
+      }
       mfma_steps(As[buf], Bs[buf], 0, 16);
       if (more) {
         gw_store<BM, TA>(As[buf ^ 1], ra);
@@ -1458,6 +1492,113 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __
   }
 }
 
+// ---------------------------------------------------------------------------
+// MLP output layer with few classes (C <= 8, e.g. the 2-class softmax): the
+// weight gradient dW[C][N] = dZ^T H and dZ_prev = (dZ W) * act'(H) are
+// bandwidth work over H [M][N] (16 MB at 8192 x 512), not GEMMs: split-K MFMA
+// tiles of a 2-row output (19.6 us + reduce) and a thin-K GEMM followed by the
+// activation backward (9.5 + 9.8 us) become one streaming pass each.
+// Block = 64 float4 columns (256 columns) x 4 row phases over one row slice.
+// ---------------------------------------------------------------------------
+constexpr int OUT_C = 8;
+
+// stage 1: row z of ws[slice][C * N + C] = partial dZ^T H ([C][N]) followed by the
+// partial column sums of dZ ([C]); the fold sums the slices of both in one pass
+template <int C>
+__global__ __launch_bounds__(256) void out_wgrad_kernel(const float* __restrict__ dZ, const float* __restrict__ H,
+                                                        float* __restrict__ ws, int M, int N) {
+  const int64_t T = (int64_t)C * N + C;
+  __shared__ float4 red[4][64][C];
+  const int c4 = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int j = (blockIdx.x * 64 + c4) * 4;
+  const int S = gridDim.y;
+  const int rows = (M + S - 1) / S;
+  const int r0 = blockIdx.y * rows, r1 = min(M, r0 + rows);
+  float4 acc[C];
+  float bs[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) { acc[c] = make_float4(0.f, 0.f, 0.f, 0.f); bs[c] = 0.f; }
+  if (j < N) {
+    for (int i = r0 + ph; i < r1; i += 4) {
+      const float4 h = *reinterpret_cast<const float4*>(H + (int64_t)i * N + j);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float z = dZ[(int64_t)i * C + c];
+        acc[c].x += z * h.x; acc[c].y += z * h.y; acc[c].z += z * h.z; acc[c].w += z * h.w;
+        bs[c] += z;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) red[ph][c4][c] = acc[c];
+  __syncthreads();
+  if (ph == 0 && j < N) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float4 a = red[0][c4][c], b = red[1][c4][c], d = red[2][c4][c], e = red[3][c4][c];
+      float* o = ws + blockIdx.y * T + (int64_t)c * N + j;      // T may be odd: scalar stores
+      o[0] = (a.x + b.x) + (d.x + e.x);
+      o[1] = (a.y + b.y) + (d.y + e.y);
+      o[2] = (a.z + b.z) + (d.z + e.z);
+      o[3] = (a.w + b.w) + (d.w + e.w);
+    }
+  }
+  if (blockIdx.x == 0) {
+    // column sums of dZ over the slice (every column block computes them; block 0 writes)
+    __syncthreads();
+    float* rb = reinterpret_cast<float*>(red);     // [4 phases][64 lanes][C]
+#pragma unroll
+    for (int c = 0; c < C; ++c) rb[(ph * 64 + c4) * C + c] = (c4 == 0) ? bs[c] : 0.0f;
+    __syncthreads();
+    if (threadIdx.x < C) {
+      const int c = threadIdx.x;
+      ws[blockIdx.y * T + (int64_t)C * N + c] = (rb[(0 * 64) * C + c] + rb[(1 * 64) * C + c]) +
+                                                (rb[(2 * 64) * C + c] + rb[(3 * 64) * C + c]);
+    }
+  }
+}
+
+// dZ_prev [M][N] = (dZ [M][C] W [C][N]) * act'(Y [M][N]) plus its column partial sums ws[slice][N]
+template <int C>
+__global__ __launch_bounds__(256) void thin_dact_kernel(const float* __restrict__ dZ, const float* __restrict__ W,
+                                                        const float* __restrict__ Y, float* __restrict__ out,
+                                                        float* __restrict__ ws, int M, int N, int act) {
+  __shared__ float4 red[4][64];
+  const int c4 = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int j = (blockIdx.x * 64 + c4) * 4;
+  const int S = gridDim.y;
+  const int rows = (M + S - 1) / S;
+  const int r0 = blockIdx.y * rows, r1 = min(M, r0 + rows);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (j < N) {
+    float4 w[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) w[c] = *reinterpret_cast<const float4*>(W + (int64_t)c * N + j);
+    for (int i = r0 + ph; i < r1; i += 4) {
+      const int64_t e = (int64_t)i * N + j;
+      const float4 y = *reinterpret_cast<const float4*>(Y + e);
+      float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float z = dZ[(int64_t)i * C + c];
+        g.x += z * w[c].x; g.y += z * w[c].y; g.z += z * w[c].z; g.w += z * w[c].w;
+      }
+      g = make_float4(act_grad(g.x, y.x, act), act_grad(g.y, y.y, act), act_grad(g.z, y.z, act),
+                      act_grad(g.w, y.w, act));
+      *reinterpret_cast<float4*>(out + e) = g;
+      s.x += g.x; s.y += g.y; s.z += g.z; s.w += g.w;
+    }
+  }
+  red[ph][c4] = s;
+  __syncthreads();
+  if (ph == 0 && j < N) {
+    const float4 a = red[0][c4], b = red[1][c4], d = red[2][c4], e = red[3][c4];
+    *reinterpret_cast<float4*>(ws + (int64_t)blockIdx.y * N + j) =
+        make_float4((a.x + b.x) + (d.x + e.x), (a.y + b.y) + (d.y + e.y), (a.z + b.z) + (d.z + e.z),
+                    (a.w + b.w) + (d.w + e.w));
+  }
+}
+
 // column sums of dY [M][N] (bias gradients), stage 1: block (64 columns x
 // 4 row phases) sums one row slice, folds the phases in LDS -> ws[slice][col]
 __global__ __launch_bounds__(256) void bias_grad_split_kernel(const float* __restrict__ dY, float* __restrict__ ws,
@@ -1523,6 +1664,7 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
       if (k == yi) l = -logf(fmaxf(pk, 1e-30f));
     }
   }
+  if (loss == nullptr) return;      // training steps that do not report the loss
   l = wave_sum(l);
   if ((threadIdx.x & 63) == 0) atomicAdd(loss, l / (float)M);
 }
@@ -1870,6 +2012,7 @@ __global__ __launch_bounds__(256) void softmax_xent_bf16_kernel(const float* __r
       if (k == yi) l = -logf(fmaxf(pk, 1e-30f));
     }
   }
+  if (loss == nullptr) return;      // training steps that do not report the loss
   l = wave_sum(l);
   if ((threadIdx.x & 63) == 0) atomicAdd(loss, l / (float)M);
 }
@@ -2045,9 +2188,8 @@ template <int BM, int BN, int EPI>
 static void launch_w64(const float* A, const float* B, float* out, const float* bias, const float* Y, float* bws,
                        int M, int N, int K, int ta, int tb, int act, float beta_c, int splitk, hipStream_t stream) {
   const dim3 grid(cdiv(N, BN), cdiv(M, BM), splitk), blk(GW_T);
-  const int kchunk = ((K + splitk - 1) / splitk + 31) / 32 * 32;
   const bool aligned = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0;
-  const bool full = g_gemm_full && aligned && M % BM == 0 && N % BN == 0 && K % 32 == 0 && kchunk * splitk == K;
+  const bool full = g_gemm_full && aligned && M % 4 == 0 && N % 4 == 0 && K % 4 == 0;
 #define GW_L(TA_, TB_, F_)                                                                                     \
   hipLaunchKernelGGL((gemm_w64_kernel<TA_, TB_, BM, BN, EPI, F_>), grid, blk, 0, stream, A, B, out, bias, Y, bws, M, \
                      N, K, act, beta_c)
@@ -2061,8 +2203,24 @@ static void launch_w64(const float* A, const float* B, float* out, const float* 
 #undef GW_L
 }
 
+// M, N, K % 4 == 0, aligned operands: gemm_w64_kernel's FULL pipeline
+static bool w64_full_ok(const float* A, const float* B, int M, int N, int K, int splitk) {
+  (void)splitk;
+  // partial edge tiles are fine (masked loads, checked epilogue) but a grid of
+  // mostly-empty tiles is not: whole 128 x 64 rows / columns of work or more
+  return g_gemm_full && ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0 &&
+         M % 4 == 0 && N % 4 == 0 && K % 4 == 0 && M >= 128 && N >= 64;
+}
+
 static void launch_gemm(const float* A, const float* B, float* out, const float* bias, int M, int N, int K, int ta,
                         int tb, int act, float beta_c, int splitk, hipStream_t stream) {
+  // default: the FULL 64 x 64-wave-tile pipeline on 128 x 64 blocks whenever the shape
+  // allows it (8192 x 512 x 512: 50 vs 59 us for gemm64_kernel; same fmaf chain per
+  // element, so bit-identical results)
+  if (g_gemm_tile == 0 && w64_full_ok(A, B, M, N, K, splitk)) {
+    launch_w64<128, 64, 0>(A, B, out, bias, nullptr, nullptr, M, N, K, ta, tb, act, beta_c, splitk, stream);
+    return;
+  }
   if (g_gemm_tile == 1 || g_gemm_tile == 2) {
     if (g_gemm_tile == 1) launch_w64<128, 128, 0>(A, B, out, bias, nullptr, nullptr, M, N, K, ta, tb, act, beta_c, splitk, stream);
     else launch_w64<128, 64, 0>(A, B, out, bias, nullptr, nullptr, M, N, K, ta, tb, act, beta_c, splitk, stream);
@@ -2123,6 +2281,55 @@ H2OMX_API int h2omx_gemm_thin_k(const float* A, const float* B, float* C, int64_
   if (K < 1 || K > 8) return kBadArg;
   const int64_t blocks = std::min<int64_t>(cdiv(M * N, 256), 8192);
   hipLaunchKernelGGL(gemm_thin_k_kernel, dim3(blocks), dim3(256), 0, stream, A, B, C, M, N, K, act_y, act);
+  return launch_status();
+}
+
+// output-layer weight gradient (C <= 8 classes): out[C * N + C] = [dW (dZ^T H) | db
+// (column sums of dZ)] - the layer's contiguous gradient span.  ws >= splits * (C * N + C).
+H2OMX_API int h2omx_out_wgrad(const float* dZ, const float* H, float* out, float* ws, int M, int N, int C,
+                              int splits, hipStream_t stream) {
+  if (C < 1 || C > OUT_C || N % 4 || splits < 1 || !ws || (reinterpret_cast<uintptr_t>(H) & 15)) return kBadArg;
+  const dim3 grid(cdiv(N, 256), splits);
+#define OW_L(C_) hipLaunchKernelGGL(out_wgrad_kernel<C_>, grid, dim3(256), 0, stream, dZ, H, ws, M, N)
+  switch (C) {
+    case 1: OW_L(1); break;
+    case 2: OW_L(2); break;
+    case 3: OW_L(3); break;
+    case 4: OW_L(4); break;
+    case 5: OW_L(5); break;
+    case 6: OW_L(6); break;
+    case 7: OW_L(7); break;
+    default: OW_L(8); break;
+  }
+#undef OW_L
+  // fold: only the reducer's second job (64 columns x 4 slice phases per block, two
+  // loads in flight) - its per-element serial loop would chain `splits` loads
+  const int T = C * N + C;
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(cdiv(T, 64)), dim3(256), 0, stream, ws, splits, 0, 0, out,
+                     nullptr, 0, 0.0f, 0, ws, splits, T, out);
+  return launch_status();
+}
+
+// dZ_prev = (dZ [M][C] W [C][N]) * act'(Y), column partial sums -> ws[splits][N]
+H2OMX_API int h2omx_thin_dact(const float* dZ, const float* W, const float* Y, float* out, float* ws, int M, int N,
+                              int C, int splits, int act, hipStream_t stream) {
+  if (C < 1 || C > OUT_C || N % 4 || splits < 1 || !ws ||
+      ((reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(Y) | reinterpret_cast<uintptr_t>(out) |
+        reinterpret_cast<uintptr_t>(ws)) & 15))
+    return kBadArg;
+  const dim3 grid(cdiv(N, 256), splits);
+#define TD_L(C_) hipLaunchKernelGGL(thin_dact_kernel<C_>, grid, dim3(256), 0, stream, dZ, W, Y, out, ws, M, N, act)
+  switch (C) {
+    case 1: TD_L(1); break;
+    case 2: TD_L(2); break;
+    case 3: TD_L(3); break;
+    case 4: TD_L(4); break;
+    case 5: TD_L(5); break;
+    case 6: TD_L(6); break;
+    case 7: TD_L(7); break;
+    default: TD_L(8); break;
+  }
+#undef TD_L
   return launch_status();
 }
 

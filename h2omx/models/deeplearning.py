@@ -24,6 +24,7 @@ standardized response) and autoencoders with ``anomaly()``.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -291,6 +292,8 @@ class _DLTrainer:
         self.since_sync = 0
         self.perm = None
         self.spi = None      # steps per iteration (model averaging)
+        self.graph = None
+        self.idx_buf = None
         self._t0 = None
         if self.avg:
             t = int(p_.get("train_samples_per_iteration", -2))
@@ -313,14 +316,49 @@ class _DLTrainer:
             return self.world * self.M
         return self.world * self.M * (self.spi or self.steps_per_epoch)
 
+    def graph_eligible(self) -> bool:
+        """the whole update replays as one HIP graph: device data, ADADELTA, no
+        dropout / L1 / max_w2 / per-step collectives (host-side state per step)"""
+        return (self.X.is_cuda and self.adaptive and self.drop_in == 0 and not any(self.hd) and self.l1 == 0
+                and not math.isfinite(float(self.p["max_w2"])) and not self.sync_grad
+                and os.environ.get("H2OMX_DL_GRAPH", "1") == "1")
+
     def step(self) -> None:
-        p_, net, M = self.p, self.net, self.M
+        p_, M = self.p, self.M
         e_pos = self.n_steps % self.steps_per_epoch
         n = self.X.shape[0]
         if e_pos == 0:
             self.perm = (torch.randperm(n, generator=self.gen).to(self.X.device) if p_["shuffle_training_data"]
                          else torch.arange(n, device=self.X.device))
         idx = self.perm[e_pos * M:(e_pos + 1) * M]
+        # small mini-batches are launch-bound (~25 kernels of a few us): after one eager
+        # step (workspaces allocated) the update is captured once and replayed with the
+        # batch's row ids copied into a fixed index buffer
+        if self.graph is not None:
+            self.idx_buf.copy_(idx)
+            self.graph.replay()
+        elif self.n_steps >= 1 and self.graph_eligible():
+            self.idx_buf = idx.clone()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._body(self.idx_buf)
+            self.graph = g
+            g.replay()
+        else:
+            self._body(idx)
+        self.samples += M * self.world
+        self.n_steps += 1
+        self.since_sync += 1
+        if not self.avg:
+            return
+        if self.spi is None:
+            self._autotune()
+        elif self.since_sync >= self.spi:
+            self.sync()
+
+    def _body(self, idx) -> None:
+        """one mini-batch update (forward, loss gradient, backward, optimizer)"""
+        p_, net, M = self.p, self.net, self.M
         xb = self.X.index_select(0, idx)
         mlp = self.mlp
         if mlp is not None:
@@ -333,7 +371,7 @@ class _DLTrainer:
         if self.auto:
             dZ = (Z - xb) * (2.0 / Z.numel())
         elif self.cls:
-            dZ, _ = D.softmax_xent(Z, self.Y.index_select(0, idx))
+            dZ, _ = D.softmax_xent(Z, self.Y.index_select(0, idx), with_loss=False)
         else:
             r = Z[:, 0] - self.Y.index_select(0, idx)
             if self.loss_kind == "absolute":
@@ -349,13 +387,13 @@ class _DLTrainer:
             mlp.backward(dZ, xbt, comm, self.world)
         else:
             self.backward(net, Hs, aux, dZ, self.act, comm, self.world)
-        self.samples += M * self.world
         if self.adaptive:
             D.adadelta_(net.flat, net.grad, self.Eg2, self.Edx2, float(p_["rho"]), float(p_["epsilon"]), self.l2)
         else:
             # H2O's rate is per row: a mean-gradient step over M rows takes M of them
-            lr = M * float(p_["rate"]) / (1.0 + float(p_["rate_annealing"]) * self.samples)
-            ramp = min(1.0, self.samples / max(float(p_["momentum_ramp"]), 1.0))
+            done = self.samples + M * self.world
+            lr = M * float(p_["rate"]) / (1.0 + float(p_["rate_annealing"]) * done)
+            ramp = min(1.0, done / max(float(p_["momentum_ramp"]), 1.0))
             mom = float(p_["momentum_start"]) + (float(p_["momentum_stable"]) - float(p_["momentum_start"])) * ramp
             D.sgd_momentum_(net.flat, net.grad, self.V, lr, mom, self.l2)
         if self.l1 > 0:
@@ -364,14 +402,6 @@ class _DLTrainer:
             H2ODeepLearningEstimator._clip_w2(net, float(p_["max_w2"]))
         if mlp is not None:
             mlp.refresh()
-        self.n_steps += 1
-        self.since_sync += 1
-        if not self.avg:
-            return
-        if self.spi is None:
-            self._autotune()
-        elif self.since_sync >= self.spi:
-            self.sync()
 
     def _autotune(self) -> None:
         """train_samples_per_iteration = -2: after PROBE_STEPS local steps, time one
@@ -638,6 +668,8 @@ class H2ODeepLearningEstimator(ModelBuilder):
             W = net.W(i)
             if bpart is not None:
                 D.wgrad_bias(dZ, Hin, net.W(i, net.grad), net.b(i, net.grad), bpart)   # dW = dZ^T H, db
+            elif i == L - 1 and D.out_layer_ok(dZ, Hin):
+                D.out_wgrad(dZ, Hin, net.W(i, net.grad), net.b(i, net.grad))          # few classes: one pass
             else:
                 D.gemm(dZ, Hin, ta=True, out=net.W(i, net.grad))          # dW = dZ^T H
                 D.bias_grad(dZ, out=net.b(i, net.grad))
@@ -647,8 +679,15 @@ class H2ODeepLearningEstimator(ModelBuilder):
                 handles.append(comm.all_reduce_async(net.grad[a:b]))
             if i == 0:
                 break
-            dH = D.gemm(dZ, W)                                            # [M][in]
             arg, mask = aux[i - 1]
+            if act in (1, 2) and mask is None and i == L - 1 and D.out_layer_ok(dZ, Hs[i]):
+                dZ, bpart = D.thin_dact(dZ, W, Hs[i], act)
+                continue
+            if act in (1, 2) and mask is None and D.dact_ok(dZ, W):
+                # dZ_prev = (dZ W) * act'(H) and its bias-gradient slices in the GEMM epilogue
+                dZ, bpart = D.gemm_dact(dZ.contiguous(), W, Hs[i], act)
+                continue
+            dH = D.gemm(dZ, W)                                            # [M][in]
             if mask is not None:
                 dH = dH * mask
             if act == 3:

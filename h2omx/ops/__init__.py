@@ -77,6 +77,8 @@ DENSE_SIGS = {
     "h2omx_gemm_thin_k": "PPPLIIPIS",
     "h2omx_act_backward_bias": "PPPIIIIS",
     "h2omx_gemm_dact": "PPPPPIIIIIPS",
+    "h2omx_out_wgrad": "PPPPIIIIS",
+    "h2omx_thin_dact": "PPPPPIIIIIS",
     "h2omx_gemm_wgrad_bias": "PPPIIIIPPIIPS",
     "h2omx_bias_grad": "PPIIPIS",
     "h2omx_softmax_xent": "PPPPIIS",

@@ -241,13 +241,18 @@ ACTS = {"linear": 0, "none": 0, "rectifier": 1, "relu": 1, "tanh": 2}  # maxout:
 
 
 _WS: dict = {}
+_WS_RETIRED: list = []
 
 
 def _workspace(dev, numel: int, slot: int = 0) -> torch.Tensor:
-    """Per-device scratch for split-K partials (stream-ordered reuse)."""
+    """Per-device scratch for split-K partials (stream-ordered reuse).  A grown
+    workspace keeps its predecessor alive: a captured HIP graph (DL training
+    step) may still hold the old pointer."""
     key = (str(dev), slot)
     w = _WS.get(key)
     if w is None or w.numel() < numel:
+        if w is not None:
+            _WS_RETIRED.append(w)
         w = torch.empty((numel,), dtype=torch.float32, device=dev)
         _WS[key] = w
     return w
@@ -299,8 +304,64 @@ def set_gemm_full(on: int) -> None:
     check(dense_lib().h2omx_gemm_set_full(int(on)), "gemm_set_full")
 
 
+def _row_splits(M: int, N: int) -> int:
+    # 256-column blocks x row slices of >= 64 rows: ~512 workgroups
+    return max(1, min(256, M // 64, 512 // max(1, -(-N // 256))))
+
+
+def out_layer_ok(dZ: torch.Tensor, H: torch.Tensor) -> bool:
+    """few-class output layer (C <= 8) over a float4-aligned hidden width:
+    streaming weight-gradient / activation-backward kernels instead of GEMMs"""
+    return dZ.shape[1] <= 8 and H.shape[1] % 4 == 0 and H.is_contiguous()
+
+
+def out_wgrad(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Tensor) -> None:
+    """dW [C][N] = dZ^T H and db = column sums of dZ for C <= 8 classes (one
+    streaming pass over H, fixed-order split reduce)."""
+    M, C = dZ.shape
+    N = H.shape[1]
+    _dev(dZ, "out_wgrad")
+    S = _row_splits(M, N)
+    T = C * N + C
+    ws = _workspace(dZ.device, S * T)
+    contiguous = (dW.is_contiguous() and db.is_contiguous()
+                  and db.data_ptr() == dW.data_ptr() + dW.numel() * dW.element_size())
+    out = dW.view(-1) if contiguous else torch.empty((T,), dtype=torch.float32, device=dZ.device)
+    if contiguous:
+        # the layer's [W | b] gradient span (models/deeplearning.py _Net): write it in place
+        out = torch.as_strided(dW, (T,), (1,))
+    check(dense_lib().h2omx_out_wgrad(P(dZ.contiguous()), P(H), P(out), P(ws), M, N, C, S, stream(dZ.device)),
+          "out_wgrad")
+    if not contiguous:
+        dW.copy_(out[: C * N].view(C, N))
+        db.copy_(out[C * N:])
+
+
+def thin_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int):
+    """dZ_prev = (dZ [M][C] W [C][N]) * act'(Y) and its per-slice column sums
+    (bias-gradient partials), one pass; returns (dZ_prev, (ws, splits))."""
+    M, C = dZ.shape
+    N = W.shape[1]
+    _dev(dZ, "thin_dact")
+    S = _row_splits(M, N)
+    ws = _workspace(dZ.device, S * N, slot=1)
+    out = torch.empty((M, N), dtype=torch.float32, device=dZ.device)
+    check(dense_lib().h2omx_thin_dact(P(dZ.contiguous()), P(W.contiguous()), P(Y), P(out), P(ws), M, N, C, S,
+                                      int(act), stream(dZ.device)), "thin_dact")
+    return out, (ws, S)
+
+
+def dact_ok(dZ: torch.Tensor, W: torch.Tensor) -> bool:
+    """gemm_dact (dZ [M][K] x W [K][N]) pays off when its 128 x 64 blocks fill the
+    GPU without split-K (small mini-batches keep the split-K GEMM +
+    act_backward_bias pair)"""
+    M, K = dZ.shape
+    N = W.shape[1]
+    return M % 128 == 0 and N % 64 == 0 and K % 4 == 0 and (M // 128) * (N // 64) >= 128
+
+
 def gemm_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int, out: torch.Tensor | None = None,
-              tile: int = 1):
+              tile: int = 2):
     """Back-propagation through a Rectifier / Tanh layer in one GEMM:
     dZ_prev = (dZ[M][K] W[K][N]) * act'(Y[M][N]) (Y = that layer's output), plus
     the column sums of dZ_prev per 128-row block (its bias gradient before the
@@ -322,11 +383,16 @@ def gemm_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int, out:
 
 
 def _splitk(M: int, N: int, K: int) -> int:
-    """split-K when the output has too few 128x128 tiles to fill 256 CUs
-    (weight gradients: [out][in] outputs with K = batch rows)"""
+    """split-K when the output has too few tiles to fill 256 CUs: weight
+    gradients ([out][in] outputs, K = batch rows) and every GEMM of a small
+    mini-batch (256 x 512 x 512: 32 64x64 tiles of 16 serial K-steps each ->
+    8 K-splits of 2 steps, ~4x faster)"""
     tiles = -(-M // 128) * -(-N // 128)
     if tiles < 128 and K >= 1024:
         return max(1, min(64, 256 // tiles, K // 256))
+    tiles64 = -(-M // 64) * -(-N // 64)
+    if tiles64 < 128 and K >= 256:
+        return max(1, min(16, 256 // tiles64, K // 64))
     return 1
 
 
@@ -389,13 +455,14 @@ def bias_grad(dY: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor
     return db
 
 
-def softmax_xent(Z: torch.Tensor, y: torch.Tensor):
-    """Z [M][K] logits, y int32 class ids -> (dZ = (softmax - onehot) / M, mean loss)."""
+def softmax_xent(Z: torch.Tensor, y: torch.Tensor, with_loss: bool = True):
+    """Z [M][K] logits, y int32 class ids -> (dZ = (softmax - onehot) / M, mean
+    loss); ``with_loss=False`` skips the loss (None) and its zero-fill launch."""
     M, K = Z.shape
     _dev(Z, "softmax_xent")
     y = y.to(torch.int32).contiguous()
     dZ = torch.empty_like(Z)
-    loss = torch.zeros((1,), dtype=torch.float32, device=Z.device)
+    loss = torch.zeros((1,), dtype=torch.float32, device=Z.device) if with_loss else None
     check(dense_lib().h2omx_softmax_xent(P(Z), P(y), P(dZ), P(loss), M, K, stream(Z.device)), "softmax_xent")
     return dZ, loss
 

@@ -163,6 +163,37 @@ def act_backward_bias(Y: torch.Tensor, dY: torch.Tensor, act: int):
     return dY, (dY.sum(0)[None, :], 1)
 
 
+def out_layer_ok(dZ: torch.Tensor, H: torch.Tensor) -> bool:
+    return False
+
+
+def out_wgrad(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Tensor) -> None:
+    dW.copy_(dZ.T @ H)
+    db.copy_(dZ.sum(0))
+
+
+def thin_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int):
+    C = dZ @ W
+    act_backward(Y, C, act)
+    return C, (C.sum(0)[None, :], 1)
+
+
+def dact_ok(dZ: torch.Tensor, W: torch.Tensor) -> bool:
+    """the CPU path keeps the unfused GEMM + act_backward_bias pair"""
+    return False
+
+
+def gemm_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int, out: torch.Tensor | None = None,
+              tile: int = 2):
+    """Reference of ops.dense.gemm_dact: (dZ W) * act'(Y) and its column sums."""
+    C = dZ @ W
+    act_backward(Y, C, act)
+    if out is not None:
+        out.copy_(C)
+        C = out
+    return C, (C.sum(0)[None, :], 1)
+
+
 def wgrad_bias(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Tensor, bpart) -> None:
     dW.copy_(dZ.T @ H)
     db.copy_(bpart[0].sum(0))
@@ -176,7 +207,7 @@ def bias_grad(dY: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor
     return r
 
 
-def softmax_xent(Z: torch.Tensor, y: torch.Tensor):
+def softmax_xent(Z: torch.Tensor, y: torch.Tensor, with_loss: bool = True):
     M, K = Z.shape
     pr = torch.softmax(Z, 1)
     oh = torch.nn.functional.one_hot(y.long(), K).float()

@@ -5,7 +5,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r3s5
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
-  tests/test_dense_gpu.py -k "gemm" > $O/pytest_gemm.log 2>&1 || exit $?
+  tests/test_dense_gpu.py tests/test_estimators_gpu.py -k "gemm or deeplearning" > $O/pytest_gemm.log 2>&1 || exit $?
 timeout -k 10 200 python scripts/r3/gemm_bench.py > $O/gemm_bench.jsonl 2> $O/gemm_bench.err || exit $?
 i=0
 for cfg in "1 0" "1 1" "2 1"; do

@@ -182,7 +182,8 @@ def test_act_backward_bias_and_wgrad(cuda_dev, M, out, inp, act):
 
 @pytest.mark.parametrize("M,N,K,ta,tb", [(8192, 512, 512, False, True), (8192, 512, 512, False, False),
                                          (512, 512, 8192, True, False), (1000, 300, 77, False, False),
-                                         (130, 70, 5000, True, True)])
+                                         (130, 70, 5000, True, True), (8192, 512, 200, False, True),
+                                         (256, 512, 512, False, True), (512, 200, 8192, True, False)])
 def test_gemm_64_tiles_bit_identical_to_128(cuda_dev, M, N, K, ta, tb):
     """The 64 x 64-tile kernel keeps each element's k-ordered fmaf chain (and
     the split-K chunking) of the 128 x 128 one: bit-identical outputs."""
@@ -194,11 +195,12 @@ def test_gemm_64_tiles_bit_identical_to_128(cuda_dev, M, N, K, ta, tb):
     bias = None if ta else torch.randn(N, device=cuda_dev)
     out = {}
     try:
-        for tile in (128, 64, 1, 2):     # 1 / 2: 64 x 64 wave tiles on 128 x 128 / 128 x 64 blocks
+        for tile in (128, 64, 1, 2, 0):  # 1 / 2: 64 x 64 wave tiles on 128 x 128 / 128 x 64 blocks; 0 = auto
             OD.set_gemm_tile(tile)
             out[tile] = D.gemm(A, B, bias, 0 if ta else 1, ta, tb)
     finally:
         OD.set_gemm_tile(0)
+    assert torch.equal(out[0], out[128])
     assert torch.equal(out[64], out[128])
     assert torch.equal(out[1], out[128]) and torch.equal(out[2], out[128])
     ref = (A.T if ta else A).double() @ (B.T if tb else B).double()
@@ -309,3 +311,25 @@ def test_gemm_dact_matches_reference(cuda_dev, M, K, N, act, tile):
         OD.set_gemm_tile(0)
     dZ2, _ = D.act_backward_bias(Y, dH32, act)
     assert torch.equal(out, dZ2)
+
+
+@pytest.mark.parametrize("M,N,C,act", [(8192, 512, 2, 1), (1000, 300, 3, 2), (333, 64, 8, 1), (8192, 200, 1, 2)])
+def test_output_layer_streaming_kernels(cuda_dev, M, N, C, act):
+    """few-class output layer: dW = dZ^T H, db = sum dZ (out_wgrad) and
+    dZ_prev = (dZ W) * act'(H) with its bias partials (thin_dact), fp64 reference"""
+    from h2omx.ops import dense as OD
+
+    torch.manual_seed(8)
+    dZ = torch.randn((M, C), device=cuda_dev)
+    H = torch.randn((M, N), device=cuda_dev)
+    H = H.clamp_min(0) if act == 1 else torch.tanh(H)
+    W = torch.randn((C, N), device=cuda_dev)
+    dW = torch.empty((C, N), device=cuda_dev)
+    db = torch.empty((C,), device=cuda_dev)
+    OD.out_wgrad(dZ, H, dW, db)
+    assert torch.allclose(dW.double(), dZ.double().T @ H.double(), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(db.double(), dZ.double().sum(0), atol=1e-3)
+    out, (ws, S) = OD.thin_dact(dZ, W, H, act)
+    ref = (dZ.double() @ W.double()) * ((H > 0).double() if act == 1 else (1 - H.double() ** 2))
+    assert torch.allclose(out.double(), ref, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(ws[: S * N].view(S, N).double().sum(0), ref.sum(0), atol=1e-3)

@@ -130,6 +130,21 @@ def test_deeplearning_gpu(cuda_dev):
     assert np.isfinite(r.training_metrics["MSE"])
 
 
+@pytest.mark.parametrize("act,precision", [("Rectifier", "fp32"), ("Maxout", "fp32"), ("Tanh", "bf16")])
+def test_deeplearning_graph_replay_matches_eager(cuda_dev, monkeypatch, act, precision):
+    """The HIP-graph replay of the update step (models/deeplearning.py _DLTrainer)
+    runs the same kernels in the same order as the eager step: identical weights."""
+    df = _binary_df(n=30000)
+    fr = Frame.from_pandas(df, device=cuda_dev)
+    kw = dict(hidden=[64, 32], epochs=2, seed=4, activation=act, precision=precision)
+    out = {}
+    for g in ("0", "1"):
+        monkeypatch.setenv("H2OMX_DL_GRAPH", g)
+        out[g] = H2ODeepLearningEstimator(**kw).train(y="y", training_frame=fr)
+    assert torch.equal(out["0"].net.flat, out["1"].net.flat)
+    assert out["1"].training_metrics["AUC"] == out["0"].training_metrics["AUC"]
+
+
 @pytest.mark.parametrize("cls", [H2OGradientBoostingEstimator, H2OXGBoostEstimator, H2ORandomForestEstimator])
 def test_tree_estimators_gpu(cuda_dev, cls):
     df = _binary_df()
