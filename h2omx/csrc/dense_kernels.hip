@@ -746,6 +746,34 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
   out[j] = acc;
 }
 
+// Many slabs of a narrow width (per-wave K-Means slabs: ~1000 x 1020): one
+// 1024-thread block per 32 columns, 32 slab groups of strided slabs with 4
+// loads in flight per thread, folded through LDS in fixed order (deterministic)
+__global__ __launch_bounds__(1024) void slab_sum_wide_kernel(const float* __restrict__ slab, int n_slabs, int width,
+                                                             double* __restrict__ out) {
+  __shared__ double red[32][33];
+  const int c = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int j = blockIdx.x * 32 + c;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (j < width) {
+    int s = grp;
+    for (; s + 96 < n_slabs; s += 128) {
+      a0 += slab[(int64_t)s * width + j];
+      a1 += slab[(int64_t)(s + 32) * width + j];
+      a2 += slab[(int64_t)(s + 64) * width + j];
+      a3 += slab[(int64_t)(s + 96) * width + j];
+    }
+    for (; s < n_slabs; s += 32) a0 += slab[(int64_t)s * width + j];
+  }
+  red[grp][c] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (grp == 0 && j < width) {
+    double acc = 0.0;
+    for (int g = 0; g < 32; ++g) acc += red[g][c];
+    out[j] = acc;
+  }
+}
+
 // ===========================================================================
 // MLP: tiled fp32-MFMA GEMM with fused bias + activation
 // C[M][N] = act(op(A)[M][K] op(B)[K][N] + bias[N]);  row-major storage.
@@ -2098,7 +2126,10 @@ H2OMX_API int h2omx_slab_reduce_upper(const float* slab, int n_slabs, int width,
 }
 
 H2OMX_API int h2omx_slab_sum(const float* slab, int n_slabs, int width, double* out, hipStream_t stream) {
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(cdiv(width, 256)), dim3(256), 0, stream, slab, n_slabs, width, out);
+  if (n_slabs >= 64 && width < 64 * 1024)   // narrow and deep: column x slab-group parallel
+    hipLaunchKernelGGL(slab_sum_wide_kernel, dim3(cdiv(width, 32)), dim3(1024), 0, stream, slab, n_slabs, width, out);
+  else
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(cdiv(width, 256)), dim3(256), 0, stream, slab, n_slabs, width, out);
   return launch_status();
 }
 

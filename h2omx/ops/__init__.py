@@ -64,6 +64,7 @@ DENSE_SIGS = {
     "h2omx_slab_reduce16": "PIIPS",
     "h2omx_slab_sum": "PIIPS",
     "h2omx_kmeans": "PLLIPPIIPPS",
+    "h2omx_kmeans_wave": "PLLIPPPIIIIPPS",
     "h2omx_glm_wz": "PLPPPPPPPPIS",
     "h2omx_glm_aug": "PILPPPPS",
     "h2omx_kmeans_stage": "PLILLPS",

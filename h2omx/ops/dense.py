@@ -28,6 +28,10 @@ GLM_UNITS = int(os.environ.get("H2OMX_GLM_UNITS", "2048"))
 GLM_UNIT_MIN_ROWS = 512
 SLAB_SPLIT = 32          # dense_kernels.hip slab_reduce16_kernel
 KM_WGS = int(os.environ.get("H2OMX_KM_WGS", "1024"))
+# K-Means Lloyd pass on the wave-unit kernel (k <= 32, d <= 128 / 64); 0: the
+# workgroup-tile kernel.  KM_WAVE_CUS: CUs the wave kernel's grid is sized for
+KM_WAVE = os.environ.get("H2OMX_KM_WAVE", "1") == "1"
+KM_WAVE_CUS = int(os.environ.get("H2OMX_KM_WAVE_CUS", "256"))
 
 FAMILIES = {"gaussian": 0, "binomial": 1, "poisson": 2, "gamma": 3, "tweedie": 4, "multinomial": 5,
             "quasibinomial": 6, "fractionalbinomial": 6, "negativebinomial": 7}
@@ -178,17 +182,36 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor):
     Xc = X.contiguous()
     Cc = C.float().contiguous()
     cn = (Cc.double() ** 2).sum(1).float()
-    n_wg = max(1, min(KM_WGS, math.ceil(n / 4096)))
     width = k * d + 2 * k
-    slab = torch.empty((n_wg * width,), dtype=torch.float32, device=dev)
     out = torch.empty((width,), dtype=torch.float64, device=dev)
     assign = torch.empty((n,), dtype=torch.int32, device=dev)
     st = stream(dev)
-    rc = lib.h2omx_kmeans(P(Xc), Xc.stride(0), n, d, P(Cc), P(cn), k, n_wg, P(assign), P(slab), st)
-    if rc == KBADARG:
-        return _kmeans_large(Xc, Cc)
-    check(rc, "kmeans")
-    check(lib.h2omx_slab_sum(P(slab), n_wg, width, P(out), st), "slab_sum")
+    kp = -(-k // 4) * 4 if k <= 16 else -(-k // 8) * 8
+    dp = -(-d // 16) * 16
+    if KM_WAVE and k <= 32 and (dp <= 128 if kp <= 16 else dp <= 64):
+        # wave-unit kernel (csrc/dense_kernels.hip kmeans_wave_kernel): zero-padded
+        # centroids [kp][dp], +inf norms for the padding clusters
+        Cp = torch.zeros((kp, dp), dtype=torch.float32, device=dev)
+        Cp[:k, :d] = Cc
+        cnp = torch.full((kp,), float("inf"), dtype=torch.float32, device=dev)
+        cnp[:k] = cn
+        CT = Cp.t().contiguous()   # [dp][kp]: one feature's centroid values per scalar load
+        # one workgroup (4 waves) per CU at dp = 128 (LDS tiles 4 x dp x 65 floats);
+        # smaller tiles fit more per CU.  >= ~4 chunks of 64 rows per wave
+        per_cu = max(1, (160 * 1024) // ((4 * dp * 65 + dp * kp) * 4))
+        n_wg = max(1, min(KM_WAVE_CUS * per_cu, math.ceil(n / (64 * 4 * 4))))
+        slab = torch.empty((4 * n_wg * width,), dtype=torch.float32, device=dev)
+        check(lib.h2omx_kmeans_wave(P(Xc), Xc.stride(0), n, d, P(Cp), P(CT), P(cnp), k, kp, dp, n_wg, P(assign), P(slab),
+                                    st), "kmeans_wave")
+        check(lib.h2omx_slab_sum(P(slab), 4 * n_wg, width, P(out), st), "slab_sum")
+    else:
+        n_wg = max(1, min(KM_WGS, math.ceil(n / 4096)))
+        slab = torch.empty((n_wg * width,), dtype=torch.float32, device=dev)
+        rc = lib.h2omx_kmeans(P(Xc), Xc.stride(0), n, d, P(Cc), P(cn), k, n_wg, P(assign), P(slab), st)
+        if rc == KBADARG:
+            return _kmeans_large(Xc, Cc)
+        check(rc, "kmeans")
+        check(lib.h2omx_slab_sum(P(slab), n_wg, width, P(out), st), "slab_sum")
     o = out.cpu().numpy()
     return assign, o[: k * d].reshape(k, d), o[k * d: k * d + k], o[k * d + k:]
 

@@ -66,6 +66,36 @@ def test_kmeans_step_matches_reference(cuda_dev, d, k):
         np.testing.assert_allclose(eg, er, rtol=1e-3)
 
 
+@pytest.mark.parametrize("d,k", [(4, 3), (33, 16), (64, 17), (64, 32), (100, 10), (128, 16), (96, 5)])
+def test_kmeans_wave_kernel_matches_reference(cuda_dev, monkeypatch, d, k):
+    """Wave-unit Lloyd pass (csrc/kmeans_wave.hip) against the fp64 NumPy oracle
+    and the workgroup-tile kernel: tail chunk (n % 64 != 0), NA cells, empty clusters."""
+    rng = np.random.default_rng(100 + d + k)
+    n = 40_003
+    X = rng.normal(size=(d, n)).astype(np.float32)
+    X[rng.integers(0, d, 50), rng.integers(0, n, 50)] = np.nan
+    C = rng.normal(size=(k, d)).astype(np.float32)
+    C[-1] += 50.0   # far away: empty cluster
+    Xc = np.nan_to_num(X, nan=0.0)
+    ar, sr, cr, er = D.kmeans_step(torch.from_numpy(Xc), torch.from_numpy(C))
+    outs = {}
+    import h2omx.ops.dense as OD
+
+    for wave in (True, False):
+        monkeypatch.setattr(OD, "KM_WAVE", wave)
+        outs[wave] = D.kmeans_step(torch.from_numpy(X).to(cuda_dev), torch.from_numpy(C).to(cuda_dev))
+    ag, sg, cg, eg = outs[True]
+    agree = (ag.cpu().numpy() == ar.numpy()).mean()
+    assert agree > 0.999
+    assert cg[-1] == 0 and cg.sum() == n
+    if agree == 1.0:
+        np.testing.assert_array_equal(cg, cr)
+        np.testing.assert_allclose(sg, sr, rtol=1e-4, atol=2e-3)
+        np.testing.assert_allclose(eg, er, rtol=1e-4)
+    # same assignment as the tile kernel up to fp32 near-ties
+    assert (outs[False][0].cpu().numpy() == ag.cpu().numpy()).mean() > 0.999
+
+
 @pytest.mark.parametrize("M,N,K,ta,tb,act", [(1000, 512, 200, False, False, 1), (513, 257, 129, False, True, 2),
                                              (200, 512, 1000, True, False, 0), (64, 64, 64, True, True, 1)])
 def test_gemm_matches_torch(cuda_dev, M, N, K, ta, tb, act):

@@ -152,7 +152,8 @@ def test_tree_estimators_gpu(cuda_dev, cls):
     m = cls(**kw).train(y="y", training_frame=Frame.from_pandas(df, device=cuda_dev))
     mc = cls(**kw).train(y="y", training_frame=Frame.from_pandas(df))
     assert abs(m.training_metrics["AUC"] - mc.training_metrics["AUC"]) < 0.01
-    assert m.training_metrics["AUC"] > 0.75
+    # DRF reports out-of-bag training metrics (H2O semantics): lower than in-sample
+    assert m.training_metrics["AUC"] > (0.72 if cls is H2ORandomForestEstimator else 0.75)
     assert "tree" in " ".join(_native.loaded_libraries())
 
 
