@@ -26,14 +26,27 @@ import time
 import uuid
 
 import numpy as np
+import torch
 
 from .frame.frame import DKV, Frame
 from .models import (H2ODeepLearningEstimator, H2OGeneralizedLinearEstimator, H2OGradientBoostingEstimator,
                      H2ORandomForestEstimator, H2OXGBoostEstimator)
+from .frame.frame import ENUM, Vec
 from .models.base import ModelCategory
 from .models.ensemble import H2OStackedEnsembleEstimator
+from .models.target_encoder import H2OTargetEncoderEstimator
 
 ALGOS = ("GLM", "DRF", "GBM", "XGBoost", "DeepLearning", "StackedEnsemble")
+
+# preprocessing=["target_encoding"] (H2O AutoML TargetEncoding step): categorical
+# predictors with at least TE_CARDINALITY levels are replaced by their blended
+# target means (inflection point 5, smoothing 10, no noise; out-of-fold means on
+# the training rows when the run cross-validates) for the algos below.  The
+# threshold / blending values follow H2O's AutoML step; h2o is not importable
+# here, so parity with its encoded values is unpinned.
+TE_CARDINALITY = 25
+TE_ALGOS = ("gbm", "drf", "xgboost")
+TE_FOLD = "__automl_te_fold"
 
 # (algo, id suffix, estimator class, params) in H2O's default training order
 PRESETS = [
@@ -178,12 +191,29 @@ class H2OAutoML:
             return m
 
         self._log("Workflow", f"AutoML build started: {self.project_name}")
-        if self.preprocessing:
-            self._log("Workflow", f"preprocessing {self.preprocessing} not applied (models see the raw columns)")
+        task_mode = self.parallelism == "task" and comm is not None and comm.world_size > 1
+        # (task-parallel runs fit the step on the replicated frame, _train_task_parallel)
+        te = None if task_mode else self._target_encoding(x, y, training_frame, validation_frame, seed, comm)
+        if te is not None:
+            fit_raw = fit
+
+            def fit(name, cls, params):   # noqa: F811 - TE'd algos train on the encoded frames
+                nonlocal x, training_frame, validation_frame
+                if cls.algo not in TE_ALGOS:
+                    return fit_raw(name, cls, params)
+                saved = x, training_frame, validation_frame
+                x, training_frame, validation_frame = te["x"], te["train"], te["valid"]
+                try:
+                    m = fit_raw(name, cls, params)
+                finally:
+                    x, training_frame, validation_frame = saved
+                if m is not None:
+                    m.preprocessors = (te["model"],)
+                return m
         start_models = len(self.models)
         if self.max_models:
             self.max_models = int(self.max_models) + start_models
-        if self.parallelism == "task" and comm is not None and comm.world_size > 1:
+        if task_mode:
             category = self._train_task_parallel(x, y, training_frame, validation_frame, comm, cv, rng, budget, t0,
                                                  start_models)
             training_frame = self._local_frame
@@ -235,6 +265,43 @@ class H2OAutoML:
                 out.append((f"{name[f]}_grid_1_model_{counters[f]}", cls, params))
                 counters[f] += 1
         return out[:cap] if self.max_models else out
+
+    def _target_encoding(self, x, y, frame, valid, seed, comm):
+        """Fit the TargetEncoding preprocessing step (see TE_CARDINALITY) and
+        return the encoded training / validation frames and predictor list,
+        or None when the step is off or finds no high-cardinality predictor."""
+        steps = [str(p).lower().replace("_", "") for p in (self.preprocessing or [])]
+        if "targetencoding" not in steps or y is None:
+            return None
+        xs = list(x) if x else [n for n in frame.names if n != y]
+        cols = [c for c in xs if frame.vec(c).vtype == ENUM and len(frame.vec(c).domain or []) >= TE_CARDINALITY]
+        if not cols:
+            self._log("Preprocessing", "target_encoding: no categorical predictor with >= "
+                                       f"{TE_CARDINALITY} levels, step skipped")
+            return None
+        kfold = self.nfolds > 1
+        fr = frame
+        if kfold:
+            # the same Modulo folds the cross-validated models use (global row index)
+            from .models.tree.engine import global_row_base
+
+            base = global_row_base(frame.nrows, comm)
+            fid = (torch.arange(frame.nrows, device=frame.device) + base) % self.nfolds
+            fr = Frame(list(frame.vecs) + [Vec(TE_FOLD, fid.to(torch.int32), "int")])
+        te_model = H2OTargetEncoderEstimator(
+            model_id=f"TargetEncoder_AutoML_{self.project_name}", blending=True, inflection_point=5.0,
+            smoothing=10.0, noise=0.0, keep_original_categorical_columns=False, seed=seed,
+            data_leakage_handling="KFold" if kfold else "None", fold_column=TE_FOLD if kfold else None,
+        ).train(x=cols, y=y, training_frame=fr, comm=comm)
+        train = te_model.transform(fr, as_training=True)
+        if kfold:
+            train = Frame([v for v in train.vecs if v.name != TE_FOLD])
+        enc = [n for n in train.names if n not in frame.names]
+        x_te = [c for c in xs if c not in cols] + enc
+        self._log("Preprocessing", f"target_encoding: {len(cols)} column(s) encoded for "
+                                   f"{', '.join(TE_ALGOS)}: {', '.join(cols)}")
+        return {"model": te_model, "train": train, "x": x_te,
+                "valid": te_model.transform(valid) if valid is not None else None}
 
     def _train_sequential(self, fit, rng, out_of_budget):
         category = None
@@ -303,6 +370,9 @@ class H2OAutoML:
         local = gather_frame(training_frame, comm)
         valid = gather_frame(validation_frame, comm) if validation_frame is not None else None
         self._local_frame = local
+        seed = self.seed if self.seed is not None and self.seed >= 0 else 42
+        # every rank fits the same encoder on the same replicated rows (comm=None)
+        te = self._target_encoding(x, y, local, valid, seed, None)
         plan = self._plan_models(rng)
         mine = []
         self._log("Workflow", f"task-parallel: {len(plan)} models over {comm.world_size} ranks "
@@ -318,14 +388,19 @@ class H2OAutoML:
                 rt = min(rt, left) if rt else left
             if rt:
                 params = dict(params, max_runtime_secs=rt)
+            use_te = te is not None and cls.algo in TE_ALGOS
             try:
-                m = cls(model_id=mid, **params, **cv).train(x=x, y=y, training_frame=local, validation_frame=valid,
-                                                            comm=None)
+                m = cls(model_id=mid, **params, **cv).train(
+                    x=te["x"] if use_te else x, y=y, training_frame=te["train"] if use_te else local,
+                    validation_frame=te["valid"] if use_te else valid, comm=None)
             except Exception as e:  # noqa: BLE001
                 self._log("ModelTraining", f"{name} failed on rank {comm.rank}: {type(e).__name__}: {e}")
                 continue
             h = m.cross_validation_holdout
-            mine.append((i, {"model_id": m.model_id, "algo": m.algo, "mojo": mojo_bytes(m),
+            blob = mojo_bytes(m)   # the bare model (its encoder is refitted identically on every rank)
+            if use_te:
+                m.preprocessors = (te["model"],)
+            mine.append((i, {"model_id": m.model_id, "algo": m.algo, "mojo": blob,
                              "training_metrics": m.training_metrics, "validation_metrics": m.validation_metrics,
                              "cross_validation_metrics": m.cross_validation_metrics,
                              "holdout": None if h is None else h.detach().cpu().numpy(),
@@ -339,6 +414,8 @@ class H2OAutoML:
                 # trained on another rank: scoring model from its MOJO + the training-side metrics
                 m = GenericModel(pl["mojo"], pl["model_id"])
                 m.algo = pl["algo"]
+                if te is not None and pl["algo"] in TE_ALGOS:
+                    m.preprocessors = (te["model"],)
                 m.training_metrics = pl["training_metrics"]
                 m.validation_metrics = pl["validation_metrics"]
                 m.cross_validation_metrics = pl["cross_validation_metrics"]

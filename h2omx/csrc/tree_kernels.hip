@@ -1888,6 +1888,8 @@ __global__ __launch_bounds__(1024) void split_level_kernel(
 // measured 4.3M LDS bank-conflict cycles per last-level dispatch with the
 // previous [copy][slot] layout).  Each workgroup folds its copies and adds
 // the window with integer global atomics (order-independent: deterministic).
+constexpr int PART_LDS_NODES = 256;   // levels up to this many nodes read their split records from LDS
+
 template <bool PREF, int RPL>
 __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restrict__ codes, int64_t npad,
                                                         int* nid, const PartInfo* __restrict__ part,
@@ -1899,23 +1901,30 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
                                                         const int* __restrict__ ctl_next, int win_max, int R,
                                                         short* __restrict__ slot16, int* nid_out, int all_rows) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lacc[];
+  __shared__ PartInfo ps[PART_LDS_NODES];
   const bool use_lds = leaf_acc != nullptr && win_max > 0;
   // all_rows (final level of the fused-routing pipeline): rows that retired at
   // earlier levels (nid = ~gid) add their sums here too; the LDS window is the
   // whole tree [0, win_max)
   const int base = all_rows ? 0 : ctl_cur[CTL_BASE];
   const int win = use_lds ? (all_rows ? win_max : min(win_max, ctl_cur[CTL_N] + ctl_next[CTL_N])) : 0;
-  if (use_lds) {
+  // the level's split records: LDS-staged when they fit (the node id -> split
+  // record -> split code chain then has one dependent global load, not two)
+  const int n_cur = ctl_cur[CTL_N];
+  const bool rec_lds = n_cur <= PART_LDS_NODES;
+  if (rec_lds)
+    for (int j = threadIdx.x; j < n_cur; j += blockDim.x) ps[j] = part[j];
+  if (use_lds)
     for (int j = threadIdx.x; j < 3 * win * R; j += blockDim.x) lacc[j] = 0ull;
-    __syncthreads();
-  }
+  __syncthreads();
   const int copy = (threadIdx.x & 63) % R;
   float lg = 0, lh = 0, lw = 0;
   if (leaf_acc) { lg = (float)qs[4]; lh = (float)qs[5]; lw = (float)qs[6]; }
-  // RPL rows per lane per step: every node-id load of a step is issued before
-  // the dependent split-record and code loads (the chain nid -> split -> code
-  // is latency bound; a grid that covers all rows in one step keeps the whole
-  // chain in flight once)
+  // RPL rows per lane per step.  All loads of a step are issued before any
+  // row is decided: node ids (+ g / h / w on the last level), then - after the
+  // split records - the RPL split-code gathers together (unconditionally, at
+  // a clamped address), so a step pays the nid -> code chain once, not once
+  // per row behind each row's branches
   const int64_t nq = npad / RPL;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r0 = q * RPL;
@@ -1925,8 +1934,6 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
       const int4 na = *reinterpret_cast<int4*>(nid + r0 + 4 * v);
       nn[4 * v] = na.x; nn[4 * v + 1] = na.y; nn[4 * v + 2] = na.z; nn[4 * v + 3] = na.w;
     }
-    // last level (every row retires): issue the gradient loads together with
-    // the node-id loads instead of after the node -> split -> code chain
     float gv[RPL], hv[RPL], wv8[RPL];
     if (PREF) {
 #pragma unroll
@@ -1943,6 +1950,18 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
         }
       }
     }
+    PartInfo pi[RPL];
+    int bc[RPL];
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      const int n = nn[k] >= 0 ? nn[k] : 0;   // retired rows / padding: any record, unused
+      pi[k] = rec_lds ? ps[n] : part[n];
+    }
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      const int f = (nn[k] >= 0 && pi[k].child >= 0) ? pi[k].feat : 0;
+      bc[k] = codes[(int64_t)f * npad + r0 + k];
+    }
     bool changed = false;
     int sv[RPL];  // next level's build slot per row (-1: retired, or histogram derived from the sibling)
 #pragma unroll
@@ -1950,50 +1969,45 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
       sv[k] = -1;
       const int n = nn[k];
       int leaf = -1;
-      PartInfo pi;
       if (n < 0) {
         if (!all_rows) continue;
         leaf = ~n;  // retired earlier (padding: INT_MIN -> beyond cap, no sums)
-        pi.child = -2;
       } else {
         changed = true;
-        pi = part[n];
-      }
-      if (pi.child == -2) {
-      } else if (pi.child < 0) {
-        leaf = pi.gid;
-      } else {
-        const int b = codes[(int64_t)pi.feat * npad + r0 + k];
-        const int right = (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
-        if (pi.leaf_children) {
-          leaf = pi.child_gid + right;
+        const PartInfo& p = pi[k];
+        if (p.child < 0) {
+          leaf = p.gid;
         } else {
-          nn[k] = pi.child + right;
-          sv[k] = right ? (pi.pad >> 16) : (int)(short)(pi.pad & 0xFFFF);
+          const int b = bc[k];
+          const int right = (b == nbt - 1) ? !p.na_left : (b > p.bin);
+          if (p.leaf_children) {
+            leaf = p.child_gid + right;
+          } else {
+            nn[k] = p.child + right;
+            sv[k] = right ? (p.pad >> 16) : (int)(short)(p.pad & 0xFFFF);
+          }
         }
+        if (leaf >= 0) nn[k] = ~leaf;
       }
-      if (leaf >= 0) {
-        if (n >= 0) nn[k] = ~leaf;
-        if (leaf_acc && leaf < cap) {
-          const float wv = PREF ? wv8[k] : (w ? w[r0 + k] : 1.0f);
-          if (wv != 0.0f) {
-            const float gk = PREF ? gv[k] : g[r0 + k], hk = PREF ? hv[k] : h[r0 + k];
-            const unsigned long long a = (unsigned long long)(long long)__float2int_rn(gk * lg);
-            const unsigned long long b = (unsigned long long)(long long)__float2int_rn(hk * lh);
-            const unsigned long long c = (unsigned long long)(long long)__float2int_rn(wv * lw);
-            const int li = leaf - base;
-            // separate call sites keep LDS atomics as ds_add_u64 (a pointer
-            // selected between LDS and global memory would become FLAT)
-            if (li >= 0 && li < win) {
-              unsigned long long* d = lacc + (3 * li) * R + copy;
-              atomicAdd(d, a);
-              atomicAdd(d + R, b);
-              atomicAdd(d + 2 * R, c);
-            } else {
-              atomicAdd(leaf_acc + 3 * leaf + 0, a);
-              atomicAdd(leaf_acc + 3 * leaf + 1, b);
-              atomicAdd(leaf_acc + 3 * leaf + 2, c);
-            }
+      if (leaf >= 0 && leaf_acc && leaf < cap) {
+        const float wv = PREF ? wv8[k] : (w ? w[r0 + k] : 1.0f);
+        if (wv != 0.0f) {
+          const float gk = PREF ? gv[k] : g[r0 + k], hk = PREF ? hv[k] : h[r0 + k];
+          const unsigned long long a = (unsigned long long)(long long)__float2int_rn(gk * lg);
+          const unsigned long long b = (unsigned long long)(long long)__float2int_rn(hk * lh);
+          const unsigned long long c = (unsigned long long)(long long)__float2int_rn(wv * lw);
+          const int li = leaf - base;
+          // separate call sites keep LDS atomics as ds_add_u64 (a pointer
+          // selected between LDS and global memory would become FLAT)
+          if (li >= 0 && li < win) {
+            unsigned long long* d = lacc + (3 * li) * R + copy;
+            atomicAdd(d, a);
+            atomicAdd(d + R, b);
+            atomicAdd(d + 2 * R, c);
+          } else {
+            atomicAdd(leaf_acc + 3 * leaf + 0, a);
+            atomicAdd(leaf_acc + 3 * leaf + 1, b);
+            atomicAdd(leaf_acc + 3 * leaf + 2, c);
           }
         }
       }
@@ -2014,10 +2028,16 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
   }
   if (use_lds) {
     __syncthreads();
-    for (int s = threadIdx.x; s < 3 * win; s += blockDim.x) {
-      unsigned long long v = 0ull;
-      for (int c = 0; c < R; ++c) v += lacc[s * R + c];
-      if (v && base + s / 3 < cap) atomicAdd(leaf_acc + 3 * base + s, v);
+    // fold the R copies: consecutive threads read consecutive u64 (no bank
+    // conflicts; R divides 64 so a copy group never straddles a wave), the
+    // group of R lanes reduces with cross-lane adds, its first lane adds to
+    // the global sums
+    const int total = 3 * win * R;
+    for (int j0 = 0; j0 < total; j0 += blockDim.x) {
+      const int j = j0 + threadIdx.x;
+      unsigned long long v = (j < total) ? lacc[j] : 0ull;
+      for (int off = 1; off < R; off <<= 1) v += __shfl_xor(v, off, 64);
+      if (j < total && (j % R) == 0 && v && base + (j / R) / 3 < cap) atomicAdd(leaf_acc + 3 * base + j / R, v);
     }
   }
 }
@@ -2948,6 +2968,26 @@ H2OMX_API int h2omx_boost_update(float* F, const float* y, const float* wobs, in
   const GradParams gp = *reinterpret_cast<const GradParams*>(gparams);
   hipLaunchKernelGGL(boost_update_kernel, dim3(stream_grid(npad)), dim3(256), 0, stream, F, y, wobs, n, npad, nid,
                      reinterpret_cast<const TreeNode*>(tree), gp, g, h, wout, stat_max);
+  return launch_status();
+}
+
+// Graph replay: the finished tree -> slot (tree_ctr - 1) mod R of a ring of R
+// tree heaps (tree_begin advanced the counter), so a replayed step needs no
+// host-side snapshot copy per tree (boost.TreeGraph freezes the ring every R trees)
+__global__ __launch_bounds__(256) void tree_archive_kernel(const uint4* __restrict__ src, int n16,
+                                                           uint4* __restrict__ ring, int R,
+                                                           const int* __restrict__ tree_ctr) {
+  const int slot = (int)(((unsigned)(tree_ctr[0] - 1)) % (unsigned)R);
+  uint4* dst = ring + (int64_t)slot * n16;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
+H2OMX_API int h2omx_tree_archive(const void* tree, int64_t bytes, void* ring, int R, const int* tree_ctr,
+                                 hipStream_t stream) {
+  if (bytes % 16 != 0 || R < 1 || tree_ctr == nullptr) return kBadArg;
+  const int n16 = (int)(bytes / 16);
+  hipLaunchKernelGGL(tree_archive_kernel, dim3(grid_for(n16, 256, 64)), dim3(256), 0, stream,
+                     reinterpret_cast<const uint4*>(tree), n16, reinterpret_cast<uint4*>(ring), R, tree_ctr);
   return launch_status();
 }
 

@@ -48,12 +48,18 @@ class Model:
     ``Model.adaptTestForTrain``: unseen levels become NA)."""
 
     algo = "model"
+    # fitted transformers applied to a scored frame before predict_raw (H2O
+    # AutoML preprocessing, e.g. a TargetEncoderModel); empty for plain models
+    preprocessors: tuple = ()
 
     def __init_subclass__(cls, **kw):
         super().__init_subclass__(**kw)
         fn = cls.__dict__.get("predict_raw")
         if fn is not None and not getattr(fn, "_adapts_domains", False):
             def predict_raw(self, frame, *a, _fn=fn, **k):
+                # preprocessing pipeline (AutoML target encoding) before the model
+                for pp in self.preprocessors:
+                    frame = pp.transform(frame)
                 return _fn(self, self.adapt_frame(frame), *a, **k)
 
             predict_raw._adapts_domains = True

@@ -385,7 +385,6 @@ class GpuBooster:
             self._try_capture()
         if self.graph is not None:
             self.graph.replay(t)
-            self.trees_dev.append(b.tree_buf.clone())
             self.t += 1
             return
         fmask = _tree_fmask(self.tp, bm.F, t, self.dev)
@@ -471,6 +470,8 @@ class GpuBooster:
 
     def finish(self) -> TreeEnsemble:
         self.flush()
+        if self.graph is not None:
+            self.graph.freeze()
         torch.cuda.synchronize(self.dev)
         if self.builder.timer.enabled:
             self.ens.timings.update({f"gpu_ms_{k}": v for k, v in self.builder.timer.totals().items()})
@@ -519,6 +520,8 @@ class _GpuView:
     def trees(self, lo: int, hi: int) -> np.ndarray:
         """Tree records of iterations [lo, hi) (K trees each)."""
         K = self.gb.K
+        if self.gb.graph is not None:
+            self.gb.graph.freeze()
         bufs = self.gb.trees_dev[lo * K: hi * K]
         if not bufs:
             return np.zeros((0, self.gb.cap), TREE_NODE_DTYPE)
@@ -562,12 +565,21 @@ class TreeGraph:
     stream capture; not exercised on the one-GPU development box).
     """
 
+    # finished trees go to a device ring of RING slots inside the graph
+    # (tree_archive kernel); trees_dev holds views of the live ring until
+    # freeze() swaps them for views of one ring snapshot (every RING trees, and
+    # whenever the trees are read)
+    RING = 64
+
     def __init__(self, booster):
         self.gb = booster
         self.comm = booster.builder.comm
         self.graphs: list = []
         self.colls: list = []
         self.pool = None
+        self.ring = None
+        self.live: list = []      # (trees_dev index, ring slot) still pointing into the ring
+        self.expect = None        # tree index the device counter holds
 
     def capture(self):
         gb, b = self.gb, self.gb.builder
@@ -576,6 +588,7 @@ class TreeGraph:
         # the graph's own tree buffer: eager steps hand their tree_buf to trees_dev
         # (fresh buffers), which replays must not overwrite
         b.tree_buf = torch.zeros_like(b.tree_buf)
+        self.ring = torch.zeros((self.RING, b.tree_buf.numel()), dtype=torch.uint8, device=dev)
         multi = self.comm is not None and self.comm.world_size > 1
         segmented = multi and os.environ.get("H2OMX_GRAPH_COLLECTIVES", "0") != "1"
         self.pool = torch.cuda.graph_pool_handle()
@@ -599,6 +612,9 @@ class TreeGraph:
                 try:
                     gb._body_k1(gb.t, fresh=False)
                     gb._update(apply=True, next_tree=gb.t + 1, k=0)
+                    ops.check(gb.lib.h2omx_tree_archive(ops.P(b.tree_buf), b.tree_buf.numel(), ops.P(self.ring),
+                                                        self.RING, ops.P(b.tree_ctr), ops.stream(dev)),
+                              "tree_archive")
                 finally:
                     b.comm = self.comm
                     self._open.capture_end()
@@ -622,12 +638,27 @@ class TreeGraph:
 
     def replay(self, t: int):
         """Grow tree ``t`` (and update margins / gradients for tree t + 1)."""
-        self.gb.builder.tree_ctr.fill_(t & 0x7FFFFFFF)
+        if self.expect != t:   # tree_begin advances the counter: set only when out of step
+            self.gb.builder.tree_ctr.fill_(t & 0x7FFFFFFF)
+        self.expect = t + 1
+        if len(self.live) >= self.RING:
+            self.freeze()
         for i, g in enumerate(self.graphs):
             g.replay()
             if i < len(self.colls):
                 buf, op = self.colls[i]
                 self.comm.all_reduce_(buf, op)
+        slot = (t & 0x7FFFFFFF) % self.RING
+        self.live.append((len(self.gb.trees_dev), slot))
+        self.gb.trees_dev.append(self.ring[slot])
+
+    def freeze(self):
+        """Point the trees still living in the ring at one snapshot of it."""
+        if self.live:
+            snap = self.ring.clone()
+            for i, slot in self.live:
+                self.gb.trees_dev[i] = snap[slot]
+            self.live = []
 
 
 class _SegmentComm:

@@ -191,6 +191,9 @@ def _design_columns(design):
 
 
 def mojo_bytes(model: Model) -> bytes:
+    if model.preprocessors:
+        raise ValueError(f"{model.model_id}: a model trained behind a preprocessing pipeline (AutoML target "
+                         "encoding) has no single-model MOJO; export the TargetEncoder and the model separately")
     algo = model.algo
     info: dict = {}
     files: dict[str, bytes] = {}

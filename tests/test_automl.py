@@ -89,3 +89,51 @@ def test_exploitation_xgboost_lr_search():
     assert any(i.startswith("GBM_lr_annealing_selection") for i in ids)
     xs = [m for m in aml.models if m.model_id.startswith("XGBoost_lr_search_selection")][0]
     assert xs.algo == "xgboost" and "failed" not in " ".join(str(e) for e in aml.event_log.to_pandas().values.ravel())
+
+
+def _hicard_frame(n=3000, seed=5):
+    rng = np.random.default_rng(seed)
+    city = rng.integers(0, 40, n)
+    effect = rng.normal(scale=1.5, size=40)
+    a = rng.normal(size=n)
+    logit = effect[city] + 0.8 * a
+    df = pd.DataFrame({"city": pd.Categorical([f"c{v}" for v in city]), "color": pd.Categorical(
+        rng.choice(["r", "g", "b"], n)), "a": a})
+    df["y"] = pd.Categorical(np.where(logit + rng.logistic(size=n) > 0, "yes", "no"))
+    return df
+
+
+def test_automl_target_encoding_preprocessing():
+    """preprocessing=["target_encoding"]: the 40-level predictor is replaced by its
+    out-of-fold blended target mean for the tree algos (the 3-level one is left
+    alone); the encoder travels with each model, so raw frames score as-is."""
+    df = _hicard_frame()
+    fr = Frame.from_pandas(df)
+    aml = H2OAutoML(max_models=3, nfolds=3, seed=1, include_algos=["GLM", "GBM", "DRF"],
+                    preprocessing=["target_encoding"]).train(y="y", training_frame=fr)
+    by = {m.algo: m for m in aml.models}
+    assert {"glm", "gbm", "drf"} <= set(by)
+    for algo in ("gbm", "drf"):
+        m = by[algo]
+        assert len(m.preprocessors) == 1 and "city_te" in m.x and "city" not in m.x and "color" in m.x
+        assert m.training_metrics["AUC"] > 0.7
+    assert not by["glm"].preprocessors and "city" in by["glm"].x
+    assert any("target_encoding" in e["msg"] for e in aml.events)
+    # scoring the raw frame goes through the encoder (no *_te columns needed)
+    p = by["gbm"].predict(Frame.from_pandas(df.head(50)))
+    assert p.nrows == 50
+    perf = by["gbm"].model_performance(fr)
+    assert perf["AUC"] > 0.7
+    import pytest
+
+    from h2omx.mojo import mojo_bytes
+    with pytest.raises(ValueError, match="preprocessing"):
+        mojo_bytes(by["gbm"])
+
+
+def test_automl_target_encoding_skips_low_cardinality():
+    fr = _frame(400)
+    aml = H2OAutoML(max_models=1, nfolds=0, seed=1, include_algos=["GBM"],
+                    preprocessing=["target_encoding"]).train(y="y", training_frame=fr)
+    assert not aml.models[0].preprocessors
+    assert any("step skipped" in e["msg"] for e in aml.events)
