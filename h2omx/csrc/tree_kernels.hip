@@ -1890,6 +1890,34 @@ __global__ __launch_bounds__(1024) void split_level_kernel(
 // the window with integer global atomics (order-independent: deterministic).
 constexpr int PART_LDS_NODES = 256;   // levels up to this many nodes read their split records from LDS
 
+// exact fixed-point (g, h, w) of a retiring row into its leaf's lane-private LDS
+// copy (window [base, base + win)) or, outside the window, the global sums
+__device__ __forceinline__ void part_leaf_add(int leaf, int base, int win, int cap, int R, int copy, float wv,
+                                              float gk, float hk, float lg, float lh, float lw,
+                                              unsigned long long* lacc, unsigned long long* leaf_acc) {
+  if (leaf_acc == nullptr || leaf >= cap || wv == 0.0f) return;
+  const unsigned long long a = (unsigned long long)(long long)__float2int_rn(gk * lg);
+  const unsigned long long b = (unsigned long long)(long long)__float2int_rn(hk * lh);
+  const unsigned long long c = (unsigned long long)(long long)__float2int_rn(wv * lw);
+  const int li = leaf - base;
+  // separate call sites keep LDS atomics as ds_add_u64 (a pointer selected
+  // between LDS and global memory would become FLAT)
+  if (li >= 0 && li < win) {
+    unsigned long long* d = lacc + (3 * li) * R + copy;
+    atomicAdd(d, a);
+    atomicAdd(d + R, b);
+    atomicAdd(d + 2 * R, c);
+  } else {
+    atomicAdd(leaf_acc + 3 * leaf + 0, a);
+    atomicAdd(leaf_acc + 3 * leaf + 1, b);
+    atomicAdd(leaf_acc + 3 * leaf + 2, c);
+  }
+}
+// A/B switches (H2OMX_PART_RECLDS / H2OMX_PART_RECLDS_FINAL, read by the launcher):
+// LDS-staged split records for the routing / final-level variants
+__constant__ int g_part_rec_lds = 1;
+__constant__ int g_part_rec_lds_final = 1;
+
 template <bool PREF, int RPL>
 __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restrict__ codes, int64_t npad,
                                                         int* nid, const PartInfo* __restrict__ part,
@@ -1911,7 +1939,7 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
   // the level's split records: LDS-staged when they fit (the node id -> split
   // record -> split code chain then has one dependent global load, not two)
   const int n_cur = ctl_cur[CTL_N];
-  const bool rec_lds = n_cur <= PART_LDS_NODES;
+  const bool rec_lds = n_cur <= PART_LDS_NODES && (PREF ? g_part_rec_lds_final : g_part_rec_lds);
   if (rec_lds)
     for (int j = threadIdx.x; j < n_cur; j += blockDim.x) ps[j] = part[j];
   if (use_lds)
@@ -1950,64 +1978,101 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
         }
       }
     }
-    PartInfo pi[RPL];
-    int bc[RPL];
-#pragma unroll
-    for (int k = 0; k < RPL; ++k) {
-      const int n = nn[k] >= 0 ? nn[k] : 0;   // retired rows / padding: any record, unused
-      pi[k] = rec_lds ? ps[n] : part[n];
-    }
-#pragma unroll
-    for (int k = 0; k < RPL; ++k) {
-      const int f = (nn[k] >= 0 && pi[k].child >= 0) ? pi[k].feat : 0;
-      bc[k] = codes[(int64_t)f * npad + r0 + k];
-    }
     bool changed = false;
     int sv[RPL];  // next level's build slot per row (-1: retired, or histogram derived from the sibling)
+    if constexpr (PREF) {
+      // final level: per-row node -> split -> code chain (the batched form below
+      // measured no faster here, profiles/r3/part_ab.txt)
 #pragma unroll
-    for (int k = 0; k < RPL; ++k) {
-      sv[k] = -1;
-      const int n = nn[k];
-      int leaf = -1;
-      if (n < 0) {
-        if (!all_rows) continue;
-        leaf = ~n;  // retired earlier (padding: INT_MIN -> beyond cap, no sums)
-      } else {
-        changed = true;
-        const PartInfo& p = pi[k];
-        if (p.child < 0) {
-          leaf = p.gid;
+      for (int k = 0; k < RPL; ++k) {
+        sv[k] = -1;
+        const int n = nn[k];
+        int leaf = -1;
+        PartInfo pi;
+        if (n < 0) {
+          if (!all_rows) continue;
+          leaf = ~n;  // retired earlier (padding: INT_MIN -> beyond cap, no sums)
+          pi.child = -2;
         } else {
-          const int b = bc[k];
-          const int right = (b == nbt - 1) ? !p.na_left : (b > p.bin);
-          if (p.leaf_children) {
-            leaf = p.child_gid + right;
+          changed = true;
+          pi = rec_lds ? ps[n] : part[n];
+        }
+        if (pi.child == -2) {
+        } else if (pi.child < 0) {
+          leaf = pi.gid;
+        } else {
+          const int b = codes[(int64_t)pi.feat * npad + r0 + k];
+          const int right = (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
+          if (pi.leaf_children) {
+            leaf = pi.child_gid + right;
           } else {
-            nn[k] = p.child + right;
-            sv[k] = right ? (p.pad >> 16) : (int)(short)(p.pad & 0xFFFF);
+            nn[k] = pi.child + right;
+            sv[k] = right ? (pi.pad >> 16) : (int)(short)(pi.pad & 0xFFFF);
           }
         }
-        if (leaf >= 0) nn[k] = ~leaf;
+        if (leaf >= 0) {
+          if (n >= 0) nn[k] = ~leaf;
+          part_leaf_add(leaf, base, win, cap, R, copy, wv8[k], gv[k], hv[k], lg, lh, lw, lacc, leaf_acc);
+        }
       }
-      if (leaf >= 0 && leaf_acc && leaf < cap) {
-        const float wv = PREF ? wv8[k] : (w ? w[r0 + k] : 1.0f);
-        if (wv != 0.0f) {
-          const float gk = PREF ? gv[k] : g[r0 + k], hk = PREF ? hv[k] : h[r0 + k];
-          const unsigned long long a = (unsigned long long)(long long)__float2int_rn(gk * lg);
-          const unsigned long long b = (unsigned long long)(long long)__float2int_rn(hk * lh);
-          const unsigned long long c = (unsigned long long)(long long)__float2int_rn(wv * lw);
-          const int li = leaf - base;
-          // separate call sites keep LDS atomics as ds_add_u64 (a pointer
-          // selected between LDS and global memory would become FLAT)
-          if (li >= 0 && li < win) {
-            unsigned long long* d = lacc + (3 * li) * R + copy;
-            atomicAdd(d, a);
-            atomicAdd(d + R, b);
-            atomicAdd(d + 2 * R, c);
+    } else {
+      PartInfo pi[RPL];
+      int bc[RPL];
+#pragma unroll
+      for (int k = 0; k < RPL; ++k) {
+        const int n = nn[k] >= 0 ? nn[k] : 0;   // retired rows / padding: any record, unused
+        pi[k] = rec_lds ? ps[n] : part[n];
+      }
+#pragma unroll
+      for (int k = 0; k < RPL; ++k) {
+        const int f = (nn[k] >= 0 && pi[k].child >= 0) ? pi[k].feat : 0;
+        bc[k] = codes[(int64_t)f * npad + r0 + k];
+      }
+#pragma unroll
+      for (int k = 0; k < RPL; ++k) {
+        sv[k] = -1;
+        const int n = nn[k];
+        int leaf = -1;
+        if (n < 0) {
+          if (!all_rows) continue;
+          leaf = ~n;  // retired earlier (padding: INT_MIN -> beyond cap, no sums)
+        } else {
+          changed = true;
+          const PartInfo& p = pi[k];
+          if (p.child < 0) {
+            leaf = p.gid;
           } else {
-            atomicAdd(leaf_acc + 3 * leaf + 0, a);
-            atomicAdd(leaf_acc + 3 * leaf + 1, b);
-            atomicAdd(leaf_acc + 3 * leaf + 2, c);
+            const int b = bc[k];
+            const int right = (b == nbt - 1) ? !p.na_left : (b > p.bin);
+            if (p.leaf_children) {
+              leaf = p.child_gid + right;
+            } else {
+              nn[k] = p.child + right;
+              sv[k] = right ? (p.pad >> 16) : (int)(short)(p.pad & 0xFFFF);
+            }
+          }
+          if (leaf >= 0) nn[k] = ~leaf;
+        }
+        if (leaf >= 0 && leaf_acc && leaf < cap) {
+          const float wv = PREF ? wv8[k] : (w ? w[r0 + k] : 1.0f);
+          if (wv != 0.0f) {
+            const float gk = PREF ? gv[k] : g[r0 + k], hk = PREF ? hv[k] : h[r0 + k];
+            const unsigned long long a = (unsigned long long)(long long)__float2int_rn(gk * lg);
+            const unsigned long long b = (unsigned long long)(long long)__float2int_rn(hk * lh);
+            const unsigned long long c = (unsigned long long)(long long)__float2int_rn(wv * lw);
+            const int li = leaf - base;
+            // separate call sites keep LDS atomics as ds_add_u64 (a pointer
+            // selected between LDS and global memory would become FLAT)
+            if (li >= 0 && li < win) {
+              unsigned long long* d = lacc + (3 * li) * R + copy;
+              atomicAdd(d, a);
+              atomicAdd(d + R, b);
+              atomicAdd(d + 2 * R, c);
+            } else {
+              atomicAdd(leaf_acc + 3 * leaf + 0, a);
+              atomicAdd(leaf_acc + 3 * leaf + 1, b);
+              atomicAdd(leaf_acc + 3 * leaf + 2, c);
+            }
           }
         }
       }
@@ -2028,16 +2093,15 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
   }
   if (use_lds) {
     __syncthreads();
-    // fold the R copies: consecutive threads read consecutive u64 (no bank
-    // conflicts; R divides 64 so a copy group never straddles a wave), the
-    // group of R lanes reduces with cross-lane adds, its first lane adds to
-    // the global sums
-    const int total = 3 * win * R;
-    for (int j0 = 0; j0 < total; j0 += blockDim.x) {
-      const int j = j0 + threadIdx.x;
-      unsigned long long v = (j < total) ? lacc[j] : 0ull;
-      for (int off = 1; off < R; off <<= 1) v += __shfl_xor(v, off, 64);
-      if (j < total && (j % R) == 0 && v && base + (j / R) / 3 < cap) atomicAdd(leaf_acc + 3 * base + j / R, v);
+    // fold the R copies: thread t sums slot t's copies starting at copy t mod R
+    // (rotated so the threads of a lane group hit different banks; a shuffle
+    // butterfly over consecutive copies measured 168 vs 100 us per final level)
+    {
+      for (int t = threadIdx.x; t < 3 * win; t += blockDim.x) {
+        unsigned long long v = 0ull;
+        for (int c = 0; c < R; ++c) v += lacc[t * R + ((c + t) & (R - 1))];
+        if (v && base + t / 3 < cap) atomicAdd(leaf_acc + 3 * base + t, v);
+      }
     }
   }
 }
@@ -2876,11 +2940,23 @@ H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_n
 constexpr int PARTITION_BLOCKS = 8192;
 constexpr int PART_RPL = 8;    // rows per lane per step (16: 1.52 vs 1.47 ms/tree on HIGGS)
 
+static void part_env_once() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  const char* a = getenv("H2OMX_PART_RECLDS");
+  const char* b = getenv("H2OMX_PART_RECLDS_FINAL");
+  const int va = a ? atoi(a) : 1, vb = b ? atoi(b) : 1;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_part_rec_lds), &va, sizeof(int));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_part_rec_lds_final), &vb, sizeof(int));
+}
+
 static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt, const float* g,
                             const float* h, const float* w, const double* qscale, int cap,
                             unsigned long long* leaf_acc, const int* ctl_cur, const int* ctl_next, int win_max,
                             int blocks, int prefetch, short* slot16, int* nid_out, int all_rows, hipStream_t stream) {
   if (slot16 && prefetch) return kBadArg;
+  part_env_once();
   if (npad % PART_RPL != 0 || blocks < 1 || blocks > PARTITION_BLOCKS || win_max < 0) return kBadArg;
   if (all_rows && (leaf_acc == nullptr || win_max > cap)) return kBadArg;
   // lane-private copies: the largest power of two <= 64 that fits 64 KB

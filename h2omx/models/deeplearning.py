@@ -23,6 +23,7 @@ standardized response) and autoencoders with ``anomaly()``.
 """
 from __future__ import annotations
 
+import gc
 import math
 import os
 
@@ -340,8 +341,17 @@ class _DLTrainer:
         elif self.n_steps >= 1 and self.graph_eligible():
             self.idx_buf = idx.clone()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._body(self.idx_buf)
+            # no automatic garbage collection while the stream captures: a cyclic
+            # earlier model holding a graph (e.g. a tree booster's TreeGraph) would
+            # be destroyed mid-capture, which aborts the process
+            gc_was = gc.isenabled()
+            gc.disable()
+            try:
+                with torch.cuda.graph(g):
+                    self._body(self.idx_buf)
+            finally:
+                if gc_was:
+                    gc.enable()
             self.graph = g
             g.replay()
         else:

@@ -297,6 +297,7 @@ class GpuBooster:
         self.builder = HipTreeBuilder(bm, tp, comm)
         self.cap = self.builder.capacity
         self.trees_dev = []
+        self.graph_used = False   # a step graph was captured (finish() releases the graph itself)
         need_w = sample_rate < 1.0 or self.st.w is not None
         self.wout = torch.empty((bm.npad,), dtype=torch.float32, device=self.dev) if need_w else None
         self.kw = dict(tweedie_power=dist_kw.get("tweedie_power", 1.5),
@@ -457,6 +458,7 @@ class GpuBooster:
             warnings.warn(f"h2omx: tree step graph capture failed, running eagerly ({self.graph_error})")
             return
         self.graph = g
+        self.graph_used = True
 
     def _snapshot(self) -> torch.Tensor:
         """Copy of the finished tree.  Shallow trees copy the whole capacity-sized
@@ -471,7 +473,12 @@ class GpuBooster:
     def finish(self) -> TreeEnsemble:
         self.flush()
         if self.graph is not None:
+            # trees out of the ring, then drop the graph: booster <-> TreeGraph is
+            # a reference cycle, and a graph freed later by the cyclic collector
+            # could land inside another capture
             self.graph.freeze()
+            self.graph.gb = None
+            self.graph = None
         torch.cuda.synchronize(self.dev)
         if self.builder.timer.enabled:
             self.ens.timings.update({f"gpu_ms_{k}": v for k, v in self.builder.timer.totals().items()})
