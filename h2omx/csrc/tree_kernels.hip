@@ -60,6 +60,13 @@ struct SplitParams {
   // [capacity][2] = [lo, hi] interval of every node's value, set by its parent
   const signed char* mono;
   double* gbound;
+  // interaction constraints (nullptr = none): ifsets[F] = bit mask of the
+  // user's interaction sets holding feature f (0: unlisted, interacts only
+  // with itself); istate[capacity][2] = (compatible-set mask, solo feature)
+  // of every node, written by its parent's split (root: all sets, -2 = no
+  // feature on the path yet)
+  const unsigned long long* ifsets;
+  long long* istate;
 };
 
 struct NodeSplit {  // best split of one node at the current level (64 B)
@@ -156,6 +163,31 @@ __device__ __forceinline__ bool mono_ok(int mf, double GL, double SL, double G, 
   if (mf == 0) return true;
   const double wl = leaf_value(GL, SL, SL, p), wr = leaf_value(G - GL, S - SL, S - SL, p);
   return mf > 0 ? wl <= wr : wl >= wr;
+}
+
+// H2O / XGBoost interaction_constraints: may node gid split on feature f?
+// (every feature on the root path and f must share one interaction set;
+// an unlisted feature only combines with itself)
+__device__ __forceinline__ bool inter_ok(const SplitParams& p, int gid, int f) {
+  if (p.istate == nullptr) return true;
+  const long long solo = p.istate[2 * gid + 1];
+  if (solo == -2) return true;            // nothing on the path yet
+  if (solo >= 0) return f == (int)solo;   // path used an unlisted feature
+  return (p.ifsets[f] & (unsigned long long)p.istate[2 * gid]) != 0ull;
+}
+
+// the state a split of node gid on feature f hands to both children
+__device__ __forceinline__ void inter_children(const SplitParams& p, int gid, int f, int cg) {
+  const long long solo = p.istate[2 * gid + 1];
+  const unsigned long long fs = p.ifsets[f];
+  long long c_mask = 0, c_solo = f;
+  if (fs != 0ull) {
+    const unsigned long long comp = (solo == -2) ? ~0ull : (unsigned long long)p.istate[2 * gid];
+    c_mask = (long long)(comp & fs);
+    c_solo = -1;
+  }
+  p.istate[2 * cg] = c_mask; p.istate[2 * cg + 1] = c_solo;
+  p.istate[2 * cg + 2] = c_mask; p.istate[2 * cg + 3] = c_solo;
 }
 
 __device__ __forceinline__ double clamp_bound(double v, const SplitParams& p, int gid, int cap) {
@@ -1302,7 +1334,7 @@ __device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__
                                                    long long* __restrict__ full, const NodeLink& lk, int node, int f,
                                                    const int* __restrict__ nvb,
                                                    const uint8_t* __restrict__ tree_fmask, double ig, double is,
-                                                   const SplitParams& p) {
+                                                   const SplitParams& p, int gid) {
   constexpr int B = NBT <= 64 ? 1 : NBT / 64;  // bins per lane
   const int F = p.F;
   const int lane = threadIdx.x & 63;
@@ -1332,6 +1364,7 @@ __device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__
       allowed = u01(hf) < p.col_rate;
     }
   }
+  allowed = allowed && inter_ok(p, gid, f);
   if (!allowed && full == nullptr && f != 0) {
     // last level: no histogram row to keep and the node totals come from
     // feature 0 (node_best reads fbest[node][0]) - nothing to load at all
@@ -1462,7 +1495,7 @@ __global__ __launch_bounds__(256) void split_find_kernel(const long long* __rest
   if (f >= p.F) return;  // whole wave
   const NodeLink lk = link[node];
   const WaveBest w = feat_best_wave<NBT>(built, parent_full, full, lk, node, f, nvb, tree_fmask, qscale[2],
-                                         qscale[3], p);
+                                         qscale[3], p, ctl[CTL_BASE] + node);
   if ((threadIdx.x & 63) == 0) {
     FeatBest r{};
     r.gain = w.gain; r.GL = w.GL; r.SL = w.SL;
@@ -1590,6 +1623,7 @@ __device__ __forceinline__ void lf_write_node(int i, const NodeSplit& s, bool do
       p.gbound[2 * cg] = llo; p.gbound[2 * cg + 1] = lhi;
       p.gbound[2 * cg + 2] = rlo; p.gbound[2 * cg + 3] = rhi;
     }
+    if (p.istate != nullptr && cg + 1 < tree_capacity && gid < tree_capacity) inter_children(p, gid, s.feat, cg);
     if (p.children_leaves) {
       // children are final: their totals come from this split's left stats
       pi.leaf_children = 1;
@@ -1822,7 +1856,8 @@ __global__ __launch_bounds__(1024) void split_level_kernel(
   double bg = -INFINITY, bgl = 0.0, bsl = 0.0;
   long long key = 0x7fffffffffffffffLL;
   for (int f = wave; f < F; f += nw) {
-    const WaveBest w = feat_best_wave<NBT>(built, parent_full, full, lk, node, f, nvb, tree_fmask, ig, is, p);
+    const WaveBest w = feat_best_wave<NBT>(built, parent_full, full, lk, node, f, nvb, tree_fmask, ig, is, p,
+                                           ctl[CTL_BASE] + node);
     if (f == 0 && lane == 0) { s_tot[0] = w.G; s_tot[1] = w.S; }
     if (w.code != 0x7fffffff && w.gain > -INFINITY) {
       const long long k = ((long long)f << 32) | (unsigned)w.code;
@@ -3818,6 +3853,7 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
   const int F = p.F;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int lo = seg_start[node], cnt = seg_cnt[node];
+  const int gid_i = ctl[CTL_BASE] + node;   // interaction-constraint state
   // eligible features of this node (wave 0), in ascending order; the mtries
   // rank of feature f counts the features whose hash is smaller (ties: lower
   // index), as split_find - with the F hashes computed once into LDS
@@ -3831,7 +3867,7 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
     int c = 0;
     for (int f0 = 0; f0 < F; f0 += 64) {
       const int f = f0 + lane;
-      bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]);
+      bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]) && inter_ok(p, gid_i, f);
       if (ok && sampled) {
         const uint32_t hf = hsh_s[f];
         if (p.mtries > 0) {
@@ -3935,7 +3971,8 @@ __device__ __forceinline__ int chunk_node_wave(const int* __restrict__ first, in
 // 256: per-lane hashes in registers ranked with scalar lane reads; wider: the
 // hashes go through LDS (hsh_s, F entries).
 template <typename FL>
-__device__ __forceinline__ int direct_eligible(int node, const SplitParams& p, const uint8_t* __restrict__ tree_fmask,
+__device__ __forceinline__ int direct_eligible(int node, int gid_i, const SplitParams& p,
+                                              const uint8_t* __restrict__ tree_fmask,
                                               FL* flist, uint32_t* hsh_s, int lane) {
   const int F = p.F;
   const uint32_t key = (uint32_t)p.tree_index * 131u + (uint32_t)p.depth;
@@ -3965,7 +4002,7 @@ __device__ __forceinline__ int direct_eligible(int node, const SplitParams& p, c
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int f = lane + 64 * k;
-      bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]);
+      bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]) && inter_ok(p, gid_i, f);
       if (ok && sampled) ok = p.mtries > 0 ? rank[k] < p.mtries : u01(hv[k]) < p.col_rate;
       const unsigned long long bal = __ballot(ok);
       if (ok) flist[nfl + __popcll(bal & ((1ull << lane) - 1ull))] = (FL)f;
@@ -3978,7 +4015,7 @@ __device__ __forceinline__ int direct_eligible(int node, const SplitParams& p, c
   wave_lds_sync();
   for (int f0 = 0; f0 < F; f0 += 64) {
     const int f = f0 + lane;
-    bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]);
+    bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]) && inter_ok(p, gid_i, f);
     if (ok && sampled) {
       const uint32_t hf = hsh_s[f];
       if (p.mtries > 0) {
@@ -4040,7 +4077,7 @@ __global__ __launch_bounds__(256) void seg_direct_chunk_kernel(
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   if (wid == 0) {
     const int node = chunk_node_wave(pc_first, n, c, lane);
-    const int nfl = direct_eligible(node, p, tree_fmask, flist, hsh_s, lane);
+    const int nfl = direct_eligible(node, ctl[CTL_BASE] + node, p, tree_fmask, flist, hsh_s, lane);
     if (lane == 0) { node_s = node; nfl_s = min(nfl, nfl_max); }
   }
   __syncthreads();
@@ -4163,6 +4200,7 @@ __global__ __launch_bounds__(256) void seg_direct_wave_kernel(
   short* flist = flist_all[wid];
   const int F = p.F;
   const int lo = seg_start[node], cnt = seg_cnt[node];
+  const int gid_i = ctl[CTL_BASE] + node;   // interaction-constraint state
   // eligible features, ascending
   const uint32_t key = (uint32_t)p.tree_index * 131u + (uint32_t)p.depth;
   const bool sampled = p.mtries > 0 || p.col_rate < 1.0f;
@@ -4190,7 +4228,7 @@ __global__ __launch_bounds__(256) void seg_direct_wave_kernel(
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int f = lane + 64 * k;
-    bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]);
+    bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]) && inter_ok(p, gid_i, f);
     if (ok && sampled) ok = p.mtries > 0 ? rank[k] < p.mtries : u01(hv[k]) < p.col_rate;
     const unsigned long long bal = __ballot(ok);
     if (ok) flist[nfl + __popcll(bal & ((1ull << lane) - 1ull))] = (short)f;

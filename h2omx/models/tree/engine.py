@@ -28,7 +28,7 @@ from ... import ops
 from .binning import BinnedMatrix
 from ...utils.trace import PhaseTimer
 from .structs import (FEAT_BEST_BYTES, NODE_LINK_BYTES, PART_INFO_BYTES, TREE_NODE_DTYPE, GradParams,
-                      SplitParams, check_layout)
+                      SplitParams, check_layout, interaction_masks)
 
 
 @dataclass
@@ -51,6 +51,9 @@ class TreeParams:
     seed: int = 0
     # per-feature monotone constraint (-1 / 0 / +1), None = unconstrained
     monotone: tuple | None = None
+    # interaction constraints: tuple of feature-index tuples (features of one set
+    # may share a root path; unlisted features only with themselves), None = off
+    interactions: tuple | None = None
     extra: dict = field(default_factory=dict)
 
 
@@ -155,6 +158,14 @@ class HipTreeBuilder:
                 raise ValueError(f"monotone has {len(params.monotone)} entries for {self.F} features")
             self.mono = torch.tensor([int(np.sign(m)) for m in params.monotone], dtype=torch.int8, device=d)
             self.gbound = torch.zeros((2 * self.capacity,), dtype=torch.float64, device=d)
+        # interaction constraints: per-feature set masks + every node's state
+        # (compatible sets, solo feature), written by the parent's finalisation
+        self.ifsets = self.istate = None
+        if params.interactions:
+            fs = interaction_masks(params.interactions, self.F)
+            self.ifsets = torch.from_numpy(fs.view(np.int64).copy()).to(d)
+            self.istate = torch.zeros((2 * self.capacity,), dtype=torch.int64, device=d)
+            self.istate[0], self.istate[1] = -1, -2     # root: every set, empty path
         self.stats = {"host_syncs": 0}
         self.timer = PhaseTimer(device=d)
         # global index of this rank's first row: the stochastic-rounding dither and
@@ -380,6 +391,8 @@ class HipTreeBuilder:
         sp.col_rate, sp.mtries = p.col_sample_rate, p.mtries
         sp.mono = self.mono.data_ptr() if self.mono is not None else None
         sp.gbound = self.gbound.data_ptr() if self.gbound is not None else None
+        sp.ifsets = self.ifsets.data_ptr() if self.ifsets is not None else None
+        sp.istate = self.istate.data_ptr() if self.istate is not None else None
         return ctypes.addressof(sp)
 
     # -- one tree ------------------------------------------------------------

@@ -23,6 +23,7 @@ class SplitParams(ctypes.Structure):
         ("seed", ctypes.c_uint32), ("tree_index", ctypes.c_int), ("depth", ctypes.c_int),
         ("col_rate", ctypes.c_float), ("mtries", ctypes.c_int), ("children_leaves", ctypes.c_int),
         ("pad2", ctypes.c_int), ("mono", ctypes.c_void_p), ("gbound", ctypes.c_void_p),
+        ("ifsets", ctypes.c_void_p), ("istate", ctypes.c_void_p),
     ]
 
 
@@ -33,6 +34,41 @@ class GradParams(ctypes.Structure):
         ("quantile_alpha", ctypes.c_float), ("huber_delta", ctypes.c_float), ("row_base", ctypes.c_int64),
         ("skip_nid", ctypes.c_int), ("pad", ctypes.c_int),
     ]
+
+
+def interaction_masks(sets, F: int) -> np.ndarray:
+    """Per-feature bit masks of the interaction sets holding it (uint64; 0 =
+    unlisted: such a feature only interacts with itself).  ``sets`` holds
+    feature indices; at most 64 sets."""
+    if len(sets) > 64:
+        raise ValueError(f"interaction_constraints: at most 64 sets, got {len(sets)}")
+    m = np.zeros(F, np.uint64)
+    for si, st in enumerate(sets):
+        for f in st:
+            if not 0 <= int(f) < F:
+                raise ValueError(f"interaction_constraints: feature index {f} out of range")
+            m[int(f)] |= np.uint64(1) << np.uint64(si)
+    return m
+
+
+def interaction_allowed(state, fsets: np.ndarray, f: int) -> bool:
+    """Mirror of inter_ok (csrc/tree_kernels.hip): state = (set mask, solo)."""
+    mask, solo = state
+    if solo == -2:
+        return True
+    if solo >= 0:
+        return f == solo
+    return bool(int(fsets[f]) & mask)
+
+
+def interaction_child(state, fsets: np.ndarray, f: int):
+    """Mirror of inter_children: the state both children of a split on f get."""
+    mask, solo = state
+    fs = int(fsets[f])
+    if fs == 0:
+        return (0, f)
+    comp = (1 << 64) - 1 if solo == -2 else mask
+    return (comp & fs, -1)
 
 
 # distribution codes of boost_update_kernel

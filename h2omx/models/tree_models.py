@@ -148,6 +148,24 @@ class _TreeBuilder(ModelBuilder):
             raise ValueError("monotone_constraints are not supported for multinomial models")
         return tuple(signs)
 
+    def _interactions(self):
+        """H2O ``interaction_constraints`` (a list of lists of column names whose
+        columns may appear together on a root path) as feature-index tuples;
+        None if unset.  Columns outside every list only combine with
+        themselves (hex/tree/GlobalInteractionConstraints)."""
+        ic = self.params.get("interaction_constraints")
+        if not ic:
+            return None
+        sets = []
+        for grp in ic:
+            idx = []
+            for col in ([grp] if isinstance(grp, str) else grp):
+                if col not in self.x:
+                    raise ValueError(f"interaction_constraints: column {col!r} is not a predictor")
+                idx.append(self.x.index(col))
+            sets.append(tuple(sorted(set(idx))))
+        return tuple(sets)
+
     def _fit(self, train: Frame, valid: Frame | None, model_id: str) -> Model:
         enc = str(self.params.get("categorical_encoding") or "AUTO").lower().replace("_", "")
         if enc == "sortbyresponse":
@@ -556,7 +574,7 @@ class H2OGradientBoostingEstimator(_TreeBuilder):
                     offset_column=None, balance_classes=False, class_sampling_factors=None,
                     max_after_balance_size=5.0, categorical_encoding="AUTO", checkpoint=None,
                     calibrate_model=False, calibration_frame=None, calibration_method="AUTO",
-                    monotone_constraints=None)
+                    monotone_constraints=None, interaction_constraints=None)
 
     def _tree_params(self, nfeat):
         p = self.params
@@ -566,7 +584,7 @@ class H2OGradientBoostingEstimator(_TreeBuilder):
                           col_sample_rate=float(p["col_sample_rate"]),
                           col_sample_rate_per_tree=float(p["col_sample_rate_per_tree"]),
                           max_abs_leaf=float(p["max_abs_leafnode_pred"] or 0.0), seed=self._seed(),
-                          monotone=self._monotone())
+                          monotone=self._monotone(), interactions=self._interactions())
 
 
 # ---------------------------------------------------------------------------
@@ -590,7 +608,7 @@ class H2OXGBoostEstimator(_TreeBuilder):
                     stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0,
                     offset_column=None, backend="gpu", nbins=None, categorical_encoding="AUTO", checkpoint=None,
                     calibrate_model=False, calibration_frame=None, calibration_method="AUTO",
-                    monotone_constraints=None)
+                    monotone_constraints=None, interaction_constraints=None)
 
     def _tree_params(self, nfeat):
         p = self.params
@@ -607,7 +625,7 @@ class H2OXGBoostEstimator(_TreeBuilder):
                           min_split_improvement=0.0, learn_rate=float(eta), mode=1, leaf_mode=0,
                           col_sample_rate=csr, col_sample_rate_per_tree=float(cst),
                           max_abs_leaf=float(p["max_abs_leafnode_pred"] or 0.0), seed=self._seed(),
-                          monotone=self._monotone())
+                          monotone=self._monotone(), interactions=self._interactions())
 
 
 # ---------------------------------------------------------------------------

@@ -21,7 +21,8 @@ import torch
 from ..models.tree.binning import BinnedMatrix
 from ..models.tree.engine import TreeParams, tree_capacity
 from ..models.tree.hashing import M32, _mix32, hash4, u01  # noqa: F401
-from ..models.tree.structs import DIST_CODES, TREE_NODE_DTYPE
+from ..models.tree.structs import (DIST_CODES, TREE_NODE_DTYPE, interaction_allowed, interaction_child,
+                                   interaction_masks)
 
 
 
@@ -142,6 +143,12 @@ class RefTreeBuilder:
                 v = np.clip(v, -p.max_abs_leaf, p.max_abs_leaf)
             return v
 
+        # interaction constraints (mirror of inter_ok / inter_children): state per node id
+        fsets = istate = None
+        if p.interactions:
+            fsets = interaction_masks(p.interactions, F)
+            istate = {0: ((1 << 64) - 1, -2)}
+
         def mono_mask(mf, GLv, SLv, Gs, Ss):
             wl, wr = lv_vec(GLv, SLv), lv_vec(Gs - GLv, Ss - SLv)
             return wl <= wr if mf > 0 else wl >= wr
@@ -162,6 +169,9 @@ class RefTreeBuilder:
                 tot = hist[0].sum(axis=1)  # feature 0 totals [3]
                 Gt, Ht, Wt = tot
                 allowed = feature_allowed(p, F, tree_index, d, i, tree_fmask)
+                if fsets is not None:
+                    st = istate[base + i]
+                    allowed &= np.array([interaction_allowed(st, fsets, f) for f in range(F)])
                 best = (-np.inf, None)
                 for f in range(F):
                     if not allowed[f]:
@@ -203,6 +213,9 @@ class RefTreeBuilder:
                 rec["weight"] = Wt
                 if do_split:
                     f, t, na_left, GL, HL, WL = best[1]
+                    if fsets is not None:
+                        cs_ = interaction_child(istate[gid], fsets, f)
+                        istate[next_base + 2 * k] = istate[next_base + 2 * k + 1] = cs_
                     if mono is not None:
                         cg = next_base + 2 * k
                         lo, hi = bounds.get(gid, (-np.inf, np.inf)) if gid else (-np.inf, np.inf)
