@@ -7,9 +7,11 @@ cross-validates every model with shared folds, and finishes with two
 Stacked Ensembles (all models, best of family).  Models are ranked on a
 leaderboard by the H2O default metric for the problem type.
 
-Two schedulers (``parallelism``, an h2omx extension):
+Two schedulers (``parallelism``, an h2omx extension), picked
+per run by ``"auto"`` (default): task-parallel when the replicated training
+frame takes at most TASK_MEM_FRACTION of one device's memory, else data:
 
-* ``"data"`` (default): every model is data-parallel over all ranks (the row
+* ``"data"``: every model is data-parallel over all ranks (the row
   shards stay where they are and each model's collectives run over RCCL), so
   AutoML on 8 MI355X trains each model 8-way parallel in sequence.
 * ``"task"``: the training frame is replicated on every GPU (all-gather; 288
@@ -106,9 +108,9 @@ class H2OAutoML:
                  project_name=None, include_algos=None, exclude_algos=None, sort_metric="AUTO",
                  keep_cross_validation_predictions=True, stopping_rounds=3, stopping_tolerance=None,
                  stopping_metric="AUTO", balance_classes=False, verbosity="warn", modeling_plan=None,
-                 preprocessing=None, exploitation_ratio=-1.0, parallelism="data", **_ignored):
-        if parallelism not in ("data", "task"):
-            raise ValueError("parallelism must be 'data' or 'task'")
+                 preprocessing=None, exploitation_ratio=-1.0, parallelism="auto", **_ignored):
+        if parallelism not in ("auto", "data", "task"):
+            raise ValueError("parallelism must be 'auto', 'data' or 'task'")
         self.parallelism = parallelism
         self.max_models = max_models
         self.max_runtime_secs = max_runtime_secs
@@ -191,7 +193,7 @@ class H2OAutoML:
             return m
 
         self._log("Workflow", f"AutoML build started: {self.project_name}")
-        task_mode = self.parallelism == "task" and comm is not None and comm.world_size > 1
+        task_mode = self._scheduler(training_frame, comm) == "task"
         # (task-parallel runs fit the step on the replicated frame, _train_task_parallel)
         te = None if task_mode else self._target_encoding(x, y, training_frame, validation_frame, seed, comm)
         if te is not None:
@@ -265,6 +267,28 @@ class H2OAutoML:
                 out.append((f"{name[f]}_grid_1_model_{counters[f]}", cls, params))
                 counters[f] += 1
         return out[:cap] if self.max_models else out
+
+    # "auto": replicate the frame (task-parallel) while it takes at most this share
+    # of one device's memory (288 GB HBM per MI355X: AutoML's 10M x 100 frame is ~1.4 %)
+    TASK_MEM_FRACTION = 0.25
+
+    def _scheduler(self, frame, comm) -> str:
+        if comm is None or comm.world_size <= 1:
+            return "data"
+        if self.parallelism != "auto":
+            return self.parallelism
+        rows = int(comm.all_reduce_numpy(np.array([float(frame.nrows)]))[0])
+        need = rows * max(1, len(frame.names)) * 8          # float64-sized upper bound per cell
+        if frame.device.type == "cuda":
+            cap = torch.cuda.get_device_properties(frame.device).total_memory
+        else:
+            import psutil
+
+            cap = psutil.virtual_memory().total // comm.world_size
+        mode = "task" if need <= self.TASK_MEM_FRACTION * cap else "data"
+        self._log("Workflow", f"parallelism auto -> {mode} ({need / 2**30:.2f} GiB replicated frame, "
+                              f"{cap / 2**30:.0f} GiB per rank)")
+        return mode
 
     def _target_encoding(self, x, y, frame, valid, seed, comm):
         """Fit the TargetEncoding preprocessing step (see TE_CARDINALITY) and
@@ -569,7 +593,7 @@ def run_automl(spec: dict, comm=None) -> dict:
                     sort_metric=isp.get("sort_metric", "AUTO"), modeling_plan=bm.get("modeling_plan"),
                     stopping_rounds=sc.get("stopping_rounds", 3), stopping_metric=sc.get("stopping_metric", "AUTO"),
                     stopping_tolerance=sc.get("stopping_tolerance"), preprocessing=bm.get("preprocessing"),
-                    parallelism=bc.get("parallelism", "data"))
+                    parallelism=bc.get("parallelism", "auto"))
     tf = DKV.get(_key(isp.get("training_frame")))
     lf = DKV.get(_key(isp.get("leaderboard_frame"))) if isp.get("leaderboard_frame") else None
     y = isp.get("response_column")

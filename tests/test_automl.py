@@ -137,3 +137,24 @@ def test_automl_target_encoding_skips_low_cardinality():
                     preprocessing=["target_encoding"]).train(y="y", training_frame=fr)
     assert not aml.models[0].preprocessors
     assert any("step skipped" in e["msg"] for e in aml.events)
+
+
+def test_automl_auto_scheduler_choice():
+    """parallelism="auto": task-parallel while the replicated frame fits a share
+    of one device's memory, data-parallel otherwise / when asked / on one rank."""
+
+    class _Comm:
+        world_size, rank = 2, 0
+
+        def all_reduce_numpy(self, a):
+            return a * 2
+
+    fr = _frame(300)
+    aml = H2OAutoML(max_models=1, seed=1)
+    assert aml.parallelism == "auto"
+    assert aml._scheduler(fr, None) == "data"
+    assert aml._scheduler(fr, _Comm()) == "task"
+    aml.TASK_MEM_FRACTION = 1e-12
+    assert aml._scheduler(fr, _Comm()) == "data"
+    assert H2OAutoML(max_models=1, parallelism="data")._scheduler(fr, _Comm()) == "data"
+    assert any("parallelism auto" in e["msg"] for e in aml.events)
