@@ -442,7 +442,35 @@ def _design_info(design, info, files, tag="design"):
     _put(files, info, f"{tag}_center", getattr(design, "center", np.zeros(len(design.names))))
 
 
+def _uplift_genmodel_trees(model, files) -> int:
+    """genmodel SharedTree layout of the uplift forest: every tree twice, the
+    same splits with the treatment leaf predictions (trees/t00_*) and the
+    control ones (trees/t01_*), i.e. two tree classes per group as
+    UpliftDrfMojoModel reads them (uplift = mean t00 - mean t01).  Bin splits
+    become value thresholds: code <= bin  <=>  x <= edges[f][bin]."""
+    from ..models.tree.structs import TREE_NODE_DTYPE
+
+    edges = np.asarray(model.edges, np.float32)
+    nvb = np.asarray(model.nvb, np.int64)
+    for t, tr in enumerate(model.trees):
+        m = len(tr["feat"])
+        for k, key in enumerate(("pt", "pc")):
+            a = np.zeros(m, TREE_NODE_DTYPE)
+            a["feat"], a["left"], a["na_left"] = tr["feat"], tr["left"], tr["na_left"]
+            a["bin"] = tr["bin"]
+            f = np.maximum(np.asarray(tr["feat"], np.int64), 0)
+            b = np.asarray(tr["bin"], np.int64)
+            inner = b < nvb[f] - 1
+            a["thr"] = np.where(inner, edges[f, np.minimum(b, edges.shape[1] - 1)], np.float32(np.inf))
+            a["value"] = np.asarray(tr[key], np.float32)
+            files[f"trees/t{k:02d}_{t:03d}.bin"] = _encode_tree(a)
+    return len(model.trees)
+
+
 def _uplift_info(model, info, files):
+    nt = _uplift_genmodel_trees(model, files)
+    info.update(n_trees=nt, n_trees_per_class=2, n_tree_groups=nt, init_f=0.0, distribution="bernoulli",
+                binomial_double_trees=False, default_threshold=0.5)
     for k in ("feat", "bin", "na_left", "left", "pt", "pc"):
         _put(files, info, f"uplift_{k}", np.concatenate([np.asarray(t[k], np.float64) for t in model.trees]))
     _put(files, info, "uplift_tree_sizes", [len(t["feat"]) for t in model.trees])
@@ -878,7 +906,11 @@ class GenericModel(Model):
             for i in range(len(self.te_columns)):
                 self.arr[f"te_sums_{i}"] = _get(z, info, f"te_sums_{i}")
                 self.arr[f"te_counts_{i}"] = _get(z, info, f"te_counts_{i}")
-        if a == "upliftdrf":
+        if a == "upliftdrf" and "h2omx_shape_uplift_feat" not in info:
+            # genmodel layout only: treatment (class 0) / control (class 1) trees
+            self._load_trees(z, dict(info, h2omx_average=True, h2omx_engine_dist="drf"))
+            self.uplift_trees = None
+        elif a == "upliftdrf":
             sizes = _get(z, info, "uplift_tree_sizes").astype(np.int64)
             cols = {k: _get(z, info, f"uplift_{k}") for k in ("feat", "bin", "na_left", "left", "pt", "pc")}
             self.uplift_trees, o = [], 0
@@ -990,6 +1022,9 @@ class GenericModel(Model):
             if self.category == ModelCategory.BINOMIAL:
                 return torch.stack([1 - mu, mu]).float()
             return mu[None, :].float()
+        if a == "upliftdrf" and self.uplift_trees is None:
+            m = self.ens.raw_margin(self._matrix(frame)).to(dev).float()   # [2][n]: mean p_t, mean p_c
+            return torch.stack([m[0] - m[1], m[0], m[1]])
         if a == "upliftdrf":
             from ..models.tree import bin_matrix
             from ..models.uplift import predict_tree

@@ -223,3 +223,26 @@ def test_eif_genmodel_trees(tmp_path):
     g = import_mojo(_genmodel_only(m.download_mojo(str(tmp_path)), str(tmp_path / "eif_gm.zip")))
     assert "h2omx_shape_normals" not in g.info
     _same(m.predict(fr), g.predict(fr), rtol=1e-5, atol=1e-6)
+
+
+def test_uplift_genmodel_trees(tmp_path):
+    """Uplift DRF MOJOs carry the forest in genmodel's SharedTree layout
+    (trees/t00_* treatment, trees/t01_* control leaf predictions, threshold
+    splits) and score identically when imported from those trees alone."""
+    from h2omx.models import H2OUpliftRandomForestEstimator
+
+    rng = np.random.default_rng(5)
+    n = 2500
+    X = rng.normal(size=(n, 3))
+    trt = rng.random(n) < 0.5
+    p = np.clip(0.3 + 0.1 * X[:, 1] + trt * np.where(X[:, 0] > 0, 0.3, -0.1), 0.02, 0.98)
+    df = pd.DataFrame(X, columns=list("abc"))
+    df.loc[::11, "a"] = np.nan
+    df["trt"] = pd.Categorical(np.where(trt, "treatment", "control"), categories=["control", "treatment"])
+    df["y"] = pd.Categorical(np.where(rng.random(n) < p, "1", "0"), categories=["0", "1"])
+    fr = Frame.from_pandas(df)
+    m = H2OUpliftRandomForestEstimator(ntrees=5, max_depth=4, treatment_column="trt", seed=2).train(
+        x=list("abc"), y="y", training_frame=fr)
+    g = import_mojo(_genmodel_only(m.download_mojo(str(tmp_path)), str(tmp_path / "uplift_gm.zip")))
+    assert "h2omx_shape_uplift_feat" not in g.info and int(g.info["n_trees_per_class"]) == 2
+    _same(g.predict(fr), m.predict(fr), rtol=1e-5, atol=1e-6)
