@@ -21,7 +21,7 @@ _libs: dict[str, ctypes.CDLL] = {}
 
 # library name -> source files (relative to h2omx/csrc)
 KERNEL_LIBS = {
-    "tree": ["tree_kernels.hip"],
+    "tree": ["tree_kernels.hip", "sketch_kernels.hip"],
     "dense": ["dense_kernels.hip", "kmeans_wave.hip"],
     "metrics": ["metrics_kernels.hip"],
     "explain": ["explain_kernels.hip"],

@@ -9,6 +9,7 @@ so that histogram lanes can issue 16-byte loads of 16 consecutive rows.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -117,7 +118,7 @@ def compute_edges(X: torch.Tensor, nbins: int, sample_rows: int = 1 << 20, seed:
     edges = np.full((F, nbt), np.inf, np.float32)
     nvb = np.zeros(F, np.int32)
     if S.is_cuda:
-        for f, e in enumerate(_edges_device(sort_rows(S.float()), max_value_bins)):
+        for f, e in enumerate(_edges_sketch(S.float(), max_value_bins)):
             edges[f, : e.size] = e
             nvb[f] = e.size + 1
         return edges, nvb, nbt
@@ -146,6 +147,70 @@ def sort_rows(S: torch.Tensor) -> torch.Tensor:
     keys = torch.sort(((rows << 32) | ok).view(-1)).values.view(F, m) & 0xFFFFFFFF
     back = torch.where(keys >= 0x80000000, keys & 0x7FFFFFFF, keys ^ 0xFFFFFFFF)
     return back.to(torch.int32).view(torch.float32)
+
+
+# device quantile sketch (csrc/sketch_kernels.hip); 0: sort the sample instead
+SKETCH = os.environ.get("H2OMX_SKETCH", "0") == "1"
+
+
+def _key_to_float(k: np.ndarray) -> np.ndarray:
+    k = k.astype(np.uint32)
+    b = np.where(k >= 0x80000000, k & 0x7FFFFFFF, ~k)
+    return b.astype(np.uint32).view(np.float32)
+
+
+def _edges_sketch(S: torch.Tensor, max_value_bins: int) -> list:
+    """``_edges_from_sorted`` for every row of the sample S [F][m] without
+    sorting it: the two-level radix select of csrc/sketch_kernels.hip finds
+    the numpy 'lower' quantile order statistics and the maximum exactly;
+    low-cardinality features read their distinct values off the key
+    histogram.  Features the sketch hands back (a refinement bin above 8192
+    keys, or a low-cardinality candidate with two values in one bin) take the
+    sort path."""
+    F, m = S.shape
+    if not SKETCH or m < 2:
+        return _edges_device(sort_rows(S), max_value_bins)
+    dev = S.device
+    S = S.contiguous()
+    lib = ops.tree_lib()
+    NB = int(lib.h2omx_sketch_bins())
+    qv = np.linspace(0.0, 1.0, max_value_bins + 1)[1:-1]
+    T = qv.size
+    u32 = torch.int32
+    H, P, mark, off, fill = (torch.empty((F, NB), dtype=u32, device=dev) for _ in range(5))
+    tbin, trank, okey = (torch.zeros((F, T + 1), dtype=u32, device=dev) for _ in range(3))
+    lcbin, lckey = (torch.zeros((F, 256), dtype=u32, device=dev) for _ in range(2))
+    info = torch.empty((F, 4), dtype=u32, device=dev)
+    buf = torch.empty((F, m), dtype=u32, device=dev)
+    qv_t = torch.from_numpy(qv).to(dev)
+    P_ = ops.P
+    ops.check(lib.h2omx_sketch(P_(S), S.stride(0), m, F, T, P_(qv_t), max_value_bins, P_(H), P_(P), P_(mark),
+                               P_(off), P_(fill), P_(tbin), P_(trank), P_(okey), P_(lcbin), P_(lckey), P_(info),
+                               P_(buf), ops.stream(dev)), "sketch")
+    info_h = info.cpu().numpy()
+    keys = okey.cpu().numpy().view(np.uint32)
+    lck = lckey.cpu().numpy().view(np.uint32)
+    cnt, nonempty, lowc, fb = info_h[:, 0], info_h[:, 1], info_h[:, 2], info_h[:, 3]
+    dist = {f: _key_to_float(lck[f, : nonempty[f]]) for f in range(F) if lowc[f] and not fb[f] and cnt[f] > 0}
+    sort_f = [f for f in range(F) if fb[f]]
+    sorted_out = {}
+    if sort_f:
+        for f, e in zip(sort_f, _edges_device(sort_rows(S[sort_f]), max_value_bins)):
+            sorted_out[f] = e
+    out = []
+    for f in range(F):
+        if f in sorted_out:
+            out.append(sorted_out[f])
+        elif cnt[f] == 0:
+            out.append(np.zeros(0, np.float32))
+        elif f in dist:
+            out.append(dist[f][:-1].astype(np.float32))
+        else:
+            qf = _key_to_float(keys[f])
+            e = np.unique(qf[:T])
+            e = e[e < qf[T]]
+            out.append(e[: max_value_bins - 1])
+    return out
 
 
 def _edges_device(S: torch.Tensor, max_value_bins: int) -> list:

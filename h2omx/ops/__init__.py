@@ -36,6 +36,8 @@ TREE_SIGS = {
     "h2omx_boost_update": "PPPLLPPPPPPPS",
     "h2omx_apply_tree": "PLPPS",
     "h2omx_tree_archive": "PLPIPS",
+    "h2omx_sketch_bins": "",
+    "h2omx_sketch": "PLIIIPIPPPPPPPPPPPPS",
     "h2omx_softmax_grad": "PILPPLLIPPPPPPS",
     "h2omx_oob_accumulate": "PPLPPPUIFLIS",
     "h2omx_stat_blocks": "",
