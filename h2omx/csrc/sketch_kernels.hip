@@ -16,7 +16,8 @@
 //      expression), each target's bin and its rank inside it; those bins are
 //      marked.  A feature with <= max_value_bins non-empty bins is a
 //      low-cardinality candidate instead: all its non-empty bins are marked.
-//   3. sketch_gather: the keys of marked bins into per-bin segments.
+//   3. sketch_gather: the keys of marked bins (<= 256 slots per feature) into
+//      per-bin segments, one global range claim per (chunk, slot).
 //   4. sketch_select (one workgroup per target): bitonic sort of the bin's
 //      segment in LDS (<= SK_MAX_BIN keys) and the key at the in-bin rank; a
 //      larger bin must hold one distinct key.  sketch_distinct: the single
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(1024) void sketch_plan_kernel(const unsigned int* _
   }
   unsigned int total, nonempty;
   unsigned int run = sk_block_excl_scan(local, wsum, &total);
-  unsigned int nrun = sk_block_excl_scan(ne, wsum, &nonempty);
+  sk_block_excl_scan(ne, wsum, &nonempty);
   const bool lowcand = (int)nonempty <= max_value_bins;
   for (int i = 0; i < PER; ++i) {
     const int b = t * PER + i;
@@ -125,8 +126,6 @@ __global__ __launch_bounds__(1024) void sketch_plan_kernel(const unsigned int* _
     run += c;
     const bool used = c != 0u && b != SK_BINS - 1;
     mk[b] = (lowcand && used) ? 1 : 0;
-    if (lowcand && used) lcbin[f * 256 + (int)nrun] = b;
-    nrun += used ? 1u : 0u;
   }
   __syncthreads();
   const int cnt = (int)(total - h[SK_BINS - 1]);   // non-NaN samples
@@ -147,17 +146,25 @@ __global__ __launch_bounds__(1024) void sketch_plan_kernel(const unsigned int* _
     }
   }
   __syncthreads();
-  // 3. segment offsets of the marked bins
+  // 3. segment offsets of the marked bins, and their slot ids (ascending bin
+  //    order, <= 256 per feature): mark[b] = slot + 1, lcbin[f][slot] = b
   local = 0;
+  unsigned int nm = 0;
   for (int i = 0; i < PER; ++i) {
     const int b = t * PER + i;
-    if (mk[b]) local += h[b];
+    if (mk[b]) { local += h[b]; ++nm; }
   }
   run = sk_block_excl_scan(local, wsum, nullptr);
+  unsigned int srun = sk_block_excl_scan(nm, wsum, nullptr);
   for (int i = 0; i < PER; ++i) {
     const int b = t * PER + i;
     of[b] = run;
-    if (mk[b]) run += h[b];
+    if (mk[b]) {
+      run += h[b];
+      mk[b] = (int)srun + 1;
+      lcbin[f * 256 + (int)srun] = b;
+      ++srun;
+    }
   }
   if (t == 0) {
     info[4 * f + 0] = cnt;
@@ -167,44 +174,41 @@ __global__ __launch_bounds__(1024) void sketch_plan_kernel(const unsigned int* _
   }
 }
 
-__global__ __launch_bounds__(256) void sketch_gather_kernel(const float* __restrict__ S, int64_t ld, int m,
-                                                            const int* __restrict__ mark,
-                                                            const unsigned int* __restrict__ off,
-                                                            unsigned int* __restrict__ fill,
-                                                            unsigned int* __restrict__ buf) {
+// one 1024-thread workgroup per (chunk of SK_CHUNK samples, feature): marked
+// samples counted per slot in LDS, one global claim per (chunk, slot), then a
+// second pass writes each sample into its claimed range (LDS slot cursors)
+__global__ __launch_bounds__(1024) void sketch_gather_kernel(const float* __restrict__ S, int64_t ld, int m,
+                                                             const int* __restrict__ mark,
+                                                             const unsigned int* __restrict__ off,
+                                                             const int* __restrict__ lcbin,
+                                                             unsigned int* __restrict__ fill,
+                                                             unsigned int* __restrict__ buf) {
+  __shared__ unsigned int cnt[256], base[256];
   const int f = blockIdx.y;
   const int* mk = mark + (int64_t)f * SK_BINS;
-  const unsigned int* of = off + (int64_t)f * SK_BINS;
-  unsigned int* fl = fill + (int64_t)f * SK_BINS;
   unsigned int* out = buf + (int64_t)f * m;
   const float* col = S + (int64_t)f * ld;
-  // wave-aggregated slot claims: one atomic per distinct marked bin of the
-  // wave (a low-cardinality feature sends whole waves into one bin)
-  const int lane = threadIdx.x & 63;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  const int64_t step = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < m; i0 += step) {
-    const int64_t i = i0 + lane;
-    uint32_t k = 0u;
-    int b = 0;
-    bool want = false;
-    if (i < m) {
-      k = sk_key(col[i]);
-      b = (int)(k >> 16);
-      want = mk[b] != 0;
+  const int i0 = blockIdx.x * SK_CHUNK, i1 = min(m, i0 + SK_CHUNK);
+  if (threadIdx.x < 256) cnt[threadIdx.x] = 0u;
+  __syncthreads();
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int sl = mk[sk_key(col[i]) >> 16] - 1;
+    if (sl >= 0) atomicAdd(&cnt[sl], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    const unsigned int c = cnt[threadIdx.x];
+    if (c) {
+      const int b = lcbin[f * 256 + threadIdx.x];
+      base[threadIdx.x] = off[(int64_t)f * SK_BINS + b] + atomicAdd(fill + (int64_t)f * SK_BINS + b, c);
     }
-    unsigned long long pend = __ballot(want);
-    while (pend) {
-      const int leader = __ffsll((long long)pend) - 1;
-      const int lb = __shfl(b, leader, 64);
-      const bool mine = want && b == lb;
-      const unsigned long long mask = __ballot(mine);
-      unsigned int base = 0u;
-      if (lane == leader) base = atomicAdd(fl + lb, (unsigned int)__popcll(mask));
-      base = __shfl(base, leader, 64);
-      if (mine) out[of[lb] + base + __popcll(mask & lt)] = k;
-      pend &= ~mask;
-    }
+    cnt[threadIdx.x] = 0u;
+  }
+  __syncthreads();
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const uint32_t k = sk_key(col[i]);
+    const int sl = mk[k >> 16] - 1;
+    if (sl >= 0) out[base[sl] + atomicAdd(&cnt[sl], 1u)] = k;
   }
 }
 
@@ -317,8 +321,8 @@ H2OMX_API int h2omx_sketch(const float* S, int64_t ld, int m, int F, int T, cons
   hipLaunchKernelGGL(sketch_hist_kernel, dim3(chunks, F), dim3(1024), 0, stream, S, ld, m, H);
   hipLaunchKernelGGL(sketch_plan_kernel, dim3(F), dim3(1024), 0, stream, H, T, qv, max_value_bins, P, tbin, trank,
                      mark, off, lcbin, info);
-  const int gx = (int)std::min<int64_t>((m + 255) / 256, 512);
-  hipLaunchKernelGGL(sketch_gather_kernel, dim3(gx, F), dim3(256), 0, stream, S, ld, m, mark, off, fill, buf);
+  hipLaunchKernelGGL(sketch_gather_kernel, dim3(chunks, F), dim3(1024), 0, stream, S, ld, m, mark, off, lcbin, fill,
+                     buf);
   hipLaunchKernelGGL(sketch_select_kernel, dim3(T + 1, F), dim3(1024), 0, stream, H, m, T, tbin, trank, off, info,
                      buf, out_key);
   hipLaunchKernelGGL(sketch_distinct_kernel, dim3(256, F), dim3(1024), 0, stream, H, m, lcbin, off, info, buf,

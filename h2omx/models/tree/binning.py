@@ -150,7 +150,7 @@ def sort_rows(S: torch.Tensor) -> torch.Tensor:
 
 
 # device quantile sketch (csrc/sketch_kernels.hip); 0: sort the sample instead
-SKETCH = os.environ.get("H2OMX_SKETCH", "0") == "1"
+SKETCH = os.environ.get("H2OMX_SKETCH", "1") == "1"
 
 
 def _key_to_float(k: np.ndarray) -> np.ndarray:
