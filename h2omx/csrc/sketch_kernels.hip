@@ -35,6 +35,7 @@ constexpr int SK_MAX_BIN = 8192;     // largest bin refined in LDS (32 KB of key
 
 __device__ __forceinline__ uint32_t sk_key(float v) {
   if (v != v) return 0xFFFFFFFFu;    // NaN: sorts last, alone in the last bin
+  if (v == 0.0f) return 0x80000000u;  // -0 == +0 (one value, as numpy's unique / sort compare)
   const uint32_t b = __float_as_uint(v);
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }

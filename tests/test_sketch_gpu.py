@@ -21,6 +21,8 @@ def _cols(n, seed=0):
         np.where(rng.random(n) < 0.6, np.nan, rng.uniform(-2, 2, n)),  # NaN heavy
         np.full(n, np.nan),                                   # all NaN
         np.round(rng.exponential(1.0, n), 2),                 # many ties, > 255 distinct
+        np.round(rng.normal(size=n), 1),                      # -0.0 and +0.0 (one value)
+        np.round(rng.normal(size=n) * 30, 0),                 # signed zeros, > 255 distinct
         rng.uniform(0, 1, n).astype(np.float32).astype(float) * 1e-30,   # tiny magnitudes
     ]
     return np.stack(cols).astype(np.float32)
