@@ -37,12 +37,15 @@ class _Dispatch:
             return dev_attr                       # shared constants (FAMILIES, LINKS, ...)
 
         def call(*args, **kw):
-            first = next((a for a in args if isinstance(a, torch.Tensor)), None)
-            if first is None:
-                first = next((a for a in args if isinstance(a, (list, tuple)) and a
-                              and isinstance(a[0], (list, tuple)) and isinstance(a[0][0], torch.Tensor)), None)
-                first = first[0][0] if first is not None else None
-            mod = self._device() if (first is not None and first.is_cuda) else self._hostmod()
+            # device path if ANY tensor argument lives on the GPU (a host tensor in
+            # the first position must not route a GPU fit to the NumPy oracle)
+            tensors = [a for a in list(args) + list(kw.values()) if isinstance(a, torch.Tensor)]
+            for a in args:
+                if isinstance(a, (list, tuple)) and a and isinstance(a[0], (list, tuple)) and a[0] \
+                        and isinstance(a[0][0], torch.Tensor):
+                    tensors.append(a[0][0])
+            on_gpu = any(t.is_cuda for t in tensors)
+            mod = self._device() if on_gpu else self._hostmod()
             return getattr(mod, name)(*args, **kw)
 
         call.__name__ = name

@@ -219,3 +219,22 @@ def test_deeplearning_bf16_precision_gpu(cuda_dev):
     r = H2ODeepLearningEstimator(hidden=[32], epochs=3, seed=1, activation="Tanh", precision="bf16").train(
         y="x0", training_frame=fr)
     assert np.isfinite(r.training_metrics["MSE"]) and r.training_metrics["MSE"] < 1.0
+
+
+def test_gpu_fits_never_touch_the_cpu_reference(cuda_dev):
+    """The backend router sends every op with a device tensor to the HIP layer:
+    GBM / XGBoost / DRF / GLM / DL / K-Means fits on a GPU frame import no
+    module of h2omx.reference (fresh interpreter)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, os.path.join(here, "_gpu_no_reference_worker.py")], capture_output=True,
+                       text=True, timeout=300, cwd=root, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["reference_loaded"] == [], out
