@@ -373,7 +373,12 @@ constexpr int CMP_STAGE_BYTES = 2048;   // per wave
 #endif
 constexpr int HB_PF = H2OMX_HB_PF;     // feature code loads kept in flight per lane
 
-template <int NBT, int ROWS, int PKM, bool ROUTE, bool CMP>
+// COP > 1 (level 0, PKM 1 / 3): every (slot, feature, bin) entry is COP
+// interleaved u64 copies, [bin][copy], lane l adding into copy l % COP: the
+// 16 lanes of a ds_add_u64 group then hit at most two addresses per bank pair
+// (bench_micro/lds_atomics.hip: random bins 14.4 CU-cycles per wave-atomic,
+// conflict-free 7.3), at COP x the LDS per feature (fewer features per group)
+template <int NBT, int ROWS, int PKM, bool ROUTE, bool CMP, int COP = 1>
 __global__ __launch_bounds__(1024) void hist_build_kernel(
     const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ s2,
     const int* __restrict__ nid, const NodeLink* __restrict__ link, const int* __restrict__ ctl,
@@ -396,16 +401,18 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
   if (!build && !route_w) return;
   const int f0 = group * fg;
   const int nf = min(fg, F - f0);
+  static_assert(COP == 1 || ((PKM == 1 || PKM == 3) && !ROUTE && !CMP), "copies: level-0 kernel only");
   const int hist_elems = slot_cnt * fg * NBT;
   const int lane = threadIdx.x & 63;
 
-  for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) lds64[j] = 0ull;
+  for (int j = threadIdx.x; j < hist_elems * COP; j += blockDim.x) lds64[j] = 0ull;
   if (threadIdx.x < fg) {
     const int fi = threadIdx.x;
     const int w = (fi < nf) ? nvb[f0 + fi] + 1 : NBT;
     width_s[fi] = w;
     int r = NBT / w;
     r = r < 1 ? 1 : (r > 64 ? 64 : r);
+    if (COP > 1) r = 1;   // the copies already spread the lanes
     rep_s[fi] = r;
     rcp_s[fi] = 1.0f / (float)r;   // lane % rep without an integer division (lane < 64: exact)
   }
@@ -760,6 +767,13 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
                 atomicAdd(hb + so[r] + bin, pk[r]);
               }
             }
+          } else if (COP > 1) {
+            // interleaved copies: entry (slot, fi, bin) at ((slot * fg + fi) * NBT + bin) * COP + copy
+            unsigned long long* hb = lds64 + fi * NBT * COP + (lane & (COP - 1));
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+              if (so[r] >= 0) atomicAdd(hb + (so[r] + ((cw[r >> 2] >> (8 * (r & 3))) & 0xff)) * COP, pk[r]);
+            }
           } else {
             // one NBT-wide slice: the NA code NBT - 1 is its own slot (no remap)
             unsigned long long* hb = lds64 + fi * NBT;
@@ -775,6 +789,16 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
   __syncthreads();
   // fold the lane copies and write this workgroup's slab (plain stores)
   unsigned long long* out = partials + (int64_t)(group * wgpg + chunk) * hist_elems;
+  if constexpr (COP > 1) {
+    // fold the copies (rotated start: the threads of a lane group read different banks)
+    for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) {
+      unsigned long long acc = 0ull;
+#pragma unroll
+      for (int c = 0; c < COP; ++c) acc += lds64[j * COP + ((c + j) & (COP - 1))];
+      out[j] = acc;
+    }
+    return;
+  }
   for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) {
     const int bin = j % NBT;
     const int fi = (j / NBT) % fg;
@@ -2681,7 +2705,10 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
   if (gfp) gfz = *gfp;
   // pkm bit 3: wave-compacted atomics (CMP; stored rows, 16-row units, <= 64 slots per pass)
   const bool cmp = (pkm & 8) != 0;
+  // pkm bit 4 / 5: level-0 histograms in 8 / 4 interleaved lane copies (PKM 1 / 3 only)
+  const int cop = (pkm & 16) ? 8 : ((pkm & 32) ? 4 : 1);
   pkm &= 7;
+  if (cop > 1 && ((pkm != 1 && pkm != 3) || route || cmp)) return kBadArg;
   if (cmp && ((pkm != 2 && pkm != 4) || rows_per_lane != 16 || slot_cnt > 64)) return kBadArg;
   if (route && (ctl_prev == nullptr || nid_out == nullptr || nid_out == nid || (pkm != 2 && pkm != 4)))
     return kBadArg;
@@ -2697,7 +2724,7 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
     return kBadArg;
   const int64_t units = npad / rows_per_lane;
   if ((units + wgpg - 1) / wgpg * rows_per_lane > ROWS_CAP) return kBadArg;  // fixed-point headroom
-  const size_t lds = (size_t)slot_cnt * fg * nbt * sizeof(unsigned long long) +
+  const size_t lds = (size_t)slot_cnt * fg * nbt * cop * sizeof(unsigned long long) +
                      (cmp ? (size_t)(threads / 64) * CMP_STAGE_BYTES : 0);
   if (lds > 156 * 1024) return kBadArg;
   const int grid = n_groups * wgpg;
@@ -2706,9 +2733,17 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
   hipLaunchKernelGGL((hist_build_kernel<NB, R, M, RT, C>), dim3(grid), dim3(threads), lds, stream, codes, npad, \
                      g, s2, nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt,  \
                      slot16, pk_buf, partials, pp, ctl_prev, nid_out, writer, gfz)
+#define H2OMX_HBKC(NB, R, M, CP)                                                                                \
+  hipLaunchKernelGGL((hist_build_kernel<NB, R, M, false, false, CP>), dim3(grid), dim3(threads), lds, stream, codes, \
+                     npad, g, s2, nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo,        \
+                     slot_cnt, slot16, pk_buf, partials, pp, ctl_prev, nid_out, writer, gfz)
 #define H2OMX_HB(NB, R)                                            \
   do {                                                             \
     if (pkm == 0) H2OMX_HBK(NB, R, 0, false, false);               \
+    else if (pkm == 1 && cop == 8) H2OMX_HBKC(NB, R, 1, 8);        \
+    else if (pkm == 3 && cop == 8) H2OMX_HBKC(NB, R, 3, 8);        \
+    else if (pkm == 1 && cop == 4) H2OMX_HBKC(NB, R, 1, 4);        \
+    else if (pkm == 3 && cop == 4) H2OMX_HBKC(NB, R, 3, 4);        \
     else if (pkm == 1) H2OMX_HBK(NB, R, 1, false, false);          \
     else if (pkm == 2 && route) H2OMX_HBK(NB, R, 2, true, false);  \
     else if (pkm == 2) H2OMX_HBK(NB, R, 2, false, false);          \
@@ -2754,6 +2789,7 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
 #undef H2OMX_HB
 #undef H2OMX_HBCMP
 #undef H2OMX_HBK
+#undef H2OMX_HBKC
   return launch_status();
 }
 

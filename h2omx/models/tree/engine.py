@@ -328,8 +328,21 @@ class HipTreeBuilder:
     # column load per distinct split feature) instead of partition_kernel's gathers
     ROUTE_KERNEL = os.environ.get("H2OMX_ROUTE_KERNEL", "0") == "1"
 
-    def _plan(self, max_slots: int, budget: int, threads: int, units: int | None = None):
-        per_slot_feat = self.nbt * 8
+    # level 0 of the scan engine: histograms in 8 interleaved lane copies
+    # (hist_build COP: fewer LDS bank conflicts, 8x the LDS per feature, so
+    # feature groups of DEEP_LDS_BUDGET); 1 = plain slices
+    L0_COPIES = int(os.environ.get("H2OMX_HIST_L0_COPIES", "8"))
+
+    def plan_l0(self):
+        key = ("l0", self.L0_COPIES)
+        if key not in self.plans:
+            plan = self._plan(1, self.DEEP_LDS_BUDGET, self.THREADS, mult=self.L0_COPIES)
+            plan["cmp"] = False
+            self.plans[key] = plan
+        return self.plans[key]
+
+    def _plan(self, max_slots: int, budget: int, threads: int, units: int | None = None, mult: int = 1):
+        per_slot_feat = self.nbt * 8 * mult
         F = self.F
         if max_slots * per_slot_feat <= budget:
             slot_cnt = max_slots
@@ -466,6 +479,9 @@ class HipTreeBuilder:
             last = d == max_depth - 1
             plan = self.plan_level(max_slots, cmp=d > 0 and self.CMP and not self.COMPACT)
             cmp_flag = 8 if plan["cmp"] else 0
+            l0_copies = d == 0 and grad_fuse is None and self.L0_COPIES in (4, 8)
+            if l0_copies:
+                plan = self.plan_l0()
             built = self._buf("built", max_slots * self.per_node, torch.int64)
             hist_elems = plan["slot_cnt"] * plan["fg"] * nbt
             partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_elems, torch.int64)
@@ -532,7 +548,8 @@ class HipTreeBuilder:
                             P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, plan["fg"], plan["n_groups"],
                             plan["wgpg"], slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],
                             P(self.slot16), P(self.pk),
-                            (1 if d == 0 else 2 + cmp_flag) + (2 if self.pk32 else 0), P(partials), st),
+                            (1 if d == 0 else 2 + cmp_flag) + (2 if self.pk32 else 0) + ({8: 16, 4: 32}.get(self.L0_COPIES, 0) if l0_copies else 0),
+                            P(partials), st),
                             "hist_build")
                 with T("hist_reduce"):
                     ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F,
