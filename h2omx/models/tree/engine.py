@@ -341,6 +341,27 @@ class HipTreeBuilder:
             self.plans[key] = plan
         return self.plans[key]
 
+    # grids that overflow one round of resident workgroups are widened to fill
+    # their last round: the chunk cap (ROWS_CAP) puts Airlines-shape 18.75M rows
+    # at 72 x 4 = 288 one-per-CU workgroups, so 32 of them ran alone in a
+    # second round
+    FILL_ROUNDS = os.environ.get("H2OMX_HIST_FILL", "1") == "1"
+    N_CUS = 256
+    MAX_WG_THREADS_PER_CU = 2048      # 32 waves per CU
+
+    def _fill_rounds(self, wgpg: int, n_groups: int, lds_bytes: int, threads: int, units: int) -> int:
+        per_cu = max(1, min((160 * 1024) // max(1, lds_bytes + 3072), self.MAX_WG_THREADS_PER_CU // threads))
+        resident = self.N_CUS * per_cu
+        total = n_groups * wgpg
+        if total <= resident:
+            return wgpg
+        rounds = math.ceil(total / resident)
+        fill = (rounds * resident // n_groups) // 8 * 8
+        # keep >= 1 row unit per lane
+        if fill > wgpg and fill * threads <= units:
+            return fill
+        return wgpg
+
     def _plan(self, max_slots: int, budget: int, threads: int, units: int | None = None, mult: int = 1):
         per_slot_feat = self.nbt * 8 * mult
         F = self.F
@@ -363,6 +384,8 @@ class HipTreeBuilder:
         cap = self.ROWS_CAP if self.max_rows_per_wg is None else min(self.ROWS_CAP, self.max_rows_per_wg)
         min_wgpg = math.ceil(math.ceil(units / (cap // self.ROWS_PER_LANE)) / 8) * 8
         wgpg = max(wgpg, min_wgpg)
+        if self.FILL_ROUNDS:
+            wgpg = self._fill_rounds(wgpg, n_groups, slot_cnt * fg * per_slot_feat, threads, units)
         return dict(slot_cnt=slot_cnt, fg=fg, n_groups=n_groups, passes=passes, wgpg=wgpg, threads=threads)
 
     def plan_level(self, max_slots: int, cmp: bool = False):
