@@ -235,8 +235,9 @@ def mojo_bytes(model: Model) -> bytes:
     elif algo in ARRAY_ALGOS:
         columns = list(model.x)
         if algo == "gam":
-            basis = {f"{c}_cr_{i}" for c, sp in model.gam_spec.items() for i in range(sp["Z"].shape[1])}
-            columns = [c for c in model.x if c not in basis] + [c for c in model.gam_spec if c not in model.x]
+            # genmodel GAM column order: categorical, numeric, then the gam columns
+            cats, nums = _gam_design_columns(model)
+            columns = cats + nums + [c for c in model.gam_spec if c not in cats + nums]
         info.update(_array_info(model, files))
     elif algo == "generic":
         return model.raw_mojo
@@ -727,7 +728,66 @@ def _array_info(model, files):
             _put(files, info, f"gam_F_{i}", sp["F"])
             _put(files, info, f"gam_Z_{i}", sp["Z"])
             info[f"gam_mean_{i}"] = float(sp["mean"])
+        _gam_genmodel(model, info, files)
     return info
+
+
+def _gam_design_columns(model):
+    """(categorical, numeric) non-gam predictors of a GAM, DataInfo order."""
+    basis = {f"{c}_cr_{i}" for c, sp in model.gam_spec.items() for i in range(sp["Z"].shape[1])}
+    cats, nums = _design_columns(model.design)
+    return [c for c in cats if c not in basis], [c for c in nums if c not in basis]
+
+
+def _gam_genmodel(model, info, files):
+    """GamMojoReader-style entries: the GLM part (cats / cat_offsets / nums, NA
+    fills, coefficients over [one-hot cats, nums, centred gam basis columns,
+    intercept] on the original scale: ``beta_center``; the same with every gam
+    column's basis un-centred through Z: ``beta``), the spline settings
+    (``gam_columns``, ``num_knots``, ``bs``, the gam columns' NA fills) and
+    big-endian float64 blobs ``knots`` (per column, concatenated), ``binvD``
+    (B^-1 D, (k-2) x k) and ``zTranspose`` (Z^T, (k-1) x k).  No genmodel jar
+    exists here, so byte parity with H2O's GamMojoWriter is unpinned; h2omx
+    imports GAM MOJOs from these entries alone (tests/test_mojo_more.py)."""
+    d = model.design
+    cats, nums = _gam_design_columns(model)
+    spec = model.gam_spec
+    basis = [f"{c}_cr_{i}" for c, sp in spec.items() for i in range(sp["Z"].shape[1])]
+    pos = {n: i for i, n in enumerate(d.names)}
+    order = _reorder(d.names, d, cats, nums) + [pos[b] for b in basis]
+    beta = np.asarray(model.beta, np.float64).reshape(-1, len(d.names) + 1)
+    centre, full = [], []
+    for k in range(beta.shape[0]):
+        bc = [float(beta[k, i]) for i in order] + [float(beta[k, -1])]
+        centre += bc
+        nb = len(order) - len(basis)
+        row, o = bc[:nb], nb
+        for c, sp in spec.items():
+            kc = sp["Z"].shape[1]
+            row += [float(v) for v in np.asarray(sp["Z"]) @ np.asarray(bc[o:o + kc])]
+            o += kc
+        full += row + [bc[-1]]
+    offs = [0]
+    for c in cats:
+        offs.append(offs[-1] + sum(1 for cc, _ in d.spec if cc == c))
+    num_means = [float(d.means[[i for i, (cc, _) in enumerate(d.spec) if cc == c][0]]) for c in nums]
+    # NA categorical: each one-hot column takes its training mean (DesignInfo.transform)
+    cat_level_means = [float(d.means[i]) for i in _reorder(d.names, d, cats, [])]
+    knots =[np.asarray(sp["knots"], np.float64) for sp in spec.values()]
+    info.update({
+        "use_all_factor_levels": bool(d.use_all_levels), "cats": len(cats), "cat_offsets": offs, "nums": len(nums),
+        "mean_imputation": True, "num_means": num_means, "cat_level_means": cat_level_means,
+        "beta_center": centre, "beta": full,
+        "beta center length per class": len(order) + 1, "beta length per class": len(full) // beta.shape[0],
+        "gam_columns": list(spec), "num_knots": [int(k.size) for k in knots], "bs": [0] * len(spec),
+        "num_expanded_gam_columns": int(sum(k.size for k in knots)),
+        "num_expanded_gam_columns_center": int(sum(k.size - 1 for k in knots)),
+        "gam_col_means": [float(sp["mean"]) for sp in spec.values()]})
+    files["knots"] = np.concatenate(knots).astype(">f8").tobytes()
+    files["binvD"] = np.concatenate([np.asarray(sp["F"], np.float64)[1:-1].ravel() for sp in spec.values()]
+                                    ).astype(">f8").tobytes()
+    files["zTranspose"] = np.concatenate([np.asarray(sp["Z"], np.float64).T.ravel() for sp in spec.values()]
+                                         ).astype(">f8").tobytes()
 
 
 def export_mojo(model: Model, path: str) -> str:
@@ -880,7 +940,7 @@ class GenericModel(Model):
                  "isotonicregression": ("thresholds_x", "thresholds_y"), "coxph": ("coef", "x_mean_num"),
                  "extendedisolationforest": ("normals", "offsets", "leaf_sizes"), "gam": ("beta",)}.get(a, ())
         for nm in names:
-            if f"h2omx_shape_{nm}" not in info and (a == "isotonicregression" or eif_gm):
+            if f"h2omx_shape_{nm}" not in info and (a in ("isotonicregression", "gam") or eif_gm):
                 continue   # H2O-written MOJO: genmodel key/values below
             self.arr[nm] = _get(z, info, nm)
         if a == "isotonicregression" and "thresholds_x" not in self.arr:
@@ -931,7 +991,25 @@ class GenericModel(Model):
                 self.words = z.read("vocabulary").decode().split("\n")[:nv]
                 vec = np.frombuffer(z.read("vectors"), dtype=">f4", count=nv * vs).reshape(nv, vs)
                 self.vectors = torch.from_numpy(vec.astype(np.float32))
-        if a == "gam":
+        if a == "gam" and "h2omx_design_x" not in info:
+            # H2O-layout GAM MOJO: splines from the knots / binvD / zTranspose blobs
+            def _lst(v):
+                return v if isinstance(v, list) else [v]
+
+            gcols, nk = _lst(info["gam_columns"]), [int(k) for k in _lst(info["num_knots"])]
+            gm = [float(v) for v in _lst(info.get("gam_col_means", [0.0] * len(gcols)))]
+            kn, bd, zt = (np.frombuffer(z.read(n), dtype=">f8").astype(np.float64)
+                          for n in ("knots", "binvD", "zTranspose"))
+            self.gam_spec, o1, o2, o3 = {}, 0, 0, 0
+            for c, k, mean in zip(gcols, nk, gm):
+                F = np.zeros((k, k))
+                F[1:-1] = bd[o2:o2 + (k - 2) * k].reshape(k - 2, k)
+                self.gam_spec[c] = {"knots": kn[o1:o1 + k].copy(), "F": F,
+                                    "Z": zt[o3:o3 + (k - 1) * k].reshape(k - 1, k).T.copy(), "mean": mean}
+                o1, o2, o3 = o1 + k, o2 + (k - 2) * k, o3 + (k - 1) * k
+                self.feature_types[c] = "real"
+            self.gam_genmodel = True
+        elif a == "gam":
             dx = info["h2omx_design_x"]
             for n in (dx if isinstance(dx, list) else [dx]):
                 self.feature_types.setdefault(n, "real")
@@ -1041,6 +1119,28 @@ class GenericModel(Model):
             k = max(len(self.uplift_trees), 1)
             pt, pc = (pt / k).float(), (pc / k).float()
             return torch.stack([pt - pc, pt, pc]).to(dev)
+        if a == "gam" and getattr(self, "gam_genmodel", False):
+            from ..models.gam import cr_basis
+            from ..models.glm import _torch_linkinv
+
+            nc, nn = int(info["cats"]), int(info["nums"])
+            X = self._matrix(frame).double()
+            lm = info.get("cat_level_means", [])
+            means = (lm if isinstance(lm, list) else [lm]) + list(info.get("num_means") or [])
+            parts = [self._expand(X[: nc + nn], bool(info["use_all_factor_levels"]), means=means or None)]
+            for j, (c, sp) in enumerate(self.gam_spec.items()):
+                x = X[nc + nn + j]
+                x = torch.where(torch.isnan(x), torch.full_like(x, sp["mean"]), x)
+                parts.append((cr_basis(x, sp["knots"], sp["F"]) @ torch.from_numpy(sp["Z"]).to(dev)).T)
+            Zd = torch.cat(parts)
+            beta = torch.tensor(info["beta_center"], dtype=torch.float64, device=dev).view(-1, Zd.shape[0] + 1)
+            eta = beta[:, :-1] @ Zd + beta[:, -1:]
+            if info["family"] == "multinomial":
+                return torch.softmax(eta, 0).float()
+            mu = _torch_linkinv(eta[0], info["link"], info.get("tweedie_link_power", 0.0))
+            if self.category == ModelCategory.BINOMIAL:
+                return torch.stack([1 - mu, mu]).float()
+            return mu[None, :].float()
         if a == "gam":
             from ..models.gam import _augment
 

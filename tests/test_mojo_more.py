@@ -246,3 +246,32 @@ def test_uplift_genmodel_trees(tmp_path):
     g = import_mojo(_genmodel_only(m.download_mojo(str(tmp_path)), str(tmp_path / "uplift_gm.zip")))
     assert "h2omx_shape_uplift_feat" not in g.info and int(g.info["n_trees_per_class"]) == 2
     _same(g.predict(fr), m.predict(fr), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("family", ["gaussian", "binomial"])
+def test_gam_genmodel_entries(family, tmp_path):
+    """GAM MOJOs carry GamMojoReader-style entries (cats / nums / NA fills,
+    centred and un-centred coefficients, gam_columns / num_knots / bs and the
+    big-endian knots / binvD / zTranspose blobs) and score identically when
+    imported from those alone (categorical + NA predictors, two gam columns)."""
+    import zipfile
+
+    df = _df()
+    df.loc[::13, "g"] = np.nan
+    df.loc[::7, "a"] = np.nan
+    fr = Frame.from_pandas(df)
+    y = "y" if family == "gaussian" else "yb"
+    m = H2OGeneralizedAdditiveEstimator(family=family, gam_columns=["a", "c"], num_knots=[6, 5], lambda_=0.0).train(
+        x=["a", "b", "c", "g"], y=y, training_frame=fr)
+    path = m.download_mojo(str(tmp_path))
+    with zipfile.ZipFile(path) as z:
+        ini = z.read("model.ini").decode()
+        knots = np.frombuffer(z.read("knots"), dtype=">f8")
+        zt = np.frombuffer(z.read("zTranspose"), dtype=">f8")
+    kv = dict(ln.split(" = ", 1) for ln in ini.split("\n") if " = " in ln)
+    assert kv["num_knots"] == "[6, 5]" and int(kv["cats"]) == 1 and int(kv["nums"]) == 1
+    np.testing.assert_array_equal(knots[:6], m.gam_spec["a"]["knots"])
+    np.testing.assert_array_equal(zt[:30].reshape(5, 6), m.gam_spec["a"]["Z"].T)
+    g = import_mojo(_genmodel_only(path, str(tmp_path / "gam_gm.zip")))
+    assert getattr(g, "gam_genmodel", False)
+    np.testing.assert_allclose(g.predict_raw(fr).numpy(), m.predict_raw(fr).numpy(), rtol=1e-4, atol=1e-5)
