@@ -347,6 +347,7 @@ class HipTreeBuilder:
     # second round
     FILL_ROUNDS = os.environ.get("H2OMX_HIST_FILL", "1") == "1"
     N_CUS = 256
+    SMALL_SHARD = os.environ.get("H2OMX_HIST_SMALL", "1") == "1"
     MAX_WG_THREADS_PER_CU = 2048      # 32 waves per CU
 
     def _fill_rounds(self, wgpg: int, n_groups: int, lds_bytes: int, threads: int, units: int) -> int:
@@ -377,11 +378,27 @@ class HipTreeBuilder:
             passes = math.ceil(max_slots / slot_cnt)
         if units is None:
             units = self.bm.npad // self.ROWS_PER_LANE
-        target = self.TARGET_WGS * 512 // threads
-        wgpg = max(8, (target // n_groups) // 8 * 8)
-        max_wgpg = max(8, (units // (threads * 2)) // 8 * 8)   # keep >= ~2 row units per lane
-        wgpg = min(wgpg, max_wgpg)
-        cap = self.ROWS_CAP if self.max_rows_per_wg is None else min(self.ROWS_CAP, self.max_rows_per_wg)
+        def target(t: int) -> int:
+            return max(8, (self.TARGET_WGS * 512 // t // n_groups) // 8 * 8)
+
+        def grid(t: int, upl: int) -> int:
+            return min(target(t), max(8, (units // (t * upl)) // 8 * 8))   # keep >= upl row units per lane
+
+        wgpg = grid(threads, 2)
+        if self.SMALL_SHARD and n_groups * wgpg < self.N_CUS and wgpg < target(threads):
+            # small shards (strong scaling: 11M / 8 ranks = 86K row units) put the
+            # 2-units-per-lane grid on a fraction of the CUs (level 1: 40 of 256
+            # workgroups); spread them over every CU with 1 unit per lane and, if
+            # still short, more feature groups (the re-read rows of a small shard
+            # stay in L2 / MALL; narrower 512 / 256-thread workgroups measured slower)
+            wgpg = grid(threads, 1)
+            if n_groups * wgpg < self.N_CUS and passes == 1:
+                ng = min(F, math.ceil(self.N_CUS / wgpg))
+                if ng > n_groups:
+                    fg = math.ceil(F / ng)
+                    n_groups = math.ceil(F / fg)
+                    wgpg = grid(threads, 1)
+        cap =self.ROWS_CAP if self.max_rows_per_wg is None else min(self.ROWS_CAP, self.max_rows_per_wg)
         min_wgpg = math.ceil(math.ceil(units / (cap // self.ROWS_PER_LANE)) / 8) * 8
         wgpg = max(wgpg, min_wgpg)
         if self.FILL_ROUNDS:
