@@ -348,6 +348,7 @@ class HipTreeBuilder:
     FILL_ROUNDS = os.environ.get("H2OMX_HIST_FILL", "1") == "1"
     N_CUS = 256
     SMALL_SHARD = os.environ.get("H2OMX_HIST_SMALL", "1") == "1"
+    MIN_GROUPS = int(os.environ.get("H2OMX_HIST_MIN_GROUPS", "1"))   # A/B knob
     MAX_WG_THREADS_PER_CU = 2048      # 32 waves per CU
 
     def _fill_rounds(self, wgpg: int, n_groups: int, lds_bytes: int, threads: int, units: int) -> int:
@@ -376,8 +377,12 @@ class HipTreeBuilder:
             fg, n_groups = 1, F
             slot_cnt = max(1, budget // per_slot_feat)
             passes = math.ceil(max_slots / slot_cnt)
+        if passes == 1 and self.MIN_GROUPS > n_groups and mult == 1:
+            fg = math.ceil(F / min(F, self.MIN_GROUPS))
+            n_groups = math.ceil(F / fg)
         if units is None:
             units = self.bm.npad // self.ROWS_PER_LANE
+
         def target(t: int) -> int:
             return max(8, (self.TARGET_WGS * 512 // t // n_groups) // 8 * 8)
 
