@@ -1935,6 +1935,63 @@ __global__ __launch_bounds__(1024) void split_level_kernel(
                         tree_capacity);
 }
 
+// split_find with the per-node arg-max and the level finalisation handed to
+// the LAST block to finish (agent-scope release / ticket / acquire, as
+// split_level_kernel), keeping split_find's grid (nodes x ceil(F / 4) blocks,
+// one wave per feature): the separate node_best_finalize launch per level
+// disappears without split_level's one-workgroup-per-node scan.  Every block
+// takes a ticket (also blocks past the live node count) so the last one is
+// well defined; it resets the ticket.  Levels of <= 64 nodes (host check).
+template <int NBT>
+__global__ __launch_bounds__(256) void split_find_fin_kernel(
+    const long long* __restrict__ built, const long long* __restrict__ parent_full, long long* __restrict__ full,
+    const int* __restrict__ ctl, const NodeLink* __restrict__ link, const int* __restrict__ nvb,
+    const uint8_t* __restrict__ tree_fmask, const double* __restrict__ qscale, SplitParams p,
+    FeatBest* __restrict__ fbest, unsigned int* __restrict__ ticket, int* __restrict__ ctl_next,
+    const float* __restrict__ edges, int max_next_nodes, PartInfo* __restrict__ part,
+    NodeLink* __restrict__ next_link, TreeNode* __restrict__ tree, int tree_capacity,
+    NodeSplit* __restrict__ nsplit) {
+  __shared__ int s_last;
+  const int n = ctl[CTL_N];
+  const int node = blockIdx.x;
+  const int f = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (node < n && f < p.F) {   // wave-uniform
+    const NodeLink lk = link[node];
+    const WaveBest w = feat_best_wave<NBT>(built, parent_full, full, lk, node, f, nvb, tree_fmask, qscale[2],
+                                           qscale[3], p, ctl[CTL_BASE] + node);
+    if ((threadIdx.x & 63) == 0) {
+      FeatBest r{};
+      r.gain = w.gain; r.GL = w.GL; r.SL = w.SL;
+      r.G = w.G; r.S = w.S;
+      r.code = w.code;
+      fbest[(int64_t)node * p.F + f] = r;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned total = gridDim.x * gridDim.y;
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t == total - 1u);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int nd = wid; nd < n; nd += nw) node_best_wave(fbest, p.F, nd, lane, nsplit);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, NBT, max_next_nodes, part, next_link, tree,
+                      tree_capacity);
+}
+
 // K6: route every row to its child, or retire it into its leaf (nid = ~gid).
 // Rows retiring at this level add their (g, h, w) to the exact int64 leaf
 // sums (every row retires exactly once per tree, so after the last level the
@@ -2958,6 +3015,32 @@ H2OMX_API int h2omx_split_level(const long long* built, const long long* parent_
     default: return kBadArg;
   }
 #undef H2OMX_SL
+  return launch_status();
+}
+
+H2OMX_API int h2omx_split_find_fin(const long long* built, const long long* parent_full, long long* full,
+                                   const int* ctl, const void* link, const int* nvb, const uint8_t* tree_fmask,
+                                   const double* qscale, const void* params, int max_nodes, int nbt, void* fbest,
+                                   unsigned int* ticket, int* ctl_next, const float* edges, int max_next_nodes,
+                                   void* part, void* next_link, void* tree, int tree_capacity, void* nsplit,
+                                   hipStream_t stream) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  if (max_nodes < 1 || max_nodes > 64 || ticket == nullptr || p.F < 1) return kBadArg;
+  const dim3 grid(max_nodes, (p.F + 3) / 4);
+#define H2OMX_SFF(NB)                                                                                             \
+  hipLaunchKernelGGL(split_find_fin_kernel<NB>, grid, dim3(256), 0, stream, built, parent_full, full, ctl,          \
+                     reinterpret_cast<const NodeLink*>(link), nvb, tree_fmask, qscale, p,                         \
+                     reinterpret_cast<FeatBest*>(fbest), ticket, ctl_next, edges, max_next_nodes,                 \
+                     reinterpret_cast<PartInfo*>(part), reinterpret_cast<NodeLink*>(next_link),                   \
+                     reinterpret_cast<TreeNode*>(tree), tree_capacity, reinterpret_cast<NodeSplit*>(nsplit))
+  switch (nbt) {
+    case 32: H2OMX_SFF(32); break;
+    case 64: H2OMX_SFF(64); break;
+    case 128: H2OMX_SFF(128); break;
+    case 256: H2OMX_SFF(256); break;
+    default: return kBadArg;
+  }
+#undef H2OMX_SFF
   return launch_status();
 }
 

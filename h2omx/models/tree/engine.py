@@ -349,6 +349,10 @@ class HipTreeBuilder:
     N_CUS = 256
     SMALL_SHARD = os.environ.get("H2OMX_HIST_SMALL", "1") == "1"
     MIN_GROUPS = int(os.environ.get("H2OMX_HIST_MIN_GROUPS", "1"))   # A/B knob
+    # scan-engine levels of <= 64 nodes: split_find_fin (last block finalises the level).
+    # Bit-identical but no faster (11-13 us vs 6.6-7.9 + 4.9-5.0 us a level: the tail is
+    # a dependent-latency chain, not launch overhead, profiles/r3/hist_threads_ab.txt ab25/26)
+    SPLIT_FIN = os.environ.get("H2OMX_SPLIT_FIN", "0") == "1"
     MAX_WG_THREADS_PER_CU = 2048      # 32 waves per CU
 
     def _fill_rounds(self, wgpg: int, n_groups: int, lds_bytes: int, threads: int, units: int) -> int:
@@ -621,6 +625,14 @@ class HipTreeBuilder:
                                                     P(nsplit), P(self.ticket), P(ctl_nxt), P(bm.edges),
                                                     next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
                                                     st), "split_level")
+                elif self.SPLIT_FIN and max_nodes <= 64:
+                    # split scan + per-node arg-max + finalisation: the last block finalises
+                    fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
+                    ops.check(lib.h2omx_split_find_fin(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
+                                                       P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
+                                                       P(fbest), P(self.ticket), P(ctl_nxt), P(bm.edges), next_nodes,
+                                                       P(part), P(nl), P(self.tree_buf), self.capacity, P(nsplit),
+                                                       st), "split_find_fin")
                 else:
                     fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
                     ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),

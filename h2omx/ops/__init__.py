@@ -27,6 +27,7 @@ TREE_SIGS = {
     "h2omx_split_find": "PPPPPPPPPIIPS",
     "h2omx_level_finalize": "PPPPPPIIPPPIPIPS",
     "h2omx_split_level": "PPPPPPPPPIIPPPPIPPPIS",
+    "h2omx_split_find_fin": "PPPPPPPPPIIPPPPIPPPIPS",
     "h2omx_partition": "PLPPIPPPPIPPPIIIPS",
     "h2omx_partition_blocks": "",
     "h2omx_partition_final": "PLPPPIPPPPIPPPIS",
