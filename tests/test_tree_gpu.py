@@ -387,6 +387,34 @@ def test_fused_split_level_matches(cuda_dev, monkeypatch, dist, depth, sample_ra
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
 
 
+@pytest.mark.parametrize("dist,depth,sample_rate,mtries", [("bernoulli", 5, 1.0, 0), ("gaussian", 7, 0.7, 0),
+                                                           ("multinomial", 4, 1.0, 0), ("drf", 8, 0.632, 3)])
+def test_split_find_fin_matches(cuda_dev, monkeypatch, dist, depth, sample_rate, mtries):
+    """split_find_fin (split_find's grid, the last block to finish runs the
+    node arg-max + level finalisation) builds the same trees as split_find +
+    node_best_finalize."""
+    import h2omx.models.tree.engine as E
+
+    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi", "drf": "bin"}[dist]
+    X, y = _data(n=40000, F=9, seed=17, task=task)
+    _, bg = _both(X, y, 63)
+    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2, leaf_mode=1 if dist == "drf" else 0,
+                    mtries=mtries)
+    yt = torch.from_numpy(y).cuda()
+    nclass = 3 if dist == "multinomial" else (2 if dist == "drf" else 1)
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(E.HipTreeBuilder, "SPLIT_FIN", flag)
+        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
+                                   nclass=nclass, seed=2)
+    a, b = out[False], out[True]
+    for t in range(a.trees.shape[0]):
+        reach = a.compact()[t]
+        assert reach == b.compact()[t]
+        for f in ("feat", "bin", "value", "weight", "gain"):
+            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
+
+
 @pytest.mark.parametrize("nbins", [20, 255])
 def test_device_edges_match_host_edges(cuda_dev, nbins):
     """compute_edges on the device == the NumPy sketch on the same sample."""
