@@ -182,6 +182,10 @@ def _trees(args, comm, torch, np, model):
         "collectives_per_tree": {"calls": coll["all_reduce_calls"] / max(args.steps, 1),
                                  "bytes": coll["all_reduce_bytes"] / max(args.steps, 1),
                                  "host_us": 1e6 * coll["all_reduce_s"] / max(args.steps, 1)},
+        # collectives the host issued per timed tree (RCCL / gloo calls between graph
+        # segments); 0 when the step graph carries its own P2P collectives
+        "collectives_host_issued_per_tree": coll["all_reduce_calls"] / max(args.steps, 1),
+        "collective_transport": _transport(comm),
     }
     if per_tree is not None:
         out.update(per_tree)
@@ -201,6 +205,17 @@ def _trees(args, comm, torch, np, model):
         out["oracle"] = {"rows": m, "sklearn_hgb_train_auc": float(roc_auc_score(ys, clf.decision_function(Xs))),
                          "h2omx_train_auc_same_rows": float(roc_auc_score(ys, margin[:m].cpu().numpy()))}
     return out
+
+
+def _transport(comm):
+    if comm.world_size == 1:
+        return "none (1 rank)"
+    if comm.p2p is not None:
+        return "p2p (one-shot IPC all-reduce kernels in the step graph)"
+    import torch.distributed as dist
+
+    be = dist.get_backend()
+    return ("rccl" if be == "nccl" else be) + (f" (p2p off: {comm.p2p_error})" if comm.p2p_error else "")
 
 
 def _instrument(gb, args, comm, torch, dev):
@@ -256,7 +271,7 @@ def _instrument(gb, args, comm, torch, dev):
     out["small_kernel_us_per_tree"] = round(sum(ph.get(n, 0.0) for n in ("hist_reduce", "split", "tree_begin",
                                                                          "leaf")), 1)
     out["allreduce_us_per_tree"] = round(ph.get("allreduce", 0.0), 1)
-    out["allreduce_calls_per_tree"] = coll["all_reduce_calls"] / k
+    out["allreduce_calls_per_tree"] = (coll["all_reduce_calls"] + coll.get("p2p_calls", 0)) / k
     out["allreduce_bytes_per_tree"] = coll["all_reduce_bytes"] / k
     out["instrument_note"] = (f"{k} extra eager trees after the timed run with HIP-event phase timers "
                               "(phase sums include event overhead); host enqueue = median over steps with the GPU idle")

@@ -25,6 +25,7 @@ KERNEL_LIBS = {
     "dense": ["dense_kernels.hip", "kmeans_wave.hip"],
     "metrics": ["metrics_kernels.hip"],
     "explain": ["explain_kernels.hip"],
+    "p2p": ["p2p_kernels.hip"],
 }
 HOST_LIBS = {
     "host": ["host/parser.cpp", "host/solvers.cpp"],

@@ -2677,6 +2677,94 @@ __global__ __launch_bounds__(256) void leaf_finalize_kernel(const unsigned long 
   }
 }
 
+// Monotone constraints with H2O's squared-error splits (mode 0) and Newton
+// leaves (leaf_mode 0): the histograms carry (G, W), so the node intervals the
+// level finalisation cut at W-scale midpoints (-G/W) are on the wrong scale for
+// Newton leaf values (-G/H; bernoulli H <= W / 4).  After the leaf sums are
+// exact this one-workgroup pass re-derives every interval on the leaf scale,
+// as H2O's gamma-based bounds do: depth of each reachable node (top-down),
+// subtree (G, H) sums (bottom-up), then [lo, hi] cut at the midpoint of the
+// clipped Newton child values (top-down), and every leaf is clamped into its
+// interval.  scratch: int dep[cap] | double SG[cap], SH[cap], LO[cap], HI[cap].
+__global__ __launch_bounds__(1024) void mono_newton_kernel(const unsigned long long* __restrict__ acc,
+                                                           const int* __restrict__ ctl_final,
+                                                           const double* __restrict__ qs, SplitParams p,
+                                                           TreeNode* __restrict__ tree, int cap, char* scratch) {
+  const int total = min(ctl_final[CTL_TOTAL], cap);
+  int* dep = reinterpret_cast<int*>(scratch);
+  double* SG = reinterpret_cast<double*>(scratch + (((int64_t)cap * 4 + 15) / 16) * 16);
+  double* SH = SG + cap;
+  double* LO = SH + cap;
+  double* HI = LO + cap;
+  __shared__ int s_any;
+  for (int i = threadIdx.x; i < total; i += blockDim.x) dep[i] = (i == 0) ? 0 : -1;
+  __syncthreads();
+  int maxd = 0;
+  for (int d = 0;; ++d) {
+    if (threadIdx.x == 0) s_any = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < total; i += blockDim.x) {
+      if (dep[i] != d) continue;
+      const TreeNode nd = tree[i];
+      if (nd.feat >= 0 && nd.left > 0 && nd.left + 1 < total) {
+        dep[nd.left] = d + 1;
+        dep[nd.left + 1] = d + 1;
+        s_any = 1;
+      }
+    }
+    __syncthreads();
+    const int any = s_any;
+    __syncthreads();
+    if (!any) { maxd = d; break; }
+  }
+  for (int i = threadIdx.x; i < total; i += blockDim.x) {
+    if (dep[i] >= 0 && tree[i].feat < 0) {
+      SG[i] = (double)(long long)acc[3 * i] / qs[4];
+      SH[i] = (double)(long long)acc[3 * i + 1] / qs[5];
+    }
+  }
+  __syncthreads();
+  for (int d = maxd - 1; d >= 0; --d) {
+    for (int i = threadIdx.x; i < total; i += blockDim.x) {
+      if (dep[i] != d) continue;
+      const TreeNode nd = tree[i];
+      if (nd.feat >= 0) {
+        SG[i] = SG[nd.left] + SG[nd.left + 1];
+        SH[i] = SH[nd.left] + SH[nd.left + 1];
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { LO[0] = -INFINITY; HI[0] = INFINITY; }
+  __syncthreads();
+  for (int d = 0; d <= maxd; ++d) {
+    for (int i = threadIdx.x; i < total; i += blockDim.x) {
+      if (dep[i] != d) continue;
+      TreeNode nd = tree[i];
+      const double lo = LO[i], hi = HI[i];
+      if (nd.feat < 0) {
+        const double W = (double)(long long)acc[3 * i + 2] / qs[6];
+        nd.value = (float)fmin(fmax(leaf_value(SG[i], SH[i], W, p), lo), hi);
+        tree[i] = nd;
+        continue;
+      }
+      const int l = nd.left;
+      double llo = lo, lhi = hi, rlo = lo, rhi = hi;
+      const int mf = (int)p.mono[nd.feat];
+      if (mf != 0) {
+        const double wl = fmin(fmax(leaf_value(SG[l], SH[l], SH[l], p), lo), hi);
+        const double wr = fmin(fmax(leaf_value(SG[l + 1], SH[l + 1], SH[l + 1], p), lo), hi);
+        const double mid = 0.5 * (wl + wr);
+        if (mf > 0) { lhi = mid; rlo = mid; } else { llo = mid; rhi = mid; }
+      }
+      LO[l] = llo; HI[l] = lhi; LO[l + 1] = rlo; HI[l + 1] = rhi;
+    }
+    __syncthreads();
+  }
+}
+
+H2OMX_API int64_t h2omx_mono_scratch_bytes(int cap) { return (((int64_t)cap * 4 + 15) / 16) * 16 + (int64_t)cap * 32; }
+
 // ---------------------------------------------------------------------------
 // K8: score raw (unbinned) feature-major data with a tree ensemble.
 // nodes: all trees concatenated; roots[t] = offset of tree t; out[cls][r] +=
@@ -3286,6 +3374,19 @@ H2OMX_API int h2omx_leaf_finalize(const unsigned long long* acc, const int* ctl_
   const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
   hipLaunchKernelGGL(leaf_finalize_kernel, dim3(grid_for(cap, 256, 1024)), dim3(256), 0, stream, acc, ctl_final,
                      qscale, p, reinterpret_cast<TreeNode*>(tree), cap);
+  return launch_status();
+}
+
+// leaf_finalize + (mode 0, Newton leaves, monotone constraints) the leaf-scale
+// interval pass; scratch of h2omx_mono_scratch_bytes(cap) bytes
+H2OMX_API int h2omx_leaf_finalize_mono(const unsigned long long* acc, const int* ctl_final, const double* qscale,
+                                       const void* params, void* tree, int cap, void* scratch, hipStream_t stream) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  if (p.mono == nullptr || scratch == nullptr) return kBadArg;
+  hipLaunchKernelGGL(leaf_finalize_kernel, dim3(grid_for(cap, 256, 1024)), dim3(256), 0, stream, acc, ctl_final,
+                     qscale, p, reinterpret_cast<TreeNode*>(tree), cap);
+  hipLaunchKernelGGL(mono_newton_kernel, dim3(1), dim3(1024), 0, stream, acc, ctl_final, qscale, p,
+                     reinterpret_cast<TreeNode*>(tree), cap, static_cast<char*>(scratch));
   return launch_status();
 }
 

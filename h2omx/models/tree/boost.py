@@ -565,11 +565,12 @@ class TreeGraph:
     step) and the tree is grown in place in ``builder.tree_buf``; the caller
     snapshots it after every replay.
 
-    Multi-rank: by default the step is captured in SEGMENTS split at the
-    collectives, which are issued eagerly between segment replays (works with
-    any backend, nothing of RCCL inside a graph).  ``H2OMX_GRAPH_COLLECTIVES=1``
-    captures the RCCL all-reduces inside one graph instead (RCCL supports
-    stream capture; not exercised on the one-GPU development box).
+    Multi-rank: with the one-shot P2P all-reduce (``parallel/p2p.py``, on by
+    default when peer memory maps) the collectives are kernels of the step, so
+    the whole N-rank step is ONE graph replay with no host-issued collective.
+    Otherwise the step is captured in SEGMENTS split at the collectives, which
+    are issued eagerly between segment replays (works with any backend);
+    ``H2OMX_GRAPH_COLLECTIVES=1`` captures RCCL calls inside one graph instead.
     """
 
     # finished trees go to a device ring of RING slots inside the graph
@@ -597,7 +598,10 @@ class TreeGraph:
         b.tree_buf = torch.zeros_like(b.tree_buf)
         self.ring = torch.zeros((self.RING, b.tree_buf.numel()), dtype=torch.uint8, device=dev)
         multi = self.comm is not None and self.comm.world_size > 1
-        segmented = multi and os.environ.get("H2OMX_GRAPH_COLLECTIVES", "0") != "1"
+        # P2P collectives are ordinary kernels: the whole step is one graph.  RCCL
+        # calls become segment boundaries unless H2OMX_GRAPH_COLLECTIVES=1
+        segmented = (multi and not getattr(self.comm, "graph_collectives", False)
+                     and os.environ.get("H2OMX_GRAPH_COLLECTIVES", "0") != "1")
         self.pool = torch.cuda.graph_pool_handle()
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))

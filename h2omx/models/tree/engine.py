@@ -679,8 +679,7 @@ class HipTreeBuilder:
             with T("allreduce"):
                 comm.all_reduce_(self.leaf_acc)
         with T("leaf"):
-            ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(final_ctl), P(self.qscale), spp,
-                                              P(self.tree_buf), self.capacity, st), "leaf_finalize")
+            self._leaf_finalize(final_ctl, spp, st)
         self._final_ctl = final_ctl
         return self.tree_buf
 
@@ -916,10 +915,25 @@ class HipTreeBuilder:
             max_nodes = next_nodes
         if comm is not None:
             comm.all_reduce_(self.leaf_acc)
-        ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(final_ctl), P(self.qscale), spp,
-                                          P(self.tree_buf), self.capacity, st), "leaf_finalize")
+        self._leaf_finalize(final_ctl, spp, st)
         self._final_ctl = final_ctl
         return self.tree_buf
+
+    def _leaf_finalize(self, final_ctl, spp, st):
+        """Leaf values from the exact leaf sums.  Monotone constraints with
+        squared-error splits and Newton leaves (GBM, mode 0 / leaf_mode 0): the
+        node intervals are re-derived on the Newton (-G/H) scale of the leaf
+        values (mono_newton_kernel) instead of the -G/W scale the level
+        finalisation could use (the histograms carry W, not H)."""
+        lib, P, p = self.lib, ops.P, self.p
+        if self.gbound is not None and p.mode == 0 and p.leaf_mode == 0:
+            cap = self.capacity
+            scratch = self._buf("mono_scratch", ((cap * 4 + 15) // 16) * 16 + cap * 32, torch.uint8)
+            ops.check(lib.h2omx_leaf_finalize_mono(P(self.leaf_acc), P(final_ctl), P(self.qscale), spp,
+                                                   P(self.tree_buf), cap, P(scratch), st), "leaf_finalize_mono")
+        else:
+            ops.check(lib.h2omx_leaf_finalize(P(self.leaf_acc), P(final_ctl), P(self.qscale), spp,
+                                              P(self.tree_buf), self.capacity, st), "leaf_finalize")
 
     def reduce_stats(self) -> None:
         """Fold the per-block maxima written by the gradient kernels into stat_max."""

@@ -46,6 +46,7 @@ TREE_SIGS = {
     "h2omx_tree_begin": "PIIPPPPILIPS",
     "h2omx_leaf_stats": "PPPPLPIPS",
     "h2omx_leaf_finalize": "PPPPPIS",
+    "h2omx_leaf_finalize_mono": "PPPPPIPS",
     "h2omx_predict_raw": "PLLPPIIPLS",
     "h2omx_predict_binned": "PLLPPIIIPLS",
     "h2omx_pc_rows": "",
@@ -70,6 +71,8 @@ DENSE_SIGS = {
     "h2omx_kmeans": "PLLIPPIIPPS",
     "h2omx_kmeans_wave": "PLLIPPPIIIIPPS",
     "h2omx_glm_wz": "PLPPPPPPPPIS",
+    "h2omx_glm_grad": "PLLPPPPPPPIPIS",
+    "h2omx_glm_grad_max_k": "",
     "h2omx_glm_aug": "PILPPPPS",
     "h2omx_kmeans_stage": "PLILLPS",
     "h2omx_kmeans_argmin": "PILPPIPPIS",
@@ -105,6 +108,21 @@ EXPLAIN_SIGS = {
     "h2omx_tree_shap": "PLLIPIPPIPS",
 }
 
+P2P_SIGS = {
+    "h2omx_p2p_allreduce": "PPLIIS",
+    "h2omx_p2p_desc_bytes": "",
+    "h2omx_p2p_clock_khz": "",
+    "h2omx_p2p_max_ranks": "",
+    "h2omx_p2p_flags_bytes": "",
+    "h2omx_p2p_alloc": "LIP",
+    "h2omx_p2p_free": "P",
+    "h2omx_p2p_handle_bytes": "",
+    "h2omx_p2p_get_handle": "PP",
+    "h2omx_p2p_open_handle": "PP",
+    "h2omx_p2p_close_handle": "P",
+    "h2omx_p2p_enable_peers": "",
+}
+
 _bound: dict[str, ctypes.CDLL] = {}
 
 
@@ -137,6 +155,12 @@ def metrics_lib() -> ctypes.CDLL:
 
 def explain_lib() -> ctypes.CDLL:
     return _bind("explain", EXPLAIN_SIGS)
+
+
+def p2p_lib() -> ctypes.CDLL:
+    lib = _bind("p2p", P2P_SIGS)
+    lib.h2omx_p2p_flags_bytes.restype = ctypes.c_int64
+    return lib
 
 
 P = _native.ptr

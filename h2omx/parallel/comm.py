@@ -39,6 +39,11 @@ class Comm:
         # set by the peer watchdog (runtime/watchdog.py) once a rank is lost:
         # collectives then fail fast instead of blocking on the missing peer
         self.failed: str | None = None
+        # one-shot P2P all-reduce over IPC-mapped HBM for small messages
+        # (parallel/p2p.py): graph-capturable, so tree steps replay as one graph
+        self.p2p = None
+        self.p2p_error: str | None = None
+        self.stats.update({"p2p_calls": 0, "p2p_bytes": 0, "p2p_s": 0.0})
 
     def _check(self) -> None:
         if self.failed is not None:
@@ -71,7 +76,26 @@ class Comm:
                 kw["device_id"] = dev
             dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
-        return cls(rank, world, dev)
+        c = cls(rank, world, dev)
+        # H2OMX_P2P: auto (default: on when IPC works and the self-test passes), 0 off, 1 required
+        mode = os.environ.get("H2OMX_P2P", "auto")
+        if world > 1 and dev.type == "cuda" and mode != "0":
+            c.enable_p2p(required=mode == "1")
+        return c
+
+    def enable_p2p(self, required: bool = False) -> bool:
+        """Set up the one-shot P2P all-reduce (collective over the group)."""
+        from .p2p import setup
+
+        if self.p2p is None and self.world_size > 1:
+            self.p2p = setup(self, required=required)
+        return self.p2p is not None
+
+    @property
+    def graph_collectives(self) -> bool:
+        """True when the small collectives are device-side kernels (P2P), so a
+        step graph can be captured whole instead of segmented at collectives."""
+        return self.p2p is not None
 
     @property
     def is_leader(self) -> bool:
@@ -114,6 +138,8 @@ class Comm:
         if reset:
             for k in self.stats:
                 self.stats[k] = 0.0 if k.endswith("_s") else 0
+            if self.p2p is not None:
+                self.p2p.check()
             self._device_ms.clear()
         return out
 
@@ -121,6 +147,12 @@ class Comm:
         if self.world_size == 1:
             return t
         self._check()
+        if self.p2p is not None and self.p2p.supports(t, op):
+            # device-side one-shot collective (a kernel: no host-issued RCCL call)
+            tok = self._begin("p2p", t.numel() * t.element_size())
+            self.p2p.all_reduce_(t, op)
+            self._end(tok)
+            return t
         tok = self._begin("all_reduce", t.numel() * t.element_size())
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
         dist.all_reduce(t, op=rop, group=self.group)
@@ -215,6 +247,11 @@ class Comm:
         return float(t.item())
 
     def shutdown(self) -> None:
+        if self.p2p is not None:
+            self.p2p.check()
+            self.barrier()
+            self.p2p.close()
+            self.p2p = None
         if self.world_size > 1 and dist.is_initialized():
             dist.destroy_process_group()
 

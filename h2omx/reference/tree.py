@@ -153,6 +153,7 @@ class RefTreeBuilder:
             wl, wr = lv_vec(GLv, SLv), lv_vec(Gs - GLv, Ss - SLv)
             return wl <= wr if mf > 0 else wl >= wr
 
+        leaf_gh = {}     # gid -> (G, H) of every node created as a leaf (Newton mono refine)
         for d in range(p.max_depth):
             last = d == p.max_depth - 1
             contrib = np.where((nid >= 0) & (w != 0), nid, -1)
@@ -211,6 +212,7 @@ class RefTreeBuilder:
                 rec = tree[gid] if gid < self.capacity else np.zeros((), TREE_NODE_DTYPE)
                 rec["value"] = clip(leaf_value(Gt, Ht, Wt, p), gid)
                 rec["weight"] = Wt
+                leaf_gh[gid] = (Gt, Ht)
                 if do_split:
                     f, t, na_left, GL, HL, WL = best[1]
                     if fsets is not None:
@@ -245,6 +247,7 @@ class RefTreeBuilder:
                         lc["value"] = clip(leaf_value(GL, HL, WL, p), next_base + 2 * k)
                         rc["value"] = clip(leaf_value(Gt - GL, Ht - HL, Wt - WL, p), next_base + 2 * k + 1)
                         lc["weight"], rc["weight"] = WL, Wt - WL
+                        leaf_gh[next_base + 2 * k], leaf_gh[next_base + 2 * k + 1] = (GL, HL), (Gt - GL, Ht - HL)
                     k += 1
                 else:
                     rec["feat"], rec["left"] = -1, -1
@@ -271,7 +274,48 @@ class RefTreeBuilder:
             self.n_nodes_total = base + n_nodes
             if n_nodes == 0:
                 break
+        if mono is not None and p.mode == 0 and p.leaf_mode == 0:
+            _mono_newton_refine(tree, mono, leaf_gh, p)
         return tree
+
+
+def _mono_newton_refine(tree, mono, leaf_gh, p):
+    """Mirror of mono_newton_kernel: node intervals re-derived on the Newton
+    (-G/H) scale of the leaf values from the subtree (G, H) sums, leaves
+    clamped into them (squared-error splits carry W, not H)."""
+    sums = {}
+
+    def gh(gid):
+        if gid not in sums:
+            rec = tree[gid]
+            if rec["feat"] < 0:
+                sums[gid] = leaf_gh.get(gid, (0.0, 0.0))
+            else:
+                a, b = gh(int(rec["left"])), gh(int(rec["left"]) + 1)
+                sums[gid] = (a[0] + b[0], a[1] + b[1])
+        return sums[gid]
+
+    stack = [(0, -np.inf, np.inf)]
+    while stack:
+        gid, lo, hi = stack.pop()
+        rec = tree[gid]
+        if rec["feat"] < 0:
+            G, H = gh(gid)
+            rec["value"] = min(max(leaf_value(G, H, H, p), lo), hi)
+            continue
+        l = int(rec["left"])
+        llo, lhi, rlo, rhi = lo, hi, lo, hi
+        mf = int(mono[int(rec["feat"])])
+        if mf != 0:
+            (GL, HL), (GR, HR) = gh(l), gh(l + 1)
+            wl = min(max(leaf_value(GL, HL, HL, p), lo), hi)
+            wr = min(max(leaf_value(GR, HR, HR, p), lo), hi)
+            mid = 0.5 * (wl + wr)
+            if mf > 0:
+                lhi = rlo = mid
+            else:
+                llo = rhi = mid
+        stack += [(l, llo, lhi), (l + 1, rlo, rhi)]
 
 
 # ---------------------------------------------------------------------------

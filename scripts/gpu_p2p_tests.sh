@@ -1,0 +1,3 @@
+cd $GRAFT_REPO_ROOT
+timeout -k 10 500 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_p2p_gpu.py tests/test_bench_contract.py -m gpu > gpurun_out/p2p_tests.log 2>&1 &&
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_monotone.py -m gpu > gpurun_out/mono_tests.log 2>&1

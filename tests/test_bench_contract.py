@@ -113,7 +113,9 @@ def test_bench_strong_two_ranks_reproduce_one_rank_gpu(tmp_path):
     extra = ["--rows", "300000", "--scaling", "strong", "--instrument-steps", "2", "--fit-trees", "0"]
     one, two = tmp_path / "one.npy", tmp_path / "two.npy"
     o1 = _run(1, extra + ["--dump-trees", str(one)], timeout=300)
-    o2 = _run(2, extra + ["--dump-trees", str(two)], {"H2OMX_DIST_BACKEND": "gloo"}, timeout=300)
+    # P2P off: the segmented graph with host-issued gloo collectives (the RCCL
+    # fallback's structure); tests/test_p2p_gpu.py covers the one-graph P2P path
+    o2 = _run(2, extra + ["--dump-trees", str(two)], {"H2OMX_DIST_BACKEND": "gloo", "H2OMX_P2P": "0"}, timeout=300)
     assert o1["graph_replay"] and o2["graph_replay"]
     _assert_same_trees(np.load(one), np.load(two), exact_values=True)
     assert o1["train_auc"] == o2["train_auc"]

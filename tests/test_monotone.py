@@ -125,3 +125,54 @@ def test_monotone_gpu_matches_reference(cuda_dev, mode):
     Xs[0] = torch.linspace(-3.5, 3.5, 101).repeat(8)
     s = ef.raw_margin(Xs.cuda())[0].cpu().numpy().reshape(8, 101)
     assert (np.diff(s, axis=1) < -1e-6).any()
+
+
+def _mono_signal(n=6000, seed=4):
+    rng = np.random.default_rng(seed)
+    X = np.stack([rng.uniform(-2, 2, n), rng.normal(size=n)]).astype(np.float32)
+    p = 1 / (1 + np.exp(-(1.5 * X[0] + 0.7 * X[1])))
+    y = (rng.uniform(size=n) < p).astype(np.float32)
+    return X, y
+
+
+def _fit_bernoulli(X, y, monotone, dev=None):
+    from h2omx.models.tree import TreeParams, bin_matrix, compute_edges, train_ensemble
+
+    Xt = torch.tensor(X)
+    if dev is not None:
+        Xt = Xt.to(dev)
+    tp = TreeParams(max_depth=3, min_rows=10.0, learn_rate=0.3, mode=0, seed=1, monotone=monotone)
+    e, nv, nbt = compute_edges(Xt, 64)
+    ens = train_ensemble(bin_matrix(Xt, e, nv, nbt), y, dist="bernoulli", ntrees=10, tparams=tp)
+    return ens, ens.raw_margin(Xt)[0].cpu().numpy()
+
+
+def test_monotone_bernoulli_newton_scale_bounds():
+    """Bernoulli GBM (squared-error splits on (G, W), Newton leaves -G/H with
+    H <= W / 4): on an already monotone signal the constraint should barely
+    bind.  Bounds cut at -G/W midpoints would clamp the 4x larger Newton
+    values of deeper leaves and shrink the constrained model's margins."""
+    X, y = _mono_signal()
+    _, free = _fit_bernoulli(X, y, None)
+    ens, con = _fit_bernoulli(X, y, (1, 0))
+    spread = np.ptp(free)
+    assert np.abs(con - free).mean() < 0.02 * spread, (np.abs(con - free).mean(), spread)
+    assert np.ptp(con) > 0.9 * spread
+    # monotone in x0 for fixed x1
+    xs = np.linspace(-2.5, 2.5, 81, dtype=np.float32)
+    for x1 in (-1.0, 0.0, 1.3):
+        Xs = np.stack([xs, np.full_like(xs, x1)])
+        s = ens.raw_margin(torch.tensor(Xs))[0].numpy()
+        assert (np.diff(s) >= -1e-9).all()
+
+
+@pytest.mark.gpu
+def test_monotone_bernoulli_gpu_matches_reference(cuda_dev):
+    X, y = _mono_signal(n=20000, seed=9)
+    ec, mc = _fit_bernoulli(X, y, (1, -1))
+    eg, mg = _fit_bernoulli(X, y, (1, -1), dev=cuda_dev)
+    same = np.mean([(a["feat"] == b["feat"]).all() for a, b in zip(ec.trees, eg.trees)])
+    assert same >= 0.75
+    assert (np.abs(mc - mg) < 1e-3 * max(1.0, np.abs(mc).max())).mean() > 0.9
+    _, free = _fit_bernoulli(X, y, None, dev=cuda_dev)
+    assert np.ptp(mg) > 0.5 * np.ptp(free)
