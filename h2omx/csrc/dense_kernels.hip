@@ -164,6 +164,106 @@ __global__ __launch_bounds__(256) void glm_wz_kernel(const float* __restrict__ E
   if (threadIdx.x == 0) dev_part[blockIdx.x] = red[0];
 }
 
+// ---------------------------------------------------------------------------
+// GLM gradient pass (solver L_BFGS): two streaming kernels over the
+// feature-major design, no Gram.  glm_resid_kernel: one thread per row, the
+// K linear predictors eta = B x + b0 (+ offset) from coalesced feature rows,
+// then the row's gradient weight r_k = w (mu - y) mu'(eta) / V(mu)
+// (multinomial: w (p_k - [y == k])) and its deviance.  glm_xtr_kernel:
+// grad[k][j] = sum_i x_ji r_ki, one workgroup per (feature, row split) doing
+// contiguous dot products (the intercept row j = p sums r).  fp64 throughout
+// the accumulation; per-split partials are summed on the host in fixed order.
+// ---------------------------------------------------------------------------
+constexpr int kGradMaxK = 16;
+
+__global__ __launch_bounds__(256) void glm_resid_kernel(const float* __restrict__ X, int64_t ld, int64_t n,
+                                                        const double* __restrict__ beta, const float* __restrict__ y,
+                                                        const float* __restrict__ wprior,
+                                                        const float* __restrict__ offset, GlmParams P,
+                                                        float* __restrict__ R, double* __restrict__ dev_part) {
+  extern __shared__ double sb[];   // beta [K][p + 1]
+  __shared__ double red[256];
+  const int p = P.p, K = P.K;
+  for (int i = threadIdx.x; i < K * (p + 1); i += 256) sb[i] = beta[i];
+  __syncthreads();
+  double dacc = 0.0;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
+    double eta[kGradMaxK];
+#pragma unroll
+    for (int k = 0; k < kGradMaxK; ++k) eta[k] = (k < K) ? sb[k * (p + 1) + p] : 0.0;
+    for (int j = 0; j < p; ++j) {
+      const double x = X[(int64_t)j * ld + r];
+#pragma unroll
+      for (int k = 0; k < kGradMaxK; ++k)
+        if (k < K) eta[k] += sb[k * (p + 1) + j] * x;
+    }
+    const double wpv = wprior ? wprior[r] : 1.0;
+    if (P.family == 5) {
+      double mx = -1e300;
+#pragma unroll
+      for (int k = 0; k < kGradMaxK; ++k)
+        if (k < K) mx = fmax(mx, eta[k]);
+      double den = 0.0;
+#pragma unroll
+      for (int k = 0; k < kGradMaxK; ++k)
+        if (k < K) den += exp(eta[k] - mx);
+      const int yc = (int)y[r];
+#pragma unroll
+      for (int k = 0; k < kGradMaxK; ++k) {
+        if (k < K) {
+          const double pk = exp(eta[k] - mx) / den;
+          R[(int64_t)k * n + r] = (float)(wpv * (pk - (k == yc ? 1.0 : 0.0)));
+          if (k == yc) dacc += wpv * -2.0 * log(fmax(pk, 1e-300));
+        }
+      }
+    } else {
+      const double e = eta[0] + (offset ? offset[r] : 0.0);
+      double mu, dmu;
+      glm_link(P, e, mu, dmu);
+      const double yv = y[r];
+      R[r] = (float)(wpv * (mu - yv) * dmu / glm_var(P, mu));
+      dacc += wpv * glm_dev(P, yv, mu);
+    }
+  }
+  red[threadIdx.x] = dacc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dev_part[blockIdx.x] = red[0];
+}
+
+// grid (p + 1, splits): out[split][k][j] = sum over the split's rows of x_ji r_ki
+__global__ __launch_bounds__(256) void glm_xtr_kernel(const float* __restrict__ X, int64_t ld, int64_t n, int p,
+                                                      int K, const float* __restrict__ R, double* __restrict__ out) {
+  __shared__ double red[kGradMaxK][4];
+  const int j = blockIdx.x, sp = blockIdx.y, ns = gridDim.y;
+  const int64_t per = (n + ns - 1) / ns;
+  const int64_t r0 = (int64_t)sp * per, r1 = min(n, r0 + per);
+  double acc[kGradMaxK];
+#pragma unroll
+  for (int k = 0; k < kGradMaxK; ++k) acc[k] = 0.0;
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+    const double x = (j < p) ? (double)X[(int64_t)j * ld + r] : 1.0;
+#pragma unroll
+    for (int k = 0; k < kGradMaxK; ++k)
+      if (k < K) acc[k] += x * (double)R[(int64_t)k * n + r];
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kGradMaxK; ++k) {
+    if (k < K) {
+      const double v = wave_sum(acc[k]);
+      if (lane == 0) red[k][wv] = v;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < K)
+    out[((int64_t)sp * K + threadIdx.x) * (p + 1) + j] =
+        red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+}
+
 // A [(p+2)][m] = sqrt(w) * [x (NaN -> column mean) | 1 | z]; Xc [p][m] is the
 // staged chunk (NaN kept), grid.y = augmented row
 __global__ __launch_bounds__(256) void glm_aug_kernel(const float* __restrict__ Xc, int p, int64_t m,
@@ -2142,6 +2242,23 @@ H2OMX_API int h2omx_glm_wz(const float* E, int64_t m, const float* y, const floa
                      dev_part);
   return launch_status();
 }
+
+// GLM gradient (L_BFGS): R [K][n] residual weights + per-block deviance, then
+// the per-split partial gradients out [splits][K][p + 1] (host sums the splits)
+H2OMX_API int h2omx_glm_grad(const float* X, int64_t ld, int64_t n, const double* beta, const float* y,
+                             const float* wprior, const float* offset, const void* params, float* R, double* dev_part,
+                             int n_blk, double* out, int splits, hipStream_t stream) {
+  const GlmParams P = *reinterpret_cast<const GlmParams*>(params);
+  if (n < 1 || n_blk < 1 || splits < 1 || P.K < 1 || P.K > kGradMaxK || P.p < 0) return kBadArg;
+  const size_t lds = sizeof(double) * (size_t)P.K * (P.p + 1);
+  if (lds > 64 * 1024) return kBadArg;
+  hipLaunchKernelGGL(glm_resid_kernel, dim3(n_blk), dim3(256), lds, stream, X, ld, n, beta, y, wprior, offset, P, R,
+                     dev_part);
+  hipLaunchKernelGGL(glm_xtr_kernel, dim3(P.p + 1, splits), dim3(256), 0, stream, X, ld, n, P.p, P.K, R, out);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_glm_grad_max_k() { return kGradMaxK; }
 
 H2OMX_API int h2omx_glm_aug(const float* Xc, int p, int64_t m, const float* means, const float* sw, const float* z,
                             float* A, hipStream_t stream) {

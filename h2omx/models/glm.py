@@ -6,6 +6,11 @@ weighted Gram of [X | 1 | z] on the fp32 matrix cores, reduced in fp64 and
 (for multi-rank clusters) all-reduced once.  The tiny (p+1)x(p+1) elastic-net
 sub-problem is solved on the host by Cholesky (ridge) or cyclic coordinate
 descent on the Gram (lasso / elastic net), like H2O's IRLSM solver.
+``solver``: AUTO (IRLSM; L_BFGS for > 5000 columns or wide multinomials),
+IRLSM, COORDINATE_DESCENT(_NAIVE) (IRLS with the coordinate-descent inner
+solver every iteration), L_BFGS (OWL-QN over Gram-free gradient passes,
+models/glm_solvers.py); GRADIENT_DESCENT_LH is the ordinal family's solver.
+Unknown values raise.
 
 Families: gaussian, binomial, quasibinomial, fractionalbinomial, poisson,
 gamma, tweedie, negativebinomial (fixed ``theta``), multinomial (per-class
@@ -26,6 +31,7 @@ import torch
 from ..frame.frame import ENUM, Frame
 from ..backend import dense as D
 from .base import Model, ModelBuilder, ModelCategory
+from .glm_solvers import owlqn, resolve_solver
 
 
 class DesignInfo:
@@ -119,11 +125,14 @@ def _enet_cd(A, r, pen, l1, free_idx, non_negative, b, max_iter, tol) -> int:
 
 
 def solve_enet(G: np.ndarray, p: int, N: float, lam: float, alpha: float, beta0: np.ndarray, intercept: bool,
-               non_negative: bool = False, max_iter: int = 500, tol: float = 1e-9, penalty: np.ndarray | None = None):
+               non_negative: bool = False, max_iter: int = 500, tol: float = 1e-9, penalty: np.ndarray | None = None,
+               force_cd: bool = False):
     """Minimise (1/2N) sum w (z - x.b)^2 + lam (alpha |b|_1 + (1-alpha)/2 |b|^2)
     (+ 1/2 bᵀ P b for a quadratic ``penalty`` P on the p coefficients, GAM
     smoothness) given the augmented Gram G of [x | 1 | z].  Returns beta (p
-    coefficients + intercept)."""
+    coefficients + intercept).  Ridge / unpenalised problems take a Cholesky
+    solve unless ``force_cd`` (solver COORDINATE_DESCENT) asks for the
+    covariance-update coordinate descent every time."""
     XtX = G[: p + 1, : p + 1] / N
     if penalty is not None:
         XtX = XtX.copy()
@@ -138,7 +147,7 @@ def solve_enet(G: np.ndarray, p: int, N: float, lam: float, alpha: float, beta0:
         Xtz = Xtz[:p]
         pen = pen[:p]
     k = len(Xtz)
-    if l1 == 0 and not non_negative:
+    if l1 == 0 and not non_negative and not force_cd:
         A = XtX + np.diag(pen)
         try:
             L = np.linalg.cholesky(A + 1e-12 * np.eye(k) * max(1.0, np.abs(A).max()))
@@ -264,7 +273,7 @@ def _torch_linkinv(eta, link, link_power=0.0):
 
 class H2OGeneralizedLinearEstimator(ModelBuilder):
     algo = "glm"
-    DEFAULTS = dict(family="AUTO", link="family_default", solver="IRLSM", alpha=None, lambda_=None, Lambda=None,
+    DEFAULTS = dict(family="AUTO", link="family_default", solver="AUTO", alpha=None, lambda_=None, Lambda=None,
                     lambda_search=False, nlambdas=-1, lambda_min_ratio=-1.0, standardize=True, intercept=True,
                     max_iterations=-1, beta_epsilon=1e-4, objective_epsilon=-1.0, gradient_epsilon=-1.0,
                     non_negative=False, compute_p_values=False, remove_collinear_columns=False,
@@ -310,6 +319,9 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
     def _fit_ordinal(self, X, y, w, N, design, lam_param, alpha, model_id):
         return _fit_ordinal_impl(self, X, y, w, N, design, lam_param, alpha, model_id)
 
+    def _fit_lbfgs(self, *a):
+        return _fit_lbfgs_impl(self, *a)
+
     def _penalty_matrix(self, design):
         """Quadratic coefficient penalty (raw scale, p×p) added to the IRLS normal
         equations; None for plain GLM (overridden by GAM)."""
@@ -344,8 +356,12 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
         # standardised scale: b_raw = b_std / sd  ->  P_std = D⁻¹ P D⁻¹
         pen_raw = self._penalty_matrix(design)
         pen_std = None if pen_raw is None else pen_raw / np.outer(design.sds, design.sds)
+        solver = resolve_solver(p_["solver"], family, p, K)
+        if solver == "GRADIENT_DESCENT_SQERR":
+            raise ValueError("glm: solver GRADIENT_DESCENT_SQERR (ordinal squared-error objective) is not supported; "
+                             "use GRADIENT_DESCENT_LH")
         alpha = p_["alpha"]
-        alpha = (0.0 if p_["solver"] == "L_BFGS" else 0.5) if alpha is None else float(alpha[0] if isinstance(alpha, (list, tuple)) else alpha)
+        alpha = (0.0 if solver == "L_BFGS" else 0.5) if alpha is None else float(alpha[0] if isinstance(alpha, (list, tuple)) else alpha)
         lam_param = p_["lambda_"] if p_["lambda_"] is not None else p_["Lambda"]
         var_power = float(p_["theta"]) if family == "negativebinomial" else float(p_["tweedie_variance_power"] or 1.5)
         link_power = float(p_["tweedie_link_power"]) if family == "tweedie" else 0.0
@@ -387,6 +403,8 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
         else:
             beta[0, p] = ybar if link == "identity" else beta[0, p]
         G0, null_dev = allreduce(*D.glm_irls_pass(X, y, w, off, beta, family, link, 0, var_power, link_power))
+        for k in range(1, K):
+            null_dev += allreduce(*D.glm_irls_pass(X, y, w, off, beta, family, link, k, var_power, link_power))[1]
         lam_max = float(np.abs(G0[:p, p + 1]).max() / N / max(alpha, 1e-3)) if p > 0 else 0.0
         if lam_param is not None:
             lambdas = [float(v) for v in (lam_param if isinstance(lam_param, (list, tuple)) else [lam_param])]
@@ -401,14 +419,21 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
         history = []
         best = None
         lam_devs = []
+        if solver == "L_BFGS":
+            return self._fit_lbfgs(X, y, w, off, beta, family, link, var_power, link_power, N, null_dev, lam_max,
+                                   lambdas, alpha, intercept, pen_std, design, model_id)
+        force_cd = solver in ("COORDINATE_DESCENT", "COORDINATE_DESCENT_NAIVE")
         for lam in lambdas:
             for it in range(max_iter):
                 iters_total += 1
                 old = beta.copy()
+                dev_k = 0.0
                 for k in range(K):
                     G, dev = allreduce(*D.glm_irls_pass(X, y, w, off, beta, family, link, k, var_power, link_power))
+                    dev_k += dev    # multinomial: pass k carries the rows of class k
                     beta[k] = solve_enet(G, p, N, lam, alpha, beta[k], intercept, bool(p_["non_negative"]),
-                                         penalty=pen_std)
+                                         penalty=pen_std, force_cd=force_cd)
+                dev = dev_k
                 history.append({"iteration": iters_total, "lambda": lam, "deviance": dev})
                 if np.abs(beta - old).max() < beps:
                     break
@@ -421,10 +446,12 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
                 if len(lam_devs) >= 4 and lam_devs[-4] - lam_devs[-1] < 1e-4 * max(null_dev, 1e-300):
                     break
         lam, beta, _ = best
-        # final deviance at the chosen beta
+        # final deviance at the chosen beta (multinomial: every class's pass)
         G, dev = allreduce(*D.glm_irls_pass(X, y, w, off, beta, family, link, 0, var_power, link_power))
+        for k in range(1, K):
+            dev += allreduce(*D.glm_irls_pass(X, y, w, off, beta, family, link, k, var_power, link_power))[1]
         stats = {"lambda": lam, "iterations": iters_total, "null_deviance": null_dev, "residual_deviance": dev,
-                 "lambda_max": lam_max, "nobs": N}
+                 "lambda_max": lam_max, "nobs": N, "solver": solver}
         k_active = int((np.abs(beta[:, :p]) > 0).sum()) + (K if intercept else 0)
         if family in ("binomial", "poisson", "multinomial"):
             stats["aic"] = dev + 2 * k_active
@@ -433,6 +460,68 @@ class H2OGeneralizedLinearEstimator(ModelBuilder):
         model = GLMModel(self, model_id, design, beta, family, link, stats)
         model.scoring_history = history
         return model
+
+
+def _fit_lbfgs_impl(est, X, y, w, off, beta, family, link, var_power, link_power, N, null_dev, lam_max, lambdas,
+                    alpha, intercept, pen_std, design, model_id):
+    """solver=L_BFGS: OWL-QN over the gradient passes (glm_solvers.owlqn),
+    warm-started along the lambda list; lambda_search keeps the last lambda
+    (as the IRLSM path does)."""
+    p_ = est.params
+    comm = est.comm
+    K, p1 = beta.shape
+    p = p1 - 1
+    pen_mask = np.zeros((K, p1), bool)
+    pen_mask[:, :p] = True
+    free = np.ones((K, p1), bool)
+    if not intercept:
+        beta[:, p] = 0.0
+        free[:, p] = False
+    fam_grad = "multinomial" if family == "multinomial" else family
+
+    def fg_at(l2):
+        def fg(bflat):
+            B = bflat.reshape(K, p1)
+            g, dv = D.glm_grad_pass(X, y, w, off, B, fam_grad, link, var_power, link_power)
+            if comm is not None and comm.world_size > 1:
+                arr = comm.all_reduce_numpy(np.concatenate([g.ravel(), [dv]]))
+                g, dv = arr[:-1].reshape(K, p1), float(arr[-1])
+            Bp = np.where(pen_mask, B, 0.0)
+            fs = dv / (2 * N) + 0.5 * l2 * float((Bp * Bp).sum())
+            grad = g / N + l2 * Bp
+            if pen_std is not None:
+                fs += 0.5 * float(B[0, :p] @ pen_std @ B[0, :p])
+                grad[0, :p] += pen_std @ B[0, :p]
+            grad = np.where(free, grad, 0.0)
+            return fs, grad.ravel(), dv
+        return fg
+
+    max_iter = int(p_["max_iterations"]) if int(p_["max_iterations"]) > 0 else 500
+    geps = float(p_["gradient_epsilon"]) if float(p_["gradient_epsilon"]) > 0 else 1e-6
+    oeps = float(p_["objective_epsilon"]) if float(p_["objective_epsilon"]) > 0 else 1e-10
+    history, best, iters = [], None, 0
+    for lam in lambdas:
+        res = owlqn(fg_at(lam * (1 - alpha)), beta.ravel(), pen_mask.ravel(), lam * alpha, max_iter=max_iter,
+                    grad_eps=geps, obj_eps=oeps, non_negative=bool(p_["non_negative"]))
+        beta = res.beta.reshape(K, p1)
+        iters += res.iters
+        history.append({"iteration": iters, "lambda": lam, "deviance": res.dev, "objective": res.f,
+                        "function_evaluations": res.evals})
+        best = (lam, beta.copy(), res.dev)
+    lam, beta, dev = best
+    stats = {"lambda": lam, "iterations": iters, "null_deviance": null_dev, "residual_deviance": dev,
+             "lambda_max": lam_max, "nobs": N, "solver": "L_BFGS"}
+    k_active = int((np.abs(beta[:, :p]) > 0).sum()) + (K if intercept else 0)
+    if family in ("binomial", "poisson", "multinomial"):
+        stats["aic"] = dev + 2 * k_active
+    if p_["compute_p_values"] and family != "multinomial" and lam == 0.0:
+        G, _ = D.glm_irls_pass(X, y, w, off, beta, family, link, 0, var_power, link_power)
+        if comm is not None and comm.world_size > 1:
+            G = comm.all_reduce_numpy(G)
+        stats.update(_p_values(G, p, family, dev, N, k_active, design, beta[0]))
+    model = GLMModel(est, model_id, design, beta, family, link, stats)
+    model.scoring_history = history
+    return model
 
 
 def _fit_ordinal_impl(est, X, y, w, N, design, lam_param, alpha, model_id):

@@ -140,6 +140,34 @@ def glm_irls_pass(X: torch.Tensor, y: torch.Tensor, wprior, offset, beta: np.nda
     return G, float(devs.sum().item())
 
 
+def glm_grad_pass(X: torch.Tensor, y: torch.Tensor, wprior, offset, beta: np.ndarray, family: str, link: str,
+                  var_power: float = 1.5, link_power: float = 0.0):
+    """Gradient pass of the GLM objective (solver L_BFGS): no Gram, two streaming
+    HIP kernels over the feature-major design (glm_resid_kernel, glm_xtr_kernel).
+    beta: float64 [K][p+1].  Returns (g float64 [K][p+1] = sum_i r_ki [x_i | 1],
+    deviance); r = w (mu - y) mu' / V(mu) (multinomial: w (p_k - [y = k])), so
+    d(deviance / 2) / d beta = g."""
+    _dev(X, "glm_grad_pass")
+    lib = dense_lib()
+    p, n = X.shape
+    K = beta.shape[0]
+    if K > lib.h2omx_glm_grad_max_k():
+        raise ValueError(f"glm_grad_pass: {K} classes > {lib.h2omx_glm_grad_max_k()} per pass")
+    dev = X.device
+    Xc = X if X.stride(1) == 1 else X.contiguous()
+    R = _workspace(dev, K * n, slot=3)
+    n_blk = int(max(1, min(2048, -(-n // 1024))))
+    splits = int(max(1, min(64, -(-n // (1 << 16)), 4096 // max(p + 1, 1))))
+    devs = torch.empty((n_blk,), dtype=torch.float64, device=dev)
+    out = torch.empty((splits * K * (p + 1),), dtype=torch.float64, device=dev)
+    b64 = torch.from_numpy(np.ascontiguousarray(beta, np.float64)).to(dev)
+    gp = GlmParams(FAMILIES[family], LINKS[link], p, K, 0, 0, var_power, link_power)
+    check(lib.h2omx_glm_grad(P(Xc), Xc.stride(0), n, P(b64), P(y), P(wprior), P(offset), ctypes.addressof(gp), P(R),
+                             P(devs), n_blk, P(out), splits, stream(dev)), "glm_grad")
+    g = out.view(splits, K, p + 1).cpu().numpy().sum(0)
+    return g, float(devs.sum().item())
+
+
 def _glm_irls_wave(X, y, wprior, offset, beta, family, link, cls, var_power, link_power):
     """glm_irls_wave_kernel: independent wave units over contiguous row ranges
     (register-resident 32-row chunks, 16x16x4 fp32 MFMA Gram tiles), then the

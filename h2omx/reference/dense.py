@@ -20,6 +20,34 @@ def glm_irls_pass(X: torch.Tensor, y: torch.Tensor, wprior, offset, beta: np.nda
     return _irls_pass_ref(X, y, wprior, offset, beta, family, link, cls, var_power, link_power)
 
 
+def glm_grad_pass(X: torch.Tensor, y: torch.Tensor, wprior, offset, beta: np.ndarray, family: str, link: str,
+                  var_power: float = 1.5, link_power: float = 0.0):
+    """fp64 NumPy mirror of the HIP gradient pass: (sum_i r_ki [x_i | 1], deviance)."""
+    Xn = X.detach().cpu().double().numpy()
+    yn = y.detach().cpu().double().numpy()
+    w = np.ones_like(yn) if wprior is None else wprior.detach().cpu().double().numpy()
+    off = 0.0 if offset is None else offset.detach().cpu().double().numpy()
+    p, n = Xn.shape
+    K = beta.shape[0]
+    eta = beta[:, :p] @ Xn + beta[:, p:p + 1]
+    if family == "multinomial":
+        e = np.exp(eta - eta.max(0))
+        pr = e / e.sum(0)
+        Y = (yn[None, :].astype(np.int64) == np.arange(K)[:, None]).astype(np.float64)
+        R = w * (pr - Y)
+        dev = float((w * -2 * np.log(np.maximum(pr[yn.astype(np.int64), np.arange(n)], 1e-300))).sum())
+    else:
+        e0 = eta[0] + off
+        mu, dmu = _linkinv(e0, link, link_power)
+        if dmu is None:
+            dmu = np.maximum(mu * (1 - mu), 1e-10)
+        dmu = np.maximum(dmu, 1e-10) if link in ("log", "tweedie") and link_power == 0 else dmu
+        R = (w * (mu - yn) * dmu / glm_variance(family, mu, var_power))[None, :]
+        dev = float((w * glm_deviance(family, yn, mu, var_power)).sum())
+    g = np.concatenate([R @ Xn.T, R.sum(1, keepdims=True)], axis=1)
+    return g, dev
+
+
 def _linkinv(eta, link, link_power=0.0):
     if link == "logit":
         return 1 / (1 + np.exp(-eta)), None
