@@ -98,12 +98,96 @@ def _edges_from_sorted(col: np.ndarray, max_value_bins: int) -> np.ndarray:
     return e[: max_value_bins - 1]
 
 
+HISTOGRAM_TYPES = {"auto": "quantilesglobal", "quantilesglobal": "quantilesglobal",
+                   "uniformadaptive": "uniformadaptive", "uniformrobust": "uniformrobust", "random": "random"}
+
+
+def resolve_histogram_type(h) -> str:
+    """H2O ``histogram_type`` -> the cut-point rule of :func:`compute_edges`.
+
+    * QuantilesGlobal (and AUTO, the h2omx default: documented deviation from
+      H2O, whose AUTO is UniformAdaptive): global quantile cut points.
+    * UniformAdaptive: equal-width bins over the column's range.  H2O re-bins
+      every node's own [min, max] into ``nbins``; the global u8 codes here
+      cannot change per node, so the grid is the root's (nbins_top_level
+      resolution, capped at 255 bins).
+    * UniformRobust: equal-width bins over the central 99 % of the column
+      (values beyond fall into the outer bins).
+    * Random: sorted uniformly random cut points in the column's range
+      (seeded; H2O draws them per node).
+    * RoundRobin (a different type per tree) needs re-binned codes per tree
+      and is rejected."""
+    key = str(h or "AUTO").replace("_", "").lower()
+    if key == "roundrobin":
+        raise ValueError("histogram_type RoundRobin is not supported (it needs re-binned codes for every tree); "
+                         "use QuantilesGlobal, UniformAdaptive, UniformRobust or Random")
+    if key not in HISTOGRAM_TYPES:
+        raise ValueError(f"unknown histogram_type {h!r}")
+    return HISTOGRAM_TYPES[key]
+
+
+def _range_edges(lo: float, hi: float, nb: int, kind: str, rng: np.random.Generator) -> np.ndarray:
+    if not (np.isfinite(lo) and np.isfinite(hi)) or hi <= lo or nb < 2:
+        return np.zeros(0, np.float32)
+    if kind == "random":
+        e = np.sort(rng.uniform(lo, hi, nb - 1))
+    else:
+        e = lo + (hi - lo) * np.arange(1, nb) / nb
+    e = np.unique(e.astype(np.float32))
+    return e[(e >= lo) & (e < hi)]
+
+
 def compute_edges(X: torch.Tensor, nbins: int, sample_rows: int = 1 << 20, seed: int = 1234,
-                  comm=None) -> tuple[np.ndarray, np.ndarray, int]:
-    """Per-feature cut points from a row sample of feature-major ``X`` [F][n].
+                  comm=None, histogram_type: str = "QuantilesGlobal") -> tuple[np.ndarray, np.ndarray, int]:
+    """Per-feature cut points from a row sample of feature-major ``X`` [F][n]
+    (``histogram_type``: see :func:`resolve_histogram_type`; columns with at
+    most ``nbins`` distinct values always get one bin per value).
 
     Returns (edges [F][nbt] float32, nvb [F] int32, nbt).
     """
+    kind = resolve_histogram_type(histogram_type)
+    edges, nvb, nbt = _quantile_edges(X, nbins, sample_rows, seed, comm)
+    if kind == "quantilesglobal":
+        return edges, nvb, nbt
+    max_value_bins = min(nbins, nbt - 1)
+    # the column ranges over the same (all-gathered) sample on every rank
+    F, n = X.shape
+    Xs = X if n <= sample_rows else X.index_select(
+        1, torch.randint(0, n, (sample_rows,), generator=torch.Generator(device="cpu").manual_seed(seed)).to(X.device))
+    if comm is not None and comm.world_size > 1:
+        Xs = comm.all_gather_cat(Xs.contiguous(), dim=1)
+    Xs = Xs.float()
+    if kind == "uniformrobust":
+        q = torch.tensor([0.005, 0.995], dtype=torch.float32, device=Xs.device)
+        los, his = [], []
+        for f in range(F):
+            col = Xs[f][~torch.isnan(Xs[f])]
+            if col.numel() == 0:
+                los.append(np.nan)
+                his.append(np.nan)
+                continue
+            col = col[:: max(1, col.numel() // (1 << 22))]      # torch.quantile input limit
+            a, b = torch.quantile(col, q).tolist()
+            los.append(a)
+            his.append(b)
+        lo, hi = np.array(los), np.array(his)
+    else:
+        big = torch.finfo(torch.float32).max
+        nanm = torch.isnan(Xs)
+        lo = torch.where(nanm, big, Xs).amin(1).cpu().double().numpy()
+        hi = torch.where(nanm, -big, Xs).amax(1).cpu().double().numpy()
+    for f in range(F):
+        if int(nvb[f]) - 1 < max_value_bins - 1:
+            continue                     # few distinct values: exact value bins
+        rng = np.random.default_rng([seed & 0xFFFFFFFF, f])
+        e = _range_edges(float(lo[f]), float(hi[f]), max_value_bins, kind, rng)
+        edges[f, :] = np.inf
+        edges[f, : e.size] = e
+        nvb[f] = e.size + 1
+    return edges, nvb, nbt
+
+
+def _quantile_edges(X: torch.Tensor, nbins: int, sample_rows: int, seed: int, comm):
     F, n = X.shape
     nbt = hist_width(nbins)
     max_value_bins = min(nbins, nbt - 1)

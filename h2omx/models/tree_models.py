@@ -17,6 +17,7 @@ import torch
 from ..frame.frame import ENUM, Frame, Vec
 from .base import Model, ModelBuilder, ModelCategory
 from .tree import TreeParams, bin_matrix, compute_edges, train_ensemble
+from .tree.binning import resolve_histogram_type
 from .tree.boost import concat_trees
 
 
@@ -187,7 +188,12 @@ class _TreeBuilder(ModelBuilder):
                                                                      ModelCategory.MULTINOMIAL):
             w, balance = _balance_weights(y, w, len(self.response_domain), self.params, self.comm)
         nbins = int(self.params.get("nbins") or self.params.get("max_bins") or self.default_nbins)
-        edges, nvb, nbt = compute_edges(X, min(nbins, 255), seed=self._seed(), comm=self.comm)
+        htype = resolve_histogram_type(self.params.get("histogram_type"))
+        if htype in ("uniformadaptive", "random") and self.params.get("nbins_top_level"):
+            # root resolution of H2O's adaptive grid (per-node re-binning: see binning.py)
+            nbins = max(nbins, int(self.params["nbins_top_level"]))
+        edges, nvb, nbt = compute_edges(X, min(nbins, 255), seed=self._seed(), comm=self.comm,
+                                        histogram_type=htype)
         bm = bin_matrix(X, edges, nvb, nbt, names=self.x)
         tp = self._tree_params(len(self.x))
         nclass = len(self.response_domain) if self.response_domain else 1
@@ -568,7 +574,7 @@ class H2OGradientBoostingEstimator(_TreeBuilder):
     model_cls = GBMModel
     DEFAULTS = dict(ntrees=50, max_depth=5, min_rows=10.0, nbins=255, nbins_top_level=1024, nbins_cats=1024,
                     learn_rate=0.1, learn_rate_annealing=1.0, sample_rate=1.0, col_sample_rate=1.0,
-                    col_sample_rate_per_tree=1.0, min_split_improvement=1e-5, histogram_type="QuantilesGlobal",
+                    col_sample_rate_per_tree=1.0, min_split_improvement=1e-5, histogram_type="AUTO",
                     max_abs_leafnode_pred=0.0, tweedie_power=1.5, quantile_alpha=0.5, huber_alpha=0.9,
                     stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0,
                     offset_column=None, balance_classes=False, class_sampling_factors=None,
@@ -643,7 +649,7 @@ class H2ORandomForestEstimator(_TreeBuilder):
     default_nbins = 20
     DEFAULTS = dict(ntrees=50, max_depth=20, min_rows=1.0, nbins=20, nbins_top_level=1024, nbins_cats=1024,
                     mtries=-1, sample_rate=0.632, col_sample_rate_per_tree=1.0, min_split_improvement=1e-5,
-                    binomial_double_trees=False, histogram_type="QuantilesGlobal", stopping_rounds=0,
+                    binomial_double_trees=False, histogram_type="AUTO", stopping_rounds=0,
                     stopping_metric="AUTO", stopping_tolerance=1e-3, score_tree_interval=0, balance_classes=False,
                     class_sampling_factors=None, max_after_balance_size=5.0,
                     categorical_encoding="AUTO", offset_column=None, checkpoint=None,

@@ -289,7 +289,7 @@ class H2OUpliftRandomForestEstimator(ModelBuilder):
         dev = X.device
         nbins = max(2, min(int(p_["nbins"]), 254))
         seed = self._seed()
-        edges, nvb, nbt = compute_edges(X, nbins, seed=seed, comm=comm)
+        edges, nvb, nbt = compute_edges(X, nbins, seed=seed, comm=comm, histogram_type=p_.get("histogram_type"))
         bm = bin_matrix(X, edges, nvb, nbt, names=self.x)
         codes = bm.codes[:, :n]
         F = len(self.x)

@@ -25,3 +25,34 @@ def test_sort_rows_matches_torch_sort():
     for nb in (20, 255):
         for x, y in zip(_edges_device(a, nb), _edges_device(b, nb)):
             np.testing.assert_array_equal(x, y)
+
+
+def test_histogram_types():
+    """histogram_type: quantile vs equal-width vs robust vs random cut points;
+    few-valued columns keep one bin per value; RoundRobin / unknown rejected."""
+    import numpy as np
+    import pytest
+    import torch
+
+    from h2omx.models.tree.binning import compute_edges
+
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn((3, 20000), generator=g)
+    X[1] = X[1] ** 3                       # heavy tails
+    X[2] = torch.randint(0, 6, (20000,), generator=g).float()
+    eq, nvq, _ = compute_edges(X, 32, histogram_type="QuantilesGlobal")
+    eu, nvu, _ = compute_edges(X, 32, histogram_type="UniformAdaptive")
+    er, nvr, _ = compute_edges(X, 32, histogram_type="UniformRobust")
+    ex, nvx, _ = compute_edges(X, 32, histogram_type="Random")
+    ea, _, _ = compute_edges(X, 32, histogram_type="AUTO")
+    np.testing.assert_array_equal(ea, eq)
+    for e, nv in ((eu, nvu), (er, nvr), (ex, nvx)):
+        np.testing.assert_array_equal(e[2, : nv[2] - 1], np.arange(5, dtype=np.float32))   # value bins
+    d = np.diff(eu[0, : nvu[0] - 1])
+    assert np.allclose(d, d[0], rtol=1e-3)                                  # equal width
+    assert eu[1, 0] < er[1, 0] and er[1, nvr[1] - 2] < eu[1, nvu[1] - 2]     # robust range inside the full one
+    assert not np.allclose(np.diff(ex[0, : nvx[0] - 1]), d[0], rtol=1e-2)   # random spacing
+    with pytest.raises(ValueError, match="RoundRobin"):
+        compute_edges(X, 32, histogram_type="RoundRobin")
+    with pytest.raises(ValueError, match="unknown histogram_type"):
+        compute_edges(X, 32, histogram_type="Sturges")
