@@ -3,8 +3,9 @@
 //
 // The host flattens every root-to-leaf path of the ensemble into a leaf
 // record {first element, unique features m, leaf value} and m path elements
-// {feature | na_ok << 30, zero fraction z, lo, hi}: a row "follows" the path
-// on feature f (one fraction o = 1) when lo < x <= hi (NA: na_ok), and z is
+// {feature | na_ok << 30 | categorical << 29, zero fraction z, lo, hi}: a row
+// "follows" the path on feature f (one fraction o = 1) when lo < x <= hi (NA:
+// na_ok; categorical: level x in the path's level set sets[lo]), and z is
 // the product of the cover ratios of the path's edges on f.  For the path
 // polynomial P(t) = prod_j (z_j + o_j t) the Shapley contribution of
 // element i is
@@ -22,7 +23,8 @@ template <int MAXM, bool LDS>
 __global__ __launch_bounds__(256) void tree_shap_kernel(const float* __restrict__ X, int64_t ld, int64_t n, int F,
                                                         const int4* __restrict__ leaves, int nleaves,
                                                         const float4* __restrict__ elems,
-                                                        const float* __restrict__ wtab, float* __restrict__ out) {
+                                                        const float* __restrict__ wtab, float* __restrict__ out,
+                                                        const uint32_t* __restrict__ sets) {
   extern __shared__ float acc[];
   __shared__ float w_s[(MAXM + 1) * (MAXM + 1)];
   const int tid = threadIdx.x;
@@ -49,9 +51,19 @@ __global__ __launch_bounds__(256) void tree_shap_kernel(const float* __restrict_
       if (j < m) {
         const float4 e = elems[hd.x + j];
         const int fi = __float_as_int(e.x);
-        const int f = fi & 0x3FFFFFFF;
+        const int f = fi & 0x1FFFFFFF;
         const float x = X[(int64_t)f * ld + rr];
-        const float oj = (x != x) ? (float)((fi >> 30) & 1) : ((x > e.z && x <= e.w) ? 1.0f : 0.0f);
+        float oj;
+        if (x != x) {
+          oj = (float)((fi >> 30) & 1);
+        } else if ((fi >> 29) & 1) {
+          // categorical feature: the path's allowed level set (unseen levels: NA direction)
+          const int b = (int)x;
+          const uint32_t* st = sets + 8 * (int64_t)e.z;
+          oj = (b < 0 || b > 255) ? (float)((fi >> 30) & 1) : (float)((st[b >> 5] >> (b & 31)) & 1u);
+        } else {
+          oj = (x > e.z && x <= e.w) ? 1.0f : 0.0f;
+        }
         z[j] = e.y; o[j] = oj; fe[j] = f;
 #pragma unroll
         for (int k = MAXM; k >= 1; --k)
@@ -98,7 +110,8 @@ __global__ __launch_bounds__(256) void tree_shap_kernel(const float* __restrict_
 }  // namespace
 
 H2OMX_API int h2omx_tree_shap(const float* X, int64_t ld, int64_t n, int F, const void* leaves, int nleaves,
-                              const void* elems, const float* wtab, int maxm, float* out, hipStream_t stream) {
+                              const void* elems, const float* wtab, int maxm, float* out, const uint32_t* sets,
+                              hipStream_t stream) {
   if (n <= 0) return kOk;
   if (F <= 0 || maxm < 1 || maxm > 32) return kBadArg;
   const int grid = (int)((n + 255) / 256);
@@ -110,10 +123,10 @@ H2OMX_API int h2omx_tree_shap(const float* X, int64_t ld, int64_t n, int F, cons
   do {                                                                                                          \
     if (lds)                                                                                                    \
       hipLaunchKernelGGL((tree_shap_kernel<M, true>), dim3(grid), dim3(256), shm, stream, X, ld, n, F, lv,      \
-                         nleaves, el, wtab, out);                                                               \
+                         nleaves, el, wtab, out, sets);                                                         \
     else                                                                                                        \
       hipLaunchKernelGGL((tree_shap_kernel<M, false>), dim3(grid), dim3(256), 0, stream, X, ld, n, F, lv,       \
-                         nleaves, el, wtab, out);                                                               \
+                         nleaves, el, wtab, out, sets);                                                         \
   } while (0)
   if (maxm <= 8) H2OMX_SHAP(8);
   else if (maxm <= 16) H2OMX_SHAP(16);

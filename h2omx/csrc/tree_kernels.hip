@@ -67,6 +67,15 @@ struct SplitParams {
   // feature on the path yet)
   const unsigned long long* ifsets;
   long long* istate;
+  // categorical group splits (nullptr = no categorical features): catf[F] = 1
+  // for an identity-binned enum column (bin = level code); a split of such a
+  // feature sends a SET of levels left (levels sorted by G / S inside the node,
+  // best prefix of that order).  fbcat [max_nodes][F][8] holds each (node,
+  // feature) winner's left-set bitset (256 bits); the finalisation copies the
+  // chosen one into treecat [capacity][8] (the tree's bitsets, by node id)
+  const uint8_t* catf;
+  uint32_t* fbcat;
+  uint32_t* treecat;
 };
 
 struct NodeSplit {  // best split of one node at the current level (64 B)
@@ -88,8 +97,8 @@ struct NodeLink {  // per node of a level: where its histogram comes from
 
 struct PartInfo {  // per node of a level: routing decision for partition
   int feat;
-  int bin;
-  int na_left;
+  int bin;       // threshold bin; categorical split: low 32 bits of its bitset pointer
+  int na_left;   // bit 0: NA goes left; bit 1: categorical split; bits 8..31: bitset pointer >> 32
   int child;  // local id of left child at next level, -1 = node is a leaf
   int gid;    // global node id inside the tree
   int leaf_children;  // 1: children are leaves, rows retire into them now
@@ -101,12 +110,32 @@ struct TreeNode {  // model representation (32 B)
   int feat;      // -1 = leaf
   int bin;
   int left;      // global id of left child (right = left + 1)
-  int na_left;
+  int na_left;   // bit 0: NA goes left; bit 1: categorical split (left set = the tree's bitset of this node)
   float thr;     // raw-value threshold: x <= thr goes left (NaN -> na_left)
   float value;   // leaf value (already scaled by the learning rate)
   float gain;
   float weight;  // sum of weights in the node
 };
+
+// Routing of a row with bin code b through a split record: 1 = right.
+// Categorical splits test the left-set bitset the record points to (bits of
+// the tree's bitset table, see SplitParams::treecat); numeric ones the bin.
+__device__ __forceinline__ int part_right(const PartInfo& pi, int b, int nbt) {
+  if (b == nbt - 1) return !(pi.na_left & 1);
+  if (pi.na_left & 2) {
+    const uint32_t* bits = reinterpret_cast<const uint32_t*>(
+        (uint64_t)(uint32_t)pi.bin | ((uint64_t)((uint32_t)pi.na_left >> 8) << 32));
+    return !((bits[b >> 5] >> (b & 31)) & 1u);
+  }
+  return b > pi.bin;
+}
+
+// the record fields of a categorical split whose left set is `bits`
+__device__ __forceinline__ void part_set_cat(PartInfo& pi, const uint32_t* bits, int na_left) {
+  const uint64_t a = reinterpret_cast<uint64_t>(bits);
+  pi.bin = (int)(uint32_t)a;
+  pi.na_left = (na_left & 1) | 2 | (int)((uint32_t)(a >> 32) << 8);
+}
 
 // ctl layout (int32 device array, one per level buffer):
 //   [0] n_nodes at this level, [1] n_slots built at this level,
@@ -484,7 +513,7 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
         for (int k = 0; k < ROWS; ++k) {
           if (nn[k] == j) {
             const int bc = (cw[k >> 2] >> (8 * (k & 3))) & 0xff;
-            const int right = (bc == NBT - 1) ? !pj.na_left : (bc > pj.bin);
+            const int right = part_right(pj, bc, NBT);
             nx[k] = pj.child + right;
             s[k] = right ? sl_r : sl_l;
           }
@@ -1114,7 +1143,7 @@ __global__ __launch_bounds__(ROUTE ? 512 : 1024) void hist_build_rm_kernel(
         for (int k = 0; k < ROWS; ++k) {
           if (nn[k] == j) {
             const int bc = (cw[k >> 2] >> (8 * (k & 3))) & 0xff;
-            const int right = (bc == NBT - 1) ? !pj.na_left : (bc > pj.bin);
+            const int right = part_right(pj, bc, NBT);
             nx[k] = pj.child + right;
             s[k] = right ? sl_r : sl_l;
           }
@@ -1352,7 +1381,121 @@ struct WaveBest {
   int code;
 };
 
+// Categorical (node, feature): H2O / LightGBM group split.  The non-empty
+// level bins are ordered by G / S (S = W or H by mode; ties by level code,
+// empty bins last), and every prefix of that order is a candidate left set,
+// scored for both NA directions like a threshold.  One wave, no LDS: each
+// lane's inclusive prefix in sorted order comes from an all-pairs pass over
+// the NBT bins (256 shuffled (key, G, S) triples - categorical features are
+// few and this runs per node only for them).  The winner's left set is
+// written as a 256-bit bitset to p.fbcat[node][f].
 template <int NBT>
+__device__ __forceinline__ WaveBest feat_best_cat_wave(const long long* gi, const long long* si, long long ng_i,
+                                                    long long ns_i, int node, int f, int m, double ig, double is,
+                                                    const SplitParams& p) {
+  constexpr int B = NBT <= 64 ? 1 : NBT / 64;
+  const int lane = threadIdx.x & 63;
+  double key[B];
+  bool ne[B];
+  long long tg_l = 0, ts_l = 0;
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const int bin = lane * B + k;
+    ne[k] = bin < m && bin < NBT - 1 && si[k] > 0;
+    key[k] = ne[k] ? (double)gi[k] / (double)si[k] : INFINITY;
+    tg_l += gi[k];
+    ts_l += si[k];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    tg_l += __shfl_xor(tg_l, o, kWave);
+    ts_l += __shfl_xor(ts_l, o, kWave);
+  }
+  const double tg = (double)(tg_l + ng_i) * ig, ts = (double)(ts_l + ns_i) * is;
+  const double ng = (double)ng_i * ig, ns = (double)ns_i * is;
+  long long cg[B], cs[B];
+#pragma unroll
+  for (int k = 0; k < B; ++k) { cg[k] = 0; cs[k] = 0; }
+  const int lanes = NBT < 64 ? NBT : 64;
+  for (int jl = 0; jl < lanes; ++jl) {
+#pragma unroll
+    for (int jk = 0; jk < B; ++jk) {
+      const double kj = __shfl(key[jk], jl, kWave);
+      const long long gj = __shfl(gi[jk], jl, kWave), sj = __shfl(si[jk], jl, kWave);
+      const int j = jl * B + jk;
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const int bin = lane * B + k;
+        if (ne[k] && (kj < key[k] || (kj == key[k] && j <= bin))) { cg[k] += gj; cs[k] += sj; }
+      }
+    }
+  }
+  double best_gain = -INFINITY;
+  int best_code = 0x7fffffff;
+  double bGL = 0, bSL = 0;
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const int t = lane * B + k;
+    if (!ne[k]) continue;
+    const double sg = (double)cg[k] * ig, ssum = (double)cs[k] * is;
+    const double gA = split_gain(sg, ssum, tg, ts, p);
+    const double gB = ns > 0.0 ? split_gain(sg + ng, ssum + ns, tg, ts, p) : -INFINITY;
+    if (gA > -INFINITY && (gA > best_gain || (gA == best_gain && 2 * t < best_code))) {
+      best_gain = gA; best_code = 2 * t; bGL = sg; bSL = ssum;
+    }
+    if (gB > -INFINITY && (gB > best_gain || (gB == best_gain && 2 * t + 1 < best_code))) {
+      best_gain = gB; best_code = 2 * t + 1; bGL = sg + ng; bSL = ssum + ns;
+    }
+  }
+  double bg = best_gain;
+  int bc = best_code;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(bg, o, kWave);
+    const int oc = __shfl_xor(bc, o, kWave);
+    if (og > bg || (og == bg && oc < bc)) { bg = og; bc = oc; }
+  }
+  WaveBest r;
+  r.G = tg; r.S = ts;
+  r.gain = (bc == 0x7fffffff) ? -INFINITY : bg;
+  r.code = bc;
+  r.GL = r.SL = 0.0;
+  uint32_t word = 0;
+  if (bc != 0x7fffffff) {
+    const unsigned long long own = __ballot(best_code == bc);
+    const int src = __ffsll((long long)own) - 1;
+    r.GL = __shfl(bGL, src, kWave);
+    r.SL = __shfl(bSL, src, kWave);
+    // left set: every non-empty bin at or before the winner in (key, level) order
+    const int wb = bc >> 1;
+    double kown = key[0];
+#pragma unroll
+    for (int k = 1; k < B; ++k)
+      if (k == wb % B) kown = key[k];
+    const double kw = __shfl(kown, wb / B, kWave);
+    uint32_t nib = 0;
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+      const int bin = lane * B + k;
+      if (ne[k] && (key[k] < kw || (key[k] == kw && bin <= wb))) nib |= 1u << k;
+    }
+    constexpr int LPW = 32 / B;   // lanes per 32-bit bitset word
+    word = nib << (B * (lane % LPW));
+#pragma unroll
+    for (int o = 1; o < LPW; o <<= 1) word |= __shfl_xor(word, o, kWave);
+  }
+  // lanes 0..7 store the 8 words (word w lives in lane w * LPW; words past the
+  // last lane's bins are zero)
+  {
+    constexpr int LPW = 32 / B;
+    const int srcl = lane * LPW;
+    const uint32_t wv = __shfl(word, srcl < 64 ? srcl : 63, kWave);
+    if (lane < 8) p.fbcat[((int64_t)node * p.F + f) * 8 + lane] = (srcl < 64) ? wv : 0u;
+  }
+  return r;
+}
+
+template <int NBT, bool CAT = false>
 __device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__ built,
                                                    const long long* __restrict__ parent_full,
                                                    long long* __restrict__ full, const NodeLink& lk, int node, int f,
@@ -1435,6 +1578,10 @@ __device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__
   constexpr int NA_LANE = (NBT - 1) / B, NA_K = (NBT - 1) % B;
   const long long ng_i = __shfl(gi[NA_K], NA_LANE, kWave), ns_i = __shfl(si[NA_K], NA_LANE, kWave);
   if (lane == NA_LANE) { gi[NA_K] = 0; si[NA_K] = 0; }
+  if constexpr (CAT) {   // instantiated only for data with categorical features
+    if (p.catf != nullptr && p.catf[f])
+      return feat_best_cat_wave<NBT>(gi, si, ng_i, ns_i, node, f, nvb[f], ig, is, p);
+  }
   long long lg = 0, ls = 0;  // inclusive local prefix
   long long pg[B], ps[B];
 #pragma unroll
@@ -1504,7 +1651,7 @@ __device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__
 // level, so per-block latency dominates), converted to fp64 exactly and
 // scored for both NA directions.  mtries / column sampling ranks the
 // feature's hash among all features with one ballot per 64 features.
-template <int NBT>
+template <int NBT, bool CAT>
 __global__ __launch_bounds__(256) void split_find_kernel(const long long* __restrict__ built,
                                                          const long long* __restrict__ parent_full,
                                                          long long* __restrict__ full, const int* __restrict__ ctl,
@@ -1518,8 +1665,8 @@ __global__ __launch_bounds__(256) void split_find_kernel(const long long* __rest
   const int f = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (f >= p.F) return;  // whole wave
   const NodeLink lk = link[node];
-  const WaveBest w = feat_best_wave<NBT>(built, parent_full, full, lk, node, f, nvb, tree_fmask, qscale[2],
-                                         qscale[3], p, ctl[CTL_BASE] + node);
+  const WaveBest w = feat_best_wave<NBT, CAT>(built, parent_full, full, lk, node, f, nvb, tree_fmask, qscale[2],
+                                              qscale[3], p, ctl[CTL_BASE] + node);
   if ((threadIdx.x & 63) == 0) {
     FeatBest r{};
     r.gain = w.gain; r.GL = w.GL; r.SL = w.SL;
@@ -1616,6 +1763,17 @@ __device__ __forceinline__ void lf_write_node(int i, const NodeSplit& s, bool do
     tn.feat = s.feat; tn.bin = s.bin; tn.na_left = s.na_left; tn.left = next_base + 2 * k_idx;
     const int m = nvb[s.feat];
     tn.thr = (s.bin < m - 1) ? edges[(int64_t)s.feat * nbt + s.bin] : INFINITY;
+    if (p.catf != nullptr && p.catf[s.feat] && gid < tree_capacity) {
+      // categorical group split: the (node, feature) scan's left-set bitset
+      // becomes the tree's bitset of this node, and the partition record points at it
+      const uint32_t* src = p.fbcat + ((int64_t)i * p.F + s.feat) * 8;
+      uint32_t* dst = p.treecat + (int64_t)gid * 8;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) dst[w] = src[w];
+      part_set_cat(pi, dst, s.na_left);
+      tn.na_left = (s.na_left & 1) | 2;
+      tn.thr = __int_as_float(0x7fc00000);   // NaN: not a threshold split
+    }
     const bool build_left = s.WL <= (s.W - s.WL);
     NodeLink L, R;
     L.parent = R.parent = i;
@@ -2118,7 +2276,7 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
           leaf = pi.gid;
         } else {
           const int b = codes[(int64_t)pi.feat * npad + r0 + k];
-          const int right = (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
+          const int right = part_right(pi, b, nbt);
           if (pi.leaf_children) {
             leaf = pi.child_gid + right;
           } else {
@@ -2159,7 +2317,7 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
             leaf = p.gid;
           } else {
             const int b = bc[k];
-            const int right = (b == nbt - 1) ? !p.na_left : (b > p.bin);
+            const int right = part_right(p, b, nbt);
             if (p.leaf_children) {
               leaf = p.child_gid + right;
             } else {
@@ -2327,7 +2485,7 @@ __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ 
             if (fe[k] == f) {
               const PartInfo& pi = pi_s[nn[k]];
               const int bc = (cw[k >> 2] >> (8 * (k & 3))) & 0xff;
-              const int rt = (bc == nbt - 1) ? !pi.na_left : (bc > pi.bin);
+              const int rt = part_right(pi, bc, nbt);
               right |= (uint32_t)rt << k;
             }
           }
@@ -2770,10 +2928,18 @@ H2OMX_API int64_t h2omx_mono_scratch_bytes(int cap) { return (((int64_t)cap * 4 
 // nodes: all trees concatenated; roots[t] = offset of tree t; out[cls][r] +=
 // sum of leaf values of the trees of class cls (tree t belongs to class t % K).
 // ---------------------------------------------------------------------------
+// categorical split of a tree node: is level / bin code b in its left set?
+// (codes outside 0..255 - unseen levels - follow the NA direction)
+__device__ __forceinline__ bool cat_left(const uint32_t* __restrict__ bits, int b, int na_left) {
+  if (b < 0 || b > 255) return (na_left & 1) != 0;
+  return ((bits[b >> 5] >> (b & 31)) & 1u) != 0;
+}
+
 __global__ __launch_bounds__(256) void predict_raw_kernel(const float* __restrict__ X, int64_t ld, int64_t n,
                                                           const TreeNode* __restrict__ nodes,
                                                           const int* __restrict__ roots, int ntrees, int K,
-                                                          float* __restrict__ out, int64_t ldo) {
+                                                          float* __restrict__ out, int64_t ldo,
+                                                          const uint32_t* __restrict__ catbits) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   for (int t = 0; t < ntrees; ++t) {
@@ -2783,7 +2949,10 @@ __global__ __launch_bounds__(256) void predict_raw_kernel(const float* __restric
       const TreeNode nd = tr[id];
       if (nd.feat < 0) break;
       const float v = X[(int64_t)nd.feat * ld + r];
-      const bool left = (v != v) ? (nd.na_left != 0) : (v <= nd.thr);
+      bool left;
+      if (v != v) left = (nd.na_left & 1) != 0;
+      else if (nd.na_left & 2) left = cat_left(catbits + 8 * ((int64_t)roots[t] + id), (int)v, nd.na_left);
+      else left = v <= nd.thr;
       id = left ? nd.left : nd.left + 1;
     }
     out[(int64_t)(t % K) * ldo + r] += tr[id].value;
@@ -2794,7 +2963,8 @@ __global__ __launch_bounds__(256) void predict_raw_kernel(const float* __restric
 __global__ __launch_bounds__(256) void predict_binned_kernel(const uint8_t* __restrict__ codes, int64_t npad,
                                                              int64_t n, const TreeNode* __restrict__ nodes,
                                                              const int* __restrict__ roots, int ntrees, int K,
-                                                             int nbt, float* __restrict__ out, int64_t ldo) {
+                                                             int nbt, float* __restrict__ out, int64_t ldo,
+                                                             const uint32_t* __restrict__ catbits) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   for (int t = 0; t < ntrees; ++t) {
@@ -2804,7 +2974,10 @@ __global__ __launch_bounds__(256) void predict_binned_kernel(const uint8_t* __re
       const TreeNode nd = tr[id];
       if (nd.feat < 0) break;
       const int b = codes[(int64_t)nd.feat * npad + r];
-      const bool left = (b == nbt - 1) ? (nd.na_left != 0) : (b <= nd.bin);
+      bool left;
+      if (b == nbt - 1) left = (nd.na_left & 1) != 0;
+      else if (nd.na_left & 2) left = cat_left(catbits + 8 * ((int64_t)roots[t] + id), b, nd.na_left);
+      else left = b <= nd.bin;
       id = left ? nd.left : nd.left + 1;
     }
     out[(int64_t)(t % K) * ldo + r] += tr[id].value;
@@ -3068,9 +3241,13 @@ H2OMX_API int h2omx_split_find(const long long* built, const long long* parent_f
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
   FeatBest* o = reinterpret_cast<FeatBest*>(out);
   const dim3 grid(max_nodes, (p.F + 3) / 4);
-#define H2OMX_SF(NB)                                                                                      \
-  hipLaunchKernelGGL(split_find_kernel<NB>, grid, dim3(256), 0, stream, built, parent_full, full, ctl, lk, \
-                     nvb, tree_fmask, qscale, p, o)
+#define H2OMX_SF(NB)                                                                                          \
+  if (p.catf != nullptr)                                                                                      \
+    hipLaunchKernelGGL((split_find_kernel<NB, true>), grid, dim3(256), 0, stream, built, parent_full, full, ctl, \
+                       lk, nvb, tree_fmask, qscale, p, o);                                                    \
+  else                                                                                                        \
+    hipLaunchKernelGGL((split_find_kernel<NB, false>), grid, dim3(256), 0, stream, built, parent_full, full,    \
+                       ctl, lk, nvb, tree_fmask, qscale, p, o)
   switch (nbt) {
     case 32: H2OMX_SF(32); break;
     case 64: H2OMX_SF(64); break;
@@ -3390,18 +3567,21 @@ H2OMX_API int h2omx_leaf_finalize_mono(const unsigned long long* acc, const int*
   return launch_status();
 }
 
+// catbits: [total nodes][8] left-set bitsets aligned with `nodes` (nullptr:
+// no categorical splits)
 H2OMX_API int h2omx_predict_raw(const float* X, int64_t ld, int64_t n, const void* nodes, const int* roots,
-                                int ntrees, int K, float* out, int64_t ldo, hipStream_t stream) {
+                                int ntrees, int K, float* out, int64_t ldo, const uint32_t* catbits,
+                                hipStream_t stream) {
   hipLaunchKernelGGL(predict_raw_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, X, ld, n,
-                     reinterpret_cast<const TreeNode*>(nodes), roots, ntrees, K, out, ldo);
+                     reinterpret_cast<const TreeNode*>(nodes), roots, ntrees, K, out, ldo, catbits);
   return launch_status();
 }
 
 H2OMX_API int h2omx_predict_binned(const uint8_t* codes, int64_t npad, int64_t n, const void* nodes,
                                    const int* roots, int ntrees, int K, int nbt, float* out, int64_t ldo,
-                                   hipStream_t stream) {
+                                   const uint32_t* catbits, hipStream_t stream) {
   hipLaunchKernelGGL(predict_binned_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, codes, npad, n,
-                     reinterpret_cast<const TreeNode*>(nodes), roots, ntrees, K, nbt, out, ldo);
+                     reinterpret_cast<const TreeNode*>(nodes), roots, ntrees, K, nbt, out, ldo, catbits);
   return launch_status();
 }
 
@@ -3581,7 +3761,7 @@ __global__ __launch_bounds__(256) void hist_reduce_seg_kernel(const unsigned lon
 __device__ __forceinline__ int split_dir(const uint8_t* __restrict__ codes, int64_t npad, const PartInfo& pi,
                                          int nbt, int r) {
   const int b = codes[(int64_t)pi.feat * npad + r];
-  return (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
+  return part_right(pi, b, nbt);
 }
 
 // number of rows of chunk c going left (nodes that split into inner nodes)
@@ -4644,7 +4824,7 @@ __global__ __launch_bounds__(256) void part_count_wave_kernel(const uint8_t* __r
       int d;
       if (ecodes) {
         const int b = ecodes[(int64_t)j * ecs + eq];
-        d = (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
+        d = part_right(pi, b, nbt);
       } else {
         d = split_dir(codes, npad, pi, nbt, idx ? idx[j] : j);
       }
@@ -4698,7 +4878,7 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
           dir = dirb[j];
         } else if (ecodes) {
           const int b = ecodes[(int64_t)j * ecs + nodeq[node]];
-          dir = (b == nbt - 1) ? !pi.na_left : (b > pi.bin);
+          dir = part_right(pi, b, nbt);
         } else {
           dir = split_dir(codes, npad, pi, nbt, r);
         }

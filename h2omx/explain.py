@@ -27,16 +27,21 @@ from .models.base import ModelCategory
 # ---------------------------------------------------------------------------
 # TreeSHAP
 # ---------------------------------------------------------------------------
-def tree_paths(trees: np.ndarray, scale: float = 1.0):
+def tree_paths(trees: np.ndarray, scale: float = 1.0, catbits: np.ndarray | None = None):
     """Flatten every root-to-leaf path: returns (leaves [L][4] int32 =
     {first element, m, value bits, tree}, elems [E][4] float32 = {feature |
-    na_ok << 30, z, lo, hi}, expected value, max unique features)."""
-    leaves, elems = [], []
+    na_ok << 30 | categorical << 29, z, lo, hi}, expected value, max unique
+    features, sets [S][8] uint32).  A categorical feature's element keeps the
+    set of levels the path allows (intersection of its group splits' sides)
+    in ``sets[lo]``."""
+    leaves, elems, sets = [], [], []
     expected = 0.0
     maxm = 1
+    full = np.full(8, 0xFFFFFFFF, np.uint32)
     for t in range(trees.shape[0]):
         tr = trees[t]
-        # stack entries: (node, {feature: [z, lo, hi, na_ok]})
+        cb = None if catbits is None else catbits[t]
+        # stack entries: (node, {feature: [z, lo, hi, na_ok, level set or None]})
         stack = [(0, {})]
         while stack:
             i, path = stack.pop()
@@ -46,33 +51,43 @@ def tree_paths(trees: np.ndarray, scale: float = 1.0):
                 m = len(path)
                 zprod = 1.0
                 start = len(elems)
-                for f, (z, lo, hi, na) in path.items():
-                    elems.append((np.int32(f | (int(na) << 30)).view(np.float32), z, lo, hi))
+                for f, (z, lo, hi, na, st) in path.items():
+                    if st is not None:
+                        elems.append((np.int32(f | (int(na) << 30) | (1 << 29)).view(np.float32), z,
+                                      float(len(sets)), 0.0))
+                        sets.append(st)
+                    else:
+                        elems.append((np.int32(f | (int(na) << 30)).view(np.float32), z, lo, hi))
                     zprod *= z
                 leaves.append((start, m, np.float32(v).view(np.int32), t))
                 expected += v * zprod
                 maxm = max(maxm, m)
                 continue
             f, thr, left = int(nd["feat"]), float(nd["thr"]), int(nd["left"])
+            is_cat = cb is not None and (int(nd["na_left"]) & 2) != 0
             w = float(nd["weight"])
             for child, go_left in ((left, True), (left + 1, False)):
                 cw = float(tr[child]["weight"])
                 r = cw / w if w > 0 else 0.0
-                z, lo, hi, na = path.get(f, (1.0, -np.inf, np.inf, True))
-                if go_left:
+                z, lo, hi, na, st = path.get(f, (1.0, -np.inf, np.inf, True, None))
+                if is_cat:
+                    side = cb[i] if go_left else ~cb[i]
+                    st = (full if st is None else st) & side
+                elif go_left:
                     hi = min(hi, thr)
                 else:
                     lo = max(lo, thr)
-                na = na and (bool(nd["na_left"]) == go_left)
+                na = na and (bool(int(nd["na_left"]) & 1) == go_left)
                 p2 = dict(path)
-                p2[f] = (z * r, lo, hi, na)
+                p2[f] = (z * r, lo, hi, na, st)
                 stack.append((child, p2))
     lv = np.asarray(leaves, np.int32).reshape(-1, 4)
     el = np.asarray([(e[0], e[1], e[2], e[3]) for e in elems], np.float32).reshape(-1, 4) if elems else \
         np.zeros((0, 4), np.float32)
     if elems:
         el[:, 0] = np.asarray([e[0] for e in elems], np.float32)
-    return lv, el, expected, maxm
+    st = np.asarray(sets, np.uint32).reshape(-1, 8) if sets else np.zeros((1, 8), np.uint32)
+    return lv, el, expected, maxm, st
 
 
 def shapley_weights(M: int) -> np.ndarray:
@@ -88,7 +103,7 @@ def _bucket(maxm: int) -> int:
     return 8 if maxm <= 8 else (16 if maxm <= 16 else 32)
 
 
-def _shap_numpy(X: np.ndarray, lv, el, maxm) -> np.ndarray:
+def _shap_numpy(X: np.ndarray, lv, el, maxm, sets=None) -> np.ndarray:
     F, n = X.shape
     out = np.zeros((F, n), np.float64)
     W = shapley_weights(maxm)
@@ -98,12 +113,22 @@ def _shap_numpy(X: np.ndarray, lv, el, maxm) -> np.ndarray:
             continue
         E = el[start: start + m]
         feats = E[:, 0].view(np.int32)
-        f = feats & 0x3FFFFFFF
+        f = feats & 0x1FFFFFFF
         na_ok = (feats >> 30) & 1
+        iscat = (feats >> 29) & 1
         z = E[:, 1].astype(np.float64)
         x = X[f]                                       # [m][n]
-        o = np.where(np.isnan(x), na_ok[:, None].astype(np.float64),
-                     ((x > E[:, 2:3]) & (x <= E[:, 3:4])).astype(np.float64))
+        with np.errstate(invalid="ignore"):
+            o = np.where(np.isnan(x), na_ok[:, None].astype(np.float64),
+                         ((x > E[:, 2:3]) & (x <= E[:, 3:4])).astype(np.float64))
+        if sets is not None and iscat.any():
+            from .models.tree.structs import bitset_has
+
+            for j in np.nonzero(iscat)[0]:
+                c = np.where(np.isnan(x[j]), -1, x[j]).astype(np.int64)
+                oor = (c < 0) | (c > 255)
+                inside = bitset_has(sets[int(E[j, 2])], c).astype(np.float64)
+                o[j] = np.where(np.isnan(x[j]) | oor, float(na_ok[j]), inside)
         P = np.zeros((m + 1, n))
         P[0] = 1.0
         for j in range(m):
@@ -137,7 +162,8 @@ def predict_contributions(model, frame: Frame) -> Frame:
     F, n = X.shape
     nt = ens.ntrees
     scale = 1.0 / nt if (ens.average and nt > 0) else 1.0
-    lv, el, expected, maxm = tree_paths(ens.trees[:nt], scale)
+    cb = getattr(ens, "catbits", None)
+    lv, el, expected, maxm, sets = tree_paths(ens.trees[:nt], scale, None if cb is None else cb[:nt])
     bias = expected + (0.0 if ens.average else float(ens.init_f[0]))
     if X.is_cuda:
         from .ops import P, check, explain_lib, stream
@@ -149,10 +175,11 @@ def predict_contributions(model, frame: Frame) -> Frame:
         lvd = torch.from_numpy(lv).to(dev)
         eld = torch.from_numpy(el if el.size else np.zeros((1, 4), np.float32)).to(dev)
         out = torch.zeros((F, n), dtype=torch.float32, device=dev)
+        setd = torch.from_numpy(sets.view(np.int32).copy()).to(dev)
         check(explain_lib().h2omx_tree_shap(P(Xc), Xc.stride(0), n, F, P(lvd), int(lv.shape[0]), P(eld), P(wt),
-                                            maxm, P(out), stream(dev)), "tree_shap")
+                                            maxm, P(out), P(setd), stream(dev)), "tree_shap")
     else:
-        out = torch.from_numpy(_shap_numpy(X.double().numpy(), lv, el, maxm).astype(np.float32))
+        out = torch.from_numpy(_shap_numpy(X.double().numpy(), lv, el, maxm, sets).astype(np.float32))
     vecs = [Vec(c, out[j], "real") for j, c in enumerate(model.x)]
     vecs.append(Vec("BiasTerm", torch.full((n,), float(bias), dtype=torch.float32, device=out.device), "real"))
     return Frame(vecs)

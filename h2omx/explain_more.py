@@ -43,13 +43,13 @@ def _tree_models(model):
     return ens
 
 
-def _walk(tree: np.ndarray, X: torch.Tensor):
+def _walk(tree: np.ndarray, X: torch.Tensor, catbits: np.ndarray | None = None):
     """Leaf index and path bits (bit d = went right at depth d) for every row."""
+    from .models.tree.structs import TreeWalker
+
     dev = X.device
-    feat = torch.from_numpy(tree["feat"].astype(np.int64)).to(dev)
-    thr = torch.from_numpy(tree["thr"].astype(np.float32)).to(dev)
-    nal = torch.from_numpy(tree["na_left"].astype(np.int64)).to(dev) != 0
-    left = torch.from_numpy(tree["left"].astype(np.int64)).to(dev)
+    tw = TreeWalker(tree, catbits, dev)
+    feat, left = tw.feat, tw.left
     n = X.shape[1]
     idx = torch.zeros(n, dtype=torch.long, device=dev)
     bits = torch.zeros(n, dtype=torch.long, device=dev)
@@ -62,13 +62,18 @@ def _walk(tree: np.ndarray, X: torch.Tensor):
         if not bool(inner.any()):
             break
         v = X[f.clamp_min(0), rows]
-        go_left = torch.where(torch.isnan(v), nal[idx], v <= thr[idx])
+        go_left = tw.go_left(idx, v)
         right = inner & ~go_left
         used.append(torch.where(inner, f, torch.full_like(f, -1)))
         bits = bits | (right.long() << depth.clamp(max=62))
         depth = depth + inner.long()
         idx = torch.where(inner, left[idx] + right.long(), idx)
     return idx, bits, depth, used
+
+
+def _cb(ens, t):
+    cb = getattr(ens, "catbits", None)
+    return None if cb is None else cb[t]
 
 
 def _X(model, frame):
@@ -81,7 +86,7 @@ def predict_leaf_node_assignment(model, frame: Frame, type: str = "Path") -> Fra
     X = _X(model, frame).float()
     vecs = []
     for t in range(ens.ntrees * ens.K):
-        idx, bits, depth, _ = _walk(ens.trees[t], X)
+        idx, bits, depth, _ = _walk(ens.trees[t], X, _cb(ens, t))
         name = f"T{t // ens.K + 1}.C{t % ens.K + 1}"
         if str(type).lower() == "node_id":
             vecs.append(Vec(name, idx.float(), "int"))
@@ -106,7 +111,7 @@ def staged_predict_proba(model, frame: Frame) -> Frame:
     vecs = []
     for t in range(ens.ntrees):
         for k in range(K):
-            idx, _, _, _ = _walk(ens.trees[t * K + k], X)
+            idx, _, _, _ = _walk(ens.trees[t * K + k], X, _cb(ens, t * K + k))
             acc[k] += torch.from_numpy(ens.trees[t * K + k]["value"].astype(np.float64)).to(X.device)[idx]
         margin = (acc / (t + 1)) if ens.average else acc
         P = model._link(margin.float())
@@ -124,7 +129,7 @@ def feature_frequencies(model, frame: Frame) -> Frame:
     F, n = X.shape
     cnt = torch.zeros((F + 1, n), dtype=torch.float32, device=X.device)
     for t in range(ens.ntrees * ens.K):
-        _, _, _, used = _walk(ens.trees[t], X)
+        _, _, _, used = _walk(ens.trees[t], X, _cb(ens, t))
         for f in used:
             cnt.scatter_add_(0, torch.where(f >= 0, f, torch.full_like(f, F))[None, :],
                              torch.ones((1, n), device=X.device))

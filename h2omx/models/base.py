@@ -67,6 +67,9 @@ class Model:
             cls.predict_raw = predict_raw
 
     def adapt_frame(self, frame: Frame) -> Frame:
+        enc = getattr(self, "cat_encoder", None)
+        if enc is not None:
+            frame = enc.transform(frame)
         cols = [c for c in self.x if self.feature_types.get(c) == ENUM]
         doms = {c: self.feature_domains.get(c) or [] for c in cols}
         if self.y is not None and self.response_domain is not None:
@@ -98,6 +101,7 @@ class Model:
         self.response_domain = builder.response_domain
         self.feature_types = dict(builder.feature_types)
         self.feature_domains = dict(builder.feature_domains)
+        self.cat_encoder = getattr(builder, "cat_encoder", None)
         self.training_metrics: dict | None = None
         self.validation_metrics: dict | None = None
         self.cross_validation_metrics: dict | None = None
@@ -356,6 +360,7 @@ class ModelBuilder:
             v = training_frame.vec(c)
             self.feature_types[c] = v.vtype
             self.feature_domains[c] = v.domain
+        training_frame, validation_frame = self._encode_categoricals(training_frame, validation_frame)
         model_id = self.params.get("model_id") or f"{self.algo.upper()}_model_{next(_model_counter)}_{uuid.uuid4().hex[:6]}"
         nfolds = int(self.params.get("nfolds") or 0)
         cv_models, holdout = [], None
@@ -376,6 +381,37 @@ class ModelBuilder:
         DKV.put(model.model_id, model)
         self.model = model
         return model
+
+    # categorical_encoding schemes the algorithm handles itself (frame/encoding.py)
+    NATIVE_ENCODINGS = ("auto", "enum", "onehotinternal")
+
+    def _encoding_scheme(self) -> str:
+        """The effective categorical_encoding of this algorithm (validated)."""
+        from ..frame.encoding import normalize_scheme
+
+        return normalize_scheme(self.params.get("categorical_encoding"))
+
+    def _encode_categoricals(self, train: Frame, valid: Frame | None):
+        """Apply a frame-transform categorical_encoding (OneHotExplicit, Binary,
+        Eigen, LabelEncoder, EnumLimited, SortByResponse where the algorithm
+        has no native form) to the training / validation frames; the fitted
+        encoder is kept for scoring (Model.adapt_frame)."""
+        from ..frame.encoding import TRANSFORMS, CategoricalEncoder
+
+        self.cat_encoder = None
+        scheme = self._encoding_scheme()
+        if scheme in self.NATIVE_ENCODINGS or scheme not in TRANSFORMS:
+            return train, valid
+        if not any(self.feature_types.get(c) == ENUM for c in self.x):
+            return train, valid
+        ce = CategoricalEncoder(scheme, self.x, self.feature_types, self.feature_domains,
+                                max_levels=int(self.params.get("max_categorical_levels") or 10), y=self.y)
+        ce.fit(train, self.comm)
+        self.cat_encoder = ce
+        self.x = list(ce.x_out)
+        self.feature_types = dict(ce.out_types)
+        self.feature_domains = dict(ce.out_domains)
+        return ce.transform(train), (ce.transform(valid) if valid is not None else None)
 
     def fold_ids(self, frame: Frame, nfolds: int) -> torch.Tensor:
         fc = self.params.get("fold_column")

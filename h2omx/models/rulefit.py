@@ -42,9 +42,19 @@ def _rules_from_ensemble(ens, names, types, domains):
             if tr[i]["feat"] >= 0:
                 f = int(tr[i]["feat"])
                 thr = float(tr[i]["thr"])
-                nal = bool(tr[i]["na_left"])
+                nal = bool(int(tr[i]["na_left"]) & 1)
                 c = names[f]
-                if types.get(c) == ENUM:
+                cb = getattr(ens, "catbits", None)
+                if (int(tr[i]["na_left"]) & 2) and cb is not None:
+                    from .tree.structs import bitset_has
+
+                    dom = domains.get(c) or []
+                    inl = bitset_has(cb[t][i], np.arange(len(dom)))
+                    left = [d for k, d in enumerate(dom) if inl[k]]
+                    right = [d for k, d in enumerate(dom) if not inl[k]]
+                    lt = f"({c} in {{{', '.join(left)}}}{' or NA' if nal else ''})"
+                    rt = f"({c} in {{{', '.join(right)}}}{'' if nal else ' or NA'})"
+                elif types.get(c) == ENUM:
                     dom = domains.get(c) or []
                     left = [d for k, d in enumerate(dom) if k <= thr]
                     right = [d for k, d in enumerate(dom) if k > thr]
@@ -68,10 +78,11 @@ def _rule_matrix(ens, rules, X: torch.Tensor) -> torch.Tensor:
     for t in range(ens.trees.shape[0]):
         tr = ens.trees[t]
         cap = tr.shape[0]
-        feat = torch.from_numpy(tr["feat"].astype(np.int64)).to(dev)
-        thr = torch.from_numpy(tr["thr"].astype(np.float32)).to(dev)
-        left = torch.from_numpy(tr["left"].astype(np.int64)).to(dev)
-        nal = torch.from_numpy(tr["na_left"].astype(np.bool_)).to(dev)
+        from .tree.structs import TreeWalker
+
+        cbt = getattr(ens, "catbits", None)
+        tw = TreeWalker(tr, None if cbt is None else cbt[t], dev)
+        feat, left = tw.feat, tw.left
         cmap = torch.full((cap,), -1, dtype=torch.long, device=dev)
         for (tt, i), k in col_of.items():
             if tt == t:
@@ -84,7 +95,7 @@ def _rule_matrix(ens, rules, X: torch.Tensor) -> torch.Tensor:
             if not bool(inner.any()):
                 break
             x = X[f.clamp_min(0), rows]
-            go_left = torch.where(torch.isnan(x), nal[node], x <= thr[node])
+            go_left = tw.go_left(node, x)
             child = torch.where(go_left, left[node], left[node] + 1)
             node = torch.where(inner, child, node)
             k = cmap[node]

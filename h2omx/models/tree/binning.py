@@ -29,6 +29,21 @@ class BinnedMatrix:
     npad: int
     nbt: int                 # histogram width; bin nbt-1 is the NA bin
     names: list
+    # categorical group splits: per feature True for an identity-binned enum
+    # column (bin = level code, <= 255 levels); None = all numeric
+    cat: np.ndarray | None = None
+
+    @property
+    def catf(self) -> torch.Tensor | None:
+        """Device uint8 [F] copy of ``cat`` (SplitParams::catf), None without
+        categorical features."""
+        if self.cat is None or not np.any(self.cat):
+            return None
+        t = getattr(self, "_catf", None)
+        if t is None or t.device != self.codes.device:
+            t = torch.from_numpy(np.asarray(self.cat, np.uint8)).to(self.codes.device)
+            self._catf = t
+        return t
 
     @property
     def F(self) -> int:
@@ -341,8 +356,41 @@ def _edges_device(S: torch.Tensor, max_value_bins: int) -> list:
     return out
 
 
-def bin_matrix(X: torch.Tensor, edges: np.ndarray, nvb: np.ndarray, nbt: int, names=None) -> BinnedMatrix:
-    """Bin feature-major float32 ``X`` [F][n] (any stride on dim 1 == 1)."""
+MAX_CAT_LEVELS = 255
+
+
+def categorical_bins(edges: np.ndarray, nvb: np.ndarray, nbt: int, levels: dict) -> tuple:
+    """Identity bins for categorical features: ``levels`` maps feature index ->
+    number of levels L (codes 0..L-1); a feature with 2 <= L <= 255 gets the
+    cut points 0.5, 1.5, ..., L - 1.5 (bin = level code) and is flagged for
+    group splits.  The histogram width grows to hold the widest one.  Enum
+    columns with more levels keep the ordinal quantile bins of their codes
+    (H2O groups levels beyond nbins_cats similarly).  Returns (edges, nvb,
+    nbt, cat [F] bool)."""
+    F = edges.shape[0]
+    cat = np.zeros(F, bool)
+    use = {f: L for f, L in levels.items() if 2 <= L <= MAX_CAT_LEVELS}
+    if not use:
+        return edges, nvb, nbt, cat
+    nbt2 = max(nbt, hist_width(max(use.values())))
+    if nbt2 > nbt:
+        wide = np.full((F, nbt2), np.inf, np.float32)
+        wide[:, :nbt] = edges
+        edges = wide
+    edges = np.array(edges, np.float32, copy=True)
+    nvb = np.array(nvb, np.int32, copy=True)
+    for f, L in use.items():
+        edges[f, :] = np.inf
+        edges[f, : L - 1] = np.arange(L - 1, dtype=np.float32) + 0.5
+        nvb[f] = L
+        cat[f] = True
+    return edges, nvb, nbt2, cat
+
+
+def bin_matrix(X: torch.Tensor, edges: np.ndarray, nvb: np.ndarray, nbt: int, names=None,
+               cat: np.ndarray | None = None) -> BinnedMatrix:
+    """Bin feature-major float32 ``X`` [F][n] (any stride on dim 1 == 1);
+    ``cat``: categorical flags from :func:`categorical_bins`."""
     F, n = X.shape
     npad = max(ROW_ALIGN, int(math.ceil(n / ROW_ALIGN) * ROW_ALIGN))
     dev = X.device
@@ -365,5 +413,6 @@ def bin_matrix(X: torch.Tensor, edges: np.ndarray, nvb: np.ndarray, nbt: int, na
             c[np.isnan(col)] = nbt - 1
             codes_np[f, :n] = c
         codes = torch.from_numpy(codes_np)
-    return BinnedMatrix(codes=codes, edges=e_t, nvb=nv_t, n=n, npad=npad, nbt=nbt, names=names)
+    return BinnedMatrix(codes=codes, edges=e_t, nvb=nv_t, n=n, npad=npad, nbt=nbt, names=names,
+                        cat=None if cat is None else np.asarray(cat, bool))
 

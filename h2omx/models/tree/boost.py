@@ -39,6 +39,23 @@ def concat_trees(*parts: np.ndarray) -> np.ndarray:
     return out
 
 
+def concat_catbits(first, second) -> np.ndarray:
+    """Categorical bitsets of two ensembles stacked like concat_trees (trees
+    without categorical splits get zero bitsets)."""
+    parts = []
+    for e in (first, second):
+        n, w = e.trees.shape[0], e.trees.shape[1] if e.trees.ndim == 2 else 1
+        c = e.catbits if e.catbits is not None else np.zeros((n, w, 8), np.uint32)
+        parts.append(c)
+    width = max(p.shape[1] for p in parts)
+    out = np.zeros((sum(p.shape[0] for p in parts), width, 8), np.uint32)
+    r = 0
+    for p in parts:
+        out[r: r + p.shape[0], : p.shape[1]] = p
+        r += p.shape[0]
+    return out
+
+
 @dataclass
 class TreeEnsemble:
     trees: np.ndarray            # [n_trees_total][capacity] TREE_NODE_DTYPE
@@ -50,6 +67,9 @@ class TreeEnsemble:
     feature_names: list = field(default_factory=list)
     edges: list = field(default_factory=list)   # per-feature numpy cut points
     timings: dict = field(default_factory=dict)
+    # categorical group splits: [n_trees_total][capacity][8] uint32 left-set
+    # bitsets by node (TreeNode.na_left bit 1 marks such a split); None = none
+    catbits: np.ndarray | None = None
 
     @property
     def ntrees(self) -> int:
@@ -78,13 +98,17 @@ class TreeEnsemble:
         if X.is_cuda:
             dev = X.device
             Xc = X.float().contiguous()
-            key = (T, str(dev), self.trees.shape, id(self.trees))
+            key = (T, str(dev), self.trees.shape, id(self.trees), id(self.catbits))
             cache = getattr(self, "_dev_nodes", None)
             if cache is not None and cache[0] == key:
-                nodes = cache[1]
+                nodes, cbits = cache[1], cache[2]
             else:
                 nodes = torch.from_numpy(self.trees[:T].reshape(-1).view(np.uint8).copy()).to(dev)
-                self._dev_nodes = (key, nodes)
+                cbits = None
+                if self.catbits is not None:
+                    cb = np.ascontiguousarray(self.catbits[:T], np.uint32).reshape(-1)
+                    cbits = torch.from_numpy(cb.view(np.int32).copy()).to(dev)
+                self._dev_nodes = (key, nodes, cbits)
             cap = self.trees.shape[1]
             roots = torch.arange(T, dtype=torch.int32, device=dev) * cap
             out = torch.empty((self.K, n), dtype=torch.float32, device=dev)
@@ -95,7 +119,8 @@ class TreeEnsemble:
             if T:
                 lib = ops.tree_lib()
                 ops.check(lib.h2omx_predict_raw(ops.P(Xc), Xc.stride(0), n, ops.P(nodes), ops.P(roots), T, self.K,
-                                                ops.P(out), out.stride(0), ops.stream(dev)), "predict_raw")
+                                                ops.P(out), out.stride(0), ops.P(cbits), ops.stream(dev)),
+                          "predict_raw")
             if self.average and nt > 0:
                 out /= nt
             return out
@@ -297,6 +322,7 @@ class GpuBooster:
         self.builder = HipTreeBuilder(bm, tp, comm)
         self.cap = self.builder.capacity
         self.trees_dev = []
+        self.cats_dev = []         # categorical left-set bitsets, parallel to trees_dev
         self.graph_used = False   # a step graph was captured (finish() releases the graph itself)
         need_w = sample_rate < 1.0 or self.st.w is not None
         self.wout = torch.empty((bm.npad,), dtype=torch.float32, device=self.dev) if need_w else None
@@ -370,7 +396,7 @@ class GpuBooster:
         return (self.K == 1 and not self.fused and self.sample_rate >= 1.0 and tp.col_sample_rate >= 1.0
                 and tp.col_sample_rate_per_tree >= 1.0 and tp.mtries == 0 and tp.learn_rate_annealing == 1.0
                 and not b.segmented and not b.timer.enabled and self.cap <= self.COMPACT_CAP
-                and self.dev.type == "cuda")
+                and self.dev.type == "cuda" and b.catf is None)
 
     def _body_k1(self, t: int, fresh: bool):
         b = self.builder
@@ -395,6 +421,7 @@ class GpuBooster:
             b.build(st.g[0], st.h[0], None, t, fmask, grad_fuse=gf)
             self.pending = True
             self.trees_dev.append(self._snapshot())
+            self._snap_cat()
         elif self.K == 1:
             fresh = self.cap <= self.COMPACT_CAP
             if fresh:
@@ -403,6 +430,7 @@ class GpuBooster:
                 b.tree_buf = torch.empty_like(b.tree_buf)
             b.build(st.g[0], st.h[0], self.wout, t, fmask, stat=self._bounds)
             self.trees_dev.append(b.tree_buf if fresh else self._snapshot())
+            self._snap_cat()
             self._oob(t, 0)
             self._update(apply=True, next_tree=t + 1, k=0)
         else:
@@ -427,6 +455,7 @@ class GpuBooster:
                 b.stat_max.copy_(maxes[k])
                 b.build(st.g[k], st.h[k], self.wout, t * self.K + k, fmask)
                 self.trees_dev.append(self._snapshot())
+                self._snap_cat()
                 self._oob(t, k)
                 ops.check(self.lib.h2omx_apply_tree(P(st.Fm[k]), bm.n, P(b.nid), P(b.tree_buf), s), "apply_tree")
         self.t += 1
@@ -460,6 +489,17 @@ class GpuBooster:
         self.graph = g
         self.graph_used = True
 
+    def _snap_cat(self) -> None:
+        """Copy of the finished tree's categorical bitsets (nodes of the tree only)."""
+        b = self.builder
+        if b.treecat is None:
+            return
+        if self.cap <= self.COMPACT_CAP:
+            self.cats_dev.append(b.treecat.clone())
+        else:
+            total = max(1, int(b.tree_size()))
+            self.cats_dev.append(b.treecat[: total * 8].clone())
+
     def _snapshot(self) -> torch.Tensor:
         """Copy of the finished tree.  Shallow trees copy the whole capacity-sized
         heap without a host sync; deep trees (DRF depth 20: 2^21 slots, 64 MB)
@@ -491,6 +531,8 @@ class GpuBooster:
                 for i, t in enumerate(self.trees_dev):
                     raw[i, : t.numel()] = t
             self.ens.trees = trees_from_bytes(raw.cpu().numpy(), width // TREE_NODE_DTYPE.itemsize)
+            if self.cats_dev:
+                self.ens.catbits = _stack_cats(self.cats_dev, width // TREE_NODE_DTYPE.itemsize)
         self.ens._state = self.st
         if self.oob is not None:
             self.ens._oob = (self.oob[0][:, : self.bm.n], self.oob[1][: self.bm.n])
@@ -510,6 +552,15 @@ def _train_gpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callbac
     gb.finish()
     gb.builder.p.learn_rate = lr0
     ens.timings["train_s"] = time.perf_counter() - t0
+
+
+def _stack_cats(cats: list, width_nodes: int) -> np.ndarray:
+    """[n_trees][width_nodes][8] uint32 from per-tree device bitset snapshots."""
+    out = np.zeros((len(cats), width_nodes, 8), np.uint32)
+    for i, c in enumerate(cats):
+        a = c.cpu().numpy().view(np.uint32).reshape(-1, 8)
+        out[i, : a.shape[0]] = a[:width_nodes]
+    return out
 
 
 class _GpuView:
@@ -537,6 +588,15 @@ class _GpuView:
         for i, t in enumerate(bufs):
             raw[i, : t.numel()] = t
         return trees_from_bytes(raw.cpu().numpy(), width // TREE_NODE_DTYPE.itemsize)
+
+    def catbits(self, lo: int, hi: int) -> np.ndarray | None:
+        """Categorical bitsets of iterations [lo, hi) aligned with trees(lo, hi)."""
+        K = self.gb.K
+        cats = self.gb.cats_dev[lo * K: hi * K]
+        if not cats:
+            return None
+        width = max(t.numel() for t in self.gb.trees_dev[lo * K: hi * K]) // TREE_NODE_DTYPE.itemsize
+        return _stack_cats(cats, width)
 
 
 

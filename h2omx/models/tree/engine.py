@@ -170,6 +170,12 @@ class HipTreeBuilder:
             self.ifsets = torch.from_numpy(fs.view(np.int64).copy()).to(d)
             self.istate = torch.zeros((2 * self.capacity,), dtype=torch.int64, device=d)
             self.istate[0], self.istate[1] = -1, -2     # root: every set, empty path
+        # categorical group splits: feature flags on the device, the tree's left-set
+        # bitsets ([capacity][8] uint32, one tree at a time, snapshotted with tree_buf)
+        # and the per-(node, feature) scan bitsets (fbcat, per level)
+        self.catf = bm.catf
+        self.treecat = (torch.zeros((self.capacity * 8,), dtype=torch.int32, device=d)
+                        if self.catf is not None else None)
         self.stats = {"host_syncs": 0}
         self.timer = PhaseTimer(device=d)
         # global index of this rank's first row: the stochastic-rounding dither and
@@ -210,7 +216,8 @@ class HipTreeBuilder:
         # slower on HIGGS depth 5 (1.108 vs 1.071 ms/tree: one workgroup per node halves
         # the scan parallelism and the agent-scope hand-off costs about a launch), so
         # opt-in (H2OMX_FUSE_SPLIT=1)
-        self.fuse_split = self.F <= 64 and os.environ.get("H2OMX_FUSE_SPLIT", "0") == "1"
+        self.fuse_split = (self.F <= 64 and os.environ.get("H2OMX_FUSE_SPLIT", "0") == "1"
+                           and self.catf is None)
         self.ticket = torch.zeros((4,), dtype=torch.int32, device=d)
         # graph replay (boost.TreeGraph): tree_begin takes the tree index (dither salt,
         # qscale[9]) from this device counter instead of the host argument, and advances it
@@ -459,7 +466,15 @@ class HipTreeBuilder:
         sp.gbound = self.gbound.data_ptr() if self.gbound is not None else None
         sp.ifsets = self.ifsets.data_ptr() if self.ifsets is not None else None
         sp.istate = self.istate.data_ptr() if self.istate is not None else None
+        sp.catf = self.catf.data_ptr() if self.catf is not None else None
+        sp.treecat = self.treecat.data_ptr() if self.treecat is not None else None
+        sp.fbcat = None
         return ctypes.addressof(sp)
+
+    def _cat_level(self, max_nodes: int) -> None:
+        """Point SplitParams::fbcat at a [max_nodes][F][8] scratch for this level."""
+        if self.catf is not None:
+            self._sp.fbcat = self._buf("fbcat", max_nodes * self.F * 8, torch.int32).data_ptr()
 
     # -- one tree ------------------------------------------------------------
     def can_fuse_grad(self, dist: str, weighted: bool, sample_rate: float) -> bool:
@@ -617,6 +632,7 @@ class HipTreeBuilder:
                 nl = self._buf(f"link{nxt}", next_nodes * NODE_LINK_BYTES // 4, torch.int32)
                 link[nxt] = nl
             nsplit = self._buf("nsplit", max_nodes * 9, torch.float64)  # NodeSplit = 72 B
+            self._cat_level(max_nodes)
             with T("split"):
                 if self.fuse_split:
                     # scan + per-node arg-max + level finalisation in one launch
@@ -625,7 +641,7 @@ class HipTreeBuilder:
                                                     P(nsplit), P(self.ticket), P(ctl_nxt), P(bm.edges),
                                                     next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
                                                     st), "split_level")
-                elif self.SPLIT_FIN and max_nodes <= 64:
+                elif self.SPLIT_FIN and max_nodes <= 64 and self.catf is None:
                     # split scan + per-node arg-max + finalisation: the last block finalises
                     fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
                     ops.check(lib.h2omx_split_find_fin(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
@@ -794,7 +810,7 @@ class HipTreeBuilder:
         # n / 2 x F + nodes x F x bins: direct only for few eligible features (DRF mtries)
         exp_elig = min(p.mtries, F) if p.mtries > 0 else F * min(1.0, p.col_sample_rate)
         direct_ok = (comm is None and self.DIRECT_MIN_NODES > 0 and F <= 1024
-                     and exp_elig <= self.DIRECT_MAX_ELIG)
+                     and exp_elig <= self.DIRECT_MAX_ELIG and self.catf is None)
         for d in range(max_depth):
             cur, nxt = d % 2, (d + 1) % 2
             ctl_cur, ctl_nxt = self.ctl[cur], self.ctl[nxt]
@@ -893,6 +909,7 @@ class HipTreeBuilder:
                 comm.all_reduce_(built[: max_slots * self.per_node])
             full_cur = None if last else B(f"full{cur}", max_nodes * self.per_node, torch.int64)
             fbest = B("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
+            self._cat_level(max_nodes)
             sp.depth = d
             sp.children_leaves = 1 if last else 0
             ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),

@@ -24,7 +24,33 @@ class SplitParams(ctypes.Structure):
         ("col_rate", ctypes.c_float), ("mtries", ctypes.c_int), ("children_leaves", ctypes.c_int),
         ("pad2", ctypes.c_int), ("mono", ctypes.c_void_p), ("gbound", ctypes.c_void_p),
         ("ifsets", ctypes.c_void_p), ("istate", ctypes.c_void_p),
+        ("catf", ctypes.c_void_p), ("fbcat", ctypes.c_void_p), ("treecat", ctypes.c_void_p),
     ]
+
+
+# TreeNode.na_left bit 1: categorical group split (the tree's bitset table holds
+# the LEFT set of level codes, 8 x uint32 per node)
+NA_LEFT_BIT, CAT_SPLIT_BIT = 1, 2
+CAT_WORDS = 8
+
+
+def bitset_words(levels) -> np.ndarray:
+    """8 uint32 words with the bits of ``levels`` (codes 0..255) set."""
+    w = np.zeros(CAT_WORDS, np.uint32)
+    for b in np.asarray(levels, np.int64).ravel():
+        w[b >> 5] |= np.uint32(1) << np.uint32(b & 31)
+    return w
+
+
+def bitset_has(words: np.ndarray, codes: np.ndarray) -> np.ndarray:
+    """Membership of integer ``codes`` (out of 0..255: False) in bitsets
+    ``words`` [..., 8] (broadcast against codes)."""
+    c = np.asarray(codes, np.int64)
+    ok = (c >= 0) & (c <= 255)
+    cc = np.where(ok, c, 0)
+    word = np.take_along_axis(np.asarray(words, np.uint32), (cc >> 5)[..., None], axis=-1)[..., 0] \
+        if np.ndim(words) > 1 else np.asarray(words, np.uint32)[cc >> 5]
+    return ok & (((word >> (cc & 31).astype(np.uint32)) & np.uint32(1)) != 0)
 
 
 class GradParams(ctypes.Structure):
@@ -86,3 +112,37 @@ def check_layout(lib) -> None:
     got = list(sizes)[:6]
     if got != want:
         raise RuntimeError(f"tree kernel ABI mismatch: kernel sizes {got} != python {want}")
+
+
+class TreeWalker:
+    """Device-side routing of raw feature values through one tree's records
+    (Python scoring helpers: leaf assignment, RuleFit rules, ...), numeric
+    thresholds and categorical group splits alike."""
+
+    def __init__(self, tree: np.ndarray, catbits: np.ndarray | None, dev):
+        import torch
+
+        self.feat = torch.from_numpy(tree["feat"].astype(np.int64)).to(dev)
+        self.thr = torch.from_numpy(tree["thr"].astype(np.float32)).to(dev)
+        self.left = torch.from_numpy(tree["left"].astype(np.int64)).to(dev)
+        nl = tree["na_left"].astype(np.int64)
+        self.nal = torch.from_numpy((nl & NA_LEFT_BIT) != 0).to(dev)
+        self.iscat = torch.from_numpy((nl & CAT_SPLIT_BIT) != 0).to(dev)
+        self.cb = None
+        if catbits is not None and bool(self.iscat.any()):
+            self.cb = torch.from_numpy(np.asarray(catbits, np.uint32).astype(np.int64)).to(dev)
+
+    def go_left(self, idx, v):
+        import torch
+
+        nan = torch.isnan(v)
+        res = torch.where(nan, self.nal[idx], v <= self.thr[idx])
+        if self.cb is not None:
+            cat = self.iscat[idx] & ~nan
+            c = torch.nan_to_num(v, nan=-1.0).long()
+            oor = (c < 0) | (c > 255)
+            cc = c.clamp(0, 255)
+            word = self.cb[idx.clamp(max=self.cb.shape[0] - 1), cc >> 5]
+            inset = ((word >> (cc & 31)) & 1) != 0
+            res = torch.where(cat, torch.where(oor, self.nal[idx], inset), res)
+        return res

@@ -17,8 +17,8 @@ import torch
 from ..frame.frame import ENUM, Frame, Vec
 from .base import Model, ModelBuilder, ModelCategory
 from .tree import TreeParams, bin_matrix, compute_edges, train_ensemble
-from .tree.binning import resolve_histogram_type
-from .tree.boost import concat_trees
+from .tree.binning import categorical_bins, resolve_histogram_type
+from .tree.boost import concat_catbits, concat_trees
 
 
 class TreeModel(Model):
@@ -121,6 +121,23 @@ class _TreeBuilder(ModelBuilder):
     def _tree_params(self, nfeat: int) -> TreeParams:
         raise NotImplementedError
 
+    # categorical group splits for enum predictors (GBM / DRF under
+    # categorical_encoding AUTO / Enum; H2O's XGBoost one-hot encodes instead)
+    group_splits = True
+
+    def _group_splits(self, enc: str) -> bool:
+        return self.group_splits and enc in ("auto", "enum", "enumlimited")
+
+    # SortByResponse is applied by the tree builder itself (_sort_levels_by_response)
+    NATIVE_ENCODINGS = ("auto", "enum", "sortbyresponse")
+
+    def _encoding_scheme(self) -> str:
+        s = super()._encoding_scheme()
+        if s == "onehotinternal":
+            raise ValueError(f"{self.algo}: categorical_encoding OneHotInternal is not supported by tree algorithms "
+                             "(as in H2O); use OneHotExplicit")
+        return s
+
     def _monotone(self):
         """H2O ``monotone_constraints`` ({column: +1 / -1}, or the REST form
         [{"key": column, "value": sign}]) as one sign per predictor; None if
@@ -168,7 +185,7 @@ class _TreeBuilder(ModelBuilder):
         return tuple(sets)
 
     def _fit(self, train: Frame, valid: Frame | None, model_id: str) -> Model:
-        enc = str(self.params.get("categorical_encoding") or "AUTO").lower().replace("_", "")
+        enc = self._encoding_scheme()
         if enc == "sortbyresponse":
             train, valid = self._sort_levels_by_response(train, valid)
         X = train.feature_matrix(self.x)
@@ -194,7 +211,14 @@ class _TreeBuilder(ModelBuilder):
             nbins = max(nbins, int(self.params["nbins_top_level"]))
         edges, nvb, nbt = compute_edges(X, min(nbins, 255), seed=self._seed(), comm=self.comm,
                                         histogram_type=htype)
-        bm = bin_matrix(X, edges, nvb, nbt, names=self.x)
+        cat = None
+        if self._group_splits(enc):
+            # H2O's default for enum predictors (categorical_encoding AUTO / Enum):
+            # identity level bins + group splits (sets of levels) in GBM / DRF
+            levels = {i: len(self.feature_domains.get(c) or []) for i, c in enumerate(self.x)
+                      if self.feature_types.get(c) == ENUM}
+            edges, nvb, nbt, cat = categorical_bins(edges, nvb, nbt, levels)
+        bm = bin_matrix(X, edges, nvb, nbt, names=self.x, cat=cat)
         tp = self._tree_params(len(self.x))
         nclass = len(self.response_domain) if self.response_domain else 1
         ens_dist = self._engine_dist(dist)
@@ -229,6 +253,8 @@ class _TreeBuilder(ModelBuilder):
                                       "quantile_alpha": float(self.params.get("quantile_alpha", 0.5)),
                                       "huber_delta": float(self.params.get("huber_alpha", 0.9))})
         if ckpt is not None:
+            if ckpt.catbits is not None or ens.catbits is not None:
+                ens.catbits = concat_catbits(ckpt, ens)
             ens.trees = concat_trees(ckpt.trees, ens.trees) if len(ens.trees) else ckpt.trees
             ens.init_f = ckpt.init_f
         model = self.model_cls(self, model_id, ens, ens_dist)
@@ -548,6 +574,7 @@ class _TreeScoring:
 
             new = view.trees(self.done, t + 1)
             part = TreeEnsemble(new, self.K, self.dist, np.zeros(self.K), average=False)
+            part.catbits = view.catbits(self.done, t + 1) if hasattr(view, "catbits") else None
             m = part.raw_margin(self.Xv).to(self.Xv.device) if len(new) else 0.0
             if self.vmargin is None:
                 init = 0.0 if self.dist == "drf" else torch.from_numpy(
@@ -604,6 +631,15 @@ class H2OXGBoostEstimator(_TreeBuilder):
     min_child_weight on hessian mass, eta-scaled leaves."""
     algo = "xgboost"
     model_cls = XGBoostModel
+    group_splits = False
+
+    def _encoding_scheme(self) -> str:
+        """H2O XGBoost: AUTO / OneHotInternal one-hot encode the levels; Enum
+        feeds the level codes (ordinal)."""
+        from ..frame.encoding import normalize_scheme
+
+        s = normalize_scheme(self.params.get("categorical_encoding"))
+        return {"auto": "onehotexplicit", "onehotinternal": "onehotexplicit", "enum": "labelencoder"}.get(s, s)
     mode = 1
     default_nbins = 255
     DEFAULTS = dict(ntrees=50, max_depth=6, min_rows=1.0, min_child_weight=None, learn_rate=0.3, eta=None,

@@ -76,15 +76,21 @@ NSD_NA_LEFT, NSD_NA_RIGHT = 2, 3
 # ---------------------------------------------------------------------------
 # tree encoding
 # ---------------------------------------------------------------------------
-def _encode_tree(tree: np.ndarray) -> bytes:
+def _encode_tree(tree: np.ndarray, catbits: np.ndarray | None = None, nlev=None) -> bytes:
+    """``catbits`` [nodes][8]: left sets of categorical group splits
+    (TreeNode.na_left bit 1), written as genmodel bitset splits (nodeType
+    equal = 12: ``bitOff:u16 | nBits:u32 | bytes``) holding the levels that go
+    RIGHT over the column's domain ``nlev[feat]`` levels (out-of-range levels
+    follow the NA direction, as unseen levels do in h2omx)."""
     def enc(i) -> tuple[bytes, bool]:
         nd = tree[i]
         if nd["feat"] < 0:
             return struct.pack("<f", float(nd["value"])), True
         lb, lleaf = enc(int(nd["left"]))
         rb, rleaf = enc(int(nd["left"]) + 1)
+        is_cat = (int(nd["na_left"]) & 2) != 0 and catbits is not None
         split = np.nextafter(np.float32(nd["thr"]), np.float32(np.inf))
-        node_type = 0
+        node_type = 12 if is_cat else 0
         head_left = b""
         if lleaf:
             node_type |= 48
@@ -95,8 +101,17 @@ def _encode_tree(tree: np.ndarray) -> bytes:
             head_left = n.to_bytes(size_bytes, "little")
         if rleaf:
             node_type |= 192
-        hdr = struct.pack("<BHBf", node_type, int(nd["feat"]), NSD_NA_LEFT if nd["na_left"] else NSD_NA_RIGHT,
-                          float(split))
+        nsd = NSD_NA_LEFT if (int(nd["na_left"]) & 1) else NSD_NA_RIGHT
+        if is_cat:
+            from ..models.tree.structs import bitset_has
+
+            nb = int(nlev[int(nd["feat"])]) if nlev is not None else 256
+            nb = max(1, min(nb, 256))
+            right = ~bitset_has(catbits[i], np.arange(nb))
+            by = np.packbits(right.astype(np.uint8), bitorder="little").tobytes()
+            hdr = struct.pack("<BHBHI", node_type, int(nd["feat"]), nsd, 0, nb) + by
+        else:
+            hdr = struct.pack("<BHBf", node_type, int(nd["feat"]), nsd, float(split))
         return hdr + head_left + lb + rb, False
 
     body, leaf = enc(0)
@@ -113,6 +128,7 @@ class _TreeCodec:
         from ..models.tree.structs import TREE_NODE_DTYPE
 
         feat, left, na_left, thr, value = [], [], [], [], []
+        cats = {}       # node -> left-set words of a bitset split
 
         def new():
             feat.append(-1)
@@ -137,12 +153,35 @@ class _TreeCodec:
                     pos += 4
                     continue
                 idx = top
-                node_type, col, nsd, split = struct.unpack_from("<BHBf", data, pos)
-                pos += 8
+                node_type, col, nsd = struct.unpack_from("<BHB", data, pos)
                 lp, rp = new(), new()
                 feat[idx], left[idx] = col, lp
                 na_left[idx] = 1 if nsd == NSD_NA_LEFT else 0
-                thr[idx] = float(np.nextafter(np.float32(split), np.float32(-np.inf)))
+                equal = node_type & 12
+                if equal == 0:
+                    split = struct.unpack_from("<f", data, pos + 4)[0]
+                    pos += 8
+                    thr[idx] = float(np.nextafter(np.float32(split), np.float32(-np.inf)))
+                else:
+                    # bitset split: the set holds the levels going right; levels
+                    # outside [bitoff, bitoff + nbits) follow the NA direction
+                    if equal == 8:
+                        bitoff, nbits, pos = 0, 32, pos + 4
+                    else:
+                        bitoff, nbits = struct.unpack_from("<HI", data, pos + 4)
+                        pos += 10
+                    nby = (nbits + 7) // 8
+                    rbits = np.unpackbits(np.frombuffer(data, np.uint8, nby, pos), bitorder="little")[:nbits]
+                    pos += nby
+                    lv = np.arange(256)
+                    inr = (lv >= bitoff) & (lv < bitoff + nbits)
+                    rel = np.clip(lv - bitoff, 0, max(nbits - 1, 0))
+                    goes_right = np.where(inr, rbits[rel] != 0 if nbits else False, na_left[idx] == 0)
+                    from ..models.tree.structs import bitset_words
+
+                    cats[idx] = bitset_words(np.nonzero(~goes_right)[0])
+                    na_left[idx] |= 2
+                    thr[idx] = float("nan")
                 # push right first so the left subtree is decoded next
                 stack.append(("leaf", rp) if node_type & 192 else rp)
                 if node_type & 48:
@@ -153,14 +192,24 @@ class _TreeCodec:
         arr = np.zeros(len(feat), TREE_NODE_DTYPE)
         arr["feat"], arr["left"], arr["na_left"] = feat, left, na_left
         arr["thr"], arr["value"] = thr, value
-        return arr
+        if cats:
+            cb = np.zeros((len(feat), 8), np.uint32)
+            for i, w in cats.items():
+                cb[i] = w
+            return arr, cb
+        return arr, None
 
 
-def encode_tree(tree: np.ndarray) -> bytes:
-    return _encode_tree(tree)
+def encode_tree(tree: np.ndarray, catbits: np.ndarray | None = None, nlev=None) -> bytes:
+    return _encode_tree(tree, catbits, nlev)
 
 
 def decode_tree(data: bytes) -> np.ndarray:
+    return _TreeCodec.decode(data)[0]
+
+
+def decode_tree_cat(data: bytes):
+    """(tree records, categorical bitsets [nodes][8] or None)."""
     return _TreeCodec.decode(data)
 
 
@@ -243,11 +292,23 @@ def mojo_bytes(model: Model) -> bytes:
         return model.raw_mojo
     else:
         raise NotImplementedError(f"MOJO export for {algo}")
+    enc = getattr(model, "cat_encoder", None)
+    enc_domains = {}
+    if enc is not None:
+        # frame-transform categorical_encoding: the MOJO takes the ORIGINAL
+        # predictors (genmodel applies the scheme named in model.ini); the fitted
+        # encoding itself travels as h2omx payload (exact round trip)
+        info["categorical_encoding"] = {"onehotexplicit": "OneHotExplicit", "binary": "Binary", "eigen": "Eigen",
+                                        "labelencoder": "LabelEncoder", "enumlimited": "EnumLimited",
+                                        "sortbyresponse": "SortByResponse"}[enc.scheme]
+        files["h2omx/categorical_encoder.json"] = json.dumps(enc.to_json()).encode()
+        columns = list(enc.x_in)
+        enc_domains = {c: enc.domains.get(c) for c in enc.x_in}
     if model.y is not None and algo not in ("kmeans", "coxph") and not getattr(model, "autoencoder", False):
         columns = columns + [model.y]
     domains = []
     for j, c in enumerate(columns):
-        dom = model.response_domain if c == model.y else (model.feature_domains.get(c) or (
+        dom = model.response_domain if c == model.y else (enc_domains.get(c) or model.feature_domains.get(c) or (
             model.gam_frame_domains.get(c) if hasattr(model, "gam_frame_domains") else None))
         if dom:
             domains.append((j, dom))
@@ -298,9 +359,12 @@ def _tree_info(model, files):
     ens = model.ens
     K = ens.K
     nt = ens.ntrees
+    nlev = [len(model.feature_domains.get(c) or []) for c in model.x] if ens.catbits is not None else None
     for t in range(nt):
         for k in range(K):
-            files[f"trees/t{k:02d}_{t:03d}.bin"] = _encode_tree(ens.trees[t * K + k])
+            i = t * K + k
+            files[f"trees/t{k:02d}_{t:03d}.bin"] = _encode_tree(
+                ens.trees[i], None if ens.catbits is None else ens.catbits[i], nlev)
     dist = {"drf": "AUTO"}.get(model.dist, model.dist)
     return {"n_trees": nt, "n_trees_per_class": K, "init_f": float(ens.init_f[0]) if K == 1 else 0.0,
             "init_f_per_class": [float(x) for x in ens.init_f], "distribution": dist,
@@ -882,6 +946,15 @@ class GenericModel(Model):
         self.run_time_ms = 0
         self.comm = None
         z = m["zip"]
+        self.cat_encoder = None
+        if "h2omx/categorical_encoder.json" in z.namelist():
+            # frame-transform categorical_encoding: original columns in, encoded predictors to the trees
+            from ..frame.encoding import CategoricalEncoder
+
+            ce = CategoricalEncoder.from_json(json.loads(z.read("h2omx/categorical_encoder.json")))
+            self.cat_encoder = ce
+            self.x = list(ce.x_out)
+            self.feature_types, self.feature_domains = dict(ce.out_types), dict(ce.out_domains)
         if self.mojo_algo in ("gbm", "drf", "xgboost", "isolationforest"):
             self._load_trees(z, info)
         elif self.mojo_algo == "stackedensemble":
@@ -1243,7 +1316,8 @@ class GenericModel(Model):
         from ..models.tree.boost import TreeEnsemble
 
         K, nt = int(info["n_trees_per_class"]), int(info["n_trees"])
-        trees = [decode_tree(z.read(f"trees/t{k:02d}_{t:03d}.bin")) for t in range(nt) for k in range(K)]
+        dec = [decode_tree_cat(z.read(f"trees/t{k:02d}_{t:03d}.bin")) for t in range(nt) for k in range(K)]
+        trees = [d[0] for d in dec]
         cap = max((len(t) for t in trees), default=1)
         from ..models.tree.structs import TREE_NODE_DTYPE
 
@@ -1251,10 +1325,17 @@ class GenericModel(Model):
         arr["feat"] = -1
         for i, t in enumerate(trees):
             arr[i, : len(t)] = t
+        catbits = None
+        if any(d[1] is not None for d in dec):
+            catbits = np.zeros((len(trees), cap, 8), np.uint32)
+            for i, d in enumerate(dec):
+                if d[1] is not None:
+                    catbits[i, : len(d[1])] = d[1]
         init = info.get("init_f_per_class")
         init = np.array(init if isinstance(init, list) else [info.get("init_f", 0.0)] * K, np.float64)
         self.ens = TreeEnsemble(arr, K, str(info.get("h2omx_engine_dist", info.get("distribution"))), init,
                                 average=bool(info.get("h2omx_average", False)))
+        self.ens.catbits = catbits
         self.link = info.get("link_function", "identity")
 
     # -- scoring ---------------------------------------------------------------

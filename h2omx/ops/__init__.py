@@ -47,8 +47,8 @@ TREE_SIGS = {
     "h2omx_leaf_stats": "PPPPLPIPS",
     "h2omx_leaf_finalize": "PPPPPIS",
     "h2omx_leaf_finalize_mono": "PPPPPIPS",
-    "h2omx_predict_raw": "PLLPPIIPLS",
-    "h2omx_predict_binned": "PLLPPIIIPLS",
+    "h2omx_predict_raw": "PLLPPIIPLPS",
+    "h2omx_predict_binned": "PLLPPIIIPLPS",
     "h2omx_pc_rows": "",
     "h2omx_tree_begin_seg": "PIIPPPPIPIIIPPPPPLIPS",
     "h2omx_hist_build_seg": "PIPPPPPPPPPIIIIIIIIPIS",
@@ -105,7 +105,7 @@ METRICS_SIGS = {
 }
 
 EXPLAIN_SIGS = {
-    "h2omx_tree_shap": "PLLIPIPPIPS",
+    "h2omx_tree_shap": "PLLIPIPPIPPS",
 }
 
 P2P_SIGS = {

@@ -21,7 +21,8 @@ import torch
 from ..models.tree.binning import BinnedMatrix
 from ..models.tree.engine import TreeParams, tree_capacity
 from ..models.tree.hashing import M32, _mix32, hash4, u01  # noqa: F401
-from ..models.tree.structs import (DIST_CODES, TREE_NODE_DTYPE, interaction_allowed, interaction_child,
+from ..models.tree.structs import (CAT_SPLIT_BIT, CAT_WORDS, DIST_CODES, NA_LEFT_BIT, TREE_NODE_DTYPE,
+                                   bitset_has, bitset_words, interaction_allowed, interaction_child,
                                    interaction_masks)
 
 
@@ -88,6 +89,9 @@ class RefTreeBuilder:
         self.capacity = tree_capacity(min(params.max_depth, 24))
         self.nid = np.full(bm.npad, -1, np.int64)
         self.n_nodes_total = 0
+        # categorical group splits (mirror of feat_best_cat_wave / part_right)
+        self.cat = None if getattr(bm, "cat", None) is None or not np.any(bm.cat) else np.asarray(bm.cat, bool)
+        self.catbits = None
 
     def _hist(self, rows_node, g, h, w, n_nodes):
         """Full histograms [n_nodes][F][3][nbt] (float64) of active rows."""
@@ -113,6 +117,8 @@ class RefTreeBuilder:
         h = np.asarray(h, np.float32)
         w = np.ones_like(g) if w is None else np.asarray(w, np.float32)
         tree = np.zeros(self.capacity, TREE_NODE_DTYPE)
+        catbits = np.zeros((self.capacity, CAT_WORDS), np.uint32) if self.cat is not None else None
+        self.catbits = catbits
         nid = self.nid
         # rows of weight zero still get routed but do not contribute
         contrib = np.where((nid >= 0) & (w != 0), nid, -1)
@@ -165,6 +171,7 @@ class RefTreeBuilder:
             bin_of = np.zeros(n_nodes, np.int64)
             naleft_of = np.zeros(n_nodes, np.int64)
             leafkids = np.zeros(n_nodes, bool)
+            catleft_of = {}      # node -> bool [nbt] left set of a categorical split
             for i in range(n_nodes):
                 hist = H[i]
                 tot = hist[0].sum(axis=1)  # feature 0 totals [3]
@@ -180,7 +187,22 @@ class RefTreeBuilder:
                     m = int(self.nvb[f])
                     hv = hist[f]
                     tg, th, tw = hv.sum(axis=1)
-                    cs = np.cumsum(hv[:, : nbt - 1], axis=1)[:, : min(m, nbt - 1)]
+                    is_cat = self.cat is not None and self.cat[f]
+                    if is_cat:
+                        # levels ordered by G / S inside the node (S = W or H by mode), ties by
+                        # level code, empty levels dropped; candidate left sets = prefixes
+                        vals = hv[:, : min(m, nbt - 1)]
+                        S = vals[2] if p.mode == 0 else vals[1]
+                        ne = S > 0
+                        with np.errstate(divide="ignore", invalid="ignore"):
+                            key = np.where(ne, vals[0] / np.where(ne, S, 1.0), np.inf)
+                        order = np.lexsort((np.arange(key.size), key))
+                        order = order[ne[order]]
+                        if order.size == 0:
+                            continue
+                        cs = np.cumsum(vals[:, order], axis=1)
+                    else:
+                        cs = np.cumsum(hv[:, : nbt - 1], axis=1)[:, : min(m, nbt - 1)]
                     na = hv[:, nbt - 1]
                     gA = split_gain(cs[0], cs[1], cs[2], tg, th, tw, p)
                     if na[2] > 0:
@@ -196,14 +218,26 @@ class RefTreeBuilder:
                     both = np.stack([gA, gB], axis=1).reshape(-1)
                     if not np.any(both > -np.inf):
                         continue
-                    c = int(np.argmax(both))  # first max = smallest code
+                    if is_cat:
+                        # positions in sorted order; ties broken by the code 2 * level + na
+                        codes = np.stack([2 * order, 2 * order + 1], axis=1).reshape(-1)
+                        gmax = both.max()
+                        cand = np.nonzero(both == gmax)[0]
+                        c = int(cand[np.argmin(codes[cand])])
+                    else:
+                        c = int(np.argmax(both))  # first max = smallest code
                     gval = both[c]
                     if gval > best[0]:
                         t, na_left = c // 2, c % 2
                         GL, HL, WL = cs[0, t], cs[1, t], cs[2, t]
                         if na_left:
                             GL, HL, WL = GL + na[0], HL + na[1], WL + na[2]
-                        best = (gval, (f, t, na_left, GL, HL, WL))
+                        if is_cat:
+                            left = np.zeros(nbt, bool)
+                            left[order[: t + 1]] = True
+                            best = (gval, (f, int(order[t]), na_left, GL, HL, WL, left))
+                        else:
+                            best = (gval, (f, t, na_left, GL, HL, WL, None))
                 do_split = (not False) and best[1] is not None and np.isfinite(best[0]) and best[0] > 0
                 if do_split and p.mode == 0 and p.min_split_improvement > 0:
                     base_term = Gt * Gt / Wt if Wt > 0 else 0.0
@@ -214,7 +248,7 @@ class RefTreeBuilder:
                 rec["weight"] = Wt
                 leaf_gh[gid] = (Gt, Ht)
                 if do_split:
-                    f, t, na_left, GL, HL, WL = best[1]
+                    f, t, na_left, GL, HL, WL, catleft = best[1]
                     if fsets is not None:
                         cs_ = interaction_child(istate[gid], fsets, f)
                         istate[next_base + 2 * k] = istate[next_base + 2 * k + 1] = cs_
@@ -237,6 +271,12 @@ class RefTreeBuilder:
                     rec["left"] = next_base + 2 * k
                     rec["gain"] = best[0]
                     rec["thr"] = self.edges[f, t] if t < m - 1 else np.inf
+                    if catleft is not None:
+                        rec["na_left"] = na_left | CAT_SPLIT_BIT
+                        rec["thr"] = np.nan
+                        catleft_of[i] = catleft
+                        if gid < self.capacity:
+                            catbits[gid] = bitset_words(np.nonzero(catleft)[0])
                     child_of[i], feat_of[i], bin_of[i], naleft_of[i] = 2 * k, f, t, na_left
                     if last:
                         leafkids[i] = True
@@ -265,6 +305,9 @@ class RefTreeBuilder:
                     nsp = nn[sp]
                     b = self.codes[feat_of[nsp], a_sp].astype(np.int64)
                     right = np.where(b == nbt - 1, 1 - naleft_of[nsp], (b > bin_of[nsp]).astype(np.int64))
+                    for ci, cl in catleft_of.items():
+                        sel = (nsp == ci) & (b != nbt - 1)
+                        right[sel] = (~cl[b[sel]]).astype(np.int64)
                     lk = leafkids[nsp]
                     new_sp = np.where(lk, ~(next_base + ch[sp] + right), ch[sp] + right)
                     new[sp] = new_sp
@@ -359,7 +402,9 @@ def dist_grad(dist: str, F, y, tweedie_power=1.5, quantile_alpha=0.5, huber_delt
 
 
 # ---- CPU boosting loop and scoring (moved out of models/tree/boost.py) ----
-def predict_tree_numpy(tree: np.ndarray, Xn: np.ndarray) -> np.ndarray:
+def predict_tree_numpy(tree: np.ndarray, Xn: np.ndarray, catbits: np.ndarray | None = None) -> np.ndarray:
+    """Leaf values of one tree for raw feature-major ``Xn``; ``catbits``
+    [nodes][8]: left sets of categorical splits (raw value = level code)."""
     n = Xn.shape[1]
     idx = np.zeros(n, np.int64)
     for _ in range(64):
@@ -370,7 +415,15 @@ def predict_tree_numpy(tree: np.ndarray, Xn: np.ndarray) -> np.ndarray:
         r = np.nonzero(inner)[0]
         v = Xn[feat[r], r]
         nd = tree[idx[r]]
-        left = np.where(np.isnan(v), nd["na_left"] != 0, v <= nd["thr"])
+        nal = (nd["na_left"] & NA_LEFT_BIT) != 0
+        with np.errstate(invalid="ignore"):
+            left = np.where(np.isnan(v), nal, v <= nd["thr"])
+        iscat = (nd["na_left"] & CAT_SPLIT_BIT) != 0
+        if catbits is not None and iscat.any():
+            c = np.where(np.isnan(v), -1, v).astype(np.int64)
+            inset = bitset_has(catbits[np.minimum(idx[r], len(catbits) - 1)], c)
+            oor = (c < 0) | (c > 255)
+            left = np.where(iscat & ~np.isnan(v), np.where(oor, nal, inset), left)
         idx[r] = np.where(left, nd["left"], nd["left"] + 1)
     return tree["value"][idx].astype(np.float64)
 
@@ -383,24 +436,38 @@ def raw_margin_cpu(ens, X, nt: int):
     n = X.shape[1]
     Xn = X.float().numpy()
     out = np.zeros((ens.K, n), np.float64) if ens.average else np.repeat(ens.init_f[:, None], n, 1).astype(np.float64)
+    cb = getattr(ens, "catbits", None)
     for t in range(T):
-        out[t % ens.K] += predict_tree_numpy(ens.trees[t], Xn)
+        out[t % ens.K] += predict_tree_numpy(ens.trees[t], Xn, None if cb is None else cb[t])
     if ens.average and nt > 0:
         out /= nt
     return torch.from_numpy(out.astype(np.float32))
 
 
 class _CpuView:
-    def __init__(self, Fm, trees, K, init_f):
+    def __init__(self, Fm, trees, K, init_f, cats=None):
         self.Fm, self._trees, self.K, self.init_f = Fm, trees, K, init_f
+        self._cats = cats or []
+
+    def catbits(self, lo: int, hi: int):
+        sel = self._cats[lo * self.K: hi * self.K]
+        if not sel:
+            return None
+        width = max(len(t) for t in self._trees[lo * self.K: hi * self.K])
+        out = np.zeros((len(sel), width, CAT_WORDS), np.uint32)
+        for i, c in enumerate(sel):
+            out[i, : c.shape[0]] = c
+        return out
 
     @property
     def margin(self) -> torch.Tensor:
         return torch.from_numpy(self.Fm)
 
     def trees(self, lo: int, hi: int) -> np.ndarray:
+        from ..models.tree.boost import concat_trees
+
         sel = self._trees[lo * self.K: hi * self.K]
-        return np.stack(sel) if sel else np.zeros((0, 1), TREE_NODE_DTYPE)
+        return concat_trees(*[t[None] for t in sel]) if sel else np.zeros((0, 1), TREE_NODE_DTYPE)
 
 
 def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw, tree_offset=0):
@@ -415,6 +482,7 @@ def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback
           else np.repeat(ens.init_f[:, None], n, 1).astype(np.float32))
     wobs = np.ones(n, np.float32) if w_np is None else w_np.astype(np.float32)
     trees = []
+    cats = []      # categorical left-set bitsets per tree (builder.catbits)
     # DRF out-of-bag sums (GPU: oob_accumulate_kernel)
     oob = (np.zeros((K, n), np.float64), np.zeros(n, np.float64)) if (dist == "drf" and sample_rate < 1.0) else None
     t0 = time.perf_counter()
@@ -445,17 +513,29 @@ def train_cpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback
             tree = builder.build(g32, h32, w32, ti * K + k, fmask)
             leaf = ~builder.nid[:n]
             Fm[k] += tree["value"][leaf]
-            trees.append(tree)
+            # keep the used prefix only (deep trees: capacity 2^(d+1) - 1 slots)
+            used = max(1, min(builder.n_nodes_total, builder.capacity))
+            trees.append(tree[:used].copy())
+            if builder.catbits is not None:
+                cats.append(builder.catbits[:used].copy())
             if oob is not None:
                 out_of_bag = (wb == 0) & (wobs != 0)
                 oob[0][k][out_of_bag] += tree["value"][leaf[out_of_bag]].astype(np.float32)
                 if k == 0:
                     oob[1][out_of_bag] += 1.0
-        if callback is not None and callback(t, _CpuView(Fm, trees, K, ens.init_f)) is True:
+        if callback is not None and callback(t, _CpuView(Fm, trees, K, ens.init_f, cats)) is True:
             break
     ens.timings["train_s"] = time.perf_counter() - t0
     builder.p.learn_rate = lr0
-    ens.trees = np.stack(trees) if trees else ens.trees
+    if trees:
+        from ..models.tree.boost import concat_trees
+
+        ens.trees = concat_trees(*[t[None] for t in trees])
+        if cats:
+            width = ens.trees.shape[1]
+            ens.catbits = np.zeros((len(cats), width, CAT_WORDS), np.uint32)
+            for i, c in enumerate(cats):
+                ens.catbits[i, : c.shape[0]] = c
     ens._cpu_margin = Fm
     if oob is not None:
         import torch

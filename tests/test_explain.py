@@ -71,7 +71,7 @@ def test_tree_shap_matches_bruteforce(cls, kw):
 def test_tree_paths_expected_value():
     df = _data(seed=2)
     m = H2OGradientBoostingEstimator(ntrees=3, max_depth=2, seed=1).train(y="y", training_frame=Frame.from_pandas(df))
-    lv, el, expected, maxm = tree_paths(m.ens.trees)
+    lv, el, expected, maxm, _ = tree_paths(m.ens.trees)
     ref = sum(cond_expect(t, np.zeros(4), set()) for t in m.ens.trees)
     assert abs(expected - ref) < 1e-6 and maxm <= 2
     assert lv.shape[0] <= 3 * 4 and el.shape[0] == lv[:, 1].sum()

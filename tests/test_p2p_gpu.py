@@ -66,7 +66,14 @@ def test_p2p_allreduce_two_ranks_one_gpu():
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tests", "_p2p_worker.py")]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
-    outs = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    # the two ranks share stdout: their JSON objects may land on one line
+    dec, outs, txt, i = json.JSONDecoder(), [], r.stdout, 0
+    while True:
+        i = txt.find('{"rank"', i)
+        if i < 0:
+            break
+        obj, i = dec.raw_decode(txt, i)
+        outs.append(obj)
     assert len(outs) == 2, r.stdout
     for o in outs:
         assert o["p2p"], o
