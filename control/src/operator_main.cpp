@@ -9,12 +9,14 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <chrono>
 #include <iostream>
 #include <map>
 #include <thread>
 
 #include "deployment.hpp"
+#include "http.hpp"
 #include "k8s.hpp"
 
 using namespace h2ok;
@@ -292,7 +294,7 @@ class Reconciler {
                      const IngressState& ing) {
     const std::string ns = s.ns;
     int ready = 0, total = 0;
-    std::string leader;
+    std::string leader, leader_ip;
     try {
       Json pods = c_.list(kinds::Pod, ns, "app=" + s.name);
       if (const Json* items = pods.find("items"))
@@ -304,6 +306,7 @@ class Reconciler {
                 if (c.get_string("type") == "Ready" && c.get_string("status") == "True") {
                   ++ready;
                   leader = object_name(p);
+                  leader_ip = p.get_string("status.podIP");
                 }
         }
     } catch (...) {
@@ -318,6 +321,13 @@ class Reconciler {
     st["serviceName"] = s.name + "-service";
     st["observedGeneration"] = cr.get_int("metadata.generation", 0);
     if (!msg.empty()) st["message"] = msg;
+    if (!leader.empty()) {
+      // GPU peer topology + collective transport as the formed cloud reports it
+      // (/3/Cloud h2omx_topology): a pod-per-GPU deployment without peer
+      // visibility shows up here, not only in the leader's log
+      Json topo = leader_topology(leader, leader_ip);
+      if (!topo.is_null()) st["topology"] = topo;
+    }
     if (ing.enabled) {
       st["ingressIP"] = ing.ip;
       st["ingressPath"] = ing.path;
@@ -347,6 +357,34 @@ class Reconciler {
       }
     } catch (...) {
     }
+  }
+
+  // GET <leader>/3/Cloud and return its h2omx_topology (null when unreachable).
+  // The leader serves the H2O REST API on :54321 at its pod IP;
+  // H2OMX_OPERATOR_CLOUD_URL ("http://host:port", "{pod}" replaced by the
+  // leader pod name) overrides that address (local test clusters).
+  Json leader_topology(const std::string& pod, const std::string& ip) {
+    std::string base;
+    if (const char* o = std::getenv("H2OMX_OPERATOR_CLOUD_URL")) {
+      base = o;
+      const auto k = base.find("{pod}");
+      if (k != std::string::npos) base.replace(k, 5, pod);
+    } else if (!ip.empty()) {
+      base = "http://" + ip + ":54321";
+    } else {
+      return Json();
+    }
+    try {
+      HttpRequest req;
+      req.target = "/3/Cloud";
+      req.timeout_s = 3.0;
+      HttpResponse r = http_request(parse_url(base), req, TlsConfig{});
+      if (r.status != 200) return Json();
+      Json cloud = Json::parse(r.body);
+      if (const Json* t = cloud.find("h2omx_topology")) return t->deep_copy();
+    } catch (...) {
+    }
+    return Json();
   }
 
   void log(const std::string& ns, const std::string& name, const std::string& what) {

@@ -244,4 +244,13 @@ def cloud_json(cluster, started_ms: int, node_infos: list[dict]) -> dict:
         "internal_security_enabled": False,
         "leader_idx": 0,
         "web_ip": None,
+        # h2omx extension: GPU peer topology + collective transport of the cloud
+        # (runtime/topology.py); the operator copies it into the H2O CR status
+        "h2omx_topology": _topology(cluster),
     }
+
+
+def _topology(cluster) -> dict:
+    from ..runtime.topology import cloud_summary
+
+    return cloud_summary(getattr(cluster, "topology", None), getattr(cluster, "comm", None))

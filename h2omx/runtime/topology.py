@@ -140,3 +140,28 @@ def check_cloud(comm, require: bool | None = None, probe_mb: float | None = None
     if rep["problems"] and require:
         raise RuntimeError("GPU peer access required (H2OMX_REQUIRE_P2P=1) but: " + "; ".join(rep["problems"]))
     return rep
+
+
+def cloud_summary(report: dict | None, comm=None) -> dict:
+    """Compact topology verdict for /3/Cloud and the operator's CR status:
+    per-host peer access, problems, and the transport the small collectives
+    use (one-shot P2P kernels over IPC-mapped HBM, or RCCL / gloo)."""
+    out = {"world": 1, "p2p": {}, "problems": [], "ok": True, "collectives": "none (1 rank)"}
+    if report:
+        out.update(world=report.get("world", 1), p2p={h: e.get("p2p") for h, e in report.get("hosts", {}).items()},
+                   problems=list(report.get("problems", [])), ok=bool(report.get("ok", True)))
+        if "probe" in report:
+            out["allreduce_busbw_GBs"] = report["probe"].get("busbw_GBs")
+    if comm is not None and comm.world_size > 1:
+        if getattr(comm, "p2p", None) is not None:
+            out["collectives"] = "p2p one-shot (IPC-mapped HBM) + rccl for large messages"
+        else:
+            try:
+                import torch.distributed as dist
+
+                be = dist.get_backend(comm.group) if dist.is_initialized() else "?"
+            except Exception:        # noqa: BLE001
+                be = "?"
+            out["collectives"] = ("rccl" if be == "nccl" else be) + (
+                f" (p2p off: {comm.p2p_error})" if getattr(comm, "p2p_error", None) else "")
+    return out

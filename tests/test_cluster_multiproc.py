@@ -138,6 +138,8 @@ def test_two_node_cloud_end_to_end(two_node_cloud):
     conn, csv, df, procs, d = two_node_cloud
     cloud = conn.request("GET /3/Cloud")
     assert cloud["cloud_size"] == 2
+    topo = cloud["h2omx_topology"]
+    assert topo["world"] == 2 and "collectives" in topo and isinstance(topo["problems"], list)
     key = conn.import_file(csv, destination_frame="train.hex")
     fr = conn.frame(key, rows=3)
     assert fr["rows"] == len(df)                          # both shards counted

@@ -64,10 +64,14 @@ def test_rendered_pod_runs_and_leader_probe(cloud):
     port = info["ports"][probe["port"]]
     with urllib.request.urlopen(f"http://127.0.0.1:{port}{probe['path']}", timeout=5) as r:
         assert r.status == 200
-    # second operator pass: pod Ready -> CR Ready with the leader pod
-    subprocess.run([OPERATOR, "--kubeconfig", cloud["cfg"], "--once"], check=True, capture_output=True, timeout=60)
+    # second operator pass: pod Ready -> CR Ready with the leader pod, and the
+    # cloud's GPU topology / collective transport from the leader's /3/Cloud
+    rest = info["ports"][54321]
+    subprocess.run([OPERATOR, "--kubeconfig", cloud["cfg"], "--once"], check=True, capture_output=True, timeout=60,
+                   env=dict(os.environ, H2OMX_OPERATOR_CLOUD_URL=f"http://127.0.0.1:{rest}"))
     st = k8s.get("h2os", "default", "iris")["status"]
     assert st["phase"] == "Ready" and st["leaderPod"] == "iris-stateful-set-0" and st["readyNodes"] == 1
+    assert st["topology"]["world"] == 1 and st["topology"]["ok"] is True
 
 
 def _iris_csv(tmp):

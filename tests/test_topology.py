@@ -53,3 +53,14 @@ def test_ranks_sharing_one_gpu_are_reported_as_such():
     infos = [dict(_r("n0", 0, 1), gpu_id="GPU-A") for _ in range(2)]
     rep = assess(infos)
     assert rep["hosts"]["n0"]["p2p"] == "shared device"
+
+
+def test_cloud_summary_for_rest_and_operator():
+    from h2omx.parallel.comm import Comm
+    from h2omx.runtime.topology import cloud_summary
+
+    rep = assess([_r("n0", 0, 1) for _ in range(2)])
+    out = cloud_summary(rep, Comm(0, 1))
+    assert out["world"] == 2 and out["ok"] is False and out["p2p"] == {"n0": "not visible"}
+    assert out["problems"] and out["collectives"] == "none (1 rank)"
+    assert cloud_summary(None)["ok"] is True
