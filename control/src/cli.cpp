@@ -1,7 +1,6 @@
 #include "cli.hpp"
+#include "platform.hpp"
 
-#include <sys/stat.h>
-#include <unistd.h>
 
 #include <cstdio>
 #include <iostream>
@@ -147,10 +146,7 @@ std::string general_help(const std::vector<SubSpec>& subs) {
   return os.str();
 }
 
-bool is_file(const std::string& p) {
-  struct stat st{};
-  return ::stat(p.c_str(), &st) == 0 && S_ISREG(st.st_mode);
-}
+bool is_file(const std::string& p) { return plat::is_regular_file(p); }
 
 std::optional<std::string> validate(const ArgSpec& a, const std::string& v) {
   auto parse_int = [&](long long& out) -> bool {
@@ -385,8 +381,7 @@ ParseOutcome parse_command_line(const std::vector<std::string>& args, const std:
   if (is_file(path)) {
     cmd.descriptor_path = path;
   } else {
-    char cwd[4096];
-    std::string rel = (getcwd(cwd, sizeof cwd) ? std::string(cwd) : std::string(".")) + "/" + path;
+    std::string rel = plat::current_dir() + "/" + path;
     if (!is_file(rel)) {
       out.input_error = UserInputError{CommandErrorKind::UnreachableDeploymentDescriptor};
       return out;

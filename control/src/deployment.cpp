@@ -1,7 +1,6 @@
 #include "deployment.hpp"
+#include "platform.hpp"
 
-#include <sys/stat.h>
-#include <unistd.h>
 
 #include <chrono>
 #include <cstdio>
@@ -392,10 +391,7 @@ void deploy_ingress(KubeClient& client, Deployment& d, int watch_timeout_s) {
 // descriptor files
 // ---------------------------------------------------------------------------
 namespace {
-bool path_exists(const std::string& p) {
-  struct stat st{};
-  return ::stat(p.c_str(), &st) == 0;
-}
+bool path_exists(const std::string& p) { return plat::path_exists(p); }
 }  // namespace
 
 std::string persist_deployment(const Deployment& d, bool overwrite, const std::string& explicit_path) {

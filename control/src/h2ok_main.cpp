@@ -3,12 +3,12 @@
 // (command dispatch :18-37, deploy :39-69, persist :71-101, undeploy
 // :103-115, ingress :117-141, descriptor load :143-164, TTY switch :166-169);
 // deviations are the fixes listed in SURVEY.md §7.6 (Q1, Q4-Q7, Q13).
-#include <unistd.h>
 
 #include <iostream>
 
 #include "cli.hpp"
 #include "deployment.hpp"
+#include "platform.hpp"
 #include "k8s.hpp"
 #include "yaml.hpp"
 
@@ -18,7 +18,7 @@ namespace {
 
 constexpr int kExitPanic = 101;  // the reference's exit status on a panic
 
-bool running_on_terminal() { return ::isatty(STDOUT_FILENO) == 1; }
+bool running_on_terminal() { return plat::stdout_is_tty(); }
 
 KubeClient client_for(const std::optional<std::string>& kubeconfig) {
   if (kubeconfig) return KubeClient(load_kubeconfig(*kubeconfig));

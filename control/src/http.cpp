@@ -1,16 +1,21 @@
 #include "http.hpp"
 
+#ifdef _WIN32
+#ifndef _WIN32_WINNT
+#define _WIN32_WINNT 0x0601   // inet_pton, getaddrinfo
+#endif
+#include <winsock2.h>
+#include <ws2tcpip.h>
+#else
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/in.h>
-#include <netinet/tcp.h>
+#include <sys/socket.h>
+#endif
 #include <openssl/err.h>
 #include <openssl/pem.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
-#include <poll.h>
-#include <sys/socket.h>
-#include <unistd.h>
 
 #include <cerrno>
 #include <chrono>
@@ -18,10 +23,7 @@
 #include <memory>
 #include <sstream>
 
-
-#ifndef MSG_NOSIGNAL
-#define MSG_NOSIGNAL 0   // macOS: SO_NOSIGPIPE is set on every socket instead
-#endif
+#include "platform.hpp"
 
 namespace h2ok {
 
@@ -57,7 +59,7 @@ class Conn {
       SSL_free(ssl_);
     }
     if (ctx_) SSL_CTX_free(ctx_);
-    if (fd_ >= 0) ::close(fd_);
+    plat::sock_close(fd_);
   }
   Conn(const Conn&) = delete;
   Conn& operator=(const Conn&) = delete;
@@ -65,16 +67,13 @@ class Conn {
   void write_all(const std::string& data) {
     size_t off = 0;
     while (off < data.size()) {
-      ssize_t n;
+      long n;
       if (ssl_) {
         n = SSL_write(ssl_, data.data() + off, (int)(data.size() - off));
         if (n <= 0) throw HttpError("TLS write failed: " + ssl_err());
       } else {
-        n = ::send(fd_, data.data() + off, data.size() - off, MSG_NOSIGNAL);
-        if (n < 0) {
-          if (errno == EINTR) continue;
-          throw HttpError(std::string("send failed: ") + std::strerror(errno));
-        }
+        n = plat::sock_send(fd_, data.data() + off, data.size() - off);
+        if (n < 0) throw HttpError("send failed: " + plat::sock_error());
       }
       off += (size_t)n;
     }
@@ -87,16 +86,15 @@ class Conn {
       auto now = std::chrono::steady_clock::now();
       double left = timeout_s_ - std::chrono::duration<double>(now - start_).count();
       if (left <= 0) return false;
-      pollfd p{fd_, POLLIN, 0};
-      int r = ::poll(&p, 1, (int)(left * 1000) + 1);
+      int r = plat::sock_wait_readable(fd_, (int)(left * 1000) + 1);
       if (r <= 0) return false;
     }
-    ssize_t n;
+    long n;
     if (ssl_) {
       n = SSL_read(ssl_, tmp, sizeof tmp);
       if (n <= 0) return false;
     } else {
-      n = ::recv(fd_, tmp, sizeof tmp, 0);
+      n = plat::sock_recv(fd_, tmp, sizeof tmp);
       if (n <= 0) return false;
     }
     buf_.append(tmp, (size_t)n);
@@ -135,6 +133,7 @@ class Conn {
 
  private:
   void connect_tcp(const std::string& host, int port) {
+    plat::net_init();
     addrinfo hints{};
     hints.ai_family = AF_UNSPEC;
     hints.ai_socktype = SOCK_STREAM;
@@ -144,24 +143,15 @@ class Conn {
     std::unique_ptr<addrinfo, void (*)(addrinfo*)> guard(res, freeaddrinfo);
     std::string last = "no address";
     for (addrinfo* a = res; a; a = a->ai_next) {
-      int fd = ::socket(a->ai_family, a->ai_socktype, a->ai_protocol);
-      if (fd < 0) continue;
-      timeval tv{};
-      tv.tv_sec = (long)timeout_s_;
-      tv.tv_usec = (long)((timeout_s_ - (long)timeout_s_) * 1e6);
-      setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
-      int one = 1;
-      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-#ifdef SO_NOSIGPIPE
-      // macOS has no MSG_NOSIGNAL: a closed peer must not SIGPIPE the CLI
-      setsockopt(fd, SOL_SOCKET, SO_NOSIGPIPE, &one, sizeof one);
-#endif
-      if (::connect(fd, a->ai_addr, a->ai_addrlen) == 0) {
+      plat::socket_t fd = plat::sock_open(a->ai_family, a->ai_socktype, a->ai_protocol);
+      if (fd == plat::kBadSocket) continue;
+      plat::sock_setup(fd, timeout_s_);
+      if (plat::sock_connect(fd, a->ai_addr, a->ai_addrlen)) {
         fd_ = fd;
         return;
       }
-      last = std::strerror(errno);
-      ::close(fd);
+      last = plat::sock_error();
+      plat::sock_close(fd);
     }
     throw HttpError("cannot connect to " + host + ":" + std::to_string(port) + ": " + last);
   }
@@ -199,7 +189,7 @@ class Conn {
     }
     SSL_CTX_set_verify(ctx_, tls.insecure ? SSL_VERIFY_NONE : SSL_VERIFY_PEER, nullptr);
     ssl_ = SSL_new(ctx_);
-    SSL_set_fd(ssl_, fd_);
+    SSL_set_fd(ssl_, (int)fd_);
     const std::string name = tls.server_name.empty() ? host : tls.server_name;
     if (!is_ip_literal(name)) SSL_set_tlsext_host_name(ssl_, name.c_str());
     if (!tls.insecure) {
@@ -210,7 +200,7 @@ class Conn {
     if (SSL_connect(ssl_) != 1) throw HttpError("TLS handshake with " + host + " failed: " + ssl_err());
   }
 
-  int fd_ = -1;
+  plat::socket_t fd_ = plat::kBadSocket;
   SSL_CTX* ctx_ = nullptr;
   SSL* ssl_ = nullptr;
   std::string buf_;

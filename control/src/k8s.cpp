@@ -1,12 +1,5 @@
 #include "k8s.hpp"
 
-#include <fcntl.h>
-#include <poll.h>
-#include <signal.h>
-#include <sys/stat.h>
-#include <sys/wait.h>
-#include <unistd.h>
-
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -14,6 +7,7 @@
 #include <fstream>
 #include <sstream>
 
+#include "platform.hpp"
 #include "yaml.hpp"
 
 namespace h2ok {
@@ -31,10 +25,7 @@ const ResourceKind CRD{"/apis/apiextensions.k8s.io/v1", "customresourcedefinitio
 
 namespace {
 
-bool file_exists(const std::string& p) {
-  struct stat st{};
-  return ::stat(p.c_str(), &st) == 0 && S_ISREG(st.st_mode);
-}
+bool file_exists(const std::string& p) { return plat::is_regular_file(p); }
 
 std::string read_file(const std::string& p) {
   std::ifstream in(p, std::ios::binary);
@@ -45,12 +36,18 @@ std::string read_file(const std::string& p) {
 }
 
 std::string dir_of(const std::string& p) {
-  size_t s = p.rfind('/');
+  size_t s = p.find_last_of(plat::path_sep() == '/' ? "/" : "/\\");
   return s == std::string::npos ? "." : p.substr(0, s);
 }
 
+bool is_absolute(const std::string& p) {
+  if (p.empty()) return false;
+  if (p[0] == '/' || p[0] == '\\') return true;
+  return plat::path_sep() == '\\' && p.size() > 2 && p[1] == ':';   // C:\...
+}
+
 std::string resolve(const std::string& base_dir, const std::string& p) {
-  if (p.empty() || p[0] == '/') return p;
+  if (p.empty() || is_absolute(p)) return p;
   return base_dir + "/" + p;
 }
 
@@ -149,75 +146,12 @@ KubeConfig load_kubeconfig(const std::string& path, const std::string& context) 
 
 namespace {
 
-// fork/exec argv with extra environment; stdout / stderr captured; killed
-// after timeout_s.  Returns the exit status (-1: could not run / timed out).
 int run_capture(const std::vector<std::string>& argv, const std::vector<std::pair<std::string, std::string>>& env,
                 std::string& out, std::string& err, double timeout_s) {
-  int po[2], pe[2];
-  if (pipe(po) != 0) return -1;
-  if (pipe(pe) != 0) {
-    close(po[0]);
-    close(po[1]);
-    return -1;
-  }
-  pid_t pid = fork();
-  if (pid < 0) return -1;
-  if (pid == 0) {
-    dup2(po[1], 1);
-    dup2(pe[1], 2);
-    close(po[0]);
-    close(pe[0]);
-    int devnull = open("/dev/null", O_RDONLY);
-    if (devnull >= 0) dup2(devnull, 0);
-    for (auto& [k, v] : env) setenv(k.c_str(), v.c_str(), 1);
-    std::vector<char*> av;
-    for (auto& a : argv) av.push_back(const_cast<char*>(a.c_str()));
-    av.push_back(nullptr);
-    execvp(av[0], av.data());
-    std::fprintf(stderr, "exec %s: %s\n", av[0], std::strerror(errno));
-    _exit(127);
-  }
-  close(po[1]);
-  close(pe[1]);
-  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds((long long)(timeout_s * 1000));
-  struct pollfd fds[2] = {{po[0], POLLIN, 0}, {pe[0], POLLIN, 0}};
-  int open_fds = 2;
-  bool timed_out = false;
-  char buf[4096];
-  while (open_fds > 0) {
-    auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now());
-    if (left.count() <= 0) {
-      timed_out = true;
-      break;
-    }
-    if (poll(fds, 2, (int)left.count()) <= 0) continue;
-    for (int i = 0; i < 2; ++i) {
-      if (fds[i].fd < 0 || !(fds[i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
-      ssize_t n = read(fds[i].fd, buf, sizeof buf);
-      if (n > 0) {
-        (i == 0 ? out : err).append(buf, (size_t)n);
-      } else {
-        close(fds[i].fd);
-        fds[i].fd = -1;
-        --open_fds;
-      }
-    }
-  }
-  for (auto& f : fds)
-    if (f.fd >= 0) close(f.fd);
-  if (timed_out) kill(pid, SIGKILL);
-  int st = 0;
-  waitpid(pid, &st, 0);
-  if (timed_out) return -1;
-  return WIFEXITED(st) ? WEXITSTATUS(st) : -1;
+  return plat::run_capture(argv, env, out, err, timeout_s);
 }
 
-long long parse_rfc3339(const std::string& t) {
-  if (t.size() < 19) return 0;
-  struct tm tm{};
-  if (!strptime(t.c_str(), "%Y-%m-%dT%H:%M:%S", &tm)) return 0;
-  return (long long)timegm(&tm);
-}
+long long parse_rfc3339(const std::string& t) { return plat::parse_rfc3339_utc(t); }
 
 std::string resolve_command(const std::string& base_dir, const std::string& cmd) {
   // a path with a separator is relative to the kubeconfig; a bare name is a PATH lookup
@@ -328,10 +262,13 @@ KubeConfig infer_kubeconfig() {
   if (const char* env = std::getenv("KUBECONFIG")) {
     std::stringstream ss(env);
     std::string item;
-    while (std::getline(ss, item, ':'))
+    // list separator: ':' (POSIX), ';' (Windows, where ':' follows drive letters)
+    while (std::getline(ss, item, plat::path_sep() == '/' ? ':' : ';'))
       if (!item.empty() && file_exists(item)) return load_kubeconfig(item);
   }
-  if (const char* home = std::getenv("HOME")) {
+  const char* home = std::getenv("HOME");
+  if (!home) home = std::getenv("USERPROFILE");   // Windows
+  if (home) {
     std::string p = std::string(home) + "/.kube/config";
     if (file_exists(p)) return load_kubeconfig(p);
   }

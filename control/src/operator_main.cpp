@@ -6,7 +6,6 @@
 // Cargo.toml:10 of isgasho/h2o-kubernetes); the CR schema mirrors its
 // DeploymentSpecification (src/k8s/mod.rs:58-74) as designed in SURVEY.md §7.2.
 #include <signal.h>
-#include <unistd.h>
 
 #include <atomic>
 #include <cstdlib>
