@@ -1495,22 +1495,14 @@ __device__ __forceinline__ WaveBest feat_best_cat_wave(const long long* gi, cons
   return r;
 }
 
-template <int NBT, bool CAT = false>
-__device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__ built,
-                                                   const long long* __restrict__ parent_full,
-                                                   long long* __restrict__ full, const NodeLink& lk, int node, int f,
-                                                   const int* __restrict__ nvb,
-                                                   const uint8_t* __restrict__ tree_fmask, double ig, double is,
-                                                   const SplitParams& p, int gid) {
-  constexpr int B = NBT <= 64 ? 1 : NBT / 64;  // bins per lane
+// Feature eligibility of (node, f), wave-uniform: a feature outside the node's
+// mtries / column sample only needs its histogram row completed for the next
+// level and the node totals - no prefix scan, no gains (DRF looks at sqrt(F)
+// of F features, so this skips most of the per-node work)
+__device__ __forceinline__ bool feat_allowed(const uint8_t* __restrict__ tree_fmask, const SplitParams& p, int node,
+                                             int f, int gid) {
   const int F = p.F;
   const int lane = threadIdx.x & 63;
-  const int64_t per = (int64_t)F * 2 * NBT;
-  const int64_t off = ((int64_t)f * 2) * NBT;
-  // feature eligibility first (wave-uniform): a feature outside the node's
-  // mtries / column sample only needs its histogram row completed for the
-  // next level and the node totals - no prefix scan, no gains (DRF looks at
-  // sqrt(F) of F features, so this skips most of the per-node work)
   bool allowed = (tree_fmask == nullptr) || tree_fmask[f];
   if (allowed && (p.mtries > 0 || p.col_rate < 1.0f)) {
     const uint32_t key = (uint32_t)p.tree_index * 131u + (uint32_t)p.depth;
@@ -1531,35 +1523,24 @@ __device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__
       allowed = u01(hf) < p.col_rate;
     }
   }
-  allowed = allowed && inter_ok(p, gid, f);
-  if (!allowed && full == nullptr && f != 0) {
-    // last level: no histogram row to keep and the node totals come from
-    // feature 0 (node_best reads fbest[node][0]) - nothing to load at all
-    WaveBest r;
-    r.G = r.S = 0.0;
-    r.gain = -INFINITY; r.code = 0x7fffffff; r.GL = r.SL = 0.0;
-    return r;
-  }
-  long long gi[B], si[B];
-#pragma unroll
-  for (int k = 0; k < B; ++k) {
-    const int bin = lane * B + k;
-    gi[k] = 0; si[k] = 0;
-    if (bin < NBT) {
-      if (lk.slot >= 0) {
-        const long long* bp = built + lk.slot * per + off + bin;
-        gi[k] = bp[0]; si[k] = bp[NBT];
-      } else {
-        const long long* pp = parent_full + lk.parent * per + off + bin;
-        const long long* sp = built + lk.sib_slot * per + off + bin;
-        gi[k] = pp[0] - sp[0]; si[k] = pp[NBT] - sp[NBT];
-      }
-      if (full) {
-        long long* fp = full + node * per + off + bin;
-        fp[0] = gi[k]; fp[NBT] = si[k];
-      }
-    }
-  }
+  return allowed && inter_ok(p, gid, f);
+}
+
+__device__ __forceinline__ WaveBest wave_best_none() {
+  WaveBest r;
+  r.G = r.S = 0.0;
+  r.gain = -INFINITY; r.code = 0x7fffffff; r.GL = r.SL = 0.0;
+  return r;
+}
+
+// Best threshold of (node, f) from the completed histogram row held in
+// registers (lane owns bins lane * B .. lane * B + B - 1; B = NBT / 64).
+template <int NBT, bool CAT>
+__device__ __forceinline__ WaveBest feat_scan_wave(long long* gi, long long* si, bool allowed, int node, int f,
+                                                   const int* __restrict__ nvb, double ig, double is,
+                                                   const SplitParams& p) {
+  constexpr int B = NBT <= 64 ? 1 : NBT / 64;  // bins per lane
+  const int lane = threadIdx.x & 63;
   if (!allowed) {
     long long tg_i = 0, ts_i = 0;
 #pragma unroll
@@ -1641,6 +1622,152 @@ __device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__
     r.SL = __shfl(bSL, src, kWave);
   }
   return r;
+}
+
+// Best threshold of (node, f) computed by one wave from the level's built
+// histograms (slot, or parent - built sibling); also stores the completed row
+// into `full` (parent of the next level) when given.
+template <int NBT, bool CAT = false>
+__device__ __forceinline__ WaveBest feat_best_wave(const long long* __restrict__ built,
+                                                   const long long* __restrict__ parent_full,
+                                                   long long* __restrict__ full, const NodeLink& lk, int node, int f,
+                                                   const int* __restrict__ nvb,
+                                                   const uint8_t* __restrict__ tree_fmask, double ig, double is,
+                                                   const SplitParams& p, int gid) {
+  constexpr int B = NBT <= 64 ? 1 : NBT / 64;  // bins per lane
+  const int lane = threadIdx.x & 63;
+  const int64_t per = (int64_t)p.F * 2 * NBT;
+  const int64_t off = ((int64_t)f * 2) * NBT;
+  const bool allowed = feat_allowed(tree_fmask, p, node, f, gid);
+  // last level: no histogram row to keep and the node totals come from
+  // feature 0 (node_best reads fbest[node][0]) - nothing to load at all
+  if (!allowed && full == nullptr && f != 0) return wave_best_none();
+  long long gi[B], si[B];
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const int bin = lane * B + k;
+    gi[k] = 0; si[k] = 0;
+    if (bin < NBT) {
+      if (lk.slot >= 0) {
+        const long long* bp = built + lk.slot * per + off + bin;
+        gi[k] = bp[0]; si[k] = bp[NBT];
+      } else {
+        const long long* pp = parent_full + lk.parent * per + off + bin;
+        const long long* sp = built + lk.sib_slot * per + off + bin;
+        gi[k] = pp[0] - sp[0]; si[k] = pp[NBT] - sp[NBT];
+      }
+      if (full) {
+        long long* fp = full + node * per + off + bin;
+        fp[0] = gi[k]; fp[NBT] = si[k];
+      }
+    }
+  }
+  return feat_scan_wave<NBT, CAT>(gi, si, allowed, node, f, nvb, ig, is, p);
+}
+
+__device__ __forceinline__ void store_feat_best(FeatBest* __restrict__ out, int64_t i, const WaveBest& w) {
+  FeatBest r{};
+  r.gain = w.gain; r.GL = w.GL; r.SL = w.SL;
+  r.G = w.G; r.S = w.S;
+  r.code = w.code;
+  out[i] = r;
+}
+
+// K3 tail + K5 fused (single rank): one 1024-thread workgroup per (built slot,
+// feature) sums that histogram row's workgroup slabs (16-byte loads: LANES
+// slab lanes x NBT / 2 bin pairs, 8 loads of a lane in flight), keeps the
+// exact int64 row in LDS and scans the slot's two nodes right away (wave 0:
+// node 2s, wave 1: node 2s + 1 - the children of the s-th splitting node; the
+// unbuilt one is parent - built).  The built rows never round-trip through
+// global memory and the level drops the split_find launch (hist_reduce +
+// split_find were 4.7 + 7.5 us a level at 1.375M rows, mostly fixed cost).
+// Multi-rank levels keep hist_reduce -> all-reduce -> split_find.
+template <int NBT, bool CAT>
+__global__ __launch_bounds__(1024) void reduce_split_kernel(
+    const unsigned long long* __restrict__ partials, int wgpg, int fg, int slot_lo, int slot_cnt,
+    const long long* __restrict__ parent_full, long long* __restrict__ full, const int* __restrict__ ctl,
+    const NodeLink* __restrict__ link, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
+    const double* __restrict__ qscale, SplitParams p, FeatBest* __restrict__ out) {
+  constexpr int PAIRS = NBT / 2, LANES = 1024 / PAIRS;
+  __shared__ long long red[LANES][PAIRS][4];   // 32 KB
+  __shared__ long long row[2][NBT];            // exact (G_q, S_q) of the built slot
+  const int s = blockIdx.x, f = blockIdx.y;
+  const int slot = slot_lo + s;
+  if (slot >= ctl[CTL_SLOTS]) return;   // whole workgroup
+  const int F = p.F;
+  const int group = f / fg, fi = f % fg;
+  const int64_t hist_elems = (int64_t)slot_cnt * fg * NBT;
+  const unsigned long long* src = partials + (int64_t)group * wgpg * hist_elems + ((int64_t)s * fg + fi) * NBT;
+  const int t = threadIdx.x, bp = t % PAIRS, c0 = t / PAIRS;
+  long long g0 = 0, s0 = 0, g1 = 0, s1 = 0;
+  {
+    const uint4* q = reinterpret_cast<const uint4*>(src) + bp;
+    const int64_t stride = hist_elems / 2;   // uint4 per slab
+    int c = c0;
+    // 8 slab loads in flight per lane (wgpg is typically 64-256: one or two batches)
+    for (; c + 7 * LANES < wgpg; c += 8 * LANES) {
+      uint4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = q[(int64_t)(c + k * LANES) * stride];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        g0 += (long long)(int32_t)v[k].y; s0 += (long long)v[k].x;
+        g1 += (long long)(int32_t)v[k].w; s1 += (long long)v[k].z;
+      }
+    }
+    for (; c < wgpg; c += LANES) {
+      const uint4 v = q[(int64_t)c * stride];
+      g0 += (long long)(int32_t)v.y; s0 += (long long)v.x;
+      g1 += (long long)(int32_t)v.w; s1 += (long long)v.z;
+    }
+  }
+  red[c0][bp][0] = g0; red[c0][bp][1] = s0; red[c0][bp][2] = g1; red[c0][bp][3] = s1;
+  __syncthreads();
+  if (t < NBT) {
+    const int pr = t >> 1, h = (t & 1) * 2;
+    long long tg = 0, ts = 0;
+#pragma unroll 8
+    for (int k = 0; k < LANES; ++k) { tg += red[k][pr][h]; ts += red[k][pr][h + 1]; }
+    row[0][t] = tg;
+    row[1][t] = ts;
+  }
+  __syncthreads();
+  const int wid = t >> 6, lane = t & 63;
+  if (wid >= 2) return;
+  const int n = ctl[CTL_N];
+  const int node = 2 * slot + wid;   // level 0: slot 0 = the root, n = 1
+  if (node >= n) return;
+  const NodeLink lk = link[node];
+  if (lk.slot != slot && lk.sib_slot != slot) return;   // (not a child pair: cannot happen)
+  const int gid = ctl[CTL_BASE] + node;
+  const bool allowed = feat_allowed(tree_fmask, p, node, f, gid);
+  WaveBest w;
+  if (!allowed && full == nullptr && f != 0) {
+    w = wave_best_none();
+  } else {
+    constexpr int B = NBT <= 64 ? 1 : NBT / 64;
+    const int64_t per = (int64_t)F * 2 * NBT;
+    const int64_t off = ((int64_t)f * 2) * NBT;
+    long long gi[B], si[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+      const int bin = lane * B + k;
+      gi[k] = 0; si[k] = 0;
+      if (bin < NBT) {
+        gi[k] = row[0][bin]; si[k] = row[1][bin];
+        if (lk.slot != slot) {
+          const long long* pp = parent_full + lk.parent * per + off + bin;
+          gi[k] = pp[0] - gi[k]; si[k] = pp[NBT] - si[k];
+        }
+        if (full) {
+          long long* fp = full + node * per + off + bin;
+          fp[0] = gi[k]; fp[NBT] = si[k];
+        }
+      }
+    }
+    w = feat_scan_wave<NBT, CAT>(gi, si, allowed, node, f, nvb, qscale[2], qscale[3], p);
+  }
+  if (lane == 0) store_feat_best(out, (int64_t)node * F + f, w);
 }
 
 // K5: best threshold of every (node, feature).  One wave per (node, feature)
@@ -2595,7 +2722,17 @@ __global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F
                                                            const float* __restrict__ wobs, int64_t n, int64_t npad,
                                                            int* __restrict__ nid, const TreeNode* __restrict__ tree,
                                                            GradParams gp, float* __restrict__ g, float* __restrict__ h,
-                                                           float* __restrict__ wout, unsigned int* __restrict__ stat_max) {
+                                                           float* __restrict__ wout, unsigned int* __restrict__ stat_max,
+                                                           const uint4* __restrict__ arch_src, int arch_n16,
+                                                           uint4* __restrict__ ring, int ring_n,
+                                                           const int* __restrict__ tree_ctr, int ctr_off) {
+  if (ring != nullptr) {
+    // graph replay: the applied tree also goes to ring slot (tree_ctr - ctr_off)
+    // mod ring_n (tree_archive folded into this launch)
+    const int slot = (int)(((unsigned)(tree_ctr[0] - ctr_off)) % (unsigned)ring_n);
+    uint4* dst = ring + (int64_t)slot * arch_n16;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < arch_n16; i += gridDim.x * blockDim.x) dst[i] = arch_src[i];
+  }
   float mg = 0.f, mh = 0.f, mw = 0.f;
   const int64_t nq = npad / 4;  // 4 rows per lane, 16-byte accesses
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
@@ -2833,6 +2970,32 @@ __global__ __launch_bounds__(256) void leaf_finalize_kernel(const unsigned long 
       tree[gid] = nd;
     }
   }
+}
+
+// Graph replay with fixed gradient bounds: leaf_finalize, then (same
+// workgroup, after every leaf sum was read) the NEXT tree's tree_begin - the
+// leaf sums it read are zeroed (only [0, 3 * total) was written this tree,
+// so the whole buffer is zero again), scales / level-0 control / root link
+// set and the tree counter advanced.  Saves the tree_begin launch per tree.
+__global__ __launch_bounds__(1024) void leaf_finalize_begin_kernel(
+    unsigned long long* __restrict__ acc, const int* __restrict__ ctl_final, double* __restrict__ qs, SplitParams p,
+    TreeNode* __restrict__ tree, int cap, const unsigned int* __restrict__ stat_max, int mode, double qg, double qsr,
+    int* __restrict__ ctl0, NodeLink* __restrict__ link0, long long row_base, int* __restrict__ tree_ctr) {
+  const int total = min(ctl_final[CTL_TOTAL], cap);
+  const double s4 = qs[4], s5 = qs[5], s6 = qs[6];
+  for (int gid = threadIdx.x; gid < total; gid += blockDim.x) {
+    const long long ag = (long long)acc[3 * gid], ah = (long long)acc[3 * gid + 1], aw = (long long)acc[3 * gid + 2];
+    acc[3 * gid] = 0ull; acc[3 * gid + 1] = 0ull; acc[3 * gid + 2] = 0ull;
+    TreeNode nd = tree[gid];
+    if (nd.feat < 0) {
+      const double G = (double)ag / s4, H = (double)ah / s5, W = (double)aw / s6;
+      nd.value = (float)clamp_bound(leaf_value(G, H, W, p), p, gid, cap);
+      nd.weight = (float)W;
+      tree[gid] = nd;
+    }
+  }
+  __syncthreads();   // ctl_final may be ctl0 (even depth); qs read above
+  if (threadIdx.x == 0) tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0, row_base, 0, tree_ctr);
 }
 
 // Monotone constraints with H2O's squared-error splits (mode 0) and Newton
@@ -3259,6 +3422,33 @@ H2OMX_API int h2omx_split_find(const long long* built, const long long* parent_f
   return launch_status();
 }
 
+H2OMX_API int h2omx_reduce_split(const unsigned long long* partials, int wgpg, int fg, int slot_lo, int slot_cnt,
+                                 const long long* parent_full, long long* full, const int* ctl, const void* link,
+                                 const int* nvb, const uint8_t* tree_fmask, const double* qscale, const void* params,
+                                 int nbt, void* out, hipStream_t stream) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  if (slot_cnt < 1 || wgpg < 1 || fg < 1 || p.F < 1) return kBadArg;
+  const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
+  FeatBest* o = reinterpret_cast<FeatBest*>(out);
+  const dim3 grid(slot_cnt, p.F);
+#define H2OMX_RS(NB)                                                                                              \
+  if (p.catf != nullptr)                                                                                          \
+    hipLaunchKernelGGL((reduce_split_kernel<NB, true>), grid, dim3(1024), 0, stream, partials, wgpg, fg, slot_lo, \
+                       slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o);                      \
+  else                                                                                                            \
+    hipLaunchKernelGGL((reduce_split_kernel<NB, false>), grid, dim3(1024), 0, stream, partials, wgpg, fg,         \
+                       slot_lo, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o)
+  switch (nbt) {
+    case 32: H2OMX_RS(32); break;
+    case 64: H2OMX_RS(64); break;
+    case 128: H2OMX_RS(128); break;
+    case 256: H2OMX_RS(256); break;
+    default: return kBadArg;
+  }
+#undef H2OMX_RS
+  return launch_status();
+}
+
 H2OMX_API int h2omx_split_level(const long long* built, const long long* parent_full, long long* full, const int* ctl,
                                 const void* link, const int* nvb, const uint8_t* tree_fmask, const double* qscale,
                                 const void* params, int max_nodes, int nbt, void* nsplit, unsigned int* ticket,
@@ -3457,12 +3647,18 @@ H2OMX_API int h2omx_route_level(const uint8_t* codes, int64_t npad, const int* n
 
 static inline int stream_grid(int64_t) { return STAT_BLOCKS; }
 
+// ring != nullptr: also copy `tree` (tree_bytes) into ring slot
+// (tree_ctr - ctr_off) mod ring_n (graph replay's tree archive)
 H2OMX_API int h2omx_boost_update(float* F, const float* y, const float* wobs, int64_t n, int64_t npad, int* nid,
                                  const void* tree, const void* gparams, float* g, float* h, float* wout,
-                                 unsigned int* stat_max, hipStream_t stream) {
+                                 unsigned int* stat_max, int64_t tree_bytes, void* ring, int ring_n,
+                                 const int* tree_ctr, int ctr_off, hipStream_t stream) {
   const GradParams gp = *reinterpret_cast<const GradParams*>(gparams);
+  if (ring != nullptr && (tree_bytes % 16 != 0 || ring_n < 1 || tree_ctr == nullptr)) return kBadArg;
   hipLaunchKernelGGL(boost_update_kernel, dim3(stream_grid(npad)), dim3(256), 0, stream, F, y, wobs, n, npad, nid,
-                     reinterpret_cast<const TreeNode*>(tree), gp, g, h, wout, stat_max);
+                     reinterpret_cast<const TreeNode*>(tree), gp, g, h, wout, stat_max,
+                     reinterpret_cast<const uint4*>(tree), (int)(tree_bytes / 16), reinterpret_cast<uint4*>(ring),
+                     ring_n, tree_ctr, ctr_off);
   return launch_status();
 }
 
@@ -3551,6 +3747,20 @@ H2OMX_API int h2omx_leaf_finalize(const unsigned long long* acc, const int* ctl_
   const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
   hipLaunchKernelGGL(leaf_finalize_kernel, dim3(grid_for(cap, 256, 1024)), dim3(256), 0, stream, acc, ctl_final,
                      qscale, p, reinterpret_cast<TreeNode*>(tree), cap);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_leaf_finalize_begin(unsigned long long* acc, const int* ctl_final, double* qscale,
+                                        const void* params, void* tree, int cap, const unsigned int* stat_max,
+                                        int mode, int max_rows_per_wg, int* ctl0, void* link0, long long row_base,
+                                        int* tree_ctr, hipStream_t stream) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  if (max_rows_per_wg < 1 || max_rows_per_wg > ROWS_CAP || tree_ctr == nullptr || p.gbound != nullptr) return kBadArg;
+  const double qg = exp2(floor(log2(1073741824.0 / max_rows_per_wg)));
+  const double qsr = exp2(floor(log2(2147483648.0 / max_rows_per_wg)));
+  hipLaunchKernelGGL(leaf_finalize_begin_kernel, dim3(1), dim3(1024), 0, stream, acc, ctl_final, qscale, p,
+                     reinterpret_cast<TreeNode*>(tree), cap, stat_max, mode, qg, qsr, ctl0,
+                     reinterpret_cast<NodeLink*>(link0), row_base, tree_ctr);
   return launch_status();
 }
 

@@ -164,44 +164,55 @@ def init_margin(dist: str, y, w, K: int) -> np.ndarray:
     return np.array([(ww * y).sum() / sw])
 
 
+def _order_keys(r: torch.Tensor) -> torch.Tensor:
+    """int64 keys ordered like the float64 values (IEEE bits, negative values
+    with the magnitude bits flipped)."""
+    b = r.contiguous().view(torch.int64)
+    return torch.where(b < 0, b ^ 0x7FFFFFFFFFFFFFFF, b)
+
+
+def _key_value(k: int) -> float:
+    b = k ^ 0x7FFFFFFFFFFFFFFF if k < 0 else k
+    return float(np.array([b], np.int64).view(np.float64)[0])
+
+
 def weighted_quantile(r, w, q: float, comm=None) -> float:
     """Weighted 'lower' q-quantile of ``r`` over every rank: the smallest value
-    v of the data with sum(w[r <= v]) >= q * sum(w).  Bisection on the value
-    with one all-reduced weight sum per step (no gather of the rows, any row
-    count; torch.quantile is limited to 2^24 elements), then snapped to the
-    smallest data value >= the bracket."""
+    v of the data with sum(w[r <= v]) >= q * sum(w).  Bisection on the
+    order-preserving int64 key of the float64 value (at most 64 steps, exact:
+    the bracket ends on adjacent keys, and the upper one is a data value),
+    one all-reduced weight sum per step (no gather of the rows, any row
+    count; torch.quantile is limited to 2^24 elements)."""
     multi = comm is not None and comm.world_size > 1
     r = r.detach().double() if torch.is_tensor(r) else torch.from_numpy(np.asarray(r, np.float64))
     wt = torch.ones_like(r) if w is None else (w.detach().double() if torch.is_tensor(w)
                                                else torch.from_numpy(np.asarray(w, np.float64))).to(r.device)
     keep = wt > 0
     r, wt = r[keep], wt[keep]
+    keys = _order_keys(r)
 
     def red(v, op="sum"):
         a = np.array(v, np.float64)
         return comm.all_reduce_numpy(a, op) if multi else a
 
-    big = 1e300
-    lo = -float(red([-(float(r.min()) if r.numel() else -big)], "max")[0])
-    hi = float(red([float(r.max()) if r.numel() else -big], "max")[0])
     W = float(red([float(wt.sum())])[0])
     if W <= 0:
         return 0.0
+    # key range over every rank: reduce the min / max values, then key them
+    lo_v = -float(red([-(float(r.min()) if r.numel() else 1e300)], "max")[0])
+    hi_v = float(red([float(r.max()) if r.numel() else -1e300], "max")[0])
+    lo = int(_order_keys(torch.tensor([lo_v], dtype=torch.float64))[0])
+    hi = int(_order_keys(torch.tensor([hi_v], dtype=torch.float64))[0])
     target = q * W
-    if float(red([float(wt[r <= lo].sum())])[0]) >= target:
-        return lo
-    for _ in range(200):            # invariant: cum(lo) < target <= cum(hi)
-        mid = 0.5 * (lo + hi)
-        if mid <= lo or mid >= hi:
-            break
-        if float(red([float(wt[r <= mid].sum())])[0]) >= target:
+    if float(red([float(wt[keys <= lo].sum())])[0]) >= target:
+        return lo_v
+    while hi - lo > 1:              # invariant: cum(lo) < target <= cum(hi)
+        mid = lo + (hi - lo) // 2
+        if float(red([float(wt[keys <= mid].sum())])[0]) >= target:
             hi = mid
         else:
             lo = mid
-    # smallest data value in (lo, hi]
-    cand = r[(r > lo) & (r <= hi)]
-    v = -float(red([-(float(cand.min()) if cand.numel() else big)], "max")[0])
-    return v if v < big else hi
+    return _key_value(hi)
 
 
 def train_ensemble(bm: BinnedMatrix, y, w=None, *, dist: str = "bernoulli", ntrees: int = 50,
@@ -324,6 +335,7 @@ class GpuBooster:
         self.trees_dev = []
         self.cats_dev = []         # categorical left-set bitsets, parallel to trees_dev
         self.graph_used = False   # a step graph was captured (finish() releases the graph itself)
+        self.graph_chain = False  # ... with tree_begin / archive folded into neighbours (TreeGraph.chain)
         need_w = sample_rate < 1.0 or self.st.w is not None
         self.wout = torch.empty((bm.npad,), dtype=torch.float32, device=self.dev) if need_w else None
         self.kw = dict(tweedie_power=dist_kw.get("tweedie_power", 1.5),
@@ -348,6 +360,7 @@ class GpuBooster:
                         torch.zeros((bm.npad,), dtype=torch.float32, device=self.dev))
             self.use_graph = False
         self.pending = False
+        self._archive = None     # TreeGraph capture: (ring, slots, counter offset)
         # bounded gradients (unweighted rows; bagging only zeroes rows) quantise with
         # the bound scales on every path, fused or not
         self._bounds = None
@@ -377,10 +390,13 @@ class GpuBooster:
         # per-block maxima, no maxima reduction and no bounds copy per tree
         fixed = self._bounds is not None and k == 0 and self.K == 1
         with b.timer.phase("grad"):
+            arch = self._archive    # (ring, slots, counter offset): graph replay's tree archive
             ops.check(self.lib.h2omx_boost_update(P(st.Fm[k]), P(y), P(st.w), self.bm.n, self.bm.npad, P(b.nid),
                                                   P(b.tree_buf), ctypes.addressof(gp), P(st.g[k]), P(st.h[k]),
                                                   P(self.wout), P(None if fixed else b.stat_slab),
-                                                  ops.stream(self.dev)),
+                                                  b.tree_buf.numel(), P(arch[0] if arch else None),
+                                                  arch[1] if arch else 0, P(b.tree_ctr if arch else None),
+                                                  arch[2] if arch else 0, ops.stream(self.dev)),
                       "boost_update")
             if not fixed:
                 b.reduce_stats()
@@ -398,13 +414,13 @@ class GpuBooster:
                 and not b.segmented and not b.timer.enabled and self.cap <= self.COMPACT_CAP
                 and self.dev.type == "cuda" and b.catf is None)
 
-    def _body_k1(self, t: int, fresh: bool):
+    def _body_k1(self, t: int, fresh: bool, chain: bool = False):
         b = self.builder
         if fresh:
             # grow the tree straight into its own buffer (no copy afterwards);
             # the next boost_update applies it from there
             b.tree_buf = torch.empty_like(b.tree_buf)
-        b.build(self.st.g[0], self.st.h[0], self.wout, t, None, stat=self._bounds)
+        b.build(self.st.g[0], self.st.h[0], self.wout, t, None, stat=self._bounds, chain=chain)
 
     def step(self):
         P, st, b, bm, t = ops.P, self.st, self.builder, self.bm, self.t
@@ -488,6 +504,7 @@ class GpuBooster:
             return
         self.graph = g
         self.graph_used = True
+        self.graph_chain = g.chain
 
     def _snap_cat(self) -> None:
         """Copy of the finished tree's categorical bitsets (nodes of the tree only)."""
@@ -648,6 +665,7 @@ class TreeGraph:
         self.ring = None
         self.live: list = []      # (trees_dev index, ring slot) still pointing into the ring
         self.expect = None        # tree index the device counter holds
+        self.chain = False        # tree_begin folded into the previous step (see capture)
 
     def capture(self):
         gb, b = self.gb, self.gb.builder
@@ -673,6 +691,10 @@ class TreeGraph:
         # regular pool are safe during capture.)
         gc_was = gc.isenabled()
         gc.disable()
+        # tree_begin of the next tree runs inside this tree's leaf finalisation
+        # (fixed gradient bounds), the tree archive inside boost_update: the
+        # replayed step is levels -> leaf_finalize(+begin) -> boost_update(+archive)
+        self.chain = b.can_chain(gb._bounds is not None)
         try:
             with torch.cuda.stream(side):
                 g = torch.cuda.CUDAGraph()
@@ -680,13 +702,14 @@ class TreeGraph:
                 self._open = g
                 if segmented:
                     b.comm = _SegmentComm(self, self.comm)
+                # archive slot: tree_ctr - 1 after this tree's begin, - 2 once the
+                # leaf finalisation has begun the next tree
+                gb._archive = (self.ring, self.RING, 2 if self.chain else 1)
                 try:
-                    gb._body_k1(gb.t, fresh=False)
+                    gb._body_k1(gb.t, fresh=False, chain=self.chain)
                     gb._update(apply=True, next_tree=gb.t + 1, k=0)
-                    ops.check(gb.lib.h2omx_tree_archive(ops.P(b.tree_buf), b.tree_buf.numel(), ops.P(self.ring),
-                                                        self.RING, ops.P(b.tree_ctr), ops.stream(dev)),
-                              "tree_archive")
                 finally:
+                    gb._archive = None
                     b.comm = self.comm
                     self._open.capture_end()
                     self.graphs.append(self._open)
@@ -710,7 +733,10 @@ class TreeGraph:
     def replay(self, t: int):
         """Grow tree ``t`` (and update margins / gradients for tree t + 1)."""
         if self.expect != t:   # tree_begin advances the counter: set only when out of step
-            self.gb.builder.tree_ctr.fill_(t & 0x7FFFFFFF)
+            b = self.gb.builder
+            b.tree_ctr.fill_(t & 0x7FFFFFFF)
+            if self.chain:     # the graph starts at level 0: begin this tree here
+                b.begin(self.gb._bounds, t)
         self.expect = t + 1
         if len(self.live) >= self.RING:
             self.freeze()
@@ -724,11 +750,13 @@ class TreeGraph:
         self.gb.trees_dev.append(self.ring[slot])
 
     def freeze(self):
-        """Point the trees still living in the ring at one snapshot of it."""
+        """Point the trees still living in the ring at one copy of their slots
+        (only the live ones: scoring reads the trees every few replays)."""
         if self.live:
-            snap = self.ring.clone()
-            for i, slot in self.live:
-                self.gb.trees_dev[i] = snap[slot]
+            slots = torch.tensor([slot for _, slot in self.live], dtype=torch.int64, device=self.ring.device)
+            snap = self.ring.index_select(0, slots)
+            for j, (i, _) in enumerate(self.live):
+                self.gb.trees_dev[i] = snap[j]
             self.live = []
 
 

@@ -360,6 +360,8 @@ class HipTreeBuilder:
     # Bit-identical but no faster (11-13 us vs 6.6-7.9 + 4.9-5.0 us a level: the tail is
     # a dependent-latency chain, not launch overhead, profiles/r3/hist_threads_ab.txt ab25/26)
     SPLIT_FIN = os.environ.get("H2OMX_SPLIT_FIN", "0") == "1"
+    # single rank: slab reduction + split scan in one launch per pass (reduce_split)
+    FUSE_RS = os.environ.get("H2OMX_FUSE_RS", "1") == "1"
     MAX_WG_THREADS_PER_CU = 2048      # 32 waves per CU
 
     def _fill_rounds(self, wgpg: int, n_groups: int, lds_bytes: int, threads: int, units: int) -> int:
@@ -489,13 +491,17 @@ class HipTreeBuilder:
 
     def build(self, g: torch.Tensor, h: torch.Tensor, w: torch.Tensor | None, tree_index: int,
               tree_fmask: torch.Tensor | None = None, grad_fuse: dict | None = None,
-              stat: torch.Tensor | None = None) -> torch.Tensor:
+              stat: torch.Tensor | None = None, chain: bool = False) -> torch.Tensor:
         """Grow one tree from per-row (g, h, w).  Preconditions (established by
         the boost / softmax kernels): ``self.nid`` is 0 for rows of the tree and
         INT_MIN for padding; ``self.stat_max`` holds this tree's maxima.
         Returns the device tree buffer (``TREE_NODE_DTYPE`` heap of capacity
         nodes; unreachable records are garbage).  ``self.stat_max`` must hold
-        this tree's gradient maxima (see :meth:`reduce_stats`)."""
+        this tree's gradient maxima (see :meth:`reduce_stats`).
+
+        ``chain`` (graph replay, fixed bounds ``stat``): this tree's begin was
+        done by the previous tree's leaf finalisation (or :meth:`begin`), and
+        this one's leaf finalisation begins the next tree."""
         # ``stat``: fixed gradient bounds (stat_max image, identical on every rank)
         # used instead of this tree's maxima: no maxima reduction, no all-reduce
         if grad_fuse is not None:
@@ -517,10 +523,9 @@ class HipTreeBuilder:
         link = [self._buf("link0", 4, torch.int32), None]
         # scales + level-0 control block/link + zeroed leaf sums in one launch
         T = self.timer.phase
-        with T("tree_begin"):
-            ops.check(lib.h2omx_tree_begin(P(smax), p.mode, self.max_rows_per_wg, P(self.qscale),
-                                           P(self.ctl[0]), P(link[0]), P(self.leaf_acc), self.leaf_acc.numel(),
-                                           self.row_base, tree_index & 0x7FFFFFFF, P(self.tree_ctr), st), "tree_begin")
+        if not chain:
+            with T("tree_begin"):
+                self.begin(smax, tree_index)
         full_prev = None
         max_depth = p.max_depth
         final_ctl = self.ctl[max_depth % 2]
@@ -547,6 +552,26 @@ class HipTreeBuilder:
             if l0_copies:
                 plan = self.plan_l0()
             built = self._buf("built", max_slots * self.per_node, torch.int64)
+            full_cur = None if last else self._buf(f"full{cur}", max_nodes * self.per_node, torch.int64)
+            sp.depth = d
+            sp.children_leaves = 1 if last else 0
+            self._cat_level(max_nodes)
+            # single rank: each pass's slab reduction runs the split scan of its slots
+            # right away (reduce_split); multi-rank levels all-reduce `built` in between
+            rs = (comm is None and self.FUSE_RS and not self.fuse_split
+                  and not (self.SPLIT_FIN and max_nodes <= 64 and self.catf is None))
+            fbest = (self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
+                     if not self.fuse_split else None)
+
+            def reduce(n_groups, wgpg, fg, slot_lo, slot_cnt):
+                if rs:
+                    ops.check(lib.h2omx_reduce_split(P(partials), wgpg, fg, slot_lo, slot_cnt, P(full_prev),
+                                                     P(full_cur), P(ctl_cur), P(link[cur]), P(bm.nvb),
+                                                     P(tree_fmask), P(self.qscale), spp, nbt, P(fbest), st),
+                              "reduce_split")
+                else:
+                    ops.check(lib.h2omx_hist_reduce(P(partials), n_groups, wgpg, fg, F, nbt, slot_lo, slot_cnt,
+                                                    P(ctl_cur), P(built), st), "hist_reduce")
             hist_elems = plan["slot_cnt"] * plan["fg"] * nbt
             partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_elems, torch.int64)
             routed = fuse and d > 0 and self._fused_level(d)
@@ -568,9 +593,7 @@ class HipTreeBuilder:
                             P(ctl_nxt if routed else None), P(nid_buf[d % 2] if routed else None),
                             1 if ps == 0 else 0, st), "hist_build_rm")
                     with T("hist_reduce"):
-                        ops.check(lib.h2omx_hist_reduce(P(partials), 1, plan["wgpg"], F, F, nbt, slot_lo,
-                                                        plan["slot_cnt"], P(ctl_cur), P(built), st),
-                                  "hist_reduce")
+                        reduce(1, plan["wgpg"], F, slot_lo, plan["slot_cnt"])
                 plan = dict(passes=0)
             # level 0 streams every row; deeper levels touch only the built
             # (smaller) children -> wave-compacted kernel keeps atomics dense
@@ -616,15 +639,10 @@ class HipTreeBuilder:
                             P(partials), st),
                             "hist_build")
                 with T("hist_reduce"):
-                    ops.check(lib.h2omx_hist_reduce(P(partials), plan["n_groups"], plan["wgpg"], plan["fg"], F,
-                                                    nbt, slot_lo, plan["slot_cnt"], P(ctl_cur), P(built), st),
-                              "hist_reduce")
+                    reduce(plan["n_groups"], plan["wgpg"], plan["fg"], slot_lo, plan["slot_cnt"])
             if comm is not None:
                 with T("allreduce"):
                     comm.all_reduce_(built[: max_slots * self.per_node])
-            full_cur = None if last else self._buf(f"full{cur}", max_nodes * self.per_node, torch.int64)
-            sp.depth = d
-            sp.children_leaves = 1 if last else 0
             next_nodes = 2 * max_nodes
             part = self._buf("part", max_nodes * PART_INFO_BYTES // 4, torch.int32)
             nl = None
@@ -632,7 +650,6 @@ class HipTreeBuilder:
                 nl = self._buf(f"link{nxt}", next_nodes * NODE_LINK_BYTES // 4, torch.int32)
                 link[nxt] = nl
             nsplit = self._buf("nsplit", max_nodes * 9, torch.float64)  # NodeSplit = 72 B
-            self._cat_level(max_nodes)
             with T("split"):
                 if self.fuse_split:
                     # scan + per-node arg-max + level finalisation in one launch
@@ -643,17 +660,16 @@ class HipTreeBuilder:
                                                     st), "split_level")
                 elif self.SPLIT_FIN and max_nodes <= 64 and self.catf is None:
                     # split scan + per-node arg-max + finalisation: the last block finalises
-                    fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
                     ops.check(lib.h2omx_split_find_fin(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
                                                        P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
                                                        P(fbest), P(self.ticket), P(ctl_nxt), P(bm.edges), next_nodes,
                                                        P(part), P(nl), P(self.tree_buf), self.capacity, P(nsplit),
                                                        st), "split_find_fin")
                 else:
-                    fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
-                    ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
-                                                   P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
-                                                   P(fbest), st), "split_find")
+                    if not rs:
+                        ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur),
+                                                       P(link[cur]), P(bm.nvb), P(tree_fmask), P(self.qscale), spp,
+                                                       max_nodes, nbt, P(fbest), st), "split_find")
                     ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
                                                        P(bm.nvb), nbt, next_nodes, P(part), P(nl),
                                                        P(self.tree_buf), self.capacity, P(nsplit), max_nodes,
@@ -695,9 +711,33 @@ class HipTreeBuilder:
             with T("allreduce"):
                 comm.all_reduce_(self.leaf_acc)
         with T("leaf"):
-            self._leaf_finalize(final_ctl, spp, st)
+            if chain:
+                ops.check(lib.h2omx_leaf_finalize_begin(P(self.leaf_acc), P(final_ctl), P(self.qscale), spp,
+                                                        P(self.tree_buf), self.capacity, P(smax), p.mode,
+                                                        self.max_rows_per_wg, P(self.ctl[0]), P(link[0]),
+                                                        self.row_base, P(self.tree_ctr), st), "leaf_finalize_begin")
+            else:
+                self._leaf_finalize(final_ctl, spp, st)
         self._final_ctl = final_ctl
         return self.tree_buf
+
+    def can_chain(self, fixed: bool) -> bool:
+        """Graph replay may fold tree_begin into the previous tree's leaf
+        finalisation: fixed gradient bounds (the scales do not depend on the
+        boost pass that runs in between), the scan engine, the plain leaf pass
+        (no monotone Newton re-derivation) and a device tree counter."""
+        return (fixed and not self.segmented and self.gbound is None and self.tree_ctr is not None
+                and os.environ.get("H2OMX_CHAIN_BEGIN", "1") == "1")
+
+    def begin(self, smax: torch.Tensor, tree_index: int) -> None:
+        """tree_begin: fixed-point scales, level-0 control block / root link,
+        zeroed leaf sums (and, with a device tree counter, its advance)."""
+        P = ops.P
+        ops.check(self.lib.h2omx_tree_begin(P(smax), self.p.mode, self.max_rows_per_wg, P(self.qscale),
+                                            P(self.ctl[0]), P(self._buf("link0", 4, torch.int32)),
+                                            P(self.leaf_acc), self.leaf_acc.numel(), self.row_base,
+                                            tree_index & 0x7FFFFFFF, P(self.tree_ctr), ops.stream(self.dev)),
+                  "tree_begin")
 
     def _build_seg(self, g, h, w, tree_index, tree_fmask, smax, fixed):
         """Row-partitioned level pipeline (csrc/tree_kernels.hip, "segmented"

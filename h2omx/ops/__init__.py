@@ -25,6 +25,7 @@ TREE_SIGS = {
     "h2omx_hist_build_route": "PLPPPPIPPPIIIIIIIIIPIPS",
     "h2omx_hist_build_grad": "PLPPPIIIIIIIIIPPPPPPIPPIIIPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
+    "h2omx_reduce_split": "PIIIIPPPPPPPPIPS",
     "h2omx_level_finalize": "PPPPPPIIPPPIPIPS",
     "h2omx_split_level": "PPPPPPPPPIIPPPPIPPPIS",
     "h2omx_split_find_fin": "PPPPPPPPPIIPPPPIPPPIPS",
@@ -34,7 +35,7 @@ TREE_SIGS = {
     "h2omx_partition_route": "PLPPPIPPIPS",
     "h2omx_route_level": "PLPPPIPPPPIPPIIPIS",
     "h2omx_leaf_reduce": "PIIPS",
-    "h2omx_boost_update": "PPPLLPPPPPPPS",
+    "h2omx_boost_update": "PPPLLPPPPPPPLPIPIS",
     "h2omx_apply_tree": "PLPPS",
     "h2omx_tree_archive": "PLPIPS",
     "h2omx_sketch_bins": "",
@@ -46,6 +47,7 @@ TREE_SIGS = {
     "h2omx_tree_begin": "PIIPPPPILIPS",
     "h2omx_leaf_stats": "PPPPLPIPS",
     "h2omx_leaf_finalize": "PPPPPIS",
+    "h2omx_leaf_finalize_begin": "PPPPPIPIIPPLPS",
     "h2omx_leaf_finalize_mono": "PPPPPIPS",
     "h2omx_predict_raw": "PLLPPIIPLPS",
     "h2omx_predict_binned": "PLLPPIIIPLPS",

@@ -1,4 +1,6 @@
 """HIP tree kernels vs the NumPy reference implementation of the same algorithm."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -468,12 +470,18 @@ def test_fused_gradient_level_matches_boost_update(cuda_dev, monkeypatch, n, mod
     torch.testing.assert_close(fa, fb, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("dist,depth,min_rows,n", [("bernoulli", 5, 10, 400_000), ("gaussian", 7, 3, 150_000),
-                                                   ("bernoulli", 1, 3, 50_000)])
-def test_graph_replay_matches_eager(cuda_dev, monkeypatch, dist, depth, min_rows, n):
+@pytest.mark.parametrize("dist,depth,min_rows,n,ntrees", [("bernoulli", 5, 10, 400_000, 6),
+                                                          ("gaussian", 7, 3, 150_000, 6),
+                                                          ("bernoulli", 1, 3, 50_000, 6),
+                                                          ("bernoulli", 4, 3, 60_000, 70)])
+def test_graph_replay_matches_eager(cuda_dev, monkeypatch, dist, depth, min_rows, n, ntrees):
     """Each boosting step replayed as one HIP graph (tree index / dither salt
     taken from the device counter) builds bit-identical trees and margins to
-    the eager launch sequence."""
+    the eager launch sequence.  Bernoulli (fixed gradient bounds) replays the
+    chained step (next tree's begin inside the leaf finalisation, the tree
+    archive inside boost_update); even depth puts the final control block in
+    the level-0 slot the chained begin rewrites; 70 trees wrap the 64-slot
+    archive ring."""
     from h2omx.models.tree import boost as B
 
     X, y = _data(n=n, F=11, seed=21, task="bin" if dist == "bernoulli" else "reg")
@@ -491,8 +499,10 @@ def test_graph_replay_matches_eager(cuda_dev, monkeypatch, dist, depth, min_rows
     out = {}
     for flag in ("0", "1"):
         monkeypatch.setenv("H2OMX_TREE_GRAPH", flag)
-        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=6, tparams=tp, seed=5)
+        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=ntrees, tparams=tp, seed=5)
     assert not made[0].graph_used and made[1].graph_used, made[1].graph_error
+    if dist == "bernoulli" and os.environ.get("H2OMX_CHAIN_BEGIN", "1") == "1":
+        assert made[1].graph_chain
     a, b = out["0"], out["1"]
     assert a.trees.shape == b.trees.shape
     for t in range(a.trees.shape[0]):

@@ -133,3 +133,25 @@ def test_laplace_quantile_init_weighted_quantile():
         want = r.numpy()[order][np.searchsorted(cw, q * cw[-1])]
         assert v == want, (q, v, want)
     assert weighted_quantile(r, None, 0.5) == float(np.sort(r.numpy())[10000])
+
+
+def test_weighted_quantile_extreme_ranges_exact():
+    """Bisection on the ordered int64 key of the value: exact for values
+    spanning hundreds of decades, ties and tiny non-zero targets."""
+    import torch
+
+    from h2omx.models.tree.boost import weighted_quantile
+
+    rng = np.random.default_rng(0)
+    for trial in range(200):
+        n = int(rng.integers(1, 40))
+        r = rng.standard_normal(n) * 10.0 ** int(rng.integers(-300, 300))
+        if trial % 3 == 0:
+            r = np.round(r)
+        if trial % 7 == 0:
+            r[0] = 5e-324                       # smallest subnormal
+        w = rng.random(n)
+        q = float(rng.random())
+        v = weighted_quantile(torch.from_numpy(r), torch.from_numpy(w), q)
+        want = min(x for x in np.unique(r) if w[r <= x].sum() >= q * w.sum())
+        assert v == want, (trial, v, want)
