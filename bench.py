@@ -46,15 +46,21 @@ def _sync(torch, dev):
         torch.cuda.synchronize(dev)
 
 
-def _timed(step, args, comm, torch, dev):
+def _timed(step, args, comm, torch, dev, finish=None):
+    """W untimed + K timed steps; ``finish`` (inside both windows) completes
+    work the step function may hold back (multi-tree graph replays)."""
     for _ in range(args.warmup):
         step()
+    if finish is not None:
+        finish()
     _sync(torch, dev)
     comm.barrier()
     _sync(torch, dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if finish is not None:
+        finish()
     _sync(torch, dev)
     comm.barrier()
     _sync(torch, dev)
@@ -118,11 +124,12 @@ def _trees(args, comm, torch, np, model):
         comm.barrier()
         setup_s = time.perf_counter() - t_setup
         comm.collective_stats(reset=True)
-        elapsed = _timed(gb.step, args, comm, torch, dev)
+        elapsed = _timed(gb.step, args, comm, torch, dev, finish=gb.flush)
         coll = comm.collective_stats()
         gb.flush()   # fused mode: the last tree is applied inside the next step's level 0
         margin = gb.st.Fm[0, : bm.n]
         graph_used = gb.graph is not None
+        graph_group = gb.graph.group if gb.graph is not None else 0
     else:
         # CPU rehearsal (reference tree builder): the boosting loop owns the
         # iterations, so the timed window is opened / closed from its callback
@@ -143,7 +150,7 @@ def _trees(args, comm, torch, np, model):
         comm.barrier()
         elapsed = comm.max_scalar(time.perf_counter() - clock["t0"])
         margin = torch.from_numpy(ens._cpu_margin[0])
-        coll, graph_used = comm.collective_stats(), False
+        coll, graph_used, graph_group = comm.collective_stats(), False, 0
     total_rows = int(comm.all_reduce_numpy(np.array([float(n_local)]))[0])
     if args.dump_trees:
         trees = gb.finish().trees if gb is not None else ens.trees
@@ -179,6 +186,7 @@ def _trees(args, comm, torch, np, model):
         "train_auc": auc,
         "setup_s": setup_s,
         "graph_replay": graph_used,
+        "graph_trees_per_replay": graph_group,
         "collectives_per_tree": {"calls": coll["all_reduce_calls"] / max(args.steps, 1),
                                  "bytes": coll["all_reduce_bytes"] / max(args.steps, 1),
                                  "host_us": 1e6 * coll["all_reduce_s"] / max(args.steps, 1)},
@@ -242,6 +250,7 @@ def _instrument(gb, args, comm, torch, dev):
             comm.barrier()
             t0 = time.perf_counter()
             gb.step()
+            gb.flush()     # one step = one single-tree replay here
             ts.append(time.perf_counter() - t0)
             _sync(torch, dev)
         return 1e6 * float(np.median(ts))

@@ -360,6 +360,7 @@ class GpuBooster:
                         torch.zeros((bm.npad,), dtype=torch.float32, device=self.dev))
             self.use_graph = False
         self.pending = False
+        self.deferred: list = []  # graph mode: steps held back for a multi-tree replay
         self._archive = None     # TreeGraph capture: (ring, slots, counter offset)
         # bounded gradients (unweighted rows; bagging only zeroes rows) quantise with
         # the bound scales on every path, fused or not
@@ -373,7 +374,12 @@ class GpuBooster:
 
     def flush(self):
         """Bring the margins up to date (fused mode applies each tree inside the
-        next tree's first level)."""
+        next tree's first level; graph mode may hold steps back to replay them
+        as one multi-tree graph)."""
+        if self.graph is not None and self.deferred:
+            for t in self.deferred:
+                self.graph.replay(t)
+            self.deferred = []
         if self.pending:
             b = self.builder
             ops.check(self.lib.h2omx_apply_tree(ops.P(self.st.Fm[0]), self.bm.n, ops.P(b.nid), ops.P(b.tree_buf),
@@ -427,7 +433,15 @@ class GpuBooster:
         if self.graph is None and self.use_graph and t >= self.t_start + 1:
             self._try_capture()
         if self.graph is not None:
-            self.graph.replay(t)
+            if self.graph.group > 1:
+                # consecutive steps replay as one G-tree graph (no inter-graph gap
+                # between them); readers of the margins / trees flush() first
+                self.deferred.append(t)
+                if len(self.deferred) == self.graph.group:
+                    self.graph.replay_group(self.deferred[0])
+                    self.deferred = []
+            else:
+                self.graph.replay(t)
             self.t += 1
             return
         fmask = _tree_fmask(self.tp, bm.F, t, self.dev)
@@ -594,6 +608,7 @@ class _GpuView:
 
     def trees(self, lo: int, hi: int) -> np.ndarray:
         """Tree records of iterations [lo, hi) (K trees each)."""
+        self.gb.flush()
         K = self.gb.K
         if self.gb.graph is not None:
             self.gb.graph.freeze()
@@ -655,6 +670,7 @@ class TreeGraph:
     # freeze() swaps them for views of one ring snapshot (every RING trees, and
     # whenever the trees are read)
     RING = 64
+    GROUP = 4      # trees per replay of the multi-tree graph (H2OMX_GRAPH_TREES)
 
     def __init__(self, booster):
         self.gb = booster
@@ -666,6 +682,9 @@ class TreeGraph:
         self.live: list = []      # (trees_dev index, ring slot) still pointing into the ring
         self.expect = None        # tree index the device counter holds
         self.chain = False        # tree_begin folded into the previous step (see capture)
+        # chained single-graph steps: GROUP consecutive trees per replay
+        self.group = 1
+        self.graph_g = None
 
     def capture(self):
         gb, b = self.gb, self.gb.builder
@@ -714,6 +733,21 @@ class TreeGraph:
                     self._open.capture_end()
                     self.graphs.append(self._open)
                     self._open = None
+                group = int(os.environ.get("H2OMX_GRAPH_TREES", str(self.GROUP)))
+                if self.chain and not segmented and group > 1:
+                    # the same step G times in one graph: the chained step's only
+                    # state hand-off is on the device (tree counter, scales, leaf sums)
+                    g = torch.cuda.CUDAGraph()
+                    g.capture_begin(pool=self.pool)
+                    gb._archive = (self.ring, self.RING, 2)
+                    try:
+                        for _ in range(group):
+                            gb._body_k1(gb.t, fresh=False, chain=True)
+                            gb._update(apply=True, next_tree=gb.t + 1, k=0)
+                    finally:
+                        gb._archive = None
+                        g.capture_end()
+                    self.graph_g, self.group = g, group
         finally:
             if gc_was:
                 gc.enable()
@@ -748,6 +782,21 @@ class TreeGraph:
         slot = (t & 0x7FFFFFFF) % self.RING
         self.live.append((len(self.gb.trees_dev), slot))
         self.gb.trees_dev.append(self.ring[slot])
+
+    def replay_group(self, t: int):
+        """Grow trees t .. t + group - 1 with one replay of the multi-tree graph."""
+        if self.expect != t:
+            b = self.gb.builder
+            b.tree_ctr.fill_(t & 0x7FFFFFFF)
+            b.begin(self.gb._bounds, t)
+        self.expect = t + self.group
+        if len(self.live) + self.group > self.RING:
+            self.freeze()
+        self.graph_g.replay()
+        for u in range(t, t + self.group):
+            slot = (u & 0x7FFFFFFF) % self.RING
+            self.live.append((len(self.gb.trees_dev), slot))
+            self.gb.trees_dev.append(self.ring[slot])
 
     def freeze(self):
         """Point the trees still living in the ring at one copy of their slots
