@@ -4647,6 +4647,117 @@ __device__ __forceinline__ int direct_eligible(int node, int gid_i, const SplitP
   return nfl < 1024 ? nfl : 1024;
 }
 
+// Data-parallel direct levels (N ranks, row shards): the direct engine split
+// at its reduction point.  direct_dp_hist_kernel builds, per node of the
+// chunk [node0, node0 + gridDim.x), the exact int64 histograms of the node's
+// eligible features (G and S planes) from this rank's rows and writes them
+// with the node totals to dh[slot] = [G_q, S_q, (q, plane, bin)...] (stride
+// 2 + max_elig * 2 * NBT; every slot written, zeros past the node's list), so
+// the caller all-reduces the chunk; direct_dp_scan_kernel then scans the
+// summed histograms exactly like seg_direct (same eligible list, same
+// tie-breaks), so N ranks grow the 1-rank trees bit for bit.
+template <int NBT>
+__global__ __launch_bounds__(256) void direct_dp_hist_kernel(
+    const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
+    const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
+    const int* __restrict__ ctl, const uint8_t* __restrict__ tree_fmask, const double* __restrict__ qscale,
+    SplitParams p, int batch, int node0, int max_elig, long long* __restrict__ dh, int gpos) {
+  extern __shared__ __attribute__((aligned(16))) long long hist[];   // [batch][2][NBT]
+  __shared__ int flist[1024];
+  __shared__ uint32_t hsh_s[1024];
+  __shared__ int nfl_s;
+  __shared__ long long tot_s[2][4];
+  const uint32_t salt = (uint32_t)qscale[9];
+  const int node = node0 + blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int64_t stride = 2 + (int64_t)max_elig * 2 * NBT;
+  long long* out = dh + (int64_t)blockIdx.x * stride;
+  const bool live = node < ctl[CTL_N];
+  if (wid == 0) {
+    const int nfl = live ? direct_eligible(node, ctl[CTL_BASE] + node, p, tree_fmask, flist, hsh_s, lane) : 0;
+    if (lane == 0) nfl_s = min(nfl, max_elig);
+  }
+  if (t < 8) tot_s[t >> 2][t & 3] = 0;
+  __syncthreads();
+  const int nfl = nfl_s;
+  for (int64_t j = 2 + (int64_t)nfl * 2 * NBT + t; j < stride; j += blockDim.x) out[j] = 0;   // unused tail
+  const int lo = live ? seg_start[node] : 0, cnt = live ? seg_cnt[node] : 0;
+  const float sg = (float)qscale[0], ss = (float)qscale[1];
+  const int64_t rb = (int64_t)qscale[7];
+  long long tg_row = 0, ts_row = 0;
+  for (int b0 = 0; b0 < nfl; b0 += batch) {   // (no eligible feature: zero totals, as seg_direct)
+    const int nb = min(batch, nfl - b0);
+    for (int j = t; j < nb * 2 * NBT; j += blockDim.x) hist[j] = 0;
+    __syncthreads();
+    for (int j = lo + t; j < lo + cnt; j += blockDim.x) {
+      const int r = idx ? idx[j] : j;
+      const uint8_t* row = codes_rm + (int64_t)r * fp;
+      uint32_t c0[DIRECT_FB];
+#pragma unroll
+      for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
+      long long gq, sq;
+      direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
+      if (b0 == 0) { tg_row += gq; ts_row += sq; }
+      direct_row_atomics<NBT>(row, flist + b0, nb, false, 2 * NBT, hist, gq, sq, c0, nullptr, 0);
+    }
+    __syncthreads();
+    for (int j = t; j < nb * 2 * NBT; j += blockDim.x) out[2 + (int64_t)b0 * 2 * NBT + j] = hist[j];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    tg_row += __shfl_xor(tg_row, o, kWave);
+    ts_row += __shfl_xor(ts_row, o, kWave);
+  }
+  if (lane == 0) { tot_s[0][wid] = tg_row; tot_s[1][wid] = ts_row; }
+  __syncthreads();
+  if (t == 0) {
+    out[0] = tot_s[0][0] + tot_s[0][1] + tot_s[0][2] + tot_s[0][3];
+    out[1] = tot_s[1][0] + tot_s[1][1] + tot_s[1][2] + tot_s[1][3];
+  }
+}
+
+template <int NBT>
+__global__ __launch_bounds__(256) void direct_dp_scan_kernel(
+    const int* __restrict__ ctl, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
+    const double* __restrict__ qscale, SplitParams p, int node0, int max_elig, const long long* __restrict__ dh,
+    NodeSplit* __restrict__ ns) {
+  __shared__ int flist[1024];
+  __shared__ uint32_t hsh_s[1024];
+  __shared__ int nfl_s;
+  __shared__ double wb_gain[4], wb_GL[4], wb_SL[4];
+  __shared__ long long wb_key[4];
+  const int node = node0 + blockIdx.x;
+  if (node >= ctl[CTL_N]) return;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int64_t stride = 2 + (int64_t)max_elig * 2 * NBT;
+  const long long* h = dh + (int64_t)blockIdx.x * stride;
+  if (wid == 0) {
+    const int nfl = direct_eligible(node, ctl[CTL_BASE] + node, p, tree_fmask, flist, hsh_s, lane);
+    if (lane == 0) nfl_s = min(nfl, max_elig);
+  }
+  __syncthreads();
+  const int nfl = nfl_s;
+  const double ig = qscale[2], is = qscale[3];
+  DirectBest best;
+  best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  for (int q = wid; q < nfl; q += 4) {
+    const int f = flist[q];
+    direct_scan_feature<NBT, false>(h + 2 + (int64_t)q * 2 * NBT, f, nvb[f], ig, is, p, lane, best);
+  }
+  if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
+  __syncthreads();
+  if (t == 0) {
+    DirectBest b;
+    b.gain = -INFINITY; b.GL = b.SL = 0.0; b.key = 0x7fffffffffffffffLL;
+    for (int w = 0; w < 4; ++w)
+      if (wb_key[w] != 0x7fffffffffffffffLL && (wb_gain[w] > b.gain || (wb_gain[w] == b.gain && wb_key[w] < b.key))) {
+        b.gain = wb_gain[w]; b.key = wb_key[w]; b.GL = wb_GL[w]; b.SL = wb_SL[w];
+      }
+    ns[node] = direct_node_split(b, h[0], h[1], ig, is);
+  }
+}
+
 // Direct levels whose nodes still hold thousands of rows (the first direct
 // levels): one workgroup per PC_ROWS row chunk, not per node, so a large node
 // is spread over many workgroups instead of being the kernel's tail.  Each
@@ -5281,6 +5392,45 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
     default: return kBadArg;
   }
 #undef H2OMX_SD
+  return launch_status();
+}
+
+// int64 entries per node of the data-parallel direct histogram buffer
+H2OMX_API long long h2omx_direct_dp_stride(const void* params, int nbt) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  const int max_elig = p.mtries > 0 ? std::min(p.mtries, p.F) : p.F;
+  return 2 + (long long)max_elig * 2 * nbt;
+}
+
+// phase 0: histograms of nodes [node0, node0 + n_chunk) into dh; phase 1: scan them
+H2OMX_API int h2omx_direct_dp(int phase, const uint8_t* codes_rm, int fp, const int* idx, const float* g,
+                              const float* s2, const int* seg_start, const int* seg_cnt, const int* ctl,
+                              const int* nvb, const uint8_t* tree_fmask, const double* qscale, const void* params,
+                              int nbt, int node0, int n_chunk, long long* dh, void* nsplit, int gpos,
+                              hipStream_t stream) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  if (n_chunk < 1 || p.F > 1024 || p.F > fp || nbt < 2 || dh == nullptr) return kBadArg;
+  const int max_elig = p.mtries > 0 ? std::min(p.mtries, p.F) : p.F;
+  const int per_f_bytes = 2 * nbt * 8;
+  const int batch = std::max(1, std::min(max_elig, DIRECT_LDS_BYTES / per_f_bytes));
+  const size_t lds = (size_t)batch * per_f_bytes;
+  NodeSplit* ns = reinterpret_cast<NodeSplit*>(nsplit);
+#define H2OMX_DDP(NB)                                                                                        \
+  if (phase == 0)                                                                                            \
+    hipLaunchKernelGGL(direct_dp_hist_kernel<NB>, dim3(n_chunk), dim3(256), lds, stream, codes_rm, fp, idx,  \
+                       g, s2, seg_start, seg_cnt, ctl, tree_fmask, qscale, p, batch, node0, max_elig, dh,   \
+                       gpos);                                                                                \
+  else                                                                                                       \
+    hipLaunchKernelGGL(direct_dp_scan_kernel<NB>, dim3(n_chunk), dim3(256), 0, stream, ctl, nvb, tree_fmask,  \
+                       qscale, p, node0, max_elig, dh, ns)
+  switch (nbt) {
+    case 32: H2OMX_DDP(32); break;
+    case 64: H2OMX_DDP(64); break;
+    case 128: H2OMX_DDP(128); break;
+    case 256: H2OMX_DDP(256); break;
+    default: return kBadArg;
+  }
+#undef H2OMX_DDP
   return launch_status();
 }
 

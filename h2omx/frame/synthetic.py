@@ -75,6 +75,62 @@ def higgs_like(n: int, seed: int = 42, device="cpu") -> tuple[torch.Tensor, torc
     return X, y
 
 
+def higgs_like_portable(n: int, seed: int = 1) -> tuple[torch.Tensor, torch.Tensor]:
+    """HIGGS-shape binary data that every x86 host generates BIT-identically:
+    NumPy's PCG64 stream (scalar C) and only IEEE-exact operations (+, -, *,
+    /, abs, min / max) in float64, rounded once to float32 - no
+    vectorised transcendental (exp / log / sin) whose last bit depends on the
+    host's SIMD level.  Used by scripts/precision_parity.py, whose GPU part
+    runs on the GPU box and whose fp64-oracle part runs elsewhere: both must
+    bin the same values.  Returns (X [28][n] float32 on the CPU, y [n])."""
+    import numpy as np
+
+    rng = np.random.Generator(np.random.PCG64(seed))
+
+    def unif():
+        return rng.random(n)
+
+    def normal(std=1.0):            # Irwin-Hall: sum of 12 uniforms - 6, added one array at a time
+        s = unif()
+        for _ in range(11):
+            s += unif()
+        return (s - 6.0) * std
+
+    def heavy(scale):               # exponential-like tail without a log: u / (1 - u)
+        u = unif()
+        return np.minimum(u / (1.0 - u + 1e-4), 50.0) * scale
+
+    def angle():
+        return (unif() * 2.0 - 1.0) * 3.141592653589793
+
+    def squash(t):                  # rational sigmoid in (-1, 1)
+        return t / (1.0 + np.abs(t))
+
+    X = np.empty((28, n), np.float64)
+    z = normal()
+    X[0] = heavy(0.8) + 0.25 * (0.5 + 0.5 * squash(z))
+    X[1] = np.clip(normal(), -2.5, 2.5)
+    X[2] = angle()
+    X[3] = heavy(0.9) + 0.15 * np.abs(z)
+    X[4] = angle()
+    for j in range(4):
+        b = 5 + 4 * j
+        X[b] = heavy(0.9 - 0.1 * j) + 0.1 * np.maximum(z, 0.0)
+        X[b + 1] = np.clip(normal(), -2.5, 2.5)
+        X[b + 2] = angle()
+        u = unif()
+        X[b + 3] = np.where(u < 0.55, 0.0, np.where(u < 0.8, 1.0865, 2.173))
+    for k in range(7):
+        t = normal(0.35) + 0.12 * z * (1 + 0.3 * k) - 0.05 * k
+        X[21 + k] = 1.0 + t + 0.5 * t * t          # positive-skewed "mass" around 1
+    dphi = X[2] - X[4]
+    logit = (1.1 * z + 0.8 * squash(X[23] * 2.0 - 2.0) - 0.6 * (X[26] - 1.0) ** 2
+             + 0.175 * (X[8] + X[12]) - 0.3 * np.minimum(np.abs(dphi), 2.0))
+    pr = 0.5 + 0.5 * squash(logit)
+    y = (unif() < pr).astype(np.float32)
+    return torch.from_numpy(X.astype(np.float32)), torch.from_numpy(y)
+
+
 def airlines_like(n: int, seed: int = 7, device="cpu") -> tuple[torch.Tensor, torch.Tensor]:
     """Airlines-shape (31 columns: dates, carrier/origin/dest codes, times,
     distance) synthetic delay classification; categoricals are integer codes."""

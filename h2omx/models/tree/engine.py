@@ -739,6 +739,29 @@ class HipTreeBuilder:
                                             tree_index & 0x7FFFFFFF, P(self.tree_ctr), ops.stream(self.dev)),
                   "tree_begin")
 
+    # data-parallel direct levels: histogram chunk all-reduced per call (bytes)
+    DIRECT_DP = os.environ.get("H2OMX_DIRECT_DP", "1") == "1"
+    DIRECT_DP_CHUNK_BYTES = int(os.environ.get("H2OMX_DIRECT_DP_CHUNK_MB", "64")) << 20
+
+    def _direct_dp(self, comm, idx_in, gs, seg_start, seg_cnt, ctl_cur, tree_fmask, spp, max_nodes, nsplit, st):
+        """Direct level over N row shards: per node chunk, this rank's eligible-
+        feature histograms (h2omx_direct_dp phase 0) -> all-reduce -> the scan
+        (phase 1) writes the nodes' NodeSplit records, identical on every rank."""
+        lib, P, bm = self.lib, ops.P, self.bm
+        stride = int(lib.h2omx_direct_dp_stride(spp, self.nbt))
+        chunk = max(1, min(max_nodes, self.DIRECT_DP_CHUNK_BYTES // (8 * stride)))
+        dh = self._buf("direct_dp", chunk * stride, torch.int64)
+        for node0 in range(0, max_nodes, chunk):
+            nc = min(chunk, max_nodes - node0)
+            for phase in (0, 1):
+                ops.check(lib.h2omx_direct_dp(phase, P(self.codes_rm), bm.fp, P(idx_in), P(gs["g"]), P(gs["s"]),
+                                              P(seg_start), P(seg_cnt), P(ctl_cur), P(bm.nvb), P(tree_fmask),
+                                              P(self.qscale), spp, self.nbt, node0, nc, P(dh), P(nsplit),
+                                              gs["pos"], st), "direct_dp")
+                if phase == 0:
+                    comm.all_reduce_(dh[: nc * stride])
+        self.stats["direct_dp_levels"] = self.stats.get("direct_dp_levels", 0) + 1
+
     def _build_seg(self, g, h, w, tree_index, tree_fmask, smax, fixed):
         """Row-partitioned level pipeline (csrc/tree_kernels.hip, "segmented"
         section): each level reads only the rows of the nodes it builds."""
@@ -849,8 +872,11 @@ class HipTreeBuilder:
         # direct mode pays n x (eligible features) per level; the subtraction path
         # n / 2 x F + nodes x F x bins: direct only for few eligible features (DRF mtries)
         exp_elig = min(p.mtries, F) if p.mtries > 0 else F * min(1.0, p.col_sample_rate)
-        direct_ok = (comm is None and self.DIRECT_MIN_NODES > 0 and F <= 1024
-                     and exp_elig <= self.DIRECT_MAX_ELIG and self.catf is None)
+        # (N ranks: the direct histograms of a node chunk are all-reduced between
+        # the build and the scan, h2omx_direct_dp)
+        direct_ok = (self.DIRECT_MIN_NODES > 0 and F <= 1024
+                     and exp_elig <= self.DIRECT_MAX_ELIG and self.catf is None
+                     and (comm is None or self.DIRECT_DP))
         for d in range(max_depth):
             cur, nxt = d % 2, (d + 1) % 2
             ctl_cur, ctl_nxt = self.ctl[cur], self.ctl[nxt]
@@ -898,11 +924,16 @@ class HipTreeBuilder:
                     ecs = 8 if n_elig <= 8 else 16
                     ec = (B("ecodes", (n + 64) * ecs, torch.uint8), ecs, B("nodeq", max_nodes, i32))
                 ecodes, ecs, nodeq = ec if ec is not None else (None, 0, None)
-                ops.check(lib.h2omx_seg_direct(P(self.codes_rm), bm.fp, P(idx_in), P(gs["g"]), P(gs["s"]),
-                                               P(seg_start), P(seg_cnt), P(ctl_cur), P(bm.nvb), P(tree_fmask),
-                                               P(self.qscale), tree_index & 0x7FFFFFFF, spp, nbt, max_nodes, dmode,
-                                               P(pc_first), max_pc, P(slab), P(tot_slab), P(ticket), P(nsplit),
-                                               gs["pos"], P(ecodes), ecs, P(nodeq), st), "seg_direct")
+                if comm is not None:
+                    self._direct_dp(comm, idx_in, gs, seg_start, seg_cnt, ctl_cur, tree_fmask, spp, max_nodes,
+                                    nsplit, st)
+                    ec = None
+                else:
+                    ops.check(lib.h2omx_seg_direct(P(self.codes_rm), bm.fp, P(idx_in), P(gs["g"]), P(gs["s"]),
+                                                   P(seg_start), P(seg_cnt), P(ctl_cur), P(bm.nvb), P(tree_fmask),
+                                                   P(self.qscale), tree_index & 0x7FFFFFFF, spp, nbt, max_nodes,
+                                                   dmode, P(pc_first), max_pc, P(slab), P(tot_slab), P(ticket),
+                                                   P(nsplit), gs["pos"], P(ecodes), ecs, P(nodeq), st), "seg_direct")
                 ops.check(lib.h2omx_level_finalize_ns(P(nsplit), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
                                                       P(bm.nvb), nbt, next_nodes, P(part), P(nl), P(self.tree_buf),
                                                       self.capacity, max_nodes,

@@ -61,6 +61,8 @@ TREE_SIGS = {
     "h2omx_part_scatter": "PLPPPIPPPPPPPIPPPPIPIIPPPPPPIPS",
     "h2omx_seg_direct": "PIPPPPPPPPPIPIIIPIPPPPIPIPS",
     "h2omx_level_finalize_ns": "PPPPPPIIPPPIIPS",
+    "h2omx_direct_dp_stride": "PI",
+    "h2omx_direct_dp": "IPIPPPPPPPPPPIIIPPIS",
 }
 
 DENSE_SIGS = {
@@ -144,7 +146,9 @@ def _bind(name: str, sigs: dict[str, str]) -> ctypes.CDLL:
 
 
 def tree_lib() -> ctypes.CDLL:
-    return _bind("tree", TREE_SIGS)
+    lib = _bind("tree", TREE_SIGS)
+    lib.h2omx_direct_dp_stride.restype = ctypes.c_int64
+    return lib
 
 
 def dense_lib() -> ctypes.CDLL:

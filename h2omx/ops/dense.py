@@ -334,11 +334,29 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
             check(dense_lib().h2omx_gemm_thin_k(P(A), P(B), P(C), M, N, K, None, 0, stream(A.device)),
                   "gemm_thin_k")
             return C
+    if out is None and _lib_gemm_ok(M, N, K, ta, tb, act, beta_c, bias):
+        # plain fp32 GEMM (+ bias / ReLU epilogue): the vendor library's tuned
+        # kernel (hipBLASLt) - the fused kernels below stay ours
+        Bm = B.t() if tb else B
+        if act == 1:
+            return torch._addmm_activation(bias, A, Bm, use_gelu=False)
+        return torch.addmm(bias, A, Bm) if bias is not None else torch.mm(A, Bm)
     S = _splitk(M, N, K)
     ws = _workspace(A.device, S * M * N) if S > 1 else None
     check(dense_lib().h2omx_gemm(P(A), P(B), P(C), P(bias), M, N, K, int(ta), int(tb), act, beta_c, S, P(ws),
                              stream(A.device)), "gemm")
     return C
+
+
+# fp32 forward GEMMs (act none / ReLU with bias) on hipBLASLt: 8192 x 512 x 512
+# ran 40 us there vs 51.5 us for gemm_w64_kernel (profiles/r3/dl/gemm_variants_r3s8.jsonl)
+LIB_GEMM = os.environ.get("H2OMX_GEMM_LIB", "1")
+LIB_GEMM_MIN_MNK = 1 << 27
+
+
+def _lib_gemm_ok(M, N, K, ta, tb, act, beta_c, bias) -> bool:
+    return (LIB_GEMM == "1" and not ta and beta_c == 0.0 and act in (0, 1) and (act == 0 or bias is not None)
+            and M * N * K >= LIB_GEMM_MIN_MNK and N >= 64 and K >= 64)
 
 
 def set_gemm_tile(tile: int) -> None:

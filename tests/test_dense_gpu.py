@@ -8,6 +8,31 @@ from h2omx.backend import dense as D
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _own_gemm_kernels(monkeypatch):
+    """These tests pin the hand-written GEMM kernels: no hipBLASLt routing."""
+    from h2omx.ops import dense as OD
+
+    monkeypatch.setattr(OD, "LIB_GEMM", "0")
+
+
+def test_library_gemm_route_matches_own_kernel(cuda_dev, monkeypatch):
+    """Plain fp32 forward GEMMs (bias + ReLU) routed to hipBLASLt agree with
+    gemm_w64_kernel to fp32 rounding."""
+    from h2omx.ops import dense as OD
+
+    g = torch.Generator(device="cpu").manual_seed(3)
+    A = torch.randn((4096, 512), generator=g).cuda()
+    W = torch.randn((512, 512), generator=g).cuda() * 0.05
+    b = torch.randn((512,), generator=g).cuda()
+    own = D.gemm(A, W, b, 1, False, True)
+    monkeypatch.setattr(OD, "LIB_GEMM", "1")
+    lib = D.gemm(A, W, b, 1, False, True)
+    ref = torch.relu(A.double() @ W.double().t() + b.double()).float()
+    torch.testing.assert_close(lib, ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(own, ref, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("p,family,link", [(5, "binomial", "logit"), (30, "gaussian", "identity"),
                                            (61, "poisson", "log"), (100, "binomial", "logit"),
                                            (300, "binomial", "logit"), (700, "gaussian", "identity")])
