@@ -430,7 +430,7 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
   if (!build && !route_w) return;
   const int f0 = group * fg;
   const int nf = min(fg, F - f0);
-  static_assert(COP == 1 || ((PKM == 1 || PKM == 3) && !ROUTE && !CMP), "copies: level-0 kernel only");
+  static_assert(COP == 1 || ((PKM == 1 || PKM == 3 || PKM == 6) && !ROUTE && !CMP), "copies: level-0 kernel only");
   const int hist_elems = slot_cnt * fg * NBT;
   const int lane = threadIdx.x & 63;
 
@@ -603,7 +603,8 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
         pk[2 * q] = p2.x;
         pk[2 * q + 1] = p2.y;
       }
-    } else if constexpr (PKM == 4) {
+    } else if constexpr (PKM == 4 || PKM == 6) {
+      // PKM 6 (level 0): the 16-bit packed rows boost_update quantised for this tree
       const uint32_t* pk32 = reinterpret_cast<const uint32_t*>(pk_buf);
 #pragma unroll
       for (int q = 0; q < ROWS / 4; ++q) {
@@ -2725,7 +2726,9 @@ __global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F
                                                            float* __restrict__ wout, unsigned int* __restrict__ stat_max,
                                                            const uint4* __restrict__ arch_src, int arch_n16,
                                                            uint4* __restrict__ ring, int ring_n,
-                                                           const int* __restrict__ tree_ctr, int ctr_off) {
+                                                           const int* __restrict__ tree_ctr, int ctr_off,
+                                                           uint32_t* __restrict__ pk32_out,
+                                                           const double* __restrict__ qs, int s_is_h) {
   if (ring != nullptr) {
     // graph replay: the applied tree also goes to ring slot (tree_ctr - ctr_off)
     // mod ring_n (tree_archive folded into this launch)
@@ -2764,6 +2767,24 @@ __global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F
       hv[k] *= wv[k];
       nn[k] = 0;
       mg = fmaxf(mg, fabsf(gv[k])); mh = fmaxf(mh, hv[k]); mw = fmaxf(mw, wv[k]);
+    }
+    if (pk32_out != nullptr) {
+      // the next tree's level-0 rows, quantised exactly as hist_build does it
+      // (scales and dither salt of that tree: its begin already ran)
+      const float sg = (float)qs[0], ss = (float)qs[1];
+      const uint32_t salt = (uint32_t)qs[9];
+      const int64_t rb = (int64_t)qs[7];
+      uint32_t pw[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t hsh = row_hash(rb + r0 + k, salt);
+        const float d1 = (hsh & 0xFFFF) * (1.0f / 65536.0f), d2 = (hsh >> 16) * (1.0f / 65536.0f);
+        const float sv = s_is_h ? hv[k] : wv[k];
+        const int gq = (int)floorf(fmaf(gv[k], sg, d1));
+        const uint32_t sq = (uint32_t)floorf(fmaf(sv, ss, d2));
+        pw[k] = ((uint32_t)gq << 16) | (sq & 0xFFFFu);
+      }
+      *reinterpret_cast<uint4*>(pk32_out + r0) = make_uint4(pw[0], pw[1], pw[2], pw[3]);
     }
     if (gp.apply_tree) *reinterpret_cast<float4*>(F + r0) = make_float4(fv[0], fv[1], fv[2], fv[3]);
     *reinterpret_cast<float4*>(g + r0) = make_float4(gv[0], gv[1], gv[2], gv[3]);
@@ -3189,14 +3210,16 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
   // pkm bit 4 / 5: level-0 histograms in 8 / 4 interleaved lane copies (PKM 1 / 3 only)
   const int cop = (pkm & 16) ? 8 : ((pkm & 32) ? 4 : 1);
   pkm &= 7;
-  if (cop > 1 && ((pkm != 1 && pkm != 3) || route || cmp)) return kBadArg;
+  if (cop > 1 && ((pkm != 1 && pkm != 3 && pkm != 6) || route || cmp)) return kBadArg;
+  // pkm 6: level 0 reading the packed rows boost_update wrote (implicit root)
+  if (pkm == 6 && (nid != nullptr || route || cmp || pk_buf == nullptr)) return kBadArg;
   if (cmp && ((pkm != 2 && pkm != 4) || rows_per_lane != 16 || slot_cnt > 64)) return kBadArg;
   if (route && (ctl_prev == nullptr || nid_out == nullptr || nid_out == nid || (pkm != 2 && pkm != 4)))
     return kBadArg;
   const PartInfo* pp = reinterpret_cast<const PartInfo*>(part_prev);
   if (wgpg % 8 != 0 || npad % 16 != 0 || fg > 256 || threads % 64 != 0 || threads > 1024 || threads < fg)
     return kBadArg;
-  if (pkm < 0 || pkm > 5 || (pkm > 0 && pk_buf == nullptr) || ((pkm == 2 || pkm == 4) && !route && slot16 == nullptr))
+  if (pkm < 0 || pkm > 6 || (pkm > 0 && pk_buf == nullptr) || ((pkm == 2 || pkm == 4) && !route && slot16 == nullptr))
     return kBadArg;
   // fused gradient level: implicit root (no node ids), 32-bit packed rows, no compaction / routing
   if ((pkm == 5) != (gfp != nullptr) || (pkm == 5 && (nid != nullptr || route || cmp || gfz.F == nullptr ||
@@ -3225,6 +3248,9 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
     else if (pkm == 3 && cop == 8) H2OMX_HBKC(NB, R, 3, 8);        \
     else if (pkm == 1 && cop == 4) H2OMX_HBKC(NB, R, 1, 4);        \
     else if (pkm == 3 && cop == 4) H2OMX_HBKC(NB, R, 3, 4);        \
+    else if (pkm == 6 && cop == 8) H2OMX_HBKC(NB, R, 6, 8);        \
+    else if (pkm == 6 && cop == 4) H2OMX_HBKC(NB, R, 6, 4);        \
+    else if (pkm == 6) H2OMX_HBK(NB, R, 6, false, false);          \
     else if (pkm == 1) H2OMX_HBK(NB, R, 1, false, false);          \
     else if (pkm == 2 && route) H2OMX_HBK(NB, R, 2, true, false);  \
     else if (pkm == 2) H2OMX_HBK(NB, R, 2, false, false);          \
@@ -3652,13 +3678,15 @@ static inline int stream_grid(int64_t) { return STAT_BLOCKS; }
 H2OMX_API int h2omx_boost_update(float* F, const float* y, const float* wobs, int64_t n, int64_t npad, int* nid,
                                  const void* tree, const void* gparams, float* g, float* h, float* wout,
                                  unsigned int* stat_max, int64_t tree_bytes, void* ring, int ring_n,
-                                 const int* tree_ctr, int ctr_off, hipStream_t stream) {
+                                 const int* tree_ctr, int ctr_off, void* pk32_out, const double* qscale,
+                                 int s_is_h, hipStream_t stream) {
   const GradParams gp = *reinterpret_cast<const GradParams*>(gparams);
   if (ring != nullptr && (tree_bytes % 16 != 0 || ring_n < 1 || tree_ctr == nullptr)) return kBadArg;
+  if (pk32_out != nullptr && qscale == nullptr) return kBadArg;
   hipLaunchKernelGGL(boost_update_kernel, dim3(stream_grid(npad)), dim3(256), 0, stream, F, y, wobs, n, npad, nid,
                      reinterpret_cast<const TreeNode*>(tree), gp, g, h, wout, stat_max,
                      reinterpret_cast<const uint4*>(tree), (int)(tree_bytes / 16), reinterpret_cast<uint4*>(ring),
-                     ring_n, tree_ctr, ctr_off);
+                     ring_n, tree_ctr, ctr_off, reinterpret_cast<uint32_t*>(pk32_out), qscale, s_is_h);
   return launch_status();
 }
 

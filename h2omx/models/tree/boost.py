@@ -386,7 +386,7 @@ class GpuBooster:
                                                 ops.stream(self.dev)), "apply_tree")
             self.pending = False
 
-    def _update(self, apply: bool, next_tree: int, k: int, dist=None):
+    def _update(self, apply: bool, next_tree: int, k: int, dist=None, pack: bool = False):
         P, st, b = ops.P, self.st, self.builder
         gp = make_grad_params(dist or self.dist, apply, self.sample_rate, self.seed, next_tree,
                               row_base=self.builder.row_base, **self.kw)
@@ -397,12 +397,14 @@ class GpuBooster:
         fixed = self._bounds is not None and k == 0 and self.K == 1
         with b.timer.phase("grad"):
             arch = self._archive    # (ring, slots, counter offset): graph replay's tree archive
+            pk = b.pk if (pack or (arch is not None and b.pk_in_boost)) else None
             ops.check(self.lib.h2omx_boost_update(P(st.Fm[k]), P(y), P(st.w), self.bm.n, self.bm.npad, P(b.nid),
                                                   P(b.tree_buf), ctypes.addressof(gp), P(st.g[k]), P(st.h[k]),
                                                   P(self.wout), P(None if fixed else b.stat_slab),
                                                   b.tree_buf.numel(), P(arch[0] if arch else None),
                                                   arch[1] if arch else 0, P(b.tree_ctr if arch else None),
-                                                  arch[2] if arch else 0, ops.stream(self.dev)),
+                                                  arch[2] if arch else 0, P(pk), P(b.qscale if pk is not None else None),
+                                                  1 if b.p.mode == 1 else 0, ops.stream(self.dev)),
                       "boost_update")
             if not fixed:
                 b.reduce_stats()
@@ -714,6 +716,7 @@ class TreeGraph:
         # (fixed gradient bounds), the tree archive inside boost_update: the
         # replayed step is levels -> leaf_finalize(+begin) -> boost_update(+archive)
         self.chain = b.can_chain(gb._bounds is not None)
+        b.pk_in_boost = self.chain and b.can_pack_in_boost()
         try:
             with torch.cuda.stream(side):
                 g = torch.cuda.CUDAGraph()
@@ -770,7 +773,7 @@ class TreeGraph:
             b = self.gb.builder
             b.tree_ctr.fill_(t & 0x7FFFFFFF)
             if self.chain:     # the graph starts at level 0: begin this tree here
-                b.begin(self.gb._bounds, t)
+                self._begin_eager(t)
         self.expect = t + 1
         if len(self.live) >= self.RING:
             self.freeze()
@@ -783,12 +786,20 @@ class TreeGraph:
         self.live.append((len(self.gb.trees_dev), slot))
         self.gb.trees_dev.append(self.ring[slot])
 
+    def _begin_eager(self, t: int):
+        """Out of step (first replay, or after eager steps): begin tree t here and,
+        when level 0 reads boost_update's packed rows, re-derive them from the
+        current margins (same gradients, this tree's scales and dither salt)."""
+        gb, b = self.gb, self.gb.builder
+        b.begin(gb._bounds, t)
+        if b.pk_in_boost:
+            gb._update(apply=False, next_tree=t, k=0, pack=True)
+
     def replay_group(self, t: int):
         """Grow trees t .. t + group - 1 with one replay of the multi-tree graph."""
         if self.expect != t:
-            b = self.gb.builder
-            b.tree_ctr.fill_(t & 0x7FFFFFFF)
-            b.begin(self.gb._bounds, t)
+            self.gb.builder.tree_ctr.fill_(t & 0x7FFFFFFF)
+            self._begin_eager(t)
         self.expect = t + self.group
         if len(self.live) + self.group > self.RING:
             self.freeze()

@@ -526,6 +526,9 @@ class HipTreeBuilder:
         if not chain:
             with T("tree_begin"):
                 self.begin(smax, tree_index)
+        # level 0 reads the packed rows the previous step's boost_update quantised
+        # for this tree (chained graph steps, see can_pack_in_boost)
+        pk_boost = chain and self.pk_in_boost
         full_prev = None
         max_depth = p.max_depth
         final_ctl = self.ctl[max_depth % 2]
@@ -635,7 +638,9 @@ class HipTreeBuilder:
                             P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, plan["fg"], plan["n_groups"],
                             plan["wgpg"], slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],
                             P(self.slot16), P(self.pk),
-                            (1 if d == 0 else 2 + cmp_flag) + (2 if self.pk32 else 0) + ({8: 16, 4: 32}.get(self.L0_COPIES, 0) if l0_copies else 0),
+                            ((6 if pk_boost else 1 + (2 if self.pk32 else 0)) if d == 0
+                             else 2 + cmp_flag + (2 if self.pk32 else 0))
+                            + ({8: 16, 4: 32}.get(self.L0_COPIES, 0) if l0_copies else 0),
                             P(partials), st),
                             "hist_build")
                 with T("hist_reduce"):
@@ -729,6 +734,16 @@ class HipTreeBuilder:
         return (fixed and not self.segmented and self.gbound is None and self.tree_ctr is not None
                 and os.environ.get("H2OMX_CHAIN_BEGIN", "1") == "1")
 
+    # chained graph steps: boost_update also writes the next tree's 16-bit packed
+    # level-0 rows, so level 0 reads 4 bytes per row and feature group instead of
+    # (g, s2) = 8 bytes (4 groups at level 0: ~220 MB less traffic at 11M rows)
+    PK_IN_BOOST = os.environ.get("H2OMX_PK_IN_BOOST", "1") == "1"
+    pk_in_boost = False
+
+    def can_pack_in_boost(self) -> bool:
+        return (self.PK_IN_BOOST and self.pk32 and self.implicit_root and not self.segmented and not self.COMPACT
+                and self.L0_COPIES in (1, 4, 8))
+
     def begin(self, smax: torch.Tensor, tree_index: int) -> None:
         """tree_begin: fixed-point scales, level-0 control block / root link,
         zeroed leaf sums (and, with a device tree counter, its advance)."""
@@ -739,6 +754,9 @@ class HipTreeBuilder:
                                             tree_index & 0x7FFFFFFF, P(self.tree_ctr), ops.stream(self.dev)),
                   "tree_begin")
 
+    # timing experiment only (wrong trees): direct levels read code rows in
+    # segment order as if the rows had been moved with their segments
+    DBG_SEQ_ROWS = os.environ.get("H2OMX_DBG_SEQ_ROWS", "0") == "1"
     # data-parallel direct levels: histogram chunk all-reduced per call (bytes)
     DIRECT_DP = os.environ.get("H2OMX_DIRECT_DP", "1") == "1"
     DIRECT_DP_CHUNK_BYTES = int(os.environ.get("H2OMX_DIRECT_DP_CHUNK_MB", "64")) << 20
@@ -929,7 +947,8 @@ class HipTreeBuilder:
                                     nsplit, st)
                     ec = None
                 else:
-                    ops.check(lib.h2omx_seg_direct(P(self.codes_rm), bm.fp, P(idx_in), P(gs["g"]), P(gs["s"]),
+                    ops.check(lib.h2omx_seg_direct(P(self.codes_rm), bm.fp,
+                                                   P(None if self.DBG_SEQ_ROWS else idx_in), P(gs["g"]), P(gs["s"]),
                                                    P(seg_start), P(seg_cnt), P(ctl_cur), P(bm.nvb), P(tree_fmask),
                                                    P(self.qscale), tree_index & 0x7FFFFFFF, spp, nbt, max_nodes,
                                                    dmode, P(pc_first), max_pc, P(slab), P(tot_slab), P(ticket),

@@ -35,7 +35,7 @@ TREE_SIGS = {
     "h2omx_partition_route": "PLPPPIPPIPS",
     "h2omx_route_level": "PLPPPIPPPPIPPIIPIS",
     "h2omx_leaf_reduce": "PIIPS",
-    "h2omx_boost_update": "PPPLLPPPPPPPLPIPIS",
+    "h2omx_boost_update": "PPPLLPPPPPPPLPIPIPPIS",
     "h2omx_apply_tree": "PLPPS",
     "h2omx_tree_archive": "PLPIPS",
     "h2omx_sketch_bins": "",

@@ -334,6 +334,19 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
             check(dense_lib().h2omx_gemm_thin_k(P(A), P(B), P(C), M, N, K, None, 0, stream(A.device)),
                   "gemm_thin_k")
             return C
+    if _lib_small_ok(M, N, K, act, beta_c, bias):
+        # small mini-batch GEMMs on hipBLASLt: no split-K reduce launch
+        Am = A.t() if ta else A
+        Bm = B.t() if tb else B
+        if act == 1:
+            r = torch._addmm_activation(bias, Am, Bm, use_gelu=False)
+            if out is None:
+                return r
+            C.copy_(r)
+            return C
+        if bias is not None:
+            return torch.addmm(bias, Am, Bm, out=C)
+        return torch.mm(Am, Bm, out=C)
     if out is None and _lib_gemm_ok(M, N, K, ta, tb, act, beta_c, bias):
         # plain fp32 GEMM (+ bias / ReLU epilogue): the vendor library's tuned
         # kernel (hipBLASLt) - the fused kernels below stay ours
@@ -352,6 +365,17 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
 # ran 40 us there vs 51.5 us for gemm_w64_kernel (profiles/r3/dl/gemm_variants_r3s8.jsonl)
 LIB_GEMM = os.environ.get("H2OMX_GEMM_LIB", "1")
 LIB_GEMM_MIN_MNK = 1 << 27
+
+
+# small mini-batch GEMMs (M N K < LIB_GEMM_MIN_MNK, e.g. the estimator's 256-row
+# batches) on hipBLASLt instead of split-K + reduce launches: estimator-default
+# DL 1.22 -> 1.50 M samples/s (profiles/r4/dl/estimator_small_gemm_ab.txt)
+LIB_GEMM_SMALL = os.environ.get("H2OMX_GEMM_LIB_SMALL", "1")
+
+
+def _lib_small_ok(M, N, K, act, beta_c, bias) -> bool:
+    return (LIB_GEMM_SMALL == "1" and beta_c == 0.0 and act in (0, 1) and (act == 0 or bias is not None)
+            and M * N * K < LIB_GEMM_MIN_MNK and min(M, N, K) >= 64)
 
 
 def _lib_gemm_ok(M, N, K, ta, tb, act, beta_c, bias) -> bool:
@@ -495,7 +519,7 @@ def wgrad_bias(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Te
     N = H.shape[1]
     S = _splitk(M, N, K)
     bws, bsplits = bpart
-    if S < 2:
+    if S < 2 or _lib_small_ok(M, N, K, 0, 0.0, None):
         gemm(dZ, H, ta=True, out=dW)
         tmp = torch.empty((M,), dtype=torch.float64, device=dZ.device)
         check(dense_lib().h2omx_slab_sum(P(bws), bsplits, M, P(tmp), stream(dZ.device)), "slab_sum")

@@ -122,7 +122,9 @@ def main():
         torch.cuda.synchronize()
         t_gpu = time.time() - t
         m = ens._state.Fm[0, : a.rows].double().cpu().numpy()
-        np.save(os.path.join(a.out, "margin_gpu.npy"), m.astype(np.float32))
+        if a.rows <= 2_000_000:   # (11M margins: 44 MB; compare re-applies the trees instead)
+            np.save(os.path.join(a.out, "margin_gpu.npy"), m.astype(np.float32))
+        np.save(os.path.join(a.out, "init_f.npy"), np.asarray(ens.init_f, np.float64))
         np.save(os.path.join(a.out, "trees_gpu.npy"), ens.trees)
         out = {"rows": a.rows, "trees": a.trees, "data": a.data, "auc_gpu_fixed_point": _auc(m, yn),
                "fit_s_gpu": t_gpu, "hashes_gpu_box": hashes}
@@ -132,9 +134,21 @@ def main():
         c = json.load(open(os.path.join(a.out, "cpu.json")))
         g = json.load(open(os.path.join(a.gpu, "gpu.json")))
         mr = np.load(os.path.join(a.out, "margin_ref.npy")).astype(np.float64)
-        mg = np.load(os.path.join(a.gpu, "margin_gpu.npy")).astype(np.float64)
         tr = np.load(os.path.join(a.out, "trees_ref.npy"))
         tg = np.load(os.path.join(a.gpu, "trees_gpu.npy"))
+        mpath = os.path.join(a.gpu, "margin_gpu.npy")
+        if os.path.exists(mpath):
+            mg = np.load(mpath).astype(np.float64)
+        else:
+            # GPU margins = init + every GPU tree applied through its thresholds
+            # (training routing == threshold routing on the device, route_check)
+            from h2omx.reference.tree import predict_tree_numpy
+
+            X, _, _, _ = _data(c["rows"], a.seed, c.get("data", "portable"))
+            Xn = X.numpy()
+            mg = np.full(c["rows"], float(np.load(os.path.join(a.gpu, "init_f.npy"))[0]), np.float64)
+            for t in range(tg.shape[0]):
+                mg += predict_tree_numpy(tg[t], Xn)
         # every field of every reachable node: split feature / bin, NA
         # direction, raw threshold, child ids, leaf values
         same_tree, first_diff, nodes, diff = 0, None, 0, {"feat": 0, "bin": 0, "na_left": 0, "thr": 0, "left": 0}

@@ -14,6 +14,7 @@ def _own_gemm_kernels(monkeypatch):
     from h2omx.ops import dense as OD
 
     monkeypatch.setattr(OD, "LIB_GEMM", "0")
+    monkeypatch.setattr(OD, "LIB_GEMM_SMALL", "0")
 
 
 def test_library_gemm_route_matches_own_kernel(cuda_dev, monkeypatch):
