@@ -2329,7 +2329,9 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
                                                         unsigned long long* __restrict__ leaf_acc,
                                                         const int* __restrict__ ctl_cur,
                                                         const int* __restrict__ ctl_next, int win_max, int R,
-                                                        short* __restrict__ slot16, int* nid_out, int all_rows) {
+                                                        short* __restrict__ slot16, int* nid_out, int all_rows,
+                                                        const float* __restrict__ Fm, const float* __restrict__ yv,
+                                                        GradParams gp) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lacc[];
   __shared__ PartInfo ps[PART_LDS_NODES];
   const bool use_lds = leaf_acc != nullptr && win_max > 0;
@@ -2368,10 +2370,20 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
     if (PREF) {
 #pragma unroll
       for (int v = 0; v < RPL / 4; ++v) {
-        const float4 g0 = *reinterpret_cast<const float4*>(g + r0 + 4 * v);
-        const float4 h0 = *reinterpret_cast<const float4*>(h + r0 + 4 * v);
-        gv[4 * v] = g0.x; gv[4 * v + 1] = g0.y; gv[4 * v + 2] = g0.z; gv[4 * v + 3] = g0.w;
-        hv[4 * v] = h0.x; hv[4 * v + 1] = h0.y; hv[4 * v + 2] = h0.z; hv[4 * v + 3] = h0.w;
+        if (Fm != nullptr) {
+          // chained graph steps: boost_update no longer stores (g, h); re-derive
+          // them from the margins / labels exactly as it did (unweighted rows)
+          const float4 f0 = *reinterpret_cast<const float4*>(Fm + r0 + 4 * v);
+          const float4 y0 = *reinterpret_cast<const float4*>(yv + r0 + 4 * v);
+          const float fa[4] = {f0.x, f0.y, f0.z, f0.w}, ya[4] = {y0.x, y0.y, y0.z, y0.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) dist_grad(gp.dist, fa[k], ya[k], gp, gv[4 * v + k], hv[4 * v + k]);
+        } else {
+          const float4 g0 = *reinterpret_cast<const float4*>(g + r0 + 4 * v);
+          const float4 h0 = *reinterpret_cast<const float4*>(h + r0 + 4 * v);
+          gv[4 * v] = g0.x; gv[4 * v + 1] = g0.y; gv[4 * v + 2] = g0.z; gv[4 * v + 3] = g0.w;
+          hv[4 * v] = h0.x; hv[4 * v + 1] = h0.y; hv[4 * v + 2] = h0.z; hv[4 * v + 3] = h0.w;
+        }
         if (w) {
           const float4 w0 = *reinterpret_cast<const float4*>(w + r0 + 4 * v);
           wv8[4 * v] = w0.x; wv8[4 * v + 1] = w0.y; wv8[4 * v + 2] = w0.z; wv8[4 * v + 3] = w0.w;
@@ -2728,7 +2740,7 @@ __global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F
                                                            uint4* __restrict__ ring, int ring_n,
                                                            const int* __restrict__ tree_ctr, int ctr_off,
                                                            uint32_t* __restrict__ pk32_out,
-                                                           const double* __restrict__ qs, int s_is_h) {
+                                                           const double* __restrict__ qs, int s_is_h, int store_gh) {
   if (ring != nullptr) {
     // graph replay: the applied tree also goes to ring slot (tree_ctr - ctr_off)
     // mod ring_n (tree_archive folded into this launch)
@@ -2787,8 +2799,10 @@ __global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F
       *reinterpret_cast<uint4*>(pk32_out + r0) = make_uint4(pw[0], pw[1], pw[2], pw[3]);
     }
     if (gp.apply_tree) *reinterpret_cast<float4*>(F + r0) = make_float4(fv[0], fv[1], fv[2], fv[3]);
-    *reinterpret_cast<float4*>(g + r0) = make_float4(gv[0], gv[1], gv[2], gv[3]);
-    *reinterpret_cast<float4*>(h + r0) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+    if (store_gh) {   // (chained graph steps: the final partition re-derives them)
+      *reinterpret_cast<float4*>(g + r0) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+      *reinterpret_cast<float4*>(h + r0) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+    }
     if (wout) *reinterpret_cast<float4*>(wout + r0) = make_float4(wv[0], wv[1], wv[2], wv[3]);
     if (!gp.skip_nid) *reinterpret_cast<int4*>(nid + r0) = make_int4(nn[0], nn[1], nn[2], nn[3]);
   }
@@ -3589,7 +3603,12 @@ static void part_env_once() {
 static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt, const float* g,
                             const float* h, const float* w, const double* qscale, int cap,
                             unsigned long long* leaf_acc, const int* ctl_cur, const int* ctl_next, int win_max,
-                            int blocks, int prefetch, short* slot16, int* nid_out, int all_rows, hipStream_t stream) {
+                            int blocks, int prefetch, short* slot16, int* nid_out, int all_rows, hipStream_t stream,
+                            const float* Fm = nullptr, const float* yv = nullptr, const GradParams* gpp = nullptr) {
+  GradParams gp{};
+  if (gpp) gp = *gpp;
+  if ((Fm != nullptr) != (gpp != nullptr) || (Fm != nullptr && (yv == nullptr || w != nullptr || !prefetch)))
+    return kBadArg;
   if (slot16 && prefetch) return kBadArg;
   part_env_once();
   if (npad % PART_RPL != 0 || blocks < 1 || blocks > PARTITION_BLOCKS || win_max < 0) return kBadArg;
@@ -3606,11 +3625,11 @@ static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const 
   if (prefetch && leaf_acc)
     hipLaunchKernelGGL((partition_kernel<true, PART_RPL>), dim3(blocks), dim3(256), lds, stream, codes, npad, nid,
                        reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
-                       ctl_next, win_max, R, slot16, nid_out, all_rows);
+                       ctl_next, win_max, R, slot16, nid_out, all_rows, Fm, yv, gp);
   else
     hipLaunchKernelGGL((partition_kernel<false, PART_RPL>), dim3(blocks), dim3(256), lds, stream, codes, npad, nid,
                        reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
-                       ctl_next, leaf_acc ? win_max : 0, R, slot16, nid_out, all_rows);
+                       ctl_next, leaf_acc ? win_max : 0, R, slot16, nid_out, all_rows, Fm, yv, gp);
   return launch_status();
 }
 
@@ -3639,9 +3658,12 @@ H2OMX_API int h2omx_partition_route(const uint8_t* codes, int64_t npad, const in
 H2OMX_API int h2omx_partition_final(const uint8_t* codes, int64_t npad, const int* nid_in, int* nid_out,
                                     const void* part, int nbt, const float* g, const float* h, const float* w,
                                     const double* qscale, int cap, unsigned long long* leaf_acc, const int* ctl_cur,
-                                    const int* ctl_next, int blocks, hipStream_t stream) {
+                                    const int* ctl_next, int blocks, const float* Fm, const float* y,
+                                    const void* gparams, hipStream_t stream) {
+  // Fm / y / gparams (optional): the rows' (g, h) are re-derived from the margins
   return partition_launch(codes, npad, const_cast<int*>(nid_in), part, nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
-                          ctl_next, cap, blocks, 1, nullptr, nid_out, 1, stream);
+                          ctl_next, cap, blocks, 1, nullptr, nid_out, 1, stream, Fm, y,
+                          reinterpret_cast<const GradParams*>(gparams));
 }
 
 // route_kernel entry (fused pipeline): final = 1 -> last level (leaf sums of
@@ -3679,14 +3701,14 @@ H2OMX_API int h2omx_boost_update(float* F, const float* y, const float* wobs, in
                                  const void* tree, const void* gparams, float* g, float* h, float* wout,
                                  unsigned int* stat_max, int64_t tree_bytes, void* ring, int ring_n,
                                  const int* tree_ctr, int ctr_off, void* pk32_out, const double* qscale,
-                                 int s_is_h, hipStream_t stream) {
+                                 int s_is_h, int store_gh, hipStream_t stream) {
   const GradParams gp = *reinterpret_cast<const GradParams*>(gparams);
   if (ring != nullptr && (tree_bytes % 16 != 0 || ring_n < 1 || tree_ctr == nullptr)) return kBadArg;
   if (pk32_out != nullptr && qscale == nullptr) return kBadArg;
   hipLaunchKernelGGL(boost_update_kernel, dim3(stream_grid(npad)), dim3(256), 0, stream, F, y, wobs, n, npad, nid,
                      reinterpret_cast<const TreeNode*>(tree), gp, g, h, wout, stat_max,
                      reinterpret_cast<const uint4*>(tree), (int)(tree_bytes / 16), reinterpret_cast<uint4*>(ring),
-                     ring_n, tree_ctr, ctr_off, reinterpret_cast<uint32_t*>(pk32_out), qscale, s_is_h);
+                     ring_n, tree_ctr, ctr_off, reinterpret_cast<uint32_t*>(pk32_out), qscale, s_is_h, store_gh);
   return launch_status();
 }
 
@@ -3892,7 +3914,7 @@ __global__ __launch_bounds__(512) void hist_build_seg_kernel(
     const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
     const int* __restrict__ hc_first, const int* __restrict__ ctl, const int* __restrict__ nvb,
     const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups, int hc_rows,
-    unsigned long long* __restrict__ slab, int gpos) {
+    unsigned long long* __restrict__ slab, int gpos, const uint8_t* __restrict__ crow) {
   salt = (uint32_t)qscale[9];  // per-tree dither salt, written by tree_begin (graph-replay safe)
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
   __shared__ int width_s[256], rep_s[256];
@@ -3937,7 +3959,7 @@ __global__ __launch_bounds__(512) void hist_build_seg_kernel(
     const uint32_t sq = (uint32_t)floorf(fmaf(sv, ss, d2));
     const unsigned long long pk = ((unsigned long long)(uint32_t)gq << 32) | (unsigned long long)sq;
     if (pk == 0ull) continue;
-    const uint32_t* row = reinterpret_cast<const uint32_t*>(codes_rm + (int64_t)r * fp + f0);
+    const uint32_t* row = reinterpret_cast<const uint32_t*>((crow ? crow + (int64_t)j * fp : codes_rm + (int64_t)r * fp) + f0);
     for (int wq = 0; wq < nw; ++wq) {
       const uint32_t cw = row[wq];
 #pragma unroll
@@ -4002,13 +4024,39 @@ __device__ __forceinline__ int split_dir(const uint8_t* __restrict__ codes, int6
   return part_right(pi, b, nbt);
 }
 
+// Row-major code rows kept in segment order (segmented engine, H2OMX_MOVE_ROWS):
+// in = this level's rows by segment position j (nullptr: gather codes_rm by row
+// id), out = the next level's (part_scatter moves every inner row's fp bytes
+// with it), so deep levels read their nodes' rows contiguously instead of one
+// random cache line per row
+struct SegRows {
+  const uint8_t* in;
+  uint8_t* out;
+  int fp;
+};
+
+// copy row r's (segment position j) fp code bytes to segment position dst of sr.out
+__device__ __forceinline__ void seg_move_row(const SegRows& sr, const uint8_t* __restrict__ codes_rm, int r, int j,
+                                             int dst) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(sr.in ? sr.in + (int64_t)j * sr.fp
+                                                                : codes_rm + (int64_t)r * sr.fp);
+  uint32_t* d = reinterpret_cast<uint32_t*>(sr.out + (int64_t)dst * sr.fp);
+  for (int q = 0; q < (sr.fp >> 2); ++q) d[q] = src[q];
+}
+
+__device__ __forceinline__ int seg_split_dir(const uint8_t* __restrict__ codes, int64_t npad, const PartInfo& pi,
+                                             int nbt, int r, int j, const SegRows& sr) {
+  if (sr.in != nullptr) return part_right(pi, sr.in[(int64_t)j * sr.fp + pi.feat], nbt);
+  return split_dir(codes, npad, pi, nbt, r);
+}
+
 // number of rows of chunk c going left (nodes that split into inner nodes)
 __global__ __launch_bounds__(256) void part_count_kernel(const uint8_t* __restrict__ codes, int64_t npad,
                                                          const int* __restrict__ idx, const int* __restrict__ seg_start,
                                                          const int* __restrict__ seg_cnt,
                                                          const int* __restrict__ pc_first, const int* __restrict__ ctl,
                                                          const PartInfo* __restrict__ part, int nbt,
-                                                         int* __restrict__ pc_left) {
+                                                         int* __restrict__ pc_left, SegRows sr) {
   __shared__ int red[4];
   const int n = ctl[CTL_N];
   const int c = blockIdx.x;
@@ -4021,7 +4069,7 @@ __global__ __launch_bounds__(256) void part_count_kernel(const uint8_t* __restri
     const int hi = min(lo + PC_ROWS, seg_start[node] + seg_cnt[node]);
     for (int j = lo + threadIdx.x; j < hi; j += blockDim.x) {
       const int r = idx ? idx[j] : j;
-      cnt += 1 - split_dir(codes, npad, pi, nbt, r);
+      cnt += 1 - seg_split_dir(codes, npad, pi, nbt, r, j, sr);
     }
   }
   cnt = (int)wave_sum((float)cnt);
@@ -4405,6 +4453,7 @@ struct ECodes {
   uint8_t* codes;   // nullptr = off; the host enables it only when the node's features fit one batch
   int stride;       // 8 or 16 bytes per row
   int* nodeq;
+  const uint8_t* crow;   // code rows in segment order (SegRows::in), nullptr = gather codes_rm by row id
 };
 
 template <typename FL>
@@ -4544,7 +4593,7 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
     __syncthreads();
     for (int j = lo + t; j < lo + cnt; j += blockDim.x) {
       const int r = idx ? idx[j] : j;
-      const uint8_t* row = codes_rm + (int64_t)r * fp;
+      const uint8_t* row = ec.crow ? ec.crow + (int64_t)j * fp : codes_rm + (int64_t)r * fp;
       uint32_t c0[DIRECT_FB];
 #pragma unroll
       for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
@@ -4689,8 +4738,10 @@ __global__ __launch_bounds__(256) void direct_dp_hist_kernel(
     const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
     const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
     const int* __restrict__ ctl, const uint8_t* __restrict__ tree_fmask, const double* __restrict__ qscale,
-    SplitParams p, int batch, int node0, int max_elig, long long* __restrict__ dh, int gpos) {
+    SplitParams p, int batch, int node0, int max_elig, long long* __restrict__ dh, int gpos,
+    const uint8_t* __restrict__ crow) {
   extern __shared__ __attribute__((aligned(16))) long long hist[];   // [batch][2][NBT]
+  const ECodes ec{nullptr, 0, nullptr, crow};
   __shared__ int flist[1024];
   __shared__ uint32_t hsh_s[1024];
   __shared__ int nfl_s;
@@ -4719,7 +4770,7 @@ __global__ __launch_bounds__(256) void direct_dp_hist_kernel(
     __syncthreads();
     for (int j = lo + t; j < lo + cnt; j += blockDim.x) {
       const int r = idx ? idx[j] : j;
-      const uint8_t* row = codes_rm + (int64_t)r * fp;
+      const uint8_t* row = ec.crow ? ec.crow + (int64_t)j * fp : codes_rm + (int64_t)r * fp;
       uint32_t c0[DIRECT_FB];
 #pragma unroll
       for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
@@ -4843,7 +4894,7 @@ __global__ __launch_bounds__(256) void seg_direct_chunk_kernel(
   long long tg_row = 0, ts_row = 0;
   for (int j = lo + t; j < hi; j += blockDim.x) {
     const int r = idx ? idx[j] : j;
-    const uint8_t* row = codes_rm + (int64_t)r * fp;
+    const uint8_t* row = ec.crow ? ec.crow + (int64_t)j * fp : codes_rm + (int64_t)r * fp;
     uint32_t cc[DIRECT_FB];
 #pragma unroll
     for (int u = 0; u < DIRECT_FB; ++u) cc[u] = (u < nfl) ? row[flist[u]] : 0u;
@@ -4999,7 +5050,7 @@ __global__ __launch_bounds__(256) void seg_direct_wave_kernel(
     wave_lds_sync();
     for (int j = lo + lane; j < lo + cnt; j += 64) {
       const int r = idx ? idx[j] : j;
-      const uint8_t* row = codes_rm + (int64_t)r * fp;
+      const uint8_t* row = ec.crow ? ec.crow + (int64_t)j * fp : codes_rm + (int64_t)r * fp;
       uint32_t c0[DIRECT_FB];
 #pragma unroll
       for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
@@ -5055,7 +5106,7 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
     const int* __restrict__ ctl, const PartInfo* __restrict__ part, int nbt, const float* __restrict__ g,
     const float* __restrict__ h, const float* __restrict__ w, const double* __restrict__ qs, int cap,
     unsigned long long* __restrict__ leaf_acc, const float* __restrict__ gin, const float* __restrict__ sin,
-    float* __restrict__ gout, float* __restrict__ sout) {
+    float* __restrict__ gout, float* __restrict__ sout, SegRows sr, const uint8_t* __restrict__ codes_rm) {
   __shared__ int wl[4];
   __shared__ long long red[4];
   const int n = ctl[CTL_N];
@@ -5081,7 +5132,7 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
     int r = 0, dir = 0;
     if (valid) {
       r = idx ? idx[j] : j;
-      if (pi.child >= 0) dir = split_dir(codes, npad, pi, nbt, r);
+      if (pi.child >= 0) dir = seg_split_dir(codes, npad, pi, nbt, r, j, sr);
     }
     if (inner) {
       const bool goes_left = valid && dir == 0;
@@ -5106,6 +5157,7 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
           gout[start + pos] = gin[j];
           if (sout) sout[start + pos] = sin[j];
         }
+        if (sr.out) seg_move_row(sr, codes_rm, r, j, start + pos);
       }
       base_l += tot_l;
       base_r += tot_v - tot_l;
@@ -5157,7 +5209,7 @@ __global__ __launch_bounds__(256) void part_count_wave_kernel(const uint8_t* __r
                                                               const PartInfo* __restrict__ part, int nbt,
                                                               int* __restrict__ pc_left, int8_t* __restrict__ dirb,
                                                               const uint8_t* __restrict__ ecodes, int ecs,
-                                                              const int* __restrict__ nodeq) {
+                                                              const int* __restrict__ nodeq, SegRows sr) {
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int n = ctl[CTL_N];
@@ -5175,7 +5227,7 @@ __global__ __launch_bounds__(256) void part_count_wave_kernel(const uint8_t* __r
         const int b = ecodes[(int64_t)j * ecs + eq];
         d = part_right(pi, b, nbt);
       } else {
-        d = split_dir(codes, npad, pi, nbt, idx ? idx[j] : j);
+        d = seg_split_dir(codes, npad, pi, nbt, idx ? idx[j] : j, j, sr);
       }
       if (dirb) dirb[j] = (int8_t)d;
       cnt += 1 - d;
@@ -5195,7 +5247,8 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
     const float* __restrict__ h, const float* __restrict__ w, const double* __restrict__ qs, int cap,
     unsigned long long* __restrict__ leaf_acc, const int8_t* __restrict__ dirb, const float* __restrict__ gin,
     const float* __restrict__ sin, float* __restrict__ gout, float* __restrict__ sout,
-    const uint8_t* __restrict__ ecodes, int ecs, const int* __restrict__ nodeq, int segf) {
+    const uint8_t* __restrict__ ecodes, int ecs, const int* __restrict__ nodeq, int segf, SegRows sr,
+    const uint8_t* __restrict__ codes_rm) {
   // segf (last level): bit 0 - gin / sin hold g and s2 in segment order (read
   // them at j instead of gathering g[r] / s2[r] by row: one random 4-byte
   // gather per row left instead of three); bit 1 - s2 is h (else w)
@@ -5229,7 +5282,7 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
           const int b = ecodes[(int64_t)j * ecs + nodeq[node]];
           dir = part_right(pi, b, nbt);
         } else {
-          dir = split_dir(codes, npad, pi, nbt, r);
+          dir = seg_split_dir(codes, npad, pi, nbt, r, j, sr);
         }
       }
     }
@@ -5245,6 +5298,7 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
           gout[start + pos] = gin[j];
           if (sout) sout[start + pos] = sin[j];
         }
+        if (sr.out) seg_move_row(sr, codes_rm, r, j, start + pos);
       }
       base_l += __popcll(bl);
       base_r += __popcll(bv) - __popcll(bl);
@@ -5306,7 +5360,7 @@ H2OMX_API int h2omx_hist_build_seg(const uint8_t* codes_rm, int fp, const int* i
                                    const int* seg_start, const int* seg_cnt, const int* hc_first, const int* ctl,
                                    const int* nvb, const double* qscale, int salt, int F, int nbt, int fg,
                                    int n_groups, int hc_rows, int max_chunks, int threads,
-                                   unsigned long long* slab, int gpos, hipStream_t stream) {
+                                   unsigned long long* slab, int gpos, const uint8_t* crow, hipStream_t stream) {
   if (fg > 256 || threads > 512 || threads % 64 || threads < fg || fp % 4 || (n_groups > 1 && fg % 4) ||
       hc_rows > ROWS_CAP)
     return kBadArg;
@@ -5316,7 +5370,7 @@ H2OMX_API int h2omx_hist_build_seg(const uint8_t* codes_rm, int fp, const int* i
 #define H2OMX_HBS(NB)                                                                                        \
   hipLaunchKernelGGL(hist_build_seg_kernel<NB>, dim3(grid), dim3(threads), lds, stream, codes_rm, fp, idx, g, s2, \
                      seg_start, seg_cnt, hc_first, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, hc_rows, slab, \
-                     gpos)
+                     gpos, crow)
   switch (nbt) {
     case 32: H2OMX_HBS(32); break;
     case 64: H2OMX_HBS(64); break;
@@ -5341,16 +5395,17 @@ H2OMX_API int h2omx_hist_reduce_seg(const unsigned long long* slab, const int* h
 H2OMX_API int h2omx_part_count(const uint8_t* codes, int64_t npad, const int* idx, const int* seg_start,
                                const int* seg_cnt, const int* pc_first, const int* ctl, const void* part, int nbt,
                                int max_chunks, int* pc_left, int wave, int8_t* dirb, const uint8_t* ecodes,
-                               int ecs, const int* nodeq, hipStream_t stream) {
+                               int ecs, const int* nodeq, const uint8_t* crow, int fp, hipStream_t stream) {
   if (ecodes && !wave) return kBadArg;
+  const SegRows sr{crow, nullptr, fp};
   if (wave) {
     hipLaunchKernelGGL(part_count_wave_kernel, dim3((max_chunks + 3) / 4), dim3(256), 0, stream, codes, npad, idx,
                        seg_start, seg_cnt, pc_first, ctl, reinterpret_cast<const PartInfo*>(part), nbt, pc_left, dirb,
-                       ecodes, ecs, nodeq);
+                       ecodes, ecs, nodeq, sr);
     return launch_status();
   }
   hipLaunchKernelGGL(part_count_kernel, dim3(max_chunks), dim3(256), 0, stream, codes, npad, idx, seg_start, seg_cnt,
-                     pc_first, ctl, reinterpret_cast<const PartInfo*>(part), nbt, pc_left);
+                     pc_first, ctl, reinterpret_cast<const PartInfo*>(part), nbt, pc_left, sr);
   return launch_status();
 }
 
@@ -5359,9 +5414,9 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
                                const uint8_t* tree_fmask, const double* qscale, int salt, const void* params, int nbt,
                                int max_nodes, int mode, const int* pc_first, int max_pc, unsigned long long* slab,
                                long long* tot_slab, int* ticket, void* nsplit, int gpos, uint8_t* ecodes, int ecs,
-                               int* nodeq, hipStream_t stream) {
+                               int* nodeq, const uint8_t* crow, hipStream_t stream) {
   if (ecodes && ecs != 8 && ecs != 16) return kBadArg;
-  const ECodes ec{ecodes, ecs, nodeq};
+  const ECodes ec{ecodes, ecs, nodeq, crow};
   // mode 0: one workgroup per node, 1: one wave per node (F <= 256),
   // 2: one workgroup per PC_ROWS chunk (slab / tot_slab: max_pc x max_elig x
   //    nbt and max_pc x 2 int64, ticket: max_nodes zeroed ints)
@@ -5435,7 +5490,7 @@ H2OMX_API int h2omx_direct_dp(int phase, const uint8_t* codes_rm, int fp, const 
                               const float* s2, const int* seg_start, const int* seg_cnt, const int* ctl,
                               const int* nvb, const uint8_t* tree_fmask, const double* qscale, const void* params,
                               int nbt, int node0, int n_chunk, long long* dh, void* nsplit, int gpos,
-                              hipStream_t stream) {
+                              const uint8_t* crow, hipStream_t stream) {
   const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
   if (n_chunk < 1 || p.F > 1024 || p.F > fp || nbt < 2 || dh == nullptr) return kBadArg;
   const int max_elig = p.mtries > 0 ? std::min(p.mtries, p.F) : p.F;
@@ -5447,7 +5502,7 @@ H2OMX_API int h2omx_direct_dp(int phase, const uint8_t* codes_rm, int fp, const 
   if (phase == 0)                                                                                            \
     hipLaunchKernelGGL(direct_dp_hist_kernel<NB>, dim3(n_chunk), dim3(256), lds, stream, codes_rm, fp, idx,  \
                        g, s2, seg_start, seg_cnt, ctl, tree_fmask, qscale, p, batch, node0, max_elig, dh,   \
-                       gpos);                                                                                \
+                       gpos, crow);                                                                          \
   else                                                                                                       \
     hipLaunchKernelGGL(direct_dp_scan_kernel<NB>, dim3(n_chunk), dim3(256), 0, stream, ctl, nvb, tree_fmask,  \
                        qscale, p, node0, max_elig, dh, ns)
@@ -5524,7 +5579,12 @@ H2OMX_API int h2omx_part_scatter(const uint8_t* codes, int64_t npad, const int* 
                                  const float* g, const float* h, const float* w, const double* qscale, int cap,
                                  unsigned long long* leaf_acc, int max_chunks, int wave, const int8_t* dirb,
                                  const float* gin, const float* sin, float* gout, float* sout,
-                                 const uint8_t* ecodes, int ecs, const int* nodeq, hipStream_t stream) {
+                                 const uint8_t* ecodes, int ecs, const int* nodeq, const uint8_t* codes_rm,
+                                 const uint8_t* crow_in, uint8_t* crow_out, int fp, hipStream_t stream) {
+  // crow_out: move every inner row's code row into the next level's segment order
+  // (source crow_in by position, or codes_rm by row id when crow_in is nullptr)
+  const SegRows sr{crow_in, crow_out, fp};
+  if (crow_out != nullptr && ((crow_in == nullptr && codes_rm == nullptr) || fp % 4 != 0)) return kBadArg;
   // wave: bit 0 wave-granular kernel; bits 1-2 its segf flags (last level)
   const int segf = wave >> 1;
   wave &= 1;
@@ -5534,12 +5594,12 @@ H2OMX_API int h2omx_part_scatter(const uint8_t* codes, int64_t npad, const int* 
     hipLaunchKernelGGL(part_scatter_wave_kernel, dim3((max_chunks + 3) / 4), dim3(256), 0, stream, codes, npad, idx,
                        idx_out, nid, write_nid, seg_start, seg_cnt, pc_first, pc_off, node_nl, ctl,
                        reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, dirb, gin, sin,
-                       gout, sout, ecodes, ecs, nodeq, segf);
+                       gout, sout, ecodes, ecs, nodeq, segf, sr, codes_rm);
     return launch_status();
   }
   hipLaunchKernelGGL(part_scatter_kernel, dim3(max_chunks), dim3(256), 0, stream, codes, npad, idx, idx_out, nid,
                      write_nid, seg_start, seg_cnt, pc_first, pc_off, node_nl, ctl,
                      reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, gin, sin, gout,
-                     sout);
+                     sout, sr, codes_rm);
   return launch_status();
 }

@@ -404,7 +404,9 @@ class GpuBooster:
                                                   b.tree_buf.numel(), P(arch[0] if arch else None),
                                                   arch[1] if arch else 0, P(b.tree_ctr if arch else None),
                                                   arch[2] if arch else 0, P(pk), P(b.qscale if pk is not None else None),
-                                                  1 if b.p.mode == 1 else 0, ops.stream(self.dev)),
+                                                  1 if b.p.mode == 1 else 0,
+                                                  0 if (arch is not None and b.regrad is not None) else 1,
+                                                  ops.stream(self.dev)),
                       "boost_update")
             if not fixed:
                 b.reduce_stats()
@@ -717,6 +719,12 @@ class TreeGraph:
         # replayed step is levels -> leaf_finalize(+begin) -> boost_update(+archive)
         self.chain = b.can_chain(gb._bounds is not None)
         b.pk_in_boost = self.chain and b.can_pack_in_boost()
+        b.regrad = None
+        if b.pk_in_boost and gb.wout is None and gb.K == 1 and os.environ.get("H2OMX_REGRAD", "0") == "1":
+            # the final partition re-derives (g, h) from the margins: boost_update
+            # stores only the packed rows (8 bytes per row less each way)
+            gpr = make_grad_params(gb.dist, False, 1.0, gb.seed, 0, row_base=b.row_base, **gb.kw)
+            b.regrad = (gb.st.Fm[0], gb.st.y, gpr)
         try:
             with torch.cuda.stream(side):
                 g = torch.cuda.CUDAGraph()

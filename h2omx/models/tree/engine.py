@@ -693,10 +693,14 @@ class HipTreeBuilder:
                                                     max_nodes, self.part_blocks, P(None if last else self.slot16),
                                                     1 if last else 0, st), "route_level")
                 elif fuse and last:
+                    rg = self.regrad if (chain and w is None) else None   # (F, y, GradParams)
                     ops.check(lib.h2omx_partition_final(P(bm.codes), bm.npad, P(nid_buf[d % 2]), P(self.nid),
                                                         P(part), nbt, P(g), P(h), P(w), P(self.qscale),
                                                         self.capacity, P(self.leaf_acc), P(ctl_cur), P(ctl_nxt),
-                                                        self.part_blocks, st), "partition_final")
+                                                        self.part_blocks, P(rg[0] if rg else None),
+                                                        P(rg[1] if rg else None),
+                                                        ctypes.addressof(rg[2]) if rg else None, st),
+                              "partition_final")
                 elif fuse and not self._fused_level(d + 1):
                     ops.check(lib.h2omx_partition_route(P(bm.codes), bm.npad, P(nid_buf[d % 2]),
                                                         P(nid_buf[(d + 1) % 2]), P(part), nbt, P(ctl_cur),
@@ -739,6 +743,9 @@ class HipTreeBuilder:
     # (g, s2) = 8 bytes (4 groups at level 0: ~220 MB less traffic at 11M rows)
     PK_IN_BOOST = os.environ.get("H2OMX_PK_IN_BOOST", "1") == "1"
     pk_in_boost = False
+    # chained graph steps of unweighted rows: boost_update stores no (g, h); the
+    # final partition re-derives them from (margins, labels, GradParams)
+    regrad = None
 
     def can_pack_in_boost(self) -> bool:
         return (self.PK_IN_BOOST and self.pk32 and self.implicit_root and not self.segmented and not self.COMPACT
@@ -761,7 +768,20 @@ class HipTreeBuilder:
     DIRECT_DP = os.environ.get("H2OMX_DIRECT_DP", "1") == "1"
     DIRECT_DP_CHUNK_BYTES = int(os.environ.get("H2OMX_DIRECT_DP_CHUNK_MB", "64")) << 20
 
-    def _direct_dp(self, comm, idx_in, gs, seg_start, seg_cnt, ctl_cur, tree_fmask, spp, max_nodes, nsplit, st):
+    # segmented engine: move the row-major code rows with their segments once the
+    # next level reads rows by segment (direct levels: a random cache line per
+    # row otherwise); "direct" / "seg" / "0" (off)
+    MOVE_ROWS = os.environ.get("H2OMX_MOVE_ROWS", "0")
+
+    def _move_rows(self, crow, next_direct: bool, next_seg_hist: bool) -> bool:
+        if self.MOVE_ROWS == "0" or self.segmented is False:
+            return False
+        if crow["cur"] is not None:
+            return True
+        return next_direct or (self.MOVE_ROWS == "seg" and next_seg_hist)
+
+    def _direct_dp(self, comm, idx_in, gs, seg_start, seg_cnt, ctl_cur, tree_fmask, spp, max_nodes, nsplit, st,
+                   crow=None):
         """Direct level over N row shards: per node chunk, this rank's eligible-
         feature histograms (h2omx_direct_dp phase 0) -> all-reduce -> the scan
         (phase 1) writes the nodes' NodeSplit records, identical on every rank."""
@@ -775,7 +795,7 @@ class HipTreeBuilder:
                 ops.check(lib.h2omx_direct_dp(phase, P(self.codes_rm), bm.fp, P(idx_in), P(gs["g"]), P(gs["s"]),
                                               P(seg_start), P(seg_cnt), P(ctl_cur), P(bm.nvb), P(tree_fmask),
                                               P(self.qscale), spp, self.nbt, node0, nc, P(dh), P(nsplit),
-                                              gs["pos"], st), "direct_dp")
+                                              gs["pos"], P(crow), st), "direct_dp")
                 if phase == 0:
                     comm.all_reduce_(dh[: nc * stride])
         self.stats["direct_dp_levels"] = self.stats.get("direct_dp_levels", 0) + 1
@@ -816,9 +836,11 @@ class HipTreeBuilder:
         # (g, s2) as the current level reads them: by row at level 0, afterwards in segment order
         # (part_scatter moves them with the rows, so the histogram passes read them contiguously)
         gs = {"g": g, "s": s2, "pos": 0}
+        # row-major code rows in the current level's segment order (MOVE_ROWS), None = gather by row id
+        crow = {"cur": None}
 
         def route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first, ctl_cur, ctl_nxt,
-                  idx_in, next_direct, ec=None):
+                  idx_in, next_direct, ec=None, move=False):
             """part_count -> level_close -> part_scatter: rows into their next-level segments.
             ec: (codes, stride, nodeq) of the direct pass - split codes read in segment order."""
             cur, nxt = d % 2, (d + 1) % 2
@@ -847,7 +869,8 @@ class HipTreeBuilder:
                     nbuilt = B("built", max_nodes * self.per_node, torch.int64)
                 ops.check(lib.h2omx_part_count(P(bm.codes), bm.npad, P(idx_in), P(seg_start), P(seg_cnt),
                                                P(pc_first), P(ctl_cur), P(part), nbt, max_pc, P(pc_left), pwave,
-                                               P(dirb), P(ecodes), ecs, P(nodeq), st), "part_count")
+                                               P(dirb), P(ecodes), ecs, P(nodeq), P(crow["cur"]), bm.fp, st),
+                          "part_count")
                 if max_nodes <= self.CLOSE_SINGLE_BLOCK:
                     ops.check(lib.h2omx_level_close(P(ctl_cur), P(ctl_nxt), P(part), P(nl), P(seg_start),
                                                     P(seg_cnt), P(pc_first), P(pc_left), P(node_nl), P(nstart),
@@ -874,12 +897,20 @@ class HipTreeBuilder:
             if not last and self.PERMUTE_GS:
                 gout = B(f"gperm{d % 2}", n + 64, torch.float32)
                 sout = None if s2 is None else B(f"sperm{d % 2}", n + 64, torch.float32)
+            crow_out = None
+            if move and not last:
+                # the next level's code rows in its segment order (double-buffered)
+                crow_out = B(f"crow{d % 2}", (n + 1) * bm.fp, torch.uint8)
             ops.check(lib.h2omx_part_scatter(P(bm.codes), bm.npad, P(idx_in), P(idx_out), P(self.nid), write_nid,
                                              P(seg_start), P(seg_cnt), P(pc_first), P(pc_left), P(node_nl),
                                              P(ctl_cur), P(part), nbt, P(g), P(h), P(w), P(self.qscale),
                                              self.capacity, P(self.leaf_acc), max_pc, pwave | segf, P(dirb), P(gs["g"]),
-                                             P(gs["s"]), P(gout), P(sout), P(ecodes), ecs, P(nodeq), st),
+                                             P(gs["s"]), P(gout), P(sout), P(ecodes), ecs, P(nodeq),
+                                             P(self.codes_rm), P(crow["cur"]), P(crow_out), bm.fp, st),
                       "part_scatter")
+            crow["cur"] = crow_out
+            if crow_out is not None:
+                self.stats["moved_row_levels"] = self.stats.get("moved_row_levels", 0) + 1
             if gout is not None:
                 gs.update(g=gout, s=sout, pos=1)
             else:
@@ -944,7 +975,7 @@ class HipTreeBuilder:
                 ecodes, ecs, nodeq = ec if ec is not None else (None, 0, None)
                 if comm is not None:
                     self._direct_dp(comm, idx_in, gs, seg_start, seg_cnt, ctl_cur, tree_fmask, spp, max_nodes,
-                                    nsplit, st)
+                                    nsplit, st, crow["cur"])
                     ec = None
                 else:
                     ops.check(lib.h2omx_seg_direct(P(self.codes_rm), bm.fp,
@@ -952,14 +983,15 @@ class HipTreeBuilder:
                                                    P(seg_start), P(seg_cnt), P(ctl_cur), P(bm.nvb), P(tree_fmask),
                                                    P(self.qscale), tree_index & 0x7FFFFFFF, spp, nbt, max_nodes,
                                                    dmode, P(pc_first), max_pc, P(slab), P(tot_slab), P(ticket),
-                                                   P(nsplit), gs["pos"], P(ecodes), ecs, P(nodeq), st), "seg_direct")
+                                                   P(nsplit), gs["pos"], P(ecodes), ecs, P(nodeq), P(crow["cur"]), st),
+                              "seg_direct")
                 ops.check(lib.h2omx_level_finalize_ns(P(nsplit), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
                                                       P(bm.nvb), nbt, next_nodes, P(part), P(nl), P(self.tree_buf),
                                                       self.capacity, max_nodes,
                                                       self._lf_tiles(max_nodes), st),
                           "level_finalize_ns")
                 idx_in, _ = route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first, ctl_cur,
-                                  ctl_nxt, idx_in, True, ec)
+                                  ctl_nxt, idx_in, True, ec, move=self._move_rows(crow, True, False))
                 full_prev = None
                 max_nodes = next_nodes
                 continue
@@ -975,7 +1007,7 @@ class HipTreeBuilder:
                                                    P(seg_start), P(seg_cnt), P(hc_first), P(ctl_cur), P(bm.nvb),
                                                    P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, self.seg_fg,
                                                    self.seg_groups, self.hc_rows, max_hc, self.seg_threads, P(slab),
-                                                   gs["pos"], st), "hist_build_seg")
+                                                   gs["pos"], P(crow["cur"]), st), "hist_build_seg")
                 ksplit = max(1, min(32, 4096 // max(1, max_slots * ((F * nbt + 255) // 256))))
                 ksplit = max(ksplit, 4)
                 ops.check(lib.h2omx_hist_reduce_seg(P(slab), P(hc_first), P(slot_node), P(ctl_cur), F, nbt,
@@ -1016,8 +1048,10 @@ class HipTreeBuilder:
                                                next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
                                                P(nsplit), max_nodes, self._lf_tiles(max_nodes), st),
                       "level_finalize")
+            nd = direct_ok and next_nodes >= self.DIRECT_MIN_NODES        # next level direct (upper bound)
+            ns = max_nodes > self.SCAN_SLOTS or next_nodes > self.SYNC_NODE_CAP
             idx_in, built_zeroed = route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first,
-                                         ctl_cur, ctl_nxt, idx_in, False)
+                                         ctl_cur, ctl_nxt, idx_in, False, move=self._move_rows(crow, nd, ns))
             full_prev = full_cur
             max_nodes = next_nodes
         if comm is not None:

@@ -31,11 +31,11 @@ TREE_SIGS = {
     "h2omx_split_find_fin": "PPPPPPPPPIIPPPPIPPPIPS",
     "h2omx_partition": "PLPPIPPPPIPPPIIIPS",
     "h2omx_partition_blocks": "",
-    "h2omx_partition_final": "PLPPPIPPPPIPPPIS",
+    "h2omx_partition_final": "PLPPPIPPPPIPPPIPPPS",
     "h2omx_partition_route": "PLPPPIPPIPS",
     "h2omx_route_level": "PLPPPIPPPPIPPIIPIS",
     "h2omx_leaf_reduce": "PIIPS",
-    "h2omx_boost_update": "PPPLLPPPPPPPLPIPIPPIS",
+    "h2omx_boost_update": "PPPLLPPPPPPPLPIPIPPIIS",
     "h2omx_apply_tree": "PLPPS",
     "h2omx_tree_archive": "PLPIPS",
     "h2omx_sketch_bins": "",
@@ -53,16 +53,16 @@ TREE_SIGS = {
     "h2omx_predict_binned": "PLLPPIIIPLPS",
     "h2omx_pc_rows": "",
     "h2omx_tree_begin_seg": "PIIPPPPIPIIIPPPPPLIPS",
-    "h2omx_hist_build_seg": "PIPPPPPPPPPIIIIIIIIPIS",
+    "h2omx_hist_build_seg": "PIPPPPPPPPPIIIIIIIIPIPS",
     "h2omx_hist_reduce_seg": "PPPPIIIIIIPS",
-    "h2omx_part_count": "PLPPPPPPIIPIPPIPS",
+    "h2omx_part_count": "PLPPPPPPIIPIPPIPPIS",
     "h2omx_level_close": "PPPPPPPPPPPPPPIPIS",
     "h2omx_level_close_mb": "PPPPPPPPPPPPPPIPIIIPPPPPS",
-    "h2omx_part_scatter": "PLPPPIPPPPPPPIPPPPIPIIPPPPPPIPS",
-    "h2omx_seg_direct": "PIPPPPPPPPPIPIIIPIPPPPIPIPS",
+    "h2omx_part_scatter": "PLPPPIPPPPPPPIPPPPIPIIPPPPPPIPPPPIS",
+    "h2omx_seg_direct": "PIPPPPPPPPPIPIIIPIPPPPIPIPPS",
     "h2omx_level_finalize_ns": "PPPPPPIIPPPIIPS",
     "h2omx_direct_dp_stride": "PI",
-    "h2omx_direct_dp": "IPIPPPPPPPPPPIIIPPIS",
+    "h2omx_direct_dp": "IPIPPPPPPPPPPIIIPPIPS",
 }
 
 DENSE_SIGS = {

@@ -269,17 +269,20 @@ def test_direct_deep_levels_match_subtraction(cuda_dev, monkeypatch, dist, depth
     out = {}
     # engine switches: direct from this many nodes, wave-per-node below this many rows per node,
     # multi-block finalise, wave-chunk partition from this many nodes, chunked direct workgroups,
-    # (g, s2) moved into segment order, eligible-feature codes stored for the partition
+    # (g, s2) moved into segment order, eligible-feature codes stored for the partition,
+    # code rows moved with their segments (from the first direct / segmented level)
     keys = ("DIRECT_MIN_NODES", "DIRECT_WAVE_ROWS", "LF_MULTI_BLOCK", "PART_WAVE_NODES", "DIRECT_CHUNKED",
-            "PERMUTE_GS", "ECODES")
-    for cfg in ((0, 0, False, 1 << 30, True, False, False), (0, 0, True, 1, True, True, True),
-                (2, 0, True, 1 << 30, True, True, True), (64, 0, True, 1 << 30, False, False, True),
-                (64, 1 << 30, True, 1, True, True, False), (64, 1 << 30, False, 2048, True, False, True)):
+            "PERMUTE_GS", "ECODES", "MOVE_ROWS")
+    for cfg in ((0, 0, False, 1 << 30, True, False, False, "0"), (0, 0, True, 1, True, True, True, "0"),
+                (2, 0, True, 1 << 30, True, True, True, "0"), (64, 0, True, 1 << 30, False, False, True, "0"),
+                (64, 1 << 30, True, 1, True, True, False, "0"), (64, 1 << 30, False, 2048, True, False, True, "0"),
+                (2, 0, True, 1 << 30, True, True, True, "seg"), (64, 1 << 30, True, 1, True, True, False, "direct"),
+                (64, 0, True, 1 << 30, False, False, True, "seg"), (0, 0, True, 1, True, True, True, "seg")):
         for k, v in zip(keys, cfg):
             monkeypatch.setattr(E.HipTreeBuilder, k, v)
         out[cfg] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
                                   nclass=nclass, seed=13)
-    a = out[(0, 0, False, 1 << 30, True, False, False)]
+    a = out[(0, 0, False, 1 << 30, True, False, False, "0")]
     for cfg, b in out.items():
         for t in range(a.trees.shape[0]):
             reach = a.compact()[t]
