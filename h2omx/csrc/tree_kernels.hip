@@ -407,7 +407,9 @@ constexpr int HB_PF = H2OMX_HB_PF;     // feature code loads kept in flight per 
 // 16 lanes of a ds_add_u64 group then hit at most two addresses per bank pair
 // (bench_micro/lds_atomics.hip: random bins 14.4 CU-cycles per wave-atomic,
 // conflict-free 7.3), at COP x the LDS per feature (fewer features per group)
-template <int NBT, int ROWS, int PKM, bool ROUTE, bool CMP, int COP = 1>
+// NID16 (fused-routing levels): the previous / next node ids are int16 streams
+// (2 bytes a row each way instead of 4; padding rows hold INT16_MIN)
+template <int NBT, int ROWS, int PKM, bool ROUTE, bool CMP, int COP = 1, bool NID16 = false>
 __global__ __launch_bounds__(1024) void hist_build_kernel(
     const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ s2,
     const int* __restrict__ nid, const NodeLink* __restrict__ link, const int* __restrict__ ctl,
@@ -474,6 +476,15 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
         // no node-id stream to read (boost_update no longer resets it)
 #pragma unroll
         for (int k = 0; k < ROWS; ++k) nn[k] = (r0 + k < n_rows) ? 0 : INT32_MIN;
+      } else if constexpr (NID16) {
+        const short* n16 = reinterpret_cast<const short*>(nid);
+#pragma unroll
+        for (int q = 0; q < ROWS / 8; ++q) {
+          const uint4 v = *reinterpret_cast<const uint4*>(n16 + r0 + 8 * q);
+          const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int k = 0; k < 8; ++k) nn[8 * q + k] = (int)(short)(w4[k >> 1] >> (16 * (k & 1)));
+        }
       } else {
 #pragma unroll
         for (int q = 0; q < ROWS / 4; ++q) {
@@ -527,9 +538,22 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
         any |= (sl >= 0);
       }
       if (route_w) {
+        if constexpr (NID16) {
+          short* o16 = reinterpret_cast<short*>(nid_out);
 #pragma unroll
-        for (int q = 0; q < ROWS / 4; ++q)
-          *reinterpret_cast<int4*>(nid_out + r0 + 4 * q) = make_int4(nx[4 * q], nx[4 * q + 1], nx[4 * q + 2], nx[4 * q + 3]);
+          for (int q = 0; q < ROWS / 8; ++q) {
+            uint32_t w4[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              w4[k] = ((uint32_t)(uint16_t)max(nx[8 * q + 2 * k], -32768)) |
+                      ((uint32_t)(uint16_t)max(nx[8 * q + 2 * k + 1], -32768) << 16);
+            *reinterpret_cast<uint4*>(o16 + r0 + 8 * q) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < ROWS / 4; ++q)
+            *reinterpret_cast<int4*>(nid_out + r0 + 4 * q) = make_int4(nx[4 * q], nx[4 * q + 1], nx[4 * q + 2], nx[4 * q + 3]);
+        }
       }
     } else if constexpr (PKM == 2 || PKM == 4) {
 #pragma unroll
@@ -2320,7 +2344,8 @@ __device__ __forceinline__ void part_leaf_add(int leaf, int base, int win, int c
 __constant__ int g_part_rec_lds = 1;
 __constant__ int g_part_rec_lds_final = 1;
 
-template <bool PREF, int RPL>
+// NIDM bit 0: nid (input) is an int16 stream, bit 1: nid_out is int16 (fused pipeline)
+template <bool PREF, int RPL, int NIDM = 0>
 __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restrict__ codes, int64_t npad,
                                                         int* nid, const PartInfo* __restrict__ part,
                                                         int nbt, const float* __restrict__ g,
@@ -2361,10 +2386,21 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r0 = q * RPL;
     int nn[RPL];
+    if constexpr (NIDM & 1) {
+      static_assert(RPL % 8 == 0, "int16 node ids: 8-row vectors");
 #pragma unroll
-    for (int v = 0; v < RPL / 4; ++v) {
-      const int4 na = *reinterpret_cast<int4*>(nid + r0 + 4 * v);
-      nn[4 * v] = na.x; nn[4 * v + 1] = na.y; nn[4 * v + 2] = na.z; nn[4 * v + 3] = na.w;
+      for (int v = 0; v < RPL / 8; ++v) {
+        const uint4 q4 = *reinterpret_cast<const uint4*>(reinterpret_cast<const short*>(nid) + r0 + 8 * v);
+        const uint32_t w4[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) nn[8 * v + k] = (int)(short)(w4[k >> 1] >> (16 * (k & 1)));
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < RPL / 4; ++v) {
+        const int4 na = *reinterpret_cast<int4*>(nid + r0 + 4 * v);
+        nn[4 * v] = na.x; nn[4 * v + 1] = na.y; nn[4 * v + 2] = na.z; nn[4 * v + 3] = na.w;
+      }
     }
     float gv[RPL], hv[RPL], wv8[RPL];
     if (PREF) {
@@ -2492,10 +2528,23 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
       }
     }
     if (changed || nid_out != nid) {
+      if constexpr (NIDM & 2) {
 #pragma unroll
-      for (int v = 0; v < RPL / 4; ++v)
-        *reinterpret_cast<int4*>(nid_out + r0 + 4 * v) =
-            make_int4(nn[4 * v], nn[4 * v + 1], nn[4 * v + 2], nn[4 * v + 3]);
+        for (int v = 0; v < RPL / 8; ++v) {
+          uint32_t w4[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            w4[k] = ((uint32_t)(uint16_t)max(nn[8 * v + 2 * k], -32768)) |
+                    ((uint32_t)(uint16_t)max(nn[8 * v + 2 * k + 1], -32768) << 16);
+          *reinterpret_cast<uint4*>(reinterpret_cast<short*>(nid_out) + r0 + 8 * v) =
+              make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+      } else {
+#pragma unroll
+        for (int v = 0; v < RPL / 4; ++v)
+          *reinterpret_cast<int4*>(nid_out + r0 + 4 * v) =
+              make_int4(nn[4 * v], nn[4 * v + 1], nn[4 * v + 2], nn[4 * v + 3]);
+      }
     }
     if (slot16) {  // every row, so rows outside the tree read -1 on the next level
 #pragma unroll
@@ -3223,7 +3272,10 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
   const bool cmp = (pkm & 8) != 0;
   // pkm bit 4 / 5: level-0 histograms in 8 / 4 interleaved lane copies (PKM 1 / 3 only)
   const int cop = (pkm & 16) ? 8 : ((pkm & 32) ? 4 : 1);
+  // pkm bit 6: int16 node-id streams (routed levels only)
+  const bool nid16 = (pkm & 64) != 0;
   pkm &= 7;
+  if (nid16 && (!route || cmp || rows_per_lane != 16)) return kBadArg;
   if (cop > 1 && ((pkm != 1 && pkm != 3 && pkm != 6) || route || cmp)) return kBadArg;
   // pkm 6: level 0 reading the packed rows boost_update wrote (implicit root)
   if (pkm == 6 && (nid != nullptr || route || cmp || pk_buf == nullptr)) return kBadArg;
@@ -3254,6 +3306,10 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
 #define H2OMX_HBKC(NB, R, M, CP)                                                                                \
   hipLaunchKernelGGL((hist_build_kernel<NB, R, M, false, false, CP>), dim3(grid), dim3(threads), lds, stream, codes, \
                      npad, g, s2, nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo,        \
+                     slot_cnt, slot16, pk_buf, partials, pp, ctl_prev, nid_out, writer, gfz)
+#define H2OMX_HBK16(NB, M)                                                                                      \
+  hipLaunchKernelGGL((hist_build_kernel<NB, 16, M, true, false, 1, true>), dim3(grid), dim3(threads), lds, stream, \
+                     codes, npad, g, s2, nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo,    \
                      slot_cnt, slot16, pk_buf, partials, pp, ctl_prev, nid_out, writer, gfz)
 #define H2OMX_HB(NB, R)                                            \
   do {                                                             \
@@ -3288,6 +3344,14 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
       case 256: H2OMX_HBCMP(256); break;
       default: return kBadArg;
     }
+  } else if (nid16) {
+    switch (nbt) {
+      case 32: if (pkm == 2) H2OMX_HBK16(32, 2); else H2OMX_HBK16(32, 4); break;
+      case 64: if (pkm == 2) H2OMX_HBK16(64, 2); else H2OMX_HBK16(64, 4); break;
+      case 128: if (pkm == 2) H2OMX_HBK16(128, 2); else H2OMX_HBK16(128, 4); break;
+      case 256: if (pkm == 2) H2OMX_HBK16(256, 2); else H2OMX_HBK16(256, 4); break;
+      default: return kBadArg;
+    }
   } else if (rows_per_lane == 16) {
     switch (nbt) {
       case 32: H2OMX_HB(32, 16); break;
@@ -3308,6 +3372,7 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
     return kBadArg;
   }
 #undef H2OMX_HB
+#undef H2OMX_HBK16
 #undef H2OMX_HBCMP
 #undef H2OMX_HBK
 #undef H2OMX_HBKC
@@ -3604,7 +3669,10 @@ static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const 
                             const float* h, const float* w, const double* qscale, int cap,
                             unsigned long long* leaf_acc, const int* ctl_cur, const int* ctl_next, int win_max,
                             int blocks, int prefetch, short* slot16, int* nid_out, int all_rows, hipStream_t stream,
-                            const float* Fm = nullptr, const float* yv = nullptr, const GradParams* gpp = nullptr) {
+                            const float* Fm = nullptr, const float* yv = nullptr, const GradParams* gpp = nullptr,
+                            int nidm = 0) {
+  // nidm bit 0: nid is an int16 stream, bit 1: nid_out is (fused pipeline; distinct buffers)
+  if (nidm != 0 && (nid_out == nid || (nidm & 2 && prefetch))) return kBadArg;
   GradParams gp{};
   if (gpp) gp = *gpp;
   if ((Fm != nullptr) != (gpp != nullptr) || (Fm != nullptr && (yv == nullptr || w != nullptr || !prefetch)))
@@ -3622,14 +3690,20 @@ static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const 
     win_max = 0;
   }
   const size_t lds = (leaf_acc && win_max > 0) ? (size_t)3 * win_max * R * sizeof(unsigned long long) : 0;
-  if (prefetch && leaf_acc)
-    hipLaunchKernelGGL((partition_kernel<true, PART_RPL>), dim3(blocks), dim3(256), lds, stream, codes, npad, nid,
-                       reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
-                       ctl_next, win_max, R, slot16, nid_out, all_rows, Fm, yv, gp);
-  else
-    hipLaunchKernelGGL((partition_kernel<false, PART_RPL>), dim3(blocks), dim3(256), lds, stream, codes, npad, nid,
-                       reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
-                       ctl_next, leaf_acc ? win_max : 0, R, slot16, nid_out, all_rows, Fm, yv, gp);
+#define H2OMX_PK(PF, NM, WIN)                                                                                  \
+  hipLaunchKernelGGL((partition_kernel<PF, PART_RPL, NM>), dim3(blocks), dim3(256), lds, stream, codes, npad, nid, \
+                     reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,        \
+                     ctl_next, WIN, R, slot16, nid_out, all_rows, Fm, yv, gp)
+  if (prefetch && leaf_acc) {
+    if (nidm & 1) H2OMX_PK(true, 1, win_max);
+    else H2OMX_PK(true, 0, win_max);
+  } else {
+    if (nidm == 3) H2OMX_PK(false, 3, leaf_acc ? win_max : 0);
+    else if (nidm == 1) H2OMX_PK(false, 1, leaf_acc ? win_max : 0);
+    else if (nidm == 2) H2OMX_PK(false, 2, leaf_acc ? win_max : 0);
+    else H2OMX_PK(false, 0, leaf_acc ? win_max : 0);
+  }
+#undef H2OMX_PK
   return launch_status();
 }
 
@@ -3646,10 +3720,11 @@ H2OMX_API int h2omx_partition(const uint8_t* codes, int64_t npad, int* nid, cons
 // nid_in -> nid_out and writes slot16; no leaf sums (the final level adds them).
 H2OMX_API int h2omx_partition_route(const uint8_t* codes, int64_t npad, const int* nid_in, int* nid_out,
                                     const void* part, int nbt, const int* ctl_cur, const int* ctl_next, int blocks,
-                                    short* slot16, hipStream_t stream) {
+                                    short* slot16, int nidm, hipStream_t stream) {
   if (slot16 == nullptr) return kBadArg;
   return partition_launch(codes, npad, const_cast<int*>(nid_in), part, nbt, nullptr, nullptr, nullptr, nullptr, 0,
-                          nullptr, ctl_cur, ctl_next, 0, blocks, 0, slot16, nid_out, 0, stream);
+                          nullptr, ctl_cur, ctl_next, 0, blocks, 0, slot16, nid_out, 0, stream, nullptr, nullptr,
+                          nullptr, nidm);
 }
 
 // Final level of the fused-routing pipeline: nid_in (this level's node ids,
@@ -3659,11 +3734,12 @@ H2OMX_API int h2omx_partition_final(const uint8_t* codes, int64_t npad, const in
                                     const void* part, int nbt, const float* g, const float* h, const float* w,
                                     const double* qscale, int cap, unsigned long long* leaf_acc, const int* ctl_cur,
                                     const int* ctl_next, int blocks, const float* Fm, const float* y,
-                                    const void* gparams, hipStream_t stream) {
-  // Fm / y / gparams (optional): the rows' (g, h) are re-derived from the margins
+                                    const void* gparams, int nidm, hipStream_t stream) {
+  // Fm / y / gparams (optional): the rows' (g, h) are re-derived from the margins;
+  // nidm 1: nid_in is an int16 stream (nid_out stays int32: boost_update reads it)
   return partition_launch(codes, npad, const_cast<int*>(nid_in), part, nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
                           ctl_next, cap, blocks, 1, nullptr, nid_out, 1, stream, Fm, y,
-                          reinterpret_cast<const GradParams*>(gparams));
+                          reinterpret_cast<const GradParams*>(gparams), nidm);
 }
 
 // route_kernel entry (fused pipeline): final = 1 -> last level (leaf sums of

@@ -253,6 +253,13 @@ class HipTreeBuilder:
             self.seg_threads = 512
             self.codes_rm = bm.codes_rm
             self.idx = [torch.empty((max(bm.n, 1),), dtype=torch.int32, device=d) for _ in range(2)]
+        # int16 node ids between the fused-routing levels (2 bytes a row each way
+        # instead of 4); the opt-in routing variants (RM / route_kernel) keep int32
+        self.nid16 = None
+        if (self.fuse_route and self.implicit_root and not self.RM and not self.ROUTE_KERNEL
+                and self.capacity < 32767 and os.environ.get("H2OMX_NID16", "1") == "1"):
+            self.nid16 = (torch.full((bm.npad,), -1, dtype=torch.int16, device=d),
+                          torch.full((bm.npad,), -1, dtype=torch.int16, device=d))
         # the fixed-point scales (tree_begin) derive from max_rows_per_wg: every rank
         # quantises with the SAME scale (derived from the global row count above), so
         # the summed int64 histograms are in one unit
@@ -534,7 +541,10 @@ class HipTreeBuilder:
         final_ctl = self.ctl[max_depth % 2]
         max_nodes = 1
         fuse = self.fuse_route
-        nid_buf = (self.nid, self.nid2)
+        # int16 node-id streams between the fused levels (NID16): the final
+        # partition writes the int32 leaf ids boost_update reads into self.nid
+        nid16 = self.nid16 is not None
+        nid_buf = self.nid16 if nid16 else (self.nid, self.nid2)
         part_prev = None
         for d in range(max_depth):
             cur, nxt = d % 2, (d + 1) % 2
@@ -610,7 +620,8 @@ class HipTreeBuilder:
                             P(part_prev), P(ctl_nxt),
                             P(nid_buf[d % 2]), 1 if ps == 0 else 0, P(ctl_cur), P(bm.nvb), P(self.qscale), F, nbt,
                             plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo, plan["slot_cnt"],
-                            self.ROWS_PER_LANE, plan["threads"], P(self.pk), (4 if self.pk32 else 2) + cmp_flag,
+                            self.ROWS_PER_LANE, plan["threads"], P(self.pk),
+                            (4 if self.pk32 else 2) + cmp_flag + (64 if nid16 else 0),
                             P(partials), st),
                             "hist_build_route")
                     elif d == 0 and grad_fuse is not None:
@@ -699,12 +710,14 @@ class HipTreeBuilder:
                                                         self.capacity, P(self.leaf_acc), P(ctl_cur), P(ctl_nxt),
                                                         self.part_blocks, P(rg[0] if rg else None),
                                                         P(rg[1] if rg else None),
-                                                        ctypes.addressof(rg[2]) if rg else None, st),
+                                                        ctypes.addressof(rg[2]) if rg else None,
+                                                        1 if nid16 else 0, st),
                               "partition_final")
                 elif fuse and not self._fused_level(d + 1):
                     ops.check(lib.h2omx_partition_route(P(bm.codes), bm.npad, P(nid_buf[d % 2]),
                                                         P(nid_buf[(d + 1) % 2]), P(part), nbt, P(ctl_cur),
-                                                        P(ctl_nxt), self.part_blocks, P(self.slot16), st),
+                                                        P(ctl_nxt), self.part_blocks, P(self.slot16),
+                                                        3 if nid16 else 0, st),
                               "partition_route")
                 elif not fuse:
                     ops.check(lib.h2omx_partition(P(bm.codes), bm.npad, P(self.nid), P(part), nbt, P(g), P(h),

@@ -31,8 +31,8 @@ TREE_SIGS = {
     "h2omx_split_find_fin": "PPPPPPPPPIIPPPPIPPPIPS",
     "h2omx_partition": "PLPPIPPPPIPPPIIIPS",
     "h2omx_partition_blocks": "",
-    "h2omx_partition_final": "PLPPPIPPPPIPPPIPPPS",
-    "h2omx_partition_route": "PLPPPIPPIPS",
+    "h2omx_partition_final": "PLPPPIPPPPIPPPIPPPIS",
+    "h2omx_partition_route": "PLPPPIPPIPIS",
     "h2omx_route_level": "PLPPPIPPPPIPPIIPIS",
     "h2omx_leaf_reduce": "PIIPS",
     "h2omx_boost_update": "PPPLLPPPPPPPLPIPIPPIIS",
