@@ -4111,13 +4111,28 @@ struct SegRows {
   int fp;
 };
 
-// copy row r's (segment position j) fp code bytes to segment position dst of sr.out
-__device__ __forceinline__ void seg_move_row(const SegRows& sr, const uint8_t* __restrict__ codes_rm, int r, int j,
-                                             int dst) {
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(sr.in ? sr.in + (int64_t)j * sr.fp
-                                                                : codes_rm + (int64_t)r * sr.fp);
-  uint32_t* d = reinterpret_cast<uint32_t*>(sr.out + (int64_t)dst * sr.fp);
-  for (int q = 0; q < (sr.fp >> 2); ++q) d[q] = src[q];
+// The wave's rows (lane i: row r / segment position j -> segment position dst,
+// dst < 0 = nothing to move) copied cooperatively: consecutive lanes move
+// consecutive 4-byte words of one row, so the reads (rows j contiguous) and
+// the writes (left / right children are two order-preserving runs) coalesce.
+// Called by every lane of the wave.
+__device__ __forceinline__ void seg_move_rows_wave(const SegRows& sr, const uint8_t* __restrict__ codes_rm, int r,
+                                                   int j, int dst) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long act = __ballot(dst >= 0);
+  if (act == 0ull) return;
+  const int nr = 64 - __clzll((long long)act);   // rows of lanes [0, nr)
+  const int W = sr.fp >> 2;
+  for (int base = 0; base < nr * W; base += 64) {
+    const int q = base + lane;
+    const int i = min(q / W, 63), k = q - (q / W) * W;
+    const int di = __shfl(dst, i, kWave), ri = __shfl(r, i, kWave), ji = __shfl(j, i, kWave);
+    if (q < nr * W && di >= 0) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(sr.in ? sr.in + (int64_t)ji * sr.fp
+                                                                    : codes_rm + (int64_t)ri * sr.fp);
+      reinterpret_cast<uint32_t*>(sr.out + (int64_t)di * sr.fp)[k] = src[k];
+    }
+  }
 }
 
 __device__ __forceinline__ int seg_split_dir(const uint8_t* __restrict__ codes, int64_t npad, const PartInfo& pi,
@@ -5233,7 +5248,11 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
           gout[start + pos] = gin[j];
           if (sout) sout[start + pos] = sin[j];
         }
-        if (sr.out) seg_move_row(sr, codes_rm, r, j, start + pos);
+      }
+      if (sr.out) {
+        int dst = -1;
+        if (valid) dst = start + (goes_left ? base_l + my_l : nl + base_r + (my_v - my_l));
+        seg_move_rows_wave(sr, codes_rm, r, j, dst);
       }
       base_l += tot_l;
       base_r += tot_v - tot_l;
@@ -5374,7 +5393,14 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
           gout[start + pos] = gin[j];
           if (sout) sout[start + pos] = sin[j];
         }
-        if (sr.out) seg_move_row(sr, codes_rm, r, j, start + pos);
+      }
+      if (sr.out) {
+        int dst = -1;
+        if (valid) {
+          const int my_l = __popcll(bl & lt), my_v = __popcll(bv & lt);
+          dst = start + (dir == 0 ? base_l + my_l : nl + base_r + (my_v - my_l));
+        }
+        seg_move_rows_wave(sr, codes_rm, r, j, dst);
       }
       base_l += __popcll(bl);
       base_r += __popcll(bv) - __popcll(bl);

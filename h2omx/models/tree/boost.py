@@ -720,7 +720,7 @@ class TreeGraph:
         self.chain = b.can_chain(gb._bounds is not None)
         b.pk_in_boost = self.chain and b.can_pack_in_boost()
         b.regrad = None
-        if b.pk_in_boost and gb.wout is None and gb.K == 1 and os.environ.get("H2OMX_REGRAD", "0") == "1":
+        if b.pk_in_boost and gb.wout is None and gb.K == 1 and os.environ.get("H2OMX_REGRAD", "1") == "1":
             # the final partition re-derives (g, h) from the margins: boost_update
             # stores only the packed rows (8 bytes per row less each way)
             gpr = make_grad_params(gb.dist, False, 1.0, gb.seed, 0, row_base=b.row_base, **gb.kw)

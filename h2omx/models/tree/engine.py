@@ -256,8 +256,9 @@ class HipTreeBuilder:
         # int16 node ids between the fused-routing levels (2 bytes a row each way
         # instead of 4); the opt-in routing variants (RM / route_kernel) keep int32
         self.nid16 = None
-        if (self.fuse_route and self.implicit_root and not self.RM and not self.ROUTE_KERNEL
-                and self.capacity < 32767 and os.environ.get("H2OMX_NID16", "1") == "1"):
+        if (self.fuse_route and self.implicit_root and not self.RM and not self.ROUTE_KERNEL and not self.CMP
+                and self.ROWS_PER_LANE == 16 and self.capacity < 32767
+                and os.environ.get("H2OMX_NID16", "1") == "1"):
             self.nid16 = (torch.full((bm.npad,), -1, dtype=torch.int16, device=d),
                           torch.full((bm.npad,), -1, dtype=torch.int16, device=d))
         # the fixed-point scales (tree_begin) derive from max_rows_per_wg: every rank
