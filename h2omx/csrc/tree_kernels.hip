@@ -1729,7 +1729,8 @@ __global__ __launch_bounds__(1024) void reduce_split_kernel(
     const uint4* q = reinterpret_cast<const uint4*>(src) + bp;
     const int64_t stride = hist_elems / 2;   // uint4 per slab
     int c = c0;
-    // 8 slab loads in flight per lane (wgpg is typically 64-256: one or two batches)
+    // 8 slab loads in flight per lane (wgpg is typically 64-256: one or two
+    // batches; 16 deep measured slower: 10.4-14.8 vs 8-13 us a level)
     for (; c + 7 * LANES < wgpg; c += 8 * LANES) {
       uint4 v[8];
 #pragma unroll
@@ -2356,7 +2357,7 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
                                                         const int* __restrict__ ctl_next, int win_max, int R,
                                                         short* __restrict__ slot16, int* nid_out, int all_rows,
                                                         const float* __restrict__ Fm, const float* __restrict__ yv,
-                                                        GradParams gp) {
+                                                        GradParams gp, const uint8_t* __restrict__ y8) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lacc[];
   __shared__ PartInfo ps[PART_LDS_NODES];
   const bool use_lds = leaf_acc != nullptr && win_max > 0;
@@ -2410,7 +2411,14 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
           // chained graph steps: boost_update no longer stores (g, h); re-derive
           // them from the margins / labels exactly as it did (unweighted rows)
           const float4 f0 = *reinterpret_cast<const float4*>(Fm + r0 + 4 * v);
-          const float4 y0 = *reinterpret_cast<const float4*>(yv + r0 + 4 * v);
+          float4 y0;
+          if (y8 != nullptr) {
+            const uint32_t b4 = *reinterpret_cast<const uint32_t*>(y8 + r0 + 4 * v);
+            y0 = make_float4((float)(b4 & 0xff), (float)((b4 >> 8) & 0xff), (float)((b4 >> 16) & 0xff),
+                             (float)(b4 >> 24));
+          } else {
+            y0 = *reinterpret_cast<const float4*>(yv + r0 + 4 * v);
+          }
           const float fa[4] = {f0.x, f0.y, f0.z, f0.w}, ya[4] = {y0.x, y0.y, y0.z, y0.w};
 #pragma unroll
           for (int k = 0; k < 4; ++k) dist_grad(gp.dist, fa[k], ya[k], gp, gv[4 * v + k], hv[4 * v + k]);
@@ -2789,7 +2797,9 @@ __global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F
                                                            uint4* __restrict__ ring, int ring_n,
                                                            const int* __restrict__ tree_ctr, int ctr_off,
                                                            uint32_t* __restrict__ pk32_out,
-                                                           const double* __restrict__ qs, int s_is_h, int store_gh) {
+                                                           const double* __restrict__ qs, int s_is_h, int store_gh,
+                                                           const uint8_t* __restrict__ y8,
+                                                           const short* __restrict__ nid16) {
   if (ring != nullptr) {
     // graph replay: the applied tree also goes to ring slot (tree_ctr - ctr_off)
     // mod ring_n (tree_archive folded into this launch)
@@ -2802,11 +2812,25 @@ __global__ __launch_bounds__(256) void boost_update_kernel(float* __restrict__ F
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r0 = 4 * q;
     float4 f4 = *reinterpret_cast<const float4*>(F + r0);
-    const float4 y4 = *reinterpret_cast<const float4*>(y + r0);
+    float4 y4;
+    if (y8 != nullptr) {   // 0 / 1 labels as bytes (a quarter of the label traffic)
+      const uint32_t b4 = *reinterpret_cast<const uint32_t*>(y8 + r0);
+      y4 = make_float4((float)(b4 & 0xff), (float)((b4 >> 8) & 0xff), (float)((b4 >> 16) & 0xff), (float)(b4 >> 24));
+    } else {
+      y4 = *reinterpret_cast<const float4*>(y + r0);
+    }
     float4 w4 = make_float4(1.f, 1.f, 1.f, 1.f);
     if (wobs) w4 = *reinterpret_cast<const float4*>(wobs + r0);
     int4 n4 = make_int4(0, 0, 0, 0);
-    if (gp.apply_tree) n4 = *reinterpret_cast<const int4*>(nid + r0);
+    if (gp.apply_tree) {
+      if (nid16 != nullptr) {   // int16 leaf ids (fused pipeline graph steps)
+        const uint2 v = *reinterpret_cast<const uint2*>(nid16 + r0);
+        n4 = make_int4((int)(short)(v.x & 0xffff), (int)(short)(v.x >> 16), (int)(short)(v.y & 0xffff),
+                       (int)(short)(v.y >> 16));
+      } else {
+        n4 = *reinterpret_cast<const int4*>(nid + r0);
+      }
+    }
     float fv[4] = {f4.x, f4.y, f4.z, f4.w}, yv[4] = {y4.x, y4.y, y4.z, y4.w}, wv[4] = {w4.x, w4.y, w4.z, w4.w};
     const int nv[4] = {n4.x, n4.y, n4.z, n4.w};
     float gv[4], hv[4];
@@ -3670,9 +3694,9 @@ static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const 
                             unsigned long long* leaf_acc, const int* ctl_cur, const int* ctl_next, int win_max,
                             int blocks, int prefetch, short* slot16, int* nid_out, int all_rows, hipStream_t stream,
                             const float* Fm = nullptr, const float* yv = nullptr, const GradParams* gpp = nullptr,
-                            int nidm = 0) {
+                            int nidm = 0, const uint8_t* y8 = nullptr) {
   // nidm bit 0: nid is an int16 stream, bit 1: nid_out is (fused pipeline; distinct buffers)
-  if (nidm != 0 && (nid_out == nid || (nidm & 2 && prefetch))) return kBadArg;
+  if (nidm != 0 && nid_out == nid) return kBadArg;
   GradParams gp{};
   if (gpp) gp = *gpp;
   if ((Fm != nullptr) != (gpp != nullptr) || (Fm != nullptr && (yv == nullptr || w != nullptr || !prefetch)))
@@ -3693,9 +3717,10 @@ static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const 
 #define H2OMX_PK(PF, NM, WIN)                                                                                  \
   hipLaunchKernelGGL((partition_kernel<PF, PART_RPL, NM>), dim3(blocks), dim3(256), lds, stream, codes, npad, nid, \
                      reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,        \
-                     ctl_next, WIN, R, slot16, nid_out, all_rows, Fm, yv, gp)
+                     ctl_next, WIN, R, slot16, nid_out, all_rows, Fm, yv, gp, y8)
   if (prefetch && leaf_acc) {
-    if (nidm & 1) H2OMX_PK(true, 1, win_max);
+    if (nidm == 3) H2OMX_PK(true, 3, win_max);
+    else if (nidm & 1) H2OMX_PK(true, 1, win_max);
     else H2OMX_PK(true, 0, win_max);
   } else {
     if (nidm == 3) H2OMX_PK(false, 3, leaf_acc ? win_max : 0);
@@ -3734,12 +3759,12 @@ H2OMX_API int h2omx_partition_final(const uint8_t* codes, int64_t npad, const in
                                     const void* part, int nbt, const float* g, const float* h, const float* w,
                                     const double* qscale, int cap, unsigned long long* leaf_acc, const int* ctl_cur,
                                     const int* ctl_next, int blocks, const float* Fm, const float* y,
-                                    const void* gparams, int nidm, hipStream_t stream) {
+                                    const void* gparams, int nidm, const uint8_t* y8, hipStream_t stream) {
   // Fm / y / gparams (optional): the rows' (g, h) are re-derived from the margins;
   // nidm 1: nid_in is an int16 stream (nid_out stays int32: boost_update reads it)
   return partition_launch(codes, npad, const_cast<int*>(nid_in), part, nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
                           ctl_next, cap, blocks, 1, nullptr, nid_out, 1, stream, Fm, y,
-                          reinterpret_cast<const GradParams*>(gparams), nidm);
+                          reinterpret_cast<const GradParams*>(gparams), nidm, y8);
 }
 
 // route_kernel entry (fused pipeline): final = 1 -> last level (leaf sums of
@@ -3777,14 +3802,15 @@ H2OMX_API int h2omx_boost_update(float* F, const float* y, const float* wobs, in
                                  const void* tree, const void* gparams, float* g, float* h, float* wout,
                                  unsigned int* stat_max, int64_t tree_bytes, void* ring, int ring_n,
                                  const int* tree_ctr, int ctr_off, void* pk32_out, const double* qscale,
-                                 int s_is_h, int store_gh, hipStream_t stream) {
+                                 int s_is_h, int store_gh, const uint8_t* y8, const void* nid16, hipStream_t stream) {
   const GradParams gp = *reinterpret_cast<const GradParams*>(gparams);
   if (ring != nullptr && (tree_bytes % 16 != 0 || ring_n < 1 || tree_ctr == nullptr)) return kBadArg;
   if (pk32_out != nullptr && qscale == nullptr) return kBadArg;
   hipLaunchKernelGGL(boost_update_kernel, dim3(stream_grid(npad)), dim3(256), 0, stream, F, y, wobs, n, npad, nid,
                      reinterpret_cast<const TreeNode*>(tree), gp, g, h, wout, stat_max,
                      reinterpret_cast<const uint4*>(tree), (int)(tree_bytes / 16), reinterpret_cast<uint4*>(ring),
-                     ring_n, tree_ctr, ctr_off, reinterpret_cast<uint32_t*>(pk32_out), qscale, s_is_h, store_gh);
+                     ring_n, tree_ctr, ctr_off, reinterpret_cast<uint32_t*>(pk32_out), qscale, s_is_h, store_gh, y8,
+                     reinterpret_cast<const short*>(nid16));
   return launch_status();
 }
 
@@ -4219,10 +4245,19 @@ __global__ __launch_bounds__(1024) void level_close_kernel(
   }
   __syncthreads();
   // chunks of node i are [pc_first[i], pc_first[i+1]): node-parallel rebase
-  // (a binary search per chunk costs ~17 dependent loads at 10^5 nodes)
-  for (int i = t; i < n; i += blockDim.x) {
-    const int base = node_nl[n + i];
-    for (int c = pc_first[i]; c < pc_first[i + 1]; ++c) pc_left[c] -= base;
+  // (a binary search per chunk costs ~17 dependent loads at 10^5 nodes); few
+  // nodes own thousands of chunks each (10M rows at the root: 2441 chunks, one
+  // thread walking them took 157 us), so they rebase with the whole block
+  if (n <= 64) {
+    for (int i = 0; i < n; ++i) {
+      const int base = node_nl[n + i];
+      for (int c = pc_first[i] + t; c < pc_first[i + 1]; c += blockDim.x) pc_left[c] -= base;
+    }
+  } else {
+    for (int i = t; i < n; i += blockDim.x) {
+      const int base = node_nl[n + i];
+      for (int c = pc_first[i]; c < pc_first[i + 1]; ++c) pc_left[c] -= base;
+    }
   }
   // (c) children segments
   for (int i = t; i < n; i += blockDim.x) {
@@ -4272,11 +4307,8 @@ __global__ __launch_bounds__(1024) void level_close_kernel(
     __syncthreads();
   }
   if (t == 0) { nhc_first[nn] = carry_s[0]; npc_first[nn] = carry_s[1]; }
-  // (e) zero the next level's built histograms
-  if (nbuilt) {
-    const int64_t m = (int64_t)ctl_next[CTL_SLOTS] * per_slot;
-    for (int64_t k = t; k < m; k += blockDim.x) nbuilt[k] = 0ll;
-  }
+  // (e) the next level's built histograms are zeroed by zero_slots_kernel over
+  // the whole chip (13-26 MB at DRF levels 8-9: 186 / 356 us in this one block)
 }
 
 // --- multi-block level close (levels with thousands of nodes) --------------
@@ -5638,6 +5670,8 @@ H2OMX_API int h2omx_level_close(const int* ctl, const int* ctl_next, const void*
                      reinterpret_cast<const PartInfo*>(part), reinterpret_cast<const NodeLink*>(link_next), seg_start,
                      seg_cnt, pc_first, pc_left, node_nl, nseg_start, nseg_cnt, nhc_first, npc_first, nslot_node,
                      hc_rows, nbuilt, per_slot);
+  if (nbuilt)
+    hipLaunchKernelGGL(zero_slots_kernel, dim3(1024), dim3(256), 0, stream, nbuilt, ctl_next, per_slot);
   return launch_status();
 }
 

@@ -360,6 +360,12 @@ class GpuBooster:
                         torch.zeros((bm.npad,), dtype=torch.float32, device=self.dev))
             self.use_graph = False
         self.pending = False
+        # 0 / 1 labels as bytes for the gradient passes (bernoulli; exact as floats)
+        self.y8 = None
+        if self.K == 1 and self.dist == "bernoulli" and os.environ.get("H2OMX_Y8", "1") == "1":
+            yv = self.st.y
+            if bool(((yv == 0) | (yv == 1)).all()):
+                self.y8 = yv.to(torch.uint8)
         self.deferred: list = []  # graph mode: steps held back for a multi-tree replay
         self._archive = None     # TreeGraph capture: (ring, slots, counter offset)
         # bounded gradients (unweighted rows; bagging only zeroes rows) quantise with
@@ -406,6 +412,8 @@ class GpuBooster:
                                                   arch[2] if arch else 0, P(pk), P(b.qscale if pk is not None else None),
                                                   1 if b.p.mode == 1 else 0,
                                                   0 if (arch is not None and b.regrad is not None) else 1,
+                                                  P(self.y8 if y is st.y else None),
+                                                  P(b.leaf16_buf if (arch is not None and apply) else None),
                                                   ops.stream(self.dev)),
                       "boost_update")
             if not fixed:
@@ -724,7 +732,7 @@ class TreeGraph:
             # the final partition re-derives (g, h) from the margins: boost_update
             # stores only the packed rows (8 bytes per row less each way)
             gpr = make_grad_params(gb.dist, False, 1.0, gb.seed, 0, row_base=b.row_base, **gb.kw)
-            b.regrad = (gb.st.Fm[0], gb.st.y, gpr)
+            b.regrad = (gb.st.Fm[0], gb.st.y, gpr, gb.y8)
         try:
             with torch.cuda.stream(side):
                 g = torch.cuda.CUDAGraph()

@@ -706,13 +706,19 @@ class HipTreeBuilder:
                                                     1 if last else 0, st), "route_level")
                 elif fuse and last:
                     rg = self.regrad if (chain and w is None) else None   # (F, y, GradParams)
-                    ops.check(lib.h2omx_partition_final(P(bm.codes), bm.npad, P(nid_buf[d % 2]), P(self.nid),
+                    # chained graph steps: int16 leaf ids into the free node-id buffer
+                    # for boost_update; otherwise int32 into self.nid
+                    leaf16 = chain and nid16
+                    self.leaf16_buf = nid_buf[(d + 1) % 2] if leaf16 else None
+                    ops.check(lib.h2omx_partition_final(P(bm.codes), bm.npad, P(nid_buf[d % 2]),
+                                                        P(self.leaf16_buf if leaf16 else self.nid),
                                                         P(part), nbt, P(g), P(h), P(w), P(self.qscale),
                                                         self.capacity, P(self.leaf_acc), P(ctl_cur), P(ctl_nxt),
                                                         self.part_blocks, P(rg[0] if rg else None),
                                                         P(rg[1] if rg else None),
                                                         ctypes.addressof(rg[2]) if rg else None,
-                                                        1 if nid16 else 0, st),
+                                                        (3 if leaf16 else 1) if nid16 else 0,
+                                                        P(rg[3] if rg else None), st),
                               "partition_final")
                 elif fuse and not self._fused_level(d + 1):
                     ops.check(lib.h2omx_partition_route(P(bm.codes), bm.npad, P(nid_buf[d % 2]),
@@ -758,8 +764,9 @@ class HipTreeBuilder:
     PK_IN_BOOST = os.environ.get("H2OMX_PK_IN_BOOST", "1") == "1"
     pk_in_boost = False
     # chained graph steps of unweighted rows: boost_update stores no (g, h); the
-    # final partition re-derives them from (margins, labels, GradParams)
+    # final partition re-derives them from (margins, labels, GradParams, byte labels)
     regrad = None
+    leaf16_buf = None   # int16 leaf ids of the last chained tree (boost_update reads them)
 
     def can_pack_in_boost(self) -> bool:
         return (self.PK_IN_BOOST and self.pk32 and self.implicit_root and not self.segmented and not self.COMPACT

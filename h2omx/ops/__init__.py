@@ -31,11 +31,11 @@ TREE_SIGS = {
     "h2omx_split_find_fin": "PPPPPPPPPIIPPPPIPPPIPS",
     "h2omx_partition": "PLPPIPPPPIPPPIIIPS",
     "h2omx_partition_blocks": "",
-    "h2omx_partition_final": "PLPPPIPPPPIPPPIPPPIS",
+    "h2omx_partition_final": "PLPPPIPPPPIPPPIPPPIPS",
     "h2omx_partition_route": "PLPPPIPPIPIS",
     "h2omx_route_level": "PLPPPIPPPPIPPIIPIS",
     "h2omx_leaf_reduce": "PIIPS",
-    "h2omx_boost_update": "PPPLLPPPPPPPLPIPIPPIIS",
+    "h2omx_boost_update": "PPPLLPPPPPPPLPIPIPPIIPPS",
     "h2omx_apply_tree": "PLPPS",
     "h2omx_tree_archive": "PLPIPS",
     "h2omx_sketch_bins": "",
