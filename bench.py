@@ -376,7 +376,7 @@ def _mlp(args, comm, torch, np):
 
     def step():
         if trainer is not None:
-            trainer.step()
+            trainer.step_deferred()     # (grouped graph replays; flushed inside the timed window)
             return
         i = state["i"] % nb
         state["i"] += 1
@@ -398,7 +398,7 @@ def _mlp(args, comm, torch, np):
     _sync(torch, dev)
     comm.barrier()
     setup_s = time.perf_counter() - t_setup
-    elapsed = _timed(step, args, comm, torch, dev)
+    elapsed = _timed(step, args, comm, torch, dev, finish=trainer.flush if trainer is not None else None)
     if trainer is not None:
         trainer.sync()
     with torch.no_grad():

@@ -4016,7 +4016,8 @@ __global__ __launch_bounds__(512) void hist_build_seg_kernel(
     const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
     const int* __restrict__ hc_first, const int* __restrict__ ctl, const int* __restrict__ nvb,
     const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups, int hc_rows,
-    unsigned long long* __restrict__ slab, int gpos, const uint8_t* __restrict__ crow) {
+    unsigned long long* __restrict__ slab, int gpos, const uint8_t* __restrict__ crow,
+    const int* __restrict__ cpos) {
   salt = (uint32_t)qscale[9];  // per-tree dither salt, written by tree_begin (graph-replay safe)
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
   __shared__ int width_s[256], rep_s[256];
@@ -4061,7 +4062,8 @@ __global__ __launch_bounds__(512) void hist_build_seg_kernel(
     const uint32_t sq = (uint32_t)floorf(fmaf(sv, ss, d2));
     const unsigned long long pk = ((unsigned long long)(uint32_t)gq << 32) | (unsigned long long)sq;
     if (pk == 0ull) continue;
-    const uint32_t* row = reinterpret_cast<const uint32_t*>((crow ? crow + (int64_t)j * fp : codes_rm + (int64_t)r * fp) + f0);
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(
+        (crow ? crow + (int64_t)(cpos ? cpos[j] : j) * fp : codes_rm + (int64_t)r * fp) + f0);
     for (int wq = 0; wq < nw; ++wq) {
       const uint32_t cw = row[wq];
 #pragma unroll
@@ -4135,6 +4137,8 @@ struct SegRows {
   const uint8_t* in;
   uint8_t* out;
   int fp;
+  const int* cpos_in;   // row j's position in `in` (nullptr = j)
+  int* cpos_out;        // rows stay put: the next level's positions (moved like idx)
 };
 
 // The wave's rows (lane i: row r / segment position j -> segment position dst,
@@ -4163,7 +4167,8 @@ __device__ __forceinline__ void seg_move_rows_wave(const SegRows& sr, const uint
 
 __device__ __forceinline__ int seg_split_dir(const uint8_t* __restrict__ codes, int64_t npad, const PartInfo& pi,
                                              int nbt, int r, int j, const SegRows& sr) {
-  if (sr.in != nullptr) return part_right(pi, sr.in[(int64_t)j * sr.fp + pi.feat], nbt);
+  if (sr.in != nullptr)
+    return part_right(pi, sr.in[(int64_t)(sr.cpos_in ? sr.cpos_in[j] : j) * sr.fp + pi.feat], nbt);
   return split_dir(codes, npad, pi, nbt, r);
 }
 
@@ -4577,7 +4582,16 @@ struct ECodes {
   int stride;       // 8 or 16 bytes per row
   int* nodeq;
   const uint8_t* crow;   // code rows in segment order (SegRows::in), nullptr = gather codes_rm by row id
+  const int* cpos;       // row j's position in crow (rows moved once, then only positions), nullptr = j
 };
+
+// XCD-aware block order: dispatch puts block b on XCD b % 8; renumber so XCD x
+// takes the contiguous range [x * g / 8, (x + 1) * g / 8) - neighbouring
+// nodes (descendants of one ancestor, whose code rows sit together once the
+// rows were moved) then share an L2.  g must be a multiple of 8 (the host pads).
+__device__ __forceinline__ int xcd_block(int b, int g) {
+  return ((g & 7) == 0) ? (b & 7) * (g >> 3) + (b >> 3) : b;
+}
 
 template <typename FL>
 __device__ __forceinline__ int direct_feat_pos(const FL* flist, int nfl, long long key) {
@@ -4658,7 +4672,7 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
   __shared__ long long tot_s[2][4];
   __shared__ double wb_gain[4], wb_GL[4], wb_SL[4];
   __shared__ long long wb_key[4];
-  const int node = blockIdx.x;
+  const int node = ec.crow ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   if (node >= ctl[CTL_N]) return;
   const int F = p.F;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -4716,7 +4730,7 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
     __syncthreads();
     for (int j = lo + t; j < lo + cnt; j += blockDim.x) {
       const int r = idx ? idx[j] : j;
-      const uint8_t* row = ec.crow ? ec.crow + (int64_t)j * fp : codes_rm + (int64_t)r * fp;
+      const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * fp : codes_rm + (int64_t)r * fp;
       uint32_t c0[DIRECT_FB];
 #pragma unroll
       for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
@@ -4864,7 +4878,7 @@ __global__ __launch_bounds__(256) void direct_dp_hist_kernel(
     SplitParams p, int batch, int node0, int max_elig, long long* __restrict__ dh, int gpos,
     const uint8_t* __restrict__ crow) {
   extern __shared__ __attribute__((aligned(16))) long long hist[];   // [batch][2][NBT]
-  const ECodes ec{nullptr, 0, nullptr, crow};
+  const ECodes ec{nullptr, 0, nullptr, crow, nullptr};
   __shared__ int flist[1024];
   __shared__ uint32_t hsh_s[1024];
   __shared__ int nfl_s;
@@ -4893,7 +4907,7 @@ __global__ __launch_bounds__(256) void direct_dp_hist_kernel(
     __syncthreads();
     for (int j = lo + t; j < lo + cnt; j += blockDim.x) {
       const int r = idx ? idx[j] : j;
-      const uint8_t* row = ec.crow ? ec.crow + (int64_t)j * fp : codes_rm + (int64_t)r * fp;
+      const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * fp : codes_rm + (int64_t)r * fp;
       uint32_t c0[DIRECT_FB];
 #pragma unroll
       for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
@@ -4995,7 +5009,7 @@ __global__ __launch_bounds__(256) void seg_direct_chunk_kernel(
   __shared__ double wb_gain[4], wb_GL[4], wb_SL[4];
   __shared__ long long wb_key[4];
   const int n = ctl[CTL_N];
-  const int c = blockIdx.x;
+  const int c = ec.crow ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   if (c >= pc_first[n]) return;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   if (wid == 0) {
@@ -5017,7 +5031,7 @@ __global__ __launch_bounds__(256) void seg_direct_chunk_kernel(
   long long tg_row = 0, ts_row = 0;
   for (int j = lo + t; j < hi; j += blockDim.x) {
     const int r = idx ? idx[j] : j;
-    const uint8_t* row = ec.crow ? ec.crow + (int64_t)j * fp : codes_rm + (int64_t)r * fp;
+    const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * fp : codes_rm + (int64_t)r * fp;
     uint32_t cc[DIRECT_FB];
 #pragma unroll
     for (int u = 0; u < DIRECT_FB; ++u) cc[u] = (u < nfl) ? row[flist[u]] : 0u;
@@ -5117,7 +5131,7 @@ __global__ __launch_bounds__(256) void seg_direct_wave_kernel(
   extern __shared__ __attribute__((aligned(16))) long long hist_all[];   // [4][batch * 2 * NBT]
   __shared__ short flist_all[4][DIRECT_WAVE_F];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int node = blockIdx.x * 4 + wid;
+  const int node = (ec.crow ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + wid;
   if (node >= ctl[CTL_N]) return;   // whole wave: no workgroup barrier below
   long long* hist = hist_all + wid * batch * 2 * NBT;
   short* flist = flist_all[wid];
@@ -5173,7 +5187,7 @@ __global__ __launch_bounds__(256) void seg_direct_wave_kernel(
     wave_lds_sync();
     for (int j = lo + lane; j < lo + cnt; j += 64) {
       const int r = idx ? idx[j] : j;
-      const uint8_t* row = ec.crow ? ec.crow + (int64_t)j * fp : codes_rm + (int64_t)r * fp;
+      const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * fp : codes_rm + (int64_t)r * fp;
       uint32_t c0[DIRECT_FB];
 #pragma unroll
       for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
@@ -5275,6 +5289,7 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
       if (valid) {
         const int pos = goes_left ? base_l + my_l : nl + base_r + (my_v - my_l);
         idx_out[start + pos] = r;
+        if (sr.cpos_out) sr.cpos_out[start + pos] = sr.cpos_in ? sr.cpos_in[j] : j;
         if (write_nid) nid[r] = pi.child + dir;
         if (gout) {   // the (g, s2) the next level reads, moved with the row into segment order
           gout[start + pos] = gin[j];
@@ -5420,6 +5435,7 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
         const int my_l = __popcll(bl & lt), my_v = __popcll(bv & lt);
         const int pos = dir == 0 ? base_l + my_l : nl + base_r + (my_v - my_l);
         idx_out[start + pos] = r;
+        if (sr.cpos_out) sr.cpos_out[start + pos] = sr.cpos_in ? sr.cpos_in[j] : j;
         if (write_nid) nid[r] = pi.child + dir;
         if (gout) {
           gout[start + pos] = gin[j];
@@ -5494,7 +5510,8 @@ H2OMX_API int h2omx_hist_build_seg(const uint8_t* codes_rm, int fp, const int* i
                                    const int* seg_start, const int* seg_cnt, const int* hc_first, const int* ctl,
                                    const int* nvb, const double* qscale, int salt, int F, int nbt, int fg,
                                    int n_groups, int hc_rows, int max_chunks, int threads,
-                                   unsigned long long* slab, int gpos, const uint8_t* crow, hipStream_t stream) {
+                                   unsigned long long* slab, int gpos, const uint8_t* crow, const int* cpos,
+                                   hipStream_t stream) {
   if (fg > 256 || threads > 512 || threads % 64 || threads < fg || fp % 4 || (n_groups > 1 && fg % 4) ||
       hc_rows > ROWS_CAP)
     return kBadArg;
@@ -5504,7 +5521,7 @@ H2OMX_API int h2omx_hist_build_seg(const uint8_t* codes_rm, int fp, const int* i
 #define H2OMX_HBS(NB)                                                                                        \
   hipLaunchKernelGGL(hist_build_seg_kernel<NB>, dim3(grid), dim3(threads), lds, stream, codes_rm, fp, idx, g, s2, \
                      seg_start, seg_cnt, hc_first, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, hc_rows, slab, \
-                     gpos, crow)
+                     gpos, crow, cpos)
   switch (nbt) {
     case 32: H2OMX_HBS(32); break;
     case 64: H2OMX_HBS(64); break;
@@ -5529,9 +5546,10 @@ H2OMX_API int h2omx_hist_reduce_seg(const unsigned long long* slab, const int* h
 H2OMX_API int h2omx_part_count(const uint8_t* codes, int64_t npad, const int* idx, const int* seg_start,
                                const int* seg_cnt, const int* pc_first, const int* ctl, const void* part, int nbt,
                                int max_chunks, int* pc_left, int wave, int8_t* dirb, const uint8_t* ecodes,
-                               int ecs, const int* nodeq, const uint8_t* crow, int fp, hipStream_t stream) {
+                               int ecs, const int* nodeq, const uint8_t* crow, int fp, const int* cpos,
+                               hipStream_t stream) {
   if (ecodes && !wave) return kBadArg;
-  const SegRows sr{crow, nullptr, fp};
+  const SegRows sr{crow, nullptr, fp, cpos, nullptr};
   if (wave) {
     hipLaunchKernelGGL(part_count_wave_kernel, dim3((max_chunks + 3) / 4), dim3(256), 0, stream, codes, npad, idx,
                        seg_start, seg_cnt, pc_first, ctl, reinterpret_cast<const PartInfo*>(part), nbt, pc_left, dirb,
@@ -5548,9 +5566,11 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
                                const uint8_t* tree_fmask, const double* qscale, int salt, const void* params, int nbt,
                                int max_nodes, int mode, const int* pc_first, int max_pc, unsigned long long* slab,
                                long long* tot_slab, int* ticket, void* nsplit, int gpos, uint8_t* ecodes, int ecs,
-                               int* nodeq, const uint8_t* crow, hipStream_t stream) {
+                               int* nodeq, const uint8_t* crow, const int* cpos, hipStream_t stream) {
   if (ecodes && ecs != 8 && ecs != 16) return kBadArg;
-  const ECodes ec{ecodes, ecs, nodeq, crow};
+  const ECodes ec{ecodes, ecs, nodeq, crow, cpos};
+  // moved code rows: XCD-aware block order over grids padded to a multiple of 8
+  auto pad8 = [&](int g) { return crow ? (g + 7) / 8 * 8 : g; };
   // mode 0: one workgroup per node, 1: one wave per node (F <= 256),
   // 2: one workgroup per PC_ROWS chunk (slab / tot_slab: max_pc x max_elig x
   //    nbt and max_pc x 2 int64, ticket: max_nodes zeroed ints)
@@ -5566,7 +5586,7 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
     hipLaunchKernelGGL(direct_empty_kernel, dim3((max_nodes + 255) / 256), dim3(256), 0, stream, seg_cnt, ctl, ns);
     const size_t lds = (size_t)max_elig * per_f_bytes;
 #define H2OMX_SDC(NB)                                                                                            \
-  hipLaunchKernelGGL(seg_direct_chunk_kernel<NB>, dim3(max_pc), dim3(256), lds, stream, codes_rm, fp, idx, g, s2, \
+  hipLaunchKernelGGL(seg_direct_chunk_kernel<NB>, dim3(pad8(max_pc)), dim3(256), lds, stream, codes_rm, fp, idx, g, s2, \
                      seg_start, seg_cnt, pc_first, ctl, nvb, tree_fmask, qscale, (uint32_t)salt, p, max_elig, slab, \
                      tot_slab, ticket, ns, gpos, ec)
     switch (nbt) {
@@ -5583,7 +5603,7 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
     const int batch = std::max(1, std::min(max_elig, DIRECT_WAVE_LDS / per_f_bytes));
     const size_t lds = (size_t)4 * batch * per_f_bytes;
 #define H2OMX_SDW(NB)                                                                                              \
-  hipLaunchKernelGGL(seg_direct_wave_kernel<NB>, dim3((max_nodes + 3) / 4), dim3(256), lds, stream, codes_rm, fp, \
+  hipLaunchKernelGGL(seg_direct_wave_kernel<NB>, dim3(pad8((max_nodes + 3) / 4)), dim3(256), lds, stream, codes_rm, fp, \
                      idx, g, s2, seg_start, seg_cnt, ctl, nvb, tree_fmask, qscale, (uint32_t)salt, p, batch, ns, gpos, ec)
     switch (nbt) {
       case 32: H2OMX_SDW(32); break;
@@ -5598,7 +5618,7 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
   const int batch = std::max(1, std::min(max_elig, DIRECT_LDS_BYTES / per_f_bytes));
   const size_t lds = (size_t)batch * per_f_bytes;
 #define H2OMX_SD(NB)                                                                                             \
-  hipLaunchKernelGGL(seg_direct_kernel<NB>, dim3(max_nodes), dim3(64 * DIRECT_WAVES), lds, stream, codes_rm, fp, \
+  hipLaunchKernelGGL(seg_direct_kernel<NB>, dim3(pad8(max_nodes)), dim3(64 * DIRECT_WAVES), lds, stream, codes_rm, fp, \
                      idx, g, s2,                                                                                 \
                      seg_start, seg_cnt, ctl, nvb, tree_fmask, qscale, (uint32_t)salt, p, batch, ns, gpos, ec)
   switch (nbt) {
@@ -5716,11 +5736,15 @@ H2OMX_API int h2omx_part_scatter(const uint8_t* codes, int64_t npad, const int* 
                                  unsigned long long* leaf_acc, int max_chunks, int wave, const int8_t* dirb,
                                  const float* gin, const float* sin, float* gout, float* sout,
                                  const uint8_t* ecodes, int ecs, const int* nodeq, const uint8_t* codes_rm,
-                                 const uint8_t* crow_in, uint8_t* crow_out, int fp, hipStream_t stream) {
+                                 const uint8_t* crow_in, uint8_t* crow_out, int fp, const int* cpos_in, int* cpos_out,
+                                 hipStream_t stream) {
   // crow_out: move every inner row's code row into the next level's segment order
-  // (source crow_in by position, or codes_rm by row id when crow_in is nullptr)
-  const SegRows sr{crow_in, crow_out, fp};
-  if (crow_out != nullptr && ((crow_in == nullptr && codes_rm == nullptr) || fp % 4 != 0)) return kBadArg;
+  // (source crow_in by position, or codes_rm by row id when crow_in is nullptr);
+  // cpos_out: the rows stay where they are in crow_in, their positions move
+  const SegRows sr{crow_in, crow_out, fp, cpos_in, cpos_out};
+  if (crow_out != nullptr && ((crow_in == nullptr && codes_rm == nullptr) || fp % 4 != 0 || cpos_in || cpos_out))
+    return kBadArg;
+  if (cpos_out != nullptr && crow_in == nullptr) return kBadArg;
   // wave: bit 0 wave-granular kernel; bits 1-2 its segf flags (last level)
   const int segf = wave >> 1;
   wave &= 1;

@@ -294,6 +294,8 @@ class _DLTrainer:
         self.perm = None
         self.spi = None      # steps per iteration (model averaging)
         self.graph = None
+        self.graph_g = None
+        self.pending = 0
         self.idx_buf = None
         self._t0 = None
         if self.avg:
@@ -323,6 +325,58 @@ class _DLTrainer:
         return (self.X.is_cuda and self.adaptive and self.drop_in == 0 and not any(self.hd) and self.l1 == 0
                 and not math.isfinite(float(self.p["max_w2"])) and not self.sync_grad
                 and os.environ.get("H2OMX_DL_GRAPH", "1") == "1")
+
+    # single-GPU graph replays: GROUP consecutive mini-batches per launch (the
+    # inter-graph gap and the per-step index copy paid once per group)
+    GROUP = int(os.environ.get("H2OMX_DL_GRAPH_STEPS", "4"))
+
+    def step_deferred(self) -> None:
+        """step(), possibly held back so GROUP steps replay as one graph;
+        readers of the weights call flush() first (the training loop does at
+        every scoring point, bench.py inside its timed window)."""
+        if self.graph is None or self.world != 1 or self.GROUP <= 1:
+            self.flush()
+            self.step()
+            return
+        self.pending += 1
+        e_pos = (self.n_steps + self.pending - 1) % self.steps_per_epoch
+        if e_pos == self.steps_per_epoch - 1 or self.pending == self.GROUP:
+            self.flush()
+
+    def flush(self) -> None:
+        k = getattr(self, "pending", 0)
+        self.pending = 0
+        if k <= 0:
+            return
+        e_pos = self.n_steps % self.steps_per_epoch
+        if k == self.GROUP and e_pos != 0 and e_pos + k <= self.steps_per_epoch:
+            self._group_replay(e_pos, k)
+        else:
+            for _ in range(k):
+                self.step()
+
+    def _group_replay(self, e_pos: int, k: int) -> None:
+        M = self.M
+        if self.graph_g is None:
+            self.idx_g = torch.empty((k * M,), dtype=self.idx_buf.dtype, device=self.idx_buf.device)
+            self.idx_g.copy_(self.perm[e_pos * M:(e_pos + k) * M])
+            g = torch.cuda.CUDAGraph()
+            gc_was = gc.isenabled()
+            gc.disable()
+            try:
+                with torch.cuda.graph(g):
+                    for i in range(k):
+                        self._body(self.idx_g[i * M:(i + 1) * M])
+            finally:
+                if gc_was:
+                    gc.enable()
+            self.graph_g = g
+        else:
+            self.idx_g.copy_(self.perm[e_pos * M:(e_pos + k) * M])
+        self.graph_g.replay()
+        self.samples += M * self.world * k
+        self.n_steps += k
+        self.since_sync += k
 
     def step(self) -> None:
         p_, M = self.p, self.M
@@ -644,10 +698,11 @@ class H2ODeepLearningEstimator(ModelBuilder):
                         len(hidden), backward=self._backward)
         step = -1
         for step in range(total_steps):
-            tr.step()
+            tr.step_deferred()
             if job is not None:
                 job.progress = (step + 1) / total_steps
             if (step + 1) % score_every == 0 or step == total_steps - 1:
+                tr.flush()
                 tr.sync()     # replicas agree before they are scored
                 ent = self._score_entry(model, X, Y, cls, auto, epochs_done + (step + 1) / steps_per_epoch,
                                         tr.samples, comm)
@@ -660,6 +715,7 @@ class H2ODeepLearningEstimator(ModelBuilder):
                     cancel = float(comm.all_reduce_numpy(np.array([cancel]), "max")[0])
                 if stop or cancel > 0:
                     break
+        tr.flush()
         tr.sync()
         model.train_samples_per_iteration = tr.samples_per_iteration()
         model.scoring_history = history

@@ -791,11 +791,15 @@ class HipTreeBuilder:
 
     # segmented engine: move the row-major code rows with their segments once the
     # next level reads rows by segment (direct levels: a random cache line per
-    # row otherwise); "direct" / "seg" / "0" (off)
+    # row otherwise); "direct" / "seg" (copy every level) / "once" / "0" (off)
     MOVE_ROWS = os.environ.get("H2OMX_MOVE_ROWS", "0")
 
     def _move_rows(self, crow, next_direct: bool, next_seg_hist: bool) -> bool:
-        if self.MOVE_ROWS == "0" or self.segmented is False:
+        """Route with code-row moves (MOVE_ROWS direct / seg: every level from the
+        first reader on; once: copy at the first direct level, afterwards only
+        the rows' positions move - deeper nodes read inside their ancestor's
+        contiguous block, which the XCD-aware direct grids keep in one L2)."""
+        if self.MOVE_ROWS == "0" or self.segmented is False or (self.comm is not None and self.comm.world_size > 1):
             return False
         if crow["cur"] is not None:
             return True
@@ -858,7 +862,7 @@ class HipTreeBuilder:
         # (part_scatter moves them with the rows, so the histogram passes read them contiguously)
         gs = {"g": g, "s": s2, "pos": 0}
         # row-major code rows in the current level's segment order (MOVE_ROWS), None = gather by row id
-        crow = {"cur": None}
+        crow = {"cur": None, "pos": None}   # pos: rows' positions in cur (MOVE_ROWS=once), None = j
 
         def route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first, ctl_cur, ctl_nxt,
                   idx_in, next_direct, ec=None, move=False):
@@ -890,7 +894,8 @@ class HipTreeBuilder:
                     nbuilt = B("built", max_nodes * self.per_node, torch.int64)
                 ops.check(lib.h2omx_part_count(P(bm.codes), bm.npad, P(idx_in), P(seg_start), P(seg_cnt),
                                                P(pc_first), P(ctl_cur), P(part), nbt, max_pc, P(pc_left), pwave,
-                                               P(dirb), P(ecodes), ecs, P(nodeq), P(crow["cur"]), bm.fp, st),
+                                               P(dirb), P(ecodes), ecs, P(nodeq), P(crow["cur"]), bm.fp,
+                                               P(crow["pos"]), st),
                           "part_count")
                 if max_nodes <= self.CLOSE_SINGLE_BLOCK:
                     ops.check(lib.h2omx_level_close(P(ctl_cur), P(ctl_nxt), P(part), P(nl), P(seg_start),
@@ -918,18 +923,26 @@ class HipTreeBuilder:
             if not last and self.PERMUTE_GS:
                 gout = B(f"gperm{d % 2}", n + 64, torch.float32)
                 sout = None if s2 is None else B(f"sperm{d % 2}", n + 64, torch.float32)
-            crow_out = None
+            crow_out = cpos_out = None
             if move and not last:
-                # the next level's code rows in its segment order (double-buffered)
-                crow_out = B(f"crow{d % 2}", (n + 1) * bm.fp, torch.uint8)
+                if self.MOVE_ROWS == "once" and crow["cur"] is not None:
+                    # rows moved once: only their positions follow the segments
+                    cpos_out = B(f"cpos{d % 2}", n + 64, i32)
+                else:
+                    # the next level's code rows in its segment order (double-buffered)
+                    crow_out = B(f"crow{d % 2}", (n + 1) * bm.fp, torch.uint8)
             ops.check(lib.h2omx_part_scatter(P(bm.codes), bm.npad, P(idx_in), P(idx_out), P(self.nid), write_nid,
                                              P(seg_start), P(seg_cnt), P(pc_first), P(pc_left), P(node_nl),
                                              P(ctl_cur), P(part), nbt, P(g), P(h), P(w), P(self.qscale),
                                              self.capacity, P(self.leaf_acc), max_pc, pwave | segf, P(dirb), P(gs["g"]),
                                              P(gs["s"]), P(gout), P(sout), P(ecodes), ecs, P(nodeq),
-                                             P(self.codes_rm), P(crow["cur"]), P(crow_out), bm.fp, st),
+                                             P(self.codes_rm), P(crow["cur"]), P(crow_out), bm.fp,
+                                             P(crow["pos"]), P(cpos_out), st),
                       "part_scatter")
-            crow["cur"] = crow_out
+            if cpos_out is not None:
+                crow["pos"] = cpos_out
+            else:
+                crow["cur"], crow["pos"] = crow_out, None
             if crow_out is not None:
                 self.stats["moved_row_levels"] = self.stats.get("moved_row_levels", 0) + 1
             if gout is not None:
@@ -1004,7 +1017,8 @@ class HipTreeBuilder:
                                                    P(seg_start), P(seg_cnt), P(ctl_cur), P(bm.nvb), P(tree_fmask),
                                                    P(self.qscale), tree_index & 0x7FFFFFFF, spp, nbt, max_nodes,
                                                    dmode, P(pc_first), max_pc, P(slab), P(tot_slab), P(ticket),
-                                                   P(nsplit), gs["pos"], P(ecodes), ecs, P(nodeq), P(crow["cur"]), st),
+                                                   P(nsplit), gs["pos"], P(ecodes), ecs, P(nodeq), P(crow["cur"]),
+                                                   P(crow["pos"]), st),
                               "seg_direct")
                 ops.check(lib.h2omx_level_finalize_ns(P(nsplit), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
                                                       P(bm.nvb), nbt, next_nodes, P(part), P(nl), P(self.tree_buf),
@@ -1028,7 +1042,7 @@ class HipTreeBuilder:
                                                    P(seg_start), P(seg_cnt), P(hc_first), P(ctl_cur), P(bm.nvb),
                                                    P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, self.seg_fg,
                                                    self.seg_groups, self.hc_rows, max_hc, self.seg_threads, P(slab),
-                                                   gs["pos"], P(crow["cur"]), st), "hist_build_seg")
+                                                   gs["pos"], P(crow["cur"]), P(crow["pos"]), st), "hist_build_seg")
                 ksplit = max(1, min(32, 4096 // max(1, max_slots * ((F * nbt + 255) // 256))))
                 ksplit = max(ksplit, 4)
                 ops.check(lib.h2omx_hist_reduce_seg(P(slab), P(hc_first), P(slot_node), P(ctl_cur), F, nbt,

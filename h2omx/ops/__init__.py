@@ -53,13 +53,13 @@ TREE_SIGS = {
     "h2omx_predict_binned": "PLLPPIIIPLPS",
     "h2omx_pc_rows": "",
     "h2omx_tree_begin_seg": "PIIPPPPIPIIIPPPPPLIPS",
-    "h2omx_hist_build_seg": "PIPPPPPPPPPIIIIIIIIPIPS",
+    "h2omx_hist_build_seg": "PIPPPPPPPPPIIIIIIIIPIPPS",
     "h2omx_hist_reduce_seg": "PPPPIIIIIIPS",
-    "h2omx_part_count": "PLPPPPPPIIPIPPIPPIS",
+    "h2omx_part_count": "PLPPPPPPIIPIPPIPPIPS",
     "h2omx_level_close": "PPPPPPPPPPPPPPIPIS",
     "h2omx_level_close_mb": "PPPPPPPPPPPPPPIPIIIPPPPPS",
-    "h2omx_part_scatter": "PLPPPIPPPPPPPIPPPPIPIIPPPPPPIPPPPIS",
-    "h2omx_seg_direct": "PIPPPPPPPPPIPIIIPIPPPPIPIPPS",
+    "h2omx_part_scatter": "PLPPPIPPPPPPPIPPPPIPIIPPPPPPIPPPPIPPS",
+    "h2omx_seg_direct": "PIPPPPPPPPPIPIIIPIPPPPIPIPPPS",
     "h2omx_level_finalize_ns": "PPPPPPIIPPPIIPS",
     "h2omx_direct_dp_stride": "PI",
     "h2omx_direct_dp": "IPIPPPPPPPPPPIIIPPIPS",

@@ -277,7 +277,9 @@ def test_direct_deep_levels_match_subtraction(cuda_dev, monkeypatch, dist, depth
                 (2, 0, True, 1 << 30, True, True, True, "0"), (64, 0, True, 1 << 30, False, False, True, "0"),
                 (64, 1 << 30, True, 1, True, True, False, "0"), (64, 1 << 30, False, 2048, True, False, True, "0"),
                 (2, 0, True, 1 << 30, True, True, True, "seg"), (64, 1 << 30, True, 1, True, True, False, "direct"),
-                (64, 0, True, 1 << 30, False, False, True, "seg"), (0, 0, True, 1, True, True, True, "seg")):
+                (64, 0, True, 1 << 30, False, False, True, "seg"), (0, 0, True, 1, True, True, True, "seg"),
+                (2, 0, True, 1 << 30, True, True, True, "once"), (64, 1 << 30, True, 1, True, True, False, "once"),
+                (64, 0, True, 1 << 30, True, True, True, "once")):
         for k, v in zip(keys, cfg):
             monkeypatch.setattr(E.HipTreeBuilder, k, v)
         out[cfg] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
