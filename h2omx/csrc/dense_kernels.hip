@@ -837,13 +837,16 @@ __global__ __launch_bounds__(256) void kmeans_onehot_kernel(const int* __restric
     OH[(int64_t)c * m + r] = (assign[r] == c) ? 1.0f : 0.0f;
 }
 
+// OutT float: the fp64 sum rounded once into an fp32 destination (a bias
+// gradient written in place: no separate fp64 -> fp32 copy launch)
+template <typename OutT = double>
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int n_slabs, int width,
-                                                       double* __restrict__ out) {
+                                                       OutT* __restrict__ out) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= width) return;
   double acc = 0.0;
   for (int s = 0; s < n_slabs; ++s) acc += slab[(int64_t)s * width + j];
-  out[j] = acc;
+  out[j] = (OutT)acc;
 }
 
 // Many slabs of a narrow width (per-wave K-Means slabs: ~1000 x 1020): one
@@ -2229,7 +2232,14 @@ H2OMX_API int h2omx_slab_sum(const float* slab, int n_slabs, int width, double* 
   if (n_slabs >= 64 && width < 64 * 1024)   // narrow and deep: column x slab-group parallel
     hipLaunchKernelGGL(slab_sum_wide_kernel, dim3(cdiv(width, 32)), dim3(1024), 0, stream, slab, n_slabs, width, out);
   else
-    hipLaunchKernelGGL(slab_sum_kernel, dim3(cdiv(width, 256)), dim3(256), 0, stream, slab, n_slabs, width, out);
+    hipLaunchKernelGGL(slab_sum_kernel<double>, dim3(cdiv(width, 256)), dim3(256), 0, stream, slab, n_slabs, width,
+                       out);
+  return launch_status();
+}
+
+// fp64 column sums of fp32 slabs rounded into an fp32 vector (few slabs)
+H2OMX_API int h2omx_slab_sum_f32(const float* slab, int n_slabs, int width, float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(slab_sum_kernel<float>, dim3(cdiv(width, 256)), dim3(256), 0, stream, slab, n_slabs, width, out);
   return launch_status();
 }
 

@@ -328,7 +328,7 @@ class _DLTrainer:
 
     # single-GPU graph replays: GROUP consecutive mini-batches per launch (the
     # inter-graph gap and the per-step index copy paid once per group)
-    GROUP = int(os.environ.get("H2OMX_DL_GRAPH_STEPS", "4"))
+    GROUP = int(os.environ.get("H2OMX_DL_GRAPH_STEPS", "8"))
 
     def step_deferred(self) -> None:
         """step(), possibly held back so GROUP steps replay as one graph;

@@ -72,6 +72,7 @@ DENSE_SIGS = {
     "h2omx_glm_irls_wave": "PLLPPPPPPILPPS",
     "h2omx_slab_reduce16": "PIIPS",
     "h2omx_slab_sum": "PIIPS",
+    "h2omx_slab_sum_f32": "PIIPS",
     "h2omx_kmeans": "PLLIPPIIPPS",
     "h2omx_kmeans_wave": "PLLIPPPIIIIPPS",
     "h2omx_glm_wz": "PLPPPPPPPPIS",

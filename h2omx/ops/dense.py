@@ -521,9 +521,12 @@ def wgrad_bias(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Te
     bws, bsplits = bpart
     if S < 2 or _lib_small_ok(M, N, K, 0, 0.0, None):
         gemm(dZ, H, ta=True, out=dW)
-        tmp = torch.empty((M,), dtype=torch.float64, device=dZ.device)
-        check(dense_lib().h2omx_slab_sum(P(bws), bsplits, M, P(tmp), stream(dZ.device)), "slab_sum")
-        db.copy_(tmp)
+        if db.dtype == torch.float32 and db.is_contiguous():
+            check(dense_lib().h2omx_slab_sum_f32(P(bws), bsplits, M, P(db), stream(dZ.device)), "slab_sum_f32")
+        else:
+            tmp = torch.empty((M,), dtype=torch.float64, device=dZ.device)
+            check(dense_lib().h2omx_slab_sum(P(bws), bsplits, M, P(tmp), stream(dZ.device)), "slab_sum")
+            db.copy_(tmp)
         return
     ws = _workspace(dZ.device, S * M * N)
     check(dense_lib().h2omx_gemm_wgrad_bias(P(dZ.contiguous()), P(H.contiguous()), P(dW), M, N, K, S, P(ws), P(bws),
