@@ -30,7 +30,7 @@ def test_tree_shap_kernel(cuda_dev, cls, kw, F):
     margin = m.ens.raw_margin(fr.feature_matrix(m.x))[0]
     assert torch.allclose(out.sum(0), margin, atol=5e-4 * max(1.0, float(margin.abs().max())))
     nt = m.ens.ntrees
-    lv, el, _, maxm = tree_paths(m.ens.trees[:nt], 1.0 / nt if m.ens.average else 1.0)
-    ref = _shap_numpy(X[:300].T.astype(np.float64), lv, el, maxm)
+    lv, el, _, maxm, sets = tree_paths(m.ens.trees[:nt], 1.0 / nt if m.ens.average else 1.0)
+    ref = _shap_numpy(X[:300].T.astype(np.float64), lv, el, maxm, sets)
     np.testing.assert_allclose(out[:F, :300].cpu().numpy(), ref, atol=2e-4 * max(1.0, np.abs(ref).max()))
     assert "explain" in " ".join(_native.loaded_libraries())
