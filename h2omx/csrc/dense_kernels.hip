@@ -633,6 +633,215 @@ __global__ __launch_bounds__(256) void glm_irls_wave_kernel(const float* __restr
   if (lane == 0) dev_out[unit] = d;
 }
 
+// ---------------------------------------------------------------------------
+// GLM IRLS pass with the Gram on the bf16 matrix cores (glm_irls_split_kernel,
+// the default for the wave path).
+//
+// glm_irls_wave_kernel above is bound by its fp32 MFMAs: 28 upper tiles x 8
+// v_mfma_f32_16x16x4_f32 per 32-row chunk at 32 cycles each = 7.2k cycles,
+// 1.1 ms of a 2.5 ms pass at 10M x 100 (SQ_VALU_MFMA_BUSY_CYCLES,
+// profiles/r3/dense_pmc).  bf16 MFMA runs 16x the fp32 rate, and every fp32
+// value splits EXACTLY into three bf16 pieces by truncation:
+//   hi = x with the low 16 bits cleared (sign, exponent, 7 mantissa bits),
+//   r = x - hi (exact: the low 16 mantissa bits, <= 16 significant bits),
+//   mid = r with the low 16 bits cleared (the top 8 significant bits of r),
+//   lo = r - mid (exact, <= 8 significant bits, so a bf16 exactly),
+// x = hi + mid + lo with no rounding.  A product a * b then sums 9 partial
+// products; the 6 with weight >= 2^-16 (hh, hm, mh, hl, lh, mm) are kept, the
+// dropped ml + lm + ll are below ~2^-23 |a b|: fp32-product accuracy (each
+// bf16 x bf16 product is exact in the fp32 accumulator).  6 x
+// v_mfma_f32_16x16x32_bf16 (16 cycles) per tile and chunk = 96 cycles vs 256.
+//
+// The register layout is glm_irls_wave_kernel's (lane (h, c) holds column
+// blk * 16 + c of rows h * 8 .. h * 8 + 7), which is exactly the A / B operand
+// layout of the 16x16x32 bf16 MFMA (i = lane % 16, k = 8 (lane / 16) + 0..7),
+// so a tile (bi, bj) is 6 MFMAs on the packed pieces of blocks bi and bj.
+// Also cut from the VALU stream: the design has no NA (the GLM imputes
+// before the pass, `means` is unused here), the intercept column is loaded
+// as the constant 1 (then scaled like any column), the working response
+// column is always in the last block (p + 1 >= 16 (NB - 1)), and the
+// per-lane partial linear predictors run in fp32 (x and beta are fp32, each
+// lane sums <= NB products; the 16-lane reduction stays fp64).
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8_g __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4_g __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8_g as_bf16x8(u32x4_g v) { return __builtin_bit_cast(bf16x8_g, v); }
+
+// exact three-way bf16 split of 8 fp32 values (see above), packed 2 per dword
+__device__ __forceinline__ void split3_bf16(const float (&x)[GW_S], u32x4_g& H, u32x4_g& M, u32x4_g& L) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const unsigned u0 = __float_as_uint(x[2 * q]), u1 = __float_as_uint(x[2 * q + 1]);
+    const float r0 = x[2 * q] - __uint_as_float(u0 & 0xffff0000u);
+    const float r1 = x[2 * q + 1] - __uint_as_float(u1 & 0xffff0000u);
+    const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
+    const float l0 = r0 - __uint_as_float(v0 & 0xffff0000u);
+    const float l1 = r1 - __uint_as_float(v1 & 0xffff0000u);
+    // high halves of (first, second) -> (low, high) half of the packed dword
+    H[q] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+    M[q] = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
+    L[q] = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
+  }
+}
+
+template <int NB, bool VEC>
+__global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __restrict__ X, int64_t ld, int64_t n,
+                                                             const float* __restrict__ y,
+                                                             const float* __restrict__ wprior,
+                                                             const float* __restrict__ offset,
+                                                             const float* __restrict__ beta, GlmParams P,
+                                                             int64_t rows_per_unit, int n_units,
+                                                             float* __restrict__ slab, double* __restrict__ dev_out) {
+  constexpr int PW = NB * 16;
+  constexpr int T = NB * (NB + 1) / 2;
+  __shared__ float bsh[PW];
+  const int p = P.p;
+  for (int c = threadIdx.x; c < PW; c += blockDim.x) bsh[c] = (c < p) ? beta[c] : 0.0f;
+  __syncthreads();   // the only barrier: before any wave can leave
+  const int lane = threadIdx.x & 63;
+  // wave-uniform unit: the row loop, the full-chunk test and the row bases are scalar
+  const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  if (unit >= n_units) return;
+  const int h = lane >> 4, cl = lane & 15;
+  const int64_t r_begin = (int64_t)unit * rows_per_unit;
+  const int64_t r_end = min(n, r_begin + rows_per_unit);
+  const bool zlane = (NB - 1) * 16 + cl == p + 1;   // this lane's last-block column is z
+
+  f32x4 acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const double b0 = (double)beta[p];
+  double dev_acc = 0.0;
+
+  float xc[NB][GW_S], xn[NB][GW_S];
+  float yc = 0.f, wc = 1.f, oc = 0.f, yn = 0.f, wn = 1.f, on = 0.f;
+  // Branch-free loads: blocks 0 .. NB-3 are all data columns (p >= 16 NB - 17);
+  // the last two read a clamped column and select data / 1 (intercept) / 0.
+  // Rows past r_end (the last unit's tail chunk) read the clamped last row:
+  // finite values that the zero sqrt(w) of those rows removes from the Gram.
+  auto load = [&](int64_t r0, float (&xb)[NB][GW_S], float& yv, float& wv, float& ov) {
+    const int64_t rr = r0 + h * GW_S;
+    const bool full = VEC && r0 + GW_RB <= r_end;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int c = b * 16 + cl;
+      const float* src = X + (int64_t)(b >= NB - 2 ? min(c, p - 1) : c) * ld;
+      if (full) {
+#pragma unroll
+        for (int q = 0; q < GW_S / 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(src + rr + 4 * q);
+          xb[b][4 * q] = v.x; xb[b][4 * q + 1] = v.y; xb[b][4 * q + 2] = v.z; xb[b][4 * q + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < GW_S; ++s) xb[b][s] = src[min(rr + s, r_end - 1)];
+      }
+      if (b >= NB - 2) {
+        const float k = (c == p) ? 1.0f : 0.0f;   // intercept column
+#pragma unroll
+        for (int s = 0; s < GW_S; ++s) xb[b][s] = (c < p) ? xb[b][s] : k;
+      }
+    }
+    const int64_t row = min(r0 + h * GW_S + (cl & (GW_S - 1)), r_end - 1);
+    yv = y[row];
+    wv = wprior ? wprior[row] : 1.0f;
+    ov = offset ? offset[row] : 0.0f;
+  };
+  auto compute = [&](int64_t r0, float (&xb)[NB][GW_S], float yv, float wv, float ov) {
+    // 1. partial linear predictors of the lane's 8 rows over its NB columns
+    float pf[GW_S];
+#pragma unroll
+    for (int s = 0; s < GW_S; ++s) pf[s] = 0.f;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float bc = bsh[b * 16 + cl];
+#pragma unroll
+      for (int s = 0; s < GW_S; ++s) pf[s] = fmaf(xb[b][s], bc, pf[s]);
+    }
+    // 2. fp64 sum over the 16 column lanes: butterfly over lane bit 3, then a
+    //    reduce-scatter over bits 2..0 -> lane c owns row c % 8
+    double part[GW_S];
+#pragma unroll
+    for (int s = 0; s < GW_S; ++s) {
+      part[s] = (double)pf[s];
+      part[s] += __shfl_xor(part[s], 8, kWave);
+    }
+#pragma unroll
+    for (int off = GW_S / 2; off >= 1; off >>= 1) {
+      const bool hi = (cl & off) != 0;
+#pragma unroll
+      for (int j = 0; j < off; ++j) {
+        const double send = hi ? part[j] : part[j + off];
+        const double recv = __shfl_xor(send, off, kWave);
+        part[j] = (hi ? part[j + off] : part[j]) + recv;
+      }
+    }
+    // 3. link / IRLS weight / working response / deviance of this lane's row
+    const int64_t row = r0 + h * GW_S + (cl & (GW_S - 1));
+    float sw = 0.f, zz = 0.f;
+    if (row < r_end) {
+      const double eta = part[0] + b0 + (double)ov;
+      double mu, dmu;
+      glm_link(P, eta, mu, dmu);
+      const double wi = (double)wv * dmu * dmu / glm_var(P, mu);
+      zz = (float)(eta - (double)ov + ((double)yv - mu) / dmu);
+      sw = (float)sqrt(fmax(wi, 0.0));
+      if (cl < GW_S) dev_acc += (double)wv * glm_dev(P, (double)yv, mu);
+    }
+    // 4. scale by sqrt(w) of the rows (the intercept column becomes sqrt(w)),
+    //    z column, then the exact bf16 pieces of every block
+    const int base = lane & 48;
+#pragma unroll
+    for (int s = 0; s < GW_S; ++s) {
+      const float sws = __shfl(sw, base + s, kWave);
+      const float zs = __shfl(zz, base + s, kWave);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) xb[b][s] *= sws;
+      xb[NB - 1][s] = zlane ? zs * sws : xb[NB - 1][s];
+    }
+    u32x4_g H[NB], M[NB], L[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) split3_bf16(xb[b], H[b], M[b], L[b]);
+    // 5. upper Gram tiles: the 6 significant piece products per tile
+    int t = 0;
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int bj = bi; bj < NB; ++bj, ++t) {
+        f32x4 a = acc[t];
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(M[bi]), as_bf16x8(M[bj]), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(L[bi]), as_bf16x8(H[bj]), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[bi]), as_bf16x8(L[bj]), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(M[bi]), as_bf16x8(H[bj]), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[bi]), as_bf16x8(M[bj]), a, 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[bi]), as_bf16x8(H[bj]), a, 0, 0, 0);
+      }
+  };
+
+  int64_t r0 = r_begin;
+  if (r0 < r_end) load(r0, xc, yc, wc, oc);
+  for (; r0 < r_end; r0 += GW_RB) {
+    if (r0 + GW_RB < r_end) load(r0 + GW_RB, xn, yn, wn, on);
+    compute(r0, xc, yc, wc, oc);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int s = 0; s < GW_S; ++s) xc[b][s] = xn[b][s];
+    yc = yn; wc = wn; oc = on;
+  }
+  float* out = slab + (int64_t)unit * PW * PW;
+  int t = 0;
+#pragma unroll
+  for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+    for (int bj = bi; bj < NB; ++bj, ++t)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) out[(bi * 16 + 4 * h + v) * PW + bj * 16 + cl] = acc[t][v];
+  const double d = wave_sum(dev_acc);
+  if (lane == 0) dev_out[unit] = d;
+}
+
 // fp64 sum of the per-unit slabs of glm_irls_wave_kernel (upper 16x16 tiles;
 // strictly-lower tile entries come out 0 and are mirrored on the host).
 // Pass 1 (grid.y = SLAB_SPLIT): each thread sums every SLAB_SPLIT-th slab of
@@ -2210,6 +2419,40 @@ H2OMX_API int h2omx_glm_irls_wave(const float* X, int64_t ld, int64_t n, const f
   }
 #undef GWL_NB
 #undef GWL
+  return launch_status();
+}
+
+// glm_irls_split_kernel: same contract and slab layout as h2omx_glm_irls_wave
+// for an NA-free design (`means` is not read)
+H2OMX_API int h2omx_glm_irls_split(const float* X, int64_t ld, int64_t n, const float* y, const float* wprior,
+                                   const float* offset, const float* means, const float* beta, const void* params,
+                                   int n_units, int64_t rows_per_unit, float* slab, double* dev_out,
+                                   hipStream_t stream) {
+  (void)means;
+  const GlmParams P = *reinterpret_cast<const GlmParams*>(params);
+  if (P.family == 5 || P.p < 1 || P.p + 2 > 128 || n_units < 1 || rows_per_unit % GW_RB != 0 ||
+      (int64_t)n_units * rows_per_unit < n)
+    return kBadArg;
+  const int nb = (P.p + 2 + 15) / 16;
+  const bool vec = (ld % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0);
+  const int blocks = cdiv(n_units, 4);
+#define GSL(NB, V)                                                                                             \
+  hipLaunchKernelGGL((glm_irls_split_kernel<NB, V>), dim3(blocks), dim3(256), 0, stream, X, ld, n, y, wprior,   \
+                     offset, beta, P, rows_per_unit, n_units, slab, dev_out)
+#define GSL_NB(NB) do { if (vec) GSL(NB, true); else GSL(NB, false); } while (0)
+  switch (nb) {
+    case 1: GSL_NB(1); break;
+    case 2: GSL_NB(2); break;
+    case 3: GSL_NB(3); break;
+    case 4: GSL_NB(4); break;
+    case 5: GSL_NB(5); break;
+    case 6: GSL_NB(6); break;
+    case 7: GSL_NB(7); break;
+    case 8: GSL_NB(8); break;
+    default: return kBadArg;
+  }
+#undef GSL_NB
+#undef GSL
   return launch_status();
 }
 

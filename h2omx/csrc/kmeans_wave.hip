@@ -184,6 +184,186 @@ __global__ __launch_bounds__(256) void kmeans_wave_kernel(const float* __restric
 }
 
 
+// ---------------------------------------------------------------------------
+// K-Means Lloyd pass, wave-unit form with the cluster sums on the matrix cores
+// (kmeans_mfma_kernel; d + 2 <= 128, k <= 32).
+//
+// kmeans_wave_kernel above parks every 64-row chunk in a per-wave LDS tile
+// [DP][65] (29 KB at d = 100: one wave per SIMD) and walks the rows of each
+// cluster one at a time (a dependent LDS read per row).  Here:
+//   * distances straight from the load registers (lane = row), centroids
+//     through the scalar cache as above; no full-tile LDS round trip;
+//   * the cluster sums are the GEMM S[c][f] += sum_r onehot[r][c] x[r][f] on
+//     v_mfma_f32_16x16x4_f32 (exact fp32 products, a k-ordered fmaf chain):
+//     A = onehot (i = cluster, k = row), B = x (k = row, j = feature).  Step s
+//     of 16 takes rows 16 (lane / 16) + s: the onehot column comes from the
+//     row's lane by one ds_bpermute per step, and each 16-feature block of the
+//     chunk is transposed through a 16 x 68 LDS buffer (16 ds_write_b32, 4
+//     ds_read_b128 per lane, double-buffered) - 8.7 KB per wave, so LDS no
+//     longer limits occupancy (2 waves per SIMD: one wave's loads and matrix
+//     work overlap the other's VALU distances);
+//   * the counts and the per-cluster SSE are two more B columns (x[d] = 1,
+//     x[d + 1] = the row's squared distance), so the same MFMAs produce them.
+// Slab layout per wave as kmeans_wave_kernel: [k][d] sums | k counts | k SSE.
+// ---------------------------------------------------------------------------
+typedef float f32x4_k __attribute__((ext_vector_type(4)));
+constexpr int KM_LDP = 68;   // LDS row pitch (floats): conflict-free ds_read_b128 of 16 feature rows
+
+template <int NT, int KD, bool NA>
+__global__ __launch_bounds__(256, 2) void kmeans_mfma_kernel(const float* __restrict__ X, int64_t ld, int64_t n, int d,
+                                                            const float* __restrict__ CT2,
+                                                            const float* __restrict__ cnp, int k,
+                                                            int* __restrict__ assign, float* __restrict__ slab) {
+  constexpr int DP = NT * 16;            // x registers: d features, count column, SSE column, zero padding
+  constexpr int KG = (KD + 15) / 16;     // 16-cluster groups of the MFMA i dimension
+  __shared__ float kbuf[4][2][16 * KM_LDP];
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* buf0 = &kbuf[wid][0][0];
+  float* buf1 = &kbuf[wid][1][0];
+  const int64_t nch = (n + 63) / 64;
+  const int64_t W = (int64_t)gridDim.x * 4;
+  // d >= 16 NT - 17 (NT = ceil((d + 2) / 16)): features below F0 are always data
+  constexpr int F0 = DP - 17 > 0 ? DP - 17 : 0;
+  f32x4_k acc[KG][NT];
+#pragma unroll
+  for (int g = 0; g < KG; ++g)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[g][t] = f32x4_k{0.f, 0.f, 0.f, 0.f};
+  const int kq = lane >> 4, jl = lane & 15;
+
+  for (int64_t ch = (int64_t)blockIdx.x * 4 + wid; ch < nch; ch += W) {
+    const int64_t r = ch * 64 + lane;
+    const bool valid = r < n;
+    const uint32_t ro = (uint32_t)min(r, n - 1);
+    // feature pairs: (x[2 i], x[2 i + 1]) is one 64-bit register pair, the
+    // operand of the packed distance FMAs below
+    f32x2 xx[DP / 2];
+    {
+      int64_t co = 0;
+#pragma unroll
+      for (int f = 0; f < DP; ++f) {
+        float v = 0.f;
+        if (f < F0 || f < d) v = X[co + ro];
+        if (NA && v != v) v = 0.f;   // NA -> mean (0 in standardized space)
+        xx[f / 2][f % 2] = v;
+        co += ld;
+        asm volatile("" : "+s"(co));
+      }
+    }
+    // distances: per cluster an (even, odd) feature partial pair, packed fp32
+    // FMAs whose centroid operand is an SGPR pair from CT2 [DP / 2][KD][2]
+    // (scalar-cache reads; the two halves are summed after the loop)
+    f32x2 accp[KD];
+#pragma unroll
+    for (int c = 0; c < KD; ++c) accp[c] = f32x2{0.f, 0.f};
+    f32x2 x2p{0.f, 0.f};
+#pragma unroll
+    for (int f2 = 0; f2 < DP / 2; ++f2) {
+      if (2 * f2 < F0 || 2 * f2 < d) {   // wave-uniform: the padded features cost nothing
+        int co = f2 * 2 * KD;
+        asm volatile("" : "+s"(co));
+        const f32x2 xv = xx[f2];
+        x2p = __builtin_elementwise_fma(xv, xv, x2p);
+#pragma unroll
+        for (int c2 = 0; c2 < KD / 2; ++c2) {
+          const float4 cv = *reinterpret_cast<const float4*>(CT2 + co + 4 * c2);   // clusters 2 c2, 2 c2 + 1
+          accp[2 * c2] = __builtin_elementwise_fma(xv, f32x2{cv.x, cv.y}, accp[2 * c2]);
+          accp[2 * c2 + 1] = __builtin_elementwise_fma(xv, f32x2{cv.z, cv.w}, accp[2 * c2 + 1]);
+        }
+      }
+    }
+    const float x2 = x2p.x + x2p.y;
+    float best = INFINITY;
+    int bi = 0;
+#pragma unroll
+    for (int c = 0; c < KD; ++c) {
+      const float dist = cnp[c] - 2.0f * (accp[c].x + accp[c].y);
+      if (dist < best) { best = dist; bi = c; }
+    }
+    if (valid) assign[r] = bi;
+    bi = valid ? bi : -1;                  // rows past n join no cluster
+    // count and SSE columns (d and d + 1 < DP by the launcher's NT)
+#pragma unroll
+    for (int f = F0; f < DP; ++f) {
+      if (f == d) xx[f / 2][f % 2] = 1.0f;
+      if (f == d + 1) xx[f / 2][f % 2] = fmaxf(best + x2, 0.f);
+    }
+    // A operands: step s covers rows 16 kq + s; lane (kq, jl) holds onehot[row][16 g + jl]
+    float a[KG][16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int bs = __shfl(bi, (lane & 48) + s, kWave);
+#pragma unroll
+      for (int g = 0; g < KG; ++g) a[g][s] = (bs == 16 * g + jl) ? 1.0f : 0.0f;
+    }
+    // B operands: block t of 16 features transposed through the wave's LDS buffer
+#pragma unroll
+    for (int j = 0; j < 16; ++j) buf0[j * KM_LDP + lane] = xx[j / 2][j % 2];
+    kw_wave_sync();
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float* cur = (t & 1) ? buf1 : buf0;
+      float* nxt = (t & 1) ? buf0 : buf1;
+      float b[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(cur + jl * KM_LDP + 16 * kq + 4 * q);
+        b[4 * q] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
+      }
+      if (t + 1 < NT) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) nxt[j * KM_LDP + lane] = xx[8 * (t + 1) + j / 2][j % 2];
+      }
+      kw_wave_sync();   // this block's reads and the next block's writes are done
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int g = 0; g < KG; ++g) acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][s], b[s], acc[g][t], 0, 0, 0);
+    }
+  }
+  // D layout: lane holds D[i = 4 kq + v][j = jl] -> cluster 16 g + 4 kq + v, feature 16 t + jl
+  const int gw = blockIdx.x * 4 + wid;
+  float* out = slab + (int64_t)gw * (k * d + 2 * k);
+#pragma unroll
+  for (int g = 0; g < KG; ++g)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int c = 16 * g + 4 * kq + v, f = 16 * t + jl;
+        if (c < k) {
+          if (f < d) out[c * d + f] = acc[g][t][v];
+          else if (f == d) out[k * d + c] = acc[g][t][v];
+          else if (f == d + 1) out[k * d + k + c] = acc[g][t][v];
+        }
+      }
+}
+
+// MFMA-sum Lloyd pass: CT2 [8 * nt][kd][2] zero-padded centroids by feature pair,
+// cnp [kd] (+inf padding); nt = ceil((d + 2) / 16); n_wg workgroups of 4 waves,
+// slab holds 4 * n_wg per-wave slabs; na = 0 asserts an NA-free design
+H2OMX_API int h2omx_kmeans_mfma(const float* X, int64_t ld, int64_t n, int d, const float* CT2, const float* cnp,
+                                int k, int kd, int nt, int na, int n_wg, int* assign, float* slab,
+                                hipStream_t stream) {
+  if (n_wg < 1 || n < 1 || d < 1 || k < 1 || k > kd || kd % 4 != 0 || nt != (d + 2 + 15) / 16) return kBadArg;
+#define KMM(NT, KD)                                                                                          \
+  if (nt == NT && kd == KD) {                                                                                \
+    if (na)                                                                                                  \
+      hipLaunchKernelGGL((kmeans_mfma_kernel<NT, KD, true>), dim3(n_wg), dim3(256), 0, stream, X, ld, n, d,   \
+                         CT2, cnp, k, assign, slab);                                                         \
+    else                                                                                                     \
+      hipLaunchKernelGGL((kmeans_mfma_kernel<NT, KD, false>), dim3(n_wg), dim3(256), 0, stream, X, ld, n, d,  \
+                         CT2, cnp, k, assign, slab);                                                         \
+    return launch_status();                                                                                  \
+  }
+#define KMM_NT(NT) KMM(NT, 4) KMM(NT, 8) KMM(NT, 12) KMM(NT, 16)
+  KMM_NT(1) KMM_NT(2) KMM_NT(3) KMM_NT(4) KMM_NT(5) KMM_NT(6) KMM_NT(7) KMM_NT(8)
+  KMM(1, 24) KMM(2, 24) KMM(3, 24) KMM(4, 24) KMM(1, 32) KMM(2, 32) KMM(3, 32) KMM(4, 32)
+#undef KMM_NT
+#undef KMM
+  return kBadArg;
+}
+
 // wave-unit Lloyd pass: Cp [KP][DP] zero-padded centroids, cnp [KP] (+inf
 // padding); n_wg workgroups of 4 waves, slab holds 4 * n_wg per-wave slabs
 H2OMX_API int h2omx_kmeans_wave(const float* X, int64_t ld, int64_t n, int d, const float* Cp, const float* CTg,

@@ -70,11 +70,13 @@ DENSE_SIGS = {
     "h2omx_glm_irls": "PLLPPPPPPIIPPS",
     "h2omx_slab_reduce_upper": "PIIPS",
     "h2omx_glm_irls_wave": "PLLPPPPPPILPPS",
+    "h2omx_glm_irls_split": "PLLPPPPPPILPPS",
     "h2omx_slab_reduce16": "PIIPS",
     "h2omx_slab_sum": "PIIPS",
     "h2omx_slab_sum_f32": "PIIPS",
     "h2omx_kmeans": "PLLIPPIIPPS",
     "h2omx_kmeans_wave": "PLLIPPPIIIIPPS",
+    "h2omx_kmeans_mfma": "PLLIPPIIIIIPPS",
     "h2omx_glm_wz": "PLPPPPPPPPIS",
     "h2omx_glm_grad": "PLLPPPPPPPIPIS",
     "h2omx_glm_grad_max_k": "",

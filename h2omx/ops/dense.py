@@ -26,12 +26,18 @@ GLM_WGS = int(os.environ.get("H2OMX_GLM_WGS", "512"))
 GLM_WAVE = os.environ.get("H2OMX_GLM_WAVE", "1") != "0"
 GLM_UNITS = int(os.environ.get("H2OMX_GLM_UNITS", "2048"))
 GLM_UNIT_MIN_ROWS = 512
+# Gram of the wave path: "split" = exact 3-way bf16 split on the bf16 matrix
+# cores (glm_irls_split_kernel), "f32" = fp32 MFMA (glm_irls_wave_kernel)
+GLM_GRAM = os.environ.get("H2OMX_GLM_GRAM", "split")
 SLAB_SPLIT = 32          # dense_kernels.hip slab_reduce16_kernel
 KM_WGS = int(os.environ.get("H2OMX_KM_WGS", "1024"))
 # K-Means Lloyd pass on the wave-unit kernel (k <= 32, d <= 128 / 64); 0: the
 # workgroup-tile kernel.  KM_WAVE_CUS: CUs the wave kernel's grid is sized for
 KM_WAVE = os.environ.get("H2OMX_KM_WAVE", "1") == "1"
 KM_WAVE_CUS = int(os.environ.get("H2OMX_KM_WAVE_CUS", "256"))
+# K-Means cluster sums on the fp32 matrix cores (kmeans_mfma_kernel): d + 2 <= 128, k <= 32
+KM_MFMA = os.environ.get("H2OMX_KM_MFMA", "1") == "1"
+KM_MFMA_WGS = int(os.environ.get("H2OMX_KM_MFMA_WGS", "512"))
 
 FAMILIES = {"gaussian": 0, "binomial": 1, "poisson": 2, "gamma": 3, "tweedie": 4, "multinomial": 5,
             "quasibinomial": 6, "fractionalbinomial": 6, "negativebinomial": 7}
@@ -169,9 +175,11 @@ def glm_grad_pass(X: torch.Tensor, y: torch.Tensor, wprior, offset, beta: np.nda
 
 
 def _glm_irls_wave(X, y, wprior, offset, beta, family, link, cls, var_power, link_power):
-    """glm_irls_wave_kernel: independent wave units over contiguous row ranges
-    (register-resident 32-row chunks, 16x16x4 fp32 MFMA Gram tiles), then the
-    fp64 sum of the per-unit upper tiles."""
+    """glm_irls_split_kernel (GLM_GRAM "split": exact three-way bf16 split,
+    6 bf16 MFMAs per 16x16 tile) or glm_irls_wave_kernel ("f32": 16x16x4 fp32
+    MFMA): independent wave units over contiguous row ranges, register-resident
+    32-row chunks, then the fp64 sum of the per-unit upper tiles.  X has no NA
+    (the GLM imputes column means before the pass)."""
     lib = dense_lib()
     p, n = X.shape
     K = beta.shape[0]
@@ -188,8 +196,9 @@ def _glm_irls_wave(X, y, wprior, offset, beta, family, link, cls, var_power, lin
     gp = GlmParams(FAMILIES[family], LINKS[link], p, K, cls, 0, var_power, link_power)
     Xc = X if X.stride(1) == 1 else X.contiguous()
     st = stream(dev)
-    check(lib.h2omx_glm_irls_wave(P(Xc), Xc.stride(0), n, P(y), P(wprior), P(offset), P(means), P(b32),
-                                  ctypes.addressof(gp), units, rows, P(slab), P(devs), st), "glm_irls_wave")
+    fn = lib.h2omx_glm_irls_split if (GLM_GRAM == "split" and p >= 1) else lib.h2omx_glm_irls_wave
+    check(fn(P(Xc), Xc.stride(0), n, P(y), P(wprior), P(offset), P(means), P(b32),
+             ctypes.addressof(gp), units, rows, P(slab), P(devs), st), "glm_irls_wave")
     check(lib.h2omx_slab_reduce16(P(slab), units, pw, P(out), st), "slab_reduce16")
     G = out[: pw * pw].view(pw, pw)[: p + 2, : p + 2].cpu().numpy()
     G = np.triu(G) + np.triu(G, 1).T
@@ -199,9 +208,10 @@ def _glm_irls_wave(X, y, wprior, offset, beta, family, link, cls, var_power, lin
 # ---------------------------------------------------------------------------
 # K-Means
 # ---------------------------------------------------------------------------
-def kmeans_step(X: torch.Tensor, C: torch.Tensor):
-    """One Lloyd pass.  X feature-major float32 [d][n] (standardized, NA -> 0),
-    C [k][d].  Returns (assign int32 [n], sums float64 [k][d], counts [k], sse [k])."""
+def kmeans_step(X: torch.Tensor, C: torch.Tensor, na_free: bool = False):
+    """One Lloyd pass.  X feature-major float32 [d][n] (standardized; NA cells
+    count as 0 unless ``na_free`` asserts there are none), C [k][d].
+    Returns (assign int32 [n], sums float64 [k][d], counts [k], sse [k])."""
     _dev(X, "kmeans_step")
     d, n = X.shape
     k = C.shape[0]
@@ -216,7 +226,21 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor):
     st = stream(dev)
     kp = -(-k // 4) * 4 if k <= 16 else -(-k // 8) * 8
     dp = -(-d // 16) * 16
-    if KM_WAVE and k <= 32 and (dp <= 128 if kp <= 16 else dp <= 64):
+    nt = -(-(d + 2) // 16)
+    if KM_MFMA and k <= 32 and nt <= (8 if kp <= 16 else 4):
+        # csrc/kmeans_wave.hip kmeans_mfma_kernel: centroids by feature pair
+        # CT2 [8 nt][kp][2] (zero padding), +inf norms for the padding clusters
+        Cp = torch.zeros((kp, 16 * nt), dtype=torch.float32, device=dev)
+        Cp[:k, :d] = Cc
+        CT2 = Cp.view(kp, 8 * nt, 2).permute(1, 0, 2).contiguous()
+        cnp = torch.full((kp,), float("inf"), dtype=torch.float32, device=dev)
+        cnp[:k] = cn
+        n_wg = max(1, min(KM_MFMA_WGS, math.ceil(n / (64 * 4 * 4))))
+        slab = torch.empty((4 * n_wg * width,), dtype=torch.float32, device=dev)
+        check(lib.h2omx_kmeans_mfma(P(Xc), Xc.stride(0), n, d, P(CT2), P(cnp), k, kp, nt, 0 if na_free else 1, n_wg,
+                                    P(assign), P(slab), st), "kmeans_mfma")
+        check(lib.h2omx_slab_sum(P(slab), 4 * n_wg, width, P(out), st), "slab_sum")
+    elif KM_WAVE and k <= 32 and (dp <= 128 if kp <= 16 else dp <= 64):
         # wave-unit kernel (csrc/dense_kernels.hip kmeans_wave_kernel): zero-padded
         # centroids [kp][dp], +inf norms for the padding clusters
         Cp = torch.zeros((kp, dp), dtype=torch.float32, device=dev)

@@ -142,8 +142,9 @@ def _irls_pass_ref(X, y, wprior, offset, beta, family, link, cls, var_power, lin
 
 
 
-def kmeans_step(X: torch.Tensor, C: torch.Tensor):
-    """One Lloyd pass in fp64 (same outputs as the HIP kernel)."""
+def kmeans_step(X: torch.Tensor, C: torch.Tensor, na_free: bool = False):
+    """One Lloyd pass in fp64 (same outputs as the HIP kernel; ``na_free`` is
+    the device kernels' no-NA hint, unused here)."""
     d, n = X.shape
     k = C.shape[0]
     Xn = X.double().numpy()

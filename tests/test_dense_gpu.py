@@ -92,10 +92,14 @@ def test_kmeans_step_matches_reference(cuda_dev, d, k):
         np.testing.assert_allclose(eg, er, rtol=1e-3)
 
 
-@pytest.mark.parametrize("d,k", [(4, 3), (33, 16), (64, 17), (64, 32), (100, 10), (128, 16), (96, 5)])
-def test_kmeans_wave_kernel_matches_reference(cuda_dev, monkeypatch, d, k):
-    """Wave-unit Lloyd pass (csrc/kmeans_wave.hip) against the fp64 NumPy oracle
-    and the workgroup-tile kernel: tail chunk (n % 64 != 0), NA cells, empty clusters."""
+@pytest.mark.parametrize("mfma", [True, False])
+@pytest.mark.parametrize("d,k", [(4, 3), (33, 16), (64, 17), (64, 32), (100, 10), (128, 16), (96, 5), (14, 12),
+                                 (110, 16), (126, 4), (30, 29)])
+def test_kmeans_wave_kernel_matches_reference(cuda_dev, monkeypatch, d, k, mfma):
+    """Wave-unit Lloyd passes (csrc/kmeans_wave.hip: MFMA cluster sums, or the
+    LDS-tile row walk) against the fp64 NumPy oracle and the workgroup-tile
+    kernel: tail chunk (n % 64 != 0), NA cells, empty clusters, the count / SSE
+    columns at the end of a 16-feature block (d = 14, 30, 110, 126)."""
     rng = np.random.default_rng(100 + d + k)
     n = 40_003
     X = rng.normal(size=(d, n)).astype(np.float32)
@@ -109,7 +113,14 @@ def test_kmeans_wave_kernel_matches_reference(cuda_dev, monkeypatch, d, k):
 
     for wave in (True, False):
         monkeypatch.setattr(OD, "KM_WAVE", wave)
+        monkeypatch.setattr(OD, "KM_MFMA", wave and mfma)
         outs[wave] = D.kmeans_step(torch.from_numpy(X).to(cuda_dev), torch.from_numpy(C).to(cuda_dev))
+    if mfma:   # the NA-free variant on the imputed design gives the same pass
+        monkeypatch.setattr(OD, "KM_MFMA", True)
+        monkeypatch.setattr(OD, "KM_WAVE", True)
+        a2, s2, c2, e2 = D.kmeans_step(torch.from_numpy(Xc).to(cuda_dev), torch.from_numpy(C).to(cuda_dev), na_free=True)
+        assert torch.equal(a2, outs[True][0]) and np.array_equal(c2, outs[True][2])
+        np.testing.assert_allclose(s2, outs[True][1], rtol=1e-6, atol=1e-5)
     ag, sg, cg, eg = outs[True]
     agree = (ag.cpu().numpy() == ar.numpy()).mean()
     assert agree > 0.999
@@ -302,6 +313,59 @@ def test_glm_wave_kernel_matches_workgroup_kernel_and_reference(cuda_dev, monkey
     assert np.abs(Gw - Gr).max() / scale < 2e-5
     assert np.abs(Gw - Gk).max() / scale < 2e-5
     assert abs(dw - dr) / abs(dr) < 1e-5
+
+
+@pytest.mark.parametrize("p,family,link,n,off", [(100, "binomial", "logit", 100_003, True),
+                                                 (15, "gaussian", "identity", 4_096, False),
+                                                 (14, "poisson", "log", 777, True),
+                                                 (30, "binomial", "logit", 65_536, False),
+                                                 (1, "gamma", "inverse", 5_000, False),
+                                                 (126, "tweedie", "tweedie", 9_000, True)])
+def test_glm_split_gram_matches_f32_and_reference(cuda_dev, monkeypatch, p, family, link, n, off):
+    """glm_irls_split_kernel (exact 3-way bf16 split, 6 bf16 MFMAs per tile) vs
+    the fp32-MFMA wave kernel and the fp64 oracle: tails (n % 32 != 0),
+    unaligned columns (n % 4 != 0 -> scalar loads), the intercept at the end of
+    block NB-2 (p = 15) and alone in a block (p = 14, p = 126), one feature."""
+    from h2omx.ops import dense as DD
+
+    rng = np.random.default_rng(3 * p + n)
+    X = rng.normal(size=(p, n)).astype(np.float32)
+    X[0] *= 50.0                     # a wide dynamic range across columns
+    beta = np.zeros((1, p + 1))
+    beta[0, :p] = rng.normal(scale=0.05, size=p)
+    beta[0, p] = 0.3 if family not in ("gamma", "tweedie") else 2.0
+    beta[0, 0] *= 0.02
+    eta = beta[0, :p] @ X + beta[0, p]
+    if family == "binomial":
+        y = (rng.random(n) < 1 / (1 + np.exp(-eta))).astype(np.float32)
+    elif family == "poisson":
+        y = rng.poisson(np.exp(eta)).astype(np.float32)
+    elif family == "gaussian":
+        y = (eta + rng.normal(size=n)).astype(np.float32)
+    else:
+        y = rng.gamma(2.0, 1.0 / np.maximum(eta, 0.2) / 2.0).astype(np.float32)
+    w = rng.uniform(0.5, 2.0, n).astype(np.float32)
+    o = (0.1 * rng.normal(size=n)).astype(np.float32) if off else None
+    Xt, yt, wt = torch.from_numpy(X), torch.from_numpy(y), torch.from_numpy(w)
+    ot = None if o is None else torch.from_numpy(o)
+    kw = dict(var_power=1.5, link_power=0.0) if family == "tweedie" else {}
+    Gr, dr = D.glm_irls_pass(Xt, yt, wt, ot, beta, family, link, **kw)
+    g = lambda: DD.glm_irls_pass(Xt.to(cuda_dev), yt.to(cuda_dev), wt.to(cuda_dev),
+                                 None if ot is None else ot.to(cuda_dev), beta, family, link, **kw)
+    monkeypatch.setattr(DD, "GLM_WAVE", True)
+    monkeypatch.setattr(DD, "GLM_GRAM", "split")
+    Gs, ds = g()
+    monkeypatch.setattr(DD, "GLM_GRAM", "f32")
+    Gf, df = g()
+    scale = np.abs(Gr).max()
+    es, ef = np.abs(Gs - Gr).max() / scale, np.abs(Gf - Gr).max() / scale
+    assert es < 2e-6 and ef < 2e-6, (es, ef)
+    # entry-wise on the significant entries: the split is as accurate as fp32 MFMA
+    big = np.abs(Gr) > 1e-4 * scale
+    rs = (np.abs(Gs - Gr) / np.abs(Gr))[big].max()
+    rf = (np.abs(Gf - Gr) / np.abs(Gr))[big].max()
+    assert rs < 1e-5 and rs < 4 * rf + 1e-6, (rs, rf)
+    assert abs(ds - dr) / abs(dr) < 1e-5 and abs(ds - df) / abs(df) < 1e-6
 
 
 def test_glm_gram_ill_conditioned_collinear_design(cuda_dev):
