@@ -23,6 +23,7 @@ standardized response) and autoencoders with ``anomaly()``.
 """
 from __future__ import annotations
 
+import contextlib
 import gc
 import math
 import os
@@ -258,6 +259,7 @@ class _DLTrainer:
     """
 
     PROBE_STEPS = 32
+    DL_SIDE = os.environ.get("H2OMX_DL_SIDE", "0") == "1"
 
     def __init__(self, p_, net, X, Y, act, cls, auto, drop_in, hd, M, steps_per_epoch, comm, gen, gen_dev,
                  n_hidden, backward):
@@ -306,6 +308,9 @@ class _DLTrainer:
                 self.spi = max(1, round(t / (self.world * M)))
         # h2omx extension: precision="bf16" trains Rectifier / Tanh nets without dropout
         # on the bf16 matrix cores (fp32 accumulation, fp32 master weights / optimizer)
+        # weight gradients on a second stream beside the dgrad chain (DL_SIDE)
+        self.side = (torch.cuda.Stream(device=dev) if dev.type == "cuda" and self.DL_SIDE and not self.sync_grad
+                     else None)
         self.mlp = None
         if (str(p_.get("precision", "fp32")).lower() == "bf16" and X.is_cuda and act in (1, 2) and drop_in == 0
                 and not any(hd[:n_hidden]) and M % 8 == 0):
@@ -449,6 +454,8 @@ class _DLTrainer:
         comm = self.comm if self.sync_grad else None
         if mlp is not None:
             mlp.backward(dZ, xbt, comm, self.world)
+        elif self.side is not None and comm is None:
+            self.backward(net, Hs, aux, dZ, self.act, comm, self.world, side=self.side)
         else:
             self.backward(net, Hs, aux, dZ, self.act, comm, self.world)
         if self.adaptive:
@@ -725,52 +732,73 @@ class H2ODeepLearningEstimator(ModelBuilder):
         return model
 
     @staticmethod
-    def _backward(net, Hs, aux, dZ, act, comm, world):
+    def _backward(net, Hs, aux, dZ, act, comm, world, side=None):
+        """Back-propagation into net.grad.  ``side`` (single rank): a second
+        stream for the weight / bias gradients, which nothing later in the
+        backward reads, so they run beside the critical dgrad -> activation
+        backward chain and join before the optimizer.  Each layer's ops then
+        take their own workspace namespace (no two in-flight kernels share
+        scratch) and the tensors the side stream reads stay referenced until
+        the join."""
         L = len(net.layers)
         handles = []
         bpart = None   # bias-gradient slices of dZ from the fused activation backward
+        main = torch.cuda.current_stream(dZ.device) if side is not None else None
+        keep = []
         for i in range(L - 1, -1, -1):
             Hin = Hs[i]
             W = net.W(i)
-            if bpart is not None:
-                D.wgrad_bias(dZ, Hin, net.W(i, net.grad), net.b(i, net.grad), bpart)   # dW = dZ^T H, db
-            elif i == L - 1 and D.out_layer_ok(dZ, Hin):
-                D.out_wgrad(dZ, Hin, net.W(i, net.grad), net.b(i, net.grad))          # few classes: one pass
-            else:
-                D.gemm(dZ, Hin, ta=True, out=net.W(i, net.grad))          # dW = dZ^T H
-                D.bias_grad(dZ, out=net.b(i, net.grad))
-            bpart = None
+            with contextlib.ExitStack() as es:
+                if side is not None:
+                    side.wait_stream(main)
+                    es.enter_context(torch.cuda.stream(side))
+                    es.enter_context(D.workspace_ns(1000 + i))
+                    keep.append((dZ, Hin, bpart))
+                if bpart is not None:
+                    D.wgrad_bias(dZ, Hin, net.W(i, net.grad), net.b(i, net.grad), bpart)   # dW = dZ^T H, db
+                elif i == L - 1 and D.out_layer_ok(dZ, Hin):
+                    D.out_wgrad(dZ, Hin, net.W(i, net.grad), net.b(i, net.grad))          # few classes: one pass
+                else:
+                    D.gemm(dZ, Hin, ta=True, out=net.W(i, net.grad))          # dW = dZ^T H
+                    D.bias_grad(dZ, out=net.b(i, net.grad))
             if comm is not None and world > 1:
                 a, b = net.span(i)
                 handles.append(comm.all_reduce_async(net.grad[a:b]))
             if i == 0:
                 break
-            arg, mask = aux[i - 1]
-            if act in (1, 2) and mask is None and i == L - 1 and D.out_layer_ok(dZ, Hs[i]):
-                dZ, bpart = D.thin_dact(dZ, W, Hs[i], act)
-                continue
-            if act in (1, 2) and mask is None and D.dact_ok(dZ, W):
-                # dZ_prev = (dZ W) * act'(H) and its bias-gradient slices in the GEMM epilogue
-                dZ, bpart = D.gemm_dact(dZ.contiguous(), W, Hs[i], act)
-                continue
-            dH = D.gemm(dZ, W)                                            # [M][in]
-            if mask is not None:
-                dH = dH * mask
-            if act == 3:
-                g2 = torch.zeros((dH.shape[0], dH.shape[1], 2), device=dH.device)
-                g2.scatter_(2, arg[..., None], dH[..., None])
-                dZ = g2.view(dH.shape[0], -1)
-            elif act == 4:
-                Hn = Hs[i]
-                dZ = dH * torch.where(Hn > 0, torch.ones_like(Hn), Hn + 1.0)
-            elif mask is None:
-                dZ, bpart = D.act_backward_bias(Hs[i], dH, act)
-            else:
-                dZ = D.act_backward(Hs[i] / mask.clamp_min(1e-30) * (mask > 0), dH, act)
+            with D.workspace_ns(i) if side is not None else contextlib.nullcontext():
+                dZ, bpart = H2ODeepLearningEstimator._dgrad(Hs, aux, dZ, W, act, i, L)
+        if side is not None:
+            main.wait_stream(side)
+            del keep
         for h in handles:
             h.wait()
         if comm is not None and world > 1:
             net.grad.div_(world)
+
+    @staticmethod
+    def _dgrad(Hs, aux, dZ, W, act, i, L):
+        """dZ of layer i - 1 from layer i's (dZ, W): (dZ_prev, bias-gradient
+        slices or None)"""
+        arg, mask = aux[i - 1]
+        if act in (1, 2) and mask is None and i == L - 1 and D.out_layer_ok(dZ, Hs[i]):
+            return D.thin_dact(dZ, W, Hs[i], act)
+        if act in (1, 2) and mask is None and D.dact_ok(dZ, W):
+            # dZ_prev = (dZ W) * act'(H) and its bias-gradient slices in the GEMM epilogue
+            return D.gemm_dact(dZ.contiguous(), W, Hs[i], act)
+        dH = D.gemm(dZ, W)                                            # [M][in]
+        if mask is not None:
+            dH = dH * mask
+        if act == 3:
+            g2 = torch.zeros((dH.shape[0], dH.shape[1], 2), device=dH.device)
+            g2.scatter_(2, arg[..., None], dH[..., None])
+            return g2.view(dH.shape[0], -1), None
+        if act == 4:
+            Hn = Hs[i]
+            return dH * torch.where(Hn > 0, torch.ones_like(Hn), Hn + 1.0), None
+        if mask is None:
+            return D.act_backward_bias(Hs[i], dH, act)
+        return D.act_backward(Hs[i] / mask.clamp_min(1e-30) * (mask > 0), dH, act), None
 
     @staticmethod
     def _clip_w2(net, max_w2):

@@ -9,6 +9,7 @@ routes a call to one or the other by the device of its data.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import math
 import os
@@ -319,11 +320,28 @@ _WS: dict = {}
 _WS_RETIRED: list = []
 
 
+_WS_NS = [0]
+
+
+@contextlib.contextmanager
+def workspace_ns(ns: int):
+    """Scratch namespace for the ops issued inside: work that may run
+    concurrently on another stream (the DL backward's weight-gradient side
+    stream) takes a namespace of its own, so no two in-flight kernels share a
+    workspace."""
+    old = _WS_NS[0]
+    _WS_NS[0] = ns
+    try:
+        yield
+    finally:
+        _WS_NS[0] = old
+
+
 def _workspace(dev, numel: int, slot: int = 0) -> torch.Tensor:
-    """Per-device scratch for split-K partials (stream-ordered reuse).  A grown
-    workspace keeps its predecessor alive: a captured HIP graph (DL training
-    step) may still hold the old pointer."""
-    key = (str(dev), slot)
+    """Per-device scratch for split-K partials (stream-ordered reuse within a
+    namespace, see workspace_ns).  A grown workspace keeps its predecessor
+    alive: a captured HIP graph (DL training step) may still hold the old pointer."""
+    key = (str(dev), slot, _WS_NS[0])
     w = _WS.get(key)
     if w is None or w.numel() < numel:
         if w is not None:

@@ -25,9 +25,12 @@ C = X[:, :k].T.contiguous()
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 NA_FREE = len(sys.argv) > 2 and sys.argv[2] == "na_free"   # the K-Means model's imputed design
 out = {}
+WHICH = sys.argv[3] if len(sys.argv) > 3 else "both"
 for name, fn, flops in (("glm_irls", lambda: D.glm_irls_pass(X, y, None, None, beta, "binomial", "logit"),
                          n * (p + 2) * (p + 2)),
                         ("kmeans", lambda: D.kmeans_step(X, C, na_free=NA_FREE), 2.0 * n * k * p)):
+    if WHICH not in ("both", name.split("_")[0]):
+        continue
     fn()
     torch.cuda.synchronize()
     t = time.perf_counter()
@@ -36,5 +39,6 @@ for name, fn, flops in (("glm_irls", lambda: D.glm_irls_pass(X, y, None, None, b
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / reps
     out[name] = {"ms_per_pass": dt * 1e3, "useful_tflops": flops / dt / 1e12, "rows": n, "cols": p}
-out["kmeans"]["k"] = k
+if "kmeans" in out:
+    out["kmeans"]["k"] = k
 print(json.dumps(out))
