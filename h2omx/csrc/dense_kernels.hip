@@ -663,6 +663,9 @@ __global__ __launch_bounds__(256) void glm_irls_wave_kernel(const float* __restr
 // per-lane partial linear predictors run in fp32 (x and beta are fp32, each
 // lane sums <= NB products; the 16-lane reduction stays fp64).
 // ---------------------------------------------------------------------------
+#ifndef GLM_ROW_F32
+#define GLM_ROW_F32 1
+#endif
 typedef __bf16 bf16x8_g __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4_g __attribute__((ext_vector_type(4)));
 
@@ -685,7 +688,50 @@ __device__ __forceinline__ void split3_bf16(const float (&x)[GW_S], u32x4_g& H, 
   }
 }
 
-template <int NB, bool VEC>
+// binomial / logit per-row IRLS quantities without branches: mu = sigmoid(eta)
+// from e = exp(-|eta|), var(mu) = mu' (so w = prior * mu'), and the deviance
+// from one log1p: log mu = min(eta, 0) - log1p(e), log(1 - mu) = -max(eta, 0)
+// - log1p(e), each floored at log(1e-15) like glm_dev's clamp of mu.
+__device__ __forceinline__ void glm_row_binomial(double eta, double ov, double yv, double wv, float& sw, float& zz,
+                                                 double& dev) {
+  const double e = exp(-fabs(eta));
+  const double r1 = 1.0 / (1.0 + e);
+  const double mu = eta >= 0 ? r1 : e * r1;
+  const double dmu = fmax(mu * (1.0 - mu), 1e-10);
+  zz = (float)(eta - ov + (yv - mu) / dmu);
+  sw = (float)sqrt(wv * dmu);
+  const double l1p = log1p(e);
+  const double lfloor = -34.538776394910684;   // log(1e-15)
+  const double lm = fmax(fmin(eta, 0.0) - l1p, lfloor), l1m = fmax(-fmax(eta, 0.0) - l1p, lfloor);
+  dev = -2.0 * wv * (yv * lm + (1.0 - yv) * l1m);
+}
+
+// the same in fp32 (native v_exp_f32 / v_log_f32 / v_rcp_f32 paths): sw and
+// zz are rounded to fp32 anyway and their error stays within ~2 fp32 ulps of
+// the fp64 route; the deviance terms enter the fp64 accumulator
+__device__ __forceinline__ void glm_row_binomial_f32(double eta_d, float ov, float yv, float wv, float& sw, float& zz,
+                                                     double& dev) {
+  const float eta = (float)eta_d;
+  const float e = __expf(-fabsf(eta));
+  const float r1 = 1.0f / (1.0f + e);
+  const float mu = eta >= 0.f ? r1 : e * r1;
+  const float dmu = fmaxf(mu * (1.0f - mu), 1e-10f);
+  zz = (float)(eta_d - (double)ov) + (yv - mu) / dmu;
+  sw = sqrtf(wv * dmu);
+  const float l1p = log1pf(e);
+  const float lfloor = -34.538776f;   // log(1e-15)
+  const float lm = fmaxf(fminf(eta, 0.f) - l1p, lfloor), l1m = fmaxf(-fmaxf(eta, 0.f) - l1p, lfloor);
+  dev = -2.0 * (double)(wv * (yv * lm + (1.0f - yv) * l1m));
+}
+
+// FAM 1: binomial family with the logit link (branch-free row math, so the
+// previous chunk's MFMAs and this chunk's link math share one basic block and
+// the scheduler overlaps them); FAM 0: any family / link (glm_link / glm_var /
+// glm_dev switches).  Software pipeline: iteration i issues chunk i + 1's
+// loads, the MFMAs of chunk i - 1's bf16 pieces, and chunk i's linear
+// predictors, link math, scaling and split (one wave per SIMD: 4 chunks' worth
+// of registers - accumulators, pieces, current and next chunk).
+template <int NB, bool VEC, int FAM, int PD>
 __global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __restrict__ X, int64_t ld, int64_t n,
                                                              const float* __restrict__ y,
                                                              const float* __restrict__ wprior,
@@ -707,19 +753,27 @@ __global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __rest
   const int64_t r_begin = (int64_t)unit * rows_per_unit;
   const int64_t r_end = min(n, r_begin + rows_per_unit);
   const bool zlane = (NB - 1) * 16 + cl == p + 1;   // this lane's last-block column is z
+  float bl[NB];                                      // this lane's coefficients, one per block
+#pragma unroll
+  for (int b = 0; b < NB; ++b) bl[b] = bsh[b * 16 + cl];
 
   f32x4 acc[T];
 #pragma unroll
   for (int t = 0; t < T; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const double b0 = (double)beta[p];
   double dev_acc = 0.0;
+  u32x4_g H[NB], M[NB], L[NB];   // the previous chunk's pieces (zero before the first)
+#pragma unroll
+  for (int b = 0; b < NB; ++b) H[b] = M[b] = L[b] = u32x4_g{0u, 0u, 0u, 0u};
 
-  float xc[NB][GW_S], xn[NB][GW_S];
-  float yc = 0.f, wc = 1.f, oc = 0.f, yn = 0.f, wn = 1.f, on = 0.f;
-  // Branch-free loads: blocks 0 .. NB-3 are all data columns (p >= 16 NB - 17);
-  // the last two read a clamped column and select data / 1 (intercept) / 0.
-  // Rows past r_end (the last unit's tail chunk) read the clamped last row:
-  // finite values that the zero sqrt(w) of those rows removes from the Gram.
+  // three chunks of registers: this one, and the next two in flight (two
+  // chunks ahead keep ~28 KB per wave outstanding: one wave per SIMD is
+  // latency-bound with only one chunk ahead)
+  float xc[NB][GW_S], xn[NB][GW_S], xm[NB][GW_S];
+  float yc = 0.f, wc = 1.f, oc = 0.f, yn = 0.f, wn = 1.f, on = 0.f, ym = 0.f, wm = 1.f, om = 0.f;
+  // Blocks 0 .. NB-3 are all data columns (p >= 16 NB - 17); the last two read
+  // a clamped column and select data / 1 (intercept) / 0.  Rows past r_end
+  // (the last unit's tail chunk) load as 0 and get a zero sqrt(w).
   auto load = [&](int64_t r0, float (&xb)[NB][GW_S], float& yv, float& wv, float& ov) {
     const int64_t rr = r0 + h * GW_S;
     const bool full = VEC && r0 + GW_RB <= r_end;
@@ -733,9 +787,9 @@ __global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __rest
           const float4 v = *reinterpret_cast<const float4*>(src + rr + 4 * q);
           xb[b][4 * q] = v.x; xb[b][4 * q + 1] = v.y; xb[b][4 * q + 2] = v.z; xb[b][4 * q + 3] = v.w;
         }
-      } else {
+      } else {   // (guarded loads: a form the 16-byte path above is not merged with)
 #pragma unroll
-        for (int s = 0; s < GW_S; ++s) xb[b][s] = src[min(rr + s, r_end - 1)];
+        for (int s = 0; s < GW_S; ++s) xb[b][s] = (rr + s < r_end) ? src[rr + s] : 0.0f;
       }
       if (b >= NB - 2) {
         const float k = (c == p) ? 1.0f : 0.0f;   // intercept column
@@ -748,17 +802,31 @@ __global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __rest
     wv = wprior ? wprior[row] : 1.0f;
     ov = offset ? offset[row] : 0.0f;
   };
-  auto compute = [&](int64_t r0, float (&xb)[NB][GW_S], float yv, float wv, float ov) {
+  // upper Gram tiles of the pieces in H / M / L: 6 significant products per tile
+  auto gram = [&]() {
+    int t = 0;
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int bj = bi; bj < NB; ++bj, ++t) {
+        f32x4 a = acc[t];
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(M[bi]), as_bf16x8(M[bj]), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(L[bi]), as_bf16x8(H[bj]), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[bi]), as_bf16x8(L[bj]), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(M[bi]), as_bf16x8(H[bj]), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[bi]), as_bf16x8(M[bj]), a, 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[bi]), as_bf16x8(H[bj]), a, 0, 0, 0);
+      }
+  };
+  auto prepare = [&](int64_t r0, float (&xb)[NB][GW_S], float yv, float wv, float ov) {
     // 1. partial linear predictors of the lane's 8 rows over its NB columns
     float pf[GW_S];
 #pragma unroll
     for (int s = 0; s < GW_S; ++s) pf[s] = 0.f;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const float bc = bsh[b * 16 + cl];
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
-      for (int s = 0; s < GW_S; ++s) pf[s] = fmaf(xb[b][s], bc, pf[s]);
-    }
+      for (int s = 0; s < GW_S; ++s) pf[s] = fmaf(xb[b][s], bl[b], pf[s]);
     // 2. fp64 sum over the 16 column lanes: butterfly over lane bit 3, then a
     //    reduce-scatter over bits 2..0 -> lane c owns row c % 8
     double part[GW_S];
@@ -777,18 +845,29 @@ __global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __rest
         part[j] = (hi ? part[j + off] : part[j]) + recv;
       }
     }
-    // 3. link / IRLS weight / working response / deviance of this lane's row
+    // 3. IRLS weight / working response / deviance of this lane's row
     const int64_t row = r0 + h * GW_S + (cl & (GW_S - 1));
-    float sw = 0.f, zz = 0.f;
-    if (row < r_end) {
-      const double eta = part[0] + b0 + (double)ov;
+    const bool live = row < r_end;
+    const double eta = part[0] + b0 + (double)ov;
+    float sw, zz;
+    double dv;
+    if (FAM == 1) {
+#if GLM_ROW_F32
+      glm_row_binomial_f32(eta, ov, yv, wv, sw, zz, dv);
+#else
+      glm_row_binomial(eta, (double)ov, (double)yv, (double)wv, sw, zz, dv);
+#endif
+    } else {
       double mu, dmu;
       glm_link(P, eta, mu, dmu);
       const double wi = (double)wv * dmu * dmu / glm_var(P, mu);
       zz = (float)(eta - (double)ov + ((double)yv - mu) / dmu);
       sw = (float)sqrt(fmax(wi, 0.0));
-      if (cl < GW_S) dev_acc += (double)wv * glm_dev(P, (double)yv, mu);
+      dv = (double)wv * glm_dev(P, (double)yv, mu);
     }
+    sw = live ? sw : 0.f;
+    zz = live ? zz : 0.f;
+    dev_acc += (live && cl < GW_S) ? dv : 0.0;   // lanes c and c + 8 share a row
     // 4. scale by sqrt(w) of the rows (the intercept column becomes sqrt(w)),
     //    z column, then the exact bf16 pieces of every block
     const int base = lane & 48;
@@ -800,36 +879,33 @@ __global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __rest
       for (int b = 0; b < NB; ++b) xb[b][s] *= sws;
       xb[NB - 1][s] = zlane ? zs * sws : xb[NB - 1][s];
     }
-    u32x4_g H[NB], M[NB], L[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) split3_bf16(xb[b], H[b], M[b], L[b]);
-    // 5. upper Gram tiles: the 6 significant piece products per tile
-    int t = 0;
-#pragma unroll
-    for (int bi = 0; bi < NB; ++bi)
-#pragma unroll
-      for (int bj = bi; bj < NB; ++bj, ++t) {
-        f32x4 a = acc[t];
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(M[bi]), as_bf16x8(M[bj]), a, 0, 0, 0);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(L[bi]), as_bf16x8(H[bj]), a, 0, 0, 0);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[bi]), as_bf16x8(L[bj]), a, 0, 0, 0);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(M[bi]), as_bf16x8(H[bj]), a, 0, 0, 0);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[bi]), as_bf16x8(M[bj]), a, 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[bi]), as_bf16x8(H[bj]), a, 0, 0, 0);
-      }
   };
 
   int64_t r0 = r_begin;
   if (r0 < r_end) load(r0, xc, yc, wc, oc);
+  if (PD == 2 && r0 + GW_RB < r_end) load(r0 + GW_RB, xn, yn, wn, on);
   for (; r0 < r_end; r0 += GW_RB) {
-    if (r0 + GW_RB < r_end) load(r0 + GW_RB, xn, yn, wn, on);
-    compute(r0, xc, yc, wc, oc);
+    // PD = 1: the next chunk in flight; PD = 2: the next two (register copies
+    // rotate the buffers: unrolled renaming made the allocator spill)
+    if (r0 + PD * GW_RB < r_end) {
+      if (PD == 2) load(r0 + 2 * GW_RB, xm, ym, wm, om);
+      else load(r0 + GW_RB, xn, yn, wn, on);
+    }
+    gram();                        // previous chunk (zero pieces on the first pass)
+    prepare(r0, xc, yc, wc, oc);   // this chunk -> H / M / L
 #pragma unroll
     for (int b = 0; b < NB; ++b)
 #pragma unroll
-      for (int s = 0; s < GW_S; ++s) xc[b][s] = xn[b][s];
+      for (int s = 0; s < GW_S; ++s) {
+        xc[b][s] = xn[b][s];
+        if (PD == 2) xn[b][s] = xm[b][s];
+      }
     yc = yn; wc = wn; oc = on;
+    if (PD == 2) { yn = ym; wn = wm; on = om; }
   }
+  gram();                          // the last chunk
   float* out = slab + (int64_t)unit * PW * PW;
   int t = 0;
 #pragma unroll
@@ -2422,6 +2498,13 @@ H2OMX_API int h2omx_glm_irls_wave(const float* X, int64_t ld, int64_t n, const f
   return launch_status();
 }
 
+static int glm_split_pd = 1;   // chunks in flight ahead of the one computed (1 or 2)
+H2OMX_API int h2omx_glm_split_set_prefetch(int pd) {
+  if (pd != 1 && pd != 2) return kBadArg;
+  glm_split_pd = pd;
+  return kOk;
+}
+
 // glm_irls_split_kernel: same contract and slab layout as h2omx_glm_irls_wave
 // for an NA-free design (`means` is not read)
 H2OMX_API int h2omx_glm_irls_split(const float* X, int64_t ld, int64_t n, const float* y, const float* wprior,
@@ -2435,11 +2518,27 @@ H2OMX_API int h2omx_glm_irls_split(const float* X, int64_t ld, int64_t n, const 
     return kBadArg;
   const int nb = (P.p + 2 + 15) / 16;
   const bool vec = (ld % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0);
+  const bool logit = P.family == 1 && P.link == 1;
   const int blocks = cdiv(n_units, 4);
-#define GSL(NB, V)                                                                                             \
-  hipLaunchKernelGGL((glm_irls_split_kernel<NB, V>), dim3(blocks), dim3(256), 0, stream, X, ld, n, y, wprior,   \
-                     offset, beta, P, rows_per_unit, n_units, slab, dev_out)
-#define GSL_NB(NB) do { if (vec) GSL(NB, true); else GSL(NB, false); } while (0)
+#define GSL(NB, V, F)                                                                                          \
+  do {                                                                                                         \
+    if (glm_split_pd == 2)                                                                                     \
+      hipLaunchKernelGGL((glm_irls_split_kernel<NB, V, F, 2>), dim3(blocks), dim3(256), 0, stream, X, ld, n, y, \
+                         wprior, offset, beta, P, rows_per_unit, n_units, slab, dev_out);                      \
+    else                                                                                                       \
+      hipLaunchKernelGGL((glm_irls_split_kernel<NB, V, F, 1>), dim3(blocks), dim3(256), 0, stream, X, ld, n, y, \
+                         wprior, offset, beta, P, rows_per_unit, n_units, slab, dev_out);                      \
+  } while (0)
+#define GSL_NB(NB)                      \
+  do {                                  \
+    if (logit) {                        \
+      if (vec) GSL(NB, true, 1);        \
+      else GSL(NB, false, 1);           \
+    } else {                            \
+      if (vec) GSL(NB, true, 0);        \
+      else GSL(NB, false, 0);           \
+    }                                   \
+  } while (0)
   switch (nb) {
     case 1: GSL_NB(1); break;
     case 2: GSL_NB(2); break;
