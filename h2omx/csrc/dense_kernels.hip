@@ -664,7 +664,7 @@ __global__ __launch_bounds__(256) void glm_irls_wave_kernel(const float* __restr
 // lane sums <= NB products; the 16-lane reduction stays fp64).
 // ---------------------------------------------------------------------------
 #ifndef GLM_ROW_F32
-#define GLM_ROW_F32 1
+#define GLM_ROW_F32 0   // fp32 binomial row math: measured no faster (profiles/r4/dense), fp64 kept
 #endif
 typedef __bf16 bf16x8_g __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4_g __attribute__((ext_vector_type(4)));
@@ -731,7 +731,11 @@ __device__ __forceinline__ void glm_row_binomial_f32(double eta_d, float ov, flo
 // loads, the MFMAs of chunk i - 1's bf16 pieces, and chunk i's linear
 // predictors, link math, scaling and split (one wave per SIMD: 4 chunks' worth
 // of registers - accumulators, pieces, current and next chunk).
-template <int NB, bool VEC, int FAM, int PD>
+// G: full chunks staged global -> LDS by LDS-DMA (global_load_lds_dwordx4), two
+// chunks in flight per wave in two LDS slots, read back lane-linear (each
+// lane its own 16-byte pieces) - no prefetch registers, no register copies.
+// !G: one chunk ahead in registers (unaligned designs).
+template <int NB, bool VEC, int FAM, bool G>
 __global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __restrict__ X, int64_t ld, int64_t n,
                                                              const float* __restrict__ y,
                                                              const float* __restrict__ wprior,
@@ -741,7 +745,12 @@ __global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __rest
                                                              float* __restrict__ slab, double* __restrict__ dev_out) {
   constexpr int PW = NB * 16;
   constexpr int T = NB * (NB + 1) / 2;
-  __shared__ float bsh[PW];
+  // ONE shared array (per-slot staging of every wave, then the coefficients):
+  // the compiler's LDS-DMA wait tracking then needs no extra vmcnt(0)
+  constexpr int SLOTF = NB * 512 + 192;      // floats: NB x 2 x 64 lanes x 16 B, then y / w / offset
+  constexpr int GLDS = G ? 4 * 2 * SLOTF : 0;
+  __shared__ __attribute__((aligned(16))) float lds_all[GLDS + PW];
+  float* bsh = lds_all + GLDS;
   const int p = P.p;
   for (int c = threadIdx.x; c < PW; c += blockDim.x) bsh[c] = (c < p) ? beta[c] : 0.0f;
   __syncthreads();   // the only barrier: before any wave can leave
@@ -766,11 +775,8 @@ __global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __rest
 #pragma unroll
   for (int b = 0; b < NB; ++b) H[b] = M[b] = L[b] = u32x4_g{0u, 0u, 0u, 0u};
 
-  // three chunks of registers: this one, and the next two in flight (two
-  // chunks ahead keep ~28 KB per wave outstanding: one wave per SIMD is
-  // latency-bound with only one chunk ahead)
-  float xc[NB][GW_S], xn[NB][GW_S], xm[NB][GW_S];
-  float yc = 0.f, wc = 1.f, oc = 0.f, yn = 0.f, wn = 1.f, on = 0.f, ym = 0.f, wm = 1.f, om = 0.f;
+  float xc[NB][GW_S], xn[NB][GW_S];
+  float yc = 0.f, wc = 1.f, oc = 0.f, yn = 0.f, wn = 1.f, on = 0.f;
   // Blocks 0 .. NB-3 are all data columns (p >= 16 NB - 17); the last two read
   // a clamped column and select data / 1 (intercept) / 0.  Rows past r_end
   // (the last unit's tail chunk) load as 0 and get a zero sqrt(w).
@@ -883,27 +889,100 @@ __global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __rest
     for (int b = 0; b < NB; ++b) split3_bf16(xb[b], H[b], M[b], L[b]);
   };
 
-  int64_t r0 = r_begin;
-  if (r0 < r_end) load(r0, xc, yc, wc, oc);
-  if (PD == 2 && r0 + GW_RB < r_end) load(r0 + GW_RB, xn, yn, wn, on);
-  for (; r0 < r_end; r0 += GW_RB) {
-    // PD = 1: the next chunk in flight; PD = 2: the next two (register copies
-    // rotate the buffers: unrolled renaming made the allocator spill)
-    if (r0 + PD * GW_RB < r_end) {
-      if (PD == 2) load(r0 + 2 * GW_RB, xm, ym, wm, om);
-      else load(r0 + GW_RB, xn, yn, wn, on);
-    }
-    gram();                        // previous chunk (zero pieces on the first pass)
-    prepare(r0, xc, yc, wc, oc);   // this chunk -> H / M / L
+  if (G) {
+    const int wid = threadIdx.x >> 6;
+    // chunk r (full) -> slot: per block two 1 KB lane-linear pieces, then y / w / offset
+    auto issue = [&](int64_t r, int slot) {
+      float* sb = lds_all + (wid * 2 + slot) * SLOTF;
+      const int64_t rr = r + h * GW_S;
 #pragma unroll
-    for (int b = 0; b < NB; ++b)
+      for (int b = 0; b < NB; ++b) {
+        const int c = b * 16 + cl;
+        const float* src = X + (int64_t)(b >= NB - 2 ? min(c, p - 1) : c) * ld + rr;
 #pragma unroll
-      for (int s = 0; s < GW_S; ++s) {
-        xc[b][s] = xn[b][s];
-        if (PD == 2) xn[b][s] = xm[b][s];
+        for (int q = 0; q < GW_S / 4; ++q)
+          __builtin_amdgcn_global_load_lds(src + 4 * q, sb + (b * 2 + q) * 256, 16, 0, 0);
       }
-    yc = yn; wc = wn; oc = on;
-    if (PD == 2) { yn = ym; wn = wm; on = om; }
+      const int64_t row = r + h * GW_S + (cl & (GW_S - 1));
+      __builtin_amdgcn_global_load_lds(y + row, sb + NB * 512, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((wprior ? wprior : y) + row, sb + NB * 512 + 64, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((offset ? offset : y) + row, sb + NB * 512 + 128, 4, 0, 0);
+    };
+    // s_waitcnt immediates (gfx9 encoding; expcnt / lgkmcnt left at their maxima)
+    constexpr int NI = 2 * NB + 3;                                   // LDS-DMAs per chunk
+    constexpr int W_ONE = (NI & 15) | (7 << 4) | (15 << 8) | ((NI >> 4) << 14);   // vmcnt <= NI
+    constexpr int W_ALL = (7 << 4) | (15 << 8);                      // vmcnt 0
+    const int64_t nfull = (r_end - r_begin) / GW_RB;
+    if (nfull > 0) issue(r_begin, 0);
+    if (nfull > 1) issue(r_begin + GW_RB, 1);
+    for (int64_t i = 0; i < nfull; ++i) {
+      const int64_t r = r_begin + i * GW_RB;
+      const int slot = (int)(i & 1);
+      if (i + 1 < nfull) __builtin_amdgcn_s_waitcnt(W_ONE);          // chunk i landed, i + 1 in flight
+      else __builtin_amdgcn_s_waitcnt(W_ALL);
+      // the slot's reads in inline asm: hipcc cannot see that they only touch
+      // the landed chunk and would drain every LDS-DMA (vmcnt(0)) before a
+      // compiler-visible ds_read; one lgkmcnt(0) wait, then register fences
+      // order every use after it (and the slot's refill after the reads)
+      const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(
+                              lds_all + (wid * 2 + slot) * SLOTF) + (uint32_t)lane * 16u;
+      const uint32_t lb = la - (uint32_t)lane * 12u;   // + lane * 4: the y / w / offset rows
+      f32x4 t[NB][2];
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(t[b][q]) : "v"(la), "i"((b * 2 + q) * 1024));
+      float ty, tw, to;
+      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(ty) : "v"(lb), "i"(NB * 2048));
+      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(tw) : "v"(lb), "i"(NB * 2048 + 256));
+      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(to) : "v"(lb), "i"(NB * 2048 + 512));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) asm volatile("" : "+v"(t[b][q]));
+      asm volatile("" : "+v"(ty), "+v"(tw), "+v"(to));
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int c = b * 16 + cl;
+#pragma unroll
+        for (int q = 0; q < GW_S / 4; ++q) {
+          const f32x4 v = t[b][q];
+          xc[b][4 * q] = v[0]; xc[b][4 * q + 1] = v[1]; xc[b][4 * q + 2] = v[2]; xc[b][4 * q + 3] = v[3];
+        }
+        if (b >= NB - 2) {
+          const float kk = (c == p) ? 1.0f : 0.0f;   // intercept column
+#pragma unroll
+          for (int s = 0; s < GW_S; ++s) xc[b][s] = (c < p) ? xc[b][s] : kk;
+        }
+      }
+      yc = ty;
+      wc = wprior ? tw : 1.0f;
+      oc = offset ? to : 0.0f;
+      if (i + 2 < nfull) issue(r + 2 * GW_RB, slot);
+      gram();                        // previous chunk (zero pieces on the first pass)
+      prepare(r, xc, yc, wc, oc);    // this chunk -> H / M / L
+    }
+    const int64_t rt = r_begin + nfull * GW_RB;   // partial tail chunk: ordinary guarded loads
+    if (rt < r_end) {
+      load(rt, xc, yc, wc, oc);
+      gram();
+      prepare(rt, xc, yc, wc, oc);
+    }
+  } else {
+    int64_t r0 = r_begin;
+    if (r0 < r_end) load(r0, xc, yc, wc, oc);
+    for (; r0 < r_end; r0 += GW_RB) {
+      if (r0 + GW_RB < r_end) load(r0 + GW_RB, xn, yn, wn, on);
+      gram();                        // previous chunk (zero pieces on the first pass)
+      prepare(r0, xc, yc, wc, oc);   // this chunk -> H / M / L
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int s = 0; s < GW_S; ++s) xc[b][s] = xn[b][s];
+      yc = yn; wc = wn; oc = on;
+    }
   }
   gram();                          // the last chunk
   float* out = slab + (int64_t)unit * PW * PW;
@@ -2498,10 +2577,9 @@ H2OMX_API int h2omx_glm_irls_wave(const float* X, int64_t ld, int64_t n, const f
   return launch_status();
 }
 
-static int glm_split_pd = 1;   // chunks in flight ahead of the one computed (1 or 2)
-H2OMX_API int h2omx_glm_split_set_prefetch(int pd) {
-  if (pd != 1 && pd != 2) return kBadArg;
-  glm_split_pd = pd;
+static int glm_split_glds = 1;   // LDS-DMA staging of aligned designs (0: register prefetch; A/B)
+H2OMX_API int h2omx_glm_split_set_prefetch(int glds) {
+  glm_split_glds = glds ? 1 : 0;
   return kOk;
 }
 
@@ -2522,12 +2600,12 @@ H2OMX_API int h2omx_glm_irls_split(const float* X, int64_t ld, int64_t n, const 
   const int blocks = cdiv(n_units, 4);
 #define GSL(NB, V, F)                                                                                          \
   do {                                                                                                         \
-    if (glm_split_pd == 2)                                                                                     \
-      hipLaunchKernelGGL((glm_irls_split_kernel<NB, V, F, 2>), dim3(blocks), dim3(256), 0, stream, X, ld, n, y, \
+    if (V && glm_split_glds)                                                                                   \
+      hipLaunchKernelGGL((glm_irls_split_kernel<NB, V, F, V>), dim3(blocks), dim3(256), 0, stream, X, ld, n, y,  \
                          wprior, offset, beta, P, rows_per_unit, n_units, slab, dev_out);                      \
     else                                                                                                       \
-      hipLaunchKernelGGL((glm_irls_split_kernel<NB, V, F, 1>), dim3(blocks), dim3(256), 0, stream, X, ld, n, y, \
-                         wprior, offset, beta, P, rows_per_unit, n_units, slab, dev_out);                      \
+      hipLaunchKernelGGL((glm_irls_split_kernel<NB, V, F, false>), dim3(blocks), dim3(256), 0, stream, X, ld, n, \
+                         y, wprior, offset, beta, P, rows_per_unit, n_units, slab, dev_out);                   \
   } while (0)
 #define GSL_NB(NB)                      \
   do {                                  \
@@ -2552,6 +2630,29 @@ H2OMX_API int h2omx_glm_irls_split(const float* X, int64_t ld, int64_t n, const 
   }
 #undef GSL_NB
 #undef GSL
+  return launch_status();
+}
+
+__global__ __launch_bounds__(256) void dev_sum_kernel(const double* __restrict__ d, int n, double* __restrict__ out) {
+  __shared__ double red[4];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) a += d[i];   // fixed order per thread
+  a = wave_sum(a);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// GLM pass epilogue: out = [sum of the slabs (pw * pw) | sum of dev (1) |
+// SLAB_SPLIT * pw * pw partials]; one contiguous read-back for the host
+H2OMX_API int h2omx_slab_reduce16_dev(const float* slab, int n_slabs, int pw, const double* dev, double* out,
+                                      hipStream_t stream) {
+  const int64_t w = (int64_t)pw * pw;
+  double* part = out + w + 1;
+  hipLaunchKernelGGL(slab_reduce16_kernel, dim3(cdiv(w, 256), SLAB_SPLIT), dim3(256), 0, stream, slab, n_slabs, pw,
+                     part);
+  hipLaunchKernelGGL(slab_fold_kernel, dim3(cdiv(w, 256)), dim3(256), 0, stream, part, w, out);
+  hipLaunchKernelGGL(dev_sum_kernel, dim3(1), dim3(256), 0, stream, dev, n_slabs, out + w);
   return launch_status();
 }
 

@@ -72,6 +72,7 @@ DENSE_SIGS = {
     "h2omx_glm_irls_wave": "PLLPPPPPPILPPS",
     "h2omx_glm_irls_split": "PLLPPPPPPILPPS",
     "h2omx_glm_split_set_prefetch": "I",
+    "h2omx_slab_reduce16_dev": "PIIPPS",
     "h2omx_slab_reduce16": "PIIPS",
     "h2omx_slab_sum": "PIIPS",
     "h2omx_slab_sum_f32": "PIIPS",

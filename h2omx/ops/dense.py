@@ -30,8 +30,8 @@ GLM_UNIT_MIN_ROWS = 512
 # Gram of the wave path: "split" = exact 3-way bf16 split on the bf16 matrix
 # cores (glm_irls_split_kernel), "f32" = fp32 MFMA (glm_irls_wave_kernel)
 GLM_GRAM = os.environ.get("H2OMX_GLM_GRAM", "split")
-# chunks the split kernel keeps in flight ahead of the one it computes (1 or 2)
-GLM_PD = int(os.environ.get("H2OMX_GLM_PD", "1"))
+# the split kernel stages aligned designs through LDS by LDS-DMA (0: register prefetch)
+GLM_PD = int(os.environ.get("H2OMX_GLM_GLDS", "1"))   # LDS-DMA staging on/off (A/B)
 _GLM_PD_SET = [None]
 SLAB_SPLIT = 32          # dense_kernels.hip slab_reduce16_kernel
 KM_WGS = int(os.environ.get("H2OMX_KM_WGS", "1024"))
@@ -194,26 +194,26 @@ def _glm_irls_wave(X, y, wprior, offset, beta, family, link, cls, var_power, lin
     units = max(1, math.ceil(n / rows))
     slab = torch.empty((units * pw * pw,), dtype=torch.float32, device=dev)
     devs = torch.empty((units,), dtype=torch.float64, device=dev)
-    # sum | SLAB_SPLIT partials | the deviance
+    # sum [pw * pw] | the deviance | SLAB_SPLIT partials (h2omx_slab_reduce16_dev)
     out = torch.empty(((SLAB_SPLIT + 1) * pw * pw + 1,), dtype=torch.float64, device=dev)
-    b32 = torch.from_numpy(np.ascontiguousarray(beta, np.float32)).to(dev)
-    means = torch.zeros((max(p, 1),), dtype=torch.float32, device=dev)
+    b32 = _pinned_to(np.ascontiguousarray(beta, np.float32).ravel(), dev)
+    split = GLM_GRAM == "split" and p >= 1
+    means = None if split else torch.zeros((max(p, 1),), dtype=torch.float32, device=dev)
     gp = GlmParams(FAMILIES[family], LINKS[link], p, K, cls, 0, var_power, link_power)
     Xc = X if X.stride(1) == 1 else X.contiguous()
     st = stream(dev)
     if _GLM_PD_SET[0] != GLM_PD:
         check(lib.h2omx_glm_split_set_prefetch(GLM_PD), "glm_split_set_prefetch")
         _GLM_PD_SET[0] = GLM_PD
-    fn = lib.h2omx_glm_irls_split if (GLM_GRAM == "split" and p >= 1) else lib.h2omx_glm_irls_wave
+    fn = lib.h2omx_glm_irls_split if split else lib.h2omx_glm_irls_wave
     check(fn(P(Xc), Xc.stride(0), n, P(y), P(wprior), P(offset), P(means), P(b32),
              ctypes.addressof(gp), units, rows, P(slab), P(devs), st), "glm_irls_wave")
-    check(lib.h2omx_slab_reduce16(P(slab), units, pw, P(out), st), "slab_reduce16")
     # the Gram and the deviance come back in ONE device -> host copy (one sync)
-    out[-1] = devs.sum()
-    host = torch.cat([out[: pw * pw], out[-1:]]).cpu().numpy()
+    check(lib.h2omx_slab_reduce16_dev(P(slab), units, pw, P(devs), P(out), st), "slab_reduce16_dev")
+    host = out[: pw * pw + 1].cpu().numpy()
     G = host[: pw * pw].reshape(pw, pw)[: p + 2, : p + 2]
     G = np.triu(G) + np.triu(G, 1).T
-    return G, float(host[-1])
+    return G, float(host[pw * pw])
 
 
 # ---------------------------------------------------------------------------
@@ -345,6 +345,22 @@ def workspace_ns(ns: int):
         yield
     finally:
         _WS_NS[0] = old
+
+
+_PINNED: dict = {}
+
+
+def _pinned_to(a: np.ndarray, dev) -> torch.Tensor:
+    """Small host array -> device through a reused pinned staging buffer (an
+    asynchronous copy on the current stream; callers sync before the next
+    reuse, e.g. the GLM pass reads its result back)."""
+    key = (str(dev), a.dtype.str, a.size)
+    hb = _PINNED.get(key)
+    if hb is None:
+        hb = torch.empty((a.size,), dtype=torch.from_numpy(a[:0]).dtype).pin_memory()
+        _PINNED[key] = hb
+    hb.numpy()[:] = a
+    return hb.to(dev, non_blocking=True)
 
 
 def _workspace(dev, numel: int, slot: int = 0) -> torch.Tensor:
