@@ -1827,9 +1827,14 @@ __global__ __launch_bounds__(GW_T) void gemm_w64_kernel(const float* __restrict_
 // streams its A row with float4 loads (B rows stay in L1/L2) and reduces
 // the N dot products with wave shuffles.
 constexpr int SKINNY_N = 8;
+// (y != nullptr: softmax cross-entropy epilogue - the row's N logits are in
+// every lane after the wave reduction, so dZ = (softmax - onehot(y)) / M is
+// written beside them with softmax_xent_kernel's exact arithmetic)
 __global__ __launch_bounds__(256) void gemm_skinny_nt_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                              float* __restrict__ C, const float* __restrict__ bias,
-                                                             int M, int N, int K, int act) {
+                                                             int M, int N, int K, int act,
+                                                             const int* __restrict__ y = nullptr,
+                                                             float* __restrict__ dZ = nullptr) {
   const int lane = threadIdx.x & 63;
   const int waves = gridDim.x * (blockDim.x >> 6);
   const bool vec = (K % 4 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0) &&
@@ -1872,6 +1877,28 @@ __global__ __launch_bounds__(256) void gemm_skinny_nt_kernel(const float* __rest
       if (act == 1) v = fmaxf(v, 0.0f);
       else if (act == 2) v = tanhf(v);
       C[(int64_t)i * N + lane] = v;
+    }
+    if (y != nullptr) {
+      float z[SKINNY_N];
+#pragma unroll
+      for (int n = 0; n < SKINNY_N; ++n) z[n] = (n < N) ? acc[n] + (bias ? bias[n] : 0.0f) : 0.0f;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int n = 0; n < SKINNY_N; ++n)
+        if (n < N) mx = fmaxf(mx, z[n]);
+      float den = 0.0f;
+#pragma unroll
+      for (int n = 0; n < SKINNY_N; ++n)
+        if (n < N) den += __expf(z[n] - mx);
+      const int yi = y[i];
+      if (lane < N) {
+        float zl = 0.0f;
+#pragma unroll
+        for (int n = 0; n < SKINNY_N; ++n)
+          if (n == lane) zl = z[n];
+        const float pk = __expf(zl - mx) / den;
+        dZ[(int64_t)i * N + lane] = (pk - (lane == yi ? 1.0f : 0.0f)) / (float)M;
+      }
     }
   }
 }
@@ -2094,6 +2121,83 @@ __global__ __launch_bounds__(256) void thin_dact_kernel(const float* __restrict_
   }
 }
 
+// The output layer's whole backward in one pass over its input H [M][N]
+// (out_wgrad_kernel + thin_dact_kernel fused: both stream the same H and dZ
+// with the same (column block, row slice) grid): the weight / bias gradient
+// partial rows -> wsw[slice][C * N + C], dZ_prev = (dZ W) * act'(H) -> out and
+// its column partial sums -> wsb[slice][N].  Same arithmetic, same order.
+template <int C>
+__global__ __launch_bounds__(256) void out_backward_kernel(const float* __restrict__ dZ, const float* __restrict__ H,
+                                                           const float* __restrict__ W, float* __restrict__ out,
+                                                           float* __restrict__ wsw, float* __restrict__ wsb, int M,
+                                                           int N, int act) {
+  const int64_t T = (int64_t)C * N + C;
+  __shared__ float4 red[4][64][C];
+  __shared__ float4 redb[4][64];
+  const int c4 = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int j = (blockIdx.x * 64 + c4) * 4;
+  const int S = gridDim.y;
+  const int rows = (M + S - 1) / S;
+  const int r0 = blockIdx.y * rows, r1 = min(M, r0 + rows);
+  float4 acc[C];
+  float bs[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) { acc[c] = make_float4(0.f, 0.f, 0.f, 0.f); bs[c] = 0.f; }
+  float4 sb = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (j < N) {
+    float4 w[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) w[c] = *reinterpret_cast<const float4*>(W + (int64_t)c * N + j);
+    for (int i = r0 + ph; i < r1; i += 4) {
+      const int64_t e = (int64_t)i * N + j;
+      const float4 h = *reinterpret_cast<const float4*>(H + e);
+      float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float z = dZ[(int64_t)i * C + c];
+        acc[c].x += z * h.x; acc[c].y += z * h.y; acc[c].z += z * h.z; acc[c].w += z * h.w;
+        bs[c] += z;
+        g.x += z * w[c].x; g.y += z * w[c].y; g.z += z * w[c].z; g.w += z * w[c].w;
+      }
+      g = make_float4(act_grad(g.x, h.x, act), act_grad(g.y, h.y, act), act_grad(g.z, h.z, act),
+                      act_grad(g.w, h.w, act));
+      *reinterpret_cast<float4*>(out + e) = g;
+      sb.x += g.x; sb.y += g.y; sb.z += g.z; sb.w += g.w;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) red[ph][c4][c] = acc[c];
+  redb[ph][c4] = sb;
+  __syncthreads();
+  if (ph == 0 && j < N) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float4 a = red[0][c4][c], b = red[1][c4][c], d = red[2][c4][c], e = red[3][c4][c];
+      float* o = wsw + blockIdx.y * T + (int64_t)c * N + j;      // T may be odd: scalar stores
+      o[0] = (a.x + b.x) + (d.x + e.x);
+      o[1] = (a.y + b.y) + (d.y + e.y);
+      o[2] = (a.z + b.z) + (d.z + e.z);
+      o[3] = (a.w + b.w) + (d.w + e.w);
+    }
+    const float4 a = redb[0][c4], b = redb[1][c4], d = redb[2][c4], e = redb[3][c4];
+    *reinterpret_cast<float4*>(wsb + (int64_t)blockIdx.y * N + j) =
+        make_float4((a.x + b.x) + (d.x + e.x), (a.y + b.y) + (d.y + e.y), (a.z + b.z) + (d.z + e.z),
+                    (a.w + b.w) + (d.w + e.w));
+  }
+  if (blockIdx.x == 0) {
+    __syncthreads();
+    float* rb = reinterpret_cast<float*>(red);     // [4 phases][64 lanes][C]
+#pragma unroll
+    for (int c = 0; c < C; ++c) rb[(ph * 64 + c4) * C + c] = (c4 == 0) ? bs[c] : 0.0f;
+    __syncthreads();
+    if (threadIdx.x < C) {
+      const int c = threadIdx.x;
+      wsw[blockIdx.y * T + (int64_t)C * N + c] = (rb[(0 * 64) * C + c] + rb[(1 * 64) * C + c]) +
+                                                 (rb[(2 * 64) * C + c] + rb[(3 * 64) * C + c]);
+    }
+  }
+}
+
 // column sums of dY [M][N] (bias gradients), stage 1: block (64 columns x
 // 4 row phases) sums one row slice, folds the phases in LDS -> ws[slice][col]
 __global__ __launch_bounds__(256) void bias_grad_split_kernel(const float* __restrict__ dY, float* __restrict__ ws,
@@ -2176,6 +2280,62 @@ __global__ __launch_bounds__(256) void adadelta_kernel(float* __restrict__ W, co
   Eg2[i] = eg;
   Edx2[i] = rho * Edx2[i] + (1.0f - rho) * dx * dx;
   W[i] += dx;
+}
+
+// ADADELTA with the last reductions of the backward folded in: gradient
+// entries [off, off + len) are the fp64 sum of `splits` fp32 partial rows
+// (stride floats apart) - the bias gradients' act-backward slices and the
+// output layer's split weight gradient - written back to G and used at once
+// (saves one small launch per layer on launch-bound mini-batch steps)
+struct GradFix {
+  int64_t off;
+  const float* ws;
+  int len, splits, stride, pad;
+};
+constexpr int MAX_GRAD_FIX = 8;
+struct GradFixes {
+  int n, pad;
+  GradFix f[MAX_GRAD_FIX];
+};
+
+__device__ __forceinline__ float grad_fixed(const GradFixes& fx, int64_t i, float gi, bool& fixed) {
+  for (int e = 0; e < fx.n; ++e) {
+    const int64_t j = i - fx.f[e].off;
+    if (j >= 0 && j < fx.f[e].len) {
+      double a = 0.0;
+      for (int s = 0; s < fx.f[e].splits; ++s) a += fx.f[e].ws[(int64_t)s * fx.f[e].stride + j];
+      fixed = true;
+      return (float)a;
+    }
+  }
+  return gi;
+}
+
+__device__ __forceinline__ void adadelta_one(float& w, float g, float& eg2, float& edx2, float rho, float eps,
+                                             float l2) {
+  g += l2 * w;
+  const float eg = rho * eg2 + (1.0f - rho) * g * g;
+  const float dx = -sqrtf(edx2 + eps) / sqrtf(eg + eps) * g;
+  eg2 = eg;
+  edx2 = rho * edx2 + (1.0f - rho) * dx * dx;
+  w += dx;
+}
+
+// one parameter per thread: the few fold entries spread over many threads
+// (a 4-per-thread float4 version measured slower: its fold blocks straggle)
+__global__ __launch_bounds__(256) void adadelta_fix_kernel(float* __restrict__ W, float* __restrict__ G,
+                                                           float* __restrict__ Eg2, float* __restrict__ Edx2, int64_t n,
+                                                           float rho, float eps, float l2, GradFixes fx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool fixed = false;
+  const float gi = grad_fixed(fx, i, G[i], fixed);
+  if (fixed) G[i] = gi;
+  float w = W[i], eg2 = Eg2[i], edx2 = Edx2[i];
+  adadelta_one(w, gi, eg2, edx2, rho, eps, l2);
+  W[i] = w;
+  Eg2[i] = eg2;
+  Edx2[i] = edx2;
 }
 
 __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ W, const float* __restrict__ G,
@@ -2877,6 +3037,16 @@ H2OMX_API int h2omx_gemm_skinny_nt(const float* A, const float* B, float* C, con
   return launch_status();
 }
 
+// output layer + softmax cross-entropy gradient in one launch (act none):
+// Z = A B^T + bias [M][N], dZ = (softmax(Z) - onehot(y)) / M
+H2OMX_API int h2omx_gemm_skinny_softmax(const float* A, const float* B, float* C, const float* bias, int M, int N,
+                                        int K, const int* y, float* dZ, hipStream_t stream) {
+  if (N < 1 || N > SKINNY_N || !y || !dZ) return kBadArg;
+  const int blocks = std::min(cdiv(M, 4), 4096);
+  hipLaunchKernelGGL(gemm_skinny_nt_kernel, dim3(blocks), dim3(256), 0, stream, A, B, C, bias, M, N, K, 0, y, dZ);
+  return launch_status();
+}
+
 H2OMX_API int h2omx_gemm_thin_k(const float* A, const float* B, float* C, int64_t M, int N, int K, const float* act_y,
                                 int act, hipStream_t stream) {
   if (K < 1 || K > 8) return kBadArg;
@@ -2912,6 +3082,29 @@ H2OMX_API int h2omx_out_wgrad(const float* dZ, const float* H, float* out, float
 }
 
 // dZ_prev = (dZ [M][C] W [C][N]) * act'(Y), column partial sums -> ws[splits][N]
+H2OMX_API int h2omx_out_backward(const float* dZ, const float* H, const float* W, float* out, float* wsw, float* wsb,
+                                 int M, int N, int C, int splits, int act, hipStream_t stream) {
+  if (C < 1 || C > OUT_C || N % 4 || splits < 1 || !wsw || !wsb ||
+      ((reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(H) | reinterpret_cast<uintptr_t>(out) |
+        reinterpret_cast<uintptr_t>(wsb)) & 15))
+    return kBadArg;
+  const dim3 grid(cdiv(N, 256), splits);
+#define OB_L(C_) \
+  hipLaunchKernelGGL(out_backward_kernel<C_>, grid, dim3(256), 0, stream, dZ, H, W, out, wsw, wsb, M, N, act)
+  switch (C) {
+    case 1: OB_L(1); break;
+    case 2: OB_L(2); break;
+    case 3: OB_L(3); break;
+    case 4: OB_L(4); break;
+    case 5: OB_L(5); break;
+    case 6: OB_L(6); break;
+    case 7: OB_L(7); break;
+    default: OB_L(8); break;
+  }
+#undef OB_L
+  return launch_status();
+}
+
 H2OMX_API int h2omx_thin_dact(const float* dZ, const float* W, const float* Y, float* out, float* ws, int M, int N,
                               int C, int splits, int act, hipStream_t stream) {
   if (C < 1 || C > OUT_C || N % 4 || splits < 1 || !ws ||
@@ -2976,6 +3169,36 @@ H2OMX_API int h2omx_softmax_xent(const float* Z, const int* y, float* dZ, float*
 H2OMX_API int h2omx_adadelta(float* W, const float* G, float* Eg2, float* Edx2, int64_t n, float rho, float eps,
                              float l2, hipStream_t stream) {
   hipLaunchKernelGGL(adadelta_kernel, dim3(cdiv(n, 256)), dim3(256), 0, stream, W, G, Eg2, Edx2, n, rho, eps, l2);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_adadelta_fix(float* W, float* G, float* Eg2, float* Edx2, int64_t n, float rho, float eps,
+                                 float l2, const void* fixes, hipStream_t stream) {
+  const GradFixes fx = *reinterpret_cast<const GradFixes*>(fixes);
+  if (fx.n < 0 || fx.n > MAX_GRAD_FIX) return kBadArg;
+  hipLaunchKernelGGL(adadelta_fix_kernel, dim3(cdiv(n, 256)), dim3(256), 0, stream, W, G, Eg2, Edx2, n, rho, eps, l2,
+                     fx);
+  return launch_status();
+}
+
+// out_wgrad without its fold: the S partial rows [S][C * N + C] stay in ws
+// (folded later, e.g. by adadelta_fix_kernel)
+H2OMX_API int h2omx_out_wgrad_partial(const float* dZ, const float* H, float* ws, int M, int N, int C, int splits,
+                                      hipStream_t stream) {
+  if (C < 1 || C > OUT_C || N % 4 || splits < 1 || !ws || (reinterpret_cast<uintptr_t>(H) & 15)) return kBadArg;
+  const dim3 grid(cdiv(N, 256), splits);
+#define OW_L(C_) hipLaunchKernelGGL(out_wgrad_kernel<C_>, grid, dim3(256), 0, stream, dZ, H, ws, M, N)
+  switch (C) {
+    case 1: OW_L(1); break;
+    case 2: OW_L(2); break;
+    case 3: OW_L(3); break;
+    case 4: OW_L(4); break;
+    case 5: OW_L(5); break;
+    case 6: OW_L(6); break;
+    case 7: OW_L(7); break;
+    default: OW_L(8); break;
+  }
+#undef OW_L
   return launch_status();
 }
 

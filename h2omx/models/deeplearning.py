@@ -33,6 +33,7 @@ import torch
 
 from ..frame.frame import ENUM, Frame, Vec
 from ..backend import dense as D
+from ..ops import dense as OD
 from .base import Model, ModelBuilder, ModelCategory
 from .glm import DesignInfo
 
@@ -96,8 +97,9 @@ class _Net:
         return off, off + w * f + w
 
 
-def _forward(net: _Net, X, act, train, drop_in, drop_hid, gen_dev, out_act=0):
-    """Returns activations list [X, H1, ..., Z] and the maxout arg masks / dropout masks."""
+def _forward(net: _Net, X, act, train, drop_in, drop_hid, gen_dev, out_act=0, skip_last=False):
+    """Returns activations list [X, H1, ..., Z] and the maxout arg masks / dropout
+    masks (``skip_last``: stop before the output layer, the caller fuses it)."""
     Hs = [X]
     aux = []
     H = X
@@ -110,6 +112,8 @@ def _forward(net: _Net, X, act, train, drop_in, drop_hid, gen_dev, out_act=0):
         last = i == L - 1
         W, b = net.W(i), net.b(i)
         if last:
+            if skip_last:
+                break
             Z = D.gemm(H, W, bias=b, act=out_act, tb=True)
             Hs.append(Z)
             aux.append(None)
@@ -260,6 +264,8 @@ class _DLTrainer:
 
     PROBE_STEPS = 32
     DL_SIDE = os.environ.get("H2OMX_DL_SIDE", "0") == "1"
+    # bias / output-layer gradient folds inside the ADADELTA kernel (fewer launches)
+    FOLD = os.environ.get("H2OMX_DL_FOLD", "1") == "1"
 
     def __init__(self, p_, net, X, Y, act, cls, auto, drop_in, hd, M, steps_per_epoch, comm, gen, gen_dev,
                  n_hidden, backward):
@@ -370,8 +376,11 @@ class _DLTrainer:
             gc.disable()
             try:
                 with torch.cuda.graph(g):
+                    # the group's k mini-batches gathered by two launches, not 2 k
+                    xg = self.X.index_select(0, self.idx_g)
+                    yg = self.Y.index_select(0, self.idx_g) if not self.auto else None
                     for i in range(k):
-                        self._body(self.idx_g[i * M:(i + 1) * M])
+                        self._body(None, xg[i * M:(i + 1) * M], None if yg is None else yg[i * M:(i + 1) * M])
             finally:
                 if gc_was:
                     gc.enable()
@@ -425,24 +434,35 @@ class _DLTrainer:
         elif self.since_sync >= self.spi:
             self.sync()
 
-    def _body(self, idx) -> None:
-        """one mini-batch update (forward, loss gradient, backward, optimizer)"""
+    def _body(self, idx, xb=None, yb=None) -> None:
+        """one mini-batch update (forward, loss gradient, backward, optimizer) of
+        rows ``idx``, or of the pre-gathered batch (xb, yb)"""
         p_, net, M = self.p, self.net, self.M
-        xb = self.X.index_select(0, idx)
+        if xb is None:
+            xb = self.X.index_select(0, idx)
+            yb = self.Y.index_select(0, idx) if not self.auto else None
         mlp = self.mlp
         if mlp is not None:
             xbb, xbt = mlp.load_batch(xb)
             Z = mlp.forward(xbb)
             Hs = aux = None
         else:
-            Hs, aux = _forward(net, xb, self.act, True, self.drop_in, self.hd, self.gen_dev)
+            L = len(net.layers)
+            fuse = self.cls and not self.auto and OD.out_softmax_ok(xb, net.W(L - 1))
+            Hs, aux = _forward(net, xb, self.act, True, self.drop_in, self.hd, self.gen_dev, skip_last=fuse)
+            if fuse:   # output layer + softmax cross-entropy gradient in one launch
+                Z, dZ = OD.gemm_softmax_xent(Hs[-1], net.W(L - 1), net.b(L - 1), yb)
+                Hs.append(Z)
+                aux.append(None)
             Z = Hs[-1]
         if self.auto:
             dZ = (Z - xb) * (2.0 / Z.numel())
+        elif self.cls and mlp is None and fuse:
+            pass
         elif self.cls:
-            dZ, _ = D.softmax_xent(Z, self.Y.index_select(0, idx), with_loss=False)
+            dZ, _ = D.softmax_xent(Z, yb, with_loss=False)
         else:
-            r = Z[:, 0] - self.Y.index_select(0, idx)
+            r = Z[:, 0] - yb
             if self.loss_kind == "absolute":
                 g = torch.sign(r)
             elif self.loss_kind == "huber":
@@ -452,13 +472,23 @@ class _DLTrainer:
                 g = r
             dZ = (g / r.numel())[:, None].contiguous()
         comm = self.comm if self.sync_grad else None
+        folds = None
         if mlp is not None:
             mlp.backward(dZ, xbt, comm, self.world)
+        elif self.adaptive and comm is None and net.flat.is_cuda and self.FOLD:
+            # the last reductions of the backward (bias-gradient slices, the output
+            # layer's split partials) run inside the ADADELTA kernel
+            with OD.defer_grad_folds() as folds:
+                self.backward(net, Hs, aux, dZ, self.act, comm, self.world,
+                              side=self.side if self.side is not None else None)
         elif self.side is not None and comm is None:
             self.backward(net, Hs, aux, dZ, self.act, comm, self.world, side=self.side)
         else:
             self.backward(net, Hs, aux, dZ, self.act, comm, self.world)
-        if self.adaptive:
+        if self.adaptive and folds:
+            OD.adadelta_(net.flat, net.grad, self.Eg2, self.Edx2, float(p_["rho"]), float(p_["epsilon"]), self.l2,
+                         folds=folds)
+        elif self.adaptive:
             D.adadelta_(net.flat, net.grad, self.Eg2, self.Edx2, float(p_["rho"]), float(p_["epsilon"]), self.l2)
         else:
             # H2O's rate is per row: a mean-gradient step over M rows takes M of them
@@ -745,15 +775,25 @@ class H2ODeepLearningEstimator(ModelBuilder):
         bpart = None   # bias-gradient slices of dZ from the fused activation backward
         main = torch.cuda.current_stream(dZ.device) if side is not None else None
         keep = []
+        # per-layer scratch when kernels of different layers may be in flight at
+        # once (side stream) or their partial sums are folded later (deferred folds)
+        layer_ns = side is not None or OD._GRAD_FOLDS[0] is not None
         for i in range(L - 1, -1, -1):
             Hin = Hs[i]
             W = net.W(i)
+            if (i == L - 1 and i > 0 and side is None and comm is None and act in (1, 2) and aux[i - 1][1] is None
+                    and OD.out_backward_ok(dZ, Hin, net.W(i, net.grad), net.b(i, net.grad))):
+                # output layer: weight / bias gradients (a pending fold) and dZ_prev in one pass
+                with OD.workspace_ns(1000 + i):
+                    dZ, bpart = OD.out_backward(dZ, Hin, W, net.W(i, net.grad), net.b(i, net.grad), act)
+                continue
             with contextlib.ExitStack() as es:
                 if side is not None:
                     side.wait_stream(main)
                     es.enter_context(torch.cuda.stream(side))
-                    es.enter_context(D.workspace_ns(1000 + i))
                     keep.append((dZ, Hin, bpart))
+                if layer_ns:
+                    es.enter_context(OD.workspace_ns(1000 + i))
                 if bpart is not None:
                     D.wgrad_bias(dZ, Hin, net.W(i, net.grad), net.b(i, net.grad), bpart)   # dW = dZ^T H, db
                 elif i == L - 1 and D.out_layer_ok(dZ, Hin):
@@ -766,7 +806,7 @@ class H2ODeepLearningEstimator(ModelBuilder):
                 handles.append(comm.all_reduce_async(net.grad[a:b]))
             if i == 0:
                 break
-            with D.workspace_ns(i) if side is not None else contextlib.nullcontext():
+            with OD.workspace_ns(i) if layer_ns else contextlib.nullcontext():
                 dZ, bpart = H2ODeepLearningEstimator._dgrad(Hs, aux, dZ, W, act, i, L)
         if side is not None:
             main.wait_stream(side)

@@ -73,6 +73,10 @@ DENSE_SIGS = {
     "h2omx_glm_irls_split": "PLLPPPPPPILPPS",
     "h2omx_glm_split_set_prefetch": "I",
     "h2omx_slab_reduce16_dev": "PIIPPS",
+    "h2omx_adadelta_fix": "PPPPLFFFPS",
+    "h2omx_out_wgrad_partial": "PPPIIIIS",
+    "h2omx_gemm_skinny_softmax": "PPPPIIIPPS",
+    "h2omx_out_backward": "PPPPPPIIIIIS",
     "h2omx_slab_reduce16": "PIIPS",
     "h2omx_slab_sum": "PIIPS",
     "h2omx_slab_sum_f32": "PIIPS",

@@ -347,6 +347,25 @@ def workspace_ns(ns: int):
         _WS_NS[0] = old
 
 
+# deferred gradient folds (see defer_grad_folds): [(grad view, ws, splits, stride)]
+_GRAD_FOLDS: list = [None]
+
+
+@contextlib.contextmanager
+def defer_grad_folds():
+    """Inside: wgrad_bias (small path) and out_wgrad leave their last reduction
+    (bias-gradient slices, the output layer's split partial rows) as pending
+    folds instead of launching it; :func:`adadelta_` with ``folds`` performs
+    them inside the optimizer kernel.  Yields the list of pending folds.  The
+    workspaces must stay untouched until then (per-layer workspace_ns)."""
+    old = _GRAD_FOLDS[0]
+    _GRAD_FOLDS[0] = []
+    try:
+        yield _GRAD_FOLDS[0]
+    finally:
+        _GRAD_FOLDS[0] = old
+
+
 _PINNED: dict = {}
 
 
@@ -491,11 +510,41 @@ def out_wgrad(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Ten
     if contiguous:
         # the layer's [W | b] gradient span (models/deeplearning.py _Net): write it in place
         out = torch.as_strided(dW, (T,), (1,))
+        if _GRAD_FOLDS[0] is not None and len(_GRAD_FOLDS[0]) < 8:
+            check(dense_lib().h2omx_out_wgrad_partial(P(dZ.contiguous()), P(H), P(ws), M, N, C, S, stream(dZ.device)),
+                  "out_wgrad_partial")
+            _GRAD_FOLDS[0].append((out, ws, S, T))
+            return
     check(dense_lib().h2omx_out_wgrad(P(dZ.contiguous()), P(H), P(out), P(ws), M, N, C, S, stream(dZ.device)),
           "out_wgrad")
     if not contiguous:
         dW.copy_(out[: C * N].view(C, N))
         db.copy_(out[C * N:])
+
+
+def out_backward(dZ: torch.Tensor, H: torch.Tensor, W: torch.Tensor, dW: torch.Tensor, db: torch.Tensor, act: int):
+    """The few-class output layer's backward in one pass (inside
+    defer_grad_folds only): its weight / bias gradient partial rows become a
+    pending fold into the contiguous [dW | db] span, and dZ_prev = (dZ W) *
+    act'(H) comes back with its bias-gradient slices (like thin_dact)."""
+    M, C = dZ.shape
+    N = H.shape[1]
+    _dev(dZ, "out_backward")
+    S = _row_splits(M, N)
+    T = C * N + C
+    wsw = _workspace(dZ.device, S * T)
+    wsb = _workspace(dZ.device, S * N, slot=1)
+    out = torch.empty((M, N), dtype=torch.float32, device=dZ.device)
+    check(dense_lib().h2omx_out_backward(P(dZ.contiguous()), P(H), P(W.contiguous()), P(out), P(wsw), P(wsb), M, N,
+                                         C, S, int(act), stream(dZ.device)), "out_backward")
+    _GRAD_FOLDS[0].append((torch.as_strided(dW, (T,), (1,)), wsw, S, T))
+    return out, (wsb, S)
+
+
+def out_backward_ok(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Tensor) -> bool:
+    return (_GRAD_FOLDS[0] is not None and len(_GRAD_FOLDS[0]) < 8 and out_layer_ok(dZ, H)
+            and dW.is_contiguous() and db.is_contiguous()
+            and db.data_ptr() == dW.data_ptr() + dW.numel() * dW.element_size())
 
 
 def thin_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int):
@@ -589,6 +638,10 @@ def wgrad_bias(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Te
     bws, bsplits = bpart
     if S < 2 or _lib_small_ok(M, N, K, 0, 0.0, None):
         gemm(dZ, H, ta=True, out=dW)
+        if (_GRAD_FOLDS[0] is not None and len(_GRAD_FOLDS[0]) < 8 and db.dtype == torch.float32
+                and db.is_contiguous()):
+            _GRAD_FOLDS[0].append((db, bws, bsplits, M))
+            return
         if db.dtype == torch.float32 and db.is_contiguous():
             check(dense_lib().h2omx_slab_sum_f32(P(bws), bsplits, M, P(db), stream(dZ.device)), "slab_sum_f32")
         else:
@@ -619,6 +672,29 @@ def bias_grad(dY: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor
     return db
 
 
+def out_softmax_ok(H: torch.Tensor, W: torch.Tensor) -> bool:
+    """the output layer Z = H W^T + b of <= 8 classes runs as gemm_skinny_nt"""
+    return W.shape[0] <= 8 and W.shape[1] >= 16 and H.is_cuda
+
+
+def gemm_softmax_xent(H: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y: torch.Tensor):
+    """Output layer and softmax cross-entropy gradient in one launch: returns
+    (Z = H W^T + b, dZ = (softmax(Z) - onehot(y)) / M), the same values as
+    gemm(...) followed by softmax_xent(..., with_loss=False)."""
+    _dev(H, "gemm_softmax_xent")
+    M, K = H.shape
+    N = W.shape[0]
+    H = H.float().contiguous()
+    W = W.float().contiguous()
+    b = b.float().contiguous()
+    y = y.to(torch.int32).contiguous()
+    Z = torch.empty((M, N), dtype=torch.float32, device=H.device)
+    dZ = torch.empty_like(Z)
+    check(dense_lib().h2omx_gemm_skinny_softmax(P(H), P(W), P(Z), P(b), M, N, K, P(y), P(dZ), stream(H.device)),
+          "gemm_skinny_softmax")
+    return Z, dZ
+
+
 def softmax_xent(Z: torch.Tensor, y: torch.Tensor, with_loss: bool = True):
     """Z [M][K] logits, y int32 class ids -> (dZ = (softmax - onehot) / M, mean
     loss); ``with_loss=False`` skips the loss (None) and its zero-fill launch."""
@@ -631,8 +707,32 @@ def softmax_xent(Z: torch.Tensor, y: torch.Tensor, with_loss: bool = True):
     return dZ, loss
 
 
-def adadelta_(W, G, Eg2, Edx2, rho=0.99, eps=1e-8, l2=0.0):
+class _GradFix(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_int64), ("ws", ctypes.c_void_p), ("len", ctypes.c_int), ("splits", ctypes.c_int),
+                ("stride", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
+class _GradFixes(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("pad", ctypes.c_int), ("f", _GradFix * 8)]
+
+
+def adadelta_(W, G, Eg2, Edx2, rho=0.99, eps=1e-8, l2=0.0, folds=None):
+    """ADADELTA step; ``folds`` (from defer_grad_folds): pending gradient
+    reductions, each a view of G summed from its partial rows first."""
     _dev(W, "adadelta_")
+    if folds:
+        fx = _GradFixes()
+        fx.n = len(folds)
+        base = G.data_ptr()
+        for e, (view, ws, splits, stride) in enumerate(folds):
+            fx.f[e].off = (view.data_ptr() - base) // 4
+            fx.f[e].ws = ws.data_ptr()
+            fx.f[e].len = view.numel()
+            fx.f[e].splits = int(splits)
+            fx.f[e].stride = int(stride)
+        check(dense_lib().h2omx_adadelta_fix(P(W), P(G), P(Eg2), P(Edx2), W.numel(), rho, eps, l2,
+                                             ctypes.addressof(fx), stream(W.device)), "adadelta_fix")
+        return
     check(dense_lib().h2omx_adadelta(P(W), P(G), P(Eg2), P(Edx2), W.numel(), rho, eps, l2, stream(W.device)),
           "adadelta")
 

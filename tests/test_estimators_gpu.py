@@ -162,6 +162,25 @@ def test_deeplearning_side_stream_weight_grads_identical(cuda_dev, monkeypatch, 
     assert torch.equal(out[False].net.flat, out[True].net.flat)
 
 
+def test_deeplearning_folds_in_adadelta_match_separate_reduces(cuda_dev, monkeypatch):
+    """Bias-gradient slices and the output layer's split partials folded inside
+    the ADADELTA kernel (H2OMX_DL_FOLD) train the same model as the separate
+    reduce launches: the bias folds are the same fp64 sums, the output layer's
+    fold only changes the fp32 summation order."""
+    from h2omx.models import deeplearning as DLM
+
+    df = _binary_df(n=30000)
+    fr = Frame.from_pandas(df, device=cuda_dev)
+    kw = dict(hidden=[64, 64, 32], epochs=1, seed=6)
+    out = {}
+    for fold in (False, True):
+        monkeypatch.setattr(DLM._DLTrainer, "FOLD", fold)
+        out[fold] = H2ODeepLearningEstimator(**kw).train(y="y", training_frame=fr)
+    a, b = out[False].net.flat, out[True].net.flat
+    assert float((a - b).abs().max()) < 1e-3 * float(a.abs().max())
+    assert abs(out[False].training_metrics["AUC"] - out[True].training_metrics["AUC"]) < 0.005
+
+
 @pytest.mark.parametrize("cls", [H2OGradientBoostingEstimator, H2OXGBoostEstimator, H2ORandomForestEstimator])
 def test_tree_estimators_gpu(cuda_dev, cls):
     df = _binary_df()
