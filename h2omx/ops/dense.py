@@ -561,13 +561,20 @@ def thin_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int):
     return out, (ws, S)
 
 
+# gemm_dact's 128 x 64 output blocks needed to prefer it over GEMM + act_backward_bias
+# (256-row mini-batches: 16 blocks ran 38 us vs 8 + 5 us, profiles/r4/dl/gemm_dact_small_ab_r4ag.txt)
+DACT_MIN_BLOCKS = int(os.environ.get("H2OMX_DACT_MIN_BLOCKS", "128"))
+
+
 def dact_ok(dZ: torch.Tensor, W: torch.Tensor) -> bool:
     """gemm_dact (dZ [M][K] x W [K][N]) pays off when its 128 x 64 blocks fill the
     GPU without split-K (small mini-batches keep the split-K GEMM +
     act_backward_bias pair)"""
     M, K = dZ.shape
     N = W.shape[1]
-    return M % 128 == 0 and N % 64 == 0 and K % 4 == 0 and (M // 128) * (N // 64) >= 128
+    if M % 128 or N % 64 or K % 4:
+        return False
+    return (M // 128) * (N // 64) >= DACT_MIN_BLOCKS
 
 
 def gemm_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int, out: torch.Tensor | None = None,
