@@ -2328,8 +2328,12 @@ __global__ __launch_bounds__(256) void adadelta_fix_kernel(float* __restrict__ W
                                                            float rho, float eps, float l2, GradFixes fx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  // block-uniform test first: most blocks touch no fold range and skip the per-element search
+  const int64_t blo = (int64_t)blockIdx.x * blockDim.x, bhi = blo + blockDim.x;
+  bool touch = false;
+  for (int e = 0; e < fx.n; ++e) touch |= fx.f[e].off < bhi && fx.f[e].off + fx.f[e].len > blo;
   bool fixed = false;
-  const float gi = grad_fixed(fx, i, G[i], fixed);
+  const float gi = touch ? grad_fixed(fx, i, G[i], fixed) : G[i];
   if (fixed) G[i] = gi;
   float w = W[i], eg2 = Eg2[i], edx2 = Edx2[i];
   adadelta_one(w, gi, eg2, edx2, rho, eps, l2);
