@@ -83,7 +83,7 @@ class HipTreeBuilder:
     # rows per workgroup chunk: bounds the fixed-point headroom, so the gradient
     # resolution is 2^30 / (largest chunk) levels (see tree_begin)
     ROWS_CAP = int(os.environ.get("H2OMX_ROWS_CAP", "262144"))
-    SYNC_NODE_CAP = 4096       # above this many potential nodes the host reads the real count
+    SYNC_NODE_CAP = int(os.environ.get("H2OMX_SYNC_NODE_CAP", "4096"))   # above this many potential nodes the host reads the real count
     # wave-compacted histogram kernel for levels > 0 (H2OMX_HIST_COMPACT=1): bit-identical
     # but measured slower (byte gathers of column-major codes are TA-bound:
     # depth-5 HIGGS 2.03 vs 1.52 ms/tree, profiles/compact_hist_p9.txt)
