@@ -34,14 +34,14 @@ class KMeansModel(Model):
 
     def predict_raw(self, frame: Frame) -> torch.Tensor:
         X = self._X(frame)
-        a, _, _, _ = D.kmeans_step(X, torch.from_numpy(self.centers_std.astype(np.float32)).to(X.device), na_free=True)
+        a, _, _, _ = D.kmeans_step(X, self.centers_std.astype(np.float32), na_free=True)
         return a.to(X.device).float()[None, :]
 
     def model_performance(self, frame: Frame | None = None):
         if frame is None:
             return self.training_metrics
         X = self._X(frame)
-        _, _, cnt, sse = D.kmeans_step(X, torch.from_numpy(self.centers_std.astype(np.float32)).to(X.device), na_free=True)
+        _, _, cnt, sse = D.kmeans_step(X, self.centers_std.astype(np.float32), na_free=True)
         totss = float((X.double() - X.double().mean(1, keepdim=True)).pow(2).sum())
         return {"tot_withinss": float(sse.sum()), "totss": totss, "betweenss": totss - float(sse.sum()),
                 "size": cnt.tolist(), "withinss": sse.tolist()}
@@ -85,7 +85,7 @@ class H2OKMeansEstimator(ModelBuilder):
         prev = None
         stats = {}
         for it in range(1, int(p_["max_iterations"]) + 1):
-            assign, sums, cnt, sse = D.kmeans_step(X, torch.from_numpy(C.astype(np.float32)).to(X.device), na_free=True)
+            assign, sums, cnt, sse = D.kmeans_step(X, C.astype(np.float32), na_free=True)
             if comm is not None and comm.world_size > 1:
                 red = comm.all_reduce_numpy(np.concatenate([sums.ravel(), cnt, sse]))
                 sums, cnt, sse = red[: k * d].reshape(k, d), red[k * d: k * d + k], red[k * d + k:]
@@ -104,7 +104,7 @@ class H2OKMeansEstimator(ModelBuilder):
             if changed == 0:
                 break
         # final statistics at the converged centers
-        assign, sums, cnt, sse = D.kmeans_step(X, torch.from_numpy(C.astype(np.float32)).to(X.device), na_free=True)
+        assign, sums, cnt, sse = D.kmeans_step(X, C.astype(np.float32), na_free=True)
         tot = torch.stack([X.double().sum(1), X.double().pow(2).sum(1)])
         nn = float(n)
         if comm is not None and comm.world_size > 1:
@@ -144,7 +144,7 @@ class H2OKMeansEstimator(ModelBuilder):
                     far = np.asarray([best_c[2]], np.float64)
                 C = np.concatenate([C, far])
             for _ in range(int(self.params["max_iterations"])):
-                assign, sums, cnt, sse = D.kmeans_step(X, torch.from_numpy(C.astype(np.float32)).to(X.device), na_free=True)
+                assign, sums, cnt, sse = D.kmeans_step(X, C.astype(np.float32), na_free=True)
                 if comm is not None and comm.world_size > 1:
                     red = comm.all_reduce_numpy(np.concatenate([sums.ravel(), cnt, sse]))
                     d = X.shape[0]

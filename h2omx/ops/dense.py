@@ -219,9 +219,11 @@ def _glm_irls_wave(X, y, wprior, offset, beta, family, link, cls, var_power, lin
 # ---------------------------------------------------------------------------
 # K-Means
 # ---------------------------------------------------------------------------
-def kmeans_step(X: torch.Tensor, C: torch.Tensor, na_free: bool = False):
+def kmeans_step(X: torch.Tensor, C, na_free: bool = False):
     """One Lloyd pass.  X feature-major float32 [d][n] (standardized; NA cells
-    count as 0 unless ``na_free`` asserts there are none), C [k][d].
+    count as 0 unless ``na_free`` asserts there are none), C [k][d] (tensor, or
+    a host array: the MFMA path then builds its padded centroid tables on the
+    host and uploads them in one copy).
     Returns (assign int32 [n], sums float64 [k][d], counts [k], sse [k])."""
     _dev(X, "kmeans_step")
     d, n = X.shape
@@ -229,15 +231,25 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor, na_free: bool = False):
     lib = dense_lib()
     dev = X.device
     Xc = X.contiguous()
+    width = k * d + 2 * k
+    kp = -(-k // 4) * 4 if k <= 16 else -(-k // 8) * 8
+    nt = -(-(d + 2) // 16)
+    if isinstance(C, np.ndarray):
+        if KM_MFMA and k <= 32 and nt <= (8 if kp <= 16 else 4):
+            Cf = np.ascontiguousarray(C, np.float32)
+            Cp = np.zeros((kp, 16 * nt), np.float32)
+            Cp[:k, :d] = Cf
+            cnp = np.full((kp,), np.inf, np.float32)
+            cnp[:k] = (Cf.astype(np.float64) ** 2).sum(1).astype(np.float32)
+            tab = _pinned_to(np.concatenate([Cp.reshape(kp, 8 * nt, 2).transpose(1, 0, 2).ravel(), cnp]), dev)
+            return _kmeans_mfma(Xc, d, n, k, kp, nt, tab[: kp * 16 * nt], tab[kp * 16 * nt:], na_free, width)
+        C = torch.from_numpy(np.ascontiguousarray(C, np.float32)).to(dev)
     Cc = C.float().contiguous()
     cn = (Cc.double() ** 2).sum(1).float()
-    width = k * d + 2 * k
     out = torch.empty((width,), dtype=torch.float64, device=dev)
     assign = torch.empty((n,), dtype=torch.int32, device=dev)
     st = stream(dev)
-    kp = -(-k // 4) * 4 if k <= 16 else -(-k // 8) * 8
     dp = -(-d // 16) * 16
-    nt = -(-(d + 2) // 16)
     if KM_MFMA and k <= 32 and nt <= (8 if kp <= 16 else 4):
         # csrc/kmeans_wave.hip kmeans_mfma_kernel: centroids by feature pair
         # CT2 [8 nt][kp][2] (zero padding), +inf norms for the padding clusters
@@ -246,11 +258,7 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor, na_free: bool = False):
         CT2 = Cp.view(kp, 8 * nt, 2).permute(1, 0, 2).contiguous()
         cnp = torch.full((kp,), float("inf"), dtype=torch.float32, device=dev)
         cnp[:k] = cn
-        n_wg = max(1, min(KM_MFMA_WGS, math.ceil(n / (64 * 4 * 4))))
-        slab = torch.empty((4 * n_wg * width,), dtype=torch.float32, device=dev)
-        check(lib.h2omx_kmeans_mfma(P(Xc), Xc.stride(0), n, d, P(CT2), P(cnp), k, kp, nt, 0 if na_free else 1, n_wg,
-                                    P(assign), P(slab), st), "kmeans_mfma")
-        check(lib.h2omx_slab_sum(P(slab), 4 * n_wg, width, P(out), st), "slab_sum")
+        return _kmeans_mfma(Xc, d, n, k, kp, nt, CT2, cnp, na_free, width)
     elif KM_WAVE and k <= 32 and (dp <= 128 if kp <= 16 else dp <= 64):
         # wave-unit kernel (csrc/dense_kernels.hip kmeans_wave_kernel): zero-padded
         # centroids [kp][dp], +inf norms for the padding clusters
@@ -275,6 +283,22 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor, na_free: bool = False):
             return _kmeans_large(Xc, Cc)
         check(rc, "kmeans")
         check(lib.h2omx_slab_sum(P(slab), n_wg, width, P(out), st), "slab_sum")
+    o = out.cpu().numpy()
+    return assign, o[: k * d].reshape(k, d), o[k * d: k * d + k], o[k * d + k:]
+
+
+def _kmeans_mfma(Xc, d, n, k, kp, nt, CT2, cnp, na_free, width):
+    """kmeans_mfma_kernel + the fp64 slab sum; one device -> host copy"""
+    lib = dense_lib()
+    dev = Xc.device
+    st = stream(dev)
+    out = torch.empty((width,), dtype=torch.float64, device=dev)
+    assign = torch.empty((n,), dtype=torch.int32, device=dev)
+    n_wg = max(1, min(KM_MFMA_WGS, math.ceil(n / (64 * 4 * 4))))
+    slab = torch.empty((4 * n_wg * width,), dtype=torch.float32, device=dev)
+    check(lib.h2omx_kmeans_mfma(P(Xc), Xc.stride(0), n, d, P(CT2), P(cnp), k, kp, nt, 0 if na_free else 1, n_wg,
+                                P(assign), P(slab), st), "kmeans_mfma")
+    check(lib.h2omx_slab_sum(P(slab), 4 * n_wg, width, P(out), st), "slab_sum")
     o = out.cpu().numpy()
     return assign, o[: k * d].reshape(k, d), o[k * d: k * d + k], o[k * d + k:]
 

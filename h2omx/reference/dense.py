@@ -142,9 +142,11 @@ def _irls_pass_ref(X, y, wprior, offset, beta, family, link, cls, var_power, lin
 
 
 
-def kmeans_step(X: torch.Tensor, C: torch.Tensor, na_free: bool = False):
+def kmeans_step(X: torch.Tensor, C, na_free: bool = False):
     """One Lloyd pass in fp64 (same outputs as the HIP kernel; ``na_free`` is
-    the device kernels' no-NA hint, unused here)."""
+    the device kernels' no-NA hint, unused here; C a tensor or host array)."""
+    if isinstance(C, np.ndarray):
+        C = torch.from_numpy(np.ascontiguousarray(C, np.float32))
     d, n = X.shape
     k = C.shape[0]
     Xn = X.double().numpy()

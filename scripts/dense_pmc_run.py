@@ -22,13 +22,14 @@ beta[0, :p] = np.random.default_rng(1).normal(scale=0.05, size=p)
 eta = torch.from_numpy(beta[0, :p].astype(np.float32)).to(dev) @ X
 y = (torch.rand(n, device=dev, generator=g) < torch.sigmoid(eta)).float()
 C = X[:, :k].T.contiguous()
+Cn = C.cpu().numpy()   # host centroids, as the K-Means model passes them
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 NA_FREE = len(sys.argv) > 2 and sys.argv[2] == "na_free"   # the K-Means model's imputed design
 out = {}
 WHICH = sys.argv[3] if len(sys.argv) > 3 else "both"
 for name, fn, flops in (("glm_irls", lambda: D.glm_irls_pass(X, y, None, None, beta, "binomial", "logit"),
                          n * (p + 2) * (p + 2)),
-                        ("kmeans", lambda: D.kmeans_step(X, C, na_free=NA_FREE), 2.0 * n * k * p)):
+                        ("kmeans", lambda: D.kmeans_step(X, Cn if NA_FREE else C, na_free=NA_FREE), 2.0 * n * k * p)):
     if WHICH not in ("both", name.split("_")[0]):
         continue
     fn()
