@@ -320,19 +320,26 @@ class Reconciler {
     st["serviceName"] = s.name + "-service";
     st["observedGeneration"] = cr.get_int("metadata.generation", 0);
     if (!msg.empty()) st["message"] = msg;
+    const Json* old = cr.find("status");
     if (!leader.empty()) {
       // GPU peer topology + collective transport as the formed cloud reports it
       // (/3/Cloud h2omx_topology): a pod-per-GPU deployment without peer
-      // visibility shows up here, not only in the leader's log
-      Json topo = leader_topology(leader, leader_ip);
-      if (!topo.is_null()) st["topology"] = topo;
+      // visibility shows up here, not only in the leader's log.  A cloud's
+      // topology is fixed once formed, so it is fetched only when the leader or
+      // the phase changed (or it is still missing), not on every reconcile.
+      const Json* ot = (old && old->is_object()) ? old->find("topology") : nullptr;
+      if (ot && !ot->is_null() && old->get_string("leaderPod") == leader && old->get_string("phase") == phase) {
+        st["topology"] = ot->deep_copy();
+      } else {
+        Json topo = leader_topology(leader, leader_ip);
+        if (!topo.is_null()) st["topology"] = topo;
+      }
     }
     if (ing.enabled) {
       st["ingressIP"] = ing.ip;
       st["ingressPath"] = ing.path;
       if (!ing.ip.empty()) st["connectURL"] = "http://" + ing.ip + ":80/" + s.name;
     }
-    const Json* old = cr.find("status");
     if (old && old->is_object()) {
       Json cmp = st.deep_copy();
       if (*old == cmp) return;
@@ -340,9 +347,9 @@ class Reconciler {
     Json patch = Json::object();
     Json pst = st.deep_copy();
     // a merge patch only removes keys that are explicitly null: clear a stale
-    // message / ingress address from an earlier pass
+    // message / ingress address / topology (leader gone) from an earlier pass
     if (old && old->is_object())
-      for (const char* k : {"message", "ingressIP", "ingressPath", "connectURL"})
+      for (const char* k : {"message", "ingressIP", "ingressPath", "connectURL", "topology"})
         if (old->has(k) && !st.has(k)) pst[k] = Json();
     patch["status"] = pst;
     try {

@@ -6,6 +6,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <map>
 
 #ifdef _WIN32
 #ifndef _WIN32_WINNT
@@ -113,13 +114,27 @@ int run_capture(const std::vector<std::string>& argv, const std::vector<std::pai
   }
   SetHandleInformation(or_, HANDLE_FLAG_INHERIT, 0);
   SetHandleInformation(er, HANDLE_FLAG_INHERIT, 0);
-  // environment block: ours plus the extras (later entries win)
-  std::string block;
+  // environment block: ours with the extras REPLACING inherited entries of the
+  // same name (Windows names are case-insensitive and a block with duplicates
+  // resolves to the first one), sorted case-insensitively as CreateProcess expects
+  struct CiLess {
+    bool operator()(const std::string& a, const std::string& b) const {
+      return _stricmp(a.c_str(), b.c_str()) < 0;
+    }
+  };
+  std::map<std::string, std::string, CiLess> vars;
   if (LPCH cur = GetEnvironmentStringsA()) {
-    for (LPCH p = cur; *p; p += std::strlen(p) + 1) block.append(p).push_back('\0');
+    for (LPCH p = cur; *p; p += std::strlen(p) + 1) {
+      const std::string e(p);
+      const size_t eq = e.find('=', 1);   // "=C:=C:\dir" drive entries start with '='
+      if (eq == std::string::npos) continue;
+      vars.emplace(e.substr(0, eq), e.substr(eq + 1));
+    }
     FreeEnvironmentStringsA(cur);
   }
-  for (auto& [k, v] : env) block.append(k + "=" + v).push_back('\0');
+  for (auto& [k, v] : env) vars[k] = v;
+  std::string block;
+  for (auto& [k, v] : vars) block.append(k + "=" + v).push_back('\0');
   block.push_back('\0');
   std::string cmd;
   for (auto& a : argv) cmd += (cmd.empty() ? "" : " ") + quote_arg(a);
@@ -132,15 +147,27 @@ int run_capture(const std::vector<std::string>& argv, const std::vector<std::pai
   PROCESS_INFORMATION pi{};
   std::vector<char> cmdline(cmd.begin(), cmd.end());
   cmdline.push_back('\0');
-  const BOOL ok = CreateProcessA(nullptr, cmdline.data(), nullptr, nullptr, TRUE, CREATE_NO_WINDOW, block.data(),
-                                 nullptr, &si, &pi);
+  // the child and every helper it spawns live in one job object that is killed
+  // as a whole on timeout (and when the handle closes): a helper that inherited
+  // the pipe's write end can then never keep the reads below waiting
+  HANDLE job = CreateJobObjectA(nullptr, nullptr);
+  if (job) {
+    JOBOBJECT_EXTENDED_LIMIT_INFORMATION li{};
+    li.BasicLimitInformation.LimitFlags = JOB_OBJECT_LIMIT_KILL_ON_JOB_CLOSE;
+    SetInformationJobObject(job, JobObjectExtendedLimitInformation, &li, sizeof li);
+  }
+  const BOOL ok = CreateProcessA(nullptr, cmdline.data(), nullptr, nullptr, TRUE, CREATE_NO_WINDOW | CREATE_SUSPENDED,
+                                 block.data(), nullptr, &si, &pi);
   CloseHandle(ow);
   CloseHandle(ew);
   if (!ok) {
+    if (job) CloseHandle(job);
     CloseHandle(or_);
     CloseHandle(er);
     return -1;
   }
+  if (job) AssignProcessToJobObject(job, pi.hProcess);
+  ResumeThread(pi.hThread);
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds((long long)(timeout_s * 1000));
   bool timed_out = false;
   char buf[4096];
@@ -161,23 +188,34 @@ int run_capture(const std::vector<std::string>& argv, const std::vector<std::pai
     if (WaitForSingleObject(pi.hProcess, 0) == WAIT_OBJECT_0 && !any) break;
     if (std::chrono::steady_clock::now() > deadline) {
       timed_out = true;
-      TerminateProcess(pi.hProcess, 1);
+      if (job) TerminateJobObject(job, 1);
+      else TerminateProcess(pi.hProcess, 1);
       break;
     }
     if (!any) Sleep(5);
   }
-  // drain what is left after exit
-  for (int i = 0; i < 2; ++i) {
-    DWORD n = 0;
-    while (ReadFile(hs[i], buf, sizeof buf, &n, nullptr) && n > 0) dst[i]->append(buf, n);
+  // drain what is already buffered, never blocking: only what PeekNamedPipe
+  // reports, for at most 200 ms (a surviving grandchild may hold the pipe open)
+  const auto drain_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
+  for (bool more = true; more && std::chrono::steady_clock::now() < drain_end;) {
+    more = false;
+    for (int i = 0; i < 2; ++i) {
+      DWORD avail = 0, n = 0;
+      if (PeekNamedPipe(hs[i], nullptr, 0, nullptr, &avail, nullptr) && avail > 0 &&
+          ReadFile(hs[i], buf, (DWORD)std::min<DWORD>(avail, sizeof buf), &n, nullptr) && n > 0) {
+        dst[i]->append(buf, n);
+        more = true;
+      }
+    }
   }
   DWORD code = 1;
-  WaitForSingleObject(pi.hProcess, INFINITE);
+  WaitForSingleObject(pi.hProcess, timed_out ? 5000 : INFINITE);
   GetExitCodeProcess(pi.hProcess, &code);
   CloseHandle(pi.hProcess);
   CloseHandle(pi.hThread);
   CloseHandle(or_);
   CloseHandle(er);
+  if (job) CloseHandle(job);   // KILL_ON_JOB_CLOSE: no helper outlives the call
   return timed_out ? -1 : (int)code;
 }
 #else

@@ -506,11 +506,13 @@ def _fit_lbfgs_impl(est, X, y, w, off, beta, family, link, var_power, link_power
         beta = res.beta.reshape(K, p1)
         iters += res.iters
         history.append({"iteration": iters, "lambda": lam, "deviance": res.dev, "objective": res.f,
-                        "function_evaluations": res.evals})
-        best = (lam, beta.copy(), res.dev)
-    lam, beta, dev = best
+                        "function_evaluations": res.evals, "converged": res.converged,
+                        "stop_reason": res.stop_reason})
+        best = (lam, beta.copy(), res.dev, res)
+    lam, beta, dev, last = best
     stats = {"lambda": lam, "iterations": iters, "null_deviance": null_dev, "residual_deviance": dev,
-             "lambda_max": lam_max, "nobs": N, "solver": "L_BFGS"}
+             "lambda_max": lam_max, "nobs": N, "solver": "L_BFGS", "converged": bool(last.converged),
+             "stop_reason": last.stop_reason}
     k_active = int((np.abs(beta[:, :p]) > 0).sum()) + (K if intercept else 0)
     if family in ("binomial", "poisson", "multinomial"):
         stats["aic"] = dev + 2 * k_active

@@ -46,8 +46,10 @@ def resolve_solver(solver, family: str, p: int, K: int) -> str:
 
 
 class LbfgsResult:
-    def __init__(self, beta, f, dev, iters, evals, converged):
+    def __init__(self, beta, f, dev, iters, evals, converged, stop_reason=""):
         self.beta, self.f, self.dev, self.iters, self.evals, self.converged = beta, f, dev, iters, evals, converged
+        # "gradient" / "objective" (converged), "line_search_failed", "max_iterations"
+        self.stop_reason = stop_reason
 
 
 def owlqn(fg, b0: np.ndarray, pen_mask: np.ndarray, l1: float, max_iter: int = 500, m: int = 10,
@@ -83,11 +85,13 @@ def owlqn(fg, b0: np.ndarray, pen_mask: np.ndarray, l1: float, max_iter: int = 5
     S, Y, RHO = [], [], []
     f = total(fs, b)
     converged = False
+    stop = "max_iterations"
     it = 0
+    retried = False     # steepest-descent retry after a failed line search
     for it in range(1, max_iter + 1):
         pg = pseudo(b, g)
         if np.abs(pg).max() <= grad_eps:
-            converged = True
+            converged, stop = True, "gradient"
             break
         # two-loop recursion on the pseudo-gradient
         q = pg.copy()
@@ -127,8 +131,17 @@ def owlqn(fg, b0: np.ndarray, pen_mask: np.ndarray, l1: float, max_iter: int = 5
                 break
             t *= 0.5
         if not accepted:
-            converged = True        # no further decrease at machine precision
+            # no Armijo step along the quasi-Newton direction: drop the curvature
+            # history and retry once from steepest descent; a second failure stops
+            # WITHOUT claiming convergence (fp32 gradients of the HIP pass can stall
+            # the search well before grad_eps / obj_eps are met)
+            if S and not retried:
+                S, Y, RHO = [], [], []
+                retried = True
+                continue
+            stop = "line_search_failed"
             break
+        retried = False
         s_, y_ = bn - b, gn - g
         sy = s_.dot(y_)
         if sy > 1e-12 * max(1.0, np.abs(s_).max() * np.abs(y_).max()):
@@ -142,6 +155,6 @@ def owlqn(fg, b0: np.ndarray, pen_mask: np.ndarray, l1: float, max_iter: int = 5
         rel = abs(f - fn) / max(abs(f), abs(fn), 1e-300)
         b, g, f, dev = bn, gn, fn, devn
         if rel <= obj_eps:
-            converged = True
+            converged, stop = True, "objective"
             break
-    return LbfgsResult(b, f, dev, it, evals, converged)
+    return LbfgsResult(b, f, dev, it, evals, converged, stop)

@@ -410,6 +410,16 @@ def test_crd_manifest_matches_operator():
     assert set(props["spec"]["properties"]["ingress"]["properties"]) == {"enabled", "apiVersion"}
     for k in ("ingressIP", "ingressPath", "connectURL", "message"):
         assert k in props["status"]["properties"]
+    # a structural schema prunes undeclared status fields on a real apiserver:
+    # every key the operator writes must be declared, the free-form topology
+    # object with preserve-unknown-fields
+    import re
+
+    src = open(os.path.join(ROOT, "control", "src", "operator_main.cpp")).read()
+    written = set(re.findall(r'st\["(\w+)"\]', src))
+    assert written and written <= set(props["status"]["properties"]), written - set(props["status"]["properties"])
+    topo = props["status"]["properties"]["topology"]
+    assert topo["type"] == "object" and topo["x-kubernetes-preserve-unknown-fields"] is True
 
 
 # ---- kubeconfig credential plugins (kube-rs Config::infer parity) ---------------

@@ -148,3 +148,25 @@ def test_lbfgs_gpu_matches_irlsm(cuda_dev):
     a = GLM(family="binomial", solver="IRLSM", alpha=0.5, lambda_=1e-3).train(y="y", training_frame=fr)
     b = GLM(family="binomial", solver="L_BFGS", alpha=0.5, lambda_=1e-3).train(y="y", training_frame=fr)
     np.testing.assert_allclose(list(b.coef().values()), list(a.coef().values()), atol=5e-4)
+
+
+def test_owlqn_line_search_failure_is_not_convergence():
+    """A direction that never satisfies Armijo (here: a gradient of the wrong
+    sign, as a badly rounded gradient pass could give) stops the solver with
+    converged=False and the stop reason recorded - not a claimed optimum."""
+    import numpy as np
+
+    from h2omx.models.glm_solvers import owlqn
+
+    def fg(b):
+        return float((b ** 2).sum()), -2.0 * b, float((b ** 2).sum())
+
+    res = owlqn(fg, np.array([1.0, -2.0]), np.array([False, False]), 0.0, max_iter=20)
+    assert not res.converged and res.stop_reason == "line_search_failed"
+
+    def fg_ok(b):
+        return float(((b - 3.0) ** 2).sum()), 2.0 * (b - 3.0), 0.0
+
+    ok = owlqn(fg_ok, np.zeros(3), np.zeros(3, bool), 0.0)
+    assert ok.converged and ok.stop_reason in ("gradient", "objective")
+    assert np.allclose(ok.beta, 3.0, atol=1e-5)
