@@ -77,6 +77,18 @@ def _trees(args, comm, torch, np, model):
     world, rank = comm.world_size, comm.rank
     rows = args.rows or (11_000_000 if model == "gbm-higgs" else 150_000_000 // 8)
     strong = args.scaling == "strong"
+    # --loopback-ranks N (1 GPU): this process stands in for N ranks of the
+    # strong-scaled job - `rows` is ONE rank's shard and the tree engine runs the
+    # N-rank launch sequence (P2P exchanges against its own buffers), so the
+    # timed step is the 8-GPU step minus only the xGMI link
+    tcomm = comm
+    if args.loopback_ranks > 1:
+        if world != 1 or dev.type != "cuda":
+            raise SystemExit("--loopback-ranks needs one rank on a GPU")
+        from h2omx.parallel.comm import LoopbackComm
+
+        tcomm = LoopbackComm(dev, args.loopback_ranks)
+        strong = False
     t_setup = time.perf_counter()
     gen = higgs_like if model == "gbm-higgs" else airlines_like
     if strong:
@@ -112,20 +124,20 @@ def _trees(args, comm, torch, np, model):
         edges, nvb, nbt = compute_edges(X, args.nbins, comm=comm)
     bm = bin_matrix(X, edges, nvb, nbt)
     y_np = y.cpu().numpy()
-    sums = comm.all_reduce_numpy(np.array([y_np.sum(), float(len(y_np))]))
+    sums = tcomm.all_reduce_numpy(np.array([y_np.sum(), float(len(y_np))]))
     p0 = min(max(sums[0] / sums[1], 1e-6), 1 - 1e-6)
     init = np.log(p0 / (1 - p0)) if model == "gbm-higgs" else 0.0   # XGBoost base_score 0.5
     ens = TreeEnsemble(trees=np.zeros((0, 1)), K=1, dist="bernoulli", init_f=np.array([init]), nbt=nbt,
                        feature_names=bm.names)
     gb = None
     if dev.type == "cuda":
-        gb = GpuBooster(bm, y_np, None, ens, tp, 1.0, args.seed, comm, {})
+        gb = GpuBooster(bm, y_np, None, ens, tp, 1.0, args.seed, tcomm, {})
         _sync(torch, dev)
         comm.barrier()
         setup_s = time.perf_counter() - t_setup
-        comm.collective_stats(reset=True)
+        tcomm.collective_stats(reset=True)
         elapsed = _timed(gb.step, args, comm, torch, dev, finish=gb.flush)
-        coll = comm.collective_stats()
+        coll = tcomm.collective_stats()
         gb.flush()   # fused mode: the last tree is applied inside the next step's level 0
         margin = gb.st.Fm[0, : bm.n]
         graph_used = gb.graph is not None
@@ -161,9 +173,9 @@ def _trees(args, comm, torch, np, model):
         auc = auc_from_scores(margin, y, comm=comm)
     per_tree = None
     if gb is not None and args.instrument_steps > 0:
-        per_tree = _instrument(gb, args, comm, torch, dev)
+        per_tree = _instrument(gb, args, tcomm, torch, dev)
     fit = None
-    fit_trees = args.fit_trees if args.fit_trees >= 0 else (50 if dev.type == "cuda" else 0)
+    fit_trees = args.fit_trees if args.fit_trees >= 0 else (50 if dev.type == "cuda" and tcomm is comm else 0)
     if fit_trees > 0:
         gb = None   # release the timed booster's buffers before the end-to-end fit
         fit = _fit_end_to_end(X, y, fit_trees, tp, args, comm, torch, dev, total_rows)
@@ -193,8 +205,15 @@ def _trees(args, comm, torch, np, model):
         # collectives the host issued per timed tree (RCCL / gloo calls between graph
         # segments); 0 when the step graph carries its own P2P collectives
         "collectives_host_issued_per_tree": coll["all_reduce_calls"] / max(args.steps, 1),
-        "collective_transport": _transport(comm),
+        "collective_transport": _transport(tcomm),
     }
+    if tcomm is not comm:
+        out["metric"] += f" [LOOPBACK PROXY: 1 GPU standing in for {tcomm.world_size} ranks of {rows} rows each]"
+        out["value"] = None
+        out["loopback"] = {"ranks": tcomm.world_size, "rows_per_rank": n_local,
+                           "note": "the N-rank launch sequence timed on one GPU (P2P exchanges read this GPU's own "
+                                   "buffers N times); trees are those of N identical shards"}
+        tcomm.shutdown()
     if per_tree is not None:
         out.update(per_tree)
     if fit is not None:
@@ -218,6 +237,8 @@ def _trees(args, comm, torch, np, model):
 def _transport(comm):
     if comm.world_size == 1:
         return "none (1 rank)"
+    if getattr(comm.p2p, "loopback", False):
+        return f"p2p loopback ({comm.world_size} stand-in ranks, one GPU)"
     if comm.p2p is not None:
         return "p2p (one-shot IPC all-reduce kernels in the step graph)"
     import torch.distributed as dist
@@ -462,6 +483,9 @@ def main(argv=None) -> int:
                          "-1 = 5 on GPU, 0 on CPU")
     ap.add_argument("--tree-graph", choices=["auto", "0", "1"], default="auto",
                     help="tree models: HIP-graph replay of each boosting step (H2OMX_TREE_GRAPH)")
+    ap.add_argument("--loopback-ranks", type=int, default=0,
+                    help="tree models, 1 GPU: run the N-rank step (fused P2P exchanges against this GPU's own "
+                         "buffers) on --rows rows = one rank's shard; a timing proxy of the N-GPU step")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto",
                     help="cpu: the torch reference paths (multi-rank rehearsal of this script over gloo)")

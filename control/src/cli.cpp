@@ -23,7 +23,7 @@ struct ArgSpec {
   bool required = false;
   bool flag = false;  // takes no value
   std::vector<std::string> aliases;
-  enum Validator { None, Path, IntGtZero, Percentage, Memory, UInt, DnsLabel, IngressApi } validator = None;
+  enum Validator { None, Path, IntGtZero, Percentage, Memory, UInt, DnsLabel, IngressApi, IngressClass } validator = None;
 };
 
 struct SubSpec {
@@ -72,6 +72,10 @@ std::vector<SubSpec> build_app() {
                          "Ingress API version used by later 'ingress' calls: networking.k8s.io/v1 or "
                          "networking.k8s.io/v1beta1.",
                          std::string("networking.k8s.io/v1"), false, false, {"ingress-api"}, ArgSpec::IngressApi});
+  deploy.args.push_back({"ingress_class", "ingress_class", "",
+                         "Ingress controller of later 'ingress' calls: nginx, traefik (Traefik v2, e.g. K3s: Prefix "
+                         "path + StripPrefix middleware) or empty for the cluster default class (nginx-style paths).",
+                         std::string(""), false, false, {"ingress-class"}, ArgSpec::IngressClass});
   deploy.args.push_back({"dry_run", "dry_run", "", "Print the Kubernetes manifests as YAML instead of deploying.",
                          std::nullopt, false, true, {"dry-run"}, ArgSpec::None});
   subs.push_back(deploy);
@@ -184,6 +188,9 @@ std::optional<std::string> validate(const ArgSpec& a, const std::string& v) {
     case ArgSpec::DnsLabel:
       if (!valid_dns_label(v))
         return "Error: '" + v + "' must be a lowercase DNS-1123 label (a-z, 0-9, '-'; at most 52 characters).";
+      return std::nullopt;
+    case ArgSpec::IngressClass:
+      if (!valid_ingress_class(v)) return "Error: unsupported ingress class '" + v + "' (nginx or traefik).";
       return std::nullopt;
     case ArgSpec::IngressApi:
       if (v != "networking.k8s.io/v1" && v != "networking.k8s.io/v1beta1")
@@ -352,6 +359,7 @@ ParseOutcome parse_command_line(const std::vector<std::string>& args, const std:
     d.image = vals["image"];
     d.image_tag = vals["image_tag"];
     d.ingress_api = vals["ingress_api"];
+    d.ingress_class = vals["ingress_class"];
     d.dry_run = vals.count("dry_run") > 0;
     if (d.dry_run) cmd.kind = CommandKind::Template;
     out.command = cmd;

@@ -29,6 +29,7 @@ struct UserDeploymentSpecification {
   std::string image_tag = "latest";
   uint32_t gpus_per_node = 1;
   std::string ingress_api = "networking.k8s.io/v1";
+  std::string ingress_class;
   bool dry_run = false;
 };
 

@@ -27,6 +27,7 @@ Json DeploymentSpecification::to_json() const {
   j["image_tag"] = image_tag;
   j["gpus_per_node"] = (int64_t)gpus_per_node;
   j["ingress_api"] = ingress_api;
+  if (!ingress_class.empty()) j["ingress_class"] = ingress_class;
   return j;
 }
 
@@ -45,6 +46,7 @@ DeploymentSpecification DeploymentSpecification::from_json(const Json& j) {
   s.gpus_per_node = (uint32_t)j.get_int("gpus_per_node", 1);
   // descriptors written by the reference tool used the v1beta1 Ingress API
   s.ingress_api = j.get_string("ingress_api", j.has("image") ? s.ingress_api : "networking.k8s.io/v1beta1");
+  s.ingress_class = j.get_string("ingress_class", "");
   return s;
 }
 
@@ -54,6 +56,7 @@ Json Deployment::to_json() const {
   j["ingresses"] = Json(JsonArray(ingresses.begin(), ingresses.end()));
   j["stateful_sets"] = Json(JsonArray(stateful_sets.begin(), stateful_sets.end()));
   j["services"] = Json(JsonArray(services.begin(), services.end()));
+  if (!middlewares.empty()) j["middlewares"] = Json(JsonArray(middlewares.begin(), middlewares.end()));
   return j;
 }
 
@@ -68,6 +71,7 @@ Deployment Deployment::from_json(const Json& j) {
   grab("ingresses", d.ingresses);
   grab("stateful_sets", d.stateful_sets);
   grab("services", d.services);
+  grab("middlewares", d.middlewares);
   return d;
 }
 
@@ -240,14 +244,29 @@ Json h2o_ingress(const DeploymentSpecification& s) {
   md["namespace"] = s.ns;
   md["labels"] = labels_for(s);
   Json ann = Json::object();
-  // strip the /<name> prefix before forwarding (Q12: capture groups exist)
-  ann["nginx.ingress.kubernetes.io/rewrite-target"] = "/$2";
-  ann["nginx.ingress.kubernetes.io/use-regex"] = "true";
-  ann["traefik.frontend.rule.type"] = "PathPrefixStrip";
+  const bool traefik = s.ingress_class == "traefik";
+  if (traefik) {
+    // Traefik v2 (K3s' bundled controller, the reference CI's cluster): a plain
+    // Prefix route plus the StripPrefix middleware (h2o_strip_prefix_middleware);
+    // v2 ignores v1's frontend annotations and takes a regex path literally
+    ann["traefik.ingress.kubernetes.io/router.middlewares"] = s.ns + "-" + s.name + "-stripprefix@kubernetescrd";
+  } else {
+    // strip the /<name> prefix before forwarding (Q12: capture groups exist)
+    ann["nginx.ingress.kubernetes.io/rewrite-target"] = "/$2";
+    ann["nginx.ingress.kubernetes.io/use-regex"] = "true";
+    ann["traefik.frontend.rule.type"] = "PathPrefixStrip";   // Traefik v1
+  }
   md["annotations"] = ann;
   ing["metadata"] = md;
   Json path = Json::object();
-  if (v1) {
+  if (v1 && traefik) {
+    path["path"] = "/" + s.name;
+    path["pathType"] = "Prefix";
+    Json svc = Json::object();
+    svc["name"] = s.name + "-service";
+    svc["port"] = kv("number", 80);
+    path["backend"] = kv("service", svc);
+  } else if (v1) {
     path["path"] = "/" + s.name + "(/|$)(.*)";
     path["pathType"] = "ImplementationSpecific";
     Json svc = Json::object();
@@ -267,9 +286,29 @@ Json h2o_ingress(const DeploymentSpecification& s) {
   Json rule = kv("http", kv("paths", paths));
   Json rules = Json::array();
   rules.push_back(rule);
-  ing["spec"] = kv("rules", rules);
+  Json spec = kv("rules", rules);
+  if (v1 && !s.ingress_class.empty()) spec["ingressClassName"] = s.ingress_class;
+  ing["spec"] = spec;
+  if (!v1 && !s.ingress_class.empty()) ing["metadata"]["annotations"]["kubernetes.io/ingress.class"] = s.ingress_class;
   return ing;
 }
+
+Json h2o_strip_prefix_middleware(const DeploymentSpecification& s, const std::string& api_version) {
+  Json mw = Json::object();
+  mw["apiVersion"] = api_version;
+  mw["kind"] = "Middleware";
+  Json md = Json::object();
+  md["name"] = s.name + "-stripprefix";
+  md["namespace"] = s.ns;
+  md["labels"] = labels_for(s);
+  mw["metadata"] = md;
+  Json prefixes = Json::array();
+  prefixes.push_back("/" + s.name);
+  mw["spec"] = kv("stripPrefix", kv("prefixes", prefixes));
+  return mw;
+}
+
+bool valid_ingress_class(const std::string& c) { return c.empty() || c == "nginx" || c == "traefik"; }
 
 Json owner_reference(const Json& owner) {
   Json o = Json::object();
@@ -336,6 +375,10 @@ std::vector<std::string> undeploy_h2o(KubeClient& client, const Deployment& d) {
     const bool beta = i.get_string("apiVersion") == "networking.k8s.io/v1beta1";
     del(beta ? kinds::IngressV1beta1 : kinds::IngressV1, i);
   }
+  for (auto& m : d.middlewares) {
+    const bool legacy = m.get_string("apiVersion") == "traefik.containo.us/v1alpha1";
+    del(legacy ? kinds::TraefikMiddlewareLegacy : kinds::TraefikMiddleware, m);
+  }
   for (auto& s : d.services) del(kinds::Service, s);
   for (auto& s : d.stateful_sets) del(kinds::StatefulSet, s);
   return failed;
@@ -364,10 +407,36 @@ std::optional<std::string> any_path(const Json& ingress) {
   return p;
 }
 
+Json create_strip_prefix_middleware(KubeClient& client, const DeploymentSpecification& spec) {
+  // traefik.io/v1alpha1 (Traefik >= 2.10); clusters with an earlier v2 only
+  // serve the traefik.containo.us group (404 / 405 on the new one)
+  try {
+    return client.create(kinds::TraefikMiddleware, spec.ns, h2o_strip_prefix_middleware(spec, "traefik.io/v1alpha1"));
+  } catch (const ApiError& e) {
+    if (e.status != 404 && e.status != 405) throw;
+  }
+  return client.create(kinds::TraefikMiddlewareLegacy, spec.ns,
+                       h2o_strip_prefix_middleware(spec, "traefik.containo.us/v1alpha1"));
+}
+
 void deploy_ingress(KubeClient& client, Deployment& d, int watch_timeout_s) {
   const auto& spec = d.specification;
   const ResourceKind& k = ingress_kind(spec);
-  Json created = client.create(k, spec.ns, h2o_ingress(spec));
+  if (spec.ingress_class == "traefik") d.middlewares.push_back(create_strip_prefix_middleware(client, spec));
+  Json created;
+  try {
+    created = client.create(k, spec.ns, h2o_ingress(spec));
+  } catch (...) {
+    // Q13: no half-made ingress - the middleware created above goes again
+    if (spec.ingress_class == "traefik") {
+      Deployment part;
+      part.specification = spec;
+      part.middlewares.push_back(d.middlewares.back());
+      d.middlewares.pop_back();
+      undeploy_h2o(client, part);
+    }
+    throw;
+  }
   std::string name = object_name(created);
   Json latest = created;
   if (!any_ip(latest) && watch_timeout_s > 0) {

@@ -38,6 +38,10 @@ struct DeploymentSpecification {
   std::string image_tag = "latest";
   uint32_t gpus_per_node = 1;
   std::string ingress_api = "networking.k8s.io/v1";
+  // ingress controller flavour: "" (nginx-style regex path, class left to the
+  // cluster default), "nginx" (same, ingressClassName nginx) or "traefik"
+  // (Traefik v2 - K3s' default: Prefix path + a StripPrefix Middleware CR)
+  std::string ingress_class;
 
   Json to_json() const;
   static DeploymentSpecification from_json(const Json& j);
@@ -48,6 +52,7 @@ struct Deployment {
   std::vector<Json> ingresses;
   std::vector<Json> stateful_sets;
   std::vector<Json> services;
+  std::vector<Json> middlewares;   // Traefik StripPrefix middlewares of the ingress (ingress_class traefik)
 
   Json to_json() const;
   static Deployment from_json(const Json& j);
@@ -57,6 +62,9 @@ struct Deployment {
 Json h2o_service(const DeploymentSpecification& s);
 Json h2o_stateful_set(const DeploymentSpecification& s);
 Json h2o_ingress(const DeploymentSpecification& s);
+// Traefik v2 StripPrefix middleware for /<name> (ingress_class "traefik")
+Json h2o_strip_prefix_middleware(const DeploymentSpecification& s, const std::string& api_version);
+bool valid_ingress_class(const std::string& c);
 // common labels / owner reference helpers used by the operator
 Json owner_reference(const Json& owner);
 
@@ -77,6 +85,8 @@ std::vector<std::string> undeploy_h2o(KubeClient& client, const Deployment& d);
 // Create the ingress, then watch it up to watch_timeout_s for a load-balancer
 // address; the last-seen object is appended to d.ingresses.
 void deploy_ingress(KubeClient& client, Deployment& d, int watch_timeout_s = 3);
+// Traefik StripPrefix middleware (traefik.io, falling back to traefik.containo.us)
+Json create_strip_prefix_middleware(KubeClient& client, const DeploymentSpecification& spec);
 
 std::optional<std::string> any_ip(const Json& ingress);
 std::optional<std::string> any_path(const Json& ingress);

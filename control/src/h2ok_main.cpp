@@ -38,6 +38,7 @@ DeploymentSpecification to_spec(const UserDeploymentSpecification& u, const std:
   s.image_tag = u.image_tag;
   s.gpus_per_node = u.gpus_per_node;
   s.ingress_api = u.ingress_api;
+  s.ingress_class = u.ingress_class;
   return s;
 }
 

@@ -19,6 +19,8 @@ const ResourceKind IngressV1{"/apis/networking.k8s.io/v1", "ingresses", "Ingress
 const ResourceKind IngressV1beta1{"/apis/networking.k8s.io/v1beta1", "ingresses", "Ingress", true};
 const ResourceKind Pod{"/api/v1", "pods", "Pod", true};
 const ResourceKind H2O{"/apis/h2o.ai/v1beta", "h2os", "H2O", true};
+const ResourceKind TraefikMiddleware{"/apis/traefik.io/v1alpha1", "middlewares", "Middleware", true};
+const ResourceKind TraefikMiddlewareLegacy{"/apis/traefik.containo.us/v1alpha1", "middlewares", "Middleware", true};
 const ResourceKind CRD{"/apis/apiextensions.k8s.io/v1", "customresourcedefinitions", "CustomResourceDefinition",
                        false};
 }  // namespace kinds

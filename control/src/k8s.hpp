@@ -86,6 +86,8 @@ extern const ResourceKind IngressV1;
 extern const ResourceKind IngressV1beta1;
 extern const ResourceKind Pod;
 extern const ResourceKind H2O;       // h2o.ai/v1beta  h2os
+extern const ResourceKind TraefikMiddleware;         // traefik.io/v1alpha1 middlewares (Traefik >= 2.10)
+extern const ResourceKind TraefikMiddlewareLegacy;   // traefik.containo.us/v1alpha1 (earlier Traefik v2)
 extern const ResourceKind CRD;
 }  // namespace kinds
 

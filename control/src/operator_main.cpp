@@ -256,6 +256,8 @@ class Reconciler {
     st.enabled = spec_ing && spec_ing->is_object() && spec_ing->find("enabled") &&
                  spec_ing->at("enabled").is_bool() && spec_ing->at("enabled").as_bool();
     s.ingress_api = cr.get_string("spec.ingress.apiVersion", "networking.k8s.io/v1");
+    s.ingress_class = cr.get_string("spec.ingress.className", "");
+    if (!valid_ingress_class(s.ingress_class)) s.ingress_class.clear();
     const ResourceKind& ik = s.ingress_api == "networking.k8s.io/v1beta1" ? kinds::IngressV1beta1 : kinds::IngressV1;
     const ResourceKind& other = &ik == &kinds::IngressV1 ? kinds::IngressV1beta1 : kinds::IngressV1;
     const std::string iname = s.name + "-ingress";
@@ -267,9 +269,39 @@ class Reconciler {
         if (e.status != 404 && e.status != 405) throw;
       }
     };
+    // Traefik v2 StripPrefix middleware (className traefik), owned like the ingress
+    const std::string mname = s.name + "-stripprefix";
+    auto drop_mw = [&]() {
+      for (const ResourceKind* mk : {&kinds::TraefikMiddleware, &kinds::TraefikMiddlewareLegacy}) {
+        try {
+          if (c_.get_opt(*mk, ns, mname)) {
+            c_.remove(*mk, ns, mname, "Background");
+            log(ns, name, "deleted middleware " + mname);
+          }
+        } catch (const ApiError& e) {
+          if (e.status != 404 && e.status != 405) throw;
+        }
+      }
+    };
     if (!st.enabled) {
       if (c_.get_opt(ik, ns, iname)) drop(ik);
+      drop_mw();
       return st;
+    }
+    if (s.ingress_class == "traefik") {
+      bool have = false;
+      for (const ResourceKind* mk : {&kinds::TraefikMiddleware, &kinds::TraefikMiddlewareLegacy}) {
+        try {
+          if (c_.get_opt(*mk, ns, mname)) have = true;
+        } catch (const ApiError&) {
+        }
+      }
+      if (!have) {
+        create_strip_prefix_middleware(c_, s);
+        log(ns, name, "created middleware " + mname);
+      }
+    } else {
+      drop_mw();
     }
     Json ing = h2o_ingress(s);
     adopt(ing, cr, hash);

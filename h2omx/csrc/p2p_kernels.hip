@@ -31,23 +31,15 @@
 //
 // All stores are vector-memory stores/atomics (global_*); flags live in
 // uncached device memory.
-#include "common.h"
+#include "p2p_device.h"
 
 namespace {
 
-constexpr int kMaxRanks = 8;
-constexpr int kMaxBlocks = 128;
+using p2pdev::kMaxBlocks;
+using p2pdev::kMaxRanks;
+using p2pdev::P2PDesc;
+constexpr int kArMaxBlocks = 128;   // blocks of one all-reduce launch (<= kMaxBlocks flag slots)
 constexpr int kThreads = 256;
-
-struct P2PDesc {
-  void* sym[kMaxRanks];        // symmetric data buffers (2 parities x cap bytes), peer-mapped
-  uint32_t* flags[kMaxRanks];  // flags[kMaxBlocks][kMaxRanks] per rank, peer-mapped
-  uint32_t* ctrl;              // local: [0] epoch, [1] finish ticket, [2] error, [3] timeouts
-  int64_t cap;                 // bytes per parity
-  int64_t timeout_ticks;       // wall_clock64 ticks (100 MHz) before a poll gives up
-  int32_t world;
-  int32_t rank;
-};
 
 enum Op : int { kSum = 0, kMax = 1 };
 
@@ -118,9 +110,7 @@ template <typename T, int OP>
 __global__ __launch_bounds__(kThreads) void p2p_allreduce_kernel(P2PDesc d, T* data, int64_t nelem, int nblocks) {
   __shared__ uint32_t s_epoch;
   const int b = blockIdx.x;
-  if (threadIdx.x == 0) s_epoch = d.ctrl[0] + 1u;
-  __syncthreads();
-  const uint32_t e = s_epoch;
+  const uint32_t e = p2pdev::begin_epoch(d, &s_epoch);
   const int64_t parity_off = (int64_t)(e & 1u) * d.cap;
   const int64_t nbytes = nelem * (int64_t)sizeof(T);
   const int64_t nvec = nbytes / 16;
@@ -136,38 +126,9 @@ __global__ __launch_bounds__(kThreads) void p2p_allreduce_kernel(P2PDesc d, T* d
     *reinterpret_cast<uint4*>(mine + v * 16) = *reinterpret_cast<const uint4*>(reinterpret_cast<char*>(data) + v * 16);
   if (tail)
     for (int64_t i = t0 + threadIdx.x; i < nelem; i += kThreads) reinterpret_cast<T*>(mine)[i] = data[i];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 
-  // 2. publish: system-scope release (write back this XCD's L2), then post the
-  //    epoch into every rank's flag slot [b][my rank]
-  if (threadIdx.x < kWave) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int lane = threadIdx.x;
-    if (lane < d.world)
-      __hip_atomic_store(d.flags[lane] + b * kMaxRanks + d.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // 3. wait for every rank's post of this epoch (lane r polls rank r's slot)
-    const uint32_t* my = d.flags[d.rank] + b * kMaxRanks;
-    const uint64_t t_start = wall_clock64();
-    bool timed_out = false;
-    while (true) {
-      uint32_t f = lane < d.world ? __hip_atomic_load(my + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : e;
-      if (__all((int32_t)(f - e) >= 0)) break;
-      if ((int64_t)(wall_clock64() - t_start) > d.timeout_ticks) {
-        timed_out = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (timed_out && lane == 0) {
-      __hip_atomic_store(d.ctrl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      atomicAdd(d.ctrl + 3, 1u);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
+  // 2. + 3. publish chunk b to every rank and wait for every rank's chunk b
+  p2pdev::post_wait(d, b, e);
 
   // 4. reduce chunk b over the ranks, in rank order
   char* out = reinterpret_cast<char*>(data);
@@ -183,14 +144,7 @@ __global__ __launch_bounds__(kThreads) void p2p_allreduce_kernel(P2PDesc d, T* d
   if (tail) reduce_tail<T, OP>(d, data, parity_off, t0, nelem);
 
   // 5. the last block to finish advances the epoch for the next launch
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t done = atomicAdd(d.ctrl + 1, 1u);
-    if (done == (uint32_t)nblocks - 1) {
-      d.ctrl[1] = 0u;
-      d.ctrl[0] = e;
-    }
-  }
+  p2pdev::finish(d, nblocks, e);
 }
 
 template <typename T, int OP>
@@ -198,7 +152,7 @@ int launch(const P2PDesc& d, void* data, int64_t nelem, hipStream_t st) {
   const int64_t nbytes = nelem * (int64_t)sizeof(T);
   if (nbytes > d.cap) return kBadArg;
   // ~16 KB per block (each block reads world x that over the links), <= kMaxBlocks
-  int nblocks = (int)std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, (nbytes + 16383) / 16384));
+  int nblocks = (int)std::min<int64_t>(kArMaxBlocks, std::max<int64_t>(1, (nbytes + 16383) / 16384));
   hipLaunchKernelGGL((p2p_allreduce_kernel<T, OP>), dim3(nblocks), dim3(kThreads), 0, st, d,
                      static_cast<T*>(data), nelem, nblocks);
   return launch_status();
@@ -236,15 +190,18 @@ H2OMX_API int h2omx_p2p_clock_khz() {
   return khz;
 }
 H2OMX_API int h2omx_p2p_max_ranks() { return kMaxRanks; }
-H2OMX_API int64_t h2omx_p2p_flags_bytes() { return (int64_t)kMaxBlocks * kMaxRanks * sizeof(uint32_t); }
+H2OMX_API int64_t h2omx_p2p_flags_bytes() { return (int64_t)p2pdev::kFlagWords * sizeof(uint32_t); }
 
-// Symmetric-buffer allocation: data (plain device memory) or flags (uncached,
-// zeroed).  Returns the device pointer through *out.
-H2OMX_API int h2omx_p2p_alloc(int64_t bytes, int uncached, void** out) {
-  if (out == nullptr || bytes <= 0) return kBadArg;
+// Symmetric-buffer allocation: kind 0 plain (coarse-grained) device memory,
+// 1 uncached (the flags), 2 fine-grained (the default data buffers: coherent
+// with peer reads at system scope, no reliance on remote-L2 write-back).
+// Zeroed; returns the device pointer through *out.
+H2OMX_API int h2omx_p2p_alloc(int64_t bytes, int kind, void** out) {
+  if (out == nullptr || bytes <= 0 || kind < 0 || kind > 2) return kBadArg;
   void* p = nullptr;
-  hipError_t rc = uncached ? hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached)
-                           : hipMalloc(&p, (size_t)bytes);
+  hipError_t rc = kind == 1   ? hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached)
+                  : kind == 2 ? hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocFinegrained)
+                              : hipMalloc(&p, (size_t)bytes);
   if (rc != hipSuccess) return kLaunchFailed;
   if (hipMemset(p, 0, (size_t)bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     (void)hipFree(p);
@@ -253,6 +210,25 @@ H2OMX_API int h2omx_p2p_alloc(int64_t bytes, int uncached, void** out) {
   *out = p;
   return kOk;
 }
+
+// Pinned, device-mapped host words (the error mirror the host polls without
+// a device synchronisation): *host is the CPU address, *dev the GPU one.
+H2OMX_API int h2omx_p2p_host_alloc(int64_t bytes, void** host, void** dev) {
+  if (host == nullptr || dev == nullptr || bytes <= 0) return kBadArg;
+  void* h = nullptr;
+  if (hipHostMalloc(&h, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return kLaunchFailed;
+  __builtin_memset(h, 0, (size_t)bytes);
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    (void)hipHostFree(h);
+    return kLaunchFailed;
+  }
+  *host = h;
+  *dev = d;
+  return kOk;
+}
+
+H2OMX_API int h2omx_p2p_host_free(void* h) { return hipHostFree(h) == hipSuccess ? kOk : kLaunchFailed; }
 
 H2OMX_API int h2omx_p2p_free(void* p) { return hipFree(p) == hipSuccess ? kOk : kLaunchFailed; }
 

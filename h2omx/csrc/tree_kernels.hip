@@ -29,6 +29,7 @@
 // algorithms (src/k8s/templates.rs:28-30 launches h2o.jar); this file is the
 // MI355X-native replacement of that compute path.
 #include "common.h"
+#include "p2p_device.h"
 #include <math.h>
 
 #include <algorithm>
@@ -1698,28 +1699,23 @@ __device__ __forceinline__ void store_feat_best(FeatBest* __restrict__ out, int6
   out[i] = r;
 }
 
-// K3 tail + K5 fused (single rank): one 1024-thread workgroup per (built slot,
-// feature) sums that histogram row's workgroup slabs (16-byte loads: LANES
-// slab lanes x NBT / 2 bin pairs, 8 loads of a lane in flight), keeps the
-// exact int64 row in LDS and scans the slot's two nodes right away (wave 0:
-// node 2s, wave 1: node 2s + 1 - the children of the s-th splitting node; the
-// unbuilt one is parent - built).  The built rows never round-trip through
-// global memory and the level drops the split_find launch (hist_reduce +
-// split_find were 4.7 + 7.5 us a level at 1.375M rows, mostly fixed cost).
-// Multi-rank levels keep hist_reduce -> all-reduce -> split_find.
-template <int NBT, bool CAT>
-__global__ __launch_bounds__(1024) void reduce_split_kernel(
-    const unsigned long long* __restrict__ partials, int wgpg, int fg, int slot_lo, int slot_cnt,
-    const long long* __restrict__ parent_full, long long* __restrict__ full, const int* __restrict__ ctl,
-    const NodeLink* __restrict__ link, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
-    const double* __restrict__ qscale, SplitParams p, FeatBest* __restrict__ out) {
+// K3 tail + K5 fused: one 1024-thread workgroup per (built slot, feature)
+// sums that histogram row's workgroup slabs (16-byte loads: LANES slab lanes
+// x NBT / 2 bin pairs, 8 loads of a lane in flight), keeps the exact int64
+// row in LDS and scans the slot's two nodes right away (wave 0: node 2s,
+// wave 1: node 2s + 1 - the children of the s-th splitting node; the unbuilt
+// one is parent - built).  The built rows never round-trip through global
+// memory and the level drops the split_find launch (hist_reduce + split_find
+// were 4.7 + 7.5 us a level at 1.375M rows, mostly fixed cost).
+// N ranks run the same single launch with the row exchange inside it
+// (reduce_split_p2p_kernel below).
+
+// slab partials of built slot s (pass-local), feature f -> row[2][NBT] (LDS)
+template <int NBT>
+__device__ __forceinline__ void rs_reduce_row(const unsigned long long* __restrict__ partials, int wgpg, int fg,
+                                              int slot_cnt, int s, int f, long long (*red)[NBT / 2][4],
+                                              long long (*row)[NBT]) {
   constexpr int PAIRS = NBT / 2, LANES = 1024 / PAIRS;
-  __shared__ long long red[LANES][PAIRS][4];   // 32 KB
-  __shared__ long long row[2][NBT];            // exact (G_q, S_q) of the built slot
-  const int s = blockIdx.x, f = blockIdx.y;
-  const int slot = slot_lo + s;
-  if (slot >= ctl[CTL_SLOTS]) return;   // whole workgroup
-  const int F = p.F;
   const int group = f / fg, fi = f % fg;
   const int64_t hist_elems = (int64_t)slot_cnt * fg * NBT;
   const unsigned long long* src = partials + (int64_t)group * wgpg * hist_elems + ((int64_t)s * fg + fi) * NBT;
@@ -1758,8 +1754,21 @@ __global__ __launch_bounds__(1024) void reduce_split_kernel(
     row[1][t] = ts;
   }
   __syncthreads();
+}
+
+// waves 0 / 1 of the block: split scan of the two children of `slot` for
+// feature f from the completed built row in LDS
+template <int NBT, bool CAT>
+__device__ __forceinline__ void rs_scan_slot(const long long (*row)[NBT], int slot, int f,
+                                             const long long* __restrict__ parent_full, long long* __restrict__ full,
+                                             const int* __restrict__ ctl, const NodeLink* __restrict__ link,
+                                             const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
+                                             const double* __restrict__ qscale, const SplitParams& p,
+                                             FeatBest* __restrict__ out) {
+  const int t = threadIdx.x;
   const int wid = t >> 6, lane = t & 63;
   if (wid >= 2) return;
+  const int F = p.F;
   const int n = ctl[CTL_N];
   const int node = 2 * slot + wid;   // level 0: slot 0 = the root, n = 1
   if (node >= n) return;
@@ -1794,6 +1803,78 @@ __global__ __launch_bounds__(1024) void reduce_split_kernel(
     w = feat_scan_wave<NBT, CAT>(gi, si, allowed, node, f, nvb, qscale[2], qscale[3], p);
   }
   if (lane == 0) store_feat_best(out, (int64_t)node * F + f, w);
+}
+
+template <int NBT, bool CAT>
+__global__ __launch_bounds__(1024) void reduce_split_kernel(
+    const unsigned long long* __restrict__ partials, int wgpg, int fg, int slot_lo, int slot_cnt,
+    const long long* __restrict__ parent_full, long long* __restrict__ full, const int* __restrict__ ctl,
+    const NodeLink* __restrict__ link, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
+    const double* __restrict__ qscale, SplitParams p, FeatBest* __restrict__ out) {
+  __shared__ long long red[1024 / (NBT / 2)][NBT / 2][4];   // 32 KB
+  __shared__ long long row[2][NBT];                         // exact (G_q, S_q) of the built slot
+  const int s = blockIdx.x, f = blockIdx.y;
+  const int slot = slot_lo + s;
+  if (slot >= ctl[CTL_SLOTS]) return;   // whole workgroup
+  rs_reduce_row<NBT>(partials, wgpg, fg, slot_cnt, s, f, red, row);
+  rs_scan_slot<NBT, CAT>(row, slot, f, parent_full, full, ctl, link, nvb, tree_fmask, qscale, p, out);
+}
+
+// N-rank level in ONE launch (one pass: slot_lo = 0, slot_cnt = the level's
+// built slots): persistent blocks walk the (slot, feature) items, reduce each
+// item's slabs into this rank's symmetric buffer, exchange their chunk of
+// items with every peer (p2p_device.h: one flag post / poll per block), sum
+// the N rows in rank order (exact int64) and run the split scan - so an
+// N-rank level is hist_build -> reduce_split_p2p -> level_finalize, the same
+// three launches as one rank, and the level's all-reduce is no separate
+// kernel.  Items map to blocks identically on every rank (same grid).
+template <int NBT, bool CAT>
+__global__ __launch_bounds__(1024) void reduce_split_p2p_kernel(
+    p2pdev::P2PDesc d, const unsigned long long* __restrict__ partials, int wgpg, int fg, int slot_cnt,
+    const long long* __restrict__ parent_full, long long* __restrict__ full, const int* __restrict__ ctl,
+    const NodeLink* __restrict__ link, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
+    const double* __restrict__ qscale, SplitParams p, FeatBest* __restrict__ out) {
+  __shared__ long long red[1024 / (NBT / 2)][NBT / 2][4];
+  __shared__ long long row[2][NBT];
+  __shared__ uint32_t s_epoch;
+  constexpr int64_t ROW = 2 * NBT;
+  const int F = p.F, t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+  const int items = slot_cnt * F;
+  const uint32_t e = p2pdev::begin_epoch(d, &s_epoch);
+  const int n_slots = ctl[CTL_SLOTS];
+  long long* mine = reinterpret_cast<long long*>(p2pdev::parity_base(d, d.rank, e));
+  for (int it = b; it < items; it += nb) {
+    const int s = it / F, f = it % F;
+    if (s >= n_slots) continue;   // block-uniform
+    rs_reduce_row<NBT>(partials, wgpg, fg, slot_cnt, s, f, red, row);
+    if (t < NBT) {
+      mine[it * ROW + t] = row[0][t];
+      mine[it * ROW + NBT + t] = row[1][t];
+    }
+    __syncthreads();
+  }
+  p2pdev::post_wait(d, b, e);
+  for (int it = b; it < items; it += nb) {
+    const int s = it / F, f = it % F;
+    if (s >= n_slots) continue;
+    if (t < 2 * NBT) {
+      // thread t owns (plane t / NBT, bin t % NBT): every rank's value loaded
+      // before the rank-order sum
+      const int64_t o = it * ROW + t;
+      long long v[p2pdev::kMaxRanks];
+#pragma unroll
+      for (int r = 0; r < p2pdev::kMaxRanks; ++r)
+        v[r] = r < d.world ? reinterpret_cast<const long long*>(p2pdev::parity_base(d, r, e))[o] : 0ll;
+      long long acc = v[0];
+#pragma unroll
+      for (int r = 1; r < p2pdev::kMaxRanks; ++r) acc += v[r];
+      row[t / NBT][t % NBT] = acc;
+    }
+    __syncthreads();
+    rs_scan_slot<NBT, CAT>(row, s, f, parent_full, full, ctl, link, nvb, tree_fmask, qscale, p, out);
+    __syncthreads();
+  }
+  p2pdev::finish(d, nb, e);
 }
 
 // K5: best threshold of every (node, feature).  One wave per (node, feature)
@@ -3106,6 +3187,44 @@ __global__ __launch_bounds__(1024) void leaf_finalize_begin_kernel(
   if (threadIdx.x == 0) tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0, row_base, 0, tree_ctr);
 }
 
+// N ranks: the exact leaf sums exchanged inside the leaf finalisation (one
+// workgroup; p2p_device.h) - each rank's [0, 3 * total) sums go into its
+// symmetric buffer, every rank's are summed in rank order (exact int64), then
+// leaf_finalize (+ with `begin`, the chained next tree's tree_begin exactly as
+// leaf_finalize_begin_kernel).  The tree's leaf all-reduce is no separate launch.
+__global__ __launch_bounds__(1024) void leaf_finalize_p2p_kernel(
+    p2pdev::P2PDesc d, unsigned long long* __restrict__ acc, const int* __restrict__ ctl_final,
+    double* __restrict__ qs, SplitParams p, TreeNode* __restrict__ tree, int cap, int begin,
+    const unsigned int* __restrict__ stat_max, int mode, double qg, double qsr, int* __restrict__ ctl0,
+    NodeLink* __restrict__ link0, long long row_base, int* __restrict__ tree_ctr) {
+  __shared__ uint32_t s_epoch;
+  const uint32_t e = p2pdev::begin_epoch(d, &s_epoch);
+  const int total = min(ctl_final[CTL_TOTAL], cap);
+  unsigned long long* mine = reinterpret_cast<unsigned long long*>(p2pdev::parity_base(d, d.rank, e));
+  for (int i = threadIdx.x; i < 3 * total; i += blockDim.x) mine[i] = acc[i];
+  p2pdev::post_wait(d, 0, e);
+  const double s4 = qs[4], s5 = qs[5], s6 = qs[6];
+  for (int gid = threadIdx.x; gid < total; gid += blockDim.x) {
+    long long a3[3] = {0, 0, 0};
+    for (int r = 0; r < d.world; ++r) {
+      const unsigned long long* src = reinterpret_cast<const unsigned long long*>(p2pdev::parity_base(d, r, e));
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a3[k] += (long long)src[3 * gid + k];
+    }
+    if (begin) { acc[3 * gid] = 0ull; acc[3 * gid + 1] = 0ull; acc[3 * gid + 2] = 0ull; }
+    TreeNode nd = tree[gid];
+    if (nd.feat < 0) {
+      const double G = (double)a3[0] / s4, H = (double)a3[1] / s5, W = (double)a3[2] / s6;
+      nd.value = (float)clamp_bound(leaf_value(G, H, W, p), p, gid, cap);
+      nd.weight = (float)W;
+      tree[gid] = nd;
+    }
+  }
+  p2pdev::finish(d, 1, e);   // (block barrier first: qs and ctl_final read above)
+  if (begin && threadIdx.x == 0)
+    tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0, row_base, 0, tree_ctr);
+}
+
 // Monotone constraints with H2O's squared-error splits (mode 0) and Newton
 // leaves (leaf_mode 0): the histograms carry (G, W), so the node intervals the
 // level finalisation cut at W-scale midpoints (-G/W) are on the wrong scale for
@@ -3578,6 +3697,42 @@ H2OMX_API int h2omx_reduce_split(const unsigned long long* partials, int wgpg, i
   return launch_status();
 }
 
+// N-rank fused level (reduce_split_p2p_kernel); desc = host P2PDesc image.
+// One pass only (slot_cnt = the level's slots): the host routes multi-pass
+// levels through hist_reduce + all-reduce + split_find.
+H2OMX_API int h2omx_reduce_split_p2p(const void* desc, const unsigned long long* partials, int wgpg, int fg,
+                                     int slot_cnt, const long long* parent_full, long long* full, const int* ctl,
+                                     const void* link, const int* nvb, const uint8_t* tree_fmask,
+                                     const double* qscale, const void* params, int nbt, void* out, int max_blocks,
+                                     hipStream_t stream) {
+  if (desc == nullptr) return kBadArg;
+  const p2pdev::P2PDesc d = *reinterpret_cast<const p2pdev::P2PDesc*>(desc);
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  if (slot_cnt < 1 || wgpg < 1 || fg < 1 || p.F < 1) return kBadArg;
+  if (d.world < 2 || d.world > p2pdev::kMaxRanks || d.rank < 0 || d.rank >= d.world) return kBadArg;
+  const int64_t items = (int64_t)slot_cnt * p.F;
+  if (items * 2 * nbt * 8 > d.cap) return kBadArg;
+  const int nb = (int)std::min<int64_t>(items, std::min(std::max(max_blocks, 1), p2pdev::kMaxBlocks));
+  const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
+  FeatBest* o = reinterpret_cast<FeatBest*>(out);
+#define H2OMX_RSP(NB)                                                                                             \
+  if (p.catf != nullptr)                                                                                          \
+    hipLaunchKernelGGL((reduce_split_p2p_kernel<NB, true>), dim3(nb), dim3(1024), 0, stream, d, partials, wgpg,   \
+                       fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o);                  \
+  else                                                                                                            \
+    hipLaunchKernelGGL((reduce_split_p2p_kernel<NB, false>), dim3(nb), dim3(1024), 0, stream, d, partials, wgpg,  \
+                       fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o)
+  switch (nbt) {
+    case 32: H2OMX_RSP(32); break;
+    case 64: H2OMX_RSP(64); break;
+    case 128: H2OMX_RSP(128); break;
+    case 256: H2OMX_RSP(256); break;
+    default: return kBadArg;
+  }
+#undef H2OMX_RSP
+  return launch_status();
+}
+
 H2OMX_API int h2omx_split_level(const long long* built, const long long* parent_full, long long* full, const int* ctl,
                                 const void* link, const int* nvb, const uint8_t* tree_fmask, const double* qscale,
                                 const void* params, int max_nodes, int nbt, void* nsplit, unsigned int* ticket,
@@ -3912,6 +4067,29 @@ H2OMX_API int h2omx_leaf_finalize_begin(unsigned long long* acc, const int* ctl_
   const double qsr = exp2(floor(log2(2147483648.0 / max_rows_per_wg)));
   hipLaunchKernelGGL(leaf_finalize_begin_kernel, dim3(1), dim3(1024), 0, stream, acc, ctl_final, qscale, p,
                      reinterpret_cast<TreeNode*>(tree), cap, stat_max, mode, qg, qsr, ctl0,
+                     reinterpret_cast<NodeLink*>(link0), row_base, tree_ctr);
+  return launch_status();
+}
+
+// N-rank leaf finalisation with the leaf-sum exchange inside (one launch);
+// begin = 1: also the chained next tree's tree_begin (as leaf_finalize_begin)
+H2OMX_API int h2omx_leaf_finalize_p2p(const void* desc, unsigned long long* acc, const int* ctl_final, double* qscale,
+                                      const void* params, void* tree, int cap, int begin,
+                                      const unsigned int* stat_max, int mode, int max_rows_per_wg, int* ctl0,
+                                      void* link0, long long row_base, int* tree_ctr, hipStream_t stream) {
+  if (desc == nullptr) return kBadArg;
+  const p2pdev::P2PDesc d = *reinterpret_cast<const p2pdev::P2PDesc*>(desc);
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  if (d.world < 2 || d.world > p2pdev::kMaxRanks || d.rank < 0 || d.rank >= d.world) return kBadArg;
+  if ((int64_t)cap * 3 * 8 > d.cap || p.gbound != nullptr) return kBadArg;
+  double qg = 0.0, qsr = 0.0;
+  if (begin) {
+    if (max_rows_per_wg < 1 || max_rows_per_wg > ROWS_CAP || tree_ctr == nullptr) return kBadArg;
+    qg = exp2(floor(log2(1073741824.0 / max_rows_per_wg)));
+    qsr = exp2(floor(log2(2147483648.0 / max_rows_per_wg)));
+  }
+  hipLaunchKernelGGL(leaf_finalize_p2p_kernel, dim3(1), dim3(1024), 0, stream, d, acc, ctl_final, qscale, p,
+                     reinterpret_cast<TreeNode*>(tree), cap, begin ? 1 : 0, stat_max, mode, qg, qsr, ctl0,
                      reinterpret_cast<NodeLink*>(link0), row_base, tree_ctr);
   return launch_status();
 }

@@ -378,10 +378,30 @@ class GpuBooster:
         elif self.K == 1:
             self._update(apply=False, next_tree=self.t, k=0)
 
+    def _health(self):
+        """Raise PeerLost when a peer is gone (watchdog) or a P2P exchange of an
+        earlier step timed out on the device (pinned host word: no sync).  In
+        graph mode no collective is host-issued, so this is the check that
+        stops a multi-rank fit from returning a model built on timed-out sums."""
+        c = self.builder.comm
+        if c is not None and c.world_size > 1 and hasattr(c, "check_health"):
+            c.check_health()
+
+    def _fault_stall(self):
+        """Test-only fault injection: H2OMX_FAULT_STALL="rank:tree:seconds"
+        makes that rank sleep before enqueueing that tree, past the peers' P2P timeout."""
+        spec = os.environ.get("H2OMX_FAULT_STALL")
+        c = self.builder.comm
+        if spec and c is not None:
+            r, t, sec = spec.split(":")
+            if int(r) == c.rank and int(t) == self.t:
+                time.sleep(float(sec))
+
     def flush(self):
         """Bring the margins up to date (fused mode applies each tree inside the
         next tree's first level; graph mode may hold steps back to replay them
         as one multi-tree graph)."""
+        self._health()
         if self.graph is not None and self.deferred:
             for t in self.deferred:
                 self.graph.replay(t)
@@ -442,6 +462,8 @@ class GpuBooster:
 
     def step(self):
         P, st, b, bm, t = ops.P, self.st, self.builder, self.bm, self.t
+        self._health()
+        self._fault_stall()
         if self.graph is None and self.use_graph and t >= self.t_start + 1:
             self._try_capture()
         if self.graph is not None:
@@ -563,6 +585,7 @@ class GpuBooster:
             self.graph.gb = None
             self.graph = None
         torch.cuda.synchronize(self.dev)
+        self._health()     # every exchange of the fit has completed: a timeout raises here
         if self.builder.timer.enabled:
             self.ens.timings.update({f"gpu_ms_{k}": v for k, v in self.builder.timer.totals().items()})
         if self.trees_dev:

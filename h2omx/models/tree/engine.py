@@ -370,6 +370,8 @@ class HipTreeBuilder:
     SPLIT_FIN = os.environ.get("H2OMX_SPLIT_FIN", "0") == "1"
     # single rank: slab reduction + split scan in one launch per pass (reduce_split)
     FUSE_RS = os.environ.get("H2OMX_FUSE_RS", "1") == "1"
+    # persistent workgroups of the N-rank fused level (<= 256 P2P flag slots)
+    P2P_BLOCKS = int(os.environ.get("H2OMX_P2P_BLOCKS", "256"))
     MAX_WG_THREADS_PER_CU = 2048      # 32 waves per CU
 
     def _fill_rounds(self, wgpg: int, n_groups: int, lds_bytes: int, threads: int, units: int) -> int:
@@ -524,6 +526,10 @@ class HipTreeBuilder:
         spp = self._params(tree_index)
         sp = self._sp
         comm = self.comm if (self.comm is not None and self.comm.world_size > 1) else None
+        # one-shot P2P transport: N-rank levels exchange their histogram rows inside
+        # reduce_split_p2p and the leaf sums inside leaf_finalize_p2p (one launch
+        # each, as on one rank); without it (RCCL / gloo) the level all-reduces `built`
+        p2p = getattr(comm, "p2p", None) if comm is not None else None
 
         if comm is not None and stat is None:   # fixed bounds are the same on every rank
             comm.all_reduce_(smax, "max")
@@ -570,15 +576,35 @@ class HipTreeBuilder:
             sp.depth = d
             sp.children_leaves = 1 if last else 0
             self._cat_level(max_nodes)
-            # single rank: each pass's slab reduction runs the split scan of its slots
-            # right away (reduce_split); multi-rank levels all-reduce `built` in between
-            rs = (comm is None and self.FUSE_RS and not self.fuse_split
+            routed = fuse and d > 0 and self._fused_level(d)
+            rm_level = d > 0 and self._rm_ok() and self.plan_rm(max_slots, routed)["passes"] <= self.RM_MAX_PASSES
+            # N ranks over P2P: the level's exchange runs inside the fused reduce +
+            # split scan when the level is one histogram pass on EVERY rank (the
+            # slot budget alone decides that - rank-independent - while feature
+            # groups / grids follow each rank's row count) and its rows fit the
+            # symmetric buffer
+            fuse_p2p = (p2p is not None and self.FUSE_RS and not self.fuse_split and not rm_level
+                        and max_slots * nbt * 8 <= self.LDS_BUDGET
+                        and max_slots * F * 2 * nbt * 8 <= p2p.cap)
+            # each pass's slab reduction runs the split scan of its slots right away
+            # (reduce_split; N ranks: reduce_split_p2p); otherwise the level's
+            # histograms are reduced, all-reduced and scanned in separate launches
+            rs = ((comm is None or fuse_p2p) and self.FUSE_RS and not self.fuse_split
                   and not (self.SPLIT_FIN and max_nodes <= 64 and self.catf is None))
             fbest = (self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
                      if not self.fuse_split else None)
 
             def reduce(n_groups, wgpg, fg, slot_lo, slot_cnt):
-                if rs:
+                if rs and fuse_p2p:
+                    if slot_lo != 0 or slot_cnt < max_slots:
+                        raise RuntimeError("reduce_split_p2p: multi-pass level")   # excluded by fuse_p2p
+                    ops.check(lib.h2omx_reduce_split_p2p(p2p.desc_ptr, P(partials), wgpg, fg, slot_cnt, P(full_prev),
+                                                         P(full_cur), P(ctl_cur), P(link[cur]), P(bm.nvb),
+                                                         P(tree_fmask), P(self.qscale), spp, nbt, P(fbest),
+                                                         self.P2P_BLOCKS, st), "reduce_split_p2p")
+                    comm.stats["p2p_calls"] += 1
+                    comm.stats["p2p_bytes"] += max_slots * self.per_node * 8
+                elif rs:
                     ops.check(lib.h2omx_reduce_split(P(partials), wgpg, fg, slot_lo, slot_cnt, P(full_prev),
                                                      P(full_cur), P(ctl_cur), P(link[cur]), P(bm.nvb),
                                                      P(tree_fmask), P(self.qscale), spp, nbt, P(fbest), st),
@@ -588,8 +614,7 @@ class HipTreeBuilder:
                                                     P(ctl_cur), P(built), st), "hist_reduce")
             hist_elems = plan["slot_cnt"] * plan["fg"] * nbt
             partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_elems, torch.int64)
-            routed = fuse and d > 0 and self._fused_level(d)
-            if d > 0 and self._rm_ok() and self.plan_rm(max_slots, routed)["passes"] <= self.RM_MAX_PASSES:
+            if rm_level:
                 # deeper levels: built rows only, whole rows gathered row-major
                 plan = self.plan_rm(max_slots, routed)
                 hist_elems = plan["slot_cnt"] * self.F * nbt
@@ -657,7 +682,7 @@ class HipTreeBuilder:
                             "hist_build")
                 with T("hist_reduce"):
                     reduce(plan["n_groups"], plan["wgpg"], plan["fg"], slot_lo, plan["slot_cnt"])
-            if comm is not None:
+            if comm is not None and not fuse_p2p:
                 with T("allreduce"):
                     comm.all_reduce_(built[: max_slots * self.per_node])
             next_nodes = 2 * max_nodes
@@ -735,12 +760,24 @@ class HipTreeBuilder:
             part_prev = part
             full_prev = full_cur
             max_nodes = next_nodes
-        # exact leaf values (sums accumulated by the partition kernels)
-        if comm is not None:
+        # exact leaf values (sums accumulated by the partition kernels); N ranks over
+        # P2P exchange the sums inside the leaf finalisation
+        leaf_p2p = p2p is not None and self.gbound is None and self.capacity * 3 * 8 <= p2p.cap
+        if comm is not None and not leaf_p2p:
             with T("allreduce"):
                 comm.all_reduce_(self.leaf_acc)
         with T("leaf"):
-            if chain:
+            if leaf_p2p:
+                ops.check(lib.h2omx_leaf_finalize_p2p(p2p.desc_ptr, P(self.leaf_acc), P(final_ctl), P(self.qscale),
+                                                      spp, P(self.tree_buf), self.capacity, 1 if chain else 0,
+                                                      P(smax if chain else None), p.mode,
+                                                      self.max_rows_per_wg if chain else 0,
+                                                      P(self.ctl[0] if chain else None),
+                                                      P(link[0] if chain else None), self.row_base,
+                                                      P(self.tree_ctr if chain else None), st), "leaf_finalize_p2p")
+                comm.stats["p2p_calls"] += 1
+                comm.stats["p2p_bytes"] += self.leaf_acc.numel() * 8
+            elif chain:
                 ops.check(lib.h2omx_leaf_finalize_begin(P(self.leaf_acc), P(final_ctl), P(self.qscale), spp,
                                                         P(self.tree_buf), self.capacity, P(smax), p.mode,
                                                         self.max_rows_per_wg, P(self.ctl[0]), P(link[0]),

@@ -26,6 +26,8 @@ TREE_SIGS = {
     "h2omx_hist_build_grad": "PLPPPIIIIIIIIIPPPPPPIPPIIIPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
     "h2omx_reduce_split": "PIIIIPPPPPPPPIPS",
+    "h2omx_reduce_split_p2p": "PPIIIPPPPPPPPIPIS",
+    "h2omx_leaf_finalize_p2p": "PPPPPPIIPIIPPLPS",
     "h2omx_level_finalize": "PPPPPPIIPPPIPIPS",
     "h2omx_split_level": "PPPPPPPPPIIPPPPIPPPIS",
     "h2omx_split_find_fin": "PPPPPPPPPIIPPPPIPPPIPS",
@@ -129,6 +131,8 @@ P2P_SIGS = {
     "h2omx_p2p_flags_bytes": "",
     "h2omx_p2p_alloc": "LIP",
     "h2omx_p2p_free": "P",
+    "h2omx_p2p_host_alloc": "LPP",
+    "h2omx_p2p_host_free": "P",
     "h2omx_p2p_handle_bytes": "",
     "h2omx_p2p_get_handle": "PP",
     "h2omx_p2p_open_handle": "PP",

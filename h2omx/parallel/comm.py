@@ -42,14 +42,29 @@ class Comm:
         # one-shot P2P all-reduce over IPC-mapped HBM for small messages
         # (parallel/p2p.py): graph-capturable, so tree steps replay as one graph
         self.p2p = None
+        self._p2p_dead = None     # a P2P instance disabled after a timeout (closed at shutdown)
         self.p2p_error: str | None = None
         self.stats.update({"p2p_calls": 0, "p2p_bytes": 0, "p2p_s": 0.0})
 
     def _check(self) -> None:
+        """Raise ``PeerLost`` once a peer is known lost: by the watchdog
+        (``failed``) or by a P2P exchange whose poll timed out on the device
+        (pinned host word, read without a device sync).  A timed-out exchange
+        also disables P2P on this Comm for good: the ranks' epochs no longer
+        line up, so every later result of it would be wrong."""
+        if self.failed is None and self.p2p is not None and self.p2p.failed():
+            self._p2p_dead = self.p2p
+            self.p2p = None
+            self.failed = (f"{self._p2p_dead.failure_reason()} (H2OMX_P2P_TIMEOUT_S; rank {self.rank} of "
+                           f"{self.world_size}); results computed since are invalid")
         if self.failed is not None:
             from ..runtime.watchdog import PeerLost
 
             raise PeerLost(self.failed)
+
+    def check_health(self) -> None:
+        """Public form of :meth:`_check` (tree steps, graph flushes, fit ends)."""
+        self._check()
 
     # ------------------------------------------------------------------
     @classmethod
@@ -247,13 +262,80 @@ class Comm:
         return float(t.item())
 
     def shutdown(self) -> None:
-        if self.p2p is not None:
-            self.p2p.check()
-            self.barrier()
-            self.p2p.close()
-            self.p2p = None
+        """Barrier, release the P2P buffers, tear the group down - and only then
+        report a P2P timeout nobody checked (raising first would leave the
+        other ranks waiting in the barrier)."""
+        err = None
+        p2p = self.p2p or self._p2p_dead
+        if p2p is not None:
+            lost = p2p.failed()
+            if not lost and self.failed is None:
+                self.barrier()
+            p2p.close()
+            self.p2p = self._p2p_dead = None
+            if lost and self.failed is None:
+                err = RuntimeError(f"P2P all-reduce: a poll timed out waiting for a peer (rank {self.rank} of "
+                                   f"{self.world_size}); results computed since then are invalid")
         if self.world_size > 1 and dist.is_initialized():
             dist.destroy_process_group()
+        if err is not None:
+            raise err
+
+
+class LoopbackComm(Comm):
+    """One process standing in for ``world`` identical ranks on one GPU (the
+    strong-scaling proxy, ``bench.py --loopback-ranks N``): the one-shot P2P
+    path runs with every "peer" buffer mapped to this process's own, so the
+    N-rank launch sequence - fused level exchanges, N-way sums, the same
+    grids - is what gets timed.  Host-side collectives behave as N copies of
+    this rank (sums x N, max / min / gathers of identical values).  Results
+    are those of N identical shards, not of one: this is a timing harness."""
+
+    def __init__(self, device: torch.device, world: int):
+        if world < 2:
+            raise ValueError("loopback needs a stand-in world of >= 2 ranks")
+        super().__init__(0, world, device)
+        from .p2p import P2PAllReduce
+
+        self.p2p = P2PAllReduce.loopback_for(self)
+
+    def barrier(self) -> None:
+        self._check()
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        self._check()
+        if self.p2p is not None and self.p2p.supports(t, op):
+            tok = self._begin("p2p", t.numel() * t.element_size())
+            self.p2p.all_reduce_(t, op)
+            self._end(tok)
+        elif op == "sum":
+            t.mul_(self.world_size)
+        return t
+
+    def all_reduce_async(self, t: torch.Tensor, op: str = "sum"):
+        self.all_reduce_(t, op)
+        return _Done()
+
+    def all_gather_cat(self, t: torch.Tensor, dim: int = 0) -> torch.Tensor:
+        return torch.cat([t] * self.world_size, dim=dim)
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        return t
+
+    def broadcast_object(self, obj, src: int = 0):
+        return obj
+
+    def all_gather_object(self, obj) -> list:
+        return [obj] * self.world_size
+
+    def max_scalar(self, v: float) -> float:
+        return v
+
+    def shutdown(self) -> None:
+        p2p = self.p2p or self._p2p_dead
+        if p2p is not None:
+            p2p.close()
+        self.p2p = self._p2p_dead = None
 
 
 class _Done:

@@ -407,7 +407,7 @@ def test_crd_manifest_matches_operator():
     v = crd["spec"]["versions"][0]
     assert v["name"] == "v1beta" and "status" in v["subresources"]
     props = v["schema"]["openAPIV3Schema"]["properties"]
-    assert set(props["spec"]["properties"]["ingress"]["properties"]) == {"enabled", "apiVersion"}
+    assert set(props["spec"]["properties"]["ingress"]["properties"]) == {"enabled", "apiVersion", "className"}
     for k in ("ingressIP", "ingressPath", "connectURL", "message"):
         assert k in props["status"]["properties"]
     # a structural schema prunes undeclared status fields on a real apiserver:
@@ -546,3 +546,64 @@ def test_ci_and_release_workflows():
     assert "scripts/e2e/iris_glm_rest.py" in steps and "kind load docker-image" in steps
     assert any("macos" in str(j.get("runs-on", "")) or "macos" in str(j.get("strategy", ""))
                for j in rel["jobs"].values())
+
+
+# ---- Traefik v2 ingress (K3s, the reference CI's cluster: rust.yml:18-20) -----------
+def test_traefik_v2_ingress(k8s, tmp_path):
+    """--ingress_class traefik: a Prefix route on /<name> plus a StripPrefix
+    Middleware CR referenced by the router annotation (Traefik v2 ignores v1's
+    PathPrefixStrip annotation and takes a regex path literally); undeploy
+    removes the middleware too."""
+    r = run(["deploy", "--cluster_size", "1", "--kubeconfig", k8s.cfg, "-c", "h2o-tr", "--ingress_class", "traefik"],
+            tmp_path)
+    assert r.returncode == 0, r.stderr
+    desc = str(tmp_path / "h2o-tr.h2ok")
+    r = run(["ingress", "-f", desc], tmp_path)
+    assert r.returncode == 0, r.stderr
+    mws = k8s.list("middlewares")
+    assert len(mws) == 1
+    mw = mws[0]
+    assert mw["apiVersion"] == "traefik.io/v1alpha1" and mw["metadata"]["name"] == "h2o-tr-stripprefix"
+    assert mw["spec"] == {"stripPrefix": {"prefixes": ["/h2o-tr"]}}
+    assert any(m == "POST" and p.startswith("/apis/traefik.io/v1alpha1/namespaces/default/middlewares")
+               for m, p in k8s.requests)
+    ing = k8s.list("ingresses")[0]
+    path = ing["spec"]["rules"][0]["http"]["paths"][0]
+    assert path["path"] == "/h2o-tr" and path["pathType"] == "Prefix"
+    assert ing["spec"]["ingressClassName"] == "traefik"
+    ann = ing["metadata"]["annotations"]
+    assert ann == {"traefik.ingress.kubernetes.io/router.middlewares": "default-h2o-tr-stripprefix@kubernetescrd"}
+    d = json.load(open(desc))
+    assert d["specification"]["ingress_class"] == "traefik" and len(d["middlewares"]) == 1
+    r = run(["undeploy", "-f", desc], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert k8s.list("middlewares") == [] and k8s.list("ingresses") == []
+    r = run(["deploy", "--cluster_size", "1", "--kubeconfig", k8s.cfg, "--ingress_class", "haproxy"], tmp_path)
+    assert r.returncode != 0 and "ingress class" in r.stderr
+
+
+def test_nginx_ingress_class_keeps_regex_route(k8s, tmp_path):
+    r = run(["deploy", "--cluster_size", "1", "--kubeconfig", k8s.cfg, "-c", "h2o-nx", "--ingress_class", "nginx"],
+            tmp_path)
+    assert r.returncode == 0, r.stderr
+    r = run(["ingress", "-f", str(tmp_path / "h2o-nx.h2ok")], tmp_path)
+    assert r.returncode == 0, r.stderr
+    ing = k8s.list("ingresses")[0]
+    assert ing["spec"]["ingressClassName"] == "nginx"
+    assert ing["spec"]["rules"][0]["http"]["paths"][0]["path"] == "/h2o-nx(/|$)(.*)"
+    assert k8s.list("middlewares") == []
+
+
+def test_operator_traefik_ingress_from_cr(k8s, tmp_path):
+    k8s.put("h2os", "default", _cr("h2o-otr", nodes=1, ingress={"enabled": True, "className": "traefik"}))
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    mw = k8s.get("middlewares", "default", "h2o-otr-stripprefix")
+    assert mw and mw["spec"]["stripPrefix"]["prefixes"] == ["/h2o-otr"]
+    ing = k8s.get("ingresses", "default", "h2o-otr-ingress")
+    assert ing["spec"]["rules"][0]["http"]["paths"][0]["pathType"] == "Prefix"
+    cr = k8s.get("h2os", "default", "h2o-otr")
+    cr["spec"]["ingress"]["enabled"] = False
+    k8s.put("h2os", "default", cr, "MODIFIED")
+    subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
+    assert k8s.get("middlewares", "default", "h2o-otr-stripprefix") is None
+    assert k8s.get("ingresses", "default", "h2o-otr-ingress") is None

@@ -111,6 +111,53 @@ def test_gbm_two_ranks_p2p_one_graph_reproduces_one_rank(tmp_path):
     assert o2["collective_transport"].startswith("p2p"), o2["collective_transport"]
     assert o1["graph_replay"] and o2["graph_replay"]
     assert o2["collectives_host_issued_per_tree"] == 0
-    assert o2["allreduce_calls_per_tree"] >= 5        # device-side: one per level (+ leaf sums)
+    # device-side exchanges, each inside a kernel the 1-rank step also runs:
+    # 5 fused level reduce + split scans and the leaf finalisation
+    assert o2["allreduce_calls_per_tree"] == 6
     _assert_same_trees(np.load(one), np.load(two), exact_values=True)
     assert o1["train_auc"] == o2["train_auc"]
+
+
+def _ranks(txt):
+    dec, outs, i = json.JSONDecoder(), [], 0
+    while True:
+        i = txt.find('{"rank"', i)
+        if i < 0:
+            return outs
+        obj, i = dec.raw_decode(txt, i)
+        outs.append(obj)
+
+
+@pytest.mark.gpu
+def test_p2p_timeout_fails_the_fit():
+    """Rank 1 stalls past the P2P timeout before tree 6: the survivor's exchanges
+    time out on the device, abort every rank's exchanges, and BOTH ranks' GBM
+    jobs end FAILED with PeerLost - no model is returned from timed-out sums."""
+    env = dict(os.environ, H2OMX_DIST_BACKEND="gloo", H2OMX_P2P="1", OMP_NUM_THREADS="2",
+               H2OMX_P2P_TIMEOUT_S="2", H2OMX_FAULT_STALL="1:6:5")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "_p2p_fault_worker.py")]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-4000:]
+    outs = _ranks(r.stdout)
+    assert len(outs) == 2, r.stdout + r.stderr[-2000:]
+    for o in outs:
+        assert o["p2p"], o
+        assert o["job_status"] == "FAILED", o
+        assert o["job_exception"].startswith("PeerLost"), o
+        assert not o["model_returned"], o
+
+
+@pytest.mark.gpu
+def test_loopback_proxy_runs_the_n_rank_sequence():
+    """bench.py --loopback-ranks 4: one GPU runs the 4-rank step (fused P2P level
+    exchanges and leaf exchange against its own buffers) as one graph replay."""
+    out = _bench(1, ["--rows", "200000", "--loopback-ranks", "4", "--instrument-steps", "2", "--fit-trees", "0"],
+                 {})
+    assert out["loopback"]["ranks"] == 4
+    assert out["collective_transport"].startswith("p2p loopback")
+    assert out["graph_replay"]
+    assert out["collectives_host_issued_per_tree"] == 0
+    assert out["allreduce_calls_per_tree"] == 6
+    assert out["ms_per_step"] > 0
