@@ -26,6 +26,7 @@ KERNEL_LIBS = {
     "metrics": ["metrics_kernels.hip"],
     "explain": ["explain_kernels.hip"],
     "p2p": ["p2p_kernels.hip"],
+    "mlp": ["mlp_kernels.hip"],
 }
 HOST_LIBS = {
     "host": ["host/parser.cpp", "host/solvers.cpp"],

@@ -217,7 +217,7 @@ class H2OAutoML:
             self.max_models = int(self.max_models) + start_models
         if task_mode:
             category = self._train_task_parallel(x, y, training_frame, validation_frame, comm, cv, rng, budget, t0,
-                                                 start_models)
+                                                 start_models, explo, explo_models)
             training_frame = self._local_frame
             comm_se = None
         else:
@@ -353,16 +353,22 @@ class H2OAutoML:
                 counters[f] += 1
         return category
 
-    def _exploit(self, fit, category, out_of_budget):
-        """Exploitation step ``GBM_lr_annealing_selection`` (H2O AutoML): the
-        best explored GBM retrained with its hyper-parameters and learning rate,
-        decaying by 0.99 per tree (``learn_rate_annealing``) over twice the
-        trees, early stopping as configured; ranked like any other model."""
+    def _exploit_plan(self, category) -> list:
+        """H2O AutoML's exploitation steps over the explored models, as a plan of
+        (name, estimator class, params):
+
+        * ``XGBoost_lr_search_selection``: the best XGBoost at half its learning
+          rate over twice the trees;
+        * ``GBM_lr_annealing_selection``: the best explored GBM retrained with its
+          hyper-parameters and learning rate, decaying by 0.99 per tree
+          (``learn_rate_annealing``) over twice the trees.
+
+        Early stopping as configured; ranked like any other model.  Both
+        schedulers run this plan (task-parallel: dealt over the ranks)."""
+        out = []
         best_of = {m.algo: m for m in self._best_of_family(list(self.models), category)}
         xgb = best_of.get("xgboost")
-        if xgb is not None and not out_of_budget():
-            # XGBoost_lr_search_selection: the best XGBoost at half its learning rate
-            # over twice the trees (early stopping as configured)
+        if xgb is not None:
             keep = ("max_depth", "min_rows", "min_child_weight", "sample_rate", "subsample", "col_sample_rate",
                     "colsample_bylevel", "col_sample_rate_per_tree", "colsample_bytree", "reg_lambda", "reg_alpha",
                     "gamma", "distribution")
@@ -371,25 +377,35 @@ class H2OAutoML:
             params.update(learn_rate=lr / 2, ntrees=int(xgb.params.get("ntrees", 50)) * 2, score_tree_interval=5)
             params.update({k: v for k, v in self.stopping.items() if v is not None})
             self._log("ModelTraining", f"exploitation: XGBoost_lr_search_selection from {xgb.model_id}")
-            fit("XGBoost_lr_search_selection", H2OXGBoostEstimator, params)
-        if "gbm" not in best_of or out_of_budget():
-            return
-        best = best_of["gbm"]
-        keep = ("max_depth", "min_rows", "sample_rate", "col_sample_rate", "col_sample_rate_per_tree",
-                "min_split_improvement", "distribution", "nbins")
-        params = {k: best.params[k] for k in keep if k in best.params}
-        lr = float(best.params.get("learn_rate", 0.1))
-        params.update(learn_rate=lr, learn_rate_annealing=0.99, ntrees=int(best.params.get("ntrees", 50)) * 2,
-                      score_tree_interval=5)
-        params.update({k: v for k, v in self.stopping.items() if v is not None})
-        self._log("ModelTraining", f"exploitation: GBM_lr_annealing_selection from {best.model_id}")
-        fit("GBM_lr_annealing_selection", H2OGradientBoostingEstimator, params)
+            out.append(("XGBoost_lr_search_selection", H2OXGBoostEstimator, params))
+        best = best_of.get("gbm")
+        if best is not None:
+            keep = ("max_depth", "min_rows", "sample_rate", "col_sample_rate", "col_sample_rate_per_tree",
+                    "min_split_improvement", "distribution", "nbins")
+            params = {k: best.params[k] for k in keep if k in best.params}
+            lr = float(best.params.get("learn_rate", 0.1))
+            params.update(learn_rate=lr, learn_rate_annealing=0.99, ntrees=int(best.params.get("ntrees", 50)) * 2,
+                          score_tree_interval=5)
+            params.update({k: v for k, v in self.stopping.items() if v is not None})
+            self._log("ModelTraining", f"exploitation: GBM_lr_annealing_selection from {best.model_id}")
+            out.append(("GBM_lr_annealing_selection", H2OGradientBoostingEstimator, params))
+        return out
 
-    def _train_task_parallel(self, x, y, training_frame, validation_frame, comm, cv, rng, budget, t0, start_models):
+    def _exploit(self, fit, category, out_of_budget):
+        """Sequential scheduler: the exploitation plan, one model at a time."""
+        for name, cls, params in self._exploit_plan(category):
+            if out_of_budget():
+                break
+            fit(name, cls, params)
+
+    def _train_task_parallel(self, x, y, training_frame, validation_frame, comm, cv, rng, budget, t0, start_models,
+                             explo=0.0, explo_models=0):
         """parallelism="task": replicate the frame, deal the plan round-robin to
-        the ranks, train locally (comm=None), exchange the trained models."""
-        from .frame.distributed import _gather_objects, gather_frame
-        from .mojo import GenericModel, mojo_bytes
+        the ranks, train locally (comm=None), exchange the trained models.  With
+        ``exploitation_ratio`` > 0 the exploration round keeps its share of the
+        time / model budget and a second round deals the exploitation plan
+        (built from the exchanged leaderboard, identical on every rank)."""
+        from .frame.distributed import gather_frame
 
         local = gather_frame(training_frame, comm)
         valid = gather_frame(validation_frame, comm) if validation_frame is not None else None
@@ -398,11 +414,32 @@ class H2OAutoML:
         # every rank fits the same encoder on the same replicated rows (comm=None)
         te = self._target_encoding(x, y, local, valid, seed, None)
         plan = self._plan_models(rng)
-        mine = []
+        if explo_models:
+            plan = plan[: max(0, len(plan) - explo_models)] if self.max_models else plan
         self._log("Workflow", f"task-parallel: {len(plan)} models over {comm.world_size} ranks "
                               f"({local.nrows} rows replicated per rank)")
-        for i in range(comm.rank, len(plan), comm.world_size):
-            if budget and time.time() - t0 > budget:
+        ctx = (x, y, local, valid, te, cv, budget, t0, comm)
+        category = self._deal(plan, 0, ctx, budget * (1.0 - explo) if (budget and explo) else budget)
+        if explo > 0 and category is not None:
+            ex = self._exploit_plan(category)
+            if ex:
+                self._log("Workflow", f"task-parallel exploitation: {len(ex)} models over {comm.world_size} ranks")
+                category = self._deal(ex, len(plan), ctx, budget) or category
+        return category
+
+    def _deal(self, plan, base, ctx, time_limit):
+        """One task-parallel round: plan entry i trains on rank (base + i) % world;
+        the trained models are exchanged (MOJO + metrics + CV holdout + params)
+        and appended to the leaderboard in plan order on every rank."""
+        from .frame.distributed import _gather_objects
+        from .mojo import GenericModel, mojo_bytes
+
+        x, y, local, valid, te, cv, budget, t0, comm = ctx
+        mine = []
+        for i in range(len(plan)):
+            if (base + i) % comm.world_size != comm.rank:
+                continue
+            if time_limit and time.time() - t0 > time_limit:
                 break
             name, cls, params = plan[i]
             mid = f"{name}_AutoML_{self.project_name}"
@@ -424,11 +461,12 @@ class H2OAutoML:
             blob = mojo_bytes(m)   # the bare model (its encoder is refitted identically on every rank)
             if use_te:
                 m.preprocessors = (te["model"],)
-            mine.append((i, {"model_id": m.model_id, "algo": m.algo, "mojo": blob,
-                             "training_metrics": m.training_metrics, "validation_metrics": m.validation_metrics,
-                             "cross_validation_metrics": m.cross_validation_metrics,
-                             "holdout": None if h is None else h.detach().cpu().numpy(),
-                             "run_time_ms": getattr(m, "run_time_ms", 0), "rank": comm.rank}, m))
+            mine.append((base + i, {"model_id": m.model_id, "algo": m.algo, "mojo": blob,
+                                    "params": dict(m.params),
+                                    "training_metrics": m.training_metrics, "validation_metrics": m.validation_metrics,
+                                    "cross_validation_metrics": m.cross_validation_metrics,
+                                    "holdout": None if h is None else h.detach().cpu().numpy(),
+                                    "run_time_ms": getattr(m, "run_time_ms", 0), "rank": comm.rank}, m))
         payloads = _gather_objects(comm, [(i, pl) for i, pl, _ in mine])
         native = {i: m for i, _, m in mine}
         category = None
@@ -438,6 +476,7 @@ class H2OAutoML:
                 # trained on another rank: scoring model from its MOJO + the training-side metrics
                 m = GenericModel(pl["mojo"], pl["model_id"])
                 m.algo = pl["algo"]
+                m.params = pl["params"]     # the exploitation plan reads the explored hyper-parameters
                 if te is not None and pl["algo"] in TE_ALGOS:
                     m.preprocessors = (te["model"],)
                 m.training_metrics = pl["training_metrics"]
@@ -445,8 +484,6 @@ class H2OAutoML:
                 m.cross_validation_metrics = pl["cross_validation_metrics"]
                 m.run_time_ms = pl["run_time_ms"]
                 if pl["holdout"] is not None:
-                    import torch
-
                     m.cross_validation_holdout = torch.from_numpy(pl["holdout"]).to(local.device)
                 DKV.put(m.model_id, m)
             category = m.category

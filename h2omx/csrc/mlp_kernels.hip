@@ -1,0 +1,398 @@
+// Small-batch MLP training step (H2O DeepLearning estimator defaults: 256-row
+// mini-batches) as a short chain of latency-optimised fp32 MFMA kernels.
+//
+// Measured on MI355X (bench_micro/grid_barrier.hip): a grid-wide barrier in
+// one persistent kernel costs ~14 us at 256 workgroups, a kernel boundary
+// inside a HIP graph ~2 us.  So the step is NOT one persistent kernel; it is
+// the minimum chain of dependent launches, each as short as its critical
+// path allows:
+//
+//   F_0 .. F_{L-2}  a_{l+1} = act(a_l W_l^T + b_l)                 (1 launch each)
+//   OUT             z = a_{L-1} W_{L-1}^T + b, softmax / squared loss,
+//                   g_{L-1} = dLoss/dz, g_{L-2} = (g_{L-1} W_{L-1}) * act'(a_{L-1})
+//   Q_j (j = L-2 .. 0), one launch each, independent jobs side by side:
+//                   dW_j = g_j^T a_j, db_j (+ dW_{L-1}, db_{L-1} in the first)
+//                   g_{j-1} = (g_j W_j) * act'(a_j)                 (j >= 1)
+//                   ADADELTA of layers whose gradient is complete and whose
+//                   weights no kernel reads any more (layer j + 2, and in
+//                   Q_0 layer 1; layer 0 is updated inside its own dW tiles)
+//
+// Every GEMM job is tiled so that ~one 16 RI x 16 RJ output tile lands on
+// each CU; the tile's 4 waves split K and meet in LDS (fixed wave order), so
+// a 256 x 512 x 512 product is ~0.9 us of v_mfma_f32_16x16x4f32 per wave
+// instead of a 512-long serial K chain.  Operands stream from global memory
+// straight into MFMA registers: K-contiguous operands as one float4 per lane
+// and k-group (lane group g holds k = 16 t + 4 g + j for MFMA j of group t -
+// any k permutation is a valid sum as long as A and B share it), MN-contiguous
+// operands as dword loads coalesced over 16 lanes.
+#include "common.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kT = 256;      // threads per workgroup (4 waves)
+constexpr int kMaxR = 2;     // tile side <= 2 x 16
+
+struct Opnd {
+  const float* p;
+  int ld;
+  int kc;    // 1: element (i, k) at p[i * ld + k]; 0: at p[k * ld + i]
+  int vec;   // kc operands with 16-byte aligned rows: float4 loads
+};
+
+struct GemmJob {
+  Opnd A, B;             // A: I x K, B: J x K
+  int I, J, K;
+  int RI, RJ;            // tile = 16 RI x 16 RJ
+  int tiles_j, tiles;
+  int epi;               // 0: act(acc + bias), 1: acc * act'(Y), 2: weight gradient
+  int act;               // 1 relu, 2 tanh
+  float* out;
+  int ldo, ldy;
+  const float* bias;
+  const float* Y;
+  // epi 2: bias gradient (tiles of j-tile 0) and in-tile ADADELTA
+  float* db;
+  float* W;
+  float* Eg2;
+  float* Edx2;
+  float* bW;
+  float* bEg2;
+  float* bEdx2;
+  int ada;
+  int rot;               // rotate the k-group order per tile (L2 channel spread)
+};
+
+struct AdaJob {
+  float* W;
+  const float* G;
+  float* Eg2;
+  float* Edx2;
+  long long n;
+};
+
+constexpr int kMaxJobs = 3, kMaxAda = 4;
+struct Phase {
+  GemmJob g[kMaxJobs];
+  AdaJob a[kMaxAda];
+  int ng, na;
+  float rho, eps, l2;
+  int pad;
+};
+
+__device__ __forceinline__ float act_grad_of(float y, int act) {
+  return act == 1 ? (y > 0.0f ? 1.0f : 0.0f) : (1.0f - y * y);
+}
+
+// H2O ADADELTA (reference/dense.py adadelta_): one parameter
+__device__ __forceinline__ void ada_update(float* W, const float gval, float* Eg2, float* Edx2, int64_t e, float rho,
+                                           float eps, float l2) {
+  const float w = W[e];
+  const float g = gval + l2 * w;
+  const float eg = rho * Eg2[e] + (1.0f - rho) * g * g;
+  const float ed = Edx2[e];
+  const float dx = -sqrtf(ed + eps) / sqrtf(eg + eps) * g;
+  Eg2[e] = eg;
+  Edx2[e] = rho * ed + (1.0f - rho) * dx * dx;
+  W[e] = w + dx;
+}
+
+// one 16-k group of a 16 R-row operand slice into registers (see header)
+__device__ __forceinline__ void load_group(const Opnd& o, int rows, int kend, int i0, int R, int k0, int c, int g,
+                                           float (&v)[kMaxR][4]) {
+#pragma unroll
+  for (int r = 0; r < kMaxR; ++r) {
+    const int i = i0 + 16 * r + c;
+    const bool rok = r < R && i < rows;
+    if (o.kc) {
+      const int k = k0 + 4 * g;
+      if (rok && o.vec && k + 3 < kend) {
+        const float4 q = *reinterpret_cast<const float4*>(o.p + (int64_t)i * o.ld + k);
+        v[r][0] = q.x; v[r][1] = q.y; v[r][2] = q.z; v[r][3] = q.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[r][j] = (rok && k + j < kend) ? o.p[(int64_t)i * o.ld + k + j] : 0.0f;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + 4 * g + j;
+        v[r][j] = (rok && k < kend) ? o.p[(int64_t)k * o.ld + i] : 0.0f;
+      }
+    }
+  }
+}
+
+// One output tile of job `jb`: 4 waves split K, partials meet in LDS.
+template <int kDepth>
+__device__ void tile_gemm(const GemmJob& jb, int tile, float (*red)[32 * 32], float (*dbr)[32], float rho, float eps,
+                          float l2) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int ti = tile / jb.tiles_j, tj = tile % jb.tiles_j;
+  const int i0 = ti * 16 * jb.RI, j0 = tj * 16 * jb.RJ;
+  const int kq = ((jb.K + 3) / 4 + 15) / 16 * 16;
+  const int kb = w * kq, ke = min(jb.K, kb + kq);
+  const bool dbon = jb.epi == 2 && jb.db != nullptr && tj == 0;
+  f32x4 acc[kMaxR][kMaxR];
+#pragma unroll
+  for (int a = 0; a < kMaxR; ++a)
+#pragma unroll
+    for (int b = 0; b < kMaxR; ++b) acc[a][b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  float dbacc[kMaxR] = {0.0f, 0.0f};
+  // Up to kDepth 16-k groups of loads in flight per wave: a wave's K range is
+  // at most a few hundred k, so its whole operand slice is requested before the
+  // first MFMA waits (one memory latency per tile instead of one per group -
+  // with a single group in flight the 256 x 512 x 512 layer took 13.5 us)
+  float va[kDepth][kMaxR][4], vb[kDepth][kMaxR][4];
+  const int ng = kb < ke ? (ke - kb + 15) / 16 : 0;
+  // k-group order rotated per (tile, wave): rows of 512 floats are 2 KB apart,
+  // so a 16-row fetch of one k-group sits on a single L2 channel; tiles walking
+  // K in lockstep would queue on the same few channels (Phase.rot = 0: off)
+  const int rot = (jb.rot && ng > 1) ? (int)(((unsigned)tile * 7u + (unsigned)w * 3u) % (unsigned)ng) : 0;
+  auto kgrp = [&](int q) { const int r = q + rot; return kb + 16 * (r >= ng ? r - ng : r); };
+#pragma unroll
+  for (int s = 0; s < kDepth; ++s)
+    if (s < ng) {
+      load_group(jb.A, jb.I, ke, i0, jb.RI, kgrp(s), c, g, va[s]);
+      load_group(jb.B, jb.J, ke, j0, jb.RJ, kgrp(s), c, g, vb[s]);
+    }
+  for (int base = 0; base < ng; base += kDepth) {
+#pragma unroll
+    for (int s = 0; s < kDepth; ++s) {
+      if (base + s >= ng) break;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int a = 0; a < kMaxR; ++a)
+#pragma unroll
+          for (int b = 0; b < kMaxR; ++b)
+            if (a < jb.RI && b < jb.RJ)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s][a][j], vb[s][b][j], acc[a][b], 0, 0, 0);
+      if (dbon) {
+#pragma unroll
+        for (int a = 0; a < kMaxR; ++a) dbacc[a] += (va[s][a][0] + va[s][a][1]) + (va[s][a][2] + va[s][a][3]);
+      }
+      // refill this slot with the group kDepth ahead
+      const int nxt = base + s + kDepth;
+      if (nxt < ng) {
+        load_group(jb.A, jb.I, ke, i0, jb.RI, kgrp(nxt), c, g, va[s]);
+        load_group(jb.B, jb.J, ke, j0, jb.RJ, kgrp(nxt), c, g, vb[s]);
+      }
+    }
+  }
+  // partial tiles -> LDS (16x16 layout: lane holds D[4 g + v][c])
+#pragma unroll
+  for (int a = 0; a < kMaxR; ++a)
+#pragma unroll
+    for (int b = 0; b < kMaxR; ++b)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) red[w][(16 * a + 4 * g + v) * 32 + 16 * b + c] = acc[a][b][v];
+  if (dbon) {
+#pragma unroll
+    for (int a = 0; a < kMaxR; ++a) {
+      float s = dbacc[a];
+      s += __shfl_xor(s, 16, kWave);
+      s += __shfl_xor(s, 32, kWave);
+      if (g == 0) dbr[w][16 * a + c] = s;
+    }
+  }
+  __syncthreads();
+  const int ri = 16 * jb.RI, rj = 16 * jb.RJ;
+  for (int e = t; e < 32 * 32; e += kT) {
+    const int row = e >> 5, col = e & 31;
+    const int i = i0 + row, j = j0 + col;
+    if (row >= ri || col >= rj || i >= jb.I || j >= jb.J) continue;
+    const float v = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    const int64_t o = (int64_t)i * jb.ldo + j;
+    if (jb.epi == 0) {
+      float r = v + (jb.bias ? jb.bias[j] : 0.0f);
+      r = jb.act == 1 ? fmaxf(r, 0.0f) : (jb.act == 2 ? tanhf(r) : r);
+      jb.out[o] = r;
+    } else if (jb.epi == 1) {
+      jb.out[o] = v * act_grad_of(jb.Y[(int64_t)i * jb.ldy + j], jb.act);
+    } else {
+      jb.out[o] = v;
+      if (jb.ada) ada_update(jb.W, v, jb.Eg2, jb.Edx2, o, rho, eps, l2);
+    }
+  }
+  if (dbon && t < ri && i0 + t < jb.I) {
+    const float s = ((dbr[0][t] + dbr[1][t]) + dbr[2][t]) + dbr[3][t];
+    jb.db[i0 + t] = s;
+    if (jb.ada) ada_update(jb.bW, s, jb.bEg2, jb.bEdx2, i0 + t, rho, eps, l2);
+  }
+  __syncthreads();   // LDS reuse by the caller's next tile
+}
+
+template <int kDepth>
+__global__ __launch_bounds__(kT, 2) void mlp_phase_kernel(Phase ph) {
+  __shared__ float red[4][32 * 32];
+  __shared__ float dbr[4][32];
+  // job selection with constant indices only: a runtime index into the kernel
+  // argument array would copy the whole Phase to scratch (752 B/lane measured)
+  int b = blockIdx.x;
+#pragma unroll
+  for (int q = 0; q < kMaxJobs; ++q) {
+    if (q < ph.ng) {
+      if (b >= 0 && b < ph.g[q].tiles) tile_gemm<kDepth>(ph.g[q], b, red, dbr, ph.rho, ph.eps, ph.l2);
+      b -= ph.g[q].tiles;
+    }
+  }
+  // this workgroup's even share of the ADADELTA updates listed for the phase
+#pragma unroll
+  for (int q = 0; q < kMaxAda; ++q) {
+    if (q >= ph.na) break;
+    const AdaJob& aj = ph.a[q];
+    const int64_t chunk = (aj.n + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min<int64_t>(aj.n, lo + chunk);
+    for (int64_t e = lo + threadIdx.x; e < hi; e += kT) ada_update(aj.W, aj.G[e], aj.Eg2, aj.Edx2, e, ph.rho, ph.eps, ph.l2);
+  }
+}
+
+// Output layer (C <= 8) + loss gradient + the last hidden layer's pre-activation
+// gradient, one wave per row: z = a W^T + b, g_out = (softmax(z) - onehot(y)) / M
+// (mode 0) or (z - y) / M (mode 1, C = 1), g_prev = (g_out W) * act'(a).
+struct OutDesc {
+  const float* A;     // a_{L-1} [M][Hd]
+  const float* W;     // [C][Hd]
+  const float* b;     // [C]
+  const int* y;       // class labels (mode 0)
+  const float* yr;    // targets (mode 1)
+  float* gout;        // [M][C]
+  float* gprev;       // [M][Hd]
+  int M, Hd, C, act, mode, vec;
+  int lda, ldp;       // row strides of A and gprev
+  float inv_m;
+  int pad;
+};
+
+__global__ __launch_bounds__(kT) void mlp_out_kernel(OutDesc d) {
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (m >= d.M) return;
+  const float* a = d.A + (int64_t)m * d.lda;
+  float z[8];
+#pragma unroll
+  for (int cc = 0; cc < 8; ++cc) z[cc] = 0.0f;
+  if (d.vec) {
+    for (int n = 4 * lane; n < d.Hd; n += 256) {
+      const float4 av = *reinterpret_cast<const float4*>(a + n);
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc)
+        if (cc < d.C) {
+          const float4 wv = *reinterpret_cast<const float4*>(d.W + (int64_t)cc * d.Hd + n);
+          z[cc] += (av.x * wv.x + av.y * wv.y) + (av.z * wv.z + av.w * wv.w);
+        }
+    }
+  } else {
+    for (int n = lane; n < d.Hd; n += 64) {
+      const float av = a[n];
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc)
+        if (cc < d.C) z[cc] += av * d.W[(int64_t)cc * d.Hd + n];
+    }
+  }
+#pragma unroll
+  for (int cc = 0; cc < 8; ++cc) {
+    float s = z[cc];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
+    z[cc] = s + (cc < d.C ? d.b[cc] : 0.0f);
+  }
+  float gz[8];
+  if (d.mode == 0) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc)
+      if (cc < d.C) mx = fmaxf(mx, z[cc]);
+    float den = 0.0f;
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc)
+      if (cc < d.C) den += __expf(z[cc] - mx);
+    const int yi = d.y[m];
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) gz[cc] = cc < d.C ? (__expf(z[cc] - mx) / den - (cc == yi ? 1.0f : 0.0f)) * d.inv_m : 0.0f;
+  } else {
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) gz[cc] = cc == 0 ? (z[0] - d.yr[m]) * d.inv_m : 0.0f;
+  }
+  if (lane < d.C) {
+    float v = gz[0];
+#pragma unroll
+    for (int cc = 1; cc < 8; ++cc)
+      if (cc == lane) v = gz[cc];
+    d.gout[(int64_t)m * d.C + lane] = v;
+  }
+  float* gp = d.gprev + (int64_t)m * d.ldp;
+  if (d.vec) {
+    for (int n = 4 * lane; n < d.Hd; n += 256) {
+      const float4 av = *reinterpret_cast<const float4*>(a + n);
+      float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc)
+        if (cc < d.C) {
+          const float4 wv = *reinterpret_cast<const float4*>(d.W + (int64_t)cc * d.Hd + n);
+          s.x += gz[cc] * wv.x; s.y += gz[cc] * wv.y; s.z += gz[cc] * wv.z; s.w += gz[cc] * wv.w;
+        }
+      s.x *= act_grad_of(av.x, d.act); s.y *= act_grad_of(av.y, d.act);
+      s.z *= act_grad_of(av.z, d.act); s.w *= act_grad_of(av.w, d.act);
+      *reinterpret_cast<float4*>(gp + n) = s;
+    }
+  } else {
+    for (int n = lane; n < d.Hd; n += 64) {
+      float s = 0.0f;
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc)
+        if (cc < d.C) s += gz[cc] * d.W[(int64_t)cc * d.Hd + n];
+      gp[n] = s * act_grad_of(a[n], d.act);
+    }
+  }
+}
+
+}  // namespace
+
+H2OMX_API int h2omx_mlp_sizes(int* out) {
+  if (out == nullptr) return kBadArg;
+  out[0] = (int)sizeof(Opnd);
+  out[1] = (int)sizeof(GemmJob);
+  out[2] = (int)sizeof(AdaJob);
+  out[3] = (int)sizeof(Phase);
+  out[4] = (int)sizeof(OutDesc);
+  out[5] = kMaxJobs;
+  out[6] = kMaxAda;
+  return kOk;
+}
+
+H2OMX_API int h2omx_mlp_phase(const void* phase, hipStream_t stream) {
+  if (phase == nullptr) return kBadArg;
+  const Phase ph = *static_cast<const Phase*>(phase);
+  if (ph.ng < 0 || ph.ng > kMaxJobs || ph.na < 0 || ph.na > kMaxAda) return kBadArg;
+  int blocks = 0;
+  for (int q = 0; q < ph.ng; ++q) {
+    const GemmJob& j = ph.g[q];
+    if (j.RI < 1 || j.RI > kMaxR || j.RJ < 1 || j.RJ > kMaxR || j.tiles_j < 1 || j.K < 1 || j.out == nullptr)
+      return kBadArg;
+    if (j.tiles != j.tiles_j * ((j.I + 16 * j.RI - 1) / (16 * j.RI)) || j.tiles_j != (j.J + 16 * j.RJ - 1) / (16 * j.RJ))
+      return kBadArg;
+    if ((j.epi == 1 && j.Y == nullptr) || (j.epi == 2 && j.ada && (j.W == nullptr || j.Eg2 == nullptr)))
+      return kBadArg;
+    blocks += j.tiles;
+  }
+  if (blocks == 0) blocks = 256;   // ADADELTA-only phase
+  // loads in flight per wave (16-k groups): Phase.pad, 0 = default
+  switch (ph.pad) {
+    case 1: hipLaunchKernelGGL(mlp_phase_kernel<1>, dim3(blocks), dim3(kT), 0, stream, ph); break;
+    case 2: hipLaunchKernelGGL(mlp_phase_kernel<2>, dim3(blocks), dim3(kT), 0, stream, ph); break;
+    case 4: hipLaunchKernelGGL(mlp_phase_kernel<4>, dim3(blocks), dim3(kT), 0, stream, ph); break;
+    case 6: hipLaunchKernelGGL(mlp_phase_kernel<6>, dim3(blocks), dim3(kT), 0, stream, ph); break;
+    default: hipLaunchKernelGGL(mlp_phase_kernel<4>, dim3(blocks), dim3(kT), 0, stream, ph); break;
+  }
+  return launch_status();
+}
+
+H2OMX_API int h2omx_mlp_out(const void* desc, hipStream_t stream) {
+  if (desc == nullptr) return kBadArg;
+  const OutDesc d = *static_cast<const OutDesc*>(desc);
+  if (d.C < 1 || d.C > 8 || d.M < 1 || d.Hd < 1 || (d.mode == 1 && d.C != 1)) return kBadArg;
+  hipLaunchKernelGGL(mlp_out_kernel, dim3((d.M + 3) / 4), dim3(kT), 0, stream, d);
+  return launch_status();
+}

@@ -34,6 +34,7 @@ import torch
 from ..frame.frame import ENUM, Frame, Vec
 from ..backend import dense as D
 from ..ops import dense as OD
+from ..ops import mlp as OM
 from .base import Model, ModelBuilder, ModelCategory
 from .glm import DesignInfo
 
@@ -321,6 +322,18 @@ class _DLTrainer:
         if (str(p_.get("precision", "fp32")).lower() == "bf16" and X.is_cuda and act in (1, 2) and drop_in == 0
                 and not any(hd[:n_hidden]) and M % 8 == 0):
             self.mlp = _Bf16Mlp(net, act, M, dev)
+        # fp32 small-batch updates (the estimator defaults' 256-row mini-batches) as
+        # one chain of latency-optimised launches: forward, loss gradient, backward
+        # and ADADELTA (ops/mlp.py).  H2OMX_DL_FUSED=0 keeps the per-op path.
+        self.fused = None
+        classes = net.layers[-1][1]
+        regression = not cls and not auto
+        if (self.mlp is None and not self.sync_grad and os.environ.get("H2OMX_DL_FUSED", "1") == "1"
+                and not auto and (cls or self.loss_kind in ("automatic", "quadratic"))
+                and OM.FusedMlpStep.supported(net, act, classes, regression, drop_in > 0 or any(hd[:n_hidden]),
+                                              self.adaptive, M)):
+            self.fused = OM.FusedMlpStep(net, act, M, self.Eg2, self.Edx2, float(p_["rho"]), float(p_["epsilon"]),
+                                         self.l2, regression=regression)
 
     def samples_per_iteration(self) -> int:
         """global samples between replica synchronisations (0: single GPU)"""
@@ -441,6 +454,13 @@ class _DLTrainer:
         if xb is None:
             xb = self.X.index_select(0, idx)
             yb = self.Y.index_select(0, idx) if not self.auto else None
+        if self.fused is not None:
+            self.fused.step(xb.contiguous(), yb)
+            if self.l1 > 0:
+                net.flat.sub_(self.l1 * torch.sign(net.flat))
+            if math.isfinite(float(p_["max_w2"])):
+                H2ODeepLearningEstimator._clip_w2(net, float(p_["max_w2"]))
+            return
         mlp = self.mlp
         if mlp is not None:
             xbb, xbt = mlp.load_batch(xb)
@@ -733,6 +753,7 @@ class H2ODeepLearningEstimator(ModelBuilder):
         score_every = max(1, steps_per_epoch)
         tr = _DLTrainer(p_, net, X, Y, act, cls, auto, drop_in, hd, M, steps_per_epoch, comm, gen, gen_dev,
                         len(hidden), backward=self._backward)
+        self._last_trainer = tr
         step = -1
         for step in range(total_steps):
             tr.step_deferred()

@@ -17,6 +17,7 @@ from h2omx.parallel.comm import Comm  # noqa: E402
 
 def main():
     out_path, parallelism = sys.argv[1], sys.argv[2]
+    explo = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0
     comm = Comm.from_env(device="cpu")
     c = comm if comm.world_size > 1 else None
     rng = np.random.default_rng(21)
@@ -28,7 +29,8 @@ def main():
     df["y"] = pd.Categorical(np.where(rng.random(n) < 1 / (1 + np.exp(-eta)), "1", "0"))
     lo, hi = n * comm.rank // comm.world_size, n * (comm.rank + 1) // comm.world_size
     fr = unify_domains(Frame.from_pandas(df.iloc[lo:hi].reset_index(drop=True)), c)
-    aml = H2OAutoML(max_models=3, nfolds=2, seed=5, project_name=f"p_{parallelism}", parallelism=parallelism)
+    aml = H2OAutoML(max_models=5 if explo else 3, nfolds=2, seed=5, project_name=f"p_{parallelism}",
+                    parallelism=parallelism, exploitation_ratio=explo)
     aml.train(y="y", training_frame=fr, comm=c)
     json.dump({"leaderboard": aml.leaderboard, "events": aml.events}, open(f"{out_path}.{comm.rank}", "w"))
     comm.shutdown()

@@ -17,14 +17,14 @@ ROOT = os.path.dirname(HERE)
 WORKER = os.path.join(HERE, "_automl_worker.py")
 
 
-def _run(world, mode, tmp):
-    out = str(tmp / f"lb_{mode}_{world}")
+def _run(world, mode, tmp, explo=0.0):
+    out = str(tmp / f"lb_{mode}_{world}_{explo}")
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
     if world == 1:
-        subprocess.run([sys.executable, WORKER, out, mode], env=env, check=True, timeout=600)
+        subprocess.run([sys.executable, WORKER, out, mode, str(explo)], env=env, check=True, timeout=600)
     else:
         r = subprocess.run([sys.executable, "-m", "h2omx.runtime.launch", "--nproc", str(world), "--", sys.executable,
-                            WORKER, out, mode], env=env, cwd=ROOT, timeout=600)
+                            WORKER, out, mode, str(explo)], env=env, cwd=ROOT, timeout=600)
         assert r.returncode == 0
     return [json.load(open(f"{out}.{r}")) for r in range(world)]
 
@@ -69,3 +69,20 @@ def test_data_parallel_matches_one_rank(runs):
     assert set(one) == set(dp)
     for k, r in one.items():
         assert abs(dp[k]["auc"] - r["auc"]) < 2e-3, k
+
+
+def test_task_parallel_exploitation_phase(tmp_path):
+    """exploitation_ratio > 0 under parallelism="task": the exploration round
+    keeps its share of max_models, then the exploitation plan (built from the
+    exchanged leaderboard) is dealt over the ranks - the same exploitation models
+    with the same metrics as the one-rank sequential run."""
+    one = _by_id(_run(1, "data", tmp_path, 0.4)[0]["leaderboard"])
+    a, b = _run(2, "task", tmp_path, 0.4)
+    assert [r["model_id"] for r in a["leaderboard"]] == [r["model_id"] for r in b["leaderboard"]]
+    task = _by_id(a["leaderboard"])
+    sel = [k for k in one if "_selection_AutoML" in k]
+    assert sel, sorted(one)
+    for name in sel:
+        assert name in task, (sorted(one), sorted(task))
+        assert abs(task[name]["auc"] - one[name]["auc"]) < 1e-9, name
+    assert set(one) == set(task)
