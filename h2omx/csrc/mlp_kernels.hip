@@ -60,7 +60,7 @@ struct GemmJob {
   float* bEg2;
   float* bEdx2;
   int ada;
-  int rot;               // rotate the k-group order per tile (L2 channel spread)
+  int pad;
 };
 
 struct AdaJob {
@@ -97,35 +97,54 @@ __device__ __forceinline__ void ada_update(float* W, const float gval, float* Eg
   W[e] = w + dx;
 }
 
-// one 16-k group of a 16 R-row operand slice into registers (see header)
+// Operand layouts (template codes): kLdV K-contiguous with 16-byte aligned
+// rows (one float4 per lane and group), kLdK K-contiguous otherwise (4 dwords),
+// kLdM MN-contiguous (4 dwords, each coalesced over 16 lanes).
+constexpr int kLdV = 0, kLdK = 1, kLdM = 2;
+
+__device__ __forceinline__ int op_layout(const Opnd& o) { return o.kc ? (o.vec ? kLdV : kLdK) : kLdM; }
+
+// 16 zero floats: the load address of masked-off lanes
+__device__ __attribute__((aligned(16))) float g_mlp_zeros[16];
+
+// One 16-k group of a 16 R-row operand slice into registers (see header).
+// Branch-free: a masked-off element (row >= rows, k >= kend) is loaded from
+// g_mlp_zeros instead of being zeroed after its load - every load is issued
+// unconditionally and its value used unconditionally, so the compiler can
+// neither sink it into a branch nor lose track of it in the vmcnt accounting
+// (masked selects after the loads compiled to a branch + vmcnt(0) per load:
+// ~0.4-0.75 us per 16-k group, measured).  kLdV operands need K % 4 == 0.
+template <int LY>
 __device__ __forceinline__ void load_group(const Opnd& o, int rows, int kend, int i0, int R, int k0, int c, int g,
                                            float (&v)[kMaxR][4]) {
 #pragma unroll
   for (int r = 0; r < kMaxR; ++r) {
     const int i = i0 + 16 * r + c;
     const bool rok = r < R && i < rows;
-    if (o.kc) {
+    if constexpr (LY == kLdV) {
       const int k = k0 + 4 * g;
-      if (rok && o.vec && k + 3 < kend) {
-        const float4 q = *reinterpret_cast<const float4*>(o.p + (int64_t)i * o.ld + k);
-        v[r][0] = q.x; v[r][1] = q.y; v[r][2] = q.z; v[r][3] = q.w;
-      } else {
+      const float* a = (rok && k < kend) ? o.p + (int64_t)i * o.ld + k : g_mlp_zeros;
+      const float4 q = *reinterpret_cast<const float4*>(a);
+      v[r][0] = q.x; v[r][1] = q.y; v[r][2] = q.z; v[r][3] = q.w;
+    } else if constexpr (LY == kLdK) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[r][j] = (rok && k + j < kend) ? o.p[(int64_t)i * o.ld + k + j] : 0.0f;
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + 4 * g + j;
+        v[r][j] = *((rok && k < kend) ? o.p + (int64_t)i * o.ld + k : g_mlp_zeros);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int k = k0 + 4 * g + j;
-        v[r][j] = (rok && k < kend) ? o.p[(int64_t)k * o.ld + i] : 0.0f;
+        v[r][j] = *((rok && k < kend) ? o.p + (int64_t)k * o.ld + i : g_mlp_zeros);
       }
     }
   }
 }
 
 // One output tile of job `jb`: 4 waves split K, partials meet in LDS.
-template <int kDepth>
-__device__ void tile_gemm(const GemmJob& jb, int tile, float (*red)[32 * 32], float (*dbr)[32], float rho, float eps,
+template <int kDepth, int LA, int LB>
+__device__ __attribute__((always_inline)) void tile_gemm(const GemmJob& jb, int tile, float (*red)[32 * 32], float (*dbr)[32], float rho, float eps,
                           float l2) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int c = lane & 15, g = lane >> 4;
@@ -146,39 +165,35 @@ __device__ void tile_gemm(const GemmJob& jb, int tile, float (*red)[32 * 32], fl
   // with a single group in flight the 256 x 512 x 512 layer took 13.5 us)
   float va[kDepth][kMaxR][4], vb[kDepth][kMaxR][4];
   const int ng = kb < ke ? (ke - kb + 15) / 16 : 0;
-  // k-group order rotated per (tile, wave): rows of 512 floats are 2 KB apart,
-  // so a 16-row fetch of one k-group sits on a single L2 channel; tiles walking
-  // K in lockstep would queue on the same few channels (Phase.rot = 0: off)
-  const int rot = (jb.rot && ng > 1) ? (int)(((unsigned)tile * 7u + (unsigned)w * 3u) % (unsigned)ng) : 0;
-  auto kgrp = [&](int q) { const int r = q + rot; return kb + 16 * (r >= ng ? r - ng : r); };
+  // Every slot load is unconditional (a group past the wave's range loads
+  // zeros: load_group masks k >= ke), so the number of loads in flight is the
+  // same on every path and vmcnt waits only for the slot being consumed.
 #pragma unroll
-  for (int s = 0; s < kDepth; ++s)
-    if (s < ng) {
-      load_group(jb.A, jb.I, ke, i0, jb.RI, kgrp(s), c, g, va[s]);
-      load_group(jb.B, jb.J, ke, j0, jb.RJ, kgrp(s), c, g, vb[s]);
-    }
+  for (int s = 0; s < kDepth; ++s) {
+    load_group<LA>(jb.A, jb.I, ke, i0, jb.RI, kb + 16 * s, c, g, va[s]);
+    load_group<LB>(jb.B, jb.J, ke, j0, jb.RJ, kb + 16 * s, c, g, vb[s]);
+  }
   for (int base = 0; base < ng; base += kDepth) {
 #pragma unroll
     for (int s = 0; s < kDepth; ++s) {
-      if (base + s >= ng) break;
+      // (tile-shape test once per accumulator and group, not per MFMA)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int a = 0; a < kMaxR; ++a)
 #pragma unroll
-        for (int a = 0; a < kMaxR; ++a)
+        for (int b = 0; b < kMaxR; ++b)
+          if (a < jb.RI && b < jb.RJ) {
 #pragma unroll
-          for (int b = 0; b < kMaxR; ++b)
-            if (a < jb.RI && b < jb.RJ)
+            for (int j = 0; j < 4; ++j)
               acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s][a][j], vb[s][b][j], acc[a][b], 0, 0, 0);
+          }
       if (dbon) {
 #pragma unroll
         for (int a = 0; a < kMaxR; ++a) dbacc[a] += (va[s][a][0] + va[s][a][1]) + (va[s][a][2] + va[s][a][3]);
       }
       // refill this slot with the group kDepth ahead
       const int nxt = base + s + kDepth;
-      if (nxt < ng) {
-        load_group(jb.A, jb.I, ke, i0, jb.RI, kgrp(nxt), c, g, va[s]);
-        load_group(jb.B, jb.J, ke, j0, jb.RJ, kgrp(nxt), c, g, vb[s]);
-      }
+      load_group<LA>(jb.A, jb.I, ke, i0, jb.RI, kb + 16 * nxt, c, g, va[s]);
+      load_group<LB>(jb.B, jb.J, ke, j0, jb.RJ, kb + 16 * nxt, c, g, vb[s]);
     }
   }
   // partial tiles -> LDS (16x16 layout: lane holds D[4 g + v][c])
@@ -228,14 +243,34 @@ template <int kDepth>
 __global__ __launch_bounds__(kT, 2) void mlp_phase_kernel(Phase ph) {
   __shared__ float red[4][32 * 32];
   __shared__ float dbr[4][32];
-  // job selection with constant indices only: a runtime index into the kernel
-  // argument array would copy the whole Phase to scratch (752 B/lane measured)
+  // job selection with constant indices only, copied into a local (uniform,
+  // SGPR-resident) descriptor: a runtime index into the kernel-argument array,
+  // or a reference into it passed to a call, copies the whole Phase to scratch
   int b = blockIdx.x;
+  GemmJob jb;
+  bool have = false;
 #pragma unroll
   for (int q = 0; q < kMaxJobs; ++q) {
-    if (q < ph.ng) {
-      if (b >= 0 && b < ph.g[q].tiles) tile_gemm<kDepth>(ph.g[q], b, red, dbr, ph.rho, ph.eps, ph.l2);
-      b -= ph.g[q].tiles;
+    if (!have && q < ph.ng) {
+      if (b < ph.g[q].tiles) {
+        jb = ph.g[q];
+        have = true;
+      } else {
+        b -= ph.g[q].tiles;
+      }
+    }
+  }
+  if (have) {
+    // operand layouts as template parameters: no branch inside the K loop
+    switch (op_layout(jb.A) * 3 + op_layout(jb.B)) {
+      case 0: tile_gemm<kDepth, kLdV, kLdV>(jb, b, red, dbr, ph.rho, ph.eps, ph.l2); break;
+      case 1: tile_gemm<kDepth, kLdV, kLdK>(jb, b, red, dbr, ph.rho, ph.eps, ph.l2); break;
+      case 2: tile_gemm<kDepth, kLdV, kLdM>(jb, b, red, dbr, ph.rho, ph.eps, ph.l2); break;
+      case 3: tile_gemm<kDepth, kLdK, kLdV>(jb, b, red, dbr, ph.rho, ph.eps, ph.l2); break;
+      case 4: tile_gemm<kDepth, kLdK, kLdK>(jb, b, red, dbr, ph.rho, ph.eps, ph.l2); break;
+      case 5: tile_gemm<kDepth, kLdK, kLdM>(jb, b, red, dbr, ph.rho, ph.eps, ph.l2); break;
+      case 8: tile_gemm<kDepth, kLdM, kLdM>(jb, b, red, dbr, ph.rho, ph.eps, ph.l2); break;
+      default: break;   // (A MN-contiguous with a K-contiguous B: no MLP job has it)
     }
   }
   // this workgroup's even share of the ADADELTA updates listed for the phase
@@ -383,7 +418,7 @@ H2OMX_API int h2omx_mlp_phase(const void* phase, hipStream_t stream) {
     case 1: hipLaunchKernelGGL(mlp_phase_kernel<1>, dim3(blocks), dim3(kT), 0, stream, ph); break;
     case 2: hipLaunchKernelGGL(mlp_phase_kernel<2>, dim3(blocks), dim3(kT), 0, stream, ph); break;
     case 4: hipLaunchKernelGGL(mlp_phase_kernel<4>, dim3(blocks), dim3(kT), 0, stream, ph); break;
-    case 6: hipLaunchKernelGGL(mlp_phase_kernel<6>, dim3(blocks), dim3(kT), 0, stream, ph); break;
+    case 8: hipLaunchKernelGGL(mlp_phase_kernel<8>, dim3(blocks), dim3(kT), 0, stream, ph); break;
     default: hipLaunchKernelGGL(mlp_phase_kernel<4>, dim3(blocks), dim3(kT), 0, stream, ph); break;
   }
   return launch_status();
@@ -394,5 +429,164 @@ H2OMX_API int h2omx_mlp_out(const void* desc, hipStream_t stream) {
   const OutDesc d = *static_cast<const OutDesc*>(desc);
   if (d.C < 1 || d.C > 8 || d.M < 1 || d.Hd < 1 || (d.mode == 1 && d.C != 1)) return kBadArg;
   hipLaunchKernelGGL(mlp_out_kernel, dim3((d.M + 3) / 4), dim3(kT), 0, stream, d);
+  return launch_status();
+}
+
+// ===========================================================================
+// Large-batch fp32 GEMM on the bf16 matrix cores: "x3" split.
+//
+// C[M][N] = act(A[M][K] . B[N][K]^T + bias), fp32 in, fp32 out (the forward
+// products of the 8192-row DL bench, where the fp32 MFMA rate - 157 TF/s -
+// bounds a 8192 x 512 x 512 layer at 27 us).  Every fp32 operand is split
+// EXACTLY into three bf16 pieces while it is staged to LDS:
+//     x = hi + mid + lo,  hi = bf16(x), mid = bf16(x - hi), lo = x - hi - mid
+// (round-to-nearest at each step leaves <= 8 significant bits per piece, so
+// the three pieces hold all 24 bits of x).  The product keeps the six terms
+// hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid - every one exact in fp32 -
+// and drops mid.lo, lo.mid, lo.lo (<= 2^-24 |a||b|, the size of one fp32
+// rounding), accumulating in fp32 on v_mfma_f32_32x32x16_bf16: fp32-equivalent
+// accuracy (pinned against float64 in tests/test_dl_step_gpu.py) at 6 bf16
+// MFMAs per 16-k step instead of 8 fp32 ones of 4 k each (2.7x the rate).
+// 128 x 128 block tile, 4 waves of 64 x 64 (2 x 2 accumulators of 32 x 32),
+// 32-k stages: coalesced float4 global loads -> split -> three bf16 planes in
+// LDS (rows padded to 40 elements: conflict-free ds_read_b128 fragments);
+// the next stage's loads are in flight under the current stage's MFMAs.
+// ===========================================================================
+namespace {
+
+typedef __bf16 x3_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float x3_f32x16 __attribute__((ext_vector_type(16)));
+constexpr int X3_BM = 128, X3_BN = 128, X3_BK = 32, X3_ROW = X3_BK + 8;   // bf16 elements per LDS row
+constexpr int X3_PLANE = 128 * X3_ROW;                                   // one plane of one operand
+
+__device__ __forceinline__ void x3_split(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;
+  m = (__bf16)r1;
+  l = (__bf16)(r1 - (float)m);
+}
+
+// float4 k-run of one row -> the three planes (4 bf16 = 8 bytes each)
+__device__ __forceinline__ void x3_store(__bf16* L, int row, int k, const float4 v) {
+  __bf16 h[4], m[4], l[4];
+  x3_split(v.x, h[0], m[0], l[0]);
+  x3_split(v.y, h[1], m[1], l[1]);
+  x3_split(v.z, h[2], m[2], l[2]);
+  x3_split(v.w, h[3], m[3], l[3]);
+  __bf16* p = L + row * X3_ROW + k;
+  *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(h);
+  *reinterpret_cast<uint2*>(p + X3_PLANE) = *reinterpret_cast<const uint2*>(m);
+  *reinterpret_cast<uint2*>(p + 2 * X3_PLANE) = *reinterpret_cast<const uint2*>(l);
+}
+
+struct X3Regs {
+  float4 a[4], b[4];
+};
+
+__device__ __forceinline__ void x3_load(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb,
+                                        int M, int N, int K, int m0, int n0, int k0, X3Regs& r) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int f = q * 256 + t, row = f >> 3, k = k0 + (f & 7) * 4;
+    const int i = m0 + row, j = n0 + row;
+    r.a[q] = (i < M && k < K) ? *reinterpret_cast<const float4*>(A + (int64_t)i * lda + k) : make_float4(0, 0, 0, 0);
+    r.b[q] = (j < N && k < K) ? *reinterpret_cast<const float4*>(B + (int64_t)j * ldb + k) : make_float4(0, 0, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict__ A, int lda,
+                                                        const float* __restrict__ B, int ldb, float* __restrict__ C,
+                                                        int ldc, const float* __restrict__ bias, int M, int N, int K,
+                                                        int act) {
+  __shared__ __attribute__((aligned(16))) __bf16 La[3 * X3_PLANE];
+  __shared__ __attribute__((aligned(16))) __bf16 Lb[3 * X3_PLANE];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  // XCD-aware order: linear block b runs on XCD b % 8; give each XCD a
+  // contiguous range of tiles (row-major over the tile grid: shared A rows
+  // stay in that XCD's L2)
+  const int gx = gridDim.x, nb = gx * gridDim.y;
+  int bid = blockIdx.y * gx + blockIdx.x;
+  if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
+  const int m0 = (bid / gx) * X3_BM, n0 = (bid % gx) * X3_BN;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  x3_f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+  const int nst = (K + X3_BK - 1) / X3_BK;
+  X3Regs r;
+  x3_load(A, lda, B, ldb, M, N, K, m0, n0, 0, r);
+  for (int st = 0; st < nst; ++st) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = q * 256 + t, row = f >> 3, k = (f & 7) * 4;
+      x3_store(La, row, k, r.a[q]);
+      x3_store(Lb, row, k, r.b[q]);
+    }
+    __syncthreads();
+    if (st + 1 < nst) x3_load(A, lda, B, ldb, M, N, K, m0, n0, (st + 1) * X3_BK, r);
+#pragma unroll
+    for (int kk = 0; kk < X3_BK; kk += 16) {
+      x3_bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          fa[a][p] = *reinterpret_cast<const x3_bf16x8*>(La + p * X3_PLANE + (wm + 32 * a + li) * X3_ROW + kk + 8 * lh);
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          fb[b][p] = *reinterpret_cast<const x3_bf16x8*>(Lb + p * X3_PLANE + (wn + 32 * b + li) * X3_ROW + kk + 8 * lh);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          // small terms first (fp32 accumulation order: lo-order products then hi.hi)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], fb[b][1], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][2], fb[b][0], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][2], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], fb[b][0], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][1], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][0], acc[a][b], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+  }
+  // epilogue: lane owns column j, registers e are rows (e & 3) + 8 (e >> 2) + 4 lh
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int j = n0 + wn + 32 * b + li;
+      if (j >= N) continue;
+      const float bj = bias ? bias[j] : 0.0f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int i = m0 + wm + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        if (i < M) {
+          float v = acc[a][b][e] + bj;
+          v = act == 1 ? fmaxf(v, 0.0f) : (act == 2 ? tanhf(v) : v);
+          C[(int64_t)i * ldc + j] = v;
+        }
+      }
+    }
+}
+
+}  // namespace
+
+// fp32 NT GEMM on the bf16 matrix cores (x3 split, see above); A, B rows
+// 16-byte aligned (lda, ldb % 4 == 0), K % 4 == 0
+H2OMX_API int h2omx_gemm_x3(const float* A, int lda, const float* B, int ldb, float* C, int ldc, const float* bias,
+                            int M, int N, int K, int act, hipStream_t stream) {
+  if (A == nullptr || B == nullptr || C == nullptr || M < 1 || N < 1 || K < 1) return kBadArg;
+  if ((lda & 3) || (ldb & 3) || (K & 3) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return kBadArg;
+  const dim3 grid((N + X3_BN - 1) / X3_BN, (M + X3_BM - 1) / X3_BM);
+  hipLaunchKernelGGL(gemm_x3_nt_kernel, grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, N, K, act);
   return launch_status();
 }

@@ -872,465 +872,6 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
   }
 }
 
-// Same histogram, for levels where only part of the rows belong to the
-// nodes being built (smaller children: <= 50 % of the rows, fewer per slot
-// pass).  hist_build_kernel issues one wave-level LDS atomic per (16-row
-// slot, feature) whenever ANY lane holds a live row, so a half-empty wave
-// costs as much LDS issue time as a full one (the kernel is LDS-issue bound:
-// SQ_WAIT_INST_LDS ~ SQ_BUSY_CYCLES, profiles/pmc1_summary.txt).  Here each
-// wave streams its rows 64 at a time, keeps the live ones in a register
-// queue (ballot + k-th-set-bit lane selection + ds_bpermute pulls) and
-// issues the fg feature atomics only for full batches of 64 live rows.
-// Quantisation and dither are identical to hist_build_kernel, so the
-// integer histograms are bit-identical.
-__device__ __forceinline__ int kth_set_bit(unsigned long long m, int k) {
-  int pos = 0;
-  int c = __popc((uint32_t)m);
-  if (k >= c) { k -= c; m >>= 32; pos += 32; }
-  c = __popc((uint32_t)m & 0xFFFFu);
-  if (k >= c) { k -= c; m >>= 16; pos += 16; }
-  c = __popc((uint32_t)m & 0xFFu);
-  if (k >= c) { k -= c; m >>= 8; pos += 8; }
-  c = __popc((uint32_t)m & 0xFu);
-  if (k >= c) { k -= c; m >>= 4; pos += 4; }
-  c = __popc((uint32_t)m & 0x3u);
-  if (k >= c) { k -= c; m >>= 2; pos += 2; }
-  c = (int)(m & 1ull);
-  if (k >= c) pos += 1;
-  return pos;
-}
-
-constexpr int HC_UNROLL = 4;   // 64-row steps whose loads are issued together
-constexpr int HC_FB = 16;      // features whose codes are gathered before their atomics
-
-template <int NBT>
-__global__ __launch_bounds__(1024) void hist_build_compact_kernel(
-    const uint8_t* __restrict__ codes, int64_t npad, const float* __restrict__ g, const float* __restrict__ s2,
-    const int* __restrict__ nid, const NodeLink* __restrict__ link, const int* __restrict__ ctl,
-    const int* __restrict__ nvb, const double* __restrict__ qscale, uint32_t salt, int F, int fg, int n_groups,
-    int wgpg, int slot_lo, int slot_cnt, int rows_per_unit, unsigned long long* __restrict__ partials) {
-  salt = (uint32_t)qscale[9];  // per-tree dither salt, written by tree_begin (graph-replay safe)
-  extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
-  __shared__ int width_s[256], rep_s[256];
-  const int n_slots = ctl[CTL_SLOTS];
-  if (slot_lo >= n_slots) return;
-  const int b = blockIdx.x;
-  const int xcd = b & 7, i = b >> 3;
-  const int group = i % n_groups;
-  const int chunk = xcd + 8 * (i / n_groups);
-  const int f0 = group * fg;
-  const int nf = min(fg, F - f0);
-  const int hist_elems = slot_cnt * fg * NBT;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-  for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) lds64[j] = 0ull;
-  if (threadIdx.x < fg) {
-    const int fi = threadIdx.x;
-    const int w = (fi < nf) ? nvb[f0 + fi] + 1 : NBT;
-    width_s[fi] = w;
-    int r = NBT / w;
-    rep_s[fi] = r < 1 ? 1 : (r > 64 ? 64 : r);
-  }
-  const float sg = (float)qscale[0], ss = (float)qscale[1];
-  const int64_t rb = (int64_t)qscale[7];  // global row offset of this rank (dither)
-  __syncthreads();
-  const int64_t units = npad / rows_per_unit;
-  const int64_t u0 = units * chunk / wgpg, u1 = units * (chunk + 1) / wgpg;
-  const int64_t row0 = u0 * rows_per_unit, row1 = u1 * rows_per_unit;
-  constexpr int STEP = 64 * HC_UNROLL;
-  const int64_t per = ((row1 - row0 + nwaves - 1) / nwaves + STEP - 1) / STEP * STEP;
-  const int64_t wr0 = row0 + wid * per, wr1 = min(row1, wr0 + per);
-  int p_row = 0, p_slot = 0;
-  unsigned long long p_pk = 0ull;
-  int pend = 0;
-  const uint8_t* cbase = codes + (int64_t)f0 * npad;
-  auto flush = [&](int nact) {
-    const bool on = lane < nact;
-    unsigned long long* hb = lds64 + p_slot * fg * NBT;
-    for (int fb = 0; fb < nf; fb += HC_FB) {
-      int bins[HC_FB];
-#pragma unroll
-      for (int q = 0; q < HC_FB; ++q)
-        bins[q] = (on && fb + q < nf) ? (int)cbase[(int64_t)(fb + q) * npad + p_row] : 0;
-#pragma unroll
-      for (int q = 0; q < HC_FB; ++q) {
-        const int fi = fb + q;
-        if (on && fi < nf) {
-          const int width = width_s[fi], rep = rep_s[fi];
-          const int bin = (bins[q] == NBT - 1) ? width - 1 : bins[q];
-          const int copy_off = (rep > 1) ? (lane % rep) * width : 0;
-          atomicAdd(hb + fi * NBT + copy_off + bin, p_pk);
-        }
-      }
-    }
-  };
-  for (int64_t base = wr0; base < wr1; base += STEP) {
-    int sl[HC_UNROLL];
-    unsigned long long pk[HC_UNROLL];
-    int nd[HC_UNROLL];
-#pragma unroll
-    for (int u = 0; u < HC_UNROLL; ++u) {
-      const int64_t r = base + 64 * u + lane;
-      nd[u] = (r < wr1) ? nid[r] : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < HC_UNROLL; ++u) {
-      int v = -1;
-      if (nd[u] >= 0) {
-        v = link[nd[u]].slot - slot_lo;
-        if (v >= slot_cnt) v = -1;
-      }
-      sl[u] = v;
-    }
-#pragma unroll
-    for (int u = 0; u < HC_UNROLL; ++u) {
-      const int64_t r = base + 64 * u + lane;
-      pk[u] = 0ull;
-      if (sl[u] >= 0) {
-        const uint32_t hsh = row_hash(rb + r, salt);
-        const float d1 = (hsh & 0xFFFF) * (1.0f / 65536.0f), d2 = (hsh >> 16) * (1.0f / 65536.0f);
-        const float sv = s2 ? s2[r] : 1.0f;
-        const int gq = (int)floorf(fmaf(g[r], sg, d1));
-        const uint32_t sq = (uint32_t)floorf(fmaf(sv, ss, d2));
-        pk[u] = ((unsigned long long)(uint32_t)gq << 32) | (unsigned long long)sq;
-        if (pk[u] == 0ull) sl[u] = -1;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < HC_UNROLL; ++u) {
-      const unsigned long long m = __ballot(sl[u] >= 0);
-      const int cnt = __popcll(m);
-      if (cnt == 0) continue;
-      const int my_row = (int)(base + 64 * u + lane);
-      const int total = pend + cnt;
-      {
-        const int k = lane - pend;
-        const bool take = lane >= pend && k < cnt;
-        const int src = take ? kth_set_bit(m, k) : lane;
-        const int nr = __shfl(my_row, src, 64);
-        const int ns = __shfl(sl[u], src, 64);
-        const unsigned long long npk = __shfl(pk[u], src, 64);
-        if (take) { p_row = nr; p_slot = ns; p_pk = npk; }
-      }
-      if (total >= 64) {
-        flush(64);
-        const int rem = total - 64;
-        const int k = (64 - pend) + lane;
-        const bool take = lane < rem;
-        const int src = take ? kth_set_bit(m, k) : lane;
-        const int nr = __shfl(my_row, src, 64);
-        const int ns = __shfl(sl[u], src, 64);
-        const unsigned long long npk = __shfl(pk[u], src, 64);
-        if (take) { p_row = nr; p_slot = ns; p_pk = npk; }
-        pend = rem;
-      } else {
-        pend = total;
-      }
-    }
-  }
-  if (pend > 0) flush(pend);
-  __syncthreads();
-  unsigned long long* out = partials + (int64_t)(group * wgpg + chunk) * hist_elems;
-  for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) {
-    const int bin = j % NBT;
-    const int fi = (j / NBT) % fg;
-    const int sl2 = j / (NBT * fg);
-    const int width = width_s[fi], rep = rep_s[fi];
-    const int src = (bin == NBT - 1) ? width - 1 : bin;
-    unsigned long long acc = 0ull;
-    if (src < width - 1 || bin == NBT - 1) {
-      const unsigned long long* hb = lds64 + (sl2 * fg + fi) * NBT;
-      for (int c = 0; c < rep; ++c) acc += hb[c * width + src];
-    }
-    out[j] = acc;
-  }
-}
-
-// Row-major compacted histogram build for levels >= 1 of the scan engine
-// (H2OMX_HIST_RM).  Levels >= 1 histogram only the smaller children (built
-// slots: ~30-50 % of the rows), but the column-major kernel issues one
-// ds_add_u64 wave-instruction per (16-row position, feature) whenever ANY
-// lane holds a built row, and a wave-instruction costs ~14-17 CU-cycles
-// whatever its lane mask (bench_micro/lds_mask.hip), so those levels cost
-// about as much LDS time as level 0.  Here every wave
-//   1. computes the build slot of its 1024 rows (64 lanes x 16 consecutive
-//      rows) exactly as hist_build_kernel does (slot16 from the previous
-//      partition, or the previous level's routing fused in: ROUTE),
-//   2. ranks the built rows with five bit-plane ballots and stages them as
-//      16-bit entries (row offset | slot << 10) in a per-wave 2 KB LDS area,
-//   3. hands lane j the entries j, j + 64, ... and gathers each entry's
-//      WHOLE row from the row-major code copy (codes_rm: [npad][32] bytes,
-//      two 16-byte loads, F <= 32) plus its stored packed (G_q, S_q),
-//   4. issues the F atomics of 64 built rows per wave-instruction.
-// So the atomic count follows the built rows, not the row positions, and no
-// per-feature code tile goes through LDS (the round-2 CMP variant staged one
-// per feature and lost on the extra LDS round trips).  The adds are the same
-// integers as hist_build_kernel's (same slots, same stored rows, same
-// low-cardinality replication), so histograms are bit-identical.  One
-// feature group only (fg = F <= 32); the next row's loads are issued before
-// the current row's atomics.
-constexpr int RM_PITCH = 32;     // bytes per row of codes_rm
-constexpr int RM_STAGE = 1024;   // u16 entries per wave
-
-// (routing keeps 48 more row registers live: 512-thread workgroups, 8 waves of up to 256 VGPRs)
-template <int NBT, int PKM, bool ROUTE>
-__global__ __launch_bounds__(ROUTE ? 512 : 1024) void hist_build_rm_kernel(
-    const uint8_t* __restrict__ codes, const uint8_t* __restrict__ codes_rm, int64_t npad,
-    const int* __restrict__ nid, const int* __restrict__ ctl, const int* __restrict__ nvb,
-    const double* __restrict__ qscale, int F, int wgpg, int slot_lo, int slot_cnt,
-    const short* __restrict__ slot16, const unsigned long long* __restrict__ pk_buf,
-    unsigned long long* __restrict__ partials, const PartInfo* __restrict__ part_prev,
-    const int* __restrict__ ctl_prev, int* __restrict__ nid_out, int writer) {
-  constexpr int ROWS = 16;
-  extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
-  __shared__ int width_s[32], rep_s[32];
-  __shared__ float rcp_s[32];
-  const int n_slots = ctl[CTL_SLOTS];
-  const int chunk = blockIdx.x;   // one feature group: the grid is the row chunks
-  const bool route_w = ROUTE && writer && ctl_prev[CTL_N] > 0;
-  const bool build = slot_lo < n_slots;
-  if (!build && !route_w) return;
-  const int fg = F;
-  const int hist_elems = slot_cnt * fg * NBT;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-  for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) lds64[j] = 0ull;
-  if (threadIdx.x < fg) {
-    const int w = nvb[threadIdx.x] + 1;
-    width_s[threadIdx.x] = w;
-    int r = NBT / w;
-    r = r < 1 ? 1 : (r > 64 ? 64 : r);
-    rep_s[threadIdx.x] = r;
-    rcp_s[threadIdx.x] = 1.0f / (float)r;
-  }
-  uint16_t* st16 = reinterpret_cast<uint16_t*>(lds64 + hist_elems) + wave * RM_STAGE;
-  const int64_t n_rows = (int64_t)qscale[8];
-  __syncthreads();
-  // features whose histogram slice is replicated (rep > 1): one uniform bit mask
-  uint32_t rep_mask = 0;
-  for (int fi = 0; fi < fg; ++fi) rep_mask |= (rep_s[fi] > 1 ? 1u : 0u) << fi;
-  rep_mask = __builtin_amdgcn_readfirstlane(rep_mask);
-
-  const int64_t units = npad / ROWS;
-  const int64_t u0 = units * chunk / wgpg, u1 = units * (chunk + 1) / wgpg;
-  const int64_t ustep = (int64_t)nwaves * 64;
-  // Pipeline (per wave, tiles of 64 lanes x 16 rows):
-  //   * a tile's per-row inputs (slot16) are loaded one tile ahead;
-  //   * stage(): slots -> ballot ranks -> 16-bit entries through the wave's LDS
-  //     area -> this lane's entries into registers (packed pairs);
-  //   * the gathers run two entries ahead, and the NEXT tile is staged (and its
-  //     first two gathers issued) before the current tile's last two entries'
-  //     atomics, so no tile boundary exposes a memory latency.
-  int4 in_a = make_int4(0, 0, 0, 0), in_b = make_int4(0, 0, 0, 0);
-  auto load_inputs = [&](int64_t uu) {
-    if constexpr (!ROUTE) {   // (routing loads its node ids in place: register pressure)
-      const int64_t u = (uu + lane < u1) ? uu + lane : u1 - 1;
-      const int4* sp = reinterpret_cast<const int4*>(slot16 + u * ROWS);
-      in_a = sp[0];
-      in_b = sp[1];
-    }
-  };
-  // stage tile uu: returns its built-row count (wave-uniform), entries in ep[8]
-  // (lane's entries i = 0..15 as 16-bit halves: ep[i / 2] >> 16 * (i % 2)), 0xFFFF = none
-  auto stage = [&](int64_t uu, uint32_t* ep) -> int {
-    const bool inb = uu + lane < u1;
-    const int64_t u = inb ? uu + lane : u1 - 1;
-    const int64_t r0 = u * ROWS;
-    int s[ROWS];
-    if constexpr (ROUTE) {
-      int nn[ROWS], nx[ROWS];
-      if (nid == nullptr) {
-#pragma unroll
-        for (int k = 0; k < ROWS; ++k) nn[k] = (r0 + k < n_rows) ? 0 : INT32_MIN;
-      } else {
-#pragma unroll
-        for (int q = 0; q < ROWS / 4; ++q) {
-          const int4 n4 = *reinterpret_cast<const int4*>(nid + r0 + 4 * q);
-          nn[4 * q] = n4.x; nn[4 * q + 1] = n4.y; nn[4 * q + 2] = n4.z; nn[4 * q + 3] = n4.w;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < ROWS; ++k) { nx[k] = nn[k]; s[k] = -1; }
-      const int n_prev = ctl_prev[CTL_N];
-      for (int j = 0; j < n_prev; ++j) {
-        bool mine = false;
-#pragma unroll
-        for (int k = 0; k < ROWS; ++k) mine |= (nn[k] == j);
-        if (!mine) continue;
-        const PartInfo pj = part_prev[j];
-        if (pj.child < 0) {
-#pragma unroll
-          for (int k = 0; k < ROWS; ++k)
-            if (nn[k] == j) nx[k] = ~pj.gid;
-          continue;
-        }
-        const uint4 c4 = *reinterpret_cast<const uint4*>(codes + (int64_t)pj.feat * npad + r0);
-        const uint32_t cw[4] = {c4.x, c4.y, c4.z, c4.w};
-        const int sl_l = (int)(short)(pj.pad & 0xFFFF), sl_r = pj.pad >> 16;
-#pragma unroll
-        for (int k = 0; k < ROWS; ++k) {
-          if (nn[k] == j) {
-            const int bc = (cw[k >> 2] >> (8 * (k & 3))) & 0xff;
-            const int right = part_right(pj, bc, NBT);
-            nx[k] = pj.child + right;
-            s[k] = right ? sl_r : sl_l;
-          }
-        }
-      }
-      if (route_w && inb) {
-#pragma unroll
-        for (int q = 0; q < ROWS / 4; ++q)
-          *reinterpret_cast<int4*>(nid_out + r0 + 4 * q) = make_int4(nx[4 * q], nx[4 * q + 1], nx[4 * q + 2], nx[4 * q + 3]);
-      }
-    } else {
-      const int vw[8] = {in_a.x, in_a.y, in_a.z, in_a.w, in_b.x, in_b.y, in_b.z, in_b.w};
-#pragma unroll
-      for (int k = 0; k < ROWS; ++k) s[k] = (int)(short)(vw[k >> 1] >> (16 * (k & 1)));
-    }
-    if (uu + ustep < u1) load_inputs(uu + ustep);   // the following tile's inputs in flight
-    uint32_t m = 0;
-#pragma unroll
-    for (int k = 0; k < ROWS; ++k) {
-      const int sl = s[k] - slot_lo;
-      if (inb && build && sl >= 0 && sl < slot_cnt && s[k] >= 0) m |= 1u << k;
-      s[k] = sl;
-    }
-    // exclusive rank of this lane's first built row in the wave (five ballots)
-    const uint32_t cnt = __popc(m);
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    int excl = 0, total = 0;
-#pragma unroll
-    for (int bit = 0; bit < 5; ++bit) {
-      const unsigned long long bm = __ballot((cnt >> bit) & 1u);
-      excl += __popcll(bm & lt) << bit;
-      total += __popcll(bm) << bit;
-    }
-#pragma unroll
-    for (int i = 0; i < ROWS / 2; ++i) ep[i] = 0xFFFFFFFFu;
-    if (total == 0) return 0;   // wave-uniform
-    {
-      int j = excl;
-#pragma unroll
-      for (int k = 0; k < ROWS; ++k)
-        if ((m >> k) & 1u) st16[j++] = (uint16_t)((lane * ROWS + k) | (s[k] << 10));
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int i = 0; i < ROWS; ++i) {
-      const uint32_t v = (i * 64 + lane < total) ? (uint32_t)st16[i * 64 + lane] : 0xFFFFu;
-      ep[i >> 1] = (i & 1) ? ((ep[i >> 1] & 0xFFFFu) | (v << 16)) : ((ep[i >> 1] & 0xFFFF0000u) | v);
-    }
-    wave_lds_sync();   // entries in registers: the area is free for the next tile
-    return total;
-  };
-  struct Ent { uint4 c0, c1; unsigned long long pk; int so; };
-  auto fetch = [&](uint32_t en, int64_t tile0, Ent& E) {
-    E.so = -1;
-    if (en != 0xFFFFu) {
-      const int64_t row = tile0 + (en & 1023u);
-      E.so = (int)(en >> 10) * fg * NBT;
-      const uint4* rp = reinterpret_cast<const uint4*>(codes_rm + row * RM_PITCH);
-      E.c0 = rp[0];
-      E.c1 = rp[1];
-      if constexpr (PKM == 2) {
-        E.pk = pk_buf[row];
-      } else {
-        const uint32_t pw = reinterpret_cast<const uint32_t*>(pk_buf)[row];
-        E.pk = ((unsigned long long)(uint32_t)(int)(short)(pw >> 16) << 32) | (unsigned long long)(pw & 0xFFFFu);
-      }
-    }
-  };
-  // shift a packed entry window by one entry
-  auto shift = [&](uint32_t* ep) {
-#pragma unroll
-    for (int k = 0; k < ROWS / 2 - 1; ++k) ep[k] = (ep[k] >> 16) | (ep[k + 1] << 16);
-    ep[ROWS / 2 - 1] = (ep[ROWS / 2 - 1] >> 16) | 0xFFFF0000u;
-  };
-
-  int64_t uu = u0 + (int64_t)wave * 64;
-  if (uu < u1) load_inputs(uu);
-  uint32_t ec[ROWS / 2], en_[ROWS / 2];
-  int nC = 0;
-  Ent e0, e1, e2, f0, f1;
-  e0.so = e1.so = e2.so = f0.so = f1.so = -1;
-  if (uu < u1) {
-    nC = stage(uu, ec);
-    fetch(ec[0] & 0xFFFFu, uu * ROWS, e0);
-    fetch(ec[0] >> 16, uu * ROWS, e1);
-  }
-  while (uu < u1) {
-    const int64_t uuN = uu + ustep;
-    const int niter = (nC + 63) >> 6;
-    int nN = 0;
-    bool staged = false;
-#pragma unroll 1
-    for (int it = 0; it < niter; ++it) {
-      // entry it + 2 of this tile (window position 2 after the shifts)
-      fetch(ec[1] & 0xFFFFu, uu * ROWS, e2);
-      if (it == (niter >= 2 ? niter - 2 : 0) && uuN < u1) {
-        // stage the next tile now: its first gathers overlap this tile's last atomics
-        nN = stage(uuN, en_);
-        fetch(en_[0] & 0xFFFFu, uuN * ROWS, f0);
-        fetch(en_[0] >> 16, uuN * ROWS, f1);
-        staged = true;
-      }
-      const uint32_t w[8] = {e0.c0.x, e0.c0.y, e0.c0.z, e0.c0.w, e0.c1.x, e0.c1.y, e0.c1.z, e0.c1.w};
-      // opaque per iteration: keeps the compiler from hoisting 32 per-feature lane
-      // masks out of the loop (they spill and come back as v_readlane pairs)
-      uint32_t rmask = rep_mask;
-      asm volatile("" : "+s"(rmask));
-      if (e0.so >= 0 && e0.pk != 0ull)
-#pragma unroll
-      for (int fi = 0; fi < 32; ++fi) {
-        if (fi < fg) {
-          int bin = (w[fi >> 2] >> (8 * (fi & 3))) & 0xff;
-          if ((rmask >> fi) & 1u) {
-            // replicated low-cardinality slice (rare): per-feature values read in
-            // place (relaxed atomic loads are not hoisted into registers)
-            const int rep = __hip_atomic_load(&rep_s[fi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int width = __hip_atomic_load(&width_s[fi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int copy = lane % rep;
-            if (bin == NBT - 1) bin = width - 1;
-            atomicAdd(lds64 + e0.so + fi * NBT + copy * width + bin, e0.pk);
-          } else {
-            atomicAdd(lds64 + e0.so + fi * NBT + bin, e0.pk);
-          }
-        }
-      }
-      shift(ec);
-      e0 = e1;
-      e1 = e2;
-    }
-    if (!staged && uuN < u1) {   // empty tile: stage the next one here
-      nN = stage(uuN, en_);
-      fetch(en_[0] & 0xFFFFu, uuN * ROWS, f0);
-      fetch(en_[0] >> 16, uuN * ROWS, f1);
-    }
-    uu = uuN;
-    nC = nN;
-#pragma unroll
-    for (int k = 0; k < ROWS / 2; ++k) ec[k] = en_[k];
-    e0 = f0;
-    e1 = f1;
-  }
-  __syncthreads();
-  unsigned long long* out = partials + (int64_t)chunk * hist_elems;
-  for (int j = threadIdx.x; j < hist_elems; j += blockDim.x) {
-    const int bin = j % NBT;
-    const int fi = (j / NBT) % fg;
-    const int sl = j / (NBT * fg);
-    const int width = width_s[fi], rep = rep_s[fi];
-    const unsigned long long* hb = lds64 + (sl * fg + fi) * NBT;
-    unsigned long long acc = 0ull;
-    if (rep == 1) {
-      acc = hb[bin];
-    } else {
-      const int src = (bin == NBT - 1) ? width - 1 : bin;
-      if (src < width - 1 || bin == NBT - 1)
-        for (int c = 0; c < rep; ++c) acc += hb[c * width + src];
-    }
-    out[j] = acc;
-  }
-}
-
 // Sum the per-workgroup slabs of one pass into exact int64 histograms
 // built[slot][F][2][NBT] (plane 0: G_q, plane 1: S_q).
 // Each 256-thread block owns 32 consecutive output bins and splits the
@@ -2237,152 +1778,6 @@ __global__ __launch_bounds__(1024) void node_best_finalize_kernel(
                       tree_capacity);
 }
 
-// K5 fused with the per-node arg-max and the level finalisation: one
-// 1024-thread workgroup per node, wave w scans features w, w + 16, ... and
-// the workgroup reduces the 16 wave winners (gain desc, then (feature, code)
-// asc - the node_best order) into the node's NodeSplit.  The last node
-// workgroup to finish (agent-scope release / ticket / acquire hand-off) runs
-// level_finalize_body, so a level's split decision is ONE launch instead of
-// three (split_find, node_best, level_finalize).  The ticket is reset by that
-// last workgroup (buffer zeroed once at allocation).
-template <int NBT>
-__global__ __launch_bounds__(1024) void split_level_kernel(
-    const long long* __restrict__ built, const long long* __restrict__ parent_full, long long* __restrict__ full,
-    const int* __restrict__ ctl, const NodeLink* __restrict__ link, const int* __restrict__ nvb,
-    const uint8_t* __restrict__ tree_fmask, const double* __restrict__ qscale, SplitParams p,
-    NodeSplit* __restrict__ nsplit, unsigned int* __restrict__ ticket, int* __restrict__ ctl_next,
-    const float* __restrict__ edges, int max_next_nodes, PartInfo* __restrict__ part,
-    NodeLink* __restrict__ next_link, TreeNode* __restrict__ tree, int tree_capacity) {
-  __shared__ double s_gain[16], s_gl[16], s_sl[16], s_tot[2];
-  __shared__ long long s_key[16];
-  __shared__ int s_last;
-  const int n = ctl[CTL_N];
-  const int node = blockIdx.x;
-  if (n == 0) {  // tree already finished: still publish the (empty) next level
-    if (node == 0)
-      level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, NBT, max_next_nodes, part, next_link, tree,
-                          tree_capacity);
-    return;
-  }
-  if (node >= n) return;
-  const int F = p.F;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  const NodeLink lk = link[node];
-  const double ig = qscale[2], is = qscale[3];
-  double bg = -INFINITY, bgl = 0.0, bsl = 0.0;
-  long long key = 0x7fffffffffffffffLL;
-  for (int f = wave; f < F; f += nw) {
-    const WaveBest w = feat_best_wave<NBT>(built, parent_full, full, lk, node, f, nvb, tree_fmask, ig, is, p,
-                                           ctl[CTL_BASE] + node);
-    if (f == 0 && lane == 0) { s_tot[0] = w.G; s_tot[1] = w.S; }
-    if (w.code != 0x7fffffff && w.gain > -INFINITY) {
-      const long long k = ((long long)f << 32) | (unsigned)w.code;
-      if (key == 0x7fffffffffffffffLL || w.gain > bg || (w.gain == bg && k < key)) {
-        bg = w.gain; key = k; bgl = w.GL; bsl = w.SL;
-      }
-    }
-  }
-  if (lane == 0) { s_gain[wave] = bg; s_key[wave] = key; s_gl[wave] = bgl; s_sl[wave] = bsl; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double g = -INFINITY, gl = 0.0, sl = 0.0;
-    long long k = 0x7fffffffffffffffLL;
-    for (int w = 0; w < nw; ++w) {
-      if (s_key[w] == 0x7fffffffffffffffLL) continue;
-      if (k == 0x7fffffffffffffffLL || s_gain[w] > g || (s_gain[w] == g && s_key[w] < k)) {
-        g = s_gain[w]; k = s_key[w]; gl = s_gl[w]; sl = s_sl[w];
-      }
-    }
-    NodeSplit ns;
-    ns.G = s_tot[0]; ns.H = s_tot[1]; ns.W = s_tot[1];
-    ns.pad = 0;
-    if (k != 0x7fffffffffffffffLL) {
-      const int code = (int)(k & 0xffffffff);
-      ns.gain = g; ns.GL = gl; ns.HL = sl; ns.WL = sl;
-      ns.feat = (int)(k >> 32); ns.bin = code >> 1; ns.na_left = code & 1;
-    } else {
-      ns.gain = -INFINITY; ns.GL = ns.HL = ns.WL = 0.0;
-      ns.feat = -1; ns.bin = 0; ns.na_left = 0;
-    }
-    nsplit[node] = ns;
-  }
-  // hand-off to the last arriving node workgroup (cdna_hip_programming.md split-K recipe)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = (t == (unsigned)(n - 1));
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_last = last;
-  }
-  __syncthreads();
-  if (s_last)
-    level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, NBT, max_next_nodes, part, next_link, tree,
-                        tree_capacity);
-}
-
-// split_find with the per-node arg-max and the level finalisation handed to
-// the LAST block to finish (agent-scope release / ticket / acquire, as
-// split_level_kernel), keeping split_find's grid (nodes x ceil(F / 4) blocks,
-// one wave per feature): the separate node_best_finalize launch per level
-// disappears without split_level's one-workgroup-per-node scan.  Every block
-// takes a ticket (also blocks past the live node count) so the last one is
-// well defined; it resets the ticket.  Levels of <= 64 nodes (host check).
-template <int NBT>
-__global__ __launch_bounds__(256) void split_find_fin_kernel(
-    const long long* __restrict__ built, const long long* __restrict__ parent_full, long long* __restrict__ full,
-    const int* __restrict__ ctl, const NodeLink* __restrict__ link, const int* __restrict__ nvb,
-    const uint8_t* __restrict__ tree_fmask, const double* __restrict__ qscale, SplitParams p,
-    FeatBest* __restrict__ fbest, unsigned int* __restrict__ ticket, int* __restrict__ ctl_next,
-    const float* __restrict__ edges, int max_next_nodes, PartInfo* __restrict__ part,
-    NodeLink* __restrict__ next_link, TreeNode* __restrict__ tree, int tree_capacity,
-    NodeSplit* __restrict__ nsplit) {
-  __shared__ int s_last;
-  const int n = ctl[CTL_N];
-  const int node = blockIdx.x;
-  const int f = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (node < n && f < p.F) {   // wave-uniform
-    const NodeLink lk = link[node];
-    const WaveBest w = feat_best_wave<NBT>(built, parent_full, full, lk, node, f, nvb, tree_fmask, qscale[2],
-                                           qscale[3], p, ctl[CTL_BASE] + node);
-    if ((threadIdx.x & 63) == 0) {
-      FeatBest r{};
-      r.gain = w.gain; r.GL = w.GL; r.SL = w.SL;
-      r.G = w.G; r.S = w.S;
-      r.code = w.code;
-      fbest[(int64_t)node * p.F + f] = r;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned total = gridDim.x * gridDim.y;
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = (t == total - 1u);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int nd = wid; nd < n; nd += nw) node_best_wave(fbest, p.F, nd, lane, nsplit);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, NBT, max_next_nodes, part, next_link, tree,
-                      tree_capacity);
-}
 
 // K6: route every row to its child, or retire it into its leaf (nid = ~gid).
 // Rows retiring at this level add their (g, h, w) to the exact int64 leaf
@@ -2421,10 +1816,6 @@ __device__ __forceinline__ void part_leaf_add(int leaf, int base, int win, int c
     atomicAdd(leaf_acc + 3 * leaf + 2, c);
   }
 }
-// A/B switches (H2OMX_PART_RECLDS / H2OMX_PART_RECLDS_FINAL, read by the launcher):
-// LDS-staged split records for the routing / final-level variants
-__constant__ int g_part_rec_lds = 1;
-__constant__ int g_part_rec_lds_final = 1;
 
 // NIDM bit 0: nid (input) is an int16 stream, bit 1: nid_out is int16 (fused pipeline)
 template <bool PREF, int RPL, int NIDM = 0>
@@ -2450,7 +1841,7 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
   // the level's split records: LDS-staged when they fit (the node id -> split
   // record -> split code chain then has one dependent global load, not two)
   const int n_cur = ctl_cur[CTL_N];
-  const bool rec_lds = n_cur <= PART_LDS_NODES && (PREF ? g_part_rec_lds_final : g_part_rec_lds);
+  const bool rec_lds = n_cur <= PART_LDS_NODES;   // split records staged in LDS
   if (rec_lds)
     for (int j = threadIdx.x; j < n_cur; j += blockDim.x) ps[j] = part[j];
   if (use_lds)
@@ -2654,172 +2045,6 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
         for (int c = 0; c < R; ++c) v += lacc[t * R + ((c + t) & (R - 1))];
         if (v && base + t / 3 < cap) atomicAdd(leaf_acc + 3 * base + t, v);
       }
-    }
-  }
-}
-// Routing pass of the fused pipeline (levels whose partition is not fused
-// into the next histogram, and the final level).  Same decisions as
-// partition_kernel(all_rows), restructured for the memory system:
-//   * the level's PartInfo table is staged in LDS (no dependent global
-//     gather per row between the node id and the split code);
-//   * split codes come from ONE coalesced 16-byte column load per distinct
-//     split feature of the level and lane (wave-uniform loop; a feature no
-//     row of the wave needs is skipped), not from per-row byte gathers
-//     scattered over up to n_nodes columns;
-//   * 16 rows per lane: node ids / g / h / w / slot16 move as 16-byte vectors.
-// LEAF (final level): every row retires and adds its exact fixed-point
-// (g, h, w) to the whole-tree LDS window (lane-private copies [slot][copy]),
-// folded into leaf_acc with integer atomics (deterministic).
-constexpr int ROUTE_MAX_NODES = 256;
-constexpr int ROUTE_RPL = 16;
-#ifndef H2OMX_ROUTE_FB
-#define H2OMX_ROUTE_FB 8
-#endif
-constexpr int ROUTE_FB = H2OMX_ROUTE_FB;
-
-template <bool LEAF>
-__global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ codes, int64_t npad,
-                                                    const int* nid_in, int* nid_out,
-                                                    const PartInfo* __restrict__ part, int nbt,
-                                                    const float* __restrict__ g, const float* __restrict__ h,
-                                                    const float* __restrict__ w, const double* __restrict__ qs,
-                                                    int cap, unsigned long long* __restrict__ leaf_acc,
-                                                    const int* __restrict__ ctl_cur, int R,
-                                                    short* __restrict__ slot16) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long lacc[];
-  __shared__ PartInfo pi_s[ROUTE_MAX_NODES];
-  __shared__ int first_s[ROUTE_MAX_NODES];
-  __shared__ int flist[ROUTE_MAX_NODES];
-  __shared__ int nfl_s;
-  const int n_nodes = ctl_cur[CTL_N];
-  for (int j = threadIdx.x; j < n_nodes; j += blockDim.x) pi_s[j] = part[j];
-  if (LEAF)
-    for (int j = threadIdx.x; j < 3 * cap * R; j += blockDim.x) lacc[j] = 0ull;
-  __syncthreads();
-  // distinct split features of the level, in node order
-  for (int j = threadIdx.x; j < n_nodes; j += blockDim.x) {
-    int first = pi_s[j].child >= 0;
-    for (int i = 0; i < j && first; ++i)
-      if (pi_s[i].child >= 0 && pi_s[i].feat == pi_s[j].feat) first = 0;
-    first_s[j] = first;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int c = 0;
-    for (int j = 0; j < n_nodes; ++j)
-      if (first_s[j]) flist[c++] = pi_s[j].feat;
-    nfl_s = c;
-  }
-  __syncthreads();
-  const int nfl = nfl_s;
-  const int lane = threadIdx.x & 63;
-  const int copy = lane % R;
-  float lg = 0.f, lh = 0.f, lw = 0.f;
-  if (LEAF) { lg = (float)qs[4]; lh = (float)qs[5]; lw = (float)qs[6]; }
-  const int64_t nq = npad / ROUTE_RPL;
-  // waves step together (the per-feature ballot needs converged waves)
-  const int64_t qstep = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t qb = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); qb < nq; qb += qstep) {
-    const int64_t q = qb + lane;
-    const bool inb = q < nq;
-    const int64_t r0 = (inb ? q : nq - 1) * ROUTE_RPL;
-    int nn[ROUTE_RPL];
-#pragma unroll
-    for (int v = 0; v < ROUTE_RPL / 4; ++v) {
-      const int4 a = *reinterpret_cast<const int4*>(nid_in + r0 + 4 * v);
-      nn[4 * v] = a.x; nn[4 * v + 1] = a.y; nn[4 * v + 2] = a.z; nn[4 * v + 3] = a.w;
-    }
-    float gv[ROUTE_RPL], hv[ROUTE_RPL], wv[ROUTE_RPL];
-    if (LEAF) {
-#pragma unroll
-      for (int v = 0; v < ROUTE_RPL / 4; ++v) {
-        const float4 g4 = *reinterpret_cast<const float4*>(g + r0 + 4 * v);
-        const float4 h4 = *reinterpret_cast<const float4*>(h + r0 + 4 * v);
-        float4 w4 = make_float4(1.f, 1.f, 1.f, 1.f);
-        if (w) w4 = *reinterpret_cast<const float4*>(w + r0 + 4 * v);
-        gv[4 * v] = g4.x; gv[4 * v + 1] = g4.y; gv[4 * v + 2] = g4.z; gv[4 * v + 3] = g4.w;
-        hv[4 * v] = h4.x; hv[4 * v + 1] = h4.y; hv[4 * v + 2] = h4.z; hv[4 * v + 3] = h4.w;
-        wv[4 * v] = w4.x; wv[4 * v + 1] = w4.y; wv[4 * v + 2] = w4.z; wv[4 * v + 3] = w4.w;
-      }
-    }
-    int fe[ROUTE_RPL];   // split feature of the row's node (-1: none)
-#pragma unroll
-    for (int k = 0; k < ROUTE_RPL; ++k) fe[k] = (nn[k] >= 0 && pi_s[nn[k]].child >= 0) ? pi_s[nn[k]].feat : -1;
-    uint32_t right = 0;
-    // ROUTE_FB column loads issued together per batch (a loop with one dependent
-    // load per feature exposed ~16 HBM latencies per lane step)
-    for (int t0 = 0; t0 < nfl; t0 += ROUTE_FB) {
-      uint4 c4[ROUTE_FB];
-#pragma unroll
-      for (int q = 0; q < ROUTE_FB; ++q)
-        if (t0 + q < nfl) c4[q] = *reinterpret_cast<const uint4*>(codes + (int64_t)flist[t0 + q] * npad + r0);
-#pragma unroll
-      for (int q = 0; q < ROUTE_FB; ++q) {
-        if (t0 + q < nfl) {
-          const int f = flist[t0 + q];
-          const uint32_t cw[4] = {c4[q].x, c4[q].y, c4[q].z, c4[q].w};
-#pragma unroll
-          for (int k = 0; k < ROUTE_RPL; ++k) {
-            if (fe[k] == f) {
-              const PartInfo& pi = pi_s[nn[k]];
-              const int bc = (cw[k >> 2] >> (8 * (k & 3))) & 0xff;
-              const int rt = part_right(pi, bc, nbt);
-              right |= (uint32_t)rt << k;
-            }
-          }
-        }
-      }
-    }
-    int sv[ROUTE_RPL];
-#pragma unroll
-    for (int k = 0; k < ROUTE_RPL; ++k) {
-      sv[k] = -1;
-      const int n = nn[k];
-      int leaf = -1;
-      if (n < 0) {
-        leaf = ~n;   // retired at an earlier level (padding INT_MIN -> beyond cap)
-      } else {
-        const PartInfo& pi = pi_s[n];
-        const int rt = (right >> k) & 1;
-        if (pi.child < 0) {
-          leaf = pi.gid;
-        } else if (pi.leaf_children) {
-          leaf = pi.child_gid + rt;
-        } else {
-          nn[k] = pi.child + rt;
-          sv[k] = rt ? (pi.pad >> 16) : (int)(short)(pi.pad & 0xFFFF);
-        }
-        if (leaf >= 0) nn[k] = ~leaf;
-      }
-      if (LEAF && inb && leaf >= 0 && leaf < cap && wv[k] != 0.0f) {
-        const unsigned long long a = (unsigned long long)(long long)__float2int_rn(gv[k] * lg);
-        const unsigned long long b = (unsigned long long)(long long)__float2int_rn(hv[k] * lh);
-        const unsigned long long c = (unsigned long long)(long long)__float2int_rn(wv[k] * lw);
-        unsigned long long* d = lacc + (3 * leaf) * R + copy;
-        atomicAdd(d, a);
-        atomicAdd(d + R, b);
-        atomicAdd(d + 2 * R, c);
-      }
-    }
-    if (inb) {
-#pragma unroll
-      for (int v = 0; v < ROUTE_RPL / 4; ++v)
-        *reinterpret_cast<int4*>(nid_out + r0 + 4 * v) = make_int4(nn[4 * v], nn[4 * v + 1], nn[4 * v + 2], nn[4 * v + 3]);
-      if (!LEAF) {
-#pragma unroll
-        for (int v = 0; v < ROUTE_RPL / 8; ++v)
-          *reinterpret_cast<int4*>(slot16 + r0 + 8 * v) =
-              make_int4((sv[8 * v] & 0xFFFF) | (sv[8 * v + 1] << 16), (sv[8 * v + 2] & 0xFFFF) | (sv[8 * v + 3] << 16),
-                        (sv[8 * v + 4] & 0xFFFF) | (sv[8 * v + 5] << 16), (sv[8 * v + 6] & 0xFFFF) | (sv[8 * v + 7] << 16));
-      }
-    }
-  }
-  if (LEAF) {
-    __syncthreads();
-    for (int s = threadIdx.x; s < 3 * cap; s += blockDim.x) {
-      unsigned long long v = 0ull;
-      for (int c = 0; c < R; ++c) v += lacc[s * R + c];
-      if (v) atomicAdd(leaf_acc + s, v);
     }
   }
 }
@@ -3564,79 +2789,6 @@ H2OMX_API int h2omx_hist_build_route(const uint8_t* codes, int64_t npad, const i
                            ctl_prev, nid_out, writer, stream);
 }
 
-H2OMX_API int h2omx_hist_build_compact(const uint8_t* codes, int64_t npad, const float* g, const float* s2,
-                                       const int* nid, const void* link, const int* ctl, const int* nvb,
-                                       const double* qscale, int salt, int F, int nbt, int fg, int n_groups, int wgpg,
-                                       int slot_lo, int slot_cnt, int rows_per_lane, int threads,
-                                       unsigned long long* partials, hipStream_t stream) {
-  if (wgpg % 8 != 0 || npad % 16 != 0 || fg > 256 || threads % 64 != 0 || threads > 1024 || threads < fg)
-    return kBadArg;
-  const int64_t units = npad / rows_per_lane;
-  if ((units + wgpg - 1) / wgpg * rows_per_lane > ROWS_CAP) return kBadArg;
-  const size_t lds = (size_t)slot_cnt * fg * nbt * sizeof(unsigned long long);
-  if (lds > 156 * 1024) return kBadArg;
-  const int grid = n_groups * wgpg;
-  const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
-#define H2OMX_HBC(NB)                                                                                         \
-  hipLaunchKernelGGL((hist_build_compact_kernel<NB>), dim3(grid), dim3(threads), lds, stream, codes, npad, g, s2, \
-                     nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt,          \
-                     rows_per_lane, partials)
-  switch (nbt) {
-    case 32: H2OMX_HBC(32); break;
-    case 64: H2OMX_HBC(64); break;
-    case 128: H2OMX_HBC(128); break;
-    case 256: H2OMX_HBC(256); break;
-    default: return kBadArg;
-  }
-#undef H2OMX_HBC
-  return launch_status();
-}
-
-// Row-major compacted histograms (hist_build_rm_kernel): levels >= 1, one
-// feature group (F <= 32), stored rows (pkm 2: 64-bit, 4: 32-bit); slot16
-// rows, or the previous level's routing fused in (part_prev != NULL).  The
-// partial slabs have the hist_build layout with n_groups = 1.
-H2OMX_API int h2omx_hist_build_rm(const uint8_t* codes, const uint8_t* codes_rm, int64_t npad, const int* nid,
-                                  const int* ctl, const int* nvb, const double* qscale, int F, int nbt, int wgpg,
-                                  int slot_lo, int slot_cnt, int threads, const short* slot16,
-                                  const unsigned long long* pk_buf, int pkm, unsigned long long* partials,
-                                  const void* part_prev, const int* ctl_prev, int* nid_out, int writer,
-                                  hipStream_t stream) {
-  const bool route = part_prev != nullptr;
-  if (F < 1 || F > RM_PITCH || npad % 16 != 0 || slot_cnt < 1 || slot_cnt > 63 || (pkm != 2 && pkm != 4) ||
-      pk_buf == nullptr || codes_rm == nullptr || threads % 64 != 0 || threads > 1024 || threads < 64 || wgpg < 1)
-    return kBadArg;
-  if (route && (ctl_prev == nullptr || nid_out == nullptr || nid_out == nid || codes == nullptr || threads > 512))
-    return kBadArg;
-  if (!route && slot16 == nullptr) return kBadArg;
-  const int64_t units = npad / 16;
-  if ((units + wgpg - 1) / wgpg * 16 > ROWS_CAP) return kBadArg;
-  const size_t lds = (size_t)slot_cnt * F * nbt * sizeof(unsigned long long) + (size_t)(threads / 64) * RM_STAGE * 2;
-  if (lds > 160 * 1024) return kBadArg;
-  const PartInfo* pp = reinterpret_cast<const PartInfo*>(part_prev);
-#define H2OMX_HRM(NB, M, RT)                                                                                   \
-  hipLaunchKernelGGL((hist_build_rm_kernel<NB, M, RT>), dim3(wgpg), dim3(threads), lds, stream, codes, codes_rm, \
-                     npad, nid, ctl, nvb, qscale, F, wgpg, slot_lo, slot_cnt, slot16, pk_buf, partials, pp,       \
-                     ctl_prev, nid_out, writer)
-#define H2OMX_HRM_NB(NB)                                   \
-  do {                                                     \
-    if (pkm == 2 && route) H2OMX_HRM(NB, 2, true);         \
-    else if (pkm == 2) H2OMX_HRM(NB, 2, false);            \
-    else if (route) H2OMX_HRM(NB, 4, true);                \
-    else H2OMX_HRM(NB, 4, false);                          \
-  } while (0)
-  switch (nbt) {
-    case 32: H2OMX_HRM_NB(32); break;
-    case 64: H2OMX_HRM_NB(64); break;
-    case 128: H2OMX_HRM_NB(128); break;
-    case 256: H2OMX_HRM_NB(256); break;
-    default: return kBadArg;
-  }
-#undef H2OMX_HRM_NB
-#undef H2OMX_HRM
-  return launch_status();
-}
-
 H2OMX_API int h2omx_hist_reduce(const unsigned long long* partials, int n_groups, int wgpg, int fg, int F, int nbt,
                                 int slot_lo, int slot_cnt, const int* ctl, long long* built, hipStream_t stream) {
   const int64_t total = (int64_t)slot_cnt * F * nbt;  // nbt is a multiple of 32
@@ -3733,56 +2885,6 @@ H2OMX_API int h2omx_reduce_split_p2p(const void* desc, const unsigned long long*
   return launch_status();
 }
 
-H2OMX_API int h2omx_split_level(const long long* built, const long long* parent_full, long long* full, const int* ctl,
-                                const void* link, const int* nvb, const uint8_t* tree_fmask, const double* qscale,
-                                const void* params, int max_nodes, int nbt, void* nsplit, unsigned int* ticket,
-                                int* ctl_next, const float* edges, int max_next_nodes, void* part, void* next_link,
-                                void* tree, int tree_capacity, hipStream_t stream) {
-  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
-  if (max_nodes < 1 || ticket == nullptr) return kBadArg;
-#define H2OMX_SL(NB)                                                                                            \
-  hipLaunchKernelGGL(split_level_kernel<NB>, dim3(max_nodes), dim3(1024), 0, stream, built, parent_full, full, ctl, \
-                     reinterpret_cast<const NodeLink*>(link), nvb, tree_fmask, qscale, p,                        \
-                     reinterpret_cast<NodeSplit*>(nsplit), ticket, ctl_next, edges, max_next_nodes,              \
-                     reinterpret_cast<PartInfo*>(part), reinterpret_cast<NodeLink*>(next_link),                  \
-                     reinterpret_cast<TreeNode*>(tree), tree_capacity)
-  switch (nbt) {
-    case 32: H2OMX_SL(32); break;
-    case 64: H2OMX_SL(64); break;
-    case 128: H2OMX_SL(128); break;
-    case 256: H2OMX_SL(256); break;
-    default: return kBadArg;
-  }
-#undef H2OMX_SL
-  return launch_status();
-}
-
-H2OMX_API int h2omx_split_find_fin(const long long* built, const long long* parent_full, long long* full,
-                                   const int* ctl, const void* link, const int* nvb, const uint8_t* tree_fmask,
-                                   const double* qscale, const void* params, int max_nodes, int nbt, void* fbest,
-                                   unsigned int* ticket, int* ctl_next, const float* edges, int max_next_nodes,
-                                   void* part, void* next_link, void* tree, int tree_capacity, void* nsplit,
-                                   hipStream_t stream) {
-  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
-  if (max_nodes < 1 || max_nodes > 64 || ticket == nullptr || p.F < 1) return kBadArg;
-  const dim3 grid(max_nodes, (p.F + 3) / 4);
-#define H2OMX_SFF(NB)                                                                                             \
-  hipLaunchKernelGGL(split_find_fin_kernel<NB>, grid, dim3(256), 0, stream, built, parent_full, full, ctl,          \
-                     reinterpret_cast<const NodeLink*>(link), nvb, tree_fmask, qscale, p,                         \
-                     reinterpret_cast<FeatBest*>(fbest), ticket, ctl_next, edges, max_next_nodes,                 \
-                     reinterpret_cast<PartInfo*>(part), reinterpret_cast<NodeLink*>(next_link),                   \
-                     reinterpret_cast<TreeNode*>(tree), tree_capacity, reinterpret_cast<NodeSplit*>(nsplit))
-  switch (nbt) {
-    case 32: H2OMX_SFF(32); break;
-    case 64: H2OMX_SFF(64); break;
-    case 128: H2OMX_SFF(128); break;
-    case 256: H2OMX_SFF(256); break;
-    default: return kBadArg;
-  }
-#undef H2OMX_SFF
-  return launch_status();
-}
-
 // level finalisation from per-node splits: one workgroup for small levels,
 // count / scan / write tiles (lf_*_kernel) when the level can hold more than
 // LF_MB_NODES nodes and the caller passed a tile scratch (>= max_nodes / 1024 + 1 ints)
@@ -3833,17 +2935,6 @@ H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_n
 constexpr int PARTITION_BLOCKS = 8192;
 constexpr int PART_RPL = 8;    // rows per lane per step (16: 1.52 vs 1.47 ms/tree on HIGGS)
 
-static void part_env_once() {
-  static bool done = false;
-  if (done) return;
-  done = true;
-  const char* a = getenv("H2OMX_PART_RECLDS");
-  const char* b = getenv("H2OMX_PART_RECLDS_FINAL");
-  const int va = a ? atoi(a) : 1, vb = b ? atoi(b) : 1;
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_part_rec_lds), &va, sizeof(int));
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_part_rec_lds_final), &vb, sizeof(int));
-}
-
 static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const void* part, int nbt, const float* g,
                             const float* h, const float* w, const double* qscale, int cap,
                             unsigned long long* leaf_acc, const int* ctl_cur, const int* ctl_next, int win_max,
@@ -3857,7 +2948,6 @@ static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const 
   if ((Fm != nullptr) != (gpp != nullptr) || (Fm != nullptr && (yv == nullptr || w != nullptr || !prefetch)))
     return kBadArg;
   if (slot16 && prefetch) return kBadArg;
-  part_env_once();
   if (npad % PART_RPL != 0 || blocks < 1 || blocks > PARTITION_BLOCKS || win_max < 0) return kBadArg;
   if (all_rows && (leaf_acc == nullptr || win_max > cap)) return kBadArg;
   // lane-private copies: the largest power of two <= 64 that fits 64 KB
@@ -3920,33 +3010,6 @@ H2OMX_API int h2omx_partition_final(const uint8_t* codes, int64_t npad, const in
   return partition_launch(codes, npad, const_cast<int*>(nid_in), part, nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,
                           ctl_next, cap, blocks, 1, nullptr, nid_out, 1, stream, Fm, y,
                           reinterpret_cast<const GradParams*>(gparams), nidm, y8);
-}
-
-// route_kernel entry (fused pipeline): final = 1 -> last level (leaf sums of
-// every row into leaf_acc, nid_out = ~leaf gid); final = 0 -> intermediate
-// level (nid_out, slot16).  max_nodes bounds the level's node count.
-H2OMX_API int h2omx_route_level(const uint8_t* codes, int64_t npad, const int* nid_in, int* nid_out, const void* part,
-                                int nbt, const float* g, const float* h, const float* w, const double* qscale,
-                                int cap, unsigned long long* leaf_acc, const int* ctl_cur, int max_nodes, int blocks,
-                                short* slot16, int final_level, hipStream_t stream) {
-  // nid_in == nid_out is allowed (each lane rewrites only the rows it read)
-  if (max_nodes > ROUTE_MAX_NODES || npad % ROUTE_RPL != 0 || blocks < 1) return kBadArg;
-  const PartInfo* pp = reinterpret_cast<const PartInfo*>(part);
-  if (final_level) {
-    if (leaf_acc == nullptr || g == nullptr || h == nullptr || qscale == nullptr) return kBadArg;
-    constexpr size_t kWinLds = 64 * 1024;
-    int R = 64;
-    while (R > 1 && (size_t)3 * cap * R * sizeof(unsigned long long) > kWinLds) R >>= 1;
-    if ((size_t)3 * cap * R * sizeof(unsigned long long) > kWinLds) return kBadArg;
-    hipLaunchKernelGGL(route_kernel<true>, dim3(blocks), dim3(256), (size_t)3 * cap * R * sizeof(unsigned long long),
-                       stream, codes, npad, nid_in, nid_out, pp, nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur, R,
-                       nullptr);
-  } else {
-    if (slot16 == nullptr) return kBadArg;
-    hipLaunchKernelGGL(route_kernel<false>, dim3(blocks), dim3(256), 0, stream, codes, npad, nid_in, nid_out, pp, nbt,
-                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, ctl_cur, 1, slot16);
-  }
-  return launch_status();
 }
 
 static inline int stream_grid(int64_t) { return STAT_BLOCKS; }

@@ -264,7 +264,6 @@ class _DLTrainer:
     """
 
     PROBE_STEPS = 32
-    DL_SIDE = os.environ.get("H2OMX_DL_SIDE", "0") == "1"
     # bias / output-layer gradient folds inside the ADADELTA kernel (fewer launches)
     FOLD = os.environ.get("H2OMX_DL_FOLD", "1") == "1"
 
@@ -315,9 +314,6 @@ class _DLTrainer:
                 self.spi = max(1, round(t / (self.world * M)))
         # h2omx extension: precision="bf16" trains Rectifier / Tanh nets without dropout
         # on the bf16 matrix cores (fp32 accumulation, fp32 master weights / optimizer)
-        # weight gradients on a second stream beside the dgrad chain (DL_SIDE)
-        self.side = (torch.cuda.Stream(device=dev) if dev.type == "cuda" and self.DL_SIDE and not self.sync_grad
-                     else None)
         self.mlp = None
         if (str(p_.get("precision", "fp32")).lower() == "bf16" and X.is_cuda and act in (1, 2) and drop_in == 0
                 and not any(hd[:n_hidden]) and M % 8 == 0):
@@ -499,10 +495,7 @@ class _DLTrainer:
             # the last reductions of the backward (bias-gradient slices, the output
             # layer's split partials) run inside the ADADELTA kernel
             with OD.defer_grad_folds() as folds:
-                self.backward(net, Hs, aux, dZ, self.act, comm, self.world,
-                              side=self.side if self.side is not None else None)
-        elif self.side is not None and comm is None:
-            self.backward(net, Hs, aux, dZ, self.act, comm, self.world, side=self.side)
+                self.backward(net, Hs, aux, dZ, self.act, comm, self.world)
         else:
             self.backward(net, Hs, aux, dZ, self.act, comm, self.world)
         if self.adaptive and folds:
@@ -783,38 +776,26 @@ class H2ODeepLearningEstimator(ModelBuilder):
         return model
 
     @staticmethod
-    def _backward(net, Hs, aux, dZ, act, comm, world, side=None):
-        """Back-propagation into net.grad.  ``side`` (single rank): a second
-        stream for the weight / bias gradients, which nothing later in the
-        backward reads, so they run beside the critical dgrad -> activation
-        backward chain and join before the optimizer.  Each layer's ops then
-        take their own workspace namespace (no two in-flight kernels share
-        scratch) and the tensors the side stream reads stay referenced until
-        the join."""
+    def _backward(net, Hs, aux, dZ, act, comm, world):
+        """Back-propagation into net.grad (gradient buckets all-reduced per layer,
+        overlapped with the rest of the backward, when ``comm`` syncs them).
+        (A side stream for the weight gradients measured slower inside the step
+        graph, profiles/r4/dl/side_stream_ab_r4u.txt, and was removed.)"""
         L = len(net.layers)
         handles = []
         bpart = None   # bias-gradient slices of dZ from the fused activation backward
-        main = torch.cuda.current_stream(dZ.device) if side is not None else None
-        keep = []
-        # per-layer scratch when kernels of different layers may be in flight at
-        # once (side stream) or their partial sums are folded later (deferred folds)
-        layer_ns = side is not None or OD._GRAD_FOLDS[0] is not None
+        # per-layer scratch when the partial sums are folded later (deferred folds)
+        layer_ns = OD._GRAD_FOLDS[0] is not None
         for i in range(L - 1, -1, -1):
             Hin = Hs[i]
             W = net.W(i)
-            if (i == L - 1 and i > 0 and side is None and comm is None and act in (1, 2) and aux[i - 1][1] is None
+            if (i == L - 1 and i > 0 and comm is None and act in (1, 2) and aux[i - 1][1] is None
                     and OD.out_backward_ok(dZ, Hin, net.W(i, net.grad), net.b(i, net.grad))):
                 # output layer: weight / bias gradients (a pending fold) and dZ_prev in one pass
                 with OD.workspace_ns(1000 + i):
                     dZ, bpart = OD.out_backward(dZ, Hin, W, net.W(i, net.grad), net.b(i, net.grad), act)
                 continue
-            with contextlib.ExitStack() as es:
-                if side is not None:
-                    side.wait_stream(main)
-                    es.enter_context(torch.cuda.stream(side))
-                    keep.append((dZ, Hin, bpart))
-                if layer_ns:
-                    es.enter_context(OD.workspace_ns(1000 + i))
+            with OD.workspace_ns(1000 + i) if layer_ns else contextlib.nullcontext():
                 if bpart is not None:
                     D.wgrad_bias(dZ, Hin, net.W(i, net.grad), net.b(i, net.grad), bpart)   # dW = dZ^T H, db
                 elif i == L - 1 and D.out_layer_ok(dZ, Hin):
@@ -829,9 +810,6 @@ class H2ODeepLearningEstimator(ModelBuilder):
                 break
             with OD.workspace_ns(i) if layer_ns else contextlib.nullcontext():
                 dZ, bpart = H2ODeepLearningEstimator._dgrad(Hs, aux, dZ, W, act, i, L)
-        if side is not None:
-            main.wait_stream(side)
-            del keep
         for h in handles:
             h.wait()
         if comm is not None and world > 1:

@@ -70,21 +70,6 @@ class BinnedMatrix:
             self._codes_rm = rm
         return self._codes_rm
 
-    _codes_rm32: torch.Tensor | None = None
-
-    @property
-    def codes_rm32(self) -> torch.Tensor:
-        """Row-major copy uint8 [npad][32] (F <= 32, lazily built once): the
-        compacted histogram kernel (hist_build_rm) gathers a built row's codes
-        with two 16-byte loads."""
-        if self._codes_rm32 is None:
-            if self.F > 32:
-                raise ValueError("codes_rm32 needs F <= 32")
-            rm = torch.zeros((self.npad, 32), dtype=torch.uint8, device=self.codes.device)
-            rm[:, : self.F] = self.codes.t()
-            self._codes_rm32 = rm
-        return self._codes_rm32
-
     def edges_numpy(self):
         e = self.edges.cpu().numpy()
         nv = self.nvb.cpu().numpy()

@@ -83,11 +83,13 @@ class HipTreeBuilder:
     # rows per workgroup chunk: bounds the fixed-point headroom, so the gradient
     # resolution is 2^30 / (largest chunk) levels (see tree_begin)
     ROWS_CAP = int(os.environ.get("H2OMX_ROWS_CAP", "262144"))
-    SYNC_NODE_CAP = int(os.environ.get("H2OMX_SYNC_NODE_CAP", "4096"))   # above this many potential nodes the host reads the real count
-    # wave-compacted histogram kernel for levels > 0 (H2OMX_HIST_COMPACT=1): bit-identical
-    # but measured slower (byte gathers of column-major codes are TA-bound:
-    # depth-5 HIGGS 2.03 vs 1.52 ms/tree, profiles/compact_hist_p9.txt)
-    COMPACT = os.environ.get("H2OMX_HIST_COMPACT", "0") == "1"
+    SYNC_NODE_CAP = 4096   # above this many potential nodes the host reads the real count
+    # (Removed A/B variants that measured slower and no longer exist: the
+    # wave-compacted column gather (profiles/compact_hist_p9.txt), the
+    # row-major built-row gather (profiles/r3/hist_rm_ab.txt), the route_kernel
+    # routing pass, split_find_fin / split_level fused splits
+    # (profiles/r3/hist_threads_ab.txt) and the segment-ordered code-row moves
+    # (profiles/r4/drf/move_rows_ab.txt).)
     SEG_TARGET_CHUNKS = 1024   # level-0 histogram chunks (2 resident 57 KB workgroups per CU)
     SEG_LDS_BUDGET = 64 * 1024
     SCAN_SLOTS = int(os.environ.get("H2OMX_SCAN_SLOTS", "16"))  # seg engine: scan hist up to this many slots
@@ -190,9 +192,7 @@ class HipTreeBuilder:
         # one GPU); the local plans are then held to chunks <= this (see _plan).
         self.max_rows_per_wg = None
         g_units = max(1, -(-n_global // 64) * 64) // self.ROWS_PER_LANE
-        # (compacted plans included either way: the scale must not depend on the CMP switch)
-        cands = [self._choose(1 << k, c, g_units) for k in range(0, 13) for c in (False, True)] + \
-                [self._choose(1 << 20, False, g_units)]
+        cands = [self._choose(1 << k, g_units) for k in range(0, 13)] + [self._choose(1 << 20, g_units)]
         self.max_rows_per_wg = max(self.ROWS_PER_LANE * math.ceil(g_units / c["wgpg"]) for c in cands)
         # >= 2^16 rows per workgroup bounds the per-row fixed-point values to 16 bits
         # (tree_begin: |G_q| <= 2^14, S_q <= 2^15): the packed rows are then stored in
@@ -202,7 +202,7 @@ class HipTreeBuilder:
         # level d+1's histogram kernel (node ids double-buffered), and the last level's
         # partition adds the exact sums of every row, early leaves included, into a
         # whole-tree LDS window (needs the tree capacity to fit it: depth <= 8)
-        self.fuse_route = (params.max_depth <= self.FUSE_MAX_DEPTH and not self.COMPACT
+        self.fuse_route = (params.max_depth <= self.FUSE_MAX_DEPTH
                            and os.environ.get("H2OMX_FUSE_ROUTE", "1") == "1")
         # scan engine with fused routing: levels 0 / 1 take "every live row is in the
         # root" from the row count instead of a node-id stream, so boost_update no
@@ -211,13 +211,6 @@ class HipTreeBuilder:
         self.implicit_root = (self.fuse_route and not getattr(self, "segmented", False)
                               and params.max_depth >= 2 and os.environ.get("H2OMX_IMPLICIT_ROOT", "1") != "0")
         self.nid2 = torch.full((bm.npad,), -1, dtype=torch.int32, device=d) if self.fuse_route else None
-        # one-launch split decision (split_level: 16 waves per node scan <= 4 features each,
-        # last-arriver hand-off into the level finalisation).  Bit-identical but measured
-        # slower on HIGGS depth 5 (1.108 vs 1.071 ms/tree: one workgroup per node halves
-        # the scan parallelism and the agent-scope hand-off costs about a launch), so
-        # opt-in (H2OMX_FUSE_SPLIT=1)
-        self.fuse_split = (self.F <= 64 and os.environ.get("H2OMX_FUSE_SPLIT", "0") == "1"
-                           and self.catf is None)
         self.ticket = torch.zeros((4,), dtype=torch.int32, device=d)
         # graph replay (boost.TreeGraph): tree_begin takes the tree index (dither salt,
         # qscale[9]) from this device counter instead of the host argument, and advances it
@@ -254,9 +247,9 @@ class HipTreeBuilder:
             self.codes_rm = bm.codes_rm
             self.idx = [torch.empty((max(bm.n, 1),), dtype=torch.int32, device=d) for _ in range(2)]
         # int16 node ids between the fused-routing levels (2 bytes a row each way
-        # instead of 4); the opt-in routing variants (RM / route_kernel) keep int32
+        # instead of 4)
         self.nid16 = None
-        if (self.fuse_route and self.implicit_root and not self.RM and not self.ROUTE_KERNEL and not self.CMP
+        if (self.fuse_route and self.implicit_root
                 and self.ROWS_PER_LANE == 16 and self.capacity < 32767
                 and os.environ.get("H2OMX_NID16", "1") == "1"):
             self.nid16 = (torch.full((bm.npad,), -1, dtype=torch.int16, device=d),
@@ -290,59 +283,6 @@ class HipTreeBuilder:
     # -- planning ------------------------------------------------------------
     DEEP_LDS_BUDGET = int(os.environ.get("H2OMX_HIST_DEEP_LDS_KB", "128")) * 1024
     DEEP_MIN_GROUPS = int(os.environ.get("H2OMX_HIST_DEEP_MIN_GROUPS", "4"))
-    # levels >= 1 of the scan engine: wave-compacted LDS atomics (hist_build CMP: a
-    # partly-masked ds_add_u64 costs as much as a full one, bench_micro/lds_mask.hip).
-    # The kernel adds a 2 KB staging area per wave, so the histogram budgets shrink
-    # to keep 2 (512 threads) / 1 (1024 threads) workgroups per CU.  Bit-identical
-    # but measured slower on HIGGS depth 5 (built fraction 0.3-0.45 per level: 1.28
-    # vs 0.97 ms/tree; the staging round trips cost more than the ~40 % of atomics
-    # saved), so opt-in (H2OMX_HIST_CMP=1)
-    CMP = os.environ.get("H2OMX_HIST_CMP", "0") == "1"
-    CMP_LDS_BUDGET = 56 * 1024
-    CMP_DEEP_LDS_BUDGET = 112 * 1024
-    CMP_MAX_SLOTS = 64
-    # levels >= 1 of the scan engine (F <= 32): built rows compacted per wave and
-    # gathered from the row-major code copy (hist_build_rm_kernel).  Bit-identical
-    # but measured slower on HIGGS 11M depth 5 (1.25 vs 0.945 ms/tree: routed
-    # levels 135-149 vs 110-127 us although they issue ~2.2x fewer LDS atomics,
-    # profiles/r3/hist_rm_ab.txt), so opt-in (H2OMX_HIST_RM=1)
-    RM = os.environ.get("H2OMX_HIST_RM", "0") == "1"
-    RM_THREADS = int(os.environ.get("H2OMX_RM_THREADS", "1024"))
-    RM_ROWS_PER_WG = int(os.environ.get("H2OMX_RM_ROWS_PER_WG", "32768"))
-    RM_MAX_WGS = int(os.environ.get("H2OMX_RM_MAX_WGS", "256"))
-    # levels needing more slot passes re-gather the rows once per pass: column path
-    RM_MAX_PASSES = int(os.environ.get("H2OMX_RM_MAX_PASSES", "8"))
-
-    def plan_rm(self, max_slots: int, routed: bool = False):
-        """Slots per pass / passes / grid of the compacted row-major kernel (one
-        feature group; 160 KB LDS = histograms + a 2 KB entry stage per wave).
-        Routed levels run 512-thread workgroups (register pressure)."""
-        key = ("rm", max_slots, routed)
-        if key in self.plans:
-            return self.plans[key]
-        threads = min(self.RM_THREADS, 512) if routed else self.RM_THREADS
-        per_slot = self.F * self.nbt * 8
-        budget = 160 * 1024 - (threads // 64) * 2048
-        slot_cnt = max(1, min(max_slots, 63, budget // per_slot))
-        passes = math.ceil(max_slots / slot_cnt)
-        npad = self.bm.npad
-        wgpg = min(self.RM_MAX_WGS, max(1, math.ceil(npad / self.RM_ROWS_PER_WG)))
-        # rows per workgroup <= the fixed-point headroom the scales were chosen for
-        units = npad // 16
-        while 16 * math.ceil(units / wgpg) > self.max_rows_per_wg:
-            wgpg += 1
-        plan = dict(slot_cnt=slot_cnt, passes=passes, wgpg=wgpg, threads=threads, fg=self.F, n_groups=1)
-        self.plans[key] = plan
-        return plan
-
-    def _rm_ok(self) -> bool:
-        return (self.RM and self.F <= 32 and not self.COMPACT and not self.CMP and per_slot_fits(self.F, self.nbt,
-                                                                                                self.RM_THREADS))
-
-    # fused pipeline: routing passes via route_kernel (PartInfo in LDS, one coalesced
-    # column load per distinct split feature) instead of partition_kernel's gathers
-    ROUTE_KERNEL = os.environ.get("H2OMX_ROUTE_KERNEL", "0") == "1"
-
     # level 0 of the scan engine: histograms in 8 interleaved lane copies
     # (hist_build COP: fewer LDS bank conflicts, 8x the LDS per feature, so
     # feature groups of DEEP_LDS_BUDGET); 1 = plain slices
@@ -351,9 +291,7 @@ class HipTreeBuilder:
     def plan_l0(self):
         key = ("l0", self.L0_COPIES)
         if key not in self.plans:
-            plan = self._plan(1, self.DEEP_LDS_BUDGET, self.THREADS, mult=self.L0_COPIES)
-            plan["cmp"] = False
-            self.plans[key] = plan
+            self.plans[key] = self._plan(1, self.DEEP_LDS_BUDGET, self.THREADS, mult=self.L0_COPIES)
         return self.plans[key]
 
     # grids that overflow one round of resident workgroups are widened to fill
@@ -364,10 +302,6 @@ class HipTreeBuilder:
     N_CUS = 256
     SMALL_SHARD = os.environ.get("H2OMX_HIST_SMALL", "1") == "1"
     MIN_GROUPS = int(os.environ.get("H2OMX_HIST_MIN_GROUPS", "1"))   # A/B knob
-    # scan-engine levels of <= 64 nodes: split_find_fin (last block finalises the level).
-    # Bit-identical but no faster (11-13 us vs 6.6-7.9 + 4.9-5.0 us a level: the tail is
-    # a dependent-latency chain, not launch overhead, profiles/r3/hist_threads_ab.txt ab25/26)
-    SPLIT_FIN = os.environ.get("H2OMX_SPLIT_FIN", "0") == "1"
     # single rank: slab reduction + split scan in one launch per pass (reduce_split)
     FUSE_RS = os.environ.get("H2OMX_FUSE_RS", "1") == "1"
     # persistent workgroups of the N-rank fused level (<= 256 P2P flag slots)
@@ -433,31 +367,26 @@ class HipTreeBuilder:
             wgpg = self._fill_rounds(wgpg, n_groups, slot_cnt * fg * per_slot_feat, threads, units)
         return dict(slot_cnt=slot_cnt, fg=fg, n_groups=n_groups, passes=passes, wgpg=wgpg, threads=threads)
 
-    def plan_level(self, max_slots: int, cmp: bool = False):
+    def plan_level(self, max_slots: int):
         """Feature grouping / slot passes / grid for a level with max_slots built nodes.
         Shallow levels use 64 KB / 512-thread workgroups (2 per CU); levels
         that would need >= 4 feature groups switch to 128 KB / 1024 threads
-        (1 per CU) so each row chunk is re-read by fewer groups.  ``cmp``
-        plans for the wave-compacted kernel (smaller histogram budgets, <= 64
-        slots per pass; plan["cmp"] is False when that does not fit)."""
-        key = (max_slots, cmp)
+        (1 per CU) so each row chunk is re-read by fewer groups."""
+        key = max_slots
         if key in self.plans:
             return self.plans[key]
-        plan = self._choose(max_slots, cmp)
+        plan = self._choose(max_slots)
         self.plans[key] = plan
         return plan
 
-    def _choose(self, max_slots: int, cmp: bool, units: int | None = None):
+    def _choose(self, max_slots: int, units: int | None = None):
         """plan_level's choice for ``units`` row units (default: this rank's)."""
-        lo, hi = (self.CMP_LDS_BUDGET, self.CMP_DEEP_LDS_BUDGET) if cmp else (self.LDS_BUDGET, self.DEEP_LDS_BUDGET)
+        lo, hi = self.LDS_BUDGET, self.DEEP_LDS_BUDGET
         plan = self._plan(max_slots, lo, self.THREADS, units)
         if hi > lo and plan["n_groups"] >= self.DEEP_MIN_GROUPS:
             deep = self._plan(max_slots, hi, 1024, units)
             if deep["n_groups"] < plan["n_groups"] or deep["passes"] < plan["passes"]:
                 plan = deep
-        plan["cmp"] = cmp
-        if cmp and (plan["slot_cnt"] > self.CMP_MAX_SLOTS or self.ROWS_PER_LANE != 16):
-            plan = dict(self._choose(max_slots, False, units))
         return plan
 
     def _fused_level(self, d: int) -> bool:
@@ -566,8 +495,7 @@ class HipTreeBuilder:
             else:
                 max_slots = 1 if d == 0 else max(1, max_nodes // 2)
             last = d == max_depth - 1
-            plan = self.plan_level(max_slots, cmp=d > 0 and self.CMP and not self.COMPACT)
-            cmp_flag = 8 if plan["cmp"] else 0
+            plan = self.plan_level(max_slots)
             l0_copies = d == 0 and grad_fuse is None and self.L0_COPIES in (4, 8)
             if l0_copies:
                 plan = self.plan_l0()
@@ -576,23 +504,19 @@ class HipTreeBuilder:
             sp.depth = d
             sp.children_leaves = 1 if last else 0
             self._cat_level(max_nodes)
-            routed = fuse and d > 0 and self._fused_level(d)
-            rm_level = d > 0 and self._rm_ok() and self.plan_rm(max_slots, routed)["passes"] <= self.RM_MAX_PASSES
             # N ranks over P2P: the level's exchange runs inside the fused reduce +
             # split scan when the level is one histogram pass on EVERY rank (the
             # slot budget alone decides that - rank-independent - while feature
             # groups / grids follow each rank's row count) and its rows fit the
             # symmetric buffer
-            fuse_p2p = (p2p is not None and self.FUSE_RS and not self.fuse_split and not rm_level
+            fuse_p2p = (p2p is not None and self.FUSE_RS
                         and max_slots * nbt * 8 <= self.LDS_BUDGET
                         and max_slots * F * 2 * nbt * 8 <= p2p.cap)
             # each pass's slab reduction runs the split scan of its slots right away
             # (reduce_split; N ranks: reduce_split_p2p); otherwise the level's
             # histograms are reduced, all-reduced and scanned in separate launches
-            rs = ((comm is None or fuse_p2p) and self.FUSE_RS and not self.fuse_split
-                  and not (self.SPLIT_FIN and max_nodes <= 64 and self.catf is None))
-            fbest = (self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
-                     if not self.fuse_split else None)
+            rs = (comm is None or fuse_p2p) and self.FUSE_RS
+            fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
 
             def reduce(n_groups, wgpg, fg, slot_lo, slot_cnt):
                 if rs and fuse_p2p:
@@ -614,26 +538,6 @@ class HipTreeBuilder:
                                                     P(ctl_cur), P(built), st), "hist_reduce")
             hist_elems = plan["slot_cnt"] * plan["fg"] * nbt
             partials = self._buf("partials", plan["n_groups"] * plan["wgpg"] * hist_elems, torch.int64)
-            if rm_level:
-                # deeper levels: built rows only, whole rows gathered row-major
-                plan = self.plan_rm(max_slots, routed)
-                hist_elems = plan["slot_cnt"] * self.F * nbt
-                partials = self._buf("partials", plan["wgpg"] * hist_elems, torch.int64)
-                for ps in range(plan["passes"]):
-                    slot_lo = ps * plan["slot_cnt"]
-                    with T("hist"):
-                        ops.check(lib.h2omx_hist_build_rm(
-                            P(bm.codes), P(bm.codes_rm32), bm.npad,
-                            P((None if (d == 1 and self.implicit_root) else nid_buf[(d - 1) % 2]) if routed
-                              else None),
-                            P(ctl_cur), P(bm.nvb), P(self.qscale), F, nbt, plan["wgpg"], slot_lo,
-                            plan["slot_cnt"], plan["threads"], P(None if routed else self.slot16), P(self.pk),
-                            4 if self.pk32 else 2, P(partials), P(part_prev if routed else None),
-                            P(ctl_nxt if routed else None), P(nid_buf[d % 2] if routed else None),
-                            1 if ps == 0 else 0, st), "hist_build_rm")
-                    with T("hist_reduce"):
-                        reduce(1, plan["wgpg"], F, slot_lo, plan["slot_cnt"])
-                plan = dict(passes=0)
             # level 0 streams every row; deeper levels touch only the built
             # (smaller) children -> wave-compacted kernel keeps atomics dense
             for ps in range(plan["passes"]):
@@ -647,7 +551,7 @@ class HipTreeBuilder:
                             P(nid_buf[d % 2]), 1 if ps == 0 else 0, P(ctl_cur), P(bm.nvb), P(self.qscale), F, nbt,
                             plan["fg"], plan["n_groups"], plan["wgpg"], slot_lo, plan["slot_cnt"],
                             self.ROWS_PER_LANE, plan["threads"], P(self.pk),
-                            (4 if self.pk32 else 2) + cmp_flag + (64 if nid16 else 0),
+                            (4 if self.pk32 else 2) + (64 if nid16 else 0),
                             P(partials), st),
                             "hist_build_route")
                     elif d == 0 and grad_fuse is not None:
@@ -659,12 +563,6 @@ class HipTreeBuilder:
                             P(self.nid), P(self.tree_buf), self.capacity, P(g), P(h), 1 if gf["apply"] else 0,
                             0 if p.mode == 0 else 1, 0 if self.pk32 else 1, ctypes.addressof(gf["gp"]), st),
                             "hist_build_grad")
-                    elif d > 0 and self.COMPACT:
-                        ops.check(lib.h2omx_hist_build_compact(
-                            P(bm.codes), bm.npad, P(g), P(s2), P(self.nid), P(link[cur]), P(ctl_cur), P(bm.nvb),
-                            P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, plan["fg"], plan["n_groups"],
-                            plan["wgpg"], slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],
-                            P(partials), st), "hist_build")
                     else:
                         # level 0 stores the packed quantised rows; deeper levels read them
                         # with the build slots the previous partition wrote
@@ -676,7 +574,7 @@ class HipTreeBuilder:
                             plan["wgpg"], slot_lo, plan["slot_cnt"], self.ROWS_PER_LANE, plan["threads"],
                             P(self.slot16), P(self.pk),
                             ((6 if pk_boost else 1 + (2 if self.pk32 else 0)) if d == 0
-                             else 2 + cmp_flag + (2 if self.pk32 else 0))
+                             else 2 + (2 if self.pk32 else 0))
                             + ({8: 16, 4: 32}.get(self.L0_COPIES, 0) if l0_copies else 0),
                             P(partials), st),
                             "hist_build")
@@ -693,43 +591,19 @@ class HipTreeBuilder:
                 link[nxt] = nl
             nsplit = self._buf("nsplit", max_nodes * 9, torch.float64)  # NodeSplit = 72 B
             with T("split"):
-                if self.fuse_split:
-                    # scan + per-node arg-max + level finalisation in one launch
-                    ops.check(lib.h2omx_split_level(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
-                                                    P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
-                                                    P(nsplit), P(self.ticket), P(ctl_nxt), P(bm.edges),
-                                                    next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
-                                                    st), "split_level")
-                elif self.SPLIT_FIN and max_nodes <= 64 and self.catf is None:
-                    # split scan + per-node arg-max + finalisation: the last block finalises
-                    ops.check(lib.h2omx_split_find_fin(P(built), P(full_prev), P(full_cur), P(ctl_cur), P(link[cur]),
-                                                       P(bm.nvb), P(tree_fmask), P(self.qscale), spp, max_nodes, nbt,
-                                                       P(fbest), P(self.ticket), P(ctl_nxt), P(bm.edges), next_nodes,
-                                                       P(part), P(nl), P(self.tree_buf), self.capacity, P(nsplit),
-                                                       st), "split_find_fin")
-                else:
-                    if not rs:
-                        ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur),
-                                                       P(link[cur]), P(bm.nvb), P(tree_fmask), P(self.qscale), spp,
-                                                       max_nodes, nbt, P(fbest), st), "split_find")
-                    ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
-                                                       P(bm.nvb), nbt, next_nodes, P(part), P(nl),
-                                                       P(self.tree_buf), self.capacity, P(nsplit), max_nodes,
-                                                       self._lf_tiles(max_nodes),
-                                                       st), "level_finalize")
+                if not rs:
+                    ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur),
+                                                   P(link[cur]), P(bm.nvb), P(tree_fmask), P(self.qscale), spp,
+                                                   max_nodes, nbt, P(fbest), st), "split_find")
+                ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
+                                                   P(bm.nvb), nbt, next_nodes, P(part), P(nl),
+                                                   P(self.tree_buf), self.capacity, P(nsplit), max_nodes,
+                                                   self._lf_tiles(max_nodes),
+                                                   st), "level_finalize")
             # leaves that can retire at this level: gids [base, base + n + n_next)
             win = min(3 * max_nodes, self.capacity)
             with T("partition"):
-                route_k = self.ROUTE_KERNEL and max_nodes <= 256
-                if fuse and route_k and (last or not self._fused_level(d + 1)):
-                    ops.check(lib.h2omx_route_level(P(bm.codes), bm.npad, P(nid_buf[d % 2]),
-                                                    P(self.nid if last else nid_buf[(d + 1) % 2]), P(part), nbt,
-                                                    P(g if last else None), P(h if last else None),
-                                                    P(w if last else None), P(self.qscale if last else None),
-                                                    self.capacity, P(self.leaf_acc if last else None), P(ctl_cur),
-                                                    max_nodes, self.part_blocks, P(None if last else self.slot16),
-                                                    1 if last else 0, st), "route_level")
-                elif fuse and last:
+                if fuse and last:
                     rg = self.regrad if (chain and w is None) else None   # (F, y, GradParams)
                     # chained graph steps: int16 leaf ids into the free node-id buffer
                     # for boost_update; otherwise int32 into self.nid
@@ -806,7 +680,7 @@ class HipTreeBuilder:
     leaf16_buf = None   # int16 leaf ids of the last chained tree (boost_update reads them)
 
     def can_pack_in_boost(self) -> bool:
-        return (self.PK_IN_BOOST and self.pk32 and self.implicit_root and not self.segmented and not self.COMPACT
+        return (self.PK_IN_BOOST and self.pk32 and self.implicit_root and not self.segmented
                 and self.L0_COPIES in (1, 4, 8))
 
     def begin(self, smax: torch.Tensor, tree_index: int) -> None:
@@ -819,31 +693,11 @@ class HipTreeBuilder:
                                             tree_index & 0x7FFFFFFF, P(self.tree_ctr), ops.stream(self.dev)),
                   "tree_begin")
 
-    # timing experiment only (wrong trees): direct levels read code rows in
-    # segment order as if the rows had been moved with their segments
-    DBG_SEQ_ROWS = os.environ.get("H2OMX_DBG_SEQ_ROWS", "0") == "1"
     # data-parallel direct levels: histogram chunk all-reduced per call (bytes)
     DIRECT_DP = os.environ.get("H2OMX_DIRECT_DP", "1") == "1"
     DIRECT_DP_CHUNK_BYTES = int(os.environ.get("H2OMX_DIRECT_DP_CHUNK_MB", "64")) << 20
 
-    # segmented engine: move the row-major code rows with their segments once the
-    # next level reads rows by segment (direct levels: a random cache line per
-    # row otherwise); "direct" / "seg" (copy every level) / "once" / "0" (off)
-    MOVE_ROWS = os.environ.get("H2OMX_MOVE_ROWS", "0")
-
-    def _move_rows(self, crow, next_direct: bool, next_seg_hist: bool) -> bool:
-        """Route with code-row moves (MOVE_ROWS direct / seg: every level from the
-        first reader on; once: copy at the first direct level, afterwards only
-        the rows' positions move - deeper nodes read inside their ancestor's
-        contiguous block, which the XCD-aware direct grids keep in one L2)."""
-        if self.MOVE_ROWS == "0" or self.segmented is False or (self.comm is not None and self.comm.world_size > 1):
-            return False
-        if crow["cur"] is not None:
-            return True
-        return next_direct or (self.MOVE_ROWS == "seg" and next_seg_hist)
-
-    def _direct_dp(self, comm, idx_in, gs, seg_start, seg_cnt, ctl_cur, tree_fmask, spp, max_nodes, nsplit, st,
-                   crow=None):
+    def _direct_dp(self, comm, idx_in, gs, seg_start, seg_cnt, ctl_cur, tree_fmask, spp, max_nodes, nsplit, st):
         """Direct level over N row shards: per node chunk, this rank's eligible-
         feature histograms (h2omx_direct_dp phase 0) -> all-reduce -> the scan
         (phase 1) writes the nodes' NodeSplit records, identical on every rank."""
@@ -857,7 +711,7 @@ class HipTreeBuilder:
                 ops.check(lib.h2omx_direct_dp(phase, P(self.codes_rm), bm.fp, P(idx_in), P(gs["g"]), P(gs["s"]),
                                               P(seg_start), P(seg_cnt), P(ctl_cur), P(bm.nvb), P(tree_fmask),
                                               P(self.qscale), spp, self.nbt, node0, nc, P(dh), P(nsplit),
-                                              gs["pos"], P(crow), st), "direct_dp")
+                                              gs["pos"], None, st), "direct_dp")
                 if phase == 0:
                     comm.all_reduce_(dh[: nc * stride])
         self.stats["direct_dp_levels"] = self.stats.get("direct_dp_levels", 0) + 1
@@ -898,11 +752,9 @@ class HipTreeBuilder:
         # (g, s2) as the current level reads them: by row at level 0, afterwards in segment order
         # (part_scatter moves them with the rows, so the histogram passes read them contiguously)
         gs = {"g": g, "s": s2, "pos": 0}
-        # row-major code rows in the current level's segment order (MOVE_ROWS), None = gather by row id
-        crow = {"cur": None, "pos": None}   # pos: rows' positions in cur (MOVE_ROWS=once), None = j
 
         def route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first, ctl_cur, ctl_nxt,
-                  idx_in, next_direct, ec=None, move=False):
+                  idx_in, next_direct, ec=None):
             """part_count -> level_close -> part_scatter: rows into their next-level segments.
             ec: (codes, stride, nodeq) of the direct pass - split codes read in segment order."""
             cur, nxt = d % 2, (d + 1) % 2
@@ -931,8 +783,7 @@ class HipTreeBuilder:
                     nbuilt = B("built", max_nodes * self.per_node, torch.int64)
                 ops.check(lib.h2omx_part_count(P(bm.codes), bm.npad, P(idx_in), P(seg_start), P(seg_cnt),
                                                P(pc_first), P(ctl_cur), P(part), nbt, max_pc, P(pc_left), pwave,
-                                               P(dirb), P(ecodes), ecs, P(nodeq), P(crow["cur"]), bm.fp,
-                                               P(crow["pos"]), st),
+                                               P(dirb), P(ecodes), ecs, P(nodeq), None, bm.fp, None, st),
                           "part_count")
                 if max_nodes <= self.CLOSE_SINGLE_BLOCK:
                     ops.check(lib.h2omx_level_close(P(ctl_cur), P(ctl_nxt), P(part), P(nl), P(seg_start),
@@ -960,28 +811,13 @@ class HipTreeBuilder:
             if not last and self.PERMUTE_GS:
                 gout = B(f"gperm{d % 2}", n + 64, torch.float32)
                 sout = None if s2 is None else B(f"sperm{d % 2}", n + 64, torch.float32)
-            crow_out = cpos_out = None
-            if move and not last:
-                if self.MOVE_ROWS == "once" and crow["cur"] is not None:
-                    # rows moved once: only their positions follow the segments
-                    cpos_out = B(f"cpos{d % 2}", n + 64, i32)
-                else:
-                    # the next level's code rows in its segment order (double-buffered)
-                    crow_out = B(f"crow{d % 2}", (n + 1) * bm.fp, torch.uint8)
             ops.check(lib.h2omx_part_scatter(P(bm.codes), bm.npad, P(idx_in), P(idx_out), P(self.nid), write_nid,
                                              P(seg_start), P(seg_cnt), P(pc_first), P(pc_left), P(node_nl),
                                              P(ctl_cur), P(part), nbt, P(g), P(h), P(w), P(self.qscale),
                                              self.capacity, P(self.leaf_acc), max_pc, pwave | segf, P(dirb), P(gs["g"]),
                                              P(gs["s"]), P(gout), P(sout), P(ecodes), ecs, P(nodeq),
-                                             P(self.codes_rm), P(crow["cur"]), P(crow_out), bm.fp,
-                                             P(crow["pos"]), P(cpos_out), st),
+                                             P(self.codes_rm), None, None, bm.fp, None, None, st),
                       "part_scatter")
-            if cpos_out is not None:
-                crow["pos"] = cpos_out
-            else:
-                crow["cur"], crow["pos"] = crow_out, None
-            if crow_out is not None:
-                self.stats["moved_row_levels"] = self.stats.get("moved_row_levels", 0) + 1
             if gout is not None:
                 gs.update(g=gout, s=sout, pos=1)
             else:
@@ -1046,16 +882,15 @@ class HipTreeBuilder:
                 ecodes, ecs, nodeq = ec if ec is not None else (None, 0, None)
                 if comm is not None:
                     self._direct_dp(comm, idx_in, gs, seg_start, seg_cnt, ctl_cur, tree_fmask, spp, max_nodes,
-                                    nsplit, st, crow["cur"])
+                                    nsplit, st)
                     ec = None
                 else:
                     ops.check(lib.h2omx_seg_direct(P(self.codes_rm), bm.fp,
-                                                   P(None if self.DBG_SEQ_ROWS else idx_in), P(gs["g"]), P(gs["s"]),
+                                                   P(idx_in), P(gs["g"]), P(gs["s"]),
                                                    P(seg_start), P(seg_cnt), P(ctl_cur), P(bm.nvb), P(tree_fmask),
                                                    P(self.qscale), tree_index & 0x7FFFFFFF, spp, nbt, max_nodes,
                                                    dmode, P(pc_first), max_pc, P(slab), P(tot_slab), P(ticket),
-                                                   P(nsplit), gs["pos"], P(ecodes), ecs, P(nodeq), P(crow["cur"]),
-                                                   P(crow["pos"]), st),
+                                                   P(nsplit), gs["pos"], P(ecodes), ecs, P(nodeq), None, None, st),
                               "seg_direct")
                 ops.check(lib.h2omx_level_finalize_ns(P(nsplit), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
                                                       P(bm.nvb), nbt, next_nodes, P(part), P(nl), P(self.tree_buf),
@@ -1063,7 +898,7 @@ class HipTreeBuilder:
                                                       self._lf_tiles(max_nodes), st),
                           "level_finalize_ns")
                 idx_in, _ = route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first, ctl_cur,
-                                  ctl_nxt, idx_in, True, ec, move=self._move_rows(crow, True, False))
+                                  ctl_nxt, idx_in, True, ec)
                 full_prev = None
                 max_nodes = next_nodes
                 continue
@@ -1079,7 +914,7 @@ class HipTreeBuilder:
                                                    P(seg_start), P(seg_cnt), P(hc_first), P(ctl_cur), P(bm.nvb),
                                                    P(self.qscale), tree_index & 0x7FFFFFFF, F, nbt, self.seg_fg,
                                                    self.seg_groups, self.hc_rows, max_hc, self.seg_threads, P(slab),
-                                                   gs["pos"], P(crow["cur"]), P(crow["pos"]), st), "hist_build_seg")
+                                                   gs["pos"], None, None, st), "hist_build_seg")
                 ksplit = max(1, min(32, 4096 // max(1, max_slots * ((F * nbt + 255) // 256))))
                 ksplit = max(ksplit, 4)
                 ops.check(lib.h2omx_hist_reduce_seg(P(slab), P(hc_first), P(slot_node), P(ctl_cur), F, nbt,
@@ -1120,10 +955,8 @@ class HipTreeBuilder:
                                                next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
                                                P(nsplit), max_nodes, self._lf_tiles(max_nodes), st),
                       "level_finalize")
-            nd = direct_ok and next_nodes >= self.DIRECT_MIN_NODES        # next level direct (upper bound)
-            ns = max_nodes > self.SCAN_SLOTS or next_nodes > self.SYNC_NODE_CAP
             idx_in, built_zeroed = route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first,
-                                         ctl_cur, ctl_nxt, idx_in, False, move=self._move_rows(crow, nd, ns))
+                                         ctl_cur, ctl_nxt, idx_in, False)
             full_prev = full_cur
             max_nodes = next_nodes
         if comm is not None:

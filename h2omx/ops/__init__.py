@@ -20,8 +20,6 @@ TREE_SIGS = {
     "h2omx_bin_features": "PLLIPPIPLS",
     "h2omx_hist_build": "PLPPPPPPPIIIIIIIIIIPPIPS",
     "h2omx_hist_reduce": "PIIIIIIIPPS",
-    "h2omx_hist_build_rm": "PPLPPPPIIIIIIPPIPPPPIS",
-    "h2omx_hist_build_compact": "PLPPPPPPPIIIIIIIIIIPS",
     "h2omx_hist_build_route": "PLPPPPIPPPIIIIIIIIIPIPS",
     "h2omx_hist_build_grad": "PLPPPIIIIIIIIIPPPPPPIPPIIIPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
@@ -29,13 +27,10 @@ TREE_SIGS = {
     "h2omx_reduce_split_p2p": "PPIIIPPPPPPPPIPIS",
     "h2omx_leaf_finalize_p2p": "PPPPPPIIPIIPPLPS",
     "h2omx_level_finalize": "PPPPPPIIPPPIPIPS",
-    "h2omx_split_level": "PPPPPPPPPIIPPPPIPPPIS",
-    "h2omx_split_find_fin": "PPPPPPPPPIIPPPPIPPPIPS",
     "h2omx_partition": "PLPPIPPPPIPPPIIIPS",
     "h2omx_partition_blocks": "",
     "h2omx_partition_final": "PLPPPIPPPPIPPPIPPPIPS",
     "h2omx_partition_route": "PLPPPIPPIPIS",
-    "h2omx_route_level": "PLPPPIPPPPIPPIIPIS",
     "h2omx_leaf_reduce": "PIIPS",
     "h2omx_boost_update": "PPPLLPPPPPPPLPIPIPPIIPPS",
     "h2omx_apply_tree": "PLPPS",

@@ -587,7 +587,7 @@ def thin_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int):
 
 # gemm_dact's 128 x 64 output blocks needed to prefer it over GEMM + act_backward_bias
 # (256-row mini-batches: 16 blocks ran 38 us vs 8 + 5 us, profiles/r4/dl/gemm_dact_small_ab_r4ag.txt)
-DACT_MIN_BLOCKS = int(os.environ.get("H2OMX_DACT_MIN_BLOCKS", "128"))
+DACT_MIN_BLOCKS = 128
 
 
 def dact_ok(dZ: torch.Tensor, W: torch.Tensor) -> bool:

@@ -36,7 +36,10 @@ def lib():
         L = _native.require("mlp")
         for fn, args in (("h2omx_mlp_sizes", [ctypes.c_void_p]),
                          ("h2omx_mlp_phase", [ctypes.c_void_p, ctypes.c_void_p]),
-                         ("h2omx_mlp_out", [ctypes.c_void_p, ctypes.c_void_p])):
+                         ("h2omx_mlp_out", [ctypes.c_void_p, ctypes.c_void_p]),
+                         ("h2omx_gemm_x3", [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])):
             f = getattr(L, fn)
             f.argtypes = args
             f.restype = ctypes.c_int
@@ -56,7 +59,7 @@ class GemmJob(ctypes.Structure):
                 ("ldy", ctypes.c_int), ("bias", ctypes.c_void_p), ("Y", ctypes.c_void_p), ("db", ctypes.c_void_p),
                 ("W", ctypes.c_void_p), ("Eg2", ctypes.c_void_p), ("Edx2", ctypes.c_void_p),
                 ("bW", ctypes.c_void_p), ("bEg2", ctypes.c_void_p), ("bEdx2", ctypes.c_void_p),
-                ("ada", ctypes.c_int), ("rot", ctypes.c_int)]
+                ("ada", ctypes.c_int), ("pad", ctypes.c_int)]
 
 
 class AdaJob(ctypes.Structure):
@@ -94,8 +97,9 @@ def _ptr(t) -> int:
 
 
 def _op(t: torch.Tensor | None, ld: int, kc: bool, ptr: int | None = None) -> Opnd:
+    # vec: K-contiguous rows that are 16-byte aligned (float4 loads along k)
     p = ptr if ptr is not None else t.data_ptr()
-    return Opnd(p, ld, 1 if kc else 0, 1 if (kc and ld % 4 == 0 and p % 16 == 0) else 0)
+    return Opnd(p, ld, 1 if kc else 0, 1 if (kc and ld % 4 == 0 and p % 16 == 0 and ld >= 4) else 0)
 
 
 N_CUS = 256
@@ -105,9 +109,8 @@ N_CUS = 256
 # H2OMX_MLP_DEPTH the 16-k load groups in flight per wave (1, 2, 4, 8)
 _TILE = os.environ.get("H2OMX_MLP_TILE", "")
 DEPTH = int(os.environ.get("H2OMX_MLP_DEPTH", "4"))
-# rotate each tile's k-group order (L2 channel spread) / pad activation rows off
-# the 2 KB channel period (A/B knobs; see csrc/mlp_kernels.hip tile_gemm)
-ROT = os.environ.get("H2OMX_MLP_ROT", "1") == "1"
+# activation rows padded off the 2 KB L2-channel period (A/B knob: no measured
+# difference either way on MI355X, profiles/r5/dl/fused_step_ab_r5f.jsonl)
 PAD = os.environ.get("H2OMX_MLP_PAD", "1") == "1"
 
 
@@ -141,11 +144,12 @@ def gemm_job(A: Opnd, B: Opnd, I: int, J: int, K: int, epi: int, act: int, out: 
              bias=None, Y=None, ldy: int = 0, db=None, ada=None) -> GemmJob:
     ri, rj = pick_tile(I, J)
     tj = -(-J // (16 * rj))
+    if K % 4:   # float4 (kLdV) operands need whole float4 groups of k
+        A.vec = B.vec = 0
     j = GemmJob()
     j.A, j.B, j.I, j.J, j.K = A, B, I, J, K
     j.RI, j.RJ, j.tiles_j, j.tiles = ri, rj, tj, tj * -(-I // (16 * ri))
     j.epi, j.act, j.out, j.ldo, j.ldy = epi, act, _ptr(out), ldo, ldy
-    j.rot = 1 if ROT else 0
     j.bias, j.Y, j.db = _ptr(bias), _ptr(Y), _ptr(db)
     if ada is not None:
         W, Eg2, Edx2, bW, bEg2, bEdx2 = ada
@@ -311,3 +315,26 @@ class FusedMlpStep:
     @property
     def launches(self) -> int:
         return len(self.fwd) + 1 + len(self.bwd) + (1 if self.tail is not None else 0)
+
+
+def gemm_x3_ok(A: torch.Tensor, B: torch.Tensor) -> bool:
+    """Operands the x3 GEMM takes: K-contiguous fp32 rows, 16-byte aligned, K % 4 == 0."""
+    return (A.is_cuda and A.dtype == torch.float32 and B.dtype == torch.float32 and A.stride(1) == 1
+            and B.stride(1) == 1 and A.stride(0) % 4 == 0 and B.stride(0) % 4 == 0 and A.shape[1] % 4 == 0
+            and A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0 and _native.available("mlp"))
+
+
+def gemm_x3(A: torch.Tensor, B: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
+            out: torch.Tensor | None = None) -> torch.Tensor:
+    """C = act(A B^T + bias) for fp32 A [M][K], B [N][K] on the bf16 matrix cores
+    with an exact 3-piece operand split (csrc/mlp_kernels.hip gemm_x3_nt_kernel):
+    fp32-equivalent accuracy at ~2.7x the fp32-MFMA rate."""
+    M, K = A.shape
+    N = B.shape[0]
+    C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=A.device)
+    if bias is not None:
+        bias = bias.float().contiguous()
+    _native.check(lib().h2omx_gemm_x3(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
+                                      0 if bias is None else bias.data_ptr(), M, N, K, act,
+                                      _native.stream_of(A.device)), "gemm_x3")
+    return C

@@ -28,11 +28,11 @@ def test_headline_plans_unchanged():
     b = _builder(11_000_000, 28)
     l0 = b._plan(1, b.DEEP_LDS_BUDGET, b.THREADS, mult=8)
     assert (l0["n_groups"], l0["fg"], l0["wgpg"], l0["threads"]) == (4, 7, 64, 1024)
-    got = {s: (lambda p: (p["n_groups"], p["wgpg"], p["threads"]))(b._choose(s, False)) for s in (1, 2, 4, 8)}
+    got = {s: (lambda p: (p["n_groups"], p["wgpg"], p["threads"]))(b._choose(s)) for s in (1, 2, 4, 8)}
     assert got == {1: (1, 256, 1024), 2: (2, 128, 1024), 4: (2, 128, 1024), 8: (4, 64, 1024)}
     ref = _builder(11_000_000, 28, small=False, fill=False)
     for s in (1, 2, 4, 8):
-        assert b._choose(s, False) == ref._choose(s, False)
+        assert b._choose(s) == ref._choose(s)
 
 
 @pytest.mark.parametrize("n", [1_375_000, 2_750_000, 5_500_000])
@@ -40,11 +40,11 @@ def test_small_shards_fill_every_cu(n):
     b = _builder(n, 28)
     old = _builder(n, 28, small=False)
     for s in (1, 2, 4, 8):
-        p = b._choose(s, False)
-        assert _wgs(p) >= HipTreeBuilder.N_CUS or _wgs(p) >= _wgs(old._choose(s, False))
+        p = b._choose(s)
+        assert _wgs(p) >= HipTreeBuilder.N_CUS or _wgs(p) >= _wgs(old._choose(s))
         assert p["threads"] == 1024 and p["wgpg"] % 8 == 0 and p["fg"] * p["n_groups"] >= 28
     if n == 1_375_000:   # 11M / 8: level 1 went from 40 to 256 workgroups
-        assert _wgs(old._choose(1, False)) == 40 and _wgs(b._choose(1, False)) == 256
+        assert _wgs(old._choose(1)) == 40 and _wgs(b._choose(1)) == 256
 
 
 def test_fill_rounds_widens_capped_grids():

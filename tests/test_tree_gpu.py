@@ -160,91 +160,6 @@ def test_segmented_engine_matches_scan_engine(cuda_dev, monkeypatch, dist, depth
                 np.testing.assert_allclose(a.trees[t][i]["value"], b.trees[t][i]["value"], rtol=1e-6, atol=1e-7)
 
 
-@pytest.mark.parametrize("dist,depth,sample_rate", [("bernoulli", 6, 1.0), ("gaussian", 9, 0.7),
-                                                    ("multinomial", 4, 1.0)])
-def test_compact_hist_matches_plain(cuda_dev, monkeypatch, dist, depth, sample_rate):
-    """The wave-compacted histogram kernel produces bit-identical trees."""
-    import h2omx.models.tree.engine as E
-
-    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi"}[dist]
-    X, y = _data(n=50000, F=9, seed=5, task=task)
-    _, bg = _both(X, y, 255)
-    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2)
-    yt = torch.from_numpy(y).cuda()
-    out = {}
-    for flag in (False, True):
-        monkeypatch.setattr(E.HipTreeBuilder, "COMPACT", flag)
-        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
-                                   nclass=3 if dist == "multinomial" else 1, seed=7)
-    a, b = out[False], out[True]
-    for t in range(a.trees.shape[0]):
-        reach = a.compact()[t]
-        assert reach == b.compact()[t]
-        for f in ("feat", "bin", "value"):
-            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
-
-
-@pytest.mark.parametrize("dist,depth,sample_rate,nbins,fuse", [
-    ("bernoulli", 5, 1.0, 255, True), ("bernoulli", 5, 1.0, 255, False), ("gaussian", 9, 0.7, 63, True),
-    ("multinomial", 4, 1.0, 255, True), ("drf", 12, 0.632, 20, False)])
-def test_wave_compacted_atomics_match_plain(cuda_dev, monkeypatch, dist, depth, sample_rate, nbins, fuse):
-    """hist_build's LDS-staged wave compaction (CMP, levels >= 1) builds
-    bit-identical trees to one atomic per row position; the depth-12 / 20-bin
-    case runs passes of 64 slots (16-bit entry 0xFFFF is a live row)."""
-    import h2omx.models.tree.engine as E
-
-    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi", "drf": "bin"}[dist]
-    X, y = _data(n=60000, F=9, seed=8, task=task)
-    _, bg = _both(X, y, nbins)
-    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2, leaf_mode=1 if dist == "drf" else 0,
-                    mtries=3 if dist == "drf" else 0)
-    yt = torch.from_numpy(y).cuda()
-    monkeypatch.setenv("H2OMX_TREE_ENGINE", "scan")
-    monkeypatch.setenv("H2OMX_FUSE_ROUTE", "1" if fuse else "0")
-    nclass = 3 if dist == "multinomial" else (2 if dist == "drf" else 1)
-    out = {}
-    for flag in (False, True):
-        monkeypatch.setattr(E.HipTreeBuilder, "CMP", flag)
-        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
-                                   nclass=nclass, seed=7)
-    a, b = out[False], out[True]
-    for t in range(a.trees.shape[0]):
-        reach = a.compact()[t]
-        assert reach == b.compact()[t]
-        for f in ("feat", "bin", "value"):
-            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
-
-
-@pytest.mark.parametrize("dist,depth,sample_rate,nbins", [
-    ("bernoulli", 5, 1.0, 255), ("gaussian", 8, 0.7, 63), ("multinomial", 4, 1.0, 255), ("bernoulli", 2, 1.0, 20),
-    ("drf", 7, 0.632, 255)])
-def test_route_kernel_matches_partition_kernel(cuda_dev, monkeypatch, dist, depth, sample_rate, nbins):
-    """The fused pipeline's routing passes through route_kernel (LDS split
-    table, per-feature coalesced code loads) build bit-identical trees and
-    exact leaf sums to partition_kernel's per-row gathers."""
-    import h2omx.models.tree.engine as E
-
-    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi", "drf": "bin"}[dist]
-    X, y = _data(n=70000, F=11, seed=4, task=task)
-    _, bg = _both(X, y, nbins)
-    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2, leaf_mode=1 if dist == "drf" else 0,
-                    mtries=4 if dist == "drf" else 0)
-    yt = torch.from_numpy(y).cuda()
-    monkeypatch.setenv("H2OMX_TREE_ENGINE", "scan")
-    nclass = 3 if dist == "multinomial" else (2 if dist == "drf" else 1)
-    out = {}
-    for flag in (False, True):
-        monkeypatch.setattr(E.HipTreeBuilder, "ROUTE_KERNEL", flag)
-        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
-                                   nclass=nclass, seed=9)
-    a, b = out[False], out[True]
-    for t in range(a.trees.shape[0]):
-        reach = a.compact()[t]
-        assert reach == b.compact()[t]
-        for f in ("feat", "bin", "value", "weight"):
-            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
-
-
 @pytest.mark.parametrize("dist,depth,sample_rate,nbins,mtries,col_rate,mode", [
     ("drf", 12, 0.632, 20, 3, 1.0, 0), ("bernoulli", 13, 0.8, 255, 0, 0.7, 1), ("gaussian", 14, 1.0, 63, 0, 1.0, 0),
     ("multinomial", 11, 1.0, 255, 0, 1.0, 0), ("drf", 16, 1.0, 127, 4, 1.0, 0)])
@@ -269,22 +184,18 @@ def test_direct_deep_levels_match_subtraction(cuda_dev, monkeypatch, dist, depth
     out = {}
     # engine switches: direct from this many nodes, wave-per-node below this many rows per node,
     # multi-block finalise, wave-chunk partition from this many nodes, chunked direct workgroups,
-    # (g, s2) moved into segment order, eligible-feature codes stored for the partition,
-    # code rows moved with their segments (from the first direct / segmented level)
+    # (g, s2) moved into segment order, eligible-feature codes stored for the partition
     keys = ("DIRECT_MIN_NODES", "DIRECT_WAVE_ROWS", "LF_MULTI_BLOCK", "PART_WAVE_NODES", "DIRECT_CHUNKED",
-            "PERMUTE_GS", "ECODES", "MOVE_ROWS")
-    for cfg in ((0, 0, False, 1 << 30, True, False, False, "0"), (0, 0, True, 1, True, True, True, "0"),
-                (2, 0, True, 1 << 30, True, True, True, "0"), (64, 0, True, 1 << 30, False, False, True, "0"),
-                (64, 1 << 30, True, 1, True, True, False, "0"), (64, 1 << 30, False, 2048, True, False, True, "0"),
-                (2, 0, True, 1 << 30, True, True, True, "seg"), (64, 1 << 30, True, 1, True, True, False, "direct"),
-                (64, 0, True, 1 << 30, False, False, True, "seg"), (0, 0, True, 1, True, True, True, "seg"),
-                (2, 0, True, 1 << 30, True, True, True, "once"), (64, 1 << 30, True, 1, True, True, False, "once"),
-                (64, 0, True, 1 << 30, True, True, True, "once")):
+            "PERMUTE_GS", "ECODES")
+    for cfg in ((0, 0, False, 1 << 30, True, False, False), (0, 0, True, 1, True, True, True),
+                (2, 0, True, 1 << 30, True, True, True), (64, 0, True, 1 << 30, False, False, True),
+                (64, 1 << 30, True, 1, True, True, False), (64, 1 << 30, False, 2048, True, False, True),
+                (64, 0, True, 1 << 30, True, True, True)):
         for k, v in zip(keys, cfg):
             monkeypatch.setattr(E.HipTreeBuilder, k, v)
         out[cfg] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
                                   nclass=nclass, seed=13)
-    a = out[(0, 0, False, 1 << 30, True, False, False, "0")]
+    a = out[(0, 0, False, 1 << 30, True, False, False)]
     for cfg, b in out.items():
         for t in range(a.trees.shape[0]):
             reach = a.compact()[t]
@@ -365,61 +276,6 @@ def test_fused_routing_matches_partition(cuda_dev, monkeypatch, dist, depth, sam
             for f in ("feat", "bin", "value", "weight"):
                 np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
         np.testing.assert_array_equal(margin(a), margin(b))
-
-
-@pytest.mark.parametrize("dist,depth,sample_rate,mtries", [("bernoulli", 5, 1.0, 0), ("gaussian", 9, 0.7, 0),
-                                                           ("multinomial", 4, 1.0, 0), ("drf", 12, 0.632, 3)])
-def test_fused_split_level_matches(cuda_dev, monkeypatch, dist, depth, sample_rate, mtries):
-    """split_level (scan + node arg-max + finalisation in one launch, last-arriver
-    hand-off) builds the same trees as split_find + node_best + level_finalize."""
-    import h2omx.models.tree.engine as E
-
-    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi", "drf": "bin"}[dist]
-    X, y = _data(n=40000, F=9, seed=13, task=task)
-    _, bg = _both(X, y, 63)
-    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2, leaf_mode=1 if dist == "drf" else 0,
-                    mtries=mtries)
-    yt = torch.from_numpy(y).cuda()
-    nclass = 3 if dist == "multinomial" else (2 if dist == "drf" else 1)
-    out = {}
-    for flag in ("0", "1"):
-        monkeypatch.setenv("H2OMX_FUSE_SPLIT", flag)
-        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
-                                   nclass=nclass, seed=2)
-    a, b = out["0"], out["1"]
-    for t in range(a.trees.shape[0]):
-        reach = a.compact()[t]
-        assert reach == b.compact()[t]
-        for f in ("feat", "bin", "value", "weight", "gain"):
-            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
-
-
-@pytest.mark.parametrize("dist,depth,sample_rate,mtries", [("bernoulli", 5, 1.0, 0), ("gaussian", 7, 0.7, 0),
-                                                           ("multinomial", 4, 1.0, 0), ("drf", 8, 0.632, 3)])
-def test_split_find_fin_matches(cuda_dev, monkeypatch, dist, depth, sample_rate, mtries):
-    """split_find_fin (split_find's grid, the last block to finish runs the
-    node arg-max + level finalisation) builds the same trees as split_find +
-    node_best_finalize."""
-    import h2omx.models.tree.engine as E
-
-    task = {"bernoulli": "bin", "gaussian": "reg", "multinomial": "multi", "drf": "bin"}[dist]
-    X, y = _data(n=40000, F=9, seed=17, task=task)
-    _, bg = _both(X, y, 63)
-    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2, leaf_mode=1 if dist == "drf" else 0,
-                    mtries=mtries)
-    yt = torch.from_numpy(y).cuda()
-    nclass = 3 if dist == "multinomial" else (2 if dist == "drf" else 1)
-    out = {}
-    for flag in (False, True):
-        monkeypatch.setattr(E.HipTreeBuilder, "SPLIT_FIN", flag)
-        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
-                                   nclass=nclass, seed=2)
-    a, b = out[False], out[True]
-    for t in range(a.trees.shape[0]):
-        reach = a.compact()[t]
-        assert reach == b.compact()[t]
-        for f in ("feat", "bin", "value", "weight", "gain"):
-            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
 
 
 @pytest.mark.parametrize("nbins", [20, 255])
@@ -517,30 +373,3 @@ def test_graph_replay_matches_eager(cuda_dev, monkeypatch, dist, depth, min_rows
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"tree {t} {f}")
     torch.testing.assert_close(a._state.Fm, b._state.Fm, rtol=0, atol=0)
 
-
-@pytest.mark.parametrize("dist,depth,sample_rate,nbins,n,F", [
-    ("bernoulli", 5, 1.0, 255, 300_000, 11), ("bernoulli", 8, 0.7, 63, 200_000, 9),
-    ("gaussian", 6, 1.0, 31, 150_000, 28), ("multinomial", 4, 1.0, 255, 100_000, 7),
-    ("bernoulli", 2, 1.0, 127, 50_000, 32)])
-def test_row_major_compacted_hist_matches_plain(cuda_dev, monkeypatch, dist, depth, sample_rate, nbins, n, F):
-    """Levels >= 1 built from compacted built rows gathered row-major
-    (hist_build_rm_kernel: routed and slot16 levels, several slot passes,
-    low-cardinality replication, bagged-out rows) give bit-identical trees."""
-    import h2omx.models.tree.engine as E
-
-    X, y = _data(n=n, F=F, seed=13, task={"bernoulli": "bin", "gaussian": "reg"}.get(dist, "multi"))
-    _, bg = _both(X, y, nbins)
-    tp = TreeParams(max_depth=depth, min_rows=3, learn_rate=0.2)
-    yt = torch.from_numpy(y).cuda()
-    monkeypatch.setenv("H2OMX_TREE_GRAPH", "0")
-    out = {}
-    for flag in (False, True):
-        monkeypatch.setattr(E.HipTreeBuilder, "RM", flag)
-        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate, seed=5,
-                                   nclass=4 if dist == "multinomial" else 1)
-    a, b = out[False], out[True]
-    for t in range(a.trees.shape[0]):
-        reach = a.compact()[t]
-        assert reach == b.compact()[t], t
-        for f in ("feat", "bin", "value", "weight"):
-            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"tree {t} {f}")
