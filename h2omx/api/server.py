@@ -571,6 +571,8 @@ class H2OApi:
             mid = self.cluster.run("train", algo=algo, params=args, x=x, y=y, training_frame=tf,
                                    validation_frame=vf, model_id=model_id)
             self.counters["models_built"] += 1
+            # deviations from H2O's semantics the builder reported (model.warnings)
+            job.warnings.extend(getattr(DKV.get(mid), "warnings", None) or [])
             return mid
 
         blocking = str(params.get("_blocking", "false")).lower() == "true"

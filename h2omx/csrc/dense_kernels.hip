@@ -2741,12 +2741,6 @@ H2OMX_API int h2omx_glm_irls_wave(const float* X, int64_t ld, int64_t n, const f
   return launch_status();
 }
 
-static int glm_split_glds = 1;   // LDS-DMA staging of aligned designs (0: register prefetch; A/B)
-H2OMX_API int h2omx_glm_split_set_prefetch(int glds) {
-  glm_split_glds = glds ? 1 : 0;
-  return kOk;
-}
-
 // glm_irls_split_kernel: same contract and slab layout as h2omx_glm_irls_wave
 // for an NA-free design (`means` is not read)
 H2OMX_API int h2omx_glm_irls_split(const float* X, int64_t ld, int64_t n, const float* y, const float* wprior,
@@ -2763,14 +2757,8 @@ H2OMX_API int h2omx_glm_irls_split(const float* X, int64_t ld, int64_t n, const 
   const bool logit = P.family == 1 && P.link == 1;
   const int blocks = cdiv(n_units, 4);
 #define GSL(NB, V, F)                                                                                          \
-  do {                                                                                                         \
-    if (V && glm_split_glds)                                                                                   \
-      hipLaunchKernelGGL((glm_irls_split_kernel<NB, V, F, V>), dim3(blocks), dim3(256), 0, stream, X, ld, n, y,  \
-                         wprior, offset, beta, P, rows_per_unit, n_units, slab, dev_out);                      \
-    else                                                                                                       \
-      hipLaunchKernelGGL((glm_irls_split_kernel<NB, V, F, false>), dim3(blocks), dim3(256), 0, stream, X, ld, n, \
-                         y, wprior, offset, beta, P, rows_per_unit, n_units, slab, dev_out);                   \
-  } while (0)
+  hipLaunchKernelGGL((glm_irls_split_kernel<NB, V, F, V>), dim3(blocks), dim3(256), 0, stream, X, ld, n, y,      \
+                     wprior, offset, beta, P, rows_per_unit, n_units, slab, dev_out)
 #define GSL_NB(NB)                      \
   do {                                  \
     if (logit) {                        \

@@ -483,24 +483,53 @@ struct X3Regs {
   float4 a[4], b[4];
 };
 
+// one 32-k stage of both operands into registers.  A: [M][K] rows (K
+// contiguous, float4 runs).  B: [N][K] rows like A, or (kBT) K-major [K][N]
+// (the NN data gradient's weight operand): each thread then gathers one
+// column's 16 consecutive k with scalar loads (coalesced across lanes along
+// N), so the LDS image is the same [n][k] plane either way
+template <bool kBT>
 __device__ __forceinline__ void x3_load(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb,
                                         int M, int N, int K, int m0, int n0, int k0, X3Regs& r) {
   const int t = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int f = q * 256 + t, row = f >> 3, k = k0 + (f & 7) * 4;
-    const int i = m0 + row, j = n0 + row;
+    const int i = m0 + row;
     r.a[q] = (i < M && k < K) ? *reinterpret_cast<const float4*>(A + (int64_t)i * lda + k) : make_float4(0, 0, 0, 0);
-    r.b[q] = (j < N && k < K) ? *reinterpret_cast<const float4*>(B + (int64_t)j * ldb + k) : make_float4(0, 0, 0, 0);
+    if (!kBT) {
+      const int j = n0 + row;
+      r.b[q] = (j < N && k < K) ? *reinterpret_cast<const float4*>(B + (int64_t)j * ldb + k) : make_float4(0, 0, 0, 0);
+    }
+  }
+  if (kBT) {
+    const int j = n0 + (t & 127), kb = k0 + (t >> 7) * 16;
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = (j < N && kb + i < K) ? B[(int64_t)(kb + i) * ldb + j] : 0.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r.b[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
   }
 }
 
+// kDB: two LDS stage buffers (one barrier per 32-k stage, the next stage's
+// split under this stage's MFMAs) - 120 KB of LDS, one workgroup per CU: for
+// grids of at most one tile per CU (8192 x 512: 40.1 vs 44.0 us); larger grids
+// keep one buffer and two workgroups per CU (8192 x 2048 x 2048: 402 vs 441 us,
+// profiles/r5/dl/gemm_x3_r5o.jsonl)
+// kBT: B is K-major [K][N] (see x3_load).  kEPI 0: C = act(acc + bias); 1
+// (back-propagation through an activation, gemm_dact's contract): C = acc *
+// act'(Y) (Y [M][ldc] = the layer's output) and bws[M / 128 block][N] = the
+// block's column sums of C (bias-gradient partials)
+template <bool kDB, bool kBT = false, int kEPI = 0>
 __global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict__ A, int lda,
                                                         const float* __restrict__ B, int ldb, float* __restrict__ C,
                                                         int ldc, const float* __restrict__ bias, int M, int N, int K,
-                                                        int act) {
-  __shared__ __attribute__((aligned(16))) __bf16 La[3 * X3_PLANE];
-  __shared__ __attribute__((aligned(16))) __bf16 Lb[3 * X3_PLANE];
+                                                        int act, const float* __restrict__ Y = nullptr,
+                                                        float* __restrict__ bws = nullptr) {
+  constexpr int NBUF = kDB ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) __bf16 La[NBUF][3 * X3_PLANE];
+  __shared__ __attribute__((aligned(16))) __bf16 Lb[NBUF][3 * X3_PLANE];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int li = lane & 31, lh = lane >> 5;
   // XCD-aware order: linear block b runs on XCD b % 8; give each XCD a
@@ -520,16 +549,22 @@ __global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
   const int nst = (K + X3_BK - 1) / X3_BK;
   X3Regs r;
-  x3_load(A, lda, B, ldb, M, N, K, m0, n0, 0, r);
-  for (int st = 0; st < nst; ++st) {
+  x3_load<kBT>(A, lda, B, ldb, M, N, K, m0, n0, 0, r);
+  auto stage = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int f = q * 256 + t, row = f >> 3, k = (f & 7) * 4;
-      x3_store(La, row, k, r.a[q]);
-      x3_store(Lb, row, k, r.b[q]);
+      x3_store(La[buf], row, k, r.a[q]);
+      x3_store(Lb[buf], row, k, r.b[q]);
     }
-    __syncthreads();
-    if (st + 1 < nst) x3_load(A, lda, B, ldb, M, N, K, m0, n0, (st + 1) * X3_BK, r);
+  };
+  if (kDB) { stage(0); __syncthreads(); }
+  for (int st = 0; st < nst; ++st) {
+    const int buf = kDB ? (st & 1) : 0;
+    if (!kDB) { stage(0); __syncthreads(); }
+    if (st + 1 < nst) x3_load<kBT>(A, lda, B, ldb, M, N, K, m0, n0, (st + 1) * X3_BK, r);
+    const __bf16* La_ = La[buf];
+    const __bf16* Lb_ = Lb[buf];
 #pragma unroll
     for (int kk = 0; kk < X3_BK; kk += 16) {
       x3_bf16x8 fa[2][3], fb[2][3];
@@ -537,28 +572,59 @@ __global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int p = 0; p < 3; ++p)
-          fa[a][p] = *reinterpret_cast<const x3_bf16x8*>(La + p * X3_PLANE + (wm + 32 * a + li) * X3_ROW + kk + 8 * lh);
+          fa[a][p] = *reinterpret_cast<const x3_bf16x8*>(La_ + p * X3_PLANE + (wm + 32 * a + li) * X3_ROW + kk + 8 * lh);
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int p = 0; p < 3; ++p)
-          fb[b][p] = *reinterpret_cast<const x3_bf16x8*>(Lb + p * X3_PLANE + (wn + 32 * b + li) * X3_ROW + kk + 8 * lh);
+          fb[b][p] = *reinterpret_cast<const x3_bf16x8*>(Lb_ + p * X3_PLANE + (wn + 32 * b + li) * X3_ROW + kk + 8 * lh);
+      // small terms first (fp32 accumulation order: lo-order products then hi.hi);
+      // product-major issue (4 independent accumulators between dependent MFMAs;
+      // measured the same as accumulator-major)
+      constexpr int PA[6] = {1, 2, 0, 1, 0, 0}, PB[6] = {1, 0, 2, 0, 1, 0};
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int q = 0; q < 6; ++q)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          // small terms first (fp32 accumulation order: lo-order products then hi.hi)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], fb[b][1], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][2], fb[b][0], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][2], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], fb[b][0], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][1], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][0], acc[a][b], 0, 0, 0);
-        }
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][PA[q]], fb[b][PB[q]], acc[a][b], 0, 0, 0);
+    }
+    if (kDB) {
+      if (st + 1 < nst) stage(buf ^ 1);
     }
     __syncthreads();
   }
   // epilogue: lane owns column j, registers e are rows (e & 3) + 8 (e >> 2) + 4 lh
+  if constexpr (kEPI == 1) {
+    float* red = reinterpret_cast<float*>(&La[0][0]);   // [2 row-waves][128] (the loop ended on a barrier)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int j = n0 + wn + 32 * b + li;
+      float cs = 0.0f;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = m0 + wm + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          if (i < M && j < N) {
+            const int64_t o = (int64_t)i * ldc + j;
+            const float y = Y[o], g = acc[a][b][e];
+            const float v = act == 1 ? (y > 0.0f ? g : 0.0f) : (act == 2 ? g * (1.0f - y * y) : g);
+            C[o] = v;
+            cs += v;
+          }
+        }
+      cs += __shfl_xor(cs, 32, 64);
+      if (lh == 0) red[(w >> 1) * X3_BN + wn + 32 * b + li] = cs;
+    }
+    __syncthreads();
+    for (int c = t; c < X3_BN; c += 256) {
+      const int j = n0 + c;
+      if (j < N) bws[(int64_t)(m0 / X3_BM) * N + j] = red[c] + red[X3_BN + c];
+    }
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -587,6 +653,28 @@ H2OMX_API int h2omx_gemm_x3(const float* A, int lda, const float* B, int ldb, fl
   if (A == nullptr || B == nullptr || C == nullptr || M < 1 || N < 1 || K < 1) return kBadArg;
   if ((lda & 3) || (ldb & 3) || (K & 3) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return kBadArg;
   const dim3 grid((N + X3_BN - 1) / X3_BN, (M + X3_BM - 1) / X3_BM);
-  hipLaunchKernelGGL(gemm_x3_nt_kernel, grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, N, K, act);
+  if ((int64_t)grid.x * grid.y <= 256)
+    hipLaunchKernelGGL(gemm_x3_nt_kernel<true>, grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, N, K, act);
+  else
+    hipLaunchKernelGGL(gemm_x3_nt_kernel<false>, grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, N, K, act);
+  return launch_status();
+}
+
+// back-propagation through an activation on the x3 kernel (h2omx_gemm_dact's
+// contract): C[M][N] = (A[M][K] B[K][N]) * act'(Y[M][N]), B K-major (the layer's
+// weights [K][N]); bws[cdiv(M, 128)][N] = per-128-row-block column sums of C.
+// A rows 16-byte aligned (lda % 4 == 0), K % 4 == 0
+H2OMX_API int h2omx_gemm_x3_dact(const float* A, int lda, const float* B, int ldb, float* C, const float* Y, float* bws,
+                                 int M, int N, int K, int act, hipStream_t stream) {
+  if (A == nullptr || B == nullptr || C == nullptr || Y == nullptr || bws == nullptr || M < 1 || N < 1 || K < 1)
+    return kBadArg;
+  if ((lda & 3) || (K & 3) || ((uintptr_t)A & 15)) return kBadArg;
+  const dim3 grid((N + X3_BN - 1) / X3_BN, (M + X3_BM - 1) / X3_BM);
+  if ((int64_t)grid.x * grid.y <= 256)
+    hipLaunchKernelGGL((gemm_x3_nt_kernel<true, true, 1>), grid, dim3(256), 0, stream, A, lda, B, ldb, C, N, nullptr,
+                       M, N, K, act, Y, bws);
+  else
+    hipLaunchKernelGGL((gemm_x3_nt_kernel<false, true, 1>), grid, dim3(256), 0, stream, A, lda, B, ldb, C, N, nullptr,
+                       M, N, K, act, Y, bws);
   return launch_status();
 }

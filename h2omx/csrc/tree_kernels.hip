@@ -77,6 +77,15 @@ struct SplitParams {
   const uint8_t* catf;
   uint32_t* fbcat;
   uint32_t* treecat;
+  // per-node histogram rule (adaptive_candidates): hist_mode 0 = every fine bin,
+  // 1 UniformAdaptive, 2 Random, 3 RoundRobin; edges [F][NBT] fine cut points,
+  // frange [F][4] = (min, max, exact, integer)
+  const float* edges;
+  const float* frange;
+  int hist_mode;
+  int hist_top;      // nbins_top_level
+  int hist_nbins;    // nbins (per-node floor)
+  int pad3;
 };
 
 struct NodeSplit {  // best split of one node at the current level (64 B)
@@ -1093,6 +1102,107 @@ __device__ __forceinline__ bool feat_allowed(const uint8_t* __restrict__ tree_fm
   return allowed && inter_ok(p, gid, f);
 }
 
+// H2O's adaptive histograms (hex/tree/DHistogram; histogram_type AUTO =
+// UniformAdaptive) re-bin every node's own [min, max] of a numeric column into
+// nb = max(nbins_top_level >> depth, nbins) equal-width bins (Random: nb - 1
+// uniform random cut points in that range, drawn per node; RoundRobin: one of
+// UniformAdaptive, UniformAdaptive, Random, QuantilesGlobal by tree index, the
+// AUTO entry of H2O's cycle being UniformAdaptive).  Here the histogram stays
+// the fine one (<= 255 quantile or one-per-value bins) and the node's candidate
+// thresholds are restricted instead: fine edge e[t] stays a candidate iff some
+// cut falls in its cell (midpoint to the previous interior edge, midpoint to
+// the next], i.e. it is the interior edge nearest to that cut (ties: the lower
+// one).  The node's range comes from its first / last non-empty fine bin
+// (their lower / upper boundaries; exact bins: their values, the true node
+// min / max).  An integer column spanning <= nb values keeps every threshold
+// (H2O: one bin per integer).  Returns bit k = bin lane * B + k is a candidate;
+// thresholds outside [lo, hi) (NA-only partitions) always are.
+// CPU mirror: reference/tree.py adaptive_mask (same double arithmetic,
+// contraction off, same hashes).
+__device__ __forceinline__ double ua_cut(double lo, double span, int k, int nb) {
+#pragma clang fp contract(off)
+  return lo + (span * (double)k) / (double)nb;
+}
+
+// number of uniform cuts c_1 .. c_{nb-1} at or below x
+__device__ __forceinline__ int ua_count(double x, double lo, double span, int nb) {
+#pragma clang fp contract(off)
+  if (x == -INFINITY) return 0;
+  if (x == INFINITY) return nb - 1;
+  const double r = (x - lo) * (double)nb / span;
+  int k = r < 0.0 ? 0 : (r >= (double)(nb - 1) ? nb - 1 : (int)r);
+  while (k < nb - 1 && ua_cut(lo, span, k + 1, nb) <= x) ++k;
+  while (k > 0 && ua_cut(lo, span, k, nb) > x) --k;
+  return k;
+}
+
+template <int NBT, int B>
+__device__ uint32_t adaptive_candidates(const long long* si, int m, int node, int f, const SplitParams& p) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  int mode = p.hist_mode;
+  if (mode == 3) mode = (0x0211 >> (4 * (p.tree_index & 3))) & 15;   // UA, UA, Random, QuantilesGlobal
+  if (mode == 0) return 0xffffffffu;
+  int lo = 0x7fffffff, hi = -1;
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const int t = lane * B + k;
+    if (t < m && t < NBT - 1 && si[k] > 0) { lo = min(lo, t); hi = max(hi, t); }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o, kWave));
+    hi = max(hi, __shfl_xor(hi, o, kWave));
+  }
+  if (hi - lo < 1) return 0xffffffffu;   // no interior threshold
+  const float* e = p.edges + (int64_t)f * NBT;
+  const float* fr = p.frange + (int64_t)f * 4;
+  const bool exact = fr[2] != 0.0f;
+  double lo_v, hi_v;
+  if (exact) {
+    lo_v = (double)(lo < m - 1 ? e[lo] : fr[1]);
+    hi_v = (double)(hi < m - 1 ? e[hi] : fr[1]);
+  } else {
+    lo_v = (double)(lo == 0 ? fr[0] : e[lo - 1]);
+    hi_v = (double)(hi == m - 1 ? fr[1] : e[hi]);
+  }
+  const double span = hi_v - lo_v;
+  if (!(span > 0.0) || !(span < INFINITY)) return 0xffffffffu;
+  const int top = p.depth < 31 ? (p.hist_top >> p.depth) : 0;
+  const int nb = max(max(top, p.hist_nbins), 2);
+  if (fr[3] != 0.0f && span + 1.0 <= (double)nb) return 0xffffffffu;
+  double mL[B], mR[B];
+  uint32_t inner = 0;
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const int t = lane * B + k;
+    mL[k] = -INFINITY; mR[k] = INFINITY;
+    if (t >= lo && t < hi) {
+      inner |= 1u << k;
+      const double x = (double)e[t];
+      if (t > lo) mL[k] = 0.5 * ((double)e[t - 1] + x);
+      if (t < hi - 1) mR[k] = 0.5 * (x + (double)e[t + 1]);
+    }
+  }
+  uint32_t hit = 0;
+  if (mode == 1) {
+#pragma unroll
+    for (int k = 0; k < B; ++k)
+      if (((inner >> k) & 1u) && ua_count(mR[k], lo_v, span, nb) > ua_count(mL[k], lo_v, span, nb)) hit |= 1u << k;
+  } else if (inner) {
+    const uint32_t key = ((uint32_t)p.tree_index * 131u + (uint32_t)p.depth) ^ ((uint32_t)f * 0x9E3779B1u);
+    const uint32_t s2 = p.seed ^ 0x52414E44u;
+    for (int j = 1; j < nb; ++j) {
+      const double c = lo_v + span * (double)u01(hash4(s2, key, (uint32_t)node, (uint32_t)j));
+#pragma unroll
+      for (int k = 0; k < B; ++k)
+        if (mL[k] < c && c <= mR[k]) hit |= 1u << k;
+    }
+    hit &= inner;
+  }
+  return (~inner) | hit;
+}
+
 __device__ __forceinline__ WaveBest wave_best_none() {
   WaveBest r;
   r.G = r.S = 0.0;
@@ -1150,11 +1260,12 @@ __device__ __forceinline__ WaveBest feat_scan_wave(long long* gi, long long* si,
   double bGL = 0, bSL = 0;
   const int m = nvb[f];
   const int mf = p.mono ? (int)p.mono[f] : 0;
+  const uint32_t cand = p.hist_mode ? adaptive_candidates<NBT, B>(si, m, node, f, p) : 0xffffffffu;
   if (allowed) {
 #pragma unroll
     for (int k = 0; k < B; ++k) {
       const int t = lane * B + k;
-      if (t < m && t < NBT - 1) {
+      if (t < m && t < NBT - 1 && ((cand >> k) & 1u)) {
         const double sg = (double)(eg + pg[k]) * ig, ssum = (double)(es + ps[k]) * is;
         const double gA = mono_ok(mf, sg, ssum, tg, ts, p) ? split_gain(sg, ssum, tg, ts, p) : -INFINITY;
         const double gB = (ns > 0.0 && mono_ok(mf, sg + ng, ssum + ns, tg, ts, p))
@@ -2914,11 +3025,7 @@ H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_n
                                    int max_nodes, int* tiles, hipStream_t stream) {
   const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
   NodeSplit* ns = reinterpret_cast<NodeSplit*>(nsplit);
-  static const int fuse_cap = [] {
-    const char* e = getenv("H2OMX_FUSE_NODE_BEST");     // max nodes for the one-launch path (0 = off)
-    return e ? atoi(e) : 64;
-  }();
-  if (max_nodes <= fuse_cap) {
+  if (max_nodes <= 64) {   // one launch: the per-node arg-max inside the finalisation
     hipLaunchKernelGGL(node_best_finalize_kernel, dim3(1), dim3(1024), 0, stream,
                        reinterpret_cast<const FeatBest*>(fbest), ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes,
                        reinterpret_cast<PartInfo*>(part), reinterpret_cast<NodeLink*>(next_link),
@@ -3369,7 +3476,7 @@ __device__ __forceinline__ int split_dir(const uint8_t* __restrict__ codes, int6
   return part_right(pi, b, nbt);
 }
 
-// Row-major code rows kept in segment order (segmented engine, H2OMX_MOVE_ROWS):
+// Row-major code rows kept in segment order (segmented engine):
 // in = this level's rows by segment position j (nullptr: gather codes_rm by row
 // id), out = the next level's (part_scatter moves every inner row's fp bytes
 // with it), so deep levels read their nodes' rows contiguously instead of one
@@ -3707,8 +3814,9 @@ struct DirectBest {
 // the split scan of one feature's LDS histogram by one wave (split_find's
 // feat_best_wave on exact int64 rows); PACKED: one packed u64 per bin
 template <int NBT, bool PACKED>
-__device__ __forceinline__ void direct_scan_feature(const long long* __restrict__ h, int f, int m, double ig,
-                                                    double is, const SplitParams& p, int lane, DirectBest& best) {
+__device__ __forceinline__ void direct_scan_feature(const long long* __restrict__ h, int node, int f, int m,
+                                                    double ig, double is, const SplitParams& p, int lane,
+                                                    DirectBest& best) {
   constexpr int B = NBT <= 64 ? 1 : NBT / 64;
   constexpr int NA_LANE = (NBT - 1) / B, NA_K = (NBT - 1) % B;
   long long gi[B], si[B];
@@ -3747,10 +3855,11 @@ __device__ __forceinline__ void direct_scan_feature(const long long* __restrict_
   int fbc = 0x7fffffff;
   double fGL = 0, fSL = 0;
   const int mf = p.mono ? (int)p.mono[f] : 0;
+  const uint32_t cand = p.hist_mode ? adaptive_candidates<NBT, B>(si, m, node, f, p) : 0xffffffffu;
 #pragma unroll
   for (int k = 0; k < B; ++k) {
     const int tt = lane * B + k;
-    if (tt < m && tt < NBT - 1) {
+    if (tt < m && tt < NBT - 1 && ((cand >> k) & 1u)) {
       const double sgd = (double)(eg + pg[k]) * ig, ssum = (double)(es + ps[k]) * is;
       const double gA = mono_ok(mf, sgd, ssum, tg, ts, p) ? split_gain(sgd, ssum, tg, ts, p) : -INFINITY;
       const double gB = (ns > 0.0 && mono_ok(mf, sgd + ng, ssum + ns, tg, ts, p))
@@ -3993,8 +4102,8 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
     // one wave per feature of the batch
     for (int q = wid; q < nb; q += DIRECT_WAVES) {
       const int f = flist[b0 + q];
-      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, f, nvb[f], ig, is, p, lane, best);
-      else direct_scan_feature<NBT, false>(hist + q * per_f, f, nvb[f], ig, is, p, lane, best);
+      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best);
+      else direct_scan_feature<NBT, false>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best);
     }
     __syncthreads();
   }
@@ -4200,7 +4309,7 @@ __global__ __launch_bounds__(256) void direct_dp_scan_kernel(
   best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
   for (int q = wid; q < nfl; q += 4) {
     const int f = flist[q];
-    direct_scan_feature<NBT, false>(h + 2 + (int64_t)q * 2 * NBT, f, nvb[f], ig, is, p, lane, best);
+    direct_scan_feature<NBT, false>(h + 2 + (int64_t)q * 2 * NBT, node, f, nvb[f], ig, is, p, lane, best);
   }
   if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
   __syncthreads();
@@ -4335,8 +4444,8 @@ __global__ __launch_bounds__(256) void seg_direct_chunk_kernel(
   best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
   for (int q = wid; q < nfl; q += 4) {
     const int f = flist[q];
-    if (packed) direct_scan_feature<NBT, true>(hist + q * NBT, f, nvb[f], ig, is, p, lane, best);
-    else direct_scan_feature<NBT, false>(hist + q * 2 * NBT, f, nvb[f], ig, is, p, lane, best);
+    if (packed) direct_scan_feature<NBT, true>(hist + q * NBT, node, f, nvb[f], ig, is, p, lane, best);
+    else direct_scan_feature<NBT, false>(hist + q * 2 * NBT, node, f, nvb[f], ig, is, p, lane, best);
   }
   if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
   __syncthreads();
@@ -4442,8 +4551,8 @@ __global__ __launch_bounds__(256) void seg_direct_wave_kernel(
     wave_lds_sync();
     for (int q = 0; q < nb; ++q) {
       const int f = flist[b0 + q];
-      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, f, nvb[f], ig, is, p, lane, best);
-      else direct_scan_feature<NBT, false>(hist + q * per_f, f, nvb[f], ig, is, p, lane, best);
+      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best);
+      else direct_scan_feature<NBT, false>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best);
     }
     wave_lds_sync();
   }

@@ -177,7 +177,8 @@ def wide_gaussian(n: int, p: int, seed: int = 3, device="cpu", task: str = "bino
     beta = torch.zeros(p, device=dev)
     k = min(p, 20)
     beta[:k] = torch.linspace(1.0, -1.0, k, device=dev)
-    logit = beta @ X + 0.5 * X[0] * X[1] - 0.4 * torch.relu(X[2]) + 0.3 * torch.sin(2 * X[3])
+    # the k-term signal as an elementwise sum (no vendor GEMV launch)
+    logit = (beta[:k, None] * X[:k]).sum(0) + 0.5 * X[0] * X[1] - 0.4 * torch.relu(X[2]) + 0.3 * torch.sin(2 * X[3])
     if task == "regression":
         y = logit + 0.5 * torch.randn(n, generator=g, device=dev)
         return X, y

@@ -51,6 +51,8 @@ class Model:
     # fitted transformers applied to a scored frame before predict_raw (H2O
     # AutoML preprocessing, e.g. a TargetEncoderModel); empty for plain models
     preprocessors: tuple = ()
+    # deviations from H2O's semantics reported by the builder (output.warnings)
+    warnings: tuple = ()
 
     def __init_subclass__(cls, **kw):
         super().__init_subclass__(**kw)
@@ -226,6 +228,7 @@ class Model:
                 "h2omx_timings": {k: _jsonable(v) for k, v in (self.timings or {}).items()},
                 "model_summary": self.summary(),
                 "cross_validation_models": [{"name": m.model_id} for m in self.cv_models],
+                "warnings": list(getattr(self, "warnings", None) or []) or None,
             },
         }
 

@@ -32,6 +32,9 @@ class BinnedMatrix:
     # categorical group splits: per feature True for an identity-binned enum
     # column (bin = level code, <= 255 levels); None = all numeric
     cat: np.ndarray | None = None
+    # per-node histogram rules: float32 [F][4] (min, max, exact, integer) from
+    # adaptive_ranges; None when every node scans all fine bins
+    frange: torch.Tensor | None = None
 
     @property
     def catf(self) -> torch.Tensor | None:
@@ -98,32 +101,83 @@ def _edges_from_sorted(col: np.ndarray, max_value_bins: int) -> np.ndarray:
     return e[: max_value_bins - 1]
 
 
-HISTOGRAM_TYPES = {"auto": "quantilesglobal", "quantilesglobal": "quantilesglobal",
-                   "uniformadaptive": "uniformadaptive", "uniformrobust": "uniformrobust", "random": "random"}
+HISTOGRAM_TYPES = {"quantilesglobal": "quantilesglobal", "uniformadaptive": "uniformadaptive",
+                   "uniformrobust": "uniformrobust", "random": "random", "roundrobin": "roundrobin"}
+
+# SplitParams::hist_mode of the per-node rules (csrc/tree_kernels.hip
+# adaptive_candidates); QuantilesGlobal / UniformRobust scan every fine bin
+PER_NODE_MODES = {"uniformadaptive": 1, "random": 2, "roundrobin": 3}
 
 
-def resolve_histogram_type(h) -> str:
-    """H2O ``histogram_type`` -> the cut-point rule of :func:`compute_edges`.
+def resolve_histogram_type(h, auto: str = "quantilesglobal") -> str:
+    """H2O ``histogram_type`` -> the binning rule (``auto``: what AUTO means
+    for the caller - UniformAdaptive for GBM / DRF as in H2O).
 
-    * QuantilesGlobal (and AUTO, the h2omx default: documented deviation from
-      H2O, whose AUTO is UniformAdaptive): global quantile cut points.
-    * UniformAdaptive: equal-width bins over the column's range.  H2O re-bins
-      every node's own [min, max] into ``nbins``; the global u8 codes here
-      cannot change per node, so the grid is the root's (nbins_top_level
-      resolution, capped at 255 bins).
+    * QuantilesGlobal: global quantile cut points.
+    * UniformAdaptive / Random / RoundRobin are per-node rules on GBM / DRF
+      (see :func:`adaptive_ranges`); callers without the per-node scan (the
+      :func:`compute_edges` grids) get one global equal-width / random grid.
     * UniformRobust: equal-width bins over the central 99 % of the column
-      (values beyond fall into the outer bins).
-    * Random: sorted uniformly random cut points in the column's range
-      (seeded; H2O draws them per node).
-    * RoundRobin (a different type per tree) needs re-binned codes per tree
-      and is rejected."""
+      (values beyond fall into the outer bins), one global grid."""
     key = str(h or "AUTO").replace("_", "").lower()
-    if key == "roundrobin":
-        raise ValueError("histogram_type RoundRobin is not supported (it needs re-binned codes for every tree); "
-                         "use QuantilesGlobal, UniformAdaptive, UniformRobust or Random")
+    if key == "auto":
+        return auto
     if key not in HISTOGRAM_TYPES:
         raise ValueError(f"unknown histogram_type {h!r}")
     return HISTOGRAM_TYPES[key]
+
+
+def node_bins(nbins_top_level: int, nbins: int, depth: int) -> int:
+    """Equal-width bins of one node at ``depth`` (H2O: nbins_top_level at the
+    root, halved per level, never below nbins; mirrors adaptive_candidates)."""
+    top = int(nbins_top_level) >> depth if depth < 31 else 0
+    return max(top, int(nbins), 2)
+
+
+def adaptive_ranges(X: torch.Tensor, bm: "BinnedMatrix", comm=None) -> torch.Tensor:
+    """Per-feature facts the per-node histogram rules need, float32 [F][4]
+    on X's device: (min, max, exact, integer).  ``min`` / ``max`` bound the
+    first / last fine bin (NaN-free values of every rank); ``exact`` = every
+    value equals its bin's value (low-cardinality columns binned one bin per
+    distinct value: a node's range is then its own min / max); ``integer`` =
+    all values are whole numbers (H2O gives an integer column spanning at most
+    nb values one bin per value)."""
+    F, n = X.shape
+    dev = X.device
+    nvb = bm.nvb.to(dev).long()
+    edges = bm.edges.to(dev)
+    lo = torch.full((F,), float("inf"), dtype=torch.float32, device=dev)
+    hi = torch.full((F,), float("-inf"), dtype=torch.float32, device=dev)
+    isint = torch.ones(F, dtype=torch.bool, device=dev)
+    step = max(1, (1 << 26) // max(F, 1))          # rows per chunk: bounded temporaries
+    for r0 in range(0, n, step):
+        x = X[:, r0: r0 + step].float()
+        nan = torch.isnan(x)
+        lo = torch.minimum(lo, torch.where(nan, float("inf"), x).amin(1))
+        hi = torch.maximum(hi, torch.where(nan, float("-inf"), x).amax(1))
+        isint &= (nan | (x == torch.floor(x))).all(1)
+    out = np.zeros((F, 4), np.float64)
+    out[:, 0], out[:, 1] = lo.double().cpu().numpy(), hi.double().cpu().numpy()
+    if comm is not None and comm.world_size > 1:
+        out[:, 0] = comm.all_reduce_numpy(np.ascontiguousarray(out[:, 0]), "min")
+        out[:, 1] = comm.all_reduce_numpy(np.ascontiguousarray(out[:, 1]), "max")
+    fmax = torch.from_numpy(out[:, 1].astype(np.float32)).to(dev)
+    exact = torch.ones(F, dtype=torch.bool, device=dev)
+    last = (nvb - 1)[:, None]
+    for r0 in range(0, n, step):
+        x = X[:, r0: r0 + step].float()
+        code = bm.codes[:, r0: r0 + x.shape[1]].to(dev).long()
+        bval = torch.where(code < last, torch.gather(edges, 1, torch.minimum(code, (last - 1).clamp_min(0))),
+                           fmax[:, None])
+        exact &= (torch.isnan(x) | (x == bval)).all(1)
+    out[:, 2] = exact.double().cpu().numpy()
+    out[:, 3] = isint.double().cpu().numpy()
+    if comm is not None and comm.world_size > 1:
+        out[:, 2] = comm.all_reduce_numpy(np.ascontiguousarray(out[:, 2]), "min")
+        out[:, 3] = comm.all_reduce_numpy(np.ascontiguousarray(out[:, 3]), "min")
+    empty = ~(out[:, 0] <= out[:, 1])
+    out[empty, 0] = out[empty, 1] = 0.0
+    return torch.from_numpy(out.astype(np.float32)).to(bm.codes.device)
 
 
 def _range_edges(lo: float, hi: float, nb: int, kind: str, rng: np.random.Generator) -> np.ndarray:
@@ -147,7 +201,7 @@ def compute_edges(X: torch.Tensor, nbins: int, sample_rows: int = 1 << 20, seed:
     """
     kind = resolve_histogram_type(histogram_type)
     edges, nvb, nbt = _quantile_edges(X, nbins, sample_rows, seed, comm)
-    if kind == "quantilesglobal":
+    if kind in ("quantilesglobal", "roundrobin"):
         return edges, nvb, nbt
     max_value_bins = min(nbins, nbt - 1)
     # the column ranges over the same (all-gathered) sample on every rank
@@ -233,8 +287,11 @@ def sort_rows(S: torch.Tensor) -> torch.Tensor:
     return back.to(torch.int32).view(torch.float32)
 
 
-# device quantile sketch (csrc/sketch_kernels.hip); 0: sort the sample instead
-SKETCH = os.environ.get("H2OMX_SKETCH", "1") == "1"
+
+
+# device quantile sketch (csrc/sketch_kernels.hip); False: sort the sample
+# (the sketch's test oracle, tests/test_sketch_gpu.py)
+SKETCH = True
 
 
 def _key_to_float(k: np.ndarray) -> np.ndarray:

@@ -362,7 +362,7 @@ class GpuBooster:
         self.pending = False
         # 0 / 1 labels as bytes for the gradient passes (bernoulli; exact as floats)
         self.y8 = None
-        if self.K == 1 and self.dist == "bernoulli" and os.environ.get("H2OMX_Y8", "1") == "1":
+        if self.K == 1 and self.dist == "bernoulli":
             yv = self.st.y
             if bool(((yv == 0) | (yv == 1)).all()):
                 self.y8 = yv.to(torch.uint8)
@@ -450,7 +450,8 @@ class GpuBooster:
         return (self.K == 1 and not self.fused and self.sample_rate >= 1.0 and tp.col_sample_rate >= 1.0
                 and tp.col_sample_rate_per_tree >= 1.0 and tp.mtries == 0 and tp.learn_rate_annealing == 1.0
                 and not b.segmented and not b.timer.enabled and self.cap <= self.COMPACT_CAP
-                and self.dev.type == "cuda" and b.catf is None)
+                and self.dev.type == "cuda" and b.catf is None
+                and tp.hist_mode in (0, 1))   # Random / RoundRobin draw per tree index
 
     def _body_k1(self, t: int, fresh: bool, chain: bool = False):
         b = self.builder
@@ -751,7 +752,7 @@ class TreeGraph:
         self.chain = b.can_chain(gb._bounds is not None)
         b.pk_in_boost = self.chain and b.can_pack_in_boost()
         b.regrad = None
-        if b.pk_in_boost and gb.wout is None and gb.K == 1 and os.environ.get("H2OMX_REGRAD", "1") == "1":
+        if b.pk_in_boost and gb.wout is None and gb.K == 1:
             # the final partition re-derives (g, h) from the margins: boost_update
             # stores only the packed rows (8 bytes per row less each way)
             gpr = make_grad_params(gb.dist, False, 1.0, gb.seed, 0, row_base=b.row_base, **gb.kw)

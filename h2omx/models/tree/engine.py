@@ -54,6 +54,12 @@ class TreeParams:
     # interaction constraints: tuple of feature-index tuples (features of one set
     # may share a root path; unlisted features only with themselves), None = off
     interactions: tuple | None = None
+    # per-node histogram rule (binning.PER_NODE_MODES: 0 every fine bin, 1
+    # UniformAdaptive, 2 Random, 3 RoundRobin) with H2O's nbins_top_level / nbins;
+    # modes 1-3 need BinnedMatrix.frange (binning.adaptive_ranges)
+    hist_mode: int = 0
+    hist_top: int = 1024
+    hist_nbins: int = 20
     extra: dict = field(default_factory=dict)
 
 
@@ -114,7 +120,6 @@ class HipTreeBuilder:
     DIRECT_CHUNKED = True
     # segmented engine: part_scatter moves each row's (g, s2) into segment order with it
     PERMUTE_GS = True
-    SEG_LEAF_GS = os.environ.get("H2OMX_SEG_LEAF_GS", "1") == "1"
     # direct levels of <= 16 eligible features store them per row for the partition
     ECODES = True
     # levels of more than 8192 nodes finalise in count / scan / write tiles (False: one workgroup)
@@ -178,6 +183,13 @@ class HipTreeBuilder:
         self.catf = bm.catf
         self.treecat = (torch.zeros((self.capacity * 8,), dtype=torch.int32, device=d)
                         if self.catf is not None else None)
+        # per-node histogram rules read the fine edges and every feature's
+        # (min, max, exact, integer) in the split scan
+        self._frange = None
+        if params.hist_mode:
+            if getattr(bm, "frange", None) is None:
+                raise ValueError("TreeParams.hist_mode needs BinnedMatrix.frange (binning.adaptive_ranges)")
+            self._frange = bm.frange.to(d).float().contiguous()
         self.stats = {"host_syncs": 0}
         self.timer = PhaseTimer(device=d)
         # global index of this rank's first row: the stochastic-rounding dither and
@@ -209,7 +221,7 @@ class HipTreeBuilder:
         # longer resets nid and levels 0 / 1 skip reading it (needs >= 2 levels: a
         # depth-1 tree's final partition reads level 0's ids)
         self.implicit_root = (self.fuse_route and not getattr(self, "segmented", False)
-                              and params.max_depth >= 2 and os.environ.get("H2OMX_IMPLICIT_ROOT", "1") != "0")
+                              and params.max_depth >= 2)
         self.nid2 = torch.full((bm.npad,), -1, dtype=torch.int32, device=d) if self.fuse_route else None
         self.ticket = torch.zeros((4,), dtype=torch.int32, device=d)
         # graph replay (boost.TreeGraph): tree_begin takes the tree index (dither salt,
@@ -230,10 +242,10 @@ class HipTreeBuilder:
             self.fuse_route, self.nid2 = False, None
             self.implicit_root = False
             self.pc_rows = int(self.lib.h2omx_pc_rows())
-            hc = int(os.environ.get("H2OMX_SEG_CHUNK", "0")) or -(-bm.n // self.SEG_TARGET_CHUNKS)
+            hc = -(-bm.n // self.SEG_TARGET_CHUNKS)
             self.hc_rows = min(self.ROWS_CAP, max(2048, -(-hc // 256) * 256))
             # the scale covers the chunk size a 1-rank run on all rows would use
-            hc_g = int(os.environ.get("H2OMX_SEG_CHUNK", "0")) or -(-n_global // self.SEG_TARGET_CHUNKS)
+            hc_g = -(-n_global // self.SEG_TARGET_CHUNKS)
             self.max_rows_per_wg = max(self.max_rows_per_wg, self.hc_rows,
                                        min(self.ROWS_CAP, max(2048, -(-hc_g // 256) * 256)))
             budget = self.SEG_LDS_BUDGET
@@ -249,9 +261,7 @@ class HipTreeBuilder:
         # int16 node ids between the fused-routing levels (2 bytes a row each way
         # instead of 4)
         self.nid16 = None
-        if (self.fuse_route and self.implicit_root
-                and self.ROWS_PER_LANE == 16 and self.capacity < 32767
-                and os.environ.get("H2OMX_NID16", "1") == "1"):
+        if self.fuse_route and self.implicit_root and self.ROWS_PER_LANE == 16 and self.capacity < 32767:
             self.nid16 = (torch.full((bm.npad,), -1, dtype=torch.int16, device=d),
                           torch.full((bm.npad,), -1, dtype=torch.int16, device=d))
         # the fixed-point scales (tree_begin) derive from max_rows_per_wg: every rank
@@ -298,12 +308,9 @@ class HipTreeBuilder:
     # their last round: the chunk cap (ROWS_CAP) puts Airlines-shape 18.75M rows
     # at 72 x 4 = 288 one-per-CU workgroups, so 32 of them ran alone in a
     # second round
-    FILL_ROUNDS = os.environ.get("H2OMX_HIST_FILL", "1") == "1"
     N_CUS = 256
-    SMALL_SHARD = os.environ.get("H2OMX_HIST_SMALL", "1") == "1"
     MIN_GROUPS = int(os.environ.get("H2OMX_HIST_MIN_GROUPS", "1"))   # A/B knob
     # single rank: slab reduction + split scan in one launch per pass (reduce_split)
-    FUSE_RS = os.environ.get("H2OMX_FUSE_RS", "1") == "1"
     # persistent workgroups of the N-rank fused level (<= 256 P2P flag slots)
     P2P_BLOCKS = int(os.environ.get("H2OMX_P2P_BLOCKS", "256"))
     MAX_WG_THREADS_PER_CU = 2048      # 32 waves per CU
@@ -320,6 +327,11 @@ class HipTreeBuilder:
         if fill > wgpg and fill * threads <= units:
             return fill
         return wgpg
+
+    # small-shard grid widening and round filling (class flags: the planner tests
+    # compare against the plans without them)
+    SMALL_SHARD = True
+    FILL_ROUNDS = True
 
     def _plan(self, max_slots: int, budget: int, threads: int, units: int | None = None, mult: int = 1):
         per_slot_feat = self.nbt * 8 * mult
@@ -410,6 +422,9 @@ class HipTreeBuilder:
         sp.catf = self.catf.data_ptr() if self.catf is not None else None
         sp.treecat = self.treecat.data_ptr() if self.treecat is not None else None
         sp.fbcat = None
+        sp.hist_mode, sp.hist_top, sp.hist_nbins = p.hist_mode, p.hist_top, p.hist_nbins
+        sp.edges = self.bm.edges.data_ptr() if p.hist_mode else None
+        sp.frange = self._frange.data_ptr() if p.hist_mode else None
         return ctypes.addressof(sp)
 
     def _cat_level(self, max_nodes: int) -> None:
@@ -509,13 +524,13 @@ class HipTreeBuilder:
             # slot budget alone decides that - rank-independent - while feature
             # groups / grids follow each rank's row count) and its rows fit the
             # symmetric buffer
-            fuse_p2p = (p2p is not None and self.FUSE_RS
+            fuse_p2p = (p2p is not None
                         and max_slots * nbt * 8 <= self.LDS_BUDGET
                         and max_slots * F * 2 * nbt * 8 <= p2p.cap)
             # each pass's slab reduction runs the split scan of its slots right away
             # (reduce_split; N ranks: reduce_split_p2p); otherwise the level's
             # histograms are reduced, all-reduced and scanned in separate launches
-            rs = (comm is None or fuse_p2p) and self.FUSE_RS
+            rs = comm is None or fuse_p2p
             fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
 
             def reduce(n_groups, wgpg, fg, slot_lo, slot_cnt):
@@ -672,7 +687,6 @@ class HipTreeBuilder:
     # chained graph steps: boost_update also writes the next tree's 16-bit packed
     # level-0 rows, so level 0 reads 4 bytes per row and feature group instead of
     # (g, s2) = 8 bytes (4 groups at level 0: ~220 MB less traffic at 11M rows)
-    PK_IN_BOOST = os.environ.get("H2OMX_PK_IN_BOOST", "1") == "1"
     pk_in_boost = False
     # chained graph steps of unweighted rows: boost_update stores no (g, h); the
     # final partition re-derives them from (margins, labels, GradParams, byte labels)
@@ -680,7 +694,7 @@ class HipTreeBuilder:
     leaf16_buf = None   # int16 leaf ids of the last chained tree (boost_update reads them)
 
     def can_pack_in_boost(self) -> bool:
-        return (self.PK_IN_BOOST and self.pk32 and self.implicit_root and not self.segmented
+        return (self.pk32 and self.implicit_root and not self.segmented
                 and self.L0_COPIES in (1, 4, 8))
 
     def begin(self, smax: torch.Tensor, tree_index: int) -> None:
@@ -694,7 +708,6 @@ class HipTreeBuilder:
                   "tree_begin")
 
     # data-parallel direct levels: histogram chunk all-reduced per call (bytes)
-    DIRECT_DP = os.environ.get("H2OMX_DIRECT_DP", "1") == "1"
     DIRECT_DP_CHUNK_BYTES = int(os.environ.get("H2OMX_DIRECT_DP_CHUNK_MB", "64")) << 20
 
     def _direct_dp(self, comm, idx_in, gs, seg_start, seg_cnt, ctl_cur, tree_fmask, spp, max_nodes, nsplit, st):
@@ -804,9 +817,9 @@ class HipTreeBuilder:
                 idx_out = self.idx[d % 2]
             gout = sout = None
             # last level: leaf sums read (g, s2) in segment order where the previous
-            # scatter left them (SEG_LEAF_GS=0: gather every row's g / h / w by row id)
+            # scatter left them
             segf = 0
-            if last and pwave and gs["pos"] == 1 and self.SEG_LEAF_GS:
+            if last and pwave and gs["pos"] == 1:
                 segf = 2 | (4 if p.mode != 0 else 0)
             if not last and self.PERMUTE_GS:
                 gout = B(f"gperm{d % 2}", n + 64, torch.float32)
@@ -831,8 +844,7 @@ class HipTreeBuilder:
         # (N ranks: the direct histograms of a node chunk are all-reduced between
         # the build and the scan, h2omx_direct_dp)
         direct_ok = (self.DIRECT_MIN_NODES > 0 and F <= 1024
-                     and exp_elig <= self.DIRECT_MAX_ELIG and self.catf is None
-                     and (comm is None or self.DIRECT_DP))
+                     and exp_elig <= self.DIRECT_MAX_ELIG and self.catf is None)
         for d in range(max_depth):
             cur, nxt = d % 2, (d + 1) % 2
             ctl_cur, ctl_nxt = self.ctl[cur], self.ctl[nxt]

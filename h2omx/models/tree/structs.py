@@ -25,6 +25,8 @@ class SplitParams(ctypes.Structure):
         ("pad2", ctypes.c_int), ("mono", ctypes.c_void_p), ("gbound", ctypes.c_void_p),
         ("ifsets", ctypes.c_void_p), ("istate", ctypes.c_void_p),
         ("catf", ctypes.c_void_p), ("fbcat", ctypes.c_void_p), ("treecat", ctypes.c_void_p),
+        ("edges", ctypes.c_void_p), ("frange", ctypes.c_void_p), ("hist_mode", ctypes.c_int),
+        ("hist_top", ctypes.c_int), ("hist_nbins", ctypes.c_int), ("pad3", ctypes.c_int),
     ]
 
 

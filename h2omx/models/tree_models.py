@@ -17,7 +17,7 @@ import torch
 from ..frame.frame import ENUM, Frame, Vec
 from .base import Model, ModelBuilder, ModelCategory
 from .tree import TreeParams, bin_matrix, compute_edges, train_ensemble
-from .tree.binning import categorical_bins, resolve_histogram_type
+from .tree.binning import PER_NODE_MODES, adaptive_ranges, categorical_bins, resolve_histogram_type
 from .tree.boost import concat_catbits, concat_trees
 
 
@@ -110,6 +110,20 @@ class _TreeBuilder(ModelBuilder):
     model_cls = TreeModel
     mode = 0
     default_nbins = 255
+    # histogram_type AUTO and the per-node rules (H2O GBM / DRF: AUTO =
+    # UniformAdaptive re-binned per node; XGBoost 'hist' bins globally)
+    auto_histogram = "quantilesglobal"
+    per_node_histograms = False
+
+    def _warn(self, msg: str, loud: bool = True) -> None:
+        """A deviation from H2O's semantics, surfaced in the model output
+        (``output.warnings``, H2O's model warnings) and, for a value the user
+        set, as a Python warning."""
+        import warnings
+
+        self._warnings.append(msg)
+        if loud:
+            warnings.warn(f"h2omx {self.algo}: {msg}", stacklevel=3)
 
     def _dist(self) -> str:
         d = str(self.params.get("distribution", "AUTO")).lower()
@@ -205,12 +219,30 @@ class _TreeBuilder(ModelBuilder):
                                                                      ModelCategory.MULTINOMIAL):
             w, balance = _balance_weights(y, w, len(self.response_domain), self.params, self.comm)
         nbins = int(self.params.get("nbins") or self.params.get("max_bins") or self.default_nbins)
-        htype = resolve_histogram_type(self.params.get("histogram_type"))
-        if htype in ("uniformadaptive", "random") and self.params.get("nbins_top_level"):
-            # root resolution of H2O's adaptive grid (per-node re-binning: see binning.py)
-            nbins = max(nbins, int(self.params["nbins_top_level"]))
-        edges, nvb, nbt = compute_edges(X, min(nbins, 255), seed=self._seed(), comm=self.comm,
-                                        histogram_type=htype)
+        htype = resolve_histogram_type(self.params.get("histogram_type"), auto=self.auto_histogram)
+        top = int(self.params.get("nbins_top_level") or 1024)
+        per_node = self.per_node_histograms and htype in PER_NODE_MODES
+        self._warnings = []
+        if per_node:
+            # H2O's per-node rules on fine quantile bins (root resolution
+            # nbins_top_level, at most 255: uint8 codes); every node then keeps the
+            # fine edges nearest its own equal-width / random cuts (binning.py)
+            fine = min(255, max(nbins, top))
+            edges, nvb, nbt = compute_edges(X, fine, seed=self._seed(), comm=self.comm,
+                                            histogram_type="QuantilesGlobal")
+            if max(nbins, top) > 255:
+                # (H2O's defaults hit this: recorded in the model, not raised as a Python warning)
+                self._warn(f"histogram_type {self.params.get('histogram_type') or 'AUTO'}: node cut points snap to "
+                           f"255 fine quantile bins per column (nbins_top_level={top} finer than the uint8 codes)",
+                           loud=max(nbins, top) != 1024)
+        else:
+            if htype in PER_NODE_MODES or htype == "uniformrobust":
+                self._warn(f"histogram_type {self.params.get('histogram_type')}: {self.algo} bins every column "
+                           "with one global grid (no per-node re-binning)")
+            if nbins > 256:      # (XGBoost's max_bins=256 default: 255 value bins + the NA bin)
+                self._warn(f"nbins={nbins} capped at 255 bins per column (uint8 codes)")
+            edges, nvb, nbt = compute_edges(X, min(nbins, 255), seed=self._seed(), comm=self.comm,
+                                            histogram_type=htype)
         cat = None
         if self._group_splits(enc):
             # H2O's default for enum predictors (categorical_encoding AUTO / Enum):
@@ -220,6 +252,9 @@ class _TreeBuilder(ModelBuilder):
             edges, nvb, nbt, cat = categorical_bins(edges, nvb, nbt, levels)
         bm = bin_matrix(X, edges, nvb, nbt, names=self.x, cat=cat)
         tp = self._tree_params(len(self.x))
+        if per_node:
+            tp.hist_mode, tp.hist_top, tp.hist_nbins = PER_NODE_MODES[htype], top, nbins
+            bm.frange = adaptive_ranges(X, bm, self.comm)
         nclass = len(self.response_domain) if self.response_domain else 1
         ens_dist = self._engine_dist(dist)
         init_f = None
@@ -258,6 +293,7 @@ class _TreeBuilder(ModelBuilder):
             ens.trees = concat_trees(ckpt.trees, ens.trees) if len(ens.trees) else ckpt.trees
             ens.init_f = ckpt.init_f
         model = self.model_cls(self, model_id, ens, ens_dist)
+        model.warnings = list(self._warnings)
         model.class_dist = balance      # (prior, modelled) class fractions for correctProbabilities
         model.calibration = None
         if self.params.get("calibrate_model"):
@@ -599,7 +635,10 @@ class H2OGradientBoostingEstimator(_TreeBuilder):
     """H2O GBM: squared-error splits on pseudo-residuals, Newton leaf steps."""
     algo = "gbm"
     model_cls = GBMModel
-    DEFAULTS = dict(ntrees=50, max_depth=5, min_rows=10.0, nbins=255, nbins_top_level=1024, nbins_cats=1024,
+    auto_histogram = "uniformadaptive"
+    per_node_histograms = True
+    default_nbins = 20
+    DEFAULTS = dict(ntrees=50, max_depth=5, min_rows=10.0, nbins=20, nbins_top_level=1024, nbins_cats=1024,
                     learn_rate=0.1, learn_rate_annealing=1.0, sample_rate=1.0, col_sample_rate=1.0,
                     col_sample_rate_per_tree=1.0, min_split_improvement=1e-5, histogram_type="AUTO",
                     max_abs_leafnode_pred=0.0, tweedie_power=1.5, quantile_alpha=0.5, huber_alpha=0.9,
@@ -682,6 +721,8 @@ class H2ORandomForestEstimator(_TreeBuilder):
     classification), predictions averaged over trees."""
     algo = "drf"
     model_cls = DRFModel
+    auto_histogram = "uniformadaptive"
+    per_node_histograms = True
     default_nbins = 20
     DEFAULTS = dict(ntrees=50, max_depth=20, min_rows=1.0, nbins=20, nbins_top_level=1024, nbins_cats=1024,
                     mtries=-1, sample_rate=0.632, col_sample_rate_per_tree=1.0, min_split_improvement=1e-5,

@@ -68,7 +68,6 @@ DENSE_SIGS = {
     "h2omx_slab_reduce_upper": "PIIPS",
     "h2omx_glm_irls_wave": "PLLPPPPPPILPPS",
     "h2omx_glm_irls_split": "PLLPPPPPPILPPS",
-    "h2omx_glm_split_set_prefetch": "I",
     "h2omx_slab_reduce16_dev": "PIIPPS",
     "h2omx_adadelta_fix": "PPPPLFFFPS",
     "h2omx_out_wgrad_partial": "PPPIIIIS",

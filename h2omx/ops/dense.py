@@ -17,30 +17,31 @@ import os
 import numpy as np
 import torch
 
+from .. import _native
 from . import P, check, dense_lib, stream
 
 KBADARG = 1  # common.h kBadArg
 # workgroups of the fused GLM Gram / K-Means kernels (sweeps: H2OMX_GLM_WGS, H2OMX_KM_WGS)
 GLM_WGS = int(os.environ.get("H2OMX_GLM_WGS", "512"))
-# wave-unit IRLS kernel (p + 2 <= 128, not multinomial): H2OMX_GLM_WAVE=0 -> workgroup kernel;
-# units = independent waves, each over a contiguous row range (fp32 within a unit, fp64 across)
-GLM_WAVE = os.environ.get("H2OMX_GLM_WAVE", "1") != "0"
+# wave-unit IRLS kernel for p + 2 <= 128 (not multinomial; False: the workgroup
+# kernel, which serves wider / multinomial designs); units = independent waves,
+# each over a contiguous row range (fp32 within a unit, fp64 across).  Module
+# flags, not environment knobs: tests pin each kernel family with them
+GLM_WAVE = True
+# Gram of the wave path: "split" = exact 3-way bf16 split on the bf16 matrix
+# cores (glm_irls_split_kernel); "f32" = fp32 MFMA (glm_irls_wave_kernel, the
+# intercept-only pass and the split kernel's test oracle)
+GLM_GRAM = "split"
 GLM_UNITS = int(os.environ.get("H2OMX_GLM_UNITS", "2048"))
 GLM_UNIT_MIN_ROWS = 512
-# Gram of the wave path: "split" = exact 3-way bf16 split on the bf16 matrix
-# cores (glm_irls_split_kernel), "f32" = fp32 MFMA (glm_irls_wave_kernel)
-GLM_GRAM = os.environ.get("H2OMX_GLM_GRAM", "split")
-# the split kernel stages aligned designs through LDS by LDS-DMA (0: register prefetch)
-GLM_PD = int(os.environ.get("H2OMX_GLM_GLDS", "1"))   # LDS-DMA staging on/off (A/B)
-_GLM_PD_SET = [None]
 SLAB_SPLIT = 32          # dense_kernels.hip slab_reduce16_kernel
 KM_WGS = int(os.environ.get("H2OMX_KM_WGS", "1024"))
-# K-Means Lloyd pass on the wave-unit kernel (k <= 32, d <= 128 / 64); 0: the
-# workgroup-tile kernel.  KM_WAVE_CUS: CUs the wave kernel's grid is sized for
-KM_WAVE = os.environ.get("H2OMX_KM_WAVE", "1") == "1"
-KM_WAVE_CUS = int(os.environ.get("H2OMX_KM_WAVE_CUS", "256"))
-# K-Means cluster sums on the fp32 matrix cores (kmeans_mfma_kernel): d + 2 <= 128, k <= 32
-KM_MFMA = os.environ.get("H2OMX_KM_MFMA", "1") == "1"
+# K-Means Lloyd pass: cluster sums on the fp32 matrix cores (kmeans_mfma_kernel,
+# d + 2 <= 128 / 64, k <= 32), else the wave-unit kernel (k <= 32, d <= 128 / 64),
+# else the workgroup-tile kernel; the wave kernel's grid is sized for 256 CUs
+KM_MFMA = True
+KM_WAVE = True
+KM_WAVE_CUS = 256
 KM_MFMA_WGS = int(os.environ.get("H2OMX_KM_MFMA_WGS", "512"))
 
 FAMILIES = {"gaussian": 0, "binomial": 1, "poisson": 2, "gamma": 3, "tweedie": 4, "multinomial": 5,
@@ -179,8 +180,9 @@ def glm_grad_pass(X: torch.Tensor, y: torch.Tensor, wprior, offset, beta: np.nda
 
 
 def _glm_irls_wave(X, y, wprior, offset, beta, family, link, cls, var_power, link_power):
-    """glm_irls_split_kernel (GLM_GRAM "split": exact three-way bf16 split,
-    6 bf16 MFMAs per 16x16 tile) or glm_irls_wave_kernel ("f32": 16x16x4 fp32
+    """glm_irls_split_kernel (GLM_GRAM "split": exact three-way bf16 split, 6
+    bf16 MFMAs per 16x16 tile, designs staged through LDS by LDS-DMA) or
+    glm_irls_wave_kernel ("f32", and the intercept-only p = 0 pass: 16x16x4 fp32
     MFMA): independent wave units over contiguous row ranges, register-resident
     32-row chunks, then the fp64 sum of the per-unit upper tiles.  X has no NA
     (the GLM imputes column means before the pass)."""
@@ -202,9 +204,6 @@ def _glm_irls_wave(X, y, wprior, offset, beta, family, link, cls, var_power, lin
     gp = GlmParams(FAMILIES[family], LINKS[link], p, K, cls, 0, var_power, link_power)
     Xc = X if X.stride(1) == 1 else X.contiguous()
     st = stream(dev)
-    if _GLM_PD_SET[0] != GLM_PD:
-        check(lib.h2omx_glm_split_set_prefetch(GLM_PD), "glm_split_set_prefetch")
-        _GLM_PD_SET[0] = GLM_PD
     fn = lib.h2omx_glm_irls_split if split else lib.h2omx_glm_irls_wave
     check(fn(P(Xc), Xc.stride(0), n, P(y), P(wprior), P(offset), P(means), P(b32),
              ctypes.addressof(gp), units, rows, P(slab), P(devs), st), "glm_irls_wave")
@@ -445,26 +444,27 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
             check(dense_lib().h2omx_gemm_thin_k(P(A), P(B), P(C), M, N, K, None, 0, stream(A.device)),
                   "gemm_thin_k")
             return C
-    if _lib_small_ok(M, N, K, act, beta_c, bias):
-        # small mini-batch GEMMs on hipBLASLt: no split-K reduce launch
-        Am = A.t() if ta else A
-        Bm = B.t() if tb else B
-        if act == 1:
-            r = torch._addmm_activation(bias, Am, Bm, use_gelu=False)
-            if out is None:
-                return r
-            C.copy_(r)
-            return C
-        if bias is not None:
-            return torch.addmm(bias, Am, Bm, out=C)
-        return torch.mm(Am, Bm, out=C)
-    if out is None and _lib_gemm_ok(M, N, K, ta, tb, act, beta_c, bias):
-        # plain fp32 GEMM (+ bias / ReLU epilogue): the vendor library's tuned
-        # kernel (hipBLASLt) - the fused kernels below stay ours
-        Bm = B.t() if tb else B
-        if act == 1:
-            return torch._addmm_activation(bias, A, Bm, use_gelu=False)
-        return torch.addmm(bias, A, Bm) if bias is not None else torch.mm(A, Bm)
+    if X3_GEMM and not ta and tb and beta_c == 0.0 and M * N * K >= X3_MIN_MNK and _x3_ok(A, B, C):
+        # large forward layers: the x3 bf16-split kernel on the bf16 matrix cores
+        # (fp32-equivalent accuracy; 8192 x 512 x 512 + ReLU 40.1 us vs 56.6 us for
+        # gemm_w64 and 41.0 us for hipBLASLt, profiles/r5/dl/gemm_x3_r5o.jsonl)
+        from .mlp import gemm_x3
+
+        return gemm_x3(A, B, bias, act, out=C)
+    return gemm_fp32(A, B, bias, act, ta, tb, C, beta_c)
+
+
+def gemm_fp32(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = False, tb: bool = False,
+              out: torch.Tensor | None = None, beta_c: float = 0.0) -> torch.Tensor:
+    """:func:`gemm` on the fp32 MFMA kernels (gemm_w64 / split-K) - every layout."""
+    M = A.shape[1] if ta else A.shape[0]
+    K = A.shape[0] if ta else A.shape[1]
+    N = B.shape[0] if tb else B.shape[1]
+    A = A.float().contiguous()
+    B = B.float().contiguous()
+    if bias is not None:
+        bias = bias.float().contiguous()
+    C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=A.device)
     S = _splitk(M, N, K)
     ws = _workspace(A.device, S * M * N) if S > 1 else None
     check(dense_lib().h2omx_gemm(P(A), P(B), P(C), P(bias), M, N, K, int(ta), int(tb), act, beta_c, S, P(ws),
@@ -472,26 +472,16 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: bool = F
     return C
 
 
-# fp32 forward GEMMs (act none / ReLU with bias) on hipBLASLt: 8192 x 512 x 512
-# ran 40 us there vs 51.5 us for gemm_w64_kernel (profiles/r3/dl/gemm_variants_r3s8.jsonl)
-LIB_GEMM = os.environ.get("H2OMX_GEMM_LIB", "1")
-LIB_GEMM_MIN_MNK = 1 << 27
+# NT GEMMs of at least this many multiply-adds go to the x3 kernel (below it a
+# 256-row mini-batch layer runs 13.8 us on gemm_w64 vs 34.4 us on x3: too few tiles)
+X3_GEMM = True
+X3_MIN_MNK = 1 << 27
 
 
-# small mini-batch GEMMs (M N K < LIB_GEMM_MIN_MNK, e.g. the estimator's 256-row
-# batches) on hipBLASLt instead of split-K + reduce launches: estimator-default
-# DL 1.22 -> 1.50 M samples/s (profiles/r4/dl/estimator_small_gemm_ab.txt)
-LIB_GEMM_SMALL = os.environ.get("H2OMX_GEMM_LIB_SMALL", "1")
-
-
-def _lib_small_ok(M, N, K, act, beta_c, bias) -> bool:
-    return (LIB_GEMM_SMALL == "1" and beta_c == 0.0 and act in (0, 1) and (act == 0 or bias is not None)
-            and M * N * K < LIB_GEMM_MIN_MNK and min(M, N, K) >= 64)
-
-
-def _lib_gemm_ok(M, N, K, ta, tb, act, beta_c, bias) -> bool:
-    return (LIB_GEMM == "1" and not ta and beta_c == 0.0 and act in (0, 1) and (act == 0 or bias is not None)
-            and M * N * K >= LIB_GEMM_MIN_MNK and N >= 64 and K >= 64)
+def _x3_ok(A, B, C) -> bool:
+    K = A.shape[1]
+    return (K % 4 == 0 and A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0 and C.is_contiguous()
+            and _native.available("mlp"))
 
 
 def set_gemm_tile(tile: int) -> None:
@@ -617,6 +607,14 @@ def gemm_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int, out:
     C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=dZ.device)
     splits = -(-M // 128)
     ws = _workspace(dZ.device, splits * N, slot=1)
+    if X3_GEMM and M * N * K >= X3_MIN_MNK and K % 4 == 0 and dZ.data_ptr() % 16 == 0 and C.is_contiguous() \
+            and _native.available("mlp"):
+        # the x3 kernel with a K-major weight operand and the same epilogue
+        # (8192 x 512 x 512: see profiles/r5/dl)
+        from .mlp import gemm_x3_dact
+
+        gemm_x3_dact(dZ, W, Y, int(act), C, ws)
+        return C, (ws, splits)
     sp = ctypes.c_int(0)
     check(dense_lib().h2omx_gemm_dact(P(dZ), P(W), P(C), P(Y), P(ws), M, N, K, int(act), int(tile),
                                       ctypes.addressof(sp), stream(dZ.device)), "gemm_dact")
@@ -667,7 +665,7 @@ def wgrad_bias(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Te
     N = H.shape[1]
     S = _splitk(M, N, K)
     bws, bsplits = bpart
-    if S < 2 or _lib_small_ok(M, N, K, 0, 0.0, None):
+    if S < 2:
         gemm(dZ, H, ta=True, out=dW)
         if (_GRAD_FOLDS[0] is not None and len(_GRAD_FOLDS[0]) < 8 and db.dtype == torch.float32
                 and db.is_contiguous()):

@@ -39,7 +39,10 @@ def lib():
                          ("h2omx_mlp_out", [ctypes.c_void_p, ctypes.c_void_p]),
                          ("h2omx_gemm_x3", [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
-                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])):
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+                         ("h2omx_gemm_x3_dact", [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])):
             f = getattr(L, fn)
             f.argtypes = args
             f.restype = ctypes.c_int
@@ -111,7 +114,6 @@ _TILE = os.environ.get("H2OMX_MLP_TILE", "")
 DEPTH = int(os.environ.get("H2OMX_MLP_DEPTH", "4"))
 # activation rows padded off the 2 KB L2-channel period (A/B knob: no measured
 # difference either way on MI355X, profiles/r5/dl/fused_step_ab_r5f.jsonl)
-PAD = os.environ.get("H2OMX_MLP_PAD", "1") == "1"
 
 
 def padded_ld(n: int) -> int:
@@ -119,7 +121,7 @@ def padded_ld(n: int) -> int:
     loads) that is not a multiple of 256 floats (rows 1 KB apart or any
     multiple of it share L2 channels)."""
     ld = -(-n // 4) * 4
-    if PAD and ld % 256 == 0:
+    if ld % 256 == 0:
         ld += 32
     return ld
 
@@ -338,3 +340,15 @@ def gemm_x3(A: torch.Tensor, B: torch.Tensor, bias: torch.Tensor | None = None, 
                                       0 if bias is None else bias.data_ptr(), M, N, K, act,
                                       _native.stream_of(A.device)), "gemm_x3")
     return C
+
+
+def gemm_x3_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int, C: torch.Tensor,
+                 bws: torch.Tensor) -> None:
+    """C = (dZ [M][K] W [K][N]) * act'(Y [M][N]) on the x3 kernel (W K-major) and
+    bws [cdiv(M, 128)][N] = per-128-row-block column sums of C
+    (``ops.dense.gemm_dact``'s contract)."""
+    M, K = dZ.shape
+    N = W.shape[1]
+    _native.check(lib().h2omx_gemm_x3_dact(dZ.data_ptr(), dZ.stride(0), W.data_ptr(), W.stride(0), C.data_ptr(),
+                                           Y.data_ptr(), bws.data_ptr(), M, N, K, act, _native.stream_of(dZ.device)),
+                  "gemm_x3_dact")

@@ -78,6 +78,70 @@ def feature_allowed(p: TreeParams, F: int, tree_index: int, depth: int, node: in
     return allowed
 
 
+def _ua_count(x: float, lo: float, span: float, nb: int) -> int:
+    """Uniform cuts lo + span k / nb (k = 1 .. nb - 1) at or below x (mirror of ua_count)."""
+    if x == -np.inf:
+        return 0
+    if x == np.inf:
+        return nb - 1
+    r = (x - lo) * float(nb) / span
+    k = 0 if r < 0.0 else (nb - 1 if r >= float(nb - 1) else int(r))
+    while k < nb - 1 and lo + (span * float(k + 1)) / float(nb) <= x:
+        k += 1
+    while k > 0 and lo + (span * float(k)) / float(nb) > x:
+        k -= 1
+    return k
+
+
+def adaptive_mask(p: TreeParams, edges_f: np.ndarray, frange_f: np.ndarray, S: np.ndarray, m: int, nbt: int,
+                  node: int, f: int, depth: int, tree_index: int) -> np.ndarray | None:
+    """Candidate thresholds of (node, f) under the per-node histogram rule
+    (mirror of adaptive_candidates in csrc/tree_kernels.hip): bool over the
+    scanned thresholds t < min(m, nbt - 1), or None when every one is kept.
+    ``S``: the node's per-bin weight (mode 0) / hessian (mode 1) sums."""
+    mode = p.hist_mode
+    if mode == 3:
+        mode = (1, 1, 2, 0)[tree_index & 3]      # UniformAdaptive, UniformAdaptive, Random, QuantilesGlobal
+    if mode == 0:
+        return None
+    T = min(m, nbt - 1)
+    ne = np.nonzero(S[:T] > 0)[0]
+    if ne.size == 0 or ne[-1] - ne[0] < 1:
+        return None
+    lo, hi = int(ne[0]), int(ne[-1])
+    e = edges_f
+    fmin, fmax, exact, isint = (float(v) for v in frange_f)
+    if exact:
+        lo_v = float(e[lo]) if lo < m - 1 else fmax
+        hi_v = float(e[hi]) if hi < m - 1 else fmax
+    else:
+        lo_v = fmin if lo == 0 else float(e[lo - 1])
+        hi_v = fmax if hi == m - 1 else float(e[hi])
+    span = hi_v - lo_v
+    if not (span > 0.0) or not (span < np.inf):
+        return None
+    top = (int(p.hist_top) >> depth) if depth < 31 else 0
+    nb = max(top, int(p.hist_nbins), 2)
+    if isint and span + 1.0 <= float(nb):
+        return None
+    keep = np.ones(T, bool)
+    ts = np.arange(lo, hi)
+    x = e[ts].astype(np.float64)
+    mL = np.full(ts.size, -np.inf)
+    mR = np.full(ts.size, np.inf)
+    mL[1:] = 0.5 * (e[ts[1:] - 1].astype(np.float64) + x[1:])
+    mR[:-1] = 0.5 * (x[:-1] + e[ts[:-1] + 1].astype(np.float64))
+    if mode == 1:
+        hit = np.array([_ua_count(b, lo_v, span, nb) > _ua_count(a, lo_v, span, nb) for a, b in zip(mL, mR)])
+    else:
+        key = (((tree_index * 131 + depth) & 0xFFFFFFFF) ^ ((f * 0x9E3779B1) & 0xFFFFFFFF))
+        s2 = (p.seed & 0xFFFFFFFF) ^ 0x52414E44
+        c = lo_v + span * u01(hash4(s2, key, node, np.arange(1, nb)))
+        hit = ((mL[:, None] < c[None, :]) & (c[None, :] <= mR[:, None])).any(axis=1)
+    keep[lo:hi] = hit
+    return keep
+
+
 class RefTreeBuilder:
     def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
         self.bm = bm
@@ -92,6 +156,11 @@ class RefTreeBuilder:
         # categorical group splits (mirror of feat_best_cat_wave / part_right)
         self.cat = None if getattr(bm, "cat", None) is None or not np.any(bm.cat) else np.asarray(bm.cat, bool)
         self.catbits = None
+        self.frange = None
+        if params.hist_mode:
+            if getattr(bm, "frange", None) is None:
+                raise ValueError("TreeParams.hist_mode needs BinnedMatrix.frange (binning.adaptive_ranges)")
+            self.frange = np.asarray(bm.frange.cpu().numpy(), np.float32)
 
     def _hist(self, rows_node, g, h, w, n_nodes):
         """Full histograms [n_nodes][F][3][nbt] (float64) of active rows."""
@@ -209,6 +278,12 @@ class RefTreeBuilder:
                         gB = split_gain(cs[0] + na[0], cs[1] + na[1], cs[2] + na[2], tg, th, tw, p)
                     else:
                         gB = np.full_like(gA, -np.inf)
+                    if self.frange is not None and not is_cat:
+                        keep = adaptive_mask(p, self.edges[f], self.frange[f], hv[2] if p.mode == 0 else hv[1],
+                                             m, nbt, i, f, d, tree_index)
+                        if keep is not None:
+                            gA = np.where(keep, gA, -np.inf)
+                            gB = np.where(keep, gB, -np.inf)
                     if mono is not None and mono[f] != 0:
                         si, ts = (2, tw) if p.mode == 0 else (1, th)
                         gA = np.where(mono_mask(mono[f], cs[0], cs[si], tg, ts), gA, -np.inf)

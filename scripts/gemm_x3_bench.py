@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """fp32 GEMM C = A B^T (+ bias, ReLU) on MI355X: hipBLASLt (torch.addmm) vs the
-own fp32 MFMA kernel (gemm_w64, ops.dense.gemm with the library off) vs the
-x3 bf16-split kernel (ops.mlp.gemm_x3).  Accuracy vs float64; one JSON line
+own fp32 MFMA kernel (gemm_w64, ops.dense.gemm_fp32) vs the x3 bf16-split
+kernel (ops.mlp.gemm_x3) and what ops.dense.gemm routes the shape to.  Accuracy vs float64; one JSON line
 per shape."""
 import json
 import os
@@ -11,8 +11,6 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["H2OMX_GEMM_LIB"] = "0"
-os.environ["H2OMX_GEMM_LIB_SMALL"] = "0"
 from h2omx.ops import dense as OD  # noqa: E402
 from h2omx.ops.mlp import gemm_x3  # noqa: E402
 
@@ -40,8 +38,8 @@ for M, N, K in ((8192, 512, 512), (8192, 512, 200), (8192, 2048, 2048), (256, 51
     ref = torch.relu(A.double() @ B.double().T + b.double())
     out = {"M": M, "N": N, "K": K}
     for name, fn in (("hipblaslt", lambda: torch._addmm_activation(b, A, B.T)),
-                     ("own_fp32_mfma", lambda: OD.gemm(A, B, bias=b, act=1, tb=True)),
-                     ("x3", lambda: gemm_x3(A, B, b, 1))):
+                     ("own_fp32_mfma", lambda: OD.gemm_fp32(A, B, bias=b, act=1, tb=True)),
+                     ("x3", lambda: gemm_x3(A, B, b, 1)), ("routed", lambda: OD.gemm(A, B, bias=b, act=1, tb=True))):
         C = fn()
         err = ((C.double() - ref).abs().max() / ref.abs().max()).item()
         us = timeit(fn)

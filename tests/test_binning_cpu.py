@@ -29,7 +29,9 @@ def test_sort_rows_matches_torch_sort():
 
 def test_histogram_types():
     """histogram_type: quantile vs equal-width vs robust vs random cut points;
-    few-valued columns keep one bin per value; RoundRobin / unknown rejected."""
+    few-valued columns keep one bin per value; unknown rejected.  (The per-node
+    rules UniformAdaptive / Random / RoundRobin of GBM / DRF are in
+    test_hist_adaptive.py; these are the global grids.)"""
     import numpy as np
     import pytest
     import torch
@@ -52,7 +54,7 @@ def test_histogram_types():
     assert np.allclose(d, d[0], rtol=1e-3)                                  # equal width
     assert eu[1, 0] < er[1, 0] and er[1, nvr[1] - 2] < eu[1, nvu[1] - 2]     # robust range inside the full one
     assert not np.allclose(np.diff(ex[0, : nvx[0] - 1]), d[0], rtol=1e-2)   # random spacing
-    with pytest.raises(ValueError, match="RoundRobin"):
-        compute_edges(X, 32, histogram_type="RoundRobin")
+    er2, _, _ = compute_edges(X, 32, histogram_type="RoundRobin")      # global grid: the quantile one
+    np.testing.assert_array_equal(er2, eq)
     with pytest.raises(ValueError, match="unknown histogram_type"):
         compute_edges(X, 32, histogram_type="Sturges")

@@ -9,29 +9,71 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _own_gemm_kernels(monkeypatch):
-    """These tests pin the hand-written GEMM kernels: no hipBLASLt routing."""
+def _fp32_gemm_kernels(monkeypatch):
+    """These tests pin the fp32 MFMA GEMM kernels (large NT GEMMs otherwise go
+    to the x3 kernel, pinned by test_x3_gemm_matches_fp64)."""
     from h2omx.ops import dense as OD
 
-    monkeypatch.setattr(OD, "LIB_GEMM", "0")
-    monkeypatch.setattr(OD, "LIB_GEMM_SMALL", "0")
+    monkeypatch.setattr(OD, "X3_GEMM", False)
 
 
-def test_library_gemm_route_matches_own_kernel(cuda_dev, monkeypatch):
-    """Plain fp32 forward GEMMs (bias + ReLU) routed to hipBLASLt agree with
-    gemm_w64_kernel to fp32 rounding."""
+@pytest.mark.parametrize("M,N,K,act,bias", [(8192, 512, 512, 1, True), (8192, 512, 200, 1, True),
+                                            (4097, 300, 516, 2, True), (1000, 130, 64, 0, False),
+                                            (50, 2048, 1024, 1, True)])
+def test_x3_gemm_matches_fp64(cuda_dev, monkeypatch, M, N, K, act, bias):
+    """The x3 bf16-split GEMM (exact 3-piece operand split, six products,
+    fp32 accumulation) has fp32 accuracy against float64; ops.dense.gemm
+    routes large NT GEMMs to it."""
+    from h2omx.ops import dense as OD
+    from h2omx.ops.mlp import gemm_x3
+
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn((M, K), generator=g).cuda()
+    W = torch.randn((N, K), generator=g).cuda() * 0.05
+    b = torch.randn((N,), generator=g).cuda() if bias else None
+    Z = A.double() @ W.double().t() + (b.double() if bias else 0.0)
+    ref = torch.relu(Z) if act == 1 else (torch.tanh(Z) if act == 2 else Z)
+    got = gemm_x3(A, W, b, act)
+    # fp32-equivalent: no worse than twice the fp32 MFMA kernel's error (and
+    # within a few fp32 roundings of the pre-activation magnitude)
+    f32 = OD.gemm_fp32(A, W, b, act, tb=True)
+    err32 = (f32.double() - ref).abs().max().item()
+    tol = max(2.0 * err32, 2e-6 * Z.abs().max().item())
+    assert (got.double() - ref).abs().max().item() <= tol
+    monkeypatch.setattr(OD, "X3_GEMM", True)
+    routed = D.gemm(A, W, b, act, False, True)
+    assert (routed.double() - ref).abs().max().item() <= tol
+    if M * N * K >= OD.X3_MIN_MNK:
+        assert torch.equal(routed, got)
+
+
+@pytest.mark.parametrize("M,N,K,act", [(8192, 512, 512, 1), (4100, 260, 516, 2), (8192, 200, 512, 1)])
+def test_x3_gemm_dact_matches_fp64(cuda_dev, monkeypatch, M, N, K, act):
+    """Back-propagation through an activation on the x3 kernel (K-major weight
+    operand): dZ_prev = (dZ W) * act'(Y) and the per-128-row-block column sums
+    (bias-gradient partials) agree with float64 to fp32 accuracy and with the
+    fp32 gemm_dact kernel's contract."""
     from h2omx.ops import dense as OD
 
-    g = torch.Generator(device="cpu").manual_seed(3)
-    A = torch.randn((4096, 512), generator=g).cuda()
-    W = torch.randn((512, 512), generator=g).cuda() * 0.05
-    b = torch.randn((512,), generator=g).cuda()
-    own = D.gemm(A, W, b, 1, False, True)
-    monkeypatch.setattr(OD, "LIB_GEMM", "1")
-    lib = D.gemm(A, W, b, 1, False, True)
-    ref = torch.relu(A.double() @ W.double().t() + b.double()).float()
-    torch.testing.assert_close(lib, ref, rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(own, ref, rtol=1e-4, atol=1e-4)
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    dZ = torch.randn((M, K), generator=g).cuda()
+    W = torch.randn((K, N), generator=g).cuda() * 0.05
+    Y = torch.randn((M, N), generator=g).cuda()
+    Y = torch.relu(Y) if act == 1 else torch.tanh(Y)
+    P = dZ.double() @ W.double()
+    ref = P * ((Y > 0).double() if act == 1 else (1 - Y.double() ** 2))
+    C32, (ws32, s32) = OD.gemm_dact(dZ, W, Y, act)              # fp32 kernel (fixture: X3 off)
+    err32 = (C32.double() - ref).abs().max().item()
+    b32 = ws32[: s32 * N].view(s32, N).double().clone()
+    monkeypatch.setattr(OD, "X3_GEMM", True)
+    C, (ws, s) = OD.gemm_dact(dZ, W, Y, act)
+    assert s == s32 == -(-M // 128)
+    tol = max(2.0 * err32, 2e-6 * P.abs().max().item())
+    assert (C.double() - ref).abs().max().item() <= tol
+    bref = torch.stack([ref[i * 128:(i + 1) * 128].sum(0) for i in range(s)])
+    bx3 = ws[: s * N].view(s, N).double()
+    scale = ref.abs().max().item() * 128
+    assert (bx3 - bref).abs().max().item() <= max(2.0 * (b32 - bref).abs().max().item(), 1e-6 * scale)
 
 
 @pytest.mark.parametrize("p,family,link", [(5, "binomial", "logit"), (30, "gaussian", "identity"),

@@ -145,23 +145,6 @@ def test_deeplearning_graph_replay_matches_eager(cuda_dev, monkeypatch, act, pre
     assert out["1"].training_metrics["AUC"] == out["0"].training_metrics["AUC"]
 
 
-@pytest.mark.parametrize("act", ["Rectifier", "Maxout"])
-def test_deeplearning_side_stream_weight_grads_identical(cuda_dev, monkeypatch, act):
-    """Weight gradients on the side stream (H2OMX_DL_SIDE, graph-captured with a
-    fork / join and per-layer workspaces) give the same weights as the
-    single-stream backward, eager and graph-replayed."""
-    from h2omx.models import deeplearning as DLM
-
-    df = _binary_df(n=30000)
-    fr = Frame.from_pandas(df, device=cuda_dev)
-    kw = dict(hidden=[64, 64, 32], epochs=2, seed=5, activation=act)
-    out = {}
-    for side in (False, True):
-        monkeypatch.setattr(DLM._DLTrainer, "DL_SIDE", side)
-        out[side] = H2ODeepLearningEstimator(**kw).train(y="y", training_frame=fr)
-    assert torch.equal(out[False].net.flat, out[True].net.flat)
-
-
 def test_deeplearning_folds_in_adadelta_match_separate_reduces(cuda_dev, monkeypatch):
     """Bias-gradient slices and the output layer's split partials folded inside
     the ADADELTA kernel (H2OMX_DL_FOLD) train the same model as the separate
