@@ -483,32 +483,15 @@ struct X3Regs {
   float4 a[4], b[4];
 };
 
-// one 32-k stage of both operands into registers.  A: [M][K] rows (K
-// contiguous, float4 runs).  B: [N][K] rows like A, or (kBT) K-major [K][N]
-// (the NN data gradient's weight operand): each thread then gathers one
-// column's 16 consecutive k with scalar loads (coalesced across lanes along
-// N), so the LDS image is the same [n][k] plane either way
-template <bool kBT>
 __device__ __forceinline__ void x3_load(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb,
                                         int M, int N, int K, int m0, int n0, int k0, X3Regs& r) {
   const int t = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int f = q * 256 + t, row = f >> 3, k = k0 + (f & 7) * 4;
-    const int i = m0 + row;
+    const int i = m0 + row, j = n0 + row;
     r.a[q] = (i < M && k < K) ? *reinterpret_cast<const float4*>(A + (int64_t)i * lda + k) : make_float4(0, 0, 0, 0);
-    if (!kBT) {
-      const int j = n0 + row;
-      r.b[q] = (j < N && k < K) ? *reinterpret_cast<const float4*>(B + (int64_t)j * ldb + k) : make_float4(0, 0, 0, 0);
-    }
-  }
-  if (kBT) {
-    const int j = n0 + (t & 127), kb = k0 + (t >> 7) * 16;
-    float v[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = (j < N && kb + i < K) ? B[(int64_t)(kb + i) * ldb + j] : 0.0f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) r.b[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    r.b[q] = (j < N && k < K) ? *reinterpret_cast<const float4*>(B + (int64_t)j * ldb + k) : make_float4(0, 0, 0, 0);
   }
 }
 
@@ -517,16 +500,15 @@ __device__ __forceinline__ void x3_load(const float* __restrict__ A, int lda, co
 // grids of at most one tile per CU (8192 x 512: 40.1 vs 44.0 us); larger grids
 // keep one buffer and two workgroups per CU (8192 x 2048 x 2048: 402 vs 441 us,
 // profiles/r5/dl/gemm_x3_r5o.jsonl)
-// kBT: B is K-major [K][N] (see x3_load).  kEPI 0: C = act(acc + bias); 1
-// (back-propagation through an activation, gemm_dact's contract): C = acc *
-// act'(Y) (Y [M][ldc] = the layer's output) and bws[M / 128 block][N] = the
-// block's column sums of C (bias-gradient partials)
-template <bool kDB, bool kBT = false, int kEPI = 0>
+// (K-major operand variants for the data / weight gradients - column gathers
+// into the same LDS planes - ran slower than the fp32 MFMA kernels: dact 58.8
+// vs 56.2 us, split-K weight gradient 50.1 vs 41.4 us at 8192 x 512 x 512,
+// profiles/r5/dl/kernel_stats_r5q.txt; removed)
+template <bool kDB>
 __global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict__ A, int lda,
                                                         const float* __restrict__ B, int ldb, float* __restrict__ C,
                                                         int ldc, const float* __restrict__ bias, int M, int N, int K,
-                                                        int act, const float* __restrict__ Y = nullptr,
-                                                        float* __restrict__ bws = nullptr) {
+                                                        int act) {
   constexpr int NBUF = kDB ? 2 : 1;
   __shared__ __attribute__((aligned(16))) __bf16 La[NBUF][3 * X3_PLANE];
   __shared__ __attribute__((aligned(16))) __bf16 Lb[NBUF][3 * X3_PLANE];
@@ -549,7 +531,7 @@ __global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
   const int nst = (K + X3_BK - 1) / X3_BK;
   X3Regs r;
-  x3_load<kBT>(A, lda, B, ldb, M, N, K, m0, n0, 0, r);
+  x3_load(A, lda, B, ldb, M, N, K, m0, n0, 0, r);
   auto stage = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -562,7 +544,7 @@ __global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict
   for (int st = 0; st < nst; ++st) {
     const int buf = kDB ? (st & 1) : 0;
     if (!kDB) { stage(0); __syncthreads(); }
-    if (st + 1 < nst) x3_load<kBT>(A, lda, B, ldb, M, N, K, m0, n0, (st + 1) * X3_BK, r);
+    if (st + 1 < nst) x3_load(A, lda, B, ldb, M, N, K, m0, n0, (st + 1) * X3_BK, r);
     const __bf16* La_ = La[buf];
     const __bf16* Lb_ = Lb[buf];
 #pragma unroll
@@ -596,35 +578,6 @@ __global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict
     __syncthreads();
   }
   // epilogue: lane owns column j, registers e are rows (e & 3) + 8 (e >> 2) + 4 lh
-  if constexpr (kEPI == 1) {
-    float* red = reinterpret_cast<float*>(&La[0][0]);   // [2 row-waves][128] (the loop ended on a barrier)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int j = n0 + wn + 32 * b + li;
-      float cs = 0.0f;
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int i = m0 + wm + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * lh;
-          if (i < M && j < N) {
-            const int64_t o = (int64_t)i * ldc + j;
-            const float y = Y[o], g = acc[a][b][e];
-            const float v = act == 1 ? (y > 0.0f ? g : 0.0f) : (act == 2 ? g * (1.0f - y * y) : g);
-            C[o] = v;
-            cs += v;
-          }
-        }
-      cs += __shfl_xor(cs, 32, 64);
-      if (lh == 0) red[(w >> 1) * X3_BN + wn + 32 * b + li] = cs;
-    }
-    __syncthreads();
-    for (int c = t; c < X3_BN; c += 256) {
-      const int j = n0 + c;
-      if (j < N) bws[(int64_t)(m0 / X3_BM) * N + j] = red[c] + red[X3_BN + c];
-    }
-    return;
-  }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -657,24 +610,5 @@ H2OMX_API int h2omx_gemm_x3(const float* A, int lda, const float* B, int ldb, fl
     hipLaunchKernelGGL(gemm_x3_nt_kernel<true>, grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, N, K, act);
   else
     hipLaunchKernelGGL(gemm_x3_nt_kernel<false>, grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, N, K, act);
-  return launch_status();
-}
-
-// back-propagation through an activation on the x3 kernel (h2omx_gemm_dact's
-// contract): C[M][N] = (A[M][K] B[K][N]) * act'(Y[M][N]), B K-major (the layer's
-// weights [K][N]); bws[cdiv(M, 128)][N] = per-128-row-block column sums of C.
-// A rows 16-byte aligned (lda % 4 == 0), K % 4 == 0
-H2OMX_API int h2omx_gemm_x3_dact(const float* A, int lda, const float* B, int ldb, float* C, const float* Y, float* bws,
-                                 int M, int N, int K, int act, hipStream_t stream) {
-  if (A == nullptr || B == nullptr || C == nullptr || Y == nullptr || bws == nullptr || M < 1 || N < 1 || K < 1)
-    return kBadArg;
-  if ((lda & 3) || (K & 3) || ((uintptr_t)A & 15)) return kBadArg;
-  const dim3 grid((N + X3_BN - 1) / X3_BN, (M + X3_BM - 1) / X3_BM);
-  if ((int64_t)grid.x * grid.y <= 256)
-    hipLaunchKernelGGL((gemm_x3_nt_kernel<true, true, 1>), grid, dim3(256), 0, stream, A, lda, B, ldb, C, N, nullptr,
-                       M, N, K, act, Y, bws);
-  else
-    hipLaunchKernelGGL((gemm_x3_nt_kernel<false, true, 1>), grid, dim3(256), 0, stream, A, lda, B, ldb, C, N, nullptr,
-                       M, N, K, act, Y, bws);
   return launch_status();
 }

@@ -509,6 +509,13 @@ def out_layer_ok(dZ: torch.Tensor, H: torch.Tensor) -> bool:
     return dZ.shape[1] <= 8 and H.shape[1] % 4 == 0 and H.is_contiguous()
 
 
+def _grad_span(dW: torch.Tensor, db: torch.Tensor) -> bool:
+    """db directly follows dW inside ONE storage (a layer's [W | b] span of the
+    flat gradient), not merely at the next address of another allocation."""
+    return (db.data_ptr() == dW.data_ptr() + dW.numel() * dW.element_size()
+            and db.untyped_storage().data_ptr() == dW.untyped_storage().data_ptr())
+
+
 def out_wgrad(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Tensor) -> None:
     """dW [C][N] = dZ^T H and db = column sums of dZ for C <= 8 classes (one
     streaming pass over H, fixed-order split reduce)."""
@@ -519,7 +526,7 @@ def out_wgrad(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Ten
     T = C * N + C
     ws = _workspace(dZ.device, S * T)
     contiguous = (dW.is_contiguous() and db.is_contiguous()
-                  and db.data_ptr() == dW.data_ptr() + dW.numel() * dW.element_size())
+                  and _grad_span(dW, db))
     out = dW.view(-1) if contiguous else torch.empty((T,), dtype=torch.float32, device=dZ.device)
     if contiguous:
         # the layer's [W | b] gradient span (models/deeplearning.py _Net): write it in place
@@ -558,7 +565,7 @@ def out_backward(dZ: torch.Tensor, H: torch.Tensor, W: torch.Tensor, dW: torch.T
 def out_backward_ok(dZ: torch.Tensor, H: torch.Tensor, dW: torch.Tensor, db: torch.Tensor) -> bool:
     return (_GRAD_FOLDS[0] is not None and len(_GRAD_FOLDS[0]) < 8 and out_layer_ok(dZ, H)
             and dW.is_contiguous() and db.is_contiguous()
-            and db.data_ptr() == dW.data_ptr() + dW.numel() * dW.element_size())
+            and _grad_span(dW, db))
 
 
 def thin_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int):
@@ -607,14 +614,6 @@ def gemm_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int, out:
     C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=dZ.device)
     splits = -(-M // 128)
     ws = _workspace(dZ.device, splits * N, slot=1)
-    if X3_GEMM and M * N * K >= X3_MIN_MNK and K % 4 == 0 and dZ.data_ptr() % 16 == 0 and C.is_contiguous() \
-            and _native.available("mlp"):
-        # the x3 kernel with a K-major weight operand and the same epilogue
-        # (8192 x 512 x 512: see profiles/r5/dl)
-        from .mlp import gemm_x3_dact
-
-        gemm_x3_dact(dZ, W, Y, int(act), C, ws)
-        return C, (ws, splits)
     sp = ctypes.c_int(0)
     check(dense_lib().h2omx_gemm_dact(P(dZ), P(W), P(C), P(Y), P(ws), M, N, K, int(act), int(tile),
                                       ctypes.addressof(sp), stream(dZ.device)), "gemm_dact")

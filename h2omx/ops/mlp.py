@@ -39,10 +39,7 @@ def lib():
                          ("h2omx_mlp_out", [ctypes.c_void_p, ctypes.c_void_p]),
                          ("h2omx_gemm_x3", [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
-                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
-                         ("h2omx_gemm_x3_dact", [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
-                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
-                                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])):
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])):
             f = getattr(L, fn)
             f.argtypes = args
             f.restype = ctypes.c_int
@@ -341,14 +338,3 @@ def gemm_x3(A: torch.Tensor, B: torch.Tensor, bias: torch.Tensor | None = None, 
                                       _native.stream_of(A.device)), "gemm_x3")
     return C
 
-
-def gemm_x3_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int, C: torch.Tensor,
-                 bws: torch.Tensor) -> None:
-    """C = (dZ [M][K] W [K][N]) * act'(Y [M][N]) on the x3 kernel (W K-major) and
-    bws [cdiv(M, 128)][N] = per-128-row-block column sums of C
-    (``ops.dense.gemm_dact``'s contract)."""
-    M, K = dZ.shape
-    N = W.shape[1]
-    _native.check(lib().h2omx_gemm_x3_dact(dZ.data_ptr(), dZ.stride(0), W.data_ptr(), W.stride(0), C.data_ptr(),
-                                           Y.data_ptr(), bws.data_ptr(), M, N, K, act, _native.stream_of(dZ.device)),
-                  "gemm_x3_dact")

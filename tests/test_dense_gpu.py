@@ -47,35 +47,6 @@ def test_x3_gemm_matches_fp64(cuda_dev, monkeypatch, M, N, K, act, bias):
         assert torch.equal(routed, got)
 
 
-@pytest.mark.parametrize("M,N,K,act", [(8192, 512, 512, 1), (4100, 260, 516, 2), (8192, 200, 512, 1)])
-def test_x3_gemm_dact_matches_fp64(cuda_dev, monkeypatch, M, N, K, act):
-    """Back-propagation through an activation on the x3 kernel (K-major weight
-    operand): dZ_prev = (dZ W) * act'(Y) and the per-128-row-block column sums
-    (bias-gradient partials) agree with float64 to fp32 accuracy and with the
-    fp32 gemm_dact kernel's contract."""
-    from h2omx.ops import dense as OD
-
-    g = torch.Generator(device="cpu").manual_seed(M + N)
-    dZ = torch.randn((M, K), generator=g).cuda()
-    W = torch.randn((K, N), generator=g).cuda() * 0.05
-    Y = torch.randn((M, N), generator=g).cuda()
-    Y = torch.relu(Y) if act == 1 else torch.tanh(Y)
-    P = dZ.double() @ W.double()
-    ref = P * ((Y > 0).double() if act == 1 else (1 - Y.double() ** 2))
-    C32, (ws32, s32) = OD.gemm_dact(dZ, W, Y, act)              # fp32 kernel (fixture: X3 off)
-    err32 = (C32.double() - ref).abs().max().item()
-    b32 = ws32[: s32 * N].view(s32, N).double().clone()
-    monkeypatch.setattr(OD, "X3_GEMM", True)
-    C, (ws, s) = OD.gemm_dact(dZ, W, Y, act)
-    assert s == s32 == -(-M // 128)
-    tol = max(2.0 * err32, 2e-6 * P.abs().max().item())
-    assert (C.double() - ref).abs().max().item() <= tol
-    bref = torch.stack([ref[i * 128:(i + 1) * 128].sum(0) for i in range(s)])
-    bx3 = ws[: s * N].view(s, N).double()
-    scale = ref.abs().max().item() * 128
-    assert (bx3 - bref).abs().max().item() <= max(2.0 * (b32 - bref).abs().max().item(), 1e-6 * scale)
-
-
 @pytest.mark.parametrize("p,family,link", [(5, "binomial", "logit"), (30, "gaussian", "identity"),
                                            (61, "poisson", "log"), (100, "binomial", "logit"),
                                            (300, "binomial", "logit"), (700, "gaussian", "identity")])
