@@ -1904,30 +1904,6 @@ __global__ __launch_bounds__(1024) void node_best_finalize_kernel(
 // the window with integer global atomics (order-independent: deterministic).
 constexpr int PART_LDS_NODES = 256;   // levels up to this many nodes read their split records from LDS
 
-// exact fixed-point (g, h, w) of a retiring row into its leaf's lane-private LDS
-// copy (window [base, base + win)) or, outside the window, the global sums
-__device__ __forceinline__ void part_leaf_add(int leaf, int base, int win, int cap, int R, int copy, float wv,
-                                              float gk, float hk, float lg, float lh, float lw,
-                                              unsigned long long* lacc, unsigned long long* leaf_acc) {
-  if (leaf_acc == nullptr || leaf >= cap || wv == 0.0f) return;
-  const unsigned long long a = (unsigned long long)(long long)__float2int_rn(gk * lg);
-  const unsigned long long b = (unsigned long long)(long long)__float2int_rn(hk * lh);
-  const unsigned long long c = (unsigned long long)(long long)__float2int_rn(wv * lw);
-  const int li = leaf - base;
-  // separate call sites keep LDS atomics as ds_add_u64 (a pointer selected
-  // between LDS and global memory would become FLAT)
-  if (li >= 0 && li < win) {
-    unsigned long long* d = lacc + (3 * li) * R + copy;
-    atomicAdd(d, a);
-    atomicAdd(d + R, b);
-    atomicAdd(d + 2 * R, c);
-  } else {
-    atomicAdd(leaf_acc + 3 * leaf + 0, a);
-    atomicAdd(leaf_acc + 3 * leaf + 1, b);
-    atomicAdd(leaf_acc + 3 * leaf + 2, c);
-  }
-}
-
 // NIDM bit 0: nid (input) is an int16 stream, bit 1: nid_out is int16 (fused pipeline)
 template <bool PREF, int RPL, int NIDM = 0>
 __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restrict__ codes, int64_t npad,
@@ -2021,42 +1997,11 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
     }
     bool changed = false;
     int sv[RPL];  // next level's build slot per row (-1: retired, or histogram derived from the sibling)
-    if constexpr (PREF) {
-      // final level: per-row node -> split -> code chain (the batched form below
-      // measured no faster here, profiles/r3/part_ab.txt)
-#pragma unroll
-      for (int k = 0; k < RPL; ++k) {
-        sv[k] = -1;
-        const int n = nn[k];
-        int leaf = -1;
-        PartInfo pi;
-        if (n < 0) {
-          if (!all_rows) continue;
-          leaf = ~n;  // retired earlier (padding: INT_MIN -> beyond cap, no sums)
-          pi.child = -2;
-        } else {
-          changed = true;
-          pi = rec_lds ? ps[n] : part[n];
-        }
-        if (pi.child == -2) {
-        } else if (pi.child < 0) {
-          leaf = pi.gid;
-        } else {
-          const int b = codes[(int64_t)pi.feat * npad + r0 + k];
-          const int right = part_right(pi, b, nbt);
-          if (pi.leaf_children) {
-            leaf = pi.child_gid + right;
-          } else {
-            nn[k] = pi.child + right;
-            sv[k] = right ? (pi.pad >> 16) : (int)(short)(pi.pad & 0xFFFF);
-          }
-        }
-        if (leaf >= 0) {
-          if (n >= 0) nn[k] = ~leaf;
-          part_leaf_add(leaf, base, win, cap, R, copy, wv8[k], gv[k], hv[k], lg, lh, lw, lacc, leaf_acc);
-        }
-      }
-    } else {
+    {
+      // every level (the final one too): the RPL split-code gathers are issued
+      // together at clamped addresses before any row is decided (the per-row
+      // node -> split -> code chain on the final level measured 0.813 vs 0.778
+      // ms/tree, profiles/r5/partition_ab.txt)
       PartInfo pi[RPL];
       int bc[RPL];
 #pragma unroll
@@ -3057,9 +3002,11 @@ static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const 
   if (slot16 && prefetch) return kBadArg;
   if (npad % PART_RPL != 0 || blocks < 1 || blocks > PARTITION_BLOCKS || win_max < 0) return kBadArg;
   if (all_rows && (leaf_acc == nullptr || win_max > cap)) return kBadArg;
-  // lane-private copies: the largest power of two <= 64 that fits 64 KB
+  // 8 lane copies of the leaf window (12 KB for a depth-5 tree): occupancy
+  // hides the split-code gathers better than conflict-free 32 copies (48 KB;
+  // 0.778 vs 0.796 ms/tree, profiles/r5/partition_ab.txt)
   constexpr size_t kWinLds = 64 * 1024;
-  int R = 64;
+  int R = 8;
   while (R > 1 && (size_t)3 * win_max * R * sizeof(unsigned long long) > kWinLds) R >>= 1;
   if ((size_t)3 * win_max * R * sizeof(unsigned long long) > kWinLds) {
     if (all_rows) return kBadArg;  // the whole-tree window must fit
