@@ -254,7 +254,7 @@ class _TreeBuilder(ModelBuilder):
         tp = self._tree_params(len(self.x))
         if per_node:
             tp.hist_mode, tp.hist_top, tp.hist_nbins = PER_NODE_MODES[htype], top, nbins
-            bm.frange = adaptive_ranges(X, bm, self.comm)
+            bm.frange = adaptive_ranges(X, bm, self.comm, seed=self._seed())
         nclass = len(self.response_domain) if self.response_domain else 1
         ens_dist = self._engine_dist(dist)
         init_f = None
