@@ -114,6 +114,9 @@ class _TreeBuilder(ModelBuilder):
     # UniformAdaptive re-binned per node; XGBoost 'hist' bins globally)
     auto_histogram = "quantilesglobal"
     per_node_histograms = False
+    # fine-grid cap of the per-node rules for trees deeper than deep_depth
+    deep_depth = 12
+    deep_fine_bins = 63
 
     def _warn(self, msg: str, loud: bool = True) -> None:
         """A deviation from H2O's semantics, surfaced in the model output
@@ -228,9 +231,16 @@ class _TreeBuilder(ModelBuilder):
             # nbins_top_level, at most 255: uint8 codes); every node then keeps the
             # fine edges nearest its own equal-width / random cuts (binning.py)
             fine = min(255, max(nbins, top))
+            if int(self.params.get("max_depth") or 0) > self.deep_depth and fine > self.deep_fine_bins:
+                # deep trees (DRF depth 20): 63 fine bins keep the direct levels' per-node
+                # histograms small - 10M x 100 DRF 27 vs 43 ms/tree for 255, AUC 0.787 vs
+                # 0.794 (QuantilesGlobal-20: 0.776; profiles/r5/hist/hist_rule_ab_r5y.jsonl)
+                fine = self.deep_fine_bins
+                self._warn(f"max_depth > {self.deep_depth}: per-node cut points snap to {fine} fine quantile "
+                           "bins per column", loud=False)
             edges, nvb, nbt = compute_edges(X, fine, seed=self._seed(), comm=self.comm,
                                             histogram_type="QuantilesGlobal")
-            if max(nbins, top) > 255:
+            if max(nbins, top) > 255 and fine == 255:
                 # (H2O's defaults hit this: recorded in the model, not raised as a Python warning)
                 self._warn(f"histogram_type {self.params.get('histogram_type') or 'AUTO'}: node cut points snap to "
                            f"255 fine quantile bins per column (nbins_top_level={top} finer than the uint8 codes)",
