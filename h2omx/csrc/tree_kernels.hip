@@ -4897,7 +4897,8 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
     return launch_status();
   }
   if (mode == 1 && p.F <= DIRECT_WAVE_F) {
-    const int batch = std::max(1, std::min(max_elig, DIRECT_WAVE_LDS / per_f_bytes));
+    static const int wave_lds = [] { const char* e = getenv("H2OMX_DIRECT_WAVE_KB"); return (e ? atoi(e) : 8) * 1024; }();
+    const int batch = std::max(1, std::min(max_elig, wave_lds / per_f_bytes));
     const size_t lds = (size_t)4 * batch * per_f_bytes;
 #define H2OMX_SDW(NB)                                                                                              \
   hipLaunchKernelGGL(seg_direct_wave_kernel<NB>, dim3(pad8((max_nodes + 3) / 4)), dim3(256), lds, stream, codes_rm, fp, \

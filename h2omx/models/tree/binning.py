@@ -111,7 +111,8 @@ PER_NODE_MODES = {"uniformadaptive": 1, "random": 2, "roundrobin": 3}
 
 def resolve_histogram_type(h, auto: str = "quantilesglobal") -> str:
     """H2O ``histogram_type`` -> the binning rule (``auto``: what AUTO means
-    for the caller - UniformAdaptive for GBM / DRF as in H2O).
+    for the caller - UniformAdaptive for GBM / DRF as in the H2O-3 image the
+    reference deploys, /root/reference/src/k8s/mod.rs:115).
 
     * QuantilesGlobal: global quantile cut points.
     * UniformAdaptive / Random / RoundRobin are per-node rules on GBM / DRF

@@ -113,6 +113,17 @@ def test_unknown_param_is_warning_and_ignored_columns(conn):
     assert names == ["a", "b", "label"]
 
 
+def test_histogram_deviation_warnings_over_rest(conn):
+    """GBM's AUTO histograms are H2O's per-node UniformAdaptive; what still
+    deviates reaches the REST caller as model warnings (H2O's output.warnings)."""
+    m = conn.train("gbm", "train.hex", y="label", ntrees=2, max_depth=3, seed=1)
+    assert any("fine quantile bins" in w for w in (m["output"].get("warnings") or []))
+    r = conn.train("gbm", "train.hex", y="label", ntrees=2, max_depth=3, seed=1, histogram_type="UniformRobust")
+    assert any("one global grid" in w for w in r["output"]["warnings"])
+    q = conn.train("gbm", "train.hex", y="label", ntrees=2, max_depth=3, seed=1, histogram_type="QuantilesGlobal")
+    assert not q["output"].get("warnings")
+
+
 def test_kmeans_rest_and_mojo_roundtrip(conn):
     from h2omx.frame.frame import DKV as dkv
     from h2omx.mojo import GenericModel
