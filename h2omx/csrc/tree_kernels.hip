@@ -1896,12 +1896,13 @@ __global__ __launch_bounds__(1024) void node_best_finalize_kernel(
 // sums are complete) - this replaces a separate pass over the rows.
 // The leaves that can appear at this level have gids in the window
 // [base, base + n + n_next) (nodes that stop here, and at the last level the
-// children of its splits); their sums are privatised in LDS as R lane-
-// private copies laid out [slot][copy] so the 64 lanes of a wave hit 64
-// consecutive u64 (no bank conflicts, no same-address serialisation:
-// measured 4.3M LDS bank-conflict cycles per last-level dispatch with the
-// previous [copy][slot] layout).  Each workgroup folds its copies and adds
-// the window with integer global atomics (order-independent: deterministic).
+// children of its splits); their sums are privatised in LDS as R = 8 lane
+// copies laid out [slot][copy] (lane l adds into copy l % R: consecutive
+// lanes hit consecutive u64; the [copy][slot] layout measured 4.3M LDS
+// bank-conflict cycles per last-level dispatch, and 32 conflict-free copies
+// cost more occupancy than they saved, profiles/r5/partition_ab.txt).  Each
+// workgroup folds its copies and adds the window with integer global atomics
+// (order-independent: deterministic).
 constexpr int PART_LDS_NODES = 256;   // levels up to this many nodes read their split records from LDS
 
 // NIDM bit 0: nid (input) is an int16 stream, bit 1: nid_out is int16 (fused pipeline)
@@ -4415,7 +4416,7 @@ __global__ __launch_bounds__(256) void seg_direct_chunk_kernel(
 // many more per CU.  Eligible features from per-lane hashes in registers
 // (F <= 256) ranked with scalar lane reads (no LDS round trips).
 constexpr int DIRECT_WAVE_F = 256;
-constexpr int DIRECT_WAVE_LDS = 8 * 1024;   // max histogram bytes per wave
+constexpr int DIRECT_WAVE_LDS = 8 * 1024;   // max histogram bytes per wave (8 / 10 / 16 KB measured alike, profiles/r5/drf_deep_ab.txt)
 
 template <int NBT>
 __global__ __launch_bounds__(256) void seg_direct_wave_kernel(
@@ -4897,8 +4898,7 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
     return launch_status();
   }
   if (mode == 1 && p.F <= DIRECT_WAVE_F) {
-    static const int wave_lds = [] { const char* e = getenv("H2OMX_DIRECT_WAVE_KB"); return (e ? atoi(e) : 8) * 1024; }();
-    const int batch = std::max(1, std::min(max_elig, wave_lds / per_f_bytes));
+    const int batch = std::max(1, std::min(max_elig, DIRECT_WAVE_LDS / per_f_bytes));
     const size_t lds = (size_t)4 * batch * per_f_bytes;
 #define H2OMX_SDW(NB)                                                                                              \
   hipLaunchKernelGGL(seg_direct_wave_kernel<NB>, dim3(pad8((max_nodes + 3) / 4)), dim3(256), lds, stream, codes_rm, fp, \

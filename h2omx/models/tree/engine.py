@@ -887,8 +887,7 @@ class HipTreeBuilder:
                     dmode = 0
                 ec = None
                 # every eligible feature in one LDS batch (batch sizes of h2omx_seg_direct)
-                one_batch = {0: 98304, 1: int(os.environ.get("H2OMX_DIRECT_WAVE_KB", "8")) * 1024,
-                             2: 1 << 30}[dmode] // (16 * nbt) >= n_elig
+                one_batch = {0: 98304, 1: 8192, 2: 1 << 30}[dmode] // (16 * nbt) >= n_elig
                 if self.ECODES and n_elig <= 16 and one_batch:
                     ecs = 8 if n_elig <= 8 else 16
                     ec = (B("ecodes", (n + 64) * ecs, torch.uint8), ecs, B("nodeq", max_nodes, i32))
