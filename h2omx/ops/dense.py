@@ -627,6 +627,8 @@ def _splitk(M: int, N: int, K: int) -> int:
     8 K-splits of 2 steps, ~4x faster)"""
     tiles = -(-M // 128) * -(-N // 128)
     if tiles < 128 and K >= 1024:
+        # (about one 128 x 128 tile per CU: 8 or 1024 / tiles splits measured slower,
+        # profiles/r5/dl/wgrad_splitk_ab.txt)
         return max(1, min(64, 256 // tiles, K // 256))
     tiles64 = -(-M // 64) * -(-N // 64)
     if tiles64 < 128 and K >= 256:
