@@ -436,7 +436,8 @@ def _mlp(args, comm, torch, np):
         "ms_per_step": 1000.0 * elapsed / args.steps,
         "higher_is_better": True,
         "dtype": ("bf16 (bf16 MFMA GEMMs with fp32 accumulation; fp32 master weights, gradients and ADADELTA)"
-                  if bf16 else "fp32 (MFMA fp32 GEMMs, fp32 ADADELTA)"),
+                  if bf16 else "fp32 (fp32-accurate GEMMs: exact 3-piece bf16 split on MFMA for the large forward / "
+                  "data-gradient products, fp32 MFMA weight gradients; fp32 ADADELTA)"),
         "data": "synthetic wide-Gaussian 200 features generated on device; random-init weights",
         "config": {"model": "MLP 200-512x4-2 Rectifier, ADADELTA(0.99,1e-8), softmax", "global_batch": world * B,
                    "seq_len": None, "rows_per_gpu": n_local, "batch_per_gpu": B,

@@ -504,11 +504,16 @@ __device__ __forceinline__ void x3_load(const float* __restrict__ A, int lda, co
 // into the same LDS planes - ran slower than the fp32 MFMA kernels: dact 58.8
 // vs 56.2 us, split-K weight gradient 50.1 vs 41.4 us at 8192 x 512 x 512,
 // profiles/r5/dl/kernel_stats_r5q.txt; removed)
-template <bool kDB>
+// kEPI 0: C = act(acc + bias) (forward layers); kEPI 1: C = acc * act'(Y) and
+// the column sums of C per 64-row wave block into ws[(row / 64)][N] (the data
+// gradient of a hidden layer with its bias-gradient slices; B = W^T, made
+// K-contiguous by x3_transpose_kernel first)
+template <bool kDB, int kEPI>
 __global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict__ A, int lda,
                                                         const float* __restrict__ B, int ldb, float* __restrict__ C,
                                                         int ldc, const float* __restrict__ bias, int M, int N, int K,
-                                                        int act) {
+                                                        int act, const float* __restrict__ Y, int ldy,
+                                                        float* __restrict__ ws) {
   constexpr int NBUF = kDB ? 2 : 1;
   __shared__ __attribute__((aligned(16))) __bf16 La[NBUF][3 * X3_PLANE];
   __shared__ __attribute__((aligned(16))) __bf16 Lb[NBUF][3 * X3_PLANE];
@@ -530,6 +535,24 @@ __global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
   const int nst = (K + X3_BK - 1) / X3_BK;
+  // kEPI 1 (always kDB: one wave per SIMD, 64 VGPRs of room): the tile's Y
+  // values (for act') are loaded before the k loop, so the epilogue waits on no
+  // global load
+  float yg[kEPI == 1 ? 2 : 1][kEPI == 1 ? 32 : 1];
+  auto load_y = [&](int b) {
+    const int j = min(n0 + wn + 32 * b + li, N - 1);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int i = min(m0 + wm + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * lh, M - 1);
+        yg[b][a * 16 + e] = Y[(int64_t)i * ldy + j];
+      }
+  };
+  if (kEPI == 1) {
+    load_y(0);
+    load_y(1);
+  }
   X3Regs r;
   x3_load(A, lda, B, ldb, M, N, K, m0, n0, 0, r);
   auto stage = [&](int buf) {
@@ -578,6 +601,29 @@ __global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict
     __syncthreads();
   }
   // epilogue: lane owns column j, registers e are rows (e & 3) + 8 (e >> 2) + 4 lh
+  if (kEPI == 1) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int j = n0 + wn + 32 * b + li;
+      float cs = 0.0f;
+      if (j < N) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int i = m0 + wm + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * lh;
+            if (i < M) {
+              const float v = acc[a][b][e] * act_grad_of(yg[b][a * 16 + e], act);
+              C[(int64_t)i * ldc + j] = v;
+              cs += v;
+            }
+          }
+      }
+      cs += __shfl_xor(cs, 32, 64);   // the other 32 rows of the wave block
+      if (lh == 0 && j < N && m0 + wm < M) ws[(int64_t)((m0 + wm) >> 6) * N + j] = cs;
+    }
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -597,6 +643,38 @@ __global__ __launch_bounds__(256) void gemm_x3_nt_kernel(const float* __restrict
     }
 }
 
+// dst[c][r] = src[r][c] through a padded 32 x 33 LDS tile, one job per
+// blockIdx.z (a network's hidden weights, [out][in] -> [in][out], in one
+// launch, so the data-gradient GEMMs read K-contiguous rows)
+constexpr int X3_TMAX = 8;
+struct X3Transpose {
+  const float* src[X3_TMAX];
+  float* dst[X3_TMAX];
+  int R[X3_TMAX], C[X3_TMAX];
+};
+
+__global__ __launch_bounds__(256) void x3_transpose_kernel(X3Transpose T) {
+  __shared__ float tile[32][33];
+  const int z = blockIdx.z;
+  const float* __restrict__ src = T.src[z];
+  float* __restrict__ dst = T.dst[z];
+  const int R = T.R[z], Cn = T.C[z];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  if (c0 >= Cn || r0 >= R) return;   // (grid sized for the largest job)
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = r0 + ty + 8 * q, c = c0 + tx;
+    if (r < R && c < Cn) tile[ty + 8 * q][tx] = src[(int64_t)r * Cn + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = c0 + ty + 8 * q, r = r0 + tx;
+    if (r < R && c < Cn) dst[(int64_t)c * R + r] = tile[tx][ty + 8 * q];
+  }
+}
+
 }  // namespace
 
 // fp32 NT GEMM on the bf16 matrix cores (x3 split, see above); A, B rows
@@ -607,8 +685,45 @@ H2OMX_API int h2omx_gemm_x3(const float* A, int lda, const float* B, int ldb, fl
   if ((lda & 3) || (ldb & 3) || (K & 3) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return kBadArg;
   const dim3 grid((N + X3_BN - 1) / X3_BN, (M + X3_BM - 1) / X3_BM);
   if ((int64_t)grid.x * grid.y <= 256)
-    hipLaunchKernelGGL(gemm_x3_nt_kernel<true>, grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, N, K, act);
+    hipLaunchKernelGGL((gemm_x3_nt_kernel<true, 0>), grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, N,
+                       K, act, nullptr, 0, nullptr);
   else
-    hipLaunchKernelGGL(gemm_x3_nt_kernel<false>, grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, N, K, act);
+    hipLaunchKernelGGL((gemm_x3_nt_kernel<false, 0>), grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, N,
+                       K, act, nullptr, 0, nullptr);
+  return launch_status();
+}
+
+// Transposes of n <= 8 row-major matrices src_i [R_i][C_i] -> dst_i [C_i][R_i]
+// in one launch (the hidden weights before the backward's data gradients).
+H2OMX_API int h2omx_x3_transpose(int n, const float* const* src, float* const* dst, const int* R, const int* C,
+                                 hipStream_t stream) {
+  if (n < 1 || n > X3_TMAX || src == nullptr || dst == nullptr || R == nullptr || C == nullptr) return kBadArg;
+  X3Transpose T{};
+  int gx = 1, gy = 1;
+  for (int z = 0; z < n; ++z) {
+    if (src[z] == nullptr || dst[z] == nullptr || R[z] < 1 || C[z] < 1) return kBadArg;
+    T.src[z] = src[z]; T.dst[z] = dst[z]; T.R[z] = R[z]; T.C[z] = C[z];
+    gx = max(gx, (C[z] + 31) / 32);
+    gy = max(gy, (R[z] + 31) / 32);
+  }
+  hipLaunchKernelGGL(x3_transpose_kernel, dim3(gx, gy, n), dim3(256), 0, stream, T);
+  return launch_status();
+}
+
+// Data gradient of a Rectifier (act 1) / Tanh (act 2) layer on the x3 GEMM:
+// C[M][N] = (dZ[M][K] . Wt[N][K]^T) * act'(Y[M][N]), Wt = W^T (h2omx_x3_transpose).
+// ws[(M + 63) / 64][N] receives the column sums of C per 64-row block.  All
+// matrices dense row-major, K % 4 == 0.
+H2OMX_API int h2omx_gemm_x3_dact(const float* dZ, const float* Wt, const float* Y, float* C, float* ws, int M, int N,
+                                 int K, int act, hipStream_t stream) {
+  if (dZ == nullptr || Wt == nullptr || Y == nullptr || C == nullptr || ws == nullptr || M < 1 || N < 1 || K < 1 ||
+      (act != 1 && act != 2))
+    return kBadArg;
+  if ((K & 3) || ((uintptr_t)dZ & 15) || ((uintptr_t)Wt & 15)) return kBadArg;
+  // (double-buffered at every grid size: the single-buffer variant's two waves
+  // per SIMD do not fit the prefetched Y registers)
+  const dim3 grid((N + X3_BN - 1) / X3_BN, (M + X3_BM - 1) / X3_BM);
+  hipLaunchKernelGGL((gemm_x3_nt_kernel<true, 1>), grid, dim3(256), 0, stream, dZ, K, Wt, K, C, N, nullptr, M, N, K,
+                     act, Y, N, ws);
   return launch_status();
 }

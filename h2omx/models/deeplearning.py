@@ -786,6 +786,12 @@ class H2ODeepLearningEstimator(ModelBuilder):
         bpart = None   # bias-gradient slices of dZ from the fused activation backward
         # per-layer scratch when the partial sums are folded later (deferred folds)
         layer_ns = OD._GRAD_FOLDS[0] is not None
+        # W^T of the layers whose data gradient runs on the x3 GEMM, one launch
+        Wts = {}
+        if dZ.is_cuda and act in (1, 2):
+            xi = [i for i in range(1, L) if aux[i - 1][1] is None and OD.x3_dact_layer(dZ.shape[0], net.W(i), act)]
+            if xi:
+                Wts = dict(zip(xi, OD.transpose_weights([net.W(i) for i in xi])))
         for i in range(L - 1, -1, -1):
             Hin = Hs[i]
             W = net.W(i)
@@ -809,21 +815,23 @@ class H2ODeepLearningEstimator(ModelBuilder):
             if i == 0:
                 break
             with OD.workspace_ns(i) if layer_ns else contextlib.nullcontext():
-                dZ, bpart = H2ODeepLearningEstimator._dgrad(Hs, aux, dZ, W, act, i, L)
+                dZ, bpart = H2ODeepLearningEstimator._dgrad(Hs, aux, dZ, W, act, i, L, Wts.get(i))
         for h in handles:
             h.wait()
         if comm is not None and world > 1:
             net.grad.div_(world)
 
     @staticmethod
-    def _dgrad(Hs, aux, dZ, W, act, i, L):
+    def _dgrad(Hs, aux, dZ, W, act, i, L, Wt=None):
         """dZ of layer i - 1 from layer i's (dZ, W): (dZ_prev, bias-gradient
-        slices or None)"""
+        slices or None); ``Wt`` = W^T for the x3 route (OD.transpose_weights)"""
         arg, mask = aux[i - 1]
         if act in (1, 2) and mask is None and i == L - 1 and D.out_layer_ok(dZ, Hs[i]):
             return D.thin_dact(dZ, W, Hs[i], act)
         if act in (1, 2) and mask is None and D.dact_ok(dZ, W):
             # dZ_prev = (dZ W) * act'(H) and its bias-gradient slices in the GEMM epilogue
+            if Wt is not None:
+                return D.gemm_dact(dZ.contiguous(), W, Hs[i], act, Wt=Wt)
             return D.gemm_dact(dZ.contiguous(), W, Hs[i], act)
         dH = D.gemm(dZ, W)                                            # [M][in]
         if mask is not None:

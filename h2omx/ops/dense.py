@@ -476,6 +476,8 @@ def gemm_fp32(A: torch.Tensor, B: torch.Tensor, bias=None, act: int = 0, ta: boo
 # 256-row mini-batch layer runs 13.8 us on gemm_w64 vs 34.4 us on x3: too few tiles)
 X3_GEMM = True
 X3_MIN_MNK = 1 << 27
+# hidden-layer data gradients (gemm_dact) on the x3 kernel as well
+X3_DACT = True
 
 
 def _x3_ok(A, B, C) -> bool:
@@ -598,8 +600,36 @@ def dact_ok(dZ: torch.Tensor, W: torch.Tensor) -> bool:
     return (M // 128) * (N // 64) >= DACT_MIN_BLOCKS
 
 
+def x3_dact_ok(M: int, K: int, N: int, act: int) -> bool:
+    """gemm_dact of a [M][K] x [K][N] product takes the x3 route"""
+    return X3_DACT and X3_GEMM and M * N * K >= X3_MIN_MNK and act in (1, 2) and K % 4 == 0 and \
+        _native.available("mlp")
+
+
+def x3_dact_layer(M: int, W: torch.Tensor, act: int) -> bool:
+    """the data gradient through W ([K][N]) for a batch of M rows runs gemm_dact
+    on the x3 route (dact_ok and x3_dact_ok)"""
+    K, N = W.shape
+    return (M % 128 == 0 and N % 64 == 0 and (M // 128) * (N // 64) >= DACT_MIN_BLOCKS
+            and x3_dact_ok(M, K, N, act))
+
+
+def transpose_weights(Ws) -> list:
+    """W^T copies ([in][out]) of the given hidden weights for the x3 data
+    gradients, in one launch; scratch per layer (workspace namespace
+    2000 + position)."""
+    from .mlp import x3_transpose
+
+    outs = []
+    for q, W in enumerate(Ws):
+        with workspace_ns(2000 + q):
+            outs.append(_workspace(W.device, W.numel(), slot=2)[: W.numel()].view(W.shape[1], W.shape[0]))
+    x3_transpose([(W.contiguous(), Wt) for W, Wt in zip(Ws, outs)])
+    return outs
+
+
 def gemm_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int, out: torch.Tensor | None = None,
-              tile: int = 2):
+              tile: int = 2, Wt: torch.Tensor | None = None):
     """Back-propagation through a Rectifier / Tanh layer in one GEMM:
     dZ_prev = (dZ[M][K] W[K][N]) * act'(Y[M][N]) (Y = that layer's output), plus
     the column sums of dZ_prev per 128-row block (its bias gradient before the
@@ -612,6 +642,16 @@ def gemm_dact(dZ: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, act: int, out:
                                                             and Y.is_contiguous()):
         raise ValueError("gemm_dact: needs contiguous dZ [M][K], W [K][N], Y [M][N]")
     C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=dZ.device)
+    if x3_dact_ok(M, K, N, act) and dZ.data_ptr() % 16 == 0 and C.is_contiguous():
+        # x3 GEMM on W^T (``Wt`` from transpose_weights, else transposed here)
+        # instead of the fp32 MFMA kernel (profiles/r5/dl/x3_dact_ab.txt)
+        from .mlp import gemm_x3_dact
+        if Wt is None:
+            Wt = transpose_weights([W])[0]
+        splits = -(-M // 64)
+        ws = _workspace(dZ.device, splits * N, slot=1)
+        gemm_x3_dact(dZ, Wt, Y, act, ws, out=C)
+        return C, (ws, splits)
     splits = -(-M // 128)
     ws = _workspace(dZ.device, splits * N, slot=1)
     sp = ctypes.c_int(0)

@@ -39,7 +39,9 @@ def lib():
                          ("h2omx_mlp_out", [ctypes.c_void_p, ctypes.c_void_p]),
                          ("h2omx_gemm_x3", [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
-                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])):
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+                         ("h2omx_gemm_x3_dact", [ctypes.c_void_p] * 5 + [ctypes.c_int] * 4 + [ctypes.c_void_p]),
+                         ("h2omx_x3_transpose", [ctypes.c_int] + [ctypes.c_void_p] * 5)):
             f = getattr(L, fn)
             f.argtypes = args
             f.restype = ctypes.c_int
@@ -338,3 +340,31 @@ def gemm_x3(A: torch.Tensor, B: torch.Tensor, bias: torch.Tensor | None = None, 
                                       _native.stream_of(A.device)), "gemm_x3")
     return C
 
+
+def x3_transpose(pairs) -> None:
+    """dst = src^T for up to 8 (src [R][C], dst [C][R]) fp32 pairs, one launch."""
+    n = len(pairs)
+    if n == 0:
+        return
+    src = (ctypes.c_void_p * n)(*[a.data_ptr() for a, _ in pairs])
+    dst = (ctypes.c_void_p * n)(*[b.data_ptr() for _, b in pairs])
+    R = (ctypes.c_int * n)(*[a.shape[0] for a, _ in pairs])
+    C = (ctypes.c_int * n)(*[a.shape[1] for a, _ in pairs])
+    for a, b in pairs:
+        if not (a.is_contiguous() and b.numel() >= a.numel()):
+            raise ValueError("x3_transpose: needs a contiguous source and a large enough destination")
+    _native.check(lib().h2omx_x3_transpose(n, src, dst, R, C, _native.stream_of(pairs[0][0].device)), "x3_transpose")
+
+
+def gemm_x3_dact(dZ: torch.Tensor, Wt: torch.Tensor, Y: torch.Tensor, act: int, ws: torch.Tensor,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """dZ_prev = (dZ [M][K] Wt [N][K]^T) * act'(Y [M][N]) on the x3 GEMM (Wt =
+    the layer's W^T from :func:`x3_transpose`, so both operands are
+    K-contiguous), with the column sums of dZ_prev per 64-row block in ``ws``
+    [(M + 63) // 64][N]."""
+    M, K = dZ.shape
+    N = Y.shape[1]
+    C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=dZ.device)
+    _native.check(lib().h2omx_gemm_x3_dact(dZ.data_ptr(), Wt.data_ptr(), Y.data_ptr(), C.data_ptr(), ws.data_ptr(),
+                                           M, N, K, int(act), _native.stream_of(dZ.device)), "gemm_x3_dact")
+    return C

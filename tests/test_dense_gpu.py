@@ -47,6 +47,41 @@ def test_x3_gemm_matches_fp64(cuda_dev, monkeypatch, M, N, K, act, bias):
         assert torch.equal(routed, got)
 
 
+@pytest.mark.parametrize("M,K,N,act", [(8192, 512, 512, 1), (8192, 512, 512, 2), (4100, 516, 300, 2),
+                                       (8000, 1024, 200, 1)])
+def test_x3_dact_matches_fp64(cuda_dev, monkeypatch, M, K, N, act):
+    """Hidden-layer data gradient on the x3 GEMM (W transposed into scratch,
+    act'(Y) and the 64-row bias partials in the epilogue) against float64,
+    with fp32-kernel accuracy."""
+    from h2omx.ops import dense as OD
+
+    g = torch.Generator(device="cpu").manual_seed(M + K + N + act)
+    dZ = torch.randn((M, K), generator=g).cuda()
+    W = torch.randn((K, N), generator=g).cuda() * 0.05
+    Y = torch.randn((M, N), generator=g).cuda()
+    Y = Y.clamp_min(0) if act == 1 else torch.tanh(Y)
+    dH = dZ.double() @ W.double()
+    ref = dH * ((Y > 0).double() if act == 1 else (1 - Y.double() ** 2))
+    f32, _ = OD.gemm_dact(dZ, W, Y, act)                 # fp32 MFMA route (X3_GEMM off)
+    err32 = (f32.double() - ref).abs().max().item()
+    monkeypatch.setattr(OD, "X3_GEMM", True)
+    out, (ws, splits) = OD.gemm_dact(dZ, W, Y, act)
+    assert splits == -(-M // 64)                        # the x3 route ran
+    tol = max(2.0 * err32, 2e-6 * dH.abs().max().item())
+    assert (out.double() - ref).abs().max().item() <= tol
+    colsum = ws[: splits * N].view(splits, N).double().sum(0)
+    assert torch.allclose(colsum, ref.sum(0), rtol=1e-5, atol=1e-3)
+    for s in (0, splits - 1):   # each slice is its own 64 rows
+        assert torch.allclose(ws[s * N:(s + 1) * N].double(), out[s * 64:(s + 1) * 64].double().sum(0),
+                              rtol=1e-5, atol=1e-4)
+    # batched transposes (one launch for several layers) feed the same bits
+    W2 = torch.randn((N, 3 * K // 4 if K % 16 == 0 else K), generator=g).cuda()
+    Wt, W2t = OD.transpose_weights([W, W2])
+    assert torch.equal(Wt, W.t()) and torch.equal(W2t, W2.t())
+    out2, _ = OD.gemm_dact(dZ, W, Y, act, Wt=Wt)
+    assert torch.equal(out2, out)
+
+
 @pytest.mark.parametrize("p,family,link", [(5, "binomial", "logit"), (30, "gaussian", "identity"),
                                            (61, "poisson", "log"), (100, "binomial", "logit"),
                                            (300, "binomial", "logit"), (700, "gaussian", "identity")])
