@@ -1990,6 +1990,20 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __
     float a = 0.0f, b = 0.0f;
     if (j < N2) {
       int z = ph;
+      // 8 (a, b) pairs of loads in flight, then the adds in the same order
+      for (; z + 60 < S2; z += 64) {
+        float la[8], lb[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          la[u] = W2[(int64_t)(z + 8 * u) * N2 + j];
+          lb[u] = W2[(int64_t)(z + 8 * u + 4) * N2 + j];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          a += la[u];
+          b += lb[u];
+        }
+      }
       for (; z + 4 < S2; z += 8) {
         a += W2[(int64_t)z * N2 + j];
         b += W2[(int64_t)(z + 4) * N2 + j];
@@ -2003,6 +2017,32 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __
   }
   const int64_t MN = (int64_t)M * N;
   const int64_t gstride = (int64_t)(W2 != nullptr ? main_blocks : gridDim.x) * blockDim.x;
+  if (bias == nullptr && act == 0 && beta_c == 0.0f && (MN & 3) == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(C) & 15) == 0) {
+    // plain sum (weight gradients): 4 columns per thread, 8 slices' loads in
+    // flight, the adds in slice order (the same bits as the scalar loop below)
+    const int64_t MN4 = MN >> 2;
+    const float4* W4 = reinterpret_cast<const float4*>(W);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < MN4; i += gstride) {
+      float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      int z = 0;
+      for (; z + 8 <= S; z += 8) {
+        float4 t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = W4[(int64_t)(z + u) * MN4 + i];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          v.x += t[u].x; v.y += t[u].y; v.z += t[u].z; v.w += t[u].w;
+        }
+      }
+      for (; z < S; ++z) {
+        const float4 t = W4[(int64_t)z * MN4 + i];
+        v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+      }
+      reinterpret_cast<float4*>(C)[i] = v;
+    }
+    return;
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < MN; i += gstride) {
     float v = 0.0f;
     for (int z = 0; z < S; ++z) v += W[z * MN + i];
