@@ -3955,6 +3955,11 @@ __device__ __forceinline__ void direct_row_atomics(const uint8_t* __restrict__ r
   }
 }
 
+template <typename FL>
+__device__ __forceinline__ int direct_eligible(int node, int gid_i, const SplitParams& p,
+                                              const uint8_t* __restrict__ tree_fmask, FL* flist, uint32_t* hsh_s,
+                                              int lane);
+
 template <int NBT>
 __global__ __launch_bounds__(256) void seg_direct_kernel(
     const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
@@ -3976,38 +3981,10 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int lo = seg_start[node], cnt = seg_cnt[node];
   const int gid_i = ctl[CTL_BASE] + node;   // interaction-constraint state
-  // eligible features of this node (wave 0), in ascending order; the mtries
-  // rank of feature f counts the features whose hash is smaller (ties: lower
-  // index), as split_find - with the F hashes computed once into LDS
+  // eligible features of this node (wave 0), in ascending order: the mtries
+  // smallest (hash, index) keys, as split_find
   if (wid == 0) {
-    const uint32_t key = (uint32_t)p.tree_index * 131u + (uint32_t)p.depth;
-    const bool sampled = p.mtries > 0 || p.col_rate < 1.0f;
-    if (sampled)
-      for (int f = lane; f < F; f += 64) hsh_s[f] = hash4(p.seed, key, (uint32_t)node, (uint32_t)f);
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-    int c = 0;
-    for (int f0 = 0; f0 < F; f0 += 64) {
-      const int f = f0 + lane;
-      bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]) && inter_ok(p, gid_i, f);
-      if (ok && sampled) {
-        const uint32_t hf = hsh_s[f];
-        if (p.mtries > 0) {
-          int rank = 0;
-          for (int j = 0; j < F; ++j) {
-            const uint32_t hj = hsh_s[j];
-            rank += (hj < hf) || (hj == hf && j < f);
-          }
-          ok = rank < p.mtries;
-        } else {
-          ok = u01(hf) < p.col_rate;
-        }
-      }
-      const unsigned long long bal = __ballot(ok);
-      const int pos = c + __popcll(bal & ((1ull << lane) - 1ull));
-      if (ok && pos < 1024) flist[pos] = f;
-      c += __popcll(bal);
-    }
+    const int c = direct_eligible(node, gid_i, p, tree_fmask, flist, hsh_s, lane);
     if (lane == 0) nfl_s = c < 1024 ? c : 1024;
   }
   if (t < 8) tot_s[t >> 2][t & 3] = 0;
@@ -4088,6 +4065,49 @@ __device__ __forceinline__ int chunk_node_wave(const int* __restrict__ first, in
 }
 
 
+// mtries selection of a wave's features (lane + 64 k, k < 4, F <= 256, hashes
+// hv): feature f is eligible iff fewer than m features have a smaller
+// (hash, index) key - the m smallest keys.  Instead of ranking every pair (F
+// readlane steps x 4 compares per lane), a 32-step ballot bisection finds v,
+// the m-th smallest hash; every feature below v is in, and of the features
+// hashing to v the first m - #below by index.  The same set as the pairwise
+// rank (rank < m), so every engine agrees.
+__device__ __forceinline__ void mtries_select(const uint32_t (&hv)[4], int F, int m, int lane, bool (&sel)[4]) {
+  bool valid[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) valid[k] = lane + 64 * k < F;
+  if (m >= F) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sel[k] = valid[k];
+    return;
+  }
+  const int kn = (F + 63) >> 6;   // wave-uniform
+  uint32_t lo = 0u, hi = 0xffffffffu;
+  while (lo < hi) {   // smallest v with #{hash <= v} >= m
+    const uint32_t mid = lo + ((hi - lo) >> 1);
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < kn) c += __popcll(__ballot(valid[k] && hv[k] <= mid));
+    if (c >= m) hi = mid;
+    else lo = mid + 1u;
+  }
+  int below = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (k < kn) below += __popcll(__ballot(valid[k] && hv[k] < lo));
+  const int need = m - below;
+  int eq_before = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool eq = valid[k] && hv[k] == lo;
+    const unsigned long long be = __ballot(eq);
+    const int pos = eq_before + __popcll(be & ((1ull << lane) - 1ull));
+    sel[k] = valid[k] && (hv[k] < lo || (eq && pos < need));
+    eq_before += __popcll(be);
+  }
+}
+
 // Eligible features of a node (mtries / column sample / tree mask), ascending,
 // computed by ONE wave into flist; returns the count (wave-uniform).  F <=
 // 256: per-lane hashes in registers ranked with scalar lane reads; wider: the
@@ -4107,25 +4127,13 @@ __device__ __forceinline__ int direct_eligible(int node, int gid_i, const SplitP
       const int f = lane + 64 * k;
       hv[k] = (sampled && f < F) ? hash4(p.seed, key, (uint32_t)node, (uint32_t)f) : 0xffffffffu;
     }
-    int rank[4] = {0, 0, 0, 0};
-    if (p.mtries > 0) {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        if (64 * kk >= F) break;
-        const int jn = min(64, F - 64 * kk);
-        for (int jj = 0; jj < jn; ++jj) {
-          const uint32_t hj = (uint32_t)__builtin_amdgcn_readlane((int)hv[kk], jj);
-          const int j = 64 * kk + jj;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) rank[k] += (hj < hv[k]) || (hj == hv[k] && j < lane + 64 * k);
-        }
-      }
-    }
+    bool msel[4] = {true, true, true, true};
+    if (p.mtries > 0) mtries_select(hv, F, p.mtries, lane, msel);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int f = lane + 64 * k;
       bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]) && inter_ok(p, gid_i, f);
-      if (ok && sampled) ok = p.mtries > 0 ? rank[k] < p.mtries : u01(hv[k]) < p.col_rate;
+      if (ok && sampled) ok = p.mtries > 0 ? msel[k] : u01(hv[k]) < p.col_rate;
       const unsigned long long bal = __ballot(ok);
       if (ok) flist[nfl + __popcll(bal & ((1ull << lane) - 1ull))] = (FL)f;
       nfl += __popcll(bal);
@@ -4445,26 +4453,14 @@ __global__ __launch_bounds__(256) void seg_direct_wave_kernel(
     const int f = lane + 64 * k;
     hv[k] = (sampled && f < F) ? hash4(p.seed, key, (uint32_t)node, (uint32_t)f) : 0xffffffffu;
   }
-  int rank[4] = {0, 0, 0, 0};
-  if (p.mtries > 0) {
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      if (64 * kk >= F) break;
-      const int jn = min(64, F - 64 * kk);
-      for (int jj = 0; jj < jn; ++jj) {
-        const uint32_t hj = (uint32_t)__builtin_amdgcn_readlane((int)hv[kk], jj);
-        const int j = 64 * kk + jj;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) rank[k] += (hj < hv[k]) || (hj == hv[k] && j < lane + 64 * k);
-      }
-    }
-  }
+  bool msel[4] = {true, true, true, true};
+  if (p.mtries > 0) mtries_select(hv, F, p.mtries, lane, msel);
   int nfl = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int f = lane + 64 * k;
     bool ok = f < F && (tree_fmask == nullptr || tree_fmask[f]) && inter_ok(p, gid_i, f);
-    if (ok && sampled) ok = p.mtries > 0 ? rank[k] < p.mtries : u01(hv[k]) < p.col_rate;
+    if (ok && sampled) ok = p.mtries > 0 ? msel[k] : u01(hv[k]) < p.col_rate;
     const unsigned long long bal = __ballot(ok);
     if (ok) flist[nfl + __popcll(bal & ((1ull << lane) - 1ull))] = (short)f;
     nfl += __popcll(bal);
