@@ -181,16 +181,30 @@ __device__ __forceinline__ double l1_thresh(double g, double a) {
 // Gain of splitting a node with totals (G, S) into L = (GL, SL) and R = total
 // - L.  S is the weight/count (mode 0, H2O squared error) or the hessian
 // (mode 1, XGBoost).  Returns -inf if the split violates a constraint.
-__device__ __forceinline__ double split_gain(double GL, double SL, double G, double S, const SplitParams& p) {
+// the parent's term of the gain (G^2 / S, or t(G)^2 / (S + lambda)): the same
+// for every candidate of a node, so scans that see many features of one node
+// compute it once (split_gain_pt; identical bits to split_gain)
+__device__ __forceinline__ double parent_term(double G, double S, const SplitParams& p) {
+  if (p.mode == 0) return G * G / S;
+  const double tt = l1_thresh(G, p.alpha);
+  return tt * tt / (S + p.lambda_);
+}
+
+__device__ __forceinline__ double split_gain_pt(double GL, double SL, double G, double S, double pt,
+                                                const SplitParams& p) {
   const double GR = G - GL, SR = S - SL;
   if (p.mode == 0) {
     if (SL < p.min_rows || SR < p.min_rows || SL <= 0.0 || SR <= 0.0) return -INFINITY;
-    return GL * GL / SL + GR * GR / SR - G * G / S;
+    return GL * GL / SL + GR * GR / SR - pt;
   }
   if (SL < p.min_child_weight || SR < p.min_child_weight || SL <= 0.0 || SR <= 0.0) return -INFINITY;
   const double lam = p.lambda_;
-  const double tl = l1_thresh(GL, p.alpha), tr = l1_thresh(GR, p.alpha), tt = l1_thresh(G, p.alpha);
-  return 0.5 * (tl * tl / (SL + lam) + tr * tr / (SR + lam) - tt * tt / (S + lam)) - p.gamma;
+  const double tl = l1_thresh(GL, p.alpha), tr = l1_thresh(GR, p.alpha);
+  return 0.5 * (tl * tl / (SL + lam) + tr * tr / (SR + lam) - pt) - p.gamma;
+}
+
+__device__ __forceinline__ double split_gain(double GL, double SL, double G, double S, const SplitParams& p) {
+  return split_gain_pt(GL, SL, G, S, parent_term(G, S, p), p);
 }
 
 // Monotone constraint of the candidate split's feature (H2O / XGBoost
@@ -3764,7 +3778,7 @@ struct DirectBest {
 template <int NBT, bool PACKED>
 __device__ __forceinline__ void direct_scan_feature(const long long* __restrict__ h, int node, int f, int m,
                                                     double ig, double is, const SplitParams& p, int lane,
-                                                    DirectBest& best) {
+                                                    DirectBest& best, double& ptc) {
   constexpr int B = NBT <= 64 ? 1 : NBT / 64;
   constexpr int NA_LANE = (NBT - 1) / B, NA_K = (NBT - 1) % B;
   long long gi[B], si[B];
@@ -3804,14 +3818,18 @@ __device__ __forceinline__ void direct_scan_feature(const long long* __restrict_
   double fGL = 0, fSL = 0;
   const int mf = p.mono ? (int)p.mono[f] : 0;
   const uint32_t cand = p.hist_mode ? adaptive_candidates<NBT, B>(si, m, node, f, p) : 0xffffffffu;
+  // (tg, ts) are the node's exact totals, the same for every feature of the node:
+  // its parent term is computed by the first feature scanned (ptc NaN before)
+  if (ptc != ptc) ptc = parent_term(tg, ts, p);
+  const double pt = ptc;
 #pragma unroll
   for (int k = 0; k < B; ++k) {
     const int tt = lane * B + k;
     if (tt < m && tt < NBT - 1 && ((cand >> k) & 1u)) {
       const double sgd = (double)(eg + pg[k]) * ig, ssum = (double)(es + ps[k]) * is;
-      const double gA = mono_ok(mf, sgd, ssum, tg, ts, p) ? split_gain(sgd, ssum, tg, ts, p) : -INFINITY;
+      const double gA = mono_ok(mf, sgd, ssum, tg, ts, p) ? split_gain_pt(sgd, ssum, tg, ts, pt, p) : -INFINITY;
       const double gB = (ns > 0.0 && mono_ok(mf, sgd + ng, ssum + ns, tg, ts, p))
-                            ? split_gain(sgd + ng, ssum + ns, tg, ts, p) : -INFINITY;
+                            ? split_gain_pt(sgd + ng, ssum + ns, tg, ts, pt, p) : -INFINITY;
       if (gA > -INFINITY && (gA > fbg || (gA == fbg && 2 * tt < fbc))) { fbg = gA; fbc = 2 * tt; fGL = sgd; fSL = ssum; }
       if (gB > -INFINITY && (gB > fbg || (gB == fbg && 2 * tt + 1 < fbc))) {
         fbg = gB; fbc = 2 * tt + 1; fGL = sgd + ng; fSL = ssum + ns;
@@ -3998,6 +4016,7 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
   const int bat = packed ? 2 * batch : batch;                 // same LDS bytes
   DirectBest best;
   best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  double ptc = NAN;   // the node's parent gain term (direct_scan_feature)
   long long tg_row = 0, ts_row = 0;   // node totals (G_q, S_q), accumulated in the first batch
   for (int b0 = 0; b0 < nfl; b0 += bat) {
     const int nb = min(bat, nfl - b0);
@@ -4027,8 +4046,8 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
     // one wave per feature of the batch
     for (int q = wid; q < nb; q += DIRECT_WAVES) {
       const int f = flist[b0 + q];
-      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best);
-      else direct_scan_feature<NBT, false>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best);
+      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best, ptc);
+      else direct_scan_feature<NBT, false>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best, ptc);
     }
     __syncthreads();
   }
@@ -4263,9 +4282,10 @@ __global__ __launch_bounds__(256) void direct_dp_scan_kernel(
   const double ig = qscale[2], is = qscale[3];
   DirectBest best;
   best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  double ptc = NAN;   // the node's parent gain term (direct_scan_feature)
   for (int q = wid; q < nfl; q += 4) {
     const int f = flist[q];
-    direct_scan_feature<NBT, false>(h + 2 + (int64_t)q * 2 * NBT, node, f, nvb[f], ig, is, p, lane, best);
+    direct_scan_feature<NBT, false>(h + 2 + (int64_t)q * 2 * NBT, node, f, nvb[f], ig, is, p, lane, best, ptc);
   }
   if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
   __syncthreads();
@@ -4398,10 +4418,11 @@ __global__ __launch_bounds__(256) void seg_direct_chunk_kernel(
   }
   DirectBest best;
   best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  double ptc = NAN;   // the node's parent gain term (direct_scan_feature)
   for (int q = wid; q < nfl; q += 4) {
     const int f = flist[q];
-    if (packed) direct_scan_feature<NBT, true>(hist + q * NBT, node, f, nvb[f], ig, is, p, lane, best);
-    else direct_scan_feature<NBT, false>(hist + q * 2 * NBT, node, f, nvb[f], ig, is, p, lane, best);
+    if (packed) direct_scan_feature<NBT, true>(hist + q * NBT, node, f, nvb[f], ig, is, p, lane, best, ptc);
+    else direct_scan_feature<NBT, false>(hist + q * 2 * NBT, node, f, nvb[f], ig, is, p, lane, best, ptc);
   }
   if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
   __syncthreads();
@@ -4424,10 +4445,13 @@ __global__ __launch_bounds__(256) void seg_direct_chunk_kernel(
 // many more per CU.  Eligible features from per-lane hashes in registers
 // (F <= 256) ranked with scalar lane reads (no LDS round trips).
 constexpr int DIRECT_WAVE_F = 256;
+#ifndef H2OMX_DWAVE_WPE
+#define H2OMX_DWAVE_WPE 4
+#endif
 constexpr int DIRECT_WAVE_LDS = 8 * 1024;   // max histogram bytes per wave (8 / 10 / 16 KB measured alike, profiles/r5/drf_deep_ab.txt)
 
 template <int NBT>
-__global__ __launch_bounds__(256) void seg_direct_wave_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2OMX_DWAVE_WPE, 8))) void seg_direct_wave_kernel(
     const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
     const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
     const int* __restrict__ ctl, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
@@ -4473,6 +4497,7 @@ __global__ __launch_bounds__(256) void seg_direct_wave_kernel(
   const int bat = packed ? 2 * batch : batch;
   DirectBest best;
   best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  double ptc = NAN;   // the node's parent gain term (direct_scan_feature)
   long long tg_row = 0, ts_row = 0;
   wave_lds_sync();
   for (int b0 = 0; b0 < max(nfl, 1); b0 += bat) {
@@ -4495,8 +4520,8 @@ __global__ __launch_bounds__(256) void seg_direct_wave_kernel(
     wave_lds_sync();
     for (int q = 0; q < nb; ++q) {
       const int f = flist[b0 + q];
-      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best);
-      else direct_scan_feature<NBT, false>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best);
+      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best, ptc);
+      else direct_scan_feature<NBT, false>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best, ptc);
     }
     wave_lds_sync();
   }
