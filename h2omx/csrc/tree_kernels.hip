@@ -4318,8 +4318,11 @@ __global__ __launch_bounds__(256) void direct_empty_kernel(const int* __restrict
   out[i] = direct_node_split(b, 0, 0, 0.0, 0.0);
 }
 
+#ifndef H2OMX_DCHUNK_WPE
+#define H2OMX_DCHUNK_WPE 4
+#endif
 template <int NBT>
-__global__ __launch_bounds__(256) void seg_direct_chunk_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2OMX_DCHUNK_WPE, 8))) void seg_direct_chunk_kernel(
     const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
     const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
     const int* __restrict__ pc_first, const int* __restrict__ ctl, const int* __restrict__ nvb,
