@@ -207,6 +207,86 @@ __device__ __forceinline__ double split_gain(double GL, double SL, double G, dou
   return split_gain_pt(GL, SL, G, S, parent_term(G, S, p), p);
 }
 
+// ---------------------------------------------------------------------------
+// DPP wave primitives for the split scans.  The row_shr 1 / 2 / 4 / 8 steps,
+// then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3), run on the VALU
+// data path; the __shfl_* forms they replace go through ds_bpermute (an LDS
+// round trip per step), and a scan is a chain of six dependent steps.  Lanes
+// without a source (or outside the row mask) take the operation's identity.
+// ---------------------------------------------------------------------------
+template <int CTRL, int RM>
+__device__ __forceinline__ long long dpp_i64(long long v) {
+  const unsigned long long u = (unsigned long long)v;
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, RM, 0xf, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, RM, 0xf, false);
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+// inclusive prefix sum over the 64 lanes (exact int64: the same values as the
+// shfl_up scan)
+__device__ __forceinline__ long long wave_incl_scan_i64(long long x) {
+  x += dpp_i64<0x111, 0xf>(x);
+  x += dpp_i64<0x112, 0xf>(x);
+  x += dpp_i64<0x114, 0xf>(x);
+  x += dpp_i64<0x118, 0xf>(x);
+  x += dpp_i64<0x142, 0xa>(x);
+  x += dpp_i64<0x143, 0xc>(x);
+  return x;
+}
+
+__device__ __forceinline__ long long readlane_i64(long long v, int l) {
+  const unsigned long long u = (unsigned long long)v;
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  return __longlong_as_double(readlane_i64(__double_as_longlong(v), l));
+}
+
+// one step of the (larger gain, then smaller code) arg-max; identity (-inf, INT_MAX)
+template <int CTRL, int RM>
+__device__ __forceinline__ void argmax_step(double& g, int& c) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(g);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, RM, 0xf, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)0xFFF00000u, (int)(unsigned)(u >> 32), CTRL, RM, 0xf,
+                                                            false);
+  const int oc = __builtin_amdgcn_update_dpp(0x7fffffff, c, CTRL, RM, 0xf, false);
+  const double og = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+  if (og > g || (og == g && oc < c)) { g = og; c = oc; }
+}
+
+// wave arg-max of (g, c) (a total order: the result is the xor-butterfly's);
+// every lane returns it
+__device__ __forceinline__ void wave_argmax(double& g, int& c) {
+  argmax_step<0x111, 0xf>(g, c);
+  argmax_step<0x112, 0xf>(g, c);
+  argmax_step<0x114, 0xf>(g, c);
+  argmax_step<0x118, 0xf>(g, c);
+  argmax_step<0x142, 0xa>(g, c);
+  argmax_step<0x143, 0xc>(g, c);
+  g = readlane_f64(g, 63);
+  c = __builtin_amdgcn_readlane(c, 63);
+}
+
+// wave min (MAX = false) / max (MAX = true) of an int; every lane returns it
+template <bool MAX, int CTRL, int RM>
+__device__ __forceinline__ int minmax_step(int v) {
+  const int o = __builtin_amdgcn_update_dpp(MAX ? (int)0x80000000 : 0x7fffffff, v, CTRL, RM, 0xf, false);
+  return MAX ? max(v, o) : min(v, o);
+}
+template <bool MAX>
+__device__ __forceinline__ int wave_minmax_i32(int v) {
+  v = minmax_step<MAX, 0x111, 0xf>(v);
+  v = minmax_step<MAX, 0x112, 0xf>(v);
+  v = minmax_step<MAX, 0x114, 0xf>(v);
+  v = minmax_step<MAX, 0x118, 0xf>(v);
+  v = minmax_step<MAX, 0x142, 0xa>(v);
+  v = minmax_step<MAX, 0x143, 0xc>(v);
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
 // Monotone constraint of the candidate split's feature (H2O / XGBoost
 // monotone_constraints): +1 needs value(left) <= value(right), -1 the
 // reverse; child values from the split's (G, S) totals (S = W or H by mode).
@@ -1039,12 +1119,7 @@ __device__ __forceinline__ WaveBest feat_best_cat_wave(const long long* gi, cons
   }
   double bg = best_gain;
   int bc = best_code;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double og = __shfl_xor(bg, o, kWave);
-    const int oc = __shfl_xor(bc, o, kWave);
-    if (og > bg || (og == bg && oc < bc)) { bg = og; bc = oc; }
-  }
+  wave_argmax(bg, bc);
   WaveBest r;
   r.G = tg; r.S = ts;
   r.gain = (bc == 0x7fffffff) ? -INFINITY : bg;
@@ -1053,9 +1128,9 @@ __device__ __forceinline__ WaveBest feat_best_cat_wave(const long long* gi, cons
   uint32_t word = 0;
   if (bc != 0x7fffffff) {
     const unsigned long long own = __ballot(best_code == bc);
-    const int src = __ffsll((long long)own) - 1;
-    r.GL = __shfl(bGL, src, kWave);
-    r.SL = __shfl(bSL, src, kWave);
+    const int src = __builtin_amdgcn_readfirstlane(__ffsll((long long)own) - 1);
+    r.GL = readlane_f64(bGL, src);
+    r.SL = readlane_f64(bSL, src);
     // left set: every non-empty bin at or before the winner in (key, level) order
     const int wb = bc >> 1;
     double kown = key[0];
@@ -1163,11 +1238,8 @@ __device__ uint32_t adaptive_candidates(const long long* si, int m, int node, in
     const int t = lane * B + k;
     if (t < m && t < NBT - 1 && si[k] > 0) { lo = min(lo, t); hi = max(hi, t); }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = min(lo, __shfl_xor(lo, o, kWave));
-    hi = max(hi, __shfl_xor(hi, o, kWave));
-  }
+  lo = wave_minmax_i32<false>(lo);
+  hi = wave_minmax_i32<true>(hi);
   if (hi - lo < 1) return 0xffffffffu;   // no interior threshold
   const float* e = p.edges + (int64_t)f * NBT;
   const float* fr = p.frange + (int64_t)f * 4;
@@ -1248,7 +1320,7 @@ __device__ __forceinline__ WaveBest feat_scan_wave(long long* gi, long long* si,
   }
   // NA bin (NBT - 1) excluded from the running sums
   constexpr int NA_LANE = (NBT - 1) / B, NA_K = (NBT - 1) % B;
-  const long long ng_i = __shfl(gi[NA_K], NA_LANE, kWave), ns_i = __shfl(si[NA_K], NA_LANE, kWave);
+  const long long ng_i = readlane_i64(gi[NA_K], NA_LANE), ns_i = readlane_i64(si[NA_K], NA_LANE);
   if (lane == NA_LANE) { gi[NA_K] = 0; si[NA_K] = 0; }
   if constexpr (CAT) {   // instantiated only for data with categorical features
     if (p.catf != nullptr && p.catf[f])
@@ -1258,13 +1330,8 @@ __device__ __forceinline__ WaveBest feat_scan_wave(long long* gi, long long* si,
   long long pg[B], ps[B];
 #pragma unroll
   for (int k = 0; k < B; ++k) { lg += gi[k]; ls += si[k]; pg[k] = lg; ps[k] = ls; }
-  long long xg = lg, xs = ls;  // wave inclusive scan of lane totals
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const long long ag = __shfl_up(xg, o, kWave), as = __shfl_up(xs, o, kWave);
-    if (lane >= o) { xg += ag; xs += as; }
-  }
-  const long long tg_i = __shfl(xg, 63, kWave) + ng_i, ts_i = __shfl(xs, 63, kWave) + ns_i;
+  const long long xg = wave_incl_scan_i64(lg), xs = wave_incl_scan_i64(ls);  // wave inclusive scan of lane totals
+  const long long tg_i = readlane_i64(xg, 63) + ng_i, ts_i = readlane_i64(xs, 63) + ns_i;
   const long long eg = xg - lg, es = xs - ls;  // exclusive lane offset
   const double ng = (double)ng_i * ig, ns = (double)ns_i * is;
   const double tg = (double)tg_i * ig, ts = (double)ts_i * is;
@@ -1295,12 +1362,7 @@ __device__ __forceinline__ WaveBest feat_scan_wave(long long* gi, long long* si,
   }
   double bg = best_gain;
   int bc = best_code;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double og = __shfl_xor(bg, o, kWave);
-    const int oc = __shfl_xor(bc, o, kWave);
-    if (og > bg || (og == bg && oc < bc)) { bg = og; bc = oc; }
-  }
+  wave_argmax(bg, bc);
   WaveBest r;
   r.G = tg; r.S = ts;
   r.gain = (bc == 0x7fffffff) ? -INFINITY : bg;
@@ -1309,9 +1371,9 @@ __device__ __forceinline__ WaveBest feat_scan_wave(long long* gi, long long* si,
   if (bc != 0x7fffffff) {
     // unique owner of the winning threshold broadcasts its left totals
     const unsigned long long own = __ballot(best_code == bc);
-    const int src = __ffsll((long long)own) - 1;
-    r.GL = __shfl(bGL, src, kWave);
-    r.SL = __shfl(bSL, src, kWave);
+    const int src = __builtin_amdgcn_readfirstlane(__ffsll((long long)own) - 1);
+    r.GL = readlane_f64(bGL, src);
+    r.SL = readlane_f64(bSL, src);
   }
   return r;
 }
@@ -3797,19 +3859,14 @@ __device__ __forceinline__ void direct_scan_feature(const long long* __restrict_
       }
     }
   }
-  const long long ng_i = __shfl(gi[NA_K], NA_LANE, kWave), ns_i = __shfl(si[NA_K], NA_LANE, kWave);
+  const long long ng_i = readlane_i64(gi[NA_K], NA_LANE), ns_i = readlane_i64(si[NA_K], NA_LANE);
   if (lane == NA_LANE) { gi[NA_K] = 0; si[NA_K] = 0; }
   long long lg = 0, ls = 0;
   long long pg[B], ps[B];
 #pragma unroll
   for (int k = 0; k < B; ++k) { lg += gi[k]; ls += si[k]; pg[k] = lg; ps[k] = ls; }
-  long long xg = lg, xs = ls;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const long long ag = __shfl_up(xg, o, kWave), as = __shfl_up(xs, o, kWave);
-    if (lane >= o) { xg += ag; xs += as; }
-  }
-  const long long tg_i = __shfl(xg, 63, kWave) + ng_i, ts_i = __shfl(xs, 63, kWave) + ns_i;
+  const long long xg = wave_incl_scan_i64(lg), xs = wave_incl_scan_i64(ls);
+  const long long tg_i = readlane_i64(xg, 63) + ng_i, ts_i = readlane_i64(xs, 63) + ns_i;
   const long long eg = xg - lg, es = xs - ls;
   const double ng = (double)ng_i * ig, ns = (double)ns_i * is;
   const double tg = (double)tg_i * ig, ts = (double)ts_i * is;
@@ -3838,16 +3895,11 @@ __device__ __forceinline__ void direct_scan_feature(const long long* __restrict_
   }
   double bg = fbg;
   int bc = fbc;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double og = __shfl_xor(bg, o, kWave);
-    const int oc = __shfl_xor(bc, o, kWave);
-    if (og > bg || (og == bg && oc < bc)) { bg = og; bc = oc; }
-  }
+  wave_argmax(bg, bc);
   if (bc != 0x7fffffff) {
     const unsigned long long own = __ballot(fbc == bc);
-    const int src = __ffsll((long long)own) - 1;
-    const double GL = __shfl(fGL, src, kWave), SL = __shfl(fSL, src, kWave);
+    const int src = __builtin_amdgcn_readfirstlane(__ffsll((long long)own) - 1);
+    const double GL = readlane_f64(fGL, src), SL = readlane_f64(fSL, src);
     const long long key = ((long long)f << 32) | (unsigned)bc;
     if (bg > best.gain || (bg == best.gain && key < best.key)) { best.gain = bg; best.key = key; best.GL = GL; best.SL = SL; }
   }
