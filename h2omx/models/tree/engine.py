@@ -1021,9 +1021,10 @@ def global_row_base(n: int, comm) -> int:
 
 
 def trees_from_bytes(buf: np.ndarray, capacity: int) -> np.ndarray:
-    """View raw bytes as [ntrees][capacity] TREE_NODE_DTYPE records."""
-    arr = np.frombuffer(buf.tobytes(), dtype=TREE_NODE_DTYPE)
-    return arr.reshape(-1, capacity)
+    """View raw bytes as [ntrees][capacity] TREE_NODE_DTYPE records (a view of
+    the downloaded buffer, no copy: a 10-tree DRF depth-20 forest is ~400 MB,
+    and the former tobytes() copy cost ~30 ms a fit)."""
+    return np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1).view(TREE_NODE_DTYPE).reshape(-1, capacity)
 
 
 # fixed (max|g|, max h, max w) of unweighted rows per distribution: a tree whose
