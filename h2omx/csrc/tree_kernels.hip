@@ -234,6 +234,21 @@ __device__ __forceinline__ long long wave_incl_scan_i64(long long x) {
   return x;
 }
 
+__device__ __forceinline__ long long readlane_i64(long long v, int l);
+
+// wave sum (exact int64), every lane returns it
+__device__ __forceinline__ long long wave_sum_i64(long long x) { return readlane_i64(wave_incl_scan_i64(x), 63); }
+
+__device__ __forceinline__ int wave_sum_i32(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  return __builtin_amdgcn_readlane(x, 63);
+}
+
 __device__ __forceinline__ long long readlane_i64(long long v, int l) {
   const unsigned long long u = (unsigned long long)v;
   const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
@@ -268,6 +283,33 @@ __device__ __forceinline__ void wave_argmax(double& g, int& c) {
   argmax_step<0x143, 0xc>(g, c);
   g = readlane_f64(g, 63);
   c = __builtin_amdgcn_readlane(c, 63);
+}
+
+// the same for (gain, 64-bit key) pairs; identity (-inf, LLONG_MAX)
+template <int CTRL, int RM>
+__device__ __forceinline__ void argmax_key_step(double& g, long long& k) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(g);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, RM, 0xf, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)0xFFF00000u, (int)(unsigned)(u >> 32), CTRL, RM, 0xf,
+                                                            false);
+  const unsigned long long uk = (unsigned long long)k;
+  const unsigned klo = (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFFu, (int)(unsigned)uk, CTRL, RM, 0xf, false);
+  const unsigned khi = (unsigned)__builtin_amdgcn_update_dpp(0x7fffffff, (int)(unsigned)(uk >> 32), CTRL, RM, 0xf,
+                                                             false);
+  const double og = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+  const long long ok = (long long)(((unsigned long long)khi << 32) | klo);
+  if (og > g || (og == g && ok < k)) { g = og; k = ok; }
+}
+
+__device__ __forceinline__ void wave_argmax_key(double& g, long long& k) {
+  argmax_key_step<0x111, 0xf>(g, k);
+  argmax_key_step<0x112, 0xf>(g, k);
+  argmax_key_step<0x114, 0xf>(g, k);
+  argmax_key_step<0x118, 0xf>(g, k);
+  argmax_key_step<0x142, 0xa>(g, k);
+  argmax_key_step<0x143, 0xc>(g, k);
+  g = readlane_f64(g, 63);
+  k = readlane_i64(k, 63);
 }
 
 // wave min (MAX = false) / max (MAX = true) of an int; every lane returns it
@@ -1076,11 +1118,8 @@ __device__ __forceinline__ WaveBest feat_best_cat_wave(const long long* gi, cons
     tg_l += gi[k];
     ts_l += si[k];
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    tg_l += __shfl_xor(tg_l, o, kWave);
-    ts_l += __shfl_xor(ts_l, o, kWave);
-  }
+  tg_l = wave_sum_i64(tg_l);
+  ts_l = wave_sum_i64(ts_l);
   const double tg = (double)(tg_l + ng_i) * ig, ts = (double)(ts_l + ns_i) * is;
   const double ng = (double)ng_i * ig, ns = (double)ns_i * is;
   long long cg[B], cs[B];
@@ -1308,11 +1347,8 @@ __device__ __forceinline__ WaveBest feat_scan_wave(long long* gi, long long* si,
     long long tg_i = 0, ts_i = 0;
 #pragma unroll
     for (int k = 0; k < B; ++k) { tg_i += gi[k]; ts_i += si[k]; }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      tg_i += __shfl_xor(tg_i, o, kWave);
-      ts_i += __shfl_xor(ts_i, o, kWave);
-    }
+    tg_i = wave_sum_i64(tg_i);
+    ts_i = wave_sum_i64(ts_i);
     WaveBest r;
     r.G = (double)tg_i * ig; r.S = (double)ts_i * is;
     r.gain = -INFINITY; r.code = 0x7fffffff; r.GL = r.SL = 0.0;
@@ -1653,12 +1689,7 @@ __device__ __forceinline__ void node_best_wave(const FeatBest* __restrict__ fbes
     const long long k = ((long long)f << 32) | (unsigned)code;
     if (bf < 0 || gn > bg || (gn == bg && k < key)) { bg = gn; key = k; bf = f; }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double og = __shfl_xor(bg, off, kWave);
-    const long long ok = __shfl_xor(key, off, kWave);
-    if (og > bg || (og == bg && ok < key)) { bg = og; key = ok; }
-  }
+  wave_argmax_key(bg, key);
   if (lane == 0) {
     NodeSplit s;
     // S is W (mode 0) or H (mode 1); exact leaf (G, H, W) sums come from the
@@ -4088,11 +4119,8 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
     }
     __syncthreads();
     if (b0 == 0) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        tg_row += __shfl_xor(tg_row, o, kWave);
-        ts_row += __shfl_xor(ts_row, o, kWave);
-      }
+      tg_row = wave_sum_i64(tg_row);
+      ts_row = wave_sum_i64(ts_row);
       if (lane == 0) { tot_s[0][wid] = tg_row; tot_s[1][wid] = ts_row; }
     }
     // one wave per feature of the batch
@@ -4297,11 +4325,8 @@ __global__ __launch_bounds__(256) void direct_dp_hist_kernel(
     for (int j = t; j < nb * 2 * NBT; j += blockDim.x) out[2 + (int64_t)b0 * 2 * NBT + j] = hist[j];
     __syncthreads();
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    tg_row += __shfl_xor(tg_row, o, kWave);
-    ts_row += __shfl_xor(ts_row, o, kWave);
-  }
+  tg_row = wave_sum_i64(tg_row);
+  ts_row = wave_sum_i64(ts_row);
   if (lane == 0) { tot_s[0][wid] = tg_row; tot_s[1][wid] = ts_row; }
   __syncthreads();
   if (t == 0) {
@@ -4422,11 +4447,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2OMX_DCHUN
     direct_row_atomics<NBT>(row, flist, nfl, true, NBT, hist, gq, sq, cc,
                             ec.codes ? ec.codes + (int64_t)j * ec.stride : nullptr, ec.stride);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    tg_row += __shfl_xor(tg_row, o, kWave);
-    ts_row += __shfl_xor(ts_row, o, kWave);
-  }
+  tg_row = wave_sum_i64(tg_row);
+  ts_row = wave_sum_i64(ts_row);
   if (lane == 0) { tot_s[0][wid] = tg_row; tot_s[1][wid] = ts_row; }
   __syncthreads();
   long long tgq = tot_s[0][0] + tot_s[0][1] + tot_s[0][2] + tot_s[0][3];
@@ -4580,11 +4602,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2OMX_DWAVE
     }
     wave_lds_sync();
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    tg_row += __shfl_xor(tg_row, o, kWave);
-    ts_row += __shfl_xor(ts_row, o, kWave);
-  }
+  tg_row = wave_sum_i64(tg_row);
+  ts_row = wave_sum_i64(ts_row);
   if (lane == 0) {
     out[node] = direct_node_split(best, tg_row, ts_row, ig, is);
     if (ec.nodeq) ec.nodeq[node] = direct_feat_pos(flist, nfl, best.key);
@@ -4750,8 +4769,7 @@ __global__ __launch_bounds__(256) void part_count_wave_kernel(const uint8_t* __r
     }
     if (pi.leaf_children) cnt = 0;   // only inner splits count (as part_count)
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, kWave);
+  cnt = wave_sum_i32(cnt);
   if (lane == 0) pc_left[c] = cnt;
 }
 
@@ -4846,12 +4864,9 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
     const int nleaf = (pi.child >= 0) ? 2 : 1;
     for (int d = 0; d < nleaf; ++d) {
       long long a = sg[d], b = sh[d], e = sw[d];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        a += __shfl_xor(a, o, kWave);
-        b += __shfl_xor(b, o, kWave);
-        e += __shfl_xor(e, o, kWave);
-      }
+      a = wave_sum_i64(a);
+      b = wave_sum_i64(b);
+      e = wave_sum_i64(e);
       const int leaf = (pi.child >= 0) ? pi.child_gid + d : pi.gid;
       if (lane == 0 && leaf < cap) {
         if (a) atomicAdd(leaf_acc + 3 * leaf, (unsigned long long)a);
