@@ -600,6 +600,13 @@ class GpuBooster:
             self.ens.trees = trees_from_bytes(raw.cpu().numpy(), width // TREE_NODE_DTYPE.itemsize)
             if self.cats_dev:
                 self.ens.catbits = _stack_cats(self.cats_dev, width // TREE_NODE_DTYPE.itemsize)
+            else:
+                # the device node array raw_margin would rebuild from ens.trees (a copy
+                # and an upload of the whole forest: ~0.1 s for a 50-tree depth-20 DRF,
+                # paid by every cross-validation holdout prediction) is this one
+                e = self.ens
+                key = (e.ntrees * e.K, str(self.dev), e.trees.shape, id(e.trees), id(e.catbits))
+                e._dev_nodes = (key, raw.reshape(-1), None)
         self.ens._state = self.st
         if self.oob is not None:
             self.ens._oob = (self.oob[0][:, : self.bm.n], self.oob[1][: self.bm.n])

@@ -26,12 +26,16 @@ def main():
     pr = cProfile.Profile()
     t = time.perf_counter()
     pr.enable()
-    m = H2ORandomForestEstimator(ntrees=10, max_depth=20, seed=1).train(y="response", training_frame=fr)
+    ntrees = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    nfolds = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    m = H2ORandomForestEstimator(ntrees=ntrees, max_depth=20, seed=1, nfolds=nfolds).train(y="response",
+                                                                                          training_frame=fr)
     torch.cuda.synchronize()
     pr.disable()
-    print(f"DRF 10 trees: {time.perf_counter() - t:.3f} s, train_s {m.timings.get('train_s')}", flush=True)
+    print(f"DRF {ntrees} trees, nfolds {nfolds}: {time.perf_counter() - t:.3f} s, train_s {m.timings.get('train_s')}",
+          flush=True)
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(60)
+    pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(70)
     print(s.getvalue())
 
 
