@@ -1271,26 +1271,6 @@ __device__ uint32_t adaptive_candidates(const long long* si, int m, int node, in
   int mode = p.hist_mode;
   if (mode == 3) mode = (0x0211 >> (4 * (p.tree_index & 3))) & 15;   // UA, UA, Random, QuantilesGlobal
   if (mode == 0) return 0xffffffffu;
-  // this lane's fine edges and their neighbours, loaded before the range
-  // reductions so their latency overlaps them (the same floats as e[t], e[t -
-  // 1], e[t + 1] read after them)
-  const float* e = p.edges + (int64_t)f * NBT;
-  float eC[B], eL[B], eR[B];
-#pragma unroll
-  for (int k = 0; k < B; ++k) {
-    const int t = lane * B + k;
-    eC[k] = e[min(t, NBT - 1)];
-    eL[k] = e[max(t - 1, 0)];
-    eR[k] = e[min(t + 1, NBT - 1)];
-  }
-  // e[idx] for a wave-uniform idx, from the lane that loaded it
-  auto e_at = [&](int idx) -> float {
-    float v = eC[0];
-#pragma unroll
-    for (int k = 1; k < B; ++k)
-      if (idx % B == k) v = eC[k];
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), idx / B));
-  };
   int lo = 0x7fffffff, hi = -1;
 #pragma unroll
   for (int k = 0; k < B; ++k) {
@@ -1300,15 +1280,16 @@ __device__ uint32_t adaptive_candidates(const long long* si, int m, int node, in
   lo = wave_minmax_i32<false>(lo);
   hi = wave_minmax_i32<true>(hi);
   if (hi - lo < 1) return 0xffffffffu;   // no interior threshold
+  const float* e = p.edges + (int64_t)f * NBT;
   const float* fr = p.frange + (int64_t)f * 4;
   const bool exact = fr[2] != 0.0f;
   double lo_v, hi_v;
   if (exact) {
-    lo_v = (double)(lo < m - 1 ? e_at(lo) : fr[1]);
-    hi_v = (double)(hi < m - 1 ? e_at(hi) : fr[1]);
+    lo_v = (double)(lo < m - 1 ? e[lo] : fr[1]);
+    hi_v = (double)(hi < m - 1 ? e[hi] : fr[1]);
   } else {
-    lo_v = (double)(lo == 0 ? fr[0] : e_at(lo - 1));
-    hi_v = (double)(hi == m - 1 ? fr[1] : e_at(hi));
+    lo_v = (double)(lo == 0 ? fr[0] : e[lo - 1]);
+    hi_v = (double)(hi == m - 1 ? fr[1] : e[hi]);
   }
   const double span = hi_v - lo_v;
   if (!(span > 0.0) || !(span < INFINITY)) return 0xffffffffu;
@@ -1323,9 +1304,9 @@ __device__ uint32_t adaptive_candidates(const long long* si, int m, int node, in
     mL[k] = -INFINITY; mR[k] = INFINITY;
     if (t >= lo && t < hi) {
       inner |= 1u << k;
-      const double x = (double)eC[k];
-      if (t > lo) mL[k] = 0.5 * ((double)eL[k] + x);
-      if (t < hi - 1) mR[k] = 0.5 * (x + (double)eR[k]);
+      const double x = (double)e[t];
+      if (t > lo) mL[k] = 0.5 * ((double)e[t - 1] + x);
+      if (t < hi - 1) mR[k] = 0.5 * (x + (double)e[t + 1]);
     }
   }
   uint32_t hit = 0;
