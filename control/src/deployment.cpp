@@ -287,9 +287,11 @@ Json h2o_ingress(const DeploymentSpecification& s) {
   Json rules = Json::array();
   rules.push_back(rule);
   Json spec = kv("rules", rules);
-  if (v1 && !s.ingress_class.empty()) spec["ingressClassName"] = s.ingress_class;
+  // a class resolved from the cluster default is not named: the default applies
+  const bool named = !s.ingress_class.empty() && !s.ingress_class_from_cluster;
+  if (v1 && named) spec["ingressClassName"] = s.ingress_class;
   ing["spec"] = spec;
-  if (!v1 && !s.ingress_class.empty()) ing["metadata"]["annotations"]["kubernetes.io/ingress.class"] = s.ingress_class;
+  if (!v1 && named) ing["metadata"]["annotations"]["kubernetes.io/ingress.class"] = s.ingress_class;
   return ing;
 }
 
@@ -309,6 +311,29 @@ Json h2o_strip_prefix_middleware(const DeploymentSpecification& s, const std::st
 }
 
 bool valid_ingress_class(const std::string& c) { return c.empty() || c == "nginx" || c == "traefik"; }
+
+std::string default_ingress_class(KubeClient& client) {
+  Json lst;
+  try {
+    lst = client.list(kinds::IngressClass, "");
+  } catch (const std::exception&) {
+    return "";   // not readable (RBAC) or not served: keep the class-less nginx-style route
+  }
+  const Json* items = lst.find("items");
+  if (!items || !items->is_array()) return "";
+  for (auto& ic : items->as_array()) {
+    const Json* ann = ic.path("metadata.annotations");
+    // (keys with dots: looked up directly, not as a path)
+    const std::string key = "ingressclass.kubernetes.io/is-default-class";
+    if (!ann || !ann->is_object() || !ann->has(key) || !ann->at(key).is_string() || ann->at(key).as_string() != "true")
+      continue;
+    const std::string ctl = ic.get_string("spec.controller");
+    if (ctl.find("traefik") != std::string::npos) return "traefik";
+    if (ctl.find("nginx") != std::string::npos) return "nginx";
+    return "";
+  }
+  return "";
+}
 
 Json owner_reference(const Json& owner) {
   Json o = Json::object();
@@ -407,20 +432,32 @@ std::optional<std::string> any_path(const Json& ingress) {
   return p;
 }
 
-Json create_strip_prefix_middleware(KubeClient& client, const DeploymentSpecification& spec) {
+Json create_strip_prefix_middleware(KubeClient& client, const DeploymentSpecification& spec,
+                                    const std::function<void(Json&)>& decorate) {
   // traefik.io/v1alpha1 (Traefik >= 2.10); clusters with an earlier v2 only
   // serve the traefik.containo.us group (404 / 405 on the new one)
+  auto build = [&](const char* api) {
+    Json mw = h2o_strip_prefix_middleware(spec, api);
+    if (decorate) decorate(mw);
+    return mw;
+  };
   try {
-    return client.create(kinds::TraefikMiddleware, spec.ns, h2o_strip_prefix_middleware(spec, "traefik.io/v1alpha1"));
+    return client.create(kinds::TraefikMiddleware, spec.ns, build("traefik.io/v1alpha1"));
   } catch (const ApiError& e) {
     if (e.status != 404 && e.status != 405) throw;
   }
-  return client.create(kinds::TraefikMiddlewareLegacy, spec.ns,
-                       h2o_strip_prefix_middleware(spec, "traefik.containo.us/v1alpha1"));
+  return client.create(kinds::TraefikMiddlewareLegacy, spec.ns, build("traefik.containo.us/v1alpha1"));
 }
 
 void deploy_ingress(KubeClient& client, Deployment& d, int watch_timeout_s) {
-  const auto& spec = d.specification;
+  // no --ingress_class at deploy time: follow the cluster's default IngressClass
+  // (K3s, the reference CI's cluster, defaults to Traefik v2, which needs the
+  // Prefix + StripPrefix pair; reference templates.rs:104-106 annotated for both)
+  DeploymentSpecification spec = d.specification;
+  if (spec.ingress_class.empty()) {
+    spec.ingress_class = default_ingress_class(client);
+    spec.ingress_class_from_cluster = !spec.ingress_class.empty();
+  }
   const ResourceKind& k = ingress_kind(spec);
   if (spec.ingress_class == "traefik") d.middlewares.push_back(create_strip_prefix_middleware(client, spec));
   Json created;

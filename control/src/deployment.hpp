@@ -15,6 +15,7 @@
 // Ready, and the StatefulSet's serviceName matches the real service
 // (SURVEY.md §7.6 Q2/Q3).
 #pragma once
+#include <functional>
 
 #include <optional>
 #include <string>
@@ -42,6 +43,9 @@ struct DeploymentSpecification {
   // cluster default), "nginx" (same, ingressClassName nginx) or "traefik"
   // (Traefik v2 - K3s' default: Prefix path + a StripPrefix Middleware CR)
   std::string ingress_class;
+  // set (never persisted) when ingress_class was resolved from the cluster's
+  // default IngressClass: the Ingress then names no class (the default applies)
+  bool ingress_class_from_cluster = false;
 
   Json to_json() const;
   static DeploymentSpecification from_json(const Json& j);
@@ -65,6 +69,12 @@ Json h2o_ingress(const DeploymentSpecification& s);
 // Traefik v2 StripPrefix middleware for /<name> (ingress_class "traefik")
 Json h2o_strip_prefix_middleware(const DeploymentSpecification& s, const std::string& api_version);
 bool valid_ingress_class(const std::string& c);
+// Ingress flavour of the cluster's default IngressClass (annotation
+// ingressclass.kubernetes.io/is-default-class "true"): "traefik" for a Traefik
+// controller (K3s' bundled one: traefik.io/ingress-controller), "nginx" for
+// ingress-nginx, "" when no class is marked default, its controller is another
+// one, or the classes cannot be read (403 / 404 / older cluster).
+std::string default_ingress_class(KubeClient& client);
 // common labels / owner reference helpers used by the operator
 Json owner_reference(const Json& owner);
 
@@ -85,8 +95,11 @@ std::vector<std::string> undeploy_h2o(KubeClient& client, const Deployment& d);
 // Create the ingress, then watch it up to watch_timeout_s for a load-balancer
 // address; the last-seen object is appended to d.ingresses.
 void deploy_ingress(KubeClient& client, Deployment& d, int watch_timeout_s = 3);
-// Traefik StripPrefix middleware (traefik.io, falling back to traefik.containo.us)
-Json create_strip_prefix_middleware(KubeClient& client, const DeploymentSpecification& spec);
+// Traefik StripPrefix middleware (traefik.io, falling back to traefik.containo.us);
+// `decorate` edits the object before the create (the operator adds its
+// ownerReference so the middleware is garbage-collected with the CR)
+Json create_strip_prefix_middleware(KubeClient& client, const DeploymentSpecification& spec,
+                                    const std::function<void(Json&)>& decorate = {});
 
 std::optional<std::string> any_ip(const Json& ingress);
 std::optional<std::string> any_path(const Json& ingress);

@@ -23,6 +23,7 @@ const ResourceKind TraefikMiddleware{"/apis/traefik.io/v1alpha1", "middlewares",
 const ResourceKind TraefikMiddlewareLegacy{"/apis/traefik.containo.us/v1alpha1", "middlewares", "Middleware", true};
 const ResourceKind CRD{"/apis/apiextensions.k8s.io/v1", "customresourcedefinitions", "CustomResourceDefinition",
                        false};
+const ResourceKind IngressClass{"/apis/networking.k8s.io/v1", "ingressclasses", "IngressClass", false};
 }  // namespace kinds
 
 namespace {

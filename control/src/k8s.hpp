@@ -89,6 +89,7 @@ extern const ResourceKind H2O;       // h2o.ai/v1beta  h2os
 extern const ResourceKind TraefikMiddleware;         // traefik.io/v1alpha1 middlewares (Traefik >= 2.10)
 extern const ResourceKind TraefikMiddlewareLegacy;   // traefik.containo.us/v1alpha1 (earlier Traefik v2)
 extern const ResourceKind CRD;
+extern const ResourceKind IngressClass;              // networking.k8s.io/v1 ingressclasses (cluster-scoped)
 }  // namespace kinds
 
 class ApiError : public std::runtime_error {

@@ -153,6 +153,8 @@ class Reconciler {
     std::string phase, message;
     bool requeue = false;
     IngressState ing;
+    // kept if the ingress pass fails: the next pass still knows what to clean up
+    ing.middleware = cr.get_string("status.ingressMiddleware", "");
     try {
       reconcile_service(cr, ns, name, s, svc);
       requeue = reconcile_statefulset(ns, name, s, sts, hash, phase, message);
@@ -172,13 +174,17 @@ class Reconciler {
     const std::string ns = cr.get_string("metadata.namespace", "default");
     const std::string api = cr.get_string("spec.ingress.apiVersion", "networking.k8s.io/v1");
     const ResourceKind& ik = api == "networking.k8s.io/v1beta1" ? kinds::IngressV1beta1 : kinds::IngressV1;
-    for (auto& [k, n] : std::vector<std::pair<const ResourceKind*, std::string>>{
-             {&ik, name + "-ingress"}, {&kinds::StatefulSet, name + "-stateful-set"},
-             {&kinds::Service, name + "-service"}}) {
+    std::vector<std::pair<const ResourceKind*, std::string>> owned{
+        {&ik, name + "-ingress"}, {&kinds::StatefulSet, name + "-stateful-set"}, {&kinds::Service, name + "-service"}};
+    const std::string mw = cr.get_string("status.ingressMiddleware", "");
+    if (!mw.empty())
+      for (const ResourceKind* mk : {&kinds::TraefikMiddleware, &kinds::TraefikMiddlewareLegacy})
+        owned.emplace_back(mk, mw);
+    for (auto& [k, n] : owned) {
       try {
         c_.remove(*k, ns, n, "Background");
       } catch (const ApiError& e) {
-        if (e.status != 404) log(ns, name, std::string("cleanup: ") + e.what());
+        if (e.status != 404 && e.status != 405) log(ns, name, std::string("cleanup: ") + e.what());
       } catch (const std::exception& e) {
         log(ns, name, std::string("cleanup: ") + e.what());
       }
@@ -190,6 +196,7 @@ class Reconciler {
   struct IngressState {
     bool enabled = false, pending = false;
     std::string ip, path;
+    std::string middleware;   // the StripPrefix middleware this CR owns ("" = none)
   };
 
   void reconcile_service(const Json& cr, const std::string& ns, const std::string& name,
@@ -258,6 +265,11 @@ class Reconciler {
     s.ingress_api = cr.get_string("spec.ingress.apiVersion", "networking.k8s.io/v1");
     s.ingress_class = cr.get_string("spec.ingress.className", "");
     if (!valid_ingress_class(s.ingress_class)) s.ingress_class.clear();
+    if (st.enabled && s.ingress_class.empty()) {
+      // no className: the cluster's default IngressClass decides the route form
+      s.ingress_class = default_ingress_class(c_);
+      s.ingress_class_from_cluster = !s.ingress_class.empty();
+    }
     const ResourceKind& ik = s.ingress_api == "networking.k8s.io/v1beta1" ? kinds::IngressV1beta1 : kinds::IngressV1;
     const ResourceKind& other = &ik == &kinds::IngressV1 ? kinds::IngressV1beta1 : kinds::IngressV1;
     const std::string iname = s.name + "-ingress";
@@ -269,17 +281,22 @@ class Reconciler {
         if (e.status != 404 && e.status != 405) throw;
       }
     };
-    // Traefik v2 StripPrefix middleware (className traefik), owned like the ingress
+    // Traefik v2 StripPrefix middleware (Traefik mode), owned like the ingress
+    // (ownerReference: garbage-collected with the CR).  The operator only ever
+    // touches a middleware it created - recorded in status.ingressMiddleware -
+    // so a cluster without the Traefik CRDs, or an RBAC role without them,
+    // never sees a middleware request from a CR that does not use Traefik.
     const std::string mname = s.name + "-stripprefix";
+    const std::string recorded = cr.get_string("status.ingressMiddleware", "");
     auto drop_mw = [&]() {
+      if (recorded.empty()) return;
       for (const ResourceKind* mk : {&kinds::TraefikMiddleware, &kinds::TraefikMiddlewareLegacy}) {
         try {
-          if (c_.get_opt(*mk, ns, mname)) {
-            c_.remove(*mk, ns, mname, "Background");
-            log(ns, name, "deleted middleware " + mname);
-          }
+          c_.remove(*mk, ns, recorded, "Background");
+          log(ns, name, "deleted middleware " + recorded);
         } catch (const ApiError& e) {
-          if (e.status != 404 && e.status != 405) throw;
+          // 404 / 405: not served or already gone; 403: not ours to touch
+          if (e.status != 404 && e.status != 405 && e.status != 403) throw;
         }
       }
     };
@@ -289,17 +306,20 @@ class Reconciler {
       return st;
     }
     if (s.ingress_class == "traefik") {
+      // a Traefik-mode CR needs the middleware RBAC (deploy/operator.yaml grants
+      // it): a 403 here fails this CR with the apiserver's message
       bool have = false;
-      for (const ResourceKind* mk : {&kinds::TraefikMiddleware, &kinds::TraefikMiddlewareLegacy}) {
+      for (const ResourceKind* mk : {&kinds::TraefikMiddleware, &kinds::TraefikMiddlewareLegacy})
+        if (!have && c_.get_opt(*mk, ns, mname)) have = true;
+      if (!have) {
         try {
-          if (c_.get_opt(*mk, ns, mname)) have = true;
-        } catch (const ApiError&) {
+          create_strip_prefix_middleware(c_, s, [&](Json& mw) { adopt(mw, cr, hash); });
+          log(ns, name, "created middleware " + mname);
+        } catch (const ApiError& e) {
+          if (e.status != 409) throw;   // created meanwhile
         }
       }
-      if (!have) {
-        create_strip_prefix_middleware(c_, s);
-        log(ns, name, "created middleware " + mname);
-      }
+      st.middleware = mname;
     } else {
       drop_mw();
     }
@@ -367,6 +387,7 @@ class Reconciler {
         if (!topo.is_null()) st["topology"] = topo;
       }
     }
+    if (!ing.middleware.empty()) st["ingressMiddleware"] = ing.middleware;
     if (ing.enabled) {
       st["ingressIP"] = ing.ip;
       st["ingressPath"] = ing.path;
@@ -381,7 +402,7 @@ class Reconciler {
     // a merge patch only removes keys that are explicitly null: clear a stale
     // message / ingress address / topology (leader gone) from an earlier pass
     if (old && old->is_object())
-      for (const char* k : {"message", "ingressIP", "ingressPath", "connectURL", "topology"})
+      for (const char* k : {"message", "ingressIP", "ingressPath", "connectURL", "topology", "ingressMiddleware"})
         if (old->has(k) && !st.has(k)) pst[k] = Json();
     patch["status"] = pst;
     try {

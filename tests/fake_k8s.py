@@ -10,6 +10,18 @@ the h2o.ai/v1beta `H2O` custom resource.  Optional TLS and bearer-token auth,
 fault injection, and a load balancer that assigns an ingress IP shortly after
 creation (so `h2ok ingress` exercises its watch loop).
 
+Authorisation (optional, ``rbac_rules``): every request is checked against a
+list of ClusterRole rules (``{apiGroups, resources, verbs}``, the rules of
+``deploy/operator.yaml`` via :func:`cluster_role_rules`) the way the real
+apiserver's RBAC authoriser does - verb from the method (get / list / watch /
+create / update / patch / delete), resource incl. the ``status``
+subresource - and answered 403 Forbidden outside them.  Authorisation runs
+before routing, as on a real apiserver, so a forbidden request to an API group
+the cluster does not serve is 403, an allowed one 404.  ``served_groups``
+(None = every group) lists the API groups the cluster serves: a K3s cluster
+with its bundled Traefik serves ``traefik.io`` / ``traefik.containo.us``, a
+plain kind cluster does not.
+
 Deletion follows the real apiserver's propagation semantics: with
 ``propagationPolicy: Foreground`` the object stays (``deletionTimestamp`` +
 ``foregroundDeletion`` finalizer, MODIFIED event) until its dependents are
@@ -37,8 +49,12 @@ _PATH = re.compile(
 
 class FakeK8s:
     def __init__(self, token: str | None = None, tls: bool = False, tmpdir: str | None = None,
-                 ingress_ip_delay: float = 0.3, foreground_delay: float = 0.5):
+                 ingress_ip_delay: float = 0.3, foreground_delay: float = 0.5,
+                 rbac_rules: list[dict] | None = None, served_groups: set[str] | None = None):
         self.objects: dict[tuple, dict] = {}
+        self.rbac_rules = rbac_rules
+        self.served_groups = served_groups
+        self.forbidden: list[tuple[str, str, str]] = []   # (verb, group, resource) answered 403
         self.rv = 100
         self.lock = threading.Condition()
         self.events: list[tuple[int, tuple, str, dict]] = []
@@ -198,6 +214,20 @@ class FakeK8s:
                     return self._status(404, "NotFound", f"no route {u.path}")
                 plural, ns, name, sub = m["plural"], m["ns"], m["name"], m["sub"]
                 q = parse_qs(u.query)
+                group = m["group"] or ""
+                if fake.rbac_rules is not None:
+                    verb = _verb(method, name, q)
+                    resource = plural + ("/status" if sub else "")
+                    if not _allowed(fake.rbac_rules, verb, group, resource):
+                        fake.forbidden.append((verb, group, resource))
+                        gr = f"{resource}.{group}" if group else resource
+                        return self._status(403, "Forbidden",
+                                            f'{gr} "{name or ""}" is forbidden: User "system:serviceaccount:'
+                                            f'h2omx-system:h2omx-operator" cannot {verb} resource "{resource}" in '
+                                            f'API group "{group}"')
+                if fake.served_groups is not None and group and group not in fake.served_groups:
+                    return self._status(404, "NotFound", f"the server could not find the requested resource "
+                                                         f"({group})")
                 inj = fake.fail.get((method, plural))
                 if inj:
                     return self._status(inj, "InternalError", f"injected failure for {method} {plural}")
@@ -335,6 +365,33 @@ class FakeK8s:
                    "status": {"phase": "Running",
                               "conditions": [{"type": "Ready", "status": "True" if i == 0 else "False"}]}}
             self.put("pods", ns, pod)
+
+
+def _verb(method: str, name: str | None, q: dict) -> str:
+    if method == "GET":
+        if name:
+            return "get"
+        return "watch" if q.get("watch", ["0"])[0] in ("1", "true") else "list"
+    return {"POST": "create", "PUT": "update", "PATCH": "patch", "DELETE": "delete"}.get(method, method.lower())
+
+
+def _allowed(rules: list[dict], verb: str, group: str, resource: str) -> bool:
+    for r in rules:
+        groups, res, verbs = r.get("apiGroups", []), r.get("resources", []), r.get("verbs", [])
+        if ("*" in groups or group in groups) and ("*" in res or resource in res) and ("*" in verbs or verb in verbs):
+            return True
+    return False
+
+
+def cluster_role_rules(manifest: str, name: str | None = None) -> list[dict]:
+    """The rules of the ClusterRole in a multi-document manifest (deploy/operator.yaml)."""
+    import yaml
+
+    with open(manifest) as f:
+        for doc in yaml.safe_load_all(f):
+            if doc and doc.get("kind") == "ClusterRole" and (name is None or doc["metadata"]["name"] == name):
+                return doc.get("rules", [])
+    raise LookupError(f"no ClusterRole in {manifest}")
 
 
 def _merge(a, b):

@@ -607,3 +607,170 @@ def test_operator_traefik_ingress_from_cr(k8s, tmp_path):
     subprocess.run([OPERATOR, "--kubeconfig", k8s.cfg, "--once"], check=True, capture_output=True, timeout=60)
     assert k8s.get("middlewares", "default", "h2o-otr-stripprefix") is None
     assert k8s.get("ingresses", "default", "h2o-otr-ingress") is None
+
+
+# ---- RBAC-enforcing apiserver (deploy/operator.yaml's ClusterRole) -------------------
+_OPERATOR_YAML = os.path.join(ROOT, "deploy", "operator.yaml")
+_TRAEFIK_CLASS = {"apiVersion": "networking.k8s.io/v1", "kind": "IngressClass",
+                  "metadata": {"name": "traefik",
+                               "annotations": {"ingressclass.kubernetes.io/is-default-class": "true"}},
+                  "spec": {"controller": "traefik.io/ingress-controller"}}
+
+
+@pytest.fixture()
+def k3s_rbac(tmp_path):
+    """A K3s-like cluster: Traefik CRDs served, Traefik the default IngressClass,
+    and every request authorised against the operator's shipped ClusterRole."""
+    from tests.fake_k8s import cluster_role_rules
+
+    srv = FakeK8s(token="s3cr3t", rbac_rules=cluster_role_rules(_OPERATOR_YAML)).start()
+    srv.put("ingressclasses", "", copy_obj(_TRAEFIK_CLASS))
+    srv.cfg = srv.kubeconfig(str(tmp_path / "kubeconfig"), namespace="default")
+    yield srv
+    srv.stop()
+
+
+def copy_obj(o):
+    return json.loads(json.dumps(o))
+
+
+def _op_once(srv):
+    return subprocess.run([OPERATOR, "--kubeconfig", srv.cfg, "--once"], capture_output=True, text=True, timeout=60)
+
+
+def test_fake_apiserver_enforces_rbac(tmp_path):
+    """The enforcement itself: outside the rules a request is 403 (before
+    routing, so even an unserved group), inside them it is served."""
+    from tests.fake_k8s import cluster_role_rules
+
+    rules = [r for r in cluster_role_rules(_OPERATOR_YAML) if "middlewares" not in r["resources"]]
+    srv = FakeK8s(rbac_rules=rules, served_groups={"apps", "networking.k8s.io", "h2o.ai"}).start()
+    try:
+        import urllib.error
+        import urllib.request
+
+        def code(path, method="GET"):
+            try:
+                return urllib.request.urlopen(urllib.request.Request(srv.url + path, method=method)).status
+            except urllib.error.HTTPError as e:
+                return e.code
+
+        assert code("/apis/traefik.io/v1alpha1/namespaces/default/middlewares/x") == 403
+        assert code("/api/v1/namespaces/default/secrets/x") == 403
+        assert code("/api/v1/namespaces/default/services/x") == 404      # allowed, absent
+        assert code("/apis/networking.k8s.io/v1/ingressclasses") == 200
+        assert code("/apis/apps/v1/namespaces/default/statefulsets/x", "PUT") == 403   # no "update"
+        assert ("get", "traefik.io", "middlewares") in srv.forbidden
+    finally:
+        srv.stop()
+
+
+def test_operator_under_rbac_ingress_modes(k3s_rbac):
+    """Round-5 regression: with the Traefik CRDs present, every CR ended
+    phase Failed because the operator GET the middlewares its role did not
+    grant.  Under the shipped ClusterRole a CR with ingress disabled, an
+    nginx-class and a traefik-class CR all reach Ready; only the traefik CR
+    touches middlewares, and its middleware is owned by the CR (garbage-
+    collected with it)."""
+    srv = k3s_rbac
+    srv.put("h2os", "default", _cr("h2o-off", nodes=1))
+    srv.put("h2os", "default", _cr("h2o-ngx", nodes=1, ingress={"enabled": True, "className": "nginx"}))
+    srv.put("h2os", "default", _cr("h2o-trf", nodes=1, ingress={"enabled": True, "className": "traefik"}))
+    for _ in range(2):
+        r = _op_once(srv)
+        assert r.returncode == 0, r.stderr
+    assert srv.forbidden == [], srv.forbidden
+    for n in ("h2o-off", "h2o-ngx", "h2o-trf"):
+        st = srv.get("h2os", "default", n)["status"]
+        assert st["phase"] == "Ready", (n, st)
+    mw_paths = [p for m, p in srv.requests if "/middlewares" in p]
+    assert mw_paths and all("h2o-trf" in p or p.endswith("/middlewares") for p in mw_paths), mw_paths
+    ngx = srv.get("ingresses", "default", "h2o-ngx-ingress")
+    assert ngx["spec"]["ingressClassName"] == "nginx"
+    assert ngx["spec"]["rules"][0]["http"]["paths"][0]["path"] == "/h2o-ngx(/|$)(.*)"
+    mw = srv.get("middlewares", "default", "h2o-trf-stripprefix")
+    cr = srv.get("h2os", "default", "h2o-trf")
+    assert mw["metadata"]["ownerReferences"][0]["uid"] == cr["metadata"]["uid"]
+    assert cr["status"]["ingressMiddleware"] == "h2o-trf-stripprefix"
+    # ingress switched off: the recorded middleware goes, the status forgets it
+    cr["spec"]["ingress"]["enabled"] = False
+    srv.put("h2os", "default", cr, "MODIFIED")
+    assert _op_once(srv).returncode == 0
+    assert srv.get("middlewares", "default", "h2o-trf-stripprefix") is None
+    st = srv.get("h2os", "default", "h2o-trf")["status"]
+    assert st["phase"] == "Ready" and "ingressMiddleware" not in st
+    # back on, then the CR deleted: the fake's GC removes the owned middleware
+    cr = srv.get("h2os", "default", "h2o-trf")
+    cr["spec"]["ingress"]["enabled"] = True
+    srv.put("h2os", "default", cr, "MODIFIED")
+    assert _op_once(srv).returncode == 0
+    assert srv.get("middlewares", "default", "h2o-trf-stripprefix") is not None
+    srv.delete("h2os", "default", "h2o-trf")
+    assert srv.get("middlewares", "default", "h2o-trf-stripprefix") is None
+    assert srv.forbidden == [], srv.forbidden
+
+
+def test_operator_default_ingress_class_is_traefik(k3s_rbac):
+    """A CR that names no className follows the cluster's default IngressClass
+    (K3s: Traefik) - Prefix route + StripPrefix middleware, no class named."""
+    srv = k3s_rbac
+    srv.put("h2os", "default", _cr("h2o-dft", nodes=1, ingress={"enabled": True}))
+    assert _op_once(srv).returncode == 0
+    ing = srv.get("ingresses", "default", "h2o-dft-ingress")
+    path = ing["spec"]["rules"][0]["http"]["paths"][0]
+    assert path["path"] == "/h2o-dft" and path["pathType"] == "Prefix"
+    assert "ingressClassName" not in ing["spec"]
+    ann = {k: v for k, v in ing["metadata"]["annotations"].items() if not k.startswith("h2o.ai/")}
+    assert ann == {"traefik.ingress.kubernetes.io/router.middlewares": "default-h2o-dft-stripprefix@kubernetescrd"}
+    assert srv.get("middlewares", "default", "h2o-dft-stripprefix") is not None
+    assert srv.get("h2os", "default", "h2o-dft")["status"]["phase"] == "Ready"
+    assert srv.forbidden == []
+
+
+def test_operator_rbac_without_middleware_rule_fails_only_traefik(tmp_path):
+    """Negative control: a role without the middleware rule fails exactly the
+    Traefik CR (403 in its status message), not the others."""
+    from tests.fake_k8s import cluster_role_rules
+
+    rules = [r for r in cluster_role_rules(_OPERATOR_YAML) if "middlewares" not in r["resources"]]
+    srv = FakeK8s(rbac_rules=rules).start()
+    try:
+        srv.cfg = srv.kubeconfig(str(tmp_path / "kubeconfig"), namespace="default")
+        srv.put("h2os", "default", _cr("h2o-a", nodes=1))
+        srv.put("h2os", "default", _cr("h2o-t", nodes=1, ingress={"enabled": True, "className": "traefik"}))
+        assert _op_once(srv).returncode == 0
+        assert _op_once(srv).returncode == 0
+        assert srv.get("h2os", "default", "h2o-a")["status"]["phase"] == "Ready"
+        st = srv.get("h2os", "default", "h2o-t")["status"]
+        assert st["phase"] == "Failed" and "forbidden" in st["message"].lower(), st
+    finally:
+        srv.stop()
+
+
+def test_h2ok_ingress_follows_default_ingress_class(k3s_rbac, tmp_path):
+    """`h2ok ingress` with no --ingress_class on a cluster whose default class
+    is Traefik (K3s, the reference CI: rust.yml:18-20) emits the Prefix +
+    StripPrefix pair; undeploy removes both."""
+    srv = k3s_rbac
+    r = run(["deploy", "--cluster_size", "1", "--kubeconfig", srv.cfg, "-c", "h2o-k3s"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    desc = str(tmp_path / "h2o-k3s.h2ok")
+    r = run(["ingress", "-f", desc], tmp_path)
+    assert r.returncode == 0, r.stderr
+    ing = srv.get("ingresses", "default", "h2o-k3s-ingress")
+    path = ing["spec"]["rules"][0]["http"]["paths"][0]
+    assert path["path"] == "/h2o-k3s" and path["pathType"] == "Prefix"
+    assert "ingressClassName" not in ing["spec"]
+    mw = srv.get("middlewares", "default", "h2o-k3s-stripprefix")
+    assert mw["spec"] == {"stripPrefix": {"prefixes": ["/h2o-k3s"]}}
+    d = json.load(open(desc))
+    assert "ingress_class" not in d["specification"] and len(d["middlewares"]) == 1
+    r = run(["undeploy", "-f", desc], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert srv.list("middlewares") == [] and srv.list("ingresses") == []
+    # no default class (or classes unreadable): the nginx-style regex route, as before
+    srv.delete("ingressclasses", "", "traefik")
+    run(["deploy", "--cluster_size", "1", "--kubeconfig", srv.cfg, "-c", "h2o-nod"], tmp_path)
+    assert run(["ingress", "-f", str(tmp_path / "h2o-nod.h2ok")], tmp_path).returncode == 0
+    ing = srv.get("ingresses", "default", "h2o-nod-ingress")
+    assert ing["spec"]["rules"][0]["http"]["paths"][0]["path"] == "/h2o-nod(/|$)(.*)"
