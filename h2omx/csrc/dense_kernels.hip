@@ -663,9 +663,6 @@ __global__ __launch_bounds__(256) void glm_irls_wave_kernel(const float* __restr
 // per-lane partial linear predictors run in fp32 (x and beta are fp32, each
 // lane sums <= NB products; the 16-lane reduction stays fp64).
 // ---------------------------------------------------------------------------
-#ifndef GLM_ROW_F32
-#define GLM_ROW_F32 0   // fp32 binomial row math: measured no faster (profiles/r4/dense), fp64 kept
-#endif
 typedef __bf16 bf16x8_g __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4_g __attribute__((ext_vector_type(4)));
 
@@ -706,23 +703,7 @@ __device__ __forceinline__ void glm_row_binomial(double eta, double ov, double y
   dev = -2.0 * wv * (yv * lm + (1.0 - yv) * l1m);
 }
 
-// the same in fp32 (native v_exp_f32 / v_log_f32 / v_rcp_f32 paths): sw and
-// zz are rounded to fp32 anyway and their error stays within ~2 fp32 ulps of
-// the fp64 route; the deviance terms enter the fp64 accumulator
-__device__ __forceinline__ void glm_row_binomial_f32(double eta_d, float ov, float yv, float wv, float& sw, float& zz,
-                                                     double& dev) {
-  const float eta = (float)eta_d;
-  const float e = __expf(-fabsf(eta));
-  const float r1 = 1.0f / (1.0f + e);
-  const float mu = eta >= 0.f ? r1 : e * r1;
-  const float dmu = fmaxf(mu * (1.0f - mu), 1e-10f);
-  zz = (float)(eta_d - (double)ov) + (yv - mu) / dmu;
-  sw = sqrtf(wv * dmu);
-  const float l1p = log1pf(e);
-  const float lfloor = -34.538776f;   // log(1e-15)
-  const float lm = fmaxf(fminf(eta, 0.f) - l1p, lfloor), l1m = fmaxf(-fmaxf(eta, 0.f) - l1p, lfloor);
-  dev = -2.0 * (double)(wv * (yv * lm + (1.0f - yv) * l1m));
-}
+// (an fp32 variant of the binomial row math measured no faster: profiles/r4/dense)
 
 // FAM 1: binomial family with the logit link (branch-free row math, so the
 // previous chunk's MFMAs and this chunk's link math share one basic block and
@@ -858,11 +839,7 @@ __global__ __launch_bounds__(256) void glm_irls_split_kernel(const float* __rest
     float sw, zz;
     double dv;
     if (FAM == 1) {
-#if GLM_ROW_F32
-      glm_row_binomial_f32(eta, ov, yv, wv, sw, zz, dv);
-#else
       glm_row_binomial(eta, (double)ov, (double)yv, (double)wv, sw, zz, dv);
-#endif
     } else {
       double mu, dmu;
       glm_link(P, eta, mu, dmu);
@@ -1248,10 +1225,7 @@ __global__ __launch_bounds__(1024) void slab_sum_wide_kernel(const float* __rest
 // 256 threads, 128x128 block tile, each wave a 64x64 quadrant = 2x2 MFMA
 // tiles of 32x32, K staged 16 at a time through LDS as [k][m] / [k][n].
 // ===========================================================================
-#ifndef H2OMX_GEMM_GK
-#define H2OMX_GEMM_GK 32
-#endif
-constexpr int GB = 128, GK = H2OMX_GEMM_GK, GPAD = 4;
+constexpr int GB = 128, GK = 32, GPAD = 4;
 
 // One K-step of a 128 x 32 operand tile: global -> registers (float4 along
 // the contiguous dimension when the leading dimension allows it).
@@ -1566,9 +1540,7 @@ __global__ __launch_bounds__(256) void gemm64_kernel(const float* __restrict__ A
 //   -> bws[blockIdx.y][N] (the bias-gradient partials gemm_wgrad_bias folds).
 // ---------------------------------------------------------------------------
 constexpr int GW_T = 256;
-#ifndef GW_SPLIT
-#define GW_SPLIT 4   // k pairs (of 16 per K-step) before the FULL pipeline's LDS write / next loads
-#endif
+constexpr int GW_SPLIT = 4;   // k pairs (of 16 per K-step) before the FULL pipeline's LDS write / next loads
 // dY * act'(Y) given the activation's output Y (Rectifier / Tanh)
 __device__ __forceinline__ float act_grad(float g, float y, int act) {
   if (act == 1) return y > 0.0f ? g : 0.0f;
@@ -2410,11 +2382,8 @@ __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ W
 // ds_read_b128 group hit 16 distinct 16-byte bank slots).
 // ===========================================================================
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-#ifndef H2OMX_BF16_HK
-#define H2OMX_BF16_HK 64
-#endif
-constexpr int HB = 128, HK = H2OMX_BF16_HK, HPAD = 8, HROW = HK + HPAD;   // bf16 elements
-static int H2OMX_BF16_VARIANT = -1;  // tile-variant override for A/B runs (h2omx_gemm_bf16_variant)
+constexpr int HB = 128, HK = 64, HPAD = 8, HROW = HK + HPAD;   // bf16 elements
+static int g_bf16_variant = -1;  // tile-variant override for A/B runs (h2omx_gemm_bf16_variant)
 
 struct BfEpi {
   const float* bias;        // [N] or null
@@ -3255,7 +3224,7 @@ H2OMX_API int h2omx_gemm_bf16(const uint16_t* A, int lda, const uint16_t* B, int
   // other's LDS / global latency: measured fastest, scripts/gemm_bf16_micro.py);
   // 128 x 64 blocks of four where the output has at most one 64-column block.
   // Variant 0 (four 64 x 64 wave tiles) is kept for A/B runs.
-  const int variant = H2OMX_BF16_VARIANT >= 0 ? H2OMX_BF16_VARIANT : (N <= 64 ? 1 : 2);
+  const int variant = g_bf16_variant >= 0 ? g_bf16_variant : (N <= 64 ? 1 : 2);
   if (variant == 1) {
     const dim3 grid(cdiv(N, 64), cdiv(M, HB), splitk);
     hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 64, 32, 64>), grid, dim3(256), 0, stream, A, lda, B, ldb, M, N, K, ws,
@@ -3315,6 +3284,6 @@ H2OMX_API int h2omx_softmax_xent_bf16(const float* Z, const int* y, uint16_t* dZ
 }
 
 H2OMX_API int h2omx_gemm_bf16_variant(int v) {
-  H2OMX_BF16_VARIANT = v;
+  g_bf16_variant = v;
   return kOk;
 }

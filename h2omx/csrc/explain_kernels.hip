@@ -119,7 +119,7 @@ H2OMX_API int h2omx_tree_shap(const float* X, int64_t ld, int64_t n, int F, cons
   const size_t shm = lds ? (size_t)F * 256 * sizeof(float) : 0;
   const int4* lv = reinterpret_cast<const int4*>(leaves);
   const float4* el = reinterpret_cast<const float4*>(elems);
-#define H2OMX_SHAP(M)                                                                                           \
+#define LAUNCH_SHAP(M)                                                                                           \
   do {                                                                                                          \
     if (lds)                                                                                                    \
       hipLaunchKernelGGL((tree_shap_kernel<M, true>), dim3(grid), dim3(256), shm, stream, X, ld, n, F, lv,      \
@@ -128,9 +128,9 @@ H2OMX_API int h2omx_tree_shap(const float* X, int64_t ld, int64_t n, int F, cons
       hipLaunchKernelGGL((tree_shap_kernel<M, false>), dim3(grid), dim3(256), 0, stream, X, ld, n, F, lv,       \
                          nleaves, el, wtab, out, sets);                                                         \
   } while (0)
-  if (maxm <= 8) H2OMX_SHAP(8);
-  else if (maxm <= 16) H2OMX_SHAP(16);
-  else H2OMX_SHAP(32);
-#undef H2OMX_SHAP
+  if (maxm <= 8) LAUNCH_SHAP(8);
+  else if (maxm <= 16) LAUNCH_SHAP(16);
+  else LAUNCH_SHAP(32);
+#undef LAUNCH_SHAP
   return launch_status();
 }

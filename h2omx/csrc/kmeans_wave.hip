@@ -18,8 +18,8 @@
 //     (v_pk_fma_f32, two clusters per instruction); the centroids are
 //     wave-uniform, so one feature's KP values come through the scalar cache
 //     (transposed copy CTg [DP][KP], s_load) straight into the FMA's SGPR
-//     operand - no LDS traffic for them (KW_CT_SCALAR=0: LDS broadcast
-//     reads instead, measured LDS-bound); ||c||^2 - 2 dot -> argmin (lowest
+//     operand - no LDS traffic for them (an LDS broadcast copy measured
+//     LDS-bound); ||c||^2 - 2 dot -> argmin (lowest
 //     index on ties);
 //   * the tile is read conflict-free both ways: lane = row for the distances,
 //     and the cluster sums run transposed: lane = feature, rows
@@ -30,9 +30,6 @@
 // ---------------------------------------------------------------------------
 constexpr int KW_LD = 65;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-#ifndef KW_CT_SCALAR
-#define KW_CT_SCALAR 1
-#endif
 
 // LDS written by some lanes of a wave, read by other lanes of the same wave
 __device__ __forceinline__ void kw_wave_sync() {
@@ -51,11 +48,6 @@ __global__ __launch_bounds__(256) void kmeans_wave_kernel(const float* __restric
   // wave index made explicitly uniform: the chunk loop is then scalar control flow
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* Xs = kw_lds + wid * DP * KW_LD;
-#if !KW_CT_SCALAR
-  float* CT = kw_lds + 4 * DP * KW_LD;   // centroids transposed [f][KP], shared by the 4 waves
-  for (int j = threadIdx.x; j < DP * KP; j += blockDim.x) CT[j] = Cp[(j % KP) * DP + j / KP];
-  __syncthreads();
-#endif
   const int64_t nch = (n + 63) / 64;
   const int64_t W = (int64_t)gridDim.x * 4;
   int64_t ch = (int64_t)blockIdx.x * 4 + wid;
@@ -127,11 +119,7 @@ __global__ __launch_bounds__(256) void kmeans_wave_kernel(const float* __restric
       x2 = fmaf(v, v, x2);
 #pragma unroll
       for (int c4 = 0; c4 < KP / 4; ++c4) {
-#if KW_CT_SCALAR
         const float4 cv = *reinterpret_cast<const float4*>(CTg + co + 4 * c4);   // scalar-cache read
-#else
-        const float4 cv = *reinterpret_cast<const float4*>(CT + co + 4 * c4);   // broadcast read
-#endif
         const f32x2 vv{v, v};
         acc2[2 * c4] = __builtin_elementwise_fma(vv, f32x2{cv.x, cv.y}, acc2[2 * c4]);
         acc2[2 * c4 + 1] = __builtin_elementwise_fma(vv, f32x2{cv.z, cv.w}, acc2[2 * c4 + 1]);
@@ -370,7 +358,7 @@ H2OMX_API int h2omx_kmeans_wave(const float* X, int64_t ld, int64_t n, int d, co
                                 const float* cnp,
                                 int k, int kp, int dp, int n_wg, int* assign, float* slab, hipStream_t stream) {
   if (n_wg < 1 || n < 1 || d < 1 || k < 1 || k > kp || d > dp || dp % 16 != 0 || kp % 4 != 0) return kBadArg;
-  const size_t lds = ((size_t)4 * dp * KW_LD + (size_t)dp * kp) * sizeof(float);
+  const size_t lds = (size_t)4 * dp * KW_LD * sizeof(float);   // the 4 waves' row tiles
 #define KW_L(DP, KP)                                                                                        \
   if (dp == DP && kp == KP) {                                                                               \
     hipLaunchKernelGGL((kmeans_wave_kernel<DP, KP>), dim3(n_wg), dim3(256), lds, stream, X, ld, n, d, Cp, CTg, \

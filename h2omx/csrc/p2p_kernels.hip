@@ -8,11 +8,12 @@
 // hipIpcOpenMemHandle, exchanged over the rendezvous store), and one kernel
 // launch does the whole collective:
 //
-//   block b:  copy my chunk b into my symmetric buffer (parity = epoch & 1)
-//             -> system-scope release -> post epoch into flags[b][my rank] of
-//             every peer -> poll my flags[b][*] >= epoch -> system acquire ->
-//             out[chunk b] = sum over ranks r = 0 .. N-1 (fixed order) of
-//             sym_r[parity][chunk b]
+//   block b:  copy my chunk b into my symmetric buffer (parity = epoch & 1,
+//             write-through system-scope stores) -> every wave drains ->
+//             post epoch into flags[b][my rank] of every peer -> poll my
+//             flags[b][*] >= epoch -> out[chunk b] = sum over ranks
+//             r = 0 .. N-1 (fixed order) of sym_r[parity][chunk b]
+//             (system-scope loads; p2p_device.h: no cache maintenance)
 //
 // * Blocks are independent: block b only waits for chunk b of its peers, so
 //   there is no grid barrier and no co-residency requirement.
@@ -31,6 +32,7 @@
 //
 // All stores are vector-memory stores/atomics (global_*); flags live in
 // uncached device memory.
+// (Tensors above the buffer cap - DL gradient buckets - stay on RCCL.)
 #include "p2p_device.h"
 
 namespace {
@@ -64,10 +66,11 @@ __device__ __forceinline__ Vec<T> vcombine(const Vec<T>& a, const Vec<T>& b) {
   return r;
 }
 
+// a peer's (or this rank's) symmetric-buffer bytes: system-scope loads
 template <typename T>
 __device__ __forceinline__ Vec<T> vload(const void* p) {
   Vec<T> r;
-  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint4 u = p2pdev::ld_sys16(p);
   __builtin_memcpy(&r, &u, 16);
   return r;
 }
@@ -99,9 +102,10 @@ __device__ void reduce_chunk(const P2PDesc& d, char* data, int64_t parity_off, i
 template <typename T, int OP>
 __device__ void reduce_tail(const P2PDesc& d, T* data, int64_t parity_off, int64_t e0, int64_t e1) {
   for (int64_t e = e0 + threadIdx.x; e < e1; e += kThreads) {
-    T acc = reinterpret_cast<const T*>(static_cast<const char*>(d.sym[0]) + parity_off)[e];
+    T acc = p2pdev::ld_sys(reinterpret_cast<const T*>(static_cast<const char*>(d.sym[0]) + parity_off) + e);
     for (int r = 1; r < d.world; ++r)
-      acc = combine<T, OP>(acc, reinterpret_cast<const T*>(static_cast<const char*>(d.sym[r]) + parity_off)[e]);
+      acc = combine<T, OP>(acc, p2pdev::ld_sys(reinterpret_cast<const T*>(static_cast<const char*>(d.sym[r]) +
+                                                                         parity_off) + e));
     data[e] = acc;
   }
 }
@@ -123,9 +127,9 @@ __global__ __launch_bounds__(kThreads) void p2p_allreduce_kernel(P2PDesc d, T* d
   // 1. my chunk into my symmetric buffer
   char* mine = static_cast<char*>(d.sym[d.rank]) + parity_off;
   for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads)
-    *reinterpret_cast<uint4*>(mine + v * 16) = *reinterpret_cast<const uint4*>(reinterpret_cast<char*>(data) + v * 16);
+    p2pdev::st_sys16(mine + v * 16, *reinterpret_cast<const uint4*>(reinterpret_cast<char*>(data) + v * 16));
   if (tail)
-    for (int64_t i = t0 + threadIdx.x; i < nelem; i += kThreads) reinterpret_cast<T*>(mine)[i] = data[i];
+    for (int64_t i = t0 + threadIdx.x; i < nelem; i += kThreads) p2pdev::st_sys(reinterpret_cast<T*>(mine) + i, data[i]);
 
   // 2. + 3. publish chunk b to every rank and wait for every rank's chunk b
   p2pdev::post_wait(d, b, e);

@@ -543,10 +543,7 @@ struct GradFuse {
 };
 
 constexpr int CMP_STAGE_BYTES = 2048;   // per wave
-#ifndef H2OMX_HB_PF
-#define H2OMX_HB_PF 1
-#endif
-constexpr int HB_PF = H2OMX_HB_PF;     // feature code loads kept in flight per lane
+constexpr int HB_PF = 1;     // feature code loads kept in flight per lane
 
 // COP > 1 (level 0, PKM 1 / 3): every (slot, feature, bin) entry is COP
 // interleaved u64 copies, [bin][copy], lane l adding into copy l % COP: the
@@ -1271,6 +1268,9 @@ __device__ uint32_t adaptive_candidates(const long long* si, int m, int node, in
   int mode = p.hist_mode;
   if (mode == 3) mode = (0x0211 >> (4 * (p.tree_index & 3))) & 15;   // UA, UA, Random, QuantilesGlobal
   if (mode == 0) return 0xffffffffu;
+  // the node's occupied fine bins: weight plane > 0, i.e. its rows of
+  // POSITIVE weight (zero-weight rows widen no node range, as H2O's
+  // histograms skip them; tests/test_hist_adaptive.py zero-weight parity)
   int lo = 0x7fffffff, hi = -1;
 #pragma unroll
   for (int k = 0; k < B; ++k) {
@@ -1521,26 +1521,27 @@ __device__ __forceinline__ void rs_reduce_row(const unsigned long long* __restri
 }
 
 // waves 0 / 1 of the block: split scan of the two children of `slot` for
-// feature f from the completed built row in LDS
+// feature f from the completed built row in LDS.  Returns false for a wave
+// without a node (waves >= 2, or a child beyond the level); otherwise `node`
+// and its best threshold `w` (every lane holds it).
 template <int NBT, bool CAT>
-__device__ __forceinline__ void rs_scan_slot(const long long (*row)[NBT], int slot, int f,
+__device__ __forceinline__ bool rs_scan_node(const long long (*row)[NBT], int slot, int f,
                                              const long long* __restrict__ parent_full, long long* __restrict__ full,
                                              const int* __restrict__ ctl, const NodeLink* __restrict__ link,
                                              const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
-                                             const double* __restrict__ qscale, const SplitParams& p,
-                                             FeatBest* __restrict__ out) {
+                                             const double* __restrict__ qscale, const SplitParams& p, int& node,
+                                             WaveBest& w) {
   const int t = threadIdx.x;
   const int wid = t >> 6, lane = t & 63;
-  if (wid >= 2) return;
+  if (wid >= 2) return false;
   const int F = p.F;
   const int n = ctl[CTL_N];
-  const int node = 2 * slot + wid;   // level 0: slot 0 = the root, n = 1
-  if (node >= n) return;
+  node = 2 * slot + wid;   // level 0: slot 0 = the root, n = 1
+  if (node >= n) return false;
   const NodeLink lk = link[node];
-  if (lk.slot != slot && lk.sib_slot != slot) return;   // (not a child pair: cannot happen)
+  if (lk.slot != slot && lk.sib_slot != slot) return false;   // (not a child pair: cannot happen)
   const int gid = ctl[CTL_BASE] + node;
   const bool allowed = feat_allowed(tree_fmask, p, node, f, gid);
-  WaveBest w;
   if (!allowed && full == nullptr && f != 0) {
     w = wave_best_none();
   } else {
@@ -1566,7 +1567,7 @@ __device__ __forceinline__ void rs_scan_slot(const long long (*row)[NBT], int sl
     }
     w = feat_scan_wave<NBT, CAT>(gi, si, allowed, node, f, nvb, qscale[2], qscale[3], p);
   }
-  if (lane == 0) store_feat_best(out, (int64_t)node * F + f, w);
+  return true;
 }
 
 template <int NBT, bool CAT>
@@ -1581,64 +1582,132 @@ __global__ __launch_bounds__(1024) void reduce_split_kernel(
   const int slot = slot_lo + s;
   if (slot >= ctl[CTL_SLOTS]) return;   // whole workgroup
   rs_reduce_row<NBT>(partials, wgpg, fg, slot_cnt, s, f, red, row);
-  rs_scan_slot<NBT, CAT>(row, slot, f, parent_full, full, ctl, link, nvb, tree_fmask, qscale, p, out);
+  int node;
+  WaveBest w;
+  if (rs_scan_node<NBT, CAT>(row, slot, f, parent_full, full, ctl, link, nvb, tree_fmask, qscale, p, node, w) &&
+      (threadIdx.x & 63) == 0)
+    store_feat_best(out, (int64_t)node * p.F + f, w);
+}
+
+// ---- N ranks: reduce-scatter by feature + all-gather of the split records ----
+// Symmetric-buffer layout of the fused N-rank level (parallel/p2p.py sizes it):
+//   [parity 0 | parity 1] (cap bytes each): the histogram rows PUSHED to this
+//     rank - rows[slot][f / N][src] of ROW = 2 * NBT int64 for the features
+//     f = rank (mod N) this rank owns (the same features at every level, so
+//     the parent rows of the next level's sibling subtraction stay local);
+//   [split records: parity 0 | parity 1] (cap / 2 bytes each, from 2 * cap):
+//     FeatBest[node][F] of the level, all-gathered (every owner pushes its
+//     features' records to every rank).
+__device__ __forceinline__ FeatBest* p2p_fbest_table(const p2pdev::P2PDesc& d, int r, uint32_t e) {
+  return reinterpret_cast<FeatBest*>(static_cast<char*>(d.sym[r]) + 2 * d.cap + (int64_t)(e & 1u) * (d.cap / 2));
+}
+
+// lanes 0 .. N-1 each push the record into one rank's table (loopback: lane 0
+// into its own); 6 write-through 8-byte words, the pads are never read
+__device__ __forceinline__ void p2p_push_feat_best(const p2pdev::P2PDesc& d, uint32_t e, int64_t i, const WaveBest& w,
+                                                   int lane) {
+  const int nr = d.loopback ? 1 : d.world;
+  if (lane >= nr) return;
+  FeatBest* dst = p2p_fbest_table(d, d.loopback ? d.rank : lane, e) + i;
+  p2pdev::st_sys(&dst->gain, w.gain);
+  p2pdev::st_sys(&dst->GL, w.GL);
+  p2pdev::st_sys(&dst->SL, w.SL);
+  p2pdev::st_sys(&dst->G, w.G);
+  p2pdev::st_sys(&dst->S, w.S);
+  p2pdev::st_sys(reinterpret_cast<long long*>(&dst->code), (long long)(uint32_t)w.code);
 }
 
 // N-rank level in ONE launch (one pass: slot_lo = 0, slot_cnt = the level's
-// built slots): persistent blocks walk the (slot, feature) items, reduce each
-// item's slabs into this rank's symmetric buffer, exchange their chunk of
-// items with every peer (p2p_device.h: one flag post / poll per block), sum
-// the N rows in rank order (exact int64) and run the split scan - so an
-// N-rank level is hist_build -> reduce_split_p2p -> level_finalize, the same
-// three launches as one rank, and the level's all-reduce is no separate
-// kernel.  Items map to blocks identically on every rank (same grid).
+// built slots).  Persistent blocks walk the (slot, feature) items:
+//   A. every rank reduces its slabs of EVERY item (its own rows only) and
+//      pushes the exact int64 row to the item's owner, rank f % N (write-
+//      through stores into the owner's symmetric buffer), then posts;
+//   B. the owner waits for block b's posts of every rank, sums the N rows in
+//      rank order (local loads: every byte it reads was pushed to it) and
+//      runs the split scan of its items only, pushing each record to every
+//      rank's split table;
+//   C. the launch's last block posts this rank's done word; the level
+//      finalisation (node_best_finalize_p2p) waits for every rank's, then
+//      reads the all-gathered records.
+// So each rank scans 1/N of the level's items, reads no peer memory (the
+// cross-rank traffic is posted writes: its rows to their owners, its records
+// to every rank), and an N-rank level is hist_build -> reduce_split_p2p ->
+// level finalisation, the same three launches as one rank.  Items map to
+// blocks identically on every rank (same grid).
+// Loopback (one GPU standing in for N ranks; bench.py --loopback-ranks): the
+// rows go to slot src 0 and the owner reads that row N times; records of the
+// features this rank does not own are written as "none" (the same number of
+// record writes as a real rank's pushes), so loopback trees split on the
+// owned features only - the timing proxy of one rank's share.
 template <int NBT, bool CAT>
 __global__ __launch_bounds__(1024) void reduce_split_p2p_kernel(
     p2pdev::P2PDesc d, const unsigned long long* __restrict__ partials, int wgpg, int fg, int slot_cnt,
     const long long* __restrict__ parent_full, long long* __restrict__ full, const int* __restrict__ ctl,
     const NodeLink* __restrict__ link, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
-    const double* __restrict__ qscale, SplitParams p, FeatBest* __restrict__ out) {
+    const double* __restrict__ qscale, SplitParams p) {
   __shared__ long long red[1024 / (NBT / 2)][NBT / 2][4];
   __shared__ long long row[2][NBT];
   __shared__ uint32_t s_epoch;
   constexpr int64_t ROW = 2 * NBT;
   const int F = p.F, t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+  const int N = d.world, FL = (F + N - 1) / N;   // owned-feature slots per rank
   const int items = slot_cnt * F;
   const uint32_t e = p2pdev::begin_epoch(d, &s_epoch);
   const int n_slots = ctl[CTL_SLOTS];
-  long long* mine = reinterpret_cast<long long*>(p2pdev::parity_base(d, d.rank, e));
+  const int src = d.loopback ? 0 : d.rank;
+  // A: reduce + push every item's row to its owner
   for (int it = b; it < items; it += nb) {
     const int s = it / F, f = it % F;
     if (s >= n_slots) continue;   // block-uniform
     rs_reduce_row<NBT>(partials, wgpg, fg, slot_cnt, s, f, red, row);
+    const int owner = f % N;
+    long long* dst = reinterpret_cast<long long*>(p2pdev::parity_base(d, d.loopback ? d.rank : owner, e)) +
+                     (((int64_t)s * FL + f / N) * N + src) * ROW;
     if (t < NBT) {
-      mine[it * ROW + t] = row[0][t];
-      mine[it * ROW + NBT + t] = row[1][t];
+      p2pdev::st_sys(dst + t, row[0][t]);
+      p2pdev::st_sys(dst + NBT + t, row[1][t]);
     }
     __syncthreads();
   }
-  p2pdev::post_wait(d, b, e);
+  p2pdev::post(d, b, e);
+  // B: the owned items of this block
+  bool waited = false;
+  const long long* mine = reinterpret_cast<const long long*>(p2pdev::parity_base(d, d.rank, e));
   for (int it = b; it < items; it += nb) {
     const int s = it / F, f = it % F;
     if (s >= n_slots) continue;
+    if (f % N != d.rank) {
+      if (d.loopback && t < 2 * kWave) {   // stand-in for the owners' pushes: "none" records
+        const int node = 2 * s + (t >> 6);
+        if (node < ctl[CTL_N]) p2p_push_feat_best(d, e, (int64_t)node * F + f, wave_best_none(), t & 63);
+      }
+      continue;
+    }
+    if (!waited) {
+      p2pdev::wait(d, b, e);
+      waited = true;
+    }
     if (t < 2 * NBT) {
       // thread t owns (plane t / NBT, bin t % NBT): every rank's value loaded
       // before the rank-order sum
-      const int64_t o = it * ROW + t;
+      const long long* base = mine + ((int64_t)s * FL + f / N) * N * ROW + t;
       long long v[p2pdev::kMaxRanks];
 #pragma unroll
-      for (int r = 0; r < p2pdev::kMaxRanks; ++r)
-        v[r] = r < d.world ? reinterpret_cast<const long long*>(p2pdev::parity_base(d, r, e))[o] : 0ll;
+      for (int r = 0; r < p2pdev::kMaxRanks; ++r) v[r] = r < N ? p2pdev::ld_sys(base + (d.loopback ? 0 : r) * ROW) : 0ll;
       long long acc = v[0];
 #pragma unroll
       for (int r = 1; r < p2pdev::kMaxRanks; ++r) acc += v[r];
       row[t / NBT][t % NBT] = acc;
     }
     __syncthreads();
-    rs_scan_slot<NBT, CAT>(row, s, f, parent_full, full, ctl, link, nvb, tree_fmask, qscale, p, out);
+    int node;
+    WaveBest w;
+    if (rs_scan_node<NBT, CAT>(row, s, f, parent_full, full, ctl, link, nvb, tree_fmask, qscale, p, node, w))
+      p2p_push_feat_best(d, e, (int64_t)node * F + f, w, t & 63);
     __syncthreads();
   }
-  p2pdev::finish(d, nb, e);
+  // C: this rank's records all pushed -> done word to every rank
+  p2pdev::finish(d, nb, e, true);
 }
 
 // K5: best threshold of every (node, feature).  One wave per (node, feature)
@@ -1676,6 +1745,16 @@ __global__ __launch_bounds__(256) void split_find_kernel(const long long* __rest
 
 // Per-node arg-max over the features' best thresholds (gain desc, then
 // feature / bin / NA-direction asc): one wave per node, lane = feature.
+// SYS: the records were pushed by peers (N-rank split table): every load of
+// them is a system-scope load (p2p_device.h)
+template <bool SYS = false>
+__device__ __forceinline__ double fb_ld(const double* p) { return SYS ? p2pdev::ld_sys(p) : *p; }
+template <bool SYS = false>
+__device__ __forceinline__ int fb_code(const FeatBest* r) {
+  return SYS ? (int)p2pdev::ld_sys(reinterpret_cast<const uint32_t*>(&r->code)) : r->code;
+}
+
+template <bool SYS = false>
 __device__ __forceinline__ void node_best_wave(const FeatBest* __restrict__ fbest, int F, int node, int lane,
                                                NodeSplit* __restrict__ out) {
   const FeatBest* fb = fbest + (int64_t)node * F;
@@ -1683,8 +1762,8 @@ __device__ __forceinline__ void node_best_wave(const FeatBest* __restrict__ fbes
   long long key = 0x7fffffffffffffffLL;  // (feature, code) order for ties
   int bf = -1;
   for (int f = lane; f < F; f += 64) {
-    const double gn = fb[f].gain;
-    const int code = fb[f].code;
+    const double gn = fb_ld<SYS>(&fb[f].gain);
+    const int code = fb_code<SYS>(&fb[f]);
     if (code == 0x7fffffff || !(gn > -INFINITY)) continue;
     const long long k = ((long long)f << 32) | (unsigned)code;
     if (bf < 0 || gn > bg || (gn == bg && k < key)) { bg = gn; key = k; bf = f; }
@@ -1694,12 +1773,12 @@ __device__ __forceinline__ void node_best_wave(const FeatBest* __restrict__ fbes
     NodeSplit s;
     // S is W (mode 0) or H (mode 1); exact leaf (G, H, W) sums come from the
     // partition kernels, these only steer the split decisions
-    s.G = fb[0].G; s.H = fb[0].S; s.W = fb[0].S;
+    s.G = fb_ld<SYS>(&fb[0].G); s.H = fb_ld<SYS>(&fb[0].S); s.W = s.H;
     s.pad = 0;
     if (key != 0x7fffffffffffffffLL) {
       const int f = (int)(key >> 32), code = (int)(key & 0xffffffff);
       const FeatBest& c = fb[f];
-      s.gain = c.gain; s.GL = c.GL; s.HL = c.SL; s.WL = c.SL;
+      s.gain = fb_ld<SYS>(&c.gain); s.GL = fb_ld<SYS>(&c.GL); s.HL = fb_ld<SYS>(&c.SL); s.WL = s.HL;
       s.feat = f; s.bin = code >> 1; s.na_left = code & 1;
     } else {
       s.gain = -INFINITY; s.GL = s.HL = s.WL = 0.0;
@@ -1991,6 +2070,25 @@ __global__ __launch_bounds__(1024) void node_best_finalize_kernel(
   const int n = ctl[CTL_N];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int node = wid; node < n; node += nw) node_best_wave(fbest, p.F, node, lane, nsplit);
+  __syncthreads();
+  level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes, part, next_link, tree,
+                      tree_capacity);
+}
+
+// N ranks (after reduce_split_p2p): wait for every rank's done word, then the
+// same per-node arg-max over the all-gathered split table + finalisation.
+// Identical records on every rank -> identical trees.
+__global__ __launch_bounds__(1024) void node_best_finalize_p2p_kernel(
+    p2pdev::P2PDesc d, const int* __restrict__ ctl, int* __restrict__ ctl_next, SplitParams p,
+    const float* __restrict__ edges, const int* __restrict__ nvb, int nbt, int max_next_nodes,
+    PartInfo* __restrict__ part, NodeLink* __restrict__ next_link, TreeNode* __restrict__ tree, int tree_capacity,
+    NodeSplit* __restrict__ nsplit) {
+  __shared__ uint32_t s_epoch;
+  const uint32_t e = p2pdev::wait_done(d, &s_epoch);
+  const FeatBest* fbest = p2p_fbest_table(d, d.rank, e);
+  const int n = ctl[CTL_N];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int node = wid; node < n; node += nw) node_best_wave<true>(fbest, p.F, node, lane, nsplit);
   __syncthreads();
   level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes, part, next_link, tree,
                       tree_capacity);
@@ -2576,12 +2674,18 @@ __global__ __launch_bounds__(1024) void leaf_finalize_begin_kernel(
   if (threadIdx.x == 0) tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0, row_base, 0, tree_ctr);
 }
 
-// N ranks: the exact leaf sums exchanged inside the leaf finalisation (one
-// workgroup; p2p_device.h) - each rank's [0, 3 * total) sums go into its
-// symmetric buffer, every rank's are summed in rank order (exact int64), then
-// leaf_finalize (+ with `begin`, the chained next tree's tree_begin exactly as
-// leaf_finalize_begin_kernel).  The tree's leaf all-reduce is no separate launch.
-__global__ __launch_bounds__(1024) void leaf_finalize_p2p_kernel(
+// N ranks: the exact leaf sums exchanged inside the leaf finalisation.  Block
+// b owns the leaves gid = 256 * (b + k * nb) + [0, 256): it pushes this rank's
+// (G, H, W) sums of those leaves into slot `rank` of every rank's symmetric
+// buffer (write-through; loopback: its own slot 0 only), posts, waits for
+// every rank's block b, sums the N copies in rank order (local loads, exact
+// int64) and writes the leaf values - so no rank reads peer memory and the
+// exchange is spread over the grid.  With `begin` the sums are zeroed after
+// the read and the launch's last block (finish ticket: every block has read
+// qs and ctl_final) runs the chained next tree's tree_begin exactly as
+// leaf_finalize_begin_kernel.  The tree's leaf all-reduce is no separate launch.
+constexpr int LEAF_P2P_THREADS = 256;
+__global__ __launch_bounds__(LEAF_P2P_THREADS) void leaf_finalize_p2p_kernel(
     p2pdev::P2PDesc d, unsigned long long* __restrict__ acc, const int* __restrict__ ctl_final,
     double* __restrict__ qs, SplitParams p, TreeNode* __restrict__ tree, int cap, int begin,
     const unsigned int* __restrict__ stat_max, int mode, double qg, double qsr, int* __restrict__ ctl0,
@@ -2589,18 +2693,37 @@ __global__ __launch_bounds__(1024) void leaf_finalize_p2p_kernel(
   __shared__ uint32_t s_epoch;
   const uint32_t e = p2pdev::begin_epoch(d, &s_epoch);
   const int total = min(ctl_final[CTL_TOTAL], cap);
-  unsigned long long* mine = reinterpret_cast<unsigned long long*>(p2pdev::parity_base(d, d.rank, e));
-  for (int i = threadIdx.x; i < 3 * total; i += blockDim.x) mine[i] = acc[i];
-  p2pdev::post_wait(d, 0, e);
+  const int b = blockIdx.x, nb = gridDim.x, t = threadIdx.x;
+  const int64_t per_src = 3 * (int64_t)cap;   // one rank's sums in the receiving buffer
+  const int src = d.loopback ? 0 : d.rank;
+  const int nr = d.loopback ? 1 : d.world;
+  for (int c = b; c * LEAF_P2P_THREADS < total; c += nb) {
+    const int gid = c * LEAF_P2P_THREADS + t;
+    if (gid < total)
+      for (int r = 0; r < nr; ++r) {
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(
+                                      p2pdev::parity_base(d, d.loopback ? d.rank : r, e)) + src * per_src + 3 * gid;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) p2pdev::st_sys(dst + k, acc[3 * gid + k]);
+      }
+  }
+  p2pdev::post_wait(d, b, e);
   const double s4 = qs[4], s5 = qs[5], s6 = qs[6];
-  for (int gid = threadIdx.x; gid < total; gid += blockDim.x) {
+  const unsigned long long* mine = reinterpret_cast<const unsigned long long*>(p2pdev::parity_base(d, d.rank, e));
+  for (int c = b; c * LEAF_P2P_THREADS < total; c += nb) {
+    const int gid = c * LEAF_P2P_THREADS + t;
+    if (gid >= total) continue;
     long long a3[3] = {0, 0, 0};
     for (int r = 0; r < d.world; ++r) {
-      const unsigned long long* src = reinterpret_cast<const unsigned long long*>(p2pdev::parity_base(d, r, e));
+      const unsigned long long* sr = mine + (d.loopback ? 0 : r) * per_src + 3 * gid;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) a3[k] += (long long)src[3 * gid + k];
+      for (int k = 0; k < 3; ++k) a3[k] += (long long)p2pdev::ld_sys(sr + k);
     }
-    if (begin) { acc[3 * gid] = 0ull; acc[3 * gid + 1] = 0ull; acc[3 * gid + 2] = 0ull; }
+    // chained: the sums are zeroed for the next tree; otherwise they keep the
+    // GLOBAL sums, as after the all-reduce path (a later reader of leaf_acc sees
+    // the same values on every rank)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) acc[3 * gid + k] = begin ? 0ull : (unsigned long long)a3[k];
     TreeNode nd = tree[gid];
     if (nd.feat < 0) {
       const double G = (double)a3[0] / s4, H = (double)a3[1] / s5, W = (double)a3[2] / s6;
@@ -2609,8 +2732,9 @@ __global__ __launch_bounds__(1024) void leaf_finalize_p2p_kernel(
       tree[gid] = nd;
     }
   }
-  p2pdev::finish(d, 1, e);   // (block barrier first: qs and ctl_final read above)
-  if (begin && threadIdx.x == 0)
+  // (drains and block barrier first: qs and ctl_final read above)
+  const bool last = p2pdev::finish(d, nb, e);
+  if (begin && last && threadIdx.x == 0)
     tree_begin_scales(stat_max, mode, qg, qsr, qs, ctl0, link0, row_base, 0, tree_ctr);
 }
 
@@ -2831,83 +2955,83 @@ static int hist_build_launch(const uint8_t* codes, int64_t npad, const float* g,
   if (lds > 156 * 1024) return kBadArg;
   const int grid = n_groups * wgpg;
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
-#define H2OMX_HBK(NB, R, M, RT, C)                                                                           \
+#define LAUNCH_HBK(NB, R, M, RT, C)                                                                           \
   hipLaunchKernelGGL((hist_build_kernel<NB, R, M, RT, C>), dim3(grid), dim3(threads), lds, stream, codes, npad, \
                      g, s2, nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo, slot_cnt,  \
                      slot16, pk_buf, partials, pp, ctl_prev, nid_out, writer, gfz)
-#define H2OMX_HBKC(NB, R, M, CP)                                                                                \
+#define LAUNCH_HBKC(NB, R, M, CP)                                                                                \
   hipLaunchKernelGGL((hist_build_kernel<NB, R, M, false, false, CP>), dim3(grid), dim3(threads), lds, stream, codes, \
                      npad, g, s2, nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo,        \
                      slot_cnt, slot16, pk_buf, partials, pp, ctl_prev, nid_out, writer, gfz)
-#define H2OMX_HBK16(NB, M)                                                                                      \
+#define LAUNCH_HBK16(NB, M)                                                                                      \
   hipLaunchKernelGGL((hist_build_kernel<NB, 16, M, true, false, 1, true>), dim3(grid), dim3(threads), lds, stream, \
                      codes, npad, g, s2, nid, lk, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, wgpg, slot_lo,    \
                      slot_cnt, slot16, pk_buf, partials, pp, ctl_prev, nid_out, writer, gfz)
-#define H2OMX_HB(NB, R)                                            \
+#define LAUNCH_HB(NB, R)                                            \
   do {                                                             \
-    if (pkm == 0) H2OMX_HBK(NB, R, 0, false, false);               \
-    else if (pkm == 1 && cop == 8) H2OMX_HBKC(NB, R, 1, 8);        \
-    else if (pkm == 3 && cop == 8) H2OMX_HBKC(NB, R, 3, 8);        \
-    else if (pkm == 1 && cop == 4) H2OMX_HBKC(NB, R, 1, 4);        \
-    else if (pkm == 3 && cop == 4) H2OMX_HBKC(NB, R, 3, 4);        \
-    else if (pkm == 6 && cop == 8) H2OMX_HBKC(NB, R, 6, 8);        \
-    else if (pkm == 6 && cop == 4) H2OMX_HBKC(NB, R, 6, 4);        \
-    else if (pkm == 6) H2OMX_HBK(NB, R, 6, false, false);          \
-    else if (pkm == 1) H2OMX_HBK(NB, R, 1, false, false);          \
-    else if (pkm == 2 && route) H2OMX_HBK(NB, R, 2, true, false);  \
-    else if (pkm == 2) H2OMX_HBK(NB, R, 2, false, false);          \
-    else if (pkm == 3) H2OMX_HBK(NB, R, 3, false, false);          \
-    else if (pkm == 5) H2OMX_HBK(NB, R, 5, false, false);          \
-    else if (route) H2OMX_HBK(NB, R, 4, true, false);              \
-    else H2OMX_HBK(NB, R, 4, false, false);                        \
+    if (pkm == 0) LAUNCH_HBK(NB, R, 0, false, false);               \
+    else if (pkm == 1 && cop == 8) LAUNCH_HBKC(NB, R, 1, 8);        \
+    else if (pkm == 3 && cop == 8) LAUNCH_HBKC(NB, R, 3, 8);        \
+    else if (pkm == 1 && cop == 4) LAUNCH_HBKC(NB, R, 1, 4);        \
+    else if (pkm == 3 && cop == 4) LAUNCH_HBKC(NB, R, 3, 4);        \
+    else if (pkm == 6 && cop == 8) LAUNCH_HBKC(NB, R, 6, 8);        \
+    else if (pkm == 6 && cop == 4) LAUNCH_HBKC(NB, R, 6, 4);        \
+    else if (pkm == 6) LAUNCH_HBK(NB, R, 6, false, false);          \
+    else if (pkm == 1) LAUNCH_HBK(NB, R, 1, false, false);          \
+    else if (pkm == 2 && route) LAUNCH_HBK(NB, R, 2, true, false);  \
+    else if (pkm == 2) LAUNCH_HBK(NB, R, 2, false, false);          \
+    else if (pkm == 3) LAUNCH_HBK(NB, R, 3, false, false);          \
+    else if (pkm == 5) LAUNCH_HBK(NB, R, 5, false, false);          \
+    else if (route) LAUNCH_HBK(NB, R, 4, true, false);              \
+    else LAUNCH_HBK(NB, R, 4, false, false);                        \
   } while (0)
-#define H2OMX_HBCMP(NB)                                             \
+#define LAUNCH_HBCMP(NB)                                             \
   do {                                                              \
-    if (pkm == 2 && route) H2OMX_HBK(NB, 16, 2, true, true);        \
-    else if (pkm == 2) H2OMX_HBK(NB, 16, 2, false, true);           \
-    else if (route) H2OMX_HBK(NB, 16, 4, true, true);               \
-    else H2OMX_HBK(NB, 16, 4, false, true);                         \
+    if (pkm == 2 && route) LAUNCH_HBK(NB, 16, 2, true, true);        \
+    else if (pkm == 2) LAUNCH_HBK(NB, 16, 2, false, true);           \
+    else if (route) LAUNCH_HBK(NB, 16, 4, true, true);               \
+    else LAUNCH_HBK(NB, 16, 4, false, true);                         \
   } while (0)
   if (cmp) {
     switch (nbt) {
-      case 32: H2OMX_HBCMP(32); break;
-      case 64: H2OMX_HBCMP(64); break;
-      case 128: H2OMX_HBCMP(128); break;
-      case 256: H2OMX_HBCMP(256); break;
+      case 32: LAUNCH_HBCMP(32); break;
+      case 64: LAUNCH_HBCMP(64); break;
+      case 128: LAUNCH_HBCMP(128); break;
+      case 256: LAUNCH_HBCMP(256); break;
       default: return kBadArg;
     }
   } else if (nid16) {
     switch (nbt) {
-      case 32: if (pkm == 2) H2OMX_HBK16(32, 2); else H2OMX_HBK16(32, 4); break;
-      case 64: if (pkm == 2) H2OMX_HBK16(64, 2); else H2OMX_HBK16(64, 4); break;
-      case 128: if (pkm == 2) H2OMX_HBK16(128, 2); else H2OMX_HBK16(128, 4); break;
-      case 256: if (pkm == 2) H2OMX_HBK16(256, 2); else H2OMX_HBK16(256, 4); break;
+      case 32: if (pkm == 2) LAUNCH_HBK16(32, 2); else LAUNCH_HBK16(32, 4); break;
+      case 64: if (pkm == 2) LAUNCH_HBK16(64, 2); else LAUNCH_HBK16(64, 4); break;
+      case 128: if (pkm == 2) LAUNCH_HBK16(128, 2); else LAUNCH_HBK16(128, 4); break;
+      case 256: if (pkm == 2) LAUNCH_HBK16(256, 2); else LAUNCH_HBK16(256, 4); break;
       default: return kBadArg;
     }
   } else if (rows_per_lane == 16) {
     switch (nbt) {
-      case 32: H2OMX_HB(32, 16); break;
-      case 64: H2OMX_HB(64, 16); break;
-      case 128: H2OMX_HB(128, 16); break;
-      case 256: H2OMX_HB(256, 16); break;
+      case 32: LAUNCH_HB(32, 16); break;
+      case 64: LAUNCH_HB(64, 16); break;
+      case 128: LAUNCH_HB(128, 16); break;
+      case 256: LAUNCH_HB(256, 16); break;
       default: return kBadArg;
     }
   } else if (rows_per_lane == 8) {
     switch (nbt) {
-      case 32: H2OMX_HB(32, 8); break;
-      case 64: H2OMX_HB(64, 8); break;
-      case 128: H2OMX_HB(128, 8); break;
-      case 256: H2OMX_HB(256, 8); break;
+      case 32: LAUNCH_HB(32, 8); break;
+      case 64: LAUNCH_HB(64, 8); break;
+      case 128: LAUNCH_HB(128, 8); break;
+      case 256: LAUNCH_HB(256, 8); break;
       default: return kBadArg;
     }
   } else {
     return kBadArg;
   }
-#undef H2OMX_HB
-#undef H2OMX_HBK16
-#undef H2OMX_HBCMP
-#undef H2OMX_HBK
-#undef H2OMX_HBKC
+#undef LAUNCH_HB
+#undef LAUNCH_HBK16
+#undef LAUNCH_HBCMP
+#undef LAUNCH_HBK
+#undef LAUNCH_HBKC
   return launch_status();
 }
 
@@ -2968,7 +3092,7 @@ H2OMX_API int h2omx_split_find(const long long* built, const long long* parent_f
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
   FeatBest* o = reinterpret_cast<FeatBest*>(out);
   const dim3 grid(max_nodes, (p.F + 3) / 4);
-#define H2OMX_SF(NB)                                                                                          \
+#define LAUNCH_SF(NB)                                                                                          \
   if (p.catf != nullptr)                                                                                      \
     hipLaunchKernelGGL((split_find_kernel<NB, true>), grid, dim3(256), 0, stream, built, parent_full, full, ctl, \
                        lk, nvb, tree_fmask, qscale, p, o);                                                    \
@@ -2976,13 +3100,13 @@ H2OMX_API int h2omx_split_find(const long long* built, const long long* parent_f
     hipLaunchKernelGGL((split_find_kernel<NB, false>), grid, dim3(256), 0, stream, built, parent_full, full,    \
                        ctl, lk, nvb, tree_fmask, qscale, p, o)
   switch (nbt) {
-    case 32: H2OMX_SF(32); break;
-    case 64: H2OMX_SF(64); break;
-    case 128: H2OMX_SF(128); break;
-    case 256: H2OMX_SF(256); break;
+    case 32: LAUNCH_SF(32); break;
+    case 64: LAUNCH_SF(64); break;
+    case 128: LAUNCH_SF(128); break;
+    case 256: LAUNCH_SF(256); break;
     default: return kBadArg;
   }
-#undef H2OMX_SF
+#undef LAUNCH_SF
   return launch_status();
 }
 
@@ -2995,7 +3119,7 @@ H2OMX_API int h2omx_reduce_split(const unsigned long long* partials, int wgpg, i
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
   FeatBest* o = reinterpret_cast<FeatBest*>(out);
   const dim3 grid(slot_cnt, p.F);
-#define H2OMX_RS(NB)                                                                                              \
+#define LAUNCH_RS(NB)                                                                                              \
   if (p.catf != nullptr)                                                                                          \
     hipLaunchKernelGGL((reduce_split_kernel<NB, true>), grid, dim3(1024), 0, stream, partials, wgpg, fg, slot_lo, \
                        slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o);                      \
@@ -3003,23 +3127,25 @@ H2OMX_API int h2omx_reduce_split(const unsigned long long* partials, int wgpg, i
     hipLaunchKernelGGL((reduce_split_kernel<NB, false>), grid, dim3(1024), 0, stream, partials, wgpg, fg,         \
                        slot_lo, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o)
   switch (nbt) {
-    case 32: H2OMX_RS(32); break;
-    case 64: H2OMX_RS(64); break;
-    case 128: H2OMX_RS(128); break;
-    case 256: H2OMX_RS(256); break;
+    case 32: LAUNCH_RS(32); break;
+    case 64: LAUNCH_RS(64); break;
+    case 128: LAUNCH_RS(128); break;
+    case 256: LAUNCH_RS(256); break;
     default: return kBadArg;
   }
-#undef H2OMX_RS
+#undef LAUNCH_RS
   return launch_status();
 }
 
 // N-rank fused level (reduce_split_p2p_kernel); desc = host P2PDesc image.
 // One pass only (slot_cnt = the level's slots): the host routes multi-pass
-// levels through hist_reduce + all-reduce + split_find.
+// levels through hist_reduce + all-reduce + split_find.  The split records
+// land in the symmetric buffer's split table (h2omx_node_best_finalize_p2p
+// reads them); capacity: the pushed rows fit a parity, the records half of one.
 H2OMX_API int h2omx_reduce_split_p2p(const void* desc, const unsigned long long* partials, int wgpg, int fg,
                                      int slot_cnt, const long long* parent_full, long long* full, const int* ctl,
                                      const void* link, const int* nvb, const uint8_t* tree_fmask,
-                                     const double* qscale, const void* params, int nbt, void* out, int max_blocks,
+                                     const double* qscale, const void* params, int nbt, int max_blocks,
                                      hipStream_t stream) {
   if (desc == nullptr) return kBadArg;
   const p2pdev::P2PDesc d = *reinterpret_cast<const p2pdev::P2PDesc*>(desc);
@@ -3027,25 +3153,26 @@ H2OMX_API int h2omx_reduce_split_p2p(const void* desc, const unsigned long long*
   if (slot_cnt < 1 || wgpg < 1 || fg < 1 || p.F < 1) return kBadArg;
   if (d.world < 2 || d.world > p2pdev::kMaxRanks || d.rank < 0 || d.rank >= d.world) return kBadArg;
   const int64_t items = (int64_t)slot_cnt * p.F;
-  if (items * 2 * nbt * 8 > d.cap) return kBadArg;
+  const int64_t fl = (p.F + d.world - 1) / d.world;
+  if ((int64_t)slot_cnt * fl * d.world * 2 * nbt * 8 > d.cap) return kBadArg;
+  if ((int64_t)2 * slot_cnt * p.F * (int64_t)sizeof(FeatBest) > d.cap / 2) return kBadArg;
   const int nb = (int)std::min<int64_t>(items, std::min(std::max(max_blocks, 1), p2pdev::kMaxBlocks));
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
-  FeatBest* o = reinterpret_cast<FeatBest*>(out);
-#define H2OMX_RSP(NB)                                                                                             \
+#define LAUNCH_RSP(NB)                                                                                             \
   if (p.catf != nullptr)                                                                                          \
     hipLaunchKernelGGL((reduce_split_p2p_kernel<NB, true>), dim3(nb), dim3(1024), 0, stream, d, partials, wgpg,   \
-                       fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o);                  \
+                       fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p);                     \
   else                                                                                                            \
     hipLaunchKernelGGL((reduce_split_p2p_kernel<NB, false>), dim3(nb), dim3(1024), 0, stream, d, partials, wgpg,  \
-                       fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o)
+                       fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p)
   switch (nbt) {
-    case 32: H2OMX_RSP(32); break;
-    case 64: H2OMX_RSP(64); break;
-    case 128: H2OMX_RSP(128); break;
-    case 256: H2OMX_RSP(256); break;
+    case 32: LAUNCH_RSP(32); break;
+    case 64: LAUNCH_RSP(64); break;
+    case 128: LAUNCH_RSP(128); break;
+    case 256: LAUNCH_RSP(256); break;
     default: return kBadArg;
   }
-#undef H2OMX_RSP
+#undef LAUNCH_RSP
   return launch_status();
 }
 
@@ -3092,6 +3219,21 @@ H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_n
   return launch_status();
 }
 
+// N-rank level finalisation (after h2omx_reduce_split_p2p, same desc)
+H2OMX_API int h2omx_node_best_finalize_p2p(const void* desc, const int* ctl, int* ctl_next, const void* params,
+                                           const float* edges, const int* nvb, int nbt, int max_next_nodes,
+                                           void* part, void* next_link, void* tree, int tree_capacity,
+                                           void* nsplit, hipStream_t stream) {
+  if (desc == nullptr) return kBadArg;
+  const p2pdev::P2PDesc d = *reinterpret_cast<const p2pdev::P2PDesc*>(desc);
+  if (d.world < 2 || d.world > p2pdev::kMaxRanks || d.rank < 0 || d.rank >= d.world) return kBadArg;
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  hipLaunchKernelGGL(node_best_finalize_p2p_kernel, dim3(1), dim3(1024), 0, stream, d, ctl, ctl_next, p, edges, nvb,
+                     nbt, max_next_nodes, reinterpret_cast<PartInfo*>(part), reinterpret_cast<NodeLink*>(next_link),
+                     reinterpret_cast<TreeNode*>(tree), tree_capacity, reinterpret_cast<NodeSplit*>(nsplit));
+  return launch_status();
+}
+
 constexpr int PARTITION_BLOCKS = 8192;
 constexpr int PART_RPL = 8;    // rows per lane per step (16: 1.52 vs 1.47 ms/tree on HIGGS)
 
@@ -3121,21 +3263,21 @@ static int partition_launch(const uint8_t* codes, int64_t npad, int* nid, const 
     win_max = 0;
   }
   const size_t lds = (leaf_acc && win_max > 0) ? (size_t)3 * win_max * R * sizeof(unsigned long long) : 0;
-#define H2OMX_PK(PF, NM, WIN)                                                                                  \
+#define LAUNCH_PK(PF, NM, WIN)                                                                                  \
   hipLaunchKernelGGL((partition_kernel<PF, PART_RPL, NM>), dim3(blocks), dim3(256), lds, stream, codes, npad, nid, \
                      reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, ctl_cur,        \
                      ctl_next, WIN, R, slot16, nid_out, all_rows, Fm, yv, gp, y8)
   if (prefetch && leaf_acc) {
-    if (nidm == 3) H2OMX_PK(true, 3, win_max);
-    else if (nidm & 1) H2OMX_PK(true, 1, win_max);
-    else H2OMX_PK(true, 0, win_max);
+    if (nidm == 3) LAUNCH_PK(true, 3, win_max);
+    else if (nidm & 1) LAUNCH_PK(true, 1, win_max);
+    else LAUNCH_PK(true, 0, win_max);
   } else {
-    if (nidm == 3) H2OMX_PK(false, 3, leaf_acc ? win_max : 0);
-    else if (nidm == 1) H2OMX_PK(false, 1, leaf_acc ? win_max : 0);
-    else if (nidm == 2) H2OMX_PK(false, 2, leaf_acc ? win_max : 0);
-    else H2OMX_PK(false, 0, leaf_acc ? win_max : 0);
+    if (nidm == 3) LAUNCH_PK(false, 3, leaf_acc ? win_max : 0);
+    else if (nidm == 1) LAUNCH_PK(false, 1, leaf_acc ? win_max : 0);
+    else if (nidm == 2) LAUNCH_PK(false, 2, leaf_acc ? win_max : 0);
+    else LAUNCH_PK(false, 0, leaf_acc ? win_max : 0);
   }
-#undef H2OMX_PK
+#undef LAUNCH_PK
   return launch_status();
 }
 
@@ -3306,14 +3448,15 @@ H2OMX_API int h2omx_leaf_finalize_p2p(const void* desc, unsigned long long* acc,
   const p2pdev::P2PDesc d = *reinterpret_cast<const p2pdev::P2PDesc*>(desc);
   const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
   if (d.world < 2 || d.world > p2pdev::kMaxRanks || d.rank < 0 || d.rank >= d.world) return kBadArg;
-  if ((int64_t)cap * 3 * 8 > d.cap || p.gbound != nullptr) return kBadArg;
+  if ((int64_t)cap * 3 * 8 * (d.loopback ? 1 : d.world) > d.cap || p.gbound != nullptr) return kBadArg;
   double qg = 0.0, qsr = 0.0;
   if (begin) {
     if (max_rows_per_wg < 1 || max_rows_per_wg > ROWS_CAP || tree_ctr == nullptr) return kBadArg;
     qg = exp2(floor(log2(1073741824.0 / max_rows_per_wg)));
     qsr = exp2(floor(log2(2147483648.0 / max_rows_per_wg)));
   }
-  hipLaunchKernelGGL(leaf_finalize_p2p_kernel, dim3(1), dim3(1024), 0, stream, d, acc, ctl_final, qscale, p,
+  const int nb = std::min(p2pdev::kMaxBlocks, (cap + LEAF_P2P_THREADS - 1) / LEAF_P2P_THREADS);
+  hipLaunchKernelGGL(leaf_finalize_p2p_kernel, dim3(nb), dim3(LEAF_P2P_THREADS), 0, stream, d, acc, ctl_final, qscale, p,
                      reinterpret_cast<TreeNode*>(tree), cap, begin ? 1 : 0, stat_max, mode, qg, qsr, ctl0,
                      reinterpret_cast<NodeLink*>(link0), row_base, tree_ctr);
   return launch_status();
@@ -3851,10 +3994,7 @@ __global__ __launch_bounds__(256) void node_close_kernel(
 // node's NodeSplit directly (level_finalize_ns follows).
 // ---------------------------------------------------------------------------
 constexpr int DIRECT_LDS_BYTES = 96 * 1024;   // histogram batch (G and S int64 planes)
-#ifndef H2OMX_DIRECT_WAVES
-#define H2OMX_DIRECT_WAVES 4
-#endif
-constexpr int DIRECT_WAVES = H2OMX_DIRECT_WAVES;   // waves per node workgroup (<= 4)
+constexpr int DIRECT_WAVES = 4;   // waves per node workgroup (<= 4)
 // Nodes with fewer rows than this accumulate ONE packed 64-bit LDS atomic per
 // (row, feature) - (int32 G_q << 32) + uint32 S_q, as hist_build_kernel - instead
 // of a G and an S plane: per-row |G_q| <= 2^15 and S_q <= 2^16 keep |sum G_q| <
@@ -4395,11 +4535,8 @@ __global__ __launch_bounds__(256) void direct_empty_kernel(const int* __restrict
   out[i] = direct_node_split(b, 0, 0, 0.0, 0.0);
 }
 
-#ifndef H2OMX_DCHUNK_WPE
-#define H2OMX_DCHUNK_WPE 4
-#endif
 template <int NBT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2OMX_DCHUNK_WPE, 8))) void seg_direct_chunk_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void seg_direct_chunk_kernel(
     const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
     const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
     const int* __restrict__ pc_first, const int* __restrict__ ctl, const int* __restrict__ nvb,
@@ -4522,13 +4659,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2OMX_DCHUN
 // many more per CU.  Eligible features from per-lane hashes in registers
 // (F <= 256) ranked with scalar lane reads (no LDS round trips).
 constexpr int DIRECT_WAVE_F = 256;
-#ifndef H2OMX_DWAVE_WPE
-#define H2OMX_DWAVE_WPE 4
-#endif
 constexpr int DIRECT_WAVE_LDS = 8 * 1024;   // max histogram bytes per wave (8 / 10 / 16 KB measured alike, profiles/r5/drf_deep_ab.txt)
 
 template <int NBT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2OMX_DWAVE_WPE, 8))) void seg_direct_wave_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void seg_direct_wave_kernel(
     const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
     const float* __restrict__ s2, const int* __restrict__ seg_start, const int* __restrict__ seg_cnt,
     const int* __restrict__ ctl, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
@@ -4907,18 +5041,18 @@ H2OMX_API int h2omx_hist_build_seg(const uint8_t* codes_rm, int fp, const int* i
   const size_t lds = (size_t)fg * nbt * sizeof(unsigned long long);
   if (lds > 156 * 1024) return kBadArg;
   const int grid = ((max_chunks + 7) / 8) * 8 * n_groups;
-#define H2OMX_HBS(NB)                                                                                        \
+#define LAUNCH_HBS(NB)                                                                                        \
   hipLaunchKernelGGL(hist_build_seg_kernel<NB>, dim3(grid), dim3(threads), lds, stream, codes_rm, fp, idx, g, s2, \
                      seg_start, seg_cnt, hc_first, ctl, nvb, qscale, (uint32_t)salt, F, fg, n_groups, hc_rows, slab, \
                      gpos, crow, cpos)
   switch (nbt) {
-    case 32: H2OMX_HBS(32); break;
-    case 64: H2OMX_HBS(64); break;
-    case 128: H2OMX_HBS(128); break;
-    case 256: H2OMX_HBS(256); break;
+    case 32: LAUNCH_HBS(32); break;
+    case 64: LAUNCH_HBS(64); break;
+    case 128: LAUNCH_HBS(128); break;
+    case 256: LAUNCH_HBS(256); break;
     default: return kBadArg;
   }
-#undef H2OMX_HBS
+#undef LAUNCH_HBS
   return launch_status();
 }
 
@@ -4974,50 +5108,50 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
     if (max_elig * per_f_bytes > DIRECT_CHUNK_LDS || !pc_first || !slab || !tot_slab || !ticket) return kBadArg;
     hipLaunchKernelGGL(direct_empty_kernel, dim3((max_nodes + 255) / 256), dim3(256), 0, stream, seg_cnt, ctl, ns);
     const size_t lds = (size_t)max_elig * per_f_bytes;
-#define H2OMX_SDC(NB)                                                                                            \
+#define LAUNCH_SDC(NB)                                                                                            \
   hipLaunchKernelGGL(seg_direct_chunk_kernel<NB>, dim3(pad8(max_pc)), dim3(256), lds, stream, codes_rm, fp, idx, g, s2, \
                      seg_start, seg_cnt, pc_first, ctl, nvb, tree_fmask, qscale, (uint32_t)salt, p, max_elig, slab, \
                      tot_slab, ticket, ns, gpos, ec)
     switch (nbt) {
-      case 32: H2OMX_SDC(32); break;
-      case 64: H2OMX_SDC(64); break;
-      case 128: H2OMX_SDC(128); break;
-      case 256: H2OMX_SDC(256); break;
+      case 32: LAUNCH_SDC(32); break;
+      case 64: LAUNCH_SDC(64); break;
+      case 128: LAUNCH_SDC(128); break;
+      case 256: LAUNCH_SDC(256); break;
       default: return kBadArg;
     }
-#undef H2OMX_SDC
+#undef LAUNCH_SDC
     return launch_status();
   }
   if (mode == 1 && p.F <= DIRECT_WAVE_F) {
     const int batch = std::max(1, std::min(max_elig, DIRECT_WAVE_LDS / per_f_bytes));
     const size_t lds = (size_t)4 * batch * per_f_bytes;
-#define H2OMX_SDW(NB)                                                                                              \
+#define LAUNCH_SDW(NB)                                                                                              \
   hipLaunchKernelGGL(seg_direct_wave_kernel<NB>, dim3(pad8((max_nodes + 3) / 4)), dim3(256), lds, stream, codes_rm, fp, \
                      idx, g, s2, seg_start, seg_cnt, ctl, nvb, tree_fmask, qscale, (uint32_t)salt, p, batch, ns, gpos, ec)
     switch (nbt) {
-      case 32: H2OMX_SDW(32); break;
-      case 64: H2OMX_SDW(64); break;
-      case 128: H2OMX_SDW(128); break;
-      case 256: H2OMX_SDW(256); break;
+      case 32: LAUNCH_SDW(32); break;
+      case 64: LAUNCH_SDW(64); break;
+      case 128: LAUNCH_SDW(128); break;
+      case 256: LAUNCH_SDW(256); break;
       default: return kBadArg;
     }
-#undef H2OMX_SDW
+#undef LAUNCH_SDW
     return launch_status();
   }
   const int batch = std::max(1, std::min(max_elig, DIRECT_LDS_BYTES / per_f_bytes));
   const size_t lds = (size_t)batch * per_f_bytes;
-#define H2OMX_SD(NB)                                                                                             \
+#define LAUNCH_SD(NB)                                                                                             \
   hipLaunchKernelGGL(seg_direct_kernel<NB>, dim3(pad8(max_nodes)), dim3(64 * DIRECT_WAVES), lds, stream, codes_rm, fp, \
                      idx, g, s2,                                                                                 \
                      seg_start, seg_cnt, ctl, nvb, tree_fmask, qscale, (uint32_t)salt, p, batch, ns, gpos, ec)
   switch (nbt) {
-    case 32: H2OMX_SD(32); break;
-    case 64: H2OMX_SD(64); break;
-    case 128: H2OMX_SD(128); break;
-    case 256: H2OMX_SD(256); break;
+    case 32: LAUNCH_SD(32); break;
+    case 64: LAUNCH_SD(64); break;
+    case 128: LAUNCH_SD(128); break;
+    case 256: LAUNCH_SD(256); break;
     default: return kBadArg;
   }
-#undef H2OMX_SD
+#undef LAUNCH_SD
   return launch_status();
 }
 
@@ -5041,7 +5175,7 @@ H2OMX_API int h2omx_direct_dp(int phase, const uint8_t* codes_rm, int fp, const 
   const int batch = std::max(1, std::min(max_elig, DIRECT_LDS_BYTES / per_f_bytes));
   const size_t lds = (size_t)batch * per_f_bytes;
   NodeSplit* ns = reinterpret_cast<NodeSplit*>(nsplit);
-#define H2OMX_DDP(NB)                                                                                        \
+#define LAUNCH_DDP(NB)                                                                                        \
   if (phase == 0)                                                                                            \
     hipLaunchKernelGGL(direct_dp_hist_kernel<NB>, dim3(n_chunk), dim3(256), lds, stream, codes_rm, fp, idx,  \
                        g, s2, seg_start, seg_cnt, ctl, tree_fmask, qscale, p, batch, node0, max_elig, dh,   \
@@ -5050,13 +5184,13 @@ H2OMX_API int h2omx_direct_dp(int phase, const uint8_t* codes_rm, int fp, const 
     hipLaunchKernelGGL(direct_dp_scan_kernel<NB>, dim3(n_chunk), dim3(256), 0, stream, ctl, nvb, tree_fmask,  \
                        qscale, p, node0, max_elig, dh, ns)
   switch (nbt) {
-    case 32: H2OMX_DDP(32); break;
-    case 64: H2OMX_DDP(64); break;
-    case 128: H2OMX_DDP(128); break;
-    case 256: H2OMX_DDP(256); break;
+    case 32: LAUNCH_DDP(32); break;
+    case 64: LAUNCH_DDP(64); break;
+    case 128: LAUNCH_DDP(128); break;
+    case 256: LAUNCH_DDP(256); break;
     default: return kBadArg;
   }
-#undef H2OMX_DDP
+#undef LAUNCH_DDP
   return launch_status();
 }
 

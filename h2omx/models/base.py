@@ -295,6 +295,7 @@ class ModelBuilder:
         if unknown:
             raise ValueError(f"{self.algo}: unknown parameter(s) {sorted(unknown)}")
         self.params = {**self.COMMON, **self.DEFAULTS, **params}
+        self._explicit_params = frozenset(params)   # what the user set (vs defaults)
         self.model: Model | None = None
         self.comm = None
         self.x = None

@@ -26,7 +26,6 @@ from __future__ import annotations
 import contextlib
 import gc
 import math
-import os
 
 import numpy as np
 import torch
@@ -233,7 +232,7 @@ class _Bf16Mlp:
                            c_last=net.b(i, net.grad))
             if comm is not None and world > 1:
                 a, b = net.span(i)
-                handles.append(comm.all_reduce_async(net.grad[a:b]))
+                handles.append(comm.all_reduce_bucket_(net.grad[a:b]))
             if i == 0:
                 break
             D.gemm_bf16_nt(self.dZ[i], self.Wbt[i], B, f, self.wp[i], ymask=self.H[i], mask_act=self.act,
@@ -264,8 +263,13 @@ class _DLTrainer:
     """
 
     PROBE_STEPS = 32
-    # bias / output-layer gradient folds inside the ADADELTA kernel (fewer launches)
-    FOLD = os.environ.get("H2OMX_DL_FOLD", "1") == "1"
+    # path switches (class attributes; the GPU tests flip them with monkeypatch):
+    # bias / output-layer gradient folds inside the ADADELTA kernel (fewer
+    # launches), the fused latency-optimised step chain (ops/mlp.py), HIP-graph
+    # replay of the update
+    FOLD = True
+    FUSED = True
+    GRAPH = True
 
     def __init__(self, p_, net, X, Y, act, cls, auto, drop_in, hd, M, steps_per_epoch, comm, gen, gen_dev,
                  n_hidden, backward):
@@ -320,11 +324,11 @@ class _DLTrainer:
             self.mlp = _Bf16Mlp(net, act, M, dev)
         # fp32 small-batch updates (the estimator defaults' 256-row mini-batches) as
         # one chain of latency-optimised launches: forward, loss gradient, backward
-        # and ADADELTA (ops/mlp.py).  H2OMX_DL_FUSED=0 keeps the per-op path.
+        # and ADADELTA (ops/mlp.py).  FUSED = False keeps the per-op path.
         self.fused = None
         classes = net.layers[-1][1]
         regression = not cls and not auto
-        if (self.mlp is None and not self.sync_grad and os.environ.get("H2OMX_DL_FUSED", "1") == "1"
+        if (self.mlp is None and not self.sync_grad and self.FUSED
                 and not auto and (cls or self.loss_kind in ("automatic", "quadratic"))
                 and OM.FusedMlpStep.supported(net, act, classes, regression, drop_in > 0 or any(hd[:n_hidden]),
                                               self.adaptive, M)):
@@ -341,14 +345,18 @@ class _DLTrainer:
 
     def graph_eligible(self) -> bool:
         """the whole update replays as one HIP graph: device data, ADADELTA, no
-        dropout / L1 / max_w2 / per-step collectives (host-side state per step)"""
+        dropout / L1 / max_w2 / host-issued collectives (host-side state per
+        step).  Synchronous gradients qualify when their bucket all-reduces are
+        device-side P2P kernels (Comm.all_reduce_bucket_): an N-rank step is then
+        one graph replay too."""
+        sync_ok = not self.sync_grad or bool(getattr(self.comm, "graph_collectives", False))
         return (self.X.is_cuda and self.adaptive and self.drop_in == 0 and not any(self.hd) and self.l1 == 0
-                and not math.isfinite(float(self.p["max_w2"])) and not self.sync_grad
-                and os.environ.get("H2OMX_DL_GRAPH", "1") == "1")
+                and not math.isfinite(float(self.p["max_w2"])) and sync_ok
+                and self.GRAPH)
 
     # single-GPU graph replays: GROUP consecutive mini-batches per launch (the
     # inter-graph gap and the per-step index copy paid once per group)
-    GROUP = int(os.environ.get("H2OMX_DL_GRAPH_STEPS", "8"))
+    GROUP = 8
 
     def step_deferred(self) -> None:
         """step(), possibly held back so GROUP steps replay as one graph;
@@ -811,7 +819,7 @@ class H2ODeepLearningEstimator(ModelBuilder):
                     D.bias_grad(dZ, out=net.b(i, net.grad))
             if comm is not None and world > 1:
                 a, b = net.span(i)
-                handles.append(comm.all_reduce_async(net.grad[a:b]))
+                handles.append(comm.all_reduce_bucket_(net.grad[a:b]))
             if i == 0:
                 break
             with OD.workspace_ns(i) if layer_ns else contextlib.nullcontext():

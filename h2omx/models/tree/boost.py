@@ -373,6 +373,7 @@ class GpuBooster:
         self._bounds = None
         if self.K == 1 and self.st.w is None and self.dist in GRAD_BOUNDS:
             self._bounds = grad_bounds_tensor(self.dist, self.dev)
+        self._stall = self._stall_plan()
         if self.fused:
             pass
         elif self.K == 1:
@@ -387,15 +388,23 @@ class GpuBooster:
         if c is not None and c.world_size > 1 and hasattr(c, "check_health"):
             c.check_health()
 
-    def _fault_stall(self):
-        """Test-only fault injection: H2OMX_FAULT_STALL="rank:tree:seconds"
-        makes that rank sleep before enqueueing that tree, past the peers' P2P timeout."""
-        spec = os.environ.get("H2OMX_FAULT_STALL")
+    # Test-only fault injection, resolved once per booster:
+    # (tree, seconds) for this rank, or None.  tests/_p2p_fault_worker.py sets it
+    # through FAULT_STALL_SPEC ("rank:tree:seconds"); the production step only
+    # compares a cached None.
+    FAULT_STALL_SPEC: str | None = None
+
+    def _stall_plan(self):
+        spec = type(self).FAULT_STALL_SPEC
         c = self.builder.comm
-        if spec and c is not None:
-            r, t, sec = spec.split(":")
-            if int(r) == c.rank and int(t) == self.t:
-                time.sleep(float(sec))
+        if not spec or c is None:
+            return None
+        r, t, sec = spec.split(":")
+        return (int(t), float(sec)) if int(r) == c.rank else None
+
+    def _fault_stall(self):
+        if self._stall is not None and self._stall[0] == self.t:
+            time.sleep(self._stall[1])
 
     def flush(self):
         """Bring the margins up to date (fused mode applies each tree inside the
@@ -704,8 +713,8 @@ class TreeGraph:
     default when peer memory maps) the collectives are kernels of the step, so
     the whole N-rank step is ONE graph replay with no host-issued collective.
     Otherwise the step is captured in SEGMENTS split at the collectives, which
-    are issued eagerly between segment replays (works with any backend);
-    ``H2OMX_GRAPH_COLLECTIVES=1`` captures RCCL calls inside one graph instead.
+    are issued eagerly between segment replays (works with any backend; a Comm
+    whose ``graph_collectives`` is set has them captured inside one graph).
     """
 
     # finished trees go to a device ring of RING slots inside the graph
@@ -713,7 +722,7 @@ class TreeGraph:
     # freeze() swaps them for views of one ring snapshot (every RING trees, and
     # whenever the trees are read)
     RING = 64
-    GROUP = 4      # trees per replay of the multi-tree graph (H2OMX_GRAPH_TREES)
+    GROUP = 4      # trees per replay of the multi-tree graph
 
     def __init__(self, booster):
         self.gb = booster
@@ -739,9 +748,8 @@ class TreeGraph:
         self.ring = torch.zeros((self.RING, b.tree_buf.numel()), dtype=torch.uint8, device=dev)
         multi = self.comm is not None and self.comm.world_size > 1
         # P2P collectives are ordinary kernels: the whole step is one graph.  RCCL
-        # calls become segment boundaries unless H2OMX_GRAPH_COLLECTIVES=1
-        segmented = (multi and not getattr(self.comm, "graph_collectives", False)
-                     and os.environ.get("H2OMX_GRAPH_COLLECTIVES", "0") != "1")
+        # calls become segment boundaries
+        segmented = multi and not getattr(self.comm, "graph_collectives", False)
         self.pool = torch.cuda.graph_pool_handle()
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
@@ -783,7 +791,7 @@ class TreeGraph:
                     self._open.capture_end()
                     self.graphs.append(self._open)
                     self._open = None
-                group = int(os.environ.get("H2OMX_GRAPH_TREES", str(self.GROUP)))
+                group = self.GROUP
                 if self.chain and not segmented and group > 1:
                     # the same step G times in one graph: the chained step's only
                     # state hand-off is on the device (tree counter, scales, leaf sums)

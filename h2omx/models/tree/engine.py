@@ -76,19 +76,20 @@ class HipTreeBuilder:
     sums (leaf_stats, [all-reduce], leaf_finalize).
     """
 
-    # LDS histogram bytes per workgroup / threads per workgroup / target grid;
-    # tunable (H2OMX_HIST_LDS_KB, H2OMX_HIST_THREADS, H2OMX_HIST_WGS) for sweeps
-    LDS_BUDGET = int(os.environ.get("H2OMX_HIST_LDS_KB", "64")) * 1024
+    # LDS histogram bytes per workgroup / threads per workgroup / target grid
+    # (the sweeps that fixed them: profiles/r3/hist_threads_ab.txt,
+    # profiles/r4/hist_knobs_11m_r4o.txt)
+    LDS_BUDGET = 64 * 1024
     # 1024-thread workgroups, 256 of them (one per CU) on shallow levels: HIGGS 11M
     # depth 5 0.886 vs 0.917 ms/tree for 512 x 512 threads (half the partial slabs
     # to reduce; 384 / 512 workgroups of 1024 threads: 1.13 / 1.08), XGBoost / DRF
     # unchanged (profiles/r3/hist_threads_ab.txt)
-    THREADS = int(os.environ.get("H2OMX_HIST_THREADS", "1024"))
-    TARGET_WGS = int(os.environ.get("H2OMX_HIST_WGS", "512"))
-    ROWS_PER_LANE = int(os.environ.get("H2OMX_HIST_ROWS", "16"))
+    THREADS = 1024
+    TARGET_WGS = 512
+    ROWS_PER_LANE = 16
     # rows per workgroup chunk: bounds the fixed-point headroom, so the gradient
     # resolution is 2^30 / (largest chunk) levels (see tree_begin)
-    ROWS_CAP = int(os.environ.get("H2OMX_ROWS_CAP", "262144"))
+    ROWS_CAP = 262144
     SYNC_NODE_CAP = 4096   # above this many potential nodes the host reads the real count
     # (Removed A/B variants that measured slower and no longer exist: the
     # wave-compacted column gather (profiles/compact_hist_p9.txt), the
@@ -98,26 +99,37 @@ class HipTreeBuilder:
     # (profiles/r4/drf/move_rows_ab.txt).)
     SEG_TARGET_CHUNKS = 1024   # level-0 histogram chunks (2 resident 57 KB workgroups per CU)
     SEG_LDS_BUDGET = 64 * 1024
-    SCAN_SLOTS = int(os.environ.get("H2OMX_SCAN_SLOTS", "16"))  # seg engine: scan hist up to this many slots
+    SCAN_SLOTS = 16  # seg engine: scan hist up to this many slots
     DEEP_DEPTH = 10
     FUSE_MAX_DEPTH = 8
-    FUSE_MAX_PREV = int(os.environ.get("H2OMX_FUSE_MAX_PREV", "4"))
-    CLOSE_SINGLE_BLOCK = int(os.environ.get("H2OMX_CLOSE_SINGLE_BLOCK", "2048"))
+    FUSE_MAX_PREV = 4
+    CLOSE_SINGLE_BLOCK = 2048
     # segmented engine, single rank: levels with >= this many potential nodes build each
     # node's eligible-feature histograms directly and scan them in LDS (seg_direct_kernel:
     # no parent histograms / subtraction); 0 = off.  Multi-rank runs keep the all-reduced
     # subtraction path (direct histograms are rank-local)
-    DIRECT_MIN_NODES = int(os.environ.get("H2OMX_DIRECT_MIN_NODES", "1024"))
+    DIRECT_MIN_NODES = 1024
     # ... and only when a node has at most this many eligible features on average
-    DIRECT_MAX_ELIG = float(os.environ.get("H2OMX_DIRECT_MAX_ELIG", "32"))
+    DIRECT_MAX_ELIG = 32.0
     # direct levels whose average node holds fewer rows than this run one wave per node
     # (seg_direct_wave_kernel, F <= 256) instead of one workgroup per node
-    DIRECT_WAVE_ROWS = int(os.environ.get("H2OMX_DIRECT_WAVE_ROWS", "256"))
+    DIRECT_WAVE_ROWS = 256
     # segmented partition: levels of at least this many potential nodes run one wave per row chunk
     # (part_count_wave / part_scatter_wave: 64-ary chunk -> node search, stored row directions)
-    PART_WAVE_NODES = int(os.environ.get("H2OMX_PART_WAVE_NODES", "2048"))
+    PART_WAVE_NODES = 2048
     # direct levels of large nodes: one workgroup per row chunk (False: one per node)
     DIRECT_CHUNKED = True
+    # partition grid: 1024 x 256 lanes (sweep on HIGGS 11M: 512 1.56, 1024 1.47,
+    # 2048 1.49, 4096 1.55 ms/tree)
+    PART_BLOCKS = 1024
+    # path switches (class attributes: the GPU tests flip them with monkeypatch to
+    # pin the alternatives bit-identical): fused routing, 16-bit packed rows,
+    # level 0 with the gradient pass fused in (off: see can_fuse_grad), chained
+    # tree_begin in graph replay
+    FUSE_ROUTE = True
+    PK32 = True
+    FUSE_GRAD = False
+    CHAIN_BEGIN = True
     # segmented engine: part_scatter moves each row's (g, s2) into segment order with it
     PERMUTE_GS = True
     # direct levels of <= 16 eligible features store them per row for the partition
@@ -156,10 +168,7 @@ class HipTreeBuilder:
         # slot (scan engine): written at level 0 / by partition, read by deeper levels
         self.pk = torch.empty((bm.npad,), dtype=torch.int64, device=d)
         self.slot16 = torch.empty((bm.npad,), dtype=torch.int16, device=d)
-        # partition grid: 1024 x 256 lanes (sweep on HIGGS 11M: 512 1.56, 1024 1.47,
-        # 2048 1.49, 4096 1.55 ms/tree)
-        self.part_blocks = min(int(self.lib.h2omx_partition_blocks()),
-                               int(os.environ.get("H2OMX_PART_BLOCKS", "1024")))
+        self.part_blocks = min(int(self.lib.h2omx_partition_blocks()), self.PART_BLOCKS)
         self._sp = SplitParams()
         # monotone constraints: per-feature sign + every node's value interval
         # (written by the parent's level finalisation, read by its children)
@@ -214,8 +223,7 @@ class HipTreeBuilder:
         # level d+1's histogram kernel (node ids double-buffered), and the last level's
         # partition adds the exact sums of every row, early leaves included, into a
         # whole-tree LDS window (needs the tree capacity to fit it: depth <= 8)
-        self.fuse_route = (params.max_depth <= self.FUSE_MAX_DEPTH
-                           and os.environ.get("H2OMX_FUSE_ROUTE", "1") == "1")
+        self.fuse_route = params.max_depth <= self.FUSE_MAX_DEPTH and self.FUSE_ROUTE
         # scan engine with fused routing: levels 0 / 1 take "every live row is in the
         # root" from the row count instead of a node-id stream, so boost_update no
         # longer resets nid and levels 0 / 1 skip reading it (needs >= 2 levels: a
@@ -267,7 +275,7 @@ class HipTreeBuilder:
         # the fixed-point scales (tree_begin) derive from max_rows_per_wg: every rank
         # quantises with the SAME scale (derived from the global row count above), so
         # the summed int64 histograms are in one unit
-        self.pk32 = self.max_rows_per_wg >= 65536 and os.environ.get("H2OMX_PK32", "1") == "1"
+        self.pk32 = self.max_rows_per_wg >= 65536 and self.PK32
 
     # -- buffers -----------------------------------------------------------
     def _ticket_buf(self, numel: int) -> torch.Tensor:
@@ -291,12 +299,12 @@ class HipTreeBuilder:
         return b
 
     # -- planning ------------------------------------------------------------
-    DEEP_LDS_BUDGET = int(os.environ.get("H2OMX_HIST_DEEP_LDS_KB", "128")) * 1024
-    DEEP_MIN_GROUPS = int(os.environ.get("H2OMX_HIST_DEEP_MIN_GROUPS", "4"))
+    DEEP_LDS_BUDGET = 128 * 1024
+    DEEP_MIN_GROUPS = 4
     # level 0 of the scan engine: histograms in 8 interleaved lane copies
     # (hist_build COP: fewer LDS bank conflicts, 8x the LDS per feature, so
     # feature groups of DEEP_LDS_BUDGET); 1 = plain slices
-    L0_COPIES = int(os.environ.get("H2OMX_HIST_L0_COPIES", "8"))
+    L0_COPIES = 8
 
     def plan_l0(self):
         key = ("l0", self.L0_COPIES)
@@ -309,10 +317,10 @@ class HipTreeBuilder:
     # at 72 x 4 = 288 one-per-CU workgroups, so 32 of them ran alone in a
     # second round
     N_CUS = 256
-    MIN_GROUPS = int(os.environ.get("H2OMX_HIST_MIN_GROUPS", "1"))   # A/B knob
+    MIN_GROUPS = 1
     # single rank: slab reduction + split scan in one launch per pass (reduce_split)
     # persistent workgroups of the N-rank fused level (<= 256 P2P flag slots)
-    P2P_BLOCKS = int(os.environ.get("H2OMX_P2P_BLOCKS", "256"))
+    P2P_BLOCKS = 256
     MAX_WG_THREADS_PER_CU = 2048      # 32 waves per CU
 
     def _fill_rounds(self, wgpg: int, n_groups: int, lds_bytes: int, threads: int, units: int) -> int:
@@ -441,7 +449,7 @@ class HipTreeBuilder:
         fused and separate gradient passes build bit-identical trees)."""
         return (not self.segmented and self.implicit_root and not weighted
                 and sample_rate >= 1.0 and dist in GRAD_BOUNDS
-                and os.environ.get("H2OMX_FUSE_GRAD", "0") == "1")
+                and self.FUSE_GRAD)
 
     def build(self, g: torch.Tensor, h: torch.Tensor, w: torch.Tensor | None, tree_index: int,
               tree_fmask: torch.Tensor | None = None, grad_fuse: dict | None = None,
@@ -519,14 +527,16 @@ class HipTreeBuilder:
             sp.depth = d
             sp.children_leaves = 1 if last else 0
             self._cat_level(max_nodes)
-            # N ranks over P2P: the level's exchange runs inside the fused reduce +
-            # split scan when the level is one histogram pass on EVERY rank (the
-            # slot budget alone decides that - rank-independent - while feature
-            # groups / grids follow each rank's row count) and its rows fit the
-            # symmetric buffer
+            # N ranks over P2P: the level's reduce-scatter runs inside the fused
+            # reduce + split scan when the level is one histogram pass on EVERY
+            # rank (the slot budget alone decides that - rank-independent - while
+            # feature groups / grids follow each rank's row count), the rows pushed
+            # to one owner fit a parity of the symmetric buffer and the level's
+            # split records fit its split table (csrc/tree_kernels.hip)
             fuse_p2p = (p2p is not None
                         and max_slots * nbt * 8 <= self.LDS_BUDGET
-                        and max_slots * F * 2 * nbt * 8 <= p2p.cap)
+                        and max_slots * -(-F // p2p.world) * p2p.world * 2 * nbt * 8 <= p2p.cap
+                        and 2 * max_slots * F * FEAT_BEST_BYTES <= p2p.cap // 2)
             # each pass's slab reduction runs the split scan of its slots right away
             # (reduce_split; N ranks: reduce_split_p2p); otherwise the level's
             # histograms are reduced, all-reduced and scanned in separate launches
@@ -539,7 +549,7 @@ class HipTreeBuilder:
                         raise RuntimeError("reduce_split_p2p: multi-pass level")   # excluded by fuse_p2p
                     ops.check(lib.h2omx_reduce_split_p2p(p2p.desc_ptr, P(partials), wgpg, fg, slot_cnt, P(full_prev),
                                                          P(full_cur), P(ctl_cur), P(link[cur]), P(bm.nvb),
-                                                         P(tree_fmask), P(self.qscale), spp, nbt, P(fbest),
+                                                         P(tree_fmask), P(self.qscale), spp, nbt,
                                                          self.P2P_BLOCKS, st), "reduce_split_p2p")
                     comm.stats["p2p_calls"] += 1
                     comm.stats["p2p_bytes"] += max_slots * self.per_node * 8
@@ -610,11 +620,19 @@ class HipTreeBuilder:
                     ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur),
                                                    P(link[cur]), P(bm.nvb), P(tree_fmask), P(self.qscale), spp,
                                                    max_nodes, nbt, P(fbest), st), "split_find")
-                ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
-                                                   P(bm.nvb), nbt, next_nodes, P(part), P(nl),
-                                                   P(self.tree_buf), self.capacity, P(nsplit), max_nodes,
-                                                   self._lf_tiles(max_nodes),
-                                                   st), "level_finalize")
+                if fuse_p2p:
+                    # waits for every rank's share of the split records (all-gathered
+                    # into this rank's split table by reduce_split_p2p)
+                    ops.check(lib.h2omx_node_best_finalize_p2p(p2p.desc_ptr, P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
+                                                               P(bm.nvb), nbt, next_nodes, P(part), P(nl),
+                                                               P(self.tree_buf), self.capacity, P(nsplit), st),
+                              "node_best_finalize_p2p")
+                else:
+                    ops.check(lib.h2omx_level_finalize(P(fbest), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
+                                                       P(bm.nvb), nbt, next_nodes, P(part), P(nl),
+                                                       P(self.tree_buf), self.capacity, P(nsplit), max_nodes,
+                                                       self._lf_tiles(max_nodes),
+                                                       st), "level_finalize")
             # leaves that can retire at this level: gids [base, base + n + n_next)
             win = min(3 * max_nodes, self.capacity)
             with T("partition"):
@@ -651,7 +669,7 @@ class HipTreeBuilder:
             max_nodes = next_nodes
         # exact leaf values (sums accumulated by the partition kernels); N ranks over
         # P2P exchange the sums inside the leaf finalisation
-        leaf_p2p = p2p is not None and self.gbound is None and self.capacity * 3 * 8 <= p2p.cap
+        leaf_p2p = p2p is not None and self.gbound is None and self.capacity * 3 * 8 * p2p.world <= p2p.cap
         if comm is not None and not leaf_p2p:
             with T("allreduce"):
                 comm.all_reduce_(self.leaf_acc)
@@ -682,7 +700,7 @@ class HipTreeBuilder:
         boost pass that runs in between), the scan engine, the plain leaf pass
         (no monotone Newton re-derivation) and a device tree counter."""
         return (fixed and not self.segmented and self.gbound is None and self.tree_ctr is not None
-                and os.environ.get("H2OMX_CHAIN_BEGIN", "1") == "1")
+                and self.CHAIN_BEGIN)
 
     # chained graph steps: boost_update also writes the next tree's 16-bit packed
     # level-0 rows, so level 0 reads 4 bytes per row and feature group instead of
@@ -708,7 +726,7 @@ class HipTreeBuilder:
                   "tree_begin")
 
     # data-parallel direct levels: histogram chunk all-reduced per call (bytes)
-    DIRECT_DP_CHUNK_BYTES = int(os.environ.get("H2OMX_DIRECT_DP_CHUNK_MB", "64")) << 20
+    DIRECT_DP_CHUNK_BYTES = 64 << 20
 
     def _direct_dp(self, comm, idx_in, gs, seg_start, seg_cnt, ctl_cur, tree_fmask, spp, max_nodes, nsplit, st):
         """Direct level over N row shards: per node chunk, this rank's eligible-

@@ -12,7 +12,6 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import math
-import os
 
 import numpy as np
 import torch
@@ -21,8 +20,8 @@ from .. import _native
 from . import P, check, dense_lib, stream
 
 KBADARG = 1  # common.h kBadArg
-# workgroups of the fused GLM Gram / K-Means kernels (sweeps: H2OMX_GLM_WGS, H2OMX_KM_WGS)
-GLM_WGS = int(os.environ.get("H2OMX_GLM_WGS", "512"))
+# workgroups of the fused GLM Gram / K-Means kernels (swept: profiles/r3/dense_pmc/, profiles/r4/dense/)
+GLM_WGS = 512
 # wave-unit IRLS kernel for p + 2 <= 128 (not multinomial; False: the workgroup
 # kernel, which serves wider / multinomial designs); units = independent waves,
 # each over a contiguous row range (fp32 within a unit, fp64 across).  Module
@@ -32,17 +31,17 @@ GLM_WAVE = True
 # cores (glm_irls_split_kernel); "f32" = fp32 MFMA (glm_irls_wave_kernel, the
 # intercept-only pass and the split kernel's test oracle)
 GLM_GRAM = "split"
-GLM_UNITS = int(os.environ.get("H2OMX_GLM_UNITS", "2048"))
+GLM_UNITS = 2048
 GLM_UNIT_MIN_ROWS = 512
 SLAB_SPLIT = 32          # dense_kernels.hip slab_reduce16_kernel
-KM_WGS = int(os.environ.get("H2OMX_KM_WGS", "1024"))
+KM_WGS = 1024
 # K-Means Lloyd pass: cluster sums on the fp32 matrix cores (kmeans_mfma_kernel,
 # d + 2 <= 128 / 64, k <= 32), else the wave-unit kernel (k <= 32, d <= 128 / 64),
 # else the workgroup-tile kernel; the wave kernel's grid is sized for 256 CUs
 KM_MFMA = True
 KM_WAVE = True
 KM_WAVE_CUS = 256
-KM_MFMA_WGS = int(os.environ.get("H2OMX_KM_MFMA_WGS", "512"))
+KM_MFMA_WGS = 512
 
 FAMILIES = {"gaussian": 0, "binomial": 1, "poisson": 2, "gamma": 3, "tweedie": 4, "multinomial": 5,
             "quasibinomial": 6, "fractionalbinomial": 6, "negativebinomial": 7}

@@ -21,7 +21,6 @@ else keeps the general path of ``models/deeplearning.py``.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -107,10 +106,11 @@ def _op(t: torch.Tensor | None, ld: int, kc: bool, ptr: int | None = None) -> Op
 N_CUS = 256
 
 
-# A/B knobs (tuning runs): H2OMX_MLP_TILE="RI,RJ" forces one tile shape,
-# H2OMX_MLP_DEPTH the 16-k load groups in flight per wave (1, 2, 4, 8)
-_TILE = os.environ.get("H2OMX_MLP_TILE", "")
-DEPTH = int(os.environ.get("H2OMX_MLP_DEPTH", "4"))
+# Tile override (tuning runs set it as a module attribute: "RI,RJ" forces one
+# tile shape; "" = the per-shape choice below) and the 16-k load groups in
+# flight per wave (1, 2, 4, 8 measured: 4 kept, profiles/r5/dl/)
+_TILE = ""
+DEPTH = 4
 # activation rows padded off the 2 KB L2-channel period (A/B knob: no measured
 # difference either way on MI355X, profiles/r5/dl/fused_step_ab_r5f.jsonl)
 

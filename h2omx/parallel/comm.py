@@ -45,6 +45,7 @@ class Comm:
         self._p2p_dead = None     # a P2P instance disabled after a timeout (closed at shutdown)
         self.p2p_error: str | None = None
         self.stats.update({"p2p_calls": 0, "p2p_bytes": 0, "p2p_s": 0.0})
+        self._side = None         # stream of the bucketed P2P all-reduces (all_reduce_bucket_)
 
     def _check(self) -> None:
         """Raise ``PeerLost`` once a peer is known lost: by the watchdog
@@ -162,10 +163,14 @@ class Comm:
         if self.world_size == 1:
             return t
         self._check()
-        if self.p2p is not None and self.p2p.supports(t, op):
-            # device-side one-shot collective (a kernel: no host-issued RCCL call)
+        if self._p2p_chunks(t, op):
+            # device-side one-shot collectives (kernels: no host-issued RCCL call);
+            # a tensor above the symmetric buffer goes as consecutive cap-sized chunks
             tok = self._begin("p2p", t.numel() * t.element_size())
-            self.p2p.all_reduce_(t, op)
+            step = self.p2p.cap // t.element_size() // 4 * 4
+            flat = t.view(-1)
+            for s in range(0, flat.numel(), step):
+                self.p2p.all_reduce_(flat[s:s + step], op)
             self._end(tok)
             return t
         tok = self._begin("all_reduce", t.numel() * t.element_size())
@@ -173,6 +178,38 @@ class Comm:
         dist.all_reduce(t, op=rop, group=self.group)
         self._end(tok)
         return t
+
+    def _p2p_chunks(self, t: torch.Tensor, op: str) -> bool:
+        """True when the P2P exchange carries ``t`` (whole, or in cap-sized chunks)."""
+        p2p = self.p2p
+        if p2p is None or not t.is_contiguous():
+            return False
+        if p2p.supports(t, op):
+            return True
+        step = p2p.cap // t.element_size() // 4 * 4
+        return step > 0 and p2p.supports(t.view(-1)[:step], op)
+
+    def all_reduce_bucket_(self, t: torch.Tensor, op: str = "sum"):
+        """In-place all-reduce of one gradient bucket, overlapped with the
+        producer's remaining work; returns a handle whose ``wait()`` joins it
+        back into the current stream.  With P2P the collective is a kernel on
+        this Comm's side stream (forked from / joined to the current stream by
+        events: graph-capturable, no host-issued collective, and every bucket
+        summed in rank order, so the replicas stay bit-identical); otherwise an
+        asynchronous RCCL call."""
+        if self.world_size == 1:
+            return _Done()
+        self._check()
+        if self._p2p_chunks(t, op) and t.is_cuda:
+            main = torch.cuda.current_stream(t.device)
+            if self._side is None:
+                self._side = torch.cuda.Stream(t.device)
+            side = self._side
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self.all_reduce_(t, op)
+            return _StreamJoin(main, side)
+        return self.all_reduce_async(t, op)
 
     def all_reduce_async(self, t: torch.Tensor, op: str = "sum"):
         """Non-blocking all-reduce; returns a handle with ``wait()`` (gradient
@@ -312,7 +349,43 @@ class LoopbackComm(Comm):
             t.mul_(self.world_size)
         return t
 
+    def _p2p_chunks(self, t: torch.Tensor, op: str) -> bool:
+        """True when the P2P exchange carries ``t`` (whole, or in cap-sized chunks)."""
+        p2p = self.p2p
+        if p2p is None or not t.is_contiguous():
+            return False
+        if p2p.supports(t, op):
+            return True
+        step = p2p.cap // t.element_size() // 4 * 4
+        return step > 0 and p2p.supports(t.view(-1)[:step], op)
+
+    def all_reduce_bucket_(self, t: torch.Tensor, op: str = "sum"):
+        """In-place all-reduce of one gradient bucket, overlapped with the
+        producer's remaining work; returns a handle whose ``wait()`` joins it
+        back into the current stream.  With P2P the collective is a kernel on
+        this Comm's side stream (forked from / joined to the current stream by
+        events: graph-capturable, no host-issued collective, and every bucket
+        summed in rank order, so the replicas stay bit-identical); otherwise an
+        asynchronous RCCL call."""
+        if self.world_size == 1:
+            return _Done()
+        self._check()
+        if self._p2p_chunks(t, op) and t.is_cuda:
+            main = torch.cuda.current_stream(t.device)
+            if self._side is None:
+                self._side = torch.cuda.Stream(t.device)
+            side = self._side
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self.all_reduce_(t, op)
+            return _StreamJoin(main, side)
+        return self.all_reduce_async(t, op)
+
     def all_reduce_async(self, t: torch.Tensor, op: str = "sum"):
+        self.all_reduce_(t, op)
+        return _Done()
+
+    def all_reduce_bucket_(self, t: torch.Tensor, op: str = "sum"):
         self.all_reduce_(t, op)
         return _Done()
 
@@ -340,6 +413,17 @@ class LoopbackComm(Comm):
 
 class _Done:
     def wait(self):
+        return True
+
+
+class _StreamJoin:
+    """Handle of a side-stream collective: wait() makes the main stream wait."""
+
+    def __init__(self, main, side):
+        self.main, self.side = main, side
+
+    def wait(self):
+        self.main.wait_stream(self.side)
         return True
 
 

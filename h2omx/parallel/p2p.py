@@ -17,7 +17,12 @@ code path (the multi-rank GPU tests use that).
 
 The tree engine runs its level-histogram and leaf-sum exchanges inside its
 own kernels over the same buffers and epoch (``csrc/p2p_device.h``): an N-rank
-level is one ``reduce_split_p2p`` launch, exactly like the single-rank level.
+level is one ``reduce_split_p2p`` launch - a reduce-scatter of the level's
+histogram rows by feature (rank r owns the features f = r mod N and scans only
+those) with an all-gather of the split records - plus the level finalisation,
+exactly the launches of the single-rank level.  Every exchange PUSHES: a rank
+writes its bytes into the consumer's buffer (write-through, system scope) and
+reads only its own buffer, so no kernel waits on a remote read over xGMI.
 
 Contract: every rank calls :meth:`all_reduce_` (and the fused tree kernels)
 with the same sequence of (numel, dtype, op), as with any collective.  A peer
@@ -28,7 +33,7 @@ sync) reports it - ``Comm._check`` turns it into ``PeerLost`` at the next
 step, graph flush or collective, and P2P is disabled for good on that Comm
 (the epochs of the ranks can no longer be trusted).
 
-Memory kinds (``H2OMX_P2P_SYM``): the symmetric data buffers are fine-grained
+Memory kinds (``P2PAllReduce.SYM_KIND``): the symmetric data buffers are fine-grained
 device memory by default, so a peer's read over xGMI is coherent at system
 scope by allocation type, not by relying on the writer's L2 write-back
 reaching the remote reader; ``coarse`` (plain hipMalloc) and ``uncached`` are
@@ -61,6 +66,9 @@ class P2PAllReduce:
     """Symmetric buffers + flags of one process group; see module docstring."""
 
     DEFAULT_CAP = 8 << 20      # bytes per parity: Airlines depth-6 last level = 32 x 127 KB = 4 MB
+    # symmetric-buffer memory kind: fine-grained by default; coarse / uncached
+    # measured within noise on one GPU (profiles/r5/p2p/README.md)
+    SYM_KIND = "fine"
 
     def __init__(self, comm, cap_bytes: int | None = None, timeout_s: float | None = None,
                  loopback: bool = False):
@@ -74,9 +82,9 @@ class P2PAllReduce:
         self.loopback = loopback
         self.cap = int(cap_bytes or int(os.environ.get("H2OMX_P2P_CAP_MB", "0")) << 20 or self.DEFAULT_CAP)
         self.timeout_s = float(timeout_s if timeout_s is not None else os.environ.get("H2OMX_P2P_TIMEOUT_S", "20"))
-        kind = os.environ.get("H2OMX_P2P_SYM", "fine")
+        kind = self.SYM_KIND
         if kind not in SYM_KINDS:
-            raise ValueError(f"H2OMX_P2P_SYM={kind!r}: expected one of {sorted(SYM_KINDS)}")
+            raise ValueError(f"P2PAllReduce.SYM_KIND={kind!r}: expected one of {sorted(SYM_KINDS)}")
         self.sym_kind = kind
         self.calls = 0
         self._own: list[int] = []       # pointers this rank allocated
@@ -84,7 +92,8 @@ class P2PAllReduce:
         self._host: int | None = None   # pinned error word (host address)
         self._err_word = None
         with torch.cuda.device(comm.device):
-            sym = self._alloc(2 * self.cap, SYM_KINDS[kind])
+            # two exchange parities + the tree level's split-record table (2 x cap / 2)
+            sym = self._alloc(3 * self.cap, SYM_KINDS[kind])
             flags = self._alloc(int(lib.h2omx_p2p_flags_bytes()), SYM_KINDS["uncached"])
             # control words live in torch memory: [epoch, ticket, error, timeouts]
             self.ctrl = torch.zeros((4,), dtype=torch.int32, device=comm.device)

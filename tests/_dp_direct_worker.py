@@ -19,6 +19,9 @@ from h2omx.parallel.comm import Comm  # noqa: E402
 
 
 def main() -> int:
+    from h2omx.models.tree.engine import HipTreeBuilder
+
+    HipTreeBuilder.DIRECT_MIN_NODES = 8   # the direct deep-level engine from 8 nodes on
     out = sys.argv[1]
     comm = Comm.from_env("cuda")
     dev, r, w = comm.device, comm.rank, comm.world_size

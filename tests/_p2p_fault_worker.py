@@ -22,6 +22,10 @@ from h2omx.runtime.jobs import JobRegistry  # noqa: E402
 
 
 def main() -> int:
+    from h2omx.models.tree.boost import GpuBooster
+
+    # the test hook is a class attribute (the production step reads no environment)
+    GpuBooster.FAULT_STALL_SPEC = os.environ.get("H2OMX_FAULT_STALL")
     comm = Comm.from_env("cuda")
     r, w = comm.rank, comm.world_size
     res = {"rank": r, "p2p": comm.p2p is not None}

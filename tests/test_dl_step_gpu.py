@@ -67,7 +67,7 @@ def test_one_training_step_matches_autograd(case, fused, monkeypatch):
     from h2omx.models.deeplearning import H2ODeepLearningEstimator, _DLTrainer, _Net
 
     sizes, act, M, regression, l2 = CASES[case]
-    monkeypatch.setenv("H2OMX_DL_FUSED", "1" if fused else "0")
+    monkeypatch.setattr(_DLTrainer, "FUSED", fused)
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(case)
     X = rng.normal(size=(M * 3, sizes[0])).astype(np.float32)

@@ -138,8 +138,10 @@ def test_deeplearning_graph_replay_matches_eager(cuda_dev, monkeypatch, act, pre
     fr = Frame.from_pandas(df, device=cuda_dev)
     kw = dict(hidden=[64, 32], epochs=2, seed=4, activation=act, precision=precision)
     out = {}
+    from h2omx.models.deeplearning import _DLTrainer
+
     for g in ("0", "1"):
-        monkeypatch.setenv("H2OMX_DL_GRAPH", g)
+        monkeypatch.setattr(_DLTrainer, "GRAPH", g == "1")
         out[g] = H2ODeepLearningEstimator(**kw).train(y="y", training_frame=fr)
     assert torch.equal(out["0"].net.flat, out["1"].net.flat)
     assert out["1"].training_metrics["AUC"] == out["0"].training_metrics["AUC"]
@@ -147,7 +149,7 @@ def test_deeplearning_graph_replay_matches_eager(cuda_dev, monkeypatch, act, pre
 
 def test_deeplearning_folds_in_adadelta_match_separate_reduces(cuda_dev, monkeypatch):
     """Bias-gradient slices and the output layer's split partials folded inside
-    the ADADELTA kernel (H2OMX_DL_FOLD) train the same model as the separate
+    the ADADELTA kernel (_DLTrainer.FOLD) train the same model as the separate
     reduce launches: the bias folds are the same fp64 sums, the output layer's
     fold only changes the fp32 summation order."""
     from h2omx.models import deeplearning as DLM

@@ -155,6 +155,36 @@ def test_cpu_reference_trees_split_on_oracle_edges(mode):
     assert not np.array_equal(eq.trees[0]["bin"], ens.trees[0]["bin"])
 
 
+def test_zero_weight_rows_do_not_widen_the_node_range():
+    """A node's [min, max] (the span UniformAdaptive re-bins) comes from its rows
+    of POSITIVE weight: a fine bin counts as occupied when its weight plane is
+    > 0 (adaptive_candidates in csrc/tree_kernels.hip, reference adaptive_mask),
+    as H2O's histograms skip zero-weight rows.  So zero-weight rows - here
+    placed at the extremes of a feature, where they would widen every node's
+    range - give the same trees as leaving those rows out (same grid)."""
+    X, y = _data(4000, seed=11)
+    rng = np.random.default_rng(5)
+    zero = rng.random(X.shape[1]) < 0.2
+    X[0, zero] = np.where(rng.random(int(zero.sum())) < 0.5, -40.0, 40.0)   # out-of-range rows
+    w = np.where(zero, 0.0, 1.0).astype(np.float32)
+    Xt = torch.from_numpy(X)
+    e, nv, nbt = compute_edges(Xt, 255)
+    fr = None
+    tp = TreeParams(max_depth=5, min_rows=5, learn_rate=0.3, min_split_improvement=0, seed=3, hist_mode=1,
+                    hist_top=1024, hist_nbins=20)
+    keep = ~zero
+    bm_all = bin_matrix(Xt, e, nv, nbt)
+    bm_all.frange = fr = adaptive_ranges(Xt, bm_all)
+    bm_kept = bin_matrix(torch.from_numpy(np.ascontiguousarray(X[:, keep])), e, nv, nbt)
+    bm_kept.frange = fr
+    ea = train_ensemble(bm_all, torch.from_numpy(y), torch.from_numpy(w), dist="bernoulli", ntrees=3, tparams=tp)
+    ek = train_ensemble(bm_kept, torch.from_numpy(y[keep]), dist="bernoulli", ntrees=3, tparams=tp)
+    for t in range(3):
+        for k in ("feat", "bin", "left"):
+            np.testing.assert_array_equal(ea.trees[t][k], ek.trees[t][k])
+        np.testing.assert_allclose(ea.trees[t]["value"], ek.trees[t]["value"], rtol=1e-5, atol=1e-7)
+
+
 def _frame(n=3000, seed=0):
     from h2omx.frame import Frame
 

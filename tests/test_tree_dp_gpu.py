@@ -22,8 +22,7 @@ def _port():
 
 
 def _run(nproc, out):
-    env = dict(os.environ, H2OMX_DIST_BACKEND="gloo", OMP_NUM_THREADS="2", H2OMX_TREE_ENGINE="seg",
-               H2OMX_DIRECT_MIN_NODES="8")
+    env = dict(os.environ, H2OMX_DIST_BACKEND="gloo", OMP_NUM_THREADS="2", H2OMX_TREE_ENGINE="seg")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "tests", "_dp_direct_worker.py"), str(out)]

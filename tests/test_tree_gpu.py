@@ -225,7 +225,7 @@ def test_pk32_rows_match_pk64(cuda_dev, monkeypatch, dist, depth, sample_rate):
     monkeypatch.setattr(E.HipTreeBuilder, "__init__", spy)
     out = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("H2OMX_PK32", flag)
+        monkeypatch.setattr(E.HipTreeBuilder, "PK32", flag == "1")
         out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate, seed=5)
     assert [m.pk32 for m in made] == [False, True]
     a, b = out["0"], out["1"]
@@ -258,7 +258,7 @@ def test_fused_routing_matches_partition(cuda_dev, monkeypatch, dist, depth, sam
     # unfused; fused while the previous level has <= 4 nodes (routing pass after);
     # fused at every level
     for key, flag, max_prev in (("off", "0", 4), ("mixed", "1", 4), ("all", "1", 1 << 20)):
-        monkeypatch.setenv("H2OMX_FUSE_ROUTE", flag)
+        monkeypatch.setattr(E.HipTreeBuilder, "FUSE_ROUTE", flag == "1")
         monkeypatch.setattr(E.HipTreeBuilder, "FUSE_MAX_PREV", max_prev)
         out[key] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
                                   nclass=3 if dist == "multinomial" else 1, seed=4)
@@ -302,6 +302,7 @@ def test_fused_gradient_level_matches_boost_update(cuda_dev, monkeypatch, n, mod
     trees and margins as the separate boost_update pass; 600k rows run the
     32-bit packed rows, 40k rows the 64-bit ones."""
     from h2omx.models.tree.boost import GpuBooster, TreeEnsemble, _GpuView
+    from h2omx.models.tree.engine import HipTreeBuilder
 
     X, y = _data(n=n, F=9, seed=12, task="bin")
     _, bg = _both(X, y, 255)
@@ -310,7 +311,7 @@ def test_fused_gradient_level_matches_boost_update(cuda_dev, monkeypatch, n, mod
     monkeypatch.setenv("H2OMX_TREE_ENGINE", "scan")
     out = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("H2OMX_FUSE_GRAD", flag)   # (default: see HipTreeBuilder.can_fuse_grad)
+        monkeypatch.setattr(HipTreeBuilder, "FUSE_GRAD", flag == "1")   # (default: see HipTreeBuilder.can_fuse_grad)
         ens = TreeEnsemble(trees=np.zeros((0, 1)), K=1, dist="bernoulli", init_f=np.array([0.1]), nbt=bg.nbt,
                            feature_names=bg.names)
         gb = GpuBooster(bg, yt, None, ens, tp, 1.0, 3, None, {})
@@ -362,7 +363,7 @@ def test_graph_replay_matches_eager(cuda_dev, monkeypatch, dist, depth, min_rows
         monkeypatch.setenv("H2OMX_TREE_GRAPH", flag)
         out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=ntrees, tparams=tp, seed=5)
     assert not made[0].graph_used and made[1].graph_used, made[1].graph_error
-    if dist == "bernoulli" and os.environ.get("H2OMX_CHAIN_BEGIN", "1") == "1":
+    if dist == "bernoulli" and E.HipTreeBuilder.CHAIN_BEGIN:
         assert made[1].graph_chain
     a, b = out["0"], out["1"]
     assert a.trees.shape == b.trees.shape
