@@ -15,8 +15,8 @@ reference/tree.adaptive_mask).  So a split can differ from H2O's in two ways:
      edge and the node has fewer candidates than H2O.
 For nodes of random axis-aligned boxes (depth 0..5) of HIGGS-shape data this
 script measures, per (node, feature): the fraction of the node's rows whose
-side differs between each H2O cut and its snapped edge (max and mean over the
-cuts), distinct candidates h2omx / H2O, and the best squared-error gain of
+side differs between each H2O cut and the closest split h2omx can make there
+(max and mean over the cuts), distinct candidates h2omx / H2O, and the best squared-error gain of
 the feature under each rule (relative shortfall), plus how often the best
 feature of a node differs.  Output: one JSON document (profiles/r6/).
 
@@ -99,13 +99,16 @@ def main():
                 G = np.bincount(c, weights=gf, minlength=nbt)
                 cgb, cwb = np.cumsum(G), np.cumsum(S)
                 gain_m = se_gain(cgb[allowed], cwb[allowed], cg[-1], float(len(xs)))
-                # every H2O cut vs the fine edge it snaps to (nearest interior edge)
+                # every H2O cut vs the closest partition h2omx can make: both are
+                # thresholds in the same row order (monotone bins), so the rows that
+                # change sides are |left fraction (H2O cut) - left fraction (candidate)|
                 e_f = edges[f][:T].astype(np.float64)
                 near = allowed[np.argmin(np.abs(e_f[allowed][None, :] - cuts[:, None]), axis=1)] if allowed.size else None
                 if near is not None:
-                    left_h = x[None, :] < cuts[:, None]
-                    left_m = c[None, :] <= near[:, None]
-                    fl = (left_h != left_m).mean(axis=1)
+                    nl = len(xs)
+                    frac_h = k / nl
+                    frac_m = cwb[allowed] / nl
+                    fl = np.abs(frac_h[:, None] - frac_m[None, :]).min(axis=1)
                     flips_max.append(float(fl.max()))
                     flips_mean.append(float(fl.mean()))
                     cand_ratio.append(np.unique(near).size / float(nb - 1))

@@ -3,8 +3,8 @@ sharing the one GPU, gloo bootstrap, device P2P exchanges): H2O DeepLearning
 with ``sync_gradients=True``.  Each rank trains on its shard; with world 1 the
 worker trains on the two shards' mini-batches interleaved (rank 0's 256 rows,
 then rank 1's, per 512-row batch) - the concatenated-batch reference.  Every
-step is timed for host-issued collectives; rank 0 (and the 1-rank run) print
-one JSON line with the weights."""
+step is checked for host-issued collectives; every rank writes one JSON
+document (weights, per-step collective counts) to <out_dir>/rank<r>.json."""
 import hashlib
 import json
 import os
@@ -26,6 +26,7 @@ M, STEPS, F = 256, 24, 12
 
 
 def main() -> int:
+    out_dir = sys.argv[1]
     comm = Comm.from_env("cuda")
     r, w = comm.rank, comm.world_size
     rng = np.random.default_rng(11)
@@ -62,7 +63,8 @@ def main() -> int:
     res = {"rank": r, "world": w, "p2p": comm.p2p is not None, "steps": per_step,
            "digest": hashlib.sha256(flat.tobytes()).hexdigest(), "w": flat.tolist(),
            "tspi": int(m.train_samples_per_iteration)}
-    print(json.dumps(res), flush=True)
+    with open(os.path.join(out_dir, f"rank{r}.json"), "w") as f:
+        json.dump(res, f)
     comm.shutdown()
     return 0
 

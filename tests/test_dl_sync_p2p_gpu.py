@@ -28,27 +28,21 @@ def _port():
     return p
 
 
-def _run(nproc):
+def _run(nproc, out_dir):
     env = dict(os.environ, H2OMX_DIST_BACKEND="gloo", H2OMX_P2P="1", OMP_NUM_THREADS="2", H2OMX_P2P_TIMEOUT_S="20")
+    out_dir.mkdir()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tests", "_dl_sync_worker.py")]
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tests", "_dl_sync_worker.py"),
+           str(out_dir)]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
-    dec, outs, i = json.JSONDecoder(), [], 0
-    while True:
-        i = r.stdout.find('{"rank"', i)
-        if i < 0:
-            break
-        o, i = dec.raw_decode(r.stdout, i)
-        outs.append(o)
-    assert len(outs) == nproc, r.stdout[-2000:]
-    return sorted(outs, key=lambda o: o["rank"])
+    return [json.load(open(out_dir / f"rank{k}.json")) for k in range(nproc)]
 
 
 @pytest.mark.gpu
-def test_sync_gradients_p2p_one_graph_bit_identical_replicas():
-    two = _run(2)
-    one = _run(1)[0]
+def test_sync_gradients_p2p_one_graph_bit_identical_replicas(tmp_path):
+    two = _run(2, tmp_path / "two")
+    one = _run(1, tmp_path / "one")[0]
     a, b = two
     assert a["p2p"] and b["p2p"]
     assert a["tspi"] == 2 * 256
