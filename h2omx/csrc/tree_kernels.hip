@@ -1570,23 +1570,83 @@ __device__ __forceinline__ bool rs_scan_node(const long long (*row)[NBT], int sl
   return true;
 }
 
-template <int NBT, bool CAT>
+// The level finalisation folded into the LAST workgroup of a level's reduce +
+// split-scan launch (one launch and one kernel boundary less per level): every
+// split record is stored write-through (agent scope, `sc1`), every wave drains
+// its stores before the workgroup's ticket (agent-scope atomic), and the
+// workgroup whose ticket comes last reads the records with `sc1` loads and runs
+// node_best + level_finalize_body - no release / acquire fences (round 5's
+// fenced version cost more than the launch it saved,
+// profiles/r5/fused_finalize_ab.txt).
+struct LevelFin {
+  int* ctl_next;
+  const float* edges;
+  PartInfo* part;
+  NodeLink* next_link;
+  TreeNode* tree;
+  NodeSplit* nsplit;
+  int* ticket;          // zeroed once; the last workgroup resets it
+  int max_next_nodes;
+  int tree_capacity;
+};
+
+__device__ __forceinline__ void store_feat_best_wt(FeatBest* __restrict__ out, int64_t i, const WaveBest& w) {
+  FeatBest* d = out + i;
+  __hip_atomic_store(&d->gain, w.gain, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&d->GL, w.GL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&d->SL, w.SL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&d->G, w.G, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&d->S, w.S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(reinterpret_cast<long long*>(&d->code), (long long)(uint32_t)w.code, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// true (to every thread) in the workgroup whose ticket came last; every wave
+// has drained its stores before the ticket
+__device__ __forceinline__ bool lf_last_block(int* ticket, int nblocks) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == nblocks - 1;
+    if (s_last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+// (defined after level_finalize_body) MODE 1: records written by this launch's
+// workgroups (agent-scope loads); 2: pushed by peer ranks (system-scope loads)
+template <int MODE>
+__device__ void level_fin_records(const FeatBest* __restrict__ fbest, const int* __restrict__ ctl, const SplitParams& p,
+                                  const int* __restrict__ nvb, int nbt, const LevelFin& fin);
+
+template <int NBT, bool CAT, bool FIN = false>
 __global__ __launch_bounds__(1024) void reduce_split_kernel(
     const unsigned long long* __restrict__ partials, int wgpg, int fg, int slot_lo, int slot_cnt,
     const long long* __restrict__ parent_full, long long* __restrict__ full, const int* __restrict__ ctl,
     const NodeLink* __restrict__ link, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
-    const double* __restrict__ qscale, SplitParams p, FeatBest* __restrict__ out) {
+    const double* __restrict__ qscale, SplitParams p, FeatBest* __restrict__ out, LevelFin fin) {
   __shared__ long long red[1024 / (NBT / 2)][NBT / 2][4];   // 32 KB
   __shared__ long long row[2][NBT];                         // exact (G_q, S_q) of the built slot
   const int s = blockIdx.x, f = blockIdx.y;
   const int slot = slot_lo + s;
-  if (slot >= ctl[CTL_SLOTS]) return;   // whole workgroup
-  rs_reduce_row<NBT>(partials, wgpg, fg, slot_cnt, s, f, red, row);
-  int node;
-  WaveBest w;
-  if (rs_scan_node<NBT, CAT>(row, slot, f, parent_full, full, ctl, link, nvb, tree_fmask, qscale, p, node, w) &&
-      (threadIdx.x & 63) == 0)
-    store_feat_best(out, (int64_t)node * p.F + f, w);
+  const bool active = slot < ctl[CTL_SLOTS];   // whole workgroup
+  if (!FIN && !active) return;
+  if (active) {
+    rs_reduce_row<NBT>(partials, wgpg, fg, slot_cnt, s, f, red, row);
+    int node;
+    WaveBest w;
+    if (rs_scan_node<NBT, CAT>(row, slot, f, parent_full, full, ctl, link, nvb, tree_fmask, qscale, p, node, w) &&
+        (threadIdx.x & 63) == 0) {
+      if constexpr (FIN) store_feat_best_wt(out, (int64_t)node * p.F + f, w);
+      else store_feat_best(out, (int64_t)node * p.F + f, w);
+    }
+  }
+  if constexpr (FIN) {
+    if (lf_last_block(fin.ticket, (int)(gridDim.x * gridDim.y))) level_fin_records<1>(out, ctl, p, nvb, NBT, fin);
+  }
 }
 
 // ---- N ranks: reduce-scatter by feature + all-gather of the split records ----
@@ -1635,16 +1695,17 @@ __device__ __forceinline__ void p2p_push_feat_best(const p2pdev::P2PDesc& d, uin
 // level finalisation, the same three launches as one rank.  Items map to
 // blocks identically on every rank (same grid).
 // Loopback (one GPU standing in for N ranks; bench.py --loopback-ranks): the
-// rows go to slot src 0 and the owner reads that row N times; records of the
+// rows of this rank's features go to source slot 0 and are read N times, the
+// other rows to the slots no one reads (the pushes' write traffic); records of the
 // features this rank does not own are written as "none" (the same number of
 // record writes as a real rank's pushes), so loopback trees split on the
 // owned features only - the timing proxy of one rank's share.
-template <int NBT, bool CAT>
+template <int NBT, bool CAT, bool FIN = false>
 __global__ __launch_bounds__(1024) void reduce_split_p2p_kernel(
     p2pdev::P2PDesc d, const unsigned long long* __restrict__ partials, int wgpg, int fg, int slot_cnt,
     const long long* __restrict__ parent_full, long long* __restrict__ full, const int* __restrict__ ctl,
     const NodeLink* __restrict__ link, const int* __restrict__ nvb, const uint8_t* __restrict__ tree_fmask,
-    const double* __restrict__ qscale, SplitParams p) {
+    const double* __restrict__ qscale, SplitParams p, LevelFin fin) {
   __shared__ long long red[1024 / (NBT / 2)][NBT / 2][4];
   __shared__ long long row[2][NBT];
   __shared__ uint32_t s_epoch;
@@ -1654,13 +1715,16 @@ __global__ __launch_bounds__(1024) void reduce_split_p2p_kernel(
   const int items = slot_cnt * F;
   const uint32_t e = p2pdev::begin_epoch(d, &s_epoch);
   const int n_slots = ctl[CTL_SLOTS];
-  const int src = d.loopback ? 0 : d.rank;
   // A: reduce + push every item's row to its owner
   for (int it = b; it < items; it += nb) {
     const int s = it / F, f = it % F;
     if (s >= n_slots) continue;   // block-uniform
     rs_reduce_row<NBT>(partials, wgpg, fg, slot_cnt, s, f, red, row);
     const int owner = f % N;
+    // loopback: every row lands in this rank's own buffer - its own features'
+    // rows in source slot 0 (read N times below), the others in slots 1 .. N - 1
+    // (never read: the stand-in for the pushes to the other owners)
+    const int src = d.loopback ? owner : d.rank;
     long long* dst = reinterpret_cast<long long*>(p2pdev::parity_base(d, d.loopback ? d.rank : owner, e)) +
                      (((int64_t)s * FL + f / N) * N + src) * ROW;
     if (t < NBT) {
@@ -1707,7 +1771,16 @@ __global__ __launch_bounds__(1024) void reduce_split_p2p_kernel(
     __syncthreads();
   }
   // C: this rank's records all pushed -> done word to every rank
-  p2pdev::finish(d, nb, e, true);
+  const bool last = p2pdev::finish(d, nb, e, true);
+  if constexpr (FIN) {
+    // the last workgroup waits for every rank's done word, then finalises the
+    // level from the all-gathered table (node_best_finalize_p2p in this launch)
+    if (last) {
+      if (threadIdx.x < kWave) p2pdev::wave_wait(d, d.flags[d.rank] + p2pdev::kDoneBase, e);
+      __syncthreads();
+      level_fin_records<2>(p2p_fbest_table(d, d.rank, e), ctl, p, nvb, NBT, fin);
+    }
+  }
 }
 
 // K5: best threshold of every (node, feature).  One wave per (node, feature)
@@ -1745,16 +1818,24 @@ __global__ __launch_bounds__(256) void split_find_kernel(const long long* __rest
 
 // Per-node arg-max over the features' best thresholds (gain desc, then
 // feature / bin / NA-direction asc): one wave per node, lane = feature.
-// SYS: the records were pushed by peers (N-rank split table): every load of
-// them is a system-scope load (p2p_device.h)
-template <bool SYS = false>
-__device__ __forceinline__ double fb_ld(const double* p) { return SYS ? p2pdev::ld_sys(p) : *p; }
-template <bool SYS = false>
+// MODE 0: plain loads (records of an earlier launch); 1: written by other
+// workgroups of this launch (agent-scope `sc1` loads); 2: pushed by peer ranks
+// (N-rank split table, system-scope loads; p2p_device.h)
+template <int MODE>
+__device__ __forceinline__ double fb_ld(const double* p) {
+  if constexpr (MODE == 2) return p2pdev::ld_sys(p);
+  else if constexpr (MODE == 1) return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <int MODE>
 __device__ __forceinline__ int fb_code(const FeatBest* r) {
-  return SYS ? (int)p2pdev::ld_sys(reinterpret_cast<const uint32_t*>(&r->code)) : r->code;
+  const uint32_t* c = reinterpret_cast<const uint32_t*>(&r->code);
+  if constexpr (MODE == 2) return (int)p2pdev::ld_sys(c);
+  else if constexpr (MODE == 1) return (int)__hip_atomic_load(const_cast<uint32_t*>(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return r->code;
 }
 
-template <bool SYS = false>
+template <int SYS = 0>
 __device__ __forceinline__ void node_best_wave(const FeatBest* __restrict__ fbest, int F, int node, int lane,
                                                NodeSplit* __restrict__ out) {
   const FeatBest* fb = fbest + (int64_t)node * F;
@@ -2088,7 +2169,7 @@ __global__ __launch_bounds__(1024) void node_best_finalize_p2p_kernel(
   const FeatBest* fbest = p2p_fbest_table(d, d.rank, e);
   const int n = ctl[CTL_N];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int node = wid; node < n; node += nw) node_best_wave<true>(fbest, p.F, node, lane, nsplit);
+  for (int node = wid; node < n; node += nw) node_best_wave<2>(fbest, p.F, node, lane, nsplit);
   __syncthreads();
   level_finalize_body(nsplit, ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes, part, next_link, tree,
                       tree_capacity);
@@ -3119,13 +3200,14 @@ H2OMX_API int h2omx_reduce_split(const unsigned long long* partials, int wgpg, i
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
   FeatBest* o = reinterpret_cast<FeatBest*>(out);
   const dim3 grid(slot_cnt, p.F);
+  const LevelFin nofin{};
 #define LAUNCH_RS(NB)                                                                                              \
   if (p.catf != nullptr)                                                                                          \
     hipLaunchKernelGGL((reduce_split_kernel<NB, true>), grid, dim3(1024), 0, stream, partials, wgpg, fg, slot_lo, \
-                       slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o);                      \
+                       slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o, nofin);               \
   else                                                                                                            \
     hipLaunchKernelGGL((reduce_split_kernel<NB, false>), grid, dim3(1024), 0, stream, partials, wgpg, fg,         \
-                       slot_lo, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o)
+                       slot_lo, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o, nofin)
   switch (nbt) {
     case 32: LAUNCH_RS(32); break;
     case 64: LAUNCH_RS(64); break;
@@ -3137,15 +3219,65 @@ H2OMX_API int h2omx_reduce_split(const unsigned long long* partials, int wgpg, i
   return launch_status();
 }
 
+// One-pass level (slot_lo = 0, slot_cnt = the level's slots) with the level
+// finalisation in its last workgroup (LevelFin): replaces reduce_split +
+// level_finalize (node_best_finalize) for levels of <= 64 nodes.  ticket: an
+// int zeroed once (each launch leaves it zero).
+static LevelFin make_fin(int* ctl_next, const float* edges, int max_next_nodes, void* part, void* next_link,
+                         void* tree, int tree_capacity, void* nsplit, int* ticket) {
+  LevelFin f;
+  f.ctl_next = ctl_next; f.edges = edges; f.part = reinterpret_cast<PartInfo*>(part);
+  f.next_link = reinterpret_cast<NodeLink*>(next_link); f.tree = reinterpret_cast<TreeNode*>(tree);
+  f.nsplit = reinterpret_cast<NodeSplit*>(nsplit); f.ticket = ticket;
+  f.max_next_nodes = max_next_nodes; f.tree_capacity = tree_capacity;
+  return f;
+}
+
+H2OMX_API int h2omx_reduce_split_fin(const unsigned long long* partials, int wgpg, int fg, int slot_cnt,
+                                     const long long* parent_full, long long* full, const int* ctl, const void* link,
+                                     const int* nvb, const uint8_t* tree_fmask, const double* qscale,
+                                     const void* params, int nbt, void* out, int* ctl_next, const float* edges,
+                                     int max_next_nodes, void* part, void* next_link, void* tree, int tree_capacity,
+                                     void* nsplit, int* ticket, hipStream_t stream) {
+  const SplitParams p = *reinterpret_cast<const SplitParams*>(params);
+  if (slot_cnt < 1 || wgpg < 1 || fg < 1 || p.F < 1 || ticket == nullptr || nsplit == nullptr) return kBadArg;
+  const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
+  FeatBest* o = reinterpret_cast<FeatBest*>(out);
+  const dim3 grid(slot_cnt, p.F);
+  const LevelFin fin = make_fin(ctl_next, edges, max_next_nodes, part, next_link, tree, tree_capacity, nsplit, ticket);
+#define LAUNCH_RSF(NB)                                                                                             \
+  if (p.catf != nullptr)                                                                                          \
+    hipLaunchKernelGGL((reduce_split_kernel<NB, true, true>), grid, dim3(1024), 0, stream, partials, wgpg, fg, 0,  \
+                       slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o, fin);                 \
+  else                                                                                                            \
+    hipLaunchKernelGGL((reduce_split_kernel<NB, false, true>), grid, dim3(1024), 0, stream, partials, wgpg, fg, 0, \
+                       slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, o, fin)
+  switch (nbt) {
+    case 32: LAUNCH_RSF(32); break;
+    case 64: LAUNCH_RSF(64); break;
+    case 128: LAUNCH_RSF(128); break;
+    case 256: LAUNCH_RSF(256); break;
+    default: return kBadArg;
+  }
+#undef LAUNCH_RSF
+  return launch_status();
+}
+
 // N-rank fused level (reduce_split_p2p_kernel); desc = host P2PDesc image.
 // One pass only (slot_cnt = the level's slots): the host routes multi-pass
 // levels through hist_reduce + all-reduce + split_find.  The split records
 // land in the symmetric buffer's split table (h2omx_node_best_finalize_p2p
 // reads them); capacity: the pushed rows fit a parity, the records half of one.
+// With a ticket (non-null), the launch's last workgroup also waits for every
+// rank's done word and finalises the level (node_best_finalize_p2p folded in:
+// the ticket is unused beyond selecting that mode - the P2P finish ticket
+// picks the workgroup).
 H2OMX_API int h2omx_reduce_split_p2p(const void* desc, const unsigned long long* partials, int wgpg, int fg,
                                      int slot_cnt, const long long* parent_full, long long* full, const int* ctl,
                                      const void* link, const int* nvb, const uint8_t* tree_fmask,
                                      const double* qscale, const void* params, int nbt, int max_blocks,
+                                     int* ctl_next, const float* edges, int max_next_nodes, void* part,
+                                     void* next_link, void* tree, int tree_capacity, void* nsplit, int* ticket,
                                      hipStream_t stream) {
   if (desc == nullptr) return kBadArg;
   const p2pdev::P2PDesc d = *reinterpret_cast<const p2pdev::P2PDesc*>(desc);
@@ -3158,13 +3290,22 @@ H2OMX_API int h2omx_reduce_split_p2p(const void* desc, const unsigned long long*
   if ((int64_t)2 * slot_cnt * p.F * (int64_t)sizeof(FeatBest) > d.cap / 2) return kBadArg;
   const int nb = (int)std::min<int64_t>(items, std::min(std::max(max_blocks, 1), p2pdev::kMaxBlocks));
   const NodeLink* lk = reinterpret_cast<const NodeLink*>(link);
+  const LevelFin fin = make_fin(ctl_next, edges, max_next_nodes, part, next_link, tree, tree_capacity, nsplit, ticket);
+  const bool with_fin = ticket != nullptr;
+  if (with_fin && nsplit == nullptr) return kBadArg;
 #define LAUNCH_RSP(NB)                                                                                             \
-  if (p.catf != nullptr)                                                                                          \
+  if (p.catf != nullptr && with_fin)                                                                              \
+    hipLaunchKernelGGL((reduce_split_p2p_kernel<NB, true, true>), dim3(nb), dim3(1024), 0, stream, d, partials,   \
+                       wgpg, fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, fin);          \
+  else if (p.catf != nullptr)                                                                                     \
     hipLaunchKernelGGL((reduce_split_p2p_kernel<NB, true>), dim3(nb), dim3(1024), 0, stream, d, partials, wgpg,   \
-                       fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p);                     \
+                       fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, fin);                \
+  else if (with_fin)                                                                                              \
+    hipLaunchKernelGGL((reduce_split_p2p_kernel<NB, false, true>), dim3(nb), dim3(1024), 0, stream, d, partials,  \
+                       wgpg, fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, fin);          \
   else                                                                                                            \
     hipLaunchKernelGGL((reduce_split_p2p_kernel<NB, false>), dim3(nb), dim3(1024), 0, stream, d, partials, wgpg,  \
-                       fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p)
+                       fg, slot_cnt, parent_full, full, ctl, lk, nvb, tree_fmask, qscale, p, fin)
   switch (nbt) {
     case 32: LAUNCH_RSP(32); break;
     case 64: LAUNCH_RSP(64); break;
@@ -3217,6 +3358,17 @@ H2OMX_API int h2omx_level_finalize(const void* fbest, const int* ctl, int* ctl_n
   level_finalize_launch(ns, ctl, ctl_next, p, edges, nvb, nbt, max_next_nodes, part, next_link, tree, tree_capacity,
                         max_nodes, tiles, stream);
   return launch_status();
+}
+
+template <int MODE>
+__device__ void level_fin_records(const FeatBest* __restrict__ fbest, const int* __restrict__ ctl, const SplitParams& p,
+                                  const int* __restrict__ nvb, int nbt, const LevelFin& fin) {
+  const int n = ctl[CTL_N];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int node = wid; node < n; node += nw) node_best_wave<MODE>(fbest, p.F, node, lane, fin.nsplit);
+  __syncthreads();
+  level_finalize_body(fin.nsplit, ctl, fin.ctl_next, p, fin.edges, nvb, nbt, fin.max_next_nodes, fin.part,
+                      fin.next_link, fin.tree, fin.tree_capacity);
 }
 
 // N-rank level finalisation (after h2omx_reduce_split_p2p, same desc)

@@ -130,6 +130,12 @@ class HipTreeBuilder:
     PK32 = True
     FUSE_GRAD = False
     CHAIN_BEGIN = True
+    # level finalisation in the last workgroup of the level's reduce + split scan:
+    # N-rank (P2P) levels -3 % on the loopback-8 proxy; one rank neutral
+    # (headline / 1.375M shard within noise, profiles/r6/fused_fin_ab_r6e.txt),
+    # so the single-rank level keeps the separate finalisation launch
+    FUSE_FIN = True
+    FUSE_FIN_LOCAL = False
     # segmented engine: part_scatter moves each row's (g, s2) into segment order with it
     PERMUTE_GS = True
     # direct levels of <= 16 eligible features store them per row for the partition
@@ -542,6 +548,22 @@ class HipTreeBuilder:
             # histograms are reduced, all-reduced and scanned in separate launches
             rs = comm is None or fuse_p2p
             fbest = self._buf("fbest", max_nodes * F * FEAT_BEST_BYTES // 8, torch.float64)
+            # the level's finalisation buffers (needed by the reduce when it finalises)
+            next_nodes = 2 * max_nodes
+            part = self._buf("part", max_nodes * PART_INFO_BYTES // 4, torch.int32)
+            nl = None
+            if not last:
+                nl = self._buf(f"link{nxt}", next_nodes * NODE_LINK_BYTES // 4, torch.int32)
+                link[nxt] = nl
+            nsplit = self._buf("nsplit", max_nodes * 9, torch.float64)  # NodeSplit = 72 B
+            # one-pass levels of <= 64 nodes finalise in the last workgroup of their
+            # reduce + split scan (LevelFin in csrc/tree_kernels.hip)
+            fin = rs and max_nodes <= 64 and ((fuse_p2p and self.FUSE_FIN)
+                                              or (comm is None and self.FUSE_FIN_LOCAL and plan["passes"] == 1))
+            if fin and getattr(self, "_fin_ticket", None) is None:
+                self._fin_ticket = torch.zeros((1,), dtype=torch.int32, device=self.dev)   # each launch leaves 0
+            fin_args = (P(ctl_nxt), P(bm.edges), next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
+                        P(nsplit), P(self._fin_ticket if fin else None))
 
             def reduce(n_groups, wgpg, fg, slot_lo, slot_cnt):
                 if rs and fuse_p2p:
@@ -550,9 +572,19 @@ class HipTreeBuilder:
                     ops.check(lib.h2omx_reduce_split_p2p(p2p.desc_ptr, P(partials), wgpg, fg, slot_cnt, P(full_prev),
                                                          P(full_cur), P(ctl_cur), P(link[cur]), P(bm.nvb),
                                                          P(tree_fmask), P(self.qscale), spp, nbt,
-                                                         self.P2P_BLOCKS, st), "reduce_split_p2p")
+                                                         self.P2P_BLOCKS,
+                                                         *(fin_args if fin else (None, None, 0, None, None, None, 0,
+                                                                                 None, None)), st),
+                              "reduce_split_p2p")
                     comm.stats["p2p_calls"] += 1
                     comm.stats["p2p_bytes"] += max_slots * self.per_node * 8
+                elif rs and fin:
+                    if slot_lo != 0 or slot_cnt < max_slots:
+                        raise RuntimeError("reduce_split_fin: multi-pass level")   # excluded by fin
+                    ops.check(lib.h2omx_reduce_split_fin(P(partials), wgpg, fg, slot_cnt, P(full_prev), P(full_cur),
+                                                         P(ctl_cur), P(link[cur]), P(bm.nvb), P(tree_fmask),
+                                                         P(self.qscale), spp, nbt, P(fbest), *fin_args, st),
+                              "reduce_split_fin")
                 elif rs:
                     ops.check(lib.h2omx_reduce_split(P(partials), wgpg, fg, slot_lo, slot_cnt, P(full_prev),
                                                      P(full_cur), P(ctl_cur), P(link[cur]), P(bm.nvb),
@@ -608,19 +640,14 @@ class HipTreeBuilder:
             if comm is not None and not fuse_p2p:
                 with T("allreduce"):
                     comm.all_reduce_(built[: max_slots * self.per_node])
-            next_nodes = 2 * max_nodes
-            part = self._buf("part", max_nodes * PART_INFO_BYTES // 4, torch.int32)
-            nl = None
-            if not last:
-                nl = self._buf(f"link{nxt}", next_nodes * NODE_LINK_BYTES // 4, torch.int32)
-                link[nxt] = nl
-            nsplit = self._buf("nsplit", max_nodes * 9, torch.float64)  # NodeSplit = 72 B
             with T("split"):
                 if not rs:
                     ops.check(lib.h2omx_split_find(P(built), P(full_prev), P(full_cur), P(ctl_cur),
                                                    P(link[cur]), P(bm.nvb), P(tree_fmask), P(self.qscale), spp,
                                                    max_nodes, nbt, P(fbest), st), "split_find")
-                if fuse_p2p:
+                if fin:
+                    pass   # finalised inside the reduce launch
+                elif fuse_p2p:
                     # waits for every rank's share of the split records (all-gathered
                     # into this rank's split table by reduce_split_p2p)
                     ops.check(lib.h2omx_node_best_finalize_p2p(p2p.desc_ptr, P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),

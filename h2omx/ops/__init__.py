@@ -24,7 +24,8 @@ TREE_SIGS = {
     "h2omx_hist_build_grad": "PLPPPIIIIIIIIIPPPPPPIPPIIIPS",
     "h2omx_split_find": "PPPPPPPPPIIPS",
     "h2omx_reduce_split": "PIIIIPPPPPPPPIPS",
-    "h2omx_reduce_split_p2p": "PPIIIPPPPPPPPIIS",
+    "h2omx_reduce_split_p2p": "PPIIIPPPPPPPPIIPPIPPPIPPS",
+    "h2omx_reduce_split_fin": "PIIIPPPPPPPPIPPPIPPPIPPS",
     "h2omx_node_best_finalize_p2p": "PPPPPPIIPPPIPS",
     "h2omx_leaf_finalize_p2p": "PPPPPPIIPIIPPLPS",
     "h2omx_level_finalize": "PPPPPPIIPPPIPIPS",

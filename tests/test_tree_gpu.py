@@ -236,6 +236,31 @@ def test_pk32_rows_match_pk64(cuda_dev, monkeypatch, dist, depth, sample_rate):
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
 
 
+@pytest.mark.parametrize("dist,depth,min_rows", [("bernoulli", 5, 3), ("gaussian", 7, 400), ("multinomial", 4, 3)])
+def test_level_finalisation_in_reduce_launch(cuda_dev, monkeypatch, dist, depth, min_rows):
+    """The level finalisation folded into the last workgroup of the reduce +
+    split scan (write-through split records, ticket, agent-scope loads:
+    FUSE_FIN_LOCAL) builds bit-identical trees to its separate launch."""
+    import h2omx.models.tree.engine as E
+
+    X, y = _data(n=300_000, F=10, seed=31, task={"bernoulli": "bin", "gaussian": "reg"}.get(dist, "multi"))
+    _, bg = _both(X, y, 255)
+    tp = TreeParams(max_depth=depth, min_rows=min_rows, learn_rate=0.2)
+    yt = torch.from_numpy(y).cuda()
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(E.HipTreeBuilder, "FUSE_FIN_LOCAL", flag)
+        out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=4, tparams=tp, seed=3,
+                                   nclass=int(y.max()) + 1 if dist == "multinomial" else 1)
+    a, b = out[False], out[True]
+    assert a.trees.shape == b.trees.shape
+    for t in range(a.trees.shape[0]):
+        reach = a.compact()[t]
+        assert reach == b.compact()[t]
+        for f in ("feat", "bin", "value"):
+            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f])
+
+
 @pytest.mark.parametrize("dist,depth,sample_rate,min_rows,lds_kb", [
     ("bernoulli", 5, 1.0, 3, 0), ("bernoulli", 6, 0.6, 400, 0), ("gaussian", 8, 0.8, 50, 0),
     ("multinomial", 4, 1.0, 3, 0), ("bernoulli", 1, 1.0, 3, 0), ("gaussian", 6, 1.0, 3, 16)])
@@ -363,7 +388,9 @@ def test_graph_replay_matches_eager(cuda_dev, monkeypatch, dist, depth, min_rows
         monkeypatch.setenv("H2OMX_TREE_GRAPH", flag)
         out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=ntrees, tparams=tp, seed=5)
     assert not made[0].graph_used and made[1].graph_used, made[1].graph_error
-    if dist == "bernoulli" and E.HipTreeBuilder.CHAIN_BEGIN:
+    from h2omx.models.tree.engine import HipTreeBuilder as _HTB
+
+    if dist == "bernoulli" and _HTB.CHAIN_BEGIN:
         assert made[1].graph_chain
     a, b = out["0"], out["1"]
     assert a.trees.shape == b.trees.shape
