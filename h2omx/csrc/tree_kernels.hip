@@ -2191,6 +2191,26 @@ __global__ __launch_bounds__(1024) void node_best_finalize_p2p_kernel(
 // (order-independent: deterministic).
 constexpr int PART_LDS_NODES = 256;   // levels up to this many nodes read their split records from LDS
 
+// Leaf-sum replicas (scan engine): each partition workgroup adds its folded
+// leaf window into slice (workgroup mod reps) of leaf_acc = [reps][3 * cap]
+// instead of all 1024 workgroups adding into the same ~3 x 63 words (the
+// same-address device atomics cost ~15 us of the 65 us final partition at 11M
+// rows, profiles/r6/partition_atomics_r6g.txt); the leaf finalisations read the
+// sum of the slices.  reps = qs[10] (the host sets it; 1 = one slice).
+__device__ __forceinline__ int leaf_reps(const double* __restrict__ qs) {
+  const int r = (int)qs[10];
+  return r < 1 ? 1 : r;
+}
+__device__ __forceinline__ long long leaf_sum(const unsigned long long* __restrict__ acc, int64_t i, int reps,
+                                              int64_t stride) {
+  long long v = (long long)acc[i];
+  for (int r = 1; r < reps; ++r) v += (long long)acc[i + r * stride];
+  return v;
+}
+__device__ __forceinline__ void leaf_zero(unsigned long long* __restrict__ acc, int64_t i, int reps, int64_t stride) {
+  for (int r = 0; r < reps; ++r) acc[i + r * stride] = 0ull;
+}
+
 // NIDM bit 0: nid (input) is an int16 stream, bit 1: nid_out is int16 (fused pipeline)
 template <bool PREF, int RPL, int NIDM = 0>
 __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restrict__ codes, int64_t npad,
@@ -2378,6 +2398,8 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
     }
   }
   if (use_lds) {
+    // this workgroup's replica slice of the leaf sums
+    const int64_t rep_off = (int64_t)(blockIdx.x % leaf_reps(qs)) * 3 * cap;
     __syncthreads();
     // fold the R copies: thread t sums slot t's copies starting at copy t mod R
     // (rotated so the threads of a lane group hit different banks; a shuffle
@@ -2386,7 +2408,7 @@ __global__ __launch_bounds__(256) void partition_kernel(const uint8_t* __restric
       for (int t = threadIdx.x; t < 3 * win; t += blockDim.x) {
         unsigned long long v = 0ull;
         for (int c = 0; c < R; ++c) v += lacc[t * R + ((c + t) & (R - 1))];
-        if (v && base + t / 3 < cap) atomicAdd(leaf_acc + 3 * base + t, v);
+        if (v && base + t / 3 < cap) atomicAdd(leaf_acc + rep_off + 3 * base + t, v);
       }
     }
   }
@@ -2716,11 +2738,13 @@ __global__ __launch_bounds__(256) void leaf_finalize_kernel(const unsigned long 
                                                             const double* __restrict__ qs, SplitParams p,
                                                             TreeNode* __restrict__ tree, int cap) {
   const int total = min(ctl_final[CTL_TOTAL], cap);
+  const int reps = leaf_reps(qs);
+  const int64_t st = 3 * (int64_t)cap;
   for (int gid = blockIdx.x * blockDim.x + threadIdx.x; gid < total; gid += gridDim.x * blockDim.x) {
     TreeNode nd = tree[gid];
-    const double G = (double)(long long)acc[3 * gid] / qs[4];
-    const double H = (double)(long long)acc[3 * gid + 1] / qs[5];
-    const double W = (double)(long long)acc[3 * gid + 2] / qs[6];
+    const double G = (double)leaf_sum(acc, 3 * gid, reps, st) / qs[4];
+    const double H = (double)leaf_sum(acc, 3 * gid + 1, reps, st) / qs[5];
+    const double W = (double)leaf_sum(acc, 3 * gid + 2, reps, st) / qs[6];
     if (nd.feat < 0) {
       nd.value = (float)clamp_bound(leaf_value(G, H, W, p), p, gid, cap);
       nd.weight = (float)W;
@@ -2740,9 +2764,13 @@ __global__ __launch_bounds__(1024) void leaf_finalize_begin_kernel(
     int* __restrict__ ctl0, NodeLink* __restrict__ link0, long long row_base, int* __restrict__ tree_ctr) {
   const int total = min(ctl_final[CTL_TOTAL], cap);
   const double s4 = qs[4], s5 = qs[5], s6 = qs[6];
+  const int reps = leaf_reps(qs);
+  const int64_t st = 3 * (int64_t)cap;
   for (int gid = threadIdx.x; gid < total; gid += blockDim.x) {
-    const long long ag = (long long)acc[3 * gid], ah = (long long)acc[3 * gid + 1], aw = (long long)acc[3 * gid + 2];
-    acc[3 * gid] = 0ull; acc[3 * gid + 1] = 0ull; acc[3 * gid + 2] = 0ull;
+    const long long ag = leaf_sum(acc, 3 * gid, reps, st), ah = leaf_sum(acc, 3 * gid + 1, reps, st),
+                    aw = leaf_sum(acc, 3 * gid + 2, reps, st);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) leaf_zero(acc, 3 * gid + k, reps, st);
     TreeNode nd = tree[gid];
     if (nd.feat < 0) {
       const double G = (double)ag / s4, H = (double)ah / s5, W = (double)aw / s6;
@@ -2778,6 +2806,8 @@ __global__ __launch_bounds__(LEAF_P2P_THREADS) void leaf_finalize_p2p_kernel(
   const int64_t per_src = 3 * (int64_t)cap;   // one rank's sums in the receiving buffer
   const int src = d.loopback ? 0 : d.rank;
   const int nr = d.loopback ? 1 : d.world;
+  const int reps = leaf_reps(qs);
+  const int64_t st = 3 * (int64_t)cap;
   for (int c = b; c * LEAF_P2P_THREADS < total; c += nb) {
     const int gid = c * LEAF_P2P_THREADS + t;
     if (gid < total)
@@ -2785,7 +2815,7 @@ __global__ __launch_bounds__(LEAF_P2P_THREADS) void leaf_finalize_p2p_kernel(
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(
                                       p2pdev::parity_base(d, d.loopback ? d.rank : r, e)) + src * per_src + 3 * gid;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) p2pdev::st_sys(dst + k, acc[3 * gid + k]);
+        for (int k = 0; k < 3; ++k) p2pdev::st_sys(dst + k, (unsigned long long)leaf_sum(acc, 3 * gid + k, reps, st));
       }
   }
   p2pdev::post_wait(d, b, e);
@@ -2804,7 +2834,10 @@ __global__ __launch_bounds__(LEAF_P2P_THREADS) void leaf_finalize_p2p_kernel(
     // GLOBAL sums, as after the all-reduce path (a later reader of leaf_acc sees
     // the same values on every rank)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) acc[3 * gid + k] = begin ? 0ull : (unsigned long long)a3[k];
+    for (int k = 0; k < 3; ++k) {
+      leaf_zero(acc, 3 * gid + k, reps, st);
+      if (!begin) acc[3 * gid + k] = (unsigned long long)a3[k];
+    }
     TreeNode nd = tree[gid];
     if (nd.feat < 0) {
       const double G = (double)a3[0] / s4, H = (double)a3[1] / s5, W = (double)a3[2] / s6;
@@ -2861,8 +2894,8 @@ __global__ __launch_bounds__(1024) void mono_newton_kernel(const unsigned long l
   }
   for (int i = threadIdx.x; i < total; i += blockDim.x) {
     if (dep[i] >= 0 && tree[i].feat < 0) {
-      SG[i] = (double)(long long)acc[3 * i] / qs[4];
-      SH[i] = (double)(long long)acc[3 * i + 1] / qs[5];
+      SG[i] = (double)leaf_sum(acc, 3 * i, leaf_reps(qs), 3 * (int64_t)cap) / qs[4];
+      SH[i] = (double)leaf_sum(acc, 3 * i + 1, leaf_reps(qs), 3 * (int64_t)cap) / qs[5];
     }
   }
   __syncthreads();
@@ -2885,7 +2918,7 @@ __global__ __launch_bounds__(1024) void mono_newton_kernel(const unsigned long l
       TreeNode nd = tree[i];
       const double lo = LO[i], hi = HI[i];
       if (nd.feat < 0) {
-        const double W = (double)(long long)acc[3 * i + 2] / qs[6];
+        const double W = (double)leaf_sum(acc, 3 * i + 2, leaf_reps(qs), 3 * (int64_t)cap) / qs[6];
         nd.value = (float)fmin(fmax(leaf_value(SG[i], SH[i], W, p), lo), hi);
         tree[i] = nd;
         continue;
@@ -4393,6 +4426,9 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
   best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
   double ptc = NAN;   // the node's parent gain term (direct_scan_feature)
   long long tg_row = 0, ts_row = 0;   // node totals (G_q, S_q), accumulated in the first batch
+  // eligible-code rows only for nodes scanned in ONE batch (the partition falls
+  // back to the code rows for the others: nodeq -1)
+  uint8_t* const ecw = (ec.codes && nfl <= bat) ? ec.codes : nullptr;
   for (int b0 = 0; b0 < nfl; b0 += bat) {
     const int nb = min(bat, nfl - b0);
     for (int j = t; j < nb * per_f; j += blockDim.x) hist[j] = 0;
@@ -4407,7 +4443,7 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
       direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
       if (b0 == 0) { tg_row += gq; ts_row += sq; }
       direct_row_atomics<NBT>(row, flist + b0, nb, packed, per_f, hist, gq, sq, c0,
-                              ec.codes ? ec.codes + (int64_t)j * ec.stride : nullptr, ec.stride);
+                              ecw ? ecw + (int64_t)j * ec.stride : nullptr, ec.stride);
     }
     __syncthreads();
     if (b0 == 0) {
@@ -4435,7 +4471,7 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
     const long long tgq = tot_s[0][0] + tot_s[0][1] + tot_s[0][2] + tot_s[0][3];
     const long long tsq = tot_s[1][0] + tot_s[1][1] + tot_s[1][2] + tot_s[1][3];
     out[node] = direct_node_split(b, tgq, tsq, ig, is);
-    if (ec.nodeq) ec.nodeq[node] = direct_feat_pos(flist, nfl, b.key);
+    if (ec.nodeq) ec.nodeq[node] = ecw ? direct_feat_pos(flist, nfl, b.key) : -1;
   }
 }
 
@@ -4862,6 +4898,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
   double ptc = NAN;   // the node's parent gain term (direct_scan_feature)
   long long tg_row = 0, ts_row = 0;
+  // eligible-code rows only for nodes scanned in ONE batch (see seg_direct_kernel)
+  uint8_t* const ecw = (ec.codes && nfl <= bat) ? ec.codes : nullptr;
   wave_lds_sync();
   for (int b0 = 0; b0 < max(nfl, 1); b0 += bat) {
     const int nb = min(bat, nfl - b0);
@@ -4878,7 +4916,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       if (b0 == 0) { tg_row += gq; ts_row += sq; }
       if (nb <= 0) continue;
       direct_row_atomics<NBT>(row, flist + b0, nb, packed, per_f, hist, gq, sq, c0,
-                              ec.codes ? ec.codes + (int64_t)j * ec.stride : nullptr, ec.stride);
+                              ecw ? ecw + (int64_t)j * ec.stride : nullptr, ec.stride);
     }
     wave_lds_sync();
     for (int q = 0; q < nb; ++q) {
@@ -4892,7 +4930,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   ts_row = wave_sum_i64(ts_row);
   if (lane == 0) {
     out[node] = direct_node_split(best, tg_row, ts_row, ig, is);
-    if (ec.nodeq) ec.nodeq[node] = direct_feat_pos(flist, nfl, best.key);
+    if (ec.nodeq) ec.nodeq[node] = ecw ? direct_feat_pos(flist, nfl, best.key) : -1;
   }
 }
 
@@ -5041,10 +5079,10 @@ __global__ __launch_bounds__(256) void part_count_wave_kernel(const uint8_t* __r
   if (pi.child >= 0) {
     const int lo = seg_start[node] + (c - pc_first[node]) * PC_ROWS;
     const int hi = min(lo + PC_ROWS, seg_start[node] + seg_cnt[node]);
-    const int eq = ecodes ? nodeq[node] : 0;
+    const int eq = ecodes ? nodeq[node] : -1;   // -1: the node's codes were not stored
     for (int j = lo + lane; j < hi; j += 64) {
       int d;
-      if (ecodes) {
+      if (eq >= 0) {
         const int b = ecodes[(int64_t)j * ecs + eq];
         d = part_right(pi, b, nbt);
       } else {
@@ -5098,7 +5136,7 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
       if (pi.child >= 0) {
         if (dirb) {
           dir = dirb[j];
-        } else if (ecodes) {
+        } else if (ecodes && nodeq[node] >= 0) {
           const int b = ecodes[(int64_t)j * ecs + nodeq[node]];
           dir = part_right(pi, b, nbt);
         } else {

@@ -130,6 +130,9 @@ class HipTreeBuilder:
     PK32 = True
     FUSE_GRAD = False
     CHAIN_BEGIN = True
+    # partition workgroups spread their leaf-sum folds over this many slices
+    # (same-address atomic contention; profiles/r6/partition_atomics_r6g.txt)
+    LEAF_REPS = 16
     # level finalisation in the last workgroup of the level's reduce + split scan:
     # N-rank (P2P) levels -3 % on the loopback-8 proxy; one rank neutral
     # (headline / 1.375M shard within noise, profiles/r6/fused_fin_ab_r6e.txt),
@@ -252,6 +255,12 @@ class HipTreeBuilder:
         #   deeper than DEEP_DEPTH (DRF's default max_depth 20).
         eng = os.environ.get("H2OMX_TREE_ENGINE", "auto")
         self.segmented = eng == "seg" or (eng == "auto" and params.max_depth > self.DEEP_DEPTH)
+        # leaf-sum replicas of the scan engine's partitions ([reps][3 x capacity],
+        # qscale[10]; csrc/tree_kernels.hip leaf_reps): small trees only
+        self.leaf_reps = self.LEAF_REPS if (not self.segmented and self.capacity <= 4096) else 1
+        if self.leaf_reps > 1:
+            self.leaf_acc = torch.zeros((self.leaf_reps * self.capacity * 3,), dtype=torch.int64, device=d)
+        self.qscale[10] = float(self.leaf_reps)
         if self.segmented:
             self.fuse_route, self.nid2 = False, None
             self.implicit_root = False
@@ -710,7 +719,7 @@ class HipTreeBuilder:
                                                       P(link[0] if chain else None), self.row_base,
                                                       P(self.tree_ctr if chain else None), st), "leaf_finalize_p2p")
                 comm.stats["p2p_calls"] += 1
-                comm.stats["p2p_bytes"] += self.leaf_acc.numel() * 8
+                comm.stats["p2p_bytes"] += self.capacity * 3 * 8
             elif chain:
                 ops.check(lib.h2omx_leaf_finalize_begin(P(self.leaf_acc), P(final_ctl), P(self.qscale), spp,
                                                         P(self.tree_buf), self.capacity, P(smax), p.mode,
@@ -931,8 +940,11 @@ class HipTreeBuilder:
                 else:
                     dmode = 0
                 ec = None
-                # every eligible feature in one LDS batch (batch sizes of h2omx_seg_direct)
-                one_batch = {0: 98304, 1: 8192, 2: 1 << 30}[dmode] // (16 * nbt) >= n_elig
+                # every eligible feature in one LDS batch (batch sizes of h2omx_seg_direct;
+                # wave mode: packed nodes - all but those of >= 64K rows - hold twice the
+                # features per batch, and a node scanned in several batches stores no
+                # eligible codes: the partition reads its code rows instead)
+                one_batch = ({0: 98304, 1: 8192, 2: 1 << 30}[dmode] // (16 * nbt)) * (2 if dmode == 1 else 1) >= n_elig
                 if self.ECODES and n_elig <= 16 and one_batch:
                     ecs = 8 if n_elig <= 8 else 16
                     ec = (B("ecodes", (n + 64) * ecs, torch.uint8), ecs, B("nodeq", max_nodes, i32))
