@@ -586,7 +586,9 @@ __global__ __launch_bounds__(1024) void hist_build_kernel(
     width_s[fi] = w;
     int r = NBT / w;
     r = r < 1 ? 1 : (r > 64 ? 64 : r);
-    if (COP > 1) r = 1;   // the copies already spread the lanes
+    // the copies already spread the lanes (slicing low-cardinality features
+    // inside the copies' space measured slower: profiles/r6/l0_sliced_ab_r6m.txt)
+    if (COP > 1) r = 1;
     rep_s[fi] = r;
     rcp_s[fi] = 1.0f / (float)r;   // lane % rep without an integer division (lane < 64: exact)
   }
@@ -1261,8 +1263,26 @@ __device__ __forceinline__ int ua_count(double x, double lo, double span, int nb
   return k;
 }
 
+// ua_count against a table of the exact cuts (cut[k] = ua_cut(lo, span, k, nb),
+// k < nb): the estimate comes from a multiply by nb / span instead of a
+// division and is then corrected against the exact cuts.  The cuts are
+// non-decreasing in k, so the two correction loops end on the unique count
+// whatever the start: the same k as ua_count, without its three divisions.
+__device__ __forceinline__ int ua_count_tab(double x, double lo, double rs, int nb, const double* __restrict__ cut) {
+#pragma clang fp contract(off)
+  if (x == -INFINITY) return 0;
+  if (x == INFINITY) return nb - 1;
+  const double r = (x - lo) * rs;
+  int k = r < 0.0 ? 0 : (r >= (double)(nb - 1) ? nb - 1 : (int)r);
+  while (k < nb - 1 && cut[k + 1] <= x) ++k;
+  while (k > 0 && cut[k] > x) --k;
+  return k;
+}
+
+// cut_tab: 64 doubles of per-wave LDS (nullptr: the division form)
 template <int NBT, int B>
-__device__ uint32_t adaptive_candidates(const long long* si, int m, int node, int f, const SplitParams& p) {
+__device__ uint32_t adaptive_candidates(const long long* si, int m, int node, int f, const SplitParams& p,
+                                        double* cut_tab = nullptr) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
   int mode = p.hist_mode;
@@ -1310,7 +1330,27 @@ __device__ uint32_t adaptive_candidates(const long long* si, int m, int node, in
     }
   }
   uint32_t hit = 0;
-  if (mode == 1) {
+  if (mode == 1 && cut_tab != nullptr && nb <= 64) {
+    // UniformAdaptive with <= 64 cuts (every level from depth 4 on with H2O's
+    // defaults): the cuts once per feature (one division per lane), and each
+    // interior boundary counted once - bin t's upper midpoint is bin t + 1's
+    // lower one (same operands, same bits), so the lower count is the
+    // neighbour's upper count.  Same candidate bits as the branch below.
+    if (lane < nb) cut_tab[lane] = ua_cut(lo_v, span, lane, nb);
+    wave_lds_sync();
+    const double rs = (double)nb / span;
+    int cR[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) cR[k] = ((inner >> k) & 1u) ? ua_count_tab(mR[k], lo_v, rs, nb, cut_tab) : 0;
+    const int prev = __shfl_up(cR[B - 1], 1, kWave);
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+      const int t = lane * B + k;
+      const int cL = t > lo ? (k > 0 ? cR[k - (k > 0)] : prev) : 0;
+      if (((inner >> k) & 1u) && cR[k] > cL) hit |= 1u << k;
+    }
+    wave_lds_sync();   // the table is rewritten by the wave's next feature
+  } else if (mode == 1) {
 #pragma unroll
     for (int k = 0; k < B; ++k)
       if (((inner >> k) & 1u) && ua_count(mR[k], lo_v, span, nb) > ua_count(mL[k], lo_v, span, nb)) hit |= 1u << k;
@@ -4191,12 +4231,46 @@ struct DirectBest {
   long long key;   // (feature << 32 | code), smallest wins ties; LLONG_MAX = none
 };
 
+// Per-lane running best over every feature a wave scans: one wave arg-max per
+// node (lane_best_reduce) instead of one per feature.  key = f * 1024 + code
+// (code = 2 * bin + na_left < 1024, f < 1024): ordered like DirectBest::key, so
+// (max gain, smallest key) over lanes is the sequential per-feature result.
+struct LaneBest {
+  double gain, GL, SL;
+  int key;   // INT_MAX = none
+};
+
+__device__ __forceinline__ void lane_best_init(LaneBest& b) {
+  b.gain = -INFINITY; b.GL = b.SL = 0.0; b.key = 0x7fffffff;
+}
+
+// every lane of the wave returns the wave's best (called by all 64 lanes)
+__device__ __forceinline__ DirectBest lane_best_reduce(const LaneBest& lb) {
+  double g = lb.gain;
+  int k = lb.key;
+  wave_argmax(g, k);
+  DirectBest r;
+  r.gain = -INFINITY; r.GL = r.SL = 0.0; r.key = 0x7fffffffffffffffLL;
+  if (k != 0x7fffffff) {
+    const unsigned long long own = __ballot(lb.key == k);   // keys are unique per lane
+    const int src = __builtin_amdgcn_readfirstlane(__ffsll((long long)own) - 1);
+    r.gain = g;
+    r.GL = readlane_f64(lb.GL, src);
+    r.SL = readlane_f64(lb.SL, src);
+    r.key = ((long long)(k >> 10) << 32) | (unsigned)(k & 1023);
+  }
+  return r;
+}
+
 // the split scan of one feature's LDS histogram by one wave (split_find's
-// feat_best_wave on exact int64 rows); PACKED: one packed u64 per bin
+// feat_best_wave on exact int64 rows) into the lanes' running bests; PACKED:
+// one packed u64 per bin, scanned as ONE int64 prefix sum ((int32 G_q << 32) +
+// uint32 S_q: the node's S_q sum stays below 2^32 - the packed-atomics bound -
+// so the halves never carry and both prefix sums are exact)
 template <int NBT, bool PACKED>
 __device__ __forceinline__ void direct_scan_feature(const long long* __restrict__ h, int node, int f, int m,
                                                     double ig, double is, const SplitParams& p, int lane,
-                                                    DirectBest& best, double& ptc) {
+                                                    LaneBest& lb, double& ptc, double* cut_tab) {
   constexpr int B = NBT <= 64 ? 1 : NBT / 64;
   constexpr int NA_LANE = (NBT - 1) / B, NA_K = (NBT - 1) % B;
   long long gi[B], si[B];
@@ -4221,7 +4295,16 @@ __device__ __forceinline__ void direct_scan_feature(const long long* __restrict_
   long long pg[B], ps[B];
 #pragma unroll
   for (int k = 0; k < B; ++k) { lg += gi[k]; ls += si[k]; pg[k] = lg; ps[k] = ls; }
-  const long long xg = wave_incl_scan_i64(lg), xs = wave_incl_scan_i64(ls);
+  long long xg, xs;
+  if constexpr (PACKED) {
+    const long long xp = wave_incl_scan_i64((long long)(((unsigned long long)(uint32_t)(int)lg << 32) +
+                                                        (unsigned long long)(uint32_t)ls));
+    xg = (long long)(int)(uint32_t)((unsigned long long)xp >> 32);
+    xs = (long long)(uint32_t)(unsigned long long)xp;
+  } else {
+    xg = wave_incl_scan_i64(lg);
+    xs = wave_incl_scan_i64(ls);
+  }
   const long long tg_i = readlane_i64(xg, 63) + ng_i, ts_i = readlane_i64(xs, 63) + ns_i;
   const long long eg = xg - lg, es = xs - ls;
   const double ng = (double)ng_i * ig, ns = (double)ns_i * is;
@@ -4230,7 +4313,7 @@ __device__ __forceinline__ void direct_scan_feature(const long long* __restrict_
   int fbc = 0x7fffffff;
   double fGL = 0, fSL = 0;
   const int mf = p.mono ? (int)p.mono[f] : 0;
-  const uint32_t cand = p.hist_mode ? adaptive_candidates<NBT, B>(si, m, node, f, p) : 0xffffffffu;
+  const uint32_t cand = p.hist_mode ? adaptive_candidates<NBT, B>(si, m, node, f, p, cut_tab) : 0xffffffffu;
   // (tg, ts) are the node's exact totals, the same for every feature of the node:
   // its parent term is computed by the first feature scanned (ptc NaN before)
   if (ptc != ptc) ptc = parent_term(tg, ts, p);
@@ -4249,15 +4332,9 @@ __device__ __forceinline__ void direct_scan_feature(const long long* __restrict_
       }
     }
   }
-  double bg = fbg;
-  int bc = fbc;
-  wave_argmax(bg, bc);
-  if (bc != 0x7fffffff) {
-    const unsigned long long own = __ballot(fbc == bc);
-    const int src = __builtin_amdgcn_readfirstlane(__ffsll((long long)own) - 1);
-    const double GL = readlane_f64(fGL, src), SL = readlane_f64(fSL, src);
-    const long long key = ((long long)f << 32) | (unsigned)bc;
-    if (bg > best.gain || (bg == best.gain && key < best.key)) { best.gain = bg; best.key = key; best.GL = GL; best.SL = SL; }
+  if (fbc != 0x7fffffff) {
+    const int key = f * 1024 + fbc;
+    if (fbg > lb.gain || (fbg == lb.gain && key < lb.key)) { lb.gain = fbg; lb.key = key; lb.GL = fGL; lb.SL = fSL; }
   }
 }
 
@@ -4307,6 +4384,11 @@ struct ECodes {
   int* nodeq;
   const uint8_t* crow;   // code rows in segment order (SegRows::in), nullptr = gather codes_rm by row id
   const int* cpos;       // row j's position in crow (rows moved once, then only positions), nullptr = j
+  // crow layout: row-major rows (rs = fp, fs = 1) or column-major feature
+  // planes (rs = 1, fs = plane positions; seg_colmajor_kernel): the code of
+  // feature f at position q is crow[q * rs + f * fs]
+  int rs;
+  int64_t fs;
 };
 
 // XCD-aware block order: dispatch puts block b on XCD b % 8; renumber so XCD x
@@ -4350,7 +4432,7 @@ __device__ __forceinline__ void direct_chunk_atomics(int q0, int nb, bool packed
 // erow (ECodes, nb <= 16): the row's codes of the node's features stored as
 // ONE 8- or 16-byte vector (estride) at its segment position
 template <int NBT, typename FL>
-__device__ __forceinline__ void direct_row_atomics(const uint8_t* __restrict__ row, const FL* flist, int nb,
+__device__ __forceinline__ void direct_row_atomics(const uint8_t* __restrict__ row, int64_t fs, const FL* flist, int nb,
                                                    bool packed, int per_f, long long* hist, long long gq, long long sq,
                                                    const uint32_t* c0, uint8_t* erow, int estride) {
   const bool live = gq != 0 || sq != 0;
@@ -4358,7 +4440,7 @@ __device__ __forceinline__ void direct_row_atomics(const uint8_t* __restrict__ r
   const unsigned long long pk = ((unsigned long long)(uint32_t)(int)gq << 32) | (unsigned long long)sq;
   uint32_t c1[DIRECT_FB];
 #pragma unroll
-  for (int u = 0; u < DIRECT_FB; ++u) c1[u] = (DIRECT_FB + u < nb) ? row[flist[DIRECT_FB + u]] : 0u;
+  for (int u = 0; u < DIRECT_FB; ++u) c1[u] = (DIRECT_FB + u < nb) ? row[flist[DIRECT_FB + u] * fs] : 0u;
   if (erow) {
     const uint32_t w0 = c0[0] | (c0[1] << 8) | (c0[2] << 16) | (c0[3] << 24);
     const uint32_t w1 = c0[4] | (c0[5] << 8) | (c0[6] << 16) | (c0[7] << 24);
@@ -4376,7 +4458,7 @@ __device__ __forceinline__ void direct_row_atomics(const uint8_t* __restrict__ r
   uint32_t c[DIRECT_FB];
   for (int q0 = 2 * DIRECT_FB; q0 < nb; q0 += DIRECT_FB) {
 #pragma unroll
-    for (int u = 0; u < DIRECT_FB; ++u) c[u] = (q0 + u < nb) ? row[flist[q0 + u]] : 0u;
+    for (int u = 0; u < DIRECT_FB; ++u) c[u] = (q0 + u < nb) ? row[flist[q0 + u] * fs] : 0u;
     direct_chunk_atomics<NBT>(q0, nb, packed, per_f, hist, pk, gq, sq, c);
   }
 }
@@ -4401,6 +4483,7 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
   __shared__ long long tot_s[2][4];
   __shared__ double wb_gain[4], wb_GL[4], wb_SL[4];
   __shared__ long long wb_key[4];
+  __shared__ double cut_s[4][64];   // per-wave UniformAdaptive cut tables
   const int node = ec.crow ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   if (node >= ctl[CTL_N]) return;
   const int F = p.F;
@@ -4422,8 +4505,8 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
   const bool packed = cnt < DIRECT_PACK_ROWS;                 // block-uniform
   const int per_f = packed ? NBT : 2 * NBT;                   // int64 entries per feature
   const int bat = packed ? 2 * batch : batch;                 // same LDS bytes
-  DirectBest best;
-  best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  LaneBest lb;
+  lane_best_init(lb);
   double ptc = NAN;   // the node's parent gain term (direct_scan_feature)
   long long tg_row = 0, ts_row = 0;   // node totals (G_q, S_q), accumulated in the first batch
   // eligible-code rows only for nodes scanned in ONE batch (the partition falls
@@ -4435,14 +4518,15 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
     __syncthreads();
     for (int j = lo + t; j < lo + cnt; j += blockDim.x) {
       const int r = idx ? idx[j] : j;
-      const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * fp : codes_rm + (int64_t)r * fp;
+      const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * ec.rs : codes_rm + (int64_t)r * fp;
+      const int64_t fs = ec.crow ? ec.fs : 1;
       uint32_t c0[DIRECT_FB];
 #pragma unroll
-      for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
+      for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u] * fs] : 0u;
       long long gq, sq;
       direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
       if (b0 == 0) { tg_row += gq; ts_row += sq; }
-      direct_row_atomics<NBT>(row, flist + b0, nb, packed, per_f, hist, gq, sq, c0,
+      direct_row_atomics<NBT>(row, fs, flist + b0, nb, packed, per_f, hist, gq, sq, c0,
                               ecw ? ecw + (int64_t)j * ec.stride : nullptr, ec.stride);
     }
     __syncthreads();
@@ -4454,12 +4538,15 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
     // one wave per feature of the batch
     for (int q = wid; q < nb; q += DIRECT_WAVES) {
       const int f = flist[b0 + q];
-      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best, ptc);
-      else direct_scan_feature<NBT, false>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best, ptc);
+      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, lb, ptc, cut_s[wid]);
+      else direct_scan_feature<NBT, false>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, lb, ptc, cut_s[wid]);
     }
     __syncthreads();
   }
-  if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
+  {
+    const DirectBest best = lane_best_reduce(lb);
+    if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
+  }
   __syncthreads();
   if (t == 0) {
     DirectBest b;
@@ -4472,6 +4559,62 @@ __global__ __launch_bounds__(256) void seg_direct_kernel(
     const long long tsq = tot_s[1][0] + tot_s[1][1] + tot_s[1][2] + tot_s[1][3];
     out[node] = direct_node_split(b, tgq, tsq, ig, is);
     if (ec.nodeq) ec.nodeq[node] = ecw ? direct_feat_pos(flist, nfl, b.key) : -1;
+  }
+}
+
+// Column-major segment codes (row-chunk direct levels, HipTreeBuilder.COLMAJOR_EVERY):
+// the code rows of this level's positions [0, n) (row idx[j] of the row-major
+// codes) transposed into F feature planes of `plane` positions, so a direct
+// pass reads each eligible feature of a node's rows as a contiguous byte run
+// instead of one random code row per row (DRF 10M x 100, level 10: 1121 ->
+// 521 us, profiles/r6/drf_colmajor_r6j.txt).  Later levels keep the planes and
+// move only positions (part_scatter cpos); the one-wave-per-node levels are
+// bound by the split scan's instruction issue, not by their code loads, and
+// read the row-major codes.  One workgroup per CM_ROWS positions: rows staged
+// in LDS (consecutive lanes load consecutive words of one row), then 4 x 4
+// byte blocks leave as one dword per feature and 4 positions.
+// Positions of retired segments hold stale row ids: rows outside [0, nrows)
+// are read as zeros (their plane bytes are never read).
+constexpr int CM_ROWS = 256;
+__global__ __launch_bounds__(256) void seg_colmajor_kernel(const uint8_t* __restrict__ codes_rm, int fp, int F,
+                                                           const int* __restrict__ idx, int n, int64_t nrows,
+                                                           uint8_t* __restrict__ ccol, int64_t plane) {
+  extern __shared__ uint32_t cm_tile[];   // [CM_ROWS][fp / 4] dwords
+  __shared__ int rows[CM_ROWS];
+  const int t = threadIdx.x;
+  const int j0 = blockIdx.x * CM_ROWS;
+  const int W = fp >> 2;
+  {
+    const int j = j0 + t;
+    const int r = j < n ? (idx ? idx[j] : j) : -1;
+    rows[t] = (r >= 0 && (int64_t)r < nrows) ? r : -1;
+  }
+  __syncthreads();
+  for (int q = t; q < CM_ROWS * W; q += 256) {
+    const int i = q / W, k = q - i * W;
+    const int r = rows[i];
+    cm_tile[q] = r >= 0 ? reinterpret_cast<const uint32_t*>(codes_rm + (int64_t)r * fp)[k] : 0u;
+  }
+  __syncthreads();
+  // 4 x 4 byte blocks: 4 rows' dword f4 (features 4 f4 .. 4 f4 + 3) in, each
+  // feature's dword of those 4 positions out (one LDS dword read per output
+  // dword instead of four byte reads)
+  constexpr int R4 = CM_ROWS / 4;
+  const int F4 = (F + 3) >> 2;
+  for (int q = t; q < F4 * R4; q += 256) {
+    const int f4 = q / R4, r4 = q - f4 * R4;
+    const uint32_t* src = cm_tile + 4 * r4 * W + f4;
+    const uint32_t a0 = src[0], a1 = src[W], a2 = src[2 * W], a3 = src[3 * W];
+    uint32_t o[4];
+    o[0] = (a0 & 0xffu) | ((a1 & 0xffu) << 8) | ((a2 & 0xffu) << 16) | (a3 << 24);
+    o[1] = ((a0 >> 8) & 0xffu) | (a1 & 0xff00u) | ((a2 & 0xff00u) << 8) | ((a3 & 0xff00u) << 16);
+    o[2] = ((a0 >> 16) & 0xffu) | ((a1 >> 8) & 0xff00u) | (a2 & 0xff0000u) | ((a3 & 0xff0000u) << 8);
+    o[3] = (a0 >> 24) | ((a1 >> 16) & 0xff00u) | ((a2 >> 8) & 0xff0000u) | (a3 & 0xff000000u);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int f = 4 * f4 + b;
+      if (f < F) reinterpret_cast<uint32_t*>(ccol + (int64_t)f * plane + j0)[r4] = o[b];
+    }
   }
 }
 
@@ -4611,7 +4754,7 @@ __global__ __launch_bounds__(256) void direct_dp_hist_kernel(
     SplitParams p, int batch, int node0, int max_elig, long long* __restrict__ dh, int gpos,
     const uint8_t* __restrict__ crow) {
   extern __shared__ __attribute__((aligned(16))) long long hist[];   // [batch][2][NBT]
-  const ECodes ec{nullptr, 0, nullptr, crow, nullptr};
+  const ECodes ec{nullptr, 0, nullptr, crow, nullptr, fp, 1};
   __shared__ int flist[1024];
   __shared__ uint32_t hsh_s[1024];
   __shared__ int nfl_s;
@@ -4640,14 +4783,15 @@ __global__ __launch_bounds__(256) void direct_dp_hist_kernel(
     __syncthreads();
     for (int j = lo + t; j < lo + cnt; j += blockDim.x) {
       const int r = idx ? idx[j] : j;
-      const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * fp : codes_rm + (int64_t)r * fp;
+      const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * ec.rs : codes_rm + (int64_t)r * fp;
+      const int64_t fs = ec.crow ? ec.fs : 1;
       uint32_t c0[DIRECT_FB];
 #pragma unroll
-      for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
+      for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u] * fs] : 0u;
       long long gq, sq;
       direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
       if (b0 == 0) { tg_row += gq; ts_row += sq; }
-      direct_row_atomics<NBT>(row, flist + b0, nb, false, 2 * NBT, hist, gq, sq, c0, nullptr, 0);
+      direct_row_atomics<NBT>(row, fs, flist + b0, nb, false, 2 * NBT, hist, gq, sq, c0, nullptr, 0);
     }
     __syncthreads();
     for (int j = t; j < nb * 2 * NBT; j += blockDim.x) out[2 + (int64_t)b0 * 2 * NBT + j] = hist[j];
@@ -4673,6 +4817,7 @@ __global__ __launch_bounds__(256) void direct_dp_scan_kernel(
   __shared__ int nfl_s;
   __shared__ double wb_gain[4], wb_GL[4], wb_SL[4];
   __shared__ long long wb_key[4];
+  __shared__ double cut_s[4][64];   // per-wave UniformAdaptive cut tables
   const int node = node0 + blockIdx.x;
   if (node >= ctl[CTL_N]) return;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -4685,14 +4830,17 @@ __global__ __launch_bounds__(256) void direct_dp_scan_kernel(
   __syncthreads();
   const int nfl = nfl_s;
   const double ig = qscale[2], is = qscale[3];
-  DirectBest best;
-  best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  LaneBest lb;
+  lane_best_init(lb);
   double ptc = NAN;   // the node's parent gain term (direct_scan_feature)
   for (int q = wid; q < nfl; q += 4) {
     const int f = flist[q];
-    direct_scan_feature<NBT, false>(h + 2 + (int64_t)q * 2 * NBT, node, f, nvb[f], ig, is, p, lane, best, ptc);
+    direct_scan_feature<NBT, false>(h + 2 + (int64_t)q * 2 * NBT, node, f, nvb[f], ig, is, p, lane, lb, ptc, cut_s[wid]);
   }
-  if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
+  {
+    const DirectBest best = lane_best_reduce(lb);
+    if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
+  }
   __syncthreads();
   if (t == 0) {
     DirectBest b;
@@ -4739,6 +4887,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   __shared__ long long tot_s[2][4];
   __shared__ double wb_gain[4], wb_GL[4], wb_SL[4];
   __shared__ long long wb_key[4];
+  __shared__ double cut_s[4][64];   // per-wave UniformAdaptive cut tables
   const int n = ctl[CTL_N];
   const int c = ec.crow ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   if (c >= pc_first[n]) return;
@@ -4762,14 +4911,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   long long tg_row = 0, ts_row = 0;
   for (int j = lo + t; j < hi; j += blockDim.x) {
     const int r = idx ? idx[j] : j;
-    const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * fp : codes_rm + (int64_t)r * fp;
+    const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * ec.rs : codes_rm + (int64_t)r * fp;
+    const int64_t fs = ec.crow ? ec.fs : 1;
     uint32_t cc[DIRECT_FB];
 #pragma unroll
-    for (int u = 0; u < DIRECT_FB; ++u) cc[u] = (u < nfl) ? row[flist[u]] : 0u;
+    for (int u = 0; u < DIRECT_FB; ++u) cc[u] = (u < nfl) ? row[flist[u] * fs] : 0u;
     long long gq, sq;
     direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
     tg_row += gq; ts_row += sq;
-    direct_row_atomics<NBT>(row, flist, nfl, true, NBT, hist, gq, sq, cc,
+    direct_row_atomics<NBT>(row, fs, flist, nfl, true, NBT, hist, gq, sq, cc,
                             ec.codes ? ec.codes + (int64_t)j * ec.stride : nullptr, ec.stride);
   }
   tg_row = wave_sum_i64(tg_row);
@@ -4818,15 +4968,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     __syncthreads();
     tgq = tot_s[0][0]; tsq = tot_s[1][0];
   }
-  DirectBest best;
-  best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  LaneBest lb;
+  lane_best_init(lb);
   double ptc = NAN;   // the node's parent gain term (direct_scan_feature)
   for (int q = wid; q < nfl; q += 4) {
     const int f = flist[q];
-    if (packed) direct_scan_feature<NBT, true>(hist + q * NBT, node, f, nvb[f], ig, is, p, lane, best, ptc);
-    else direct_scan_feature<NBT, false>(hist + q * 2 * NBT, node, f, nvb[f], ig, is, p, lane, best, ptc);
+    if (packed) direct_scan_feature<NBT, true>(hist + q * NBT, node, f, nvb[f], ig, is, p, lane, lb, ptc, cut_s[wid]);
+    else direct_scan_feature<NBT, false>(hist + q * 2 * NBT, node, f, nvb[f], ig, is, p, lane, lb, ptc, cut_s[wid]);
   }
-  if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
+  {
+    const DirectBest best = lane_best_reduce(lb);
+    if (lane == 0) { wb_gain[wid] = best.gain; wb_key[wid] = best.key; wb_GL[wid] = best.GL; wb_SL[wid] = best.SL; }
+  }
   __syncthreads();
   if (t == 0) {
     DirectBest b;
@@ -4859,6 +5012,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   salt = (uint32_t)qscale[9];  // per-tree dither salt, written by tree_begin (graph-replay safe)
   extern __shared__ __attribute__((aligned(16))) long long hist_all[];   // [4][batch * 2 * NBT]
   __shared__ short flist_all[4][DIRECT_WAVE_F];
+  __shared__ double cut_s[4][64];   // per-wave UniformAdaptive cut tables
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int node = (ec.crow ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + wid;
   if (node >= ctl[CTL_N]) return;   // whole wave: no workgroup barrier below
@@ -4894,8 +5048,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   const bool packed = cnt < DIRECT_PACK_ROWS;
   const int per_f = packed ? NBT : 2 * NBT;
   const int bat = packed ? 2 * batch : batch;
-  DirectBest best;
-  best.gain = -INFINITY; best.GL = best.SL = 0.0; best.key = 0x7fffffffffffffffLL;
+  LaneBest lb;
+  lane_best_init(lb);
   double ptc = NAN;   // the node's parent gain term (direct_scan_feature)
   long long tg_row = 0, ts_row = 0;
   // eligible-code rows only for nodes scanned in ONE batch (see seg_direct_kernel)
@@ -4907,27 +5061,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     wave_lds_sync();
     for (int j = lo + lane; j < lo + cnt; j += 64) {
       const int r = idx ? idx[j] : j;
-      const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * fp : codes_rm + (int64_t)r * fp;
+      const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * ec.rs : codes_rm + (int64_t)r * fp;
+      const int64_t fs = ec.crow ? ec.fs : 1;
       uint32_t c0[DIRECT_FB];
 #pragma unroll
-      for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u]] : 0u;
+      for (int u = 0; u < DIRECT_FB; ++u) c0[u] = (u < nb) ? row[flist[b0 + u] * fs] : 0u;
       long long gq, sq;
       direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
       if (b0 == 0) { tg_row += gq; ts_row += sq; }
       if (nb <= 0) continue;
-      direct_row_atomics<NBT>(row, flist + b0, nb, packed, per_f, hist, gq, sq, c0,
+      direct_row_atomics<NBT>(row, fs, flist + b0, nb, packed, per_f, hist, gq, sq, c0,
                               ecw ? ecw + (int64_t)j * ec.stride : nullptr, ec.stride);
     }
     wave_lds_sync();
     for (int q = 0; q < nb; ++q) {
       const int f = flist[b0 + q];
-      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best, ptc);
-      else direct_scan_feature<NBT, false>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, best, ptc);
+      if (packed) direct_scan_feature<NBT, true>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, lb, ptc, cut_s[wid]);
+      else direct_scan_feature<NBT, false>(hist + q * per_f, node, f, nvb[f], ig, is, p, lane, lb, ptc, cut_s[wid]);
     }
     wave_lds_sync();
   }
   tg_row = wave_sum_i64(tg_row);
   ts_row = wave_sum_i64(ts_row);
+  const DirectBest best = lane_best_reduce(lb);
   if (lane == 0) {
     out[node] = direct_node_split(best, tg_row, ts_row, ig, is);
     if (ec.nodeq) ec.nodeq[node] = ecw ? direct_feat_pos(flist, nfl, best.key) : -1;
@@ -5279,9 +5435,9 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
                                const uint8_t* tree_fmask, const double* qscale, int salt, const void* params, int nbt,
                                int max_nodes, int mode, const int* pc_first, int max_pc, unsigned long long* slab,
                                long long* tot_slab, int* ticket, void* nsplit, int gpos, uint8_t* ecodes, int ecs,
-                               int* nodeq, const uint8_t* crow, const int* cpos, hipStream_t stream) {
+                               int* nodeq, const uint8_t* crow, const int* cpos, long long plane, hipStream_t stream) {
   if (ecodes && ecs != 8 && ecs != 16) return kBadArg;
-  const ECodes ec{ecodes, ecs, nodeq, crow, cpos};
+  const ECodes ec{ecodes, ecs, nodeq, crow, cpos, plane > 0 ? 1 : fp, plane > 0 ? (int64_t)plane : 1};
   // moved code rows: XCD-aware block order over grids padded to a multiple of 8
   auto pad8 = [&](int g) { return crow ? (g + 7) / 8 * 8 : g; };
   // mode 0: one workgroup per node, 1: one wave per node (F <= 256),
@@ -5342,6 +5498,19 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
     default: return kBadArg;
   }
 #undef LAUNCH_SD
+  return launch_status();
+}
+
+// column-major planes of this level's positions (seg_colmajor_kernel); plane:
+// positions per feature plane (>= n rounded up to CM_ROWS, a multiple of 4)
+H2OMX_API int h2omx_seg_colmajor(const uint8_t* codes_rm, int fp, int F, const int* idx, int n, long long nrows,
+                                 uint8_t* ccol, long long plane, hipStream_t stream) {
+  const int nb = (n + CM_ROWS - 1) / CM_ROWS;
+  if (n < 1 || fp % 4 || F < 1 || F > fp || (size_t)CM_ROWS * fp > 128 * 1024 || plane % 4 ||
+      plane < (long long)nb * CM_ROWS || !codes_rm || !ccol)
+    return kBadArg;
+  hipLaunchKernelGGL(seg_colmajor_kernel, dim3(nb), dim3(256), (size_t)CM_ROWS * fp, stream, codes_rm, fp, F, idx, n,
+                     (int64_t)nrows, ccol, (int64_t)plane);
   return launch_status();
 }
 
@@ -5457,7 +5626,8 @@ H2OMX_API int h2omx_part_scatter(const uint8_t* codes, int64_t npad, const int* 
   const SegRows sr{crow_in, crow_out, fp, cpos_in, cpos_out};
   if (crow_out != nullptr && ((crow_in == nullptr && codes_rm == nullptr) || fp % 4 != 0 || cpos_in || cpos_out))
     return kBadArg;
-  if (cpos_out != nullptr && crow_in == nullptr) return kBadArg;
+  // (cpos without crow_in: column-major planes outside SegRows, the split codes
+  // are gathered from the feature-major codes by row id)
   // wave: bit 0 wave-granular kernel; bits 1-2 its segf flags (last level)
   const int segf = wave >> 1;
   wave &= 1;

@@ -145,6 +145,12 @@ class HipTreeBuilder:
     ECODES = True
     # levels of more than 8192 nodes finalise in count / scan / write tiles (False: one workgroup)
     LF_MULTI_BLOCK = True
+    # row-chunk direct levels (one rank, dmode 2): the first one and every k-th
+    # after it transpose the live rows' codes into column-major planes in
+    # segment order (seg_colmajor_kernel); the ones in between move only
+    # positions.  Wave-per-node levels read the row-major codes (their scan is
+    # issue-bound, profiles/r6/drf_pmc_r6i.txt).  0 = off
+    COLMAJOR_EVERY = 6
 
     def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
         if not bm.codes.is_cuda:
@@ -783,6 +789,30 @@ class HipTreeBuilder:
                     comm.all_reduce_(dh[: nc * stride])
         self.stats["direct_dp_levels"] = self.stats.get("direct_dp_levels", 0) + 1
 
+    # node counts of levels above SYNC_NODE_CAP read back early: a pinned copy of
+    # the next level's (nodes, slots) + event right after its finalisation, so
+    # the host waits for the finalisation only while the level's partition
+    # kernels still run (instead of draining the stream at the next level's top)
+    _ctl_host = None
+
+    def _count_ahead(self, ctl_nxt: torch.Tensor, parity: int) -> None:
+        if self._ctl_host is None:
+            self._ctl_host = torch.empty((2, 2), dtype=torch.int32, pin_memory=True)
+            self._ctl_ev = [torch.cuda.Event(), torch.cuda.Event()]
+            self._ctl_pending = [False, False]
+        self._ctl_host[parity].copy_(ctl_nxt[:2], non_blocking=True)
+        self._ctl_ev[parity].record()
+        self._ctl_pending[parity] = True
+
+    def _count_now(self, ctl_cur: torch.Tensor, parity: int) -> tuple[int, int]:
+        self.stats["host_syncs"] += 1
+        if self._ctl_host is not None and self._ctl_pending[parity]:
+            self._ctl_ev[parity].synchronize()
+            self._ctl_pending[parity] = False
+            return int(self._ctl_host[parity, 0]), int(self._ctl_host[parity, 1])
+        n_now, s_now = [int(v) for v in ctl_cur[:2].tolist()]
+        return n_now, s_now
+
     def _build_seg(self, g, h, w, tree_index, tree_fmask, smax, fixed):
         """Row-partitioned level pipeline (csrc/tree_kernels.hip, "segmented"
         section): each level reads only the rows of the nodes it builds."""
@@ -821,9 +851,10 @@ class HipTreeBuilder:
         gs = {"g": g, "s": s2, "pos": 0}
 
         def route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first, ctl_cur, ctl_nxt,
-                  idx_in, next_direct, ec=None):
+                  idx_in, next_direct, ec=None, cpos=(None, None)):
             """part_count -> level_close -> part_scatter: rows into their next-level segments.
-            ec: (codes, stride, nodeq) of the direct pass - split codes read in segment order."""
+            ec: (codes, stride, nodeq) of the direct pass - split codes read in segment order.
+            cpos: (in, out) column-major plane positions moved with the rows (COLMAJOR_EVERY)."""
             cur, nxt = d % 2, (d + 1) % 2
             nbuilt = None
             max_pc = pc_cap + max_nodes
@@ -883,7 +914,8 @@ class HipTreeBuilder:
                                              P(ctl_cur), P(part), nbt, P(g), P(h), P(w), P(self.qscale),
                                              self.capacity, P(self.leaf_acc), max_pc, pwave | segf, P(dirb), P(gs["g"]),
                                              P(gs["s"]), P(gout), P(sout), P(ecodes), ecs, P(nodeq),
-                                             P(self.codes_rm), None, None, bm.fp, None, None, st),
+                                             P(self.codes_rm), None, None, bm.fp, P(cpos[0]),
+                                             P(None if last else cpos[1]), st),
                       "part_scatter")
             if gout is not None:
                 gs.update(g=gout, s=sout, pos=1)
@@ -899,12 +931,15 @@ class HipTreeBuilder:
         # the build and the scan, h2omx_direct_dp)
         direct_ok = (self.DIRECT_MIN_NODES > 0 and F <= 1024
                      and exp_elig <= self.DIRECT_MAX_ELIG and self.catf is None)
+        # column-major planes (COLMAJOR_EVERY): level of the last transpose, positions of the next level
+        cm_last, cm_pos = None, None
+        if self._ctl_host is not None:
+            self._ctl_pending = [False, False]    # (a tree that ended early left one unread)
         for d in range(max_depth):
             cur, nxt = d % 2, (d + 1) % 2
             ctl_cur, ctl_nxt = self.ctl[cur], self.ctl[nxt]
             if max_nodes > self.SYNC_NODE_CAP:
-                n_now, s_now = [int(v) for v in ctl_cur[:2].tolist()]
-                self.stats["host_syncs"] += 1
+                n_now, s_now = self._count_now(ctl_cur, cur)
                 if n_now == 0:
                     final_ctl = ctl_cur     # tree finished early: ctl_cur holds its final TOTAL
                     break
@@ -949,25 +984,43 @@ class HipTreeBuilder:
                     ecs = 8 if n_elig <= 8 else 16
                     ec = (B("ecodes", (n + 64) * ecs, torch.uint8), ecs, B("nodeq", max_nodes, i32))
                 ecodes, ecs, nodeq = ec if ec is not None else (None, 0, None)
+                ccol = cpos_cur = cpos_next = None
+                plane = 0
                 if comm is not None:
                     self._direct_dp(comm, idx_in, gs, seg_start, seg_cnt, ctl_cur, tree_fmask, spp, max_nodes,
                                     nsplit, st)
                     ec = None
                 else:
+                    if self.COLMAJOR_EVERY > 0 and dmode == 2:
+                        plane = -(-n // 256) * 256
+                        ccol = B("ccol", F * plane, torch.uint8)
+                        if cm_pos is None or d - cm_last >= self.COLMAJOR_EVERY:
+                            ops.check(lib.h2omx_seg_colmajor(P(self.codes_rm), bm.fp, F, P(idx_in), n, bm.npad,
+                                                             P(ccol), plane, st), "seg_colmajor")
+                            cm_last = d
+                        else:
+                            cpos_cur = cm_pos
+                    # positions for the next level only if it is surely a row-chunk level too
+                    cm_pos = None
+                    if ccol is not None and not last and n >= self.DIRECT_WAVE_ROWS * next_nodes:
+                        cpos_next = cm_pos = B(f"cpos{nxt}", n + 64, i32)
                     ops.check(lib.h2omx_seg_direct(P(self.codes_rm), bm.fp,
                                                    P(idx_in), P(gs["g"]), P(gs["s"]),
                                                    P(seg_start), P(seg_cnt), P(ctl_cur), P(bm.nvb), P(tree_fmask),
                                                    P(self.qscale), tree_index & 0x7FFFFFFF, spp, nbt, max_nodes,
                                                    dmode, P(pc_first), max_pc, P(slab), P(tot_slab), P(ticket),
-                                                   P(nsplit), gs["pos"], P(ecodes), ecs, P(nodeq), None, None, st),
+                                                   P(nsplit), gs["pos"], P(ecodes), ecs, P(nodeq), P(ccol),
+                                                   P(cpos_cur), plane, st),
                               "seg_direct")
                 ops.check(lib.h2omx_level_finalize_ns(P(nsplit), P(ctl_cur), P(ctl_nxt), spp, P(bm.edges),
                                                       P(bm.nvb), nbt, next_nodes, P(part), P(nl), P(self.tree_buf),
                                                       self.capacity, max_nodes,
                                                       self._lf_tiles(max_nodes), st),
                           "level_finalize_ns")
+                if not last and next_nodes > self.SYNC_NODE_CAP:
+                    self._count_ahead(ctl_nxt, nxt)
                 idx_in, _ = route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first, ctl_cur,
-                                  ctl_nxt, idx_in, True, ec)
+                                  ctl_nxt, idx_in, True, ec, (cpos_cur, cpos_next))
                 full_prev = None
                 max_nodes = next_nodes
                 continue
@@ -1024,6 +1077,8 @@ class HipTreeBuilder:
                                                next_nodes, P(part), P(nl), P(self.tree_buf), self.capacity,
                                                P(nsplit), max_nodes, self._lf_tiles(max_nodes), st),
                       "level_finalize")
+            if not last and next_nodes > self.SYNC_NODE_CAP:
+                self._count_ahead(ctl_nxt, nxt)
             idx_in, built_zeroed = route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first,
                                          ctl_cur, ctl_nxt, idx_in, False)
             full_prev = full_cur

@@ -58,7 +58,8 @@ TREE_SIGS = {
     "h2omx_level_close": "PPPPPPPPPPPPPPIPIS",
     "h2omx_level_close_mb": "PPPPPPPPPPPPPPIPIIIPPPPPS",
     "h2omx_part_scatter": "PLPPPIPPPPPPPIPPPPIPIIPPPPPPIPPPPIPPS",
-    "h2omx_seg_direct": "PIPPPPPPPPPIPIIIPIPPPPIPIPPPS",
+    "h2omx_seg_direct": "PIPPPPPPPPPIPIIIPIPPPPIPIPPPLS",
+    "h2omx_seg_colmajor": "PIIPILPLS",
     "h2omx_level_finalize_ns": "PPPPPPIIPPPIIPS",
     "h2omx_direct_dp_stride": "PI",
     "h2omx_direct_dp": "IPIPPPPPPPPPPIIIPPIPS",

@@ -4,7 +4,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 keys = ["split_find", "seg_direct", "hist_build_seg", "hist_build_kernel", "hist_reduce", "level_finalize", "level_close",
-        "part_scatter", "zero_slots", "part_count", "node_best", "lf_"]
+        "part_scatter", "zero_slots", "part_count", "node_best", "lf_", "seg_colmajor"]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 seq = [(r["Kernel_Name"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3, r["Grid_Size_X"]) for r in rows]
 LEVEL = ("split_find", "seg_direct")   # one of these per level (direct mode replaces split_find)

@@ -3,6 +3,7 @@
 that are constants in the code):
 
     python scripts/r6/bench_ab.py h2omx.models.tree.engine:HipTreeBuilder.FUSE_FIN=0 -- --rows 1375000 ...
+    python scripts/r6/bench_ab.py h2omx.models.tree.engine:HipTreeBuilder.COLMAJOR_EVERY=3 -- scripts/drf_deep_ab.py
 """
 import importlib
 import os
@@ -25,7 +26,12 @@ def main():
             obj = getattr(obj, p)
         cur = getattr(obj, name)
         setattr(obj, name, type(cur)(int(val)) if isinstance(cur, (bool, int)) else type(cur)(val))
-    sys.argv = [os.path.join(ROOT, "bench.py")] + args[sep + 1:]
+    rest = args[sep + 1:]
+    # a script path right after "--" runs that script instead of bench.py
+    if rest and rest[0].endswith(".py"):
+        sys.argv = [os.path.join(ROOT, rest[0]) if not os.path.isabs(rest[0]) else rest[0]] + rest[1:]
+    else:
+        sys.argv = [os.path.join(ROOT, "bench.py")] + rest
     runpy.run_path(sys.argv[0], run_name="__main__")
 
 

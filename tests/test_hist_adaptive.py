@@ -266,12 +266,26 @@ def test_gpu_segmented_engine_identical_under_uniform_adaptive(cuda_dev, monkeyp
                     seed=7, hist_mode=1, hist_top=1024, hist_nbins=20)
     yt = torch.from_numpy(y).to(cuda_dev)
     out = {}
-    for eng, scan_slots in (("scan", 16), ("seg", 0)):
+    # the direct deep-level kernels (from level 1 on: per-wave cut tables wherever
+    # the level has <= 64 cuts, the division form above) in their node-workgroup,
+    # wave-per-node and row-chunk forms, with and without column-major code planes
+    cfgs = (("scan", 16, {}), ("seg", 0, {}), ("seg", 0, {"DIRECT_MIN_NODES": 2}),
+            ("seg", 0, {"DIRECT_MIN_NODES": 2, "DIRECT_WAVE_ROWS": 1 << 30}),
+            ("seg", 0, {"DIRECT_MIN_NODES": 2, "DIRECT_CHUNKED": False, "COLMAJOR_EVERY": 0}),
+            ("seg", 0, {"DIRECT_MIN_NODES": 2, "DIRECT_WAVE_ROWS": 0, "COLMAJOR_EVERY": 1}),
+            ("seg", 0, {"DIRECT_MIN_NODES": 2, "DIRECT_WAVE_ROWS": 0, "COLMAJOR_EVERY": 3}))
+    names = ("DIRECT_MIN_NODES", "DIRECT_WAVE_ROWS", "DIRECT_CHUNKED", "COLMAJOR_EVERY")
+    defaults = {name: getattr(E.HipTreeBuilder, name) for name in names}
+    for k, (eng, scan_slots, attrs) in enumerate(cfgs):
         monkeypatch.setenv("H2OMX_TREE_ENGINE", eng)
         monkeypatch.setattr(E.HipTreeBuilder, "SCAN_SLOTS", scan_slots)
-        out[eng] = train_ensemble(bg, yt, dist="drf", ntrees=3, tparams=tp, sample_rate=0.632, nclass=2, seed=11)
-    a, b = out["scan"], out["seg"]
-    for t in range(a.trees.shape[0]):
-        for i in a.compact()[t]:
-            assert a.trees[t][i]["feat"] == b.trees[t][i]["feat"], (t, i)
-            assert a.trees[t][i]["bin"] == b.trees[t][i]["bin"], (t, i)
+        for name in names:
+            monkeypatch.setattr(E.HipTreeBuilder, name, attrs.get(name, defaults[name]))
+        out[k] = train_ensemble(bg, yt, dist="drf", ntrees=3, tparams=tp, sample_rate=0.632, nclass=2, seed=11)
+    a = out[0]
+    for k in range(1, len(cfgs)):
+        b = out[k]
+        for t in range(a.trees.shape[0]):
+            for i in a.compact()[t]:
+                assert a.trees[t][i]["feat"] == b.trees[t][i]["feat"], (cfgs[k], t, i)
+                assert a.trees[t][i]["bin"] == b.trees[t][i]["bin"], (cfgs[k], t, i)

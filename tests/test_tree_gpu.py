@@ -184,18 +184,20 @@ def test_direct_deep_levels_match_subtraction(cuda_dev, monkeypatch, dist, depth
     out = {}
     # engine switches: direct from this many nodes, wave-per-node below this many rows per node,
     # multi-block finalise, wave-chunk partition from this many nodes, chunked direct workgroups,
-    # (g, s2) moved into segment order, eligible-feature codes stored for the partition
+    # (g, s2) moved into segment order, eligible-feature codes stored for the partition,
+    # column-major code planes every k direct levels
     keys = ("DIRECT_MIN_NODES", "DIRECT_WAVE_ROWS", "LF_MULTI_BLOCK", "PART_WAVE_NODES", "DIRECT_CHUNKED",
-            "PERMUTE_GS", "ECODES")
-    for cfg in ((0, 0, False, 1 << 30, True, False, False), (0, 0, True, 1, True, True, True),
-                (2, 0, True, 1 << 30, True, True, True), (64, 0, True, 1 << 30, False, False, True),
-                (64, 1 << 30, True, 1, True, True, False), (64, 1 << 30, False, 2048, True, False, True),
-                (64, 0, True, 1 << 30, True, True, True)):
+            "PERMUTE_GS", "ECODES", "COLMAJOR_EVERY")
+    for cfg in ((0, 0, False, 1 << 30, True, False, False, 0), (0, 0, True, 1, True, True, True, 0),
+                (2, 0, True, 1 << 30, True, True, True, 0), (64, 0, True, 1 << 30, False, False, True, 0),
+                (64, 1 << 30, True, 1, True, True, False, 0), (64, 1 << 30, False, 2048, True, False, True, 0),
+                (64, 0, True, 1 << 30, True, True, True, 0), (2, 0, True, 1 << 30, True, True, True, 1),
+                (2, 0, True, 1, True, True, False, 3), (64, 0, True, 1 << 30, True, False, True, 2)):
         for k, v in zip(keys, cfg):
             monkeypatch.setattr(E.HipTreeBuilder, k, v)
         out[cfg] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=sample_rate,
                                   nclass=nclass, seed=13)
-    a = out[(0, 0, False, 1 << 30, True, False, False)]
+    a = out[(0, 0, False, 1 << 30, True, False, False, 0)]
     for cfg, b in out.items():
         for t in range(a.trees.shape[0]):
             reach = a.compact()[t]
@@ -401,3 +403,34 @@ def test_graph_replay_matches_eager(cuda_dev, monkeypatch, dist, depth, min_rows
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"tree {t} {f}")
     torch.testing.assert_close(a._state.Fm, b._state.Fm, rtol=0, atol=0)
 
+
+
+@pytest.mark.parametrize("dist,mode", [("bernoulli", 0), ("bernoulli", 1), ("gaussian", 0)])
+def test_level0_copies_match_plain_slices(cuda_dev, monkeypatch, dist, mode):
+    """Level 0 with 8 / 4 interleaved lane copies - low-cardinality columns laid
+    out as up to 64 slices inside the copies' space, high-cardinality ones
+    interleaved - builds bit-identical trees to the plain one-slice kernel."""
+    import h2omx.models.tree.engine as E
+
+    rng = np.random.default_rng(23)
+    X, y = _data(n=400_000, F=9, seed=23, task="bin" if dist == "bernoulli" else "reg")
+    X[6] = rng.integers(0, 7, X.shape[1])       # weekday-like
+    X[7] = rng.integers(1, 13, X.shape[1])      # month-like
+    X[8] = rng.integers(0, 30, X.shape[1]).astype(np.float32)
+    X[8, rng.random(X.shape[1]) < 0.05] = np.nan
+    y = y + (dist != "bernoulli") * 0.3 * X[7]
+    _, bg = _both(X, y, 255)
+    tp = TreeParams(max_depth=5, min_rows=3, learn_rate=0.2, mode=mode, reg_lambda=1.0 if mode else 0.0)
+    yt = torch.from_numpy(y.astype(np.float32)).cuda()
+    out = {}
+    for cop in (1, 4, 8):
+        monkeypatch.setattr(E.HipTreeBuilder, "L0_COPIES", cop)
+        out[cop] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, seed=5)
+    a = out[1]
+    for cop in (4, 8):
+        b = out[cop]
+        for t in range(a.trees.shape[0]):
+            reach = a.compact()[t]
+            assert reach == b.compact()[t], (cop, t)
+            for f in ("feat", "bin", "value"):
+                np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"{cop} {t} {f}")
