@@ -2241,10 +2241,19 @@ __device__ __forceinline__ int leaf_reps(const double* __restrict__ qs) {
   const int r = (int)qs[10];
   return r < 1 ? 1 : r;
 }
+// the slices' loads are issued together (a runtime-count loop waited on each
+// load before the next add: 16 serial L2 round trips per sum, ~15 us of the
+// one-workgroup leaf_finalize_begin at 16 slices)
+constexpr int LEAF_REPS_MAX = 16;
 __device__ __forceinline__ long long leaf_sum(const unsigned long long* __restrict__ acc, int64_t i, int reps,
                                               int64_t stride) {
-  long long v = (long long)acc[i];
-  for (int r = 1; r < reps; ++r) v += (long long)acc[i + r * stride];
+  unsigned long long x[LEAF_REPS_MAX];
+#pragma unroll
+  for (int r = 0; r < LEAF_REPS_MAX; ++r) x[r] = r < reps ? acc[i + r * stride] : 0ull;
+  long long v = 0;
+#pragma unroll
+  for (int r = 0; r < LEAF_REPS_MAX; ++r) v += (long long)x[r];
+  for (int r = LEAF_REPS_MAX; r < reps; ++r) v += (long long)acc[i + r * stride];
   return v;
 }
 __device__ __forceinline__ void leaf_zero(unsigned long long* __restrict__ acc, int64_t i, int reps, int64_t stride) {

@@ -1,0 +1,24 @@
+#!/bin/bash
+# r6n: leaf-slice loads issued together (leaf_finalize_begin), the round's kernels vs the
+# 81078cc kernels (variants/head): GBM headline, 1.375M shard, loopback-8, XGBoost (3 reps interleaved)
+set -o pipefail
+O=$GRAFT_REPO_ROOT/gpurun_out/r6n
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+export PYTHONUNBUFFERED=1
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_tree_gpu.py tests/test_p2p_gpu.py tests/test_monotone.py -m gpu > $O/pytest.log 2>&1 || exit 1
+H=$GRAFT_REPO_ROOT/h2omx/lib/variants/head
+S="--rows 1375000 --steps 50 --warmup 5 --fit-trees 0"
+for r in 1 2 3; do
+  for arm in new head; do
+    if [ $arm = head ]; then export H2OMX_LIB_DIR=$H; else unset H2OMX_LIB_DIR; fi
+    timeout -k 10 300 python3 bench.py --fit-trees 0 > $O/n1_${arm}_$r.json 2>> $O/err.log || exit 1
+    timeout -k 10 300 python3 bench.py $S > $O/shard_${arm}_$r.json 2>> $O/err.log || exit 1
+    timeout -k 10 300 python3 bench.py $S --loopback-ranks 8 > $O/loop8_${arm}_$r.json 2>> $O/err.log || exit 1
+    timeout -k 10 300 python3 bench.py --model xgboost-airlines --steps 20 --warmup 3 > $O/xgb_${arm}_$r.json 2>> $O/err.log || exit 1
+  done
+done
+unset H2OMX_LIB_DIR
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/gbm -o gbm -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 3 --instrument-steps 0 --no-auc --fit-trees 0 > /dev/null 2> $O/gbm_prof.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/shard -o shard -- python3 $GRAFT_REPO_ROOT/bench.py --rows 1375000 --steps 50 --warmup 5 --instrument-steps 0 --no-auc --fit-trees 0 > /dev/null 2> $O/shard_prof.err || exit 1
