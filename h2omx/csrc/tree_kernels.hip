@@ -3820,16 +3820,22 @@ __global__ __launch_bounds__(512) void hist_build_seg_kernel(
     range_s[1] = min(lo + hc_rows, seg_start[node] + seg_cnt[node]);
   }
   for (int j = threadIdx.x; j < fg * NBT; j += blockDim.x) lds64[j] = 0ull;
+  bool sliced = false;
   if (threadIdx.x < fg) {
     const int fi = threadIdx.x;
     const int w = (fi < nf) ? nvb[f0 + fi] + 1 : NBT;
     width_s[fi] = w;
     const int r = NBT / w;
     rep_s[fi] = r < 1 ? 1 : (r > 64 ? 64 : r);
+    sliced = r > 1;
   }
   const float sg = (float)qscale[0], ss = (float)qscale[1];
   const int64_t rb = (int64_t)qscale[7];  // global row offset of this rank (dither)
-  __syncthreads();
+  // plain: no feature of the group is replicated - every feature is one
+  // NBT-wide slice with NA in its own slot NBT - 1, so the row loop needs no
+  // per-feature width / copy lookups (two LDS reads, a wait and a branch per
+  // code byte) and loads the row's code words 8 at a time
+  const bool plain = !__syncthreads_or(sliced);
   const int lo = range_s[0], hi = range_s[1];
   const int nw = (nf + 3) >> 2;
   for (int j = lo + threadIdx.x; j < hi; j += blockDim.x) {
@@ -3844,6 +3850,22 @@ __global__ __launch_bounds__(512) void hist_build_seg_kernel(
     if (pk == 0ull) continue;
     const uint32_t* row = reinterpret_cast<const uint32_t*>(
         (crow ? crow + (int64_t)(cpos ? cpos[j] : j) * fp : codes_rm + (int64_t)r * fp) + f0);
+    if (plain) {
+      for (int w0 = 0; w0 < nw; w0 += 8) {
+        uint32_t c8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c8[u] = (w0 + u < nw) ? row[w0 + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int fi = 4 * (w0 + u) + k;
+            if (fi < nf) atomicAdd(lds64 + fi * NBT + ((c8[u] >> (8 * k)) & 0xff), pk);
+          }
+        }
+      }
+      continue;
+    }
     for (int wq = 0; wq < nw; ++wq) {
       const uint32_t cw = row[wq];
 #pragma unroll
@@ -3862,6 +3884,10 @@ __global__ __launch_bounds__(512) void hist_build_seg_kernel(
   __syncthreads();
   unsigned long long* out = slab + ((int64_t)c * n_groups + grp) * fg * NBT;
   for (int j = threadIdx.x; j < fg * NBT; j += blockDim.x) {
+    if (plain) {   // one slice per feature, NA in its own slot
+      out[j] = lds64[j];
+      continue;
+    }
     const int bin = j % NBT, fi = j / NBT;
     const int width = width_s[fi], rep = rep_s[fi];
     const int src = (bin == NBT - 1) ? width - 1 : bin;
@@ -3952,13 +3978,16 @@ __device__ __forceinline__ int seg_split_dir(const uint8_t* __restrict__ codes, 
   return split_dir(codes, npad, pi, nbt, r);
 }
 
-// number of rows of chunk c going left (nodes that split into inner nodes)
+// number of rows of chunk c going left (nodes that split into inner nodes);
+// dirb (optional, indexed like idx): every split node's row directions, so
+// part_scatter moves rows without gathering their split codes again
 __global__ __launch_bounds__(256) void part_count_kernel(const uint8_t* __restrict__ codes, int64_t npad,
                                                          const int* __restrict__ idx, const int* __restrict__ seg_start,
                                                          const int* __restrict__ seg_cnt,
                                                          const int* __restrict__ pc_first, const int* __restrict__ ctl,
                                                          const PartInfo* __restrict__ part, int nbt,
-                                                         int* __restrict__ pc_left, SegRows sr) {
+                                                         int* __restrict__ pc_left, SegRows sr,
+                                                         int8_t* __restrict__ dirb) {
   __shared__ int red[4];
   const int n = ctl[CTL_N];
   const int c = blockIdx.x;
@@ -3966,13 +3995,16 @@ __global__ __launch_bounds__(256) void part_count_kernel(const uint8_t* __restri
   const int node = chunk_node(pc_first, n, c);
   const PartInfo pi = part[node];
   int cnt = 0;
-  if (pi.child >= 0 && !pi.leaf_children) {
+  if (pi.child >= 0 && (dirb != nullptr || !pi.leaf_children)) {
     const int lo = seg_start[node] + (c - pc_first[node]) * PC_ROWS;
     const int hi = min(lo + PC_ROWS, seg_start[node] + seg_cnt[node]);
     for (int j = lo + threadIdx.x; j < hi; j += blockDim.x) {
       const int r = idx ? idx[j] : j;
-      cnt += 1 - seg_split_dir(codes, npad, pi, nbt, r, j, sr);
+      const int d = seg_split_dir(codes, npad, pi, nbt, r, j, sr);
+      if (dirb) dirb[j] = (int8_t)d;
+      cnt += 1 - d;
     }
+    if (pi.leaf_children) cnt = 0;   // only inner splits count
   }
   cnt = (int)wave_sum((float)cnt);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
@@ -5125,7 +5157,8 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
     const int* __restrict__ ctl, const PartInfo* __restrict__ part, int nbt, const float* __restrict__ g,
     const float* __restrict__ h, const float* __restrict__ w, const double* __restrict__ qs, int cap,
     unsigned long long* __restrict__ leaf_acc, const float* __restrict__ gin, const float* __restrict__ sin,
-    float* __restrict__ gout, float* __restrict__ sout, SegRows sr, const uint8_t* __restrict__ codes_rm) {
+    float* __restrict__ gout, float* __restrict__ sout, SegRows sr, const uint8_t* __restrict__ codes_rm,
+    const int8_t* __restrict__ dirb) {
   __shared__ int wl[4];
   __shared__ long long red[4];
   const int n = ctl[CTL_N];
@@ -5151,7 +5184,7 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
     int r = 0, dir = 0;
     if (valid) {
       r = idx ? idx[j] : j;
-      if (pi.child >= 0) dir = seg_split_dir(codes, npad, pi, nbt, r, j, sr);
+      if (pi.child >= 0) dir = dirb ? (int)dirb[j] : seg_split_dir(codes, npad, pi, nbt, r, j, sr);
     }
     if (inner) {
       const bool goes_left = valid && dir == 0;
@@ -5435,7 +5468,7 @@ H2OMX_API int h2omx_part_count(const uint8_t* codes, int64_t npad, const int* id
     return launch_status();
   }
   hipLaunchKernelGGL(part_count_kernel, dim3(max_chunks), dim3(256), 0, stream, codes, npad, idx, seg_start, seg_cnt,
-                     pc_first, ctl, reinterpret_cast<const PartInfo*>(part), nbt, pc_left, sr);
+                     pc_first, ctl, reinterpret_cast<const PartInfo*>(part), nbt, pc_left, sr, dirb);
   return launch_status();
 }
 
@@ -5652,6 +5685,6 @@ H2OMX_API int h2omx_part_scatter(const uint8_t* codes, int64_t npad, const int* 
   hipLaunchKernelGGL(part_scatter_kernel, dim3(max_chunks), dim3(256), 0, stream, codes, npad, idx, idx_out, nid,
                      write_nid, seg_start, seg_cnt, pc_first, pc_off, node_nl, ctl,
                      reinterpret_cast<const PartInfo*>(part), nbt, g, h, w, qscale, cap, leaf_acc, gin, sin, gout,
-                     sout, sr, codes_rm);
+                     sout, sr, codes_rm, dirb);
   return launch_status();
 }

@@ -861,7 +861,7 @@ class HipTreeBuilder:
             pwave = int(max_nodes >= self.PART_WAVE_NODES or ec is not None)
             ecodes, ecs, nodeq = ec if ec is not None else (None, 0, None)
             # row directions stored by part_count for part_scatter (not on the last level: no count pass)
-            dirb = B("dirb", n + 64, torch.int8) if (pwave and not last) else None
+            dirb = B("dirb", n + 64, torch.int8) if not last else None
             pc_left = B("pc_left", max_pc, i32)
             node_nl = B("node_nl", 2 * max_nodes, i32)
             idx_out = None
