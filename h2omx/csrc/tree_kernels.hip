@@ -3998,7 +3998,22 @@ __global__ __launch_bounds__(256) void part_count_kernel(const uint8_t* __restri
   if (pi.child >= 0 && (dirb != nullptr || !pi.leaf_children)) {
     const int lo = seg_start[node] + (c - pc_first[node]) * PC_ROWS;
     const int hi = min(lo + PC_ROWS, seg_start[node] + seg_cnt[node]);
-    for (int j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+    // four rows per thread in flight: their row ids, then their code gathers
+    const int bs = blockDim.x;
+    int j = lo + threadIdx.x;
+    for (; j + 3 * bs < hi; j += 4 * bs) {
+      int r4[4], d4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) r4[u] = idx ? idx[j + u * bs] : j + u * bs;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d4[u] = seg_split_dir(codes, npad, pi, nbt, r4[u], j + u * bs, sr);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (dirb) dirb[j + u * bs] = (int8_t)d4[u];
+        cnt += 1 - d4[u];
+      }
+    }
+    for (; j < hi; j += bs) {
       const int r = idx ? idx[j] : j;
       const int d = seg_split_dir(codes, npad, pi, nbt, r, j, sr);
       if (dirb) dirb[j] = (int8_t)d;
@@ -5178,14 +5193,30 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
   int base_l = inner ? pc_off[c] : 0;
   int base_r = inner ? (lo - start) - base_l : 0;
   const int nl = inner ? node_nl[node] : 0;
+  // the row's id, direction and moved (g, s2) are loaded one iteration ahead
+  // (independent of the two barriers per iteration), so the loop's critical
+  // path no longer starts with their load latency
+  auto fetch = [&](int j, int& r, int& dir, float& gv, float& sv) {
+    r = 0; dir = 0; gv = 0.f; sv = 0.f;
+    if (j < hi) {
+      r = idx ? idx[j] : j;
+      if (pi.child >= 0 && dirb) dir = (int)dirb[j];
+      if (inner && gout) {
+        gv = gin[j];
+        if (sout) sv = sin[j];
+      }
+    }
+  };
+  int r_n, dir_n;
+  float gv_n, sv_n;
+  fetch(lo + t, r_n, dir_n, gv_n, sv_n);
   for (int j0 = lo; j0 < hi; j0 += blockDim.x) {
     const int j = j0 + t;
     const bool valid = j < hi;
-    int r = 0, dir = 0;
-    if (valid) {
-      r = idx ? idx[j] : j;
-      if (pi.child >= 0) dir = dirb ? (int)dirb[j] : seg_split_dir(codes, npad, pi, nbt, r, j, sr);
-    }
+    int r = r_n, dir = dir_n;
+    const float gv = gv_n, sv = sv_n;
+    fetch(j + blockDim.x, r_n, dir_n, gv_n, sv_n);
+    if (valid && pi.child >= 0 && !dirb) dir = seg_split_dir(codes, npad, pi, nbt, r, j, sr);
     if (inner) {
       const bool goes_left = valid && dir == 0;
       const unsigned long long bl = __ballot(goes_left);
@@ -5207,8 +5238,8 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
         if (sr.cpos_out) sr.cpos_out[start + pos] = sr.cpos_in ? sr.cpos_in[j] : j;
         if (write_nid) nid[r] = pi.child + dir;
         if (gout) {   // the (g, s2) the next level reads, moved with the row into segment order
-          gout[start + pos] = gin[j];
-          if (sout) sout[start + pos] = sin[j];
+          gout[start + pos] = gv;
+          if (sout) sout[start + pos] = sv;
         }
       }
       if (sr.out) {
