@@ -4965,18 +4965,68 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   for (int j = t; j < nfl * NBT; j += blockDim.x) hist[j] = 0;
   __syncthreads();
   long long tg_row = 0, ts_row = 0;
-  for (int j = lo + t; j < hi; j += blockDim.x) {
-    const int r = idx ? idx[j] : j;
-    const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * ec.rs : codes_rm + (int64_t)r * fp;
-    const int64_t fs = ec.crow ? ec.fs : 1;
-    uint32_t cc[DIRECT_FB];
+  const int64_t fs = ec.crow ? ec.fs : 1;
+  if (nfl <= 2 * DIRECT_FB) {
+    // <= 16 eligible features (DRF mtries): the features' code offsets are
+    // wave-uniform (scalar registers, no LDS read per code byte) and each
+    // row's id / plane position is loaded one iteration ahead, so a row's
+    // chain is its code loads -> atomics instead of id -> codes -> atomics
+    int64_t fo[2 * DIRECT_FB];
 #pragma unroll
-    for (int u = 0; u < DIRECT_FB; ++u) cc[u] = (u < nfl) ? row[flist[u] * fs] : 0u;
-    long long gq, sq;
-    direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
-    tg_row += gq; ts_row += sq;
-    direct_row_atomics<NBT>(row, fs, flist, nfl, true, NBT, hist, gq, sq, cc,
-                            ec.codes ? ec.codes + (int64_t)j * ec.stride : nullptr, ec.stride);
+    for (int u = 0; u < 2 * DIRECT_FB; ++u)
+      fo[u] = u < nfl ? (int64_t)__builtin_amdgcn_readfirstlane(flist[u]) * fs : 0;
+    auto row_of = [&](int j, int r) -> const uint8_t* {
+      return ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * ec.rs : codes_rm + (int64_t)r * fp;
+    };
+    int j = lo + t;
+    int r = (j < hi) ? (idx ? idx[j] : j) : 0;
+    const uint8_t* row = (j < hi) ? row_of(j, r) : codes_rm;
+    for (; j < hi; j += blockDim.x) {
+      uint32_t cc[2 * DIRECT_FB];
+#pragma unroll
+      for (int u = 0; u < 2 * DIRECT_FB; ++u) cc[u] = (u < nfl) ? row[fo[u]] : 0u;
+      long long gq, sq;
+      direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
+      // next row's id and code row (independent of this row's atomics)
+      const int jn = j + blockDim.x;
+      const int rn = (jn < hi) ? (idx ? idx[jn] : jn) : 0;
+      const uint8_t* rown = (jn < hi) ? row_of(jn, rn) : codes_rm;
+      tg_row += gq; ts_row += sq;
+      const bool live = gq != 0 || sq != 0;
+      if (ec.codes) {
+        uint8_t* erow = ec.codes + (int64_t)j * ec.stride;
+        const uint32_t w0 = cc[0] | (cc[1] << 8) | (cc[2] << 16) | (cc[3] << 24);
+        const uint32_t w1 = cc[4] | (cc[5] << 8) | (cc[6] << 16) | (cc[7] << 24);
+        if (ec.stride == 16) {
+          const uint32_t w2 = cc[8] | (cc[9] << 8) | (cc[10] << 16) | (cc[11] << 24);
+          const uint32_t w3 = cc[12] | (cc[13] << 8) | (cc[14] << 16) | (cc[15] << 24);
+          *reinterpret_cast<uint4*>(erow) = make_uint4(w0, w1, w2, w3);
+        } else {
+          *reinterpret_cast<uint2*>(erow) = make_uint2(w0, w1);
+        }
+      }
+      if (live) {
+        const unsigned long long pk = ((unsigned long long)(uint32_t)(int)gq << 32) | (unsigned long long)sq;
+#pragma unroll
+        for (int u = 0; u < 2 * DIRECT_FB; ++u)
+          if (u < nfl) atomicAdd(reinterpret_cast<unsigned long long*>(hist + u * NBT + cc[u]), pk);
+      }
+      r = rn;
+      row = rown;
+    }
+  } else {
+    for (int j = lo + t; j < hi; j += blockDim.x) {
+      const int r = idx ? idx[j] : j;
+      const uint8_t* row = ec.crow ? ec.crow + (int64_t)(ec.cpos ? ec.cpos[j] : j) * ec.rs : codes_rm + (int64_t)r * fp;
+      uint32_t cc[DIRECT_FB];
+#pragma unroll
+      for (int u = 0; u < DIRECT_FB; ++u) cc[u] = (u < nfl) ? row[flist[u] * fs] : 0u;
+      long long gq, sq;
+      direct_row_q(r, gpos ? j : r, rb, salt, g, s2, sg, ss, gq, sq);
+      tg_row += gq; ts_row += sq;
+      direct_row_atomics<NBT>(row, fs, flist, nfl, true, NBT, hist, gq, sq, cc,
+                              ec.codes ? ec.codes + (int64_t)j * ec.stride : nullptr, ec.stride);
+    }
   }
   tg_row = wave_sum_i64(tg_row);
   ts_row = wave_sum_i64(ts_row);
@@ -5356,11 +5406,33 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
   int base_r = inner ? (lo - start) - base_l : 0;
   const int nl = inner ? node_nl[node] : 0;
   const unsigned long long lt = (1ull << lane) - 1ull;
+  // inner nodes with stored directions: a row's id, direction, plane position
+  // and moved (g, s2) are loaded one iteration ahead (independent loads off
+  // the iteration's critical path)
+  const bool ahead = inner && dirb != nullptr;
+  int r_n = 0, d_n = 0, cp_n = 0;
+  float gv_n = 0.f, sv_n = 0.f;
+  auto fetch = [&](int j) {
+    if (j < hi) {
+      r_n = idx ? idx[j] : j;
+      d_n = dirb[j];
+      if (sr.cpos_out) cp_n = sr.cpos_in ? sr.cpos_in[j] : j;
+      if (gout) {
+        gv_n = gin[j];
+        if (sout) sv_n = sin[j];
+      }
+    }
+  };
+  if (ahead) fetch(lo + lane);
   for (int j0 = lo; j0 < hi; j0 += 64) {
     const int j = j0 + lane;
     const bool valid = j < hi;
-    int r = 0, dir = 0;
-    if (valid) {
+    int r = 0, dir = 0, cp = 0;
+    float gv = 0.f, sv = 0.f;
+    if (ahead) {
+      r = r_n; dir = d_n; cp = cp_n; gv = gv_n; sv = sv_n;
+      fetch(j + 64);
+    } else if (valid) {
       r = idx ? idx[j] : j;
       if (pi.child >= 0) {
         if (dirb) {
@@ -5372,6 +5444,13 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
           dir = seg_split_dir(codes, npad, pi, nbt, r, j, sr);
         }
       }
+      if (inner) {
+        if (sr.cpos_out) cp = sr.cpos_in ? sr.cpos_in[j] : j;
+        if (gout) {
+          gv = gin[j];
+          if (sout) sv = sin[j];
+        }
+      }
     }
     if (inner) {
       const unsigned long long bl = __ballot(valid && dir == 0);
@@ -5380,11 +5459,11 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
         const int my_l = __popcll(bl & lt), my_v = __popcll(bv & lt);
         const int pos = dir == 0 ? base_l + my_l : nl + base_r + (my_v - my_l);
         idx_out[start + pos] = r;
-        if (sr.cpos_out) sr.cpos_out[start + pos] = sr.cpos_in ? sr.cpos_in[j] : j;
+        if (sr.cpos_out) sr.cpos_out[start + pos] = cp;
         if (write_nid) nid[r] = pi.child + dir;
         if (gout) {
-          gout[start + pos] = gin[j];
-          if (sout) sout[start + pos] = sin[j];
+          gout[start + pos] = gv;
+          if (sout) sout[start + pos] = sv;
         }
       }
       if (sr.out) {
