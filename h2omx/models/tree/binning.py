@@ -57,11 +57,24 @@ class BinnedMatrix:
         return self.codes.device
 
     _codes_rm: torch.Tensor | None = None
+    # row-major code rows padded to line-aligned strides (False: 4-byte strides)
+    ROW_ALIGN = True
 
     @property
     def fp(self) -> int:
-        """Row stride of the row-major codes (F rounded up to 4 bytes)."""
-        return (self.F + 3) // 4 * 4
+        """Row stride of the row-major codes: a power of two up to 128 bytes
+        (F = 100 -> 128), a multiple of 128 above, so no row straddles a
+        128-byte line - a random row gather then fetches one line, not 1.8
+        on average (100-byte rows).  The pad bytes are zero and never read as
+        codes."""
+        if not self.ROW_ALIGN:
+            return (self.F + 3) // 4 * 4
+        if self.F <= 128:
+            fp = 4
+            while fp < self.F:
+                fp *= 2
+            return fp
+        return (self.F + 127) // 128 * 128
 
     @property
     def codes_rm(self) -> torch.Tensor:
