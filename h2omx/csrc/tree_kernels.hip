@@ -4635,11 +4635,14 @@ constexpr int CM_ROWS = 256;
 __global__ __launch_bounds__(256) void seg_colmajor_kernel(const uint8_t* __restrict__ codes_rm, int fp, int F,
                                                            const int* __restrict__ idx, int n, int64_t nrows,
                                                            uint8_t* __restrict__ ccol, int64_t plane) {
-  extern __shared__ uint32_t cm_tile[];   // [CM_ROWS][fp / 4] dwords
+  extern __shared__ uint32_t cm_tile[];   // [CM_ROWS][WP] dwords
   __shared__ int rows[CM_ROWS];
   const int t = threadIdx.x;
   const int j0 = blockIdx.x * CM_ROWS;
-  const int W = fp >> 2;
+  // the words holding the F codes (not the row's pad), at an odd LDS row
+  // pitch: the 4 x 4 block reads below step 4 rows per lane
+  const int W = (F + 3) >> 2;
+  const int WP = W | 1;
   {
     const int j = j0 + t;
     const int r = j < n ? (idx ? idx[j] : j) : -1;
@@ -4649,7 +4652,7 @@ __global__ __launch_bounds__(256) void seg_colmajor_kernel(const uint8_t* __rest
   for (int q = t; q < CM_ROWS * W; q += 256) {
     const int i = q / W, k = q - i * W;
     const int r = rows[i];
-    cm_tile[q] = r >= 0 ? reinterpret_cast<const uint32_t*>(codes_rm + (int64_t)r * fp)[k] : 0u;
+    cm_tile[i * WP + k] = r >= 0 ? reinterpret_cast<const uint32_t*>(codes_rm + (int64_t)r * fp)[k] : 0u;
   }
   __syncthreads();
   // 4 x 4 byte blocks: 4 rows' dword f4 (features 4 f4 .. 4 f4 + 3) in, each
@@ -4659,8 +4662,8 @@ __global__ __launch_bounds__(256) void seg_colmajor_kernel(const uint8_t* __rest
   const int F4 = (F + 3) >> 2;
   for (int q = t; q < F4 * R4; q += 256) {
     const int f4 = q / R4, r4 = q - f4 * R4;
-    const uint32_t* src = cm_tile + 4 * r4 * W + f4;
-    const uint32_t a0 = src[0], a1 = src[W], a2 = src[2 * W], a3 = src[3 * W];
+    const uint32_t* src = cm_tile + 4 * r4 * WP + f4;
+    const uint32_t a0 = src[0], a1 = src[WP], a2 = src[2 * WP], a3 = src[3 * WP];
     uint32_t o[4];
     o[0] = (a0 & 0xffu) | ((a1 & 0xffu) << 8) | ((a2 & 0xffu) << 16) | (a3 << 24);
     o[1] = ((a0 >> 8) & 0xffu) | (a1 & 0xff00u) | ((a2 & 0xff00u) << 8) | ((a3 & 0xff00u) << 16);
@@ -5179,6 +5182,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       direct_row_atomics<NBT>(row, fs, flist + b0, nb, packed, per_f, hist, gq, sq, c0,
                               ecw ? ecw + (int64_t)j * ec.stride : nullptr, ec.stride);
     }
+    if (b0 == 0) {
+      // a node whose weight (mode 0) / hessian (mode 1) total is below twice the
+      // child minimum (or not positive) has no split any scan could accept -
+      // every candidate's gain is -inf - so its feature scans are skipped
+      // (same NodeSplit: no split); deep DRF levels hold many such nodes
+      const double S = (double)wave_sum_i64(ts_row) * is;
+      const double cmin = p.mode == 0 ? p.min_rows : p.min_child_weight;
+      if (!(S > 0.0) || S < 2.0 * cmin) break;
+    }
     wave_lds_sync();
     for (int q = 0; q < nb; ++q) {
       const int f = flist[b0 + q];
@@ -5658,10 +5670,11 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
 H2OMX_API int h2omx_seg_colmajor(const uint8_t* codes_rm, int fp, int F, const int* idx, int n, long long nrows,
                                  uint8_t* ccol, long long plane, hipStream_t stream) {
   const int nb = (n + CM_ROWS - 1) / CM_ROWS;
-  if (n < 1 || fp % 4 || F < 1 || F > fp || (size_t)CM_ROWS * fp > 128 * 1024 || plane % 4 ||
-      plane < (long long)nb * CM_ROWS || !codes_rm || !ccol)
+  const size_t lds = (size_t)CM_ROWS * (fp + 4);
+  if (n < 1 || fp % 4 || F < 1 || F > fp || lds > 128 * 1024 || plane % 4 || plane < (long long)nb * CM_ROWS ||
+      !codes_rm || !ccol)
     return kBadArg;
-  hipLaunchKernelGGL(seg_colmajor_kernel, dim3(nb), dim3(256), (size_t)CM_ROWS * fp, stream, codes_rm, fp, F, idx, n,
+  hipLaunchKernelGGL(seg_colmajor_kernel, dim3(nb), dim3(256), lds, stream, codes_rm, fp, F, idx, n,
                      (int64_t)nrows, ccol, (int64_t)plane);
   return launch_status();
 }

@@ -991,8 +991,8 @@ class HipTreeBuilder:
                                     nsplit, st)
                     ec = None
                 else:
-                    # (the transpose stages 256 code rows in LDS: rows of <= 512 bytes)
-                    if self.COLMAJOR_EVERY > 0 and dmode == 2 and bm.fp <= 512:
+                    # (the transpose stages 256 code rows in LDS: rows of <= 384 bytes)
+                    if self.COLMAJOR_EVERY > 0 and dmode == 2 and bm.fp <= 384:
                         plane = -(-n // 256) * 256
                         ccol = B("ccol", F * plane, torch.uint8)
                         if cm_pos is None or d - cm_last >= self.COLMAJOR_EVERY:
