@@ -58,3 +58,27 @@ def test_histogram_types():
     np.testing.assert_array_equal(er2, eq)
     with pytest.raises(ValueError, match="unknown histogram_type"):
         compute_edges(X, 32, histogram_type="Sturges")
+
+
+def test_row_major_codes_line_aligned(monkeypatch):
+    """Row-major code rows have power-of-two strides up to 128 bytes and
+    multiples of 128 above (no row straddles a 128-byte line), zero pad bytes
+    and the same codes as the feature-major matrix; ROW_ALIGN off keeps the
+    4-byte strides."""
+    from h2omx.models.tree import bin_matrix, compute_edges
+    from h2omx.models.tree.binning import BinnedMatrix
+
+    rng = np.random.default_rng(3)
+    for F, want in ((3, 4), (13, 16), (28, 32), (100, 128), (130, 256)):
+        X = torch.from_numpy(rng.normal(size=(F, 257)).astype(np.float32))
+        e, nv, nbt = compute_edges(X, 63)
+        bm = bin_matrix(X, e, nv, nbt)
+        assert bm.fp == want
+        rm = bm.codes_rm
+        assert rm.shape == (257, want)
+        assert torch.equal(rm[:, :F], bm.codes[:, :257].t())
+        assert int(rm[:, F:].abs().sum()) == 0
+    monkeypatch.setattr(BinnedMatrix, "ROW_ALIGN", False)
+    X = torch.from_numpy(rng.normal(size=(100, 50)).astype(np.float32))
+    e, nv, nbt = compute_edges(X, 63)
+    assert bin_matrix(X, e, nv, nbt).fp == 100
