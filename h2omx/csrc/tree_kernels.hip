@@ -4651,17 +4651,50 @@ __global__ __launch_bounds__(256) void seg_colmajor_kernel(const uint8_t* __rest
   // the words holding the F codes (not the row's pad), at an odd LDS row
   // pitch: the 4 x 4 block reads below step 4 rows per lane
   const int W = (F + 3) >> 2;
-  const int WP = W | 1;
   {
     const int j = j0 + t;
     const int r = j < n ? (idx ? idx[j] : j) : -1;
     rows[t] = (r >= 0 && (int64_t)r < nrows) ? r : -1;
   }
   __syncthreads();
-  for (int q = t; q < CM_ROWS * W; q += 256) {
-    const int i = q / W, k = q - i * W;
-    const int r = rows[i];
-    cm_tile[i * WP + k] = r >= 0 ? reinterpret_cast<const uint32_t*>(codes_rm + (int64_t)r * fp)[k] : 0u;
+  // 16-byte rows (fp % 16 == 0 on an aligned base, so the W16 chunks holding
+  // the F codes stay inside the row): LPR lanes per row, 8 chunk loads per lane
+  // in flight (and no per-word index division, as in the dword loop below),
+  // stored with ds_write_b128 at a pitch of an odd number of chunks.  Row i's
+  // chunks are rotated by i / 4 so that the 4-row block reads below stay
+  // 4-way, like the dword layout's odd pitch.
+  const bool vec = (fp & 15) == 0 && (reinterpret_cast<uintptr_t>(codes_rm) & 15) == 0;
+  const int W16 = (F + 15) >> 4;
+  const int WP4 = vec ? (W16 | 1) : 0;   // pitch in 16-byte chunks
+  const int WP = vec ? 4 * WP4 : (W | 1);
+  if (vec) {
+    const int LPR = W16 <= 4 ? 4 : (W16 <= 8 ? 8 : (W16 <= 16 ? 16 : 32));   // W16 <= 24 (fp <= 384)
+    const int RPI = 256 / LPR;
+    const int k = t & (LPR - 1), tr = t / LPR;
+    for (int i0 = tr; i0 < CM_ROWS; i0 += 8 * RPI) {
+      uint4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * RPI;
+        const int r = (i < CM_ROWS && k < W16) ? rows[i] : -1;
+        v[u] = r >= 0 ? reinterpret_cast<const uint4*>(codes_rm + (int64_t)r * fp)[k] : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * RPI;
+        if (i < CM_ROWS && k < W16) {
+          int c = k + ((i >> 2) % WP4);
+          c = c >= WP4 ? c - WP4 : c;
+          reinterpret_cast<uint4*>(cm_tile + i * WP)[c] = v[u];
+        }
+      }
+    }
+  } else {
+    for (int q = t; q < CM_ROWS * W; q += 256) {
+      const int i = q / W, k = q - i * W;
+      const int r = rows[i];
+      cm_tile[i * WP + k] = r >= 0 ? reinterpret_cast<const uint32_t*>(codes_rm + (int64_t)r * fp)[k] : 0u;
+    }
   }
   __syncthreads();
   // 4 x 4 byte blocks: 4 rows' dword f4 (features 4 f4 .. 4 f4 + 3) in, each
@@ -4671,7 +4704,13 @@ __global__ __launch_bounds__(256) void seg_colmajor_kernel(const uint8_t* __rest
   const int F4 = (F + 3) >> 2;
   for (int q = t; q < F4 * R4; q += 256) {
     const int f4 = q / R4, r4 = q - f4 * R4;
-    const uint32_t* src = cm_tile + 4 * r4 * WP + f4;
+    int col = f4;
+    if (vec) {   // the chunk rotation of the rows 4 r4 .. 4 r4 + 3
+      int c = (f4 >> 2) + r4 % WP4;
+      c = c >= WP4 ? c - WP4 : c;
+      col = 4 * c + (f4 & 3);
+    }
+    const uint32_t* src = cm_tile + 4 * r4 * WP + col;
     const uint32_t a0 = src[0], a1 = src[WP], a2 = src[2 * WP], a3 = src[3 * WP];
     uint32_t o[4];
     o[0] = (a0 & 0xffu) | ((a1 & 0xffu) << 8) | ((a2 & 0xffu) << 16) | (a3 << 24);
@@ -5664,7 +5703,10 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
 H2OMX_API int h2omx_seg_colmajor(const uint8_t* codes_rm, int fp, int F, const int* idx, int n, long long nrows,
                                  uint8_t* ccol, long long plane, hipStream_t stream) {
   const int nb = (n + CM_ROWS - 1) / CM_ROWS;
-  const size_t lds = (size_t)CM_ROWS * (fp + 4);
+  // dword layout: an odd pitch of W <= fp / 4 words; 16-byte layout (fp % 16 == 0):
+  // an odd pitch of W16 = ceil(F / 16) chunks (seg_colmajor_kernel)
+  const bool vec = (fp & 15) == 0 && (reinterpret_cast<uintptr_t>(codes_rm) & 15) == 0;
+  const size_t lds = (size_t)CM_ROWS * (vec ? 16 * (((F + 15) >> 4) | 1) : fp + 4);
   if (n < 1 || fp % 4 || F < 1 || F > fp || lds > 128 * 1024 || plane % 4 || plane < (long long)nb * CM_ROWS ||
       !codes_rm || !ccol)
     return kBadArg;

@@ -434,3 +434,28 @@ def test_level0_copies_match_plain_slices(cuda_dev, monkeypatch, dist, mode):
             assert reach == b.compact()[t], (cop, t)
             for f in ("feat", "bin", "value"):
                 np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"{cop} {t} {f}")
+
+
+@pytest.mark.parametrize("F,fp", [(13, 16), (100, 128), (200, 256), (37, 40), (6, 8), (300, 384)])
+def test_seg_colmajor_transpose(cuda_dev, F, fp):
+    """h2omx_seg_colmajor: plane f, position j holds code f of row idx[j]
+    (16-byte row chunks when fp % 16 == 0, dwords otherwise); positions whose
+    row id is out of range read as zeros."""
+    from h2omx import ops
+
+    lib = ops.tree_lib()
+    g = torch.Generator().manual_seed(F)
+    nrows, n = 5000, 3001
+    codes = torch.randint(0, 256, (nrows, fp), generator=g, dtype=torch.uint8)
+    idx = torch.randint(0, nrows, (n + 64,), generator=g, dtype=torch.int32)
+    idx[::97] = nrows + 5   # stale ids of retired segments
+    plane = -(-n // 256) * 256
+    ccol = torch.full((F * plane,), 7, dtype=torch.uint8, device=cuda_dev)
+    cd, idd = codes.to(cuda_dev), idx.to(cuda_dev)
+    ops.check(lib.h2omx_seg_colmajor(ops.P(cd), fp, F, ops.P(idd), n, nrows, ops.P(ccol), plane,
+                                     ops.stream(cuda_dev)), "seg_colmajor")
+    got = ccol.view(F, plane)[:, :n].cpu()
+    ok = idx[:n].long() < nrows
+    want = torch.zeros((F, n), dtype=torch.uint8)
+    want[:, ok] = codes[idx[:n].long()[ok], :F].T
+    assert torch.equal(got, want)
