@@ -99,7 +99,11 @@ class HipTreeBuilder:
     # (profiles/r4/drf/move_rows_ab.txt).)
     SEG_TARGET_CHUNKS = 1024   # level-0 histogram chunks (2 resident 57 KB workgroups per CU)
     SEG_LDS_BUDGET = 64 * 1024
-    SCAN_SLOTS = 16  # seg engine: scan hist up to this many slots
+    # seg engine: scan hist up to this many slots - the root only: from level 1 on the
+    # segmented build reads the built children's in-bag rows instead of streaming all
+    # rows (DRF 10M x 100 depth 20: levels 2-5, histograms + partitions 2002 -> 1628 us,
+    # 17.51 -> 16.73 ms/tree; profiles/r6/drf_deep_ab_r6.txt r6ag / r6ah)
+    SCAN_SLOTS = 1
     DEEP_DEPTH = 10
     FUSE_MAX_DEPTH = 8
     FUSE_MAX_PREV = 4
@@ -256,7 +260,7 @@ class HipTreeBuilder:
         #   but each level costs at least one full pass per slot pass, so deep trees
         #   with thousands of nodes per level need hundreds of passes.
         # * seg (row-partitioned): a level only touches the rows of the nodes it
-        #   builds; shallow levels still use the scan histogram kernel (<= SCAN_SLOTS
+        #   builds; the root still uses the scan histogram kernel (<= SCAN_SLOTS
         #   built nodes), deep levels the per-node-chunk kernel.  Default for trees
         #   deeper than DEEP_DEPTH (DRF's default max_depth 20).
         eng = os.environ.get("H2OMX_TREE_ENGINE", "auto")
