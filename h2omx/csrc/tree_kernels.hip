@@ -5352,7 +5352,7 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
         const float wv = w ? w[r] : 1.0f;
         if (wv != 0.0f) {
           sg[dir] += __float2int_rn(g[r] * lg);
-          sh[dir] += __float2int_rn(h[r] * lh);
+          if (h) sh[dir] += __float2int_rn(h[r] * lh);   // (no h: mean leaves, H unused)
           sw[dir] += __float2int_rn(wv * lw);
         }
       }
@@ -5529,7 +5529,7 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
         const float wv = (sg_seg && !s_is_h) ? (sin ? sin[j] : 1.0f) : (w ? w[r] : 1.0f);
         if (wv != 0.0f) {
           const float gk = sg_seg ? gin[j] : g[r];
-          const float hk = (sg_seg && s_is_h) ? sin[j] : h[r];
+          const float hk = (sg_seg && s_is_h) ? sin[j] : (h ? h[r] : 0.f);   // (no h: mean leaves)
           sg[dir] += __float2int_rn(gk * lg);
           sh[dir] += __float2int_rn(hk * lh);
           sw[dir] += __float2int_rn(wv * lw);

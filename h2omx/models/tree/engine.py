@@ -104,6 +104,7 @@ class HipTreeBuilder:
     # rows (DRF 10M x 100 depth 20: levels 2-5, histograms + partitions 2002 -> 1628 us,
     # 17.51 -> 16.73 ms/tree; profiles/r6/drf_deep_ab_r6.txt r6ag / r6ah)
     SCAN_SLOTS = 1
+    MEAN_LEAVES_NO_H = True   # mean-leaf trees pass no h to the partitions (their H sums are unused)
     DEEP_DEPTH = 10
     FUSE_MAX_DEPTH = 8
     FUSE_MAX_PREV = 4
@@ -853,6 +854,8 @@ class HipTreeBuilder:
         # (g, s2) as the current level reads them: by row at level 0, afterwards in segment order
         # (part_scatter moves them with the rows, so the histogram passes read them contiguously)
         gs = {"g": g, "s": s2, "pos": 0}
+        # mean leaves (DRF) read no H sum: the retiring rows skip their random h[r] gather
+        mean_leaves = p.leaf_mode == 1 and self.MEAN_LEAVES_NO_H
 
         def route(d, last, max_nodes, next_nodes, part, nl, seg_start, seg_cnt, pc_first, ctl_cur, ctl_nxt,
                   idx_in, next_direct, ec=None, cpos=(None, None)):
@@ -915,7 +918,8 @@ class HipTreeBuilder:
                 sout = None if s2 is None else B(f"sperm{d % 2}", n + 64, torch.float32)
             ops.check(lib.h2omx_part_scatter(P(bm.codes), bm.npad, P(idx_in), P(idx_out), P(self.nid), write_nid,
                                              P(seg_start), P(seg_cnt), P(pc_first), P(pc_left), P(node_nl),
-                                             P(ctl_cur), P(part), nbt, P(g), P(h), P(w), P(self.qscale),
+                                             P(ctl_cur), P(part), nbt, P(g), P(None if mean_leaves else h), P(w),
+                                             P(self.qscale),
                                              self.capacity, P(self.leaf_acc), max_pc, pwave | segf, P(dirb), P(gs["g"]),
                                              P(gs["s"]), P(gout), P(sout), P(ecodes), ecs, P(nodeq),
                                              P(self.codes_rm), None, None, bm.fp, P(cpos[0]),

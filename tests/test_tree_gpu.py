@@ -459,3 +459,25 @@ def test_seg_colmajor_transpose(cuda_dev, F, fp):
     want = torch.zeros((F, n), dtype=torch.uint8)
     want[:, ok] = codes[idx[:n].long()[ok], :F].T
     assert torch.equal(got, want)
+
+
+def test_mean_leaves_without_h_match(cuda_dev, monkeypatch):
+    """DRF (mean leaves) on the segmented engine: partitions given no h (their
+    H sums are unused) grow the same trees, values and weights."""
+    import h2omx.models.tree.engine as E
+
+    X, y = _data(n=40000, F=11, seed=9, task="bin")
+    _, bg = _both(X, y, 64)
+    tp = TreeParams(max_depth=14, min_rows=2, learn_rate=1.0, leaf_mode=1, mtries=4)
+    yt = torch.from_numpy(y).cuda()
+    monkeypatch.setenv("H2OMX_TREE_ENGINE", "seg")
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(E.HipTreeBuilder, "MEAN_LEAVES_NO_H", flag)
+        out[flag] = train_ensemble(bg, yt, dist="drf", ntrees=3, tparams=tp, sample_rate=0.632, nclass=2, seed=3)
+    a, b = out[False], out[True]
+    for t in range(a.trees.shape[0]):
+        reach = a.compact()[t]
+        assert reach == b.compact()[t]
+        for f in ("feat", "bin", "value", "weight"):
+            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"tree {t} {f}")
