@@ -4727,6 +4727,54 @@ __global__ __launch_bounds__(256) void seg_colmajor_kernel(const uint8_t* __rest
 
 
 
+// Row-major code rows from the feature-major codes (BinnedMatrix.codes_rm, built
+// once per matrix for the segmented engine): [F][npad] -> [n][fp], pad bytes
+// zero.  One workgroup per 256 rows and 128 features at a time: each feature's
+// 256 bytes come in as one wave-wide dword load, and every thread leaves with
+// its own row in 16-byte stores (replaces a strided torch copy: 10M x 100,
+// 3.7 ms).
+constexpr int RM_ROWS = 256, RM_FC = 128;
+__global__ __launch_bounds__(256) void codes_rowmajor_kernel(const uint8_t* __restrict__ codes, int64_t npad, int F,
+                                                             int64_t n, uint8_t* __restrict__ rm, int fp) {
+  __shared__ uint32_t tile[RM_FC * RM_ROWS / 4];   // [feature][256 rows] bytes
+  const uint8_t* tb = reinterpret_cast<const uint8_t*>(tile);
+  const int t = threadIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.x * RM_ROWS;
+  const int64_t j = j0 + t;
+  for (int fc0 = 0; fc0 < fp; fc0 += RM_FC) {
+    const int fcnt = min(RM_FC, F - fc0);   // may be <= 0: pad-only chunk
+    for (int q = t; q < max(fcnt, 0) * (RM_ROWS / 4); q += 256) {
+      const int f = q / (RM_ROWS / 4), w = q - f * (RM_ROWS / 4);
+      const int64_t p0 = j0 + 4 * w;
+      tile[q] = p0 < npad ? reinterpret_cast<const uint32_t*>(codes + (int64_t)(fc0 + f) * npad + j0)[w] : 0u;
+    }
+    __syncthreads();
+    if (j < n) {
+      uint8_t* dst = rm + j * fp + fc0;
+      const int nb = min(RM_FC, fp - fc0);   // bytes of this chunk in the row (a multiple of 4)
+      for (int b0 = 0; b0 < nb; b0 += 16) {
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          uint32_t x = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int f = b0 + 4 * k + e;
+            if (f < fcnt) x |= (uint32_t)tb[f * RM_ROWS + t] << (8 * e);
+          }
+          v[k] = x;
+        }
+        if ((fp & 15) == 0 && b0 + 16 <= nb) {
+          *reinterpret_cast<uint4*>(dst + b0) = make_uint4(v[0], v[1], v[2], v[3]);
+        } else {
+          for (int k = 0; 4 * k < nb - b0; ++k) reinterpret_cast<uint32_t*>(dst + b0)[k] = v[k];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // mtries selection of a wave's features (lane + 64 k, k < 4, F <= 256, hashes
 // hv): feature f is eligible iff fewer than m features have a smaller
 // (hash, index) key - the m smallest keys.  Instead of ranking every pair (F
@@ -5700,6 +5748,19 @@ H2OMX_API int h2omx_seg_direct(const uint8_t* codes_rm, int fp, const int* idx, 
 
 // column-major planes of this level's positions (seg_colmajor_kernel); plane:
 // positions per feature plane (>= n rounded up to CM_ROWS, a multiple of 4)
+// BinnedMatrix.codes_rm: rm [n][fp] (fp % 4 == 0, fp >= F, rm 16-byte aligned;
+// 16-byte stores when fp % 16 == 0) from codes [F][npad] (npad % 64 == 0)
+H2OMX_API int h2omx_codes_rowmajor(const uint8_t* codes, long long npad, int F, long long n, uint8_t* rm, int fp,
+                                   hipStream_t stream) {
+  if (!codes || !rm || n < 1 || F < 1 || fp < F || fp % 4 || npad % 64 || npad < n ||
+      (reinterpret_cast<uintptr_t>(rm) & 15) || (reinterpret_cast<uintptr_t>(codes) & 3))
+    return kBadArg;
+  const int64_t nb = (n + RM_ROWS - 1) / RM_ROWS;
+  hipLaunchKernelGGL(codes_rowmajor_kernel, dim3((unsigned)nb), dim3(256), 0, stream, codes, (int64_t)npad, F,
+                     (int64_t)n, rm, fp);
+  return launch_status();
+}
+
 H2OMX_API int h2omx_seg_colmajor(const uint8_t* codes_rm, int fp, int F, const int* idx, int n, long long nrows,
                                  uint8_t* ccol, long long plane, hipStream_t stream) {
   const int nb = (n + CM_ROWS - 1) / CM_ROWS;

@@ -59,6 +59,8 @@ class BinnedMatrix:
     _codes_rm: torch.Tensor | None = None
     # row-major code rows padded to line-aligned strides (False: 4-byte strides)
     ROW_ALIGN = True
+    # codes_rm built by codes_rowmajor_kernel (False: a strided torch copy)
+    ROWMAJOR_KERNEL = True
 
     @property
     def fp(self) -> int:
@@ -81,8 +83,15 @@ class BinnedMatrix:
         """Row-major copy uint8 [n][fp] (lazily built once): the segmented
         histogram kernel gathers whole rows (28 B for HIGGS) by row index."""
         if self._codes_rm is None:
-            rm = torch.zeros((self.n, self.fp), dtype=torch.uint8, device=self.codes.device)
-            rm[:, : self.F] = self.codes[:, : self.n].t()
+            c = self.codes
+            if self.ROWMAJOR_KERNEL and c.is_cuda and c.is_contiguous() and c.shape == (self.F, self.npad) and self.npad % 64 == 0:
+                # (codes_rowmajor_kernel: LDS-tiled, writes the pad bytes too)
+                rm = torch.empty((self.n, self.fp), dtype=torch.uint8, device=c.device)
+                ops.check(ops.tree_lib().h2omx_codes_rowmajor(ops.P(c), self.npad, self.F, self.n, ops.P(rm),
+                                                              self.fp, ops.stream(c.device)), "codes_rowmajor")
+            else:
+                rm = torch.zeros((self.n, self.fp), dtype=torch.uint8, device=c.device)
+                rm[:, : self.F] = c[:, : self.n].t()
             self._codes_rm = rm
         return self._codes_rm
 

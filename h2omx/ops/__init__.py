@@ -60,6 +60,7 @@ TREE_SIGS = {
     "h2omx_part_scatter": "PLPPPIPPPPPPPIPPPPIPIIPPPPPPIPPPPIPPS",
     "h2omx_seg_direct": "PIPPPPPPPPPIPIIIPIPPPPIPIPPPLS",
     "h2omx_seg_colmajor": "PIIPILPLS",
+    "h2omx_codes_rowmajor": "PLILPIS",
     "h2omx_level_finalize_ns": "PPPPPPIIPPPIIPS",
     "h2omx_direct_dp_stride": "PI",
     "h2omx_direct_dp": "IPIPPPPPPPPPPIIIPPIPS",

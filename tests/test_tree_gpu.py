@@ -481,3 +481,16 @@ def test_mean_leaves_without_h_match(cuda_dev, monkeypatch):
         assert reach == b.compact()[t]
         for f in ("feat", "bin", "value", "weight"):
             np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"tree {t} {f}")
+
+
+@pytest.mark.parametrize("F,n", [(100, 70000), (13, 5000), (6, 300), (37, 1000), (300, 2000)])
+def test_codes_rowmajor_matches_torch(cuda_dev, F, n):
+    """BinnedMatrix.codes_rm (h2omx_codes_rowmajor): row j holds the F codes of
+    row j, the pad bytes up to fp are zero - as the strided torch copy."""
+    X = torch.from_numpy(np.random.default_rng(F).normal(size=(F, n)).astype(np.float32))
+    e, nv, nbt = compute_edges(X, 63)
+    bm = bin_matrix(X.to(cuda_dev), e, nv, nbt)
+    got = bm.codes_rm.cpu()
+    want = torch.zeros((bm.n, bm.fp), dtype=torch.uint8)
+    want[:, :F] = bm.codes[:, : bm.n].t().cpu()
+    assert bm.fp >= F and torch.equal(got, want)
