@@ -583,7 +583,69 @@ class GpuBooster:
         if self.cap <= self.COMPACT_CAP:
             return b.tree_buf.clone()
         total = max(1, int(b.tree_size()))
-        return b.tree_buf[: total * TREE_NODE_DTYPE.itemsize].clone()
+        snap = b.tree_buf[: total * TREE_NODE_DTYPE.itemsize].clone()
+        self._download(len(self.trees_dev), snap)
+        return snap
+
+    # deep trees: each snapshot is downloaded by a helper thread on its own stream
+    # while the next tree builds (a 10-tree DRF depth-20 forest is ~190 MB: the
+    # staged copy at finish() cost ~17 ms a fit), straight into the row of a
+    # zero-initialised host array (calloc'd: untouched pages stay unmapped)
+    ntrees_hint = None
+    ASYNC_DOWNLOAD = True
+
+    def _download(self, i: int, snap: torch.Tensor) -> None:
+        dl = getattr(self, "_dl", None)
+        if dl is None:
+            if not (self.ASYNC_DOWNLOAD and self.ntrees_hint and self.dev.type == "cuda"):
+                self._dl = False
+                return
+            import queue
+            import threading
+
+            host = np.zeros((int(self.ntrees_hint) * self.K, self.cap * TREE_NODE_DTYPE.itemsize), np.uint8)
+            q: queue.Queue = queue.Queue()
+            state = {"host": host, "q": q, "err": None, "n": 0}
+
+            def run():
+                side = torch.cuda.Stream(self.dev)
+                while True:
+                    item = q.get()
+                    if item is None:
+                        return
+                    j, src, ev = item
+                    try:
+                        with torch.cuda.stream(side):
+                            side.wait_event(ev)
+                            torch.from_numpy(host[j, : src.numel()]).copy_(src)
+                    except Exception as e:   # reported (and the forest downloaded again) by finish()
+                        state["err"] = e
+
+            state["thread"] = threading.Thread(target=run, name="h2omx-tree-download", daemon=True)
+            state["thread"].start()
+            self._dl = dl = state
+        if dl is False:
+            return
+        if i >= dl["host"].shape[0]:
+            dl["err"] = IndexError("more trees than ntrees_hint")
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        dl["q"].put((i, snap, ev))
+        dl["n"] += 1
+
+    def _downloaded(self, width: int):
+        """The host forest [ntrees][width] bytes from the helper thread (None:
+        not used or failed - finish() copies the device forest)."""
+        dl = getattr(self, "_dl", None)
+        if not dl:
+            return None
+        dl["q"].put(None)
+        dl["thread"].join()
+        self._dl = None
+        if dl["err"] is not None or dl["n"] != len(self.trees_dev):
+            return None
+        return dl["host"][: len(self.trees_dev), :width]
 
     def finish(self) -> TreeEnsemble:
         self.flush()
@@ -606,7 +668,10 @@ class GpuBooster:
                 raw = torch.zeros((len(self.trees_dev), width), dtype=torch.uint8, device=self.dev)
                 for i, t in enumerate(self.trees_dev):
                     raw[i, : t.numel()] = t
-            self.ens.trees = trees_from_bytes(raw.cpu().numpy(), width // TREE_NODE_DTYPE.itemsize)
+            host = self._downloaded(width)
+            if host is None:
+                host = raw.cpu().numpy()
+            self.ens.trees = trees_from_bytes(host, width // TREE_NODE_DTYPE.itemsize)
             if self.cats_dev:
                 self.ens.catbits = _stack_cats(self.cats_dev, width // TREE_NODE_DTYPE.itemsize)
             else:
@@ -625,6 +690,7 @@ class GpuBooster:
 def _train_gpu(bm, y_np, w_np, ens, ntrees, tp, sample_rate, seed, comm, callback, dist_kw, tree_offset=0):
     t0 = time.perf_counter()
     gb = GpuBooster(bm, y_np, w_np, ens, tp, sample_rate, seed, comm, dist_kw, tree_offset=tree_offset)
+    gb.ntrees_hint = ntrees
     lr0, ann = tp.learn_rate, tp.learn_rate_annealing
     for t in range(ntrees):
         if ann != 1.0:

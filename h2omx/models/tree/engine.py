@@ -1145,6 +1145,9 @@ def trees_from_bytes(buf: np.ndarray, capacity: int) -> np.ndarray:
     """View raw bytes as [ntrees][capacity] TREE_NODE_DTYPE records (a view of
     the downloaded buffer, no copy: a 10-tree DRF depth-20 forest is ~400 MB,
     and the former tobytes() copy cost ~30 ms a fit)."""
+    if buf.ndim == 2 and buf.dtype == np.uint8 and buf.shape[1] == capacity * TREE_NODE_DTYPE.itemsize \
+            and buf.strides[1] == 1:
+        return buf.view(TREE_NODE_DTYPE)   # rows of a larger host array (async download): no copy either
     return np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1).view(TREE_NODE_DTYPE).reshape(-1, capacity)
 
 

@@ -494,3 +494,23 @@ def test_codes_rowmajor_matches_torch(cuda_dev, F, n):
     want = torch.zeros((bm.n, bm.fp), dtype=torch.uint8)
     want[:, :F] = bm.codes[:, : bm.n].t().cpu()
     assert bm.fp >= F and torch.equal(got, want)
+
+
+def test_async_forest_download_matches(cuda_dev, monkeypatch):
+    """Deep trees are downloaded per tree by a helper thread while the next
+    one builds: the host forest equals the one copied at the end of the fit."""
+    from h2omx.models.tree.boost import GpuBooster
+
+    X, y = _data(n=30000, F=9, seed=4, task="bin")
+    _, bg = _both(X, y, 64)
+    tp = TreeParams(max_depth=16, min_rows=1, learn_rate=1.0, leaf_mode=1, mtries=3)
+    yt = torch.from_numpy(y).cuda()
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(GpuBooster, "ASYNC_DOWNLOAD", flag)
+        out[flag] = train_ensemble(bg, yt, dist="drf", ntrees=4, tparams=tp, sample_rate=0.632, nclass=2, seed=2)
+    a, b = out[False], out[True]
+    assert a.trees.shape == b.trees.shape and not b.trees.flags["C_CONTIGUOUS"]
+    assert a.trees.tobytes() == b.trees.tobytes()
+    Xd = torch.from_numpy(X).cuda()
+    np.testing.assert_array_equal(a.raw_margin(Xd).cpu().numpy(), b.raw_margin(Xd).cpu().numpy())
