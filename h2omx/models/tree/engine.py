@@ -117,8 +117,10 @@ class HipTreeBuilder:
     # ... and only when a node has at most this many eligible features on average
     DIRECT_MAX_ELIG = 32.0
     # direct levels whose average node holds fewer rows than this run one wave per node
-    # (seg_direct_wave_kernel, F <= 256) instead of one workgroup per node
-    DIRECT_WAVE_ROWS = 256
+    # (seg_direct_wave_kernel, F <= 256) instead of one workgroup per node (DRF 10M x 100
+    # depth 20: 128 / 256 / 512 / 1024 / 2048 -> 16.13 / 15.13 / 14.85 / 15.05 / 15.76 ms/tree,
+    # profiles/r6/drf_switches_r6o.txt r6an / r6ao)
+    DIRECT_WAVE_ROWS = 512
     # segmented partition: levels of at least this many potential nodes run one wave per row chunk
     # (part_count_wave / part_scatter_wave: 64-ary chunk -> node search, stored row directions)
     PART_WAVE_NODES = 2048
