@@ -112,8 +112,9 @@ class HipTreeBuilder:
     # segmented engine, single rank: levels with >= this many potential nodes build each
     # node's eligible-feature histograms directly and scan them in LDS (seg_direct_kernel:
     # no parent histograms / subtraction); 0 = off.  Multi-rank runs keep the all-reduced
-    # subtraction path (direct histograms are rank-local)
-    DIRECT_MIN_NODES = 1024
+    # subtraction path (direct histograms are rank-local).  DRF 10M x 100 depth 20: 512 / 1024 /
+    # 2048 / 4096 -> 15.66 / 14.85 / 14.66 / 14.74 ms/tree (profiles/r6/drf_switches_r6o.txt r6ap / r6aq)
+    DIRECT_MIN_NODES = 2048
     # ... and only when a node has at most this many eligible features on average
     DIRECT_MAX_ELIG = 32.0
     # direct levels whose average node holds fewer rows than this run one wave per node
