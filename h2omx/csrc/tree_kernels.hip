@@ -3797,6 +3797,108 @@ __global__ __launch_bounds__(256) void tree_begin_seg_kernel(
   slot_node[0] = 0;
 }
 
+// In-bag root segment (HipTreeBuilder.BAG_COMPACT, bagged deep trees): the
+// rows of weight 0 - out of this tree's bag (DRF: 37 %) - carry g = s = 0 and
+// change no histogram, split or leaf sum, yet every level would read,
+// partition and scan them.  The root segment instead holds only rows of
+// nonzero weight, ascending (per-chunk counts -> one-workgroup scan ->
+// ballot-ordered scatter, deterministic), with their (g, s2) gathered into
+// segment order; the dropped rows get their leaf by walking the finished tree
+// (bag_route_out_kernel).
+constexpr int BAG_CHUNK = 4096;
+__global__ __launch_bounds__(256) void bag_count_kernel(const float* __restrict__ w, int64_t n, int* __restrict__ cnt) {
+  __shared__ int red[4];
+  const int64_t c0 = (int64_t)blockIdx.x * BAG_CHUNK;
+  int k = 0;
+  for (int i = threadIdx.x; i < BAG_CHUNK; i += 256) {
+    const int64_t r = c0 + i;
+    k += (r < n && w[r] != 0.0f) ? 1 : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) k += __shfl_down(k, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = k;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(1024) void bag_scan_kernel(int* __restrict__ cnt, int nch, int* __restrict__ seg_cnt,
+                                                        int* __restrict__ hc_first, int* __restrict__ pc_first,
+                                                        int hc_rows) {
+  __shared__ int sc[1024];
+  const int t = threadIdx.x;
+  int carry = 0;
+  for (int b0 = 0; b0 < nch; b0 += 1024) {
+    const int v = b0 + t < nch ? cnt[b0 + t] : 0;
+    sc[t] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int x = t >= o ? sc[t - o] : 0;
+      __syncthreads();
+      sc[t] += x;
+      __syncthreads();
+    }
+    if (b0 + t < nch) cnt[b0 + t] = carry + sc[t] - v;   // exclusive offsets
+    carry += sc[1023];
+    __syncthreads();
+  }
+  if (t == 0) {
+    seg_cnt[0] = carry;
+    hc_first[1] = (carry + hc_rows - 1) / hc_rows;
+    pc_first[1] = (carry + PC_ROWS - 1) / PC_ROWS;
+  }
+}
+
+__global__ __launch_bounds__(256) void bag_scatter_kernel(const float* __restrict__ w, int64_t n,
+                                                          const int* __restrict__ off, const float* __restrict__ g,
+                                                          const float* __restrict__ s2, int* __restrict__ idx,
+                                                          float* __restrict__ gout, float* __restrict__ sout) {
+  __shared__ int wc[4];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * BAG_CHUNK;
+  int base = off[blockIdx.x];
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int i0 = 0; i0 < BAG_CHUNK; i0 += 256) {
+    const int64_t r = c0 + i0 + t;
+    const bool in = r < n && w[r] != 0.0f;
+    const unsigned long long bl = __ballot(in);
+    if (lane == 0) wc[wid] = __popcll(bl);
+    __syncthreads();
+    int before = 0, tot = 0;
+    for (int k = 0; k < 4; ++k) {
+      if (k < wid) before += wc[k];
+      tot += wc[k];
+    }
+    if (in) {
+      const int pos = base + before + __popcll(bl & lt);
+      idx[pos] = (int)r;
+      gout[pos] = g[r];
+      sout[pos] = s2[r];
+    }
+    base += tot;
+    __syncthreads();
+  }
+}
+
+// the leaf of every row of weight 0 (not in the root segment): walk the
+// finished tree on the feature-major codes (numeric splits; NA code nbt - 1
+// follows na_left), nid = ~leaf as the partitions write it
+__global__ __launch_bounds__(256) void bag_route_out_kernel(const float* __restrict__ w, int64_t n,
+                                                            const uint8_t* __restrict__ codes, int64_t npad,
+                                                            const TreeNode* __restrict__ tree, int nbt,
+                                                            int* __restrict__ nid) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    if (w[r] != 0.0f) continue;
+    int node = 0;
+    for (int it = 0; it < 64; ++it) {
+      const TreeNode nd = tree[node];
+      if (nd.feat < 0) break;
+      const int b = codes[(int64_t)nd.feat * npad + r];
+      const int right = b == nbt - 1 ? !(nd.na_left & 1) : (b > nd.bin ? 1 : 0);
+      node = nd.left + right;
+    }
+    nid[r] = ~node;
+  }
+}
+
 template <int NBT>
 __global__ __launch_bounds__(512) void hist_build_seg_kernel(
     const uint8_t* __restrict__ codes_rm, int fp, const int* __restrict__ idx, const float* __restrict__ g,
@@ -5604,6 +5706,28 @@ __global__ __launch_bounds__(256) void part_scatter_wave_kernel(
 
 // --- C ABI of the segmented pipeline -----------------------------------------
 H2OMX_API int h2omx_pc_rows() { return PC_ROWS; }
+
+// in-bag root segment (bag_*_kernel): idx / gout / sout hold >= n entries, cnt
+// >= ceil(n / BAG_CHUNK) ints; the root's seg_cnt / hc_first / pc_first are rewritten
+H2OMX_API int h2omx_bag_compact(const float* w, long long n, const float* g, const float* s2, int* cnt, int* idx,
+                                float* gout, float* sout, int* seg_cnt, int* hc_first, int* pc_first, int hc_rows,
+                                hipStream_t stream) {
+  if (!w || !g || !s2 || !cnt || !idx || !gout || !sout || !seg_cnt || !hc_first || !pc_first || n < 1 || hc_rows < 1)
+    return kBadArg;
+  const int nch = (int)((n + BAG_CHUNK - 1) / BAG_CHUNK);
+  hipLaunchKernelGGL(bag_count_kernel, dim3(nch), dim3(256), 0, stream, w, (int64_t)n, cnt);
+  hipLaunchKernelGGL(bag_scan_kernel, dim3(1), dim3(1024), 0, stream, cnt, nch, seg_cnt, hc_first, pc_first, hc_rows);
+  hipLaunchKernelGGL(bag_scatter_kernel, dim3(nch), dim3(256), 0, stream, w, (int64_t)n, cnt, g, s2, idx, gout, sout);
+  return launch_status();
+}
+
+H2OMX_API int h2omx_bag_route_out(const float* w, long long n, const uint8_t* codes, long long npad, const void* tree,
+                                  int nbt, int* nid, hipStream_t stream) {
+  if (!w || !codes || !tree || !nid || n < 1 || npad < n) return kBadArg;
+  hipLaunchKernelGGL(bag_route_out_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, stream, w, (int64_t)n, codes,
+                     (int64_t)npad, reinterpret_cast<const TreeNode*>(tree), nbt, nid);
+  return launch_status();
+}
 
 H2OMX_API int h2omx_tree_begin_seg(const unsigned int* stat_max, int mode, int max_rows_per_wg, double* qscale,
                                    int* ctl0, void* link0, unsigned long long* leaf_acc, int leaf_n,

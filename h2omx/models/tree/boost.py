@@ -331,6 +331,7 @@ class GpuBooster:
         self.K, self.dist = ens.K, ens.dist
         self.st = _GpuState(bm, y_np, w_np, self.K, self.dist, ens.init_f, getattr(ens, "_base_margin", None))
         self.builder = HipTreeBuilder(bm, tp, comm)
+        self.builder.bag_compact = sample_rate < 1.0
         self.cap = self.builder.capacity
         self.trees_dev = []
         self.cats_dev = []         # categorical left-set bitsets, parallel to trees_dev

@@ -105,6 +105,10 @@ class HipTreeBuilder:
     # 17.51 -> 16.73 ms/tree; profiles/r6/drf_deep_ab_r6.txt r6ag / r6ah)
     SCAN_SLOTS = 1
     MEAN_LEAVES_NO_H = True   # mean-leaf trees pass no h to the partitions (their H sums are unused)
+    # bagged deep trees: the root segment holds only in-bag rows (bag_compact_kernel); set per
+    # booster (bag_compact: sample_rate < 1)
+    BAG_COMPACT = True
+    bag_compact = False
     DEEP_DEPTH = 10
     FUSE_MAX_DEPTH = 8
     FUSE_MAX_PREV = 4
@@ -850,13 +854,23 @@ class HipTreeBuilder:
         max_depth = p.max_depth
         final_ctl = self.ctl[max_depth % 2]
         max_nodes = 1
-        idx_in = None
         built_zeroed = True          # tree_begin_seg zeroed level 0's histogram
         hc_cap = -(-n // self.hc_rows)
         pc_cap = -(-n // self.pc_rows)
+        idx_in = None
         # (g, s2) as the current level reads them: by row at level 0, afterwards in segment order
         # (part_scatter moves them with the rows, so the histogram passes read them contiguously)
         gs = {"g": g, "s": s2, "pos": 0}
+        # bagged trees: the root segment holds only the rows of nonzero weight, (g, s2) already
+        # in its order; the others get their leaf from the finished tree (bag_route_out)
+        bagged = (self.BAG_COMPACT and self.bag_compact and w is not None and s2 is not None and comm is None
+                  and self.catf is None and n > 0)
+        if bagged:
+            gs = {"g": B("bag_g", n + 64, torch.float32), "s": B("bag_s", n + 64, torch.float32), "pos": 1}
+            idx_in = B("bag_idx", n + 64, i32)
+            ops.check(lib.h2omx_bag_compact(P(w), n, P(g), P(s2), P(B("bag_cnt", -(-n // 4096) + 1, i32)),
+                                            P(idx_in), P(gs["g"]), P(gs["s"]), P(seg[0][1]), P(seg[0][2]),
+                                            P(seg[0][3]), self.hc_rows, st), "bag_compact")
         # mean leaves (DRF) read no H sum: the retiring rows skip their random h[r] gather
         mean_leaves = p.leaf_mode == 1 and self.MEAN_LEAVES_NO_H
 
@@ -1095,6 +1109,9 @@ class HipTreeBuilder:
                                          ctl_cur, ctl_nxt, idx_in, False)
             full_prev = full_cur
             max_nodes = next_nodes
+        if bagged:
+            ops.check(lib.h2omx_bag_route_out(P(w), n, P(bm.codes), bm.npad, P(self.tree_buf), nbt, P(self.nid), st),
+                      "bag_route_out")
         if comm is not None:
             comm.all_reduce_(self.leaf_acc)
         self._leaf_finalize(final_ctl, spp, st)
