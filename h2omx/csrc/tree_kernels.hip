@@ -3879,10 +3879,11 @@ __global__ __launch_bounds__(256) void bag_scatter_kernel(const float* __restric
 }
 
 // the leaf of every row of weight 0 (not in the root segment): walk the
-// finished tree on the feature-major codes (numeric splits; NA code nbt - 1
-// follows na_left), nid = ~leaf as the partitions write it
+// finished tree on the row-major codes - a row's ~20 code reads hit one line
+// (numeric splits; NA code nbt - 1 follows na_left), nid = ~leaf as the
+// partitions write it
 __global__ __launch_bounds__(256) void bag_route_out_kernel(const float* __restrict__ w, int64_t n,
-                                                            const uint8_t* __restrict__ codes, int64_t npad,
+                                                            const uint8_t* __restrict__ codes_rm, int fp,
                                                             const TreeNode* __restrict__ tree, int nbt,
                                                             int* __restrict__ nid) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
@@ -3891,7 +3892,7 @@ __global__ __launch_bounds__(256) void bag_route_out_kernel(const float* __restr
     for (int it = 0; it < 64; ++it) {
       const TreeNode nd = tree[node];
       if (nd.feat < 0) break;
-      const int b = codes[(int64_t)nd.feat * npad + r];
+      const int b = codes_rm[r * fp + nd.feat];
       const int right = b == nbt - 1 ? !(nd.na_left & 1) : (b > nd.bin ? 1 : 0);
       node = nd.left + right;
     }
@@ -5721,11 +5722,11 @@ H2OMX_API int h2omx_bag_compact(const float* w, long long n, const float* g, con
   return launch_status();
 }
 
-H2OMX_API int h2omx_bag_route_out(const float* w, long long n, const uint8_t* codes, long long npad, const void* tree,
+H2OMX_API int h2omx_bag_route_out(const float* w, long long n, const uint8_t* codes_rm, int fp, const void* tree,
                                   int nbt, int* nid, hipStream_t stream) {
-  if (!w || !codes || !tree || !nid || n < 1 || npad < n) return kBadArg;
-  hipLaunchKernelGGL(bag_route_out_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, stream, w, (int64_t)n, codes,
-                     (int64_t)npad, reinterpret_cast<const TreeNode*>(tree), nbt, nid);
+  if (!w || !codes_rm || !tree || !nid || n < 1 || fp < 1) return kBadArg;
+  hipLaunchKernelGGL(bag_route_out_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, stream, w, (int64_t)n, codes_rm,
+                     fp, reinterpret_cast<const TreeNode*>(tree), nbt, nid);
   return launch_status();
 }
 

@@ -1110,7 +1110,8 @@ class HipTreeBuilder:
             full_prev = full_cur
             max_nodes = next_nodes
         if bagged:
-            ops.check(lib.h2omx_bag_route_out(P(w), n, P(bm.codes), bm.npad, P(self.tree_buf), nbt, P(self.nid), st),
+            ops.check(lib.h2omx_bag_route_out(P(w), n, P(self.codes_rm), bm.fp, P(self.tree_buf), nbt,
+                                              P(self.nid), st),
                       "bag_route_out")
         if comm is not None:
             comm.all_reduce_(self.leaf_acc)

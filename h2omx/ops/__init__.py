@@ -53,7 +53,7 @@ TREE_SIGS = {
     "h2omx_pc_rows": "",
     "h2omx_tree_begin_seg": "PIIPPPPIPIIIPPPPPLIPS",
     "h2omx_bag_compact": "PLPPPPPPPPPIS",
-    "h2omx_bag_route_out": "PLPLPIPS",
+    "h2omx_bag_route_out": "PLPIPIPS",
     "h2omx_hist_build_seg": "PIPPPPPPPPPIIIIIIIIPIPPS",
     "h2omx_hist_reduce_seg": "PPPPIIIIIIPS",
     "h2omx_part_count": "PLPPPPPPIIPIPPIPPIPS",
