@@ -516,14 +516,15 @@ def test_async_forest_download_matches(cuda_dev, monkeypatch):
     np.testing.assert_array_equal(a.raw_margin(Xd).cpu().numpy(), b.raw_margin(Xd).cpu().numpy())
 
 
-@pytest.mark.parametrize("dist,mode", [("drf", 0), ("gaussian", 0), ("bernoulli", 1)])
-def test_bag_compact_matches(cuda_dev, monkeypatch, dist, mode):
+@pytest.mark.parametrize("dist,mode,nclass", [("drf", 0, 2), ("drf", 0, 3), ("gaussian", 0, 1), ("bernoulli", 1, 1),
+                                             ("multinomial", 0, 3)])
+def test_bag_compact_matches(cuda_dev, monkeypatch, dist, mode, nclass):
     """Bagged deep trees whose root segment holds only in-bag rows (the
     others walk the finished tree for their leaf) grow the same trees and
     leave the same margins and out-of-bag sums as trees that carry every row."""
     import h2omx.models.tree.engine as E
 
-    X, y = _data(n=30000, F=9, seed=7, task="reg" if dist == "gaussian" else "bin")
+    X, y = _data(n=30000, F=9, seed=7, task="reg" if dist == "gaussian" else ("multi" if nclass == 3 else "bin"))
     _, bg = _both(X, y, 64)
     tp = TreeParams(max_depth=13, min_rows=2, learn_rate=1.0 if dist == "drf" else 0.2,
                     leaf_mode=1 if dist == "drf" else 0, mtries=4 if dist == "drf" else -1, mode=mode,
@@ -534,7 +535,7 @@ def test_bag_compact_matches(cuda_dev, monkeypatch, dist, mode):
     for flag in (False, True):
         monkeypatch.setattr(E.HipTreeBuilder, "BAG_COMPACT", flag)
         out[flag] = train_ensemble(bg, yt, dist=dist, ntrees=3, tparams=tp, sample_rate=0.6,
-                                   nclass=2 if dist == "drf" else 1, seed=11)
+                                   nclass=nclass if nclass > 1 else 1, seed=11)
     a, b = out[False], out[True]
     assert a.trees.tobytes() == b.trees.tobytes()
     sa, sb = getattr(a, "_state", None), getattr(b, "_state", None)
