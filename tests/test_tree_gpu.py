@@ -545,3 +545,24 @@ def test_bag_compact_matches(cuda_dev, monkeypatch, dist, mode, nclass):
     if oa is not None:
         for u, v in zip(oa, ob):
             np.testing.assert_array_equal(u.cpu().numpy(), v.cpu().numpy())
+
+
+def test_bag_compact_early_finish(cuda_dev, monkeypatch):
+    """A bagged deep tree that runs out of splittable nodes before max_depth
+    still routes its out-of-bag rows (the walk then runs after the loop)."""
+    import h2omx.models.tree.engine as E
+
+    X, y = _data(n=3000, F=7, seed=3, task="bin")
+    _, bg = _both(X, y, 16)
+    tp = TreeParams(max_depth=18, min_rows=40, learn_rate=1.0, leaf_mode=1, mtries=2)
+    yt = torch.from_numpy(y).cuda()
+    monkeypatch.setenv("H2OMX_TREE_ENGINE", "seg")
+    monkeypatch.setattr(E.HipTreeBuilder, "SYNC_NODE_CAP", 4)   # read node counts back early: the loop may stop
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(E.HipTreeBuilder, "BAG_COMPACT", flag)
+        out[flag] = train_ensemble(bg, yt, dist="drf", ntrees=3, tparams=tp, sample_rate=0.6, nclass=2, seed=5)
+    a, b = out[False], out[True]
+    assert a.trees.tobytes() == b.trees.tobytes()
+    for u, v in zip(a._oob, b._oob):
+        np.testing.assert_array_equal(u.cpu().numpy(), v.cpu().numpy())
