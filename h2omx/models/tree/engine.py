@@ -161,8 +161,11 @@ class HipTreeBuilder:
     # after it transpose the live rows' codes into column-major planes in
     # segment order (seg_colmajor_kernel); the ones in between move only
     # positions.  Wave-per-node levels read the row-major codes (their scan is
-    # issue-bound, profiles/r6/drf_pmc_r6i.txt).  0 = off
-    COLMAJOR_EVERY = 6
+    # issue-bound, profiles/r6/drf_pmc_r6i.txt).  0 = off: once out-of-bag rows left the
+    # segments (BAG_COMPACT) and direct levels start at 2048 nodes, the one transpose no
+    # longer pays (DRF 10M x 100 depth 20: 13.95 -> 13.75 ms/tree, profiles/r6/drf_switches_r6o.txt
+    # r6bc / r6bd; it did on the earlier pipeline: level 10 1121 -> 525 us, r6j)
+    COLMAJOR_EVERY = 0
 
     def __init__(self, bm: BinnedMatrix, params: TreeParams, comm=None):
         if not bm.codes.is_cuda:
