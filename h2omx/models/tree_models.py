@@ -234,14 +234,15 @@ class _TreeBuilder(ModelBuilder):
             if (int(self.params.get("max_depth") or 0) > self.deep_depth and fine > self.deep_fine_bins
                     and "nbins_top_level" not in getattr(self, "_explicit_params", ())):
                 # deep trees (DRF depth 20) with the default nbins_top_level: 63 fine bins
-                # keep the direct levels' per-node histograms small - 10M x 100 DRF 27 vs
-                # 43 ms/tree for 255, training AUC 0.787 vs 0.794 (QuantilesGlobal-20:
-                # 0.776; profiles/r5/hist/hist_rule_ab_r5y.jsonl).  An explicit
+                # keep the direct levels' per-node histograms small - 10M x 100 DRF 13.7 vs
+                # 19.4 ms/tree for 255, OOB AUC 0.791 vs 0.794 (profiles/r6/drf_fine255_r6bg.txt;
+                # round 5: 27 vs 43 ms, profiles/r5/hist/hist_rule_ab_r5y.jsonl).  An explicit
                 # nbins_top_level keeps the 255-bin grid.
                 fine = self.deep_fine_bins
                 self._warn(f"max_depth > {self.deep_depth} with the default nbins_top_level: per-node cut points "
-                           f"snap to {fine} fine quantile bins per column (faster; on 10M x 100 training AUC "
-                           f"0.787 vs 0.794 for 255 bins) - pass nbins_top_level explicitly for the 255-bin grid")
+                           f"snap to {fine} fine quantile bins per column (faster: on 10M x 100 13.7 vs 19.4 ms/tree, "
+                           f"OOB AUC 0.791 vs 0.794 for 255 bins) - pass nbins_top_level explicitly for the "
+                           f"255-bin grid")
             edges, nvb, nbt = compute_edges(X, fine, seed=self._seed(), comm=self.comm,
                                             histogram_type="QuantilesGlobal")
             if max(nbins, top) > 255 and fine == 255:
@@ -737,9 +738,9 @@ class H2ORandomForestEstimator(_TreeBuilder):
     Histograms: H2O's AUTO = per-node UniformAdaptive with nbins=20 on fine
     quantile bins (``binning.py``).  With max_depth > 12 (the default 20) and
     the default nbins_top_level, the fine grid has 63 bins per column instead
-    of 255: 1.6x faster deep levels (10M x 100: 27 vs 43 ms/tree) at a small
-    accuracy cost (training AUC 0.787 vs 0.794 there); the model records a
-    warning.  Passing ``nbins_top_level`` (e.g. H2O's 1024) keeps 255 bins."""
+    of 255: 1.4x faster (10M x 100: 13.7 vs 19.4 ms/tree) at a small accuracy
+    cost (out-of-bag AUC 0.791 vs 0.794 there); the fit warns.  Passing
+    ``nbins_top_level`` (e.g. H2O's 1024) keeps 255 bins."""
     algo = "drf"
     model_cls = DRFModel
     auto_histogram = "uniformadaptive"
