@@ -98,7 +98,12 @@ class HipTreeBuilder:
     # (profiles/r3/hist_threads_ab.txt) and the segment-ordered code-row moves
     # (profiles/r4/drf/move_rows_ab.txt).)
     SEG_TARGET_CHUNKS = 1024   # level-0 histogram chunks (2 resident 57 KB workgroups per CU)
-    SEG_LDS_BUDGET = 64 * 1024
+    # segmented-histogram LDS per workgroup (feature group size): small histograms (<= 64 bins)
+    # run more, narrower groups - DRF 10M x 100 depth 20: 64 / 32 / 24 / 16 / 12 / 8 / 4 KB ->
+    # 13.68 / 13.21 / 13.16 / 12.71 / 12.73 / 12.81 / 12.85 ms/tree (profiles/r6/drf_switches_r6o.txt
+    # r6bh-r6bj); 255-bin histograms keep 64 KB (16 KB: 19.4 vs 19.0 ms/tree, r6bk)
+    SEG_LDS_BUDGET = 16 * 1024
+    SEG_LDS_BUDGET_WIDE = 64 * 1024
     # seg engine: scan hist up to this many slots - the root only: from level 1 on the
     # segmented build reads the built children's in-bag rows instead of streaming all
     # rows (DRF 10M x 100 depth 20: levels 2-5, histograms + partitions 2002 -> 1628 us,
@@ -292,7 +297,7 @@ class HipTreeBuilder:
             hc_g = -(-n_global // self.SEG_TARGET_CHUNKS)
             self.max_rows_per_wg = max(self.max_rows_per_wg, self.hc_rows,
                                        min(self.ROWS_CAP, max(2048, -(-hc_g // 256) * 256)))
-            budget = self.SEG_LDS_BUDGET
+            budget = self.SEG_LDS_BUDGET if self.nbt <= 64 else self.SEG_LDS_BUDGET_WIDE
             fg = max(1, min(self.F, budget // (self.nbt * 8)))
             groups = math.ceil(self.F / fg)
             if groups > 1:

@@ -16,6 +16,10 @@ def main():
     from h2omx.frame import Frame
     from h2omx.frame.synthetic import wide_gaussian
     from h2omx.models import H2ORandomForestEstimator
+    from h2omx.models.tree.engine import HipTreeBuilder
+
+    if len(sys.argv) > 1:   # segmented-histogram LDS budget for the A/B
+        HipTreeBuilder.SEG_LDS_BUDGET = int(sys.argv[1])
 
     dev = torch.device("cuda", 0)
     X, y = wide_gaussian(10_000_000, 100, seed=5, device=dev)
@@ -26,7 +30,7 @@ def main():
         m = H2ORandomForestEstimator(ntrees=10, max_depth=20, seed=1, nbins_top_level=1024).train(
             y="response", training_frame=fr)
         torch.cuda.synchronize()
-        print(json.dumps({"fine_bins": 255, "rep": rep, "fit_s": round(time.perf_counter() - t0, 3),
+        print(json.dumps({"fine_bins": 255, "budget": HipTreeBuilder.SEG_LDS_BUDGET, "rep": rep, "fit_s": round(time.perf_counter() - t0, 3),
                           "ms_per_tree": round(1000 * float(m.timings.get("train_s", 0.0)) / 10, 2),
                           "auc": round(float(m.training_metrics["AUC"]), 5)}), flush=True)
 

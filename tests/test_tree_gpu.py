@@ -566,3 +566,26 @@ def test_bag_compact_early_finish(cuda_dev, monkeypatch):
     assert a.trees.tobytes() == b.trees.tobytes()
     for u, v in zip(a._oob, b._oob):
         np.testing.assert_array_equal(u.cpu().numpy(), v.cpu().numpy())
+
+
+def test_seg_feature_groups_match(cuda_dev, monkeypatch):
+    """The segmented histograms split into several feature groups (small LDS
+    budget) build the same trees as one group of every feature."""
+    import h2omx.models.tree.engine as E
+
+    X, y = _data(n=30000, F=13, seed=12, task="bin")
+    _, bg = _both(X, y, 63)   # 64-wide histograms
+    tp = TreeParams(max_depth=12, min_rows=2, learn_rate=1.0, leaf_mode=1, mtries=4)
+    yt = torch.from_numpy(y).cuda()
+    monkeypatch.setenv("H2OMX_TREE_ENGINE", "seg")
+    out = {}
+    for budget in (64 * 1024, 2048):
+        monkeypatch.setattr(E.HipTreeBuilder, "SEG_LDS_BUDGET", budget)
+        monkeypatch.setattr(E.HipTreeBuilder, "SEG_LDS_BUDGET_WIDE", budget)
+        out[budget] = train_ensemble(bg, yt, dist="drf", ntrees=3, tparams=tp, sample_rate=0.632, nclass=2, seed=4)
+    a, b = out[64 * 1024], out[2048]
+    for t in range(a.trees.shape[0]):
+        reach = a.compact()[t]
+        assert reach == b.compact()[t], t
+        for f in ("feat", "bin", "value", "weight"):
+            np.testing.assert_array_equal(a.trees[t][reach][f], b.trees[t][reach][f], err_msg=f"tree {t} {f}")
